@@ -1,0 +1,162 @@
+/*
+ * geohip.h -- C ABI of libgeohip.so: MI355X (gfx950) evaluation of GeoFlink windowed
+ * spatial queries.  One call evaluates one window's contents; window assembly (Flink's
+ * SlidingProcessingTimeWindows, keyBy(gridID)) stays in the caller.
+ *
+ * Each entry point replaces the per-cell window-function body of one reference operator
+ * (paths relative to /root/reference/src/main/java/GeoFlink):
+ *
+ *   geohip_range_pp    <- PointPointRangeQuery.run, window branch     spatialOperators/range/PointPointRangeQuery.java:86-137
+ *                         (filter :102-107, keyBy :111-116, apply :117-136; RealTime :43-83 has the same predicate)
+ *   geohip_knn_pp      <- PointPointKNNQuery.windowBased + merge      spatialOperators/knn/PointPointKNNQuery.java:125-191,
+ *                                                                      spatialOperators/knn/KNNQuery.java:204-272
+ *   geohip_join_pp     <- PointPointJoinQuery.windowBased             spatialOperators/join/PointPointJoinQuery.java:113-172
+ *                         + JoinQuery.getReplicatedPointQueryStream    spatialOperators/join/JoinQuery.java:73-90
+ *   geohip_range_ppoly <- PointPolygonRangeQuery.run, window branch   spatialOperators/range/PointPolygonRangeQuery.java:76-124
+ *                         (one independent query per polygon)
+ *   geohip_grid        <- UniformGrid getters                         spatialIndices/UniformGrid.java:136-146
+ *                         (values copied from the Java object, so both constructors :47-85 are covered)
+ *
+ * Semantics (bit-exact contract, DESIGN.md "Parity"):
+ *   - cell of a point  = (int)Math.floor((x - minX)/cellLength) per axis  (utils/HelperClass.java:104-116)
+ *   - guaranteed cells = square of Lg=(int)floor(r/(l*sqrt2)-1) layers, candidate = Lc=(int)ceil(r/l)
+ *     layers minus guaranteed, clipped by validKey               (UniformGrid.java:165-190, 224-229, 367-444)
+ *   - distances: JTS 1.16.1 Geometry.distance (fdlibm hypot, DistanceOp MAX_VALUE start)
+ *   - range: guaranteed cells emitted without a distance check; candidate cells need dist <= r
+ *   - kNN: no radius filter; k smallest (dist, idx) over guaranteed u candidate cells, ascending
+ *   - join: pairs (p, q) with cell_uGrid(p) in Nbr_qGrid(q) and dist <= r; r == 0 -> all cells
+ *
+ * Indices are window-local (0-based position in the caller's arrays) and map back to the
+ * caller's Point objects.  Outputs of range/join/ppoly are in ascending (point, query/poly)
+ * order for range and ppoly, unordered for join; kNN is ascending (dist, idx).
+ *
+ * Memory: the caller owns every buffer; nothing is retained after a call returns.  With
+ * GEOHIP_MEM_HOST (default) input/output pointers are host memory; with GEOHIP_MEM_DEVICE
+ * they are device pointers on the ctx's device (x/y 16-byte aligned).  Scalars
+ * (out_count) are always host memory for the synchronous calls.
+ *
+ * Threading: one ctx per calling thread (Flink task slot); distinct ctxs may run
+ * concurrently.  Synchronous calls return after the results are in place.  *_async calls
+ * enqueue on the ctx stream and return immediately (device memory only).
+ *
+ * Errors: int status; never aborts.  GEOHIP_ERR_ARG covers the reference's System.exit(1)
+ * (UniformGrid.java:237-241, 272-276: join with r < 0 or NaN) and NumberFormatException in
+ * getIntCellIndices.  GEOHIP_ERR_CAPACITY reports the required size in *out_count.
+ */
+#ifndef GEOHIP_H
+#define GEOHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GEOHIP_OK 0
+#define GEOHIP_ERR_ARG 1
+#define GEOHIP_ERR_CAPACITY 2
+#define GEOHIP_ERR_DEVICE 3
+#define GEOHIP_ERR_OOM 4
+#define GEOHIP_ERR_UNSUPPORTED 5
+
+#define GEOHIP_MEM_HOST 0
+#define GEOHIP_MEM_DEVICE 1
+
+/* Largest k served by the wave-select kNN path (PointPointKNNQuery's k). */
+#define GEOHIP_KNN_MAX_K 256
+
+typedef struct geohip_ctx geohip_ctx;
+
+/* UniformGrid state: getMinX(), getMinY(), getCellLength(), getNumGridPartitions(). */
+typedef struct geohip_grid {
+    double min_x;
+    double min_y;
+    double cell_len;
+    int32_t n;
+    int32_t reserved;
+} geohip_grid;
+
+/* Inclusive cell-index rectangle (planning introspection). */
+typedef struct geohip_rect {
+    int32_t x0, x1, y0, y1;
+} geohip_rect;
+
+/* ---- context ---------------------------------------------------------------------- */
+/* device_mask: bit i selects HIP device i (exactly one bit; 0 = current device). */
+int geohip_ctx_create(uint32_t device_mask, geohip_ctx** out_ctx);
+int geohip_ctx_destroy(geohip_ctx* ctx);
+const char* geohip_last_error(const geohip_ctx* ctx);
+int geohip_ctx_set_mem(geohip_ctx* ctx, int mem_kind);
+/* Use the caller's hipStream_t (NULL = the ctx's own stream). */
+int geohip_ctx_set_stream(geohip_ctx* ctx, void* hip_stream);
+void* geohip_ctx_stream(geohip_ctx* ctx);
+/* Per-launch HIP-event timing of each query's dominant kernel (the scan kernel). */
+int geohip_ctx_set_timing(geohip_ctx* ctx, int enable);
+/* Synchronises, then reports the summed duration and launch count since the last reset. */
+int geohip_ctx_timing(geohip_ctx* ctx, double* total_ms, uint64_t* launches, int reset);
+int geohip_device_count(int* out_count);
+const char* geohip_version(void);
+
+/* ---- queries (synchronous) ------------------------------------------------------------ */
+int geohip_range_pp(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
+                    uint64_t n, double qx, double qy, double r, int approximate,
+                    uint32_t* out_idx, uint64_t cap, uint64_t* out_count);
+
+int geohip_knn_pp(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
+                  uint64_t n, double qx, double qy, double r, uint32_t k,
+                  uint32_t* out_idx, double* out_dist, uint32_t* out_count);
+
+/* out_pairs: 2*cap uint32 (p_idx, q_idx) pairs. */
+int geohip_join_pp(geohip_ctx* ctx, const geohip_grid* grid_data, const geohip_grid* grid_query,
+                   const double* dx, const double* dy, uint64_t nd,
+                   const double* qx, const double* qy, uint64_t nq, double r, int approximate,
+                   uint32_t* out_pairs, uint64_t cap, uint64_t* out_count);
+int geohip_join_pp_count_only(geohip_ctx* ctx, const geohip_grid* grid_data, const geohip_grid* grid_query,
+                              const double* dx, const double* dy, uint64_t nd,
+                              const double* qx, const double* qy, uint64_t nq, double r,
+                              int approximate, uint64_t* out_count);
+
+/* npoly single-ring polygons: vertices vx/vy[ring_off[i] .. ring_off[i+1]) as given to
+   Polygon(List<List<Coordinate>>, UniformGrid) (ring closed here if open; > 3 coords).
+   out_pairs: 2*cap uint32 (poly_idx, point_idx), ascending. */
+int geohip_range_ppoly(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
+                       uint64_t n, const uint32_t* ring_off, const double* vx, const double* vy,
+                       uint32_t npoly, double r, int approximate,
+                       uint32_t* out_pairs, uint64_t cap, uint64_t* out_count);
+
+/* ---- device-resident pipeline forms (GEOHIP_MEM_DEVICE pointers; enqueue only) -------- */
+/* Writes k (dist, idx) ascending to out_dist/out_idx (device), entries past the candidate
+   count are (+inf-bits sentinel, 0xffffffff); *out_count_dev = number of valid entries. */
+int geohip_knn_pp_async(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
+                        uint64_t n, double qx, double qy, double r, uint32_t k,
+                        uint32_t* out_idx, double* out_dist, uint32_t* out_count_dev);
+/* Merge nlists sorted (dist, idx) lists of list_len entries (e.g. the all-gathered per-shard
+   kNN results) into the k smallest; same output convention as geohip_knn_pp_async.
+   idx values are taken as global ids (shards add their base offset before the gather). */
+int geohip_knn_merge_async(geohip_ctx* ctx, const double* dist, const uint32_t* idx, uint32_t nlists,
+                           uint32_t list_len, uint32_t k, uint32_t* out_idx, double* out_dist,
+                           uint32_t* out_count_dev);
+/* Range into device buffers: out_idx (cap entries), *out_count_dev = total hits. */
+int geohip_range_pp_async(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
+                          uint64_t n, double qx, double qy, double r, int approximate,
+                          uint32_t* out_idx, uint64_t cap, uint64_t* out_count_dev);
+
+/* ---- host-side planning introspection (no device needed) ------------------------------ */
+/* Query-cell sets of a point query as rectangles: point in G iff in any g rect; point in C
+   iff in the c rect and not in G.  Returns GEOHIP_ERR_ARG where the reference throws. */
+int geohip_plan_point(const geohip_grid* grid, double qx, double qy, double r,
+                      geohip_rect* g_rects, uint32_t* n_g, geohip_rect* c_rect, uint32_t* n_c,
+                      int32_t* layers_g, int32_t* layers_c);
+/* Cell of a coordinate (HelperClass.assignGridCellID) computed by the planner. */
+int geohip_plan_cell(const geohip_grid* grid, double x, double y, int32_t* cx, int32_t* cy);
+
+/* ---- synthetic window generators (bench / tests), device pointers --------------------- */
+/* x[i] = min_x + u(seed, 2(base+i)) * (max_x - min_x), y likewise with 2(base+i)+1, where
+   u = (splitmix64(seed ^ k) >> 11) * 2^-53.  Bit-identical to spatialflink_amd.synth. */
+int geohip_synth_uniform_async(geohip_ctx* ctx, double* x, double* y, uint64_t n, uint64_t base,
+                               uint64_t seed, double min_x, double max_x, double min_y, double max_y);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GEOHIP_H */

@@ -1,0 +1,147 @@
+"""ctypes binding of the C oracle (oracle/geohip_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, never by spatialflink_amd.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import POINTER, c_double, c_int, c_int32, c_int64, c_uint32, c_uint64, c_void_p
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / "libgeohip_oracle.so"
+
+
+class Grid(ctypes.Structure):
+    _fields_ = [("min_x", c_double), ("min_y", c_double), ("cell_len", c_double), ("n", c_int32)]
+
+
+def _load():
+    if not LIB.exists():
+        import subprocess
+        subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+    lib = ctypes.CDLL(str(LIB))
+    sig = {
+        "geohip_oracle_hypot": (c_double, [c_double, c_double]),
+        "geohip_oracle_pp_distance": (c_double, [c_double] * 4),
+        "geohip_oracle_point_segment": (c_double, [c_double] * 6),
+        "geohip_oracle_point_polygon": (c_double, [c_double, c_double, c_void_p, c_void_p, c_int]),
+        "geohip_oracle_bbox_distance": (c_double, [c_double] * 6),
+        "geohip_oracle_d2i": (c_int32, [c_double]),
+        "geohip_oracle_cell": (None, [POINTER(Grid), c_double, c_double, POINTER(c_int32), POINTER(c_int32)]),
+        "geohip_oracle_layers_guaranteed": (c_int32, [POINTER(Grid), c_double]),
+        "geohip_oracle_layers_candidate": (c_int32, [POINTER(Grid), c_double]),
+        "geohip_oracle_key_roundtrip": (c_int, [c_int32, c_int32, POINTER(c_int32), POINTER(c_int32)]),
+        "geohip_oracle_key_matches": (c_int, [c_int32, c_int32, c_void_p, c_int]),
+        "geohip_oracle_range_pp": (c_int64, [POINTER(Grid), c_void_p, c_void_p, c_uint64, c_double, c_double,
+                                             c_double, c_int, c_void_p, c_uint64]),
+        "geohip_oracle_knn_pp": (c_int, [POINTER(Grid), c_void_p, c_void_p, c_uint64, c_double, c_double, c_double,
+                                         c_uint32, c_void_p, c_void_p, POINTER(c_uint32)]),
+        "geohip_oracle_join_pp": (c_int64, [POINTER(Grid), POINTER(Grid), c_void_p, c_void_p, c_uint64, c_void_p,
+                                            c_void_p, c_uint64, c_double, c_int, c_void_p, c_uint64]),
+        "geohip_oracle_range_ppoly": (c_int64, [POINTER(Grid), c_void_p, c_void_p, c_uint64, c_void_p, c_void_p,
+                                                c_void_p, c_uint32, c_double, c_int, c_void_p, c_uint64]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+class OracleError(RuntimeError):
+    pass
+
+
+def grid(min_x, min_y, cell_len, n) -> Grid:
+    return Grid(float(min_x), float(min_y), float(cell_len), int(n))
+
+
+def _p(a):
+    return a.ctypes.data_as(c_void_p)
+
+
+def hypot(x, y):
+    return lib.geohip_oracle_hypot(x, y)
+
+
+def cell(g: Grid, x, y):
+    cx, cy = c_int32(0), c_int32(0)
+    lib.geohip_oracle_cell(ctypes.byref(g), x, y, ctypes.byref(cx), ctypes.byref(cy))
+    return cx.value, cy.value
+
+
+def layers(g: Grid, r):
+    return lib.geohip_oracle_layers_guaranteed(ctypes.byref(g), r), lib.geohip_oracle_layers_candidate(ctypes.byref(g), r)
+
+
+def range_pp(g: Grid, x, y, qx, qy, r, approximate=False) -> np.ndarray:
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    out = np.empty(max(len(x), 1), np.uint32)
+    c = lib.geohip_oracle_range_pp(ctypes.byref(g), _p(x), _p(y), len(x), qx, qy, r, int(approximate), _p(out), len(out))
+    if c < 0:
+        raise OracleError(f"oracle range_pp error {c}")
+    return out[:c].copy()
+
+
+def knn_pp(g: Grid, x, y, qx, qy, r, k):
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    oi = np.empty(k, np.uint32)
+    od = np.empty(k, np.float64)
+    cnt = c_uint32(0)
+    rc = lib.geohip_oracle_knn_pp(ctypes.byref(g), _p(x), _p(y), len(x), qx, qy, r, k, _p(oi), _p(od),
+                                  ctypes.byref(cnt))
+    if rc != 0:
+        raise OracleError(f"oracle knn_pp error {rc}")
+    return oi[:cnt.value].copy(), od[:cnt.value].copy()
+
+
+def join_pp(gd: Grid, gq: Grid, dx, dy, qx, qy, r, approximate=False, cap=None) -> np.ndarray:
+    dx = np.ascontiguousarray(dx, np.float64)
+    dy = np.ascontiguousarray(dy, np.float64)
+    qx = np.ascontiguousarray(qx, np.float64)
+    qy = np.ascontiguousarray(qy, np.float64)
+    if cap is None:
+        c = lib.geohip_oracle_join_pp(ctypes.byref(gd), ctypes.byref(gq), _p(dx), _p(dy), len(dx), _p(qx), _p(qy),
+                                      len(qx), r, int(approximate), None, 0)
+        if c < 0:
+            raise OracleError(f"oracle join_pp error {c}")
+        cap = c
+    out = np.empty((max(cap, 1), 2), np.uint32)
+    c = lib.geohip_oracle_join_pp(ctypes.byref(gd), ctypes.byref(gq), _p(dx), _p(dy), len(dx), _p(qx), _p(qy),
+                                  len(qx), r, int(approximate), _p(out), cap)
+    if c < 0:
+        raise OracleError(f"oracle join_pp error {c}")
+    return out[:c].copy()
+
+
+def range_ppoly(g: Grid, x, y, ring_off, vx, vy, r, approximate=False) -> np.ndarray:
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    ring_off = np.ascontiguousarray(ring_off, np.uint32)
+    vx = np.ascontiguousarray(vx, np.float64)
+    vy = np.ascontiguousarray(vy, np.float64)
+    npoly = len(ring_off) - 1
+    c = lib.geohip_oracle_range_ppoly(ctypes.byref(g), _p(x), _p(y), len(x), _p(ring_off), _p(vx), _p(vy), npoly,
+                                      r, int(approximate), None, 0)
+    if c < 0:
+        raise OracleError(f"oracle range_ppoly error {c}")
+    out = np.empty((max(c, 1), 2), np.uint32)
+    c2 = lib.geohip_oracle_range_ppoly(ctypes.byref(g), _p(x), _p(y), len(x), _p(ring_off), _p(vx), _p(vy), npoly,
+                                       r, int(approximate), _p(out), c)
+    assert c2 == c
+    return out[:c].copy()
+
+
+def point_polygon(px, py, vx, vy):
+    vx = np.ascontiguousarray(vx, np.float64)
+    vy = np.ascontiguousarray(vy, np.float64)
+    return lib.geohip_oracle_point_polygon(px, py, _p(vx), _p(vy), len(vx))

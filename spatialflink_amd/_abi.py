@@ -1,0 +1,351 @@
+"""ctypes binding of libgeohip.so (include/geohip.h).
+
+The product path: every query call goes to the gfx950 HIP library.  There is no CPU
+fallback -- if the shared library is missing this module raises at import time, and if no
+device is present ``Context()`` raises ``GeohipDeviceError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_uint32, c_uint64, c_void_p
+from pathlib import Path
+
+import numpy as np
+
+LIB_PATH = Path(os.environ.get("GEOHIP_LIB", Path(__file__).resolve().parent / "libgeohip.so"))
+
+OK, ERR_ARG, ERR_CAPACITY, ERR_DEVICE, ERR_OOM, ERR_UNSUPPORTED = 0, 1, 2, 3, 4, 5
+MEM_HOST, MEM_DEVICE = 0, 1
+KNN_MAX_K = 256
+SENTINEL_IDX = 0xFFFFFFFF
+
+
+class GeohipError(RuntimeError):
+    code = -1
+
+
+class GeohipArgumentError(GeohipError, ValueError):
+    """Where the reference calls System.exit(1) or throws (IllegalArgument/NumberFormat)."""
+    code = ERR_ARG
+
+
+class GeohipCapacityError(GeohipError):
+    code = ERR_CAPACITY
+
+
+class GeohipDeviceError(GeohipError):
+    code = ERR_DEVICE
+
+
+class GeohipOOMError(GeohipError, MemoryError):
+    code = ERR_OOM
+
+
+class GeohipUnsupportedError(GeohipError, NotImplementedError):
+    code = ERR_UNSUPPORTED
+
+
+_ERRORS = {ERR_ARG: GeohipArgumentError, ERR_CAPACITY: GeohipCapacityError, ERR_DEVICE: GeohipDeviceError,
+           ERR_OOM: GeohipOOMError, ERR_UNSUPPORTED: GeohipUnsupportedError}
+
+
+class Grid(ctypes.Structure):
+    _fields_ = [("min_x", c_double), ("min_y", c_double), ("cell_len", c_double), ("n", c_int32),
+                ("reserved", c_int32)]
+
+
+class Rect(ctypes.Structure):
+    _fields_ = [("x0", c_int32), ("x1", c_int32), ("y0", c_int32), ("y1", c_int32)]
+
+
+if not LIB_PATH.exists():
+    raise ImportError(f"{LIB_PATH} not built: run `python -m spatialflink_amd.build` (hipcc, gfx950)")
+
+lib = ctypes.CDLL(str(LIB_PATH))
+
+_P = c_void_p
+_SIGS = {
+    "geohip_version": (c_char_p, []),
+    "geohip_device_count": (c_int, [POINTER(c_int)]),
+    "geohip_ctx_create": (c_int, [c_uint32, POINTER(c_void_p)]),
+    "geohip_ctx_destroy": (c_int, [_P]),
+    "geohip_last_error": (c_char_p, [_P]),
+    "geohip_ctx_set_mem": (c_int, [_P, c_int]),
+    "geohip_ctx_set_stream": (c_int, [_P, _P]),
+    "geohip_ctx_stream": (c_void_p, [_P]),
+    "geohip_ctx_set_timing": (c_int, [_P, c_int]),
+    "geohip_ctx_timing": (c_int, [_P, POINTER(c_double), POINTER(c_uint64), c_int]),
+    "geohip_range_pp": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_double, c_double, c_double, c_int, _P,
+                                c_uint64, POINTER(c_uint64)]),
+    "geohip_range_pp_async": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_double, c_double, c_double, c_int,
+                                      _P, c_uint64, _P]),
+    "geohip_knn_pp": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_double, c_double, c_double, c_uint32, _P, _P,
+                              POINTER(c_uint32)]),
+    "geohip_knn_pp_async": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_double, c_double, c_double, c_uint32,
+                                    _P, _P, _P]),
+    "geohip_knn_merge_async": (c_int, [_P, _P, _P, c_uint32, c_uint32, c_uint32, _P, _P, _P]),
+    "geohip_join_pp": (c_int, [_P, POINTER(Grid), POINTER(Grid), _P, _P, c_uint64, _P, _P, c_uint64, c_double,
+                               c_int, _P, c_uint64, POINTER(c_uint64)]),
+    "geohip_join_pp_count_only": (c_int, [_P, POINTER(Grid), POINTER(Grid), _P, _P, c_uint64, _P, _P, c_uint64,
+                                          c_double, c_int, POINTER(c_uint64)]),
+    "geohip_range_ppoly": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, _P, _P, _P, c_uint32, c_double, c_int, _P,
+                                   c_uint64, POINTER(c_uint64)]),
+    "geohip_plan_point": (c_int, [POINTER(Grid), c_double, c_double, c_double, POINTER(Rect), POINTER(c_uint32),
+                                  POINTER(Rect), POINTER(c_uint32), POINTER(c_int32), POINTER(c_int32)]),
+    "geohip_plan_cell": (c_int, [POINTER(Grid), c_double, c_double, POINTER(c_int32), POINTER(c_int32)]),
+    "geohip_synth_uniform_async": (c_int, [_P, _P, _P, c_uint64, c_uint64, c_uint64, c_double, c_double, c_double,
+                                           c_double]),
+    "geohip_debug_selftest_fp64": (c_int, [_P, _P, _P, c_uint64, _P, _P, _P, _P]),
+    "geohip_debug_classify": (c_int, [POINTER(Grid), c_double, c_double, c_double, _P, _P, c_uint64, _P]),
+}
+for _name, (_res, _args) in _SIGS.items():
+    _f = getattr(lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+# symbols of include/geohip.h (tests check the library exports every one)
+HEADER_SYMBOLS = [n for n in _SIGS if not n.startswith("geohip_debug_")]
+
+
+def version() -> str:
+    return lib.geohip_version().decode()
+
+
+def device_count() -> int:
+    c = c_int(0)
+    lib.geohip_device_count(ctypes.byref(c))
+    return c.value
+
+
+def make_grid(min_x: float, min_y: float, cell_len: float, n: int) -> Grid:
+    return Grid(float(min_x), float(min_y), float(cell_len), int(n), 0)
+
+
+def plan_point(grid: Grid, qx: float, qy: float, r: float):
+    """Planner introspection (host only): (g_rects, c_rects, Lg, Lc) as lists of (x0,x1,y0,y1)."""
+    g = (Rect * 16)()
+    c = Rect()
+    ng, nc = c_uint32(0), c_uint32(0)
+    lg, lc = c_int32(0), c_int32(0)
+    rc = lib.geohip_plan_point(ctypes.byref(grid), qx, qy, r, g, ctypes.byref(ng), ctypes.byref(c),
+                               ctypes.byref(nc), ctypes.byref(lg), ctypes.byref(lc))
+    if rc:
+        raise _ERRORS.get(rc, GeohipError)(f"plan_point failed ({rc})")
+    gl = [(g[i].x0, g[i].x1, g[i].y0, g[i].y1) for i in range(ng.value)]
+    cl = [(c.x0, c.x1, c.y0, c.y1)] if nc.value else []
+    return gl, cl, lg.value, lc.value
+
+
+def debug_classify(grid: Grid, qx: float, qy: float, r: float, x: np.ndarray, y: np.ndarray) -> np.ndarray:
+    """Host evaluation of the planner's boxes (test hook): bit0 inG, bit1 inC, bit2 in G u C."""
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    out = np.empty(len(x), np.uint8)
+    rc = lib.geohip_debug_classify(ctypes.byref(grid), qx, qy, r, x.ctypes.data_as(c_void_p),
+                                   y.ctypes.data_as(c_void_p), len(x), out.ctypes.data_as(c_void_p))
+    if rc:
+        raise _ERRORS.get(rc, GeohipError)(f"debug_classify failed ({rc})")
+    return out
+
+
+def plan_cell(grid: Grid, x: float, y: float):
+    cx, cy = c_int32(0), c_int32(0)
+    lib.geohip_plan_cell(ctypes.byref(grid), x, y, ctypes.byref(cx), ctypes.byref(cy))
+    return cx.value, cy.value
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data_as(c_void_p)
+    return c_void_p(a.data_ptr())  # torch tensor on the ctx device
+
+
+def _is_device(a) -> bool:
+    return not isinstance(a, np.ndarray) and getattr(a, "is_cuda", False)
+
+
+def _f64(a):
+    if isinstance(a, np.ndarray):
+        return np.ascontiguousarray(a, dtype=np.float64)
+    return a
+
+
+class Context:
+    """One geohip_ctx (one device, one stream).  Not shared between threads."""
+
+    def __init__(self, device: int = 0):
+        h = c_void_p()
+        rc = lib.geohip_ctx_create(1 << device, ctypes.byref(h))
+        if rc:
+            raise _ERRORS.get(rc, GeohipError)(f"geohip_ctx_create(device={device}) failed ({rc}); "
+                                               "libgeohip needs an MI355X (gfx950) device")
+        self.h = h
+        self.device = device
+        self._mem = MEM_HOST
+
+    def close(self):
+        if self.h:
+            lib.geohip_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int, what: str):
+        if rc:
+            msg = lib.geohip_last_error(self.h).decode(errors="replace")
+            raise _ERRORS.get(rc, GeohipError)(f"{what}: {msg}")
+
+    def set_mem(self, kind: int):
+        if kind != self._mem:
+            self._check(lib.geohip_ctx_set_mem(self.h, kind), "set_mem")
+            self._mem = kind
+
+    def set_stream(self, stream_ptr: int | None):
+        self._check(lib.geohip_ctx_set_stream(self.h, c_void_p(stream_ptr) if stream_ptr else None), "set_stream")
+
+    def stream(self) -> int:
+        return lib.geohip_ctx_stream(self.h) or 0
+
+    def set_timing(self, on: bool):
+        self._check(lib.geohip_ctx_set_timing(self.h, int(on)), "set_timing")
+
+    def timing(self, reset: bool = True):
+        ms, n = c_double(0), c_uint64(0)
+        self._check(lib.geohip_ctx_timing(self.h, ctypes.byref(ms), ctypes.byref(n), int(reset)), "timing")
+        return ms.value, n.value
+
+    def _mem_for(self, *arrays):
+        dev = [_is_device(a) for a in arrays if a is not None]
+        if any(dev) and not all(dev):
+            raise GeohipArgumentError("mix of host and device arrays")
+        self.set_mem(MEM_DEVICE if dev and dev[0] else MEM_HOST)
+        return bool(dev and dev[0])
+
+    # ---- queries -------------------------------------------------------------------------
+    def range_pp(self, grid: Grid, x, y, qx, qy, r, approximate=False, cap=None):
+        x, y = _f64(x), _f64(y)
+        n = len(x)
+        dev = self._mem_for(x, y)
+        if dev:
+            import torch
+            cap = n if cap is None else cap
+            out = torch.empty(max(cap, 1), dtype=torch.int32, device=x.device)
+        else:
+            cap = n if cap is None else cap
+            out = np.empty(max(cap, 1), dtype=np.uint32)
+        cnt = c_uint64(0)
+        rc = lib.geohip_range_pp(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), n, qx, qy, r, int(approximate),
+                                 _ptr(out), cap, ctypes.byref(cnt))
+        self._check(rc, "range_pp")
+        return out[:cnt.value]
+
+    def knn_pp(self, grid: Grid, x, y, qx, qy, r, k):
+        x, y = _f64(x), _f64(y)
+        n = len(x)
+        dev = self._mem_for(x, y)
+        if dev:
+            import torch
+            oi = torch.empty(k, dtype=torch.int32, device=x.device)
+            od = torch.empty(k, dtype=torch.float64, device=x.device)
+        else:
+            oi = np.empty(k, dtype=np.uint32)
+            od = np.empty(k, dtype=np.float64)
+        cnt = c_uint32(0)
+        rc = lib.geohip_knn_pp(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), n, qx, qy, r, k, _ptr(oi), _ptr(od),
+                               ctypes.byref(cnt))
+        self._check(rc, "knn_pp")
+        return oi[:cnt.value], od[:cnt.value]
+
+    def knn_pp_async(self, grid: Grid, x, y, qx, qy, r, k, out_idx, out_dist, out_count):
+        self.set_mem(MEM_DEVICE)
+        rc = lib.geohip_knn_pp_async(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), len(x), qx, qy, r, k,
+                                     _ptr(out_idx), _ptr(out_dist), _ptr(out_count))
+        self._check(rc, "knn_pp_async")
+
+    def knn_merge_async(self, dist, idx, nlists, list_len, k, out_idx, out_dist, out_count):
+        self.set_mem(MEM_DEVICE)
+        rc = lib.geohip_knn_merge_async(self.h, _ptr(dist), _ptr(idx), nlists, list_len, k, _ptr(out_idx),
+                                        _ptr(out_dist), _ptr(out_count))
+        self._check(rc, "knn_merge_async")
+
+    def range_pp_async(self, grid: Grid, x, y, qx, qy, r, approximate, out_idx, cap, out_count):
+        self.set_mem(MEM_DEVICE)
+        rc = lib.geohip_range_pp_async(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), len(x), qx, qy, r,
+                                       int(approximate), _ptr(out_idx), cap, _ptr(out_count))
+        self._check(rc, "range_pp_async")
+
+    def join_pp(self, grid_data: Grid, grid_query: Grid, dx, dy, qx, qy, r, approximate=False, cap=None):
+        dx, dy, qx, qy = _f64(dx), _f64(dy), _f64(qx), _f64(qy)
+        dev = self._mem_for(dx, dy, qx, qy)
+        cnt = c_uint64(0)
+        if cap is None:
+            rc = lib.geohip_join_pp_count_only(self.h, ctypes.byref(grid_data), ctypes.byref(grid_query), _ptr(dx),
+                                               _ptr(dy), len(dx), _ptr(qx), _ptr(qy), len(qx), r, int(approximate),
+                                               ctypes.byref(cnt))
+            self._check(rc, "join_pp_count_only")
+            cap = cnt.value
+        if dev:
+            import torch
+            out = torch.empty((max(cap, 1), 2), dtype=torch.int32, device=dx.device)
+        else:
+            out = np.empty((max(cap, 1), 2), dtype=np.uint32)
+        rc = lib.geohip_join_pp(self.h, ctypes.byref(grid_data), ctypes.byref(grid_query), _ptr(dx), _ptr(dy),
+                                len(dx), _ptr(qx), _ptr(qy), len(qx), r, int(approximate), _ptr(out), cap,
+                                ctypes.byref(cnt))
+        self._check(rc, "join_pp")
+        return out[:cnt.value]
+
+    def join_pp_count(self, grid_data: Grid, grid_query: Grid, dx, dy, qx, qy, r, approximate=False) -> int:
+        dx, dy, qx, qy = _f64(dx), _f64(dy), _f64(qx), _f64(qy)
+        self._mem_for(dx, dy, qx, qy)
+        cnt = c_uint64(0)
+        rc = lib.geohip_join_pp_count_only(self.h, ctypes.byref(grid_data), ctypes.byref(grid_query), _ptr(dx),
+                                           _ptr(dy), len(dx), _ptr(qx), _ptr(qy), len(qx), r, int(approximate),
+                                           ctypes.byref(cnt))
+        self._check(rc, "join_pp_count_only")
+        return cnt.value
+
+    def range_ppoly(self, grid: Grid, x, y, ring_off, vx, vy, r, approximate=False, cap=None):
+        x, y = _f64(x), _f64(y)
+        self._mem_for(x, y)
+        ring_off = np.ascontiguousarray(ring_off, dtype=np.uint32)
+        vx = np.ascontiguousarray(vx, dtype=np.float64)
+        vy = np.ascontiguousarray(vy, dtype=np.float64)
+        npoly = len(ring_off) - 1
+        cnt = c_uint64(0)
+        if cap is None:
+            rc = lib.geohip_range_ppoly(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), len(x), _ptr(ring_off),
+                                        _ptr(vx), _ptr(vy), npoly, r, int(approximate), None, 0, ctypes.byref(cnt))
+            if rc not in (OK, ERR_CAPACITY):
+                self._check(rc, "range_ppoly")
+            cap = cnt.value
+        if _is_device(x):
+            import torch
+            out = torch.empty((max(cap, 1), 2), dtype=torch.int32, device=x.device)
+        else:
+            out = np.empty((max(cap, 1), 2), dtype=np.uint32)
+        rc = lib.geohip_range_ppoly(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), len(x), _ptr(ring_off), _ptr(vx),
+                                    _ptr(vy), npoly, r, int(approximate), _ptr(out), cap, ctypes.byref(cnt))
+        self._check(rc, "range_ppoly")
+        return out[:cnt.value]
+
+    def synth_uniform_async(self, x, y, base, seed, bbox):
+        min_x, max_x, min_y, max_y = bbox
+        rc = lib.geohip_synth_uniform_async(self.h, _ptr(x), _ptr(y), len(x), base, seed, min_x, max_x, min_y, max_y)
+        self._check(rc, "synth_uniform_async")
+
+    def selftest_fp64(self, a, b):
+        """Device fp64 primitive bits (test hook): returns (sqrt|a|, a/b, hypot(a,b), a*b-b*b)."""
+        import torch
+        outs = [torch.empty_like(a) for _ in range(4)]
+        self.set_mem(MEM_DEVICE)
+        rc = lib.geohip_debug_selftest_fp64(self.h, _ptr(a), _ptr(b), len(a), *[_ptr(o) for o in outs])
+        self._check(rc, "selftest_fp64")
+        return outs

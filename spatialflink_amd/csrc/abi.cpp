@@ -1,0 +1,536 @@
+// abi.cpp -- the extern "C" boundary of libgeohip.so (include/geohip.h).
+//
+// Owns contexts (device, stream, grow-on-demand device scratch, pinned readback words,
+// optional per-launch event timing), validates arguments the way the reference fails
+// (System.exit / exceptions -> status codes, never abort), plans each query on the host
+// (plan.cpp) and launches the gfx950 kernels (pp_kernels.hip, join.hip, ppoly.hip).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "geohip_internal.h"
+#include "join.h"
+#include "pp_kernels.h"
+#include "ppoly.h"
+
+using namespace geohip;
+
+enum Slot {
+    S_X, S_Y, S_QX, S_QY, S_GTHR, S_PART_D, S_PART_I, S_OUT_D, S_OUT_I, S_OUT_CNT,
+    S_MASK, S_UCNT, S_OFFS, S_TOTAL, S_OUT_IDX, S_OUT_PAIRS,
+    S_J0, S_J1, S_J2, S_J3, S_J4, S_J5, S_J6, S_J7, S_J8, S_J9,
+    S_COUNT
+};
+
+struct geohip_ctx {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    int mem = GEOHIP_MEM_HOST;
+    std::string err;
+    void* buf[S_COUNT] = {};
+    size_t cap[S_COUNT] = {};
+    uint64_t* pinned = nullptr;  // 8 words of pinned host memory for count readback
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+    std::vector<hipEvent_t> pool;
+    double acc_ms = 0.0;
+    uint64_t launches = 0;
+};
+
+namespace {
+
+int fail(geohip_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+int hip_fail(geohip_ctx* c, hipError_t e, const char* where) {
+    return fail(c, GEOHIP_ERR_DEVICE, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+#define HIPCHK(expr)                                          \
+    do {                                                      \
+        hipError_t e_ = (expr);                               \
+        if (e_ != hipSuccess) return hip_fail(ctx, e_, #expr); \
+    } while (0)
+
+int ensure(geohip_ctx* ctx, Slot s, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (ctx->cap[s] >= bytes) return GEOHIP_OK;
+    if (ctx->buf[s]) {
+        hipStreamSynchronize(ctx->stream);
+        hipFree(ctx->buf[s]);
+        ctx->buf[s] = nullptr;
+        ctx->cap[s] = 0;
+    }
+    size_t want = bytes + bytes / 4;
+    want = (want + 255) & ~(size_t)255;
+    void* p = nullptr;
+    if (hipMalloc(&p, want) != hipSuccess) {
+        (void)hipGetLastError();
+        if (hipMalloc(&p, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(ctx, GEOHIP_ERR_OOM, "device allocation of " + std::to_string(bytes) + " bytes failed");
+        }
+        want = bytes;
+    }
+    ctx->buf[s] = p;
+    ctx->cap[s] = want;
+    return GEOHIP_OK;
+}
+
+template <typename T>
+T* B(geohip_ctx* ctx, Slot s) { return reinterpret_cast<T*>(ctx->buf[s]); }
+
+int begin(geohip_ctx* ctx) {
+    if (!ctx) return GEOHIP_ERR_ARG;
+    ctx->err.clear();
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    return GEOHIP_OK;
+}
+
+void timing_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1) {
+    *e0 = *e1 = nullptr;
+    if (!ctx->timing) return;
+    for (int t = 0; t < 2; t++) {
+        hipEvent_t ev = nullptr;
+        if (!ctx->pool.empty()) {
+            ev = ctx->pool.back();
+            ctx->pool.pop_back();
+        } else if (hipEventCreate(&ev) != hipSuccess) {
+            return;
+        }
+        (t == 0 ? *e0 : *e1) = ev;
+    }
+    ctx->pending.push_back({*e0, *e1});
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+// Stage x/y for the kernels: host pointers are copied into ctx scratch, device pointers used.
+int stage_xy(geohip_ctx* ctx, const double* x, const double* y, uint64_t n, Slot sx, Slot sy,
+             const double** dx, const double** dy) {
+    if (n == 0) {
+        *dx = *dy = nullptr;
+        return GEOHIP_OK;
+    }
+    if (!x || !y) return fail(ctx, GEOHIP_ERR_ARG, "null coordinate array");
+    if (ctx->mem == GEOHIP_MEM_DEVICE) {
+        if (!aligned16(x) || !aligned16(y)) return fail(ctx, GEOHIP_ERR_ARG, "device x/y must be 16-byte aligned");
+        *dx = x;
+        *dy = y;
+        return GEOHIP_OK;
+    }
+    int rc = ensure(ctx, sx, n * 8);
+    if (!rc) rc = ensure(ctx, sy, n * 8);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(ctx->buf[sx], x, n * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->buf[sy], y, n * 8, hipMemcpyHostToDevice, ctx->stream));
+    *dx = B<double>(ctx, sx);
+    *dy = B<double>(ctx, sy);
+    return GEOHIP_OK;
+}
+
+int plan_or_fail(geohip_ctx* ctx, const geohip_grid* grid, double qx, double qy, double r, PointPlan* plan) {
+    if (!grid) return fail(ctx, GEOHIP_ERR_ARG, "null grid");
+    std::string err;
+    int rc = plan_point(*grid, qx, qy, r, plan, nullptr, nullptr, &err);
+    if (rc) return fail(ctx, rc, err);
+    return GEOHIP_OK;
+}
+
+int kpl_for(uint32_t k) { return k <= 64 ? 1 : k <= 128 ? 2 : 4; }
+
+// kNN enqueue shared by the sync and async forms.
+int knn_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
+                double qx, double qy, double r, uint32_t k, double* out_d, unsigned* out_i, unsigned* out_cnt) {
+    if (k == 0) return fail(ctx, GEOHIP_ERR_ARG, "k must be > 0");
+    if (k > GEOHIP_KNN_MAX_K) return fail(ctx, GEOHIP_ERR_UNSUPPORTED, "k > GEOHIP_KNN_MAX_K");
+    if (n >= 0xffffffffull) return fail(ctx, GEOHIP_ERR_UNSUPPORTED, "window larger than 2^32-1 points");
+    PointPlan plan;
+    int rc = plan_or_fail(ctx, grid, qx, qy, r, &plan);
+    if (rc) return rc;
+    KnnArgs a;
+    memset(&a, 0, sizeof a);
+    for (int i = 0; i < plan.nu; i++) a.u[i] = plan.u[i];
+    a.nu = plan.nu;
+    a.k = k;
+    a.qx = qx;
+    a.qy = qy;
+    const double *dx, *dy;
+    rc = stage_xy(ctx, x, y, n, S_X, S_Y, &dx, &dy);
+    if (rc) return rc;
+    const int kpl = kpl_for(k);
+    // 4 blocks per CU target; chunks of whole 1024-point block iterations
+    const uint64_t target_blocks = 1024;
+    uint64_t chunk = (n + target_blocks - 1) / target_blocks;
+    chunk = (chunk + 1023) / 1024 * 1024;
+    if (chunk < 1024) chunk = 1024;
+    uint64_t nblocks = a.nu > 0 ? (n + chunk - 1) / chunk : 0;  // empty G u C: no candidates
+    const uint64_t N = 64ull * kpl;
+    rc = ensure(ctx, S_GTHR, 8);
+    if (!rc) rc = ensure(ctx, S_PART_D, nblocks * N * 8);
+    if (!rc) rc = ensure(ctx, S_PART_I, nblocks * N * 4);
+    if (rc) return rc;
+    hipEvent_t e0, e1;
+    timing_events(ctx, &e0, &e1);
+    hipError_t e = launch_knn(dx, dy, n, a, kpl, B<unsigned long long>(ctx, S_GTHR), B<unsigned long long>(ctx, S_PART_D),
+                              B<unsigned>(ctx, S_PART_I), (unsigned)nblocks, chunk, out_d, out_i, out_cnt, ctx->stream, e0, e1);
+    if (e != hipSuccess) return hip_fail(ctx, e, "knn launch");
+    return GEOHIP_OK;
+}
+
+int range_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n, double qx,
+                  double qy, double r, int approximate, unsigned* out, uint64_t cap, uint64_t* total) {
+    if (n >= 0xffffffffull) return fail(ctx, GEOHIP_ERR_UNSUPPORTED, "window larger than 2^32-1 points");
+    PointPlan plan;
+    int rc = plan_or_fail(ctx, grid, qx, qy, r, &plan);
+    if (rc) return rc;
+    RangeArgs a;
+    memset(&a, 0, sizeof a);
+    for (int i = 0; i < plan.ng; i++) a.g[i] = plan.g[i];
+    a.ng = plan.ng;
+    a.c = plan.c;
+    a.nc = plan.nc;
+    a.qx = qx;
+    a.qy = qy;
+    a.r = r;
+    const double *dx, *dy;
+    rc = stage_xy(ctx, x, y, n, S_X, S_Y, &dx, &dy);
+    if (rc) return rc;
+    const uint64_t units = (n + kRangeUnitPts - 1) / kRangeUnitPts;
+    rc = ensure(ctx, S_MASK, units * 16 * 8);
+    if (!rc) rc = ensure(ctx, S_UCNT, units * 4);
+    if (!rc) rc = ensure(ctx, S_OFFS, units * 8);
+    if (rc) return rc;
+    hipEvent_t e0, e1;
+    timing_events(ctx, &e0, &e1);
+    hipError_t e = launch_range(dx, dy, n, a, approximate, B<unsigned long long>(ctx, S_MASK), B<unsigned>(ctx, S_UCNT),
+                                B<uint64_t>(ctx, S_OFFS), total, out, cap, ctx->stream, e0, e1);
+    if (e != hipSuccess) return hip_fail(ctx, e, "range launch");
+    return GEOHIP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* geohip_version(void) { return "geohip 0.1 (gfx950)"; }
+
+int geohip_device_count(int* out_count) {
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) {
+        (void)hipGetLastError();
+        c = 0;
+    }
+    if (out_count) *out_count = c;
+    return GEOHIP_OK;
+}
+
+int geohip_ctx_create(uint32_t device_mask, geohip_ctx** out_ctx) {
+    if (!out_ctx) return GEOHIP_ERR_ARG;
+    *out_ctx = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        (void)hipGetLastError();
+        return GEOHIP_ERR_DEVICE;
+    }
+    int dev = 0;
+    if (device_mask == 0) {
+        if (hipGetDevice(&dev) != hipSuccess) return GEOHIP_ERR_DEVICE;
+    } else {
+        if (device_mask & (device_mask - 1)) return GEOHIP_ERR_UNSUPPORTED;  // one device per ctx
+        dev = __builtin_ctz(device_mask);
+        if (dev >= ndev) return GEOHIP_ERR_ARG;
+    }
+    geohip_ctx* ctx = new geohip_ctx();
+    ctx->device = dev;
+    if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc((void**)&ctx->pinned, 64, hipHostMallocDefault) != hipSuccess) {
+        delete ctx;
+        return GEOHIP_ERR_DEVICE;
+    }
+    ctx->stream = ctx->own;
+    *out_ctx = ctx;
+    return GEOHIP_OK;
+}
+
+int geohip_ctx_destroy(geohip_ctx* ctx) {
+    if (!ctx) return GEOHIP_ERR_ARG;
+    hipSetDevice(ctx->device);
+    hipStreamSynchronize(ctx->stream);
+    for (int s = 0; s < S_COUNT; s++)
+        if (ctx->buf[s]) hipFree(ctx->buf[s]);
+    for (auto& p : ctx->pending) {
+        hipEventDestroy(p.first);
+        hipEventDestroy(p.second);
+    }
+    for (auto ev : ctx->pool) hipEventDestroy(ev);
+    if (ctx->pinned) hipHostFree(ctx->pinned);
+    if (ctx->own) hipStreamDestroy(ctx->own);
+    delete ctx;
+    return GEOHIP_OK;
+}
+
+const char* geohip_last_error(const geohip_ctx* ctx) { return ctx ? ctx->err.c_str() : "null ctx"; }
+
+int geohip_ctx_set_mem(geohip_ctx* ctx, int mem_kind) {
+    if (!ctx || (mem_kind != GEOHIP_MEM_HOST && mem_kind != GEOHIP_MEM_DEVICE)) return GEOHIP_ERR_ARG;
+    ctx->mem = mem_kind;
+    return GEOHIP_OK;
+}
+
+int geohip_ctx_set_stream(geohip_ctx* ctx, void* hip_stream) {
+    if (!ctx) return GEOHIP_ERR_ARG;
+    ctx->stream = hip_stream ? (hipStream_t)hip_stream : ctx->own;
+    return GEOHIP_OK;
+}
+
+void* geohip_ctx_stream(geohip_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int geohip_ctx_set_timing(geohip_ctx* ctx, int enable) {
+    if (!ctx) return GEOHIP_ERR_ARG;
+    ctx->timing = enable != 0;
+    return GEOHIP_OK;
+}
+
+int geohip_ctx_timing(geohip_ctx* ctx, double* total_ms, uint64_t* launches, int reset) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    for (auto& p : ctx->pending) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, p.first, p.second) == hipSuccess) {
+            ctx->acc_ms += ms;
+            ctx->launches++;
+        } else {
+            (void)hipGetLastError();
+        }
+        ctx->pool.push_back(p.first);
+        ctx->pool.push_back(p.second);
+    }
+    ctx->pending.clear();
+    if (total_ms) *total_ms = ctx->acc_ms;
+    if (launches) *launches = ctx->launches;
+    if (reset) {
+        ctx->acc_ms = 0.0;
+        ctx->launches = 0;
+    }
+    return GEOHIP_OK;
+}
+
+int geohip_range_pp(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
+                    double qx, double qy, double r, int approximate, uint32_t* out_idx, uint64_t cap,
+                    uint64_t* out_count) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    if (!out_count || (cap && !out_idx)) return fail(ctx, GEOHIP_ERR_ARG, "null output");
+    unsigned* out = nullptr;
+    if (ctx->mem == GEOHIP_MEM_DEVICE) {
+        out = out_idx;
+    } else {
+        rc = ensure(ctx, S_OUT_IDX, cap * 4);
+        if (rc) return rc;
+        out = B<unsigned>(ctx, S_OUT_IDX);
+    }
+    rc = ensure(ctx, S_TOTAL, 8);
+    if (rc) return rc;
+    rc = range_enqueue(ctx, grid, x, y, n, qx, qy, r, approximate, out, cap, B<uint64_t>(ctx, S_TOTAL));
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(ctx->pinned, ctx->buf[S_TOTAL], 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    const uint64_t total = ctx->pinned[0];
+    *out_count = total;
+    if (ctx->mem == GEOHIP_MEM_HOST) {
+        const uint64_t m = total < cap ? total : cap;
+        if (m) HIPCHK(hipMemcpy(out_idx, out, m * 4, hipMemcpyDeviceToHost));
+    }
+    if (total > cap) return fail(ctx, GEOHIP_ERR_CAPACITY, "output capacity too small; *out_count = required");
+    return GEOHIP_OK;
+}
+
+int geohip_range_pp_async(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
+                          double qx, double qy, double r, int approximate, uint32_t* out_idx, uint64_t cap,
+                          uint64_t* out_count_dev) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    if (ctx->mem != GEOHIP_MEM_DEVICE) return fail(ctx, GEOHIP_ERR_ARG, "async forms need GEOHIP_MEM_DEVICE");
+    if (!out_count_dev || (cap && !out_idx)) return fail(ctx, GEOHIP_ERR_ARG, "null output");
+    return range_enqueue(ctx, grid, x, y, n, qx, qy, r, approximate, out_idx, cap, out_count_dev);
+}
+
+int geohip_knn_pp(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
+                  double qx, double qy, double r, uint32_t k, uint32_t* out_idx, double* out_dist,
+                  uint32_t* out_count) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    if (!out_idx || !out_dist || !out_count) return fail(ctx, GEOHIP_ERR_ARG, "null output");
+    double* od;
+    unsigned* oi;
+    if (ctx->mem == GEOHIP_MEM_DEVICE) {
+        od = out_dist;
+        oi = out_idx;
+    } else {
+        rc = ensure(ctx, S_OUT_D, (size_t)k * 8);
+        if (!rc) rc = ensure(ctx, S_OUT_I, (size_t)k * 4);
+        if (rc) return rc;
+        od = B<double>(ctx, S_OUT_D);
+        oi = B<unsigned>(ctx, S_OUT_I);
+    }
+    rc = ensure(ctx, S_OUT_CNT, 8);
+    if (rc) return rc;
+    rc = knn_enqueue(ctx, grid, x, y, n, qx, qy, r, k, od, oi, B<unsigned>(ctx, S_OUT_CNT));
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(ctx->pinned, ctx->buf[S_OUT_CNT], 4, hipMemcpyDeviceToHost, ctx->stream));
+    if (ctx->mem == GEOHIP_MEM_HOST) {
+        HIPCHK(hipMemcpyAsync(out_dist, od, (size_t)k * 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipMemcpyAsync(out_idx, oi, (size_t)k * 4, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    *out_count = (uint32_t)(ctx->pinned[0] & 0xffffffffu);
+    return GEOHIP_OK;
+}
+
+int geohip_knn_pp_async(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
+                        double qx, double qy, double r, uint32_t k, uint32_t* out_idx, double* out_dist,
+                        uint32_t* out_count_dev) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    if (ctx->mem != GEOHIP_MEM_DEVICE) return fail(ctx, GEOHIP_ERR_ARG, "async forms need GEOHIP_MEM_DEVICE");
+    if (!out_idx || !out_dist || !out_count_dev) return fail(ctx, GEOHIP_ERR_ARG, "null output");
+    return knn_enqueue(ctx, grid, x, y, n, qx, qy, r, k, out_dist, out_idx, out_count_dev);
+}
+
+int geohip_knn_merge_async(geohip_ctx* ctx, const double* dist, const uint32_t* idx, uint32_t nlists,
+                           uint32_t list_len, uint32_t k, uint32_t* out_idx, double* out_dist,
+                           uint32_t* out_count_dev) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    if (ctx->mem != GEOHIP_MEM_DEVICE) return fail(ctx, GEOHIP_ERR_ARG, "async forms need GEOHIP_MEM_DEVICE");
+    if (k == 0 || k > GEOHIP_KNN_MAX_K) return fail(ctx, GEOHIP_ERR_ARG, "bad k");
+    if (!dist || !idx || !out_idx || !out_dist || !out_count_dev) return fail(ctx, GEOHIP_ERR_ARG, "null pointer");
+    hipError_t e = launch_knn_merge(reinterpret_cast<const unsigned long long*>(dist), idx, nlists, list_len, k,
+                                    out_dist, out_idx, out_count_dev, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "knn merge launch");
+    return GEOHIP_OK;
+}
+
+int geohip_join_pp(geohip_ctx* ctx, const geohip_grid* grid_data, const geohip_grid* grid_query, const double* dx,
+                   const double* dy, uint64_t nd, const double* qx, const double* qy, uint64_t nq, double r,
+                   int approximate, uint32_t* out_pairs, uint64_t cap, uint64_t* out_count) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    return join_pp_impl(ctx, grid_data, grid_query, dx, dy, nd, qx, qy, nq, r, approximate, out_pairs, cap, out_count,
+                        false);
+}
+
+int geohip_join_pp_count_only(geohip_ctx* ctx, const geohip_grid* grid_data, const geohip_grid* grid_query,
+                              const double* dx, const double* dy, uint64_t nd, const double* qx, const double* qy,
+                              uint64_t nq, double r, int approximate, uint64_t* out_count) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    return join_pp_impl(ctx, grid_data, grid_query, dx, dy, nd, qx, qy, nq, r, approximate, nullptr, 0, out_count,
+                        true);
+}
+
+int geohip_range_ppoly(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
+                       const uint32_t* ring_off, const double* vx, const double* vy, uint32_t npoly, double r,
+                       int approximate, uint32_t* out_pairs, uint64_t cap, uint64_t* out_count) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    return ppoly_impl(ctx, grid, x, y, n, ring_off, vx, vy, npoly, r, approximate, out_pairs, cap, out_count);
+}
+
+int geohip_plan_point(const geohip_grid* grid, double qx, double qy, double r, geohip_rect* g_rects, uint32_t* n_g,
+                      geohip_rect* c_rect, uint32_t* n_c, int32_t* layers_g, int32_t* layers_c) {
+    if (!grid || !n_g || !n_c) return GEOHIP_ERR_ARG;
+    PointPlan plan;
+    std::vector<geohip_rect> gr, cr;
+    std::string err;
+    int rc = plan_point(*grid, qx, qy, r, &plan, &gr, &cr, &err);
+    if (rc) return rc;
+    *n_g = (uint32_t)gr.size();
+    *n_c = (uint32_t)cr.size();
+    for (size_t i = 0; i < gr.size() && g_rects; i++) g_rects[i] = gr[i];
+    if (c_rect && !cr.empty()) *c_rect = cr[0];
+    if (layers_g) *layers_g = plan.layers_g;
+    if (layers_c) *layers_c = plan.layers_c;
+    return GEOHIP_OK;
+}
+
+int geohip_plan_cell(const geohip_grid* grid, double x, double y, int32_t* cx, int32_t* cy) {
+    if (!grid || !cx || !cy) return GEOHIP_ERR_ARG;
+    return cell_of(*grid, x, y, cx, cy);
+}
+
+int geohip_synth_uniform_async(geohip_ctx* ctx, double* x, double* y, uint64_t n, uint64_t base, uint64_t seed,
+                               double min_x, double max_x, double min_y, double max_y) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    hipError_t e = launch_synth_uniform(x, y, n, base, seed, min_x, max_x, min_y, max_y, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "synth launch");
+    return GEOHIP_OK;
+}
+
+// Test hook (host only): classify points with the planner's exact boxes, exactly as the
+// kernels do: out[i] = inG | inC << 1 | inU << 2.
+static inline bool host_in_box(const Box& b, double x, double y) {
+    bool bx = (x >= b.xlo) && (x <= b.xhi);
+    bool by = (y >= b.ylo) && (y <= b.yhi);
+    if (b.nan_x) bx = bx || (x != x);
+    if (b.nan_y) by = by || (y != y);
+    return bx && by;
+}
+int geohip_debug_classify(const geohip_grid* grid, double qx, double qy, double r, const double* x, const double* y,
+                          uint64_t n, uint8_t* out) {
+    if (!grid) return GEOHIP_ERR_ARG;
+    PointPlan plan;
+    std::string err;
+    int rc = plan_point(*grid, qx, qy, r, &plan, nullptr, nullptr, &err);
+    if (rc) return rc;
+    for (uint64_t i = 0; i < n; i++) {
+        bool g = false, u = false;
+        for (int b = 0; b < plan.ng; b++) g = g || host_in_box(plan.g[b], x[i], y[i]);
+        for (int b = 0; b < plan.nu; b++) u = u || host_in_box(plan.u[b], x[i], y[i]);
+        const bool c = !g && plan.nc && host_in_box(plan.c, x[i], y[i]);
+        out[i] = (uint8_t)(g | (c << 1) | (u << 2));
+    }
+    return GEOHIP_OK;
+}
+
+// Test hook (not part of the operator surface): fp64 primitive bits on the device.
+int geohip_debug_selftest_fp64(geohip_ctx* ctx, const double* a, const double* b, uint64_t n, double* o_sqrt,
+                               double* o_div, double* o_hypot, double* o_mulsub) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    hipError_t e = launch_selftest_fp64(a, b, n, o_sqrt, o_div, o_hypot, o_mulsub, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "selftest launch");
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return GEOHIP_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ shared with join/ppoly --
+namespace geohip {
+int ctx_fail(geohip_ctx* ctx, int code, const std::string& msg) { return fail(ctx, code, msg); }
+int ctx_ensure(geohip_ctx* ctx, int slot, size_t bytes, void** out) {
+    int rc = ensure(ctx, (Slot)(S_J0 + slot), bytes);
+    if (!rc) *out = ctx->buf[S_J0 + slot];
+    return rc;
+}
+hipStream_t ctx_stream(geohip_ctx* ctx) { return ctx->stream; }
+int ctx_mem(geohip_ctx* ctx) { return ctx->mem; }
+uint64_t* ctx_pinned(geohip_ctx* ctx) { return ctx->pinned; }
+void ctx_timing_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1) { timing_events(ctx, e0, e1); }
+int ctx_stage_xy(geohip_ctx* ctx, const double* x, const double* y, uint64_t n, int which, const double** dx,
+                 const double** dy) {
+    return which == 0 ? stage_xy(ctx, x, y, n, S_X, S_Y, dx, dy) : stage_xy(ctx, x, y, n, S_QX, S_QY, dx, dy);
+}
+}  // namespace geohip

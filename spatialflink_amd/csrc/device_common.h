@@ -1,0 +1,220 @@
+// device_common.h -- gfx950 device helpers shared by the libgeohip kernels.
+//
+// Everything here must be compiled with -ffp-contract=off (no FMA contraction), because
+// the reference evaluates every fp64 expression in Java source order with separately
+// rounded operations.  sqrt/division are IEEE correctly rounded on this path (checked on
+// the device by tests/test_gpu_parity.py::test_fp64_primitives).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "geohip_internal.h"
+
+namespace geohip {
+
+constexpr int kWave = 64;
+constexpr unsigned long long kSentinelD = ~0ull;  // > bits of any distance in [0, MAX_VALUE]
+constexpr unsigned kSentinelI = ~0u;
+constexpr double kDblMax = 1.7976931348623157e308;
+
+// ---------------------------------------------------------------- fdlibm e_hypot -----------
+__device__ __forceinline__ int32_t dhi(double d) { return __double2hiint(d); }
+__device__ __forceinline__ uint32_t dlo(double d) { return (uint32_t)__double2loint(d); }
+__device__ __forceinline__ double dmk(int32_t hi, uint32_t lo) { return __hiloint2double(hi, (int)lo); }
+__device__ __forceinline__ double dsethi(double d, int32_t hi) { return dmk(hi, dlo(d)); }
+
+// JDK 8 StrictMath.hypot (fdlibm 5.3 e_hypot.c) = JTS 1.16.1 Coordinate.distance kernel.
+// The two "medium size" formulas are evaluated by operand selection so a wave does not
+// diverge on which coordinate difference is larger; each selected operand is bitwise the
+// value the corresponding fdlibm branch computes.
+__device__ __forceinline__ double fdlibm_hypot(double x, double y) {
+    int32_t ha = dhi(x) & 0x7fffffff;
+    int32_t hb = dhi(y) & 0x7fffffff;
+    double a, b;
+    if (hb > ha) { a = y; b = x; int32_t j = ha; ha = hb; hb = j; } else { a = x; b = y; }
+    a = dsethi(a, ha);
+    b = dsethi(b, hb);
+    if ((ha - hb) > 0x3c00000) return a + b;
+    int32_t k = 0;
+    if (ha > 0x5f300000) {
+        if (ha >= 0x7ff00000) {
+            double w = a + b;
+            if (((ha & 0xfffff) | dlo(a)) == 0) w = a;
+            if (((hb ^ 0x7ff00000) | dlo(b)) == 0) w = b;
+            return w;
+        }
+        ha -= 0x25800000; hb -= 0x25800000; k += 600;
+        a = dsethi(a, ha);
+        b = dsethi(b, hb);
+    }
+    if (hb < 0x20b00000) {
+        if (hb <= 0x000fffff) {
+            if ((hb | dlo(b)) == 0) return a;
+            double t1 = dmk(0x7fd00000, 0);
+            b *= t1; a *= t1; k -= 1022;   // fdlibm keeps the unscaled ha/hb here
+        } else {
+            ha += 0x25800000; hb += 0x25800000; k -= 600;
+            a = dsethi(a, ha);
+            b = dsethi(b, hb);
+        }
+    }
+    double w = a - b;
+    const bool big = w > b;
+    const double t1 = big ? dmk(ha, 0) : dmk(ha + 0x00100000, 0);
+    const double aa = big ? a : a + a;
+    const double t2 = aa - t1;
+    const double y1 = dmk(hb, 0);
+    const double y2 = b - y1;
+    // big:  sqrt(t1*t1 - (b*(-b) - t2*(a+t1)))
+    // else: sqrt(t1*y1 - (w*(-w) - (t1*y2 + t2*b)))
+    const double P = big ? t1 * t1 : t1 * y1;
+    const double Q = big ? b * (-b) : w * (-w);
+    const double R = big ? t2 * (a + t1) : (t1 * y2 + t2 * b);
+    w = __builtin_sqrt(P - (Q - R));
+    if (k != 0) return dmk(0x3ff00000 + (k << 20), 0) * w;
+    return w;
+}
+
+// p.point.distance(q.point): JTS DistanceOp with minDistance = Double.MAX_VALUE and strict <
+// (DistanceFunctions.java:15-18): NaN / inf / MAX all read as MAX_VALUE.
+__device__ __forceinline__ double jts_pp_distance(double ax, double ay, double bx, double by) {
+    double d = fdlibm_hypot(ax - bx, ay - by);
+    return d < kDblMax ? d : kDblMax;
+}
+
+__device__ __forceinline__ double coord_distance(double ax, double ay, double bx, double by) {
+    return fdlibm_hypot(ax - bx, ay - by);
+}
+
+// ---------------------------------------------------------------- classification ----------
+__device__ __forceinline__ bool in_box(const Box& b, double x, double y) {
+    bool bx = (x >= b.xlo) && (x <= b.xhi);
+    bool by = (y >= b.ylo) && (y <= b.yhi);
+    if (b.nan_x) bx = bx || (x != x);
+    if (b.nan_y) by = by || (y != y);
+    return bx && by;
+}
+
+// ---------------------------------------------------------------- wave64 primitives -------
+__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+
+__device__ __forceinline__ unsigned lanes_below(unsigned long long mask) {
+    return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+}
+
+// Orders LDS traffic of one wave (lanes exchange data through wave-private LDS).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct KE {  // kNN entry: distance bits (monotone for d >= 0) and window index
+    unsigned long long d;
+    unsigned i;
+};
+
+__device__ __forceinline__ bool kless(const KE& a, const KE& b) {
+    return a.d < b.d || (a.d == b.d && a.i < b.i);
+}
+__device__ __forceinline__ KE kxor(const KE& v, int m) {
+    KE r;
+    r.d = __shfl_xor(v.d, m);
+    r.i = __shfl_xor(v.i, m);
+    return r;
+}
+__device__ __forceinline__ KE kfrom(const KE& v, int src) {
+    KE r;
+    r.d = __shfl(v.d, src);
+    r.i = __shfl(v.i, src);
+    return r;
+}
+__device__ __forceinline__ KE ksentinel() {
+    KE r;
+    r.d = kSentinelD;
+    r.i = kSentinelI;
+    return r;
+}
+
+// Bitonic sort of 64 keys held one per lane (ascending by lane).
+__device__ __forceinline__ KE wave_sort64(KE v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+        for (int j = size >> 1; j > 0; j >>= 1) {
+            KE p = kxor(v, j);
+            const bool want_min = ((lane & j) == 0) == ((lane & size) == 0);
+            const bool pl = kless(p, v);
+            if (want_min == pl) v = p;
+        }
+    }
+    return v;
+}
+
+// A KPL*64-entry list: element e = s*64 + lane lives in slot s of that lane.
+template <int KPL>
+struct WList {
+    KE s[KPL];
+};
+
+// Sort a bitonic list ascending (bitonic merge network).
+template <int KPL>
+__device__ __forceinline__ void wave_bitonic_merge(WList<KPL>& L) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int jj = KPL / 2; jj >= 1; jj >>= 1) {  // distances >= 64: in-lane slot pairs
+#pragma unroll
+        for (int s = 0; s < KPL; s++) {
+            if ((s & jj) == 0) {
+                KE a = L.s[s], b = L.s[s | jj];
+                if (kless(b, a)) { L.s[s] = b; L.s[s | jj] = a; }
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 32; j > 0; j >>= 1) {
+#pragma unroll
+        for (int s = 0; s < KPL; s++) {
+            KE p = kxor(L.s[s], j);
+            const bool want_min = (lane & j) == 0;
+            if (want_min == kless(p, L.s[s])) L.s[s] = p;
+        }
+    }
+}
+
+// L <- the KPL*64 smallest of L u B, sorted; B is an ascending list of the same size.
+template <int KPL>
+__device__ __forceinline__ void wave_merge_lists(WList<KPL>& L, const WList<KPL>& B) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int s = 0; s < KPL; s++) {
+        KE rv = kfrom(B.s[KPL - 1 - s], 63 - lane);  // B reversed
+        if (kless(rv, L.s[s])) L.s[s] = rv;
+    }
+    wave_bitonic_merge<KPL>(L);
+}
+
+// L <- smallest of L u batch (64 sorted keys, one per lane), sorted.
+template <int KPL>
+__device__ __forceinline__ void wave_merge_batch(WList<KPL>& L, const KE& sorted_batch) {
+    const int lane = lane_id();
+    KE rv = kfrom(sorted_batch, 63 - lane);
+    if (kless(rv, L.s[KPL - 1])) L.s[KPL - 1] = rv;
+    wave_bitonic_merge<KPL>(L);
+}
+
+template <int KPL>
+__device__ __forceinline__ KE wave_list_get(const WList<KPL>& L, int e) {  // e wave-uniform
+    const int s = e >> 6, l = e & 63;
+    KE r = L.s[0];
+#pragma unroll
+    for (int t = 1; t < KPL; t++)
+        if (t == s) r = L.s[t];
+    KE o;
+    o.d = __shfl(r.d, l);
+    o.i = __shfl(r.i, l);
+    return o;
+}
+
+}  // namespace geohip

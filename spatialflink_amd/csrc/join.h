@@ -1,0 +1,24 @@
+// join.h -- point-point window join (PointPointJoinQuery.java:113-172).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "geohip_internal.h"
+
+namespace geohip {
+// context services implemented in abi.cpp
+int ctx_fail(geohip_ctx* ctx, int code, const std::string& msg);
+int ctx_ensure(geohip_ctx* ctx, int slot, size_t bytes, void** out);  // slot 0..9
+hipStream_t ctx_stream(geohip_ctx* ctx);
+int ctx_mem(geohip_ctx* ctx);
+uint64_t* ctx_pinned(geohip_ctx* ctx);
+void ctx_timing_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1);
+int ctx_stage_xy(geohip_ctx* ctx, const double* x, const double* y, uint64_t n, int which, const double** dx,
+                 const double** dy);
+
+int join_pp_impl(geohip_ctx* ctx, const geohip_grid* grid_data, const geohip_grid* grid_query, const double* dx,
+                 const double* dy, uint64_t nd, const double* qx, const double* qy, uint64_t nq, double r,
+                 int approximate, uint32_t* out_pairs, uint64_t cap, uint64_t* out_count, bool count_only);
+}  // namespace geohip

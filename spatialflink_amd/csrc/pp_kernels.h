@@ -1,0 +1,43 @@
+// pp_kernels.h -- launch interface of the libgeohip kernels (host side).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "geohip_internal.h"
+
+namespace geohip {
+
+struct KnnArgs {
+    Box u[kMaxPointBoxes + 1];  // G u C as boxes
+    int32_t nu;
+    uint32_t k;
+    double qx, qy;
+};
+
+struct RangeArgs {
+    Box g[kMaxPointBoxes];
+    Box c;
+    int32_t ng, nc;
+    double qx, qy, r;
+};
+
+// kNN scan over ceil(n / chunk) = nblocks blocks (chunk a multiple of 256), then the final
+// selection into out_*.  ev0/ev1 (optional) bracket the scan kernel only.
+hipError_t launch_knn(const double* x, const double* y, uint64_t n, const KnnArgs& args, int kpl,
+                      unsigned long long* gthr, unsigned long long* part_d, unsigned* part_i,
+                      unsigned nblocks, uint64_t chunk, double* out_d, unsigned* out_i, unsigned* out_count,
+                      hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
+hipError_t launch_knn_merge(const unsigned long long* d, const unsigned* i, unsigned nlists, unsigned list_len,
+                            unsigned k, double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st);
+// range: bitmask (16 words / 1024 pts), unit_count (units), offs (units) scratch.
+hipError_t launch_range(const double* x, const double* y, uint64_t n, const RangeArgs& a, int approximate,
+                        unsigned long long* bitmask, unsigned* unit_count, uint64_t* offs, uint64_t* total,
+                        unsigned* out, uint64_t cap, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
+hipError_t launch_synth_uniform(double* x, double* y, uint64_t n, uint64_t base, uint64_t seed, double min_x,
+                                double max_x, double min_y, double max_y, hipStream_t st);
+hipError_t launch_selftest_fp64(const double* a, const double* b, uint64_t n, double* o_sqrt, double* o_div,
+                                double* o_hypot, double* o_mulsub, hipStream_t st);
+
+constexpr uint64_t kRangeUnitPts = 1024;
+
+}  // namespace geohip

@@ -1,0 +1,619 @@
+// pp_kernels.hip -- point-query kernels of libgeohip for gfx950 (MI355X).
+//
+// kNN   (PointPointKNNQuery.java:125-191 + KNNQuery.java:204-272):
+//   knn_scan   one HBM pass over SoA x/y: exact box classification (4 compares, no division),
+//              candidates compacted per wave through LDS so fdlibm hypot runs on full waves,
+//              distances pruned by a chip-wide threshold (64-bit atomicMin of any unit's k-th
+//              distance, a valid upper bound of the global k-th), survivors kept in a per-wave
+//              sorted list (64*KPL entries across lanes, bitonic merge of 64-entry batches);
+//              the 4 wave lists of a block are merged into one sorted block list.
+//   knn_final  one workgroup: T = k-th smallest block-list head (an upper bound of the global
+//              k-th key), gather every entry <= T (typically ~k), bitonic sort, emit top-k.
+// range (PointPointRangeQuery.java:86-137):
+//   range_scan   same pass; guaranteed boxes -> hit without distance, candidate boxes ->
+//                compacted distance batches; hits kept as a bitmask per 1024-point unit.
+//   scan_units   exclusive scan of per-unit hit counts.
+//   range_emit   bitmask -> ascending window indices.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "device_common.h"
+#include "pp_kernels.h"
+
+namespace geohip {
+
+constexpr int kBlock = 256;            // 4 waves
+constexpr int kPtsIter = 256;          // points per wave iteration (4 per lane)
+constexpr int kCandCap = 64 + kPtsIter;
+constexpr int kSelCap = 128;
+
+struct WaveStage {  // wave-private LDS
+    double cx[kCandCap];
+    double cy[kCandCap];
+    unsigned ci[kCandCap];
+    unsigned long long sd[kSelCap];
+    unsigned si[kSelCap];
+};
+
+__device__ __forceinline__ void load4(const double* __restrict__ x, const double* __restrict__ y,
+                                      uint64_t base, uint64_t end, int lane, double px[4], double py[4],
+                                      bool valid[4]) {
+    const uint64_t i0 = base + 2 * (uint64_t)lane;
+    const uint64_t i1 = base + 128 + 2 * (uint64_t)lane;
+    if (base + kPtsIter <= end) {
+        const double2 a = *reinterpret_cast<const double2*>(x + i0);
+        const double2 b = *reinterpret_cast<const double2*>(x + i1);
+        const double2 c = *reinterpret_cast<const double2*>(y + i0);
+        const double2 d = *reinterpret_cast<const double2*>(y + i1);
+        px[0] = a.x; px[1] = a.y; px[2] = b.x; px[3] = b.y;
+        py[0] = c.x; py[1] = c.y; py[2] = d.x; py[3] = d.y;
+        valid[0] = valid[1] = valid[2] = valid[3] = true;
+    } else {
+        const uint64_t id[4] = {i0, i0 + 1, i1, i1 + 1};
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            valid[s] = id[s] < end;
+            px[s] = valid[s] ? x[id[s]] : 0.0;
+            py[s] = valid[s] ? y[id[s]] : 0.0;
+        }
+    }
+}
+
+__device__ __forceinline__ uint64_t slot_index(uint64_t base, int lane, int s) {
+    return base + (uint64_t)((s >> 1) * 128 + 2 * lane + (s & 1));
+}
+
+// ============================================================================ kNN =========
+struct KnnWave {
+    unsigned ccnt;       // staged candidates (wave-uniform)
+    unsigned scnt;       // staged selected entries
+    unsigned long long thr;       // local k-th distance bits (sentinel until full)
+    unsigned long long published;
+};
+
+template <int KPL>
+__device__ __forceinline__ void knn_flush_sel(WaveStage& st, KnnWave& w, WList<KPL>& L, unsigned k,
+                                              unsigned long long* gthr, bool partial) {
+    const int lane = lane_id();
+    while (w.scnt >= 64 || (partial && w.scnt > 0)) {
+        const unsigned take = w.scnt >= 64 ? 64u : w.scnt;
+        const unsigned from = w.scnt - take;
+        KE e = ksentinel();
+        if ((unsigned)lane < take) {
+            e.d = st.sd[from + lane];
+            e.i = st.si[from + lane];
+        }
+        wave_lds_sync();
+        w.scnt = from;
+        e = wave_sort64(e);
+        wave_merge_batch<KPL>(L, e);
+        KE kth = wave_list_get<KPL>(L, (int)k - 1);
+        w.thr = kth.d;
+        if (kth.d != kSentinelD && kth.d < w.published) {
+            w.published = kth.d;
+            if (lane == 0) atomicMin(gthr, kth.d);
+        }
+    }
+}
+
+template <int KPL>
+__device__ __forceinline__ void knn_flush_cand(WaveStage& st, KnnWave& w, WList<KPL>& L, unsigned k,
+                                               unsigned long long* gthr, unsigned long long gval,
+                                               double qx, double qy, bool partial) {
+    const int lane = lane_id();
+    while (w.ccnt >= 64 || (partial && w.ccnt > 0)) {
+        const unsigned take = w.ccnt >= 64 ? 64u : w.ccnt;
+        const unsigned from = w.ccnt - take;
+        bool ok = (unsigned)lane < take;
+        double px = 0.0, py = 0.0;
+        unsigned pi = 0;
+        if (ok) {
+            px = st.cx[from + lane];
+            py = st.cy[from + lane];
+            pi = st.ci[from + lane];
+        }
+        wave_lds_sync();
+        w.ccnt = from;
+        const double d = jts_pp_distance(qx, qy, px, py);
+        const unsigned long long db = (unsigned long long)__double_as_longlong(d);
+        const unsigned long long lim = w.thr < gval ? w.thr : gval;
+        ok = ok && db <= lim;
+        const unsigned long long m = __ballot(ok);
+        if (ok) {
+            const unsigned pos = w.scnt + lanes_below(m);
+            st.sd[pos] = db;
+            st.si[pos] = pi;
+        }
+        w.scnt += (unsigned)__popcll(m);
+        wave_lds_sync();
+        if (w.scnt >= 64) knn_flush_sel<KPL>(st, w, L, k, gthr, false);
+    }
+}
+
+template <int KPL>
+__global__ __launch_bounds__(kBlock) void knn_scan(const double* __restrict__ x, const double* __restrict__ y,
+                                                   uint64_t n, uint64_t chunk, KnnArgs args,
+                                                   unsigned long long* __restrict__ gthr,
+                                                   unsigned long long* __restrict__ part_d,
+                                                   unsigned* __restrict__ part_i) {
+    __shared__ WaveStage stage[kBlock / kWave];
+    const int lane = lane_id();
+    const int wid = threadIdx.x / kWave;
+    WaveStage& st = stage[wid];
+    const uint64_t blk_begin = (uint64_t)blockIdx.x * chunk;
+    uint64_t blk_end = blk_begin + chunk;
+    if (blk_end > n) blk_end = n;
+
+    WList<KPL> L;
+#pragma unroll
+    for (int s = 0; s < KPL; s++) L.s[s] = ksentinel();
+    KnnWave w;
+    w.ccnt = 0;
+    w.scnt = 0;
+    w.thr = kSentinelD;
+    w.published = kSentinelD;
+    const unsigned k = args.k;
+
+    for (uint64_t base = blk_begin + (uint64_t)wid * kPtsIter; base < blk_end; base += kBlock / kWave * kPtsIter) {
+        const unsigned long long gval = __hip_atomic_load(gthr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        double px[4], py[4];
+        bool valid[4];
+        load4(x, y, base, blk_end, lane, px, py, valid);
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            bool c = false;
+            for (int b = 0; b < args.nu; b++) c = c || in_box(args.u[b], px[s], py[s]);
+            c = c && valid[s];
+            const unsigned long long m = __ballot(c);
+            if (c) {
+                const unsigned pos = w.ccnt + lanes_below(m);
+                st.cx[pos] = px[s];
+                st.cy[pos] = py[s];
+                st.ci[pos] = (unsigned)slot_index(base, lane, s);
+            }
+            w.ccnt += (unsigned)__popcll(m);
+        }
+        wave_lds_sync();
+        if (w.ccnt >= 64) knn_flush_cand<KPL>(st, w, L, k, gthr, gval, args.qx, args.qy, false);
+    }
+    const unsigned long long gval = __hip_atomic_load(gthr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    knn_flush_cand<KPL>(st, w, L, k, gthr, gval, args.qx, args.qy, true);
+    knn_flush_sel<KPL>(st, w, L, k, gthr, true);
+
+    // block combine: waves 1..3 hand their lists to wave 0 through LDS (reusing the stage)
+    __syncthreads();
+    unsigned long long* ld = reinterpret_cast<unsigned long long*>(&stage[0].cx[0]);
+    unsigned* li = reinterpret_cast<unsigned*>(&stage[2].cx[0]);
+    constexpr int N = 64 * KPL;
+    if (wid > 0) {
+#pragma unroll
+        for (int s = 0; s < KPL; s++) {
+            ld[(wid - 1) * N + s * 64 + lane] = L.s[s].d;
+            li[(wid - 1) * N + s * 64 + lane] = L.s[s].i;
+        }
+    }
+    __syncthreads();
+    if (wid == 0) {
+        for (int o = 0; o < kBlock / kWave - 1; o++) {
+            WList<KPL> B;
+#pragma unroll
+            for (int s = 0; s < KPL; s++) {
+                B.s[s].d = ld[o * N + s * 64 + lane];
+                B.s[s].i = li[o * N + s * 64 + lane];
+            }
+            wave_merge_lists<KPL>(L, B);
+        }
+        const size_t off = (size_t)blockIdx.x * N;
+#pragma unroll
+        for (int s = 0; s < KPL; s++) {
+            part_d[off + s * 64 + lane] = L.s[s].d;
+            part_i[off + s * 64 + lane] = L.s[s].i;
+        }
+        KE kth = wave_list_get<KPL>(L, (int)k - 1);
+        if (lane == 0 && kth.d != kSentinelD) atomicMin(gthr, kth.d);
+    }
+}
+
+// ---------------------------------------------------------------- final selection --------
+constexpr int kFinalThreads = 1024;
+constexpr int kFinalHeads = 4096;
+constexpr int kFinalCap = 4096;
+
+__device__ __forceinline__ bool lds_kless(unsigned long long ad, unsigned ai, unsigned long long bd, unsigned bi) {
+    return ad < bd || (ad == bd && ai < bi);
+}
+
+// bitonic sort of m (power of two) keys in LDS by the whole workgroup
+__device__ void block_sort(unsigned long long* d, unsigned* i, int m) {
+    for (int size = 2; size <= m; size <<= 1) {
+        for (int j = size >> 1; j > 0; j >>= 1) {
+            for (int t = threadIdx.x; t < m / 2; t += blockDim.x) {
+                const int lo = 2 * j * (t / j) + (t % j);
+                const int hi = lo + j;
+                const bool up = (lo & size) == 0;
+                const bool swap = up ? lds_kless(d[hi], i[hi], d[lo], i[lo]) : lds_kless(d[lo], i[lo], d[hi], i[hi]);
+                if (swap) {
+                    unsigned long long td = d[lo]; d[lo] = d[hi]; d[hi] = td;
+                    unsigned ti = i[lo]; i[lo] = i[hi]; i[hi] = ti;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__global__ __launch_bounds__(kFinalThreads) void knn_final(const unsigned long long* __restrict__ part_d,
+                                                           const unsigned* __restrict__ part_i,
+                                                           unsigned nlists, unsigned list_len, unsigned k,
+                                                           double* __restrict__ out_d, unsigned* __restrict__ out_i,
+                                                           unsigned* __restrict__ out_count) {
+    __shared__ unsigned long long hd[kFinalHeads];
+    __shared__ unsigned hi_[kFinalHeads];
+    __shared__ unsigned long long bd[kFinalCap];
+    __shared__ unsigned bi[kFinalCap];
+    __shared__ unsigned cnt;
+    __shared__ unsigned long long Td;
+    __shared__ unsigned Ti;
+
+    unsigned long long T_d = kSentinelD;
+    unsigned T_i = kSentinelI;
+    if (nlists >= k && nlists <= (unsigned)kFinalHeads) {
+        int m = 1;
+        while (m < (int)nlists) m <<= 1;
+        for (int t = threadIdx.x; t < m; t += blockDim.x) {
+            if (t < (int)nlists) {
+                hd[t] = part_d[(size_t)t * list_len];
+                hi_[t] = part_i[(size_t)t * list_len];
+            } else {
+                hd[t] = kSentinelD;
+                hi_[t] = kSentinelI;
+            }
+        }
+        __syncthreads();
+        block_sort(hd, hi_, m);
+        T_d = hd[k - 1];
+        T_i = hi_[k - 1];
+    }
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    // gather every real entry <= T (lists are ascending: stop at the first one above T)
+    for (unsigned p = threadIdx.x; p < nlists; p += blockDim.x) {
+        const size_t off = (size_t)p * list_len;
+        for (unsigned j = 0; j < list_len; j++) {
+            const unsigned long long ed = part_d[off + j];
+            const unsigned ei = part_i[off + j];
+            if (ed == kSentinelD || lds_kless(T_d, T_i, ed, ei)) break;
+            const unsigned pos = atomicAdd(&cnt, 1u);
+            if (pos < (unsigned)kFinalCap) { bd[pos] = ed; bi[pos] = ei; }
+        }
+    }
+    __syncthreads();
+    const unsigned total = cnt;
+    if (total <= (unsigned)kFinalCap) {
+        int m = 1;
+        while (m < (int)total) m <<= 1;
+        for (int t = threadIdx.x + total; t < m; t += blockDim.x) { bd[t] = kSentinelD; bi[t] = kSentinelI; }
+        __syncthreads();
+        block_sort(bd, bi, m);
+        const unsigned outn = total < k ? total : k;
+        for (unsigned t = threadIdx.x; t < k; t += blockDim.x) {
+            if (t < outn) {
+                out_d[t] = __longlong_as_double((long long)bd[t]);
+                out_i[t] = bi[t];
+            } else {
+                out_d[t] = __longlong_as_double((long long)kSentinelD);
+                out_i[t] = kSentinelI;
+            }
+        }
+        if (threadIdx.x == 0) *out_count = outn;
+        return;
+    }
+    // pathological (massive exact ties): k rounds of "smallest key above the previous one"
+    unsigned long long prev_d = 0;
+    unsigned prev_i = 0;
+    bool have_prev = false;
+    unsigned outn = 0;
+    for (unsigned r = 0; r < k; r++) {
+        unsigned long long best_d = kSentinelD;
+        unsigned best_i = kSentinelI;
+        for (size_t t = threadIdx.x; t < (size_t)nlists * list_len; t += blockDim.x) {
+            const unsigned long long ed = part_d[t];
+            const unsigned ei = part_i[t];
+            if (ed == kSentinelD) continue;
+            if (have_prev && !lds_kless(prev_d, prev_i, ed, ei)) continue;
+            if (lds_kless(ed, ei, best_d, best_i)) { best_d = ed; best_i = ei; }
+        }
+        // block argmin through LDS
+        bd[threadIdx.x] = best_d;
+        bi[threadIdx.x] = best_i;
+        __syncthreads();
+        for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+            if ((int)threadIdx.x < s && lds_kless(bd[threadIdx.x + s], bi[threadIdx.x + s], bd[threadIdx.x], bi[threadIdx.x])) {
+                bd[threadIdx.x] = bd[threadIdx.x + s];
+                bi[threadIdx.x] = bi[threadIdx.x + s];
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) { Td = bd[0]; Ti = bi[0]; }
+        __syncthreads();
+        if (Td == kSentinelD) break;
+        if (threadIdx.x == 0) {
+            out_d[r] = __longlong_as_double((long long)Td);
+            out_i[r] = Ti;
+        }
+        prev_d = Td;
+        prev_i = Ti;
+        have_prev = true;
+        outn = r + 1;
+        __syncthreads();
+    }
+    for (unsigned t = outn + threadIdx.x; t < k; t += blockDim.x) {
+        out_d[t] = __longlong_as_double((long long)kSentinelD);
+        out_i[t] = kSentinelI;
+    }
+    if (threadIdx.x == 0) *out_count = outn;
+}
+
+// ============================================================================ range =======
+constexpr int kUnitPts = 1024;  // one wave's unit: 4 iterations of 256 points; 16 mask words
+
+__device__ __forceinline__ unsigned long long spread32(unsigned v) {  // bit b -> bit 2b
+    unsigned long long x = v;
+    x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+    x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+    x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    x = (x | (x << 2)) & 0x3333333333333333ull;
+    x = (x | (x << 1)) & 0x5555555555555555ull;
+    return x;
+}
+
+struct RangeStage {
+    double cx[kCandCap];
+    double cy[kCandCap];
+    unsigned ci[kCandCap];
+    unsigned long long mask[kUnitPts / 64];
+};
+
+__device__ __forceinline__ void range_flush(RangeStage& st, unsigned& ccnt, const RangeArgs& a, uint64_t unit_base,
+                                            bool partial) {
+    const int lane = lane_id();
+    while (ccnt >= 64 || (partial && ccnt > 0)) {
+        const unsigned take = ccnt >= 64 ? 64u : ccnt;
+        const unsigned from = ccnt - take;
+        bool ok = (unsigned)lane < take;
+        double px = 0.0, py = 0.0;
+        unsigned pi = 0;
+        if (ok) {
+            px = st.cx[from + lane];
+            py = st.cy[from + lane];
+            pi = st.ci[from + lane];
+        }
+        wave_lds_sync();
+        ccnt = from;
+        ok = ok && (jts_pp_distance(a.qx, a.qy, px, py) <= a.r);
+        if (ok) {
+            const unsigned off = (unsigned)(pi - unit_base);
+            atomicOr(&st.mask[off >> 6], 1ull << (off & 63));
+        }
+        wave_lds_sync();
+    }
+}
+
+template <bool APPROX>
+__global__ __launch_bounds__(kBlock) void range_scan(const double* __restrict__ x, const double* __restrict__ y,
+                                                     uint64_t n, RangeArgs a,
+                                                     unsigned long long* __restrict__ bitmask,
+                                                     unsigned* __restrict__ unit_count) {
+    __shared__ RangeStage stage[kBlock / kWave];
+    const int lane = lane_id();
+    const int wid = threadIdx.x / kWave;
+    RangeStage& st = stage[wid];
+    const uint64_t unit = (uint64_t)blockIdx.x * (kBlock / kWave) + wid;
+    const uint64_t unit_base = unit * kUnitPts;
+    if (unit_base >= n) return;
+    if (lane < kUnitPts / 64) st.mask[lane] = 0ull;
+    wave_lds_sync();
+    unsigned ccnt = 0;
+    for (int it = 0; it < kUnitPts / kPtsIter; it++) {
+        const uint64_t base = unit_base + (uint64_t)it * kPtsIter;
+        if (base >= n) break;
+        double px[4], py[4];
+        bool valid[4];
+        load4(x, y, base, n, lane, px, py, valid);
+        unsigned long long hb[4];
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            bool g = false;
+            for (int b = 0; b < a.ng; b++) g = g || in_box(a.g[b], px[s], py[s]);
+            const bool c = !g && a.nc && in_box(a.c, px[s], py[s]);
+            const bool hit = valid[s] && (g || (APPROX && c));
+            hb[s] = __ballot(hit);
+            if (!APPROX) {
+                const bool cand = valid[s] && c;
+                const unsigned long long m = __ballot(cand);
+                if (cand) {
+                    const unsigned pos = ccnt + lanes_below(m);
+                    st.cx[pos] = px[s];
+                    st.cy[pos] = py[s];
+                    st.ci[pos] = (unsigned)slot_index(base, lane, s);
+                }
+                ccnt += (unsigned)__popcll(m);
+            }
+        }
+        // iteration word q (0..3) covers points base + 64q .. +63: slots (2h, 2h+1), lane half
+        if (lane < 4) {
+            const int h = lane >> 1, half = lane & 1;
+            const unsigned e = (unsigned)(hb[2 * h] >> (32 * half));
+            const unsigned o = (unsigned)(hb[2 * h + 1] >> (32 * half));
+            const unsigned long long word = spread32(e) | (spread32(o) << 1);
+            if (word) atomicOr(&st.mask[it * 4 + lane], word);
+        }
+        wave_lds_sync();
+        if (!APPROX && ccnt >= 64) range_flush(st, ccnt, a, unit_base, false);
+    }
+    if (!APPROX) range_flush(st, ccnt, a, unit_base, true);
+    wave_lds_sync();
+    unsigned c = 0;
+    if (lane < kUnitPts / 64) {
+        const unsigned long long wv = st.mask[lane];
+        bitmask[unit * (kUnitPts / 64) + lane] = wv;
+        c = (unsigned)__popcll(wv);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if (lane == 0) unit_count[unit] = c;
+}
+
+// exclusive scan of unit counts by one workgroup; total -> *total
+__global__ __launch_bounds__(1024) void scan_units(const unsigned* __restrict__ cnt, uint64_t units,
+                                                   uint64_t* __restrict__ offs, uint64_t* __restrict__ total) {
+    __shared__ uint64_t part[1024];
+    const uint64_t per = (units + blockDim.x - 1) / blockDim.x;
+    const uint64_t b = threadIdx.x * per;
+    uint64_t e = b + per;
+    if (e > units) e = units;
+    uint64_t s = 0;
+    for (uint64_t u = b; u < e; u++) s += cnt[u];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 1; o < (int)blockDim.x; o <<= 1) {
+        uint64_t v = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint64_t run = part[threadIdx.x] - s;
+    for (uint64_t u = b; u < e; u++) {
+        offs[u] = run;
+        run += cnt[u];
+    }
+    if (threadIdx.x == blockDim.x - 1) *total = part[threadIdx.x];
+}
+
+__global__ __launch_bounds__(kBlock) void range_emit(const unsigned long long* __restrict__ bitmask,
+                                                     const uint64_t* __restrict__ offs, uint64_t units,
+                                                     unsigned* __restrict__ out, uint64_t cap) {
+    const int lane = lane_id();
+    const uint64_t unit = (uint64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
+    if (unit >= units) return;
+    const int wq = lane >> 2, q = lane & 3;
+    unsigned bits = (unsigned)((bitmask[unit * 16 + wq] >> (16 * q)) & 0xffffull);
+    const unsigned c = (unsigned)__popc(bits);
+    unsigned incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+    }
+    uint64_t pos = offs[unit] + (incl - c);
+    const unsigned base = (unsigned)(unit * kUnitPts) + (unsigned)(wq * 64 + q * 16);
+    while (bits) {
+        const int b = __builtin_ctz(bits);
+        bits &= bits - 1;
+        if (pos < cap) out[pos] = base + (unsigned)b;
+        pos++;
+    }
+}
+
+// ============================================================================ misc ========
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ double unit_uniform(uint64_t seed, uint64_t k) {
+    return (double)(splitmix64(seed * 0x632BE59BD9B4E019ull + k) >> 11) * 0x1.0p-53;
+}
+
+__global__ void synth_uniform(double* __restrict__ x, double* __restrict__ y, uint64_t n, uint64_t base,
+                              uint64_t seed, double min_x, double rx, double min_y, double ry) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t g = base + i;
+        const double ux = unit_uniform(seed, 2 * g);
+        const double uy = unit_uniform(seed, 2 * g + 1);
+        x[i] = min_x + ux * rx;
+        y[i] = min_y + uy * ry;
+    }
+}
+
+__global__ void selftest_fp64(const double* __restrict__ a, const double* __restrict__ b, uint64_t n,
+                              double* __restrict__ o_sqrt, double* __restrict__ o_div,
+                              double* __restrict__ o_hypot, double* __restrict__ o_mulsub) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const double av = a[i], bv = b[i];
+        o_sqrt[i] = __builtin_sqrt(av < 0 ? -av : av);
+        o_div[i] = av / bv;
+        o_hypot[i] = fdlibm_hypot(av, bv);
+        o_mulsub[i] = av * bv - bv * bv;  // contraction would change these bits
+    }
+}
+
+// ============================================================================ launchers ===
+hipError_t launch_knn(const double* x, const double* y, uint64_t n, const KnnArgs& args, int kpl,
+                      unsigned long long* gthr, unsigned long long* part_d, unsigned* part_i,
+                      unsigned nblocks, uint64_t chunk, double* out_d, unsigned* out_i, unsigned* out_count,
+                      hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+    hipError_t e = hipMemsetAsync(gthr, 0xff, sizeof(unsigned long long), st);
+    if (e != hipSuccess) return e;
+    if (ev0) hipEventRecord(ev0, st);
+    if (nblocks > 0) {
+        switch (kpl) {
+            case 1: knn_scan<1><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, gthr, part_d, part_i); break;
+            case 2: knn_scan<2><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, gthr, part_d, part_i); break;
+            case 4: knn_scan<4><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, gthr, part_d, part_i); break;
+            default: return hipErrorInvalidValue;
+        }
+    }
+    if (ev1) hipEventRecord(ev1, st);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    knn_final<<<1, kFinalThreads, 0, st>>>(part_d, part_i, nblocks, 64u * (unsigned)kpl, args.k, out_d, out_i, out_count);
+    return hipGetLastError();
+}
+
+hipError_t launch_knn_merge(const unsigned long long* d, const unsigned* i, unsigned nlists, unsigned list_len,
+                            unsigned k, double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st) {
+    knn_final<<<1, kFinalThreads, 0, st>>>(d, i, nlists, list_len, k, out_d, out_i, out_count);
+    return hipGetLastError();
+}
+
+hipError_t launch_range(const double* x, const double* y, uint64_t n, const RangeArgs& a, int approximate,
+                        unsigned long long* bitmask, unsigned* unit_count, uint64_t* offs, uint64_t* total,
+                        unsigned* out, uint64_t cap, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+    const uint64_t units = (n + kUnitPts - 1) / kUnitPts;
+    const uint64_t blocks = (units + 3) / 4;
+    if (units == 0) return hipMemsetAsync(total, 0, sizeof(uint64_t), st);
+    if (ev0) hipEventRecord(ev0, st);
+    if (approximate) range_scan<true><<<(unsigned)blocks, kBlock, 0, st>>>(x, y, n, a, bitmask, unit_count);
+    else range_scan<false><<<(unsigned)blocks, kBlock, 0, st>>>(x, y, n, a, bitmask, unit_count);
+    if (ev1) hipEventRecord(ev1, st);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    scan_units<<<1, 1024, 0, st>>>(unit_count, units, offs, total);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    range_emit<<<(unsigned)blocks, kBlock, 0, st>>>(bitmask, offs, units, out, cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_synth_uniform(double* x, double* y, uint64_t n, uint64_t base, uint64_t seed, double min_x,
+                                double max_x, double min_y, double max_y, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    uint64_t blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    synth_uniform<<<(unsigned)blocks, 256, 0, st>>>(x, y, n, base, seed, min_x, max_x - min_x, min_y, max_y - min_y);
+    return hipGetLastError();
+}
+
+hipError_t launch_selftest_fp64(const double* a, const double* b, uint64_t n, double* o_sqrt, double* o_div,
+                                double* o_hypot, double* o_mulsub, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    uint64_t blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    selftest_fp64<<<(unsigned)blocks, 256, 0, st>>>(a, b, n, o_sqrt, o_div, o_hypot, o_mulsub);
+    return hipGetLastError();
+}
+
+}  // namespace geohip

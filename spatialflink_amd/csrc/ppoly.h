@@ -1,0 +1,11 @@
+// ppoly.h -- point-polygon window range query (PointPolygonRangeQuery.java:76-124).
+#pragma once
+#include <stdint.h>
+
+#include "geohip_internal.h"
+
+namespace geohip {
+int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
+               const uint32_t* ring_off, const double* vx, const double* vy, uint32_t npoly, double r,
+               int approximate, uint32_t* out_pairs, uint64_t cap, uint64_t* out_count);
+}  // namespace geohip

@@ -1,0 +1,83 @@
+"""Synthetic window generators: counter-based, so any shard can
+regenerate any slice.  ``uniform`` is bit-identical to ``geohip_synth_uniform_async``."""
+from __future__ import annotations
+
+import numpy as np
+
+BEIJING = (115.5, 117.6, 39.6, 41.1)  # conf/geoflink-conf.yml:20 gridBBox (minX, maxX, minY, maxY)
+README_QUERY = (116.414899, 39.920374)  # README.md:100
+
+_M1 = np.uint64(0x9E3779B97F4A7C15)
+_M2 = np.uint64(0xBF58476D1CE4E5B9)
+_M3 = np.uint64(0x94D049BB133111EB)
+_SEEDMUL = np.uint64(0x632BE59BD9B4E019)
+
+
+def splitmix64(z: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = z + _M1
+        z = (z ^ (z >> np.uint64(30))) * _M2
+        z = (z ^ (z >> np.uint64(27))) * _M3
+        return z ^ (z >> np.uint64(31))
+
+
+def unit_uniform(seed: int, k: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        h = splitmix64(np.uint64(seed) * _SEEDMUL + k.astype(np.uint64))
+    return (h >> np.uint64(11)).astype(np.float64) * (2.0 ** -53)
+
+
+def uniform(n: int, seed: int, bbox=BEIJING, base: int = 0):
+    min_x, max_x, min_y, max_y = bbox
+    g = np.arange(base, base + n, dtype=np.uint64)
+    ux = unit_uniform(seed, np.uint64(2) * g)
+    uy = unit_uniform(seed, np.uint64(2) * g + np.uint64(1))
+    return min_x + ux * (max_x - min_x), min_y + uy * (max_y - min_y)
+
+
+def gaussian_clusters(n: int, seed: int, centres_seed: int = 1000, n_centres: int = 32, sigma: float = 0.1,
+                      bbox=BEIJING):
+    """32 isotropic Gaussian clusters with centres shared across streams (centres_seed),
+    rejection-sampled into the bbox."""
+    min_x, max_x, min_y, max_y = bbox
+    cr = np.random.default_rng(centres_seed)
+    cx = cr.uniform(min_x, max_x, n_centres)
+    cy = cr.uniform(min_y, max_y, n_centres)
+    rng = np.random.default_rng(seed)
+    xs = np.empty(n)
+    ys = np.empty(n)
+    filled = 0
+    while filled < n:
+        m = int((n - filled) * 1.3) + 16
+        c = rng.integers(0, n_centres, m)
+        x = cx[c] + rng.normal(0.0, sigma, m)
+        y = cy[c] + rng.normal(0.0, sigma, m)
+        ok = (x >= min_x) & (x < max_x) & (y >= min_y) & (y < max_y)
+        x, y = x[ok], y[ok]
+        t = min(len(x), n - filled)
+        xs[filled:filled + t] = x[:t]
+        ys[filled:filled + t] = y[:t]
+        filled += t
+    return xs, ys
+
+
+def star_polygons(n_poly: int, seed: int, n_vert: int = 50, bbox=BEIJING, r_min=0.005, r_max=0.02):
+    """n_poly star-shaped rings: centre uniform, n_vert vertices at equal angles with radius
+    R*(1 + 0.3u), R ~ U[r_min, r_max]; ring closed (n_vert + 1 coords).  Returns
+    (ring_off, vx, vy)."""
+    min_x, max_x, min_y, max_y = bbox
+    rng = np.random.default_rng(seed)
+    off = [0]
+    vx, vy = [], []
+    for _ in range(n_poly):
+        cx = rng.uniform(min_x, max_x)
+        cy = rng.uniform(min_y, max_y)
+        R = rng.uniform(r_min, r_max)
+        ang = np.arange(n_vert) * (2 * np.pi / n_vert)
+        rad = R * (1 + 0.3 * rng.uniform(0, 1, n_vert))
+        x = cx + rad * np.cos(ang)
+        y = cy + rad * np.sin(ang)
+        vx.extend(x.tolist() + [x[0]])
+        vy.extend(y.tolist() + [y[0]])
+        off.append(len(vx))
+    return np.array(off, np.uint32), np.array(vx), np.array(vy)
