@@ -27,8 +27,9 @@
  *   - join: pairs (p, q) with cell_uGrid(p) in Nbr_qGrid(q) and dist <= r; r == 0 -> all cells
  *
  * Indices are window-local (0-based position in the caller's arrays) and map back to the
- * caller's Point objects.  Outputs of range/join/ppoly are in ascending (point, query/poly)
- * order for range and ppoly, unordered for join; kNN is ascending (dist, idx).
+ * caller's Point objects.  Range output is in ascending index order; join and point-polygon
+ * outputs are sets (unordered, like the reference's output streams); kNN is ascending
+ * (dist, idx).
  *
  * Memory: the caller owns every buffer; nothing is retained after a call returns.  With
  * GEOHIP_MEM_HOST (default) input/output pointers are host memory; with GEOHIP_MEM_DEVICE
@@ -118,7 +119,7 @@ int geohip_join_pp_count_only(geohip_ctx* ctx, const geohip_grid* grid_data, con
 
 /* npoly single-ring polygons: vertices vx/vy[ring_off[i] .. ring_off[i+1]) as given to
    Polygon(List<List<Coordinate>>, UniformGrid) (ring closed here if open; > 3 coords).
-   out_pairs: 2*cap uint32 (poly_idx, point_idx), ascending. */
+   out_pairs: 2*cap uint32 (poly_idx, point_idx), unordered. */
 int geohip_range_ppoly(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
                        uint64_t n, const uint32_t* ring_off, const double* vx, const double* vy,
                        uint32_t npoly, double r, int approximate,

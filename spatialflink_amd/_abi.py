@@ -59,6 +59,15 @@ class Rect(ctypes.Structure):
     _fields_ = [("x0", c_int32), ("x1", c_int32), ("y0", c_int32), ("y1", c_int32)]
 
 
+# One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64 (SONAME
+# libamdhip64.so.7, loaded under the file name libamdhip64.so).  Loading torch first lets
+# libgeohip's NEEDED libamdhip64.so.7 bind to that same instance; loading libgeohip first
+# would bring /opt/rocm's copy and leave torch with a second runtime that sees no GPU.
+try:  # pragma: no cover - torch is optional for the C-ABI user
+    import torch  # noqa: F401
+except Exception:  # noqa: BLE001
+    torch = None
+
 if not LIB_PATH.exists():
     raise ImportError(f"{LIB_PATH} not built: run `python -m spatialflink_amd.build` (hipcc, gfx950)")
 

@@ -28,8 +28,7 @@ SOURCES = {
     "plan.cpp": ["-x", "c++", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"],
     "abi.cpp": ["-x", "c++", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"],
     "pp_kernels.hip": ["-x", "hip", f"--offload-arch={ARCH}"],
-    "join.hip": ["-x", "hip", f"--offload-arch={ARCH}"],
-    "ppoly.hip": ["-x", "hip", f"--offload-arch={ARCH}"],
+    "cell_kernels.hip": ["-x", "hip", f"--offload-arch={ARCH}"],
 }
 
 

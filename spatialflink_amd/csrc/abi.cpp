@@ -22,7 +22,7 @@ using namespace geohip;
 enum Slot {
     S_X, S_Y, S_QX, S_QY, S_GTHR, S_PART_D, S_PART_I, S_OUT_D, S_OUT_I, S_OUT_CNT,
     S_MASK, S_UCNT, S_OFFS, S_TOTAL, S_OUT_IDX, S_OUT_PAIRS,
-    S_J0, S_J1, S_J2, S_J3, S_J4, S_J5, S_J6, S_J7, S_J8, S_J9,
+    S_J0, S_J1, S_J2, S_J3, S_J4, S_J5, S_J6, S_J7, S_J8, S_J9, S_J10, S_J11, S_J12, S_J13, S_J14, S_J15,
     S_COUNT
 };
 
@@ -174,14 +174,13 @@ int knn_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const
     if (chunk < 1024) chunk = 1024;
     uint64_t nblocks = a.nu > 0 ? (n + chunk - 1) / chunk : 0;  // empty G u C: no candidates
     const uint64_t N = 64ull * kpl;
-    rc = ensure(ctx, S_GTHR, 8);
-    if (!rc) rc = ensure(ctx, S_PART_D, nblocks * N * 8);
+    rc = ensure(ctx, S_PART_D, nblocks * N * 8);
     if (!rc) rc = ensure(ctx, S_PART_I, nblocks * N * 4);
     if (rc) return rc;
     hipEvent_t e0, e1;
     timing_events(ctx, &e0, &e1);
-    hipError_t e = launch_knn(dx, dy, n, a, kpl, B<unsigned long long>(ctx, S_GTHR), B<unsigned long long>(ctx, S_PART_D),
-                              B<unsigned>(ctx, S_PART_I), (unsigned)nblocks, chunk, out_d, out_i, out_cnt, ctx->stream, e0, e1);
+    hipError_t e = launch_knn(dx, dy, n, a, kpl, B<unsigned long long>(ctx, S_PART_D), B<unsigned>(ctx, S_PART_I),
+                              (unsigned)nblocks, chunk, out_d, out_i, out_cnt, ctx->stream, e0, e1);
     if (e != hipSuccess) return hip_fail(ctx, e, "knn launch");
     return GEOHIP_OK;
 }

@@ -204,6 +204,38 @@ __device__ __forceinline__ void wave_merge_batch(WList<KPL>& L, const KE& sorted
     wave_bitonic_merge<KPL>(L);
 }
 
+// Full bitonic sort of a KPL*64-entry list (element e = s*64 + lane), ascending.
+template <int KPL>
+__device__ __forceinline__ void wave_sort_list(WList<KPL>& L) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int size = 2; size <= 64 * KPL; size <<= 1) {
+#pragma unroll
+        for (int j = size >> 1; j > 0; j >>= 1) {
+            if (j >= 64) {
+                const int jj = j >> 6;
+#pragma unroll
+                for (int s = 0; s < KPL; s++) {
+                    if ((s & jj) == 0) {
+                        const bool up = ((s * 64) & size) == 0;
+                        KE a = L.s[s], b = L.s[s | jj];
+                        if (kless(b, a) == up) { L.s[s] = b; L.s[s | jj] = a; }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int s = 0; s < KPL; s++) {
+                    const int e = s * 64 + lane;
+                    const bool up = (e & size) == 0;
+                    KE p = kxor(L.s[s], j);
+                    const bool want_min = ((lane & j) == 0) == up;
+                    if (want_min == kless(p, L.s[s])) L.s[s] = p;
+                }
+            }
+        }
+    }
+}
+
 template <int KPL>
 __device__ __forceinline__ KE wave_list_get(const WList<KPL>& L, int e) {  // e wave-uniform
     const int s = e >> 6, l = e & 63;

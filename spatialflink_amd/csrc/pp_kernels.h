@@ -21,12 +21,11 @@ struct RangeArgs {
     double qx, qy, r;
 };
 
-// kNN scan over ceil(n / chunk) = nblocks blocks (chunk a multiple of 256), then the final
+// kNN scan over ceil(n / chunk) = nblocks blocks (chunk a multiple of 1024), then the final
 // selection into out_*.  ev0/ev1 (optional) bracket the scan kernel only.
 hipError_t launch_knn(const double* x, const double* y, uint64_t n, const KnnArgs& args, int kpl,
-                      unsigned long long* gthr, unsigned long long* part_d, unsigned* part_i,
-                      unsigned nblocks, uint64_t chunk, double* out_d, unsigned* out_i, unsigned* out_count,
-                      hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
+                      unsigned long long* part_d, unsigned* part_i, unsigned nblocks, uint64_t chunk, double* out_d,
+                      unsigned* out_i, unsigned* out_count, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_knn_merge(const unsigned long long* d, const unsigned* i, unsigned nlists, unsigned list_len,
                             unsigned k, double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st);
 // range: bitmask (16 words / 1024 pts), unit_count (units), offs (units) scratch.

@@ -3,12 +3,13 @@
 // kNN   (PointPointKNNQuery.java:125-191 + KNNQuery.java:204-272):
 //   knn_scan   one HBM pass over SoA x/y: exact box classification (4 compares, no division),
 //              candidates compacted per wave through LDS so fdlibm hypot runs on full waves,
-//              distances pruned by a chip-wide threshold (64-bit atomicMin of any unit's k-th
-//              distance, a valid upper bound of the global k-th), survivors kept in a per-wave
-//              sorted list (64*KPL entries across lanes, bitonic merge of 64-entry batches);
-//              the 4 wave lists of a block are merged into one sorted block list.
+//              distances pruned by a block-wide threshold (LDS min of the waves' k-th distance,
+//              a valid upper bound of the block's k-th), survivors kept in a per-wave sorted
+//              list (64*KPL entries across lanes, bitonic merge of 64-entry batches); the 4
+//              wave lists of a block are merged into one sorted block list.
 //   knn_final  one workgroup: T = k-th smallest block-list head (an upper bound of the global
-//              k-th key), gather every entry <= T (typically ~k), bitonic sort, emit top-k.
+//              k-th key; register sorts + LDS merge tree), gather every entry <= T (typically
+//              ~k), one-wave register bitonic sort, emit top-k.
 // range (PointPointRangeQuery.java:86-137):
 //   range_scan   same pass; guaranteed boxes -> hit without distance, candidate boxes ->
 //                compacted distance batches; hits kept as a bitmask per 1024-point unit.
@@ -65,15 +66,18 @@ __device__ __forceinline__ uint64_t slot_index(uint64_t base, int lane, int s) {
 
 // ============================================================================ kNN =========
 struct KnnWave {
-    unsigned ccnt;       // staged candidates (wave-uniform)
-    unsigned scnt;       // staged selected entries
-    unsigned long long thr;       // local k-th distance bits (sentinel until full)
-    unsigned long long published;
+    unsigned ccnt;                 // staged candidates (wave-uniform)
+    unsigned scnt;                 // staged selected entries
+    unsigned long long thr;        // local k-th distance bits (sentinel until full)
+    unsigned long long published;  // last value pushed to the block threshold
 };
 
+// Block-wide pruning threshold: min over the block's waves of their k-th distance.  Shared
+// through one LDS word (ds_min_u64), never through global memory: a chip-wide atomic word
+// serialises thousands of updates on one L2 line (measured 523 us per 10M-point scan).
 template <int KPL>
 __device__ __forceinline__ void knn_flush_sel(WaveStage& st, KnnWave& w, WList<KPL>& L, unsigned k,
-                                              unsigned long long* gthr, bool partial) {
+                                              unsigned long long* bthr, bool partial) {
     const int lane = lane_id();
     while (w.scnt >= 64 || (partial && w.scnt > 0)) {
         const unsigned take = w.scnt >= 64 ? 64u : w.scnt;
@@ -91,15 +95,14 @@ __device__ __forceinline__ void knn_flush_sel(WaveStage& st, KnnWave& w, WList<K
         w.thr = kth.d;
         if (kth.d != kSentinelD && kth.d < w.published) {
             w.published = kth.d;
-            if (lane == 0) atomicMin(gthr, kth.d);
+            if (lane == 0) atomicMin(bthr, kth.d);
         }
     }
 }
 
 template <int KPL>
 __device__ __forceinline__ void knn_flush_cand(WaveStage& st, KnnWave& w, WList<KPL>& L, unsigned k,
-                                               unsigned long long* gthr, unsigned long long gval,
-                                               double qx, double qy, bool partial) {
+                                               unsigned long long* bthr, double qx, double qy, bool partial) {
     const int lane = lane_id();
     while (w.ccnt >= 64 || (partial && w.ccnt > 0)) {
         const unsigned take = w.ccnt >= 64 ? 64u : w.ccnt;
@@ -112,11 +115,12 @@ __device__ __forceinline__ void knn_flush_cand(WaveStage& st, KnnWave& w, WList<
             py = st.cy[from + lane];
             pi = st.ci[from + lane];
         }
+        const unsigned long long bval = *reinterpret_cast<volatile unsigned long long*>(bthr);
         wave_lds_sync();
         w.ccnt = from;
         const double d = jts_pp_distance(qx, qy, px, py);
         const unsigned long long db = (unsigned long long)__double_as_longlong(d);
-        const unsigned long long lim = w.thr < gval ? w.thr : gval;
+        const unsigned long long lim = w.thr < bval ? w.thr : bval;
         ok = ok && db <= lim;
         const unsigned long long m = __ballot(ok);
         if (ok) {
@@ -126,23 +130,25 @@ __device__ __forceinline__ void knn_flush_cand(WaveStage& st, KnnWave& w, WList<
         }
         w.scnt += (unsigned)__popcll(m);
         wave_lds_sync();
-        if (w.scnt >= 64) knn_flush_sel<KPL>(st, w, L, k, gthr, false);
+        if (w.scnt >= 64) knn_flush_sel<KPL>(st, w, L, k, bthr, false);
     }
 }
 
 template <int KPL>
 __global__ __launch_bounds__(kBlock) void knn_scan(const double* __restrict__ x, const double* __restrict__ y,
                                                    uint64_t n, uint64_t chunk, KnnArgs args,
-                                                   unsigned long long* __restrict__ gthr,
                                                    unsigned long long* __restrict__ part_d,
                                                    unsigned* __restrict__ part_i) {
     __shared__ WaveStage stage[kBlock / kWave];
+    __shared__ unsigned long long bthr;
     const int lane = lane_id();
     const int wid = threadIdx.x / kWave;
     WaveStage& st = stage[wid];
     const uint64_t blk_begin = (uint64_t)blockIdx.x * chunk;
     uint64_t blk_end = blk_begin + chunk;
     if (blk_end > n) blk_end = n;
+    if (threadIdx.x == 0) bthr = kSentinelD;
+    __syncthreads();
 
     WList<KPL> L;
 #pragma unroll
@@ -155,7 +161,6 @@ __global__ __launch_bounds__(kBlock) void knn_scan(const double* __restrict__ x,
     const unsigned k = args.k;
 
     for (uint64_t base = blk_begin + (uint64_t)wid * kPtsIter; base < blk_end; base += kBlock / kWave * kPtsIter) {
-        const unsigned long long gval = __hip_atomic_load(gthr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         double px[4], py[4];
         bool valid[4];
         load4(x, y, base, blk_end, lane, px, py, valid);
@@ -174,11 +179,10 @@ __global__ __launch_bounds__(kBlock) void knn_scan(const double* __restrict__ x,
             w.ccnt += (unsigned)__popcll(m);
         }
         wave_lds_sync();
-        if (w.ccnt >= 64) knn_flush_cand<KPL>(st, w, L, k, gthr, gval, args.qx, args.qy, false);
+        if (w.ccnt >= 64) knn_flush_cand<KPL>(st, w, L, k, &bthr, args.qx, args.qy, false);
     }
-    const unsigned long long gval = __hip_atomic_load(gthr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    knn_flush_cand<KPL>(st, w, L, k, gthr, gval, args.qx, args.qy, true);
-    knn_flush_sel<KPL>(st, w, L, k, gthr, true);
+    knn_flush_cand<KPL>(st, w, L, k, &bthr, args.qx, args.qy, true);
+    knn_flush_sel<KPL>(st, w, L, k, &bthr, true);
 
     // block combine: waves 1..3 hand their lists to wave 0 through LDS (reusing the stage)
     __syncthreads();
@@ -209,21 +213,24 @@ __global__ __launch_bounds__(kBlock) void knn_scan(const double* __restrict__ x,
             part_d[off + s * 64 + lane] = L.s[s].d;
             part_i[off + s * 64 + lane] = L.s[s].i;
         }
-        KE kth = wave_list_get<KPL>(L, (int)k - 1);
-        if (lane == 0 && kth.d != kSentinelD) atomicMin(gthr, kth.d);
     }
 }
 
 // ---------------------------------------------------------------- final selection --------
+// One workgroup of 16 waves.  (1) every wave sorts 64 list heads in registers and the 16
+// sorted runs are merged by a 4-level tree through LDS: T = k-th smallest head, an upper
+// bound of the global k-th key (the k smallest heads are k real entries).  (2) every entry
+// <= T is gathered (lists are ascending: a scan stops at the first entry above T; typically
+// ~k entries in all).  (3) one wave sorts them in registers and writes the top k.
 constexpr int kFinalThreads = 1024;
-constexpr int kFinalHeads = 4096;
+constexpr int kFinalWaves = kFinalThreads / kWave;
 constexpr int kFinalCap = 4096;
 
 __device__ __forceinline__ bool lds_kless(unsigned long long ad, unsigned ai, unsigned long long bd, unsigned bi) {
     return ad < bd || (ad == bd && ai < bi);
 }
 
-// bitonic sort of m (power of two) keys in LDS by the whole workgroup
+// bitonic sort of m (power of two) keys in LDS by the whole workgroup (fallback path)
 __device__ void block_sort(unsigned long long* d, unsigned* i, int m) {
     for (int size = 2; size <= m; size <<= 1) {
         for (int j = size >> 1; j > 0; j >>= 1) {
@@ -242,41 +249,78 @@ __device__ void block_sort(unsigned long long* d, unsigned* i, int m) {
     }
 }
 
+template <int KPL>
 __global__ __launch_bounds__(kFinalThreads) void knn_final(const unsigned long long* __restrict__ part_d,
                                                            const unsigned* __restrict__ part_i,
                                                            unsigned nlists, unsigned list_len, unsigned k,
                                                            double* __restrict__ out_d, unsigned* __restrict__ out_i,
                                                            unsigned* __restrict__ out_count) {
-    __shared__ unsigned long long hd[kFinalHeads];
-    __shared__ unsigned hi_[kFinalHeads];
+    constexpr int N = 64 * KPL;
+    constexpr int KPL2 = 2 * KPL;
+    __shared__ unsigned long long xd[kFinalWaves / 2 * N];
+    __shared__ unsigned xi[kFinalWaves / 2 * N];
     __shared__ unsigned long long bd[kFinalCap];
     __shared__ unsigned bi[kFinalCap];
     __shared__ unsigned cnt;
     __shared__ unsigned long long Td;
     __shared__ unsigned Ti;
+    const int lane = lane_id();
+    const int wid = threadIdx.x / kWave;
 
-    unsigned long long T_d = kSentinelD;
-    unsigned T_i = kSentinelI;
-    if (nlists >= k && nlists <= (unsigned)kFinalHeads) {
-        int m = 1;
-        while (m < (int)nlists) m <<= 1;
-        for (int t = threadIdx.x; t < m; t += blockDim.x) {
-            if (t < (int)nlists) {
-                hd[t] = part_d[(size_t)t * list_len];
-                hi_[t] = part_i[(size_t)t * list_len];
-            } else {
-                hd[t] = kSentinelD;
-                hi_[t] = kSentinelI;
+    // (1) T = k-th smallest head
+    if (threadIdx.x == 0) {
+        cnt = 0;
+        Td = kSentinelD;
+        Ti = kSentinelI;
+    }
+    if (nlists >= k) {
+        WList<KPL> L;
+#pragma unroll
+        for (int s = 0; s < KPL; s++) L.s[s] = ksentinel();
+        for (unsigned g = (unsigned)wid * 64; g < nlists; g += kFinalThreads) {
+            KE h = ksentinel();
+            const unsigned p = g + lane;
+            if (p < nlists) {
+                h.d = part_d[(size_t)p * list_len];
+                h.i = part_i[(size_t)p * list_len];
+            }
+            h = wave_sort64(h);
+            wave_merge_batch<KPL>(L, h);
+        }
+        for (int step = 1; step < kFinalWaves; step <<= 1) {
+            __syncthreads();
+            if ((wid & (2 * step - 1)) == step) {  // sender
+                const int slot = wid >> 1;
+#pragma unroll
+                for (int s = 0; s < KPL; s++) {
+                    xd[slot * N + s * 64 + lane] = L.s[s].d;
+                    xi[slot * N + s * 64 + lane] = L.s[s].i;
+                }
+            }
+            __syncthreads();
+            if ((wid & (2 * step - 1)) == 0) {  // receiver of wid + step
+                const int slot = (wid + step) >> 1;
+                WList<KPL> B;
+#pragma unroll
+                for (int s = 0; s < KPL; s++) {
+                    B.s[s].d = xd[slot * N + s * 64 + lane];
+                    B.s[s].i = xi[slot * N + s * 64 + lane];
+                }
+                wave_merge_lists<KPL>(L, B);
             }
         }
-        __syncthreads();
-        block_sort(hd, hi_, m);
-        T_d = hd[k - 1];
-        T_i = hi_[k - 1];
+        if (wid == 0) {
+            KE t = wave_list_get<KPL>(L, (int)k - 1);
+            if (lane == 0) {
+                Td = t.d;
+                Ti = t.i;
+            }
+        }
     }
-    if (threadIdx.x == 0) cnt = 0;
     __syncthreads();
-    // gather every real entry <= T (lists are ascending: stop at the first one above T)
+    const unsigned long long T_d = Td;
+    const unsigned T_i = Ti;
+    // (2) gather every real entry <= T
     for (unsigned p = threadIdx.x; p < nlists; p += blockDim.x) {
         const size_t off = (size_t)p * list_len;
         for (unsigned j = 0; j < list_len; j++) {
@@ -289,21 +333,39 @@ __global__ __launch_bounds__(kFinalThreads) void knn_final(const unsigned long l
     }
     __syncthreads();
     const unsigned total = cnt;
+    const unsigned outn = total < k ? total : k;
+    if (total <= (unsigned)(64 * KPL2)) {
+        // (3) one wave: register bitonic sort of <= 128*KPL entries
+        if (wid == 0) {
+            WList<KPL2> S;
+#pragma unroll
+            for (int s = 0; s < KPL2; s++) {
+                const unsigned e = (unsigned)(s * 64 + lane);
+                S.s[s] = ksentinel();
+                if (e < total) { S.s[s].d = bd[e]; S.s[s].i = bi[e]; }
+            }
+            wave_sort_list<KPL2>(S);
+#pragma unroll
+            for (int s = 0; s < KPL2; s++) {
+                const unsigned e = (unsigned)(s * 64 + lane);
+                if (e < k) {
+                    out_d[e] = __longlong_as_double((long long)(e < outn ? S.s[s].d : kSentinelD));
+                    out_i[e] = e < outn ? S.s[s].i : kSentinelI;
+                }
+            }
+            if (lane == 0) *out_count = outn;
+        }
+        return;
+    }
     if (total <= (unsigned)kFinalCap) {
         int m = 1;
         while (m < (int)total) m <<= 1;
         for (int t = threadIdx.x + total; t < m; t += blockDim.x) { bd[t] = kSentinelD; bi[t] = kSentinelI; }
         __syncthreads();
         block_sort(bd, bi, m);
-        const unsigned outn = total < k ? total : k;
         for (unsigned t = threadIdx.x; t < k; t += blockDim.x) {
-            if (t < outn) {
-                out_d[t] = __longlong_as_double((long long)bd[t]);
-                out_i[t] = bi[t];
-            } else {
-                out_d[t] = __longlong_as_double((long long)kSentinelD);
-                out_i[t] = kSentinelI;
-            }
+            out_d[t] = __longlong_as_double((long long)(t < outn ? bd[t] : kSentinelD));
+            out_i[t] = t < outn ? bi[t] : kSentinelI;
         }
         if (threadIdx.x == 0) *out_count = outn;
         return;
@@ -312,7 +374,7 @@ __global__ __launch_bounds__(kFinalThreads) void knn_final(const unsigned long l
     unsigned long long prev_d = 0;
     unsigned prev_i = 0;
     bool have_prev = false;
-    unsigned outn = 0;
+    unsigned got = 0;
     for (unsigned r = 0; r < k; r++) {
         unsigned long long best_d = kSentinelD;
         unsigned best_i = kSentinelI;
@@ -323,7 +385,6 @@ __global__ __launch_bounds__(kFinalThreads) void knn_final(const unsigned long l
             if (have_prev && !lds_kless(prev_d, prev_i, ed, ei)) continue;
             if (lds_kless(ed, ei, best_d, best_i)) { best_d = ed; best_i = ei; }
         }
-        // block argmin through LDS
         bd[threadIdx.x] = best_d;
         bi[threadIdx.x] = best_i;
         __syncthreads();
@@ -336,22 +397,24 @@ __global__ __launch_bounds__(kFinalThreads) void knn_final(const unsigned long l
         }
         if (threadIdx.x == 0) { Td = bd[0]; Ti = bi[0]; }
         __syncthreads();
-        if (Td == kSentinelD) break;
-        if (threadIdx.x == 0) {
-            out_d[r] = __longlong_as_double((long long)Td);
-            out_i[r] = Ti;
-        }
-        prev_d = Td;
-        prev_i = Ti;
-        have_prev = true;
-        outn = r + 1;
+        const unsigned long long vd = Td;
+        const unsigned vi = Ti;
         __syncthreads();
+        if (vd == kSentinelD) break;
+        if (threadIdx.x == 0) {
+            out_d[r] = __longlong_as_double((long long)vd);
+            out_i[r] = vi;
+        }
+        prev_d = vd;
+        prev_i = vi;
+        have_prev = true;
+        got = r + 1;
     }
-    for (unsigned t = outn + threadIdx.x; t < k; t += blockDim.x) {
+    for (unsigned t = got + threadIdx.x; t < k; t += blockDim.x) {
         out_d[t] = __longlong_as_double((long long)kSentinelD);
         out_i[t] = kSentinelI;
     }
-    if (threadIdx.x == 0) *out_count = outn;
+    if (threadIdx.x == 0) *out_count = got;
 }
 
 // ============================================================================ range =======
@@ -552,30 +615,28 @@ __global__ void selftest_fp64(const double* __restrict__ a, const double* __rest
 
 // ============================================================================ launchers ===
 hipError_t launch_knn(const double* x, const double* y, uint64_t n, const KnnArgs& args, int kpl,
-                      unsigned long long* gthr, unsigned long long* part_d, unsigned* part_i,
-                      unsigned nblocks, uint64_t chunk, double* out_d, unsigned* out_i, unsigned* out_count,
-                      hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
-    hipError_t e = hipMemsetAsync(gthr, 0xff, sizeof(unsigned long long), st);
-    if (e != hipSuccess) return e;
+                      unsigned long long* part_d, unsigned* part_i, unsigned nblocks, uint64_t chunk, double* out_d,
+                      unsigned* out_i, unsigned* out_count, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
     if (ev0) hipEventRecord(ev0, st);
     if (nblocks > 0) {
         switch (kpl) {
-            case 1: knn_scan<1><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, gthr, part_d, part_i); break;
-            case 2: knn_scan<2><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, gthr, part_d, part_i); break;
-            case 4: knn_scan<4><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, gthr, part_d, part_i); break;
+            case 1: knn_scan<1><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i); break;
+            case 2: knn_scan<2><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i); break;
+            case 4: knn_scan<4><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i); break;
             default: return hipErrorInvalidValue;
         }
     }
     if (ev1) hipEventRecord(ev1, st);
-    e = hipGetLastError();
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    knn_final<<<1, kFinalThreads, 0, st>>>(part_d, part_i, nblocks, 64u * (unsigned)kpl, args.k, out_d, out_i, out_count);
-    return hipGetLastError();
+    return launch_knn_merge(part_d, part_i, nblocks, 64u * (unsigned)kpl, args.k, out_d, out_i, out_count, st);
 }
 
 hipError_t launch_knn_merge(const unsigned long long* d, const unsigned* i, unsigned nlists, unsigned list_len,
                             unsigned k, double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st) {
-    knn_final<<<1, kFinalThreads, 0, st>>>(d, i, nlists, list_len, k, out_d, out_i, out_count);
+    if (k <= 64) knn_final<1><<<1, kFinalThreads, 0, st>>>(d, i, nlists, list_len, k, out_d, out_i, out_count);
+    else if (k <= 128) knn_final<2><<<1, kFinalThreads, 0, st>>>(d, i, nlists, list_len, k, out_d, out_i, out_count);
+    else knn_final<4><<<1, kFinalThreads, 0, st>>>(d, i, nlists, list_len, k, out_d, out_i, out_count);
     return hipGetLastError();
 }
 

@@ -250,3 +250,94 @@ def test_operator_api(ctx):
     oi, od = PointPointKNNQuery(conf, grid, ctx).run(w, Point(*Q), 0.5, 10)
     wi, _ = cref.knn_pp(cg, x, y, Q[0], Q[1], 0.5, 10)
     assert oi.tolist() == wi.tolist()
+
+
+# ------------------------------------------------------------------ join -----------------
+def test_join_golden(ctx, golden):
+    for c in golden["join_pp"]:
+        g = _abi.make_grid(*grid_vals(c["grid"]))
+        got = ctx.join_pp(g, g, arr(c["dx"]), arr(c["dy"]), arr(c["qx"]), arr(c["qy"]), fx(c["r"]), c["approximate"])
+        assert pairs_sorted(got).tolist() == c["expect"]
+
+
+JOIN_CASES = [(500, 0.05, False, 1.0), (500, 0.05, True, 1.0), (100, 0.1, False, 0.1), (200, 0.0, False, 1.0),
+              (500, 0.02, False, 0.05)]
+
+
+@pytest.mark.parametrize("case", range(len(JOIN_CASES)))
+def test_join_random(ctx, case):
+    gn, r, approx, sigma = JOIN_CASES[case]
+    dx, dy = synth.gaussian_clusters(60000, 3 + case, sigma=sigma)
+    qx, qy = synth.gaussian_clusters(300, 40 + case, sigma=sigma)
+    if r == 0.0:
+        dx[:50] = qx[:50]
+        dy[:50] = qy[:50]
+    ag, cg = agrid(gn)
+    got = ctx.join_pp(ag, ag, dx, dy, qx, qy, r, approx)
+    want = cref.join_pp(cg, cg, dx, dy, qx, qy, r, approx)
+    assert pairs_sorted(got).tolist() == pairs_sorted(want).tolist()
+
+
+def test_join_two_grids_and_errors(ctx):
+    rng = np.random.default_rng(8)
+    dx, dy = _window(rng, 30000, nan_every=101)
+    qx, qy = _window(rng, 200)
+    ag1, cg1 = agrid(100)
+    ag2, cg2 = agrid(37)
+    got = ctx.join_pp(ag1, ag2, dx, dy, qx, qy, 0.07)
+    want = cref.join_pp(cg1, cg2, dx, dy, qx, qy, 0.07)
+    assert pairs_sorted(got).tolist() == pairs_sorted(want).tolist()
+    with pytest.raises(_abi.GeohipArgumentError):  # System.exit(1) in getNeighboringCells
+        ctx.join_pp(ag1, ag1, dx, dy, qx, qy, -0.1)
+    with pytest.raises(_abi.GeohipArgumentError):
+        ctx.join_pp(ag1, ag1, dx, dy, qx, qy, math.nan)
+    assert ctx.join_pp_count(ag1, ag1, dx, dy, qx, qy, 0.07) == len(want)
+
+
+# ------------------------------------------------------------------ point-polygon --------
+def test_ppoly_golden(ctx, golden):
+    for c in golden["range_ppoly"]:
+        g = _abi.make_grid(*grid_vals(c["grid"]))
+        off, vx, vy = [0], [], []
+        for ring in c["rings"]:
+            vx += [fx(a) for a, _ in ring]
+            vy += [fx(b) for _, b in ring]
+            off.append(len(vx))
+        got = ctx.range_ppoly(g, arr(c["x"]), arr(c["y"]), np.array(off), np.array(vx), np.array(vy), fx(c["r"]),
+                              c["approximate"])
+        assert pairs_sorted(got).tolist() == c["expect"]
+
+
+PPOLY_CASES = [(500, 0.005, False, 60), (100, 0.01, False, 30), (500, 0.03, True, 20), (200, 0.05, False, 10),
+               (500, 0.0, False, 15)]
+
+
+@pytest.mark.parametrize("case", range(len(PPOLY_CASES)))
+def test_ppoly_random(ctx, case):
+    gn, r, approx, npoly = PPOLY_CASES[case]
+    x, y = synth.uniform(300000, 50 + case)
+    off, vx, vy = synth.star_polygons(npoly, 60 + case)
+    ag, cg = agrid(gn)
+    got = ctx.range_ppoly(ag, x, y, off, vx, vy, r, approx)
+    want = cref.range_ppoly(cg, x, y, off, vx, vy, r, approx)
+    assert pairs_sorted(got).tolist() == pairs_sorted(want).tolist()
+
+
+def test_ppoly_boundary_and_outside(ctx):
+    """Points on vertices/edges (boundary = distance 0), polygons crossing the grid edge with
+    Lg == 0 (guaranteed bbox cells outside the grid match out-of-grid points)."""
+    ag, cg = agrid(100)
+    l = (BJ[1] - BJ[0]) / 100
+    r = l * math.sqrt(2) * 1.2  # Lg == 0
+    ring = [(115.48, 39.58), (115.56, 39.58), (115.56, 39.66), (115.48, 39.66)]
+    ring2 = [(116.5, 40.5), (116.6, 40.5), (116.6, 40.6), (116.5, 40.6), (116.5, 40.5)]
+    vx = np.array([p[0] for p in ring] + [p[0] for p in ring2])
+    vy = np.array([p[1] for p in ring] + [p[1] for p in ring2])
+    off = np.array([0, 4, 9])
+    rng = np.random.default_rng(2)
+    x = np.concatenate([rng.uniform(115.4, 115.7, 4000), rng.uniform(116.45, 116.65, 4000), vx, [116.55, 116.5]])
+    y = np.concatenate([rng.uniform(39.5, 39.7, 4000), rng.uniform(40.45, 40.65, 4000), vy, [40.5, 40.57]])
+    for rr in (r, 0.004, 0.0):
+        got = ctx.range_ppoly(ag, x, y, off, vx, vy, rr)
+        want = cref.range_ppoly(cg, x, y, off, vx, vy, rr)
+        assert pairs_sorted(got).tolist() == pairs_sorted(want).tolist()
