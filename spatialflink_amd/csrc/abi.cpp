@@ -167,10 +167,11 @@ int knn_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const
     rc = stage_xy(ctx, x, y, n, S_X, S_Y, &dx, &dy);
     if (rc) return rc;
     const int kpl = kpl_for(k);
-    // 4 blocks per CU target; chunks of whole 1024-point block iterations
+    // exactly 4 blocks per CU (256 CUs) when n is large: equal work per CU; an even chunk keeps
+    // the 16-byte double2 loads aligned
     const uint64_t target_blocks = 1024;
     uint64_t chunk = (n + target_blocks - 1) / target_blocks;
-    chunk = (chunk + 1023) / 1024 * 1024;
+    chunk = (chunk + 1) & ~1ull;
     if (chunk < 1024) chunk = 1024;
     uint64_t nblocks = a.nu > 0 ? (n + chunk - 1) / chunk : 0;  // empty G u C: no candidates
     const uint64_t N = 64ull * kpl;
@@ -474,6 +475,51 @@ int geohip_synth_uniform_async(geohip_ctx* ctx, double* x, double* y, uint64_t n
     if (rc) return rc;
     hipError_t e = launch_synth_uniform(x, y, n, base, seed, min_x, max_x, min_y, max_y, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "synth launch");
+    return GEOHIP_OK;
+}
+
+// Measurement hook (not part of the operator surface): time `reps` launches of a kNN scan
+// ablation variant (0 full .. 3, see knn_scan) with events on the ctx stream; device memory.
+int geohip_debug_knn_scan_variant(geohip_ctx* ctx, int mode, const geohip_grid* grid, const double* x,
+                                  const double* y, uint64_t n, int nwin, double qx, double qy, double r, uint32_t k,
+                                  int reps, double* ms_per_launch) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    PointPlan plan;
+    rc = plan_or_fail(ctx, grid, qx, qy, r, &plan);
+    if (rc) return rc;
+    KnnArgs a;
+    memset(&a, 0, sizeof a);
+    for (int i = 0; i < plan.nu; i++) a.u[i] = plan.u[i];
+    a.nu = plan.nu;
+    a.k = k;
+    a.qx = qx;
+    a.qy = qy;
+    uint64_t chunk = (n + 1023) / 1024;
+    chunk = (chunk + 1) & ~1ull;
+    if (chunk < 1024) chunk = 1024;
+    const uint64_t nblocks = (n + chunk - 1) / chunk;
+    rc = ensure(ctx, S_PART_D, nblocks * 64 * 8);
+    if (!rc) rc = ensure(ctx, S_PART_I, nblocks * 64 * 4);
+    if (rc) return rc;
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(launch_knn_scan_variant(mode, x, y, n, a, B<unsigned long long>(ctx, S_PART_D), B<unsigned>(ctx, S_PART_I),
+                                   (unsigned)nblocks, chunk, ctx->stream));
+    HIPCHK(hipEventRecord(e0, ctx->stream));
+    for (int i = 0; i < reps; i++) {
+        const uint64_t w = (uint64_t)(i % (nwin > 0 ? nwin : 1)) * n;  // cycle windows: no Infinity-Cache reuse
+        HIPCHK(launch_knn_scan_variant(mode, x + w, y + w, n, a, B<unsigned long long>(ctx, S_PART_D),
+                                       B<unsigned>(ctx, S_PART_I), (unsigned)nblocks, chunk, ctx->stream));
+    }
+    HIPCHK(hipEventRecord(e1, ctx->stream));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    *ms_per_launch = ms / (reps > 0 ? reps : 1);
     return GEOHIP_OK;
 }
 

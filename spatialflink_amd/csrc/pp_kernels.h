@@ -26,6 +26,9 @@ struct RangeArgs {
 hipError_t launch_knn(const double* x, const double* y, uint64_t n, const KnnArgs& args, int kpl,
                       unsigned long long* part_d, unsigned* part_i, unsigned nblocks, uint64_t chunk, double* out_d,
                       unsigned* out_i, unsigned* out_count, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
+hipError_t launch_knn_scan_variant(int mode, const double* x, const double* y, uint64_t n, const KnnArgs& args,
+                                   unsigned long long* part_d, unsigned* part_i, unsigned nblocks, uint64_t chunk,
+                                   hipStream_t st);
 hipError_t launch_knn_merge(const unsigned long long* d, const unsigned* i, unsigned nlists, unsigned list_len,
                             unsigned k, double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st);
 // range: bitmask (16 words / 1024 pts), unit_count (units), offs (units) scratch.

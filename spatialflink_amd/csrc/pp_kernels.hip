@@ -134,7 +134,9 @@ __device__ __forceinline__ void knn_flush_cand(WaveStage& st, KnnWave& w, WList<
     }
 }
 
-template <int KPL>
+// MODE (ablation builds for measurement only; the product launches MODE 0):
+//   0 full, 1 loads only, 2 loads + classification, 3 + LDS staging and distances (no selection)
+template <int KPL, int MODE = 0>
 __global__ __launch_bounds__(kBlock) void knn_scan(const double* __restrict__ x, const double* __restrict__ y,
                                                    uint64_t n, uint64_t chunk, KnnArgs args,
                                                    unsigned long long* __restrict__ part_d,
@@ -160,16 +162,35 @@ __global__ __launch_bounds__(kBlock) void knn_scan(const double* __restrict__ x,
     w.published = kSentinelD;
     const unsigned k = args.k;
 
-    for (uint64_t base = blk_begin + (uint64_t)wid * kPtsIter; base < blk_end; base += kBlock / kWave * kPtsIter) {
+    // software pipeline: the next iteration's 4 KB per wave is in flight while this one is
+    // classified, so every wave keeps two wave-iterations of loads outstanding
+    constexpr uint64_t kStride = (uint64_t)(kBlock / kWave) * kPtsIter;
+    uint64_t base = blk_begin + (uint64_t)wid * kPtsIter;
+    double sink = 0.0;
+    double nx[4], ny[4];
+    bool nv[4];
+    if (base < blk_end) load4(x, y, base, blk_end, lane, nx, ny, nv);
+    for (; base < blk_end; base += kStride) {
         double px[4], py[4];
         bool valid[4];
-        load4(x, y, base, blk_end, lane, px, py, valid);
+#pragma unroll
+        for (int s = 0; s < 4; s++) { px[s] = nx[s]; py[s] = ny[s]; valid[s] = nv[s]; }
+        if (base + kStride < blk_end) load4(x, y, base + kStride, blk_end, lane, nx, ny, nv);
+        if (MODE == 1) {
+#pragma unroll
+            for (int s = 0; s < 4; s++) sink += px[s] + py[s];
+            continue;
+        }
 #pragma unroll
         for (int s = 0; s < 4; s++) {
             bool c = false;
             for (int b = 0; b < args.nu; b++) c = c || in_box(args.u[b], px[s], py[s]);
             c = c && valid[s];
             const unsigned long long m = __ballot(c);
+            if (MODE == 2) {
+                sink += (double)__popcll(m);
+                continue;
+            }
             if (c) {
                 const unsigned pos = w.ccnt + lanes_below(m);
                 st.cx[pos] = px[s];
@@ -178,8 +199,23 @@ __global__ __launch_bounds__(kBlock) void knn_scan(const double* __restrict__ x,
             }
             w.ccnt += (unsigned)__popcll(m);
         }
+        if (MODE == 2) continue;
         wave_lds_sync();
+        if (MODE == 3) {
+            while (w.ccnt >= 64) {
+                const unsigned from = w.ccnt - 64;
+                const double d = jts_pp_distance(args.qx, args.qy, st.cx[from + lane], st.cy[from + lane]);
+                sink += d;
+                wave_lds_sync();
+                w.ccnt = from;
+            }
+            continue;
+        }
         if (w.ccnt >= 64) knn_flush_cand<KPL>(st, w, L, k, &bthr, args.qx, args.qy, false);
+    }
+    if (MODE != 0) {
+        if (sink == 12345.678) part_d[blockIdx.x] = 1;  // keep the ablated work alive
+        return;
     }
     knn_flush_cand<KPL>(st, w, L, k, &bthr, args.qx, args.qy, true);
     knn_flush_sel<KPL>(st, w, L, k, &bthr, true);
@@ -267,25 +303,37 @@ __global__ __launch_bounds__(kFinalThreads) void knn_final(const unsigned long l
     const int lane = lane_id();
     const int wid = threadIdx.x / kWave;
 
-    // (1) T = k-th smallest head
+    // (1) T = k-th smallest head.  Thread t owns list t (t < 1024) and loads its first two
+    // entries once; lists beyond 1024 (never produced by knn_scan) are reloaded below.
     if (threadIdx.x == 0) {
         cnt = 0;
         Td = kSentinelD;
         Ti = kSentinelI;
     }
+    const unsigned own = threadIdx.x;
+    KE e0 = ksentinel(), e1 = ksentinel();
+    if (own < nlists) {
+        const size_t off = (size_t)own * list_len;
+        e0.d = part_d[off];
+        e0.i = part_i[off];
+        if (list_len > 1) {
+            e1.d = part_d[off + 1];
+            e1.i = part_i[off + 1];
+        }
+    }
     if (nlists >= k) {
         WList<KPL> L;
 #pragma unroll
         for (int s = 0; s < KPL; s++) L.s[s] = ksentinel();
-        for (unsigned g = (unsigned)wid * 64; g < nlists; g += kFinalThreads) {
+        wave_merge_batch<KPL>(L, wave_sort64(e0));
+        for (unsigned g = (unsigned)wid * 64 + kFinalThreads; g < nlists; g += kFinalThreads) {
             KE h = ksentinel();
             const unsigned p = g + lane;
             if (p < nlists) {
                 h.d = part_d[(size_t)p * list_len];
                 h.i = part_i[(size_t)p * list_len];
             }
-            h = wave_sort64(h);
-            wave_merge_batch<KPL>(L, h);
+            wave_merge_batch<KPL>(L, wave_sort64(h));
         }
         for (int step = 1; step < kFinalWaves; step <<= 1) {
             __syncthreads();
@@ -320,15 +368,29 @@ __global__ __launch_bounds__(kFinalThreads) void knn_final(const unsigned long l
     __syncthreads();
     const unsigned long long T_d = Td;
     const unsigned T_i = Ti;
-    // (2) gather every real entry <= T
-    for (unsigned p = threadIdx.x; p < nlists; p += blockDim.x) {
+    // (2) gather every real entry <= T (lists ascending: stop at the first entry above T)
+    auto take = [&](const KE& e) -> bool {
+        if (e.d == kSentinelD || lds_kless(T_d, T_i, e.d, e.i)) return false;
+        const unsigned pos = atomicAdd(&cnt, 1u);
+        if (pos < (unsigned)kFinalCap) { bd[pos] = e.d; bi[pos] = e.i; }
+        return true;
+    };
+    if (own < nlists && take(e0) && list_len > 1 && take(e1)) {
+        const size_t off = (size_t)own * list_len;
+        for (unsigned j = 2; j < list_len; j++) {
+            KE e;
+            e.d = part_d[off + j];
+            e.i = part_i[off + j];
+            if (!take(e)) break;
+        }
+    }
+    for (unsigned p = threadIdx.x + kFinalThreads; p < nlists; p += blockDim.x) {
         const size_t off = (size_t)p * list_len;
         for (unsigned j = 0; j < list_len; j++) {
-            const unsigned long long ed = part_d[off + j];
-            const unsigned ei = part_i[off + j];
-            if (ed == kSentinelD || lds_kless(T_d, T_i, ed, ei)) break;
-            const unsigned pos = atomicAdd(&cnt, 1u);
-            if (pos < (unsigned)kFinalCap) { bd[pos] = ed; bi[pos] = ei; }
+            KE e;
+            e.d = part_d[off + j];
+            e.i = part_i[off + j];
+            if (!take(e)) break;
         }
     }
     __syncthreads();
@@ -630,6 +692,19 @@ hipError_t launch_knn(const double* x, const double* y, uint64_t n, const KnnArg
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return launch_knn_merge(part_d, part_i, nblocks, 64u * (unsigned)kpl, args.k, out_d, out_i, out_count, st);
+}
+
+hipError_t launch_knn_scan_variant(int mode, const double* x, const double* y, uint64_t n, const KnnArgs& args,
+                                   unsigned long long* part_d, unsigned* part_i, unsigned nblocks, uint64_t chunk,
+                                   hipStream_t st) {
+    switch (mode) {
+        case 0: knn_scan<1, 0><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i); break;
+        case 1: knn_scan<1, 1><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i); break;
+        case 2: knn_scan<1, 2><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i); break;
+        case 3: knn_scan<1, 3><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_knn_merge(const unsigned long long* d, const unsigned* i, unsigned nlists, unsigned list_len,

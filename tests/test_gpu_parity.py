@@ -291,7 +291,7 @@ def test_join_two_grids_and_errors(ctx):
         ctx.join_pp(ag1, ag1, dx, dy, qx, qy, -0.1)
     with pytest.raises(_abi.GeohipArgumentError):
         ctx.join_pp(ag1, ag1, dx, dy, qx, qy, math.nan)
-    assert ctx.join_pp_count(ag1, ag1, dx, dy, qx, qy, 0.07) == len(want)
+    assert ctx.join_pp_count(ag1, ag2, dx, dy, qx, qy, 0.07) == len(want)
 
 
 # ------------------------------------------------------------------ point-polygon --------
