@@ -108,7 +108,7 @@ _SIGS = {
     "geohip_debug_selftest_fp64": (c_int, [_P, _P, _P, c_uint64, _P, _P, _P, _P]),
     "geohip_debug_classify": (c_int, [POINTER(Grid), c_double, c_double, c_double, _P, _P, c_uint64, _P]),
     "geohip_debug_knn_scan_variant": (c_int, [_P, c_int, POINTER(Grid), _P, _P, c_uint64, c_int, c_double,
-                                              c_double, c_double, c_uint32, c_int, POINTER(c_double)]),
+                                              c_double, c_double, c_uint32, c_int, _P]),
 }
 for _name, (_res, _args) in _SIGS.items():
     _f = getattr(lib, _name)
@@ -354,12 +354,12 @@ class Context:
 
     def debug_knn_scan_variant(self, mode, grid, x, y, n, nwin, qx, qy, r, k, reps=20):
         """x, y: [nwin * n] device arrays; launch i scans window i % nwin."""
-        ms = c_double(0)
+        ms = (c_double * 3)()
         self.set_mem(MEM_DEVICE)
         rc = lib.geohip_debug_knn_scan_variant(self.h, mode, ctypes.byref(grid), _ptr(x), _ptr(y), n, nwin, qx, qy,
-                                               r, k, reps, ctypes.byref(ms))
+                                               r, k, reps, ms)
         self._check(rc, "debug_knn_scan_variant")
-        return ms.value
+        return ms[0] if mode != 5 else (ms[0], ms[1], ms[2])
 
     def selftest_fp64(self, a, b):
         """Device fp64 primitive bits (test hook): returns (sqrt|a|, a/b, hypot(a,b), a*b-b*b)."""

@@ -8,6 +8,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
+#include <cmath>
 #include <string>
 #include <utility>
 #include <vector>
@@ -21,7 +23,7 @@ using namespace geohip;
 
 enum Slot {
     S_X, S_Y, S_QX, S_QY, S_GTHR, S_PART_D, S_PART_I, S_OUT_D, S_OUT_I, S_OUT_CNT,
-    S_MASK, S_UCNT, S_OFFS, S_TOTAL, S_OUT_IDX, S_OUT_PAIRS,
+    S_MASK, S_UCNT, S_OFFS, S_TOTAL, S_OUT_IDX, S_OUT_PAIRS, S_SPILL_D, S_SPILL_I, S_SPILL_CNT,
     S_J0, S_J1, S_J2, S_J3, S_J4, S_J5, S_J6, S_J7, S_J8, S_J9, S_J10, S_J11, S_J12, S_J13, S_J14, S_J15,
     S_COUNT
 };
@@ -87,6 +89,15 @@ int ensure(geohip_ctx* ctx, Slot s, size_t bytes) {
 template <typename T>
 T* B(geohip_ctx* ctx, Slot s) { return reinterpret_cast<T*>(ctx->buf[s]); }
 
+int ensure_zeroed(geohip_ctx* ctx, Slot s, size_t bytes) {
+    const bool fresh = ctx->cap[s] < (bytes ? bytes : 16);
+    int rc = ensure(ctx, s, bytes);
+    if (rc) return rc;
+    if (fresh && hipMemsetAsync(ctx->buf[s], 0, ctx->cap[s], ctx->stream) != hipSuccess)
+        return fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
+    return GEOHIP_OK;
+}
+
 int begin(geohip_ctx* ctx) {
     if (!ctx) return GEOHIP_ERR_ARG;
     ctx->err.clear();
@@ -147,6 +158,34 @@ int plan_or_fail(geohip_ctx* ctx, const geohip_grid* grid, double qx, double qy,
 
 int kpl_for(uint32_t k) { return k <= 64 ? 1 : k <= 128 ? 2 : 4; }
 
+KnnArgs make_knn_args(const PointPlan& plan, uint32_t k, double qx, double qy) {
+    KnnArgs a;
+    memset(&a, 0, sizeof a);
+    for (int i = 0; i < plan.nu; i++) a.u[i] = plan.u[i];
+    a.nu = plan.nu;
+    a.k = k;
+    a.qx = qx;
+    a.qy = qy;
+    // distance histogram: 32 octaves below 2^e_top, where every candidate distance is < 2^(e_top-1)
+    double ex = 0.0, ey = 0.0;
+    for (int i = 0; i < plan.nu; i++) {
+        const Box& b = plan.u[i];
+        ex = std::max(ex, std::max(std::fabs(b.xlo - qx), std::fabs(b.xhi - qx)));
+        ey = std::max(ey, std::max(std::fabs(b.ylo - qy), std::fabs(b.yhi - qy)));
+    }
+    const double dmax = std::sqrt(ex * ex + ey * ey);
+    int e_top = 1024;
+    if (std::isfinite(dmax) && dmax > 0) e_top = std::ilogb(dmax) + 2;
+    int E0 = e_top - 32 + 1023;
+    if (E0 < 0) E0 = 0;
+    if (E0 > 2047 - 32) E0 = 2047 - 32;
+    a.hist_base = E0 << 4;
+    return a;
+}
+
+// scratch that must start zeroed (the final kernel re-zeroes it after each use)
+int ensure_zeroed(geohip_ctx* ctx, Slot s, size_t bytes);
+
 // kNN enqueue shared by the sync and async forms.
 int knn_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
                 double qx, double qy, double r, uint32_t k, double* out_d, unsigned* out_i, unsigned* out_cnt) {
@@ -156,13 +195,7 @@ int knn_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const
     PointPlan plan;
     int rc = plan_or_fail(ctx, grid, qx, qy, r, &plan);
     if (rc) return rc;
-    KnnArgs a;
-    memset(&a, 0, sizeof a);
-    for (int i = 0; i < plan.nu; i++) a.u[i] = plan.u[i];
-    a.nu = plan.nu;
-    a.k = k;
-    a.qx = qx;
-    a.qy = qy;
+    KnnArgs a = make_knn_args(plan, k, qx, qy);
     const double *dx, *dy;
     rc = stage_xy(ctx, x, y, n, S_X, S_Y, &dx, &dy);
     if (rc) return rc;
@@ -177,11 +210,15 @@ int knn_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const
     const uint64_t N = 64ull * kpl;
     rc = ensure(ctx, S_PART_D, nblocks * N * 8);
     if (!rc) rc = ensure(ctx, S_PART_I, nblocks * N * 4);
+    if (!rc) rc = ensure(ctx, S_SPILL_D, n * 8);  // worst case: every point survives
+    if (!rc) rc = ensure(ctx, S_SPILL_I, n * 4);
+    if (!rc) rc = ensure_zeroed(ctx, S_SPILL_CNT, 16);
     if (rc) return rc;
     hipEvent_t e0, e1;
     timing_events(ctx, &e0, &e1);
     hipError_t e = launch_knn(dx, dy, n, a, kpl, B<unsigned long long>(ctx, S_PART_D), B<unsigned>(ctx, S_PART_I),
-                              (unsigned)nblocks, chunk, out_d, out_i, out_cnt, ctx->stream, e0, e1);
+                              (unsigned)nblocks, chunk, out_d, out_i, out_cnt, B<unsigned long long>(ctx, S_SPILL_D),
+                              B<unsigned>(ctx, S_SPILL_I), B<unsigned>(ctx, S_SPILL_CNT), ctx->stream, e0, e1);
     if (e != hipSuccess) return hip_fail(ctx, e, "knn launch");
     return GEOHIP_OK;
 }
@@ -201,6 +238,10 @@ int range_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x, con
     a.qx = qx;
     a.qy = qy;
     a.r = r;
+    // squared screens for the candidate cells (see device_common.h): a 2^-40 margin
+    const double r2 = r * r;
+    a.r2lo = (r >= 0.0) ? r2 * (1.0 - 0x1.0p-40) : -1.0;
+    a.r2hi = r2 * (1.0 + 0x1.0p-40);
     const double *dx, *dy;
     rc = stage_xy(ctx, x, y, n, S_X, S_Y, &dx, &dy);
     if (rc) return rc;
@@ -488,30 +529,30 @@ int geohip_debug_knn_scan_variant(geohip_ctx* ctx, int mode, const geohip_grid* 
     PointPlan plan;
     rc = plan_or_fail(ctx, grid, qx, qy, r, &plan);
     if (rc) return rc;
-    KnnArgs a;
-    memset(&a, 0, sizeof a);
-    for (int i = 0; i < plan.nu; i++) a.u[i] = plan.u[i];
-    a.nu = plan.nu;
-    a.k = k;
-    a.qx = qx;
-    a.qy = qy;
+    KnnArgs a = make_knn_args(plan, k, qx, qy);
     uint64_t chunk = (n + 1023) / 1024;
     chunk = (chunk + 1) & ~1ull;
     if (chunk < 1024) chunk = 1024;
     const uint64_t nblocks = (n + chunk - 1) / chunk;
     rc = ensure(ctx, S_PART_D, nblocks * 64 * 8);
     if (!rc) rc = ensure(ctx, S_PART_I, nblocks * 64 * 4);
+    if (!rc) rc = ensure(ctx, S_SPILL_D, n * 8);
+    if (!rc) rc = ensure(ctx, S_SPILL_I, n * 4);
+    if (!rc) rc = ensure_zeroed(ctx, S_SPILL_CNT, 16);
     if (rc) return rc;
+    unsigned long long* sd = B<unsigned long long>(ctx, S_SPILL_D);
+    unsigned* si = B<unsigned>(ctx, S_SPILL_I);
+    unsigned* sc = B<unsigned>(ctx, S_SPILL_CNT);
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
     HIPCHK(launch_knn_scan_variant(mode, x, y, n, a, B<unsigned long long>(ctx, S_PART_D), B<unsigned>(ctx, S_PART_I),
-                                   (unsigned)nblocks, chunk, ctx->stream));
+                                   (unsigned)nblocks, chunk, sd, si, sc, ctx->stream));
     HIPCHK(hipEventRecord(e0, ctx->stream));
     for (int i = 0; i < reps; i++) {
         const uint64_t w = (uint64_t)(i % (nwin > 0 ? nwin : 1)) * n;  // cycle windows: no Infinity-Cache reuse
         HIPCHK(launch_knn_scan_variant(mode, x + w, y + w, n, a, B<unsigned long long>(ctx, S_PART_D),
-                                       B<unsigned>(ctx, S_PART_I), (unsigned)nblocks, chunk, ctx->stream));
+                                       B<unsigned>(ctx, S_PART_I), (unsigned)nblocks, chunk, sd, si, sc, ctx->stream));
     }
     HIPCHK(hipEventRecord(e1, ctx->stream));
     HIPCHK(hipEventSynchronize(e1));
@@ -520,6 +561,17 @@ int geohip_debug_knn_scan_variant(geohip_ctx* ctx, int mode, const geohip_grid* 
     hipEventDestroy(e0);
     hipEventDestroy(e1);
     *ms_per_launch = ms / (reps > 0 ? reps : 1);
+    if (mode == 5) {  // counters of one extra launch: sorts and passing candidates, summed
+        HIPCHK(hipMemsetAsync(ctx->buf[S_PART_I], 0, 8, ctx->stream));
+        HIPCHK(launch_knn_scan_variant(mode, x, y, n, a, B<unsigned long long>(ctx, S_PART_D),
+                                       B<unsigned>(ctx, S_PART_I), (unsigned)nblocks, chunk, sd, si, sc, ctx->stream));
+        unsigned c[2];
+        HIPCHK(hipMemcpy(&c[1], sc, 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemsetAsync(sc, 0, 4, ctx->stream));
+        HIPCHK(hipMemcpy(c, ctx->buf[S_PART_I], 4, hipMemcpyDeviceToHost));
+        ms_per_launch[1] = c[0];
+        ms_per_launch[2] = c[1];
+    }
     return GEOHIP_OK;
 }
 

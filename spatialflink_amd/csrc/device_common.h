@@ -86,6 +86,14 @@ __device__ __forceinline__ double coord_distance(double ax, double ay, double bx
     return fdlibm_hypot(ax - bx, ay - by);
 }
 
+// Safe squared-distance screens.  With dx, dy as the kernels compute them, d2 = dx*dx + dy*dy
+// in fp64 is within 3 ulp of the true square and fdlibm hypot is within 1 ulp of the true
+// distance, so a 2^-40 relative margin on the bound squared separates "certainly above" and
+// "certainly below" from the band where the exact JTS distance must be computed.  NaN d2
+// fails both tests (goes to the exact path); an infinite bound never rejects.
+constexpr double kSqHi = 1.0 + 0x1.0p-40;
+constexpr double kSqLo = 1.0 - 0x1.0p-40;
+
 // ---------------------------------------------------------------- classification ----------
 __device__ __forceinline__ bool in_box(const Box& b, double x, double y) {
     bool bx = (x >= b.xlo) && (x <= b.xhi);
@@ -117,16 +125,46 @@ struct KE {  // kNN entry: distance bits (monotone for d >= 0) and window index
 __device__ __forceinline__ bool kless(const KE& a, const KE& b) {
     return a.d < b.d || (a.d == b.d && a.i < b.i);
 }
+// ---- cross-lane moves without the LDS crossbar --------------------------------------
+// lane ^ j for j = 1, 2 (DPP quad_perm), 4 (row_half_mirror + quad_perm), 8 (row_mirror +
+// row_half_mirror), 16 (ds_swizzle bit mode), 32 (v_permlane32_swap, gfx950).  j must fold to
+// a constant (all callers sit in fully unrolled loops).
+#define GEOHIP_DPP(v, ctrl) ((unsigned)__builtin_amdgcn_update_dpp(0, (int)(v), (ctrl), 0xF, 0xF, false))
+__device__ __forceinline__ unsigned xor_lane(unsigned v, int j) {
+    switch (j) {
+        case 1: return GEOHIP_DPP(v, 0xB1);
+        case 2: return GEOHIP_DPP(v, 0x4E);
+        case 4: return GEOHIP_DPP(GEOHIP_DPP(v, 0x141), 0x1B);
+        case 8: return GEOHIP_DPP(GEOHIP_DPP(v, 0x140), 0x141);
+        case 16: return (unsigned)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);
+        default: {
+            auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+            return __lane_id() < 32 ? r[1] : r[0];
+        }
+    }
+}
+__device__ __forceinline__ unsigned long long xor_lane64(unsigned long long v, int j) {
+    const unsigned lo = xor_lane((unsigned)v, j), hi = xor_lane((unsigned)(v >> 32), j);
+    return ((unsigned long long)hi << 32) | lo;
+}
+// lane ^ 63 (reverse the wave)
+__device__ __forceinline__ unsigned rev_lane(unsigned v) {
+    return xor_lane((unsigned)__builtin_amdgcn_ds_swizzle((int)GEOHIP_DPP(v, 0x140), 0x401F), 32);
+}
+__device__ __forceinline__ unsigned long long rev_lane64(unsigned long long v) {
+    return ((unsigned long long)rev_lane((unsigned)(v >> 32)) << 32) | rev_lane((unsigned)v);
+}
+
 __device__ __forceinline__ KE kxor(const KE& v, int m) {
     KE r;
-    r.d = __shfl_xor(v.d, m);
-    r.i = __shfl_xor(v.i, m);
+    r.d = xor_lane64(v.d, m);
+    r.i = xor_lane(v.i, m);
     return r;
 }
-__device__ __forceinline__ KE kfrom(const KE& v, int src) {
+__device__ __forceinline__ KE krev(const KE& v) {
     KE r;
-    r.d = __shfl(v.d, src);
-    r.i = __shfl(v.i, src);
+    r.d = rev_lane64(v.d);
+    r.i = rev_lane(v.i);
     return r;
 }
 __device__ __forceinline__ KE ksentinel() {
@@ -189,7 +227,7 @@ __device__ __forceinline__ void wave_merge_lists(WList<KPL>& L, const WList<KPL>
     const int lane = lane_id();
 #pragma unroll
     for (int s = 0; s < KPL; s++) {
-        KE rv = kfrom(B.s[KPL - 1 - s], 63 - lane);  // B reversed
+        KE rv = krev(B.s[KPL - 1 - s]);  // B reversed
         if (kless(rv, L.s[s])) L.s[s] = rv;
     }
     wave_bitonic_merge<KPL>(L);
@@ -199,7 +237,7 @@ __device__ __forceinline__ void wave_merge_lists(WList<KPL>& L, const WList<KPL>
 template <int KPL>
 __device__ __forceinline__ void wave_merge_batch(WList<KPL>& L, const KE& sorted_batch) {
     const int lane = lane_id();
-    KE rv = kfrom(sorted_batch, 63 - lane);
+    KE rv = krev(sorted_batch);
     if (kless(rv, L.s[KPL - 1])) L.s[KPL - 1] = rv;
     wave_bitonic_merge<KPL>(L);
 }
@@ -244,8 +282,10 @@ __device__ __forceinline__ KE wave_list_get(const WList<KPL>& L, int e) {  // e 
     for (int t = 1; t < KPL; t++)
         if (t == s) r = L.s[t];
     KE o;
-    o.d = __shfl(r.d, l);
-    o.i = __shfl(r.i, l);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)r.d, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(r.d >> 32), l);
+    o.d = ((unsigned long long)hi << 32) | lo;
+    o.i = (unsigned)__builtin_amdgcn_readlane((int)r.i, l);
     return o;
 }
 

@@ -12,6 +12,8 @@ struct KnnArgs {
     int32_t nu;
     uint32_t k;
     double qx, qy;
+    int32_t hist_base;  // (biased exponent of the lowest histogram octave) << 4
+    int32_t pad;
 };
 
 struct RangeArgs {
@@ -19,16 +21,18 @@ struct RangeArgs {
     Box c;
     int32_t ng, nc;
     double qx, qy, r;
+    double r2lo, r2hi;  // squared screens (device_common.h kSqLo/kSqHi); r2lo < 0 disables
 };
 
 // kNN scan over ceil(n / chunk) = nblocks blocks (chunk a multiple of 1024), then the final
 // selection into out_*.  ev0/ev1 (optional) bracket the scan kernel only.
 hipError_t launch_knn(const double* x, const double* y, uint64_t n, const KnnArgs& args, int kpl,
                       unsigned long long* part_d, unsigned* part_i, unsigned nblocks, uint64_t chunk, double* out_d,
-                      unsigned* out_i, unsigned* out_count, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
+                      unsigned* out_i, unsigned* out_count, unsigned long long* spill_d, unsigned* spill_i,
+                      unsigned* spill_cnt, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_knn_scan_variant(int mode, const double* x, const double* y, uint64_t n, const KnnArgs& args,
                                    unsigned long long* part_d, unsigned* part_i, unsigned nblocks, uint64_t chunk,
-                                   hipStream_t st);
+                                   unsigned long long* spill_d, unsigned* spill_i, unsigned* spill_cnt, hipStream_t st);
 hipError_t launch_knn_merge(const unsigned long long* d, const unsigned* i, unsigned nlists, unsigned list_len,
                             unsigned k, double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st);
 // range: bitmask (16 words / 1024 pts), unit_count (units), offs (units) scratch.

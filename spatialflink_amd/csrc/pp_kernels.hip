@@ -26,14 +26,10 @@ namespace geohip {
 constexpr int kBlock = 256;            // 4 waves
 constexpr int kPtsIter = 256;          // points per wave iteration (4 per lane)
 constexpr int kCandCap = 64 + kPtsIter;
-constexpr int kSelCap = 128;
-
 struct WaveStage {  // wave-private LDS
     double cx[kCandCap];
     double cy[kCandCap];
     unsigned ci[kCandCap];
-    unsigned long long sd[kSelCap];
-    unsigned si[kSelCap];
 };
 
 __device__ __forceinline__ void load4(const double* __restrict__ x, const double* __restrict__ y,
@@ -64,210 +60,12 @@ __device__ __forceinline__ uint64_t slot_index(uint64_t base, int lane, int s) {
     return base + (uint64_t)((s >> 1) * 128 + 2 * lane + (s & 1));
 }
 
-// ============================================================================ kNN =========
-struct KnnWave {
-    unsigned ccnt;                 // staged candidates (wave-uniform)
-    unsigned scnt;                 // staged selected entries
-    unsigned long long thr;        // local k-th distance bits (sentinel until full)
-    unsigned long long published;  // last value pushed to the block threshold
-};
-
-// Block-wide pruning threshold: min over the block's waves of their k-th distance.  Shared
-// through one LDS word (ds_min_u64), never through global memory: a chip-wide atomic word
-// serialises thousands of updates on one L2 line (measured 523 us per 10M-point scan).
-template <int KPL>
-__device__ __forceinline__ void knn_flush_sel(WaveStage& st, KnnWave& w, WList<KPL>& L, unsigned k,
-                                              unsigned long long* bthr, bool partial) {
-    const int lane = lane_id();
-    while (w.scnt >= 64 || (partial && w.scnt > 0)) {
-        const unsigned take = w.scnt >= 64 ? 64u : w.scnt;
-        const unsigned from = w.scnt - take;
-        KE e = ksentinel();
-        if ((unsigned)lane < take) {
-            e.d = st.sd[from + lane];
-            e.i = st.si[from + lane];
-        }
-        wave_lds_sync();
-        w.scnt = from;
-        e = wave_sort64(e);
-        wave_merge_batch<KPL>(L, e);
-        KE kth = wave_list_get<KPL>(L, (int)k - 1);
-        w.thr = kth.d;
-        if (kth.d != kSentinelD && kth.d < w.published) {
-            w.published = kth.d;
-            if (lane == 0) atomicMin(bthr, kth.d);
-        }
-    }
-}
-
-template <int KPL>
-__device__ __forceinline__ void knn_flush_cand(WaveStage& st, KnnWave& w, WList<KPL>& L, unsigned k,
-                                               unsigned long long* bthr, double qx, double qy, bool partial) {
-    const int lane = lane_id();
-    while (w.ccnt >= 64 || (partial && w.ccnt > 0)) {
-        const unsigned take = w.ccnt >= 64 ? 64u : w.ccnt;
-        const unsigned from = w.ccnt - take;
-        bool ok = (unsigned)lane < take;
-        double px = 0.0, py = 0.0;
-        unsigned pi = 0;
-        if (ok) {
-            px = st.cx[from + lane];
-            py = st.cy[from + lane];
-            pi = st.ci[from + lane];
-        }
-        const unsigned long long bval = *reinterpret_cast<volatile unsigned long long*>(bthr);
-        wave_lds_sync();
-        w.ccnt = from;
-        const double d = jts_pp_distance(qx, qy, px, py);
-        const unsigned long long db = (unsigned long long)__double_as_longlong(d);
-        const unsigned long long lim = w.thr < bval ? w.thr : bval;
-        ok = ok && db <= lim;
-        const unsigned long long m = __ballot(ok);
-        if (ok) {
-            const unsigned pos = w.scnt + lanes_below(m);
-            st.sd[pos] = db;
-            st.si[pos] = pi;
-        }
-        w.scnt += (unsigned)__popcll(m);
-        wave_lds_sync();
-        if (w.scnt >= 64) knn_flush_sel<KPL>(st, w, L, k, bthr, false);
-    }
-}
-
-// MODE (ablation builds for measurement only; the product launches MODE 0):
-//   0 full, 1 loads only, 2 loads + classification, 3 + LDS staging and distances (no selection)
-template <int KPL, int MODE = 0>
-__global__ __launch_bounds__(kBlock) void knn_scan(const double* __restrict__ x, const double* __restrict__ y,
-                                                   uint64_t n, uint64_t chunk, KnnArgs args,
-                                                   unsigned long long* __restrict__ part_d,
-                                                   unsigned* __restrict__ part_i) {
-    __shared__ WaveStage stage[kBlock / kWave];
-    __shared__ unsigned long long bthr;
-    const int lane = lane_id();
-    const int wid = threadIdx.x / kWave;
-    WaveStage& st = stage[wid];
-    const uint64_t blk_begin = (uint64_t)blockIdx.x * chunk;
-    uint64_t blk_end = blk_begin + chunk;
-    if (blk_end > n) blk_end = n;
-    if (threadIdx.x == 0) bthr = kSentinelD;
-    __syncthreads();
-
-    WList<KPL> L;
-#pragma unroll
-    for (int s = 0; s < KPL; s++) L.s[s] = ksentinel();
-    KnnWave w;
-    w.ccnt = 0;
-    w.scnt = 0;
-    w.thr = kSentinelD;
-    w.published = kSentinelD;
-    const unsigned k = args.k;
-
-    // software pipeline: the next iteration's 4 KB per wave is in flight while this one is
-    // classified, so every wave keeps two wave-iterations of loads outstanding
-    constexpr uint64_t kStride = (uint64_t)(kBlock / kWave) * kPtsIter;
-    uint64_t base = blk_begin + (uint64_t)wid * kPtsIter;
-    double sink = 0.0;
-    double nx[4], ny[4];
-    bool nv[4];
-    if (base < blk_end) load4(x, y, base, blk_end, lane, nx, ny, nv);
-    for (; base < blk_end; base += kStride) {
-        double px[4], py[4];
-        bool valid[4];
-#pragma unroll
-        for (int s = 0; s < 4; s++) { px[s] = nx[s]; py[s] = ny[s]; valid[s] = nv[s]; }
-        if (base + kStride < blk_end) load4(x, y, base + kStride, blk_end, lane, nx, ny, nv);
-        if (MODE == 1) {
-#pragma unroll
-            for (int s = 0; s < 4; s++) sink += px[s] + py[s];
-            continue;
-        }
-#pragma unroll
-        for (int s = 0; s < 4; s++) {
-            bool c = false;
-            for (int b = 0; b < args.nu; b++) c = c || in_box(args.u[b], px[s], py[s]);
-            c = c && valid[s];
-            const unsigned long long m = __ballot(c);
-            if (MODE == 2) {
-                sink += (double)__popcll(m);
-                continue;
-            }
-            if (c) {
-                const unsigned pos = w.ccnt + lanes_below(m);
-                st.cx[pos] = px[s];
-                st.cy[pos] = py[s];
-                st.ci[pos] = (unsigned)slot_index(base, lane, s);
-            }
-            w.ccnt += (unsigned)__popcll(m);
-        }
-        if (MODE == 2) continue;
-        wave_lds_sync();
-        if (MODE == 3) {
-            while (w.ccnt >= 64) {
-                const unsigned from = w.ccnt - 64;
-                const double d = jts_pp_distance(args.qx, args.qy, st.cx[from + lane], st.cy[from + lane]);
-                sink += d;
-                wave_lds_sync();
-                w.ccnt = from;
-            }
-            continue;
-        }
-        if (w.ccnt >= 64) knn_flush_cand<KPL>(st, w, L, k, &bthr, args.qx, args.qy, false);
-    }
-    if (MODE != 0) {
-        if (sink == 12345.678) part_d[blockIdx.x] = 1;  // keep the ablated work alive
-        return;
-    }
-    knn_flush_cand<KPL>(st, w, L, k, &bthr, args.qx, args.qy, true);
-    knn_flush_sel<KPL>(st, w, L, k, &bthr, true);
-
-    // block combine: waves 1..3 hand their lists to wave 0 through LDS (reusing the stage)
-    __syncthreads();
-    unsigned long long* ld = reinterpret_cast<unsigned long long*>(&stage[0].cx[0]);
-    unsigned* li = reinterpret_cast<unsigned*>(&stage[2].cx[0]);
-    constexpr int N = 64 * KPL;
-    if (wid > 0) {
-#pragma unroll
-        for (int s = 0; s < KPL; s++) {
-            ld[(wid - 1) * N + s * 64 + lane] = L.s[s].d;
-            li[(wid - 1) * N + s * 64 + lane] = L.s[s].i;
-        }
-    }
-    __syncthreads();
-    if (wid == 0) {
-        for (int o = 0; o < kBlock / kWave - 1; o++) {
-            WList<KPL> B;
-#pragma unroll
-            for (int s = 0; s < KPL; s++) {
-                B.s[s].d = ld[o * N + s * 64 + lane];
-                B.s[s].i = li[o * N + s * 64 + lane];
-            }
-            wave_merge_lists<KPL>(L, B);
-        }
-        const size_t off = (size_t)blockIdx.x * N;
-#pragma unroll
-        for (int s = 0; s < KPL; s++) {
-            part_d[off + s * 64 + lane] = L.s[s].d;
-            part_i[off + s * 64 + lane] = L.s[s].i;
-        }
-    }
-}
-
-// ---------------------------------------------------------------- final selection --------
-// One workgroup of 16 waves.  (1) every wave sorts 64 list heads in registers and the 16
-// sorted runs are merged by a 4-level tree through LDS: T = k-th smallest head, an upper
-// bound of the global k-th key (the k smallest heads are k real entries).  (2) every entry
-// <= T is gathered (lists are ascending: a scan stops at the first entry above T; typically
-// ~k entries in all).  (3) one wave sorts them in registers and writes the top k.
-constexpr int kFinalThreads = 1024;
-constexpr int kFinalWaves = kFinalThreads / kWave;
-constexpr int kFinalCap = 4096;
-
 __device__ __forceinline__ bool lds_kless(unsigned long long ad, unsigned ai, unsigned long long bd, unsigned bi) {
     return ad < bd || (ad == bd && ai < bi);
 }
 
 // bitonic sort of m (power of two) keys in LDS by the whole workgroup (fallback path)
-__device__ void block_sort(unsigned long long* d, unsigned* i, int m) {
+__device__ void block_sort_lds(unsigned long long* d, unsigned* i, int m) {
     for (int size = 2; size <= m; size <<= 1) {
         for (int j = size >> 1; j > 0; j >>= 1) {
             for (int t = threadIdx.x; t < m / 2; t += blockDim.x) {
@@ -285,12 +83,318 @@ __device__ void block_sort(unsigned long long* d, unsigned* i, int m) {
     }
 }
 
+// ============================================================================ kNN =========
+// Block-level selection state (LDS).  Survivors of the pruning bound go to one buffer; a
+// 512-bin histogram of their distance bits (16 bins per octave over the 32 octaves below the
+// largest possible candidate distance) yields the bound: B = upper edge of the smallest bin
+// at which the cumulative count reaches k.  That is a valid upper bound of the block's k-th
+// distance (>= k real candidates lie at or below it), shared by the four waves from the first
+// survivors on, and it costs LDS atomics instead of per-wave sorting networks.
+constexpr int kHistBins = 512;
+constexpr int kBlkCap = 768;  // 4 blocks/CU: stages 25.6 KB + this ~11.3 KB <= 40 KB
+
+struct KnnBlock {
+    unsigned hist[kHistBins];
+    unsigned long long bd[kBlkCap];
+    unsigned bi[kBlkCap];
+    unsigned long long bound;  // distance bits; kSentinelD = none yet
+    unsigned cnt;              // survivors appended (may exceed kBlkCap: the rest spilled)
+    unsigned final_cnt;
+};
+
+__device__ __forceinline__ int hist_bin(unsigned long long db, int base) {
+    const long long b = (long long)(db >> 48) - base;
+    return b < 0 ? 0 : (b >= kHistBins ? kHistBins - 1 : (int)b);
+}
+
+// One wave: smallest bin whose cumulative count reaches k -> LDS bound (atomic min).
+__device__ __forceinline__ void hist_bound(KnnBlock& kb, unsigned k, int base) {
+    const int lane = lane_id();
+    unsigned c[8];
+    unsigned tot = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        c[j] = kb.hist[lane * 8 + j];
+        tot += c[j];
+    }
+    unsigned incl = tot;  // inclusive prefix over lanes
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+    }
+    const unsigned long long m = __ballot(incl >= k);
+    if (m == 0) return;
+    const int first = __builtin_ctzll(m);
+    int bin = kHistBins - 1;
+    if (lane == first) {
+        unsigned run = incl - tot;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            run += c[j];
+            if (run >= k) { bin = lane * 8 + j; break; }
+        }
+        if (bin < kHistBins - 1) {
+            const unsigned long long B = ((unsigned long long)(bin + base + 1) << 48) - 1ull;
+            atomicMin(&kb.bound, B);
+        }
+    }
+}
+
+// exact distances of up to 64 staged candidates, survivors appended to the block buffer
+__device__ __forceinline__ void knn_dist_batch(WaveStage& st, unsigned& ccnt, KnnBlock& kb, const KnnArgs& a,
+                                               unsigned long long* __restrict__ spill_d,
+                                               unsigned* __restrict__ spill_i, unsigned* __restrict__ spill_cnt,
+                                               unsigned& appended, bool partial) {
+    const int lane = lane_id();
+    while (ccnt >= 64 || (partial && ccnt > 0)) {
+        const unsigned take = ccnt >= 64 ? 64u : ccnt;
+        const unsigned from = ccnt - take;
+        bool ok = (unsigned)lane < take;
+        double px = 0.0, py = 0.0;
+        unsigned pi = 0;
+        if (ok) {
+            px = st.cx[from + lane];
+            py = st.cy[from + lane];
+            pi = st.ci[from + lane];
+        }
+        const unsigned long long B = *reinterpret_cast<volatile unsigned long long*>(&kb.bound);
+        wave_lds_sync();
+        ccnt = from;
+        const double d = jts_pp_distance(a.qx, a.qy, px, py);
+        const unsigned long long db = (unsigned long long)__double_as_longlong(d);
+        ok = ok && db <= B;
+        const unsigned long long m = __ballot(ok);
+        if (m) {
+            const unsigned nm = (unsigned)__popcll(m);
+            unsigned pos = 0;
+            if (lane == 0) pos = atomicAdd(&kb.cnt, nm);
+            pos = __shfl(pos, 0);
+            const unsigned slot = pos + lanes_below(m);
+            unsigned gbase = 0;
+            if (pos + nm > (unsigned)kBlkCap) {  // spill the overflow to global memory (rare)
+                const unsigned first = pos > (unsigned)kBlkCap ? pos : (unsigned)kBlkCap;
+                if (lane == 0) gbase = atomicAdd(spill_cnt, pos + nm - first);
+                gbase = __shfl(gbase, 0) - (first - pos);
+            }
+            if (ok) {
+                if (slot < (unsigned)kBlkCap) {
+                    kb.bd[slot] = db;
+                    kb.bi[slot] = pi;
+                } else {
+                    spill_d[gbase + (slot - pos)] = db;
+                    spill_i[gbase + (slot - pos)] = pi;
+                }
+                atomicAdd(&kb.hist[hist_bin(db, a.hist_base)], 1u);
+            }
+            appended += nm;
+        }
+        wave_lds_sync();
+    }
+}
+
+// MODE (ablation builds for measurement only; the product launches MODE 0):
+//   0 full, 1 loads only, 2 loads + classification, 3 + LDS staging and distances (no selection),
+//   5 full + counters (survivors, spilled), 7 full without the end-of-block selection
+template <int KPL, int MODE = 0>
+__global__ __launch_bounds__(kBlock) void knn_scan(const double* __restrict__ x, const double* __restrict__ y,
+                                                   uint64_t n, uint64_t chunk, KnnArgs args,
+                                                   unsigned long long* __restrict__ part_d,
+                                                   unsigned* __restrict__ part_i,
+                                                   unsigned long long* __restrict__ spill_d,
+                                                   unsigned* __restrict__ spill_i, unsigned* __restrict__ spill_cnt) {
+    __shared__ WaveStage stage[kBlock / kWave];
+    __shared__ KnnBlock kb;
+    const int lane = lane_id();
+    const int wid = threadIdx.x / kWave;
+    WaveStage& st = stage[wid];
+    const uint64_t blk_begin = (uint64_t)blockIdx.x * chunk;
+    uint64_t blk_end = blk_begin + chunk;
+    if (blk_end > n) blk_end = n;
+    for (int t = threadIdx.x; t < kHistBins; t += kBlock) kb.hist[t] = 0;
+    if (threadIdx.x == 0) {
+        kb.bound = kSentinelD;
+        kb.cnt = 0;
+    }
+    __syncthreads();
+
+    const unsigned k = args.k;
+    unsigned ccnt = 0;
+    unsigned appended = 0, last_hist = 0;
+
+    // software pipeline: the next iteration's 4 KB per wave is in flight while this one is
+    // classified
+    constexpr uint64_t kStride = (uint64_t)(kBlock / kWave) * kPtsIter;
+    uint64_t base = blk_begin + (uint64_t)wid * kPtsIter;
+    double sink = 0.0;
+    double nx[4], ny[4];
+    bool nv[4];
+    if (base < blk_end) load4(x, y, base, blk_end, lane, nx, ny, nv);
+    for (; base < blk_end; base += kStride) {
+        double px[4], py[4];
+        bool valid[4];
+#pragma unroll
+        for (int s = 0; s < 4; s++) { px[s] = nx[s]; py[s] = ny[s]; valid[s] = nv[s]; }
+        if (base + kStride < blk_end) load4(x, y, base + kStride, blk_end, lane, nx, ny, nv);
+        if (MODE == 1) {
+#pragma unroll
+            for (int s = 0; s < 4; s++) sink += px[s] + py[s];
+            continue;
+        }
+        // squared screen against the block bound: only candidates that may beat it reach the
+        // exact fdlibm distance
+        double T2 = __builtin_huge_val();
+        if (MODE == 0 || MODE >= 5) {
+            const unsigned long long B = *reinterpret_cast<volatile unsigned long long*>(&kb.bound);
+            if (B != kSentinelD) {
+                const double t = __longlong_as_double((long long)B);
+                T2 = (t * t) * kSqHi;
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            bool c = false;
+            for (int b = 0; b < args.nu; b++) c = c || in_box(args.u[b], px[s], py[s]);
+            c = c && valid[s];
+            if (MODE == 0 || MODE >= 5) {
+                const double dx = args.qx - px[s], dy = args.qy - py[s];
+                const double d2 = dx * dx + dy * dy;
+                c = c && !(d2 > T2);
+            }
+            const unsigned long long m = __ballot(c);
+            if (MODE == 2) {
+                sink += (double)__popcll(m);
+                continue;
+            }
+            if (c) {
+                const unsigned pos = ccnt + lanes_below(m);
+                st.cx[pos] = px[s];
+                st.cy[pos] = py[s];
+                st.ci[pos] = (unsigned)slot_index(base, lane, s);
+            }
+            ccnt += (unsigned)__popcll(m);
+        }
+        if (MODE == 2) continue;
+        wave_lds_sync();
+        if (MODE == 3) {
+            while (ccnt >= 64) {
+                const unsigned from = ccnt - 64;
+                sink += jts_pp_distance(args.qx, args.qy, st.cx[from + lane], st.cy[from + lane]);
+                wave_lds_sync();
+                ccnt = from;
+            }
+            continue;
+        }
+        if (ccnt >= 64) {
+            knn_dist_batch(st, ccnt, kb, args, spill_d, spill_i, spill_cnt, appended, false);
+            // refresh the block bound once this wave has added survivors
+            if (appended != last_hist && *reinterpret_cast<volatile unsigned*>(&kb.cnt) >= k) {
+                hist_bound(kb, k, args.hist_base);
+                last_hist = appended;
+            }
+        }
+    }
+    if (MODE >= 1 && MODE <= 3) {
+        if (sink == 12345.678) part_d[blockIdx.x] = 1;  // keep the ablated work alive
+        return;
+    }
+    knn_dist_batch(st, ccnt, kb, args, spill_d, spill_i, spill_cnt, appended, true);
+    if (MODE == 5) {
+        if (lane == 0) atomicAdd(&part_i[0], appended);
+        return;
+    }
+    if (MODE == 7) {
+        if (appended == 12345) part_d[blockIdx.x] = 1;
+        return;
+    }
+
+    // ---- end of block: keep the survivors <= final bound, sort once, write the block list
+    constexpr int N = 64 * KPL;
+    constexpr int KPL2 = 2 * KPL;
+    __syncthreads();
+    if (wid == 0 && kb.cnt >= k) hist_bound(kb, k, args.hist_base);
+    if (threadIdx.x == 0) kb.final_cnt = 0;
+    __syncthreads();
+    const unsigned long long B = kb.bound;
+    const unsigned have = kb.cnt < (unsigned)kBlkCap ? kb.cnt : (unsigned)kBlkCap;
+    // compact survivors <= B into the (now idle) wave stages
+    unsigned long long* cd = reinterpret_cast<unsigned long long*>(&stage[0].cx[0]);
+    unsigned* ci = reinterpret_cast<unsigned*>(&stage[2].cx[0]);
+    for (unsigned t0 = 0; t0 < have; t0 += kBlock) {
+        const unsigned t = t0 + threadIdx.x;
+        const bool keep = t < have && kb.bd[t] <= B;
+        const unsigned long long m = __ballot(keep);
+        unsigned wbase = 0;
+        if (lane == 0 && m) wbase = atomicAdd(&kb.final_cnt, (unsigned)__popcll(m));
+        wbase = __shfl(wbase, 0);
+        if (keep) {
+            const unsigned pos = wbase + lanes_below(m);
+            cd[pos] = kb.bd[t];
+            ci[pos] = kb.bi[t];
+        }
+    }
+    __syncthreads();
+    const unsigned fc = kb.final_cnt;
+    const size_t off = (size_t)blockIdx.x * N;
+    if (fc <= 64u && KPL == 1) {
+        if (wid == 0) {  // common case: one 64-lane register sort
+            KE e = ksentinel();
+            if ((unsigned)lane < fc) { e.d = cd[lane]; e.i = ci[lane]; }
+            e = wave_sort64(e);
+            part_d[off + lane] = e.d;
+            part_i[off + lane] = e.i;
+        }
+        return;
+    }
+    if (fc <= (unsigned)(64 * KPL2)) {
+        if (wid == 0) {
+            WList<KPL2> S;
+#pragma unroll
+            for (int s = 0; s < KPL2; s++) {
+                const unsigned e = (unsigned)(s * 64 + lane);
+                S.s[s] = ksentinel();
+                if (e < fc) { S.s[s].d = cd[e]; S.s[s].i = ci[e]; }
+            }
+            wave_sort_list<KPL2>(S);
+#pragma unroll
+            for (int s = 0; s < KPL; s++) {
+                part_d[off + s * 64 + lane] = S.s[s].d;
+                part_i[off + s * 64 + lane] = S.s[s].i;
+            }
+        }
+        return;
+    }
+    // many exact ties around the bound: sort all kept survivors in LDS (uniform branch)
+    int m2 = 1;
+    while (m2 < (int)fc) m2 <<= 1;
+    for (int t = threadIdx.x + fc; t < m2; t += kBlock) { cd[t] = kSentinelD; ci[t] = kSentinelI; }
+    __syncthreads();
+    block_sort_lds(cd, ci, m2);
+    for (int t = threadIdx.x; t < N; t += kBlock) {
+        part_d[off + t] = t < (int)fc ? cd[t] : kSentinelD;
+        part_i[off + t] = t < (int)fc ? ci[t] : kSentinelI;
+    }
+}
+
+// ---------------------------------------------------------------- final selection --------
+// One workgroup of 16 waves.  (1) every wave sorts 64 list heads in registers and the 16
+// sorted runs are merged by a 4-level tree through LDS: T = k-th smallest head, an upper
+// bound of the global k-th key (the k smallest heads are k real entries).  (2) every entry
+// <= T is gathered (lists are ascending: a scan stops at the first entry above T; typically
+// ~k entries in all).  (3) one wave sorts them in registers and writes the top k.
+constexpr int kFinalThreads = 1024;
+constexpr int kFinalWaves = kFinalThreads / kWave;
+constexpr int kFinalCap = 4096;
+
 template <int KPL>
 __global__ __launch_bounds__(kFinalThreads) void knn_final(const unsigned long long* __restrict__ part_d,
                                                            const unsigned* __restrict__ part_i,
                                                            unsigned nlists, unsigned list_len, unsigned k,
                                                            double* __restrict__ out_d, unsigned* __restrict__ out_i,
-                                                           unsigned* __restrict__ out_count) {
+                                                           unsigned* __restrict__ out_count,
+                                                           const unsigned long long* __restrict__ spill_d,
+                                                           const unsigned* __restrict__ spill_i,
+                                                           unsigned* __restrict__ spill_cnt) {
     constexpr int N = 64 * KPL;
     constexpr int KPL2 = 2 * KPL;
     __shared__ unsigned long long xd[kFinalWaves / 2 * N];
@@ -393,6 +497,20 @@ __global__ __launch_bounds__(kFinalThreads) void knn_final(const unsigned long l
             if (!take(e)) break;
         }
     }
+    // survivors a scan block could not keep in LDS (unsorted, usually none)
+    unsigned spill_snapshot = 0;
+    if (spill_cnt) {
+        const unsigned ns = *spill_cnt;
+        spill_snapshot = ns;
+        for (unsigned t = threadIdx.x; t < ns; t += blockDim.x) {
+            KE e;
+            e.d = spill_d[t];
+            e.i = spill_i[t];
+            take(e);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) *spill_cnt = 0;  // ready for the next window on this stream
+    }
     __syncthreads();
     const unsigned total = cnt;
     const unsigned outn = total < k ? total : k;
@@ -424,7 +542,7 @@ __global__ __launch_bounds__(kFinalThreads) void knn_final(const unsigned long l
         while (m < (int)total) m <<= 1;
         for (int t = threadIdx.x + total; t < m; t += blockDim.x) { bd[t] = kSentinelD; bi[t] = kSentinelI; }
         __syncthreads();
-        block_sort(bd, bi, m);
+        block_sort_lds(bd, bi, m);
         for (unsigned t = threadIdx.x; t < k; t += blockDim.x) {
             out_d[t] = __longlong_as_double((long long)(t < outn ? bd[t] : kSentinelD));
             out_i[t] = t < outn ? bi[t] : kSentinelI;
@@ -433,6 +551,7 @@ __global__ __launch_bounds__(kFinalThreads) void knn_final(const unsigned long l
         return;
     }
     // pathological (massive exact ties): k rounds of "smallest key above the previous one"
+    const size_t spill_total = spill_cnt ? spill_snapshot : 0;
     unsigned long long prev_d = 0;
     unsigned prev_i = 0;
     bool have_prev = false;
@@ -440,9 +559,10 @@ __global__ __launch_bounds__(kFinalThreads) void knn_final(const unsigned long l
     for (unsigned r = 0; r < k; r++) {
         unsigned long long best_d = kSentinelD;
         unsigned best_i = kSentinelI;
-        for (size_t t = threadIdx.x; t < (size_t)nlists * list_len; t += blockDim.x) {
-            const unsigned long long ed = part_d[t];
-            const unsigned ei = part_i[t];
+        const size_t nl = (size_t)nlists * list_len;
+        for (size_t t = threadIdx.x; t < nl + spill_total; t += blockDim.x) {
+            const unsigned long long ed = t < nl ? part_d[t] : spill_d[t - nl];
+            const unsigned ei = t < nl ? part_i[t] : spill_i[t - nl];
             if (ed == kSentinelD) continue;
             if (have_prev && !lds_kless(prev_d, prev_i, ed, ei)) continue;
             if (lds_kless(ed, ei, best_d, best_i)) { best_d = ed; best_i = ei; }
@@ -550,11 +670,18 @@ __global__ __launch_bounds__(kBlock) void range_scan(const double* __restrict__ 
         for (int s = 0; s < 4; s++) {
             bool g = false;
             for (int b = 0; b < a.ng; b++) g = g || in_box(a.g[b], px[s], py[s]);
-            const bool c = !g && a.nc && in_box(a.c, px[s], py[s]);
-            const bool hit = valid[s] && (g || (APPROX && c));
+            const bool cbox = !g && a.nc && in_box(a.c, px[s], py[s]);
+            bool hit = valid[s] && (g || (APPROX && cbox));
+            bool cand = false;
+            if (!APPROX && valid[s] && cbox) {
+                // squared screen: certainly inside / outside r without the exact distance
+                const double dx = a.qx - px[s], dy = a.qy - py[s];
+                const double d2 = dx * dx + dy * dy;
+                if (d2 < a.r2lo) hit = true;
+                else if (!(d2 > a.r2hi)) cand = true;
+            }
             hb[s] = __ballot(hit);
             if (!APPROX) {
-                const bool cand = valid[s] && c;
                 const unsigned long long m = __ballot(cand);
                 if (cand) {
                     const unsigned pos = ccnt + lanes_below(m);
@@ -678,30 +805,38 @@ __global__ void selftest_fp64(const double* __restrict__ a, const double* __rest
 // ============================================================================ launchers ===
 hipError_t launch_knn(const double* x, const double* y, uint64_t n, const KnnArgs& args, int kpl,
                       unsigned long long* part_d, unsigned* part_i, unsigned nblocks, uint64_t chunk, double* out_d,
-                      unsigned* out_i, unsigned* out_count, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+                      unsigned* out_i, unsigned* out_count, unsigned long long* spill_d, unsigned* spill_i,
+                      unsigned* spill_cnt, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
     if (ev0) hipEventRecord(ev0, st);
     if (nblocks > 0) {
         switch (kpl) {
-            case 1: knn_scan<1><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i); break;
-            case 2: knn_scan<2><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i); break;
-            case 4: knn_scan<4><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i); break;
+            case 1: knn_scan<1><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt); break;
+            case 2: knn_scan<2><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt); break;
+            case 4: knn_scan<4><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt); break;
             default: return hipErrorInvalidValue;
         }
     }
     if (ev1) hipEventRecord(ev1, st);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return launch_knn_merge(part_d, part_i, nblocks, 64u * (unsigned)kpl, args.k, out_d, out_i, out_count, st);
+    const unsigned k = args.k;
+    const unsigned L = 64u * (unsigned)kpl;
+    if (k <= 64) knn_final<1><<<1, kFinalThreads, 0, st>>>(part_d, part_i, nblocks, L, k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt);
+    else if (k <= 128) knn_final<2><<<1, kFinalThreads, 0, st>>>(part_d, part_i, nblocks, L, k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt);
+    else knn_final<4><<<1, kFinalThreads, 0, st>>>(part_d, part_i, nblocks, L, k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt);
+    return hipGetLastError();
 }
 
 hipError_t launch_knn_scan_variant(int mode, const double* x, const double* y, uint64_t n, const KnnArgs& args,
                                    unsigned long long* part_d, unsigned* part_i, unsigned nblocks, uint64_t chunk,
-                                   hipStream_t st) {
+                                   unsigned long long* spill_d, unsigned* spill_i, unsigned* spill_cnt, hipStream_t st) {
     switch (mode) {
-        case 0: knn_scan<1, 0><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i); break;
-        case 1: knn_scan<1, 1><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i); break;
-        case 2: knn_scan<1, 2><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i); break;
-        case 3: knn_scan<1, 3><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i); break;
+        case 0: knn_scan<1, 0><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt); break;
+        case 1: knn_scan<1, 1><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt); break;
+        case 2: knn_scan<1, 2><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt); break;
+        case 3: knn_scan<1, 3><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt); break;
+        case 5: knn_scan<1, 5><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt); break;
+        case 7: knn_scan<1, 7><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -709,9 +844,9 @@ hipError_t launch_knn_scan_variant(int mode, const double* x, const double* y, u
 
 hipError_t launch_knn_merge(const unsigned long long* d, const unsigned* i, unsigned nlists, unsigned list_len,
                             unsigned k, double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st) {
-    if (k <= 64) knn_final<1><<<1, kFinalThreads, 0, st>>>(d, i, nlists, list_len, k, out_d, out_i, out_count);
-    else if (k <= 128) knn_final<2><<<1, kFinalThreads, 0, st>>>(d, i, nlists, list_len, k, out_d, out_i, out_count);
-    else knn_final<4><<<1, kFinalThreads, 0, st>>>(d, i, nlists, list_len, k, out_d, out_i, out_count);
+    if (k <= 64) knn_final<1><<<1, kFinalThreads, 0, st>>>(d, i, nlists, list_len, k, out_d, out_i, out_count, nullptr, nullptr, nullptr);
+    else if (k <= 128) knn_final<2><<<1, kFinalThreads, 0, st>>>(d, i, nlists, list_len, k, out_d, out_i, out_count, nullptr, nullptr, nullptr);
+    else knn_final<4><<<1, kFinalThreads, 0, st>>>(d, i, nlists, list_len, k, out_d, out_i, out_count, nullptr, nullptr, nullptr);
     return hipGetLastError();
 }
 

@@ -341,3 +341,38 @@ def test_ppoly_boundary_and_outside(ctx):
         got = ctx.range_ppoly(ag, x, y, off, vx, vy, rr)
         want = cref.range_ppoly(cg, x, y, off, vx, vy, rr)
         assert pairs_sorted(got).tolist() == pairs_sorted(want).tolist()
+
+
+def test_range_circle_band(ctx):
+    """Points within a few ulps of the query circle exercise the exact-distance band behind the
+    squared screens (fast accept / fast reject must never decide these)."""
+    ag, cg = agrid(100)
+    rng = np.random.default_rng(12)
+    r = 0.05
+    th = rng.uniform(0, 2 * np.pi, 40000)
+    x = Q[0] + r * np.cos(th)
+    y = Q[1] + r * np.sin(th)
+    xs = np.concatenate([x, np.nextafter(x, np.inf), np.nextafter(x, -np.inf), x + 1e-17, x - 3e-17])
+    ys = np.concatenate([y, y, y, np.nextafter(y, np.inf), np.nextafter(y, -np.inf)])
+    for rr in (r, np.nextafter(r, 0), np.nextafter(r, 1)):
+        got = ctx.range_pp(ag, xs, ys, Q[0], Q[1], rr)
+        want = cref.range_pp(cg, xs, ys, Q[0], Q[1], rr)
+        assert got.tolist() == sorted(want.tolist())
+
+
+def test_knn_equal_distance_shell(ctx):
+    """Thousands of points on (almost) one circle around the query: the k-th distance sits in
+    a dense band, so the squared screen and the exact comparison must agree bit for bit."""
+    ag, cg = agrid(100)
+    rng = np.random.default_rng(13)
+    th = rng.uniform(0, 2 * np.pi, 50000)
+    rad = 0.03 + rng.integers(-3, 4, 50000) * 1e-17
+    x = Q[0] + rad * np.cos(th)
+    y = Q[1] + rad * np.sin(th)
+    bx, by = _window(rng, 200000)
+    x = np.concatenate([bx, x])
+    y = np.concatenate([by, y])
+    for k in (10, 64, 256):
+        oi, od = ctx.knn_pp(ag, x, y, Q[0], Q[1], 0.5, k)
+        wi, wd = cref.knn_pp(cg, x, y, Q[0], Q[1], 0.5, k)
+        assert oi.tolist() == wi.tolist() and np.array_equal(od.view(np.uint64), wd.view(np.uint64))
