@@ -47,6 +47,8 @@ def parse():
     p.add_argument("--points", type=int, default=N_PER_GPU)
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--knn-final", choices=("fused", "separate"), default="fused",
+                   help="final selection in the scan's last block, or a separate knn_final launch")
     return p.parse_args()
 
 
@@ -107,6 +109,7 @@ def main():
 
     dev = torch.device("cuda", local)
     ctx = Context(local)
+    _abi.debug_set_knn_fused(args.knn_final == "fused")
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)  # kernels and RCCL ordered on one stream
     bj = synth.BEIJING
@@ -183,7 +186,8 @@ def main():
         "config": {"workload": "C2: point-point kNN k=50, 100x100 Beijing UniformGrid, r=0.5, README query, "
                                f"{n} uniform points per window per GPU (BASELINE.json configs[1])",
                    "points_per_window_per_gpu": n, "grid": GRID_N, "k": K, "radius": RADIUS,
-                   "windows_resident": WINDOWS, "parallelism": f"shard{world}"},
+                   "windows_resident": WINDOWS, "final_selection": args.knn_final,
+                   "parallelism": f"shard{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(),
                      "kernel": "geohip::knn_scan<1>", "avg_kernel_us": avg_scan_s * 1e6,

@@ -1,5 +1,6 @@
 """Attribute knn_scan time: ablation variants timed in one process, interleaved rounds
-(MODE 1 loads only, 2 + classification, 3 + staging/distances, 0 full), plus a plain
+(MODE 1 loads only, 2 + classification, 3 + staging/distances, 7 no block tail, 8 block lists
+only (no fused final), 9 = 8 + separate knn_final, 0 full incl. the fused final selection), plus a plain
 streaming-read reference (torch sum) on the same 4-window ring."""
 import json
 import sys
@@ -22,9 +23,9 @@ for w in range(W):
     ctx.synth_uniform_async(x[w * n:(w + 1) * n], y[w * n:(w + 1) * n], 0, 2 + 7919 * w, bj)
 torch.cuda.synchronize()
 grid = _abi.make_grid(bj[0], bj[2], (bj[1] - bj[0]) / 100, 100)
-res = {m: [] for m in (1, 2, 3, 7, 0)}
+res = {m: [] for m in (1, 2, 3, 7, 8, 9, 0)}
 for rnd in range(5):
-    for m in (1, 2, 3, 7, 0):
+    for m in (1, 2, 3, 7, 8, 9, 0):
         res[m].append(ctx.debug_knn_scan_variant(m, grid, x, y, n, W, q[0], q[1], 0.5, 50, reps=20) * 1e3)
 out = {f"mode{m}_us": sorted(v)[len(v) // 2] for m, v in res.items()}
 t5, nsurv, nspill = ctx.debug_knn_scan_variant(5, grid, x, y, n, W, q[0], q[1], 0.5, 50, reps=5)

@@ -107,6 +107,7 @@ _SIGS = {
                                            c_double]),
     "geohip_debug_selftest_fp64": (c_int, [_P, _P, _P, c_uint64, _P, _P, _P, _P]),
     "geohip_debug_classify": (c_int, [POINTER(Grid), c_double, c_double, c_double, _P, _P, c_uint64, _P]),
+    "geohip_debug_set_knn_fused": (None, [c_int]),
     "geohip_debug_knn_scan_variant": (c_int, [_P, c_int, POINTER(Grid), _P, _P, c_uint64, c_int, c_double,
                                               c_double, c_double, c_uint32, c_int, _P]),
 }
@@ -158,6 +159,12 @@ def debug_classify(grid: Grid, qx: float, qy: float, r: float, x: np.ndarray, y:
     if rc:
         raise _ERRORS.get(rc, GeohipError)(f"debug_classify failed ({rc})")
     return out
+
+
+def debug_set_knn_fused(fused: bool) -> None:
+    """Test/measurement hook: kNN final selection inside the scan's last block (default) or
+    as a separate knn_final launch."""
+    lib.geohip_debug_set_knn_fused(1 if fused else 0)
 
 
 def plan_cell(grid: Grid, x: float, y: float):

@@ -208,8 +208,8 @@ int knn_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const
     if (chunk < 1024) chunk = 1024;
     uint64_t nblocks = a.nu > 0 ? (n + chunk - 1) / chunk : 0;  // empty G u C: no candidates
     const uint64_t N = 64ull * kpl;
-    rc = ensure(ctx, S_PART_D, nblocks * N * 8);
-    if (!rc) rc = ensure(ctx, S_PART_I, nblocks * N * 4);
+    rc = ensure(ctx, S_PART_D, nblocks * (N + 4) * 8);  // block lists, then the packed heads (kHeads = 4)
+    if (!rc) rc = ensure(ctx, S_PART_I, nblocks * (N + 4) * 4);
     if (!rc) rc = ensure(ctx, S_SPILL_D, n * 8);  // worst case: every point survives
     if (!rc) rc = ensure(ctx, S_SPILL_I, n * 4);
     if (!rc) rc = ensure_zeroed(ctx, S_SPILL_CNT, 16);
@@ -534,25 +534,31 @@ int geohip_debug_knn_scan_variant(geohip_ctx* ctx, int mode, const geohip_grid* 
     chunk = (chunk + 1) & ~1ull;
     if (chunk < 1024) chunk = 1024;
     const uint64_t nblocks = (n + chunk - 1) / chunk;
-    rc = ensure(ctx, S_PART_D, nblocks * 64 * 8);
-    if (!rc) rc = ensure(ctx, S_PART_I, nblocks * 64 * 4);
+    rc = ensure(ctx, S_PART_D, nblocks * (64 + 4) * 8);
+    if (!rc) rc = ensure(ctx, S_PART_I, nblocks * (64 + 4) * 4);
     if (!rc) rc = ensure(ctx, S_SPILL_D, n * 8);
     if (!rc) rc = ensure(ctx, S_SPILL_I, n * 4);
     if (!rc) rc = ensure_zeroed(ctx, S_SPILL_CNT, 16);
+    if (!rc) rc = ensure(ctx, S_OUT_D, (size_t)(k ? k : 1) * 8);
+    if (!rc) rc = ensure(ctx, S_OUT_I, (size_t)(k ? k : 1) * 4);
+    if (!rc) rc = ensure(ctx, S_OUT_CNT, 8);
     if (rc) return rc;
     unsigned long long* sd = B<unsigned long long>(ctx, S_SPILL_D);
     unsigned* si = B<unsigned>(ctx, S_SPILL_I);
     unsigned* sc = B<unsigned>(ctx, S_SPILL_CNT);
+    double* od = B<double>(ctx, S_OUT_D);
+    unsigned* oi = B<unsigned>(ctx, S_OUT_I);
+    unsigned* oc = B<unsigned>(ctx, S_OUT_CNT);
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
     HIPCHK(launch_knn_scan_variant(mode, x, y, n, a, B<unsigned long long>(ctx, S_PART_D), B<unsigned>(ctx, S_PART_I),
-                                   (unsigned)nblocks, chunk, sd, si, sc, ctx->stream));
+                                   (unsigned)nblocks, chunk, sd, si, sc, od, oi, oc, ctx->stream));
     HIPCHK(hipEventRecord(e0, ctx->stream));
     for (int i = 0; i < reps; i++) {
         const uint64_t w = (uint64_t)(i % (nwin > 0 ? nwin : 1)) * n;  // cycle windows: no Infinity-Cache reuse
         HIPCHK(launch_knn_scan_variant(mode, x + w, y + w, n, a, B<unsigned long long>(ctx, S_PART_D),
-                                       B<unsigned>(ctx, S_PART_I), (unsigned)nblocks, chunk, sd, si, sc, ctx->stream));
+                                       B<unsigned>(ctx, S_PART_I), (unsigned)nblocks, chunk, sd, si, sc, od, oi, oc, ctx->stream));
     }
     HIPCHK(hipEventRecord(e1, ctx->stream));
     HIPCHK(hipEventSynchronize(e1));
@@ -561,10 +567,11 @@ int geohip_debug_knn_scan_variant(geohip_ctx* ctx, int mode, const geohip_grid* 
     hipEventDestroy(e0);
     hipEventDestroy(e1);
     *ms_per_launch = ms / (reps > 0 ? reps : 1);
+    HIPCHK(hipMemsetAsync(sc, 0, 16, ctx->stream));  // list-only modes leave spill counts behind
     if (mode == 5) {  // counters of one extra launch: sorts and passing candidates, summed
         HIPCHK(hipMemsetAsync(ctx->buf[S_PART_I], 0, 8, ctx->stream));
         HIPCHK(launch_knn_scan_variant(mode, x, y, n, a, B<unsigned long long>(ctx, S_PART_D),
-                                       B<unsigned>(ctx, S_PART_I), (unsigned)nblocks, chunk, sd, si, sc, ctx->stream));
+                                       B<unsigned>(ctx, S_PART_I), (unsigned)nblocks, chunk, sd, si, sc, od, oi, oc, ctx->stream));
         unsigned c[2];
         HIPCHK(hipMemcpy(&c[1], sc, 4, hipMemcpyDeviceToHost));
         HIPCHK(hipMemsetAsync(sc, 0, 4, ctx->stream));
@@ -611,6 +618,9 @@ int geohip_debug_selftest_fp64(geohip_ctx* ctx, const double* a, const double* b
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return GEOHIP_OK;
 }
+
+// Debug hook: 1 = final selection fused into the scan (default), 0 = separate knn_final launch.
+void geohip_debug_set_knn_fused(int fused) { set_knn_fused(fused); }
 
 }  // extern "C"
 

@@ -24,15 +24,19 @@ struct RangeArgs {
     double r2lo, r2hi;  // squared screens (device_common.h kSqLo/kSqHi); r2lo < 0 disables
 };
 
-// kNN scan over ceil(n / chunk) = nblocks blocks (chunk a multiple of 1024), then the final
-// selection into out_*.  ev0/ev1 (optional) bracket the scan kernel only.
+// kNN scan over ceil(n / chunk) = nblocks blocks (chunk a multiple of 1024); its last-arriving
+// block runs the final selection into out_* (spill_cnt[0] = spill count, spill_cnt[1] = arrival
+// ticket; both zero between launches).  ev0/ev1 (optional) bracket the one scan launch.
 hipError_t launch_knn(const double* x, const double* y, uint64_t n, const KnnArgs& args, int kpl,
                       unsigned long long* part_d, unsigned* part_i, unsigned nblocks, uint64_t chunk, double* out_d,
                       unsigned* out_i, unsigned* out_count, unsigned long long* spill_d, unsigned* spill_i,
                       unsigned* spill_cnt, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_knn_scan_variant(int mode, const double* x, const double* y, uint64_t n, const KnnArgs& args,
                                    unsigned long long* part_d, unsigned* part_i, unsigned nblocks, uint64_t chunk,
-                                   unsigned long long* spill_d, unsigned* spill_i, unsigned* spill_cnt, hipStream_t st);
+                                   unsigned long long* spill_d, unsigned* spill_i, unsigned* spill_cnt, double* out_d,
+                                   unsigned* out_i, unsigned* out_count, hipStream_t st);
+// 1: final selection in the scan's last-arriving block (default); 0: separate knn_final launch
+void set_knn_fused(int fused);
 hipError_t launch_knn_merge(const unsigned long long* d, const unsigned* i, unsigned nlists, unsigned list_len,
                             unsigned k, double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st);
 // range: bitmask (16 words / 1024 pts), unit_count (units), offs (units) scratch.

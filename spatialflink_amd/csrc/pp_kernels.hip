@@ -90,6 +90,26 @@ __device__ void block_sort_lds(unsigned long long* d, unsigned* i, int m) {
 // at which the cumulative count reaches k.  That is a valid upper bound of the block's k-th
 // distance (>= k real candidates lie at or below it), shared by the four waves from the first
 // survivors on, and it costs LDS atomics instead of per-wave sorting networks.
+// Re-read an LDS word other waves update.  A volatile access through a generic pointer
+// compiles to flat_load sc0 sc1, which counts against vmcnt and makes the compiler drain
+// every outstanding global load (the scan's prefetch) before it; a compiler barrier + a plain
+// access stays a ds_read with an lgkmcnt wait.
+template <typename T>
+__device__ __forceinline__ T lds_fresh(const T& v) {
+    asm volatile("" ::: "memory");
+    return v;
+}
+
+// write-through (sc1) stores: data another workgroup of the same launch reads (Guideline 16 R1)
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+__device__ __forceinline__ void store_wt(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(((gu64*)(p)), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void store_wt(unsigned* p, unsigned v) {
+    __hip_atomic_store(((gu32*)(p)), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 constexpr int kHistBins = 512;
 constexpr int kBlkCap = 768;  // 4 blocks/CU: stages 25.6 KB + this ~11.3 KB <= 40 KB
 
@@ -107,14 +127,14 @@ __device__ __forceinline__ int hist_bin(unsigned long long db, int base) {
     return b < 0 ? 0 : (b >= kHistBins ? kHistBins - 1 : (int)b);
 }
 
-// One wave: smallest bin whose cumulative count reaches k -> LDS bound (atomic min).
-__device__ __forceinline__ void hist_bound(KnnBlock& kb, unsigned k, int base) {
+// One wave: smallest bin whose cumulative count reaches k (wave-uniform), -1 if none.
+__device__ __forceinline__ int hist_kth_bin(const unsigned* hist, unsigned k) {
     const int lane = lane_id();
     unsigned c[8];
     unsigned tot = 0;
 #pragma unroll
     for (int j = 0; j < 8; j++) {
-        c[j] = kb.hist[lane * 8 + j];
+        c[j] = hist[lane * 8 + j];
         tot += c[j];
     }
     unsigned incl = tot;  // inclusive prefix over lanes
@@ -124,7 +144,7 @@ __device__ __forceinline__ void hist_bound(KnnBlock& kb, unsigned k, int base) {
         if (lane >= o) incl += v;
     }
     const unsigned long long m = __ballot(incl >= k);
-    if (m == 0) return;
+    if (m == 0) return -1;
     const int first = __builtin_ctzll(m);
     int bin = kHistBins - 1;
     if (lane == first) {
@@ -134,11 +154,19 @@ __device__ __forceinline__ void hist_bound(KnnBlock& kb, unsigned k, int base) {
             run += c[j];
             if (run >= k) { bin = lane * 8 + j; break; }
         }
-        if (bin < kHistBins - 1) {
-            const unsigned long long B = ((unsigned long long)(bin + base + 1) << 48) - 1ull;
-            atomicMin(&kb.bound, B);
-        }
     }
+    return __shfl(bin, first);
+}
+
+// upper edge (distance bits) of histogram bin `bin`
+__device__ __forceinline__ unsigned long long hist_edge(int bin, int base) {
+    return ((unsigned long long)(bin + base + 1) << 48) - 1ull;
+}
+
+// One wave: the block bound from the survivor histogram (LDS atomic min).
+__device__ __forceinline__ void hist_bound(KnnBlock& kb, unsigned k, int base) {
+    const int bin = hist_kth_bin(kb.hist, k);
+    if (bin >= 0 && bin < kHistBins - 1 && lane_id() == 0) atomicMin(&kb.bound, hist_edge(bin, base));
 }
 
 // exact distances of up to 64 staged candidates, survivors appended to the block buffer
@@ -158,7 +186,7 @@ __device__ __forceinline__ void knn_dist_batch(WaveStage& st, unsigned& ccnt, Kn
             py = st.cy[from + lane];
             pi = st.ci[from + lane];
         }
-        const unsigned long long B = *reinterpret_cast<volatile unsigned long long*>(&kb.bound);
+        const unsigned long long B = lds_fresh(kb.bound);
         wave_lds_sync();
         ccnt = from;
         const double d = jts_pp_distance(a.qx, a.qy, px, py);
@@ -182,8 +210,8 @@ __device__ __forceinline__ void knn_dist_batch(WaveStage& st, unsigned& ccnt, Kn
                     kb.bd[slot] = db;
                     kb.bi[slot] = pi;
                 } else {
-                    spill_d[gbase + (slot - pos)] = db;
-                    spill_i[gbase + (slot - pos)] = pi;
+                    store_wt(&spill_d[gbase + (slot - pos)], db);
+                    store_wt(&spill_i[gbase + (slot - pos)], pi);
                 }
                 atomicAdd(&kb.hist[hist_bin(db, a.hist_base)], 1u);
             }
@@ -192,6 +220,322 @@ __device__ __forceinline__ void knn_dist_batch(WaveStage& st, unsigned& ccnt, Kn
         wave_lds_sync();
     }
 }
+
+// ---------------------------------------------------------------- final selection --------
+// final_select<KPL, NT, OWN>: NT threads (NT/64 waves) reduce nlists ascending lists of
+// list_len entries (plus the unsorted spill buffer) to the k smallest keys.
+//  (1) every wave sorts its 64-head batches in registers and the wave runs are merged by a
+//      tree through LDS: T = k-th smallest head, an upper bound of the global k-th key (the k
+//      smallest heads are k real entries);
+//  (2) every entry <= T is gathered (lists ascending: a list scan stops at the first entry
+//      above T; ~k entries in all, nearly always within the two entries preloaded per list);
+//  (3) one wave sorts them in registers and writes the top k.
+// Every global load of (1)-(2) is issued up front (OWN lists of two entries per thread and the
+// spill count), so the selection pays one memory latency.  It runs as the knn_final kernel
+// (merges of rank results) and inside knn_scan's last-arriving block.
+constexpr int kFinalThreads = 1024;
+constexpr int kFinalCap = 4096;
+constexpr int kHeads = 4;  // entries per list preloaded by the final selection (packed heads)
+
+struct FinalIo {
+    const unsigned long long* part_d;
+    const unsigned* part_i;
+    unsigned nlists, list_len, k;
+    double* out_d;
+    unsigned* out_i;
+    unsigned* out_count;
+    const unsigned long long* spill_d;  // null: no spill buffer (rank merges)
+    const unsigned* spill_i;
+    unsigned* spill_cnt;
+    const unsigned long long* head_d;  // null, or the first kHeads entries of every list packed
+    const unsigned* head_i;            // (head_d[kHeads l + j]): coalesced head loads
+    int hist_base;                     // histogram origin for the head-histogram T (head_d != null)
+};
+
+struct FinalLds {  // LDS working set (the fused form reuses the scan's stages)
+    unsigned long long* xd;  // tree exchange, (NT / 128) * 64 * KPL entries
+    unsigned* xi;
+    unsigned long long* bd;  // gathered entries
+    unsigned* bi;
+    unsigned cap;            // >= NT
+    unsigned* cnt;
+    unsigned long long* Td;
+    unsigned* Ti;
+    unsigned* hist;          // kHistBins words (used with FinalIo::head_d)
+};
+
+template <int KPL, int NT, int OWN>
+__device__ void final_select(const FinalIo& io, const FinalLds& s) {
+    constexpr int N = 64 * KPL;
+    constexpr int KPL2 = 2 * KPL;
+    constexpr int NW = NT / kWave;
+    const int lane = lane_id();
+    const int wid = threadIdx.x / kWave;
+    const unsigned nlists = io.nlists, list_len = io.list_len, k = io.k;
+    if (threadIdx.x == 0) {
+        *s.cnt = 0;
+        *s.Td = kSentinelD;
+        *s.Ti = kSentinelI;
+    }
+    unsigned nspill = 0;
+    if (io.spill_cnt) nspill = __hip_atomic_load(io.spill_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    KE e[OWN][kHeads];  // first kHeads entries of every owned list
+#pragma unroll
+    for (int j = 0; j < OWN; j++) {
+#pragma unroll
+        for (int h = 0; h < kHeads; h++) e[j][h] = ksentinel();
+        const unsigned own = threadIdx.x + (unsigned)(j * NT);
+        if (own < nlists && io.head_d) {
+            const ulonglong2 d01 = *reinterpret_cast<const ulonglong2*>(io.head_d + (size_t)kHeads * own);
+            const ulonglong2 d23 = *reinterpret_cast<const ulonglong2*>(io.head_d + (size_t)kHeads * own + 2);
+            const uint4 i4 = *reinterpret_cast<const uint4*>(io.head_i + (size_t)kHeads * own);
+            e[j][0].d = d01.x; e[j][1].d = d01.y; e[j][2].d = d23.x; e[j][3].d = d23.y;
+            e[j][0].i = i4.x; e[j][1].i = i4.y; e[j][2].i = i4.z; e[j][3].i = i4.w;
+        } else if (own < nlists) {
+            const size_t off = (size_t)own * list_len;
+#pragma unroll
+            for (int h = 0; h < kHeads; h++) {
+                if ((unsigned)h < list_len) {
+                    e[j][h].d = io.part_d[off + h];
+                    e[j][h].i = io.part_i[off + h];
+                }
+            }
+        }
+    }
+    // (1a) T from a histogram of the heads (LDS atomics, one wave scan): the upper edge of the
+    // bin where the cumulative head count reaches k.  >= k heads lie at or below it, so it is a
+    // valid T; left unresolved (exact path below) when that bin is the lowest or the top one.
+    bool resolved = false;
+    if (nlists >= k && io.head_d && OWN * NT >= (int)nlists) {
+        for (int t = threadIdx.x; t < kHistBins; t += NT) s.hist[t] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < OWN; j++)
+            if (e[j][0].d != kSentinelD) atomicAdd(&s.hist[hist_bin(e[j][0].d, io.hist_base)], 1u);
+        __syncthreads();
+        if (wid == 0) {
+            const int bin = hist_kth_bin(s.hist, k);
+            if (lane == 0 && bin > 0 && bin < kHistBins - 1) {
+                *s.Td = hist_edge(bin, io.hist_base);
+                *s.Ti = kSentinelI;
+            }
+        }
+        __syncthreads();
+        resolved = *s.Td != kSentinelD;
+    }
+    // (1b) exact: T = k-th smallest head
+    if (nlists >= k && !resolved) {
+        WList<KPL> L;
+#pragma unroll
+        for (int q = 0; q < KPL; q++) L.s[q] = ksentinel();
+#pragma unroll
+        for (int j = 0; j < OWN; j++)
+            if ((unsigned)(j * NT + wid * kWave) < nlists) wave_merge_batch<KPL>(L, wave_sort64(e[j][0]));
+        for (unsigned g = (unsigned)(wid * kWave + OWN * NT); g < nlists; g += NT) {
+            KE h = ksentinel();
+            const unsigned p = g + lane;
+            if (p < nlists) {
+                h.d = io.part_d[(size_t)p * list_len];
+                h.i = io.part_i[(size_t)p * list_len];
+            }
+            wave_merge_batch<KPL>(L, wave_sort64(h));
+        }
+        for (int step = 1; step < NW; step <<= 1) {
+            __syncthreads();
+            if ((wid & (2 * step - 1)) == step) {  // sender
+                const int slot = wid >> 1;
+#pragma unroll
+                for (int q = 0; q < KPL; q++) {
+                    s.xd[slot * N + q * 64 + lane] = L.s[q].d;
+                    s.xi[slot * N + q * 64 + lane] = L.s[q].i;
+                }
+            }
+            __syncthreads();
+            if ((wid & (2 * step - 1)) == 0) {  // receiver of wid + step
+                const int slot = (wid + step) >> 1;
+                WList<KPL> B;
+#pragma unroll
+                for (int q = 0; q < KPL; q++) {
+                    B.s[q].d = s.xd[slot * N + q * 64 + lane];
+                    B.s[q].i = s.xi[slot * N + q * 64 + lane];
+                }
+                wave_merge_lists<KPL>(L, B);
+            }
+        }
+        if (wid == 0) {
+            const KE t = wave_list_get<KPL>(L, (int)k - 1);
+            if (lane == 0) {
+                *s.Td = t.d;
+                *s.Ti = t.i;
+            }
+        }
+    }
+    __syncthreads();
+    const unsigned long long T_d = *s.Td;
+    const unsigned T_i = *s.Ti;
+    // (2) gather every real entry <= T
+    auto take = [&](const KE& e) -> bool {
+        if (e.d == kSentinelD || lds_kless(T_d, T_i, e.d, e.i)) return false;
+        const unsigned pos = atomicAdd(s.cnt, 1u);
+        if (pos < s.cap) {
+            s.bd[pos] = e.d;
+            s.bi[pos] = e.i;
+        }
+        return true;
+    };
+#pragma unroll
+    for (int j = 0; j < OWN; j++) {
+        const unsigned own = threadIdx.x + (unsigned)(j * NT);
+        if (own >= nlists) continue;
+        bool more = true;
+#pragma unroll
+        for (int h = 0; h < kHeads; h++) more = more && take(e[j][h]);
+        if (more) {  // all preloaded entries taken: the rest of the list from memory (rare)
+            const size_t off = (size_t)own * list_len;
+            for (unsigned q = kHeads; q < list_len; q++) {
+                KE e;
+                e.d = io.part_d[off + q];
+                e.i = io.part_i[off + q];
+                if (!take(e)) break;
+            }
+        }
+    }
+    for (unsigned p = threadIdx.x + (unsigned)(OWN * NT); p < nlists; p += NT) {
+        const size_t off = (size_t)p * list_len;
+        for (unsigned q = 0; q < list_len; q++) {
+            KE e;
+            e.d = io.part_d[off + q];
+            e.i = io.part_i[off + q];
+            if (!take(e)) break;
+        }
+    }
+    // survivors a scan block could not keep in LDS (unsorted, usually none)
+    for (unsigned t = threadIdx.x; t < nspill; t += NT) {
+        KE e;
+        e.d = io.spill_d[t];
+        e.i = io.spill_i[t];
+        take(e);
+    }
+    __syncthreads();
+    if (io.spill_cnt && threadIdx.x == 0) *io.spill_cnt = 0;  // ready for the next window on this stream
+    const unsigned total = *s.cnt;
+    const unsigned outn = total < k ? total : k;
+    if (total <= (unsigned)(64 * KPL2)) {
+        // (3) one wave: register bitonic sort of <= 128*KPL entries
+        if (wid == 0) {
+            WList<KPL2> S;
+#pragma unroll
+            for (int q = 0; q < KPL2; q++) {
+                const unsigned e = (unsigned)(q * 64 + lane);
+                S.s[q] = ksentinel();
+                if (e < total) {
+                    S.s[q].d = s.bd[e];
+                    S.s[q].i = s.bi[e];
+                }
+            }
+            wave_sort_list<KPL2>(S);
+#pragma unroll
+            for (int q = 0; q < KPL2; q++) {
+                const unsigned e = (unsigned)(q * 64 + lane);
+                if (e < k) {
+                    io.out_d[e] = __longlong_as_double((long long)(e < outn ? S.s[q].d : kSentinelD));
+                    io.out_i[e] = e < outn ? S.s[q].i : kSentinelI;
+                }
+            }
+            if (lane == 0) *io.out_count = outn;
+        }
+        return;
+    }
+    if (total <= s.cap) {
+        int m = 1;
+        while (m < (int)total) m <<= 1;
+        for (int t = threadIdx.x + total; t < m; t += NT) {
+            s.bd[t] = kSentinelD;
+            s.bi[t] = kSentinelI;
+        }
+        __syncthreads();
+        block_sort_lds(s.bd, s.bi, m);
+        for (unsigned t = threadIdx.x; t < k; t += NT) {
+            io.out_d[t] = __longlong_as_double((long long)(t < outn ? s.bd[t] : kSentinelD));
+            io.out_i[t] = t < outn ? s.bi[t] : kSentinelI;
+        }
+        if (threadIdx.x == 0) *io.out_count = outn;
+        return;
+    }
+    // pathological (massive exact ties): k rounds of "smallest key above the previous one"
+    unsigned long long prev_d = 0;
+    unsigned prev_i = 0;
+    bool have_prev = false;
+    unsigned got = 0;
+    const size_t nl = (size_t)nlists * list_len;
+    for (unsigned r = 0; r < k; r++) {
+        unsigned long long best_d = kSentinelD;
+        unsigned best_i = kSentinelI;
+        for (size_t t = threadIdx.x; t < nl + nspill; t += NT) {
+            const unsigned long long ed = t < nl ? io.part_d[t] : io.spill_d[t - nl];
+            const unsigned ei = t < nl ? io.part_i[t] : io.spill_i[t - nl];
+            if (ed == kSentinelD) continue;
+            if (have_prev && !lds_kless(prev_d, prev_i, ed, ei)) continue;
+            if (lds_kless(ed, ei, best_d, best_i)) {
+                best_d = ed;
+                best_i = ei;
+            }
+        }
+        s.bd[threadIdx.x] = best_d;
+        s.bi[threadIdx.x] = best_i;
+        __syncthreads();
+        for (int h = NT / 2; h > 0; h >>= 1) {
+            if ((int)threadIdx.x < h && lds_kless(s.bd[threadIdx.x + h], s.bi[threadIdx.x + h], s.bd[threadIdx.x], s.bi[threadIdx.x])) {
+                s.bd[threadIdx.x] = s.bd[threadIdx.x + h];
+                s.bi[threadIdx.x] = s.bi[threadIdx.x + h];
+            }
+            __syncthreads();
+        }
+        const unsigned long long vd = s.bd[0];
+        const unsigned vi = s.bi[0];
+        __syncthreads();
+        if (vd == kSentinelD) break;
+        if (threadIdx.x == 0) {
+            io.out_d[r] = __longlong_as_double((long long)vd);
+            io.out_i[r] = vi;
+        }
+        prev_d = vd;
+        prev_i = vi;
+        have_prev = true;
+        got = r + 1;
+    }
+    for (unsigned t = got + threadIdx.x; t < k; t += NT) {
+        io.out_d[t] = __longlong_as_double((long long)kSentinelD);
+        io.out_i[t] = kSentinelI;
+    }
+    if (threadIdx.x == 0) *io.out_count = got;
+}
+
+template <int KPL>
+__global__ __launch_bounds__(kFinalThreads) void knn_final(FinalIo io) {
+    constexpr int N = 64 * KPL;
+    __shared__ unsigned long long xd[kFinalThreads / 128 * N];
+    __shared__ unsigned xi[kFinalThreads / 128 * N];
+    __shared__ unsigned long long bd[kFinalCap];
+    __shared__ unsigned bi[kFinalCap];
+    __shared__ unsigned cnt;
+    __shared__ unsigned long long Td;
+    __shared__ unsigned Ti;
+    __shared__ unsigned hist[kHistBins];
+    const FinalLds s{xd, xi, bd, bi, (unsigned)kFinalCap, &cnt, &Td, &Ti, hist};
+    final_select<KPL, kFinalThreads, 1>(io, s);
+}
+
+// Where a scan writes its result.  ticket != null: the block lists are stored write-through
+// (sc1) and the last block to take a ticket runs final_select into out_* (one launch per
+// window); ticket == null: only the block lists are written (knn_final merges them).
+struct KnnOut {
+    double* out_d;
+    unsigned* out_i;
+    unsigned* out_count;
+    unsigned* ticket;  // zero before the first launch; the last arriver re-zeroes it
+};
+
 
 // MODE (ablation builds for measurement only; the product launches MODE 0):
 //   0 full, 1 loads only, 2 loads + classification, 3 + LDS staging and distances (no selection),
@@ -202,7 +546,8 @@ __global__ __launch_bounds__(kBlock) void knn_scan(const double* __restrict__ x,
                                                    unsigned long long* __restrict__ part_d,
                                                    unsigned* __restrict__ part_i,
                                                    unsigned long long* __restrict__ spill_d,
-                                                   unsigned* __restrict__ spill_i, unsigned* __restrict__ spill_cnt) {
+                                                   unsigned* __restrict__ spill_i, unsigned* __restrict__ spill_cnt,
+                                                   KnnOut out) {
     __shared__ WaveStage stage[kBlock / kWave];
     __shared__ KnnBlock kb;
     const int lane = lane_id();
@@ -245,7 +590,7 @@ __global__ __launch_bounds__(kBlock) void knn_scan(const double* __restrict__ x,
         // exact fdlibm distance
         double T2 = __builtin_huge_val();
         if (MODE == 0 || MODE >= 5) {
-            const unsigned long long B = *reinterpret_cast<volatile unsigned long long*>(&kb.bound);
+            const unsigned long long B = lds_fresh(kb.bound);
             if (B != kSentinelD) {
                 const double t = __longlong_as_double((long long)B);
                 T2 = (t * t) * kSqHi;
@@ -288,7 +633,7 @@ __global__ __launch_bounds__(kBlock) void knn_scan(const double* __restrict__ x,
         if (ccnt >= 64) {
             knn_dist_batch(st, ccnt, kb, args, spill_d, spill_i, spill_cnt, appended, false);
             // refresh the block bound once this wave has added survivors
-            if (appended != last_hist && *reinterpret_cast<volatile unsigned*>(&kb.cnt) >= k) {
+            if (appended != last_hist && lds_fresh(kb.cnt) >= k) {
                 hist_bound(kb, k, args.hist_base);
                 last_hist = appended;
             }
@@ -336,17 +681,22 @@ __global__ __launch_bounds__(kBlock) void knn_scan(const double* __restrict__ x,
     __syncthreads();
     const unsigned fc = kb.final_cnt;
     const size_t off = (size_t)blockIdx.x * N;
+    // packed heads behind the lists (FinalIo::head_d)
+    unsigned long long* head_d = part_d + (size_t)gridDim.x * N;
+    unsigned* head_i = part_i + (size_t)gridDim.x * N;
     if (fc <= 64u && KPL == 1) {
         if (wid == 0) {  // common case: one 64-lane register sort
             KE e = ksentinel();
             if ((unsigned)lane < fc) { e.d = cd[lane]; e.i = ci[lane]; }
             e = wave_sort64(e);
-            part_d[off + lane] = e.d;
-            part_i[off + lane] = e.i;
+            store_wt(&part_d[off + lane], e.d);
+            store_wt(&part_i[off + lane], e.i);
+            if (lane < kHeads) {
+                store_wt(&head_d[kHeads * blockIdx.x + lane], e.d);
+                store_wt(&head_i[kHeads * blockIdx.x + lane], e.i);
+            }
         }
-        return;
-    }
-    if (fc <= (unsigned)(64 * KPL2)) {
+    } else if (fc <= (unsigned)(64 * KPL2)) {
         if (wid == 0) {
             WList<KPL2> S;
 #pragma unroll
@@ -358,245 +708,59 @@ __global__ __launch_bounds__(kBlock) void knn_scan(const double* __restrict__ x,
             wave_sort_list<KPL2>(S);
 #pragma unroll
             for (int s = 0; s < KPL; s++) {
-                part_d[off + s * 64 + lane] = S.s[s].d;
-                part_i[off + s * 64 + lane] = S.s[s].i;
+                store_wt(&part_d[off + s * 64 + lane], S.s[s].d);
+                store_wt(&part_i[off + s * 64 + lane], S.s[s].i);
+            }
+            if (lane < kHeads) {
+                store_wt(&head_d[kHeads * blockIdx.x + lane], S.s[0].d);
+                store_wt(&head_i[kHeads * blockIdx.x + lane], S.s[0].i);
             }
         }
-        return;
+    } else {
+        // many exact ties around the bound: sort all kept survivors in LDS (uniform branch)
+        int m2 = 1;
+        while (m2 < (int)fc) m2 <<= 1;
+        for (int t = threadIdx.x + fc; t < m2; t += kBlock) { cd[t] = kSentinelD; ci[t] = kSentinelI; }
+        __syncthreads();
+        block_sort_lds(cd, ci, m2);
+        for (int t = threadIdx.x; t < N; t += kBlock) {
+            store_wt(&part_d[off + t], t < (int)fc ? cd[t] : kSentinelD);
+            store_wt(&part_i[off + t], t < (int)fc ? ci[t] : kSentinelI);
+            if (t < kHeads) {
+                store_wt(&head_d[kHeads * blockIdx.x + t], cd[t]);  // fc > 64*KPL2 >= kHeads
+                store_wt(&head_i[kHeads * blockIdx.x + t], ci[t]);
+            }
+        }
     }
-    // many exact ties around the bound: sort all kept survivors in LDS (uniform branch)
-    int m2 = 1;
-    while (m2 < (int)fc) m2 <<= 1;
-    for (int t = threadIdx.x + fc; t < m2; t += kBlock) { cd[t] = kSentinelD; ci[t] = kSentinelI; }
+    if (out.ticket == nullptr) return;
+
+    // ---- fused final selection (cdna_hip_programming.md §6 Guideline 16, counter form): the
+    // block list (and any spill) was stored sc1; every storing wave drains, the block meets,
+    // one lane takes a ticket; the last arriver acquires once and merges all block lists.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    block_sort_lds(cd, ci, m2);
-    for (int t = threadIdx.x; t < N; t += kBlock) {
-        part_d[off + t] = t < (int)fc ? cd[t] : kSentinelD;
-        part_i[off + t] = t < (int)fc ? ci[t] : kSentinelI;
-    }
-}
-
-// ---------------------------------------------------------------- final selection --------
-// One workgroup of 16 waves.  (1) every wave sorts 64 list heads in registers and the 16
-// sorted runs are merged by a 4-level tree through LDS: T = k-th smallest head, an upper
-// bound of the global k-th key (the k smallest heads are k real entries).  (2) every entry
-// <= T is gathered (lists are ascending: a scan stops at the first entry above T; typically
-// ~k entries in all).  (3) one wave sorts them in registers and writes the top k.
-constexpr int kFinalThreads = 1024;
-constexpr int kFinalWaves = kFinalThreads / kWave;
-constexpr int kFinalCap = 4096;
-
-template <int KPL>
-__global__ __launch_bounds__(kFinalThreads) void knn_final(const unsigned long long* __restrict__ part_d,
-                                                           const unsigned* __restrict__ part_i,
-                                                           unsigned nlists, unsigned list_len, unsigned k,
-                                                           double* __restrict__ out_d, unsigned* __restrict__ out_i,
-                                                           unsigned* __restrict__ out_count,
-                                                           const unsigned long long* __restrict__ spill_d,
-                                                           const unsigned* __restrict__ spill_i,
-                                                           unsigned* __restrict__ spill_cnt) {
-    constexpr int N = 64 * KPL;
-    constexpr int KPL2 = 2 * KPL;
-    __shared__ unsigned long long xd[kFinalWaves / 2 * N];
-    __shared__ unsigned xi[kFinalWaves / 2 * N];
-    __shared__ unsigned long long bd[kFinalCap];
-    __shared__ unsigned bi[kFinalCap];
-    __shared__ unsigned cnt;
-    __shared__ unsigned long long Td;
-    __shared__ unsigned Ti;
-    const int lane = lane_id();
-    const int wid = threadIdx.x / kWave;
-
-    // (1) T = k-th smallest head.  Thread t owns list t (t < 1024) and loads its first two
-    // entries once; lists beyond 1024 (never produced by knn_scan) are reloaded below.
     if (threadIdx.x == 0) {
-        cnt = 0;
-        Td = kSentinelD;
-        Ti = kSentinelI;
-    }
-    const unsigned own = threadIdx.x;
-    KE e0 = ksentinel(), e1 = ksentinel();
-    if (own < nlists) {
-        const size_t off = (size_t)own * list_len;
-        e0.d = part_d[off];
-        e0.i = part_i[off];
-        if (list_len > 1) {
-            e1.d = part_d[off + 1];
-            e1.i = part_i[off + 1];
-        }
-    }
-    if (nlists >= k) {
-        WList<KPL> L;
-#pragma unroll
-        for (int s = 0; s < KPL; s++) L.s[s] = ksentinel();
-        wave_merge_batch<KPL>(L, wave_sort64(e0));
-        for (unsigned g = (unsigned)wid * 64 + kFinalThreads; g < nlists; g += kFinalThreads) {
-            KE h = ksentinel();
-            const unsigned p = g + lane;
-            if (p < nlists) {
-                h.d = part_d[(size_t)p * list_len];
-                h.i = part_i[(size_t)p * list_len];
-            }
-            wave_merge_batch<KPL>(L, wave_sort64(h));
-        }
-        for (int step = 1; step < kFinalWaves; step <<= 1) {
-            __syncthreads();
-            if ((wid & (2 * step - 1)) == step) {  // sender
-                const int slot = wid >> 1;
-#pragma unroll
-                for (int s = 0; s < KPL; s++) {
-                    xd[slot * N + s * 64 + lane] = L.s[s].d;
-                    xi[slot * N + s * 64 + lane] = L.s[s].i;
-                }
-            }
-            __syncthreads();
-            if ((wid & (2 * step - 1)) == 0) {  // receiver of wid + step
-                const int slot = (wid + step) >> 1;
-                WList<KPL> B;
-#pragma unroll
-                for (int s = 0; s < KPL; s++) {
-                    B.s[s].d = xd[slot * N + s * 64 + lane];
-                    B.s[s].i = xi[slot * N + s * 64 + lane];
-                }
-                wave_merge_lists<KPL>(L, B);
-            }
-        }
-        if (wid == 0) {
-            KE t = wave_list_get<KPL>(L, (int)k - 1);
-            if (lane == 0) {
-                Td = t.d;
-                Ti = t.i;
-            }
-        }
+        const unsigned t = __hip_atomic_fetch_add(((gu32*)(out.ticket)), 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        kb.final_cnt = t == gridDim.x - 1 ? 1u : 0u;
     }
     __syncthreads();
-    const unsigned long long T_d = Td;
-    const unsigned T_i = Ti;
-    // (2) gather every real entry <= T (lists ascending: stop at the first entry above T)
-    auto take = [&](const KE& e) -> bool {
-        if (e.d == kSentinelD || lds_kless(T_d, T_i, e.d, e.i)) return false;
-        const unsigned pos = atomicAdd(&cnt, 1u);
-        if (pos < (unsigned)kFinalCap) { bd[pos] = e.d; bi[pos] = e.i; }
-        return true;
-    };
-    if (own < nlists && take(e0) && list_len > 1 && take(e1)) {
-        const size_t off = (size_t)own * list_len;
-        for (unsigned j = 2; j < list_len; j++) {
-            KE e;
-            e.d = part_d[off + j];
-            e.i = part_i[off + j];
-            if (!take(e)) break;
-        }
-    }
-    for (unsigned p = threadIdx.x + kFinalThreads; p < nlists; p += blockDim.x) {
-        const size_t off = (size_t)p * list_len;
-        for (unsigned j = 0; j < list_len; j++) {
-            KE e;
-            e.d = part_d[off + j];
-            e.i = part_i[off + j];
-            if (!take(e)) break;
-        }
-    }
-    // survivors a scan block could not keep in LDS (unsorted, usually none)
-    unsigned spill_snapshot = 0;
-    if (spill_cnt) {
-        const unsigned ns = *spill_cnt;
-        spill_snapshot = ns;
-        for (unsigned t = threadIdx.x; t < ns; t += blockDim.x) {
-            KE e;
-            e.d = spill_d[t];
-            e.i = spill_i[t];
-            take(e);
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) *spill_cnt = 0;  // ready for the next window on this stream
+    if (kb.final_cnt == 0) return;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    const unsigned total = cnt;
-    const unsigned outn = total < k ? total : k;
-    if (total <= (unsigned)(64 * KPL2)) {
-        // (3) one wave: register bitonic sort of <= 128*KPL entries
-        if (wid == 0) {
-            WList<KPL2> S;
-#pragma unroll
-            for (int s = 0; s < KPL2; s++) {
-                const unsigned e = (unsigned)(s * 64 + lane);
-                S.s[s] = ksentinel();
-                if (e < total) { S.s[s].d = bd[e]; S.s[s].i = bi[e]; }
-            }
-            wave_sort_list<KPL2>(S);
-#pragma unroll
-            for (int s = 0; s < KPL2; s++) {
-                const unsigned e = (unsigned)(s * 64 + lane);
-                if (e < k) {
-                    out_d[e] = __longlong_as_double((long long)(e < outn ? S.s[s].d : kSentinelD));
-                    out_i[e] = e < outn ? S.s[s].i : kSentinelI;
-                }
-            }
-            if (lane == 0) *out_count = outn;
-        }
-        return;
-    }
-    if (total <= (unsigned)kFinalCap) {
-        int m = 1;
-        while (m < (int)total) m <<= 1;
-        for (int t = threadIdx.x + total; t < m; t += blockDim.x) { bd[t] = kSentinelD; bi[t] = kSentinelI; }
-        __syncthreads();
-        block_sort_lds(bd, bi, m);
-        for (unsigned t = threadIdx.x; t < k; t += blockDim.x) {
-            out_d[t] = __longlong_as_double((long long)(t < outn ? bd[t] : kSentinelD));
-            out_i[t] = t < outn ? bi[t] : kSentinelI;
-        }
-        if (threadIdx.x == 0) *out_count = outn;
-        return;
-    }
-    // pathological (massive exact ties): k rounds of "smallest key above the previous one"
-    const size_t spill_total = spill_cnt ? spill_snapshot : 0;
-    unsigned long long prev_d = 0;
-    unsigned prev_i = 0;
-    bool have_prev = false;
-    unsigned got = 0;
-    for (unsigned r = 0; r < k; r++) {
-        unsigned long long best_d = kSentinelD;
-        unsigned best_i = kSentinelI;
-        const size_t nl = (size_t)nlists * list_len;
-        for (size_t t = threadIdx.x; t < nl + spill_total; t += blockDim.x) {
-            const unsigned long long ed = t < nl ? part_d[t] : spill_d[t - nl];
-            const unsigned ei = t < nl ? part_i[t] : spill_i[t - nl];
-            if (ed == kSentinelD) continue;
-            if (have_prev && !lds_kless(prev_d, prev_i, ed, ei)) continue;
-            if (lds_kless(ed, ei, best_d, best_i)) { best_d = ed; best_i = ei; }
-        }
-        bd[threadIdx.x] = best_d;
-        bi[threadIdx.x] = best_i;
-        __syncthreads();
-        for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-            if ((int)threadIdx.x < s && lds_kless(bd[threadIdx.x + s], bi[threadIdx.x + s], bd[threadIdx.x], bi[threadIdx.x])) {
-                bd[threadIdx.x] = bd[threadIdx.x + s];
-                bi[threadIdx.x] = bi[threadIdx.x + s];
-            }
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) { Td = bd[0]; Ti = bi[0]; }
-        __syncthreads();
-        const unsigned long long vd = Td;
-        const unsigned vi = Ti;
-        __syncthreads();
-        if (vd == kSentinelD) break;
-        if (threadIdx.x == 0) {
-            out_d[r] = __longlong_as_double((long long)vd);
-            out_i[r] = vi;
-        }
-        prev_d = vd;
-        prev_i = vi;
-        have_prev = true;
-        got = r + 1;
-    }
-    for (unsigned t = got + threadIdx.x; t < k; t += blockDim.x) {
-        out_d[t] = __longlong_as_double((long long)kSentinelD);
-        out_i[t] = kSentinelI;
-    }
-    if (threadIdx.x == 0) *out_count = got;
+    // LDS: gathered entries in the (idle) wave stages, tree exchange in kb.bd/kb.bi
+    static_assert(sizeof(stage) >= 2048 * 12, "fused final: gather buffer");
+    static_assert(sizeof(kb.bd) >= 2 * N * 8 && sizeof(kb.bi) >= 2 * N * 4, "fused final: tree exchange");
+    char* sb = reinterpret_cast<char*>(&stage[0]);
+    const FinalLds fl{kb.bd, kb.bi, reinterpret_cast<unsigned long long*>(sb), reinterpret_cast<unsigned*>(sb + 2048 * 8),
+                      2048u, &kb.cnt, &kb.bound, &kb.final_cnt, kb.hist};
+    const FinalIo io{part_d, part_i, gridDim.x, (unsigned)N, k, out.out_d, out.out_i, out.out_count,
+                     spill_d, spill_i, spill_cnt, head_d, head_i, args.hist_base};
+    final_select<KPL, kBlock, 1024 / kBlock>(io, fl);
+    if (threadIdx.x == 0) __hip_atomic_store(((gu32*)(out.ticket)), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ============================================================================ range =======
@@ -803,40 +967,72 @@ __global__ void selftest_fp64(const double* __restrict__ a, const double* __rest
 }
 
 // ============================================================================ launchers ===
+static int g_knn_fused = 1;
+void set_knn_fused(int fused) { g_knn_fused = fused; }
+
+template <int KPL>
+static void launch_knn_final_heads(unsigned long long* part_d, unsigned* part_i, unsigned nblocks, unsigned k,
+                                   double* out_d, unsigned* out_i, unsigned* out_count,
+                                   unsigned long long* spill_d, unsigned* spill_i, unsigned* spill_cnt, int hist_base,
+                                   hipStream_t st) {
+    const unsigned L = 64u * KPL;
+    const FinalIo io{part_d, part_i, nblocks, L, k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt,
+                     part_d + (size_t)nblocks * L, part_i + (size_t)nblocks * L, hist_base};
+    knn_final<KPL><<<1, kFinalThreads, 0, st>>>(io);
+}
+
 hipError_t launch_knn(const double* x, const double* y, uint64_t n, const KnnArgs& args, int kpl,
                       unsigned long long* part_d, unsigned* part_i, unsigned nblocks, uint64_t chunk, double* out_d,
                       unsigned* out_i, unsigned* out_count, unsigned long long* spill_d, unsigned* spill_i,
                       unsigned* spill_cnt, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
-    if (ev0) hipEventRecord(ev0, st);
-    if (nblocks > 0) {
-        switch (kpl) {
-            case 1: knn_scan<1><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt); break;
-            case 2: knn_scan<2><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt); break;
-            case 4: knn_scan<4><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt); break;
-            default: return hipErrorInvalidValue;
-        }
-    }
-    if (ev1) hipEventRecord(ev1, st);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
     const unsigned k = args.k;
     const unsigned L = 64u * (unsigned)kpl;
-    if (k <= 64) knn_final<1><<<1, kFinalThreads, 0, st>>>(part_d, part_i, nblocks, L, k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt);
-    else if (k <= 128) knn_final<2><<<1, kFinalThreads, 0, st>>>(part_d, part_i, nblocks, L, k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt);
-    else knn_final<4><<<1, kFinalThreads, 0, st>>>(part_d, part_i, nblocks, L, k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt);
+    if (nblocks == 0) {  // empty window: the final selection alone writes the empty result
+        const FinalIo io{part_d, part_i, 0u, L, k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt, nullptr, nullptr, 0};
+        if (k <= 64) knn_final<1><<<1, kFinalThreads, 0, st>>>(io);
+        else if (k <= 128) knn_final<2><<<1, kFinalThreads, 0, st>>>(io);
+        else knn_final<4><<<1, kFinalThreads, 0, st>>>(io);
+        return hipGetLastError();
+    }
+    // fused: spill_cnt[1] is the arrival ticket of the in-kernel final selection
+    const KnnOut out = g_knn_fused ? KnnOut{out_d, out_i, out_count, spill_cnt + 1} : KnnOut{nullptr, nullptr, nullptr, nullptr};
+    if (ev0) (void)hipEventRecord(ev0, st);
+    switch (kpl) {
+        case 1: knn_scan<1><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, out); break;
+        case 2: knn_scan<2><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, out); break;
+        case 4: knn_scan<4><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, out); break;
+        default: return hipErrorInvalidValue;
+    }
+    if (ev1) (void)hipEventRecord(ev1, st);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || g_knn_fused) return e;
+    switch (kpl) {
+        case 1: launch_knn_final_heads<1>(part_d, part_i, nblocks, k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt, args.hist_base, st); break;
+        case 2: launch_knn_final_heads<2>(part_d, part_i, nblocks, k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt, args.hist_base, st); break;
+        default: launch_knn_final_heads<4>(part_d, part_i, nblocks, k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt, args.hist_base, st); break;
+    }
     return hipGetLastError();
 }
 
 hipError_t launch_knn_scan_variant(int mode, const double* x, const double* y, uint64_t n, const KnnArgs& args,
                                    unsigned long long* part_d, unsigned* part_i, unsigned nblocks, uint64_t chunk,
-                                   unsigned long long* spill_d, unsigned* spill_i, unsigned* spill_cnt, hipStream_t st) {
+                                   unsigned long long* spill_d, unsigned* spill_i, unsigned* spill_cnt, double* out_d,
+                                   unsigned* out_i, unsigned* out_count, hipStream_t st) {
+    const KnnOut fused{out_d, out_i, out_count, spill_cnt + 1};
+    const KnnOut lists{nullptr, nullptr, nullptr, nullptr};
     switch (mode) {
-        case 0: knn_scan<1, 0><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt); break;
-        case 1: knn_scan<1, 1><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt); break;
-        case 2: knn_scan<1, 2><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt); break;
-        case 3: knn_scan<1, 3><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt); break;
-        case 5: knn_scan<1, 5><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt); break;
-        case 7: knn_scan<1, 7><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt); break;
+        case 0: knn_scan<1, 0><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, fused); break;
+        case 1: knn_scan<1, 1><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, lists); break;
+        case 2: knn_scan<1, 2><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, lists); break;
+        case 3: knn_scan<1, 3><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, lists); break;
+        case 5: knn_scan<1, 5><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, lists); break;
+        case 7: knn_scan<1, 7><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, lists); break;
+        case 8: knn_scan<1, 0><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, lists); break;
+        case 9:
+            knn_scan<1, 0><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, lists);
+            launch_knn_final_heads<1>(part_d, part_i, nblocks, args.k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt,
+                                      args.hist_base, st);
+            break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -844,9 +1040,10 @@ hipError_t launch_knn_scan_variant(int mode, const double* x, const double* y, u
 
 hipError_t launch_knn_merge(const unsigned long long* d, const unsigned* i, unsigned nlists, unsigned list_len,
                             unsigned k, double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st) {
-    if (k <= 64) knn_final<1><<<1, kFinalThreads, 0, st>>>(d, i, nlists, list_len, k, out_d, out_i, out_count, nullptr, nullptr, nullptr);
-    else if (k <= 128) knn_final<2><<<1, kFinalThreads, 0, st>>>(d, i, nlists, list_len, k, out_d, out_i, out_count, nullptr, nullptr, nullptr);
-    else knn_final<4><<<1, kFinalThreads, 0, st>>>(d, i, nlists, list_len, k, out_d, out_i, out_count, nullptr, nullptr, nullptr);
+    const FinalIo io{d, i, nlists, list_len, k, out_d, out_i, out_count, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
+    if (k <= 64) knn_final<1><<<1, kFinalThreads, 0, st>>>(io);
+    else if (k <= 128) knn_final<2><<<1, kFinalThreads, 0, st>>>(io);
+    else knn_final<4><<<1, kFinalThreads, 0, st>>>(io);
     return hipGetLastError();
 }
 
@@ -856,10 +1053,10 @@ hipError_t launch_range(const double* x, const double* y, uint64_t n, const Rang
     const uint64_t units = (n + kUnitPts - 1) / kUnitPts;
     const uint64_t blocks = (units + 3) / 4;
     if (units == 0) return hipMemsetAsync(total, 0, sizeof(uint64_t), st);
-    if (ev0) hipEventRecord(ev0, st);
+    if (ev0) (void)hipEventRecord(ev0, st);
     if (approximate) range_scan<true><<<(unsigned)blocks, kBlock, 0, st>>>(x, y, n, a, bitmask, unit_count);
     else range_scan<false><<<(unsigned)blocks, kBlock, 0, st>>>(x, y, n, a, bitmask, unit_count);
-    if (ev1) hipEventRecord(ev1, st);
+    if (ev1) (void)hipEventRecord(ev1, st);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     scan_units<<<1, 1024, 0, st>>>(unit_count, units, offs, total);

@@ -376,3 +376,48 @@ def test_knn_equal_distance_shell(ctx):
         oi, od = ctx.knn_pp(ag, x, y, Q[0], Q[1], 0.5, k)
         wi, wd = cref.knn_pp(cg, x, y, Q[0], Q[1], 0.5, k)
         assert oi.tolist() == wi.tolist() and np.array_equal(od.view(np.uint64), wd.view(np.uint64))
+
+
+def test_knn_query_duplicates_spill_and_repeat(ctx):
+    """Thousands of exact copies of the query point in consecutive window slots: one scan
+    block keeps far more than its LDS survivor buffer (spill path), the head histogram's k-th
+    bin is the lowest (exact-T fallback) or the gather overflows (k-round fallback).  Every
+    call is repeated on the same context: the fused final's arrival ticket and the spill
+    count must be back at zero after each launch."""
+    ag, cg = agrid(100)
+    rng = np.random.default_rng(17)
+    x, y = _window(rng, 2_000_000)
+    x[700000:705000] = Q[0]
+    y[700000:705000] = Q[1]
+    sc = rng.integers(0, 2_000_000, 300)
+    x[sc] = Q[0]
+    y[sc] = Q[1]
+    for k in (1, 50, 256):
+        wi, wd = cref.knn_pp(cg, x, y, Q[0], Q[1], 0.5, k)
+        for _ in range(2):
+            oi, od = ctx.knn_pp(ag, x, y, Q[0], Q[1], 0.5, k)
+            assert oi.tolist() == wi.tolist() and np.array_equal(od.view(np.uint64), wd.view(np.uint64))
+    # then a plain window again: no state left behind by the spill
+    x2, y2 = _window(rng, 1_000_000)
+    wi, wd = cref.knn_pp(cg, x2, y2, Q[0], Q[1], 0.5, 50)
+    oi, od = ctx.knn_pp(ag, x2, y2, Q[0], Q[1], 0.5, 50)
+    assert oi.tolist() == wi.tolist() and np.array_equal(od.view(np.uint64), wd.view(np.uint64))
+
+
+def test_knn_separate_final_launch(ctx):
+    """The same results with the final selection as a separate knn_final launch (packed heads,
+    head histogram) instead of the scan's last-arriving block."""
+    ag, cg = agrid(100)
+    rng = np.random.default_rng(23)
+    x, y = _window(rng, 1_500_000, nan_every=1009)
+    x[400000:403000] = Q[0]
+    y[400000:403000] = Q[1]
+    _abi.debug_set_knn_fused(False)
+    try:
+        for (xx, yy) in ((x, y), (x[3000:], y[3000:]), (x[403000:], y[403000:])):
+            for k in (1, 50, 129, 256):
+                wi, wd = cref.knn_pp(cg, xx, yy, Q[0], Q[1], 0.5, k)
+                oi, od = ctx.knn_pp(ag, xx, yy, Q[0], Q[1], 0.5, k)
+                assert oi.tolist() == wi.tolist() and np.array_equal(od.view(np.uint64), wd.view(np.uint64))
+    finally:
+        _abi.debug_set_knn_fused(True)
