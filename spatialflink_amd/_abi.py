@@ -108,6 +108,8 @@ _SIGS = {
     "geohip_debug_selftest_fp64": (c_int, [_P, _P, _P, c_uint64, _P, _P, _P, _P]),
     "geohip_debug_classify": (c_int, [POINTER(Grid), c_double, c_double, c_double, _P, _P, c_uint64, _P]),
     "geohip_debug_set_knn_fused": (None, [c_int]),
+    "geohip_debug_set_knn_config": (c_int, [c_int, c_int, c_int, c_int]),
+    "geohip_debug_knn_trace": (c_int, [_P, _P, c_uint64, POINTER(c_uint32)]),
     "geohip_debug_knn_scan_variant": (c_int, [_P, c_int, POINTER(Grid), _P, _P, c_uint64, c_int, c_double,
                                               c_double, c_double, c_uint32, c_int, _P]),
 }
@@ -165,6 +167,14 @@ def debug_set_knn_fused(fused: bool) -> None:
     """Test/measurement hook: kNN final selection inside the scan's last block (default) or
     as a separate knn_final launch."""
     lib.geohip_debug_set_knn_fused(1 if fused else 0)
+
+
+def debug_set_knn_config(waves_per_block: int = 16, prefetch: int = 1, ticket_groups: int = 16,
+                         epi_sort: int = 0) -> None:
+    """Measurement hook: kNN scan launch shape (waves per block 4/8/16, load pipeline depth
+    1/2, arrival-ticket groups 1..64, block list by register sort (1) or rank placement (0))."""
+    if lib.geohip_debug_set_knn_config(waves_per_block, prefetch, ticket_groups, epi_sort):
+        raise GeohipArgumentError(f"unsupported kNN shape {waves_per_block}/{prefetch}/{ticket_groups}/{epi_sort}")
 
 
 def plan_cell(grid: Grid, x: float, y: float):
@@ -367,6 +377,14 @@ class Context:
                                                r, k, reps, ms)
         self._check(rc, "debug_knn_scan_variant")
         return ms[0] if mode != 5 else (ms[0], ms[1], ms[2])
+
+    def debug_knn_trace(self, cap_blocks=4096):
+        """Phase timestamps (100 MHz) of the last MODE 6 scan: array [nblocks + 1, 8]."""
+        buf = np.zeros(8 * (cap_blocks + 1), dtype=np.uint64)
+        nb = c_uint32(0)
+        rc = lib.geohip_debug_knn_trace(self.h, buf.ctypes.data_as(c_void_p), len(buf), ctypes.byref(nb))
+        self._check(rc, "debug_knn_trace")
+        return buf[:8 * (nb.value + 1)].reshape(nb.value + 1, 8)
 
     def selftest_fp64(self, a, b):
         """Device fp64 primitive bits (test hook): returns (sqrt|a|, a/b, hypot(a,b), a*b-b*b)."""

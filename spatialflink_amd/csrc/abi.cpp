@@ -200,19 +200,16 @@ int knn_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const
     rc = stage_xy(ctx, x, y, n, S_X, S_Y, &dx, &dy);
     if (rc) return rc;
     const int kpl = kpl_for(k);
-    // exactly 4 blocks per CU (256 CUs) when n is large: equal work per CU; an even chunk keeps
-    // the 16-byte double2 loads aligned
-    const uint64_t target_blocks = 1024;
-    uint64_t chunk = (n + target_blocks - 1) / target_blocks;
-    chunk = (chunk + 1) & ~1ull;
-    if (chunk < 1024) chunk = 1024;
-    uint64_t nblocks = a.nu > 0 ? (n + chunk - 1) / chunk : 0;  // empty G u C: no candidates
+    unsigned geo_blocks = 0;
+    uint64_t chunk = 0;
+    knn_geometry(n, &geo_blocks, &chunk);
+    const uint64_t nblocks = a.nu > 0 ? geo_blocks : 0;  // empty G u C: no candidates
     const uint64_t N = 64ull * kpl;
     rc = ensure(ctx, S_PART_D, nblocks * (N + 4) * 8);  // block lists, then the packed heads (kHeads = 4)
     if (!rc) rc = ensure(ctx, S_PART_I, nblocks * (N + 4) * 4);
     if (!rc) rc = ensure(ctx, S_SPILL_D, n * 8);  // worst case: every point survives
     if (!rc) rc = ensure(ctx, S_SPILL_I, n * 4);
-    if (!rc) rc = ensure_zeroed(ctx, S_SPILL_CNT, 16);
+    if (!rc) rc = ensure_zeroed(ctx, S_SPILL_CNT, kKnnCounterBytes);
     if (rc) return rc;
     hipEvent_t e0, e1;
     timing_events(ctx, &e0, &e1);
@@ -519,6 +516,24 @@ int geohip_synth_uniform_async(geohip_ctx* ctx, double* x, double* y, uint64_t n
     return GEOHIP_OK;
 }
 
+static unsigned long long* g_trace_dev = nullptr;  // MODE 6 phase timestamps (debug only)
+static size_t g_trace_words = 0;
+static unsigned g_trace_blocks = 0;
+
+// Measurement hook: the phase timestamps of the last MODE 6 launch (8 u64 per block, then the
+// final selection's 8), 100 MHz clock; *nblocks = blocks of that launch.
+int geohip_debug_knn_trace(geohip_ctx* ctx, uint64_t* host, uint64_t cap_words, unsigned* nblocks) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    if (!g_trace_dev) return fail(ctx, GEOHIP_ERR_ARG, "no traced launch");
+    const size_t words = 8 * ((size_t)g_trace_blocks + 1);
+    if (cap_words < words) return fail(ctx, GEOHIP_ERR_CAPACITY, "trace buffer too small");
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipMemcpy(host, g_trace_dev, words * 8, hipMemcpyDeviceToHost));
+    *nblocks = g_trace_blocks;
+    return GEOHIP_OK;
+}
+
 // Measurement hook (not part of the operator surface): time `reps` launches of a kNN scan
 // ablation variant (0 full .. 3, see knn_scan) with events on the ctx stream; device memory.
 int geohip_debug_knn_scan_variant(geohip_ctx* ctx, int mode, const geohip_grid* grid, const double* x,
@@ -530,19 +545,31 @@ int geohip_debug_knn_scan_variant(geohip_ctx* ctx, int mode, const geohip_grid* 
     rc = plan_or_fail(ctx, grid, qx, qy, r, &plan);
     if (rc) return rc;
     KnnArgs a = make_knn_args(plan, k, qx, qy);
-    uint64_t chunk = (n + 1023) / 1024;
-    chunk = (chunk + 1) & ~1ull;
-    if (chunk < 1024) chunk = 1024;
-    const uint64_t nblocks = (n + chunk - 1) / chunk;
+    unsigned nblocks = 0;
+    uint64_t chunk = 0;
+    knn_geometry(n, &nblocks, &chunk);
     rc = ensure(ctx, S_PART_D, nblocks * (64 + 4) * 8);
     if (!rc) rc = ensure(ctx, S_PART_I, nblocks * (64 + 4) * 4);
     if (!rc) rc = ensure(ctx, S_SPILL_D, n * 8);
     if (!rc) rc = ensure(ctx, S_SPILL_I, n * 4);
-    if (!rc) rc = ensure_zeroed(ctx, S_SPILL_CNT, 16);
+    if (!rc) rc = ensure_zeroed(ctx, S_SPILL_CNT, kKnnCounterBytes);
     if (!rc) rc = ensure(ctx, S_OUT_D, (size_t)(k ? k : 1) * 8);
     if (!rc) rc = ensure(ctx, S_OUT_I, (size_t)(k ? k : 1) * 4);
     if (!rc) rc = ensure(ctx, S_OUT_CNT, 8);
     if (rc) return rc;
+    if (mode == 6) {  // phase timestamps: trace buffer for this launch shape
+        const size_t words = 8 * ((size_t)nblocks + 1);
+        if (words > g_trace_words) {
+            if (g_trace_dev) (void)hipFree(g_trace_dev);
+            g_trace_dev = nullptr;
+            g_trace_words = 0;
+            HIPCHK(hipMalloc(&g_trace_dev, words * 8));
+            g_trace_words = words;
+        }
+        HIPCHK(hipMemsetAsync(g_trace_dev, 0, words * 8, ctx->stream));
+        HIPCHK(set_knn_trace(g_trace_dev));
+        g_trace_blocks = nblocks;
+    }
     unsigned long long* sd = B<unsigned long long>(ctx, S_SPILL_D);
     unsigned* si = B<unsigned>(ctx, S_SPILL_I);
     unsigned* sc = B<unsigned>(ctx, S_SPILL_CNT);
@@ -567,7 +594,7 @@ int geohip_debug_knn_scan_variant(geohip_ctx* ctx, int mode, const geohip_grid* 
     hipEventDestroy(e0);
     hipEventDestroy(e1);
     *ms_per_launch = ms / (reps > 0 ? reps : 1);
-    HIPCHK(hipMemsetAsync(sc, 0, 16, ctx->stream));  // list-only modes leave spill counts behind
+    HIPCHK(hipMemsetAsync(sc, 0, kKnnCounterBytes, ctx->stream));  // list-only modes leave spill counts behind
     if (mode == 5) {  // counters of one extra launch: sorts and passing candidates, summed
         HIPCHK(hipMemsetAsync(ctx->buf[S_PART_I], 0, 8, ctx->stream));
         HIPCHK(launch_knn_scan_variant(mode, x, y, n, a, B<unsigned long long>(ctx, S_PART_D),
@@ -621,6 +648,9 @@ int geohip_debug_selftest_fp64(geohip_ctx* ctx, const double* a, const double* b
 
 // Debug hook: 1 = final selection fused into the scan (default), 0 = separate knn_final launch.
 void geohip_debug_set_knn_fused(int fused) { set_knn_fused(fused); }
+int geohip_debug_set_knn_config(int waves_per_block, int prefetch, int ticket_groups, int epi_sort) {
+    return set_knn_config(waves_per_block, prefetch, ticket_groups, epi_sort) ? GEOHIP_ERR_ARG : GEOHIP_OK;
+}
 
 }  // extern "C"
 

@@ -155,6 +155,18 @@ __device__ __forceinline__ unsigned long long rev_lane64(unsigned long long v) {
     return ((unsigned long long)rev_lane((unsigned)(v >> 32)) << 32) | rev_lane((unsigned)v);
 }
 
+// Inclusive prefix sum over the 64 lanes by DPP (row_shr 1/2/4/8 inside each 16-lane row with
+// bound_ctrl zero fill, then row_bcast:15 / row_bcast:31 across rows): no LDS round trips.
+__device__ __forceinline__ unsigned wave_incl_scan(unsigned x) {
+    x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);
+    x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);
+    x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);
+    x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);
+    x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+    x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+    return x;
+}
+
 __device__ __forceinline__ KE kxor(const KE& v, int m) {
     KE r;
     r.d = xor_lane64(v.d, m);

@@ -37,6 +37,25 @@ hipError_t launch_knn_scan_variant(int mode, const double* x, const double* y, u
                                    unsigned* out_i, unsigned* out_count, hipStream_t st);
 // 1: final selection in the scan's last-arriving block (default); 0: separate knn_final launch
 void set_knn_fused(int fused);
+// kNN scan launch shape: waves per block (4, 8, 16), load pipeline depth (1, 2), arrival
+// ticket groups (1 .. 64).  Returns -1 for an unsupported shape.
+struct KnnConfig {
+    int nw, pf, groups, epi_sort;
+};
+int set_knn_config(int nw, int pf, int groups, int epi_sort);
+KnnConfig knn_config();
+// trace buffer of knn_scan MODE 6 (8 * (nblocks + 1) u64, device)
+hipError_t set_knn_trace(unsigned long long* buf);
+// blocks and chunk (points per block) of a kNN scan over n points under the current shape
+void knn_geometry(uint64_t n, unsigned* nblocks, uint64_t* chunk);
+// spill_cnt scratch (zeroed once; every user re-zeroes what it used): word 0 = spill count,
+// arrival tickets from word kTicketStride (128 B apart), the final selection's head
+// histogram (512 words) from word kGhistWord
+constexpr unsigned kTicketStride = 32;  // words between counters
+constexpr unsigned kMaxTicketGroups = 64;
+constexpr unsigned kGhistWord = kTicketStride * (kMaxTicketGroups + 2);
+constexpr int kGhistCopies = 8;
+constexpr size_t kKnnCounterBytes = 32768;
 hipError_t launch_knn_merge(const unsigned long long* d, const unsigned* i, unsigned nlists, unsigned list_len,
                             unsigned k, double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st);
 // range: bitmask (16 words / 1024 pts), unit_count (units), offs (units) scratch.

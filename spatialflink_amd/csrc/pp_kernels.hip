@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "device_common.h"
 #include "pp_kernels.h"
 
@@ -111,14 +113,16 @@ __device__ __forceinline__ void store_wt(unsigned* p, unsigned v) {
 }
 
 constexpr int kHistBins = 512;
-constexpr int kBlkCap = 768;  // 4 blocks/CU: stages 25.6 KB + this ~11.3 KB <= 40 KB
 
+// survivor buffer: 192 entries per wave (4 waves: stages 25.6 KB + this ~11.3 KB, 4 blocks/CU)
+template <int NW>
 struct KnnBlock {
+    static constexpr int kCap = 192 * NW;
     unsigned hist[kHistBins];
-    unsigned long long bd[kBlkCap];
-    unsigned bi[kBlkCap];
+    unsigned long long bd[kCap];
+    unsigned bi[kCap];
     unsigned long long bound;  // distance bits; kSentinelD = none yet
-    unsigned cnt;              // survivors appended (may exceed kBlkCap: the rest spilled)
+    unsigned cnt;              // survivors appended (may exceed kCap: the rest spilled)
     unsigned final_cnt;
 };
 
@@ -137,25 +141,20 @@ __device__ __forceinline__ int hist_kth_bin(const unsigned* hist, unsigned k) {
         c[j] = hist[lane * 8 + j];
         tot += c[j];
     }
-    unsigned incl = tot;  // inclusive prefix over lanes
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const unsigned v = __shfl_up(incl, o);
-        if (lane >= o) incl += v;
-    }
+    const unsigned incl = wave_incl_scan(tot);  // inclusive prefix over lanes
     const unsigned long long m = __ballot(incl >= k);
     if (m == 0) return -1;
     const int first = __builtin_ctzll(m);
+    // every lane finds its own crossing bin; the first crossing lane's is the answer
     int bin = kHistBins - 1;
-    if (lane == first) {
-        unsigned run = incl - tot;
+    unsigned run = incl - tot;
+    bool found = false;
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            run += c[j];
-            if (run >= k) { bin = lane * 8 + j; break; }
-        }
+    for (int j = 0; j < 8; j++) {
+        run += c[j];
+        if (!found && run >= k) { bin = lane * 8 + j; found = true; }
     }
-    return __shfl(bin, first);
+    return __builtin_amdgcn_readlane(bin, first);
 }
 
 // upper edge (distance bits) of histogram bin `bin`
@@ -164,13 +163,15 @@ __device__ __forceinline__ unsigned long long hist_edge(int bin, int base) {
 }
 
 // One wave: the block bound from the survivor histogram (LDS atomic min).
-__device__ __forceinline__ void hist_bound(KnnBlock& kb, unsigned k, int base) {
+template <class KB>
+__device__ __forceinline__ void hist_bound(KB& kb, unsigned k, int base) {
     const int bin = hist_kth_bin(kb.hist, k);
     if (bin >= 0 && bin < kHistBins - 1 && lane_id() == 0) atomicMin(&kb.bound, hist_edge(bin, base));
 }
 
 // exact distances of up to 64 staged candidates, survivors appended to the block buffer
-__device__ __forceinline__ void knn_dist_batch(WaveStage& st, unsigned& ccnt, KnnBlock& kb, const KnnArgs& a,
+template <class KB>
+__device__ __forceinline__ void knn_dist_batch(WaveStage& st, unsigned& ccnt, KB& kb, const KnnArgs& a,
                                                unsigned long long* __restrict__ spill_d,
                                                unsigned* __restrict__ spill_i, unsigned* __restrict__ spill_cnt,
                                                unsigned& appended, bool partial) {
@@ -200,13 +201,13 @@ __device__ __forceinline__ void knn_dist_batch(WaveStage& st, unsigned& ccnt, Kn
             pos = __shfl(pos, 0);
             const unsigned slot = pos + lanes_below(m);
             unsigned gbase = 0;
-            if (pos + nm > (unsigned)kBlkCap) {  // spill the overflow to global memory (rare)
-                const unsigned first = pos > (unsigned)kBlkCap ? pos : (unsigned)kBlkCap;
+            if (pos + nm > (unsigned)KB::kCap) {  // spill the overflow to global memory (rare)
+                const unsigned first = pos > (unsigned)KB::kCap ? pos : (unsigned)KB::kCap;
                 if (lane == 0) gbase = atomicAdd(spill_cnt, pos + nm - first);
                 gbase = __shfl(gbase, 0) - (first - pos);
             }
             if (ok) {
-                if (slot < (unsigned)kBlkCap) {
+                if (slot < (unsigned)KB::kCap) {
                     kb.bd[slot] = db;
                     kb.bi[slot] = pi;
                 } else {
@@ -224,15 +225,20 @@ __device__ __forceinline__ void knn_dist_batch(WaveStage& st, unsigned& ccnt, Kn
 // ---------------------------------------------------------------- final selection --------
 // final_select<KPL, NT, OWN>: NT threads (NT/64 waves) reduce nlists ascending lists of
 // list_len entries (plus the unsorted spill buffer) to the k smallest keys.
-//  (1) every wave sorts its 64-head batches in registers and the wave runs are merged by a
-//      tree through LDS: T = k-th smallest head, an upper bound of the global k-th key (the k
-//      smallest heads are k real entries);
+//  (1) T = an upper bound of the global k-th key: the upper edge of the histogram bin where the
+//      cumulative count of list heads reaches k (>= k real entries lie at or below it).  The
+//      scan's blocks add their head to a global histogram as they finish (off the critical
+//      path), so here it is one load per bin; without it (rank merges) the heads are binned in
+//      LDS.  When that bin is the lowest or the top one, T is exact instead: the k-th smallest
+//      head (register sorts of 64-head batches, merged by a tree through LDS);
 //  (2) every entry <= T is gathered (lists ascending: a list scan stops at the first entry
-//      above T; ~k entries in all, nearly always within the two entries preloaded per list);
-//  (3) one wave sorts them in registers and writes the top k.
-// Every global load of (1)-(2) is issued up front (OWN lists of two entries per thread and the
-// spill count), so the selection pays one memory latency.  It runs as the knn_final kernel
-// (merges of rank results) and inside knn_scan's last-arriving block.
+//      above T; ~k entries in all, nearly always within the kHeads entries preloaded per list);
+//  (3) the gathered entries are placed by rank (each thread counts the smaller keys; keys are
+//      unique, ties broken by position) and the k smallest written in order.
+// Every global load of (1)-(2) is issued up front (the histogram, kHeads entries of OWN lists
+// per thread and the spill count), so the selection pays one memory latency.  It runs as the
+// knn_final kernel (separate launch, merges of rank results) and inside knn_scan's
+// last-arriving block.
 constexpr int kFinalThreads = 1024;
 constexpr int kFinalCap = 4096;
 constexpr int kHeads = 4;  // entries per list preloaded by the final selection (packed heads)
@@ -249,7 +255,8 @@ struct FinalIo {
     unsigned* spill_cnt;
     const unsigned long long* head_d;  // null, or the first kHeads entries of every list packed
     const unsigned* head_i;            // (head_d[kHeads l + j]): coalesced head loads
-    int hist_base;                     // histogram origin for the head-histogram T (head_d != null)
+    int hist_base;                     // histogram origin (head_d != null)
+    unsigned* ghist;                   // null, or the producers' head histogram (re-zeroed here)
 };
 
 struct FinalLds {  // LDS working set (the fused form reuses the scan's stages)
@@ -261,14 +268,84 @@ struct FinalLds {  // LDS working set (the fused form reuses the scan's stages)
     unsigned* cnt;
     unsigned long long* Td;
     unsigned* Ti;
-    unsigned* hist;          // kHistBins words (used with FinalIo::head_d)
+    unsigned* hist;          // kHistBins words
 };
 
-template <int KPL, int NT, int OWN>
+// Phase timestamps of one kNN launch (measurement builds only, MODE 6 of knn_scan): per block
+// 8 slots at [8 b], the final selection's at [8 nblocks + p]; 100 MHz real-time clock.
+__device__ unsigned long long* g_knn_trace;
+#define GEOHIP_TRACE(on, slot)                                                        \
+    do {                                                                              \
+        if ((on) && threadIdx.x == 0) g_knn_trace[(slot)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+
+__device__ __forceinline__ unsigned load_sc1(const unsigned* p) {
+    return __hip_atomic_load(((const gu32*)(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Rank placement of m keys held in LDS (d 16-byte aligned, ix 8-byte aligned): entry t goes to
+// position #{j : key_j < key_t or (key_j == key_t and j < t)} (unique positions even for equal
+// keys); calls put(pos, d, i) for pos < limit.  The keys are read as broadcast LDS loads, 8 per
+// batch (4 ds_read_b128 + 4 ds_read_b64 in flight) so the loop pays LDS latency once per batch.
+__device__ __forceinline__ unsigned rank_less(unsigned long long jd, unsigned ji, unsigned j, unsigned long long kd,
+                                              unsigned ki, unsigned t) {
+    return (jd < kd || (jd == kd && (ji < ki || (ji == ki && j < t)))) ? 1u : 0u;
+}
+template <int NT, class Put>
+__device__ __forceinline__ void rank_place(const unsigned long long* d, const unsigned* ix, unsigned m, unsigned limit,
+                                           Put put) {
+    if (m <= 64) {
+        // G = NT / 64 lanes per key (consecutive lanes of one DPP row), each counting the smaller
+        // keys among every G-th; the G partial counts are summed by lane-xor DPP moves
+        constexpr int G = NT / 64 < 16 ? NT / 64 : 16;
+        const unsigned t = threadIdx.x / G, g = threadIdx.x % G;
+        unsigned r = 0;
+        unsigned long long kd = 0;
+        unsigned ki = 0;
+        if (t < m) {
+            kd = d[t];
+            ki = ix[t];
+#pragma unroll
+            for (int u = 0; u < 64 / G; u++) {
+                const unsigned j = g + (unsigned)(u * G);
+                if (j < m) r += rank_less(d[j], ix[j], j, kd, ki, t);
+            }
+        }
+#pragma unroll
+        for (int o = 1; o < G; o <<= 1) r += xor_lane(r, o);
+        if (g == 0 && t < m && r < limit) put(r, kd, ki);
+        return;
+    }
+    for (unsigned t = threadIdx.x; t < m; t += NT) {
+        const unsigned long long kd = d[t];
+        const unsigned ki = ix[t];
+        unsigned r = 0;
+        unsigned j = 0;
+        for (; j + 8 <= m; j += 8) {
+            ulonglong2 dd[4];
+            uint2 ii[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                dd[u] = *reinterpret_cast<const ulonglong2*>(d + j + 2 * u);
+                ii[u] = *reinterpret_cast<const uint2*>(ix + j + 2 * u);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                r += rank_less(dd[u].x, ii[u].x, j + 2 * u, kd, ki, t);
+                r += rank_less(dd[u].y, ii[u].y, j + 2 * u + 1, kd, ki, t);
+            }
+        }
+        for (; j < m; j++) r += rank_less(d[j], ix[j], j, kd, ki, t);
+        if (r < limit) put(r, kd, ki);
+    }
+}
+
+template <int KPL, int NT, int OWN, bool TRACE = false, bool DRY = false>
 __device__ void final_select(const FinalIo& io, const FinalLds& s) {
+    const size_t tb = (size_t)8 * gridDim.x;  // final-selection trace slots
     constexpr int N = 64 * KPL;
-    constexpr int KPL2 = 2 * KPL;
     constexpr int NW = NT / kWave;
+    constexpr int HWPT = (kHistBins + NT - 1) / NT;  // histogram bins per thread
     const int lane = lane_id();
     const int wid = threadIdx.x / kWave;
     const unsigned nlists = io.nlists, list_len = io.list_len, k = io.k;
@@ -277,8 +354,17 @@ __device__ void final_select(const FinalIo& io, const FinalLds& s) {
         *s.Td = kSentinelD;
         *s.Ti = kSentinelI;
     }
+    // ---- (0) every global load up front
     unsigned nspill = 0;
-    if (io.spill_cnt) nspill = __hip_atomic_load(io.spill_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (io.spill_cnt) nspill = load_sc1(io.spill_cnt);
+    unsigned hc[HWPT][kGhistCopies];
+#pragma unroll
+    for (int w = 0; w < HWPT; w++) {
+        const int b = threadIdx.x + w * NT;
+#pragma unroll
+        for (int c = 0; c < kGhistCopies; c++)
+            hc[w][c] = (io.ghist && b < kHistBins) ? load_sc1(io.ghist + c * kHistBins + b) : 0u;
+    }
     KE e[OWN][kHeads];  // first kHeads entries of every owned list
 #pragma unroll
     for (int j = 0; j < OWN; j++) {
@@ -302,18 +388,33 @@ __device__ void final_select(const FinalIo& io, const FinalLds& s) {
             }
         }
     }
-    // (1a) T from a histogram of the heads (LDS atomics, one wave scan): the upper edge of the
-    // bin where the cumulative head count reaches k.  >= k heads lie at or below it, so it is a
-    // valid T; left unresolved (exact path below) when that bin is the lowest or the top one.
+    GEOHIP_TRACE(TRACE, tb + 1);
+    // ---- (1a) T from the head histogram
     bool resolved = false;
-    if (nlists >= k && io.head_d && OWN * NT >= (int)nlists) {
-        for (int t = threadIdx.x; t < kHistBins; t += NT) s.hist[t] = 0;
-        __syncthreads();
+    const bool local_hist = !io.ghist && nlists >= k && io.head_d && OWN * NT >= (int)nlists;
+    if (io.ghist || local_hist) {
 #pragma unroll
-        for (int j = 0; j < OWN; j++)
-            if (e[j][0].d != kSentinelD) atomicAdd(&s.hist[hist_bin(e[j][0].d, io.hist_base)], 1u);
+        for (int w = 0; w < HWPT; w++) {
+            const int b = threadIdx.x + w * NT;
+            if (b < kHistBins) {
+                unsigned v = 0;
+#pragma unroll
+                for (int c = 0; c < kGhistCopies; c++) {
+                    v += hc[w][c];
+                    if (io.ghist) store_wt(io.ghist + c * kHistBins + b, 0u);  // ready for the next window
+                }
+                s.hist[b] = v;
+            }
+        }
         __syncthreads();
-        if (wid == 0) {
+        GEOHIP_TRACE(TRACE, tb + 5);
+        if (local_hist) {
+#pragma unroll
+            for (int j = 0; j < OWN; j++)
+                if (e[j][0].d != kSentinelD) atomicAdd(&s.hist[hist_bin(e[j][0].d, io.hist_base)], 1u);
+            __syncthreads();
+        }
+        if (wid == 0 && nlists >= k) {
             const int bin = hist_kth_bin(s.hist, k);
             if (lane == 0 && bin > 0 && bin < kHistBins - 1) {
                 *s.Td = hist_edge(bin, io.hist_base);
@@ -323,7 +424,7 @@ __device__ void final_select(const FinalIo& io, const FinalLds& s) {
         __syncthreads();
         resolved = *s.Td != kSentinelD;
     }
-    // (1b) exact: T = k-th smallest head
+    // ---- (1b) exact: T = k-th smallest head
     if (nlists >= k && !resolved) {
         WList<KPL> L;
 #pragma unroll
@@ -371,11 +472,15 @@ __device__ void final_select(const FinalIo& io, const FinalLds& s) {
         }
     }
     __syncthreads();
+    GEOHIP_TRACE(TRACE, tb + 2);
     const unsigned long long T_d = *s.Td;
     const unsigned T_i = *s.Ti;
-    // (2) gather every real entry <= T
+    // ---- (2) gather every real entry <= T.  The preloaded entries go by a block-wide prefix
+    // sum of per-thread counts (lists ascending: the passing entries of a list are a prefix);
+    // the rare rest (lists whose kHeads entries all pass, lists past OWN * NT, spill) by atomics.
+    auto pass = [&](const KE& v) -> bool { return v.d != kSentinelD && !lds_kless(T_d, T_i, v.d, v.i); };
     auto take = [&](const KE& e) -> bool {
-        if (e.d == kSentinelD || lds_kless(T_d, T_i, e.d, e.i)) return false;
+        if (!pass(e)) return false;
         const unsigned pos = atomicAdd(s.cnt, 1u);
         if (pos < s.cap) {
             s.bd[pos] = e.d;
@@ -383,67 +488,91 @@ __device__ void final_select(const FinalIo& io, const FinalLds& s) {
         }
         return true;
     };
+    unsigned npass[OWN];
+    unsigned mine = 0;
 #pragma unroll
     for (int j = 0; j < OWN; j++) {
         const unsigned own = threadIdx.x + (unsigned)(j * NT);
-        if (own >= nlists) continue;
-        bool more = true;
+        unsigned c = 0;
 #pragma unroll
-        for (int h = 0; h < kHeads; h++) more = more && take(e[j][h]);
-        if (more) {  // all preloaded entries taken: the rest of the list from memory (rare)
+        for (int h = 0; h < kHeads; h++) c += (c == (unsigned)h && own < nlists && pass(e[j][h])) ? 1u : 0u;
+        npass[j] = c;
+        mine += c;
+    }
+    const unsigned incl = wave_incl_scan(mine);
+    unsigned* wsum = s.hist;  // free once T is known
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    unsigned wbase = 0, total_fast = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+        const unsigned v = wsum[w];
+        wbase += w < wid ? v : 0u;
+        total_fast += v;
+    }
+    {
+        unsigned pos = wbase + incl - mine;
+#pragma unroll
+        for (int j = 0; j < OWN; j++) {
+#pragma unroll
+            for (int h = 0; h < kHeads; h++) {
+                if ((unsigned)h < npass[j]) {
+                    if (pos < s.cap) {
+                        s.bd[pos] = e[j][h].d;
+                        s.bi[pos] = e[j][h].i;
+                    }
+                    pos++;
+                }
+            }
+        }
+    }
+    if (threadIdx.x == 0) *s.cnt = total_fast;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < OWN; j++) {
+        const unsigned own = threadIdx.x + (unsigned)(j * NT);
+        if (npass[j] == (unsigned)kHeads && own < nlists) {  // the rest of the list from memory (rare)
             const size_t off = (size_t)own * list_len;
             for (unsigned q = kHeads; q < list_len; q++) {
-                KE e;
-                e.d = io.part_d[off + q];
-                e.i = io.part_i[off + q];
-                if (!take(e)) break;
+                KE v;
+                v.d = io.part_d[off + q];
+                v.i = io.part_i[off + q];
+                if (!take(v)) break;
             }
         }
     }
     for (unsigned p = threadIdx.x + (unsigned)(OWN * NT); p < nlists; p += NT) {
         const size_t off = (size_t)p * list_len;
         for (unsigned q = 0; q < list_len; q++) {
-            KE e;
-            e.d = io.part_d[off + q];
-            e.i = io.part_i[off + q];
-            if (!take(e)) break;
+            KE v;
+            v.d = io.part_d[off + q];
+            v.i = io.part_i[off + q];
+            if (!take(v)) break;
         }
     }
     // survivors a scan block could not keep in LDS (unsorted, usually none)
     for (unsigned t = threadIdx.x; t < nspill; t += NT) {
-        KE e;
-        e.d = io.spill_d[t];
-        e.i = io.spill_i[t];
-        take(e);
+        KE v;
+        v.d = io.spill_d[t];
+        v.i = io.spill_i[t];
+        take(v);
     }
     __syncthreads();
+    GEOHIP_TRACE(TRACE, tb + 3);
     if (io.spill_cnt && threadIdx.x == 0) *io.spill_cnt = 0;  // ready for the next window on this stream
     const unsigned total = *s.cnt;
     const unsigned outn = total < k ? total : k;
-    if (total <= (unsigned)(64 * KPL2)) {
-        // (3) one wave: register bitonic sort of <= 128*KPL entries
-        if (wid == 0) {
-            WList<KPL2> S;
-#pragma unroll
-            for (int q = 0; q < KPL2; q++) {
-                const unsigned e = (unsigned)(q * 64 + lane);
-                S.s[q] = ksentinel();
-                if (e < total) {
-                    S.s[q].d = s.bd[e];
-                    S.s[q].i = s.bi[e];
-                }
-            }
-            wave_sort_list<KPL2>(S);
-#pragma unroll
-            for (int q = 0; q < KPL2; q++) {
-                const unsigned e = (unsigned)(q * 64 + lane);
-                if (e < k) {
-                    io.out_d[e] = __longlong_as_double((long long)(e < outn ? S.s[q].d : kSentinelD));
-                    io.out_i[e] = e < outn ? S.s[q].i : kSentinelI;
-                }
-            }
-            if (lane == 0) *io.out_count = outn;
-        }
+    auto put = [&](unsigned pos, unsigned long long d, unsigned i) {
+        if (DRY) return;
+        io.out_d[pos] = __longlong_as_double((long long)d);
+        io.out_i[pos] = i;
+    };
+    if (total <= s.cap && total <= 2u * NT) {
+        // ---- (3) rank placement of the gathered entries
+        rank_place<NT>(s.bd, s.bi, total, k, put);
+        for (unsigned t = outn + threadIdx.x; t < k; t += NT) put(t, kSentinelD, kSentinelI);
+        if (threadIdx.x == 0 && !DRY) *io.out_count = outn;
+        GEOHIP_TRACE(TRACE, tb + 4);
         return;
     }
     if (total <= s.cap) {
@@ -527,64 +656,112 @@ __global__ __launch_bounds__(kFinalThreads) void knn_final(FinalIo io) {
 }
 
 // Where a scan writes its result.  ticket != null: the block lists are stored write-through
-// (sc1) and the last block to take a ticket runs final_select into out_* (one launch per
-// window); ticket == null: only the block lists are written (knn_final merges them).
+// (sc1) and the last block to arrive runs final_select into out_* (one launch per window);
+// ticket == null: only the block lists are written (knn_final merges them).
+// Arrival is counted in two levels so no counter sees more than ~max(G, nblocks/G) atomics
+// (one device-scope counter taking every block's atomic costs ~11-13 ns per arrival,
+// MI355X_MICROARCH.md "fanin"): block b counts on group counter b % G; the last arriver of
+// a group counts on the top counter; the last of those runs the final selection.  Counters
+// sit 128 B apart (ticket[32 g], top at ticket[32 G]) and are re-zeroed by their last user.
 struct KnnOut {
     double* out_d;
     unsigned* out_i;
     unsigned* out_count;
-    unsigned* ticket;  // zero before the first launch; the last arriver re-zeroes it
+    unsigned* ticket;  // zero before the first launch
+    unsigned groups;   // G >= 1
+    unsigned* ghist;   // head histogram of the final selection (zero before the launch)
+    int epi_sort;      // block list by a register sort (fc <= 64, KPL 1) instead of rank placement
 };
+static_assert(kTicketStride * (kMaxTicketGroups + 2) <= kGhistWord, "counter scratch layout");
+static_assert((kGhistWord + kGhistCopies * kHistBins) * 4 <= kKnnCounterBytes, "counter scratch layout");
 
+__device__ __forceinline__ unsigned ticket_add(unsigned* p) {
+    return __hip_atomic_fetch_add(((gu32*)(p)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ticket_zero(unsigned* p) {
+    __hip_atomic_store(((gu32*)(p)), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one lane: true for the block that arrives last
+__device__ __forceinline__ bool arrive_last(const KnnOut& out) {
+    const unsigned G = out.groups;
+    const unsigned nb = gridDim.x;
+    if (G <= 1) {
+        const bool last = ticket_add(out.ticket) == nb - 1;
+        if (last) ticket_zero(out.ticket);
+        return last;
+    }
+    const unsigned g = blockIdx.x % G;
+    const unsigned members = nb / G + (g < nb % G ? 1u : 0u);
+    unsigned* gc = out.ticket + (size_t)kTicketStride * g;
+    if (ticket_add(gc) != members - 1) return false;
+    ticket_zero(gc);
+    const unsigned geff = nb < G ? nb : G;
+    unsigned* top = out.ticket + (size_t)kTicketStride * G;
+    const bool last = ticket_add(top) == geff - 1;
+    if (last) ticket_zero(top);
+    return last;
+}
 
 // MODE (ablation builds for measurement only; the product launches MODE 0):
 //   0 full, 1 loads only, 2 loads + classification, 3 + LDS staging and distances (no selection),
-//   5 full + counters (survivors, spilled), 7 full without the end-of-block selection
-template <int KPL, int MODE = 0>
-__global__ __launch_bounds__(kBlock) void knn_scan(const double* __restrict__ x, const double* __restrict__ y,
-                                                   uint64_t n, uint64_t chunk, KnnArgs args,
-                                                   unsigned long long* __restrict__ part_d,
-                                                   unsigned* __restrict__ part_i,
-                                                   unsigned long long* __restrict__ spill_d,
-                                                   unsigned* __restrict__ spill_i, unsigned* __restrict__ spill_cnt,
-                                                   KnnOut out) {
-    __shared__ WaveStage stage[kBlock / kWave];
-    __shared__ KnnBlock kb;
+//   5 full + counters (survivors, spilled), 6 full + phase timestamps (g_knn_trace),
+//   7 full without the end-of-block selection, 10 full without the final selection (arrival
+//   protocol only), 11 full without the final selection's output writes
+template <int KPL, int NW, int PF, int MODE = 0>
+__global__ __launch_bounds__(NW * 64) void knn_scan(const double* __restrict__ x, const double* __restrict__ y,
+                                                    uint64_t n, uint64_t chunk, KnnArgs args,
+                                                    unsigned long long* __restrict__ part_d,
+                                                    unsigned* __restrict__ part_i,
+                                                    unsigned long long* __restrict__ spill_d,
+                                                    unsigned* __restrict__ spill_i, unsigned* __restrict__ spill_cnt,
+                                                    KnnOut out) {
+    constexpr int NT = NW * 64;
+    constexpr bool TR = MODE == 6;
+    GEOHIP_TRACE(TR, 8 * blockIdx.x);
+    if (TR && threadIdx.x == 0) {  // where the block runs: HW_ID (cu/sh/se) and XCC_ID
+        g_knn_trace[8 * blockIdx.x + 5] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+        g_knn_trace[8 * blockIdx.x + 6] = (unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 20);
+    }
+    using KB = KnnBlock<NW>;
+    __shared__ WaveStage stage[NW];
+    __shared__ KB kb;
     const int lane = lane_id();
     const int wid = threadIdx.x / kWave;
     WaveStage& st = stage[wid];
     const uint64_t blk_begin = (uint64_t)blockIdx.x * chunk;
     uint64_t blk_end = blk_begin + chunk;
     if (blk_end > n) blk_end = n;
-    for (int t = threadIdx.x; t < kHistBins; t += kBlock) kb.hist[t] = 0;
+    for (int t = threadIdx.x; t < kHistBins; t += NT) kb.hist[t] = 0;
     if (threadIdx.x == 0) {
         kb.bound = kSentinelD;
         kb.cnt = 0;
     }
-    __syncthreads();
 
     const unsigned k = args.k;
     unsigned ccnt = 0;
     unsigned appended = 0, last_hist = 0;
 
-    // software pipeline: the next iteration's 4 KB per wave is in flight while this one is
-    // classified
-    constexpr uint64_t kStride = (uint64_t)(kBlock / kWave) * kPtsIter;
+    constexpr uint64_t kStride = (uint64_t)NW * kPtsIter;
     uint64_t base = blk_begin + (uint64_t)wid * kPtsIter;
     double sink = 0.0;
-    double nx[4], ny[4];
-    bool nv[4];
-    if (base < blk_end) load4(x, y, base, blk_end, lane, nx, ny, nv);
-    for (; base < blk_end; base += kStride) {
-        double px[4], py[4];
-        bool valid[4];
-#pragma unroll
-        for (int s = 0; s < 4; s++) { px[s] = nx[s]; py[s] = ny[s]; valid[s] = nv[s]; }
-        if (base + kStride < blk_end) load4(x, y, base + kStride, blk_end, lane, nx, ny, nv);
+    // G u C is one box for a point query (the candidate square contains the guaranteed one),
+    // kept in registers; further boxes (unusual plans) are tested from the kernel arguments
+    const Box b0 = args.u[0];
+    const int nu = args.nu;
+    auto in_union = [&](double px, double py) -> bool {
+        bool c = in_box(b0, px, py);
+        if (nu > 1)
+            for (int b = 1; b < nu; b++) c = c || in_box(args.u[b], px, py);
+        return c;
+    };
+    // one wave iteration over 256 points (4 per lane) already in registers; FULL: all valid
+    auto iter = [&](auto full, const double (&px)[4], const double (&py)[4], const bool (&valid)[4], uint64_t ib) {
+        constexpr bool FULL = decltype(full)::value;
         if (MODE == 1) {
 #pragma unroll
             for (int s = 0; s < 4; s++) sink += px[s] + py[s];
-            continue;
+            return;
         }
         // squared screen against the block bound: only candidates that may beat it reach the
         // exact fdlibm distance
@@ -598,9 +775,8 @@ __global__ __launch_bounds__(kBlock) void knn_scan(const double* __restrict__ x,
         }
 #pragma unroll
         for (int s = 0; s < 4; s++) {
-            bool c = false;
-            for (int b = 0; b < args.nu; b++) c = c || in_box(args.u[b], px[s], py[s]);
-            c = c && valid[s];
+            bool c = in_union(px[s], py[s]);
+            if (!FULL) c = c && valid[s];
             if (MODE == 0 || MODE >= 5) {
                 const double dx = args.qx - px[s], dy = args.qy - py[s];
                 const double d2 = dx * dx + dy * dy;
@@ -615,11 +791,11 @@ __global__ __launch_bounds__(kBlock) void knn_scan(const double* __restrict__ x,
                 const unsigned pos = ccnt + lanes_below(m);
                 st.cx[pos] = px[s];
                 st.cy[pos] = py[s];
-                st.ci[pos] = (unsigned)slot_index(base, lane, s);
+                st.ci[pos] = (unsigned)slot_index(ib, lane, s);
             }
             ccnt += (unsigned)__popcll(m);
         }
-        if (MODE == 2) continue;
+        if (MODE == 2) return;
         wave_lds_sync();
         if (MODE == 3) {
             while (ccnt >= 64) {
@@ -628,7 +804,7 @@ __global__ __launch_bounds__(kBlock) void knn_scan(const double* __restrict__ x,
                 wave_lds_sync();
                 ccnt = from;
             }
-            continue;
+            return;
         }
         if (ccnt >= 64) {
             knn_dist_batch(st, ccnt, kb, args, spill_d, spill_i, spill_cnt, appended, false);
@@ -638,11 +814,47 @@ __global__ __launch_bounds__(kBlock) void knn_scan(const double* __restrict__ x,
                 last_hist = appended;
             }
         }
+    };
+    // Software pipeline of the coordinate loads over the wave's full iterations: two register
+    // sets A and B alternate, each refilled right after use, so two iterations (8 KB per wave)
+    // are in flight while one is classified and no register copy ever waits on a load.  A
+    // partial last iteration (only in the window's last block) is handled after the loop.
+    const std::integral_constant<bool, true> kFull;
+    const std::integral_constant<bool, false> kPart;
+    const bool all_valid[4] = {true, true, true, true};
+    double ax[4], ay[4], bx[4], by[4];
+    auto load_full = [&](uint64_t b, double (&px)[4], double (&py)[4]) {
+        const uint64_t i0 = b + 2 * (uint64_t)lane;
+        const double2 u0 = *reinterpret_cast<const double2*>(x + i0);
+        const double2 u1 = *reinterpret_cast<const double2*>(x + i0 + 128);
+        const double2 v0 = *reinterpret_cast<const double2*>(y + i0);
+        const double2 v1 = *reinterpret_cast<const double2*>(y + i0 + 128);
+        px[0] = u0.x; px[1] = u0.y; px[2] = u1.x; px[3] = u1.y;
+        py[0] = v0.x; py[1] = v0.y; py[2] = v1.x; py[3] = v1.y;
+    };
+    if (base + kPtsIter <= blk_end) load_full(base, ax, ay);
+    if (base + kStride + kPtsIter <= blk_end) load_full(base + kStride, bx, by);
+    __syncthreads();
+    while (base + kPtsIter <= blk_end) {
+        iter(kFull, ax, ay, all_valid, base);
+        if (base + 2 * kStride + kPtsIter <= blk_end) load_full(base + 2 * kStride, ax, ay);
+        base += kStride;
+        if (base + kPtsIter > blk_end) break;
+        iter(kFull, bx, by, all_valid, base);
+        if (base + 2 * kStride + kPtsIter <= blk_end) load_full(base + 2 * kStride, bx, by);
+        base += kStride;
+    }
+    if (base < blk_end) {
+        double px[4], py[4];
+        bool valid[4];
+        load4(x, y, base, blk_end, lane, px, py, valid);
+        iter(kPart, px, py, valid, base);
     }
     if (MODE >= 1 && MODE <= 3) {
         if (sink == 12345.678) part_d[blockIdx.x] = 1;  // keep the ablated work alive
         return;
     }
+    GEOHIP_TRACE(TR, 8 * blockIdx.x + 1);
     knn_dist_batch(st, ccnt, kb, args, spill_d, spill_i, spill_cnt, appended, true);
     if (MODE == 5) {
         if (lane == 0) atomicAdd(&part_i[0], appended);
@@ -655,17 +867,20 @@ __global__ __launch_bounds__(kBlock) void knn_scan(const double* __restrict__ x,
 
     // ---- end of block: keep the survivors <= final bound, sort once, write the block list
     constexpr int N = 64 * KPL;
-    constexpr int KPL2 = 2 * KPL;
     __syncthreads();
+    GEOHIP_TRACE(TR, 8 * blockIdx.x + 2);
     if (wid == 0 && kb.cnt >= k) hist_bound(kb, k, args.hist_base);
     if (threadIdx.x == 0) kb.final_cnt = 0;
     __syncthreads();
     const unsigned long long B = kb.bound;
-    const unsigned have = kb.cnt < (unsigned)kBlkCap ? kb.cnt : (unsigned)kBlkCap;
+    const unsigned have = kb.cnt < (unsigned)KB::kCap ? kb.cnt : (unsigned)KB::kCap;
     // compact survivors <= B into the (now idle) wave stages
-    unsigned long long* cd = reinterpret_cast<unsigned long long*>(&stage[0].cx[0]);
-    unsigned* ci = reinterpret_cast<unsigned*>(&stage[2].cx[0]);
-    for (unsigned t0 = 0; t0 < have; t0 += kBlock) {
+    // (the tie path below sorts up to the next power of two of kCap = 256 NW entries in place)
+    constexpr size_t kCdCap = 256 * NW;
+    static_assert(sizeof(stage) >= kCdCap * 12, "end-of-block compaction buffer");
+    unsigned long long* cd = reinterpret_cast<unsigned long long*>(&stage[0]);
+    unsigned* ci = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(&stage[0]) + kCdCap * 8);
+    for (unsigned t0 = 0; t0 < have; t0 += NT) {
         const unsigned t = t0 + threadIdx.x;
         const bool keep = t < have && kb.bd[t] <= B;
         const unsigned long long m = __ballot(keep);
@@ -684,53 +899,40 @@ __global__ __launch_bounds__(kBlock) void knn_scan(const double* __restrict__ x,
     // packed heads behind the lists (FinalIo::head_d)
     unsigned long long* head_d = part_d + (size_t)gridDim.x * N;
     unsigned* head_i = part_i + (size_t)gridDim.x * N;
-    if (fc <= 64u && KPL == 1) {
-        if (wid == 0) {  // common case: one 64-lane register sort
+    auto put = [&](unsigned pos, unsigned long long d, unsigned i) {
+        store_wt(&part_d[off + pos], d);
+        store_wt(&part_i[off + pos], i);
+        if (pos < (unsigned)kHeads) {
+            store_wt(&head_d[kHeads * blockIdx.x + pos], d);
+            store_wt(&head_i[kHeads * blockIdx.x + pos], i);
+        }
+        // the block head joins the final selection's histogram as the block finishes
+        // (kGhistCopies copies so no bin counter takes more than ~nblocks / 8 arrivals)
+        if (pos == 0 && d != kSentinelD && out.ghist)
+            __hip_atomic_fetch_add(((gu32*)(out.ghist + (blockIdx.x % kGhistCopies) * kHistBins +
+                                            hist_bin(d, args.hist_base))),
+                                   1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    GEOHIP_TRACE(TR, 8 * blockIdx.x + 7);
+    if (KPL == 1 && fc <= 64u && out.epi_sort) {
+        if (wid == 0) {  // one 64-lane register bitonic sort
             KE e = ksentinel();
             if ((unsigned)lane < fc) { e.d = cd[lane]; e.i = ci[lane]; }
             e = wave_sort64(e);
-            store_wt(&part_d[off + lane], e.d);
-            store_wt(&part_i[off + lane], e.i);
-            if (lane < kHeads) {
-                store_wt(&head_d[kHeads * blockIdx.x + lane], e.d);
-                store_wt(&head_i[kHeads * blockIdx.x + lane], e.i);
-            }
+            put((unsigned)lane, e.d, e.i);
         }
-    } else if (fc <= (unsigned)(64 * KPL2)) {
-        if (wid == 0) {
-            WList<KPL2> S;
-#pragma unroll
-            for (int s = 0; s < KPL2; s++) {
-                const unsigned e = (unsigned)(s * 64 + lane);
-                S.s[s] = ksentinel();
-                if (e < fc) { S.s[s].d = cd[e]; S.s[s].i = ci[e]; }
-            }
-            wave_sort_list<KPL2>(S);
-#pragma unroll
-            for (int s = 0; s < KPL; s++) {
-                store_wt(&part_d[off + s * 64 + lane], S.s[s].d);
-                store_wt(&part_i[off + s * 64 + lane], S.s[s].i);
-            }
-            if (lane < kHeads) {
-                store_wt(&head_d[kHeads * blockIdx.x + lane], S.s[0].d);
-                store_wt(&head_i[kHeads * blockIdx.x + lane], S.s[0].i);
-            }
-        }
+    } else if (fc <= (unsigned)NT) {
+        // every kept survivor placed by rank (one pass over <= NT keys in LDS)
+        rank_place<NT>(cd, ci, fc, (unsigned)N, put);
+        for (unsigned p = fc + threadIdx.x; p < (unsigned)N; p += NT) put(p, kSentinelD, kSentinelI);
     } else {
         // many exact ties around the bound: sort all kept survivors in LDS (uniform branch)
         int m2 = 1;
         while (m2 < (int)fc) m2 <<= 1;
-        for (int t = threadIdx.x + fc; t < m2; t += kBlock) { cd[t] = kSentinelD; ci[t] = kSentinelI; }
+        for (int t = threadIdx.x + fc; t < m2; t += NT) { cd[t] = kSentinelD; ci[t] = kSentinelI; }
         __syncthreads();
         block_sort_lds(cd, ci, m2);
-        for (int t = threadIdx.x; t < N; t += kBlock) {
-            store_wt(&part_d[off + t], t < (int)fc ? cd[t] : kSentinelD);
-            store_wt(&part_i[off + t], t < (int)fc ? ci[t] : kSentinelI);
-            if (t < kHeads) {
-                store_wt(&head_d[kHeads * blockIdx.x + t], cd[t]);  // fc > 64*KPL2 >= kHeads
-                store_wt(&head_i[kHeads * blockIdx.x + t], ci[t]);
-            }
-        }
+        for (int t = threadIdx.x; t < N; t += NT) put((unsigned)t, t < (int)fc ? cd[t] : kSentinelD, t < (int)fc ? ci[t] : kSentinelI);
     }
     if (out.ticket == nullptr) return;
 
@@ -739,28 +941,28 @@ __global__ __launch_bounds__(kBlock) void knn_scan(const double* __restrict__ x,
     // one lane takes a ticket; the last arriver acquires once and merges all block lists.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned t = __hip_atomic_fetch_add(((gu32*)(out.ticket)), 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-        kb.final_cnt = t == gridDim.x - 1 ? 1u : 0u;
-    }
+    GEOHIP_TRACE(TR, 8 * blockIdx.x + 3);
+    if (threadIdx.x == 0) kb.final_cnt = arrive_last(out) ? 1u : 0u;
     __syncthreads();
+    GEOHIP_TRACE(TR, 8 * blockIdx.x + 4);
     if (kb.final_cnt == 0) return;
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
+    GEOHIP_TRACE(TR, 8 * (size_t)gridDim.x);
     // LDS: gathered entries in the (idle) wave stages, tree exchange in kb.bd/kb.bi
     static_assert(sizeof(stage) >= 2048 * 12, "fused final: gather buffer");
-    static_assert(sizeof(kb.bd) >= 2 * N * 8 && sizeof(kb.bi) >= 2 * N * 4, "fused final: tree exchange");
+    static_assert(sizeof(kb.bd) >= (size_t)(NW / 2 > 0 ? NW / 2 : 1) * N * 8, "fused final: tree exchange");
     char* sb = reinterpret_cast<char*>(&stage[0]);
     const FinalLds fl{kb.bd, kb.bi, reinterpret_cast<unsigned long long*>(sb), reinterpret_cast<unsigned*>(sb + 2048 * 8),
                       2048u, &kb.cnt, &kb.bound, &kb.final_cnt, kb.hist};
     const FinalIo io{part_d, part_i, gridDim.x, (unsigned)N, k, out.out_d, out.out_i, out.out_count,
-                     spill_d, spill_i, spill_cnt, head_d, head_i, args.hist_base};
-    final_select<KPL, kBlock, 1024 / kBlock>(io, fl);
-    if (threadIdx.x == 0) __hip_atomic_store(((gu32*)(out.ticket)), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                     spill_d, spill_i, spill_cnt, head_d, head_i, args.hist_base, out.ghist};
+    if (MODE == 10) return;  // ablation: arrival protocol without the final selection
+    // (MODE 11: the final selection without its output writes)
+    final_select<KPL, NT, (1024 / NT > 0 ? 1024 / NT : 1), TR, MODE == 11>(io, fl);
 }
 
 // ============================================================================ range =======
@@ -977,8 +1179,57 @@ static void launch_knn_final_heads(unsigned long long* part_d, unsigned* part_i,
                                    hipStream_t st) {
     const unsigned L = 64u * KPL;
     const FinalIo io{part_d, part_i, nblocks, L, k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt,
-                     part_d + (size_t)nblocks * L, part_i + (size_t)nblocks * L, hist_base};
+                     part_d + (size_t)nblocks * L, part_i + (size_t)nblocks * L, hist_base, spill_cnt + kGhistWord};
     knn_final<KPL><<<1, kFinalThreads, 0, st>>>(io);
+}
+
+static KnnConfig g_knn_cfg = {16, 1, 16, 0};  // fastest measured shape (profiles/r01_knn_shape_sweep.log)
+
+hipError_t set_knn_trace(unsigned long long* buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_knn_trace), &buf, sizeof(buf));
+}
+
+int set_knn_config(int nw, int pf, int groups, int epi_sort) {
+    if (!(nw == 4 || nw == 8 || nw == 16) || !(pf == 1 || pf == 2) || groups < 1 || groups > (int)kMaxTicketGroups)
+        return -1;
+    g_knn_cfg = KnnConfig{nw, pf, groups, epi_sort ? 1 : 0};
+    return 0;
+}
+KnnConfig knn_config() { return g_knn_cfg; }
+
+void knn_geometry(uint64_t n, unsigned* nblocks, uint64_t* chunk) {
+    // 16 waves per CU on all 256 CUs when n is large (equal work per block); an even chunk keeps
+    // the 16-byte double2 loads aligned
+    const uint64_t target = 256ull * (16 / (unsigned)g_knn_cfg.nw);
+    uint64_t c = (n + target - 1) / target;
+    c = (c + kPtsIter - 1) / kPtsIter * kPtsIter;  // whole wave iterations (aligned double2 loads)
+    if (c < 1024) c = 1024;
+    *chunk = c;
+    *nblocks = (unsigned)((n + c - 1) / c);
+}
+
+template <int KPL, int MODE>
+static void knn_scan_launch(unsigned nblocks, hipStream_t st, const double* x, const double* y, uint64_t n,
+                            uint64_t chunk, const KnnArgs& args, unsigned long long* part_d, unsigned* part_i,
+                            unsigned long long* spill_d, unsigned* spill_i, unsigned* spill_cnt, KnnOut out) {
+    const KnnConfig c = g_knn_cfg;
+#define GEOHIP_SCAN(NW, PF) \
+    knn_scan<KPL, NW, PF, MODE><<<nblocks, NW * 64, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, out)
+    switch (c.nw * 10 + c.pf) {
+        case 41: GEOHIP_SCAN(4, 1); break;
+        case 42: GEOHIP_SCAN(4, 2); break;
+        case 81: GEOHIP_SCAN(8, 1); break;
+        case 82: GEOHIP_SCAN(8, 2); break;
+        case 161: GEOHIP_SCAN(16, 1); break;
+        default: GEOHIP_SCAN(16, 2); break;
+    }
+#undef GEOHIP_SCAN
+}
+
+static KnnOut knn_out(bool fused, double* out_d, unsigned* out_i, unsigned* out_count, unsigned* spill_cnt) {
+    if (!fused) return KnnOut{nullptr, nullptr, nullptr, nullptr, 1u, spill_cnt + kGhistWord, g_knn_cfg.epi_sort};
+    return KnnOut{out_d, out_i, out_count, spill_cnt + kTicketStride, (unsigned)g_knn_cfg.groups, spill_cnt + kGhistWord,
+                  g_knn_cfg.epi_sort};
 }
 
 hipError_t launch_knn(const double* x, const double* y, uint64_t n, const KnnArgs& args, int kpl,
@@ -988,19 +1239,19 @@ hipError_t launch_knn(const double* x, const double* y, uint64_t n, const KnnArg
     const unsigned k = args.k;
     const unsigned L = 64u * (unsigned)kpl;
     if (nblocks == 0) {  // empty window: the final selection alone writes the empty result
-        const FinalIo io{part_d, part_i, 0u, L, k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt, nullptr, nullptr, 0};
+        const FinalIo io{part_d, part_i, 0u, L, k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt, nullptr, nullptr, 0,
+                         nullptr};
         if (k <= 64) knn_final<1><<<1, kFinalThreads, 0, st>>>(io);
         else if (k <= 128) knn_final<2><<<1, kFinalThreads, 0, st>>>(io);
         else knn_final<4><<<1, kFinalThreads, 0, st>>>(io);
         return hipGetLastError();
     }
-    // fused: spill_cnt[1] is the arrival ticket of the in-kernel final selection
-    const KnnOut out = g_knn_fused ? KnnOut{out_d, out_i, out_count, spill_cnt + 1} : KnnOut{nullptr, nullptr, nullptr, nullptr};
+    const KnnOut out = knn_out(g_knn_fused, out_d, out_i, out_count, spill_cnt);
     if (ev0) (void)hipEventRecord(ev0, st);
     switch (kpl) {
-        case 1: knn_scan<1><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, out); break;
-        case 2: knn_scan<2><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, out); break;
-        case 4: knn_scan<4><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, out); break;
+        case 1: knn_scan_launch<1, 0>(nblocks, st, x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, out); break;
+        case 2: knn_scan_launch<2, 0>(nblocks, st, x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, out); break;
+        case 4: knn_scan_launch<4, 0>(nblocks, st, x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, out); break;
         default: return hipErrorInvalidValue;
     }
     if (ev1) (void)hipEventRecord(ev1, st);
@@ -1018,29 +1269,35 @@ hipError_t launch_knn_scan_variant(int mode, const double* x, const double* y, u
                                    unsigned long long* part_d, unsigned* part_i, unsigned nblocks, uint64_t chunk,
                                    unsigned long long* spill_d, unsigned* spill_i, unsigned* spill_cnt, double* out_d,
                                    unsigned* out_i, unsigned* out_count, hipStream_t st) {
-    const KnnOut fused{out_d, out_i, out_count, spill_cnt + 1};
-    const KnnOut lists{nullptr, nullptr, nullptr, nullptr};
+    const KnnOut fused = knn_out(true, out_d, out_i, out_count, spill_cnt);
+    const KnnOut lists = knn_out(false, out_d, out_i, out_count, spill_cnt);
+#define GEOHIP_VAR(M, O) knn_scan_launch<1, M>(nblocks, st, x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, O)
     switch (mode) {
-        case 0: knn_scan<1, 0><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, fused); break;
-        case 1: knn_scan<1, 1><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, lists); break;
-        case 2: knn_scan<1, 2><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, lists); break;
-        case 3: knn_scan<1, 3><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, lists); break;
-        case 5: knn_scan<1, 5><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, lists); break;
-        case 7: knn_scan<1, 7><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, lists); break;
-        case 8: knn_scan<1, 0><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, lists); break;
+        case 0: GEOHIP_VAR(0, fused); break;
+        case 1: GEOHIP_VAR(1, lists); break;
+        case 2: GEOHIP_VAR(2, lists); break;
+        case 3: GEOHIP_VAR(3, lists); break;
+        case 5: GEOHIP_VAR(5, lists); break;
+        case 6: GEOHIP_VAR(6, fused); break;
+        case 10: GEOHIP_VAR(10, fused); break;
+        case 11: GEOHIP_VAR(11, fused); break;
+        case 7: GEOHIP_VAR(7, lists); break;
+        case 8: GEOHIP_VAR(0, lists); break;
         case 9:
-            knn_scan<1, 0><<<nblocks, kBlock, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, lists);
+            GEOHIP_VAR(0, lists);
             launch_knn_final_heads<1>(part_d, part_i, nblocks, args.k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt,
                                       args.hist_base, st);
             break;
         default: return hipErrorInvalidValue;
     }
+#undef GEOHIP_VAR
     return hipGetLastError();
 }
 
 hipError_t launch_knn_merge(const unsigned long long* d, const unsigned* i, unsigned nlists, unsigned list_len,
                             unsigned k, double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st) {
-    const FinalIo io{d, i, nlists, list_len, k, out_d, out_i, out_count, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
+    const FinalIo io{d, i, nlists, list_len, k, out_d, out_i, out_count, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
+                     nullptr};
     if (k <= 64) knn_final<1><<<1, kFinalThreads, 0, st>>>(io);
     else if (k <= 128) knn_final<2><<<1, kFinalThreads, 0, st>>>(io);
     else knn_final<4><<<1, kFinalThreads, 0, st>>>(io);
