@@ -1,18 +1,26 @@
-"""Headline benchmark: windowed point-point kNN (BASELINE.json configs[1]).
+"""Benchmark: GeoFlink windowed spatial queries on MI355X (BASELINE.json).
 
-One step = one window: kNN (k = 50) of the README query point over 10M uniform points per
-GPU (100x100 Beijing grid, r = 0.5) -- the scan kernel, the final selection and, for N > 1,
-the RCCL all-gather of each rank's top-k plus the device merge (weak scaling: every rank
-holds its own 10M-point shard of the window; ranks shard by arrival order, which gives the
-identical result for a single-query kNN).
+Default workload (the headline, BASELINE.json configs[1] = C2): one step = one window of
+point-point kNN (k = 50) of the README query over 10M uniform points per GPU (100x100 Beijing
+grid, r = 0.5): the scan kernel with its fused final selection and, for N > 1, the RCCL
+all-gather of each rank's top-k plus the device merge (weak scaling: every rank holds its own
+10M-point shard of the window; ranks shard by arrival order, which gives the identical result
+for a single-query kNN).
 
-Windows are device-resident before the timed region (synthetic, generated on the device with
-the counter-based generator of spatialflink_amd.synth); a ring of WINDOWS distinct windows
-(> 256 MiB in total) is cycled so no step reads a window the Infinity Cache still holds.
+The other configs are measured with ``--workload`` (same JSON contract, one line each):
+  range  C1 query shape (100x100, README query, r = 0.5) over 10M uniform points per GPU
+  join   C3: 10k queries x 10M Gaussian-clustered data points per GPU, 500x500, r = 0.05
+  ppoly  C4: 1k polygons (50 vertices) over 50M uniform points per GPU, 500x500, r = 0.005
+  c5     C5 per shard: 25M uniform points per GPU, 1000x1000, kNN k = 100 + range r = 0.05
+
+Windows are device-resident before the timed region (synthetic: uniform windows are made on
+the device by the counter-based generator of spatialflink_amd.synth; Gaussian windows on the
+host by synth.gaussian_clusters then copied).  A ring of distinct windows (> 256 MiB in total)
+is cycled so no step reads a window the Infinity Cache still holds.
 
 Prints ONE JSON line (rank 0) with roofline and cpu_baseline objects.
 
-    python bench.py --gpus 1 --steps 50 --warmup 5
+    python bench.py --gpus 1 --steps 50 --warmup 5 [--workload knn|range|join|ppoly|c5]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -31,11 +39,6 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "points/sec (whole node) for windowed range/kNN/join at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-N_PER_GPU = 10_000_000
-GRID_N = 100
-K = 50
-RADIUS = 0.5
-WINDOWS = 4
 BYTES_PER_POINT = 16  # algorithmic: x + y fp64 read once
 
 
@@ -44,7 +47,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--points", type=int, default=N_PER_GPU)
+    p.add_argument("--workload", choices=("knn", "range", "join", "ppoly", "c5"), default="knn")
+    p.add_argument("--points", type=int, default=None, help="points per window per GPU (default: the config's)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--knn-final", choices=("fused", "separate"), default="fused",
@@ -52,41 +56,377 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(seconds: float):
-    """The C oracle (oracle/geohip_oracle.c, a single-threaded port of the reference
-    predicate + heap kNN) on the same workload, bounded to ~`seconds` of CPU work."""
+def _oracle():
     sys.path.insert(0, str(ROOT / "oracle"))
-    import cref
-    from spatialflink_amd import synth
-
-    bj = synth.BEIJING
-    q = synth.README_QUERY
-    cg = cref.grid(bj[0], bj[2], (bj[1] - bj[0]) / GRID_N, GRID_N)
-    n = 2_000_000
-    done = 0
-    wins = 0
-    t_total = 0.0
-    while t_total < seconds and wins < 30:
-        x, y = synth.uniform(n, 1000 + wins)
-        t0 = time.perf_counter()
-        cref.knn_pp(cg, x, y, q[0], q[1], RADIUS, K)
-        t_total += time.perf_counter() - t0
-        done += n
-        wins += 1
-    return {"value": done / t_total, "unit": "points/sec", "cores": 1, "kind": "port",
-            "sample": f"{wins} windows x {n} uniform points (C2 shape: k={K}, {GRID_N}x{GRID_N}, r={RADIUS}), "
-                      f"oracle/geohip_oracle.c single thread, {t_total:.1f} s"}
+    import cref  # the checker / CPU baseline only (test infrastructure)
+    return cref
 
 
-def pmc_traffic():
-    """HBM bytes per scan launch from the committed rocprofv3 PMC pass, if present."""
-    f = ROOT / "profiles" / "pmc_knn_scan_r01.json"
+def _timed_loop(fn, seconds, max_iter):
+    """Run fn(i) until ~seconds of measured time or max_iter calls; returns (calls, seconds)."""
+    t_total, i = 0.0, 0
+    while t_total < seconds and i < max_iter:
+        t_total += fn(i)
+        i += 1
+    return i, t_total
+
+
+def pmc_traffic(kernel_tag: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/pmc_<tag>.json)."""
+    f = ROOT / "profiles" / f"pmc_{kernel_tag}.json"
     if f.exists():
         try:
             return json.loads(f.read_text()).get("hbm_bytes_per_launch")
         except Exception:
             return None
     return None
+
+
+# ----------------------------------------------------------------------------------------------
+class Workload:
+    """One config: device-resident windows, one step = one window through the C ABI."""
+    tag = ""
+    kernel = ""
+    windows = 4
+
+    def __init__(self, args, ctx, dev, rank, world, dist):
+        self.args, self.ctx, self.dev, self.rank, self.world, self.dist = args, ctx, dev, rank, world, dist
+
+    def units_per_step(self) -> int:  # points of one window on this rank
+        raise NotImplementedError
+
+    def step(self, s: int) -> None:
+        raise NotImplementedError
+
+    def algorithmic_bytes(self) -> float:  # per timed launch (ctx timing events)
+        raise NotImplementedError
+
+    def config(self) -> dict:
+        raise NotImplementedError
+
+    def cpu_baseline(self, seconds: float) -> dict:
+        raise NotImplementedError
+
+    def roofline_extra(self) -> dict:
+        return {}
+
+
+def _uniform_windows(ctx, dev, n, rank, seeds, bbox):
+    import torch
+    xs, ys = [], []
+    for sd in seeds:
+        x = torch.empty(n, dtype=torch.float64, device=dev)
+        y = torch.empty(n, dtype=torch.float64, device=dev)
+        # window of rank r = slice [r*n, (r+1)*n) of the N*n-point window
+        ctx.synth_uniform_async(x, y, rank * n, sd, bbox)
+        xs.append(x)
+        ys.append(y)
+    return xs, ys
+
+
+class KnnWorkload(Workload):
+    """C2 (BASELINE.json configs[1]): kNN k=50, 100x100, r=0.5, 10M uniform points per GPU."""
+    tag = "knn_scan"
+    kernel = "geohip::knn_scan<1> (fused final selection)"
+    grid_n, k, radius, n_default, seed0 = 100, 50, 0.5, 10_000_000, 2
+    label = "C2: point-point kNN k=50, 100x100 Beijing UniformGrid, r=0.5, README query"
+
+    def __init__(self, *a):
+        super().__init__(*a)
+        import torch
+        from spatialflink_amd import _abi, synth
+        self.n = self.args.points or self.n_default
+        bj = synth.BEIJING
+        self.q = synth.README_QUERY
+        self.grid = _abi.make_grid(bj[0], bj[2], (bj[1] - bj[0]) / self.grid_n, self.grid_n)
+        self.xs, self.ys = _uniform_windows(self.ctx, self.dev, self.n, self.rank,
+                                            [self.seed0 + 7919 * w for w in range(self.windows)], bj)
+        K, W, dev = self.k, self.world, self.dev
+        self.out_i = torch.empty(K, dtype=torch.int32, device=dev)
+        self.out_d = torch.empty(K, dtype=torch.float64, device=dev)
+        self.cnt = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.g_d = torch.empty((W, K), dtype=torch.float64, device=dev)
+        self.g_i = torch.empty((W, K), dtype=torch.int32, device=dev)
+        self.m_i = torch.empty(K, dtype=torch.int32, device=dev)
+        self.m_d = torch.empty(K, dtype=torch.float64, device=dev)
+        self.base = torch.tensor(self.rank * self.n, dtype=torch.int64, device=dev)
+
+    def units_per_step(self):
+        return self.n
+
+    def knn_step(self, w):
+        import torch
+        self.ctx.knn_pp_async(self.grid, self.xs[w], self.ys[w], self.q[0], self.q[1], self.radius, self.k,
+                              self.out_i, self.out_d, self.cnt[0:1])
+        if self.world > 1:
+            gi = torch.where(self.out_i >= 0, (self.out_i.to(torch.int64) + self.base).to(torch.int32), self.out_i)
+            self.dist.all_gather_into_tensor(self.g_d.view(-1), self.out_d)
+            self.dist.all_gather_into_tensor(self.g_i.view(-1), gi)
+            self.ctx.knn_merge_async(self.g_d, self.g_i, self.world, self.k, self.k, self.m_i, self.m_d,
+                                     self.cnt[1:2])
+
+    def step(self, s):
+        self.knn_step(s % self.windows)
+
+    def algorithmic_bytes(self):
+        return BYTES_PER_POINT * self.n
+
+    def config(self):
+        return {"workload": f"{self.label}, {self.n} uniform points per window per GPU (BASELINE.json configs[1])",
+                "points_per_window_per_gpu": self.n, "grid": self.grid_n, "k": self.k, "radius": self.radius,
+                "windows_resident": self.windows, "final_selection": self.args.knn_final,
+                "parallelism": f"shard{self.world}"}
+
+    def cpu_baseline(self, seconds):
+        cref = _oracle()
+        from spatialflink_amd import synth
+        bj, q = synth.BEIJING, synth.README_QUERY
+        cg = cref.grid(bj[0], bj[2], (bj[1] - bj[0]) / self.grid_n, self.grid_n)
+        n = 2_000_000
+
+        def one(i):
+            x, y = synth.uniform(n, 1000 + i)
+            t0 = time.perf_counter()
+            cref.knn_pp(cg, x, y, q[0], q[1], self.radius, self.k)
+            return time.perf_counter() - t0
+        wins, t = _timed_loop(one, seconds, 30)
+        return {"value": wins * n / t, "unit": "points/sec", "cores": 1, "kind": "port",
+                "sample": f"{wins} windows x {n} uniform points (C2 shape: k={self.k}, {self.grid_n}x{self.grid_n}, "
+                          f"r={self.radius}), oracle/geohip_oracle.c single thread, {t:.1f} s"}
+
+
+class RangeWorkload(Workload):
+    """C1 query shape (BASELINE.json configs[0]: 100x100, README query, r=0.5) at 10M points per
+    GPU (C1's 1M-point window is the reference's CPU case; on the GPU it is launch-bound)."""
+    tag = "range"
+    kernel = "geohip range pass: range_scan + scan_units + range_emit"
+    grid_n, radius, n_default = 100, 0.5, 10_000_000
+
+    def __init__(self, *a):
+        super().__init__(*a)
+        import torch
+        from spatialflink_amd import _abi, synth
+        self.n = self.args.points or self.n_default
+        bj = synth.BEIJING
+        self.q = synth.README_QUERY
+        self.grid = _abi.make_grid(bj[0], bj[2], (bj[1] - bj[0]) / self.grid_n, self.grid_n)
+        self.xs, self.ys = _uniform_windows(self.ctx, self.dev, self.n, self.rank,
+                                            [1 + 7919 * w for w in range(self.windows)], bj)
+        self.out = torch.empty(self.n, dtype=torch.int32, device=self.dev)
+        self.cnt = torch.zeros(self.windows, dtype=torch.int64, device=self.dev)
+        self.counts = torch.zeros(self.world, dtype=torch.int64, device=self.dev)
+        self.hits = None
+
+    def units_per_step(self):
+        return self.n
+
+    def step(self, s):
+        w = s % self.windows
+        self.ctx.range_pp_async(self.grid, self.xs[w], self.ys[w], self.q[0], self.q[1], self.radius, False,
+                                self.out, self.n, self.cnt[w:w + 1])
+        if self.world > 1:  # result gather: every rank learns each shard's hit count (offsets)
+            self.dist.all_gather_into_tensor(self.counts, self.cnt[w:w + 1])
+
+    def algorithmic_bytes(self):
+        if self.hits is None:
+            self.hits = float(self.cnt.double().mean().item())
+        return BYTES_PER_POINT * self.n + 4 * self.hits
+
+    def config(self):
+        return {"workload": f"C1 query shape (point-point range, 100x100 Beijing UniformGrid, README query, r=0.5, "
+                            f"exact) over {self.n} uniform points per window per GPU",
+                "points_per_window_per_gpu": self.n, "grid": self.grid_n, "radius": self.radius,
+                "hits_per_window_per_gpu": self.hits, "windows_resident": self.windows,
+                "parallelism": f"shard{self.world}"}
+
+    def cpu_baseline(self, seconds):
+        cref = _oracle()
+        from spatialflink_amd import synth
+        bj, q = synth.BEIJING, synth.README_QUERY
+        cg = cref.grid(bj[0], bj[2], (bj[1] - bj[0]) / self.grid_n, self.grid_n)
+        n = 1_000_000  # C1's own window size
+
+        def one(i):
+            x, y = synth.uniform(n, 1000 + i)
+            t0 = time.perf_counter()
+            cref.range_pp(cg, x, y, q[0], q[1], self.radius)
+            return time.perf_counter() - t0
+        wins, t = _timed_loop(one, seconds, 60)
+        return {"value": wins * n / t, "unit": "points/sec", "cores": 1, "kind": "port",
+                "sample": f"{wins} windows x {n} uniform points (C1: 100x100, r={self.radius}), "
+                          f"oracle/geohip_oracle.c single thread, {t:.1f} s"}
+
+
+class JoinWorkload(Workload):
+    """C3 (BASELINE.json configs[2]): 10k queries x 10M Gaussian-clustered data points per
+    window, 500x500, r = 0.05 (32 shared centres, sigma 0.1)."""
+    tag = "join_probe"
+    kernel = "geohip::join_probe (after the counting sort bucket_count/scan/bucket_scatter)"
+    grid_n, radius, n_default, nq, sigma = 500, 0.05, 10_000_000, 10_000, 0.1
+    windows = 2
+
+    def __init__(self, *a):
+        super().__init__(*a)
+        import torch
+        from spatialflink_amd import _abi, synth
+        self.n = self.args.points or self.n_default
+        bj = synth.BEIJING
+        self.grid = _abi.make_grid(bj[0], bj[2], (bj[1] - bj[0]) / self.grid_n, self.grid_n)
+        self.dx, self.dy = [], []
+        for w in range(self.windows):
+            hx, hy = synth.gaussian_clusters(self.n, 3 + 100 * w + 7 * self.rank, sigma=self.sigma)
+            self.dx.append(torch.from_numpy(hx).to(self.dev))
+            self.dy.append(torch.from_numpy(hy).to(self.dev))
+        hqx, hqy = synth.gaussian_clusters(self.nq, 4, sigma=self.sigma)  # the query stream, on every rank
+        self.qx = torch.from_numpy(hqx).to(self.dev)
+        self.qy = torch.from_numpy(hqy).to(self.dev)
+        self.pairs = [self.ctx.join_pp_count(self.grid, self.grid, self.dx[w], self.dy[w], self.qx, self.qy,
+                                             self.radius) for w in range(self.windows)]
+        self.out = torch.empty((max(self.pairs) + 1, 2), dtype=torch.int32, device=self.dev)
+        self.counts = torch.zeros(self.world, dtype=torch.int64, device=self.dev)
+
+    def units_per_step(self):
+        return self.n
+
+    def step(self, s):
+        import torch
+        w = s % self.windows
+        self.ctx.join_pp(self.grid, self.grid, self.dx[w], self.dy[w], self.qx, self.qy, self.radius, out=self.out)
+        if self.world > 1:
+            self.dist.all_gather_into_tensor(self.counts, torch.tensor([self.pairs[w]], device=self.dev))
+
+    def algorithmic_bytes(self):
+        return BYTES_PER_POINT * self.n + BYTES_PER_POINT * self.nq + 8 * float(np.mean(self.pairs))
+
+    def config(self):
+        return {"workload": f"C3: point-point join, {self.nq} queries x {self.n} data points per window per GPU, "
+                            f"Gaussian-clustered (32 shared centres, sigma={self.sigma}), {self.grid_n}x{self.grid_n}, "
+                            f"r={self.radius}; units = data points",
+                "points_per_window_per_gpu": self.n, "queries": self.nq, "grid": self.grid_n, "radius": self.radius,
+                "pairs_per_window_per_gpu": float(np.mean(self.pairs)), "windows_resident": self.windows,
+                "parallelism": f"shard{self.world} (data by arrival, queries replicated)"}
+
+    def cpu_baseline(self, seconds):
+        cref = _oracle()
+        from spatialflink_amd import synth
+        bj = synth.BEIJING
+        cg = cref.grid(bj[0], bj[2], (bj[1] - bj[0]) / self.grid_n, self.grid_n)
+        n = 1_000_000  # data slice; all queries (the per-pair work scales with the data slice)
+        qx, qy = synth.gaussian_clusters(self.nq, 4, sigma=self.sigma)
+
+        def one(i):
+            x, y = synth.gaussian_clusters(n, 3000 + i, sigma=self.sigma)
+            t0 = time.perf_counter()
+            cref.join_pp(cg, cg, x, y, qx, qy, self.radius, cap=80_000_000)  # one pass, as the reference
+            return time.perf_counter() - t0
+        wins, t = _timed_loop(one, seconds, 20)
+        return {"value": wins * n / t, "unit": "points/sec", "cores": 1, "kind": "port",
+                "sample": f"{wins} x ({n} Gaussian data points x {self.nq} queries) (C3 shape), "
+                          f"oracle/geohip_oracle.c single thread, {t:.1f} s"}
+
+
+class PpolyWorkload(Workload):
+    """C4 (BASELINE.json configs[3]): 1k star polygons (50 vertices) over 50M uniform points per
+    window, 500x500, r = 0.005 (conf/geoflink-conf.yml:52)."""
+    tag = "ppoly_probe"
+    kernel = "geohip::ppoly_probe (after the counting sort bucket_count/scan/bucket_scatter)"
+    grid_n, radius, n_default, npoly = 500, 0.005, 50_000_000, 1000
+    windows = 2
+
+    def __init__(self, *a):
+        super().__init__(*a)
+        import torch
+        from spatialflink_amd import _abi, synth
+        self.n = self.args.points or self.n_default
+        bj = synth.BEIJING
+        self.grid = _abi.make_grid(bj[0], bj[2], (bj[1] - bj[0]) / self.grid_n, self.grid_n)
+        self.xs, self.ys = _uniform_windows(self.ctx, self.dev, self.n, self.rank,
+                                            [5 + 7919 * w for w in range(self.windows)], bj)
+        self.off, self.vx, self.vy = synth.star_polygons(self.npoly, 6)
+        torch.cuda.synchronize(self.dev)
+        self.hits = [len(self.ctx.range_ppoly(self.grid, self.xs[w], self.ys[w], self.off, self.vx, self.vy,
+                                              self.radius)) for w in range(self.windows)]
+        self.out = torch.empty((max(self.hits) + 1, 2), dtype=torch.int32, device=self.dev)
+
+    def units_per_step(self):
+        return self.n
+
+    def step(self, s):
+        w = s % self.windows
+        self.ctx.range_ppoly(self.grid, self.xs[w], self.ys[w], self.off, self.vx, self.vy, self.radius, out=self.out)
+
+    def algorithmic_bytes(self):
+        return BYTES_PER_POINT * self.n + 16 * len(self.vx) + 8 * float(np.mean(self.hits))
+
+    def config(self):
+        return {"workload": f"C4: point-polygon range, {self.npoly} polygons x 50 vertices over {self.n} uniform "
+                            f"points per window per GPU, {self.grid_n}x{self.grid_n}, r={self.radius}",
+                "points_per_window_per_gpu": self.n, "polygons": self.npoly, "grid": self.grid_n,
+                "radius": self.radius, "hits_per_window_per_gpu": float(np.mean(self.hits)),
+                "windows_resident": self.windows, "parallelism": f"shard{self.world}"}
+
+    def cpu_baseline(self, seconds):
+        cref = _oracle()
+        from spatialflink_amd import synth
+        bj = synth.BEIJING
+        cg = cref.grid(bj[0], bj[2], (bj[1] - bj[0]) / self.grid_n, self.grid_n)
+        n, npoly = 2_000_000, 10  # the reference scans the window once per polygon query
+
+        def one(i):
+            x, y = synth.uniform(n, 5000 + i)
+            sl = slice(10 * i % self.npoly, 10 * i % self.npoly + npoly + 1)
+            off = self.off[sl] - self.off[sl][0]
+            vx = self.vx[self.off[sl][0]:self.off[sl][-1]]
+            vy = self.vy[self.off[sl][0]:self.off[sl][-1]]
+            t0 = time.perf_counter()
+            cref.range_ppoly(cg, x, y, off, vx, vy, self.radius)
+            return time.perf_counter() - t0
+        reps, t = _timed_loop(one, seconds, 50)
+        # point x polygon evaluations per second, expressed as windows of n points x 1k polygons
+        pp_rate = reps * n * npoly / t
+        return {"value": pp_rate / self.npoly, "unit": "points/sec", "cores": 1, "kind": "port",
+                "sample": f"{reps} x ({n} uniform points x {npoly} polygons) (C4 shape), oracle/geohip_oracle.c single "
+                          f"thread, {t:.1f} s; value = point-polygon evaluations/s / {self.npoly} polygons"}
+
+
+class C5Workload(KnnWorkload):
+    """C5 per shard (BASELINE.json configs[4]): 1000x1000 grid, 25M uniform points per GPU
+    (200M per window on 8 GPUs), kNN k=100 + range r=0.05 of the README query."""
+    tag = "knn_scan_c5"
+    kernel = "geohip::knn_scan<2> + range pass"
+    grid_n, k, radius, n_default, seed0 = 1000, 100, 0.05, 25_000_000, 7
+    windows = 2
+    label = "C5 shard: kNN k=100 + range r=0.05, 1000x1000 Beijing UniformGrid, README query"
+
+    def __init__(self, *a):
+        super().__init__(*a)
+        import torch
+        self.rout = torch.empty(self.n, dtype=torch.int32, device=self.dev)
+        self.rcnt = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self.counts = torch.zeros(self.world, dtype=torch.int64, device=self.dev)
+
+    def step(self, s):
+        w = s % self.windows
+        self.knn_step(w)
+        self.ctx.range_pp_async(self.grid, self.xs[w], self.ys[w], self.q[0], self.q[1], self.radius, False,
+                                self.rout, self.n, self.rcnt)
+        if self.world > 1:
+            self.dist.all_gather_into_tensor(self.counts, self.rcnt)
+
+    def algorithmic_bytes(self):  # per timed launch: kNN scan and range pass each read the window once
+        return BYTES_PER_POINT * self.n
+
+    def config(self):
+        c = super().config()
+        c["workload"] = f"{self.label}, {self.n} uniform points per window per GPU (BASELINE.json configs[4])"
+        return c
+
+    def cpu_baseline(self, seconds):
+        return None
+
+
+WORKLOADS = {"knn": KnnWorkload, "range": RangeWorkload, "join": JoinWorkload, "ppoly": PpolyWorkload,
+             "c5": C5Workload}
 
 
 def main():
@@ -105,47 +445,18 @@ def main():
     else:
         torch.cuda.set_device(local)
 
-    from spatialflink_amd import Context, _abi, synth
+    from spatialflink_amd import Context, _abi
 
     dev = torch.device("cuda", local)
     ctx = Context(local)
     _abi.debug_set_knn_fused(args.knn_final == "fused")
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)  # kernels and RCCL ordered on one stream
-    bj = synth.BEIJING
-    q = synth.README_QUERY
-    grid = _abi.make_grid(bj[0], bj[2], (bj[1] - bj[0]) / GRID_N, GRID_N)
-    n = args.points
-
-    xs, ys = [], []
-    for w in range(WINDOWS):
-        x = torch.empty(n, dtype=torch.float64, device=dev)
-        y = torch.empty(n, dtype=torch.float64, device=dev)
-        # window w of rank r = slice [r*n, (r+1)*n) of the N*n-point window w
-        ctx.synth_uniform_async(x, y, rank * n, 2 + 7919 * w, bj)
-        xs.append(x)
-        ys.append(y)
-    out_i = torch.empty(K, dtype=torch.int32, device=dev)
-    out_d = torch.empty(K, dtype=torch.float64, device=dev)
-    cnt = torch.zeros(2, dtype=torch.int32, device=dev)
-    g_d = torch.empty((world, K), dtype=torch.float64, device=dev)
-    g_i = torch.empty((world, K), dtype=torch.int32, device=dev)
-    m_i = torch.empty(K, dtype=torch.int32, device=dev)
-    m_d = torch.empty(K, dtype=torch.float64, device=dev)
-    base = torch.tensor(rank * n, dtype=torch.int64, device=dev)
-
-    def step(s):
-        w = s % WINDOWS
-        ctx.knn_pp_async(grid, xs[w], ys[w], q[0], q[1], RADIUS, K, out_i, out_d, cnt[0:1])
-        if world > 1:
-            gi = torch.where(out_i >= 0, (out_i.to(torch.int64) + base).to(torch.int32), out_i)
-            dist.all_gather_into_tensor(g_d.view(-1), out_d)
-            dist.all_gather_into_tensor(g_i.view(-1), gi)
-            ctx.knn_merge_async(g_d, g_i, world, K, K, m_i, m_d, cnt[1:2])
+    wl = WORKLOADS[args.workload](args, ctx, dev, rank, world, dist)
 
     torch.cuda.synchronize(dev)
     for s in range(args.warmup):
-        step(s)
+        wl.step(s)
     torch.cuda.synchronize(dev)
     ctx.timing(reset=True)
     ctx.set_timing(True)
@@ -154,22 +465,23 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for s in range(args.steps):
-        step(args.warmup + s)
+        wl.step(args.warmup + s)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ctx.set_timing(False)
-    scan_ms, launches = ctx.timing(reset=True)
+    kern_ms, launches = ctx.timing(reset=True)
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    total_points = n * world * args.steps
+    total_points = wl.units_per_step() * world * args.steps
     value = total_points / elapsed
-    avg_scan_s = scan_ms / 1e3 / max(launches, 1)
-    achieved = BYTES_PER_POINT * n / avg_scan_s / 1e9
+    avg_s = kern_ms / 1e3 / max(launches, 1)
+    abytes = wl.algorithmic_bytes()
+    achieved = abytes / avg_s / 1e9 if avg_s > 0 else 0.0
     result = {
         "metric": METRIC,
         "value": value,
@@ -183,19 +495,15 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
-        "config": {"workload": "C2: point-point kNN k=50, 100x100 Beijing UniformGrid, r=0.5, README query, "
-                               f"{n} uniform points per window per GPU (BASELINE.json configs[1])",
-                   "points_per_window_per_gpu": n, "grid": GRID_N, "k": K, "radius": RADIUS,
-                   "windows_resident": WINDOWS, "final_selection": args.knn_final,
-                   "parallelism": f"shard{world}"},
+        "config": wl.config(),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(),
-                     "kernel": "geohip::knn_scan<1>", "avg_kernel_us": avg_scan_s * 1e6,
-                     "algorithmic_bytes_per_launch": BYTES_PER_POINT * n},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(wl.tag),
+                     "kernel": wl.kernel, "avg_kernel_us": avg_s * 1e6, "timed_launches": launches,
+                     "algorithmic_bytes_per_launch": abytes, **wl.roofline_extra()},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        result["cpu_baseline"] = wl.cpu_baseline(args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:

@@ -309,17 +309,21 @@ class Context:
                                        int(approximate), _ptr(out_idx), cap, _ptr(out_count))
         self._check(rc, "range_pp_async")
 
-    def join_pp(self, grid_data: Grid, grid_query: Grid, dx, dy, qx, qy, r, approximate=False, cap=None):
+    def join_pp(self, grid_data: Grid, grid_query: Grid, dx, dy, qx, qy, r, approximate=False, cap=None, out=None):
+        """Pairs (data idx, query idx).  ``out`` (optional): a preallocated [cap, 2] u32/i32 buffer on
+        the same side as the inputs (one pass, no count-only pass)."""
         dx, dy, qx, qy = _f64(dx), _f64(dy), _f64(qx), _f64(qy)
         dev = self._mem_for(dx, dy, qx, qy)
         cnt = c_uint64(0)
-        if cap is None:
+        if cap is None and out is None:
             rc = lib.geohip_join_pp_count_only(self.h, ctypes.byref(grid_data), ctypes.byref(grid_query), _ptr(dx),
                                                _ptr(dy), len(dx), _ptr(qx), _ptr(qy), len(qx), r, int(approximate),
                                                ctypes.byref(cnt))
             self._check(rc, "join_pp_count_only")
             cap = cnt.value
-        if dev:
+        if out is not None:
+            cap = len(out) if cap is None else min(cap, len(out))
+        elif dev:
             import torch
             out = torch.empty((max(cap, 1), 2), dtype=torch.int32, device=dx.device)
         else:
@@ -340,7 +344,8 @@ class Context:
         self._check(rc, "join_pp_count_only")
         return cnt.value
 
-    def range_ppoly(self, grid: Grid, x, y, ring_off, vx, vy, r, approximate=False, cap=None):
+    def range_ppoly(self, grid: Grid, x, y, ring_off, vx, vy, r, approximate=False, cap=None, out=None):
+        """Pairs (polygon idx, point idx).  ``out``: optional preallocated [cap, 2] buffer."""
         x, y = _f64(x), _f64(y)
         self._mem_for(x, y)
         ring_off = np.ascontiguousarray(ring_off, dtype=np.uint32)
@@ -348,13 +353,17 @@ class Context:
         vy = np.ascontiguousarray(vy, dtype=np.float64)
         npoly = len(ring_off) - 1
         cnt = c_uint64(0)
+        if out is not None:
+            cap = len(out) if cap is None else min(cap, len(out))
         if cap is None:
             rc = lib.geohip_range_ppoly(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), len(x), _ptr(ring_off),
                                         _ptr(vx), _ptr(vy), npoly, r, int(approximate), None, 0, ctypes.byref(cnt))
             if rc not in (OK, ERR_CAPACITY):
                 self._check(rc, "range_ppoly")
             cap = cnt.value
-        if _is_device(x):
+        if out is not None:
+            pass
+        elif _is_device(x):
             import torch
             out = torch.empty((max(cap, 1), 2), dtype=torch.int32, device=x.device)
         else:

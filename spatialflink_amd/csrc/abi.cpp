@@ -25,6 +25,7 @@ enum Slot {
     S_X, S_Y, S_QX, S_QY, S_GTHR, S_PART_D, S_PART_I, S_OUT_D, S_OUT_I, S_OUT_CNT,
     S_MASK, S_UCNT, S_OFFS, S_TOTAL, S_OUT_IDX, S_OUT_PAIRS, S_SPILL_D, S_SPILL_I, S_SPILL_CNT,
     S_J0, S_J1, S_J2, S_J3, S_J4, S_J5, S_J6, S_J7, S_J8, S_J9, S_J10, S_J11, S_J12, S_J13, S_J14, S_J15,
+    S_J16, S_J17, S_J18, S_J19,
     S_COUNT
 };
 
@@ -236,9 +237,7 @@ int range_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x, con
     a.qy = qy;
     a.r = r;
     // squared screens for the candidate cells (see device_common.h): a 2^-40 margin
-    const double r2 = r * r;
-    a.r2lo = (r >= 0.0) ? r2 * (1.0 - 0x1.0p-40) : -1.0;
-    a.r2hi = r2 * (1.0 + 0x1.0p-40);
+    pp_screen_bounds(r, &a.r2lo, &a.r2hi);
     const double *dx, *dy;
     rc = stage_xy(ctx, x, y, n, S_X, S_Y, &dx, &dy);
     if (rc) return rc;

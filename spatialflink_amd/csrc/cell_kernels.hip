@@ -1,18 +1,26 @@
-// cell_kernels.hip -- cell-bucketed kernels of libgeohip for gfx950: point-point window join
+// cell_kernels.hip -- tile-binned kernels of libgeohip for gfx950: point-point window join
 // (PointPointJoinQuery.java:113-172 + JoinQuery.java:73-90) and point-polygon window range
 // (PointPolygonRangeQuery.java:76-124).
 //
-// Both bucket the window's points by grid cell with a counting sort (per-cell histogram by
-// atomics, exclusive scan, scatter into SoA x/y/idx/cell), so a query reads only the
-// contiguous point ranges of its cell columns (x-major keys: one column of a cell rectangle
-// is one contiguous range).  One workgroup per query walks the concatenated ranges in
-// 256-point tiles, computes the exact JTS distance (fdlibm hypot / point-polygon), compacts
-// hits into an LDS pair buffer and flushes it with one global atomic per 8K pairs.
+// Both start from one binning pass of the window's points into square tiles of ts x ts grid
+// cells (x-major tiles, at most 128 x 128 of them): a per-block LDS histogram (no per-point
+// global atomics), a column-wise scan of the block histograms into per-(block, tile) offsets,
+// and an LDS-cursor scatter into SoA x / y / idx / cell key.  Within a tile the points are in
+// no particular order; the kernels test the exact cell of every point, so the tile is only a
+// locality unit.
+//
+// Join: the query stream's replication (JoinQuery.getReplicatedPointQueryStream: every query
+// copied to each cell of its Nbr block) becomes a tile -> query list; one workgroup per data
+// tile stages its candidate queries in LDS and streams the tile's points once against them.
+// Point-polygon: one workgroup per (polygon, tile) work item, ring in LDS, exactness-preserving
+// screens before the JTS distance.  Pairs leave through per-wave LDS buffers, one global atomic
+// per ~1K pairs.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <string>
 #include <vector>
 
@@ -22,9 +30,11 @@
 
 namespace geohip {
 
-constexpr int kTB = 256;           // threads per block
-constexpr int kPairBuf = 8192;     // LDS pair buffer (64 KB)
-constexpr unsigned kNoCell = 0xffffffffu;
+constexpr int kTB = 256;             // threads per block (probe kernels, scans)
+constexpr int kBinThreads = 1024;    // binning kernels
+constexpr unsigned kMaxTiles = 16384;
+constexpr int kWavePairs = 1024;     // per-wave LDS pair buffer (8 KB)
+constexpr unsigned kGlobalTiles = 4096;  // queries touching more tiles go to every tile's list
 
 __device__ __forceinline__ int32_t d_java_d2i(double v) {
     if (v != v) return 0;
@@ -38,64 +48,49 @@ __device__ __forceinline__ int32_t d_axis_cell(double v, double mn, double l) {
     return d_java_d2i(__builtin_floor((v - mn) / l));
 }
 
-// ------------------------------------------------------------------ bucketing -------------
-// key = cx * nb + cy for 0 <= cx, cy < nb, else kNoCell.
-__global__ void bucket_count(const double* __restrict__ x, const double* __restrict__ y, uint64_t n, double mnx,
-                             double mny, double l, int32_t nb, unsigned* __restrict__ key,
-                             unsigned* __restrict__ count, unsigned* __restrict__ outside) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const int32_t cx = d_axis_cell(x[i], mnx, l);
-        const int32_t cy = d_axis_cell(y[i], mny, l);
-        unsigned k = kNoCell;
-        if (cx >= 0 && cy >= 0 && cx < nb && cy < nb) {
-            k = (unsigned)cx * (unsigned)nb + (unsigned)cy;
-            atomicAdd(&count[k], 1u);
-        } else {
-            atomicAdd(outside, 1u);
-        }
-        key[i] = k;
-    }
-}
-
+// ------------------------------------------------------------------ scans ----------------
 // exclusive scan, 3 phases: per-block totals, scan of totals, per-block rescan + offset
 constexpr int kScanPer = 16;
 constexpr int kScanSeg = kTB * kScanPer;
 
-__device__ __forceinline__ unsigned block_excl_scan(unsigned v, unsigned* sh, unsigned* total) {
+template <typename T>
+__device__ __forceinline__ T block_excl_scan(T v, T* sh, T* total) {
     const int t = threadIdx.x;
     sh[t] = v;
     __syncthreads();
     for (int o = 1; o < kTB; o <<= 1) {
-        unsigned a = t >= o ? sh[t - o] : 0u;
+        T a = t >= o ? sh[t - o] : T(0);
         __syncthreads();
         sh[t] += a;
         __syncthreads();
     }
-    const unsigned incl = sh[t];
+    const T incl = sh[t];
     *total = sh[kTB - 1];
     __syncthreads();
     return incl - v;
 }
 
-__global__ void scan_seg_totals(const unsigned* __restrict__ in, uint64_t n, unsigned* __restrict__ seg_tot) {
-    __shared__ unsigned sh[kTB];
+template <typename T>
+__global__ void scan_seg_totals(const T* __restrict__ in, uint64_t n, T* __restrict__ seg_tot) {
+    __shared__ T sh[kTB];
     const uint64_t base = (uint64_t)blockIdx.x * kScanSeg + (uint64_t)threadIdx.x * kScanPer;
-    unsigned s = 0;
+    T s = 0;
     for (int j = 0; j < kScanPer; j++)
         if (base + j < n) s += in[base + j];
-    unsigned tot;
+    T tot;
     block_excl_scan(s, sh, &tot);
     if (threadIdx.x == 0) seg_tot[blockIdx.x] = tot;
 }
 
-__global__ void scan_totals(unsigned* __restrict__ seg_tot, uint64_t nseg, unsigned* __restrict__ grand) {
-    __shared__ unsigned sh[kTB];
-    unsigned carry = 0;
+template <typename T>
+__global__ void scan_totals(T* __restrict__ seg_tot, uint64_t nseg, T* __restrict__ grand) {
+    __shared__ T sh[kTB];
+    T carry = 0;
     for (uint64_t b = 0; b < nseg; b += kTB) {
         const uint64_t i = b + threadIdx.x;
-        const unsigned v = i < nseg ? seg_tot[i] : 0u;
-        unsigned tot;
-        const unsigned ex = block_excl_scan(v, sh, &tot);
+        const T v = i < nseg ? seg_tot[i] : T(0);
+        T tot;
+        const T ex = block_excl_scan(v, sh, &tot);
         if (i < nseg) seg_tot[i] = carry + ex;
         carry += tot;
     }
@@ -103,18 +98,19 @@ __global__ void scan_totals(unsigned* __restrict__ seg_tot, uint64_t nseg, unsig
 }
 
 // out[i] = sum(in[0..i)); out[n] = total
-__global__ void scan_apply(const unsigned* __restrict__ in, uint64_t n, const unsigned* __restrict__ seg_off,
-                           const unsigned* __restrict__ grand, unsigned* __restrict__ out) {
-    __shared__ unsigned sh[kTB];
+template <typename T>
+__global__ void scan_apply(const T* __restrict__ in, uint64_t n, const T* __restrict__ seg_off,
+                           const T* __restrict__ grand, T* __restrict__ out) {
+    __shared__ T sh[kTB];
     const uint64_t base = (uint64_t)blockIdx.x * kScanSeg + (uint64_t)threadIdx.x * kScanPer;
-    unsigned v[kScanPer];
-    unsigned s = 0;
+    T v[kScanPer];
+    T s = 0;
     for (int j = 0; j < kScanPer; j++) {
-        v[j] = base + j < n ? in[base + j] : 0u;
+        v[j] = base + j < n ? in[base + j] : T(0);
         s += v[j];
     }
-    unsigned tot;
-    unsigned run = seg_off[blockIdx.x] + block_excl_scan(s, sh, &tot);
+    T tot;
+    T run = seg_off[blockIdx.x] + block_excl_scan(s, sh, &tot);
     for (int j = 0; j < kScanPer; j++) {
         if (base + j < n) out[base + j] = run;
         run += v[j];
@@ -122,172 +118,278 @@ __global__ void scan_apply(const unsigned* __restrict__ in, uint64_t n, const un
     if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = *grand;
 }
 
-__global__ void bucket_scatter(const double* __restrict__ x, const double* __restrict__ y, uint64_t n,
-                               const unsigned* __restrict__ key, const unsigned* __restrict__ start,
-                               unsigned* __restrict__ cursor, double* __restrict__ sx, double* __restrict__ sy,
-                               unsigned* __restrict__ sidx, unsigned* __restrict__ skey,
-                               unsigned* __restrict__ outside_idx, unsigned* __restrict__ outside_cnt) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const unsigned k = key[i];
-        if (k != kNoCell) {
-            const unsigned pos = start[k] + atomicAdd(&cursor[k], 1u);
-            sx[pos] = x[i];
-            sy[pos] = y[i];
+// ------------------------------------------------------------------ tile binning ---------
+struct TileGeom {
+    double mnx, mny, l;  // grid the point cells are computed on
+    int32_t nb;          // key space: cells [0, nb)^2 (the query grid's n for the join)
+    int32_t ts;          // cells per tile side
+    int32_t nt;          // tiles per side
+    uint32_t ntiles;     // nt * nt <= kMaxTiles
+};
+
+__device__ __forceinline__ bool point_cell(const TileGeom& g, double x, double y, int32_t& cx, int32_t& cy) {
+    cx = d_axis_cell(x, g.mnx, g.l);
+    cy = d_axis_cell(y, g.mny, g.l);
+    return cx >= 0 && cy >= 0 && cx < g.nb && cy < g.nb;
+}
+__device__ __forceinline__ unsigned tile_of(const TileGeom& g, int32_t cx, int32_t cy) {
+    return (unsigned)(cx / g.ts) * (unsigned)g.nt + (unsigned)(cy / g.ts);
+}
+
+// per-block tile histogram of a contiguous chunk of points -> hist[block][tile]
+__global__ __launch_bounds__(kBinThreads) void tbin_count(const double* __restrict__ x, const double* __restrict__ y,
+                                                          uint64_t n, uint64_t chunk, TileGeom g,
+                                                          unsigned* __restrict__ hist, unsigned* __restrict__ nout) {
+    __shared__ unsigned h[kMaxTiles];
+    for (unsigned t = threadIdx.x; t < g.ntiles; t += kBinThreads) h[t] = 0;
+    __syncthreads();
+    const uint64_t b0 = (uint64_t)blockIdx.x * chunk;
+    const uint64_t b1 = b0 + chunk < n ? b0 + chunk : n;
+    unsigned outside = 0;
+    for (uint64_t i = b0 + threadIdx.x; i < b1; i += kBinThreads) {
+        int32_t cx, cy;
+        if (point_cell(g, x[i], y[i], cx, cy)) atomicAdd(&h[tile_of(g, cx, cy)], 1u);
+        else outside++;
+    }
+    if (outside) atomicAdd(nout, outside);
+    __syncthreads();
+    unsigned* row = hist + (size_t)blockIdx.x * g.ntiles;
+    for (unsigned t = threadIdx.x; t < g.ntiles; t += kBinThreads) row[t] = h[t];
+}
+
+// tot[t] = sum over blocks of hist[b][t]
+__global__ void tbin_totals(const unsigned* __restrict__ hist, unsigned nblk, uint32_t ntiles, unsigned* __restrict__ tot) {
+    const unsigned t = blockIdx.x * kTB + threadIdx.x;
+    if (t >= ntiles) return;
+    unsigned s = 0;
+    for (unsigned b = 0; b < nblk; b++) s += hist[(size_t)b * ntiles + t];
+    tot[t] = s;
+}
+
+// hist[b][t] <- start[t] + sum_{b' < b} hist[b'][t]  (where block b writes its tile-t points)
+__global__ void tbin_offsets(unsigned* __restrict__ hist, unsigned nblk, uint32_t ntiles,
+                             const unsigned* __restrict__ start) {
+    const unsigned t = blockIdx.x * kTB + threadIdx.x;
+    if (t >= ntiles) return;
+    unsigned run = start[t];
+    for (unsigned b = 0; b < nblk; b++) {
+        const unsigned v = hist[(size_t)b * ntiles + t];
+        hist[(size_t)b * ntiles + t] = run;
+        run += v;
+    }
+}
+
+__global__ __launch_bounds__(kBinThreads) void tbin_scatter(const double* __restrict__ x, const double* __restrict__ y,
+                                                            uint64_t n, uint64_t chunk, TileGeom g,
+                                                            const unsigned* __restrict__ offs, double* __restrict__ sx,
+                                                            double* __restrict__ sy, unsigned* __restrict__ sidx,
+                                                            unsigned* __restrict__ skey,
+                                                            unsigned* __restrict__ outside_idx,
+                                                            unsigned* __restrict__ outside_cur) {
+    __shared__ unsigned cur[kMaxTiles];
+    const unsigned* row = offs + (size_t)blockIdx.x * g.ntiles;
+    for (unsigned t = threadIdx.x; t < g.ntiles; t += kBinThreads) cur[t] = row[t];
+    __syncthreads();
+    const uint64_t b0 = (uint64_t)blockIdx.x * chunk;
+    const uint64_t b1 = b0 + chunk < n ? b0 + chunk : n;
+    for (uint64_t i = b0 + threadIdx.x; i < b1; i += kBinThreads) {
+        const double px = x[i], py = y[i];
+        int32_t cx, cy;
+        if (point_cell(g, px, py, cx, cy)) {
+            const unsigned pos = atomicAdd(&cur[tile_of(g, cx, cy)], 1u);
+            sx[pos] = px;
+            sy[pos] = py;
             sidx[pos] = (unsigned)i;
-            if (skey) skey[pos] = k;
+            skey[pos] = (unsigned)cx * (unsigned)g.nb + (unsigned)cy;
         } else if (outside_idx) {
-            outside_idx[atomicAdd(outside_cnt, 1u)] = (unsigned)i;
+            outside_idx[atomicAdd(outside_cur, 1u)] = (unsigned)i;
         }
     }
 }
 
-struct Bucketed {
+struct TileBins {
     const double* sx;
     const double* sy;
     const unsigned* sidx;
     const unsigned* skey;
-    const unsigned* start;  // nb*nb + 1
-    const unsigned* outside_idx;
-    unsigned n_outside;
+    const unsigned* start;  // ntiles + 1
     int32_t nb;
 };
 
-// ------------------------------------------------------------------ pair buffer ----------
-struct PairBuf {
-    unsigned a[kPairBuf];
-    unsigned b[kPairBuf];
-    unsigned cnt;
-    unsigned long long base;
+// ------------------------------------------------------------------ pair output ----------
+// Two passes, no contended counter: the count pass stores each block's pair count in
+// bcount[slot0 + block]; an exclusive scan turns the counts into offsets boff; the write pass
+// places a block's pairs at boff[slot] + a block-local (LDS) cursor.  Waves collect pairs in
+// LDS buffers and copy them out coalesced.
+struct PairSink {
+    unsigned long long* bcount;       // count pass: pairs per block slot
+    const unsigned long long* boff;   // write pass: first output pair of each block slot
+    unsigned slot0;                   // slot of block 0 of this launch
+    unsigned* out;                    // write pass: pairs, u32 x 2
+    uint64_t cap;                     // pairs at or beyond cap are dropped (size reported by the scan)
+    int aligned8;                     // out is 8-byte aligned: one 8-byte store per pair
 };
 
-__device__ __forceinline__ void pairbuf_push(PairBuf& pb, bool hit, unsigned a, unsigned b) {
-    const unsigned long long m = __ballot(hit);
-    unsigned wbase = 0;
-    if (lane_id() == 0 && m) wbase = atomicAdd(&pb.cnt, (unsigned)__popcll(m));
-    wbase = __shfl(wbase, 0);
-    if (hit) {
-        const unsigned pos = wbase + lanes_below(m);
-        pb.a[pos] = a;
-        pb.b[pos] = b;
+template <bool WRITE>
+__device__ __forceinline__ void pairs_flush(uint2* buf, unsigned long long& cnt, unsigned long long* bsh,
+                                            const PairSink& s) {
+    if (!WRITE || cnt == 0) return;
+    wave_lds_sync();
+    unsigned lo = 0, hi = 0;
+    if (lane_id() == 0) {
+        const unsigned long long b = s.boff[s.slot0 + blockIdx.x] + atomicAdd(bsh, cnt);
+        lo = (unsigned)b;
+        hi = (unsigned)(b >> 32);
     }
-}
-
-// all threads: write the buffer to out at a globally reserved offset, reset it
-__device__ __forceinline__ void pairbuf_flush(PairBuf& pb, unsigned long long* total, unsigned* out, uint64_t cap) {
-    __syncthreads();
-    const unsigned c = pb.cnt;
-    if (c) {
-        if (threadIdx.x == 0) pb.base = atomicAdd(total, (unsigned long long)c);
-        __syncthreads();
-        const unsigned long long base = pb.base;
-        if (out) {
-            for (unsigned t = threadIdx.x; t < c; t += blockDim.x) {
-                const unsigned long long p = base + t;
-                if (p < cap) {
-                    out[2 * p] = pb.a[t];
-                    out[2 * p + 1] = pb.b[t];
-                }
-            }
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) pb.cnt = 0;
-    }
-    __syncthreads();
-}
-
-// Walk the concatenated point ranges of columns x0..x1 (rows y0..y1) of one query in
-// 256-point tiles: fn(sorted position) on every point, then tile_end() (block-uniform).
-struct ColWalk {
-    unsigned colpref[kTB + 1];
-    unsigned colbeg[kTB];
-};
-
-template <typename F, typename E>
-__device__ __forceinline__ void walk_columns(ColWalk& cw, const unsigned* __restrict__ start, int32_t nb, int32_t x0,
-                                             int32_t x1, int32_t y0, int32_t y1, F fn, E tile_end) {
-    for (int32_t cb = x0; cb <= x1; cb += kTB) {
-        const int32_t ncol = min(kTB, x1 - cb + 1);
-        unsigned len = 0, beg = 0;
-        if ((int)threadIdx.x < ncol) {
-            const uint64_t c = (uint64_t)(cb + threadIdx.x) * (uint64_t)nb;
-            beg = start[c + y0];
-            len = start[c + y1 + 1] - beg;
-        }
-        __shared__ unsigned scan_sh[kTB];
-        unsigned tot;
-        const unsigned ex = block_excl_scan(len, scan_sh, &tot);
-        if ((int)threadIdx.x < ncol) {
-            cw.colpref[threadIdx.x] = ex;
-            cw.colbeg[threadIdx.x] = beg;
-        }
-        if (threadIdx.x == 0) cw.colpref[ncol] = tot;
-        __syncthreads();
-        for (unsigned t0 = 0; t0 < tot; t0 += kTB) {
-            const unsigned v = t0 + threadIdx.x;
-            if (v < tot) {
-                int lo = 0, hi = ncol - 1;  // last column with colpref <= v
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (cw.colpref[mid] <= v) lo = mid; else hi = mid - 1;
-                }
-                fn(cw.colbeg[lo] + (v - cw.colpref[lo]));
+    const unsigned long long base = ((unsigned long long)__shfl(hi, 0) << 32) | __shfl(lo, 0);
+    for (unsigned t = lane_id(); t < (unsigned)cnt; t += kWave) {
+        const unsigned long long p = base + t;
+        if (p < s.cap) {
+            const uint2 v = buf[t];
+            if (s.aligned8) {
+                reinterpret_cast<uint2*>(s.out)[p] = v;
             } else {
-                fn(0xffffffffu);
+                s.out[2 * p] = v.x;
+                s.out[2 * p + 1] = v.y;
             }
-            tile_end();
         }
-        __syncthreads();
     }
+    wave_lds_sync();
+    cnt = 0;
+}
+
+template <bool WRITE, int CAP>
+__device__ __forceinline__ void pairs_push(uint2* buf, unsigned long long& cnt, bool hit, unsigned a, unsigned b,
+                                           unsigned long long* bsh, const PairSink& s) {
+    const unsigned long long m = __ballot(hit);
+    if (!WRITE) {
+        cnt += (unsigned long long)__popcll(m);
+        return;
+    }
+    if (m == 0) return;
+    if (hit) buf[cnt + lanes_below(m)] = make_uint2(a, b);
+    cnt += (unsigned long long)__popcll(m);
+    if (cnt > (unsigned long long)(CAP - kWave)) pairs_flush<WRITE>(buf, cnt, bsh, s);
+}
+
+// every thread of the block: final flush (write) or the block's count (count)
+template <bool WRITE>
+__device__ __forceinline__ void pairs_end(uint2* buf, unsigned long long& cnt, unsigned long long* bsh,
+                                          const PairSink& s) {
+    if (WRITE) pairs_flush<WRITE>(buf, cnt, bsh, s);
+    else if (lane_id() == 0 && cnt) atomicAdd(bsh, cnt);
+    __syncthreads();
+    if (!WRITE && threadIdx.x == 0) s.bcount[s.slot0 + blockIdx.x] = *bsh;
 }
 
 // ------------------------------------------------------------------ join -----------------
 struct QRect {
-    int32_t x0, x1, y0, y1;  // bucket space, clipped; x0 > x1 = empty
+    int32_t x0, x1, y0, y1;  // key space, clipped; x0 > x1 = empty
 };
 
-template <bool COUNT_ONLY, bool APPROX>
-__global__ __launch_bounds__(kTB) void join_probe(Bucketed bk, const double* __restrict__ qx,
-                                                  const double* __restrict__ qy, const QRect* __restrict__ rect,
-                                                  uint64_t nq, double r, unsigned long long* __restrict__ total,
-                                                  unsigned* __restrict__ out, uint64_t cap) {
-    __shared__ PairBuf pb;
-    __shared__ ColWalk cw;
-    __shared__ unsigned long long bcount;
-    if (threadIdx.x == 0) { pb.cnt = 0; bcount = 0; }
-    __syncthreads();
-    for (uint64_t q = blockIdx.x; q < nq; q += gridDim.x) {
-        const QRect R = rect[q];
-        if (R.x0 > R.x1 || R.y0 > R.y1) continue;
-        const double px = qx[q], py = qy[q];
-        unsigned my = 0;
-        walk_columns(
-            cw, bk.start, bk.nb, R.x0, R.x1, R.y0, R.y1,
-            [&](unsigned pos) {
-                bool hit = false;
-                unsigned pid = 0;
-                if (pos != 0xffffffffu) {
-                    const double dx = bk.sx[pos], dy = bk.sy[pos];
-                    pid = bk.sidx[pos];
-                    // getDistance(p, q): p.point.distance(q.point)
-                    hit = APPROX || jts_pp_distance(dx, dy, px, py) <= r;
-                }
-                if (COUNT_ONLY) my += hit ? 1u : 0u;
-                else pairbuf_push(pb, hit, pid, (unsigned)q);
-            },
-            [&]() {
-                if (!COUNT_ONLY) {
-                    __syncthreads();
-                    if (pb.cnt > kPairBuf - kTB) pairbuf_flush(pb, total, out, cap);
-                }
-            });
-        if (COUNT_ONLY && my) atomicAdd(&bcount, (unsigned long long)my);
+__device__ __forceinline__ bool rect_tiles(const QRect& R, const TileGeom& g, int32_t& tx0, int32_t& tx1, int32_t& ty0,
+                                           int32_t& ty1) {
+    if (R.x0 > R.x1 || R.y0 > R.y1) return false;
+    tx0 = R.x0 / g.ts;
+    tx1 = R.x1 / g.ts;
+    ty0 = R.y0 / g.ts;
+    ty1 = R.y1 / g.ts;
+    return true;
+}
+
+// Query replication as a tile -> query list.  FILL = 0: count per tile (and collect the
+// queries whose block spans more than kGlobalTiles tiles into glist); FILL = 1: write lists.
+template <bool FILL>
+__global__ void jq_build(const QRect* __restrict__ rect, uint64_t nq, TileGeom g, unsigned* __restrict__ tcnt,
+                         const unsigned* __restrict__ qstart, unsigned* __restrict__ qlist,
+                         unsigned* __restrict__ glist, unsigned* __restrict__ gcnt) {
+    const uint64_t q = (uint64_t)blockIdx.x * kTB + threadIdx.x;
+    if (q >= nq) return;
+    int32_t tx0, tx1, ty0, ty1;
+    if (!rect_tiles(rect[q], g, tx0, tx1, ty0, ty1)) return;
+    const uint64_t ntl = (uint64_t)(tx1 - tx0 + 1) * (uint64_t)(ty1 - ty0 + 1);
+    if (ntl > kGlobalTiles) {
+        if (!FILL) glist[atomicAdd(gcnt, 1u)] = (unsigned)q;
+        return;
     }
-    if (COUNT_ONLY) {
+    for (int32_t a = tx0; a <= tx1; a++)
+        for (int32_t b = ty0; b <= ty1; b++) {
+            const unsigned t = (unsigned)a * (unsigned)g.nt + (unsigned)b;
+            const unsigned k = atomicAdd(&tcnt[t], 1u);
+            if (FILL) qlist[qstart[t] + k] = (unsigned)q;
+        }
+}
+
+// One workgroup per data tile: candidate queries (the tile's list + the global list) staged in
+// LDS 256 at a time; every wave streams 64 of the tile's points per pass against all of them.
+// Emit (p, q) iff key(p) lies in q's Nbr block and (approximate or dist(p, q) <= r)
+// (PointPointJoinQuery.java:156-160): squared screens first, the exact JTS distance in the band.
+// WRITE = false: count pass (pairs per tile into sink.bcount); true: write pass.
+template <bool APPROX, bool WRITE>
+__global__ __launch_bounds__(kTB) void join_tile(TileBins tb, const unsigned* __restrict__ qstart,
+                                                 const unsigned* __restrict__ qlist,
+                                                 const unsigned* __restrict__ glist, const unsigned* __restrict__ gcnt,
+                                                 const double* __restrict__ qx, const double* __restrict__ qy,
+                                                 const QRect* __restrict__ rect, double r, double r2lo, double r2hi,
+                                                 PairSink sink) {
+    __shared__ double lqx[kTB], lqy[kTB];
+    __shared__ QRect lrect[kTB];
+    __shared__ unsigned lqi[kTB];
+    __shared__ uint2 pbuf[WRITE ? kTB / kWave : 1][WRITE ? kWavePairs : 1];
+    __shared__ unsigned long long bsh;
+    const unsigned tile = blockIdx.x;
+    const unsigned ds = tb.start[tile], de = tb.start[tile + 1];
+    const unsigned qs = qstart[tile], nql = qstart[tile + 1] - qs;
+    const unsigned nqt = nql + *gcnt;
+    if (ds == de || nqt == 0) return;  // block-uniform (bcount is zeroed by the host)
+    const int wid = threadIdx.x / kWave, lane = lane_id();
+    uint2* buf = pbuf[WRITE ? wid : 0];
+    unsigned long long cnt = 0;
+    if (threadIdx.x == 0) bsh = 0;
+    const unsigned nb = (unsigned)tb.nb;
+    for (unsigned qb = 0; qb < nqt; qb += kTB) {
         __syncthreads();
-        if (threadIdx.x == 0 && bcount) atomicAdd(total, bcount);
-    } else {
-        pairbuf_flush(pb, total, out, cap);
+        const unsigned t = qb + threadIdx.x;
+        if (t < nqt) {
+            const unsigned q = t < nql ? qlist[qs + t] : glist[t - nql];
+            lqx[threadIdx.x] = qx[q];
+            lqy[threadIdx.x] = qy[q];
+            lrect[threadIdx.x] = rect[q];
+            lqi[threadIdx.x] = q;
+        }
+        __syncthreads();
+        const unsigned nbq = nqt - qb < (unsigned)kTB ? nqt - qb : (unsigned)kTB;
+        for (unsigned base = ds + wid * kWave; base < de; base += kTB) {
+            const unsigned i = base + lane;
+            const bool valid = i < de;
+            double px = 0.0, py = 0.0;
+            unsigned pid = 0;
+            int32_t cx = -1, cy = -1;
+            if (valid) {
+                px = tb.sx[i];
+                py = tb.sy[i];
+                pid = tb.sidx[i];
+                const unsigned key = tb.skey[i];
+                cx = (int32_t)(key / nb);
+                cy = (int32_t)(key - (unsigned)cx * nb);
+            }
+            for (unsigned j = 0; j < nbq; j++) {
+                const QRect R = lrect[j];
+                bool hit = cx >= R.x0 && cx <= R.x1 && cy >= R.y0 && cy <= R.y1;
+                if (!APPROX && hit) {
+                    const double ox = lqx[j], oy = lqy[j];
+                    const double dx = px - ox, dy = py - oy;
+                    const double d2 = dx * dx + dy * dy;
+                    if (!(d2 <= r2lo)) {
+                        if (d2 > r2hi) hit = false;
+                        else hit = jts_pp_distance(px, py, ox, oy) <= r;  // getDistance(p, q)
+                    }
+                }
+                pairs_push<WRITE, kWavePairs>(buf, cnt, hit, pid, lqi[j], &bsh, sink);
+            }
+        }
     }
+    pairs_end<WRITE>(buf, cnt, &bsh, sink);
 }
 
 // ------------------------------------------------------------------ point-polygon --------
@@ -331,55 +433,137 @@ struct PolyDev {
     uint32_t coff, nc;      // C rects (clipped)
     int32_t wx0, wx1, wy0, wy1;  // walk region (clipped union), empty if wx0 > wx1
     uint32_t outside;       // some G rect reaches outside [0,n)^2
-    uint32_t pad;
+    uint32_t ns;            // y slabs (0: no slab lists, every segment is visited)
+    double sy0, sinv;       // slab of y = clamp(floor((y - sy0) * sinv), 0, ns - 1)
+    double E;               // distance lists hold every segment within E of the slab in y
+    uint32_t loff, llen;    // slab block in the u16 list blob (SlabView)
 };
 
+// A polygon's y-slab index (u16): cbeg[ns + 1] | dbeg[ns + 1] | segment ids.  Crossing list of
+// slab s: segments (v[e], v[e+1]) whose y-range meets the slab (padded) -- every segment that
+// RayCrossingCounter.countSegment can count or flag for a point whose y falls in the slab.
+// Distance list: segments whose y-range widened by E meets the slab; a point whose screen
+// radius is <= E cannot be within it of any other segment.  Built by plan_slabs (host).
+struct SlabView {
+    const uint16_t* p;
+    uint32_t ns;
+    __device__ __forceinline__ uint32_t cbeg(uint32_t s) const { return p[s]; }
+    __device__ __forceinline__ uint32_t dbeg(uint32_t s) const { return p[ns + 1 + s]; }
+    __device__ __forceinline__ uint32_t id(uint32_t k) const { return p[2 * (ns + 1) + k]; }
+};
+
+__host__ __device__ __forceinline__ uint32_t slab_of(double y, double sy0, double sinv, uint32_t ns) {
+    const double f = (y - sy0) * sinv;
+    if (!(f >= 0.0)) return 0;  // also NaN
+    if (f >= (double)ns) return ns - 1;
+    return (uint32_t)f;
+}
+
+// Screens that only ever reject (never accept) a "distance <= r" test against geometry lying
+// inside a box B.  The true distance to anything in B is at least the distance to B; every JTS
+// distance this library computes (fdlibm hypot, Distance.pointToSegment) is within
+// 2^-50 * (|p - A|_1 + |B - A|_1) + 2^-51 d of the true one, so a margin of
+// 2^-44 * (|p - bbmin|_1 + 2 * |bb extent|_1 + r) on the radius keeps every computed
+// d <= r out of the rejected set.  NaN anywhere reads as "not rejected" (exact path).
+__device__ __forceinline__ double screen_lim2(double px, double py, const double bb[4], double r) {
+    const double m = ((__builtin_fabs(px - bb[0]) + __builtin_fabs(py - bb[1])) +
+                      2.0 * ((bb[2] - bb[0]) + (bb[3] - bb[1])) + __builtin_fabs(r)) * 0x1.0p-44;
+    const double lim = r + m;
+    return lim * lim;
+}
+__device__ __forceinline__ double box_dist2(double px, double py, double x0, double y0, double x1, double y1) {
+    const double ex = __builtin_fmax(__builtin_fmax(x0 - px, px - x1), 0.0);
+    const double ey = __builtin_fmax(__builtin_fmax(y0 - py, py - y1), 0.0);
+    return ex * ex + ey * ey;
+}
+
+// Sign of x1*y2 - y1*x2 for exact inputs: the rounded determinant decides when it clears
+// the forward error bound 2^-51.4 * (|x1*y2| + |y1*x2|) (plus an absolute term for underflow);
+// otherwise exact_det_sign.  Same result as RobustDeterminant.signOfDet2x2.
+__device__ __forceinline__ int det_sign(double x1, double y1, double x2, double y2) {
+    const double dl = x1 * y2, dr = y1 * x2;
+    const double det = dl - dr;
+    const double eb = 3.3306690738754716e-16 * (__builtin_fabs(dl) + __builtin_fabs(dr)) + 0x1.0p-1020;
+    if (det > eb) return 1;
+    if (det < -eb) return -1;
+    return exact_det_sign(x1, y1, x2, y2);
+}
+
+// One segment of RayCrossingCounter.countSegment(p1, p2) for point p.
+__device__ __forceinline__ void count_segment(double px, double py, double p1x, double p1y, double p2x, double p2y,
+                                              bool& boundary, int& crossings) {
+    const bool live = !(p1x < px && p2x < px);
+    const bool at_p2 = px == p2x && py == p2y;
+    const bool horiz = p1y == py && p2y == py;
+    const bool on_h = horiz && px >= __builtin_fmin(p1x, p2x) && px <= __builtin_fmax(p1x, p2x);
+    const bool strad = (p1y > py && p2y <= py) || (p2y > py && p1y <= py);
+    if (live && !at_p2 && strad) {
+        const double x1 = p1x - px, y1 = p1y - py, x2 = p2x - px, y2 = p2y - py;
+        int sg = det_sign(x1, y1, x2, y2);
+        boundary = boundary || sg == 0;
+        if (y2 < y1) sg = -sg;
+        crossings += sg > 0 ? 1 : 0;
+    }
+    boundary = boundary || (live && (at_p2 || on_h));
+}
+
+// Distance.pointToSegment(p, A, B) <= r, behind the box screen (lim2 = screen_lim2).
+__device__ __forceinline__ bool segment_within(double px, double py, double ax, double ay, double bx, double by,
+                                               double r, double lim2) {
+    if (box_dist2(px, py, __builtin_fmin(ax, bx), __builtin_fmin(ay, by), __builtin_fmax(ax, bx),
+                  __builtin_fmax(ay, by)) > lim2)
+        return false;
+    double d;
+    if (ax == bx && ay == by) {
+        d = coord_distance(px, py, ax, ay);
+    } else {
+        const double len2 = (bx - ax) * (bx - ax) + (by - ay) * (by - ay);
+        const double rr = ((px - ax) * (bx - ax) + (py - ay) * (by - ay)) / len2;
+        if (rr <= 0.0) d = coord_distance(px, py, ax, ay);
+        else if (rr >= 1.0) d = coord_distance(px, py, bx, by);
+        else {
+            const double s = ((ay - py) * (bx - ax) - (ax - px) * (by - ay)) / len2;
+            d = __builtin_fabs(s) * __builtin_sqrt(len2);
+        }
+    }
+    return d <= r;
+}
+
 // JTS DistanceOp(point, polygon) predicate "distance <= r" (r < MAX_VALUE):
-// PointLocator (envelope, RayCrossingCounter) -> 0; else min over segments of
-// Distance.pointToSegment.  Boolean-equivalent early exits.
+// PointLocator (envelope, RayCrossingCounter over the ring) -> 0 when not EXTERIOR; else the
+// min over segments of Distance.pointToSegment.  A boundary hit anywhere makes the answer true
+// whatever the other segments count, so segments are visited in any order and only those of
+// the point's slab lists; boolean-equivalent early exit on the first segment within r.
 __device__ bool point_polygon_within(double px, double py, const double* __restrict__ vx,
-                                     const double* __restrict__ vy, int nv, const double bb[4], double r) {
-    const bool in_env = !(px > bb[2] || px < bb[0] || py > bb[3] || py < bb[1]);
+                                     const double* __restrict__ vy, const PolyDev& P, const SlabView& sv, double r) {
+    const int nv = (int)P.nv;
+    const bool in_env = !(px > P.bb[2] || px < P.bb[0] || py > P.bb[3] || py < P.bb[1]);
+    const uint32_t s = sv.ns ? slab_of(py, P.sy0, P.sinv, sv.ns) : 0u;
     if (in_env) {
-        int crossings = 0;
         bool boundary = false;
-        for (int i = 1; i < nv; i++) {
-            const double p1x = vx[i], p1y = vy[i], p2x = vx[i - 1], p2y = vy[i - 1];
-            if (p1x < px && p2x < px) continue;
-            if (px == p2x && py == p2y) { boundary = true; break; }
-            if (p1y == py && p2y == py) {
-                double mn = p1x, mx = p2x;
-                if (mn > mx) { mn = p2x; mx = p1x; }
-                if (px >= mn && px <= mx) { boundary = true; break; }
-                continue;
+        int crossings = 0;
+        if (sv.ns) {
+            const uint32_t k1 = sv.cbeg(s + 1);
+            for (uint32_t k = sv.cbeg(s); k < k1; k++) {
+                const uint32_t e = sv.id(k);
+                count_segment(px, py, vx[e + 1], vy[e + 1], vx[e], vy[e], boundary, crossings);
             }
-            if ((p1y > py && p2y <= py) || (p2y > py && p1y <= py)) {
-                const double x1 = p1x - px, y1 = p1y - py, x2 = p2x - px, y2 = p2y - py;
-                int s = exact_det_sign(x1, y1, x2, y2);
-                if (s == 0) { boundary = true; break; }
-                if (y2 < y1) s = -s;
-                if (s > 0) crossings++;
-            }
-        }
-        if (boundary || (crossings & 1)) return true;  // not EXTERIOR: distance 0
-    }
-    for (int i = 0; i < nv - 1; i++) {
-        const double ax = vx[i], ay = vy[i], bx = vx[i + 1], by = vy[i + 1];
-        double d;
-        if (ax == bx && ay == by) {
-            d = coord_distance(px, py, ax, ay);
         } else {
-            const double len2 = (bx - ax) * (bx - ax) + (by - ay) * (by - ay);
-            const double rr = ((px - ax) * (bx - ax) + (py - ay) * (by - ay)) / len2;
-            if (rr <= 0.0) d = coord_distance(px, py, ax, ay);
-            else if (rr >= 1.0) d = coord_distance(px, py, bx, by);
-            else {
-                const double s = ((ay - py) * (bx - ax) - (ax - px) * (by - ay)) / len2;
-                d = __builtin_fabs(s) * __builtin_sqrt(len2);
-            }
+            for (int i = 1; i < nv; i++) count_segment(px, py, vx[i], vy[i], vx[i - 1], vy[i - 1], boundary, crossings);
         }
-        if (d <= r) return true;
+        if (boundary || (crossings & 1)) return true;  // distance 0
     }
+    const double lim2 = screen_lim2(px, py, P.bb, r);
+    if (sv.ns && lim2 <= P.E * P.E) {
+        const uint32_t k1 = sv.dbeg(s + 1);
+        for (uint32_t k = sv.dbeg(s); k < k1; k++) {
+            const uint32_t e = sv.id(k);
+            if (segment_within(px, py, vx[e], vy[e], vx[e + 1], vy[e + 1], r, lim2)) return true;
+        }
+        return false;
+    }
+    for (int i = 0; i < nv - 1; i++)
+        if (segment_within(px, py, vx[i], vy[i], vx[i + 1], vy[i + 1], r, lim2)) return true;
     return false;
 }
 
@@ -415,93 +599,186 @@ __device__ __forceinline__ bool in_rects(const int32_t* __restrict__ rr, uint32_
     return false;
 }
 
-constexpr int kMaxLdsVerts = 2048;
+constexpr int kMaxLdsVerts = 1024;  // larger rings are read from global memory
+constexpr int kMaxLdsSlab = 4096;   // u16 slab-list entries staged in LDS
+constexpr int kMaskWords = 512;     // hit-mask words kept in LDS (tiles up to 32768 points)
+constexpr int kCandQ = 128;         // per-wave queue of points needing the exact polygon distance
+constexpr int kPolyPairs = 512;     // per-wave pair buffer of the polygon kernels
 
-template <bool COUNT_ONLY, bool APPROX>
-__global__ __launch_bounds__(kTB) void ppoly_probe(Bucketed bk, const PolyDev* __restrict__ polys, uint32_t npoly,
-                                                   const double* __restrict__ vx, const double* __restrict__ vy,
-                                                   const int32_t* __restrict__ rects, double r, int r_is_max,
-                                                   unsigned long long* __restrict__ total, unsigned* __restrict__ out,
-                                                   uint64_t cap) {
-    __shared__ PairBuf pb;
-    __shared__ ColWalk cw;
+struct PolyWork {
+    uint32_t poly, tile;
+};
+
+struct CandQueue {
+    double x[kCandQ];
+    double y[kCandQ];
+    unsigned pos[kCandQ];
+};
+
+// hit-mask words of each work item: ceil(points of its tile / 64)
+__global__ void ppoly_words(const PolyWork* __restrict__ work, uint32_t nwork, const unsigned* __restrict__ tstart,
+                            unsigned long long* __restrict__ words) {
+    const uint32_t w = blockIdx.x * kTB + threadIdx.x;
+    if (w >= nwork) return;
+    const uint32_t t = work[w].tile;
+    words[w] = (tstart[t + 1] - tstart[t] + 63) / 64;
+}
+
+// Count pass, one workgroup per (polygon, tile): ring and slab lists in LDS; every wave
+// classifies 64 of the tile's points per pass (G -> hit; C -> approximate bbox distance, or
+// the envelope screen then a per-wave queue) and evaluates the exact JTS distance on full
+// waves of queued points.  Hits become a bitmask over the tile's points (word k = points
+// [64k, 64k + 64) of the tile) and a per-work-item count; the write pass (ppoly_emit) only
+// reads the mask.
+// Emit (polygon, p) iff key(p) in G, or key(p) in C and d <= r (PointPolygonRangeQuery.java:105-121).
+template <bool APPROX>
+__global__ __launch_bounds__(kTB) void ppoly_eval(TileBins tb, const PolyWork* __restrict__ work,
+                                                  const PolyDev* __restrict__ polys, const double* __restrict__ vx,
+                                                  const double* __restrict__ vy, const int32_t* __restrict__ rects,
+                                                  const uint16_t* __restrict__ slabs, double r, int r_is_max,
+                                                  const unsigned long long* __restrict__ wofs,
+                                                  unsigned long long* __restrict__ mask,
+                                                  unsigned long long* __restrict__ bcount) {
     __shared__ double lvx[kMaxLdsVerts];
     __shared__ double lvy[kMaxLdsVerts];
-    __shared__ unsigned long long bcount;
-    if (threadIdx.x == 0) { pb.cnt = 0; bcount = 0; }
+    __shared__ uint16_t lsl[kMaxLdsSlab];
+    __shared__ unsigned long long lmask[kMaskWords];
+    __shared__ CandQueue cq[kTB / kWave];
+    __shared__ unsigned long long bsh;
+    const PolyWork w = work[blockIdx.x];
+    const PolyDev P = polys[w.poly];
+    const unsigned ds = tb.start[w.tile], de = tb.start[w.tile + 1];
+    const unsigned nwords = (de - ds + 63) / 64;
+    const bool lds_mask = nwords <= (unsigned)kMaskWords;
+    unsigned long long* gm = mask + wofs[blockIdx.x];
+    const bool v_lds = P.nv <= (uint32_t)kMaxLdsVerts;
+    const bool s_lds = P.llen <= (uint32_t)kMaxLdsSlab;
+    if (v_lds)
+        for (uint32_t t = threadIdx.x; t < P.nv; t += kTB) {
+            lvx[t] = vx[P.voff + t];
+            lvy[t] = vy[P.voff + t];
+        }
+    if (s_lds)
+        for (uint32_t t = threadIdx.x; t < P.llen; t += kTB) lsl[t] = slabs[P.loff + t];
+    if (lds_mask)
+        for (uint32_t t = threadIdx.x; t < nwords; t += kTB) lmask[t] = 0;
+    if (threadIdx.x == 0) bsh = 0;
     __syncthreads();
-    for (uint32_t p = blockIdx.x; p < npoly; p += gridDim.x) {
-        const PolyDev P = polys[p];
-        if (P.wx0 > P.wx1 || P.wy0 > P.wy1) continue;
-        const bool in_lds = P.nv <= (uint32_t)kMaxLdsVerts;
-        __syncthreads();
-        if (in_lds)
-            for (uint32_t t = threadIdx.x; t < P.nv; t += blockDim.x) {
-                lvx[t] = vx[P.voff + t];
-                lvy[t] = vy[P.voff + t];
+    const double* rvx = v_lds ? lvx : vx + P.voff;
+    const double* rvy = v_lds ? lvy : vy + P.voff;
+    const SlabView sv{s_lds ? lsl : slabs + P.loff, P.ns};
+    unsigned long long* mk = lds_mask ? lmask : gm;  // global words: zeroed by the host, atomics only
+    const int wid = threadIdx.x / kWave, lane = lane_id();
+    CandQueue& Q = cq[wid];
+    unsigned qn = 0;
+    const unsigned nb = (unsigned)tb.nb;
+    const int32_t* grect = rects + 4 * P.goff;
+    const int32_t* crect = rects + 4 * P.coff;
+    auto drain = [&](unsigned take) {  // evaluate the top `take` queued points (wave-uniform)
+        const unsigned from = qn - take;
+        if ((unsigned)lane < take) {
+            const double px = Q.x[from + lane], py = Q.y[from + lane];
+            const unsigned pos = Q.pos[from + lane];
+            if (point_polygon_within(px, py, rvx, rvy, P, sv, r)) atomicOr(&mk[pos >> 6], 1ull << (pos & 63));
+        }
+        wave_lds_sync();
+        qn = from;
+    };
+    for (unsigned base = ds + wid * kWave; base < de; base += kTB) {
+        const unsigned i = base + lane;
+        bool hit = false, need = false;
+        double px = 0.0, py = 0.0;
+        if (i < de) {
+            const unsigned key = tb.skey[i];
+            const int32_t cx = (int32_t)(key / nb), cy = (int32_t)(key - (unsigned)cx * nb);
+            const bool g = in_rects(grect, P.ng, cx, cy);
+            const bool c = !g && in_rects(crect, P.nc, cx, cy);
+            if (g || c) {
+                px = tb.sx[i];
+                py = tb.sy[i];
+                if (g || r_is_max) hit = true;
+                else if (APPROX) hit = bbox_distance(px, py, P.bb) <= r;
+                else need = !(box_dist2(px, py, P.bb[0], P.bb[1], P.bb[2], P.bb[3]) > screen_lim2(px, py, P.bb, r));
             }
-        __syncthreads();
-        const double* rvx = in_lds ? lvx : vx + P.voff;
-        const double* rvy = in_lds ? lvy : vy + P.voff;
-        unsigned my = 0;
-        walk_columns(
-            cw, bk.start, bk.nb, P.wx0, P.wx1, P.wy0, P.wy1,
-            [&](unsigned pos) {
-                bool hit = false;
-                unsigned pid = 0;
-                if (pos != 0xffffffffu) {
-                    const unsigned key = bk.skey[pos];
-                    const int32_t cx = (int32_t)(key / (unsigned)bk.nb), cy = (int32_t)(key % (unsigned)bk.nb);
-                    const bool g = in_rects(rects + 4 * P.goff, P.ng, cx, cy);
-                    const bool c = !g && in_rects(rects + 4 * P.coff, P.nc, cx, cy);
-                    if (g || c) {
-                        pid = bk.sidx[pos];
-                        if (g || r_is_max) {
-                            hit = true;
-                        } else {
-                            const double px = bk.sx[pos], py = bk.sy[pos];
-                            if (APPROX) hit = bbox_distance(px, py, P.bb) <= r;
-                            else hit = point_polygon_within(px, py, rvx, rvy, (int)P.nv, P.bb, r);
-                        }
-                    }
-                }
-                if (COUNT_ONLY) my += hit ? 1u : 0u;
-                else pairbuf_push(pb, hit, p, pid);
-            },
-            [&]() {
-                if (!COUNT_ONLY) {
-                    __syncthreads();
-                    if (pb.cnt > kPairBuf - kTB) pairbuf_flush(pb, total, out, cap);
-                }
-            });
-        if (COUNT_ONLY && my) atomicAdd(&bcount, (unsigned long long)my);
+        }
+        const unsigned long long m = __ballot(hit);
+        if (m && lane == 0) atomicOr(&mk[(base - ds) >> 6], m);
+        if (!APPROX) {
+            const unsigned long long mq = __ballot(need);
+            if (need) {
+                const unsigned slot = qn + lanes_below(mq);
+                Q.x[slot] = px;
+                Q.y[slot] = py;
+                Q.pos[slot] = i - ds;
+            }
+            qn += (unsigned)__popcll(mq);
+            wave_lds_sync();
+            if (qn >= (unsigned)kWave) drain(kWave);
+        }
     }
-    if (COUNT_ONLY) {
-        __syncthreads();
-        if (threadIdx.x == 0 && bcount) atomicAdd(total, bcount);
-    } else {
-        pairbuf_flush(pb, total, out, cap);
+    if (!APPROX && qn) drain(qn);
+    __syncthreads();
+    if (!lds_mask) __threadfence();
+    __syncthreads();
+    unsigned long long c = 0;
+    for (uint32_t t = threadIdx.x; t < nwords; t += kTB) {
+        unsigned long long v;
+        if (lds_mask) {
+            v = lmask[t];
+            gm[t] = v;
+        } else {
+            v = __hip_atomic_load(&gm[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        c += (unsigned long long)__popcll(v);
     }
+    if (c) atomicAdd(&bsh, c);
+    __syncthreads();
+    if (threadIdx.x == 0) bcount[blockIdx.x] = bsh;
+}
+
+// Write pass: pairs (polygon, point) of every set bit of the work item's hit mask.
+__global__ __launch_bounds__(kTB) void ppoly_emit(TileBins tb, const PolyWork* __restrict__ work,
+                                                  const unsigned long long* __restrict__ wofs,
+                                                  const unsigned long long* __restrict__ mask, PairSink sink) {
+    __shared__ uint2 pbuf[kTB / kWave][kPolyPairs];
+    __shared__ unsigned long long bsh;
+    const PolyWork w = work[blockIdx.x];
+    const unsigned ds = tb.start[w.tile], de = tb.start[w.tile + 1];
+    const unsigned nwords = (de - ds + 63) / 64;
+    const unsigned long long* gm = mask + wofs[blockIdx.x];
+    if (threadIdx.x == 0) bsh = 0;
+    __syncthreads();
+    const int wid = threadIdx.x / kWave, lane = lane_id();
+    uint2* buf = pbuf[wid];
+    unsigned long long cnt = 0;
+    for (unsigned k = wid; k < nwords; k += kTB / kWave) {
+        const unsigned long long word = gm[k];
+        if (word == 0) continue;
+        const bool hit = (word >> lane) & 1ull;
+        const unsigned pid = hit ? tb.sidx[ds + k * 64 + lane] : 0u;
+        pairs_push<true, kPolyPairs>(buf, cnt, hit, w.poly, pid, &bsh, sink);
+    }
+    pairs_end<true>(buf, cnt, &bsh, sink);
 }
 
 // out-of-grid points vs guaranteed rects reaching outside the grid (Lg == 0 bbox keys)
-template <bool COUNT_ONLY>
+template <bool WRITE>
 __global__ __launch_bounds__(kTB) void ppoly_outside(const double* __restrict__ x, const double* __restrict__ y,
                                                      const unsigned* __restrict__ oidx, unsigned nout, double mnx,
                                                      double mny, double l, const PolyDev* __restrict__ polys,
-                                                     uint32_t npoly, const int32_t* __restrict__ rects,
-                                                     unsigned long long* __restrict__ total, unsigned* __restrict__ out,
-                                                     uint64_t cap) {
-    __shared__ PairBuf pb;
-    __shared__ unsigned long long bcount;
-    if (threadIdx.x == 0) { pb.cnt = 0; bcount = 0; }
+                                                     uint32_t npoly, const int32_t* __restrict__ rects, PairSink sink) {
+    __shared__ uint2 pbuf[WRITE ? kTB / kWave : 1][WRITE ? kPolyPairs : 1];
+    __shared__ unsigned long long bsh;
+    const int wid = threadIdx.x / kWave;
+    uint2* buf = pbuf[WRITE ? wid : 0];
+    unsigned long long cnt = 0;
+    if (threadIdx.x == 0) bsh = 0;
     __syncthreads();
     for (uint32_t p = blockIdx.x; p < npoly; p += gridDim.x) {
         const PolyDev P = polys[p];
         if (!P.outside) continue;
-        unsigned my = 0;
-        for (unsigned t0 = 0; t0 < nout; t0 += kTB) {
-            const unsigned t = t0 + threadIdx.x;
+        for (unsigned t0 = wid * kWave; t0 < nout; t0 += kTB) {
+            const unsigned t = t0 + lane_id();
             bool hit = false;
             unsigned pid = 0;
             if (t < nout) {
@@ -509,28 +786,23 @@ __global__ __launch_bounds__(kTB) void ppoly_outside(const double* __restrict__ 
                 const int32_t cx = d_axis_cell(x[pid], mnx, l), cy = d_axis_cell(y[pid], mny, l);
                 hit = in_rects(rects + 4 * P.goff, P.ng, cx, cy);
             }
-            if (COUNT_ONLY) {
-                my += hit ? 1u : 0u;
-            } else {
-                pairbuf_push(pb, hit, p, pid);
-                __syncthreads();
-                if (pb.cnt > kPairBuf - kTB) pairbuf_flush(pb, total, out, cap);
-            }
+            pairs_push<WRITE, kPolyPairs>(buf, cnt, hit, p, pid, &bsh, sink);
         }
-        if (COUNT_ONLY && my) atomicAdd(&bcount, (unsigned long long)my);
     }
-    if (COUNT_ONLY) {
-        __syncthreads();
-        if (threadIdx.x == 0 && bcount) atomicAdd(total, bcount);
-    } else {
-        pairbuf_flush(pb, total, out, cap);
-    }
+    pairs_end<WRITE>(buf, cnt, &bsh, sink);
 }
 
 // ================================================================== host side =============
 namespace {
 
-enum JSlot { J_KEY, J_COUNT, J_START, J_SEG, J_SX, J_SY, J_SIDX, J_SKEY, J_MISC, J_AUX, J_POLY, J_OUT, J_RECT };
+enum JSlot {
+    J_HIST, J_TTOT, J_TSTART, J_SEG, J_SX, J_SY, J_SIDX, J_SKEY, J_MISC, J_AUX, J_POLY, J_OUT, J_RECT, J_QSTART,
+    J_QLIST, J_GLIST, J_QCNT, J_BCNT, J_BOFF, J_PMASK
+};
+
+// J_MISC words: [0] outside count, [1] outside cursor, [2] scan grand total, [3] global
+// query count, [8..9] pair total (u64)
+constexpr int kMiscWords = 16;
 
 struct Scratch {
     geohip_ctx* ctx;
@@ -544,13 +816,6 @@ struct Scratch {
     }
 };
 
-unsigned grid_blocks(uint64_t n) {
-    uint64_t b = (n + kTB - 1) / kTB;
-    if (b > 8192) b = 8192;
-    if (b == 0) b = 1;
-    return (unsigned)b;
-}
-
 int check_grid_basic(geohip_ctx* ctx, const geohip_grid* g, const char* what) {
     if (!g) return ctx_fail(ctx, GEOHIP_ERR_ARG, std::string(what) + ": null grid");
     if (!(g->n > 0) || !(g->cell_len > 0) || !std::isfinite(g->cell_len) || !std::isfinite(g->min_x) ||
@@ -560,50 +825,72 @@ int check_grid_basic(geohip_ctx* ctx, const geohip_grid* g, const char* what) {
     return GEOHIP_OK;
 }
 
-// Counting sort of the points by cell of `g` over [0, nb)^2.
-int bucketize(geohip_ctx* ctx, Scratch& S, const double* dx, const double* dy, uint64_t n, const geohip_grid& g,
-              int32_t nb, bool keep_keys, bool keep_outside, Bucketed* bk, unsigned* n_outside_host) {
+TileGeom tile_geom(const geohip_grid& g, int32_t nb) {
+    TileGeom t;
+    t.mnx = g.min_x;
+    t.mny = g.min_y;
+    t.l = g.cell_len;
+    t.nb = nb;
+    t.ts = (nb + 127) / 128;
+    if (t.ts < 1) t.ts = 1;
+    t.nt = (nb + t.ts - 1) / t.ts;
+    t.ntiles = (uint32_t)t.nt * (uint32_t)t.nt;
+    return t;
+}
+
+// exclusive scan of in[0..n) into out[0..n] (out[n] = total) on the stream
+template <typename T>
+void scan_launch(hipStream_t st, const T* in, uint64_t n, T* seg, T* grand, T* out) {
+    const uint64_t nseg = (n + kScanSeg - 1) / kScanSeg;
+    const unsigned g = (unsigned)(nseg ? nseg : 1);
+    scan_seg_totals<T><<<g, kTB, 0, st>>>(in, n, seg);
+    scan_totals<T><<<1, kTB, 0, st>>>(seg, g, grand);
+    scan_apply<T><<<g, kTB, 0, st>>>(in, n, seg, grand, out);
+}
+
+// Bin the window's points into tiles of `geo` (SoA copies in scratch).  keep_outside: list the
+// out-of-grid points (their count is read back into *n_outside_host).
+int bin_tiles(geohip_ctx* ctx, Scratch& S, const double* dx, const double* dy, uint64_t n, const TileGeom& geo,
+              bool keep_outside, TileBins* tb, unsigned** outside_idx, unsigned* n_outside_host) {
     hipStream_t st = ctx_stream(ctx);
-    const uint64_t ncell = (uint64_t)nb * (uint64_t)nb;
-    if (ncell > (1ull << 27)) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "grid too large for cell bucketing (> 2^27 cells)");
-    unsigned* key = S.get<unsigned>(J_KEY, n * 4);
-    unsigned* count = S.get<unsigned>(J_COUNT, (ncell + 1) * 4);
-    unsigned* start = S.get<unsigned>(J_START, (ncell + 1) * 4);
-    const uint64_t nseg = (ncell + kScanSeg - 1) / kScanSeg;
-    unsigned* seg = S.get<unsigned>(J_SEG, (nseg + 1) * 4 + 64);
+    uint64_t nblk = (n + 16383) / 16384;
+    if (nblk > 256) nblk = 256;
+    if (nblk < 1) nblk = 1;
+    const uint64_t chunk = (n + nblk - 1) / nblk;
+    const uint64_t nt = geo.ntiles;
+    unsigned* hist = S.get<unsigned>(J_HIST, nblk * nt * 4);
+    unsigned* tot = S.get<unsigned>(J_TTOT, (nt + 1) * 4);
+    unsigned* start = S.get<unsigned>(J_TSTART, (nt + 1) * 4);
+    unsigned* seg = S.get<unsigned>(J_SEG, ((nt + kScanSeg - 1) / kScanSeg + 1) * 8 + 64);
     double* sx = S.get<double>(J_SX, n * 8);
     double* sy = S.get<double>(J_SY, n * 8);
     unsigned* sidx = S.get<unsigned>(J_SIDX, n * 4);
-    unsigned* skey = keep_keys ? S.get<unsigned>(J_SKEY, n * 4) : nullptr;
-    unsigned* misc = S.get<unsigned>(J_MISC, 64);
+    unsigned* skey = S.get<unsigned>(J_SKEY, n * 4);
+    unsigned* misc = S.get<unsigned>(J_MISC, kMiscWords * 4);
     unsigned* oidx = keep_outside ? S.get<unsigned>(J_AUX, n * 4 + 16) : nullptr;
     if (S.rc) return S.rc;
-    // misc[0] = outside count (histogram), misc[1] = outside cursor, misc[2] = grand total
-    if (hipMemsetAsync(count, 0, (ncell + 1) * 4, st) != hipSuccess || hipMemsetAsync(misc, 0, 64, st) != hipSuccess)
-        return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
-    if (n) bucket_count<<<grid_blocks(n), kTB, 0, st>>>(dx, dy, n, g.min_x, g.min_y, g.cell_len, nb, key, count, misc);
-    scan_seg_totals<<<(unsigned)nseg, kTB, 0, st>>>(count, ncell, seg);
-    scan_totals<<<1, kTB, 0, st>>>(seg, nseg, misc + 2);
-    scan_apply<<<(unsigned)nseg, kTB, 0, st>>>(count, ncell, seg, misc + 2, start);
-    if (hipMemsetAsync(count, 0, ncell * 4, st) != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
-    if (n)
-        bucket_scatter<<<grid_blocks(n), kTB, 0, st>>>(dx, dy, n, key, start, count, sx, sy, sidx, skey, oidx, misc + 1);
+    if (hipMemsetAsync(misc, 0, kMiscWords * 4, st) != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
+    const unsigned tg = (unsigned)((nt + kTB - 1) / kTB);
+    tbin_count<<<(unsigned)nblk, kBinThreads, 0, st>>>(dx, dy, n, chunk, geo, hist, misc + 0);
+    tbin_totals<<<tg, kTB, 0, st>>>(hist, (unsigned)nblk, geo.ntiles, tot);
+    scan_launch<unsigned>(st, tot, nt, seg, misc + 2, start);
+    tbin_offsets<<<tg, kTB, 0, st>>>(hist, (unsigned)nblk, geo.ntiles, start);
+    tbin_scatter<<<(unsigned)nblk, kBinThreads, 0, st>>>(dx, dy, n, chunk, geo, hist, sx, sy, sidx, skey, oidx, misc + 1);
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, std::string("bucketing: ") + hipGetErrorString(e));
+    if (e != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, std::string("tile binning: ") + hipGetErrorString(e));
     if (n_outside_host) {
         uint64_t* pin = ctx_pinned(ctx);
         if (hipMemcpyAsync(pin, misc, 4, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
             return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "outside count readback failed");
         *n_outside_host = (unsigned)(pin[0] & 0xffffffffu);
     }
-    bk->sx = sx;
-    bk->sy = sy;
-    bk->sidx = sidx;
-    bk->skey = skey;
-    bk->start = start;
-    bk->outside_idx = oidx;
-    bk->n_outside = n_outside_host ? *n_outside_host : 0;
-    bk->nb = nb;
+    tb->sx = sx;
+    tb->sy = sy;
+    tb->sidx = sidx;
+    tb->skey = skey;
+    tb->start = start;
+    tb->nb = geo.nb;
+    if (outside_idx) *outside_idx = oidx;
     return GEOHIP_OK;
 }
 
@@ -616,7 +903,26 @@ int read_total(geohip_ctx* ctx, unsigned long long* dev_total, uint64_t* out) {
     return GEOHIP_OK;
 }
 
+// Squared-distance screen bounds for "dist <= r" (device_common.h kSqLo/kSqHi), disabled
+// (r2lo < 0, r2hi = inf: every candidate takes the exact path) where r*r leaves the normal
+// range and the 2^-40 relative margin would not hold.
+void screen_bounds(double r, double* r2lo, double* r2hi) {
+    const double r2 = r * r;
+    if (r >= 0.0 && r2 >= 0x1.0p-960 && r2 <= 0x1.0p960) {
+        *r2lo = r2 * kSqLo;
+        *r2hi = r2 * kSqHi;
+    } else if (r > 0.0 && r2 > 0x1.0p960) {  // every finite square is below the bound
+        *r2lo = r2 * kSqLo;
+        *r2hi = __builtin_inf();
+    } else {
+        *r2lo = -1.0;
+        *r2hi = __builtin_inf();
+    }
+}
+
 }  // namespace
+
+void pp_screen_bounds(double r, double* r2lo, double* r2hi) { screen_bounds(r, r2lo, r2hi); }
 
 int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, const double* dx, const double* dy,
                  uint64_t nd, const double* qx, const double* qy, uint64_t nq, double r, int approximate,
@@ -648,7 +954,9 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
         pqy = hqy.data();
     }
     const int32_t nb = gq->n;
+    const TileGeom geo = tile_geom(*gd, nb);
     std::vector<QRect> rects(nq);
+    uint64_t list_entries = 0;
     for (uint64_t i = 0; i < nq; i++) {
         QRect R{0, nb - 1, 0, nb - 1};
         if (!all_cells) {
@@ -669,28 +977,39 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
             }
         }
         rects[i] = R;
+        if (R.x0 <= R.x1 && R.y0 <= R.y1) {
+            const uint64_t ntl = (uint64_t)(R.x1 / geo.ts - R.x0 / geo.ts + 1) * (uint64_t)(R.y1 / geo.ts - R.y0 / geo.ts + 1);
+            if (ntl <= kGlobalTiles) list_entries += ntl;
+        }
     }
     Scratch S{ctx};
     const double *ddx, *ddy, *dqx, *dqy;
     rc = ctx_stage_xy(ctx, dx, dy, nd, 0, &ddx, &ddy);
     if (!rc) rc = ctx_stage_xy(ctx, qx, qy, nq, 1, &dqx, &dqy);
     if (rc) return rc;
-    Bucketed bk;
-    rc = bucketize(ctx, S, ddx, ddy, nd, *gd, nb, false, false, &bk, nullptr);
+    TileBins tb;
+    rc = bin_tiles(ctx, S, ddx, ddy, nd, geo, false, &tb, nullptr, nullptr);
     if (rc) return rc;
     QRect* drect = S.get<QRect>(J_RECT, nq * sizeof(QRect) + 16);
+    unsigned* qcnt = S.get<unsigned>(J_QCNT, ((uint64_t)geo.ntiles + 1) * 4);
+    unsigned* qstart = S.get<unsigned>(J_QSTART, ((uint64_t)geo.ntiles + 1) * 4);
+    unsigned* qlist = S.get<unsigned>(J_QLIST, list_entries * 4 + 16);
+    unsigned* glist = S.get<unsigned>(J_GLIST, nq * 4 + 16);
+    unsigned* misc = S.get<unsigned>(J_MISC, kMiscWords * 4);
+    unsigned* seg = S.get<unsigned>(J_SEG, (((uint64_t)geo.ntiles + kScanSeg - 1) / kScanSeg + 1) * 8 + 64);
+    unsigned long long* bcount = S.get<unsigned long long>(J_BCNT, ((uint64_t)geo.ntiles + 1) * 8);
+    unsigned long long* boff = S.get<unsigned long long>(J_BOFF, ((uint64_t)geo.ntiles + 1) * 8);
     if (S.rc) return S.rc;
-    // total counter lives after the bucketing words in J_MISC
-    unsigned long long* total = nullptr;
-    {
-        void* p = nullptr;
-        rc = ctx_ensure(ctx, J_MISC, 64, &p);
-        if (rc) return rc;
-        total = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(p) + 32);
-    }
     if (nq && hipMemcpyAsync(drect, rects.data(), nq * sizeof(QRect), hipMemcpyHostToDevice, st) != hipSuccess)
         return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "rect upload failed");
-    if (hipMemsetAsync(total, 0, 8, st) != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
+    if (hipMemsetAsync(qcnt, 0, ((uint64_t)geo.ntiles + 1) * 4, st) != hipSuccess)
+        return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
+    const unsigned qg = (unsigned)((nq + kTB - 1) / kTB);
+    if (nq) jq_build<false><<<qg, kTB, 0, st>>>(drect, nq, geo, qcnt, nullptr, nullptr, glist, misc + 3);
+    scan_launch<unsigned>(st, qcnt, geo.ntiles, seg, misc + 2, qstart);
+    if (hipMemsetAsync(qcnt, 0, ((uint64_t)geo.ntiles + 1) * 4, st) != hipSuccess)
+        return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
+    if (nq) jq_build<true><<<qg, kTB, 0, st>>>(drect, nq, geo, qcnt, qstart, qlist, nullptr, nullptr);
     // output: device pointer directly, or a device staging buffer for host output
     unsigned* out = nullptr;
     if (!count_only && cap) {
@@ -703,22 +1022,32 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
             out = reinterpret_cast<unsigned*>(p);
         }
     }
+    PairSink sink{bcount, boff, 0u, out, out ? cap : 0, ((uintptr_t)out & 7u) == 0};
+    double r2lo, r2hi;
+    screen_bounds(r, &r2lo, &r2hi);
+    if (hipMemsetAsync(bcount, 0, (uint64_t)geo.ntiles * 8, st) != hipSuccess)
+        return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
     hipEvent_t e0, e1;
     ctx_timing_events(ctx, &e0, &e1);
     if (e0) hipEventRecord(e0, st);
-    const unsigned blocks = (unsigned)std::min<uint64_t>(nq ? nq : 1, 1u << 20);
-    if (nq) {
-        if (count_only || !cap) {
-            if (approximate) join_probe<true, true><<<blocks, kTB, 0, st>>>(bk, dqx, dqy, drect, nq, r, total, nullptr, 0);
-            else join_probe<true, false><<<blocks, kTB, 0, st>>>(bk, dqx, dqy, drect, nq, r, total, nullptr, 0);
-        } else {
-            if (approximate) join_probe<false, true><<<blocks, kTB, 0, st>>>(bk, dqx, dqy, drect, nq, r, total, out, cap);
-            else join_probe<false, false><<<blocks, kTB, 0, st>>>(bk, dqx, dqy, drect, nq, r, total, out, cap);
-        }
+    const bool work = nq && nd;
+#define GEOHIP_JOIN(A, W) \
+    join_tile<A, W><<<geo.ntiles, kTB, 0, st>>>(tb, qstart, qlist, glist, misc + 3, dqx, dqy, drect, r, r2lo, r2hi, sink)
+    if (work) {
+        if (approximate) GEOHIP_JOIN(true, false);
+        else GEOHIP_JOIN(false, false);
     }
+    scan_launch<unsigned long long>(st, bcount, geo.ntiles, reinterpret_cast<unsigned long long*>(seg),
+                                    reinterpret_cast<unsigned long long*>(misc + 8), boff);
+    if (work && out) {
+        if (approximate) GEOHIP_JOIN(true, true);
+        else GEOHIP_JOIN(false, true);
+    }
+#undef GEOHIP_JOIN
     if (e1) hipEventRecord(e1, st);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, std::string("join launch: ") + hipGetErrorString(e));
+    unsigned long long* total = boff + geo.ntiles;
     uint64_t tot = 0;
     rc = read_total(ctx, total, &tot);
     if (rc) return rc;
@@ -730,6 +1059,70 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
     }
     if (!count_only && tot > cap) return ctx_fail(ctx, GEOHIP_ERR_CAPACITY, "output capacity too small; *out_count = required");
     return GEOHIP_OK;
+}
+
+// y-slab lists of one polygon (SlabView), appended to blob; P.ns = 0 when they cannot be built
+// (few or very many segments, non-finite extent): the device then visits every segment.
+void plan_slabs(PolyDev& P, const double* ry, double r, double cell_len, std::vector<uint16_t>& blob) {
+    P.ns = 0;
+    P.sy0 = 0.0;
+    P.sinv = 0.0;
+    P.E = 0.0;
+    P.loff = (uint32_t)blob.size();
+    P.llen = 0;
+    const uint32_t nseg = P.nv >= 2 ? P.nv - 1 : 0;
+    if (nseg < 8 || nseg > 30000) return;
+    const double ext = (P.bb[2] - P.bb[0]) + (P.bb[3] - P.bb[1]);
+    // E bounds the screen radius of every point a work item evaluates (C cells lie within
+    // r + 2 cells of the envelope); a point with a larger screen radius takes the full loop
+    const double E = r + 0x1.0p-40 * 4.0 * (ext + std::fabs(r) + cell_len);
+    if (!(E >= 0.0) || !std::isfinite(E) || !std::isfinite(ext)) return;
+    const double y0 = P.bb[1] - E, y1 = P.bb[3] + E;
+    const uint32_t ns = std::min<uint32_t>(64, nseg);
+    const double span = y1 - y0;
+    if (!(span > 0.0) || !std::isfinite(span)) return;
+    const double sinv = (double)ns / span;
+    if (!(sinv > 0.0) || !std::isfinite(sinv)) return;
+    const double pad = 1e-6 * span / ns;
+    std::vector<uint32_t> ca(nseg), cb(nseg), da(nseg), db(nseg);
+    std::vector<uint32_t> cn(ns + 1, 0), dn(ns + 1, 0);
+    for (uint32_t e = 0; e < nseg; e++) {
+        const double a = ry[e], b = ry[e + 1];
+        if (a != a || b != b) {  // a NaN y never counts, flags or comes within r
+            ca[e] = da[e] = 1;
+            cb[e] = db[e] = 0;
+            continue;
+        }
+        const double lo = std::min(a, b), hi = std::max(a, b);
+        ca[e] = slab_of(lo - pad, y0, sinv, ns);
+        cb[e] = slab_of(hi + pad, y0, sinv, ns);
+        da[e] = slab_of((lo - E) - pad, y0, sinv, ns);
+        db[e] = slab_of((hi + E) + pad, y0, sinv, ns);
+        for (uint32_t t = ca[e]; t <= cb[e]; t++) cn[t]++;
+        for (uint32_t t = da[e]; t <= db[e]; t++) dn[t]++;
+    }
+    uint64_t total = 0;
+    for (uint32_t t = 0; t < ns; t++) total += cn[t] + dn[t];
+    if (total + 2ull * (ns + 1) > 65535ull) return;
+    const size_t h = blob.size();
+    blob.resize(h + 2 * (ns + 1) + total);
+    uint16_t* B = blob.data() + h;
+    uint32_t k = 0;
+    for (uint32_t t = 0; t < ns; t++) { B[t] = (uint16_t)k; k += cn[t]; }
+    B[ns] = (uint16_t)k;
+    for (uint32_t t = 0; t < ns; t++) { B[ns + 1 + t] = (uint16_t)k; k += dn[t]; }
+    B[2 * ns + 1] = (uint16_t)k;
+    std::vector<uint32_t> cf(ns, 0), df(ns, 0);
+    uint16_t* ids = B + 2 * (ns + 1);
+    for (uint32_t e = 0; e < nseg; e++) {
+        for (uint32_t t = ca[e]; t <= cb[e] && ca[e] <= cb[e]; t++) ids[B[t] + cf[t]++] = (uint16_t)e;
+        for (uint32_t t = da[e]; t <= db[e] && da[e] <= db[e]; t++) ids[B[ns + 1 + t] + df[t]++] = (uint16_t)e;
+    }
+    P.ns = ns;
+    P.sy0 = y0;
+    P.sinv = sinv;
+    P.E = E;
+    P.llen = (uint32_t)(2 * (ns + 1) + total);
 }
 
 int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
@@ -745,10 +1138,14 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const 
     hipStream_t st = ctx_stream(ctx);
     const bool dev = ctx_mem(ctx) == GEOHIP_MEM_DEVICE;
     const int32_t nb = grid->n;
-    // polygon planning (host): ring closure, envelope, G / C rectangles (plan.cpp)
+    const TileGeom geo = tile_geom(*grid, nb);
+    // polygon planning (host): ring closure, envelope, G / C rectangles (plan.cpp), and the
+    // (polygon, tile) work items of each polygon's walk region
     std::vector<PolyDev> pd(npoly);
     std::vector<double> hvx, hvy;
     std::vector<int32_t> hrects;
+    std::vector<PolyWork> hwork;
+    std::vector<uint16_t> hslab;
     bool any_outside = false;
     for (uint32_t p = 0; p < npoly; p++) {
         PolyPlan pl;
@@ -781,38 +1178,69 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const 
         for (auto& q : pl.c) { hrects.insert(hrects.end(), {q.x0, q.x1, q.y0, q.y1}); acc(q); }
         P.wx0 = wx0; P.wx1 = wx1; P.wy0 = wy0; P.wy1 = wy1;
         any_outside = any_outside || P.outside;
+        plan_slabs(P, pl.ry.data(), r, grid->cell_len, hslab);
+        if (wx0 <= wx1 && wy0 <= wy1)
+            for (int32_t a = wx0 / geo.ts; a <= wx1 / geo.ts; a++)
+                for (int32_t c = wy0 / geo.ts; c <= wy1 / geo.ts; c++)
+                    hwork.push_back(PolyWork{p, (uint32_t)a * (uint32_t)geo.nt + (uint32_t)c});
     }
+    if (hwork.size() >= 0x7fffffffull) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "too many polygon work items");
     Scratch S{ctx};
     const double *dx, *dy;
     rc = ctx_stage_xy(ctx, x, y, n, 0, &dx, &dy);
     if (rc) return rc;
-    Bucketed bk;
+    TileBins tb;
+    unsigned* oidx = nullptr;
     unsigned n_out = 0;
-    rc = bucketize(ctx, S, dx, dy, n, *grid, nb, true, any_outside, &bk, any_outside ? &n_out : nullptr);
+    rc = bin_tiles(ctx, S, dx, dy, n, geo, any_outside, &tb, &oidx, any_outside ? &n_out : nullptr);
     if (rc) return rc;
-    // polygon tables in one device blob: PolyDev[] | vx | vy | rects
+    // polygon tables in one device blob: PolyDev[] | vx | vy | rects | work | slab lists
     const size_t sz_p = npoly * sizeof(PolyDev), sz_v = hvx.size() * 8, sz_r = hrects.size() * 4;
+    const size_t sz_w = hwork.size() * sizeof(PolyWork), sz_s = hslab.size() * 2;
+    const size_t off_v = (sz_p + 15) & ~(size_t)15;
+    const size_t off_r = off_v + 2 * sz_v;
+    const size_t off_w = (off_r + sz_r + 15) & ~(size_t)15;
+    const size_t off_s = (off_w + sz_w + 15) & ~(size_t)15;
     void* pblob = nullptr;
-    rc = ctx_ensure(ctx, J_POLY, sz_p + 2 * sz_v + sz_r + 64, &pblob);
+    rc = ctx_ensure(ctx, J_POLY, off_s + sz_s + 64, &pblob);
     if (rc) return rc;
     char* bp = reinterpret_cast<char*>(pblob);
     PolyDev* dpoly = reinterpret_cast<PolyDev*>(bp);
-    double* dvx = reinterpret_cast<double*>(bp + ((sz_p + 15) & ~(size_t)15));
+    double* dvx = reinterpret_cast<double*>(bp + off_v);
     double* dvy = dvx + hvx.size();
-    int32_t* drects = reinterpret_cast<int32_t*>(dvy + hvy.size());
+    int32_t* drects = reinterpret_cast<int32_t*>(bp + off_r);
+    PolyWork* dwork = reinterpret_cast<PolyWork*>(bp + off_w);
+    uint16_t* dslab = reinterpret_cast<uint16_t*>(bp + off_s);
     if ((sz_p && hipMemcpyAsync(dpoly, pd.data(), sz_p, hipMemcpyHostToDevice, st) != hipSuccess) ||
         (sz_v && hipMemcpyAsync(dvx, hvx.data(), sz_v, hipMemcpyHostToDevice, st) != hipSuccess) ||
         (sz_v && hipMemcpyAsync(dvy, hvy.data(), sz_v, hipMemcpyHostToDevice, st) != hipSuccess) ||
-        (sz_r && hipMemcpyAsync(drects, hrects.data(), sz_r, hipMemcpyHostToDevice, st) != hipSuccess))
+        (sz_r && hipMemcpyAsync(drects, hrects.data(), sz_r, hipMemcpyHostToDevice, st) != hipSuccess) ||
+        (sz_w && hipMemcpyAsync(dwork, hwork.data(), sz_w, hipMemcpyHostToDevice, st) != hipSuccess) ||
+        (sz_s && hipMemcpyAsync(dslab, hslab.data(), sz_s, hipMemcpyHostToDevice, st) != hipSuccess))
         return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "polygon upload failed");
-    unsigned long long* total = nullptr;
-    {
-        void* p = nullptr;
-        rc = ctx_ensure(ctx, J_MISC, 64, &p);
+    const unsigned nwork = (unsigned)hwork.size();
+    const unsigned nob = (any_outside && n_out) ? (npoly < 4096u ? npoly : 4096u) : 0u;
+    const uint64_t nslots = (uint64_t)nwork + nob;
+    const uint64_t nscan = std::max<uint64_t>(nslots, nwork);
+    unsigned* misc = S.get<unsigned>(J_MISC, kMiscWords * 4);
+    unsigned* seg = S.get<unsigned>(J_SEG, ((nscan + kScanSeg - 1) / kScanSeg + 1) * 8 + 64);
+    unsigned long long* bcount = S.get<unsigned long long>(J_BCNT, (nslots + 1) * 8);
+    unsigned long long* boff = S.get<unsigned long long>(J_BOFF, (nslots + 1) * 8);
+    unsigned long long* words = S.get<unsigned long long>(J_QLIST, ((uint64_t)nwork + 1) * 8);
+    unsigned long long* wofs = S.get<unsigned long long>(J_QSTART, ((uint64_t)nwork + 1) * 8);
+    if (S.rc) return S.rc;
+    // hit-mask layout: words per work item, scanned; the total sizes the mask (one readback)
+    uint64_t nmask = 0;
+    if (nwork) {
+        ppoly_words<<<(nwork + kTB - 1) / kTB, kTB, 0, st>>>(dwork, nwork, tb.start, words);
+        scan_launch<unsigned long long>(st, words, nwork, reinterpret_cast<unsigned long long*>(seg),
+                                        reinterpret_cast<unsigned long long*>(misc + 8), wofs);
+        rc = read_total(ctx, wofs + nwork, &nmask);
         if (rc) return rc;
-        total = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(p) + 32);
     }
-    if (hipMemsetAsync(total, 0, 8, st) != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
+    unsigned long long* mask = S.get<unsigned long long>(J_PMASK, nmask * 8 + 8);
+    if (S.rc) return S.rc;
+    if (nmask && hipMemsetAsync(mask, 0, nmask * 8, st) != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
     unsigned* out = nullptr;
     if (cap) {
         if (dev) {
@@ -824,31 +1252,37 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const 
             out = reinterpret_cast<unsigned*>(p);
         }
     }
+    PairSink sink{bcount, boff, 0u, out, out ? cap : 0, ((uintptr_t)out & 7u) == 0};
+    PairSink osink = sink;
+    osink.slot0 = nwork;
     const int r_is_max = r >= 1.7976931348623157e308;
+    if (hipMemsetAsync(bcount, 0, (nslots + 1) * 8, st) != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
     hipEvent_t e0, e1;
     ctx_timing_events(ctx, &e0, &e1);
     if (e0) hipEventRecord(e0, st);
-    const unsigned blocks = npoly ? npoly : 1;
-    if (npoly) {
-        if (!cap) {
-            if (approximate) ppoly_probe<true, true><<<blocks, kTB, 0, st>>>(bk, dpoly, npoly, dvx, dvy, drects, r, r_is_max, total, nullptr, 0);
-            else ppoly_probe<true, false><<<blocks, kTB, 0, st>>>(bk, dpoly, npoly, dvx, dvy, drects, r, r_is_max, total, nullptr, 0);
-        } else {
-            if (approximate) ppoly_probe<false, true><<<blocks, kTB, 0, st>>>(bk, dpoly, npoly, dvx, dvy, drects, r, r_is_max, total, out, cap);
-            else ppoly_probe<false, false><<<blocks, kTB, 0, st>>>(bk, dpoly, npoly, dvx, dvy, drects, r, r_is_max, total, out, cap);
-        }
-        if (any_outside && n_out) {
-            if (!cap)
-                ppoly_outside<true><<<blocks, kTB, 0, st>>>(dx, dy, bk.outside_idx, n_out, grid->min_x, grid->min_y,
-                                                            grid->cell_len, dpoly, npoly, drects, total, nullptr, 0);
-            else
-                ppoly_outside<false><<<blocks, kTB, 0, st>>>(dx, dy, bk.outside_idx, n_out, grid->min_x, grid->min_y,
-                                                             grid->cell_len, dpoly, npoly, drects, total, out, cap);
-        }
+    // count pass: hit masks + per-work-item counts; out-of-grid points counted separately
+    if (nwork) {
+        if (approximate)
+            ppoly_eval<true><<<nwork, kTB, 0, st>>>(tb, dwork, dpoly, dvx, dvy, drects, dslab, r, r_is_max, wofs, mask, bcount);
+        else
+            ppoly_eval<false><<<nwork, kTB, 0, st>>>(tb, dwork, dpoly, dvx, dvy, drects, dslab, r, r_is_max, wofs, mask, bcount);
+    }
+    if (nob)
+        ppoly_outside<false><<<nob, kTB, 0, st>>>(dx, dy, oidx, n_out, grid->min_x, grid->min_y, grid->cell_len, dpoly,
+                                                  npoly, drects, osink);
+    scan_launch<unsigned long long>(st, bcount, nslots, reinterpret_cast<unsigned long long*>(seg),
+                                    reinterpret_cast<unsigned long long*>(misc + 8), boff);
+    // write pass: pairs from the masks
+    if (out) {
+        if (nwork) ppoly_emit<<<nwork, kTB, 0, st>>>(tb, dwork, wofs, mask, sink);
+        if (nob)
+            ppoly_outside<true><<<nob, kTB, 0, st>>>(dx, dy, oidx, n_out, grid->min_x, grid->min_y, grid->cell_len, dpoly,
+                                                     npoly, drects, osink);
     }
     if (e1) hipEventRecord(e1, st);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, std::string("ppoly launch: ") + hipGetErrorString(e));
+    unsigned long long* total = boff + nslots;
     uint64_t tot = 0;
     rc = read_total(ctx, total, &tot);
     if (rc) return rc;

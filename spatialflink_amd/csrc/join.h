@@ -10,13 +10,16 @@
 namespace geohip {
 // context services implemented in abi.cpp
 int ctx_fail(geohip_ctx* ctx, int code, const std::string& msg);
-int ctx_ensure(geohip_ctx* ctx, int slot, size_t bytes, void** out);  // slot 0..15
+int ctx_ensure(geohip_ctx* ctx, int slot, size_t bytes, void** out);  // slot 0..19
 hipStream_t ctx_stream(geohip_ctx* ctx);
 int ctx_mem(geohip_ctx* ctx);
 uint64_t* ctx_pinned(geohip_ctx* ctx);
 void ctx_timing_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1);
 int ctx_stage_xy(geohip_ctx* ctx, const double* x, const double* y, uint64_t n, int which, const double** dx,
                  const double** dy);
+
+// squared-distance screen bounds for "dist <= r" (r2lo < 0 / r2hi = inf where they cannot hold)
+void pp_screen_bounds(double r, double* r2lo, double* r2hi);
 
 int join_pp_impl(geohip_ctx* ctx, const geohip_grid* grid_data, const geohip_grid* grid_query, const double* dx,
                  const double* dy, uint64_t nd, const double* qx, const double* qy, uint64_t nq, double r,

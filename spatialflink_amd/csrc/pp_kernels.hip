@@ -770,7 +770,8 @@ __global__ __launch_bounds__(NW * 64) void knn_scan(const double* __restrict__ x
             const unsigned long long B = lds_fresh(kb.bound);
             if (B != kSentinelD) {
                 const double t = __longlong_as_double((long long)B);
-                T2 = (t * t) * kSqHi;
+                // below 2^-960 the square leaves the normal range and the margin fails: no screen
+                T2 = __builtin_fmax((t * t) * kSqHi, 0x1.0p-960);
             }
         }
 #pragma unroll
