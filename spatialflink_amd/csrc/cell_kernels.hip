@@ -136,74 +136,267 @@ __device__ __forceinline__ unsigned tile_of(const TileGeom& g, int32_t cx, int32
     return (unsigned)(cx / g.ts) * (unsigned)g.nt + (unsigned)(cy / g.ts);
 }
 
-// per-block tile histogram of a contiguous chunk of points -> hist[block][tile]
-__global__ __launch_bounds__(kBinThreads) void tbin_count(const double* __restrict__ x, const double* __restrict__ y,
-                                                          uint64_t n, uint64_t chunk, TileGeom g,
-                                                          unsigned* __restrict__ hist, unsigned* __restrict__ nout) {
-    __shared__ unsigned h[kMaxTiles];
-    for (unsigned t = threadIdx.x; t < g.ntiles; t += kBinThreads) h[t] = 0;
-    __syncthreads();
-    const uint64_t b0 = (uint64_t)blockIdx.x * chunk;
-    const uint64_t b1 = b0 + chunk < n ? b0 + chunk : n;
-    unsigned outside = 0;
-    for (uint64_t i = b0 + threadIdx.x; i < b1; i += kBinThreads) {
-        int32_t cx, cy;
-        if (point_cell(g, x[i], y[i], cx, cy)) atomicAdd(&h[tile_of(g, cx, cy)], 1u);
-        else outside++;
+// Two binning levels, each a local LDS counting sort so every store leaves in runs: level 1
+// sorts the raw window by band (128 consecutive tiles; out-of-grid points last), level 2 sorts
+// each band by tile.  A direct one-level scatter into 16K tiles writes partial lines from
+// every block (measured 0.3 TB/s on 50M uniform points).
+constexpr int kBandBits = 7;
+constexpr unsigned kBandTiles = 1u << kBandBits;
+constexpr int kSub = 2048;        // points per local sort (2 per thread of a 1024-thread block)
+constexpr int kLocalBins = 132;   // >= bands + 1 (level 1), >= kBandTiles (level 2)
+constexpr unsigned kL2Items = 32768;  // points per level-2 work item
+constexpr unsigned kNoKey = 0xffffffffu;
+
+struct SoA {
+    double* x;
+    double* y;
+    unsigned* idx;
+    unsigned* key;
+};
+
+struct BinPass {
+    const double* x;       // level 1 input: the window
+    const double* y;
+    SoA src;               // level 2 input: level-1 output
+    SoA dst;
+    uint64_t n, chunk;     // level 1: points, points per block
+    TileGeom g;
+    unsigned nbands;       // bands of valid tiles; level-1 bin nbands = out of grid
+    unsigned* hist;        // level 1: [block][nbands + 1]; level 2: [item][kBandTiles]
+    const uint4* items;    // level 2: (band, begin, end, -)
+    const unsigned* nitems;
+};
+
+__device__ __forceinline__ unsigned key_tile(const TileGeom& g, unsigned key) {
+    const unsigned nb = (unsigned)g.nb;
+    const unsigned cx = key / nb, cy = key - cx * nb;
+    return (cx / (unsigned)g.ts) * (unsigned)g.nt + cy / (unsigned)g.ts;
+}
+
+// level-1 point j: coordinates, key (kNoKey when out of the grid), bin
+__device__ __forceinline__ unsigned l1_point(const BinPass& a, uint64_t i, double& px, double& py, unsigned& key) {
+    px = a.x[i];
+    py = a.y[i];
+    int32_t cx, cy;
+    if (point_cell(a.g, px, py, cx, cy)) {
+        key = (unsigned)cx * (unsigned)a.g.nb + (unsigned)cy;
+        return tile_of(a.g, cx, cy) >> kBandBits;
     }
-    if (outside) atomicAdd(nout, outside);
-    __syncthreads();
-    unsigned* row = hist + (size_t)blockIdx.x * g.ntiles;
-    for (unsigned t = threadIdx.x; t < g.ntiles; t += kBinThreads) row[t] = h[t];
+    key = kNoKey;
+    return a.nbands;
 }
 
-// tot[t] = sum over blocks of hist[b][t]
-__global__ void tbin_totals(const unsigned* __restrict__ hist, unsigned nblk, uint32_t ntiles, unsigned* __restrict__ tot) {
-    const unsigned t = blockIdx.x * kTB + threadIdx.x;
-    if (t >= ntiles) return;
-    unsigned s = 0;
-    for (unsigned b = 0; b < nblk; b++) s += hist[(size_t)b * ntiles + t];
-    tot[t] = s;
-}
-
-// hist[b][t] <- start[t] + sum_{b' < b} hist[b'][t]  (where block b writes its tile-t points)
-__global__ void tbin_offsets(unsigned* __restrict__ hist, unsigned nblk, uint32_t ntiles,
-                             const unsigned* __restrict__ start) {
-    const unsigned t = blockIdx.x * kTB + threadIdx.x;
-    if (t >= ntiles) return;
-    unsigned run = start[t];
-    for (unsigned b = 0; b < nblk; b++) {
-        const unsigned v = hist[(size_t)b * ntiles + t];
-        hist[(size_t)b * ntiles + t] = run;
-        run += v;
+// the range of points a block bins: level 1 a chunk of the window, level 2 one work item
+template <int LEVEL>
+__device__ __forceinline__ bool bin_range(const BinPass& a, uint64_t& b0, uint64_t& b1, unsigned& nbins,
+                                          unsigned& band) {
+    if (LEVEL == 1) {
+        b0 = (uint64_t)blockIdx.x * a.chunk;
+        b1 = b0 + a.chunk < a.n ? b0 + a.chunk : a.n;
+        nbins = a.nbands + 1;
+        band = 0;
+        return true;
     }
+    if (blockIdx.x >= *a.nitems) return false;
+    const uint4 it = a.items[blockIdx.x];
+    band = it.x;
+    b0 = it.y;
+    b1 = it.z;
+    nbins = kBandTiles;
+    return true;
 }
 
-__global__ __launch_bounds__(kBinThreads) void tbin_scatter(const double* __restrict__ x, const double* __restrict__ y,
-                                                            uint64_t n, uint64_t chunk, TileGeom g,
-                                                            const unsigned* __restrict__ offs, double* __restrict__ sx,
-                                                            double* __restrict__ sy, unsigned* __restrict__ sidx,
-                                                            unsigned* __restrict__ skey,
-                                                            unsigned* __restrict__ outside_idx,
-                                                            unsigned* __restrict__ outside_cur) {
-    __shared__ unsigned cur[kMaxTiles];
-    const unsigned* row = offs + (size_t)blockIdx.x * g.ntiles;
-    for (unsigned t = threadIdx.x; t < g.ntiles; t += kBinThreads) cur[t] = row[t];
+template <int LEVEL>
+__global__ __launch_bounds__(kBinThreads) void bin_count(BinPass a) {
+    __shared__ unsigned h[kBinThreads / kWave][kLocalBins];
+    uint64_t b0, b1;
+    unsigned nbins, band;
+    if (!bin_range<LEVEL>(a, b0, b1, nbins, band)) return;
+    const int wid = threadIdx.x / kWave;
+    for (unsigned t = threadIdx.x; t < (kBinThreads / kWave) * kLocalBins; t += kBinThreads) (&h[0][0])[t] = 0;
     __syncthreads();
-    const uint64_t b0 = (uint64_t)blockIdx.x * chunk;
-    const uint64_t b1 = b0 + chunk < n ? b0 + chunk : n;
     for (uint64_t i = b0 + threadIdx.x; i < b1; i += kBinThreads) {
-        const double px = x[i], py = y[i];
-        int32_t cx, cy;
-        if (point_cell(g, px, py, cx, cy)) {
-            const unsigned pos = atomicAdd(&cur[tile_of(g, cx, cy)], 1u);
-            sx[pos] = px;
-            sy[pos] = py;
-            sidx[pos] = (unsigned)i;
-            skey[pos] = (unsigned)cx * (unsigned)g.nb + (unsigned)cy;
-        } else if (outside_idx) {
-            outside_idx[atomicAdd(outside_cur, 1u)] = (unsigned)i;
+        unsigned bin;
+        if (LEVEL == 1) {
+            double px, py;
+            unsigned key;
+            bin = l1_point(a, i, px, py, key);
+        } else {
+            bin = key_tile(a.g, a.src.key[i]) - (band << kBandBits);
         }
+        atomicAdd(&h[wid][bin], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < nbins) {
+        unsigned c = 0;
+        for (int w = 0; w < kBinThreads / kWave; w++) c += h[w][threadIdx.x];
+        a.hist[(size_t)blockIdx.x * nbins + threadIdx.x] = c;
+    }
+}
+
+// level 1: per band, totals over blocks, exclusive scan over bands -> start1[0..nbands+1],
+// then hist[b][band] <- where block b writes its band-`band` points.  One block.
+__global__ __launch_bounds__(kTB) void bin1_offsets(unsigned* __restrict__ hist, unsigned nblk, unsigned nbins,
+                                                    unsigned* __restrict__ start1) {
+    __shared__ unsigned sh[kTB];
+    const unsigned t = threadIdx.x;
+    unsigned tot = 0;
+    if (t < nbins)
+        for (unsigned b = 0; b < nblk; b++) tot += hist[(size_t)b * nbins + t];
+    unsigned all;
+    const unsigned st = block_excl_scan(tot, sh, &all);
+    if (t < nbins) {
+        start1[t] = st;
+        unsigned run = st;
+        for (unsigned b = 0; b < nblk; b++) {
+            const unsigned v = hist[(size_t)b * nbins + t];
+            hist[(size_t)b * nbins + t] = run;
+            run += v;
+        }
+    }
+    if (t == 0) start1[nbins] = all;
+}
+
+// level-2 work items: every band cut into pieces of kL2Items points.  One block.
+__global__ __launch_bounds__(kTB) void bin2_plan(const unsigned* __restrict__ start1, unsigned nbands,
+                                                 uint4* __restrict__ items, unsigned* __restrict__ wfirst,
+                                                 unsigned* __restrict__ nitems) {
+    __shared__ unsigned sh[kTB];
+    const unsigned t = threadIdx.x;
+    unsigned cnt = 0, b = 0, e = 0;
+    if (t < nbands) {
+        b = start1[t];
+        e = start1[t + 1];
+        cnt = (e - b + kL2Items - 1) / kL2Items;
+    }
+    unsigned all;
+    const unsigned first = block_excl_scan(cnt, sh, &all);
+    if (t < nbands) {
+        wfirst[t] = first;
+        for (unsigned k = 0; k < cnt; k++) {
+            const unsigned lo = b + k * kL2Items;
+            items[first + k] = make_uint4(t, lo, e - lo > kL2Items ? lo + kL2Items : e, 0u);
+        }
+    }
+    if (t == 0) {
+        wfirst[nbands] = all;
+        *nitems = all;
+    }
+}
+
+// level 2, per tile: total over the band's work items (tot), and, after the tile scan, the
+// per-item write offsets (OFFS)
+template <bool OFFS>
+__global__ void bin2_tiles(unsigned* __restrict__ hist, const unsigned* __restrict__ wfirst, uint32_t ntiles,
+                           unsigned* __restrict__ tot, const unsigned* __restrict__ start) {
+    const unsigned t = blockIdx.x * kTB + threadIdx.x;
+    if (t >= ntiles) return;
+    const unsigned band = t >> kBandBits, loc = t & (kBandTiles - 1);
+    const unsigned w0 = wfirst[band], w1 = wfirst[band + 1];
+    if (!OFFS) {
+        unsigned c = 0;
+        for (unsigned w = w0; w < w1; w++) c += hist[(size_t)w * kBandTiles + loc];
+        tot[t] = c;
+    } else {
+        unsigned run = start[t];
+        for (unsigned w = w0; w < w1; w++) {
+            const unsigned v = hist[(size_t)w * kBandTiles + loc];
+            hist[(size_t)w * kBandTiles + loc] = run;
+            run += v;
+        }
+    }
+}
+
+struct SortStage {
+    double x[kSub];
+    double y[kSub];
+    unsigned idx[kSub];
+    unsigned key[kSub];
+    unsigned char bin[kSub];
+};
+
+// Local-sort scatter: kSub points at a time are counted by bin in LDS, staged in bin order,
+// and stored so consecutive threads write consecutive addresses of one bin's run.
+template <int LEVEL>
+__global__ __launch_bounds__(kBinThreads) void bin_scatter(BinPass a) {
+    __shared__ SortStage st;
+    __shared__ unsigned cur[kLocalBins], lh[kLocalBins], ls[kLocalBins];
+    uint64_t b0, b1;
+    unsigned nbins, band;
+    if (!bin_range<LEVEL>(a, b0, b1, nbins, band)) return;
+    const unsigned* row = a.hist + (size_t)blockIdx.x * nbins;
+    for (unsigned t = threadIdx.x; t < kLocalBins; t += kBinThreads) {
+        cur[t] = t < nbins ? row[t] : 0u;
+        lh[t] = 0;
+    }
+    __syncthreads();
+    for (uint64_t sb = b0; sb < b1; sb += kSub) {
+        const unsigned m = b1 - sb < (uint64_t)kSub ? (unsigned)(b1 - sb) : (unsigned)kSub;
+        double px[2], py[2];
+        unsigned idx[2], key[2], bin[2], rk[2];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const unsigned j = threadIdx.x + k * kBinThreads;
+            if (j < m) {
+                const uint64_t i = sb + j;
+                if (LEVEL == 1) {
+                    bin[k] = l1_point(a, i, px[k], py[k], key[k]);
+                    idx[k] = (unsigned)i;
+                } else {
+                    px[k] = a.src.x[i];
+                    py[k] = a.src.y[i];
+                    idx[k] = a.src.idx[i];
+                    key[k] = a.src.key[i];
+                    bin[k] = key_tile(a.g, key[k]) - (band << kBandBits);
+                }
+                rk[k] = atomicAdd(&lh[bin[k]], 1u);
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < kWave) {  // exclusive scan of lh over <= 192 bins (3 per lane)
+            const int l = threadIdx.x;
+            const unsigned v0 = lh[l], v1 = lh[kWave + l], v2 = 2 * kWave + l < kLocalBins ? lh[2 * kWave + l] : 0u;
+            const unsigned i0 = wave_incl_scan(v0);
+            const unsigned t0 = (unsigned)__builtin_amdgcn_readlane((int)i0, kWave - 1);
+            const unsigned i1 = wave_incl_scan(v1) + t0;
+            const unsigned t1 = (unsigned)__builtin_amdgcn_readlane((int)i1, kWave - 1);
+            const unsigned i2 = wave_incl_scan(v2) + t1;
+            ls[l] = i0 - v0;
+            ls[kWave + l] = i1 - v1;
+            if (2 * kWave + l < kLocalBins) ls[2 * kWave + l] = i2 - v2;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const unsigned j = threadIdx.x + k * kBinThreads;
+            if (j < m) {
+                const unsigned slot = ls[bin[k]] + rk[k];
+                st.x[slot] = px[k];
+                st.y[slot] = py[k];
+                st.idx[slot] = idx[k];
+                st.key[slot] = key[k];
+                st.bin[slot] = (unsigned char)bin[k];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const unsigned j = threadIdx.x + k * kBinThreads;
+            if (j < m) {
+                const unsigned b = st.bin[j];
+                const unsigned g = cur[b] + (j - ls[b]);
+                a.dst.x[g] = st.x[j];
+                a.dst.y[g] = st.y[j];
+                a.dst.idx[g] = st.idx[j];
+                a.dst.key[g] = st.key[j];
+            }
+        }
+        __syncthreads();
+        for (unsigned t = threadIdx.x; t < nbins; t += kBinThreads) {
+            cur[t] += lh[t];
+            lh[t] = 0;
+        }
+        __syncthreads();
     }
 }
 
@@ -848,8 +1041,19 @@ void scan_launch(hipStream_t st, const T* in, uint64_t n, T* seg, T* grand, T* o
     scan_apply<T><<<g, kTB, 0, st>>>(in, n, seg, grand, out);
 }
 
-// Bin the window's points into tiles of `geo` (SoA copies in scratch).  keep_outside: list the
-// out-of-grid points (their count is read back into *n_outside_host).
+SoA carve_soa(void* base, uint64_t n) {
+    char* p = reinterpret_cast<char*>(base);
+    SoA o;
+    o.x = reinterpret_cast<double*>(p);
+    o.y = reinterpret_cast<double*>(p + 8 * n);
+    o.idx = reinterpret_cast<unsigned*>(p + 16 * n);
+    o.key = reinterpret_cast<unsigned*>(p + 20 * n);
+    return o;
+}
+
+// Bin the window's points into tiles of `geo` (two local-sort levels, SoA copies in scratch).
+// keep_outside: return the out-of-grid points' window indices (*outside_idx, count read back
+// into *n_outside_host).
 int bin_tiles(geohip_ctx* ctx, Scratch& S, const double* dx, const double* dy, uint64_t n, const TileGeom& geo,
               bool keep_outside, TileBins* tb, unsigned** outside_idx, unsigned* n_outside_host) {
     hipStream_t st = ctx_stream(ctx);
@@ -858,39 +1062,68 @@ int bin_tiles(geohip_ctx* ctx, Scratch& S, const double* dx, const double* dy, u
     if (nblk < 1) nblk = 1;
     const uint64_t chunk = (n + nblk - 1) / nblk;
     const uint64_t nt = geo.ntiles;
-    unsigned* hist = S.get<unsigned>(J_HIST, nblk * nt * 4);
+    const unsigned nbands = (unsigned)((nt + kBandTiles - 1) / kBandTiles);
+    const uint64_t maxitems = (n + kL2Items - 1) / kL2Items + nbands;
+    unsigned* hist1 = S.get<unsigned>(J_HIST, nblk * (nbands + 1) * 4);
+    unsigned* hist2 = S.get<unsigned>(J_SIDX, maxitems * kBandTiles * 4 + 16);
+    uint4* items = S.get<uint4>(J_SKEY, maxitems * sizeof(uint4) + 16);
+    unsigned* aux = S.get<unsigned>(J_AUX, (2 * (uint64_t)nbands + 8) * 4);  // start1 | wfirst
     unsigned* tot = S.get<unsigned>(J_TTOT, (nt + 1) * 4);
     unsigned* start = S.get<unsigned>(J_TSTART, (nt + 1) * 4);
     unsigned* seg = S.get<unsigned>(J_SEG, ((nt + kScanSeg - 1) / kScanSeg + 1) * 8 + 64);
-    double* sx = S.get<double>(J_SX, n * 8);
-    double* sy = S.get<double>(J_SY, n * 8);
-    unsigned* sidx = S.get<unsigned>(J_SIDX, n * 4);
-    unsigned* skey = S.get<unsigned>(J_SKEY, n * 4);
+    void* l1 = S.get<void>(J_SY, n * 24 + 64);
+    void* l2 = S.get<void>(J_SX, n * 24 + 64);
     unsigned* misc = S.get<unsigned>(J_MISC, kMiscWords * 4);
-    unsigned* oidx = keep_outside ? S.get<unsigned>(J_AUX, n * 4 + 16) : nullptr;
     if (S.rc) return S.rc;
     if (hipMemsetAsync(misc, 0, kMiscWords * 4, st) != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
+    unsigned* start1 = aux;
+    unsigned* wfirst = aux + nbands + 2;
+    BinPass a;
+    memset(&a, 0, sizeof a);
+    a.x = dx;
+    a.y = dy;
+    a.src = carve_soa(l1, n);
+    a.dst = a.src;
+    a.n = n;
+    a.chunk = chunk;
+    a.g = geo;
+    a.nbands = nbands;
+    a.hist = hist1;
+    a.nitems = misc + 4;
+    // level 1: bands
+    bin_count<1><<<(unsigned)nblk, kBinThreads, 0, st>>>(a);
+    bin1_offsets<<<1, kTB, 0, st>>>(hist1, (unsigned)nblk, nbands + 1, start1);
+    bin_scatter<1><<<(unsigned)nblk, kBinThreads, 0, st>>>(a);
+    // level 2: tiles within each band
+    bin2_plan<<<1, kTB, 0, st>>>(start1, nbands, items, wfirst, misc + 4);
+    a.dst = carve_soa(l2, n);
+    a.hist = hist2;
+    a.items = items;
+    bin_count<2><<<(unsigned)maxitems, kBinThreads, 0, st>>>(a);
     const unsigned tg = (unsigned)((nt + kTB - 1) / kTB);
-    tbin_count<<<(unsigned)nblk, kBinThreads, 0, st>>>(dx, dy, n, chunk, geo, hist, misc + 0);
-    tbin_totals<<<tg, kTB, 0, st>>>(hist, (unsigned)nblk, geo.ntiles, tot);
+    bin2_tiles<false><<<tg, kTB, 0, st>>>(hist2, wfirst, geo.ntiles, tot, nullptr);
     scan_launch<unsigned>(st, tot, nt, seg, misc + 2, start);
-    tbin_offsets<<<tg, kTB, 0, st>>>(hist, (unsigned)nblk, geo.ntiles, start);
-    tbin_scatter<<<(unsigned)nblk, kBinThreads, 0, st>>>(dx, dy, n, chunk, geo, hist, sx, sy, sidx, skey, oidx, misc + 1);
+    bin2_tiles<true><<<tg, kTB, 0, st>>>(hist2, wfirst, geo.ntiles, nullptr, start);
+    bin_scatter<2><<<(unsigned)maxitems, kBinThreads, 0, st>>>(a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, std::string("tile binning: ") + hipGetErrorString(e));
-    if (n_outside_host) {
+    if (keep_outside && n_outside_host) {
         uint64_t* pin = ctx_pinned(ctx);
-        if (hipMemcpyAsync(pin, misc, 4, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+        if (hipMemcpyAsync(pin, start1 + nbands, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
             return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "outside count readback failed");
-        *n_outside_host = (unsigned)(pin[0] & 0xffffffffu);
+        const unsigned valid = (unsigned)(pin[0] & 0xffffffffu);
+        *n_outside_host = (unsigned)(n - valid);
+        if (outside_idx) *outside_idx = a.src.idx + valid;
+    } else if (outside_idx) {
+        *outside_idx = nullptr;
     }
-    tb->sx = sx;
-    tb->sy = sy;
-    tb->sidx = sidx;
-    tb->skey = skey;
+    tb->sx = a.dst.x;
+    tb->sy = a.dst.y;
+    tb->sidx = a.dst.idx;
+    tb->skey = a.dst.key;
     tb->start = start;
     tb->nb = geo.nb;
-    if (outside_idx) *outside_idx = oidx;
     return GEOHIP_OK;
 }
 
