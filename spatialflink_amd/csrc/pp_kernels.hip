@@ -124,6 +124,7 @@ struct KnnBlock {
     unsigned long long bound;  // distance bits; kSentinelD = none yet
     unsigned cnt;              // survivors appended (may exceed kCap: the rest spilled)
     unsigned final_cnt;
+    unsigned next_it;          // next unclaimed 256-point iteration of the block's chunk
 };
 
 __device__ __forceinline__ int hist_bin(unsigned long long db, int base) {
@@ -742,8 +743,6 @@ __global__ __launch_bounds__(NW * 64) void knn_scan(const double* __restrict__ x
     unsigned ccnt = 0;
     unsigned appended = 0, last_hist = 0;
 
-    constexpr uint64_t kStride = (uint64_t)NW * kPtsIter;
-    uint64_t base = blk_begin + (uint64_t)wid * kPtsIter;
     double sink = 0.0;
     // G u C is one box for a point query (the candidate square contains the guaranteed one),
     // kept in registers; further boxes (unusual plans) are tested from the kernel arguments
@@ -816,16 +815,22 @@ __global__ __launch_bounds__(NW * 64) void knn_scan(const double* __restrict__ x
             }
         }
     };
-    // Software pipeline of the coordinate loads over the wave's full iterations: two register
-    // sets A and B alternate, each refilled right after use, so two iterations (8 KB per wave)
-    // are in flight while one is classified and no register copy ever waits on a load.  A
-    // partial last iteration (only in the window's last block) is handled after the loop.
+    // Iterations (256 points) of the block's chunk are claimed dynamically from an LDS counter:
+    // the memory system serves the 16 waves of a CU unevenly (phase trace: a block's last wave
+    // ended up to 6 us after its first with static striding), so a wave that is served faster
+    // takes more.  Two register sets A and B alternate as a software pipeline: each is refilled
+    // (claim + loads issued) right after use, so two iterations per wave are in flight while
+    // one is classified.  Claims are monotone per wave, so a slot holding an index past the
+    // end stays empty.  A partial iteration (only the window's last one) loads bounds-checked.
     const std::integral_constant<bool, true> kFull;
     const std::integral_constant<bool, false> kPart;
     const bool all_valid[4] = {true, true, true, true};
     double ax[4], ay[4], bx[4], by[4];
-    auto load_full = [&](uint64_t b, double (&px)[4], double (&py)[4]) {
-        const uint64_t i0 = b + 2 * (uint64_t)lane;
+    const unsigned niters = (unsigned)((blk_end - blk_begin + kPtsIter - 1) / kPtsIter);
+    auto it_base = [&](unsigned it) { return blk_begin + (uint64_t)it * kPtsIter; };
+    auto is_full = [&](unsigned it) { return it_base(it) + kPtsIter <= blk_end; };
+    auto load_full = [&](unsigned it, double (&px)[4], double (&py)[4]) {
+        const uint64_t i0 = it_base(it) + 2 * (uint64_t)lane;
         const double2 u0 = *reinterpret_cast<const double2*>(x + i0);
         const double2 u1 = *reinterpret_cast<const double2*>(x + i0 + 128);
         const double2 v0 = *reinterpret_cast<const double2*>(y + i0);
@@ -833,23 +838,39 @@ __global__ __launch_bounds__(NW * 64) void knn_scan(const double* __restrict__ x
         px[0] = u0.x; px[1] = u0.y; px[2] = u1.x; px[3] = u1.y;
         py[0] = v0.x; py[1] = v0.y; py[2] = v1.x; py[3] = v1.y;
     };
-    if (base + kPtsIter <= blk_end) load_full(base, ax, ay);
-    if (base + kStride + kPtsIter <= blk_end) load_full(base + kStride, bx, by);
+    auto claim = [&]() -> unsigned {
+        unsigned v = 0;
+        if (lane == 0) v = atomicAdd(&kb.next_it, 1u);
+        return (unsigned)__builtin_amdgcn_readfirstlane((int)v);
+    };
+    auto run = [&](unsigned it, double (&px)[4], double (&py)[4]) {
+        if (is_full(it)) {
+            iter(kFull, px, py, all_valid, it_base(it));
+        } else {
+            double qx4[4], qy4[4];
+            bool valid[4];
+            load4(x, y, it_base(it), blk_end, lane, qx4, qy4, valid);
+            iter(kPart, qx4, qy4, valid, it_base(it));
+        }
+    };
+    if (threadIdx.x == 0) kb.next_it = 2 * NW;  // iterations wid and NW + wid start statically
+    unsigned ia = (unsigned)wid, ib = (unsigned)(NW + wid);
+    if (ia < niters && is_full(ia)) load_full(ia, ax, ay);
+    if (ib < niters && is_full(ib)) load_full(ib, bx, by);
     __syncthreads();
-    while (base + kPtsIter <= blk_end) {
-        iter(kFull, ax, ay, all_valid, base);
-        if (base + 2 * kStride + kPtsIter <= blk_end) load_full(base + 2 * kStride, ax, ay);
-        base += kStride;
-        if (base + kPtsIter > blk_end) break;
-        iter(kFull, bx, by, all_valid, base);
-        if (base + 2 * kStride + kPtsIter <= blk_end) load_full(base + 2 * kStride, bx, by);
-        base += kStride;
-    }
-    if (base < blk_end) {
-        double px[4], py[4];
-        bool valid[4];
-        load4(x, y, base, blk_end, lane, px, py, valid);
-        iter(kPart, px, py, valid, base);
+    while (ia < niters || ib < niters) {
+        if (ia < niters) {
+            const unsigned na = claim();
+            run(ia, ax, ay);
+            ia = na;
+            if (ia < niters && is_full(ia)) load_full(ia, ax, ay);
+        }
+        if (ib < niters) {
+            const unsigned nb2 = claim();
+            run(ib, bx, by);
+            ib = nb2;
+            if (ib < niters && is_full(ib)) load_full(ib, bx, by);
+        }
     }
     if (MODE >= 1 && MODE <= 3) {
         if (sink == 12345.678) part_d[blockIdx.x] = 1;  // keep the ablated work alive
