@@ -2,7 +2,7 @@
 
 Default workload (the headline, BASELINE.json configs[1] = C2): one step = one window of
 point-point kNN (k = 50) of the README query over 10M uniform points per GPU (100x100 Beijing
-grid, r = 0.5): the scan kernel with its fused final selection and, for N > 1, the RCCL
+grid, r = 0.5): the scan kernel and the final selection (knn_final) and, for N > 1, the RCCL
 all-gather of each rank's top-k plus the device merge (weak scaling: every rank holds its own
 10M-point shard of the window; ranks shard by arrival order, which gives the identical result
 for a single-query kNN).
@@ -51,7 +51,9 @@ def parse():
     p.add_argument("--points", type=int, default=None, help="points per window per GPU (default: the config's)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--knn-final", choices=("fused", "separate"), default="fused",
+    p.add_argument("--time-every", type=int, default=8,
+                   help="bracket every N-th timed step's kernels with HIP events (1 = all)")
+    p.add_argument("--knn-final", choices=("fused", "separate"), default="separate",
                    help="final selection in the scan's last block, or a separate knn_final launch")
     return p.parse_args()
 
@@ -127,7 +129,7 @@ def _uniform_windows(ctx, dev, n, rank, seeds, bbox):
 class KnnWorkload(Workload):
     """C2 (BASELINE.json configs[1]): kNN k=50, 100x100, r=0.5, 10M uniform points per GPU."""
     tag = "knn_scan"
-    kernel = "geohip::knn_scan<1> (fused final selection)"
+    kernel = "geohip::knn_scan<1> + geohip::knn_final<1> (one window's scan and final selection)"
     grid_n, k, radius, n_default, seed0 = 100, 50, 0.5, 10_000_000, 2
     label = "C2: point-point kNN k=50, 100x100 Beijing UniformGrid, r=0.5, README query"
 
@@ -459,12 +461,15 @@ def main():
         wl.step(s)
     torch.cuda.synchronize(dev)
     ctx.timing(reset=True)
+    every = max(1, args.time_every)
     ctx.set_timing(True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for s in range(args.steps):
+        if every > 1:
+            ctx.set_timing(s % every == 0)
         wl.step(args.warmup + s)
     torch.cuda.synchronize(dev)
     if dist:

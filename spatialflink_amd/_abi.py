@@ -108,7 +108,7 @@ _SIGS = {
     "geohip_debug_selftest_fp64": (c_int, [_P, _P, _P, c_uint64, _P, _P, _P, _P]),
     "geohip_debug_classify": (c_int, [POINTER(Grid), c_double, c_double, c_double, _P, _P, c_uint64, _P]),
     "geohip_debug_set_knn_fused": (None, [c_int]),
-    "geohip_debug_set_knn_config": (c_int, [c_int, c_int, c_int, c_int]),
+    "geohip_debug_set_knn_config": (c_int, [c_int, c_int, c_int, c_int, c_int]),
     "geohip_debug_knn_trace": (c_int, [_P, _P, c_uint64, POINTER(c_uint32)]),
     "geohip_debug_knn_scan_variant": (c_int, [_P, c_int, POINTER(Grid), _P, _P, c_uint64, c_int, c_double,
                                               c_double, c_double, c_uint32, c_int, _P]),
@@ -170,10 +170,11 @@ def debug_set_knn_fused(fused: bool) -> None:
 
 
 def debug_set_knn_config(waves_per_block: int = 16, prefetch: int = 1, ticket_groups: int = 16,
-                         epi_sort: int = 0) -> None:
+                         epi_sort: int = 0, interleave: int = 0) -> None:
     """Measurement hook: kNN scan launch shape (waves per block 4/8/16, load pipeline depth
-    1/2, arrival-ticket groups 1..64, block list by register sort (1) or rank placement (0))."""
-    if lib.geohip_debug_set_knn_config(waves_per_block, prefetch, ticket_groups, epi_sort):
+    1/2, arrival-ticket groups 1..64, block list by register sort (1) or rank placement (0),
+    iterations in contiguous block chunks (0) or interleaved over the blocks (1))."""
+    if lib.geohip_debug_set_knn_config(waves_per_block, prefetch, ticket_groups, epi_sort, interleave):
         raise GeohipArgumentError(f"unsupported kNN shape {waves_per_block}/{prefetch}/{ticket_groups}/{epi_sort}")
 
 
@@ -291,23 +292,31 @@ class Context:
         self._check(rc, "knn_pp")
         return oi[:cnt.value], od[:cnt.value]
 
+    # async forms: device tensors only, no host sync; the hot per-window path, so the pointers
+    # go to ctypes as plain ints (argtypes c_void_p) without wrapper objects
     def knn_pp_async(self, grid: Grid, x, y, qx, qy, r, k, out_idx, out_dist, out_count):
-        self.set_mem(MEM_DEVICE)
-        rc = lib.geohip_knn_pp_async(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), len(x), qx, qy, r, k,
-                                     _ptr(out_idx), _ptr(out_dist), _ptr(out_count))
-        self._check(rc, "knn_pp_async")
+        if self._mem != MEM_DEVICE:
+            self.set_mem(MEM_DEVICE)
+        rc = lib.geohip_knn_pp_async(self.h, ctypes.byref(grid), x.data_ptr(), y.data_ptr(), x.numel(), qx, qy, r, k,
+                                     out_idx.data_ptr(), out_dist.data_ptr(), out_count.data_ptr())
+        if rc:
+            self._check(rc, "knn_pp_async")
 
     def knn_merge_async(self, dist, idx, nlists, list_len, k, out_idx, out_dist, out_count):
-        self.set_mem(MEM_DEVICE)
-        rc = lib.geohip_knn_merge_async(self.h, _ptr(dist), _ptr(idx), nlists, list_len, k, _ptr(out_idx),
-                                        _ptr(out_dist), _ptr(out_count))
-        self._check(rc, "knn_merge_async")
+        if self._mem != MEM_DEVICE:
+            self.set_mem(MEM_DEVICE)
+        rc = lib.geohip_knn_merge_async(self.h, dist.data_ptr(), idx.data_ptr(), nlists, list_len, k,
+                                        out_idx.data_ptr(), out_dist.data_ptr(), out_count.data_ptr())
+        if rc:
+            self._check(rc, "knn_merge_async")
 
     def range_pp_async(self, grid: Grid, x, y, qx, qy, r, approximate, out_idx, cap, out_count):
-        self.set_mem(MEM_DEVICE)
-        rc = lib.geohip_range_pp_async(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), len(x), qx, qy, r,
-                                       int(approximate), _ptr(out_idx), cap, _ptr(out_count))
-        self._check(rc, "range_pp_async")
+        if self._mem != MEM_DEVICE:
+            self.set_mem(MEM_DEVICE)
+        rc = lib.geohip_range_pp_async(self.h, ctypes.byref(grid), x.data_ptr(), y.data_ptr(), x.numel(), qx, qy, r,
+                                       int(approximate), out_idx.data_ptr(), cap, out_count.data_ptr())
+        if rc:
+            self._check(rc, "range_pp_async")
 
     def join_pp(self, grid_data: Grid, grid_query: Grid, dx, dy, qx, qy, r, approximate=False, cap=None, out=None):
         """Pairs (data idx, query idx).  ``out`` (optional): a preallocated [cap, 2] u32/i32 buffer on

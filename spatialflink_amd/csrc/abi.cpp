@@ -43,6 +43,11 @@ struct geohip_ctx {
     std::vector<hipEvent_t> pool;
     double acc_ms = 0.0;
     uint64_t launches = 0;
+    // last point plan: a continuous query plans the same (grid, q, r) for every window
+    bool plan_valid = false;
+    geohip_grid plan_grid{};
+    double plan_q[3] = {0, 0, 0};
+    PointPlan plan{};
 };
 
 namespace {
@@ -102,8 +107,12 @@ int ensure_zeroed(geohip_ctx* ctx, Slot s, size_t bytes) {
 int begin(geohip_ctx* ctx) {
     if (!ctx) return GEOHIP_ERR_ARG;
     ctx->err.clear();
-    hipError_t e = hipSetDevice(ctx->device);
-    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    // switch the calling thread's device only when it differs (hipGetDevice reads thread state)
+    int current = -1;
+    if (hipGetDevice(&current) != hipSuccess || current != ctx->device) {
+        hipError_t e = hipSetDevice(ctx->device);
+        if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    }
     return GEOHIP_OK;
 }
 
@@ -151,9 +160,18 @@ int stage_xy(geohip_ctx* ctx, const double* x, const double* y, uint64_t n, Slot
 
 int plan_or_fail(geohip_ctx* ctx, const geohip_grid* grid, double qx, double qy, double r, PointPlan* plan) {
     if (!grid) return fail(ctx, GEOHIP_ERR_ARG, "null grid");
+    const double q[3] = {qx, qy, r};
+    if (ctx->plan_valid && memcmp(&ctx->plan_grid, grid, sizeof(geohip_grid)) == 0 && memcmp(ctx->plan_q, q, sizeof q) == 0) {
+        *plan = ctx->plan;  // bitwise-identical inputs: the same plan
+        return GEOHIP_OK;
+    }
     std::string err;
     int rc = plan_point(*grid, qx, qy, r, plan, nullptr, nullptr, &err);
     if (rc) return fail(ctx, rc, err);
+    ctx->plan_valid = true;
+    memcpy(&ctx->plan_grid, grid, sizeof(geohip_grid));
+    memcpy(ctx->plan_q, q, sizeof q);
+    ctx->plan = *plan;
     return GEOHIP_OK;
 }
 
@@ -647,8 +665,8 @@ int geohip_debug_selftest_fp64(geohip_ctx* ctx, const double* a, const double* b
 
 // Debug hook: 1 = final selection fused into the scan (default), 0 = separate knn_final launch.
 void geohip_debug_set_knn_fused(int fused) { set_knn_fused(fused); }
-int geohip_debug_set_knn_config(int waves_per_block, int prefetch, int ticket_groups, int epi_sort) {
-    return set_knn_config(waves_per_block, prefetch, ticket_groups, epi_sort) ? GEOHIP_ERR_ARG : GEOHIP_OK;
+int geohip_debug_set_knn_config(int waves_per_block, int prefetch, int ticket_groups, int epi_sort, int interleave) {
+    return set_knn_config(waves_per_block, prefetch, ticket_groups, epi_sort, interleave) ? GEOHIP_ERR_ARG : GEOHIP_OK;
 }
 
 }  // extern "C"

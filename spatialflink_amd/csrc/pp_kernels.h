@@ -40,9 +40,9 @@ void set_knn_fused(int fused);
 // kNN scan launch shape: waves per block (4, 8, 16), load pipeline depth (1, 2), arrival
 // ticket groups (1 .. 64).  Returns -1 for an unsupported shape.
 struct KnnConfig {
-    int nw, pf, groups, epi_sort;
+    int nw, pf, groups, epi_sort, interleave;
 };
-int set_knn_config(int nw, int pf, int groups, int epi_sort);
+int set_knn_config(int nw, int pf, int groups, int epi_sort, int interleave);
 KnnConfig knn_config();
 // trace buffer of knn_scan MODE 6 (8 * (nblocks + 1) u64, device)
 hipError_t set_knn_trace(unsigned long long* buf);

@@ -730,8 +730,11 @@ __global__ __launch_bounds__(NW * 64) void knn_scan(const double* __restrict__ x
     const int lane = lane_id();
     const int wid = threadIdx.x / kWave;
     WaveStage& st = stage[wid];
-    const uint64_t blk_begin = (uint64_t)blockIdx.x * chunk;
-    uint64_t blk_end = blk_begin + chunk;
+    // chunk > 0: block b owns [b chunk, (b + 1) chunk); chunk == 0: iterations interleaved
+    // over the blocks (block b takes the window's iterations b, b + nblocks, ...)
+    const bool inter = chunk == 0;
+    const uint64_t blk_begin = inter ? 0 : (uint64_t)blockIdx.x * chunk;
+    uint64_t blk_end = inter ? n : blk_begin + chunk;
     if (blk_end > n) blk_end = n;
     for (int t = threadIdx.x; t < kHistBins; t += NT) kb.hist[t] = 0;
     if (threadIdx.x == 0) {
@@ -826,8 +829,12 @@ __global__ __launch_bounds__(NW * 64) void knn_scan(const double* __restrict__ x
     const std::integral_constant<bool, false> kPart;
     const bool all_valid[4] = {true, true, true, true};
     double ax[4], ay[4], bx[4], by[4];
-    const unsigned niters = (unsigned)((blk_end - blk_begin + kPtsIter - 1) / kPtsIter);
-    auto it_base = [&](unsigned it) { return blk_begin + (uint64_t)it * kPtsIter; };
+    const uint64_t n_it = (n + kPtsIter - 1) / kPtsIter;
+    const unsigned niters = inter ? (blockIdx.x < n_it ? (unsigned)((n_it - blockIdx.x + gridDim.x - 1) / gridDim.x) : 0u)
+                                  : (unsigned)((blk_end - blk_begin + kPtsIter - 1) / kPtsIter);
+    auto it_base = [&](unsigned it) {
+        return inter ? ((uint64_t)it * gridDim.x + blockIdx.x) * kPtsIter : blk_begin + (uint64_t)it * kPtsIter;
+    };
     auto is_full = [&](unsigned it) { return it_base(it) + kPtsIter <= blk_end; };
     auto load_full = [&](unsigned it, double (&px)[4], double (&py)[4]) {
         const uint64_t i0 = it_base(it) + 2 * (uint64_t)lane;
@@ -1191,7 +1198,7 @@ __global__ void selftest_fp64(const double* __restrict__ a, const double* __rest
 }
 
 // ============================================================================ launchers ===
-static int g_knn_fused = 1;
+static int g_knn_fused = 0;  // separate knn_final launch: measured faster than the fused tail (profiles/r01_knn_shape_sweep_dynamic.log, mode 9 vs 0)
 void set_knn_fused(int fused) { g_knn_fused = fused; }
 
 template <int KPL>
@@ -1205,16 +1212,16 @@ static void launch_knn_final_heads(unsigned long long* part_d, unsigned* part_i,
     knn_final<KPL><<<1, kFinalThreads, 0, st>>>(io);
 }
 
-static KnnConfig g_knn_cfg = {16, 1, 16, 0};  // fastest measured shape (profiles/r01_knn_shape_sweep.log)
+static KnnConfig g_knn_cfg = {16, 1, 16, 0, 0};  // fastest measured shape (profiles/r01_knn_shape_sweep.log)
 
 hipError_t set_knn_trace(unsigned long long* buf) {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_knn_trace), &buf, sizeof(buf));
 }
 
-int set_knn_config(int nw, int pf, int groups, int epi_sort) {
+int set_knn_config(int nw, int pf, int groups, int epi_sort, int interleave) {
     if (!(nw == 4 || nw == 8 || nw == 16) || !(pf == 1 || pf == 2) || groups < 1 || groups > (int)kMaxTicketGroups)
         return -1;
-    g_knn_cfg = KnnConfig{nw, pf, groups, epi_sort ? 1 : 0};
+    g_knn_cfg = KnnConfig{nw, pf, groups, epi_sort ? 1 : 0, interleave ? 1 : 0};
     return 0;
 }
 KnnConfig knn_config() { return g_knn_cfg; }
@@ -1223,6 +1230,12 @@ void knn_geometry(uint64_t n, unsigned* nblocks, uint64_t* chunk) {
     // 16 waves per CU on all 256 CUs when n is large (equal work per block); an even chunk keeps
     // the 16-byte double2 loads aligned
     const uint64_t target = 256ull * (16 / (unsigned)g_knn_cfg.nw);
+    if (g_knn_cfg.interleave) {  // chunk 0: iterations interleaved over the blocks
+        const uint64_t n_it = (n + kPtsIter - 1) / kPtsIter;
+        *chunk = 0;
+        *nblocks = (unsigned)(n_it < target ? n_it : target);
+        return;
+    }
     uint64_t c = (n + target - 1) / target;
     c = (c + kPtsIter - 1) / kPtsIter * kPtsIter;  // whole wave iterations (aligned double2 loads)
     if (c < 1024) c = 1024;
@@ -1276,14 +1289,17 @@ hipError_t launch_knn(const double* x, const double* y, uint64_t n, const KnnArg
         case 4: knn_scan_launch<4, 0>(nblocks, st, x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, out); break;
         default: return hipErrorInvalidValue;
     }
-    if (ev1) (void)hipEventRecord(ev1, st);
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess || g_knn_fused) return e;
+    if (e != hipSuccess || g_knn_fused) {
+        if (ev1) (void)hipEventRecord(ev1, st);
+        return e;
+    }
     switch (kpl) {
         case 1: launch_knn_final_heads<1>(part_d, part_i, nblocks, k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt, args.hist_base, st); break;
         case 2: launch_knn_final_heads<2>(part_d, part_i, nblocks, k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt, args.hist_base, st); break;
         default: launch_knn_final_heads<4>(part_d, part_i, nblocks, k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt, args.hist_base, st); break;
     }
+    if (ev1) (void)hipEventRecord(ev1, st);  // timed region: the scan and the final selection
     return hipGetLastError();
 }
 

@@ -378,12 +378,21 @@ def test_knn_equal_distance_shell(ctx):
         assert oi.tolist() == wi.tolist() and np.array_equal(od.view(np.uint64), wd.view(np.uint64))
 
 
-def test_knn_query_duplicates_spill_and_repeat(ctx):
+@pytest.mark.parametrize("fused", [False, True])
+def test_knn_query_duplicates_spill_and_repeat(ctx, fused):
     """Thousands of exact copies of the query point in consecutive window slots: one scan
     block keeps far more than its LDS survivor buffer (spill path), the head histogram's k-th
     bin is the lowest (exact-T fallback) or the gather overflows (k-round fallback).  Every
     call is repeated on the same context: the fused final's arrival ticket and the spill
-    count must be back at zero after each launch."""
+    count must be back at zero after each launch (both final-selection forms)."""
+    _abi.debug_set_knn_fused(fused)
+    try:
+        _dup_spill_repeat(ctx)
+    finally:
+        _abi.debug_set_knn_fused(False)
+
+
+def _dup_spill_repeat(ctx):
     ag, cg = agrid(100)
     rng = np.random.default_rng(17)
     x, y = _window(rng, 2_000_000)
@@ -404,15 +413,15 @@ def test_knn_query_duplicates_spill_and_repeat(ctx):
     assert oi.tolist() == wi.tolist() and np.array_equal(od.view(np.uint64), wd.view(np.uint64))
 
 
-def test_knn_separate_final_launch(ctx):
-    """The same results with the final selection as a separate knn_final launch (packed heads,
-    head histogram) instead of the scan's last-arriving block."""
+def test_knn_fused_final_select(ctx):
+    """The same results with the final selection fused into the scan's last-arriving block
+    (arrival tickets, sc1 lists) instead of the default separate knn_final launch."""
     ag, cg = agrid(100)
     rng = np.random.default_rng(23)
     x, y = _window(rng, 1_500_000, nan_every=1009)
     x[400000:403000] = Q[0]
     y[400000:403000] = Q[1]
-    _abi.debug_set_knn_fused(False)
+    _abi.debug_set_knn_fused(True)
     try:
         for (xx, yy) in ((x, y), (x[3000:], y[3000:]), (x[403000:], y[403000:])):
             for k in (1, 50, 129, 256):
@@ -420,4 +429,4 @@ def test_knn_separate_final_launch(ctx):
                 oi, od = ctx.knn_pp(ag, xx, yy, Q[0], Q[1], 0.5, k)
                 assert oi.tolist() == wi.tolist() and np.array_equal(od.view(np.uint64), wd.view(np.uint64))
     finally:
-        _abi.debug_set_knn_fused(True)
+        _abi.debug_set_knn_fused(False)
