@@ -263,7 +263,7 @@ class JoinWorkload(Workload):
     """C3 (BASELINE.json configs[2]): 10k queries x 10M Gaussian-clustered data points per
     window, 500x500, r = 0.05 (32 shared centres, sigma 0.1)."""
     tag = "join_probe"
-    kernel = "geohip::join_probe (after the counting sort bucket_count/scan/bucket_scatter)"
+    kernel = "geohip::join_tile count + write passes (tile binning before the timed region)"
     grid_n, radius, n_default, nq, sigma = 500, 0.05, 10_000_000, 10_000, 0.1
     windows = 2
 
@@ -331,7 +331,7 @@ class PpolyWorkload(Workload):
     """C4 (BASELINE.json configs[3]): 1k star polygons (50 vertices) over 50M uniform points per
     window, 500x500, r = 0.005 (conf/geoflink-conf.yml:52)."""
     tag = "ppoly_probe"
-    kernel = "geohip::ppoly_probe (after the counting sort bucket_count/scan/bucket_scatter)"
+    kernel = "geohip::ppoly_eval + ppoly_emit (tile binning before the timed region)"
     grid_n, radius, n_default, npoly = 500, 0.005, 50_000_000, 1000
     windows = 2
 
@@ -395,7 +395,7 @@ class C5Workload(KnnWorkload):
     """C5 per shard (BASELINE.json configs[4]): 1000x1000 grid, 25M uniform points per GPU
     (200M per window on 8 GPUs), kNN k=100 + range r=0.05 of the README query."""
     tag = "knn_scan_c5"
-    kernel = "geohip::knn_scan<2> + range pass"
+    kernel = "geohip::knn_scan<2> + knn_final<2>, range pass (two timed launches per step)"
     grid_n, k, radius, n_default, seed0 = 1000, 100, 0.05, 25_000_000, 7
     windows = 2
     label = "C5 shard: kNN k=100 + range r=0.05, 1000x1000 Beijing UniformGrid, README query"

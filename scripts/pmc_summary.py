@@ -14,8 +14,13 @@ from collections import defaultdict
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-TAGS = {"knn": ("knn_scan", "knn_scan"), "range": ("range", "range_"), "join": ("join_probe", "join_probe"),
-        "ppoly": ("ppoly_probe", "ppoly_probe"), "c5": ("knn_scan_c5", "knn_scan")}
+# workload -> (profiles tag, kernel-name substrings of the bench's timed region, timed launches per step)
+TAGS = {"knn": ("knn_scan", ("knn_scan", "knn_final"), 1),
+        "range": ("range", ("range_scan", "scan_units", "range_emit"), 1),
+        "join": ("join_probe", ("join_tile", "scan_seg_totals<unsigned long long>", "scan_totals<unsigned long long>",
+                                 "scan_apply<unsigned long long>"), 1),
+        "ppoly": ("ppoly_probe", ("ppoly_eval", "ppoly_emit", "ppoly_outside"), 1),
+        "c5": ("knn_scan_c5", ("knn_scan", "knn_final", "range_scan", "scan_units", "range_emit"), 2)}
 
 
 def per_kernel(path):
@@ -31,7 +36,7 @@ def main():
     d = Path(sys.argv[1])
     rnd = sys.argv[2] if len(sys.argv) > 2 else "r01"
     out_all = {}
-    for w, (tag, match) in TAGS.items():
+    for w, (tag, match, per_step) in TAGS.items():
         fs, ws = d / f"{w}_FETCH_SIZE_counter_collection.csv", d / f"{w}_WRITE_SIZE_counter_collection.csv"
         if not fs.exists() or not ws.exists():
             continue
@@ -42,11 +47,12 @@ def main():
             wr = W.get(k, [0.0])
             kernels[k] = {"dispatches": len(f), "fetch_kb_raw_avg": sum(f) / len(f),
                           "hbm_read_bytes_avg": 2 * 1024 * sum(f) / len(f), "hbm_write_bytes_avg": 1024 * sum(wr) / len(wr)}
-        hot = [k for k in kernels if match in k]
-        per_launch = sum(kernels[k]["hbm_read_bytes_avg"] + kernels[k]["hbm_write_bytes_avg"] for k in hot)
+        hot = [k for k in kernels if any(m in k for m in match)]
+        per_launch = sum(kernels[k]["hbm_read_bytes_avg"] + kernels[k]["hbm_write_bytes_avg"] for k in hot) / per_step
         rec = {"workload": w, "kernels_matched": hot, "hbm_bytes_per_launch": per_launch, "kernels": kernels,
                "note": "FETCH_SIZE x 2 (gfx950 streaming-read correction) + WRITE_SIZE, KB = 1024 B; "
-                       "per dispatch averaged over all dispatches of the matched kernels in a 5-step bench run"}
+                       "per timed launch: the matched kernels' average bytes per dispatch summed over one step "
+                       "(each runs once per step) / timed launches per step; 5-step bench run"}
         (ROOT / "profiles" / f"pmc_{tag}.json").write_text(json.dumps(rec, indent=1) + "\n")
         out_all[w] = per_launch
         print(w, hot, f"{per_launch / 1e6:.1f} MB per launch")
