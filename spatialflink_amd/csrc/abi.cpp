@@ -25,7 +25,7 @@ enum Slot {
     S_X, S_Y, S_QX, S_QY, S_GTHR, S_PART_D, S_PART_I, S_OUT_D, S_OUT_I, S_OUT_CNT,
     S_MASK, S_UCNT, S_OFFS, S_TOTAL, S_OUT_IDX, S_OUT_PAIRS, S_SPILL_D, S_SPILL_I, S_SPILL_CNT,
     S_J0, S_J1, S_J2, S_J3, S_J4, S_J5, S_J6, S_J7, S_J8, S_J9, S_J10, S_J11, S_J12, S_J13, S_J14, S_J15,
-    S_J16, S_J17, S_J18, S_J19,
+    S_J16, S_J17, S_J18, S_J19, S_J20, S_J21, S_J22, S_J23,
     S_COUNT
 };
 

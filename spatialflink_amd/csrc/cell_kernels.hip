@@ -517,14 +517,17 @@ __global__ void jq_build(const QRect* __restrict__ rect, uint64_t nq, TileGeom g
 // LDS 256 at a time; every wave streams 64 of the tile's points per pass against all of them.
 // Emit (p, q) iff key(p) lies in q's Nbr block and (approximate or dist(p, q) <= r)
 // (PointPointJoinQuery.java:156-160): squared screens first, the exact JTS distance in the band.
-// WRITE = false: count pass (pairs per tile into sink.bcount); true: write pass.
+// WRITE = false: count pass (pairs per tile into sink.bcount; with `mask`, every (64-point
+// chunk, candidate query) ballot as one word at mask[moff[tile] + chunk * nqt + candidate],
+// for join_emit); true: write pass that recomputes (used when the masks would be too large).
 template <bool APPROX, bool WRITE>
 __global__ __launch_bounds__(kTB) void join_tile(TileBins tb, const unsigned* __restrict__ qstart,
                                                  const unsigned* __restrict__ qlist,
                                                  const unsigned* __restrict__ glist, const unsigned* __restrict__ gcnt,
                                                  const double* __restrict__ qx, const double* __restrict__ qy,
                                                  const QRect* __restrict__ rect, double r, double r2lo, double r2hi,
-                                                 PairSink sink) {
+                                                 PairSink sink, unsigned long long* __restrict__ mask,
+                                                 const unsigned long long* __restrict__ moff) {
     __shared__ double lqx[kTB], lqy[kTB];
     __shared__ QRect lrect[kTB];
     __shared__ unsigned lqi[kTB];
@@ -566,6 +569,10 @@ __global__ __launch_bounds__(kTB) void join_tile(TileBins tb, const unsigned* __
                 cx = (int32_t)(key / nb);
                 cy = (int32_t)(key - (unsigned)cx * nb);
             }
+            // this chunk's mask row (count pass with masks)
+            unsigned long long* mrow = (!WRITE && mask) ? mask + moff[tile] + (size_t)((base - ds) / kWave) * nqt + qb
+                                                        : nullptr;
+            unsigned acc_lo = 0, acc_hi = 0;
             for (unsigned j = 0; j < nbq; j++) {
                 const QRect R = lrect[j];
                 bool hit = cx >= R.x0 && cx <= R.x1 && cy >= R.y0 && cy <= R.y1;
@@ -578,11 +585,79 @@ __global__ __launch_bounds__(kTB) void join_tile(TileBins tb, const unsigned* __
                         else hit = jts_pp_distance(px, py, ox, oy) <= r;  // getDistance(p, q)
                     }
                 }
-                pairs_push<WRITE, kWavePairs>(buf, cnt, hit, pid, lqi[j], &bsh, sink);
+                if (WRITE) {
+                    pairs_push<WRITE, kWavePairs>(buf, cnt, hit, pid, lqi[j], &bsh, sink);
+                } else {
+                    const unsigned long long m = __ballot(hit);
+                    cnt += (unsigned long long)__popcll(m);
+                    if (mrow) {  // lane j % 64 keeps word j; 64 words leave as one coalesced store
+                        if ((unsigned)lane == (j & 63u)) {
+                            acc_lo = (unsigned)m;
+                            acc_hi = (unsigned)(m >> 32);
+                        }
+                        if ((j & 63u) == 63u || j + 1 == nbq) {
+                            if ((unsigned)lane <= (j & 63u))
+                                mrow[(j & ~63u) + lane] = ((unsigned long long)acc_hi << 32) | acc_lo;
+                        }
+                    }
+                }
             }
         }
     }
     pairs_end<WRITE>(buf, cnt, &bsh, sink);
+}
+
+// mask words of each tile: (64-point chunks) x (candidate queries)
+__global__ void join_words(const unsigned* __restrict__ tstart, const unsigned* __restrict__ qstart,
+                           const unsigned* __restrict__ gcnt, uint32_t ntiles, unsigned long long* __restrict__ words) {
+    const unsigned t = blockIdx.x * kTB + threadIdx.x;
+    if (t >= ntiles) return;
+    const unsigned n = tstart[t + 1] - tstart[t];
+    const unsigned nqt = qstart[t + 1] - qstart[t] + *gcnt;
+    words[t] = (n == 0 || nqt == 0) ? 0ull : (unsigned long long)((n + 63) / 64) * nqt;
+}
+
+// Write pass from the count pass's masks: pairs (p, q) of every set bit, one workgroup per tile.
+__global__ __launch_bounds__(kTB) void join_emit(TileBins tb, const unsigned* __restrict__ qstart,
+                                                 const unsigned* __restrict__ qlist, const unsigned* __restrict__ glist,
+                                                 const unsigned* __restrict__ gcnt,
+                                                 const unsigned long long* __restrict__ mask,
+                                                 const unsigned long long* __restrict__ moff, PairSink sink) {
+    __shared__ uint2 pbuf[kTB / kWave][kWavePairs];
+    __shared__ unsigned long long bsh;
+    const unsigned tile = blockIdx.x;
+    const unsigned ds = tb.start[tile], de = tb.start[tile + 1];
+    const unsigned qs = qstart[tile], nql = qstart[tile + 1] - qs;
+    const unsigned nqt = nql + *gcnt;
+    if (ds == de || nqt == 0) return;
+    if (threadIdx.x == 0) bsh = 0;
+    __syncthreads();
+    const int wid = threadIdx.x / kWave, lane = lane_id();
+    uint2* buf = pbuf[wid];
+    unsigned long long cnt = 0;
+    const unsigned nchunks = (de - ds + 63) / 64;
+    const unsigned long long* mt = mask + moff[tile];
+    for (unsigned c = wid; c < nchunks; c += kTB / kWave) {
+        const unsigned i = ds + c * 64 + lane;
+        const unsigned pid = i < de ? tb.sidx[i] : 0u;
+        const unsigned long long* row = mt + (size_t)c * nqt;
+        for (unsigned j0 = 0; j0 < nqt; j0 += 64) {
+            const unsigned jj = j0 + lane;
+            const unsigned long long w = jj < nqt ? row[jj] : 0ull;
+            const unsigned qid = jj < nqt ? (jj < nql ? qlist[qs + jj] : glist[jj - nql]) : 0u;
+            unsigned long long nz = __ballot(w != 0);
+            while (nz) {
+                const int t = __builtin_ctzll(nz);
+                nz &= nz - 1;
+                const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)w, t);
+                const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(w >> 32), t);
+                const unsigned long long wt = ((unsigned long long)hi << 32) | lo;
+                const unsigned qt = (unsigned)__builtin_amdgcn_readlane((int)qid, t);
+                pairs_push<true, kWavePairs>(buf, cnt, (wt >> lane) & 1ull, pid, qt, &bsh, sink);
+            }
+        }
+    }
+    pairs_end<true>(buf, cnt, &bsh, sink);
 }
 
 // ------------------------------------------------------------------ point-polygon --------
@@ -990,8 +1065,11 @@ namespace {
 
 enum JSlot {
     J_HIST, J_TTOT, J_TSTART, J_SEG, J_SX, J_SY, J_SIDX, J_SKEY, J_MISC, J_AUX, J_POLY, J_OUT, J_RECT, J_QSTART,
-    J_QLIST, J_GLIST, J_QCNT, J_BCNT, J_BOFF, J_PMASK
+    J_QLIST, J_GLIST, J_QCNT, J_BCNT, J_BOFF, J_PMASK, J_MWORDS, J_MOFF
 };
+
+// join hit masks larger than this fall back to a recomputing write pass
+constexpr uint64_t kJoinMaskBudget = 4ull << 30;
 
 // J_MISC words: [0] outside count, [1] outside cursor, [2] scan grand total, [3] global
 // query count, [8..9] pair total (u64)
@@ -1260,21 +1338,40 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
     screen_bounds(r, &r2lo, &r2hi);
     if (hipMemsetAsync(bcount, 0, (uint64_t)geo.ntiles * 8, st) != hipSuccess)
         return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
+    const bool work = nq && nd;
+    // hit masks (count pass -> write pass): sized on the device, one readback
+    unsigned long long* mask = nullptr;
+    unsigned long long* moff = nullptr;
+    if (work && out) {
+        unsigned long long* words = S.get<unsigned long long>(J_MWORDS, ((uint64_t)geo.ntiles + 1) * 8);
+        moff = S.get<unsigned long long>(J_MOFF, ((uint64_t)geo.ntiles + 1) * 8);
+        if (S.rc) return S.rc;
+        join_words<<<(geo.ntiles + kTB - 1) / kTB, kTB, 0, st>>>(tb.start, qstart, misc + 3, geo.ntiles, words);
+        scan_launch<unsigned long long>(st, words, geo.ntiles, reinterpret_cast<unsigned long long*>(seg),
+                                        reinterpret_cast<unsigned long long*>(misc + 8), moff);
+        uint64_t nwords = 0;
+        rc = read_total(ctx, moff + geo.ntiles, &nwords);
+        if (rc) return rc;
+        if (nwords * 8 <= kJoinMaskBudget) {
+            mask = S.get<unsigned long long>(J_PMASK, nwords * 8 + 8);
+            if (S.rc) return S.rc;
+        }
+    }
     hipEvent_t e0, e1;
     ctx_timing_events(ctx, &e0, &e1);
     if (e0) hipEventRecord(e0, st);
-    const bool work = nq && nd;
-#define GEOHIP_JOIN(A, W) \
-    join_tile<A, W><<<geo.ntiles, kTB, 0, st>>>(tb, qstart, qlist, glist, misc + 3, dqx, dqy, drect, r, r2lo, r2hi, sink)
+#define GEOHIP_JOIN(A, W, M) \
+    join_tile<A, W><<<geo.ntiles, kTB, 0, st>>>(tb, qstart, qlist, glist, misc + 3, dqx, dqy, drect, r, r2lo, r2hi, sink, M, moff)
     if (work) {
-        if (approximate) GEOHIP_JOIN(true, false);
-        else GEOHIP_JOIN(false, false);
+        if (approximate) GEOHIP_JOIN(true, false, mask);
+        else GEOHIP_JOIN(false, false, mask);
     }
     scan_launch<unsigned long long>(st, bcount, geo.ntiles, reinterpret_cast<unsigned long long*>(seg),
                                     reinterpret_cast<unsigned long long*>(misc + 8), boff);
     if (work && out) {
-        if (approximate) GEOHIP_JOIN(true, true);
-        else GEOHIP_JOIN(false, true);
+        if (mask) join_emit<<<geo.ntiles, kTB, 0, st>>>(tb, qstart, qlist, glist, misc + 3, mask, moff, sink);
+        else if (approximate) GEOHIP_JOIN(true, true, nullptr);
+        else GEOHIP_JOIN(false, true, nullptr);
     }
 #undef GEOHIP_JOIN
     if (e1) hipEventRecord(e1, st);
