@@ -16,11 +16,22 @@ PointPointRangeQuery.java:111-116, PointPointKNNQuery.java:146-151; windowAll me
   the same device kernel (geohip_knn_merge_async) -> identical results on all ranks.  This
   replaces the reference's parallelism-1 windowAll funnel.
 
+* join (PointPointJoinQuery.java:113-172): the query window is small (C3: 10k x 16 B) and is
+  present on every rank.  ``partition="arrival"``: data stays where it arrived and every rank
+  joins its shard against all queries (no data exchange; the query block replication of
+  JoinQuery.getReplicatedPointQueryStream degenerates to "every rank").  ``partition="cells"``
+  mirrors keyBy(gridID) with halo replication: rank s owns the x-major key band of grid columns
+  [ceil(s n / W), ceil((s+1) n / W)), data points move to their owner with one all-to-all, and
+  each rank keeps only the queries whose Nbr block (cell +- Lc columns, one spare column) meets
+  its band.  Both give disjoint per-rank pair sets whose union is the window's result;
+* point-polygon range: the polygons (C4: 1k x 51 vertices) are on every rank, points stay.
+
 The local engine and the merge are injectable so the orchestration is testable with the
 gloo backend on CPU (tests/test_distributed_gloo.py); by default both are libgeohip.
 """
 from __future__ import annotations
 
+import math
 from dataclasses import dataclass
 from typing import Callable, Optional
 
@@ -89,6 +100,92 @@ def range_sharded(x_local, y_local, base: int, qx: float, qy: float, r: float, a
     return hits, offset, total
 
 
+def _java_cell(v, mn: float, l: float):
+    """(int)Math.floor((v - mn) / l) per element (HelperClass.java:109-110): fp64 as the
+    reference evaluates it, NaN -> 0, saturating int cast."""
+    import torch
+
+    t = torch.floor((v - mn) / l)
+    t = torch.where(torch.isnan(t), torch.zeros_like(t), t)
+    return t.clamp(-2147483648.0, 2147483647.0).to(torch.int64)
+
+
+def key_band(world: int, rank: int, nb: int):
+    """Grid columns [lo, hi) owned by `rank` when column cx belongs to rank cx * world // nb."""
+    return (rank * nb + world - 1) // world, ((rank + 1) * nb + world - 1) // world
+
+
+def join_sharded(dx_local, dy_local, dbase: int, qx, qy, r: float, approximate: bool = False, *, grid_data,
+                 grid_query, ctx=None, group=None, partition: str = "arrival", local_join: Optional[Callable] = None):
+    """Point-point join of one window over the group.  dx/dy_local: this rank's data shard
+    (window indices dbase + local position); qx/qy: the whole query window (every rank).
+    Returns (pairs int64 [m, 2] = (data window idx, query idx) of this rank, output offset,
+    total pairs); the per-rank pair sets are disjoint and their union is the window's join."""
+    import torch
+    import torch.distributed as dist
+
+    if local_join is None:
+        local_join = _device_local_join(ctx, grid_data, grid_query)
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if partition == "arrival" or world == 1:
+        pairs = local_join(dx_local, dy_local, qx, qy, r, approximate).to(torch.int64)
+        pairs[:, 0] += dbase
+    elif partition == "cells":
+        nb = int(grid_query.n)
+        cx = _java_cell(dx_local, grid_data.min_x, grid_data.cell_len)
+        cy = _java_cell(dy_local, grid_data.min_y, grid_data.cell_len)
+        valid = (cx >= 0) & (cx < nb) & (cy >= 0) & (cy < nb)  # other keys match no Nbr block
+        gidx = torch.arange(len(dx_local), dtype=torch.int64, device=dx_local.device) + dbase
+        owner = (cx * world) // nb
+        sel = torch.nonzero(valid).flatten()
+        order = sel[torch.argsort(owner[sel], stable=True)]
+        send_counts = torch.bincount(owner[order], minlength=world).to(torch.int64)
+        recv_counts = torch.empty_like(send_counts)
+        dist.all_to_all_single(recv_counts, send_counts, group=group)
+        sc, rc = send_counts.tolist(), recv_counts.tolist()
+        nrecv = sum(rc)
+
+        def exchange(t):
+            out = torch.empty(nrecv, dtype=t.dtype, device=t.device)
+            dist.all_to_all_single(out, t[order].contiguous(), rc, sc, group=group)
+            return out
+
+        rx, ry, rg = exchange(dx_local), exchange(dy_local), exchange(gidx)
+        lo, hi = key_band(world, rank, nb)
+        lq = float(grid_query.cell_len)
+        qcx = _java_cell(qx, grid_query.min_x, lq)
+        lc = math.ceil(r / lq) if r == r and abs(r / lq) < 2.0 ** 31 else nb
+        if r == 0 or lc >= nb:  # every cell (UniformGrid.java:264-266) or wider than the grid
+            keep = torch.ones(len(qx), dtype=torch.bool, device=qx.device)
+        else:
+            odd = (qcx < -9999) | (qcx > 99999)  # key round trips of getIntCellIndices: keep
+            keep = odd | ((qcx - lc - 1 <= hi - 1) & (qcx + lc + 1 >= lo))
+        kq = torch.nonzero(keep).flatten()
+        pairs = local_join(rx, ry, qx[kq], qy[kq], r, approximate).to(torch.int64)
+        if len(pairs):
+            pairs = torch.stack([rg[pairs[:, 0]], kq.to(torch.int64)[pairs[:, 1]]], dim=1)
+    else:
+        raise ValueError(f"unknown partition {partition!r}")
+    offset, total = gather_counts(len(pairs), pairs.device, group)
+    return pairs, offset, total
+
+
+def ppoly_sharded(x_local, y_local, base: int, ring_off, vx, vy, r: float, approximate: bool = False, *, grid=None,
+                  ctx=None, group=None, local_ppoly: Optional[Callable] = None):
+    """Point-polygon range of one window over the group (polygons on every rank, points by
+    arrival): returns (pairs int64 [m, 2] = (polygon, point window idx), offset, total)."""
+    import torch
+
+    if local_ppoly is None:
+        local_ppoly = _device_local_ppoly(ctx, grid)
+    pairs = local_ppoly(x_local, y_local, ring_off, vx, vy, r, approximate).to(torch.int64)
+    if len(pairs):
+        pairs[:, 1] += base
+    offset, total = gather_counts(len(pairs), pairs.device, group)
+    return pairs, offset, total
+
+
 def gather_counts(count: int, device, group=None):
     import torch
     import torch.distributed as dist
@@ -129,6 +226,20 @@ def _device_merge(ctx):
         cnt = torch.zeros(1, dtype=torch.int32, device=all_d.device)
         ctx.knn_merge_async(all_d, all_i, w, k, k, oi, od, cnt)
         return oi, od
+
+    return f
+
+
+def _device_local_join(ctx, grid_data, grid_query):
+    def f(x, y, qx, qy, r, approximate):
+        return ctx.join_pp(grid_data, grid_query, x, y, qx, qy, r, approximate).reshape(-1, 2)
+
+    return f
+
+
+def _device_local_ppoly(ctx, grid):
+    def f(x, y, ring_off, vx, vy, r, approximate):
+        return ctx.range_ppoly(grid, x, y, ring_off, vx, vy, r, approximate).reshape(-1, 2)
 
     return f
 

@@ -105,3 +105,102 @@ def test_sharded_knn_and_range_gloo(tmp_path, world):
     assert r["range_hits"].tolist() == sorted(want.tolist())
     assert r["totals"].tolist() == [len(want)] * world
     assert r["offsets"][0] == 0
+
+
+def _join_worker(rank, world, port, out_path):
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "oracle"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import cref
+    from spatialflink_amd import distributed as D
+    from spatialflink_amd import synth
+
+    bj = synth.BEIJING
+    out = {}
+    for gn, r in ((100, 0.05), (37, 0.0), (500, 0.02)):
+        cg = cref.grid(bj[0], bj[2], (bj[1] - bj[0]) / gn, gn)
+        n_total = 40_001
+        dx, dy = synth.gaussian_clusters(n_total, 3, sigma=0.1)
+        dx[::997] = np.nan  # NaN data land in cell 0 (Java (int)NaN)
+        qx, qy = synth.gaussian_clusters(257, 4, sigma=0.1)
+        lo, hi = D.shard_bounds(n_total, world, rank)
+        xl, yl = torch.from_numpy(dx[lo:hi].copy()), torch.from_numpy(dy[lo:hi].copy())
+        tqx, tqy = torch.from_numpy(qx), torch.from_numpy(qy)
+
+        def local_join(xs, ys, qxs, qys, rr, approximate):
+            p = cref.join_pp(cg, cg, xs.numpy(), ys.numpy(), qxs.numpy(), qys.numpy(), rr, approximate)
+            return torch.from_numpy(p.astype(np.int64)).reshape(-1, 2)
+
+        for part in ("arrival", "cells"):
+            pairs, off, total = D.join_sharded(xl, yl, lo, tqx, tqy, r, grid_data=cg, grid_query=cg,
+                                               partition=part, local_join=local_join)
+            got = [None] * world
+            dist.all_gather_object(got, (rank, pairs.numpy().tolist(), off, total))
+            out[f"{gn}_{r}_{part}"] = got
+    # point-polygon range, polygons replicated
+    cg = cref.grid(bj[0], bj[2], (bj[1] - bj[0]) / 200, 200)
+    n_total = 60_001
+    x, y = synth.uniform(n_total, 9)
+    off_, vx, vy = synth.star_polygons(12, 10)
+    lo, hi = D.shard_bounds(n_total, world, rank)
+
+    def local_ppoly(xs, ys, ro, pvx, pvy, rr, approximate):
+        p = cref.range_ppoly(cg, xs.numpy(), ys.numpy(), ro, pvx, pvy, rr, approximate)
+        return torch.from_numpy(p.astype(np.int64)).reshape(-1, 2)
+
+    pairs, off, total = D.ppoly_sharded(torch.from_numpy(x[lo:hi].copy()), torch.from_numpy(y[lo:hi].copy()), lo,
+                                        off_, vx, vy, 0.01, local_ppoly=local_ppoly)
+    got = [None] * world
+    dist.all_gather_object(got, (rank, pairs.numpy().tolist(), off, total))
+    out["ppoly"] = got
+    if rank == 0:
+        import json
+        with open(out_path, "w") as f:
+            json.dump(out, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _union(got):
+    pairs = [tuple(p) for _, ps, _, _ in sorted(got) for p in ps]
+    offs = [o for _, _, o, _ in sorted(got)]
+    sizes = [len(ps) for _, ps, _, _ in sorted(got)]
+    tot = {t for _, _, _, t in got}
+    return pairs, offs, sizes, tot
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_join_and_ppoly_gloo(tmp_path, world):
+    """join_sharded (arrival shards and key-band partition with an all-to-all and halo query
+    replication) and ppoly_sharded: disjoint per-rank pair sets whose union equals the
+    unsharded oracle, consistent offsets/totals."""
+    import json
+
+    out = tmp_path / "join.json"
+    mp.spawn(_join_worker, args=(world, _free_port(), str(out)), nprocs=world, join=True)
+    with open(out) as f:
+        res = json.load(f)
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import cref
+    from spatialflink_amd import synth
+
+    bj = synth.BEIJING
+    for gn, r in ((100, 0.05), (37, 0.0), (500, 0.02)):
+        cg = cref.grid(bj[0], bj[2], (bj[1] - bj[0]) / gn, gn)
+        dx, dy = synth.gaussian_clusters(40_001, 3, sigma=0.1)
+        dx[::997] = np.nan
+        qx, qy = synth.gaussian_clusters(257, 4, sigma=0.1)
+        want = sorted(map(tuple, cref.join_pp(cg, cg, dx, dy, qx, qy, r).astype(np.int64).tolist()))
+        for part in ("arrival", "cells"):
+            pairs, offs, sizes, tot = _union(res[f"{gn}_{r}_{part}"])
+            assert len(pairs) == len(set(pairs)), (gn, r, part, "ranks overlap")
+            assert sorted(pairs) == want, (gn, r, part)
+            assert tot == {len(want)} and offs == [sum(sizes[:i]) for i in range(world)]
+    cg = cref.grid(bj[0], bj[2], (bj[1] - bj[0]) / 200, 200)
+    x, y = synth.uniform(60_001, 9)
+    off_, vx, vy = synth.star_polygons(12, 10)
+    want = sorted(map(tuple, cref.range_ppoly(cg, x, y, off_, vx, vy, 0.01).astype(np.int64).tolist()))
+    pairs, offs, sizes, tot = _union(res["ppoly"])
+    assert sorted(pairs) == want and tot == {len(want)}
