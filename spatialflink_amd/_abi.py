@@ -108,6 +108,7 @@ _SIGS = {
     "geohip_debug_selftest_fp64": (c_int, [_P, _P, _P, c_uint64, _P, _P, _P, _P]),
     "geohip_debug_classify": (c_int, [POINTER(Grid), c_double, c_double, c_double, _P, _P, c_uint64, _P]),
     "geohip_debug_set_knn_fused": (None, [c_int]),
+    "geohip_debug_set_join_mask_budget": (None, [c_uint64]),
     "geohip_debug_set_knn_config": (c_int, [c_int, c_int, c_int, c_int, c_int]),
     "geohip_debug_knn_trace": (c_int, [_P, _P, c_uint64, POINTER(c_uint32)]),
     "geohip_debug_knn_scan_variant": (c_int, [_P, c_int, POINTER(Grid), _P, _P, c_uint64, c_int, c_double,
@@ -167,6 +168,11 @@ def debug_set_knn_fused(fused: bool) -> None:
     """Test/measurement hook: kNN final selection inside the scan's last block (default) or
     as a separate knn_final launch."""
     lib.geohip_debug_set_knn_fused(1 if fused else 0)
+
+
+def debug_set_join_mask_budget(nbytes: int = 4 << 30) -> None:
+    """Test hook: byte budget of the join's hit masks; beyond it the write pass recomputes."""
+    lib.geohip_debug_set_join_mask_budget(nbytes)
 
 
 def debug_set_knn_config(waves_per_block: int = 16, prefetch: int = 1, ticket_groups: int = 16,

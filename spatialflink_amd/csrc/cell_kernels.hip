@@ -1068,8 +1068,8 @@ enum JSlot {
     J_QLIST, J_GLIST, J_QCNT, J_BCNT, J_BOFF, J_PMASK, J_MWORDS, J_MOFF
 };
 
-// join hit masks larger than this fall back to a recomputing write pass
-constexpr uint64_t kJoinMaskBudget = 4ull << 30;
+// join hit masks larger than this fall back to a recomputing write pass (debug hook: settable)
+uint64_t g_join_mask_budget = 4ull << 30;
 
 // J_MISC words: [0] outside count, [1] outside cursor, [2] scan grand total, [3] global
 // query count, [8..9] pair total (u64)
@@ -1234,6 +1234,7 @@ void screen_bounds(double r, double* r2lo, double* r2hi) {
 }  // namespace
 
 void pp_screen_bounds(double r, double* r2lo, double* r2hi) { screen_bounds(r, r2lo, r2hi); }
+void set_join_mask_budget(uint64_t bytes) { g_join_mask_budget = bytes; }
 
 int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, const double* dx, const double* dy,
                  uint64_t nd, const double* qx, const double* qy, uint64_t nq, double r, int approximate,
@@ -1352,7 +1353,7 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
         uint64_t nwords = 0;
         rc = read_total(ctx, moff + geo.ntiles, &nwords);
         if (rc) return rc;
-        if (nwords * 8 <= kJoinMaskBudget) {
+        if (nwords * 8 <= g_join_mask_budget) {
             mask = S.get<unsigned long long>(J_PMASK, nwords * 8 + 8);
             if (S.rc) return S.rc;
         }

@@ -20,6 +20,8 @@ int ctx_stage_xy(geohip_ctx* ctx, const double* x, const double* y, uint64_t n, 
 
 // squared-distance screen bounds for "dist <= r" (r2lo < 0 / r2hi = inf where they cannot hold)
 void pp_screen_bounds(double r, double* r2lo, double* r2hi);
+// measurement/test hook: byte budget of the join's hit masks (beyond it the write pass recomputes)
+void set_join_mask_budget(uint64_t bytes);
 
 int join_pp_impl(geohip_ctx* ctx, const geohip_grid* grid_data, const geohip_grid* grid_query, const double* dx,
                  const double* dy, uint64_t nd, const double* qx, const double* qy, uint64_t nq, double r,

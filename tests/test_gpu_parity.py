@@ -430,3 +430,63 @@ def test_knn_fused_final_select(ctx):
                 assert oi.tolist() == wi.tolist() and np.array_equal(od.view(np.uint64), wd.view(np.uint64))
     finally:
         _abi.debug_set_knn_fused(False)
+
+
+# ------------------------------------------------------------------ less common kernel paths --
+def test_join_dense_tiles_batches_and_recompute(ctx):
+    """Join beyond the common case: > 256 candidate queries per tile (several LDS query batches)
+    and thousands of points per tile; then the same join with a zero mask budget (the write pass
+    recomputes instead of reading the count pass's hit masks)."""
+    ag, cg = agrid(100)
+    rng = np.random.default_rng(31)
+    dx = 116.40 + rng.uniform(0, 0.03, 30000)
+    dy = 40.00 + rng.uniform(0, 0.03, 30000)
+    qx = 116.39 + rng.uniform(0, 0.05, 400)
+    qy = 39.99 + rng.uniform(0, 0.05, 400)
+    want = pairs_sorted(cref.join_pp(cg, cg, dx, dy, qx, qy, 0.01)).tolist()
+    assert len(want) > 100000
+    got = ctx.join_pp(ag, ag, dx, dy, qx, qy, 0.01)
+    assert pairs_sorted(got).tolist() == want
+    _abi.debug_set_join_mask_budget(0)
+    try:
+        got = ctx.join_pp(ag, ag, dx, dy, qx, qy, 0.01)
+        assert pairs_sorted(got).tolist() == want
+    finally:
+        _abi.debug_set_join_mask_budget()
+
+
+def test_ppoly_big_tile_and_long_ring(ctx):
+    """Point-polygon with > 32768 points in one tile (hit mask in global memory), a 1500-vertex
+    ring (vertices and slab lists read from global memory) and a 5-vertex ring (no slab lists)."""
+    ag, cg = agrid(100)
+    l = (BJ[1] - BJ[0]) / 100
+    rng = np.random.default_rng(37)
+    cx0, cy0 = BJ[0] + 44.1 * l, BJ[2] + 20.1 * l  # inside cell (44, 20)
+    x = cx0 + rng.uniform(0, 0.8 * l, 50000)
+    y = cy0 + rng.uniform(0, 0.8 * l, 50000)
+    ang = np.arange(1500) * (2 * np.pi / 1500)
+    rad = 0.006 * (1 + 0.2 * np.sin(7 * ang))
+    bx = cx0 + 0.4 * l + rad * np.cos(ang)
+    by = cy0 + 0.4 * l + rad * np.sin(ang)
+    sq = [(cx0, cy0), (cx0 + 0.3 * l, cy0), (cx0 + 0.3 * l, cy0 + 0.3 * l), (cx0, cy0 + 0.3 * l), (cx0, cy0)]
+    vx = np.concatenate([bx, [bx[0]], [p[0] for p in sq]])
+    vy = np.concatenate([by, [by[0]], [p[1] for p in sq]])
+    off = np.array([0, 1501, 1506])
+    for r in (0.001, 0.0):
+        want = pairs_sorted(cref.range_ppoly(cg, x, y, off, vx, vy, r)).tolist()
+        got = ctx.range_ppoly(ag, x, y, off, vx, vy, r)
+        assert pairs_sorted(got).tolist() == want
+
+
+def test_knn_interleaved_iterations(ctx):
+    """The kNN scan with the window's 256-point iterations interleaved over the blocks (launch
+    shape switch) gives the same result as the default contiguous chunks."""
+    ag, cg = agrid(100)
+    x, y = synth.uniform(3_000_001, 41)
+    want_i, want_d = cref.knn_pp(cg, x, y, Q[0], Q[1], 0.5, 50)
+    _abi.debug_set_knn_config(interleave=1)
+    try:
+        oi, od = ctx.knn_pp(ag, x, y, Q[0], Q[1], 0.5, 50)
+        assert oi.tolist() == want_i.tolist() and np.array_equal(od.view(np.uint64), want_d.view(np.uint64))
+    finally:
+        _abi.debug_set_knn_config()
