@@ -23,7 +23,7 @@ using namespace geohip;
 
 enum Slot {
     S_X, S_Y, S_QX, S_QY, S_GTHR, S_PART_D, S_PART_I, S_OUT_D, S_OUT_I, S_OUT_CNT,
-    S_MASK, S_UCNT, S_OFFS, S_TOTAL, S_OUT_IDX, S_OUT_PAIRS, S_SPILL_D, S_SPILL_I, S_SPILL_CNT,
+    S_MASK, S_UCNT, S_OFFS, S_TOTAL, S_OUT_IDX, S_OUT_PAIRS, S_SPILL_D, S_SPILL_I, S_SPILL_CNT, S_RLB,
     S_J0, S_J1, S_J2, S_J3, S_J4, S_J5, S_J6, S_J7, S_J8, S_J9, S_J10, S_J11, S_J12, S_J13, S_J14, S_J15,
     S_J16, S_J17, S_J18, S_J19, S_J20, S_J21, S_J22, S_J23,
     S_COUNT
@@ -48,6 +48,7 @@ struct geohip_ctx {
     geohip_grid plan_grid{};
     double plan_q[3] = {0, 0, 0};
     PointPlan plan{};
+    unsigned long long range_epoch = 0;  // fused range pass: status words of this launch carry it
 };
 
 namespace {
@@ -264,10 +265,16 @@ int range_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x, con
     if (!rc) rc = ensure(ctx, S_UCNT, units * 4);
     if (!rc) rc = ensure(ctx, S_OFFS, units * 8);
     if (rc) return rc;
+    // fused pass: 256 status words + the arrival ticket (zeroed once; re-armed by each launch)
+    rc = ensure_zeroed(ctx, S_RLB, 256 * 8 + 64);
+    if (rc) return rc;
+    ctx->range_epoch = ctx->range_epoch % ((1ull << 24) - 1) + 1;
     hipEvent_t e0, e1;
     timing_events(ctx, &e0, &e1);
     hipError_t e = launch_range(dx, dy, n, a, approximate, B<unsigned long long>(ctx, S_MASK), B<unsigned>(ctx, S_UCNT),
-                                B<uint64_t>(ctx, S_OFFS), total, out, cap, ctx->stream, e0, e1);
+                                B<uint64_t>(ctx, S_OFFS), total, out, cap, ctx->stream, e0, e1,
+                                B<unsigned long long>(ctx, S_RLB), reinterpret_cast<unsigned*>(B<char>(ctx, S_RLB) + 256 * 8),
+                                ctx->range_epoch);
     if (e != hipSuccess) return hip_fail(ctx, e, "range launch");
     return GEOHIP_OK;
 }

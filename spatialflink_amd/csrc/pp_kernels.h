@@ -61,7 +61,8 @@ hipError_t launch_knn_merge(const unsigned long long* d, const unsigned* i, unsi
 // range: bitmask (16 words / 1024 pts), unit_count (units), offs (units) scratch.
 hipError_t launch_range(const double* x, const double* y, uint64_t n, const RangeArgs& a, int approximate,
                         unsigned long long* bitmask, unsigned* unit_count, uint64_t* offs, uint64_t* total,
-                        unsigned* out, uint64_t cap, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
+                        unsigned* out, uint64_t cap, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1,
+                        unsigned long long* lb_status, unsigned* lb_ticket, unsigned long long epoch);
 hipError_t launch_synth_uniform(double* x, double* y, uint64_t n, uint64_t base, uint64_t seed, double min_x,
                                 double max_x, double min_y, double max_y, hipStream_t st);
 hipError_t launch_selftest_fp64(const double* a, const double* b, uint64_t n, double* o_sqrt, double* o_div,

@@ -1111,6 +1111,201 @@ __global__ __launch_bounds__(kBlock) void range_scan(const double* __restrict__ 
     if (lane == 0) unit_count[unit] = c;
 }
 
+// ---- fused range pass: one launch per window.  Block vb (start order,
+// from a ticket) owns units [vb U, (vb + 1) U); its 16 waves claim units from an LDS counter
+// and leave each unit's hit bitmask in LDS.  The block publishes its hit count (status word
+// tagged with the launch epoch), sums the counts of every earlier block (<= 255, one parallel
+// read; earlier blocks started earlier and never wait on later ones), and writes its hits in
+// ascending order at that offset.  The last block writes the total and re-arms the ticket.
+constexpr int kRangeNW = 16;
+constexpr unsigned kRangeMaxUnits = 160;  // units (1024 points) per block: 20 KB of LDS bitmask
+constexpr unsigned kRangeMaxBlocks = 256;
+
+struct RangeLookback {
+    unsigned long long* status;  // kRangeMaxBlocks words: (epoch << 40) | count
+    unsigned* ticket;            // zero before the first launch; re-armed by the last block
+    unsigned long long epoch;    // 1 .. 2^24 - 1, new per launch
+};
+
+template <bool APPROX>
+__global__ __launch_bounds__(kRangeNW * kWave) void range_fused(const double* __restrict__ x,
+                                                                const double* __restrict__ y, uint64_t n, RangeArgs a,
+                                                                unsigned upb, RangeLookback lb,
+                                                                unsigned* __restrict__ out, uint64_t cap,
+                                                                uint64_t* __restrict__ total) {
+    constexpr int NT = kRangeNW * kWave;
+    __shared__ RangeStage stage[kRangeNW];
+    __shared__ unsigned long long bmask[kRangeMaxUnits * 16];
+    __shared__ unsigned wpre[kRangeMaxUnits * 16];
+    __shared__ unsigned wsum[kRangeNW];
+    __shared__ unsigned vb_sh, next_unit, bcount;
+    __shared__ unsigned long long excl_sh;
+    const int lane = lane_id();
+    const int wid = threadIdx.x / kWave;
+    if (threadIdx.x == 0) {
+        vb_sh = atomicAdd(lb.ticket, 1u);
+        next_unit = kRangeNW;
+        bcount = 0;
+        excl_sh = 0;
+    }
+    __syncthreads();
+    const unsigned vb = vb_sh;
+    const uint64_t units = (n + kUnitPts - 1) / kUnitPts;
+    const uint64_t u0 = (uint64_t)vb * upb;
+    const unsigned nu = u0 >= units ? 0u : (unsigned)(units - u0 < upb ? units - u0 : upb);
+    const uint64_t p0 = u0 * kUnitPts;
+    const uint64_t p1 = p0 + (uint64_t)nu * kUnitPts < n ? p0 + (uint64_t)nu * kUnitPts : n;
+    const unsigned niters = nu ? (unsigned)((p1 - p0 + kPtsIter - 1) / kPtsIter) : 0u;
+    for (unsigned t = threadIdx.x; t < nu * 16; t += NT) bmask[t] = 0ull;
+    __syncthreads();
+    RangeStage& st = stage[wid];
+    // Waves claim 256-point iterations from an LDS counter (a unit per claim left up to a third
+    // of a block's waves idle at its end); hits go straight into the block's LDS bitmask, the
+    // next claimed iteration's points load while the current one is classified.
+    auto flush = [&](unsigned& ccnt, bool partial) {
+        while (ccnt >= 64 || (partial && ccnt > 0)) {
+            const unsigned take = ccnt >= 64 ? 64u : ccnt;
+            const unsigned from = ccnt - take;
+            bool ok = (unsigned)lane < take;
+            double px = 0.0, py = 0.0;
+            unsigned pi = 0;
+            if (ok) {
+                px = st.cx[from + lane];
+                py = st.cy[from + lane];
+                pi = st.ci[from + lane];
+            }
+            wave_lds_sync();
+            ccnt = from;
+            ok = ok && (jts_pp_distance(a.qx, a.qy, px, py) <= a.r);
+            if (ok) {
+                const unsigned off = (unsigned)(pi - p0);
+                atomicOr(&bmask[off >> 6], 1ull << (off & 63));
+            }
+            wave_lds_sync();
+        }
+    };
+    // the point query's boxes in registers (G is one box unless the plan is unusual)
+    const Box g0 = a.g[0], c0 = a.c;
+    unsigned ccnt = 0;
+    double cx4[4], cy4[4];
+    bool cv[4];
+    unsigned it = (unsigned)wid;
+    if (it < niters) load4(x, y, p0 + (uint64_t)it * kPtsIter, p1, lane, cx4, cy4, cv);
+    while (it < niters) {
+        const uint64_t base = p0 + (uint64_t)it * kPtsIter;
+        unsigned c = 0;
+        if (lane == 0) c = atomicAdd(&next_unit, 1u);
+        const unsigned nit = (unsigned)__builtin_amdgcn_readfirstlane((int)c);
+        double nx4[4], ny4[4];
+        bool nv[4] = {false, false, false, false};
+        if (nit < niters) load4(x, y, p0 + (uint64_t)nit * kPtsIter, p1, lane, nx4, ny4, nv);
+        unsigned long long hb[4];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; s4++) {
+            bool g = a.ng > 0 && in_box(g0, cx4[s4], cy4[s4]);
+            for (int b = 1; b < a.ng; b++) g = g || in_box(a.g[b], cx4[s4], cy4[s4]);
+            const bool cbox = !g && a.nc && in_box(c0, cx4[s4], cy4[s4]);
+            bool hit = cv[s4] && (g || (APPROX && cbox));
+            bool cand = false;
+            if (!APPROX && cv[s4] && cbox) {
+                const double dx = a.qx - cx4[s4], dy = a.qy - cy4[s4];
+                const double d2 = dx * dx + dy * dy;
+                if (d2 < a.r2lo) hit = true;
+                else if (!(d2 > a.r2hi)) cand = true;
+            }
+            hb[s4] = __ballot(hit);
+            if (!APPROX) {
+                const unsigned long long m = __ballot(cand);
+                if (cand) {
+                    const unsigned pos = ccnt + lanes_below(m);
+                    st.cx[pos] = cx4[s4];
+                    st.cy[pos] = cy4[s4];
+                    st.ci[pos] = (unsigned)slot_index(base, lane, s4);
+                }
+                ccnt += (unsigned)__popcll(m);
+            }
+        }
+        // word q (0..3) of this iteration covers points base + 64q .. +63: slots (2h, 2h+1)
+        if (lane < 4) {
+            const int h = lane >> 1, half = lane & 1;
+            const unsigned e = (unsigned)(hb[2 * h] >> (32 * half));
+            const unsigned o = (unsigned)(hb[2 * h + 1] >> (32 * half));
+            const unsigned long long word = spread32(e) | (spread32(o) << 1);
+            if (word) atomicOr(&bmask[(unsigned)((base - p0) >> 6) + lane], word);
+        }
+        wave_lds_sync();
+        if (!APPROX && ccnt >= 64) flush(ccnt, false);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; s4++) {
+            cx4[s4] = nx4[s4];
+            cy4[s4] = ny4[s4];
+            cv[s4] = nv[s4];
+        }
+        it = nit;
+    }
+    if (!APPROX) flush(ccnt, true);
+    __syncthreads();
+    {
+        unsigned my = 0;
+        for (unsigned t = threadIdx.x; t < nu * 16; t += NT) my += (unsigned)__popcll(bmask[t]);
+        if (my) atomicAdd(&bcount, my);
+    }
+    __syncthreads();
+    // publish this block's count
+    const unsigned long long tag = lb.epoch << 40;
+    if (threadIdx.x == 0)
+        __hip_atomic_store(lb.status + vb, tag | (unsigned long long)bcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // per-word exclusive prefix of the block's bitmask (ascending point order)
+    const unsigned nw = nu * 16;
+    const unsigned per = (nw + NT - 1) / NT;
+    const unsigned w0 = threadIdx.x * per;
+    unsigned tsum = 0;
+    for (unsigned k = 0; k < per; k++)
+        if (w0 + k < nw) tsum += (unsigned)__popcll(bmask[w0 + k]);
+    const unsigned incl = wave_incl_scan(tsum);
+    if (lane == kWave - 1) wsum[wid] = incl;
+    __syncthreads();
+    unsigned wbase = 0;
+    for (int w = 0; w < wid; w++) wbase += wsum[w];
+    unsigned run = wbase + incl - tsum;
+    for (unsigned k = 0; k < per; k++)
+        if (w0 + k < nw) {
+            wpre[w0 + k] = run;
+            run += (unsigned)__popcll(bmask[w0 + k]);
+        }
+    // exclusive offset = sum of every earlier block's count: one wave polls (with back-off) so
+    // blocks that finish early do not flood the status words while others still stream
+    if (wid == 0) {
+        unsigned long long pre = 0;
+        for (unsigned j = (unsigned)lane; j < vb; j += kWave) {
+            unsigned long long v = __hip_atomic_load(lb.status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            while ((v >> 40) != lb.epoch) {
+                __builtin_amdgcn_s_sleep(32);
+                v = __hip_atomic_load(lb.status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            pre += v & ((1ull << 40) - 1);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
+        if (lane == 0) excl_sh = pre;
+    }
+    __syncthreads();
+    const unsigned long long excl = excl_sh;
+    // coalesced emission: one word (64 points) per wave step
+    for (unsigned w = (unsigned)wid; w < nw; w += kRangeNW) {
+        const unsigned long long bits = bmask[w];
+        if (!bits) continue;
+        if ((bits >> lane) & 1ull) {
+            const unsigned long long pos = excl + wpre[w] + lanes_below(bits);
+            if (pos < cap) out[pos] = (unsigned)(u0 * kUnitPts) + w * 64u + (unsigned)lane;
+        }
+    }
+    if (threadIdx.x == 0 && vb == gridDim.x - 1) {
+        *total = excl + bcount;
+        __hip_atomic_store(lb.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // exclusive scan of unit counts by one workgroup; total -> *total
 __global__ __launch_bounds__(1024) void scan_units(const unsigned* __restrict__ cnt, uint64_t units,
                                                    uint64_t* __restrict__ offs, uint64_t* __restrict__ total) {
@@ -1344,20 +1539,32 @@ hipError_t launch_knn_merge(const unsigned long long* d, const unsigned* i, unsi
 
 hipError_t launch_range(const double* x, const double* y, uint64_t n, const RangeArgs& a, int approximate,
                         unsigned long long* bitmask, unsigned* unit_count, uint64_t* offs, uint64_t* total,
-                        unsigned* out, uint64_t cap, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+                        unsigned* out, uint64_t cap, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1,
+                        unsigned long long* lb_status, unsigned* lb_ticket, unsigned long long epoch) {
     const uint64_t units = (n + kUnitPts - 1) / kUnitPts;
-    const uint64_t blocks = (units + 3) / 4;
     if (units == 0) return hipMemsetAsync(total, 0, sizeof(uint64_t), st);
+    if (lb_status && units <= (uint64_t)kRangeMaxBlocks * kRangeMaxUnits) {
+        // one fused launch: <= 256 blocks of upb units
+        const unsigned upb = (unsigned)((units + kRangeMaxBlocks - 1) / kRangeMaxBlocks);
+        const unsigned nblocks = (unsigned)((units + upb - 1) / upb);
+        const RangeLookback lb{lb_status, lb_ticket, epoch};
+        if (ev0) (void)hipEventRecord(ev0, st);
+        if (approximate) range_fused<true><<<nblocks, kRangeNW * kWave, 0, st>>>(x, y, n, a, upb, lb, out, cap, total);
+        else range_fused<false><<<nblocks, kRangeNW * kWave, 0, st>>>(x, y, n, a, upb, lb, out, cap, total);
+        if (ev1) (void)hipEventRecord(ev1, st);
+        return hipGetLastError();
+    }
+    const uint64_t blocks = (units + 3) / 4;
     if (ev0) (void)hipEventRecord(ev0, st);
     if (approximate) range_scan<true><<<(unsigned)blocks, kBlock, 0, st>>>(x, y, n, a, bitmask, unit_count);
     else range_scan<false><<<(unsigned)blocks, kBlock, 0, st>>>(x, y, n, a, bitmask, unit_count);
-    if (ev1) (void)hipEventRecord(ev1, st);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     scan_units<<<1, 1024, 0, st>>>(unit_count, units, offs, total);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     range_emit<<<(unsigned)blocks, kBlock, 0, st>>>(bitmask, offs, units, out, cap);
+    if (ev1) (void)hipEventRecord(ev1, st);  // timed region: all three kernels
     return hipGetLastError();
 }
 
