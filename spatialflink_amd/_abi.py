@@ -109,6 +109,7 @@ _SIGS = {
     "geohip_debug_classify": (c_int, [POINTER(Grid), c_double, c_double, c_double, _P, _P, c_uint64, _P]),
     "geohip_debug_set_knn_fused": (None, [c_int]),
     "geohip_debug_set_join_mask_budget": (None, [c_uint64]),
+    "geohip_debug_set_range_mode": (None, [c_int]),
     "geohip_debug_set_knn_config": (c_int, [c_int, c_int, c_int, c_int, c_int]),
     "geohip_debug_knn_trace": (c_int, [_P, _P, c_uint64, POINTER(c_uint32)]),
     "geohip_debug_knn_scan_variant": (c_int, [_P, c_int, POINTER(Grid), _P, _P, c_uint64, c_int, c_double,
@@ -168,6 +169,11 @@ def debug_set_knn_fused(fused: bool) -> None:
     """Test/measurement hook: kNN final selection inside the scan's last block (default) or
     as a separate knn_final launch."""
     lib.geohip_debug_set_knn_fused(1 if fused else 0)
+
+
+def debug_set_range_mode(mode: int = 0) -> None:
+    """Measurement hook: fused range pass ablation (0 full, 1 counts only, 2 loads only)."""
+    lib.geohip_debug_set_range_mode(mode)
 
 
 def debug_set_join_mask_budget(nbytes: int = 4 << 30) -> None:

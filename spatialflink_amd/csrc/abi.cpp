@@ -672,6 +672,7 @@ int geohip_debug_selftest_fp64(geohip_ctx* ctx, const double* a, const double* b
 
 // Debug hook: 1 = final selection fused into the scan (default), 0 = separate knn_final launch.
 void geohip_debug_set_knn_fused(int fused) { set_knn_fused(fused); }
+void geohip_debug_set_range_mode(int mode) { set_range_mode(mode); }
 void geohip_debug_set_join_mask_budget(uint64_t bytes) { set_join_mask_budget(bytes); }
 int geohip_debug_set_knn_config(int waves_per_block, int prefetch, int ticket_groups, int epi_sort, int interleave) {
     return set_knn_config(waves_per_block, prefetch, ticket_groups, epi_sort, interleave) ? GEOHIP_ERR_ARG : GEOHIP_OK;

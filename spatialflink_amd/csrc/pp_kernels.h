@@ -37,6 +37,8 @@ hipError_t launch_knn_scan_variant(int mode, const double* x, const double* y, u
                                    unsigned* out_i, unsigned* out_count, hipStream_t st);
 // 1: final selection in the scan's last-arriving block (default); 0: separate knn_final launch
 void set_knn_fused(int fused);
+// measurement hook: fused range pass ablation (0 full, 1 counts only, 2 loads only)
+void set_range_mode(int mode);
 // kNN scan launch shape: waves per block (4, 8, 16), load pipeline depth (1, 2), arrival
 // ticket groups (1 .. 64).  Returns -1 for an unsupported shape.
 struct KnnConfig {

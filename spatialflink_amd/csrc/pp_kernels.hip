@@ -1127,7 +1127,9 @@ struct RangeLookback {
     unsigned long long epoch;    // 1 .. 2^24 - 1, new per launch
 };
 
-template <bool APPROX>
+// MODE (measurement only): 0 full; 1 no look-back/emission (counts only); 2 loads only;
+// 3 no emission; 4 no look-back wait
+template <bool APPROX, int MODE = 0>
 __global__ __launch_bounds__(kRangeNW * kWave) void range_fused(const double* __restrict__ x,
                                                                 const double* __restrict__ y, uint64_t n, RangeArgs a,
                                                                 unsigned upb, RangeLookback lb,
@@ -1199,6 +1201,20 @@ __global__ __launch_bounds__(kRangeNW * kWave) void range_fused(const double* __
         double nx4[4], ny4[4];
         bool nv[4] = {false, false, false, false};
         if (nit < niters) load4(x, y, p0 + (uint64_t)nit * kPtsIter, p1, lane, nx4, ny4, nv);
+        if (MODE == 2) {
+            double sink = 0.0;
+#pragma unroll
+            for (int s4 = 0; s4 < 4; s4++) sink += cx4[s4] + cy4[s4];
+            if (sink == 12345.678) bmask[0] = 1;
+#pragma unroll
+            for (int s4 = 0; s4 < 4; s4++) {
+                cx4[s4] = nx4[s4];
+                cy4[s4] = ny4[s4];
+                cv[s4] = nv[s4];
+            }
+            it = nit;
+            continue;
+        }
         unsigned long long hb[4];
 #pragma unroll
         for (int s4 = 0; s4 < 4; s4++) {
@@ -1251,10 +1267,20 @@ __global__ __launch_bounds__(kRangeNW * kWave) void range_fused(const double* __
         if (my) atomicAdd(&bcount, my);
     }
     __syncthreads();
+    if (MODE == 1 || MODE == 2) {
+        if (threadIdx.x == 0 && vb == gridDim.x - 1) {
+            *total = bcount;
+            __hip_atomic_store(lb.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
     // publish this block's count
     const unsigned long long tag = lb.epoch << 40;
+    // published with an atomic exchange: performed at the device coherence point, so the other
+    // XCDs' polling loads see it at once (a plain store may sit in this XCD's L2)
     if (threadIdx.x == 0)
-        __hip_atomic_store(lb.status + vb, tag | (unsigned long long)bcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        (void)__hip_atomic_exchange(lb.status + vb, tag | (unsigned long long)bcount, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
     // per-word exclusive prefix of the block's bitmask (ascending point order)
     const unsigned nw = nu * 16;
     const unsigned per = (nw + NT - 1) / NT;
@@ -1275,29 +1301,67 @@ __global__ __launch_bounds__(kRangeNW * kWave) void range_fused(const double* __
         }
     // exclusive offset = sum of every earlier block's count: one wave polls (with back-off) so
     // blocks that finish early do not flood the status words while others still stream
-    if (wid == 0) {
-        unsigned long long pre = 0;
-        for (unsigned j = (unsigned)lane; j < vb; j += kWave) {
-            unsigned long long v = __hip_atomic_load(lb.status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            while ((v >> 40) != lb.epoch) {
-                __builtin_amdgcn_s_sleep(32);
-                v = __hip_atomic_load(lb.status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            pre += v & ((1ull << 40) - 1);
+    if (wid == 0 && MODE != 4) {
+        // lane l reads predecessors l, l + 64, l + 128, l + 192 with all four loads in flight
+        // (a dependent chain of device-scope loads costs a memory round trip each)
+        constexpr int kPer = kRangeMaxBlocks / kWave;
+        unsigned long long v[kPer];
+        unsigned pending = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const unsigned j = (unsigned)lane + (unsigned)k * kWave;
+            v[k] = j < vb ? __hip_atomic_load(lb.status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tag;
         }
+#pragma unroll
+        for (int k = 0; k < kPer; k++)
+            if ((v[k] >> 40) != lb.epoch) pending |= 1u << k;
+        while (pending) {
+            __builtin_amdgcn_s_sleep(8);
+#pragma unroll
+            for (int k = 0; k < kPer; k++) {
+                if (pending & (1u << k)) {
+                    v[k] = __hip_atomic_load(lb.status + lane + k * kWave, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if ((v[k] >> 40) == lb.epoch) pending &= ~(1u << k);
+                }
+            }
+        }
+        unsigned long long pre = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; k++) pre += v[k] & ((1ull << 40) - 1);
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
         if (lane == 0) excl_sh = pre;
     }
     __syncthreads();
     const unsigned long long excl = excl_sh;
-    // coalesced emission: one word (64 points) per wave step
-    for (unsigned w = (unsigned)wid; w < nw; w += kRangeNW) {
-        const unsigned long long bits = bmask[w];
-        if (!bits) continue;
-        if ((bits >> lane) & 1ull) {
-            const unsigned long long pos = excl + wpre[w] + lanes_below(bits);
-            if (pos < cap) out[pos] = (unsigned)(u0 * kUnitPts) + w * 64u + (unsigned)lane;
+    // Emission: each wave owns a contiguous run of words, so its hits are one contiguous run of
+    // the output, written word after word (consecutive stores complete each other's lines).  Lane
+    // l loads word w0 + l once; the per-word bits and offsets then come by readlane, so no LDS
+    // round trip sits between two words' stores.
+    if (MODE != 3) {
+        const unsigned wpw = (nw + kRangeNW - 1) / kRangeNW;
+        const unsigned wb = (unsigned)wid * wpw;
+        const unsigned we = wb + wpw < nw ? wb + wpw : nw;
+        unsigned long long obase = excl + (wb < we ? wpre[wb] : 0u);
+        const unsigned ibase = (unsigned)(u0 * kUnitPts);
+        for (unsigned w0 = wb; w0 < we; w0 += kWave) {
+            const unsigned long long mine = w0 + lane < we ? bmask[w0 + lane] : 0ull;
+            const unsigned c = (unsigned)__popcll(mine);
+            const unsigned incl = wave_incl_scan(c);
+            const unsigned ex = incl - c;
+            const unsigned m = we - w0 < (unsigned)kWave ? we - w0 : (unsigned)kWave;
+            for (unsigned j = 0; j < m; j++) {
+                const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)mine, (int)j);
+                const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(mine >> 32), (int)j);
+                const unsigned long long bits = ((unsigned long long)hi << 32) | lo;
+                if (!bits) continue;
+                const unsigned pj = (unsigned)__builtin_amdgcn_readlane((int)ex, (int)j);
+                if ((bits >> lane) & 1ull) {
+                    const unsigned long long pos = obase + pj + lanes_below(bits);
+                    if (pos < cap) out[pos] = ibase + (w0 + j) * 64u + (unsigned)lane;
+                }
+            }
+            obase += (unsigned)__builtin_amdgcn_readlane((int)incl, kWave - 1);
         }
     }
     if (threadIdx.x == 0 && vb == gridDim.x - 1) {
@@ -1537,6 +1601,9 @@ hipError_t launch_knn_merge(const unsigned long long* d, const unsigned* i, unsi
     return hipGetLastError();
 }
 
+static int g_range_mode = 0;
+void set_range_mode(int mode) { g_range_mode = mode; }
+
 hipError_t launch_range(const double* x, const double* y, uint64_t n, const RangeArgs& a, int approximate,
                         unsigned long long* bitmask, unsigned* unit_count, uint64_t* offs, uint64_t* total,
                         unsigned* out, uint64_t cap, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1,
@@ -1550,6 +1617,10 @@ hipError_t launch_range(const double* x, const double* y, uint64_t n, const Rang
         const RangeLookback lb{lb_status, lb_ticket, epoch};
         if (ev0) (void)hipEventRecord(ev0, st);
         if (approximate) range_fused<true><<<nblocks, kRangeNW * kWave, 0, st>>>(x, y, n, a, upb, lb, out, cap, total);
+        else if (g_range_mode == 1) range_fused<false, 1><<<nblocks, kRangeNW * kWave, 0, st>>>(x, y, n, a, upb, lb, out, cap, total);
+        else if (g_range_mode == 2) range_fused<false, 2><<<nblocks, kRangeNW * kWave, 0, st>>>(x, y, n, a, upb, lb, out, cap, total);
+        else if (g_range_mode == 3) range_fused<false, 3><<<nblocks, kRangeNW * kWave, 0, st>>>(x, y, n, a, upb, lb, out, cap, total);
+        else if (g_range_mode == 4) range_fused<false, 4><<<nblocks, kRangeNW * kWave, 0, st>>>(x, y, n, a, upb, lb, out, cap, total);
         else range_fused<false><<<nblocks, kRangeNW * kWave, 0, st>>>(x, y, n, a, upb, lb, out, cap, total);
         if (ev1) (void)hipEventRecord(ev1, st);
         return hipGetLastError();
