@@ -573,21 +573,23 @@ __global__ __launch_bounds__(kTB) void join_tile(TileBins tb, const unsigned* __
             unsigned long long* mrow = (!WRITE && mask) ? mask + moff[tile] + (size_t)((base - ds) / kWave) * nqt + qb
                                                         : nullptr;
             unsigned acc_lo = 0, acc_hi = 0;
-            for (unsigned j = 0; j < nbq; j++) {
-                const QRect R = lrect[j];
-                bool hit = cx >= R.x0 && cx <= R.x1 && cy >= R.y0 && cy <= R.y1;
-                if (!APPROX && hit) {
+            if (!WRITE) {
+                // count pass: the squared distance for every lane (no branch around it), the exact
+                // JTS distance only for the rare lanes in the screens' band; 4 queries' LDS reads
+                // in flight per step
+#pragma unroll 4
+                for (unsigned j = 0; j < nbq; j++) {
+                    const QRect R = lrect[j];
                     const double ox = lqx[j], oy = lqy[j];
-                    const double dx = px - ox, dy = py - oy;
-                    const double d2 = dx * dx + dy * dy;
-                    if (!(d2 <= r2lo)) {
-                        if (d2 > r2hi) hit = false;
-                        else hit = jts_pp_distance(px, py, ox, oy) <= r;  // getDistance(p, q)
+                    const bool inr = cx >= R.x0 && cx <= R.x1 && cy >= R.y0 && cy <= R.y1;
+                    bool hit = inr;
+                    if (!APPROX) {
+                        const double dx = px - ox, dy = py - oy;
+                        const double d2 = dx * dx + dy * dy;
+                        hit = inr && d2 <= r2lo;
+                        const bool band = inr && !(d2 <= r2lo) && !(d2 > r2hi);
+                        if (band) hit = jts_pp_distance(px, py, ox, oy) <= r;  // getDistance(p, q)
                     }
-                }
-                if (WRITE) {
-                    pairs_push<WRITE, kWavePairs>(buf, cnt, hit, pid, lqi[j], &bsh, sink);
-                } else {
                     const unsigned long long m = __ballot(hit);
                     cnt += (unsigned long long)__popcll(m);
                     if (mrow) {  // lane j % 64 keeps word j; 64 words leave as one coalesced store
@@ -600,6 +602,21 @@ __global__ __launch_bounds__(kTB) void join_tile(TileBins tb, const unsigned* __
                                 mrow[(j & ~63u) + lane] = ((unsigned long long)acc_hi << 32) | acc_lo;
                         }
                     }
+                }
+            } else {
+                for (unsigned j = 0; j < nbq; j++) {
+                    const QRect R = lrect[j];
+                    bool hit = cx >= R.x0 && cx <= R.x1 && cy >= R.y0 && cy <= R.y1;
+                    if (!APPROX && hit) {
+                        const double ox = lqx[j], oy = lqy[j];
+                        const double dx = px - ox, dy = py - oy;
+                        const double d2 = dx * dx + dy * dy;
+                        if (!(d2 <= r2lo)) {
+                            if (d2 > r2hi) hit = false;
+                            else hit = jts_pp_distance(px, py, ox, oy) <= r;  // getDistance(p, q)
+                        }
+                    }
+                    pairs_push<WRITE, kWavePairs>(buf, cnt, hit, pid, lqi[j], &bsh, sink);
                 }
             }
         }
