@@ -324,6 +324,7 @@ int geohip_ctx_create(uint32_t device_mask, geohip_ctx** out_ctx) {
 }
 
 int geohip_ctx_destroy(geohip_ctx* ctx) {
+    if (ctx) ppoly_cache_drop(ctx);
     if (!ctx) return GEOHIP_ERR_ARG;
     hipSetDevice(ctx->device);
     hipStreamSynchronize(ctx->stream);

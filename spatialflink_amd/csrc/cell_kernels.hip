@@ -20,6 +20,11 @@
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
+#include <unordered_map>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <string>
 #include <vector>
@@ -969,18 +974,36 @@ __global__ __launch_bounds__(kTB) void ppoly_eval(TileBins tb, const PolyWork* _
         wave_lds_sync();
         qn = from;
     };
+    // the first G and C rectangle in registers (one each unless the plan is unusual)
+    int32_t g0[4] = {1, 0, 1, 0}, c0[4] = {1, 0, 1, 0};
+    if (P.ng) for (int t = 0; t < 4; t++) g0[t] = grect[t];
+    if (P.nc) for (int t = 0; t < 4; t++) c0[t] = crect[t];
+    auto in_r = [](const int32_t (&q)[4], int32_t x, int32_t y) { return x >= q[0] && x <= q[1] && y >= q[2] && y <= q[3]; };
+    // key and coordinates of the next pass are loaded while the current one is classified
+    unsigned key_n = 0;
+    double px_n = 0.0, py_n = 0.0;
+    auto fetch = [&](unsigned base) {
+        const unsigned i = base + lane;
+        if (i < de) {
+            key_n = tb.skey[i];
+            px_n = tb.sx[i];
+            py_n = tb.sy[i];
+        }
+    };
+    if (ds + wid * kWave < de) fetch(ds + wid * kWave);
     for (unsigned base = ds + wid * kWave; base < de; base += kTB) {
         const unsigned i = base + lane;
+        const unsigned key = key_n;
+        const double px = px_n, py = py_n;
+        if (base + kTB < de) fetch(base + kTB);
         bool hit = false, need = false;
-        double px = 0.0, py = 0.0;
         if (i < de) {
-            const unsigned key = tb.skey[i];
             const int32_t cx = (int32_t)(key / nb), cy = (int32_t)(key - (unsigned)cx * nb);
-            const bool g = in_rects(grect, P.ng, cx, cy);
-            const bool c = !g && in_rects(crect, P.nc, cx, cy);
+            bool g = in_r(g0, cx, cy);
+            if (P.ng > 1 && !g) g = in_rects(grect + 4, P.ng - 1, cx, cy);
+            bool c = !g && in_r(c0, cx, cy);
+            if (P.nc > 1 && !g && !c) c = in_rects(crect + 4, P.nc - 1, cx, cy);
             if (g || c) {
-                px = tb.sx[i];
-                py = tb.sy[i];
                 if (g || r_is_max) hit = true;
                 else if (APPROX) hit = bbox_distance(px, py, P.bb) <= r;
                 else need = !(box_dist2(px, py, P.bb[0], P.bb[1], P.bb[2], P.bb[3]) > screen_lim2(px, py, P.bb, r));
@@ -1432,22 +1455,24 @@ void plan_slabs(PolyDev& P, const double* ry, double r, double cell_len, std::ve
     const double sinv = (double)ns / span;
     if (!(sinv > 0.0) || !std::isfinite(sinv)) return;
     const double pad = 1e-6 * span / ns;
-    std::vector<uint32_t> ca(nseg), cb(nseg), da(nseg), db(nseg);
-    std::vector<uint32_t> cn(ns + 1, 0), dn(ns + 1, 0);
-    for (uint32_t e = 0; e < nseg; e++) {
+    // slab ranges of segment e: crossing [c0, c1], distance [d0, d1] (empty for a NaN y: such a
+    // segment never counts, flags or comes within r); computed in both passes, nothing stored
+    auto ranges = [&](uint32_t e, uint32_t& c0, uint32_t& c1, uint32_t& d0, uint32_t& d1) -> bool {
         const double a = ry[e], b = ry[e + 1];
-        if (a != a || b != b) {  // a NaN y never counts, flags or comes within r
-            ca[e] = da[e] = 1;
-            cb[e] = db[e] = 0;
-            continue;
-        }
+        if (a != a || b != b) return false;
         const double lo = std::min(a, b), hi = std::max(a, b);
-        ca[e] = slab_of(lo - pad, y0, sinv, ns);
-        cb[e] = slab_of(hi + pad, y0, sinv, ns);
-        da[e] = slab_of((lo - E) - pad, y0, sinv, ns);
-        db[e] = slab_of((hi + E) + pad, y0, sinv, ns);
-        for (uint32_t t = ca[e]; t <= cb[e]; t++) cn[t]++;
-        for (uint32_t t = da[e]; t <= db[e]; t++) dn[t]++;
+        c0 = slab_of(lo - pad, y0, sinv, ns);
+        c1 = slab_of(hi + pad, y0, sinv, ns);
+        d0 = slab_of((lo - E) - pad, y0, sinv, ns);
+        d1 = slab_of((hi + E) + pad, y0, sinv, ns);
+        return true;
+    };
+    uint32_t cn[65] = {0}, dn[65] = {0};
+    for (uint32_t e = 0; e < nseg; e++) {
+        uint32_t c0, c1, d0, d1;
+        if (!ranges(e, c0, c1, d0, d1)) continue;
+        for (uint32_t t = c0; t <= c1; t++) cn[t]++;
+        for (uint32_t t = d0; t <= d1; t++) dn[t]++;
     }
     uint64_t total = 0;
     for (uint32_t t = 0; t < ns; t++) total += cn[t] + dn[t];
@@ -1460,17 +1485,55 @@ void plan_slabs(PolyDev& P, const double* ry, double r, double cell_len, std::ve
     B[ns] = (uint16_t)k;
     for (uint32_t t = 0; t < ns; t++) { B[ns + 1 + t] = (uint16_t)k; k += dn[t]; }
     B[2 * ns + 1] = (uint16_t)k;
-    std::vector<uint32_t> cf(ns, 0), df(ns, 0);
+    uint32_t cf[64] = {0}, df[64] = {0};
     uint16_t* ids = B + 2 * (ns + 1);
     for (uint32_t e = 0; e < nseg; e++) {
-        for (uint32_t t = ca[e]; t <= cb[e] && ca[e] <= cb[e]; t++) ids[B[t] + cf[t]++] = (uint16_t)e;
-        for (uint32_t t = da[e]; t <= db[e] && da[e] <= db[e]; t++) ids[B[ns + 1 + t] + df[t]++] = (uint16_t)e;
+        uint32_t c0, c1, d0, d1;
+        if (!ranges(e, c0, c1, d0, d1)) continue;
+        for (uint32_t t = c0; t <= c1; t++) ids[B[t] + cf[t]++] = (uint16_t)e;
+        for (uint32_t t = d0; t <= d1; t++) ids[B[ns + 1 + t] + df[t]++] = (uint16_t)e;
     }
     P.ns = ns;
     P.sy0 = y0;
     P.sinv = sinv;
     P.E = E;
     P.llen = (uint32_t)(2 * (ns + 1) + total);
+}
+
+// Polygon plan cache, one entry per ctx: a continuous point-polygon query evaluates the same
+// polygons on every window, so the host planning (rings, envelopes, G/C rectangles, work items,
+// slab lists: ~2 ms for 1000 polygons) and the device upload are done once; later calls compare
+// their inputs bitwise with the cached copies (the inputs decide everything the plan holds).
+struct PolyCache {
+    geohip_grid grid{};
+    double r = 0.0;
+    std::vector<uint32_t> ring_off;
+    std::vector<double> vx, vy;
+    std::vector<PolyDev> pd;
+    std::vector<double> hvx, hvy;
+    std::vector<int32_t> hrects;
+    std::vector<PolyWork> hwork;
+    std::vector<uint16_t> hslab;
+    bool any_outside = false;
+    void* dev_blob = nullptr;  // J_POLY buffer holding the uploaded tables
+    size_t blob_bytes = 0;
+};
+std::mutex g_pcache_mu;
+std::unordered_map<const geohip_ctx*, PolyCache> g_pcache;
+
+bool same_inputs(const PolyCache& c, const geohip_grid& g, double r, const uint32_t* ring_off, uint32_t npoly,
+                 const double* vx, const double* vy) {
+    if (c.grid.min_x != g.min_x || c.grid.min_y != g.min_y || c.grid.cell_len != g.cell_len || c.grid.n != g.n) return false;
+    if (memcmp(&c.r, &r, sizeof r) != 0 || c.ring_off.size() != (size_t)npoly + 1) return false;
+    if (memcmp(c.ring_off.data(), ring_off, ((size_t)npoly + 1) * 4) != 0) return false;
+    const size_t v0 = npoly ? ring_off[0] : 0, v1 = npoly ? ring_off[npoly] : 0;
+    if (v1 < v0 || c.vx.size() != v1 - v0) return false;
+    return memcmp(c.vx.data(), vx + v0, (v1 - v0) * 8) == 0 && memcmp(c.vy.data(), vy + v0, (v1 - v0) * 8) == 0;
+}
+
+void ppoly_cache_drop(geohip_ctx* ctx) {
+    std::lock_guard<std::mutex> lk(g_pcache_mu);
+    g_pcache.erase(ctx);
 }
 
 int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
@@ -1487,52 +1550,84 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const 
     const bool dev = ctx_mem(ctx) == GEOHIP_MEM_DEVICE;
     const int32_t nb = grid->n;
     const TileGeom geo = tile_geom(*grid, nb);
-    // polygon planning (host): ring closure, envelope, G / C rectangles (plan.cpp), and the
-    // (polygon, tile) work items of each polygon's walk region
-    std::vector<PolyDev> pd(npoly);
-    std::vector<double> hvx, hvy;
-    std::vector<int32_t> hrects;
-    std::vector<PolyWork> hwork;
-    std::vector<uint16_t> hslab;
-    bool any_outside = false;
-    for (uint32_t p = 0; p < npoly; p++) {
-        PolyPlan pl;
-        std::string err;
-        const uint32_t b = ring_off[p], e = ring_off[p + 1];
-        if (e < b) return ctx_fail(ctx, GEOHIP_ERR_ARG, "ring_off not ascending");
-        rc = plan_polygon(*grid, vx + b, vy + b, e - b, r, &pl, &err);
-        if (rc) return ctx_fail(ctx, rc, err);
-        PolyDev& P = pd[p];
-        memset(&P, 0, sizeof P);
-        P.voff = (uint32_t)hvx.size();
-        P.nv = (uint32_t)pl.rx.size();
-        hvx.insert(hvx.end(), pl.rx.begin(), pl.rx.end());
-        hvy.insert(hvy.end(), pl.ry.begin(), pl.ry.end());
-        for (int i = 0; i < 4; i++) P.bb[i] = pl.bbox[i];
-        P.goff = (uint32_t)(hrects.size() / 4);
-        P.ng = (uint32_t)pl.g.size();
-        int32_t wx0 = INT32_MAX, wx1 = INT32_MIN, wy0 = INT32_MAX, wy1 = INT32_MIN;
-        auto acc = [&](const geohip_rect& q) {
-            const int32_t a0 = std::max(q.x0, 0), a1 = std::min(q.x1, nb - 1);
-            const int32_t c0 = std::max(q.y0, 0), c1 = std::min(q.y1, nb - 1);
-            if (q.x0 < 0 || q.y0 < 0 || q.x1 > nb - 1 || q.y1 > nb - 1) P.outside = 1;
-            if (a0 > a1 || c0 > c1) return;
-            wx0 = std::min(wx0, a0); wx1 = std::max(wx1, a1);
-            wy0 = std::min(wy0, c0); wy1 = std::max(wy1, c1);
-        };
-        for (auto& q : pl.g) { hrects.insert(hrects.end(), {q.x0, q.x1, q.y0, q.y1}); acc(q); }
-        P.coff = (uint32_t)(hrects.size() / 4);
-        P.nc = (uint32_t)pl.c.size();
-        for (auto& q : pl.c) { hrects.insert(hrects.end(), {q.x0, q.x1, q.y0, q.y1}); acc(q); }
-        P.wx0 = wx0; P.wx1 = wx1; P.wy0 = wy0; P.wy1 = wy1;
-        any_outside = any_outside || P.outside;
-        plan_slabs(P, pl.ry.data(), r, grid->cell_len, hslab);
-        if (wx0 <= wx1 && wy0 <= wy1)
-            for (int32_t a = wx0 / geo.ts; a <= wx1 / geo.ts; a++)
-                for (int32_t c = wy0 / geo.ts; c <= wy1 / geo.ts; c++)
-                    hwork.push_back(PolyWork{p, (uint32_t)a * (uint32_t)geo.nt + (uint32_t)c});
+    static const bool prof = getenv("GEOHIP_HOST_PROFILE") != nullptr;  // measurement only
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    const auto t_start = now();
+    // polygon planning (host): ring closure, envelope, G / C rectangles (plan.cpp), the
+    // (polygon, tile) work items of each polygon's walk region and the slab lists -- or the
+    // cached plan of the same inputs
+    PolyCache* pc = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_pcache_mu);
+        pc = &g_pcache[ctx];
     }
-    if (hwork.size() >= 0x7fffffffull) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "too many polygon work items");
+    bool cached = same_inputs(*pc, *grid, r, ring_off, npoly, vx, vy);
+    if (!cached) {
+        for (uint32_t p = 0; p < npoly; p++)
+            if (ring_off[p + 1] < ring_off[p]) return ctx_fail(ctx, GEOHIP_ERR_ARG, "ring_off not ascending");
+        PolyCache fresh;
+        std::vector<PolyDev>& pd = fresh.pd;
+        std::vector<double>& hvx = fresh.hvx;
+        std::vector<double>& hvy = fresh.hvy;
+        std::vector<int32_t>& hrects = fresh.hrects;
+        std::vector<PolyWork>& hwork = fresh.hwork;
+        std::vector<uint16_t>& hslab = fresh.hslab;
+        bool& any_outside = fresh.any_outside;
+        pd.resize(npoly);
+        for (uint32_t p = 0; p < npoly; p++) {
+            PolyPlan pl;
+            std::string err;
+            const uint32_t b = ring_off[p], e = ring_off[p + 1];
+            if (e < b) return ctx_fail(ctx, GEOHIP_ERR_ARG, "ring_off not ascending");
+            rc = plan_polygon(*grid, vx + b, vy + b, e - b, r, &pl, &err);
+            if (rc) return ctx_fail(ctx, rc, err);
+            PolyDev& P = pd[p];
+            memset(&P, 0, sizeof P);
+            P.voff = (uint32_t)hvx.size();
+            P.nv = (uint32_t)pl.rx.size();
+            hvx.insert(hvx.end(), pl.rx.begin(), pl.rx.end());
+            hvy.insert(hvy.end(), pl.ry.begin(), pl.ry.end());
+            for (int i = 0; i < 4; i++) P.bb[i] = pl.bbox[i];
+            P.goff = (uint32_t)(hrects.size() / 4);
+            P.ng = (uint32_t)pl.g.size();
+            int32_t wx0 = INT32_MAX, wx1 = INT32_MIN, wy0 = INT32_MAX, wy1 = INT32_MIN;
+            auto acc = [&](const geohip_rect& q) {
+                const int32_t a0 = std::max(q.x0, 0), a1 = std::min(q.x1, nb - 1);
+                const int32_t c0 = std::max(q.y0, 0), c1 = std::min(q.y1, nb - 1);
+                if (q.x0 < 0 || q.y0 < 0 || q.x1 > nb - 1 || q.y1 > nb - 1) P.outside = 1;
+                if (a0 > a1 || c0 > c1) return;
+                wx0 = std::min(wx0, a0); wx1 = std::max(wx1, a1);
+                wy0 = std::min(wy0, c0); wy1 = std::max(wy1, c1);
+            };
+            for (auto& q : pl.g) { hrects.insert(hrects.end(), {q.x0, q.x1, q.y0, q.y1}); acc(q); }
+            P.coff = (uint32_t)(hrects.size() / 4);
+            P.nc = (uint32_t)pl.c.size();
+            for (auto& q : pl.c) { hrects.insert(hrects.end(), {q.x0, q.x1, q.y0, q.y1}); acc(q); }
+            P.wx0 = wx0; P.wx1 = wx1; P.wy0 = wy0; P.wy1 = wy1;
+            any_outside = any_outside || P.outside;
+            plan_slabs(P, pl.ry.data(), r, grid->cell_len, hslab);
+            if (wx0 <= wx1 && wy0 <= wy1)
+                for (int32_t a = wx0 / geo.ts; a <= wx1 / geo.ts; a++)
+                    for (int32_t c = wy0 / geo.ts; c <= wy1 / geo.ts; c++)
+                        hwork.push_back(PolyWork{p, (uint32_t)a * (uint32_t)geo.nt + (uint32_t)c});
+        }
+
+        if (fresh.hwork.size() >= 0x7fffffffull) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "too many polygon work items");
+        fresh.grid = *grid;
+        fresh.r = r;
+        fresh.ring_off.assign(ring_off, ring_off + npoly + 1);
+        const size_t v0 = npoly ? ring_off[0] : 0, v1 = npoly ? ring_off[npoly] : 0;
+        fresh.vx.assign(vx + v0, vx + v1);
+        fresh.vy.assign(vy + v0, vy + v1);
+        *pc = std::move(fresh);
+    }
+    const std::vector<PolyDev>& pd = pc->pd;
+    const std::vector<double>& hvx = pc->hvx;
+    const std::vector<double>& hvy = pc->hvy;
+    const std::vector<int32_t>& hrects = pc->hrects;
+    const std::vector<PolyWork>& hwork = pc->hwork;
+    const std::vector<uint16_t>& hslab = pc->hslab;
+    const bool any_outside = pc->any_outside;
     Scratch S{ctx};
     const double *dx, *dy;
     rc = ctx_stage_xy(ctx, x, y, n, 0, &dx, &dy);
@@ -1540,8 +1635,10 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const 
     TileBins tb;
     unsigned* oidx = nullptr;
     unsigned n_out = 0;
+    const auto t_planned = now();
     rc = bin_tiles(ctx, S, dx, dy, n, geo, any_outside, &tb, &oidx, any_outside ? &n_out : nullptr);
     if (rc) return rc;
+    const auto t_binned = now();
     // polygon tables in one device blob: PolyDev[] | vx | vy | rects | work | slab lists
     const size_t sz_p = npoly * sizeof(PolyDev), sz_v = hvx.size() * 8, sz_r = hrects.size() * 4;
     const size_t sz_w = hwork.size() * sizeof(PolyWork), sz_s = hslab.size() * 2;
@@ -1552,6 +1649,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const 
     void* pblob = nullptr;
     rc = ctx_ensure(ctx, J_POLY, off_s + sz_s + 64, &pblob);
     if (rc) return rc;
+    const bool upload = !(cached && pc->dev_blob == pblob && pc->blob_bytes == off_s + sz_s);
     char* bp = reinterpret_cast<char*>(pblob);
     PolyDev* dpoly = reinterpret_cast<PolyDev*>(bp);
     double* dvx = reinterpret_cast<double*>(bp + off_v);
@@ -1559,13 +1657,18 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const 
     int32_t* drects = reinterpret_cast<int32_t*>(bp + off_r);
     PolyWork* dwork = reinterpret_cast<PolyWork*>(bp + off_w);
     uint16_t* dslab = reinterpret_cast<uint16_t*>(bp + off_s);
-    if ((sz_p && hipMemcpyAsync(dpoly, pd.data(), sz_p, hipMemcpyHostToDevice, st) != hipSuccess) ||
-        (sz_v && hipMemcpyAsync(dvx, hvx.data(), sz_v, hipMemcpyHostToDevice, st) != hipSuccess) ||
-        (sz_v && hipMemcpyAsync(dvy, hvy.data(), sz_v, hipMemcpyHostToDevice, st) != hipSuccess) ||
-        (sz_r && hipMemcpyAsync(drects, hrects.data(), sz_r, hipMemcpyHostToDevice, st) != hipSuccess) ||
-        (sz_w && hipMemcpyAsync(dwork, hwork.data(), sz_w, hipMemcpyHostToDevice, st) != hipSuccess) ||
-        (sz_s && hipMemcpyAsync(dslab, hslab.data(), sz_s, hipMemcpyHostToDevice, st) != hipSuccess))
-        return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "polygon upload failed");
+    if (upload) {
+        pc->dev_blob = nullptr;  // until the copies are issued
+        if ((sz_p && hipMemcpyAsync(dpoly, pd.data(), sz_p, hipMemcpyHostToDevice, st) != hipSuccess) ||
+            (sz_v && hipMemcpyAsync(dvx, hvx.data(), sz_v, hipMemcpyHostToDevice, st) != hipSuccess) ||
+            (sz_v && hipMemcpyAsync(dvy, hvy.data(), sz_v, hipMemcpyHostToDevice, st) != hipSuccess) ||
+            (sz_r && hipMemcpyAsync(drects, hrects.data(), sz_r, hipMemcpyHostToDevice, st) != hipSuccess) ||
+            (sz_w && hipMemcpyAsync(dwork, hwork.data(), sz_w, hipMemcpyHostToDevice, st) != hipSuccess) ||
+            (sz_s && hipMemcpyAsync(dslab, hslab.data(), sz_s, hipMemcpyHostToDevice, st) != hipSuccess))
+            return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "polygon upload failed");
+        pc->dev_blob = pblob;
+        pc->blob_bytes = off_s + sz_s;
+    }
     const unsigned nwork = (unsigned)hwork.size();
     const unsigned nob = (any_outside && n_out) ? (npoly < 4096u ? npoly : 4096u) : 0u;
     const uint64_t nslots = (uint64_t)nwork + nob;
@@ -1580,6 +1683,10 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const 
     // hit-mask layout: words per work item, scanned; the total sizes the mask (one readback)
     uint64_t nmask = 0;
     if (nwork) {
+        if (prof) fprintf(stderr, "ppoly host: plan %.1f us (cached %d), bin launch %.1f us, upload %.1f us\n",
+                          std::chrono::duration<double, std::micro>(t_planned - t_start).count(), (int)cached,
+                          std::chrono::duration<double, std::micro>(t_binned - t_planned).count(),
+                          std::chrono::duration<double, std::micro>(now() - t_binned).count());
         ppoly_words<<<(nwork + kTB - 1) / kTB, kTB, 0, st>>>(dwork, nwork, tb.start, words);
         scan_launch<unsigned long long>(st, words, nwork, reinterpret_cast<unsigned long long*>(seg),
                                         reinterpret_cast<unsigned long long*>(misc + 8), wofs);

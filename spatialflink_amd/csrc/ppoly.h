@@ -5,6 +5,9 @@
 #include "geohip_internal.h"
 
 namespace geohip {
+// drop the ctx's cached polygon plan (geohip_ctx_destroy)
+void ppoly_cache_drop(geohip_ctx* ctx);
+
 int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
                const uint32_t* ring_off, const double* vx, const double* vy, uint32_t npoly, double r,
                int approximate, uint32_t* out_pairs, uint64_t cap, uint64_t* out_count);
