@@ -16,11 +16,11 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 # workload -> (profiles tag, kernel-name substrings of the bench's timed region, timed launches per step)
 TAGS = {"knn": ("knn_scan", ("knn_scan", "knn_final"), 1),
-        "range": ("range", ("range_scan", "scan_units", "range_emit"), 1),
-        "join": ("join_probe", ("join_tile", "scan_seg_totals<unsigned long long>", "scan_totals<unsigned long long>",
+        "range": ("range", ("range_fused", "range_scan", "scan_units", "range_emit"), 1),
+        "join": ("join_probe", ("join_tile", "join_emit", "scan_seg_totals<unsigned long long>", "scan_totals<unsigned long long>",
                                  "scan_apply<unsigned long long>"), 1),
         "ppoly": ("ppoly_probe", ("ppoly_eval", "ppoly_emit", "ppoly_outside"), 1),
-        "c5": ("knn_scan_c5", ("knn_scan", "knn_final", "range_scan", "scan_units", "range_emit"), 2)}
+        "c5": ("knn_scan_c5", ("knn_scan", "knn_final", "range_fused", "range_scan", "scan_units", "range_emit"), 2)}
 
 
 def per_kernel(path):
