@@ -170,6 +170,7 @@ struct BinPass {
     unsigned* hist;        // level 1: [block][nbands + 1]; level 2: [item][kBandTiles]
     const uint4* items;    // level 2: (band, begin, end, -)
     const unsigned* nitems;
+    const unsigned* keep;  // optional cell bitmap (nb * nb bits): points of other cells are dropped
 };
 
 __device__ __forceinline__ unsigned key_tile(const TileGeom& g, unsigned key) {
@@ -178,13 +179,15 @@ __device__ __forceinline__ unsigned key_tile(const TileGeom& g, unsigned key) {
     return (cx / (unsigned)g.ts) * (unsigned)g.nt + cy / (unsigned)g.ts;
 }
 
-// level-1 point j: coordinates, key (kNoKey when out of the grid), bin
+// level-1 point j: coordinates, key (kNoKey when out of the grid), bin: its band, nbands when
+// out of the grid, nbands + 1 when its cell is not in the keep bitmap (dropped)
 __device__ __forceinline__ unsigned l1_point(const BinPass& a, uint64_t i, double& px, double& py, unsigned& key) {
     px = a.x[i];
     py = a.y[i];
     int32_t cx, cy;
     if (point_cell(a.g, px, py, cx, cy)) {
         key = (unsigned)cx * (unsigned)a.g.nb + (unsigned)cy;
+        if (a.keep && !((a.keep[key >> 5] >> (key & 31u)) & 1u)) return a.nbands + 1;
         return tile_of(a.g, cx, cy) >> kBandBits;
     }
     key = kNoKey;
@@ -198,7 +201,7 @@ __device__ __forceinline__ bool bin_range(const BinPass& a, uint64_t& b0, uint64
     if (LEVEL == 1) {
         b0 = (uint64_t)blockIdx.x * a.chunk;
         b1 = b0 + a.chunk < a.n ? b0 + a.chunk : a.n;
-        nbins = a.nbands + 1;
+        nbins = a.nbands + 2;
         band = 0;
         return true;
     }
@@ -387,7 +390,7 @@ __global__ __launch_bounds__(kBinThreads) void bin_scatter(BinPass a) {
 #pragma unroll
         for (int k = 0; k < 2; k++) {
             const unsigned j = threadIdx.x + k * kBinThreads;
-            if (j < m) {
+            if (j < m && (LEVEL == 2 || st.bin[j] <= a.nbands)) {  // dropped points stay here
                 const unsigned b = st.bin[j];
                 const unsigned g = cur[b] + (j - ls[b]);
                 a.dst.x[g] = st.x[j];
@@ -1173,7 +1176,8 @@ SoA carve_soa(void* base, uint64_t n) {
 // keep_outside: return the out-of-grid points' window indices (*outside_idx, count read back
 // into *n_outside_host).
 int bin_tiles(geohip_ctx* ctx, Scratch& S, const double* dx, const double* dy, uint64_t n, const TileGeom& geo,
-              bool keep_outside, TileBins* tb, unsigned** outside_idx, unsigned* n_outside_host) {
+              bool keep_outside, TileBins* tb, unsigned** outside_idx, unsigned* n_outside_host,
+              const unsigned* keep = nullptr) {
     hipStream_t st = ctx_stream(ctx);
     uint64_t nblk = (n + 16383) / 16384;
     if (nblk > 256) nblk = 256;
@@ -1182,10 +1186,10 @@ int bin_tiles(geohip_ctx* ctx, Scratch& S, const double* dx, const double* dy, u
     const uint64_t nt = geo.ntiles;
     const unsigned nbands = (unsigned)((nt + kBandTiles - 1) / kBandTiles);
     const uint64_t maxitems = (n + kL2Items - 1) / kL2Items + nbands;
-    unsigned* hist1 = S.get<unsigned>(J_HIST, nblk * (nbands + 1) * 4);
+    unsigned* hist1 = S.get<unsigned>(J_HIST, nblk * (nbands + 2) * 4);
     unsigned* hist2 = S.get<unsigned>(J_SIDX, maxitems * kBandTiles * 4 + 16);
     uint4* items = S.get<uint4>(J_SKEY, maxitems * sizeof(uint4) + 16);
-    unsigned* aux = S.get<unsigned>(J_AUX, (2 * (uint64_t)nbands + 8) * 4);  // start1 | wfirst
+    unsigned* aux = S.get<unsigned>(J_AUX, (2 * (uint64_t)nbands + 8) * 4);  // start1 (nbands + 3) | wfirst
     unsigned* tot = S.get<unsigned>(J_TTOT, (nt + 1) * 4);
     unsigned* start = S.get<unsigned>(J_TSTART, (nt + 1) * 4);
     unsigned* seg = S.get<unsigned>(J_SEG, ((nt + kScanSeg - 1) / kScanSeg + 1) * 8 + 64);
@@ -1195,7 +1199,7 @@ int bin_tiles(geohip_ctx* ctx, Scratch& S, const double* dx, const double* dy, u
     if (S.rc) return S.rc;
     if (hipMemsetAsync(misc, 0, kMiscWords * 4, st) != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
     unsigned* start1 = aux;
-    unsigned* wfirst = aux + nbands + 2;
+    unsigned* wfirst = aux + nbands + 3;
     BinPass a;
     memset(&a, 0, sizeof a);
     a.x = dx;
@@ -1208,9 +1212,10 @@ int bin_tiles(geohip_ctx* ctx, Scratch& S, const double* dx, const double* dy, u
     a.nbands = nbands;
     a.hist = hist1;
     a.nitems = misc + 4;
+    a.keep = keep;
     // level 1: bands
     bin_count<1><<<(unsigned)nblk, kBinThreads, 0, st>>>(a);
-    bin1_offsets<<<1, kTB, 0, st>>>(hist1, (unsigned)nblk, nbands + 1, start1);
+    bin1_offsets<<<1, kTB, 0, st>>>(hist1, (unsigned)nblk, nbands + 2, start1);
     bin_scatter<1><<<(unsigned)nblk, kBinThreads, 0, st>>>(a);
     // level 2: tiles within each band
     bin2_plan<<<1, kTB, 0, st>>>(start1, nbands, items, wfirst, misc + 4);
@@ -1227,11 +1232,12 @@ int bin_tiles(geohip_ctx* ctx, Scratch& S, const double* dx, const double* dy, u
     if (e != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, std::string("tile binning: ") + hipGetErrorString(e));
     if (keep_outside && n_outside_host) {
         uint64_t* pin = ctx_pinned(ctx);
-        if (hipMemcpyAsync(pin, start1 + nbands, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        if (hipMemcpyAsync(pin, start1 + nbands, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
             hipStreamSynchronize(st) != hipSuccess)
             return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "outside count readback failed");
-        const unsigned valid = (unsigned)(pin[0] & 0xffffffffu);
-        *n_outside_host = (unsigned)(n - valid);
+        const unsigned valid = (unsigned)(pin[0] & 0xffffffffu);          // start of the out-of-grid bin
+        const unsigned dropped = (unsigned)(pin[0] >> 32);               // start of the dropped bin
+        *n_outside_host = dropped - valid;
         if (outside_idx) *outside_idx = a.src.idx + valid;
     } else if (outside_idx) {
         *outside_idx = nullptr;
@@ -1514,6 +1520,7 @@ struct PolyCache {
     std::vector<int32_t> hrects;
     std::vector<PolyWork> hwork;
     std::vector<uint16_t> hslab;
+    std::vector<uint32_t> keep;  // cells of any polygon's G or C rectangles (empty: no filter)
     bool any_outside = false;
     void* dev_blob = nullptr;  // J_POLY buffer holding the uploaded tables
     size_t blob_bytes = 0;
@@ -1613,6 +1620,23 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const 
         }
 
         if (fresh.hwork.size() >= 0x7fffffffull) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "too many polygon work items");
+        // the cells any polygon can emit from: points elsewhere are dropped while binning
+        if ((uint64_t)nb * (uint64_t)nb <= (1ull << 24)) {
+            fresh.keep.assign(((uint64_t)nb * nb + 31) / 32, 0u);
+            for (uint32_t p = 0; p < npoly; p++) {
+                const PolyDev& P = pd[p];
+                for (uint32_t q = 0; q < P.ng + P.nc; q++) {
+                    const int32_t* R = &hrects[4 * ((q < P.ng ? P.goff : P.coff) + (q < P.ng ? q : q - P.ng))];
+                    const int32_t a0 = std::max(R[0], 0), a1 = std::min(R[1], nb - 1);
+                    const int32_t c0 = std::max(R[2], 0), c1 = std::min(R[3], nb - 1);
+                    for (int32_t a = a0; a <= a1; a++)
+                        for (int32_t c = c0; c <= c1; c++) {
+                            const uint64_t k = (uint64_t)a * nb + c;
+                            fresh.keep[k >> 5] |= 1u << (k & 31);
+                        }
+                }
+            }
+        }
         fresh.grid = *grid;
         fresh.r = r;
         fresh.ring_off.assign(ring_off, ring_off + npoly + 1);
@@ -1628,28 +1652,24 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const 
     const std::vector<PolyWork>& hwork = pc->hwork;
     const std::vector<uint16_t>& hslab = pc->hslab;
     const bool any_outside = pc->any_outside;
+    const std::vector<uint32_t>& keep = pc->keep;
     Scratch S{ctx};
     const double *dx, *dy;
     rc = ctx_stage_xy(ctx, x, y, n, 0, &dx, &dy);
     if (rc) return rc;
-    TileBins tb;
-    unsigned* oidx = nullptr;
-    unsigned n_out = 0;
     const auto t_planned = now();
-    rc = bin_tiles(ctx, S, dx, dy, n, geo, any_outside, &tb, &oidx, any_outside ? &n_out : nullptr);
-    if (rc) return rc;
-    const auto t_binned = now();
     // polygon tables in one device blob: PolyDev[] | vx | vy | rects | work | slab lists
     const size_t sz_p = npoly * sizeof(PolyDev), sz_v = hvx.size() * 8, sz_r = hrects.size() * 4;
-    const size_t sz_w = hwork.size() * sizeof(PolyWork), sz_s = hslab.size() * 2;
+    const size_t sz_w = hwork.size() * sizeof(PolyWork), sz_s = hslab.size() * 2, sz_k = keep.size() * 4;
     const size_t off_v = (sz_p + 15) & ~(size_t)15;
     const size_t off_r = off_v + 2 * sz_v;
     const size_t off_w = (off_r + sz_r + 15) & ~(size_t)15;
     const size_t off_s = (off_w + sz_w + 15) & ~(size_t)15;
+    const size_t off_k = (off_s + sz_s + 15) & ~(size_t)15;
     void* pblob = nullptr;
-    rc = ctx_ensure(ctx, J_POLY, off_s + sz_s + 64, &pblob);
+    rc = ctx_ensure(ctx, J_POLY, off_k + sz_k + 64, &pblob);
     if (rc) return rc;
-    const bool upload = !(cached && pc->dev_blob == pblob && pc->blob_bytes == off_s + sz_s);
+    const bool upload = !(cached && pc->dev_blob == pblob && pc->blob_bytes == off_k + sz_k);
     char* bp = reinterpret_cast<char*>(pblob);
     PolyDev* dpoly = reinterpret_cast<PolyDev*>(bp);
     double* dvx = reinterpret_cast<double*>(bp + off_v);
@@ -1657,6 +1677,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const 
     int32_t* drects = reinterpret_cast<int32_t*>(bp + off_r);
     PolyWork* dwork = reinterpret_cast<PolyWork*>(bp + off_w);
     uint16_t* dslab = reinterpret_cast<uint16_t*>(bp + off_s);
+    unsigned* dkeep = sz_k ? reinterpret_cast<unsigned*>(bp + off_k) : nullptr;
     if (upload) {
         pc->dev_blob = nullptr;  // until the copies are issued
         if ((sz_p && hipMemcpyAsync(dpoly, pd.data(), sz_p, hipMemcpyHostToDevice, st) != hipSuccess) ||
@@ -1664,11 +1685,18 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const 
             (sz_v && hipMemcpyAsync(dvy, hvy.data(), sz_v, hipMemcpyHostToDevice, st) != hipSuccess) ||
             (sz_r && hipMemcpyAsync(drects, hrects.data(), sz_r, hipMemcpyHostToDevice, st) != hipSuccess) ||
             (sz_w && hipMemcpyAsync(dwork, hwork.data(), sz_w, hipMemcpyHostToDevice, st) != hipSuccess) ||
-            (sz_s && hipMemcpyAsync(dslab, hslab.data(), sz_s, hipMemcpyHostToDevice, st) != hipSuccess))
+            (sz_s && hipMemcpyAsync(dslab, hslab.data(), sz_s, hipMemcpyHostToDevice, st) != hipSuccess) ||
+            (sz_k && hipMemcpyAsync(dkeep, keep.data(), sz_k, hipMemcpyHostToDevice, st) != hipSuccess))
             return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "polygon upload failed");
         pc->dev_blob = pblob;
-        pc->blob_bytes = off_s + sz_s;
+        pc->blob_bytes = off_k + sz_k;
     }
+    TileBins tb;
+    unsigned* oidx = nullptr;
+    unsigned n_out = 0;
+    rc = bin_tiles(ctx, S, dx, dy, n, geo, any_outside, &tb, &oidx, any_outside ? &n_out : nullptr, dkeep);
+    if (rc) return rc;
+    const auto t_binned = now();
     const unsigned nwork = (unsigned)hwork.size();
     const unsigned nob = (any_outside && n_out) ? (npoly < 4096u ? npoly : 4096u) : 0u;
     const uint64_t nslots = (uint64_t)nwork + nob;
