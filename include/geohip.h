@@ -14,6 +14,8 @@
  *                         + JoinQuery.getReplicatedPointQueryStream    spatialOperators/join/JoinQuery.java:73-90
  *   geohip_range_ppoly <- PointPolygonRangeQuery.run, window branch   spatialOperators/range/PointPolygonRangeQuery.java:76-124
  *                         (one independent query per polygon)
+ *   geohip_ingest_points <- Deserialization.PointStream / TrajectoryStream map functions
+ *                         spatialStreams/Deserialization.java:47-80, 132-146, 223-228, 248-254, 306-321
  *   geohip_grid        <- UniformGrid getters                         spatialIndices/UniformGrid.java:136-146
  *                         (values copied from the Java object, so both constructors :47-85 are covered)
  *
@@ -141,6 +143,40 @@ int geohip_knn_merge_async(geohip_ctx* ctx, const double* dist, const uint32_t* 
 int geohip_range_pp_async(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
                           uint64_t n, double qx, double qy, double r, int approximate,
                           uint32_t* out_idx, uint64_t cap, uint64_t* out_count_dev);
+
+/* ---- ingest codec ---------------------------------------------- */
+/* A batch of '\n'-separated text records, as a Flink source hands them to the map functions of
+   Deserialization.PointStream / TrajectoryStream (spatialStreams/Deserialization.java:47-80),
+   parsed on the device into SoA coordinates:
+     GEOHIP_FMT_CSV     <- CSVTSVToSpatial.map   Deserialization.java:248-254 (attr_ts = -1)
+                           CSVTSVToTSpatial.map  Deserialization.java:306-321 (attr_ts = csvTsvSchemaAttr.get(1))
+     GEOHIP_FMT_GEOJSON <- GeoJSONToSpatial.map  Deserialization.java:132-146 (one Kafka message value per line)
+     GEOHIP_FMT_WKT     <- WKTToSpatial.map      Deserialization.java:223-228, getCoordinate :1510-1514
+   and the Point constructor's cell (spatialObjects/Point.java:60-66 -> HelperClass.java:104-116)
+   as out_cell[i] = cx * grid->n + cy for a valid key (0 <= cx, cy < n), else 0xffffffff.
+   Record i is the i-th line; a final empty line (text ending in '\n') is not a record.
+   Every parsed value is the double Double.parseDouble / the JSON and WKT readers produce
+   (correctly rounded).  Records the device grammar cannot decide -- malformed ones, where the
+   reference throws, and rare valid forms (hex significands, 6+ digit exponents, quotes inside
+   a number, Z/M ordinates) -- make the call return GEOHIP_ERR_UNSUPPORTED with *out_bad = the
+   first such record; the caller hands that batch to the reference deserializer.
+   GEOHIP_MEM_DEVICE: text (16-byte aligned) and outputs are device pointers.
+   *out_count = number of records (GEOHIP_ERR_CAPACITY if > cap; outputs hold the first cap). */
+#define GEOHIP_FMT_CSV 0
+#define GEOHIP_FMT_GEOJSON 1
+#define GEOHIP_FMT_WKT 2
+typedef struct geohip_ingest_spec {
+    int32_t format;  /* GEOHIP_FMT_* */
+    int32_t delim;   /* CSV/TSV: the one-byte `delimiter` string (not a regex metacharacter) */
+    int32_t attr_x;  /* csvTsvSchemaAttr.get(2) */
+    int32_t attr_y;  /* csvTsvSchemaAttr.get(3) */
+    int32_t attr_ts; /* csvTsvSchemaAttr.get(1) for CSVTSVToTSpatial (Long.valueOf), -1: none */
+    int32_t reserved;
+} geohip_ingest_spec;
+int geohip_ingest_points(geohip_ctx* ctx, const geohip_grid* grid, const geohip_ingest_spec* spec,
+                         const char* text, uint64_t nbytes, double* out_x, double* out_y,
+                         int64_t* out_ts /* nullable */, uint32_t* out_cell /* nullable */,
+                         uint64_t cap, uint64_t* out_count, uint64_t* out_bad);
 
 /* ---- host-side planning introspection (no device needed) ------------------------------ */
 /* Query-cell sets of a point query as rectangles: point in G iff in any g rect; point in C

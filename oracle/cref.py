@@ -19,6 +19,11 @@ class Grid(ctypes.Structure):
     _fields_ = [("min_x", c_double), ("min_y", c_double), ("cell_len", c_double), ("n", c_int32)]
 
 
+class IngestSpec(ctypes.Structure):
+    _fields_ = [("format", c_int32), ("delim", c_int32), ("fx", c_int32), ("fy", c_int32), ("fts", c_int32),
+                ("reserved", c_int32)]
+
+
 def _load():
     if not LIB.exists():
         import subprocess
@@ -42,6 +47,11 @@ def _load():
                                          c_uint32, c_void_p, c_void_p, POINTER(c_uint32)]),
         "geohip_oracle_join_pp": (c_int64, [POINTER(Grid), POINTER(Grid), c_void_p, c_void_p, c_uint64, c_void_p,
                                             c_void_p, c_uint64, c_double, c_int, c_void_p, c_uint64]),
+        "geohip_oracle_ingest_record": (c_int, [POINTER(IngestSpec), POINTER(Grid), ctypes.c_char_p, c_uint64,
+                                                POINTER(c_double), POINTER(c_double), POINTER(c_int64),
+                                                POINTER(c_uint32)]),
+        "geohip_oracle_ingest": (c_int64, [POINTER(IngestSpec), POINTER(Grid), c_void_p, c_uint64, c_void_p,
+                                           c_void_p, c_void_p, c_void_p, c_uint64]),
         "geohip_oracle_range_ppoly": (c_int64, [POINTER(Grid), c_void_p, c_void_p, c_uint64, c_void_p, c_void_p,
                                                 c_void_p, c_uint32, c_double, c_int, c_void_p, c_uint64]),
     }
@@ -145,3 +155,42 @@ def point_polygon(px, py, vx, vy):
     vx = np.ascontiguousarray(vx, np.float64)
     vy = np.ascontiguousarray(vy, np.float64)
     return lib.geohip_oracle_point_polygon(px, py, _p(vx), _p(vy), len(vx))
+
+
+# ---- ingest codec (oracle/ingest_oracle.c) -------------------------------------------------
+CSV, GEOJSON, WKT = 0, 1, 2
+
+
+class IngestRejected(OracleError):
+    """The reference throws on record ``bad`` (NumberFormatException, IndexOutOfBounds, ...)."""
+
+    def __init__(self, bad):
+        super().__init__(f"record {bad} rejected by the reference grammar")
+        self.bad = bad
+
+
+def ingest_spec(fmt, delimiter=",", fx=0, fy=1, fts=-1) -> IngestSpec:
+    return IngestSpec(fmt, delimiter.encode()[0] if delimiter else 0, fx, fy, fts, 0)
+
+
+def ingest_record(spec: IngestSpec, rec: bytes, g: Grid | None = None):
+    """One record -> (x, y, ts, cell) or None where the reference throws."""
+    g = g if g is not None else grid(0.0, 0.0, 1.0, 1)
+    x, y, ts, c = c_double(), c_double(), c_int64(), c_uint32()
+    rc = lib.geohip_oracle_ingest_record(ctypes.byref(spec), ctypes.byref(g), rec, len(rec), ctypes.byref(x),
+                                         ctypes.byref(y), ctypes.byref(ts), ctypes.byref(c))
+    return None if rc else (x.value, y.value, ts.value, c.value)
+
+
+def ingest(spec: IngestSpec, text: bytes, g: Grid | None = None):
+    """A '\n'-separated batch -> dict(x, y, ts, cell) (numpy); IngestRejected(bad) where it throws."""
+    g = g if g is not None else grid(0.0, 0.0, 1.0, 1)
+    cap = text.count(b"\n") + 1
+    x, y = np.empty(cap), np.empty(cap)
+    ts, cell = np.empty(cap, dtype=np.int64), np.empty(cap, dtype=np.uint32)
+    buf = np.frombuffer(text, dtype=np.uint8) if len(text) else np.zeros(1, dtype=np.uint8)
+    n = lib.geohip_oracle_ingest(ctypes.byref(spec), ctypes.byref(g), _p(buf), len(text), _p(x), _p(y), _p(ts),
+                                 _p(cell), cap)
+    if n < 0:
+        raise IngestRejected(-n - 1)
+    return {"x": x[:n], "y": y[:n], "ts": ts[:n], "cell": cell[:n]}

@@ -55,6 +55,22 @@ class Grid(ctypes.Structure):
                 ("reserved", c_int32)]
 
 
+FMT_CSV, FMT_GEOJSON, FMT_WKT = 0, 1, 2
+
+
+class IngestSpec(ctypes.Structure):
+    """geohip_ingest_spec: format, delimiter byte, csvTsvSchemaAttr x/y/ts indices."""
+    _fields_ = [("format", c_int32), ("delim", c_int32), ("attr_x", c_int32), ("attr_y", c_int32),
+                ("attr_ts", c_int32), ("reserved", c_int32)]
+
+
+def make_ingest_spec(fmt: int, delimiter: str = ",", attr_x: int = 0, attr_y: int = 1, attr_ts: int = -1) -> IngestSpec:
+    d = delimiter.encode() if delimiter else b"\0"
+    if len(d) != 1:
+        raise GeohipUnsupportedError("delimiter must be one byte")
+    return IngestSpec(fmt, d[0], attr_x, attr_y, attr_ts, 0)
+
+
 class Rect(ctypes.Structure):
     _fields_ = [("x0", c_int32), ("x1", c_int32), ("y0", c_int32), ("y1", c_int32)]
 
@@ -105,6 +121,10 @@ _SIGS = {
     "geohip_plan_cell": (c_int, [POINTER(Grid), c_double, c_double, POINTER(c_int32), POINTER(c_int32)]),
     "geohip_synth_uniform_async": (c_int, [_P, _P, _P, c_uint64, c_uint64, c_uint64, c_double, c_double, c_double,
                                            c_double]),
+    "geohip_ingest_points": (c_int, [_P, POINTER(Grid), POINTER(IngestSpec), _P, c_uint64, _P, _P, _P, _P, c_uint64,
+                                     POINTER(c_uint64), POINTER(c_uint64)]),
+    "geohip_debug_ingest_record": (c_int, [POINTER(IngestSpec), c_char_p, c_uint64, POINTER(c_double),
+                                           POINTER(c_double), POINTER(ctypes.c_int64)]),
     "geohip_debug_selftest_fp64": (c_int, [_P, _P, _P, c_uint64, _P, _P, _P, _P]),
     "geohip_debug_classify": (c_int, [POINTER(Grid), c_double, c_double, c_double, _P, _P, c_uint64, _P]),
     "geohip_debug_set_knn_fused": (None, [c_int]),
@@ -194,6 +214,16 @@ def plan_cell(grid: Grid, x: float, y: float):
     cx, cy = c_int32(0), c_int32(0)
     lib.geohip_plan_cell(ctypes.byref(grid), x, y, ctypes.byref(cx), ctypes.byref(cy))
     return cx.value, cy.value
+
+
+def debug_ingest_record(spec: IngestSpec, rec: bytes):
+    """The device record parser (ingest_parse.h) run on the host: (x, y, ts) or None if rejected."""
+    x, y, ts = c_double(), c_double(), ctypes.c_int64()
+    rc = lib.geohip_debug_ingest_record(ctypes.byref(spec), rec, len(rec), ctypes.byref(x), ctypes.byref(y),
+                                        ctypes.byref(ts))
+    if rc == ERR_ARG:
+        raise GeohipArgumentError("bad ingest spec")
+    return None if rc else (x.value, y.value, ts.value)
 
 
 def _ptr(a):
@@ -393,6 +423,43 @@ class Context:
                                     _ptr(vy), npoly, r, int(approximate), _ptr(out), cap, ctypes.byref(cnt))
         self._check(rc, "range_ppoly")
         return out[:cnt.value]
+
+    def ingest_points(self, spec: IngestSpec, text, grid: Grid | None = None, with_ts=False, with_cell=False,
+                      cap=None, out=None):
+        """geohip_ingest_points: text (bytes / uint8 numpy on the host, uint8 torch on the device)
+        -> dict(x, y[, ts][, cell]) trimmed to the record count.  Raises GeohipUnsupportedError
+        (attribute ``bad`` = first rejected record) where the device grammar rejects a record."""
+        if isinstance(text, (bytes, bytearray)):
+            text = np.frombuffer(text, dtype=np.uint8)
+        dev = self._mem_for(text)
+        nbytes = int(text.numel()) if dev else int(text.size)
+        if cap is None:
+            cap = nbytes // 2 + 1  # a record has at least one byte plus its '\n'
+        if out is None:
+            if dev:
+                import torch
+                mk = lambda dt: torch.empty(max(cap, 1), dtype=dt, device=text.device)  # noqa: E731
+                out = {"x": mk(torch.float64), "y": mk(torch.float64)}
+                if with_ts:
+                    out["ts"] = mk(torch.int64)
+                if with_cell:
+                    out["cell"] = mk(torch.int32)
+            else:
+                out = {"x": np.empty(max(cap, 1)), "y": np.empty(max(cap, 1))}
+                if with_ts:
+                    out["ts"] = np.empty(max(cap, 1), dtype=np.int64)
+                if with_cell:
+                    out["cell"] = np.empty(max(cap, 1), dtype=np.uint32)
+        cnt, bad = c_uint64(0), c_uint64(0)
+        rc = lib.geohip_ingest_points(self.h, ctypes.byref(grid) if grid is not None else None, ctypes.byref(spec),
+                                      _ptr(text), nbytes, _ptr(out["x"]), _ptr(out["y"]), _ptr(out.get("ts")),
+                                      _ptr(out.get("cell")), cap, ctypes.byref(cnt), ctypes.byref(bad))
+        if rc == ERR_UNSUPPORTED and bad.value != 2**64 - 1:
+            err = GeohipUnsupportedError(f"ingest_points: {lib.geohip_last_error(self.h).decode(errors='replace')}")
+            err.bad = bad.value
+            raise err
+        self._check(rc, "ingest_points")
+        return {k: v[:cnt.value] for k, v in out.items()}
 
     def synth_uniform_async(self, x, y, base, seed, bbox):
         min_x, max_x, min_y, max_y = bbox

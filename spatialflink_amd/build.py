@@ -27,8 +27,10 @@ COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "
 SOURCES = {
     "plan.cpp": ["-x", "c++", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"],
     "abi.cpp": ["-x", "c++", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"],
+    "ingest_abi.cpp": ["-x", "c++", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"],
     "pp_kernels.hip": ["-x", "hip", f"--offload-arch={ARCH}"],
     "cell_kernels.hip": ["-x", "hip", f"--offload-arch={ARCH}"],
+    "ingest.hip": ["-x", "hip", f"--offload-arch={ARCH}"],
 }
 
 

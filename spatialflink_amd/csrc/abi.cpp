@@ -26,6 +26,7 @@ enum Slot {
     S_MASK, S_UCNT, S_OFFS, S_TOTAL, S_OUT_IDX, S_OUT_PAIRS, S_SPILL_D, S_SPILL_I, S_SPILL_CNT, S_RLB,
     S_J0, S_J1, S_J2, S_J3, S_J4, S_J5, S_J6, S_J7, S_J8, S_J9, S_J10, S_J11, S_J12, S_J13, S_J14, S_J15,
     S_J16, S_J17, S_J18, S_J19, S_J20, S_J21, S_J22, S_J23,
+    S_I0, S_I1, S_I2, S_I3, S_I4, S_I5, S_I6, S_I7,
     S_COUNT
 };
 
@@ -689,6 +690,12 @@ int ctx_ensure(geohip_ctx* ctx, int slot, size_t bytes, void** out) {
     if (!rc) *out = ctx->buf[S_J0 + slot];
     return rc;
 }
+int ctx_ensure_ingest(geohip_ctx* ctx, int slot, size_t bytes, void** out) {
+    int rc = ensure(ctx, (Slot)(S_I0 + slot), bytes);
+    if (!rc) *out = ctx->buf[S_I0 + slot];
+    return rc;
+}
+int ctx_begin(geohip_ctx* ctx) { return begin(ctx); }
 hipStream_t ctx_stream(geohip_ctx* ctx) { return ctx->stream; }
 int ctx_mem(geohip_ctx* ctx) { return ctx->mem; }
 uint64_t* ctx_pinned(geohip_ctx* ctx) { return ctx->pinned; }

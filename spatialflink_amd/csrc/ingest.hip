@@ -1,0 +1,208 @@
+// ingest.hip -- gfx950 kernels of the ingest codec: a batch of
+// '\n'-separated CSV/TSV, GeoJSON or WKT point records -> SoA x[], y[] (+ timestamp, + cell).
+//
+// Replaces the per-record map functions of Deserialization.PointStream / TrajectoryStream
+// (/root/reference/src/main/java/GeoFlink/spatialStreams/Deserialization.java:47-62, 64-80;
+// CSVTSVToSpatial :248-254, CSVTSVToTSpatial :306-321, GeoJSONToSpatial :132-146,
+// WKTToSpatial :223-228) and the cell assignment of the Point constructor
+// (spatialObjects/Point.java:60-66 -> utils/HelperClass.java:104-116).
+//
+// Three launches per batch, all HBM-streaming:
+//   ingest_count  every block counts the record starts its 8 KB chunk owns (SWAR '\n' test on
+//                 16-byte loads);
+//   ingest_scan   one block turns the per-chunk counts into record bases (the record index of
+//                 a record is its position in the batch, as in the arrival-ordered stream);
+//   ingest_parse  every block stages its chunk (+ a 4 KB tail for straddling records) in LDS
+//                 with 16-byte loads, lists its record starts in order (block scan), and parses
+//                 one record per lane with the ingest_parse.h functions (Eisel-Lemire fp64),
+//                 writing x/y/ts/cell coalesced by record index.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "device_common.h"
+#include "ingest.h"
+
+namespace geohip {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr uint32_t kBytesPerThread = kIngestChunk / kThreads;  // 32: two 16-byte loads
+static_assert(kBytesPerThread == 32, "chunk layout");
+
+// bit 7 of each byte set iff that byte of w is '\n' (exact: no borrow between bytes)
+__device__ __forceinline__ uint32_t nl_bits(uint32_t w) {
+    const uint32_t t = w ^ 0x0a0a0a0au;
+    return ~(((t & 0x7f7f7f7fu) + 0x7f7f7f7fu) | t | 0x7f7f7f7fu);
+}
+
+// 16 bytes at text[p..p+16) (bytes at or past nbytes read as 0)
+__device__ __forceinline__ uint4 load16(const uint8_t* text, uint64_t p, uint64_t nbytes) {
+    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    if (p + 16 <= nbytes) {
+        const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(text + p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    }
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (int i = 0; i < 16; i++)
+        if (p + i < nbytes) w[i >> 2] |= (uint32_t)text[p + i] << (8 * (i & 3));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// '\n' mask of 32 bytes starting at p (bit i = byte p + i); only positions < lim count
+__device__ __forceinline__ uint32_t nl_mask32(const uint4& a, const uint4& b, uint64_t p, uint64_t lim) {
+    const uint32_t wv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const uint32_t z = nl_bits(wv[k]);
+        // gather bits 7, 15, 23, 31 into bits 4k .. 4k+3
+        const uint32_t g = ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+        m |= g << (4 * k);
+    }
+    if (p + 32 > lim) m &= p >= lim ? 0u : ((1u << (uint32_t)(lim - p)) - 1u);
+    return m;
+}
+
+// block-wide exclusive scan of one value per thread; returns the exclusive prefix, *total = sum
+__device__ __forceinline__ unsigned block_excl_scan(unsigned v, unsigned* s_wave, unsigned* total) {
+    const unsigned incl = wave_incl_scan(v);
+    const int lane = lane_id(), wid = threadIdx.x / kWave;
+    if (lane == kWave - 1) s_wave[wid] = incl;
+    __syncthreads();
+    unsigned base = 0, sum = 0;
+#pragma unroll
+    for (int w = 0; w < kThreads / kWave; w++) {
+        const unsigned s = s_wave[w];
+        base += w < wid ? s : 0u;
+        sum += s;
+    }
+    *total = sum;
+    return base + incl - v;
+}
+
+__global__ __launch_bounds__(kThreads) void ingest_count(const uint8_t* __restrict__ text, uint64_t nbytes,
+                                                        unsigned* __restrict__ chunk_cnt) {
+    __shared__ unsigned s_wave[kThreads / kWave];
+    const uint64_t p = (uint64_t)blockIdx.x * kIngestChunk + threadIdx.x * kBytesPerThread;
+    unsigned c = 0;
+    if (p < nbytes) {
+        const uint4 a = load16(text, p, nbytes), b = load16(text, p + 16, nbytes);
+        c = __builtin_popcount(nl_mask32(a, b, p, nbytes - 1));  // a '\n' at nbytes-1 starts nothing
+    }
+    unsigned total;
+    block_excl_scan(c, s_wave, &total);
+    if (threadIdx.x == 0) chunk_cnt[blockIdx.x] = total + (blockIdx.x == 0 ? 1u : 0u);  // record 0 at byte 0
+}
+
+__global__ __launch_bounds__(1024) void ingest_scan(const unsigned* __restrict__ cnt, uint64_t nchunks,
+                                                    unsigned long long* __restrict__ base,
+                                                    unsigned long long* __restrict__ total) {
+    __shared__ unsigned long long s_part[1024];
+    const uint64_t per = (nchunks + 1023) / 1024;
+    const uint64_t b0 = threadIdx.x * per, b1 = b0 + per < nchunks ? b0 + per : nchunks;
+    unsigned long long s = 0;
+    for (uint64_t b = b0; b < b1; b++) s += cnt[b];
+    s_part[threadIdx.x] = s;
+    __syncthreads();
+    // Hillis-Steele over 1024 partial sums (one launch per batch: not on the critical path)
+    for (int off = 1; off < 1024; off <<= 1) {
+        const unsigned long long v = threadIdx.x >= (unsigned)off ? s_part[threadIdx.x - off] : 0ull;
+        __syncthreads();
+        s_part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    unsigned long long run = s_part[threadIdx.x] - s;
+    for (uint64_t b = b0; b < b1; b++) {
+        base[b] = run;
+        run += cnt[b];
+    }
+    if (threadIdx.x == 1023) *total = s_part[1023];
+}
+
+// byte reader for the parsers: the staged LDS window first, global memory past it, and '\n'
+// past the end of the batch (every parser stops at '\n')
+struct LdsReader {
+    const uint8_t* lds;
+    uint64_t base;
+    uint32_t len;
+    const uint8_t* g;
+    uint64_t n;
+    __device__ __forceinline__ uint8_t operator()(uint64_t p) const {
+        const uint64_t o = p - base;
+        if (o < len) return lds[o];
+        return p < n ? g[p] : (uint8_t)'\n';
+    }
+};
+
+__global__ __launch_bounds__(kThreads) void ingest_parse(const uint8_t* __restrict__ text, uint64_t nbytes,
+                                                        IngestArgs a, const unsigned long long* __restrict__ chunk_base,
+                                                        double* __restrict__ x, double* __restrict__ y,
+                                                        int64_t* __restrict__ ts, uint32_t* __restrict__ cell,
+                                                        uint64_t cap, unsigned long long* __restrict__ bad) {
+    __shared__ uint4 s_text4[(kIngestChunk + kIngestTail) / 16];
+    __shared__ uint16_t s_start[kIngestChunk + 1];
+    __shared__ unsigned s_wave[kThreads / kWave];
+    const uint64_t c0 = (uint64_t)blockIdx.x * kIngestChunk;
+    const uint64_t stage_end = c0 + kIngestChunk + kIngestTail < nbytes ? c0 + kIngestChunk + kIngestTail : nbytes;
+    const uint32_t stage_len = (uint32_t)(stage_end - c0);
+    // stage: the chunk first (this thread's 32 bytes stay in registers for the '\n' scan)
+    const uint64_t p = c0 + threadIdx.x * kBytesPerThread;
+    const uint4 va = load16(text, p, nbytes), vb = load16(text, p + 16, nbytes);
+    s_text4[threadIdx.x * 2] = va;
+    s_text4[threadIdx.x * 2 + 1] = vb;
+    for (uint32_t i = kIngestChunk / 16 + threadIdx.x; i < (kIngestChunk + kIngestTail) / 16; i += kThreads) {
+        const uint64_t q = c0 + (uint64_t)i * 16;
+        if (q < nbytes) s_text4[i] = load16(text, q, nbytes);
+    }
+    // record starts owned by this chunk, in order: byte 0 of the batch, then q + 1 for each '\n' at q
+    const uint32_t m = p < nbytes ? nl_mask32(va, vb, p, nbytes - 1) : 0u;
+    const bool first = blockIdx.x == 0 && threadIdx.x == 0 && nbytes > 0;
+    const unsigned mine = __builtin_popcount(m) + (first ? 1u : 0u);
+    unsigned nrec;
+    unsigned at = block_excl_scan(mine, s_wave, &nrec);
+    if (first) s_start[at++] = 0;
+    for (uint32_t mm = m; mm; mm &= mm - 1) s_start[at++] = (uint16_t)(threadIdx.x * kBytesPerThread + __builtin_ctz(mm) + 1);
+    __syncthreads();
+    const LdsReader rd{reinterpret_cast<const uint8_t*>(s_text4), c0, stage_len, text, nbytes};
+    const uint64_t rbase = chunk_base[blockIdx.x];
+    for (unsigned i = threadIdx.x; i < nrec; i += kThreads) {
+        const uint64_t idx = rbase + i;
+        ingest::Parsed o;
+        o.ts = 0;
+        if (ingest::parse_record(rd, c0 + s_start[i], a.spec, &o) != ingest::kOk) {
+            atomicMin(bad, (unsigned long long)idx);
+            continue;
+        }
+        if (idx >= cap) continue;
+        x[idx] = o.x;
+        y[idx] = o.y;
+        if (ts) ts[idx] = o.ts;
+        if (cell) {
+            const int32_t cx = ingest::java_cell(o.x, a.min_x, a.cell_len);
+            const int32_t cy = ingest::java_cell(o.y, a.min_y, a.cell_len);
+            const bool ok = cx >= 0 && cx < a.n && cy >= 0 && cy < a.n;
+            cell[idx] = ok ? (uint32_t)cx * (uint32_t)a.n + (uint32_t)cy : 0xffffffffu;
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_ingest(const uint8_t* text, uint64_t nbytes, const IngestArgs& a, unsigned* chunk_cnt,
+                         unsigned long long* chunk_base, unsigned long long* total, double* x, double* y,
+                         int64_t* ts, uint32_t* cell, uint64_t cap, unsigned long long* bad, hipStream_t st,
+                         hipEvent_t ev0, hipEvent_t ev1) {
+    const uint64_t nchunks = ingest_chunks(nbytes);
+    if (ev0) (void)hipEventRecord(ev0, st);
+    if (nchunks == 0) {
+        (void)hipMemsetAsync(total, 0, sizeof(unsigned long long), st);
+    } else {
+        ingest_count<<<(unsigned)nchunks, kThreads, 0, st>>>(text, nbytes, chunk_cnt);
+        ingest_scan<<<1, 1024, 0, st>>>(chunk_cnt, nchunks, chunk_base, total);
+        ingest_parse<<<(unsigned)nchunks, kThreads, 0, st>>>(text, nbytes, a, chunk_base, x, y, ts, cell, cap, bad);
+    }
+    if (ev1) (void)hipEventRecord(ev1, st);
+    return hipGetLastError();
+}
+
+}  // namespace geohip

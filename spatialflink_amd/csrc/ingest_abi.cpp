@@ -1,0 +1,169 @@
+// ingest_abi.cpp -- geohip_ingest_points (include/geohip.h): argument checks the way the
+// reference fails, scratch, the three ingest launches (ingest.hip) and the count readback.
+// Also the CPU test hook geohip_debug_ingest_record, which runs the very parser the kernels run
+// (ingest_parse.h, host-compiled) on one record so the CPU suite can check its decisions.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <string>
+
+#include "geohip_internal.h"
+#include "ingest.h"
+#include "join.h"
+
+using namespace geohip;
+
+namespace {
+
+#define ICHK(expr)                                                                                  \
+    do {                                                                                            \
+        hipError_t e_ = (expr);                                                                     \
+        if (e_ != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+enum { I_TEXT, I_CNT, I_BASE, I_WORDS, I_X, I_Y, I_TS, I_CELL };
+
+// java.util.regex metacharacters: "\\s*" + delimiter + "\\s*" would not be a literal split
+bool delim_ok(int32_t d) {
+    if (d <= 0 || d >= 0x80 || d == '"' || d == '\n') return false;
+    return strchr("\\^$.|?*+()[]{}", d) == nullptr;
+}
+
+int check_spec(geohip_ctx* ctx, const geohip_ingest_spec* sp, ingest::Spec* out) {
+    if (!sp) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null spec");
+    if (sp->format < GEOHIP_FMT_CSV || sp->format > GEOHIP_FMT_WKT) return ctx_fail(ctx, GEOHIP_ERR_ARG, "unknown format");
+    out->format = sp->format;
+    out->delim = sp->delim;
+    out->fx = sp->attr_x;
+    out->fy = sp->attr_y;
+    out->fts = sp->attr_ts;
+    if (sp->format == GEOHIP_FMT_CSV) {
+        if (!delim_ok(sp->delim)) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "delimiter must be one literal byte");
+        if (sp->attr_x < 0 || sp->attr_y < 0 || sp->attr_ts < -1)
+            return ctx_fail(ctx, GEOHIP_ERR_ARG, "negative csvTsvSchemaAttr index");  // List.get(-1) throws
+        if (sp->attr_x > 4095 || sp->attr_y > 4095 || sp->attr_ts > 4095)
+            return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "field index > 4095");
+    } else {
+        out->fts = -1;
+    }
+    return GEOHIP_OK;
+}
+
+struct HostReader {
+    const uint8_t* b;
+    uint64_t n;
+    uint8_t operator()(uint64_t p) const { return p < n ? b[p] : (uint8_t)'\n'; }
+};
+
+}  // namespace
+
+extern "C" {
+
+int geohip_ingest_points(geohip_ctx* ctx, const geohip_grid* grid, const geohip_ingest_spec* spec, const char* text,
+                         uint64_t nbytes, double* out_x, double* out_y, int64_t* out_ts, uint32_t* out_cell,
+                         uint64_t cap, uint64_t* out_count, uint64_t* out_bad) {
+    int rc = ctx_begin(ctx);
+    if (rc) return rc;
+    if (!out_count || !out_bad) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null count output");
+    *out_count = 0;
+    *out_bad = UINT64_MAX;
+    if (cap && (!out_x || !out_y)) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null coordinate output");
+    if (out_cell && !grid) return ctx_fail(ctx, GEOHIP_ERR_ARG, "cell output needs a grid");
+    if (nbytes && !text) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null text");
+    IngestArgs a;
+    memset(&a, 0, sizeof a);
+    rc = check_spec(ctx, spec, &a.spec);
+    if (rc) return rc;
+    if (grid) {
+        a.min_x = grid->min_x;
+        a.min_y = grid->min_y;
+        a.cell_len = grid->cell_len;
+        a.n = grid->n;
+    }
+    if (nbytes >= (1ull << 40)) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "batch larger than 1 TiB");
+    const uint64_t nchunks = ingest_chunks(nbytes);
+    if (nchunks >= (1ull << 31)) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "batch too large");
+    hipStream_t st = ctx_stream(ctx);
+    const bool dev = ctx_mem(ctx) == GEOHIP_MEM_DEVICE;
+    void *cnt, *base, *words;
+    rc = ctx_ensure_ingest(ctx, I_CNT, nchunks * 4, &cnt);
+    if (!rc) rc = ctx_ensure_ingest(ctx, I_BASE, nchunks * 8, &base);
+    if (!rc) rc = ctx_ensure_ingest(ctx, I_WORDS, 64, &words);
+    if (rc) return rc;
+    const uint8_t* dtext = reinterpret_cast<const uint8_t*>(text);
+    double *dx = out_x, *dy = out_y;
+    int64_t* dts = out_ts;
+    uint32_t* dcell = out_cell;
+    if (dev) {
+        if (((uintptr_t)text & 15u) != 0) return ctx_fail(ctx, GEOHIP_ERR_ARG, "device text must be 16-byte aligned");
+    } else {
+        void *t, *px, *py, *pts = nullptr, *pc = nullptr;
+        rc = ctx_ensure_ingest(ctx, I_TEXT, nbytes, &t);
+        if (!rc) rc = ctx_ensure_ingest(ctx, I_X, cap * 8, &px);
+        if (!rc) rc = ctx_ensure_ingest(ctx, I_Y, cap * 8, &py);
+        if (!rc && out_ts) rc = ctx_ensure_ingest(ctx, I_TS, cap * 8, &pts);
+        if (!rc && out_cell) rc = ctx_ensure_ingest(ctx, I_CELL, cap * 4, &pc);
+        if (rc) return rc;
+        if (nbytes) ICHK(hipMemcpyAsync(t, text, nbytes, hipMemcpyHostToDevice, st));
+        dtext = static_cast<const uint8_t*>(t);
+        dx = static_cast<double*>(px);
+        dy = static_cast<double*>(py);
+        dts = static_cast<int64_t*>(pts);
+        dcell = static_cast<uint32_t*>(pc);
+    }
+    unsigned long long* w = static_cast<unsigned long long*>(words);  // [0] total, [1] first rejected record
+    ICHK(hipMemsetAsync(w + 1, 0xff, 8, st));
+    hipEvent_t e0, e1;
+    ctx_timing_events(ctx, &e0, &e1);
+    hipError_t e = launch_ingest(dtext, nbytes, a, static_cast<unsigned*>(cnt), static_cast<unsigned long long*>(base),
+                                 w, dx, dy, dts, dcell, cap, w + 1, st, e0, e1);
+    if (e != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, std::string("ingest launch: ") + hipGetErrorString(e));
+    uint64_t* pinned = ctx_pinned(ctx);
+    ICHK(hipMemcpyAsync(pinned, w, 16, hipMemcpyDeviceToHost, st));
+    ICHK(hipStreamSynchronize(st));
+    const uint64_t total = pinned[0], bad = pinned[1];
+    *out_count = total;
+    *out_bad = bad;
+    if (!dev) {
+        const uint64_t m = total < cap ? total : cap;
+        if (m) {
+            ICHK(hipMemcpy(out_x, dx, m * 8, hipMemcpyDeviceToHost));
+            ICHK(hipMemcpy(out_y, dy, m * 8, hipMemcpyDeviceToHost));
+            if (out_ts) ICHK(hipMemcpy(out_ts, dts, m * 8, hipMemcpyDeviceToHost));
+            if (out_cell) ICHK(hipMemcpy(out_cell, dcell, m * 4, hipMemcpyDeviceToHost));
+        }
+    }
+    if (bad != UINT64_MAX)
+        return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED,
+                        "record " + std::to_string(bad) + " is malformed or outside the device grammar");
+    if (total > cap) return ctx_fail(ctx, GEOHIP_ERR_CAPACITY, "output capacity too small; *out_count = required");
+    return GEOHIP_OK;
+}
+
+// Test hook: the device parser (ingest_parse.h) compiled for the host, on one record
+// (rec[0..len), no '\n' inside).  Returns GEOHIP_OK, GEOHIP_ERR_UNSUPPORTED (rejected) or
+// GEOHIP_ERR_ARG (bad spec).
+int geohip_debug_ingest_record(const geohip_ingest_spec* spec, const char* rec, uint64_t len, double* x, double* y,
+                               int64_t* ts) {
+    ingest::Spec sp;
+    if (!spec || spec->format < 0 || spec->format > 2) return GEOHIP_ERR_ARG;
+    sp.format = spec->format;
+    sp.delim = spec->delim;
+    sp.fx = spec->attr_x;
+    sp.fy = spec->attr_y;
+    sp.fts = spec->format == GEOHIP_FMT_CSV ? spec->attr_ts : -1;
+    if (spec->format == GEOHIP_FMT_CSV && (!delim_ok(spec->delim) || sp.fx < 0 || sp.fy < 0 || sp.fts < -1))
+        return GEOHIP_ERR_ARG;
+    const HostReader rd{reinterpret_cast<const uint8_t*>(rec), len};
+    ingest::Parsed o;
+    o.x = o.y = 0.0;
+    o.ts = 0;
+    if (ingest::parse_record(rd, 0, sp, &o) != ingest::kOk) return GEOHIP_ERR_UNSUPPORTED;
+    *x = o.x;
+    *y = o.y;
+    *ts = o.ts;
+    return GEOHIP_OK;
+}
+
+}  // extern "C"

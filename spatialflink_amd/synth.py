@@ -81,3 +81,47 @@ def star_polygons(n_poly: int, seed: int, n_vert: int = 50, bbox=BEIJING, r_min=
         vy.extend(y.tolist() + [y[0]])
         off.append(len(vx))
     return np.array(off, np.uint32), np.array(vx), np.array(vy)
+
+
+def _digits(v: np.ndarray, width: int) -> np.ndarray:
+    """ASCII digits of non-negative int64 v, zero-padded to width: uint8 [len(v), width]."""
+    p = np.int64(10) ** np.arange(width - 1, -1, -1, dtype=np.int64)
+    return ((v[:, None] // p[None, :]) % 10 + 48).astype(np.uint8)
+
+
+def csv_text(n: int, seed: int, bbox=BEIJING, frac_digits: int = 13, ts0: int = 1611022449423,
+             chunk: int = 1 << 20):
+    """CSVTSVToTSpatial records "oid,ts,x,y\\n" (csvTsvSchemaAttr [0, 1, 2, 3]) for the uniform
+    window ``uniform(n, seed)`` rounded to frac_digits decimals: oid = record index (no leading
+    zeros, so records are ragged), ts = ts0 + index, x/y fixed-point with frac_digits fraction digits.
+
+    Returns (text bytes as a uint8 array, X, Y) where X / 10**frac_digits (an exact int64 over an
+    exact power of ten, so one correctly rounded fp64 division) is bit-for-bit the double
+    Double.parseDouble returns for the x text; likewise Y."""
+    x, y = uniform(n, seed, bbox)
+    scale = 10.0 ** frac_digits
+    X = np.rint(x * scale).astype(np.int64)
+    Y = np.rint(y * scale).astype(np.int64)
+    if max(abs(bbox[0]), abs(bbox[1]), abs(bbox[2]), abs(bbox[3])) * scale >= 2.0 ** 53 or min(bbox) < 0:
+        raise ValueError("fixed-point synth text needs non-negative coordinates below 2^53 / 10^frac_digits")
+    xi_w = len(str(int(bbox[1])))
+    yi_w = len(str(int(bbox[3])))
+    parts = []
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        idx = np.arange(s, e, dtype=np.int64)
+        oid = _digits(idx, 10)
+        keep_oid = np.cumsum(oid != 48, axis=1) > 0
+        keep_oid[:, -1] = True
+        m = e - s
+        comma = np.full((m, 1), ord(","), np.uint8)
+        dot = np.full((m, 1), ord("."), np.uint8)
+        nl = np.full((m, 1), ord("\n"), np.uint8)
+        ip = np.int64(10) ** frac_digits
+        mat = np.hstack([oid, comma, _digits(ts0 + idx, 13), comma,
+                         _digits(X[s:e] // ip, xi_w), dot, _digits(X[s:e] % ip, frac_digits), comma,
+                         _digits(Y[s:e] // ip, yi_w), dot, _digits(Y[s:e] % ip, frac_digits), nl])
+        keep = np.ones(mat.shape, bool)
+        keep[:, :10] = keep_oid
+        parts.append(mat[keep])
+    return np.concatenate(parts) if parts else np.zeros(0, np.uint8), X, Y
