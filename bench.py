@@ -12,6 +12,7 @@ The other configs are measured with ``--workload`` (same JSON contract, one line
   join   C3: 10k queries x 10M Gaussian-clustered data points per GPU, 500x500, r = 0.05
   ppoly  C4: 1k polygons (50 vertices) over 50M uniform points per GPU, 500x500, r = 0.005
   c5     C5 per shard: 25M uniform points per GPU, 1000x1000, kNN k = 100 + range r = 0.05
+  ingest SURVEY.md 8(f) row 1: 10M CSV records -> SoA x/y + ts + cell (device-resident text)
 
 Windows are device-resident before the timed region (synthetic: uniform windows are made on
 the device by the counter-based generator of spatialflink_amd.synth; Gaussian windows on the
@@ -20,7 +21,7 @@ is cycled so no step reads a window the Infinity Cache still holds.
 
 Prints ONE JSON line (rank 0) with roofline and cpu_baseline objects.
 
-    python bench.py --gpus 1 --steps 50 --warmup 5 [--workload knn|range|join|ppoly|c5]
+    python bench.py --gpus 1 --steps 50 --warmup 5 [--workload knn|range|join|ppoly|c5|ingest]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -47,7 +48,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--workload", choices=("knn", "range", "join", "ppoly", "c5"), default="knn")
+    p.add_argument("--workload", choices=("knn", "range", "join", "ppoly", "c5", "ingest"), default="knn")
     p.add_argument("--points", type=int, default=None, help="points per window per GPU (default: the config's)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -427,8 +428,70 @@ class C5Workload(KnnWorkload):
         return None
 
 
+class IngestWorkload(Workload):
+    """the window's CSV records (CSVTSVToTSpatial, Deserialization.java:
+    288-322, schema [oid, ts, x, y]) parsed into SoA x/y + Long ts + the Point constructor's cell
+    (Point.java:91-100 -> HelperClass.java:104-116) on the device; the C2 window size (10M records)
+    and grid (100x100).  Text is device-resident before the timed region."""
+    tag = "ingest"
+    kernel = "geohip ingest: ingest_count + chunk scan + ingest_parse (one batch)"
+    grid_n, n_default = 100, 10_000_000
+    windows = 1  # one batch of ~570 MB is > the 256 MiB Infinity Cache
+
+    def __init__(self, *a):
+        super().__init__(*a)
+        import torch
+        from spatialflink_amd import _abi, synth
+        self.n = self.args.points or self.n_default
+        bj = synth.BEIJING
+        self.grid = _abi.make_grid(bj[0], bj[2], (bj[1] - bj[0]) / self.grid_n, self.grid_n)
+        text, self.X, self.Y = synth.csv_text(self.n, 2 + 7 * self.rank)
+        self.nbytes = int(text.size)
+        self.text = torch.from_numpy(text).to(self.dev)
+        del text
+        self.spec = _abi.make_ingest_spec(_abi.FMT_CSV, ",", 2, 3, 1)
+        mk = lambda dt: torch.empty(self.n, dtype=dt, device=self.dev)  # noqa: E731
+        self.out = {"x": mk(torch.float64), "y": mk(torch.float64), "ts": mk(torch.int64), "cell": mk(torch.int32)}
+        got = self.ctx.ingest_points(self.spec, self.text, self.grid, with_ts=True, with_cell=True, cap=self.n,
+                                     out=self.out)
+        assert len(got["x"]) == self.n, "ingest record count"
+
+    def units_per_step(self):
+        return self.n
+
+    def step(self, s):
+        self.ctx.ingest_points(self.spec, self.text, self.grid, with_ts=True, with_cell=True, cap=self.n, out=self.out)
+
+    def algorithmic_bytes(self):  # text read once + x, y, ts, cell written
+        return self.nbytes + (8 + 8 + 8 + 4) * self.n
+
+    def config(self):
+        return {"workload": f"ingest: {self.n} CSV records 'oid,ts,x,y' (CSVTSVToTSpatial, 13 fraction digits) -> "
+                            f"SoA x/y + ts + cell, 100x100 Beijing UniformGrid (C2 window size)",
+                "records_per_batch_per_gpu": self.n, "text_bytes": self.nbytes, "grid": self.grid_n,
+                "parallelism": f"shard{self.world}"}
+
+    def cpu_baseline(self, seconds):
+        cref = _oracle()
+        from spatialflink_amd import synth
+        bj = synth.BEIJING
+        cg = cref.grid(bj[0], bj[2], (bj[1] - bj[0]) / self.grid_n, self.grid_n)
+        spec = cref.ingest_spec(0, ",", 2, 3, 1)  # GEOHIP_FMT_CSV
+        n = 1_000_000
+        text = bytes(synth.csv_text(n, 9)[0])
+
+        def one(i):
+            t0 = time.perf_counter()
+            cref.ingest(spec, text, cg)
+            return time.perf_counter() - t0
+        reps, t = _timed_loop(one, seconds, 30)
+        return {"value": reps * n / t, "unit": "points/sec", "cores": 1, "kind": "port",
+                "sample": f"{reps} x {n} CSV records (same grammar and shape), oracle/ingest_oracle.c single thread "
+                          f"(strtod-class parse + cell), {t:.1f} s"}
+
+
 WORKLOADS = {"knn": KnnWorkload, "range": RangeWorkload, "join": JoinWorkload, "ppoly": PpolyWorkload,
-             "c5": C5Workload}
+             "c5": C5Workload, "ingest": IngestWorkload}
 
 
 def main():

@@ -7,7 +7,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/prof gpurun_out/pmc
 export TMPDIR=/tmp
-WORKLOADS=${WORKLOADS:-knn range join ppoly c5}
+WORKLOADS=${WORKLOADS:-knn range join ppoly c5 ingest}
 if [ "${TESTS:-1}" = "1" ]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread \
       > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/pytest_gpu.log; exit 1; }

@@ -20,14 +20,15 @@ TAGS = {"knn": ("knn_scan", ("knn_scan", "knn_final"), 1),
         "join": ("join_probe", ("join_tile", "join_emit", "scan_seg_totals<unsigned long long>", "scan_totals<unsigned long long>",
                                  "scan_apply<unsigned long long>"), 1),
         "ppoly": ("ppoly_probe", ("ppoly_eval", "ppoly_emit", "ppoly_outside"), 1),
-        "c5": ("knn_scan_c5", ("knn_scan", "knn_final", "range_fused", "range_scan", "scan_units", "range_emit"), 2)}
+        "c5": ("knn_scan_c5", ("knn_scan", "knn_final", "range_fused", "range_scan", "scan_units", "range_emit"), 2),
+        "ingest": ("ingest", ("ingest_count", "ingest_scan", "ingest_parse"), 1)}
 
 
 def per_kernel(path):
     acc = defaultdict(list)
     with open(path) as f:
         for row in csv.DictReader(f):
-            name = row["Kernel_Name"].split("(")[0]
+            name = row["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
             acc[name].append(float(row["Counter_Value"]))
     return acc
 
