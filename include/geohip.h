@@ -13,6 +13,10 @@
  *   geohip_join_pp     <- PointPointJoinQuery.windowBased             spatialOperators/join/PointPointJoinQuery.java:113-172
  *                         + JoinQuery.getReplicatedPointQueryStream    spatialOperators/join/JoinQuery.java:73-90
  *   geohip_range_ppoly <- PointPolygonRangeQuery.run, window branch   spatialOperators/range/PointPolygonRangeQuery.java:76-124
+ *   geohip_join_ppoly  <- PointPolygonJoinQuery.windowBased            spatialOperators/join/PointPolygonJoinQuery.java:162-201
+ *                         + JoinQuery.getReplicatedPolygonQueryStream  spatialOperators/join/JoinQuery.java:93-115
+ *   geohip_knn_ppoly   <- PointPolygonKNNQuery.windowBased + merge     spatialOperators/knn/PointPolygonKNNQuery.java:162-236,
+ *                                                                      spatialOperators/knn/KNNQuery.java:204-272
  *                         (one independent query per polygon)
  *   geohip_ingest_points <- Deserialization.PointStream / TrajectoryStream map functions
  *                         spatialStreams/Deserialization.java:47-80, 132-146, 223-228, 248-254, 306-321
@@ -126,6 +130,25 @@ int geohip_range_ppoly(geohip_ctx* ctx, const geohip_grid* grid, const double* x
                        uint64_t n, const uint32_t* ring_off, const double* vx, const double* vy,
                        uint32_t npoly, double r, int approximate,
                        uint32_t* out_pairs, uint64_t cap, uint64_t* out_count);
+
+/* Point-polygon window join: the polygon stream replicated to its guaranteed and candidate
+   cells on grid_query (UniformGrid.java:193-206, 398-410), joined with the points' gridIDs on
+   grid_points; emits (point_idx, poly_idx) iff approximate or JTS point.distance(polygon) <= r
+   (no guaranteed-cell shortcut, PointPolygonJoinQuery.java:183-195).  Rings as for
+   geohip_range_ppoly (host arrays).  out_pairs: 2*cap uint32 (point_idx, poly_idx), unordered. */
+int geohip_join_ppoly(geohip_ctx* ctx, const geohip_grid* grid_points, const geohip_grid* grid_query,
+                      const double* x, const double* y, uint64_t n, const uint32_t* ring_off,
+                      const double* vx, const double* vy, uint32_t npoly, double r, int approximate,
+                      uint32_t* out_pairs, uint64_t cap, uint64_t* out_count);
+
+/* Point-polygon kNN of one query polygon (vx/vy[nv], host arrays, ring closed here): candidates
+   are the points of the polygon's G u C cells (no radius filter); distance = JTS
+   point.distance(polygon), or the bbox distance (DistanceFunctions.java:150-200) when
+   approximate.  Output: the min(k, candidates) smallest (distance, idx) ascending by distance
+   bits then idx (a NaN bbox distance ranks after +Infinity); 1 <= k <= GEOHIP_KNN_MAX_K. */
+int geohip_knn_ppoly(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
+                     uint64_t n, const double* vx, const double* vy, uint32_t nv, double r, uint32_t k,
+                     int approximate, uint32_t* out_idx, double* out_dist, uint32_t* out_count);
 
 /* ---- device-resident pipeline forms (GEOHIP_MEM_DEVICE pointers; enqueue only) -------- */
 /* Writes k (dist, idx) ascending to out_dist/out_idx (device), entries past the candidate

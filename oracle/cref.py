@@ -54,6 +54,10 @@ def _load():
                                            c_void_p, c_void_p, c_void_p, c_uint64]),
         "geohip_oracle_range_ppoly": (c_int64, [POINTER(Grid), c_void_p, c_void_p, c_uint64, c_void_p, c_void_p,
                                                 c_void_p, c_uint32, c_double, c_int, c_void_p, c_uint64]),
+        "geohip_oracle_join_ppoly": (c_int64, [POINTER(Grid), POINTER(Grid), c_void_p, c_void_p, c_uint64, c_void_p,
+                                               c_void_p, c_void_p, c_uint32, c_double, c_int, c_void_p, c_uint64]),
+        "geohip_oracle_knn_ppoly": (c_int, [POINTER(Grid), c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32,
+                                            c_double, c_uint32, c_int, c_void_p, c_void_p, POINTER(c_uint32)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -149,6 +153,40 @@ def range_ppoly(g: Grid, x, y, ring_off, vx, vy, r, approximate=False) -> np.nda
                                        r, int(approximate), _p(out), c)
     assert c2 == c
     return out[:c].copy()
+
+
+def join_ppoly(gp: Grid, gq: Grid, x, y, ring_off, vx, vy, r, approximate=False) -> np.ndarray:
+    """PointPolygonJoinQuery window join: pairs (point, polygon), oracle order."""
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    ring_off = np.ascontiguousarray(ring_off, np.uint32)
+    vx = np.ascontiguousarray(vx, np.float64)
+    vy = np.ascontiguousarray(vy, np.float64)
+    npoly = len(ring_off) - 1
+    args = (ctypes.byref(gp), ctypes.byref(gq), _p(x), _p(y), len(x), _p(ring_off), _p(vx), _p(vy), npoly, r,
+            int(approximate))
+    c = lib.geohip_oracle_join_ppoly(*args, None, 0)
+    if c < 0:
+        raise OracleError(f"oracle join_ppoly error {c}")
+    out = np.empty((max(c, 1), 2), np.uint32)
+    assert lib.geohip_oracle_join_ppoly(*args, _p(out), c) == c
+    return out[:c].copy()
+
+
+def knn_ppoly(g: Grid, x, y, vx, vy, r, k, approximate=False):
+    """PointPolygonKNNQuery window body: (idx, dist) ascending by (dist bits, idx)."""
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    vx = np.ascontiguousarray(vx, np.float64)
+    vy = np.ascontiguousarray(vy, np.float64)
+    oi = np.empty(k, np.uint32)
+    od = np.empty(k, np.float64)
+    cnt = c_uint32(0)
+    rc = lib.geohip_oracle_knn_ppoly(ctypes.byref(g), _p(x), _p(y), len(x), _p(vx), _p(vy), len(vx), r, k,
+                                     int(approximate), _p(oi), _p(od), ctypes.byref(cnt))
+    if rc != 0:
+        raise OracleError(f"oracle knn_ppoly error {rc}")
+    return oi[:cnt.value].copy(), od[:cnt.value].copy()
 
 
 def point_polygon(px, py, vx, vy):

@@ -567,6 +567,36 @@ int64_t geohip_oracle_join_pp(const or_grid* gd, const or_grid* gq, const double
     return OR_ERR_ARG;
 }
 
+/* One query polygon as the reference builds it: ring closed (Polygon.java:147-155), JTS
+   envelope, gridIDsSet = bbox cells on grid g unclipped (HelperClass.java:123-143), then
+   G = union of guaranteed squares, C = union of candidate squares minus G
+   (UniformGrid.java:193-206, 398-410).  rx/ry get nv+1 slots; returns OR_OK or an error. */
+typedef struct { double* rx; double* ry; int nv; or_env env; cellset G, C; } or_poly;
+static void poly_free(or_poly* P) { cl_free(&P->G); cl_free(&P->C); free(P->rx); free(P->ry); }
+static int poly_prep(const or_grid* g, const double* vx, const double* vy, int nv, double r, or_poly* P) {
+    if (nv <= 3) return OR_ERR_ARG; /* Polygon.java:53 */
+    P->rx = (double*)malloc(sizeof(double) * (nv + 1));
+    P->ry = (double*)malloc(sizeof(double) * (nv + 1));
+    memcpy(P->rx, vx, sizeof(double) * nv);
+    memcpy(P->ry, vy, sizeof(double) * nv);
+    if (!(P->rx[0] == P->rx[nv - 1] && P->ry[0] == P->ry[nv - 1])) { P->rx[nv] = P->rx[0]; P->ry[nv] = P->ry[0]; nv++; }
+    P->nv = nv;
+    P->env = ring_env(P->rx, P->ry, nv);
+    cl_init(&P->G); cl_init(&P->C);
+    int32_t x1 = j_d2i(floor((P->env.minx - g->min_x) / g->cell_len));
+    int32_t y1 = j_d2i(floor((P->env.miny - g->min_y) / g->cell_len));
+    int32_t x2 = j_d2i(floor((P->env.maxx - g->min_x) / g->cell_len));
+    int32_t y2 = j_d2i(floor((P->env.maxy - g->min_y) / g->cell_len));
+    if (x2 == INT32_MAX || y2 == INT32_MAX) { poly_free(P); return OR_ERR_HANG; }
+    int rc = 0;
+    for (int64_t a = x1; a <= x2 && !rc; a++)
+        for (int64_t c = y1; c <= y2 && !rc; c++) rc = add_guaranteed(g, &P->G, r, (int32_t)a, (int32_t)c);
+    for (int64_t a = x1; a <= x2 && !rc; a++)
+        for (int64_t c = y1; c <= y2 && !rc; c++) rc = add_candidate(g, &P->C, &P->G, r, (int32_t)a, (int32_t)c);
+    if (rc) poly_free(P);
+    return rc;
+}
+
 /* PointPolygonRangeQuery window body (PointPolygonRangeQuery.java:76-124) for npoly
    independent single-ring polygons (ring_off[npoly+1] into vx/vy; rings given as the
    caller's coordinate list, closed here per Polygon.java:147-155).  Pairs (poly, pt). */
@@ -577,38 +607,19 @@ int64_t geohip_oracle_range_ppoly(const or_grid* g, const double* x, const doubl
     if (g->n <= 0 || g->n > 99999 || !(g->cell_len > 0)) return OR_ERR_ARG;
     uint64_t out = 0;
     for (uint32_t pi = 0; pi < npoly; pi++) {
-        uint32_t b = ring_off[pi], e = ring_off[pi + 1];
-        int nv = (int)(e - b);
-        if (nv <= 3) return OR_ERR_ARG; /* Polygon.java:53 */
-        double* rx = (double*)malloc(sizeof(double) * (nv + 1));
-        double* ry = (double*)malloc(sizeof(double) * (nv + 1));
-        memcpy(rx, vx + b, sizeof(double) * nv);
-        memcpy(ry, vy + b, sizeof(double) * nv);
-        if (!(rx[0] == rx[nv - 1] && ry[0] == ry[nv - 1])) { rx[nv] = rx[0]; ry[nv] = ry[0]; nv++; }
-        or_env env = ring_env(rx, ry, nv);
-        int32_t x1 = j_d2i(floor((env.minx - g->min_x) / g->cell_len));
-        int32_t y1 = j_d2i(floor((env.miny - g->min_y) / g->cell_len));
-        int32_t x2 = j_d2i(floor((env.maxx - g->min_x) / g->cell_len));
-        int32_t y2 = j_d2i(floor((env.maxy - g->min_y) / g->cell_len));
-        if (x2 == INT32_MAX || y2 == INT32_MAX) { free(rx); free(ry); return OR_ERR_HANG; }
-        cellset G, C;
-        cl_init(&G); cl_init(&C);
-        int rc = 0;
-        for (int64_t a = x1; a <= x2 && !rc; a++)
-            for (int64_t c = y1; c <= y2 && !rc; c++) rc = add_guaranteed(g, &G, r, (int32_t)a, (int32_t)c);
-        for (int64_t a = x1; a <= x2 && !rc; a++)
-            for (int64_t c = y1; c <= y2 && !rc; c++) rc = add_candidate(g, &C, &G, r, (int32_t)a, (int32_t)c);
-        if (rc) { cl_free(&G); cl_free(&C); free(rx); free(ry); return rc; }
+        or_poly P;
+        int rc = poly_prep(g, vx + ring_off[pi], vy + ring_off[pi], (int)(ring_off[pi + 1] - ring_off[pi]), r, &P);
+        if (rc) return rc;
         for (uint64_t i = 0; i < n; i++) {
             int32_t cx, cy;
             geohip_oracle_cell(g, x[i], y[i], &cx, &cy);
-            int inG = cl_has(&G, cx, cy);
-            if (!inG && !cl_has(&C, cx, cy)) continue;
+            int inG = cl_has(&P.G, cx, cy);
+            if (!inG && !cl_has(&P.C, cx, cy)) continue;
             int emit = inG;
             if (!emit) {
                 double d = approximate
-                    ? geohip_oracle_bbox_distance(x[i], y[i], env.minx, env.miny, env.maxx, env.maxy)
-                    : geohip_oracle_point_polygon(x[i], y[i], rx, ry, nv);
+                    ? geohip_oracle_bbox_distance(x[i], y[i], P.env.minx, P.env.miny, P.env.maxx, P.env.maxy)
+                    : geohip_oracle_point_polygon(x[i], y[i], P.rx, P.ry, P.nv);
                 emit = d <= r;
             }
             if (emit) {
@@ -616,7 +627,101 @@ int64_t geohip_oracle_range_ppoly(const or_grid* g, const double* x, const doubl
                 out++;
             }
         }
-        cl_free(&G); cl_free(&C); free(rx); free(ry);
+        poly_free(&P);
     }
     return (int64_t)out;
+}
+
+/* PointPolygonJoinQuery window join (PointPolygonJoinQuery.java:162-201) with the polygon
+   stream replicated to its G and C cells on the query grid (JoinQuery.getReplicatedPolygonQueryStream,
+   JoinQuery.java:93-115): a point joins a polygon iff its gridID (point grid) equals one of
+   them, and approximate or JTS distance <= r.  No guaranteed-cell shortcut.  Pairs (pt, poly). */
+int64_t geohip_oracle_join_ppoly(const or_grid* gp, const or_grid* gq, const double* x, const double* y, uint64_t n,
+                                 const uint32_t* ring_off, const double* vx, const double* vy,
+                                 uint32_t npoly, double r, int approximate,
+                                 uint32_t* out_pairs, uint64_t cap) {
+    if (gp->n <= 0 || gp->n > 99999 || !(gp->cell_len > 0)) return OR_ERR_ARG;
+    if (gq->n <= 0 || gq->n > 99999 || !(gq->cell_len > 0)) return OR_ERR_ARG;
+    uint64_t out = 0;
+    int32_t* pc = (int32_t*)malloc(sizeof(int32_t) * 2 * (n ? n : 1));
+    if (!pc) return OR_ERR_OOM;
+    for (uint64_t i = 0; i < n; i++) geohip_oracle_cell(gp, x[i], y[i], &pc[2 * i], &pc[2 * i + 1]);
+    for (uint32_t pi = 0; pi < npoly; pi++) {
+        or_poly P;
+        int rc = poly_prep(gq, vx + ring_off[pi], vy + ring_off[pi], (int)(ring_off[pi + 1] - ring_off[pi]), r, &P);
+        if (rc) { free(pc); return rc; }
+        for (uint64_t i = 0; i < n; i++) {
+            int32_t cx = pc[2 * i], cy = pc[2 * i + 1];
+            if (!cl_has(&P.G, cx, cy) && !cl_has(&P.C, cx, cy)) continue;
+            if (approximate || geohip_oracle_point_polygon(x[i], y[i], P.rx, P.ry, P.nv) <= r) {
+                if (out < cap) { out_pairs[2 * out] = (uint32_t)i; out_pairs[2 * out + 1] = pi; }
+                out++;
+            }
+        }
+        poly_free(&P);
+    }
+    free(pc);
+    return (int64_t)out;
+}
+
+/* PointPolygonKNNQuery window body (PointPolygonKNNQuery.java:162-236): candidates are the
+   points of G u C of the query polygon, distance = JTS point.distance(polygon) (or the bbox
+   distance, DistanceFunctions.java:150-200, when approximate); no radius filter; same
+   build contract as geohip_oracle_knn_pp: the k smallest (dist, idx), ascending. */
+/* (distance bits, idx) keys: for the non-negative distances of this path the bit order is the
+   value order; a NaN (the approximate bbox distance of a NaN coordinate) is canonicalised to
+   0x7ff8000000000000 and so ranks after +Infinity -- the total order the device selects by. */
+typedef struct { uint64_t d; uint32_t i; } kbent;
+static int kbless(kbent a, kbent b) { return a.d < b.d || (a.d == b.d && a.i < b.i); }
+static void kb_down(kbent* h, int n, int k) {
+    for (;;) {
+        int l = 2 * k + 1, r = l + 1, m = k;
+        if (l < n && kbless(h[m], h[l])) m = l;
+        if (r < n && kbless(h[m], h[r])) m = r;
+        if (m == k) return;
+        kbent t = h[k]; h[k] = h[m]; h[m] = t; k = m;
+    }
+}
+static void kb_up(kbent* h, int k) {
+    while (k > 0) {
+        int p = (k - 1) / 2;
+        if (!kbless(h[p], h[k])) return;
+        kbent t = h[k]; h[k] = h[p]; h[p] = t; k = p;
+    }
+}
+static int kbcmp(const void* a, const void* b) {
+    kbent x = *(const kbent*)a, y = *(const kbent*)b;
+    return kbless(x, y) ? -1 : kbless(y, x) ? 1 : 0;
+}
+
+int geohip_oracle_knn_ppoly(const or_grid* g, const double* x, const double* y, uint64_t n,
+                            const double* vx, const double* vy, uint32_t nv, double r, uint32_t k,
+                            int approximate, uint32_t* out_idx, double* out_dist, uint32_t* out_count) {
+    *out_count = 0;
+    if (g->n <= 0 || g->n > 99999 || !(g->cell_len > 0) || k == 0) return OR_ERR_ARG;
+    or_poly P;
+    int rc = poly_prep(g, vx, vy, (int)nv, r, &P);
+    if (rc) return rc;
+    kbent* h = (kbent*)malloc(sizeof(kbent) * k);
+    int hn = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        int32_t cx, cy;
+        geohip_oracle_cell(g, x[i], y[i], &cx, &cy);
+        if (!cl_has(&P.G, cx, cy) && !cl_has(&P.C, cx, cy)) continue;
+        double d = approximate
+            ? geohip_oracle_bbox_distance(x[i], y[i], P.env.minx, P.env.miny, P.env.maxx, P.env.maxy)
+            : geohip_oracle_point_polygon(x[i], y[i], P.rx, P.ry, P.nv);
+        uint64_t bits;
+        memcpy(&bits, &d, 8);
+        if (d != d) bits = 0x7ff8000000000000ull;
+        kbent e = {bits, (uint32_t)i};
+        if (hn < (int)k) { h[hn] = e; kb_up(h, hn); hn++; }
+        else if (kbless(e, h[0])) { h[0] = e; kb_down(h, hn, 0); }
+    }
+    qsort(h, (size_t)hn, sizeof(kbent), kbcmp);
+    for (int i = 0; i < hn; i++) { out_idx[i] = h[i].i; memcpy(&out_dist[i], &h[i].d, 8); }
+    *out_count = (uint32_t)hn;
+    free(h);
+    poly_free(&P);
+    return OR_OK;
 }

@@ -701,3 +701,53 @@ def range_ppoly(grid, xs, ys, rings, r, approximate=False):
             if d <= r:
                 out.append((pi, i))
     return out
+
+
+def join_ppoly(ugrid, qgrid, xs, ys, rings, r, approximate=False):
+    """PointPolygonJoinQuery window join (PointPolygonJoinQuery.java:162-201): each polygon is
+    replicated once per cell of G and of C computed on qGrid (JoinQuery.java:93-115); a point
+    joins a copy iff its uGrid gridID string equals the copy's gridID; JoinFunction emits when
+    approximate or JTS distance <= r (no guaranteed shortcut).  Returns (point_idx, poly_idx)."""
+    out = []
+    for pi, coords in enumerate(rings):
+        ring = close_ring(coords)
+        if ring is None:
+            raise ValueError("polygon needs more than 3 coordinates (Polygon.java:53)")
+        ids = bbox_grid_ids(qgrid, ring_envelope(ring))
+        G = qgrid.guaranteed_cells_poly(r, ids)
+        C = qgrid.candidate_cells_poly(r, ids, G)
+        replicated = G | C  # disjoint sets: one copy per key
+        for i, (x, y) in enumerate(zip(xs, ys)):
+            if ugrid.key(x, y) not in replicated:
+                continue
+            if approximate or jts_point_polygon_distance(x, y, ring) <= r:
+                out.append((i, pi))
+    return out
+
+
+def knn_ppoly(grid, xs, ys, coords, r, k, approximate=False):
+    """PointPolygonKNNQuery window body (PointPolygonKNNQuery.java:162-236) under the build
+    contract of knn_pp: per-cell max-heaps of size k (replace only when the head is larger,
+    :199-221) over the points of G u C, then the k smallest (distance, idx) over all cells,
+    ascending.  A NaN (approximate bbox distance of a NaN coordinate) ranks last."""
+    ring = close_ring(coords)
+    if ring is None:
+        raise ValueError("polygon needs more than 3 coordinates (Polygon.java:53)")
+    bbox = ring_envelope(ring)
+    ids = bbox_grid_ids(grid, bbox)
+    G = grid.guaranteed_cells_poly(r, ids)
+    C = grid.candidate_cells_poly(r, ids, G)
+    cells = {}
+    for i, (x, y) in enumerate(zip(xs, ys)):
+        key = grid.key(x, y)
+        if key in C or key in G:
+            d = bbox_distance(x, y, bbox) if approximate else jts_point_polygon_distance(x, y, ring)
+            cells.setdefault(key, []).append((i, d))
+
+    def rank(e):
+        d = e[1]
+        return (math.inf, 1, e[0]) if d != d else (d, 0, e[0])
+    merged = []
+    for pts in cells.values():
+        merged += sorted(pts, key=rank)[:k]  # the cell's k smallest (unique idx)
+    return sorted(merged, key=rank)[:k]

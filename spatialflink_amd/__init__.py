@@ -4,8 +4,10 @@ reference operator API (spatialflink_amd.operators).  See DESIGN.md."""
 from . import _abi
 from ._abi import Context, GeohipError, GeohipArgumentError, GeohipCapacityError, GeohipDeviceError
 from .operators import (QueryConfiguration, QueryType, UniformGrid, Point, Polygon, PointWindow,
-                        PointPointRangeQuery, PointPointKNNQuery, PointPointJoinQuery, PointPolygonRangeQuery)
+                        PointPointRangeQuery, PointPointKNNQuery, PointPointJoinQuery, PointPolygonRangeQuery,
+                        PointPolygonJoinQuery, PointPolygonKNNQuery)
 
 __all__ = ["Context", "GeohipError", "GeohipArgumentError", "GeohipCapacityError", "GeohipDeviceError",
            "QueryConfiguration", "QueryType", "UniformGrid", "Point", "Polygon", "PointWindow",
-           "PointPointRangeQuery", "PointPointKNNQuery", "PointPointJoinQuery", "PointPolygonRangeQuery"]
+           "PointPointRangeQuery", "PointPointKNNQuery", "PointPointJoinQuery", "PointPolygonRangeQuery",
+           "PointPolygonJoinQuery", "PointPolygonKNNQuery"]

@@ -116,6 +116,10 @@ _SIGS = {
                                           c_double, c_int, POINTER(c_uint64)]),
     "geohip_range_ppoly": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, _P, _P, _P, c_uint32, c_double, c_int, _P,
                                    c_uint64, POINTER(c_uint64)]),
+    "geohip_join_ppoly": (c_int, [_P, POINTER(Grid), POINTER(Grid), _P, _P, c_uint64, _P, _P, _P, c_uint32, c_double,
+                                  c_int, _P, c_uint64, POINTER(c_uint64)]),
+    "geohip_knn_ppoly": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, _P, _P, c_uint32, c_double, c_uint32, c_int, _P,
+                                 _P, POINTER(c_uint32)]),
     "geohip_plan_point": (c_int, [POINTER(Grid), c_double, c_double, c_double, POINTER(Rect), POINTER(c_uint32),
                                   POINTER(Rect), POINTER(c_uint32), POINTER(c_int32), POINTER(c_int32)]),
     "geohip_plan_cell": (c_int, [POINTER(Grid), c_double, c_double, POINTER(c_int32), POINTER(c_int32)]),
@@ -423,6 +427,54 @@ class Context:
                                     _ptr(vy), npoly, r, int(approximate), _ptr(out), cap, ctypes.byref(cnt))
         self._check(rc, "range_ppoly")
         return out[:cnt.value]
+
+    def join_ppoly(self, grid_points: Grid, grid_query: Grid, x, y, ring_off, vx, vy, r, approximate=False, cap=None,
+                   out=None):
+        """Point-polygon join: pairs (point idx, polygon idx).  ``out``: optional [cap, 2] buffer."""
+        x, y = _f64(x), _f64(y)
+        self._mem_for(x, y)
+        ring_off = np.ascontiguousarray(ring_off, dtype=np.uint32)
+        vx = np.ascontiguousarray(vx, dtype=np.float64)
+        vy = np.ascontiguousarray(vy, dtype=np.float64)
+        npoly = len(ring_off) - 1
+        cnt = c_uint64(0)
+        args = (self.h, ctypes.byref(grid_points), ctypes.byref(grid_query), _ptr(x), _ptr(y), len(x), _ptr(ring_off),
+                _ptr(vx), _ptr(vy), npoly, r, int(approximate))
+        if out is not None:
+            cap = len(out) if cap is None else min(cap, len(out))
+        if cap is None:
+            rc = lib.geohip_join_ppoly(*args, None, 0, ctypes.byref(cnt))
+            if rc not in (OK, ERR_CAPACITY):
+                self._check(rc, "join_ppoly")
+            cap = cnt.value
+        if out is None:
+            if _is_device(x):
+                import torch
+                out = torch.empty((max(cap, 1), 2), dtype=torch.int32, device=x.device)
+            else:
+                out = np.empty((max(cap, 1), 2), dtype=np.uint32)
+        rc = lib.geohip_join_ppoly(*args, _ptr(out), cap, ctypes.byref(cnt))
+        self._check(rc, "join_ppoly")
+        return out[:cnt.value]
+
+    def knn_ppoly(self, grid: Grid, x, y, vx, vy, r, k, approximate=False):
+        """Point-polygon kNN of one polygon ring: (idx, dist) ascending by (dist, idx)."""
+        x, y = _f64(x), _f64(y)
+        dev = self._mem_for(x, y)
+        vx = np.ascontiguousarray(vx, dtype=np.float64)
+        vy = np.ascontiguousarray(vy, dtype=np.float64)
+        if dev:
+            import torch
+            oi = torch.empty(k, dtype=torch.int32, device=x.device)
+            od = torch.empty(k, dtype=torch.float64, device=x.device)
+        else:
+            oi = np.empty(k, dtype=np.uint32)
+            od = np.empty(k, dtype=np.float64)
+        cnt = c_uint32(0)
+        rc = lib.geohip_knn_ppoly(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), len(x), _ptr(vx), _ptr(vy), len(vx), r,
+                                  k, int(approximate), _ptr(oi), _ptr(od), ctypes.byref(cnt))
+        self._check(rc, "knn_ppoly")
+        return oi[:cnt.value], od[:cnt.value]
 
     def ingest_points(self, spec: IngestSpec, text, grid: Grid | None = None, with_ts=False, with_cell=False,
                       cap=None, out=None):

@@ -429,6 +429,7 @@ struct PairSink {
     unsigned* out;                    // write pass: pairs, u32 x 2
     uint64_t cap;                     // pairs at or beyond cap are dropped (size reported by the scan)
     int aligned8;                     // out is 8-byte aligned: one 8-byte store per pair
+    int swap;                         // store (b, a): the point-polygon join emits (point, polygon)
 };
 
 template <bool WRITE>
@@ -446,7 +447,8 @@ __device__ __forceinline__ void pairs_flush(uint2* buf, unsigned long long& cnt,
     for (unsigned t = lane_id(); t < (unsigned)cnt; t += kWave) {
         const unsigned long long p = base + t;
         if (p < s.cap) {
-            const uint2 v = buf[t];
+            const uint2 b = buf[t];
+            const uint2 v = s.swap ? make_uint2(b.y, b.x) : b;
             if (s.aligned8) {
                 reinterpret_cast<uint2*>(s.out)[p] = v;
             } else {
@@ -1072,12 +1074,17 @@ __global__ __launch_bounds__(kTB) void ppoly_emit(TileBins tb, const PolyWork* _
     pairs_end<true>(buf, cnt, &bsh, sink);
 }
 
-// out-of-grid points vs guaranteed rects reaching outside the grid (Lg == 0 bbox keys)
-template <bool WRITE>
+// out-of-grid points vs guaranteed rects reaching outside the grid (Lg == 0 bbox keys).
+// DIST (point-polygon join, exact): the polygon's rect list is (coff, nc) and a matching point
+// also needs the JTS distance <= r (the join has no guaranteed-cell shortcut).
+template <bool WRITE, bool DIST = false>
 __global__ __launch_bounds__(kTB) void ppoly_outside(const double* __restrict__ x, const double* __restrict__ y,
                                                      const unsigned* __restrict__ oidx, unsigned nout, double mnx,
                                                      double mny, double l, const PolyDev* __restrict__ polys,
-                                                     uint32_t npoly, const int32_t* __restrict__ rects, PairSink sink) {
+                                                     uint32_t npoly, const int32_t* __restrict__ rects, PairSink sink,
+                                                     const double* __restrict__ vx = nullptr,
+                                                     const double* __restrict__ vy = nullptr,
+                                                     const uint16_t* __restrict__ slabs = nullptr, double r = 0.0) {
     __shared__ uint2 pbuf[WRITE ? kTB / kWave : 1][WRITE ? kPolyPairs : 1];
     __shared__ unsigned long long bsh;
     const int wid = threadIdx.x / kWave;
@@ -1094,13 +1101,273 @@ __global__ __launch_bounds__(kTB) void ppoly_outside(const double* __restrict__ 
             unsigned pid = 0;
             if (t < nout) {
                 pid = oidx[t];
-                const int32_t cx = d_axis_cell(x[pid], mnx, l), cy = d_axis_cell(y[pid], mny, l);
-                hit = in_rects(rects + 4 * P.goff, P.ng, cx, cy);
+                const double px = x[pid], py = y[pid];
+                const int32_t cx = d_axis_cell(px, mnx, l), cy = d_axis_cell(py, mny, l);
+                hit = DIST ? in_rects(rects + 4 * P.coff, P.nc, cx, cy) : in_rects(rects + 4 * P.goff, P.ng, cx, cy);
+                if (DIST && hit)
+                    hit = point_polygon_within(px, py, vx + P.voff, vy + P.voff, P, SlabView{slabs + P.loff, P.ns}, r);
             }
             pairs_push<WRITE, kPolyPairs>(buf, cnt, hit, p, pid, &bsh, sink);
         }
     }
     pairs_end<WRITE>(buf, cnt, &bsh, sink);
+}
+
+// ============================================================ point-polygon kNN ===========
+// PointPolygonKNNQuery window body (PointPolygonKNNQuery.java:162-236): candidates = points of
+// the polygon's G u C cells; key = (distance bits, window index), distance = JTS
+// point.distance(polygon) (DistanceFunctions.java:33-36) or the bbox distance when approximate
+// (DistanceFunctions.java:150-200); result = the k smallest keys, ascending (the deterministic
+// form of the per-cell heaps + windowAll merge, KNNQuery.java:204-272).
+//   ppknn_scan    one pass over x/y: cell (HelperClass.java:104-116) vs the G/C rects; candidate
+//                 window indices compacted per wave (one atomic per wave)
+//   ppknn_dist    full waves over the compact list: ring in LDS, exact distance, key
+//   rsel_hist/_pick  radix select of the k-th smallest 96-bit key (dist bits | idx), 12-bit
+//                 digits, 9 rounds; device-resident state, no host round trip
+//   rsel_gather   keys <= the k-th key (exactly min(k, M) of them)
+//   rsel_sort     one block: bitonic sort of <= 256 keys, emit idx / dist / count
+constexpr int kRselBins = 4096;
+constexpr int kRselRounds = 9;
+struct RselState {
+    unsigned long long pd, md;  // decided distance bits and their mask
+    unsigned pi, mi;            // decided index bits and their mask
+    unsigned kk;                // rank still to find among the matching keys (1-based)
+    unsigned nsel;              // gather cursor
+    unsigned ncand;             // candidates (scan counter)
+    unsigned pad;
+    unsigned hist[kRselBins];
+};
+// digit (field, shift, width) of round t: distance bits 63..0, then index bits 31..0
+__host__ __device__ __forceinline__ void rsel_round(int t, int& field, int& shift, int& width) {
+    const int sh[kRselRounds] = {52, 40, 28, 16, 4, 0, 20, 8, 0};
+    const int wd[kRselRounds] = {12, 12, 12, 12, 12, 4, 12, 12, 8};
+    field = t < 6 ? 0 : 1;
+    shift = sh[t];
+    width = wd[t];
+}
+
+// Distance.pointToSegment (JTS), fp64 in Java source order
+__device__ __forceinline__ double point_segment(double px, double py, double ax, double ay, double bx, double by) {
+    if (ax == bx && ay == by) return coord_distance(px, py, ax, ay);
+    const double len2 = (bx - ax) * (bx - ax) + (by - ay) * (by - ay);
+    const double rr = ((px - ax) * (bx - ax) + (py - ay) * (by - ay)) / len2;
+    if (rr <= 0.0) return coord_distance(px, py, ax, ay);
+    if (rr >= 1.0) return coord_distance(px, py, bx, by);
+    const double s = ((ay - py) * (bx - ax) - (ax - px) * (by - ay)) / len2;
+    return __builtin_fabs(s) * __builtin_sqrt(len2);
+}
+
+// JTS DistanceOp(point, polygon).distance(): 0 unless EXTERIOR (PointLocator: envelope test, then
+// RayCrossingCounter over the ring), else min over segments (start Double.MAX_VALUE, replaced
+// only by a strictly smaller value -- a NaN segment distance never is).
+__device__ double point_polygon_distance(double px, double py, const double* __restrict__ vx,
+                                         const double* __restrict__ vy, int nv, const double bb[4]) {
+    const bool in_env = !(px > bb[2] || px < bb[0] || py > bb[3] || py < bb[1]);
+    if (in_env) {
+        bool boundary = false;
+        int crossings = 0;
+        for (int i = 1; i < nv; i++) count_segment(px, py, vx[i], vy[i], vx[i - 1], vy[i - 1], boundary, crossings);
+        if (boundary || (crossings & 1)) return 0.0;
+    }
+    double md = 1.7976931348623157e308;
+    for (int i = 0; i < nv - 1; i++) {
+        const double d = point_segment(px, py, vx[i], vy[i], vx[i + 1], vy[i + 1]);
+        md = d < md ? d : md;
+    }
+    return md;
+}
+
+struct PpknnPoly {
+    double bb[4];
+    uint32_t nv, nrect;  // closed ring length; G rects then C rects (cell space)
+};
+
+__global__ __launch_bounds__(1024) void rsel_init(RselState* __restrict__ st, unsigned k) {
+    for (int t = threadIdx.x; t < kRselBins; t += 1024) st->hist[t] = 0;
+    if (threadIdx.x == 0) {
+        st->pd = 0; st->md = 0; st->pi = 0; st->mi = 0;
+        st->kk = k; st->nsel = 0; st->ncand = 0; st->pad = 0;
+    }
+}
+
+__global__ __launch_bounds__(kTB) void ppknn_scan(const double* __restrict__ x, const double* __restrict__ y,
+                                                  uint64_t n, double mnx, double mny, double l,
+                                                  const int32_t* __restrict__ rects, uint32_t nrect,
+                                                  unsigned* __restrict__ cand, RselState* __restrict__ st) {
+    __shared__ int32_t lr[4 * 64];
+    const uint32_t nr = nrect < 64 ? nrect : 64;
+    for (uint32_t t = threadIdx.x; t < 4 * nr; t += kTB) lr[t] = rects[t];
+    __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * kTB;
+    for (uint64_t b = (uint64_t)blockIdx.x * kTB; b < n; b += stride) {
+        const uint64_t i = b + threadIdx.x;
+        bool c = false;
+        if (i < n) {
+            const int32_t cx = d_axis_cell(x[i], mnx, l), cy = d_axis_cell(y[i], mny, l);
+            c = in_rects(lr, nr, cx, cy) || (nrect > nr && in_rects(rects + 4 * nr, nrect - nr, cx, cy));
+        }
+        const unsigned long long m = __ballot(c);
+        if (m == 0) continue;
+        unsigned base = 0;
+        if (lane_id() == 0) base = atomicAdd(&st->ncand, (unsigned)__popcll(m));
+        base = __shfl(base, 0);
+        if (c) cand[base + lanes_below(m)] = (unsigned)i;
+    }
+}
+
+template <bool APPROX>
+__global__ __launch_bounds__(kTB) void ppknn_dist(const double* __restrict__ x, const double* __restrict__ y,
+                                                  const unsigned* __restrict__ cand, const RselState* __restrict__ st,
+                                                  const double* __restrict__ vx, const double* __restrict__ vy,
+                                                  PpknnPoly P, unsigned long long* __restrict__ key) {
+    __shared__ double lvx[kMaxLdsVerts];
+    __shared__ double lvy[kMaxLdsVerts];
+    const bool v_lds = P.nv <= (uint32_t)kMaxLdsVerts;
+    if (!APPROX && v_lds)
+        for (uint32_t t = threadIdx.x; t < P.nv; t += kTB) {
+            lvx[t] = vx[t];
+            lvy[t] = vy[t];
+        }
+    __syncthreads();
+    const double* rvx = v_lds ? lvx : vx;
+    const double* rvy = v_lds ? lvy : vy;
+    const unsigned m = st->ncand;
+    for (unsigned t = blockIdx.x * kTB + threadIdx.x; t < m; t += gridDim.x * kTB) {
+        const unsigned i = cand[t];
+        const double px = x[i], py = y[i];
+        const double d = APPROX ? bbox_distance(px, py, P.bb) : point_polygon_distance(px, py, rvx, rvy, (int)P.nv, P.bb);
+        unsigned long long bits = (unsigned long long)__double_as_longlong(d);
+        if (d != d) bits = 0x7ff8000000000000ull;
+        key[t] = bits;
+    }
+}
+
+__device__ __forceinline__ bool rsel_match(const RselState& s, unsigned long long d, unsigned i) {
+    return (d & s.md) == s.pd && (i & s.mi) == s.pi;
+}
+
+__global__ __launch_bounds__(kTB) void rsel_hist(const unsigned long long* __restrict__ key,
+                                                 const unsigned* __restrict__ cand, RselState* __restrict__ st,
+                                                 int round, unsigned k) {
+    __shared__ unsigned h[kRselBins];
+    const unsigned m = st->ncand;
+    if (m <= k) return;  // every candidate is selected
+    for (int t = threadIdx.x; t < kRselBins; t += kTB) h[t] = 0;
+    __syncthreads();
+    int field, shift, width;
+    rsel_round(round, field, shift, width);
+    const unsigned long long md = st->md, pd = st->pd;
+    const unsigned mi = st->mi, pi = st->pi;
+    const unsigned dm = (1u << width) - 1u;
+    for (unsigned t = blockIdx.x * kTB + threadIdx.x; t < m; t += gridDim.x * kTB) {
+        const unsigned long long d = key[t];
+        const unsigned i = cand[t];
+        if ((d & md) != pd || (i & mi) != pi) continue;
+        const unsigned dg = field == 0 ? (unsigned)(d >> shift) & dm : (i >> shift) & dm;
+        atomicAdd(&h[dg], 1u);
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < kRselBins; t += kTB)
+        if (h[t]) atomicAdd(&st->hist[t], h[t]);
+}
+
+__global__ __launch_bounds__(1024) void rsel_pick(RselState* __restrict__ st, int round, unsigned k) {
+    __shared__ unsigned part[1024];
+    const unsigned m = st->ncand;
+    if (m <= k) {  // select all: the k-th key is the maximum
+        if (threadIdx.x == 0) {
+            st->md = 0; st->pd = 0; st->mi = 0; st->pi = 0;
+        }
+        return;
+    }
+    int field, shift, width;
+    rsel_round(round, field, shift, width);
+    // 4 bins per thread, inclusive scan of the per-thread sums
+    unsigned v[4], sum = 0;
+    for (int j = 0; j < 4; j++) {
+        v[j] = st->hist[4 * threadIdx.x + j];
+        sum += v[j];
+    }
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const unsigned a = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += a;
+        __syncthreads();
+    }
+    const unsigned kk = st->kk;
+    const unsigned incl = part[threadIdx.x], excl = incl - sum;
+    __syncthreads();  // every thread has read kk before it changes
+    if (excl < kk && incl >= kk) {  // exactly one thread holds the k-th
+        unsigned c = excl;
+        int j = 0;
+        while (c + v[j] < kk) c += v[j++];
+        const unsigned dg = 4 * threadIdx.x + j;
+        st->kk = kk - c;
+        const unsigned dm = (1u << width) - 1u;
+        if (field == 0) {
+            st->pd |= (unsigned long long)dg << shift;
+            st->md |= (unsigned long long)dm << shift;
+        } else {
+            st->pi |= dg << shift;
+            st->mi |= dm << shift;
+        }
+    }
+    for (int j = 0; j < 4; j++) st->hist[4 * threadIdx.x + j] = 0;
+}
+
+__global__ __launch_bounds__(kTB) void rsel_gather(const unsigned long long* __restrict__ key,
+                                                   const unsigned* __restrict__ cand, RselState* __restrict__ st,
+                                                   unsigned k, unsigned long long* __restrict__ sel_d,
+                                                   unsigned* __restrict__ sel_i) {
+    const unsigned m = st->ncand;
+    const bool all = m <= k;
+    const unsigned long long kd = st->pd;
+    const unsigned ki = st->pi;
+    for (unsigned t = blockIdx.x * kTB + threadIdx.x; t < m; t += gridDim.x * kTB) {
+        const unsigned long long d = key[t];
+        const unsigned i = cand[t];
+        if (all || d < kd || (d == kd && i <= ki)) {
+            const unsigned s = atomicAdd(&st->nsel, 1u);
+            if (s < k) {
+                sel_d[s] = d;
+                sel_i[s] = i;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void rsel_sort(const unsigned long long* __restrict__ sel_d,
+                                                 const unsigned* __restrict__ sel_i, const RselState* __restrict__ st,
+                                                 unsigned k, double* __restrict__ out_d, unsigned* __restrict__ out_i,
+                                                 unsigned* __restrict__ out_count) {
+    __shared__ unsigned long long d[256];
+    __shared__ unsigned id[256];
+    const unsigned m = st->nsel < k ? st->nsel : k;
+    const unsigned t = threadIdx.x;
+    d[t] = t < m ? sel_d[t] : ~0ull;
+    id[t] = t < m ? sel_i[t] : ~0u;
+    __syncthreads();
+    for (unsigned size = 2; size <= 256; size <<= 1) {
+        for (unsigned j = size >> 1; j > 0; j >>= 1) {
+            const unsigned p = t ^ j;
+            if (p > t) {
+                const bool up = (t & size) == 0;
+                const bool gt = d[t] > d[p] || (d[t] == d[p] && id[t] > id[p]);
+                if (gt == up) {
+                    const unsigned long long td = d[t]; d[t] = d[p]; d[p] = td;
+                    const unsigned ti = id[t]; id[t] = id[p]; id[p] = ti;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (t < m) {
+        out_d[t] = __longlong_as_double((long long)d[t]);
+        out_i[t] = id[t];
+    }
+    if (t == 0) out_count[0] = m;
 }
 
 // ================================================================== host side =============
@@ -1511,7 +1778,8 @@ void plan_slabs(PolyDev& P, const double* ry, double r, double cell_len, std::ve
 // slab lists: ~2 ms for 1000 polygons) and the device upload are done once; later calls compare
 // their inputs bitwise with the cached copies (the inputs decide everything the plan holds).
 struct PolyCache {
-    geohip_grid grid{};
+    geohip_grid grid{}, gq{};
+    int jmode = 0;
     double r = 0.0;
     std::vector<uint32_t> ring_off;
     std::vector<double> vx, vy;
@@ -1543,19 +1811,24 @@ void ppoly_cache_drop(geohip_ctx* ctx) {
     g_pcache.erase(ctx);
 }
 
-int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
-               const uint32_t* ring_off, const double* vx, const double* vy, uint32_t npoly, double r, int approximate,
-               uint32_t* out_pairs, uint64_t cap, uint64_t* out_count) {
+int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, int join, const double* x,
+               const double* y, uint64_t n, const uint32_t* ring_off, const double* vx, const double* vy, uint32_t npoly,
+               double r, int approximate, uint32_t* out_pairs, uint64_t cap, uint64_t* out_count) {
     if (!out_count) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null out_count");
     *out_count = 0;
-    int rc = check_grid_basic(ctx, grid, "grid");
+    int rc = check_grid_basic(ctx, grid, join ? "point grid" : "grid");
+    if (!rc && join) rc = check_grid_basic(ctx, gq, "query grid");
     if (rc) return rc;
+    if (!join) gq = grid;
+    // join (PointPolygonJoinQuery.java:162-201): every point of G u C is distance-checked
+    // (exact) or emitted (approximate); the range query's guaranteed shortcut does not apply
+    const int jmode = join ? (approximate ? 2 : 1) : 0;
     if (n >= 0xffffffffull) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "window larger than 2^32-1 points");
     if (npoly && (!ring_off || !vx || !vy)) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null polygon arrays");
     if (cap && !out_pairs) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null out_pairs");
     hipStream_t st = ctx_stream(ctx);
     const bool dev = ctx_mem(ctx) == GEOHIP_MEM_DEVICE;
-    const int32_t nb = grid->n;
+    const int32_t nb = gq->n;  // key space: the polygons' (query) grid; point cells on `grid`
     const TileGeom geo = tile_geom(*grid, nb);
     static const bool prof = getenv("GEOHIP_HOST_PROFILE") != nullptr;  // measurement only
     auto now = [] { return std::chrono::steady_clock::now(); };
@@ -1568,7 +1841,8 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const 
         std::lock_guard<std::mutex> lk(g_pcache_mu);
         pc = &g_pcache[ctx];
     }
-    bool cached = same_inputs(*pc, *grid, r, ring_off, npoly, vx, vy);
+    bool cached = same_inputs(*pc, *grid, r, ring_off, npoly, vx, vy) && pc->jmode == jmode &&
+                  memcmp(&pc->gq, gq, sizeof *gq) == 0;
     if (!cached) {
         for (uint32_t p = 0; p < npoly; p++)
             if (ring_off[p + 1] < ring_off[p]) return ctx_fail(ctx, GEOHIP_ERR_ARG, "ring_off not ascending");
@@ -1586,7 +1860,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const 
             std::string err;
             const uint32_t b = ring_off[p], e = ring_off[p + 1];
             if (e < b) return ctx_fail(ctx, GEOHIP_ERR_ARG, "ring_off not ascending");
-            rc = plan_polygon(*grid, vx + b, vy + b, e - b, r, &pl, &err);
+            rc = plan_polygon(*gq, vx + b, vy + b, e - b, r, &pl, &err);
             if (rc) return ctx_fail(ctx, rc, err);
             PolyDev& P = pd[p];
             memset(&P, 0, sizeof P);
@@ -1612,7 +1886,10 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const 
             for (auto& q : pl.c) { hrects.insert(hrects.end(), {q.x0, q.x1, q.y0, q.y1}); acc(q); }
             P.wx0 = wx0; P.wx1 = wx1; P.wy0 = wy0; P.wy1 = wy1;
             any_outside = any_outside || P.outside;
-            plan_slabs(P, pl.ry.data(), r, grid->cell_len, hslab);
+            // the C rects follow the G rects: the join sees one list, all checked or all emitted
+            if (jmode == 1) { P.coff = P.goff; P.nc += P.ng; P.ng = 0; }
+            if (jmode == 2) { P.ng += P.nc; P.nc = 0; }
+            plan_slabs(P, pl.ry.data(), r, gq->cell_len, hslab);
             if (wx0 <= wx1 && wy0 <= wy1)
                 for (int32_t a = wx0 / geo.ts; a <= wx1 / geo.ts; a++)
                     for (int32_t c = wy0 / geo.ts; c <= wy1 / geo.ts; c++)
@@ -1638,6 +1915,8 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const 
             }
         }
         fresh.grid = *grid;
+        fresh.gq = *gq;
+        fresh.jmode = jmode;
         fresh.r = r;
         fresh.ring_off.assign(ring_off, ring_off + npoly + 1);
         const size_t v0 = npoly ? ring_off[0] : 0, v1 = npoly ? ring_off[npoly] : 0;
@@ -1735,7 +2014,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const 
             out = reinterpret_cast<unsigned*>(p);
         }
     }
-    PairSink sink{bcount, boff, 0u, out, out ? cap : 0, ((uintptr_t)out & 7u) == 0};
+    PairSink sink{bcount, boff, 0u, out, out ? cap : 0, ((uintptr_t)out & 7u) == 0, join ? 1 : 0};
     PairSink osink = sink;
     osink.slot0 = nwork;
     const int r_is_max = r >= 1.7976931348623157e308;
@@ -1750,7 +2029,10 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const 
         else
             ppoly_eval<false><<<nwork, kTB, 0, st>>>(tb, dwork, dpoly, dvx, dvy, drects, dslab, r, r_is_max, wofs, mask, bcount);
     }
-    if (nob)
+    if (nob && jmode == 1)
+        ppoly_outside<false, true><<<nob, kTB, 0, st>>>(dx, dy, oidx, n_out, grid->min_x, grid->min_y, grid->cell_len,
+                                                        dpoly, npoly, drects, osink, dvx, dvy, dslab, r);
+    else if (nob)
         ppoly_outside<false><<<nob, kTB, 0, st>>>(dx, dy, oidx, n_out, grid->min_x, grid->min_y, grid->cell_len, dpoly,
                                                   npoly, drects, osink);
     scan_launch<unsigned long long>(st, bcount, nslots, reinterpret_cast<unsigned long long*>(seg),
@@ -1758,7 +2040,10 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const 
     // write pass: pairs from the masks
     if (out) {
         if (nwork) ppoly_emit<<<nwork, kTB, 0, st>>>(tb, dwork, wofs, mask, sink);
-        if (nob)
+        if (nob && jmode == 1)
+            ppoly_outside<true, true><<<nob, kTB, 0, st>>>(dx, dy, oidx, n_out, grid->min_x, grid->min_y,
+                                                           grid->cell_len, dpoly, npoly, drects, osink, dvx, dvy, dslab, r);
+        else if (nob)
             ppoly_outside<true><<<nob, kTB, 0, st>>>(dx, dy, oidx, n_out, grid->min_x, grid->min_y, grid->cell_len, dpoly,
                                                      npoly, drects, osink);
     }
@@ -1776,6 +2061,89 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const 
             return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "pair readback failed");
     }
     if (tot > cap) return ctx_fail(ctx, GEOHIP_ERR_CAPACITY, "output capacity too small; *out_count = required");
+    return GEOHIP_OK;
+}
+
+// Point-polygon kNN of one query polygon over one window (host side of the kernels above).
+int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
+                   const double* vx, const double* vy, uint32_t nv, double r, uint32_t k, int approximate,
+                   uint32_t* out_idx, double* out_dist, uint32_t* out_count) {
+    if (!out_idx || !out_dist || !out_count) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null output");
+    *out_count = 0;
+    if (k == 0 || k > GEOHIP_KNN_MAX_K) return ctx_fail(ctx, GEOHIP_ERR_ARG, "k must be in [1, 256]");
+    int rc = check_grid_basic(ctx, grid, "grid");
+    if (rc) return rc;
+    if (n >= 0xffffffffull) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "window larger than 2^32-1 points");
+    if (!vx || !vy) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null polygon arrays");
+    PolyPlan pl;
+    std::string err;
+    rc = plan_polygon(*grid, vx, vy, nv, r, &pl, &err);
+    if (rc) return ctx_fail(ctx, rc, err);
+    std::vector<int32_t> hrect;
+    for (auto& q : pl.g) hrect.insert(hrect.end(), {q.x0, q.x1, q.y0, q.y1});
+    for (auto& q : pl.c) hrect.insert(hrect.end(), {q.x0, q.x1, q.y0, q.y1});
+    const uint32_t nrect = (uint32_t)(hrect.size() / 4);
+    PpknnPoly P;
+    for (int i = 0; i < 4; i++) P.bb[i] = pl.bbox[i];
+    P.nv = (uint32_t)pl.rx.size();
+    P.nrect = nrect;
+    hipStream_t st = ctx_stream(ctx);
+    const bool dev = ctx_mem(ctx) == GEOHIP_MEM_DEVICE;
+    const double *dx, *dy;
+    rc = ctx_stage_xy(ctx, x, y, n, 0, &dx, &dy);
+    if (rc) return rc;
+    Scratch S{ctx};
+    const uint64_t ncap = n ? n : 1;
+    char* cbuf = S.get<char>(22, ncap * 12 + 64);
+    const size_t off_sel_d = (sizeof(RselState) + 15) & ~(size_t)15;
+    const size_t off_sel_i = off_sel_d + 256 * 8;
+    const size_t off_out = off_sel_i + 256 * 4;
+    const size_t off_vx = (off_out + 256 * 12 + 16 + 15) & ~(size_t)15;
+    const size_t off_rect = off_vx + 2 * 8 * (size_t)P.nv;
+    char* sbuf = S.get<char>(23, off_rect + 16 * (size_t)nrect + 64);
+    if (S.rc) return S.rc;
+    unsigned long long* key = reinterpret_cast<unsigned long long*>(cbuf);
+    unsigned* cand = reinterpret_cast<unsigned*>(cbuf + ncap * 8);
+    RselState* rs = reinterpret_cast<RselState*>(sbuf);
+    unsigned long long* sel_d = reinterpret_cast<unsigned long long*>(sbuf + off_sel_d);
+    unsigned* sel_i = reinterpret_cast<unsigned*>(sbuf + off_sel_i);
+    double* od = dev ? out_dist : reinterpret_cast<double*>(sbuf + off_out);
+    unsigned* oi = dev ? out_idx : reinterpret_cast<unsigned*>(sbuf + off_out + 256 * 8);
+    unsigned* ocnt = reinterpret_cast<unsigned*>(sbuf + off_out + 256 * 12);
+    double* dvx = reinterpret_cast<double*>(sbuf + off_vx);
+    double* dvy = dvx + P.nv;
+    int32_t* drect = reinterpret_cast<int32_t*>(sbuf + off_rect);
+    if ((P.nv && (hipMemcpyAsync(dvx, pl.rx.data(), 8 * (size_t)P.nv, hipMemcpyHostToDevice, st) != hipSuccess ||
+                  hipMemcpyAsync(dvy, pl.ry.data(), 8 * (size_t)P.nv, hipMemcpyHostToDevice, st) != hipSuccess)) ||
+        (nrect && hipMemcpyAsync(drect, hrect.data(), 16 * (size_t)nrect, hipMemcpyHostToDevice, st) != hipSuccess))
+        return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "polygon upload failed");
+    hipEvent_t e0, e1;
+    ctx_timing_events(ctx, &e0, &e1);
+    if (e0) hipEventRecord(e0, st);
+    rsel_init<<<1, 1024, 0, st>>>(rs, k);
+    if (n && nrect) {
+        const uint64_t nb = std::min<uint64_t>((n + kTB - 1) / kTB, 4096);
+        ppknn_scan<<<(unsigned)nb, kTB, 0, st>>>(dx, dy, n, grid->min_x, grid->min_y, grid->cell_len, drect, nrect, cand, rs);
+        if (approximate) ppknn_dist<true><<<1024, kTB, 0, st>>>(dx, dy, cand, rs, dvx, dvy, P, key);
+        else ppknn_dist<false><<<1024, kTB, 0, st>>>(dx, dy, cand, rs, dvx, dvy, P, key);
+        for (int t = 0; t < kRselRounds; t++) {
+            rsel_hist<<<512, kTB, 0, st>>>(key, cand, rs, t, k);
+            rsel_pick<<<1, 1024, 0, st>>>(rs, t, k);
+        }
+        rsel_gather<<<512, kTB, 0, st>>>(key, cand, rs, k, sel_d, sel_i);
+    }
+    rsel_sort<<<1, 256, 0, st>>>(sel_d, sel_i, rs, k, od, oi, ocnt);
+    if (e1) hipEventRecord(e1, st);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, std::string("knn_ppoly launch: ") + hipGetErrorString(e));
+    uint32_t m = 0;
+    if (hipMemcpyAsync(&m, ocnt, 4, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+        return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "count readback failed");
+    if (!dev && m &&
+        (hipMemcpy(out_dist, od, 8 * (size_t)m, hipMemcpyDeviceToHost) != hipSuccess ||
+         hipMemcpy(out_idx, oi, 4 * (size_t)m, hipMemcpyDeviceToHost) != hipSuccess))
+        return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "kNN readback failed");
+    *out_count = m;
     return GEOHIP_OK;
 }
 

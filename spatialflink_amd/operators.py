@@ -224,3 +224,46 @@ class PointPolygonRangeQuery(_Operator):
         return self._ctx().range_ppoly(self.index.abi(), window.x, window.y, np.array(off, np.uint32),
                                        np.array(vx), np.array(vy), float(query_radius),
                                        self.conf.approximate_query)
+
+
+def _rings(polys):
+    off, vx, vy = [0], [], []
+    for p in polys:
+        for c in p.coordinates:
+            vx.append(float(c[0]))
+            vy.append(float(c[1]))
+        off.append(len(vx))
+    return np.array(off, np.uint32), np.array(vx), np.array(vy)
+
+
+class PointPolygonJoinQuery(_Operator):
+    """PointPolygonJoinQuery.run (PointPolygonJoinQuery.java:27-201): the polygon stream is
+    replicated to each polygon's guaranteed and candidate cells on the query grid
+    (JoinQuery.getReplicatedPolygonQueryStream, JoinQuery.java:93-115) and joined with the
+    points' gridIDs; returns (point index, polygon index) pairs with JTS distance <= r (every
+    such pair when approximate)."""
+
+    def __init__(self, conf: QueryConfiguration, index1: UniformGrid, index2: UniformGrid,
+                 ctx: Optional[_abi.Context] = None):
+        super().__init__(conf, index1, ctx)
+        self.index2 = index2
+
+    def run(self, points: PointWindow, query_polygons, query_radius: float):
+        self._check_type()
+        polys = [query_polygons] if isinstance(query_polygons, Polygon) else list(query_polygons)
+        off, vx, vy = _rings(polys)
+        return self._ctx().join_ppoly(self.index.abi(), self.index2.abi(), points.x, points.y, off, vx, vy,
+                                      float(query_radius), self.conf.approximate_query)
+
+
+class PointPolygonKNNQuery(_Operator):
+    """PointPolygonKNNQuery.run (PointPolygonKNNQuery.java:34-236): the window's k nearest
+    points to one query polygon among its guaranteed u candidate cells, ascending
+    (distance, index); distance = JTS point.distance(polygon) or, when approximate, the
+    bounding-box distance (DistanceFunctions.java:150-200)."""
+
+    def run(self, window: PointWindow, query_polygon: Polygon, query_radius: float, k: int):
+        self._check_type()
+        _, vx, vy = _rings([query_polygon])
+        return self._ctx().knn_ppoly(self.index.abi(), window.x, window.y, vx, vy, float(query_radius), int(k),
+                                     self.conf.approximate_query)

@@ -1,0 +1,161 @@
+"""GPU parity of the point-polygon join and kNN through the C ABI.
+
+geohip_join_ppoly against the C oracle (pair sets, bit-exact membership) over one and two grids,
+radii with and without guaranteed cells, approximate mode, boundary points, NaN points and
+polygons whose guaranteed bbox cells leave the grid (out-of-grid points then need the distance
+check the join adds); geohip_knn_ppoly against the C oracle: (idx, distance bits) in
+ascending (distance, idx), including large ties at distance 0 (points inside the polygon),
+k = 1 / 256, fewer candidates than k, an empty window, approximate bbox distances, and the
+argument errors where the reference throws.
+"""
+import math
+
+import numpy as np
+import pytest
+
+import cref
+from helpers import pairs_sorted
+from spatialflink_amd import _abi, synth
+
+pytestmark = pytest.mark.gpu
+
+BJ = synth.BEIJING
+
+
+def agrid(n):
+    l = (BJ[1] - BJ[0]) / n
+    return _abi.make_grid(BJ[0], BJ[2], l, n), cref.grid(BJ[0], BJ[2], l, n)
+
+
+def with_edges(x, y, off, vx, vy):
+    """Append every vertex, edge midpoints and a NaN point to the window."""
+    mx = (vx[:-1] + vx[1:]) / 2
+    my = (vy[:-1] + vy[1:]) / 2
+    return (np.concatenate([x, vx, mx, [math.nan, 116.0]]), np.concatenate([y, vy, my, [40.0, math.nan]]))
+
+
+JOIN_CASES = [(500, 500, 0.005, False, 60), (500, 500, 0.03, False, 20), (500, 500, 0.03, True, 20),
+              (100, 100, 0.05, False, 10), (200, 500, 0.02, False, 15), (500, 200, 0.04, False, 15),
+              (100, 100, 0.0, False, 10)]
+
+
+@pytest.mark.parametrize("case", range(len(JOIN_CASES)))
+def test_join_ppoly_random(ctx, case):
+    nu, nq, r, approx, npoly = JOIN_CASES[case]
+    x, y = synth.uniform(300000, 70 + case)
+    off, vx, vy = synth.star_polygons(npoly, 80 + case)
+    x, y = with_edges(x, y, off, vx, vy)
+    au, cu = agrid(nu)
+    aq, cq = agrid(nq)
+    got = ctx.join_ppoly(au, aq, x, y, off, vx, vy, r, approx)
+    want = cref.join_ppoly(cu, cq, x, y, off, vx, vy, r, approx)
+    assert pairs_sorted(got).tolist() == pairs_sorted(want).tolist()
+
+
+def test_join_ppoly_outside_grid_and_sliver(ctx):
+    """Lg == 0: guaranteed bbox cells outside the grid match out-of-grid points, which the join
+    then distance-checks; a diagonal sliver whose bbox corners are far from the polygon."""
+    l = (BJ[1] - BJ[0]) / 100
+    r = l * math.sqrt(2) * 1.2  # Lg == 0
+    rings = [[(115.48, 39.58), (115.56, 39.58), (115.56, 39.66), (115.48, 39.66)],
+             [(116.0, 40.0), (116.3, 40.3), (116.3, 40.301), (116.0, 40.001)]]
+    vx = np.array([c[0] for ring in rings for c in ring])
+    vy = np.array([c[1] for ring in rings for c in ring])
+    off = np.array([0, 4, 8], np.uint32)
+    rng = np.random.default_rng(3)
+    x = np.concatenate([rng.uniform(115.3, 115.8, 20000), rng.uniform(115.9, 116.4, 20000)])
+    y = np.concatenate([rng.uniform(39.4, 39.8, 20000), rng.uniform(39.9, 40.4, 20000)])
+    x, y = with_edges(x, y, off, vx, vy)
+    au, cu = agrid(100)
+    for rr, approx in ((r, False), (r, True), (0.004, False), (0.05, False)):
+        got = ctx.join_ppoly(au, au, x, y, off, vx, vy, rr, approx)
+        want = cref.join_ppoly(cu, cu, x, y, off, vx, vy, rr, approx)
+        assert pairs_sorted(got).tolist() == pairs_sorted(want).tolist()
+        rg = {(p, q) for q, p in cref.range_ppoly(cu, x, y, off, vx, vy, rr, approx).tolist()}
+        if not approx:
+            assert {tuple(p) for p in got.tolist()} <= rg
+
+
+def test_join_ppoly_capacity_and_device_buffers(ctx):
+    import torch
+    x, y = synth.uniform(200000, 91)
+    off, vx, vy = synth.star_polygons(30, 92)
+    au, cu = agrid(500)
+    want = pairs_sorted(cref.join_ppoly(cu, cu, x, y, off, vx, vy, 0.01)).tolist()
+    assert len(want) > 10
+    with pytest.raises(_abi.GeohipCapacityError):
+        ctx.join_ppoly(au, au, x, y, off, vx, vy, 0.01, cap=5)
+    tx, ty = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+    got = ctx.join_ppoly(au, au, tx, ty, off, vx, vy, 0.01)
+    assert pairs_sorted(got.cpu().numpy()).tolist() == want
+
+
+KNN_CASES = [(500, 0.005, 50, False), (500, 0.005, 50, True), (100, 0.05, 10, False), (500, 0.02, 256, False),
+             (200, 0.03, 1, False), (1000, 0.0, 20, False), (100, 0.5, 100, False)]
+
+
+@pytest.mark.parametrize("case", range(len(KNN_CASES)))
+def test_knn_ppoly_random(ctx, case):
+    gn, r, k, approx = KNN_CASES[case]
+    x, y = synth.uniform(400000, 110 + case)
+    off, vx, vy = synth.star_polygons(3, 120 + case)
+    ag, cg = agrid(gn)
+    for p in range(3):
+        px, py = vx[off[p]:off[p + 1]], vy[off[p]:off[p + 1]]
+        wx, wy = with_edges(x, y, np.array([0, len(px)]), px, py)
+        gi, gd = ctx.knn_ppoly(ag, wx, wy, px, py, r, k, approx)
+        wi, wd = cref.knn_ppoly(cg, wx, wy, px, py, r, k, approx)
+        assert gi.tolist() == wi.tolist()
+        assert np.array_equal(gd.view(np.uint64), wd.view(np.uint64))
+
+
+def test_knn_ppoly_ties_small_and_empty(ctx):
+    ag, cg = agrid(500)
+    ring_x = np.array([116.30, 116.40, 116.40, 116.30])
+    ring_y = np.array([40.10, 40.10, 40.20, 40.20])
+    rng = np.random.default_rng(5)
+    # 5000 points inside (distance 0: the k smallest are the k smallest indices), some outside
+    x = np.concatenate([rng.uniform(116.29, 116.41, 3000), rng.uniform(116.31, 116.39, 5000)])
+    y = np.concatenate([rng.uniform(40.09, 40.21, 3000), rng.uniform(40.11, 40.19, 5000)])
+    perm = rng.permutation(len(x))
+    x, y = x[perm], y[perm]
+    for k in (1, 64, 256):
+        gi, gd = ctx.knn_ppoly(ag, x, y, ring_x, ring_y, 0.005, k)
+        wi, wd = cref.knn_ppoly(cg, x, y, ring_x, ring_y, 0.005, k)
+        assert gi.tolist() == wi.tolist() and np.array_equal(gd.view(np.uint64), wd.view(np.uint64))
+        assert (gd == 0).all()
+    # fewer candidates than k
+    gi, gd = ctx.knn_ppoly(ag, x[:40], y[:40], ring_x, ring_y, 0.005, 100)
+    wi, wd = cref.knn_ppoly(cg, x[:40], y[:40], ring_x, ring_y, 0.005, 100)
+    assert gi.tolist() == wi.tolist() and len(gi) <= 40
+    # empty window
+    gi, gd = ctx.knn_ppoly(ag, np.zeros(0), np.zeros(0), ring_x, ring_y, 0.005, 10)
+    assert len(gi) == 0
+
+
+def test_knn_ppoly_errors(ctx):
+    ag, _ = agrid(500)
+    x, y = synth.uniform(1000, 1)
+    sq_x, sq_y = np.array([116.3, 116.4, 116.4, 116.3]), np.array([40.1, 40.1, 40.2, 40.2])
+    for k in (0, 257):
+        with pytest.raises(_abi.GeohipArgumentError):
+            ctx.knn_ppoly(ag, x, y, sq_x, sq_y, 0.01, k)
+    with pytest.raises(_abi.GeohipArgumentError):
+        ctx.knn_ppoly(ag, x, y, sq_x[:3], sq_y[:3], 0.01, 5)  # <= 3 coordinates (Polygon.java:53)
+
+
+def test_knn_ppoly_c4_size(ctx):
+    """C4 window size (50M uniform points, 500x500) against the C oracle for one polygon."""
+    import torch
+    n = 50_000_000
+    x = torch.empty(n, dtype=torch.float64, device="cuda")
+    y = torch.empty(n, dtype=torch.float64, device="cuda")
+    ctx.synth_uniform_async(x, y, 0, 5, BJ)
+    torch.cuda.synchronize()
+    off, vx, vy = synth.star_polygons(1, 6)
+    ag, cg = agrid(500)
+    gi, gd = ctx.knn_ppoly(ag, x, y, vx, vy, 0.005, 100)
+    hx, hy = synth.uniform(n, 5)
+    wi, wd = cref.knn_ppoly(cg, hx, hy, vx, vy, 0.005, 100)
+    assert gi.cpu().numpy().tolist() == wi.tolist()
+    assert np.array_equal(gd.cpu().numpy().view(np.uint64), wd.view(np.uint64))
