@@ -13,6 +13,8 @@ The other configs are measured with ``--workload`` (same JSON contract, one line
   ppoly  C4: 1k polygons (50 vertices) over 50M uniform points per GPU, 500x500, r = 0.005
   c5     C5 per shard: 25M uniform points per GPU, 1000x1000, kNN k = 100 + range r = 0.05
   ingest SURVEY.md 8(f) row 1: 10M CSV records -> SoA x/y + ts + cell (device-resident text)
+  ppjoin SURVEY.md 8(f) row 2: the C4 shape as a point-polygon join (1k polygons x 50M points)
+  ppknn  SURVEY.md 8(f) row 2: point-polygon kNN k = 50 of one polygon over 50M points
 
 Windows are device-resident before the timed region (synthetic: uniform windows are made on
 the device by the counter-based generator of spatialflink_amd.synth; Gaussian windows on the
@@ -21,7 +23,7 @@ is cycled so no step reads a window the Infinity Cache still holds.
 
 Prints ONE JSON line (rank 0) with roofline and cpu_baseline objects.
 
-    python bench.py --gpus 1 --steps 50 --warmup 5 [--workload knn|range|join|ppoly|c5|ingest]
+    python bench.py --gpus 1 --steps 50 --warmup 5 [--workload knn|range|join|ppoly|c5|ingest|ppjoin|ppknn]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -48,7 +50,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--workload", choices=("knn", "range", "join", "ppoly", "c5", "ingest"), default="knn")
+    p.add_argument("--workload", choices=("knn", "range", "join", "ppoly", "c5", "ingest", "ppjoin", "ppknn"), default="knn")
     p.add_argument("--points", type=int, default=None, help="points per window per GPU (default: the config's)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -392,6 +394,116 @@ class PpolyWorkload(Workload):
                           f"thread, {t:.1f} s; value = point-polygon evaluations/s / {self.npoly} polygons"}
 
 
+class PpJoinWorkload(PpolyWorkload):
+    """the C4 shape as a point-polygon join (PointPolygonJoinQuery,
+    polygon stream replicated to its G/C cells, every candidate distance-checked)."""
+    tag = "ppjoin"
+    kernel = "geohip::ppoly_eval + ppoly_emit in join mode (tile binning before the timed region)"
+
+    def __init__(self, *a):
+        Workload.__init__(self, *a)
+        import torch
+        from spatialflink_amd import _abi, synth
+        self.n = self.args.points or self.n_default
+        bj = synth.BEIJING
+        self.grid = _abi.make_grid(bj[0], bj[2], (bj[1] - bj[0]) / self.grid_n, self.grid_n)
+        self.xs, self.ys = _uniform_windows(self.ctx, self.dev, self.n, self.rank,
+                                            [5 + 7919 * w for w in range(self.windows)], bj)
+        self.off, self.vx, self.vy = synth.star_polygons(self.npoly, 6)
+        torch.cuda.synchronize(self.dev)
+        self.hits = [len(self.ctx.join_ppoly(self.grid, self.grid, self.xs[w], self.ys[w], self.off, self.vx, self.vy,
+                                             self.radius)) for w in range(self.windows)]
+        self.out = torch.empty((max(self.hits) + 1, 2), dtype=torch.int32, device=self.dev)
+
+    def step(self, s):
+        w = s % self.windows
+        self.ctx.join_ppoly(self.grid, self.grid, self.xs[w], self.ys[w], self.off, self.vx, self.vy, self.radius,
+                            out=self.out)
+
+    def config(self):
+        c = super().config()
+        c["workload"] = (f"point-polygon join: {self.npoly} polygons (50 vertices) x {self.n} uniform points per window "
+                         f"per GPU, {self.grid_n}x{self.grid_n}, r={self.radius} (C4 shape, PointPolygonJoinQuery)")
+        c["pairs_per_window_per_gpu"] = c.pop("hits_per_window_per_gpu")
+        return c
+
+    def cpu_baseline(self, seconds):
+        cref = _oracle()
+        from spatialflink_amd import synth
+        bj = synth.BEIJING
+        cg = cref.grid(bj[0], bj[2], (bj[1] - bj[0]) / self.grid_n, self.grid_n)
+        n, npoly = 2_000_000, 10
+
+        def one(i):
+            x, y = synth.uniform(n, 5000 + i)
+            sl = slice(10 * i % self.npoly, 10 * i % self.npoly + npoly + 1)
+            off = self.off[sl] - self.off[sl][0]
+            vx = self.vx[self.off[sl][0]:self.off[sl][-1]]
+            vy = self.vy[self.off[sl][0]:self.off[sl][-1]]
+            t0 = time.perf_counter()
+            cref.join_ppoly(cg, cg, x, y, off, vx, vy, self.radius)
+            return time.perf_counter() - t0
+        reps, t = _timed_loop(one, seconds, 50)
+        pp_rate = reps * n * npoly / t
+        return {"value": pp_rate / self.npoly, "unit": "points/sec", "cores": 1, "kind": "port",
+                "sample": f"{reps} x ({n} uniform points x {npoly} polygons), oracle/geohip_oracle.c join_ppoly single "
+                          f"thread, {t:.1f} s; value = point-polygon evaluations/s / {self.npoly} polygons"}
+
+
+class PpKnnWorkload(Workload):
+    """point-polygon kNN (PointPolygonKNNQuery) of one star polygon,
+    k = 50, over the C4 window (50M uniform points per GPU, 500x500, r = 0.005)."""
+    tag = "ppknn"
+    kernel = "geohip ppknn_scan + ppknn_dist + radix select (9 rounds) + rsel_sort"
+    grid_n, radius, n_default, k = 500, 0.005, 50_000_000, 50
+    windows = 2
+
+    def __init__(self, *a):
+        super().__init__(*a)
+        from spatialflink_amd import _abi, synth
+        self.n = self.args.points or self.n_default
+        bj = synth.BEIJING
+        self.grid = _abi.make_grid(bj[0], bj[2], (bj[1] - bj[0]) / self.grid_n, self.grid_n)
+        self.xs, self.ys = _uniform_windows(self.ctx, self.dev, self.n, self.rank,
+                                            [5 + 7919 * w for w in range(self.windows)], bj)
+        off, vx, vy = synth.star_polygons(1, 6)
+        self.vx, self.vy = vx, vy
+
+    def units_per_step(self):
+        return self.n
+
+    def step(self, s):
+        w = s % self.windows
+        self.ctx.knn_ppoly(self.grid, self.xs[w], self.ys[w], self.vx, self.vy, self.radius, self.k)
+
+    def algorithmic_bytes(self):
+        return BYTES_PER_POINT * self.n
+
+    def config(self):
+        return {"workload": f"point-polygon kNN k={self.k}: one 50-vertex star polygon over {self.n} uniform points per "
+                            f"window per GPU, {self.grid_n}x{self.grid_n}, r={self.radius} (C4 window, "
+                            f"PointPolygonKNNQuery)",
+                "points_per_window_per_gpu": self.n, "grid": self.grid_n, "k": self.k, "radius": self.radius,
+                "windows_resident": self.windows, "parallelism": f"shard{self.world}"}
+
+    def cpu_baseline(self, seconds):
+        cref = _oracle()
+        from spatialflink_amd import synth
+        bj = synth.BEIJING
+        cg = cref.grid(bj[0], bj[2], (bj[1] - bj[0]) / self.grid_n, self.grid_n)
+        n = 5_000_000
+
+        def one(i):
+            x, y = synth.uniform(n, 6000 + i)
+            t0 = time.perf_counter()
+            cref.knn_ppoly(cg, x, y, self.vx, self.vy, self.radius, self.k)
+            return time.perf_counter() - t0
+        reps, t = _timed_loop(one, seconds, 20)
+        return {"value": reps * n / t, "unit": "points/sec", "cores": 1, "kind": "port",
+                "sample": f"{reps} windows x {n} uniform points (same polygon, k, grid, r), oracle/geohip_oracle.c "
+                          f"knn_ppoly single thread, {t:.1f} s"}
+
+
 class C5Workload(KnnWorkload):
     """C5 per shard (BASELINE.json configs[4]): 1000x1000 grid, 25M uniform points per GPU
     (200M per window on 8 GPUs), kNN k=100 + range r=0.05 of the README query."""
@@ -491,7 +603,7 @@ class IngestWorkload(Workload):
 
 
 WORKLOADS = {"knn": KnnWorkload, "range": RangeWorkload, "join": JoinWorkload, "ppoly": PpolyWorkload,
-             "c5": C5Workload, "ingest": IngestWorkload}
+             "c5": C5Workload, "ingest": IngestWorkload, "ppjoin": PpJoinWorkload, "ppknn": PpKnnWorkload}
 
 
 def main():

@@ -21,7 +21,9 @@ TAGS = {"knn": ("knn_scan", ("knn_scan", "knn_final"), 1),
                                  "scan_apply<unsigned long long>"), 1),
         "ppoly": ("ppoly_probe", ("ppoly_eval", "ppoly_emit", "ppoly_outside"), 1),
         "c5": ("knn_scan_c5", ("knn_scan", "knn_final", "range_fused", "range_scan", "scan_units", "range_emit"), 2),
-        "ingest": ("ingest", ("ingest_count", "ingest_scan", "ingest_parse"), 1)}
+        "ingest": ("ingest", ("ingest_count", "ingest_scan", "ingest_parse"), 1),
+        "ppjoin": ("ppjoin", ("ppoly_eval", "ppoly_emit", "ppoly_outside"), 1),
+        "ppknn": ("ppknn", ("rsel_", "ppknn_"), 1)}
 
 
 def per_kernel(path):

@@ -1134,7 +1134,7 @@ struct RselState {
     unsigned kk;                // rank still to find among the matching keys (1-based)
     unsigned nsel;              // gather cursor
     unsigned ncand;             // candidates (scan counter)
-    unsigned pad;
+    unsigned small_max;         // rsel_small handles ncand <= small_max
     unsigned hist[kRselBins];
 };
 // digit (field, shift, width) of round t: distance bits 63..0, then index bits 31..0
@@ -1182,11 +1182,11 @@ struct PpknnPoly {
     uint32_t nv, nrect;  // closed ring length; G rects then C rects (cell space)
 };
 
-__global__ __launch_bounds__(1024) void rsel_init(RselState* __restrict__ st, unsigned k) {
+__global__ __launch_bounds__(1024) void rsel_init(RselState* __restrict__ st, unsigned k, unsigned small_max) {
     for (int t = threadIdx.x; t < kRselBins; t += 1024) st->hist[t] = 0;
     if (threadIdx.x == 0) {
         st->pd = 0; st->md = 0; st->pi = 0; st->mi = 0;
-        st->kk = k; st->nsel = 0; st->ncand = 0; st->pad = 0;
+        st->kk = k; st->nsel = 0; st->ncand = 0; st->small_max = small_max;
     }
 }
 
@@ -1215,6 +1215,111 @@ __global__ __launch_bounds__(kTB) void ppknn_scan(const double* __restrict__ x, 
     }
 }
 
+// G u C rects as exact coordinate boxes (planner: rect_to_box), classification by compares
+constexpr int kPpBoxes = 16;
+constexpr unsigned kPpBuf = 1024;  // wave-private candidate buffer (u32 window indices)
+struct PpknnBoxes {
+    Box b[kPpBoxes];
+    int32_t nb, pad;
+};
+
+// 4 points per lane per 256-point wave iteration (double2 loads of x and y, the next full
+// iteration's loads in flight while the current one is classified; the partial last iteration
+// is handled after the loop so the main loop has one load path and the compiler's vmcnt
+// accounting keeps the prefetch in flight).  NB > 0: the boxes are wave-uniform registers;
+// NB == 0: any count, read from LDS.  One atomic per wave-iteration with candidates.
+// Candidate order in `cand` is irrelevant (the select keys carry the window index).
+template <int NB>
+__global__ __launch_bounds__(kTB) void ppknn_scan_boxes(const double* __restrict__ x, const double* __restrict__ y,
+                                                        uint64_t n, PpknnBoxes B, unsigned* __restrict__ cand,
+                                                        RselState* __restrict__ st) {
+    __shared__ Box lb[NB == 0 ? kPpBoxes : 1];
+    __shared__ unsigned wbuf[kTB / kWave][kPpBuf];
+    const int lane = lane_id();
+    Box rb[NB > 0 ? NB : 1];
+    if (NB > 0) {
+#pragma unroll
+        for (int b = 0; b < (NB > 0 ? NB : 1); b++) rb[b] = B.b[b];
+    } else {
+        if (threadIdx.x < (unsigned)B.nb) lb[threadIdx.x] = B.b[threadIdx.x];
+        __syncthreads();
+    }
+    auto cls = [&](double px, double py) {
+        bool c = false;
+        if (NB > 0) {
+#pragma unroll
+            for (int b = 0; b < (NB > 0 ? NB : 1); b++) c = c || in_box(rb[b], px, py);
+        } else {
+            for (int b = 0; b < B.nb; b++) c = c || in_box(lb[b], px, py);
+        }
+        return c;
+    };
+    // block b streams iterations [b per, (b + 1) per); its 4 waves interleave inside the chunk
+    const uint64_t all_iters = (n + 255) / 256, full_iters = n / 256;
+    const uint64_t per = (all_iters + gridDim.x - 1) / gridDim.x;
+    const uint64_t blk_end = (uint64_t)(blockIdx.x + 1) * per;
+    const uint64_t end = blk_end < all_iters ? blk_end : all_iters;
+    const uint64_t fend = end < full_iters ? end : full_iters;
+    const unsigned wid = threadIdx.x / kWave;
+    // candidates gather in a wave-private LDS buffer and leave with one global atomic per
+    // kPpBuf entries (the candidate points are scattered over the window: one atomic per
+    // wave-iteration serialises ~10^5 atomics on one address, ~400 us for the C4 window)
+    const int wslot = threadIdx.x / kWave;
+    unsigned* buf = wbuf[wslot];
+    unsigned cnt = 0;
+    auto flush = [&]() {
+        wave_lds_sync();
+        unsigned base = 0;
+        if (lane == 0) base = atomicAdd(&st->ncand, cnt);
+        base = __shfl(base, 0);
+        for (unsigned q = lane; q < cnt; q += kWave) cand[base + q] = buf[q];
+        wave_lds_sync();
+        cnt = 0;
+    };
+    auto emit = [&](uint64_t it, const bool c[4]) {
+        const uint64_t b0 = it * 256;
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const unsigned long long m = __ballot(c[s]);
+            if ((m >> lane) & 1ull) buf[cnt + lanes_below(m)] = (unsigned)(b0 + (s >> 1) * 128 + 2 * lane + (s & 1));
+            cnt += (unsigned)__popcll(m);
+        }
+        if (cnt > kPpBuf - 256) flush();
+    };
+    auto load_full = [&](uint64_t it, double2 v[4]) {
+        const uint64_t i0 = it * 256 + 2 * (uint64_t)lane;
+        v[0] = *reinterpret_cast<const double2*>(x + i0);
+        v[1] = *reinterpret_cast<const double2*>(x + i0 + 128);
+        v[2] = *reinterpret_cast<const double2*>(y + i0);
+        v[3] = *reinterpret_cast<const double2*>(y + i0 + 128);
+    };
+    uint64_t it = (uint64_t)blockIdx.x * per + wid;
+    double2 cur[4], nxt[4];
+    if (it < fend) load_full(it, cur);
+    for (; it < fend; it += kTB / kWave) {
+        const uint64_t nit = it + kTB / kWave;
+        if (nit < fend) load_full(nit, nxt);
+        const bool c[4] = {cls(cur[0].x, cur[2].x), cls(cur[0].y, cur[2].y), cls(cur[1].x, cur[3].x),
+                           cls(cur[1].y, cur[3].y)};
+        emit(it, c);
+#pragma unroll
+        for (int q = 0; q < 4; q++) cur[q] = nxt[q];
+    }
+    // the partial last iteration of the window (at most one, in the last chunk)
+    if (it < end && it == full_iters) {
+        const uint64_t i0 = it * 256 + 2 * (uint64_t)lane;
+        const bool v0 = i0 < n, v1 = i0 + 1 < n, v2 = i0 + 128 < n, v3 = i0 + 129 < n;
+        const double x0 = v0 ? x[i0] : 0.0, y0 = v0 ? y[i0] : 0.0;
+        const double x1 = v1 ? x[i0 + 1] : 0.0, y1 = v1 ? y[i0 + 1] : 0.0;
+        const double x2 = v2 ? x[i0 + 128] : 0.0, y2 = v2 ? y[i0 + 128] : 0.0;
+        const double x3 = v3 ? x[i0 + 129] : 0.0, y3 = v3 ? y[i0 + 129] : 0.0;
+        const bool c0 = cls(x0, y0), c1 = cls(x1, y1), c2 = cls(x2, y2), c3 = cls(x3, y3);
+        const bool c[4] = {v0 && c0, v1 && c1, v2 && c2, v3 && c3};
+        emit(it, c);
+    }
+    if (cnt) flush();
+}
+
 template <bool APPROX>
 __global__ __launch_bounds__(kTB) void ppknn_dist(const double* __restrict__ x, const double* __restrict__ y,
                                                   const unsigned* __restrict__ cand, const RselState* __restrict__ st,
@@ -1232,13 +1337,45 @@ __global__ __launch_bounds__(kTB) void ppknn_dist(const double* __restrict__ x, 
     const double* rvx = v_lds ? lvx : vx;
     const double* rvy = v_lds ? lvy : vy;
     const unsigned m = st->ncand;
-    for (unsigned t = blockIdx.x * kTB + threadIdx.x; t < m; t += gridDim.x * kTB) {
-        const unsigned i = cand[t];
+    if (APPROX) {
+        for (unsigned t = blockIdx.x * kTB + threadIdx.x; t < m; t += gridDim.x * kTB) {
+            const unsigned i = cand[t];
+            const double d = bbox_distance(x[i], y[i], P.bb);
+            unsigned long long bits = (unsigned long long)__double_as_longlong(d);
+            if (d != d) bits = 0x7ff8000000000000ull;
+            key[t] = bits;
+        }
+        return;
+    }
+    // exact (point_polygon_distance split over 8 lanes per candidate, each taking every 8th
+    // segment): crossings summed, boundary OR-ed, segment minima combined -- min is
+    // order-independent here, as no partial minimum is NaN (each starts at Double.MAX_VALUE and
+    // takes only strictly smaller values)
+    constexpr unsigned kG = 8;
+    const unsigned sub = threadIdx.x % kG;
+    const int nv = (int)P.nv;
+    for (unsigned t0 = (blockIdx.x * kTB + threadIdx.x) / kG; t0 < m; t0 += gridDim.x * (kTB / kG)) {
+        const unsigned i = cand[t0];
         const double px = x[i], py = y[i];
-        const double d = APPROX ? bbox_distance(px, py, P.bb) : point_polygon_distance(px, py, rvx, rvy, (int)P.nv, P.bb);
-        unsigned long long bits = (unsigned long long)__double_as_longlong(d);
-        if (d != d) bits = 0x7ff8000000000000ull;
-        key[t] = bits;
+        const bool in_env = !(px > P.bb[2] || px < P.bb[0] || py > P.bb[3] || py < P.bb[1]);
+        bool boundary = false;
+        int crossings = 0;
+        double md = 1.7976931348623157e308;
+        for (int e = (int)sub; e < nv - 1; e += (int)kG) {
+            const double ax = rvx[e], ay = rvy[e], bx = rvx[e + 1], by = rvy[e + 1];
+            if (in_env) count_segment(px, py, bx, by, ax, ay, boundary, crossings);
+            const double d = point_segment(px, py, ax, ay, bx, by);
+            md = d < md ? d : md;
+        }
+#pragma unroll
+        for (unsigned o = 1; o < kG; o <<= 1) {
+            crossings += __shfl_xor(crossings, (int)o);
+            boundary = (__shfl_xor((int)boundary, (int)o) != 0) || boundary;
+            const double od = __shfl_xor(md, (int)o);
+            md = od < md ? od : md;
+        }
+        const double d = (in_env && (boundary || (crossings & 1))) ? 0.0 : md;
+        if (sub == 0) key[t0] = (unsigned long long)__double_as_longlong(d);
     }
 }
 
@@ -1246,12 +1383,16 @@ __device__ __forceinline__ bool rsel_match(const RselState& s, unsigned long lon
     return (d & s.md) == s.pd && (i & s.mi) == s.pi;
 }
 
+// candidate counts up to this are selected by one workgroup (rsel_small); the multi-block
+// rounds below are no-ops then
+constexpr unsigned kRselSmall = 1u << 17;
+
 __global__ __launch_bounds__(kTB) void rsel_hist(const unsigned long long* __restrict__ key,
                                                  const unsigned* __restrict__ cand, RselState* __restrict__ st,
                                                  int round, unsigned k) {
     __shared__ unsigned h[kRselBins];
     const unsigned m = st->ncand;
-    if (m <= k) return;  // every candidate is selected
+    if (m <= k || m <= st->small_max) return;  // every candidate is selected / rsel_small did it
     for (int t = threadIdx.x; t < kRselBins; t += kTB) h[t] = 0;
     __syncthreads();
     int field, shift, width;
@@ -1274,6 +1415,7 @@ __global__ __launch_bounds__(kTB) void rsel_hist(const unsigned long long* __res
 __global__ __launch_bounds__(1024) void rsel_pick(RselState* __restrict__ st, int round, unsigned k) {
     __shared__ unsigned part[1024];
     const unsigned m = st->ncand;
+    if (m <= st->small_max) return;
     if (m <= k) {  // select all: the k-th key is the maximum
         if (threadIdx.x == 0) {
             st->md = 0; st->pd = 0; st->mi = 0; st->pi = 0;
@@ -1322,6 +1464,7 @@ __global__ __launch_bounds__(kTB) void rsel_gather(const unsigned long long* __r
                                                    unsigned k, unsigned long long* __restrict__ sel_d,
                                                    unsigned* __restrict__ sel_i) {
     const unsigned m = st->ncand;
+    if (m <= st->small_max) return;
     const bool all = m <= k;
     const unsigned long long kd = st->pd;
     const unsigned ki = st->pi;
@@ -1338,12 +1481,181 @@ __global__ __launch_bounds__(kTB) void rsel_gather(const unsigned long long* __r
     }
 }
 
+// slot of this lane among the wave's active lanes in a counter (one atomic per wave)
+__device__ __forceinline__ unsigned wave_reserve(unsigned* ctr) {
+    const unsigned long long m = __ballot(1);
+    const int lead = __builtin_ctzll(m);
+    unsigned b = 0;
+    if (lane_id() == lead) b = atomicAdd(ctr, (unsigned)__popcll(m));
+    b = __shfl(b, lead);
+    return b + lanes_below(m);
+}
+
+// One workgroup, M <= kRselSmall candidates (L2-resident keys): the 9 radix rounds with an LDS
+// histogram, the gather and the sort, in one launch.  Once the keys still matching the decided
+// prefix fit kCompact, they are copied into LDS and the later rounds no longer read L2 (one CU
+// streams ~64 B/clk: each full pass over 10^5 keys costs ~5 us).
+constexpr unsigned kCompact = 10240;
+__global__ __launch_bounds__(1024) void rsel_small(const unsigned long long* __restrict__ key,
+                                                   const unsigned* __restrict__ cand, const RselState* __restrict__ st,
+                                                   unsigned k, double* __restrict__ out_d, unsigned* __restrict__ out_i,
+                                                   unsigned* __restrict__ out_count) {
+    __shared__ unsigned h[kRselBins];
+    __shared__ unsigned part[64];
+    __shared__ unsigned long long sd[256];
+    __shared__ unsigned si[256];
+    __shared__ unsigned long long cd[kCompact];
+    __shared__ unsigned ci[kCompact];
+    __shared__ unsigned long long s_pd, s_md;
+    __shared__ unsigned s_pi, s_mi, s_kk, s_nsel, s_cnt, s_lds, s_lcnt;
+    const unsigned m = st->ncand;
+    if (m > st->small_max) return;
+    const unsigned t = threadIdx.x;
+    if (t == 0) {
+        s_pd = 0; s_md = 0; s_pi = 0; s_mi = 0; s_kk = k; s_nsel = 0; s_cnt = m; s_lds = 0; s_lcnt = 0;
+    }
+    __syncthreads();
+    const bool all = m <= k;
+    // visit every key of the current source (global list or the LDS copy) matching the prefix
+    auto for_matching = [&](auto&& fn) {
+        const unsigned long long md = s_md, pd = s_pd;
+        const unsigned mi = s_mi, pi = s_pi;
+        if (s_lds) {
+            const unsigned cnt = s_lcnt;  // entries of the LDS copy
+            for (unsigned c = t; c < cnt; c += 1024) {
+                const unsigned long long d = cd[c];
+                const unsigned i = ci[c];
+                if ((d & md) == pd && (i & mi) == pi) fn(d, i);
+            }
+            return;
+        }
+        for (unsigned c0 = t; c0 < m; c0 += 4 * 1024) {  // 4 independent loads per thread in flight
+            unsigned long long d[4];
+            unsigned i[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const unsigned c = c0 + u * 1024;
+                d[u] = c < m ? key[c] : ~0ull;
+                i[u] = c < m ? cand[c] : ~0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (c0 + u * 1024 < m && (d[u] & md) == pd && (i[u] & mi) == pi) fn(d[u], i[u]);
+        }
+    };
+    for (int round = 0; round < kRselRounds && !all; round++) {
+        for (int b = t; b < kRselBins; b += 1024) h[b] = 0;
+        __syncthreads();
+        int field, shift, width;
+        rsel_round(round, field, shift, width);
+        const unsigned dm = (1u << width) - 1u;
+        for_matching([&](unsigned long long d, unsigned i) {
+            // digits concentrate (distance 0 inside the polygon, shared exponents): the lanes
+            // holding the first active lane's digit add with one LDS atomic
+            const unsigned dg = field == 0 ? (unsigned)(d >> shift) & dm : (i >> shift) & dm;
+            const unsigned first = __builtin_amdgcn_readfirstlane(dg);
+            const unsigned long long same = __ballot(dg == first);
+            if (dg != first) atomicAdd(&h[dg], 1u);
+            else if (lanes_below(same) == 0) atomicAdd(&h[first], (unsigned)__popcll(same));
+        });
+        __syncthreads();
+        unsigned v[4], sum = 0;
+        for (int j = 0; j < 4; j++) {
+            v[j] = h[4 * t + j];
+            sum += v[j];
+        }
+        // block inclusive scan of the per-thread sums: DPP within waves, then 16 wave totals
+        const unsigned winc = wave_incl_scan(sum);
+        if (lane_id() == kWave - 1) part[t / kWave] = winc;
+        __syncthreads();
+        unsigned wbase = 0;
+        for (unsigned w = 0; w < t / kWave; w++) wbase += part[w];
+        const unsigned kk = s_kk;
+        const unsigned incl = wbase + winc, excl = incl - sum;
+        __syncthreads();
+        if (excl < kk && incl >= kk) {
+            unsigned c = excl;
+            int j = 0;
+            while (c + v[j] < kk) c += v[j++];
+            const unsigned dg = 4 * t + j;
+            s_kk = kk - c;
+            s_cnt = v[j];  // keys matching the extended prefix
+            if (field == 0) {
+                s_pd |= (unsigned long long)dg << shift;
+                s_md |= (unsigned long long)dm << shift;
+            } else {
+                s_pi |= dg << shift;
+                s_mi |= dm << shift;
+            }
+        }
+        __syncthreads();
+        if (!s_lds && s_cnt <= kCompact && round + 1 < kRselRounds) {  // move the survivors into LDS
+            if (t == 0) s_nsel = 0;
+            __syncthreads();
+            for_matching([&](unsigned long long d, unsigned i) {
+                const unsigned sl = wave_reserve(&s_nsel);
+                cd[sl] = d;
+                ci[sl] = i;
+            });
+            __syncthreads();
+            if (t == 0) {
+                s_lds = 1;
+                s_lcnt = s_nsel;
+                s_nsel = 0;
+            }
+            __syncthreads();
+        }
+    }
+    // keys <= the k-th key: all of the global list (M <= k), else the gather of the rounds'
+    // prefix plus every key below it -- taken from the full global list
+    const unsigned long long kd = s_pd;
+    const unsigned ki = s_pi;
+    for (unsigned c = t; c < m; c += 1024) {
+        const unsigned long long d = key[c];
+        const unsigned i = cand[c];
+        if (all || d < kd || (d == kd && i <= ki)) {
+            const unsigned sl = wave_reserve(&s_nsel);
+            if (sl < 256) {
+                sd[sl] = d;
+                si[sl] = i;
+            }
+        }
+    }
+    __syncthreads();
+    const unsigned ns = s_nsel < k ? s_nsel : k;
+    if (t < 256 && t >= ns) {
+        sd[t] = ~0ull;
+        si[t] = ~0u;
+    }
+    __syncthreads();
+    for (unsigned size = 2; size <= 256; size <<= 1) {
+        for (unsigned j = size >> 1; j > 0; j >>= 1) {
+            const unsigned p = t ^ j;
+            if (t < 256 && p > t) {
+                const bool up = (t & size) == 0;
+                const bool gt = sd[t] > sd[p] || (sd[t] == sd[p] && si[t] > si[p]);
+                if (gt == up) {
+                    const unsigned long long td = sd[t]; sd[t] = sd[p]; sd[p] = td;
+                    const unsigned ti = si[t]; si[t] = si[p]; si[p] = ti;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (t < ns) {
+        out_d[t] = __longlong_as_double((long long)sd[t]);
+        out_i[t] = si[t];
+    }
+    if (t == 0) out_count[0] = ns;
+}
+
 __global__ __launch_bounds__(256) void rsel_sort(const unsigned long long* __restrict__ sel_d,
                                                  const unsigned* __restrict__ sel_i, const RselState* __restrict__ st,
                                                  unsigned k, double* __restrict__ out_d, unsigned* __restrict__ out_i,
                                                  unsigned* __restrict__ out_count) {
     __shared__ unsigned long long d[256];
     __shared__ unsigned id[256];
+    if (st->ncand <= st->small_max) return;
     const unsigned m = st->nsel < k ? st->nsel : k;
     const unsigned t = threadIdx.x;
     d[t] = t < m ? sel_d[t] : ~0ull;
@@ -2083,6 +2395,17 @@ int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, co
     for (auto& q : pl.g) hrect.insert(hrect.end(), {q.x0, q.x1, q.y0, q.y1});
     for (auto& q : pl.c) hrect.insert(hrect.end(), {q.x0, q.x1, q.y0, q.y1});
     const uint32_t nrect = (uint32_t)(hrect.size() / 4);
+    // exact coordinate boxes of the rects (no division in the scan) when they fit the kernel args
+    PpknnBoxes PB;
+    memset(&PB, 0, sizeof PB);
+    const bool boxed = nrect <= (uint32_t)kPpBoxes;
+    if (boxed) {
+        for (uint32_t q = 0; q < nrect; q++) {
+            const geohip_rect rr{hrect[4 * q], hrect[4 * q + 1], hrect[4 * q + 2], hrect[4 * q + 3]};
+            PB.b[q] = rect_to_box(*grid, rr);
+        }
+        PB.nb = (int32_t)nrect;
+    }
     PpknnPoly P;
     for (int i = 0; i < 4; i++) P.bb[i] = pl.bbox[i];
     P.nv = (uint32_t)pl.rx.size();
@@ -2120,20 +2443,50 @@ int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, co
     hipEvent_t e0, e1;
     ctx_timing_events(ctx, &e0, &e1);
     if (e0) hipEventRecord(e0, st);
-    rsel_init<<<1, 1024, 0, st>>>(rs, k);
+    // single-workgroup select up to kRselSmall candidates (GEOHIP_RSEL_SMALL: test hook)
+    static const unsigned small_max = getenv("GEOHIP_RSEL_SMALL") ? (unsigned)atol(getenv("GEOHIP_RSEL_SMALL")) : kRselSmall;
+    rsel_init<<<1, 1024, 0, st>>>(rs, k, small_max);
     if (n && nrect) {
-        const uint64_t nb = std::min<uint64_t>((n + kTB - 1) / kTB, 4096);
-        ppknn_scan<<<(unsigned)nb, kTB, 0, st>>>(dx, dy, n, grid->min_x, grid->min_y, grid->cell_len, drect, nrect, cand, rs);
+        if (boxed) {
+            const uint64_t iters = (n + 255) / 256;
+            static const uint64_t max_blocks = getenv("GEOHIP_PPKNN_BLOCKS") ? (uint64_t)atol(getenv("GEOHIP_PPKNN_BLOCKS")) : 2048;
+            const uint64_t nb = std::max<uint64_t>(1, std::min<uint64_t>((iters + 3) / 4, max_blocks));  // 4 waves per block
+            switch (PB.nb) {
+                case 1: ppknn_scan_boxes<1><<<(unsigned)nb, kTB, 0, st>>>(dx, dy, n, PB, cand, rs); break;
+                case 2: ppknn_scan_boxes<2><<<(unsigned)nb, kTB, 0, st>>>(dx, dy, n, PB, cand, rs); break;
+                case 3: ppknn_scan_boxes<3><<<(unsigned)nb, kTB, 0, st>>>(dx, dy, n, PB, cand, rs); break;
+                case 4: ppknn_scan_boxes<4><<<(unsigned)nb, kTB, 0, st>>>(dx, dy, n, PB, cand, rs); break;
+                default: ppknn_scan_boxes<0><<<(unsigned)nb, kTB, 0, st>>>(dx, dy, n, PB, cand, rs); break;
+            }
+        } else {
+            const uint64_t nb = std::min<uint64_t>((n + kTB - 1) / kTB, 4096);
+            ppknn_scan<<<(unsigned)nb, kTB, 0, st>>>(dx, dy, n, grid->min_x, grid->min_y, grid->cell_len, drect, nrect,
+                                                     cand, rs);
+        }
         if (approximate) ppknn_dist<true><<<1024, kTB, 0, st>>>(dx, dy, cand, rs, dvx, dvy, P, key);
         else ppknn_dist<false><<<1024, kTB, 0, st>>>(dx, dy, cand, rs, dvx, dvy, P, key);
+    }
+    rsel_small<<<1, 1024, 0, st>>>(key, cand, rs, k, od, oi, ocnt);  // M <= kRselSmall (also M = 0)
+    if (e1) hipEventRecord(e1, st);  // re-recorded below when the multi-block rounds run
+    // the multi-block rounds only when the candidate count needs them (one count readback
+    // instead of 20 no-op launches, ~80 us)
+    bool big = false;
+    if (n && nrect) {
+        uint64_t* pin = ctx_pinned(ctx);
+        if (hipMemcpyAsync(pin, &rs->ncand, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "candidate count readback failed");
+        big = (uint32_t)(pin[0] & 0xffffffffu) > small_max;
+    }
+    if (big) {
         for (int t = 0; t < kRselRounds; t++) {
             rsel_hist<<<512, kTB, 0, st>>>(key, cand, rs, t, k);
             rsel_pick<<<1, 1024, 0, st>>>(rs, t, k);
         }
         rsel_gather<<<512, kTB, 0, st>>>(key, cand, rs, k, sel_d, sel_i);
+        rsel_sort<<<1, 256, 0, st>>>(sel_d, sel_i, rs, k, od, oi, ocnt);
+        if (e1) hipEventRecord(e1, st);
     }
-    rsel_sort<<<1, 256, 0, st>>>(sel_d, sel_i, rs, k, od, oi, ocnt);
-    if (e1) hipEventRecord(e1, st);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, std::string("knn_ppoly launch: ") + hipGetErrorString(e));
     uint32_t m = 0;

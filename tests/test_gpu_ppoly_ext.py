@@ -159,3 +159,15 @@ def test_knn_ppoly_c4_size(ctx):
     wi, wd = cref.knn_ppoly(cg, hx, hy, vx, vy, 0.005, 100)
     assert gi.cpu().numpy().tolist() == wi.tolist()
     assert np.array_equal(gd.cpu().numpy().view(np.uint64), wd.view(np.uint64))
+
+
+def test_knn_ppoly_large_candidate_set(ctx):
+    """More than 2^17 candidates: the multi-block radix-select rounds instead of rsel_small."""
+    x, y = synth.uniform(1_500_000, 131)
+    off, vx, vy = synth.star_polygons(1, 132)
+    ag, cg = agrid(100)
+    for k, approx in ((256, False), (7, False), (100, True)):
+        gi, gd = ctx.knn_ppoly(ag, x, y, vx, vy, 0.5, k, approx)
+        wi, wd = cref.knn_ppoly(cg, x, y, vx, vy, 0.5, k, approx)
+        assert gi.tolist() == wi.tolist()
+        assert np.array_equal(gd.view(np.uint64), wd.view(np.uint64))
