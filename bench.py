@@ -15,6 +15,7 @@ The other configs are measured with ``--workload`` (same JSON contract, one line
   ingest SURVEY.md 8(f) row 1: 10M CSV records -> SoA x/y + ts + cell (device-resident text)
   ppjoin SURVEY.md 8(f) row 2: the C4 shape as a point-polygon join (1k polygons x 50M points)
   ppknn  SURVEY.md 8(f) row 2: point-polygon kNN k = 50 of one polygon over 50M points
+  knn_incr SURVEY.md 8(f) row 3: C2 over 10 s / 5 s sliding windows, pane reuse (5M-point panes)
 
 Windows are device-resident before the timed region (synthetic: uniform windows are made on
 the device by the counter-based generator of spatialflink_amd.synth; Gaussian windows on the
@@ -23,7 +24,7 @@ is cycled so no step reads a window the Infinity Cache still holds.
 
 Prints ONE JSON line (rank 0) with roofline and cpu_baseline objects.
 
-    python bench.py --gpus 1 --steps 50 --warmup 5 [--workload knn|range|join|ppoly|c5|ingest|ppjoin|ppknn]
+    python bench.py --gpus 1 --steps 50 --warmup 5 [--workload knn|range|join|ppoly|c5|ingest|ppjoin|ppknn|knn_incr]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -50,7 +51,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--workload", choices=("knn", "range", "join", "ppoly", "c5", "ingest", "ppjoin", "ppknn"), default="knn")
+    p.add_argument("--workload", choices=("knn", "range", "join", "ppoly", "c5", "ingest", "ppjoin", "ppknn", "knn_incr"), default="knn")
     p.add_argument("--points", type=int, default=None, help="points per window per GPU (default: the config's)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -504,6 +505,33 @@ class PpKnnWorkload(Workload):
                           f"knn_ppoly single thread, {t:.1f} s"}
 
 
+class KnnIncrWorkload(KnnWorkload):
+    """the C2 kNN over 10 s / 5 s sliding windows with pane reuse -- one
+    step = one new 5M-point pane (half a 10M-point window) evaluated once, then the window's
+    top-k merged from its two panes' top-k lists (spatialflink_amd.incremental.IncrementalKNN).
+    value = stream points/sec (each point is evaluated once, not once per window)."""
+    tag = "knn_incr"
+    kernel = "geohip::knn_scan<1> + knn_final<1> on one pane (+ a 2-list knn_merge)"
+    n_default = 5_000_000
+    label = "C2 over 10s/5s sliding windows with pane reuse: kNN k=50, 100x100 Beijing UniformGrid, r=0.5"
+
+    def __init__(self, *a):
+        super().__init__(*a)
+        from spatialflink_amd.incremental import IncrementalKNN
+        self.inc = IncrementalKNN(self.ctx, self.grid, self.q[0], self.q[1], self.radius, self.k, 2)
+
+    def step(self, s):
+        w = s % self.windows
+        self.inc.push(self.xs[w], self.ys[w])
+
+    def config(self):
+        c = super().config()
+        c["workload"] = f"{self.label}, {self.n} new points per pane (window = 2 panes) per GPU"
+        c["points_per_pane_per_gpu"] = c.pop("points_per_window_per_gpu")
+        c["panes_per_window"] = 2
+        return c
+
+
 class C5Workload(KnnWorkload):
     """C5 per shard (BASELINE.json configs[4]): 1000x1000 grid, 25M uniform points per GPU
     (200M per window on 8 GPUs), kNN k=100 + range r=0.05 of the README query."""
@@ -603,7 +631,8 @@ class IngestWorkload(Workload):
 
 
 WORKLOADS = {"knn": KnnWorkload, "range": RangeWorkload, "join": JoinWorkload, "ppoly": PpolyWorkload,
-             "c5": C5Workload, "ingest": IngestWorkload, "ppjoin": PpJoinWorkload, "ppknn": PpKnnWorkload}
+             "c5": C5Workload, "ingest": IngestWorkload, "ppjoin": PpJoinWorkload, "ppknn": PpKnnWorkload,
+             "knn_incr": KnnIncrWorkload}
 
 
 def main():

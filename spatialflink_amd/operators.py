@@ -180,6 +180,19 @@ class PointPointRangeQuery(_Operator):
                                     float(query_radius), self.conf.approximate_query)
 
 
+    def queryIncremental(self, panes, query_point: Point, query_radius: float):
+        """PointPointRangeQuery.queryIncremental (PointPointRangeQuery.java:144-245): ``panes`` is
+        the stream cut into slides (PointWindow each); yields each sliding window's result
+        (window-local indices) with every point evaluated once (spatialflink_amd.incremental)."""
+        from .incremental import IncrementalRange, panes_per_window
+        self._check_type()
+        inc = IncrementalRange(self._ctx(), self.index.abi(), query_point.x, query_point.y, float(query_radius),
+                               self.conf.approximate_query,
+                               panes_per_window(self.conf.window_size, self.conf.slide_step))
+        for pane in panes:
+            yield inc.push(pane.x, pane.y)
+
+
 class PointPointKNNQuery(_Operator):
     """PointPointKNNQuery.run (PointPointKNNQuery.java:33-191): the window's k nearest
     points among guaranteed u candidate cells, ascending (distance, index); no radius filter
@@ -189,6 +202,16 @@ class PointPointKNNQuery(_Operator):
         self._check_type()
         return self._ctx().knn_pp(self.index.abi(), window.x, window.y, query_point.x, query_point.y,
                                   float(query_radius), int(k))
+
+    def queryIncremental(self, panes, query_point: Point, query_radius: float, k: int):
+        """Sliding-window kNN with pane reuse (device panes): yields each window's (idx, dist),
+        the k smallest (dist, idx) over the window's last window_size / slide_step panes."""
+        from .incremental import IncrementalKNN, panes_per_window
+        self._check_type()
+        inc = IncrementalKNN(self._ctx(), self.index.abi(), query_point.x, query_point.y, float(query_radius), int(k),
+                             panes_per_window(self.conf.window_size, self.conf.slide_step))
+        for pane in panes:
+            yield inc.push(pane.x, pane.y)
 
 
 class PointPointJoinQuery(_Operator):

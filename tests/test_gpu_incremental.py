@@ -1,0 +1,79 @@
+"""GPU: incremental sliding windows with pane reuse equal full evaluation.
+
+Every window's result, assembled from the per-pane GPU results, must be bit-identical to the C
+oracle's evaluation of the whole window (the points of its last window_size / slide_step panes,
+concatenated in arrival order): range index sets (ascending), kNN (idx, distance bits).
+Pane sizes are ragged and include an empty pane; the first windows hold fewer panes.
+"""
+import numpy as np
+import pytest
+
+import cref
+from spatialflink_amd import _abi, synth
+from spatialflink_amd.incremental import IncrementalKNN, IncrementalRange
+from spatialflink_amd.operators import Point, PointPointRangeQuery, PointWindow, QueryConfiguration, UniformGrid
+
+pytestmark = pytest.mark.gpu
+
+BJ = synth.BEIJING
+Q = synth.README_QUERY
+SIZES = [50_000, 120_000, 0, 70_001, 200_000, 33_333, 90_000]
+
+
+def grids(n):
+    l = (BJ[1] - BJ[0]) / n
+    return _abi.make_grid(BJ[0], BJ[2], l, n), cref.grid(BJ[0], BJ[2], l, n)
+
+
+def pane_stream(seed):
+    out, base = [], 0
+    for s in SIZES:
+        x, y = synth.uniform(s, seed, base=base)
+        out.append((x, y))
+        base += s
+    return out
+
+
+@pytest.mark.parametrize("p", [2, 3])
+def test_incremental_range_equals_full_window(ctx, p):
+    import torch
+    ag, cg = grids(100)
+    panes = pane_stream(11)
+    inc = IncrementalRange(ctx, ag, Q[0], Q[1], 0.5, False, p)
+    for j, (x, y) in enumerate(panes):
+        got = inc.push(torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()).cpu().numpy()
+        win = panes[max(0, j - p + 1):j + 1]
+        wx = np.concatenate([w[0] for w in win])
+        wy = np.concatenate([w[1] for w in win])
+        want = np.sort(cref.range_pp(cg, wx, wy, Q[0], Q[1], 0.5).astype(np.int64))
+        assert got.tolist() == want.tolist()
+
+
+@pytest.mark.parametrize("p,k", [(2, 50), (3, 7)])
+def test_incremental_knn_equals_full_window(ctx, p, k):
+    import torch
+    ag, cg = grids(100)
+    panes = pane_stream(12)
+    inc = IncrementalKNN(ctx, ag, Q[0], Q[1], 0.5, k, p)
+    for j, (x, y) in enumerate(panes):
+        gi, gd = inc.push(torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda())
+        win = panes[max(0, j - p + 1):j + 1]
+        wx = np.concatenate([w[0] for w in win])
+        wy = np.concatenate([w[1] for w in win])
+        wi, wd = cref.knn_pp(cg, wx, wy, Q[0], Q[1], 0.5, k)
+        assert gi.cpu().numpy().tolist() == wi.tolist()
+        assert np.array_equal(gd.cpu().numpy().view(np.uint64), wd.view(np.uint64))
+
+
+def test_query_incremental_operator(ctx):
+    """PointPointRangeQuery.queryIncremental mirror: 10 s windows sliding by 5 s (2 panes)."""
+    grid = UniformGrid(100, *BJ)
+    op = PointPointRangeQuery(QueryConfiguration(window_size=10, slide_step=5), grid, ctx)
+    panes = pane_stream(13)
+    cg = grids(100)[1]
+    windows = list(op.queryIncremental([PointWindow(x, y) for x, y in panes], Point(*Q), 0.5))
+    for j, got in enumerate(windows):
+        win = panes[max(0, j - 1):j + 1]
+        wx = np.concatenate([w[0] for w in win])
+        wy = np.concatenate([w[1] for w in win])
+        assert np.asarray(got).tolist() == np.sort(cref.range_pp(cg, wx, wy, Q[0], Q[1], 0.5)).tolist()
