@@ -16,6 +16,7 @@ The other configs are measured with ``--workload`` (same JSON contract, one line
   ppjoin SURVEY.md 8(f) row 2: the C4 shape as a point-polygon join (1k polygons x 50M points)
   ppknn  SURVEY.md 8(f) row 2: point-polygon kNN k = 50 of one polygon over 50M points
   knn_incr SURVEY.md 8(f) row 3: C2 over 10 s / 5 s sliding windows, pane reuse (5M-point panes)
+  ppoly_incr SURVEY.md 8(f) row 3: C4 over 10 s / 5 s sliding windows, pane reuse (25M-point panes)
 
 Windows are device-resident before the timed region (synthetic: uniform windows are made on
 the device by the counter-based generator of spatialflink_amd.synth; Gaussian windows on the
@@ -24,7 +25,7 @@ is cycled so no step reads a window the Infinity Cache still holds.
 
 Prints ONE JSON line (rank 0) with roofline and cpu_baseline objects.
 
-    python bench.py --gpus 1 --steps 50 --warmup 5 [--workload knn|range|join|ppoly|c5|ingest|ppjoin|ppknn|knn_incr]
+    python bench.py --gpus 1 --steps 50 --warmup 5 [--workload knn|range|join|ppoly|c5|ingest|ppjoin|ppknn|knn_incr|ppoly_incr]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -51,7 +52,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--workload", choices=("knn", "range", "join", "ppoly", "c5", "ingest", "ppjoin", "ppknn", "knn_incr"), default="knn")
+    p.add_argument("--workload", choices=("knn", "range", "join", "ppoly", "c5", "ingest", "ppjoin", "ppknn", "knn_incr", "ppoly_incr"), default="knn")
     p.add_argument("--points", type=int, default=None, help="points per window per GPU (default: the config's)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -505,6 +506,37 @@ class PpKnnWorkload(Workload):
                           f"knn_ppoly single thread, {t:.1f} s"}
 
 
+class PpolyIncrWorkload(PpolyWorkload):
+    """SURVEY.md 8(f) row 3 where pane reuse pays: the C4 point-polygon range over 10 s / 5 s
+    sliding windows -- one step = one new 25M-point pane (half the 50M-point window) evaluated
+    once against the 1k polygons, the window's pairs assembled from its two panes
+    (spatialflink_amd.incremental.IncrementalPPolyRange).  value = stream points/sec."""
+    tag = "ppoly_incr"
+    kernel = "geohip::ppoly_eval + ppoly_emit on one pane (tile binning before the timed region)"
+    n_default = 25_000_000
+    windows = 4
+
+    def __init__(self, *a):
+        super().__init__(*a)
+        from spatialflink_amd.incremental import IncrementalPPolyRange
+        import torch
+        self.inc = IncrementalPPolyRange(self.ctx, self.grid, self.off, self.vx, self.vy, self.radius, False, 2)
+        self.outs = [torch.empty((max(self.hits) + 1, 2), dtype=torch.int32, device=self.dev) for _ in range(2)]
+
+    def step(self, s):
+        w = s % self.windows
+        self.inc.push(self.xs[w], self.ys[w], out=self.outs[s % 2])
+
+    def config(self):
+        c = super().config()
+        c["workload"] = (f"C4 over 10s/5s sliding windows with pane reuse: {self.npoly} polygons x 50 vertices, "
+                         f"{self.n} new uniform points per pane (window = 2 panes) per GPU, "
+                         f"{self.grid_n}x{self.grid_n}, r={self.radius}")
+        c["points_per_pane_per_gpu"] = c.pop("points_per_window_per_gpu")
+        c["panes_per_window"] = 2
+        return c
+
+
 class KnnIncrWorkload(KnnWorkload):
     """the C2 kNN over 10 s / 5 s sliding windows with pane reuse -- one
     step = one new 5M-point pane (half a 10M-point window) evaluated once, then the window's
@@ -522,7 +554,7 @@ class KnnIncrWorkload(KnnWorkload):
 
     def step(self, s):
         w = s % self.windows
-        self.inc.push(self.xs[w], self.ys[w])
+        self.inc.push(self.xs[w], self.ys[w], sync=False)
 
     def config(self):
         c = super().config()
@@ -632,7 +664,7 @@ class IngestWorkload(Workload):
 
 WORKLOADS = {"knn": KnnWorkload, "range": RangeWorkload, "join": JoinWorkload, "ppoly": PpolyWorkload,
              "c5": C5Workload, "ingest": IngestWorkload, "ppjoin": PpJoinWorkload, "ppknn": PpKnnWorkload,
-             "knn_incr": KnnIncrWorkload}
+             "knn_incr": KnnIncrWorkload, "ppoly_incr": PpolyIncrWorkload}
 
 
 def main():

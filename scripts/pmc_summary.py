@@ -24,7 +24,8 @@ TAGS = {"knn": ("knn_scan", ("knn_scan", "knn_final"), 1),
         "ingest": ("ingest", ("ingest_count", "ingest_scan", "ingest_parse"), 1),
         "ppjoin": ("ppjoin", ("ppoly_eval", "ppoly_emit", "ppoly_outside"), 1),
         "ppknn": ("ppknn", ("rsel_", "ppknn_"), 1),
-        "knn_incr": ("knn_incr", ("knn_scan", "knn_final"), 1)}
+        "knn_incr": ("knn_incr", ("knn_scan", "knn_final"), 1),
+        "ppoly_incr": ("ppoly_incr", ("ppoly_eval", "ppoly_emit", "ppoly_outside"), 1)}
 
 
 def per_kernel(path):

@@ -100,8 +100,17 @@ __global__ __launch_bounds__(1024) void ingest_scan(const unsigned* __restrict__
     __shared__ unsigned long long s_part[1024];
     const uint64_t per = (nchunks + 1023) / 1024;
     const uint64_t b0 = threadIdx.x * per, b1 = b0 + per < nchunks ? b0 + per : nchunks;
+    // 8 independent loads in flight per thread (the serial sum paid one memory latency per count)
     unsigned long long s = 0;
-    for (uint64_t b = b0; b < b1; b++) s += cnt[b];
+    uint64_t b = b0;
+    for (; b + 8 <= b1; b += 8) {
+        unsigned v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = cnt[b + u];
+#pragma unroll
+        for (int u = 0; u < 8; u++) s += v[u];
+    }
+    for (; b < b1; b++) s += cnt[b];
     s_part[threadIdx.x] = s;
     __syncthreads();
     // Hillis-Steele over 1024 partial sums (one launch per batch: not on the critical path)
@@ -112,7 +121,17 @@ __global__ __launch_bounds__(1024) void ingest_scan(const unsigned* __restrict__
         __syncthreads();
     }
     unsigned long long run = s_part[threadIdx.x] - s;
-    for (uint64_t b = b0; b < b1; b++) {
+    for (b = b0; b + 8 <= b1; b += 8) {
+        unsigned v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = cnt[b + u];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            base[b + u] = run;
+            run += v[u];
+        }
+    }
+    for (; b < b1; b++) {
         base[b] = run;
         run += cnt[b];
     }
@@ -133,6 +152,76 @@ struct LdsReader {
         return p < n ? g[p] : (uint8_t)'\n';
     }
 };
+
+// CSV fast path over the staged bytes (LDS offsets, no bounds fallback to global memory): the
+// common record shape -- no blanks, control characters or quotes up to the last field the schema
+// names, numeric fields '-'? digits ('.' digits)? with at most 19 significant digits, the
+// timestamp '-'? digits (<= 18).  On that subset ingest::parse_csv splits the same fields and
+// computes the same (w, q) decimal (so the same Eisel-Lemire bits) and Long; anything else --
+// or a record running past the staged bytes -- returns kFallback and takes the general parser.
+// One pass, 32-bit offsets and few branches per byte: the general parser is SALU-bound on
+// divergent per-byte control flow.
+__device__ __forceinline__ int fast_csv(const uint8_t* __restrict__ s, uint32_t p, uint32_t lim,
+                                        const ingest::Spec& sp, ingest::Parsed* o) {
+    const uint8_t d = (uint8_t)sp.delim;
+    int need = sp.fx > sp.fy ? sp.fx : sp.fy;
+    if (sp.fts > need) need = sp.fts;
+    for (int f = 0; f <= need; f++) {
+        const bool isx = f == sp.fx, isy = f == sp.fy, ist = f == sp.fts;
+        if (isx || isy || ist) {
+            if (p >= lim || ((isx || isy) && ist)) return ingest::kFallback;
+            const bool neg = s[p] == '-';
+            p += neg ? 1u : 0u;
+            uint64_t w = 0;
+            int32_t q = 0;
+            int nd = 0, ni = 0, nf = 0;
+            bool dot = false, bad = false;
+            uint8_t c = 0;
+            for (; p < lim; p++) {
+                c = s[p];
+                const unsigned dg = (unsigned)c - '0';
+                if (dg < 10u) {
+                    const bool take = nd != 0 || dg != 0;
+                    bad |= take && nd == 19;
+                    w = take && nd < 19 ? w * 10u + dg : w;
+                    nd += take && nd < 19 ? 1 : 0;
+                    q -= dot ? 1 : 0;
+                    nf += dot ? 1 : 0;
+                    ni += dot ? 0 : 1;
+                } else if (c == '.' && !dot && !ist) {
+                    dot = true;
+                } else {
+                    break;
+                }
+            }
+            if (p >= lim || bad || ni == 0 || (dot && nf == 0)) return ingest::kFallback;
+            if (ist) {
+                if (ni > 18) return ingest::kFallback;
+                // Long.valueOf of the (<= 18 digit) run: w holds it exactly (leading zeros skipped)
+                o->ts = neg ? -(int64_t)w : (int64_t)w;
+            } else {
+                const uint64_t bits = ingest::decimal_to_bits(w, q) | (neg ? 1ull << 63 : 0ull);
+                const double v = __builtin_bit_cast(double, bits);
+                if (isx) o->x = v;
+                if (isy) o->y = v;
+            }
+        } else {
+            for (; p < lim; p++) {
+                const uint8_t c = s[p];
+                if (c == d || c <= ' ' || c == '"') break;
+            }
+            if (p >= lim) return ingest::kFallback;
+        }
+        const uint8_t c = s[p];
+        if (c == d && f < need) {
+            p++;
+            continue;
+        }
+        if (f == need && (c == d || c == '\n')) return ingest::kOk;
+        return ingest::kFallback;
+    }
+    return ingest::kFallback;
+}
 
 __global__ __launch_bounds__(kThreads) void ingest_parse(const uint8_t* __restrict__ text, uint64_t nbytes,
                                                         IngestArgs a, const unsigned long long* __restrict__ chunk_base,
@@ -165,11 +254,17 @@ __global__ __launch_bounds__(kThreads) void ingest_parse(const uint8_t* __restri
     __syncthreads();
     const LdsReader rd{reinterpret_cast<const uint8_t*>(s_text4), c0, stage_len, text, nbytes};
     const uint64_t rbase = chunk_base[blockIdx.x];
+    const uint8_t dl = (uint8_t)a.spec.delim;
+    const bool fast = a.spec.format == ingest::kCsv && dl > ' ' && dl != '"' && dl != '.' && dl != '-' &&
+                      (unsigned)(dl - '0') >= 10u;
     for (unsigned i = threadIdx.x; i < nrec; i += kThreads) {
         const uint64_t idx = rbase + i;
         ingest::Parsed o;
         o.ts = 0;
-        if (ingest::parse_record(rd, c0 + s_start[i], a.spec, &o) != ingest::kOk) {
+        int rc = fast ? fast_csv(reinterpret_cast<const uint8_t*>(s_text4), s_start[i], stage_len, a.spec, &o)
+                      : ingest::kFallback;
+        if (rc != ingest::kOk) rc = ingest::parse_record(rd, c0 + s_start[i], a.spec, &o);
+        if (rc != ingest::kOk) {
             atomicMin(bad, (unsigned long long)idx);
             continue;
         }

@@ -56,56 +56,101 @@ class IncrementalRange:
                               [hits.astype(np.int64) + o for (_, hits), o in zip(self.panes, offs)])
 
 
+class IncrementalPPolyRange:
+    """Point-polygon range (many query polygons) over sliding windows with pane reuse: each pane's
+    (polygon, point) pairs are computed once; a window's pairs are the panes' pairs with the
+    point index offset by the pane's position in the window (PointPolygonRangeQuery's per-point
+    predicate, PointPolygonRangeQuery.java:104-124, makes pane results independent).  The polygon
+    plan is cached by the context, so panes after the first skip planning and upload."""
+
+    def __init__(self, ctx: _abi.Context, grid: _abi.Grid, ring_off, vx, vy, r: float, approximate: bool = False,
+                 panes: int = 2, out_cap: int = 0):
+        self.ctx, self.grid, self.r, self.approx = ctx, grid, r, approximate
+        self.rings = (ring_off, vx, vy)
+        self.panes = deque(maxlen=panes)  # (pane size, pairs [m, 2] (polygon, point))
+        self.out_cap = out_cap
+
+    def push(self, x, y, out=None):
+        pairs = self.ctx.range_ppoly(self.grid, x, y, *self.rings, self.r, self.approx, out=out)
+        self.panes.append((len(x), pairs))
+        return self.window()
+
+    def window(self):
+        """Pairs of the window (polygon, window-local point index), pane by pane (a list: the
+        caller concatenates if it needs one array)."""
+        out, off = [], 0
+        for size, pairs in self.panes:
+            if off:
+                pairs = pairs.clone() if _abi._is_device(pairs) else pairs.copy()
+                pairs[:, 1] += off
+            out.append(pairs)
+            off += size
+        return out
+
+
 class IncrementalKNN:
-    """Point-point kNN over sliding windows with pane reuse (device tensors).  The device kernels
-    and the torch plumbing between them (index offsets) run on one private stream; the caller's
-    stream waits for it before the results are returned."""
+    """Point-point kNN over sliding windows with pane reuse (device tensors).  Each pane's top-k
+    (k indices, -1 padded, and distances) lands in a ring of P slots; a window merges the P lists
+    after offsetting each pane's indices by the pane's position in the window.  The kernels and the
+    torch plumbing between them run on one private stream; the caller's stream waits for it."""
 
     def __init__(self, ctx: _abi.Context, grid: _abi.Grid, qx: float, qy: float, r: float, k: int, panes: int = 2):
         import torch
-        self.ctx, self.grid, self.q, self.r, self.k = ctx, grid, (qx, qy), r, int(k)
-        self.panes = deque(maxlen=panes)  # (pane size, top-k idx int32[k] (-1 padded), dist f64[k])
+        self.ctx, self.grid, self.q, self.r, self.k, self.p = ctx, grid, (qx, qy), r, int(k), int(panes)
         self.stream = torch.cuda.Stream()
+        self.sizes = deque(maxlen=self.p)  # sizes of the panes in the ring, oldest first
+        self.count = 0                     # panes pushed so far
+        self._offs = {}                    # (slot order, offsets) -> device tensors
+        self._dev = None
 
-    def push(self, x, y):
+    def _alloc(self, dev):
         import torch
+        k, p = self.k, self.p
+        self.ring_i = torch.full((p, k), -1, dtype=torch.int32, device=dev)
+        self.ring_d = torch.empty((p, k), dtype=torch.float64, device=dev)
+        self.cnt = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.mi = torch.empty(k, dtype=torch.int32, device=dev)
+        self.md = torch.empty(k, dtype=torch.float64, device=dev)
+        self._dev = dev
+
+    def push(self, x, y, sync: bool = True):
+        """Evaluate the new pane and merge the window.  sync=True: (idx, dist) trimmed to the
+        count (one host sync); sync=False: the k-long device outputs (idx -1 padded), no sync."""
+        import torch
+        if self._dev != x.device:
+            self._alloc(x.device)
         caller = torch.cuda.current_stream()
         self.stream.wait_stream(caller)  # the pane's x, y are ready
         prev = self.ctx.stream()
         self.ctx.set_stream(self.stream.cuda_stream)
         try:
             with torch.cuda.stream(self.stream):
-                k = self.k
-                dev = x.device
-                oi = torch.empty(k, dtype=torch.int32, device=dev)
-                od = torch.empty(k, dtype=torch.float64, device=dev)
-                cnt = torch.zeros(1, dtype=torch.int32, device=dev)
-                self.ctx.knn_pp_async(self.grid, x, y, self.q[0], self.q[1], self.r, k, oi, od, cnt)
-                self.panes.append((len(x), oi, od))
-                mi, md = self._merge()
+                slot = self.count % self.p
+                self.ctx.knn_pp_async(self.grid, x, y, self.q[0], self.q[1], self.r, self.k, self.ring_i[slot],
+                                      self.ring_d[slot], self.cnt[0:1])
+                self.count += 1
+                self.sizes.append(len(x))
+                n = len(self.sizes)
+                order = tuple((self.count - n + j) % self.p for j in range(n))  # oldest first
+                offs = [0]
+                for size in list(self.sizes)[:-1]:
+                    offs.append(offs[-1] + size)
+                key = (order, tuple(offs))
+                if key not in self._offs:
+                    self._offs[key] = (torch.tensor(order, dtype=torch.int64, device=x.device),
+                                       torch.tensor(offs, dtype=torch.int32, device=x.device).view(-1, 1))
+                oidx, otens = self._offs[key]
+                li = self.ring_i.index_select(0, oidx)
+                wi = torch.where(li >= 0, li + otens, li)
+                wd = self.ring_d.index_select(0, oidx)
+                self.ctx.knn_merge_async(wd, wi, n, self.k, self.k, self.mi, self.md, self.cnt[1:2])
         finally:
             self.ctx.set_stream(prev)
         caller.wait_stream(self.stream)
-        n = int((mi != -1).sum().item())
-        return mi[:n], md[:n]
-
-    def _merge(self):
-        import torch
-        k, p = self.k, len(self.panes)
-        dev = self.panes[0][1].device
-        all_i = torch.empty((p, k), dtype=torch.int32, device=dev)
-        all_d = torch.empty((p, k), dtype=torch.float64, device=dev)
-        off = 0
-        for j, (size, oi, od) in enumerate(self.panes):
-            li = oi.to(torch.int64)
-            all_i[j] = torch.where(li >= 0, li + off, torch.full_like(li, -1)).to(torch.int32)
-            all_d[j] = od
-            off += size
-        mi = torch.empty(k, dtype=torch.int32, device=dev)
-        md = torch.empty(k, dtype=torch.float64, device=dev)
-        cnt = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.ctx.knn_merge_async(all_d, all_i, p, k, k, mi, md, cnt)
-        return mi, md
+        if not sync:
+            return self.mi, self.md
+        m = int((self.mi != -1).sum().item())
+        return self.mi[:m].clone(), self.md[:m].clone()
 
 
 def run_incremental_range(ctx, grid, panes, qx, qy, r, approximate=False, window_size=10, slide_step=5):

@@ -77,3 +77,22 @@ def test_query_incremental_operator(ctx):
         wx = np.concatenate([w[0] for w in win])
         wy = np.concatenate([w[1] for w in win])
         assert np.asarray(got).tolist() == np.sort(cref.range_pp(cg, wx, wy, Q[0], Q[1], 0.5)).tolist()
+
+
+def test_incremental_ppoly_equals_full_window(ctx):
+    import torch
+    from helpers import pairs_sorted
+    from spatialflink_amd.incremental import IncrementalPPolyRange
+    l = (BJ[1] - BJ[0]) / 500
+    ag, cg = _abi.make_grid(BJ[0], BJ[2], l, 500), cref.grid(BJ[0], BJ[2], l, 500)
+    off, vx, vy = synth.star_polygons(40, 77)
+    panes = pane_stream(14)
+    inc = IncrementalPPolyRange(ctx, ag, off, vx, vy, 0.01, False, 2)
+    for j, (x, y) in enumerate(panes):
+        got = inc.push(torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda())
+        got = np.concatenate([g.cpu().numpy().astype(np.int64).reshape(-1, 2) for g in got])
+        win = panes[max(0, j - 1):j + 1]
+        wx = np.concatenate([w[0] for w in win])
+        wy = np.concatenate([w[1] for w in win])
+        want = cref.range_ppoly(cg, wx, wy, off, vx, vy, 0.01)
+        assert pairs_sorted(got).tolist() == pairs_sorted(want).tolist()

@@ -169,3 +169,39 @@ def test_full_size_property(ctx):
     cut = int(np.searchsorted(np.cumsum(text == 10), 200_000)) + 1
     want = cref.ingest(cref.ingest_spec(cref.CSV, ",", 2, 3, 1), text[:cut].tobytes(), cg)
     assert np.array_equal(got["cell"].cpu().numpy()[:200_000].view(np.uint32), want["cell"])
+
+
+def test_csv_fast_path_shapes(ctx):
+    """Records on and just off the device's CSV fast path (no blanks/quotes, '-'? digits
+    ('.' digits)? numbers, <= 19 significant digits, <= 18 timestamp digits) against the oracle:
+    both paths must agree bit-for-bit, and every rejected shape must still parse or reject as the
+    general grammar does."""
+    rng = random.Random(11)
+    shapes = ["{x:.6f}", "-{x:.3f}", "00{x:.9f}", "{x:.16f}", "{x:.18f}", "{x:.20f}", "{i}", "-0", "0.000{i}",
+              "{x:.6f}.", ".5", "1e3", "+{x:.6f}", "{x:.6f}d", "-", ""]
+    lines = []
+    for i in range(60000):
+        x = rng.uniform(115.4, 117.7)
+        y = rng.uniform(39.5, 41.2)
+        sx = rng.choice(shapes[:9] if rng.random() < 0.9 else shapes).format(x=x, i=i)
+        sy = rng.choice(shapes[:9]).format(x=y, i=i)
+        ts = rng.choice([str(1611022449423 + i), "-" + str(i), "0" * 17 + "1", "+5"]) if rng.random() < 0.2 \
+            else str(1611022449423 + i)
+        oid = rng.choice([str(i), "id%d" % i, "a-b.c"])
+        tail = rng.choice(["", ",extra", ",x y", ",\"q\""])
+        lines.append(f"{oid},{ts},{sx},{sy}{tail}")
+    text = "\n".join(lines).encode()
+    spec = cref.ingest_spec(cref.CSV, ",", 2, 3, 1)
+    try:
+        cref.ingest(spec, text)
+        rejected = None
+    except cref.IngestRejected as e:
+        rejected = e.bad
+    if rejected is None:
+        _check(ctx, cref.CSV, text)
+    else:
+        with pytest.raises(_abi.GeohipUnsupportedError) as d:
+            ctx.ingest_points(_abi.make_ingest_spec(cref.CSV, ",", 2, 3, 1), text)
+        assert d.value.bad == rejected
+        good = b"\n".join(l for l in text.split(b"\n") if cref.ingest_record(spec, l) is not None)
+        _check(ctx, cref.CSV, good)
