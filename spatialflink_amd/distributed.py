@@ -186,6 +186,56 @@ def ppoly_sharded(x_local, y_local, base: int, ring_off, vx, vy, r: float, appro
     return pairs, offset, total
 
 
+def join_ppoly_sharded(x_local, y_local, base: int, ring_off, vx, vy, r: float, approximate: bool = False, *,
+                       grid_points=None, grid_query=None, ctx=None, group=None,
+                       local_join: Optional[Callable] = None):
+    """Point-polygon join of one window over the group (PointPolygonJoinQuery.java:162-201):
+    the polygon stream on every rank, points by arrival; returns (pairs int64 [m, 2] =
+    (point window idx, polygon), offset, total).  Per-rank pair sets are disjoint (each point
+    lives on one rank) and their union is the window's join; only W counts are exchanged."""
+    import torch
+
+    if local_join is None:
+        local_join = _device_local_join_ppoly(ctx, grid_points, grid_query)
+    pairs = local_join(x_local, y_local, ring_off, vx, vy, r, approximate).to(torch.int64)
+    if len(pairs):
+        pairs[:, 0] += base
+    offset, total = gather_counts(len(pairs), pairs.device, group)
+    return pairs, offset, total
+
+
+def knn_ppoly_sharded(x_local, y_local, base: int, vx, vy, r: float, k: int, approximate: bool = False, *,
+                      grid=None, ctx=None, group=None, local_knn: Optional[Callable] = None,
+                      merge: Optional[Callable] = None) -> KnnResult:
+    """Point-polygon kNN of one window over the group (PointPolygonKNNQuery.java:162-236 with the
+    windowAll merge of KNNQuery.java:204-272 replaced by one all-gather of each rank's top-k):
+    local_knn(x, y, vx, vy, r, k, approximate) -> (idx int32[k], dist f64[k]) padded with
+    idx -1 / dist all-ones bits; every rank returns the same (idx, dist), ascending."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    if local_knn is None:
+        local_knn = _device_local_knn_ppoly(ctx, grid)
+    if merge is None:
+        merge = _device_merge(ctx)
+    li, ld = local_knn(x_local, y_local, vx, vy, r, k, approximate)
+    li = li.to(torch.int64)
+    gi = torch.where(li >= 0, li + base, torch.full_like(li, -1)).to(torch.int32)
+    gd = ld.contiguous()
+    all_d = torch.empty((world, k), dtype=gd.dtype, device=gd.device)
+    all_i = torch.empty((world, k), dtype=gi.dtype, device=gi.device)
+    if world > 1:
+        dist.all_gather_into_tensor(all_d.view(-1), gd, group=group)
+        dist.all_gather_into_tensor(all_i.view(-1), gi, group=group)
+    else:
+        all_d[0] = gd
+        all_i[0] = gi
+    mi, md = merge(all_d, all_i, k)
+    count = int((mi != -1).sum().item())
+    return KnnResult(mi[:count], md[:count], count)
+
+
 def gather_counts(count: int, device, group=None):
     import torch
     import torch.distributed as dist
@@ -240,6 +290,27 @@ def _device_local_join(ctx, grid_data, grid_query):
 def _device_local_ppoly(ctx, grid):
     def f(x, y, ring_off, vx, vy, r, approximate):
         return ctx.range_ppoly(grid, x, y, ring_off, vx, vy, r, approximate).reshape(-1, 2)
+
+    return f
+
+
+def _device_local_join_ppoly(ctx, grid_points, grid_query):
+    def f(x, y, ring_off, vx, vy, r, approximate):
+        return ctx.join_ppoly(grid_points, grid_query, x, y, ring_off, vx, vy, r, approximate).reshape(-1, 2)
+
+    return f
+
+
+def _device_local_knn_ppoly(ctx, grid):
+    import torch
+
+    def f(x, y, vx, vy, r, k, approximate):
+        ii, dd = ctx.knn_ppoly(grid, x, y, vx, vy, r, k, approximate)
+        oi = torch.full((k,), -1, dtype=torch.int32, device=x.device)
+        od = torch.full((k,), -1, dtype=torch.int64, device=x.device).view(torch.float64)  # all-ones bits
+        oi[:len(ii)] = ii
+        od[:len(dd)] = dd
+        return oi, od
 
     return f
 

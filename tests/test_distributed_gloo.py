@@ -204,3 +204,90 @@ def test_sharded_join_and_ppoly_gloo(tmp_path, world):
     want = sorted(map(tuple, cref.range_ppoly(cg, x, y, off_, vx, vy, 0.01).astype(np.int64).tolist()))
     pairs, offs, sizes, tot = _union(res["ppoly"])
     assert sorted(pairs) == want and tot == {len(want)}
+
+
+def _ppx_worker(rank, world, port, out_path):
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "oracle"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import cref
+    from spatialflink_amd import distributed as D
+    from spatialflink_amd import synth
+
+    bj = synth.BEIJING
+    cu = cref.grid(bj[0], bj[2], (bj[1] - bj[0]) / 200, 200)
+    cq = cref.grid(bj[0], bj[2], (bj[1] - bj[0]) / 500, 500)
+    n_total = 80_001
+    x, y = synth.uniform(n_total, 31)
+    off_, vx, vy = synth.star_polygons(10, 32)
+    lo, hi = D.shard_bounds(n_total, world, rank)
+    xl, yl = torch.from_numpy(x[lo:hi].copy()), torch.from_numpy(y[lo:hi].copy())
+
+    def local_join(xs, ys, ro, pvx, pvy, rr, approximate):
+        p = cref.join_ppoly(cu, cq, xs.numpy(), ys.numpy(), ro, pvx, pvy, rr, approximate)
+        return torch.from_numpy(p.astype(np.int64)).reshape(-1, 2)
+
+    pairs, off, total = D.join_ppoly_sharded(xl, yl, lo, off_, vx, vy, 0.02, local_join=local_join)
+    got = [None] * world
+    dist.all_gather_object(got, (rank, pairs.numpy().tolist(), off, total))
+
+    def local_knn(xs, ys, pvx, pvy, rr, k, approximate):
+        oi, od = cref.knn_ppoly(cu, xs.numpy(), ys.numpy(), pvx, pvy, rr, k, approximate)
+        ti = torch.full((k,), -1, dtype=torch.int32)
+        td = _sentinel_d(k)
+        ti[:len(oi)] = torch.from_numpy(oi.astype(np.int64)).to(torch.int32)
+        td[:len(od)] = torch.from_numpy(od)
+        return ti, td
+
+    def merge(all_d, all_i, k):
+        d = all_d.reshape(-1).view(torch.int64).numpy().astype(np.uint64)
+        i = all_i.reshape(-1).numpy().astype(np.int64) & 0xFFFFFFFF
+        keep = i != 0xFFFFFFFF
+        o = np.lexsort((i[keep], d[keep]))[:k]
+        ti = torch.full((k,), -1, dtype=torch.int32)
+        td = _sentinel_d(k)
+        ti[:len(o)] = torch.from_numpy(i[keep][o].astype(np.int32))
+        td[:len(o)] = torch.from_numpy(d[keep][o].view(np.float64))
+        return ti, td
+
+    p0 = slice(off_[0], off_[1])
+    res = D.knn_ppoly_sharded(xl, yl, lo, vx[p0], vy[p0], 0.05, 40, local_knn=local_knn, merge=merge)
+    if rank == 0:
+        import json
+        with open(out_path, "w") as f:
+            json.dump({"join": got, "knn_i": res.idx.numpy().tolist(),
+                       "knn_d": res.dist.numpy().view(np.uint64).astype(str).tolist()}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_ppoly_join_and_knn_gloo(tmp_path, world):
+    """join_ppoly_sharded (two grids; pairs (point, polygon)) and knn_ppoly_sharded over arrival
+    shards equal the unsharded oracle."""
+    import json
+
+    out = tmp_path / "ppx.json"
+    mp.spawn(_ppx_worker, args=(world, _free_port(), str(out)), nprocs=world, join=True)
+    with open(out) as f:
+        res = json.load(f)
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import cref
+    from spatialflink_amd import synth
+
+    bj = synth.BEIJING
+    cu = cref.grid(bj[0], bj[2], (bj[1] - bj[0]) / 200, 200)
+    cq = cref.grid(bj[0], bj[2], (bj[1] - bj[0]) / 500, 500)
+    x, y = synth.uniform(80_001, 31)
+    off_, vx, vy = synth.star_polygons(10, 32)
+    want = sorted(map(tuple, cref.join_ppoly(cu, cq, x, y, off_, vx, vy, 0.02).astype(np.int64).tolist()))
+    pairs, offs, sizes, tot = _union(res["join"])
+    assert sorted(pairs) == want and len(pairs) == len(set(pairs)) and tot == {len(want)}
+    assert offs == [sum(sizes[:i]) for i in range(world)]
+    p0 = slice(off_[0], off_[1])
+    wi, wd = cref.knn_ppoly(cu, x, y, vx[p0], vy[p0], 0.05, 40)
+    assert res["knn_i"] == wi.astype(np.int64).tolist()
+    assert [int(v) for v in res["knn_d"]] == wd.view(np.uint64).astype(np.int64).tolist() or \
+        np.array_equal(np.array([int(v) for v in res["knn_d"]], dtype=np.uint64), wd.view(np.uint64))

@@ -171,3 +171,33 @@ def test_knn_ppoly_large_candidate_set(ctx):
         wi, wd = cref.knn_ppoly(cg, x, y, vx, vy, 0.5, k, approx)
         assert gi.tolist() == wi.tolist()
         assert np.array_equal(gd.view(np.uint64), wd.view(np.uint64))
+
+
+def test_sharded_device_paths_world1(ctx):
+    """distributed.join_ppoly_sharded / knn_ppoly_sharded with the default device engines
+    (geohip_join_ppoly, geohip_knn_ppoly + geohip_knn_merge_async) in a 1-rank group."""
+    import socket
+    import torch
+    import torch.distributed as dist
+    from spatialflink_amd import distributed as D
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        au, cu = agrid(200)
+        aq, cq = agrid(500)
+        x, y = synth.uniform(300_000, 141)
+        off, vx, vy = synth.star_polygons(12, 142)
+        tx, ty = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+        pairs, o, total = D.join_ppoly_sharded(tx, ty, 0, off, vx, vy, 0.02, grid_points=au, grid_query=aq, ctx=ctx)
+        want = cref.join_ppoly(cu, cq, x, y, off, vx, vy, 0.02)
+        assert pairs_sorted(pairs.cpu().numpy()).tolist() == pairs_sorted(want).tolist() and total == len(want)
+        p0 = slice(off[0], off[1])
+        res = D.knn_ppoly_sharded(tx, ty, 0, vx[p0], vy[p0], 0.05, 30, grid=au, ctx=ctx)
+        wi, wd = cref.knn_ppoly(cu, x, y, vx[p0], vy[p0], 0.05, 30)
+        assert res.idx.cpu().numpy().tolist() == wi.tolist()
+        assert np.array_equal(res.dist.cpu().numpy().view(np.uint64), wd.view(np.uint64))
+    finally:
+        dist.destroy_process_group()
