@@ -829,7 +829,7 @@ __device__ __forceinline__ bool segment_within(double px, double py, double ax, 
 // min over segments of Distance.pointToSegment.  A boundary hit anywhere makes the answer true
 // whatever the other segments count, so segments are visited in any order and only those of
 // the point's slab lists; boolean-equivalent early exit on the first segment within r.
-__device__ bool point_polygon_within(double px, double py, const double* __restrict__ vx,
+__device__ __forceinline__ bool point_polygon_within(double px, double py, const double* __restrict__ vx,
                                      const double* __restrict__ vy, const PolyDev& P, const SlabView& sv, double r) {
     const int nv = (int)P.nv;
     const bool in_env = !(px > P.bb[2] || px < P.bb[0] || py > P.bb[3] || py < P.bb[1]);
@@ -894,8 +894,8 @@ __device__ __forceinline__ bool in_rects(const int32_t* __restrict__ rr, uint32_
     return false;
 }
 
-constexpr int kMaxLdsVerts = 1024;  // larger rings are read from global memory
-constexpr int kMaxLdsSlab = 4096;   // u16 slab-list entries staged in LDS
+constexpr int kMaxLdsVerts = 512;   // larger rings are read from global memory
+constexpr int kMaxLdsSlab = 2048;   // u16 slab-list entries staged in LDS
 constexpr int kMaskWords = 512;     // hit-mask words kept in LDS (tiles up to 32768 points)
 constexpr int kCandQ = 128;         // per-wave queue of points needing the exact polygon distance
 constexpr int kPolyPairs = 512;     // per-wave pair buffer of the polygon kernels
