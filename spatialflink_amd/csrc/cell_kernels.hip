@@ -1136,6 +1136,7 @@ struct RselState {
     unsigned ncand;             // candidates (scan counter)
     unsigned small_max;         // rsel_small handles ncand <= small_max
     unsigned hist[kRselBins];
+    unsigned hist0[kRselBins];  // round-0 digits (distance bits 63..52) of every key, by ppknn_dist
 };
 // digit (field, shift, width) of round t: distance bits 63..0, then index bits 31..0
 __host__ __device__ __forceinline__ void rsel_round(int t, int& field, int& shift, int& width) {
@@ -1177,13 +1178,25 @@ __device__ double point_polygon_distance(double px, double py, const double* __r
     return md;
 }
 
+// LDS histogram increment; the lanes holding the first active lane's digit add with one atomic
+// (digits concentrate: distance 0 inside the polygon, shared exponents)
+__device__ __forceinline__ void hist_add(unsigned* h, unsigned dg) {
+    const unsigned first = __builtin_amdgcn_readfirstlane(dg);
+    const unsigned long long same = __ballot(dg == first);
+    if (dg != first) atomicAdd(&h[dg], 1u);
+    else if (lanes_below(same) == 0) atomicAdd(&h[first], (unsigned)__popcll(same));
+}
+
 struct PpknnPoly {
     double bb[4];
     uint32_t nv, nrect;  // closed ring length; G rects then C rects (cell space)
 };
 
 __global__ __launch_bounds__(1024) void rsel_init(RselState* __restrict__ st, unsigned k, unsigned small_max) {
-    for (int t = threadIdx.x; t < kRselBins; t += 1024) st->hist[t] = 0;
+    for (int t = threadIdx.x; t < kRselBins; t += 1024) {
+        st->hist[t] = 0;
+        st->hist0[t] = 0;
+    }
     if (threadIdx.x == 0) {
         st->pd = 0; st->md = 0; st->pi = 0; st->mi = 0;
         st->kk = k; st->nsel = 0; st->ncand = 0; st->small_max = small_max;
@@ -1322,11 +1335,13 @@ __global__ __launch_bounds__(kTB) void ppknn_scan_boxes(const double* __restrict
 
 template <bool APPROX>
 __global__ __launch_bounds__(kTB) void ppknn_dist(const double* __restrict__ x, const double* __restrict__ y,
-                                                  const unsigned* __restrict__ cand, const RselState* __restrict__ st,
+                                                  const unsigned* __restrict__ cand, RselState* __restrict__ st,
                                                   const double* __restrict__ vx, const double* __restrict__ vy,
                                                   PpknnPoly P, unsigned long long* __restrict__ key) {
     __shared__ double lvx[kMaxLdsVerts];
     __shared__ double lvy[kMaxLdsVerts];
+    __shared__ unsigned lh[kRselBins];  // round-0 digits of this block's keys (-> st->hist0)
+    for (int t = threadIdx.x; t < kRselBins; t += kTB) lh[t] = 0;
     const bool v_lds = P.nv <= (uint32_t)kMaxLdsVerts;
     if (!APPROX && v_lds)
         for (uint32_t t = threadIdx.x; t < P.nv; t += kTB) {
@@ -1344,7 +1359,11 @@ __global__ __launch_bounds__(kTB) void ppknn_dist(const double* __restrict__ x, 
             unsigned long long bits = (unsigned long long)__double_as_longlong(d);
             if (d != d) bits = 0x7ff8000000000000ull;
             key[t] = bits;
+            hist_add(lh, (unsigned)(bits >> 52));
         }
+        __syncthreads();
+        for (int b = threadIdx.x; b < kRselBins; b += kTB)
+            if (lh[b]) atomicAdd(&st->hist0[b], lh[b]);
         return;
     }
     // exact (point_polygon_distance split over 8 lanes per candidate, each taking every 8th
@@ -1375,8 +1394,15 @@ __global__ __launch_bounds__(kTB) void ppknn_dist(const double* __restrict__ x, 
             md = od < md ? od : md;
         }
         const double d = (in_env && (boundary || (crossings & 1))) ? 0.0 : md;
-        if (sub == 0) key[t0] = (unsigned long long)__double_as_longlong(d);
+        if (sub == 0) {
+            const unsigned long long bits = (unsigned long long)__double_as_longlong(d);
+            key[t0] = bits;
+            hist_add(lh, (unsigned)(bits >> 52));
+        }
     }
+    __syncthreads();
+    for (int b = threadIdx.x; b < kRselBins; b += kTB)
+        if (lh[b]) atomicAdd(&st->hist0[b], lh[b]);
 }
 
 __device__ __forceinline__ bool rsel_match(const RselState& s, unsigned long long d, unsigned i) {
@@ -1508,6 +1534,8 @@ __global__ __launch_bounds__(1024) void rsel_small(const unsigned long long* __r
     __shared__ unsigned ci[kCompact];
     __shared__ unsigned long long s_pd, s_md;
     __shared__ unsigned s_pi, s_mi, s_kk, s_nsel, s_cnt, s_lds, s_lcnt;
+    __shared__ unsigned long long s_and_d, s_or_d;  // over the LDS keys matching the prefix
+    __shared__ unsigned s_and_i, s_or_i;
     const unsigned m = st->ncand;
     if (m > st->small_max) return;
     const unsigned t = threadIdx.x;
@@ -1543,21 +1571,69 @@ __global__ __launch_bounds__(1024) void rsel_small(const unsigned long long* __r
                 if (c0 + u * 1024 < m && (d[u] & md) == pd && (i[u] & mi) == pi) fn(d[u], i[u]);
         }
     };
+    bool pre = false;  // keys below the round-0 digit were selected outright (LDS-only rounds)
     for (int round = 0; round < kRselRounds && !all; round++) {
-        for (int b = t; b < kRselBins; b += 1024) h[b] = 0;
-        __syncthreads();
         int field, shift, width;
         rsel_round(round, field, shift, width);
         const unsigned dm = (1u << width) - 1u;
-        for_matching([&](unsigned long long d, unsigned i) {
-            // digits concentrate (distance 0 inside the polygon, shared exponents): the lanes
-            // holding the first active lane's digit add with one LDS atomic
-            const unsigned dg = field == 0 ? (unsigned)(d >> shift) & dm : (i >> shift) & dm;
-            const unsigned first = __builtin_amdgcn_readfirstlane(dg);
-            const unsigned long long same = __ballot(dg == first);
-            if (dg != first) atomicAdd(&h[dg], 1u);
-            else if (lanes_below(same) == 0) atomicAdd(&h[first], (unsigned)__popcll(same));
-        });
+        if (round > 0 && s_lds) {
+            // a round whose digit every matching key shares decides nothing: take it without a
+            // histogram (keys at distance 0 inside the polygon skip all the distance rounds)
+            if (t == 0) {
+                s_and_d = ~0ull; s_or_d = 0; s_and_i = ~0u; s_or_i = 0;
+            }
+            __syncthreads();
+            const unsigned long long md = s_md, pd = s_pd;
+            const unsigned mi = s_mi, pi = s_pi, cnt = s_lcnt;
+            unsigned long long ad = ~0ull, od = 0;
+            unsigned ai = ~0u, oi = 0;
+            for (unsigned c = t; c < cnt; c += 1024) {
+                const unsigned long long d = cd[c];
+                const unsigned i = ci[c];
+                if ((d & md) == pd && (i & mi) == pi) {
+                    ad &= d; od |= d; ai &= i; oi |= i;
+                }
+            }
+#pragma unroll
+            for (int o = 1; o < kWave; o <<= 1) {
+                ad &= xor_lane64(ad, o);
+                od |= xor_lane64(od, o);
+                ai &= xor_lane(ai, o);
+                oi |= xor_lane(oi, o);
+            }
+            if (lane_id() == 0) {
+                atomicAnd(&s_and_d, ad);
+                atomicOr(&s_or_d, od);
+                atomicAnd(&s_and_i, ai);
+                atomicOr(&s_or_i, oi);
+            }
+            __syncthreads();
+            const unsigned a = field == 0 ? (unsigned)(s_and_d >> shift) & dm : (s_and_i >> shift) & dm;
+            const unsigned b = field == 0 ? (unsigned)(s_or_d >> shift) & dm : (s_or_i >> shift) & dm;
+            __syncthreads();
+            if (a == b) {  // uniform: every thread read the same shared words
+                if (t == 0) {
+                    if (field == 0) {
+                        s_pd |= (unsigned long long)a << shift;
+                        s_md |= (unsigned long long)dm << shift;
+                    } else {
+                        s_pi |= a << shift;
+                        s_mi |= dm << shift;
+                    }
+                }
+                __syncthreads();
+                continue;
+            }
+        }
+        if (round == 0) {  // the producers' histogram (ppknn_dist) of the round-0 digits
+            for (int b = t; b < kRselBins; b += 1024) h[b] = st->hist0[b];
+        } else {
+            for (int b = t; b < kRselBins; b += 1024) h[b] = 0;
+            __syncthreads();
+            for_matching([&](unsigned long long d, unsigned i) {
+                hist_add(h, field == 0 ? (unsigned)(d >> shift) & dm : (i >> shift) & dm);
+            });
+        }
         __syncthreads();
         unsigned v[4], sum = 0;
         for (int j = 0; j < 4; j++) {
@@ -1589,6 +1665,39 @@ __global__ __launch_bounds__(1024) void rsel_small(const unsigned long long* __r
             }
         }
         __syncthreads();
+        if (round == 0 && s_cnt <= kCompact) {
+            // one pass over the list: keys below the chosen digit are among the k smallest
+            // (fewer than k of them), the digit's keys move into LDS for the later rounds
+            const unsigned d0 = (unsigned)(s_pd >> 52);
+            for (unsigned c0 = t; c0 < m; c0 += 4 * 1024) {
+                unsigned long long d[4];
+                unsigned i[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const unsigned c = c0 + u * 1024;
+                    d[u] = c < m ? key[c] : ~0ull;
+                    i[u] = c < m ? cand[c] : ~0u;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    if (c0 + u * 1024 >= m) continue;
+                    const unsigned dg = (unsigned)(d[u] >> 52);
+                    if (dg < d0) {
+                        const unsigned sl = wave_reserve(&s_nsel);
+                        sd[sl] = d[u];
+                        si[sl] = i[u];
+                    } else if (dg == d0) {
+                        const unsigned sl = wave_reserve(&s_lcnt);
+                        cd[sl] = d[u];
+                        ci[sl] = i[u];
+                    }
+                }
+            }
+            __syncthreads();
+            if (t == 0) s_lds = 1;
+            pre = true;
+            __syncthreads();
+        }
         if (!s_lds && s_cnt <= kCompact && round + 1 < kRselRounds) {  // move the survivors into LDS
             if (t == 0) s_nsel = 0;
             __syncthreads();
@@ -1610,14 +1719,29 @@ __global__ __launch_bounds__(1024) void rsel_small(const unsigned long long* __r
     // prefix plus every key below it -- taken from the full global list
     const unsigned long long kd = s_pd;
     const unsigned ki = s_pi;
-    for (unsigned c = t; c < m; c += 1024) {
-        const unsigned long long d = key[c];
-        const unsigned i = cand[c];
-        if (all || d < kd || (d == kd && i <= ki)) {
-            const unsigned sl = wave_reserve(&s_nsel);
-            if (sl < 256) {
-                sd[sl] = d;
-                si[sl] = i;
+    if (pre) {  // the rest of the k smallest: the LDS copy's keys up to the k-th
+        const unsigned cnt = s_lcnt;
+        for (unsigned c = t; c < cnt; c += 1024) {
+            const unsigned long long d = cd[c];
+            const unsigned i = ci[c];
+            if (d < kd || (d == kd && i <= ki)) {
+                const unsigned sl = wave_reserve(&s_nsel);
+                if (sl < 256) {
+                    sd[sl] = d;
+                    si[sl] = i;
+                }
+            }
+        }
+    } else {
+        for (unsigned c = t; c < m; c += 1024) {
+            const unsigned long long d = key[c];
+            const unsigned i = cand[c];
+            if (all || d < kd || (d == kd && i <= ki)) {
+                const unsigned sl = wave_reserve(&s_nsel);
+                if (sl < 256) {
+                    sd[sl] = d;
+                    si[sl] = i;
+                }
             }
         }
     }
