@@ -838,8 +838,18 @@ __device__ __forceinline__ bool point_polygon_within(double px, double py, const
         bool boundary = false;
         int crossings = 0;
         if (sv.ns) {
+            // two segments per step: both ids, then all eight coordinates, in flight together
+            // (crossing counts add and boundary flags OR: order-independent)
             const uint32_t k1 = sv.cbeg(s + 1);
-            for (uint32_t k = sv.cbeg(s); k < k1; k++) {
+            uint32_t k = sv.cbeg(s);
+            for (; k + 2 <= k1; k += 2) {
+                const uint32_t e0 = sv.id(k), e1 = sv.id(k + 1);
+                const double p0x = vx[e0 + 1], p0y = vy[e0 + 1], q0x = vx[e0], q0y = vy[e0];
+                const double p1x = vx[e1 + 1], p1y = vy[e1 + 1], q1x = vx[e1], q1y = vy[e1];
+                count_segment(px, py, p0x, p0y, q0x, q0y, boundary, crossings);
+                count_segment(px, py, p1x, p1y, q1x, q1y, boundary, crossings);
+            }
+            if (k < k1) {
                 const uint32_t e = sv.id(k);
                 count_segment(px, py, vx[e + 1], vy[e + 1], vx[e], vy[e], boundary, crossings);
             }
@@ -851,7 +861,16 @@ __device__ __forceinline__ bool point_polygon_within(double px, double py, const
     const double lim2 = screen_lim2(px, py, P.bb, r);
     if (sv.ns && lim2 <= P.E * P.E) {
         const uint32_t k1 = sv.dbeg(s + 1);
-        for (uint32_t k = sv.dbeg(s); k < k1; k++) {
+        uint32_t k = sv.dbeg(s);
+        for (; k + 2 <= k1; k += 2) {  // "any segment within r": pairs, same answer
+            const uint32_t e0 = sv.id(k), e1 = sv.id(k + 1);
+            const double a0x = vx[e0], a0y = vy[e0], b0x = vx[e0 + 1], b0y = vy[e0 + 1];
+            const double a1x = vx[e1], a1y = vy[e1], b1x = vx[e1 + 1], b1y = vy[e1 + 1];
+            if (segment_within(px, py, a0x, a0y, b0x, b0y, r, lim2) ||
+                segment_within(px, py, a1x, a1y, b1x, b1y, r, lim2))
+                return true;
+        }
+        if (k < k1) {
             const uint32_t e = sv.id(k);
             if (segment_within(px, py, vx[e], vy[e], vx[e + 1], vy[e + 1], r, lim2)) return true;
         }
