@@ -162,7 +162,7 @@ struct LdsReader {
 // One pass, 32-bit offsets and few branches per byte: the general parser is SALU-bound on
 // divergent per-byte control flow.
 __device__ __forceinline__ int fast_csv(const uint8_t* __restrict__ s, uint32_t p, uint32_t lim,
-                                        const ingest::Spec& sp, ingest::Parsed* o) {
+                                        const ingest::Spec& sp, ingest::Parsed* o, int ablate = 0) {
     const uint8_t d = (uint8_t)sp.delim;
     int need = sp.fx > sp.fy ? sp.fx : sp.fy;
     if (sp.fts > need) need = sp.fts;
@@ -200,7 +200,8 @@ __device__ __forceinline__ int fast_csv(const uint8_t* __restrict__ s, uint32_t 
                 // Long.valueOf of the (<= 18 digit) run: w holds it exactly (leading zeros skipped)
                 o->ts = neg ? -(int64_t)w : (int64_t)w;
             } else {
-                const uint64_t bits = ingest::decimal_to_bits(w, q) | (neg ? 1ull << 63 : 0ull);
+                const uint64_t bits = (ablate == 2 ? __builtin_bit_cast(uint64_t, (double)w)
+                                                   : ingest::decimal_to_bits(w, q)) | (neg ? 1ull << 63 : 0ull);
                 const double v = __builtin_bit_cast(double, bits);
                 if (isx) o->x = v;
                 if (isy) o->y = v;
@@ -261,9 +262,15 @@ __global__ __launch_bounds__(kThreads) void ingest_parse(const uint8_t* __restri
         const uint64_t idx = rbase + i;
         ingest::Parsed o;
         o.ts = 0;
-        int rc = fast ? fast_csv(reinterpret_cast<const uint8_t*>(s_text4), s_start[i], stage_len, a.spec, &o)
+        int rc;
+        if (a.pad == 1) {
+            o.x = o.y = (double)s_start[i];
+            rc = ingest::kOk;
+        } else {
+            rc = fast ? fast_csv(reinterpret_cast<const uint8_t*>(s_text4), s_start[i], stage_len, a.spec, &o, a.pad)
                       : ingest::kFallback;
-        if (rc != ingest::kOk) rc = ingest::parse_record(rd, c0 + s_start[i], a.spec, &o);
+            if (rc != ingest::kOk) rc = ingest::parse_record(rd, c0 + s_start[i], a.spec, &o);
+        }
         if (rc != ingest::kOk) {
             atomicMin(bad, (unsigned long long)idx);
             continue;
@@ -272,7 +279,9 @@ __global__ __launch_bounds__(kThreads) void ingest_parse(const uint8_t* __restri
         x[idx] = o.x;
         y[idx] = o.y;
         if (ts) ts[idx] = o.ts;
-        if (cell) {
+        if (cell && a.pad == 3) {
+            cell[idx] = 0u;
+        } else if (cell) {
             const int32_t cx = ingest::java_cell(o.x, a.min_x, a.cell_len);
             const int32_t cy = ingest::java_cell(o.y, a.min_y, a.cell_len);
             const bool ok = cx >= 0 && cx < a.n && cy >= 0 && cy < a.n;

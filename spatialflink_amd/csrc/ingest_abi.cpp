@@ -10,6 +10,7 @@
 
 #include "geohip_internal.h"
 #include "ingest.h"
+#include <cstdlib>
 #include "join.h"
 
 using namespace geohip;
@@ -81,6 +82,10 @@ int geohip_ingest_points(geohip_ctx* ctx, const geohip_grid* grid, const geohip_
         a.cell_len = grid->cell_len;
         a.n = grid->n;
     }
+    // measurement hook (never set in production): 1 = stage + store only, 2 = no Eisel-Lemire,
+    // 3 = no cell division (results are wrong in modes 1-3)
+    static const int ablate = getenv("GEOHIP_INGEST_ABLATE") ? atoi(getenv("GEOHIP_INGEST_ABLATE")) : 0;
+    a.pad = ablate;
     if (nbytes >= (1ull << 40)) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "batch larger than 1 TiB");
     const uint64_t nchunks = ingest_chunks(nbytes);
     if (nchunks >= (1ull << 31)) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "batch too large");
