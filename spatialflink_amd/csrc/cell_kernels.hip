@@ -517,25 +517,30 @@ __device__ __forceinline__ bool rect_tiles(const QRect& R, const TileGeom& g, in
 
 // Query replication as a tile -> query list.  FILL = 0: count per tile (and collect the
 // queries whose block spans more than kGlobalTiles tiles into glist); FILL = 1: write lists.
+// One wave per query, its lanes over the query's tiles: the tile atomics of one query are
+// issued together instead of as one thread's serial chain.
 template <bool FILL>
-__global__ void jq_build(const QRect* __restrict__ rect, uint64_t nq, TileGeom g, unsigned* __restrict__ tcnt,
-                         const unsigned* __restrict__ qstart, unsigned* __restrict__ qlist,
-                         unsigned* __restrict__ glist, unsigned* __restrict__ gcnt) {
-    const uint64_t q = (uint64_t)blockIdx.x * kTB + threadIdx.x;
-    if (q >= nq) return;
+__global__ __launch_bounds__(kTB) void jq_build(const QRect* __restrict__ rect, uint64_t nq, TileGeom g,
+                                                unsigned* __restrict__ tcnt, const unsigned* __restrict__ qstart,
+                                                unsigned* __restrict__ qlist, unsigned* __restrict__ glist,
+                                                unsigned* __restrict__ gcnt) {
+    const uint64_t q = (uint64_t)blockIdx.x * (kTB / kWave) + threadIdx.x / kWave;
+    if (q >= nq) return;  // wave-uniform
+    const unsigned lane = (unsigned)lane_id();
     int32_t tx0, tx1, ty0, ty1;
     if (!rect_tiles(rect[q], g, tx0, tx1, ty0, ty1)) return;
-    const uint64_t ntl = (uint64_t)(tx1 - tx0 + 1) * (uint64_t)(ty1 - ty0 + 1);
+    const unsigned ny = (unsigned)(ty1 - ty0 + 1);
+    const uint64_t ntl = (uint64_t)(tx1 - tx0 + 1) * ny;
     if (ntl > kGlobalTiles) {
-        if (!FILL) glist[atomicAdd(gcnt, 1u)] = (unsigned)q;
+        if (!FILL && lane == 0) glist[atomicAdd(gcnt, 1u)] = (unsigned)q;
         return;
     }
-    for (int32_t a = tx0; a <= tx1; a++)
-        for (int32_t b = ty0; b <= ty1; b++) {
-            const unsigned t = (unsigned)a * (unsigned)g.nt + (unsigned)b;
-            const unsigned k = atomicAdd(&tcnt[t], 1u);
-            if (FILL) qlist[qstart[t] + k] = (unsigned)q;
-        }
+    for (unsigned l = lane; l < (unsigned)ntl; l += kWave) {
+        const unsigned a = (unsigned)tx0 + l / ny, b = (unsigned)ty0 + l % ny;
+        const unsigned t = a * (unsigned)g.nt + b;
+        const unsigned k = atomicAdd(&tcnt[t], 1u);
+        if (FILL) qlist[qstart[t] + k] = (unsigned)q;
+    }
 }
 
 // One workgroup per data tile: candidate queries (the tile's list + the global list) staged in
@@ -2123,7 +2128,7 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
         return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "rect upload failed");
     if (hipMemsetAsync(qcnt, 0, ((uint64_t)geo.ntiles + 1) * 4, st) != hipSuccess)
         return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
-    const unsigned qg = (unsigned)((nq + kTB - 1) / kTB);
+    const unsigned qg = (unsigned)((nq + kTB / kWave - 1) / (kTB / kWave));  // one wave per query
     if (nq) jq_build<false><<<qg, kTB, 0, st>>>(drect, nq, geo, qcnt, nullptr, nullptr, glist, misc + 3);
     scan_launch<unsigned>(st, qcnt, geo.ntiles, seg, misc + 2, qstart);
     if (hipMemsetAsync(qcnt, 0, ((uint64_t)geo.ntiles + 1) * 4, st) != hipSuccess)
