@@ -189,17 +189,18 @@ class KnnWorkload(Workload):
         from spatialflink_amd import synth
         bj, q = synth.BEIJING, synth.README_QUERY
         cg = cref.grid(bj[0], bj[2], (bj[1] - bj[0]) / self.grid_n, self.grid_n)
-        n = 2_000_000
+        n = self.n
+        x, y = synth.uniform(n, self.seed0)  # the benchmarked window itself
 
         def one(i):
-            x, y = synth.uniform(n, 1000 + i)
             t0 = time.perf_counter()
             cref.knn_pp(cg, x, y, q[0], q[1], self.radius, self.k)
             return time.perf_counter() - t0
-        wins, t = _timed_loop(one, seconds, 30)
-        return {"value": wins * n / t, "unit": "points/sec", "cores": 1, "kind": "port",
-                "sample": f"{wins} windows x {n} uniform points (C2 shape: k={self.k}, {self.grid_n}x{self.grid_n}, "
-                          f"r={self.radius}), oracle/geohip_oracle.c single thread, {t:.1f} s"}
+        wins, t = _timed_loop(one, seconds, 1000)
+        return {"value": wins * n / t, "unit": "points/sec", "cores": cref.threads(), "kind": "port",
+                "sample": f"{wins} windows x {n} uniform points (k={self.k}, {self.grid_n}x{self.grid_n}, "
+                          f"r={self.radius}), oracle/geohip_oracle.c, OpenMP {cref.threads()} threads "
+                          f"(points of a window in parallel, per-thread heaps merged), {t:.1f} s"}
 
 
 class RangeWorkload(Workload):
@@ -252,16 +253,16 @@ class RangeWorkload(Workload):
         bj, q = synth.BEIJING, synth.README_QUERY
         cg = cref.grid(bj[0], bj[2], (bj[1] - bj[0]) / self.grid_n, self.grid_n)
         n = 1_000_000  # C1's own window size
+        x, y = synth.uniform(n, 1)
 
         def one(i):
-            x, y = synth.uniform(n, 1000 + i)
             t0 = time.perf_counter()
             cref.range_pp(cg, x, y, q[0], q[1], self.radius)
             return time.perf_counter() - t0
-        wins, t = _timed_loop(one, seconds, 60)
-        return {"value": wins * n / t, "unit": "points/sec", "cores": 1, "kind": "port",
+        wins, t = _timed_loop(one, seconds, 5000)
+        return {"value": wins * n / t, "unit": "points/sec", "cores": cref.threads(), "kind": "port",
                 "sample": f"{wins} windows x {n} uniform points (C1: 100x100, r={self.radius}), "
-                          f"oracle/geohip_oracle.c single thread, {t:.1f} s"}
+                          f"oracle/geohip_oracle.c, OpenMP {cref.threads()} threads, {t:.1f} s"}
 
 
 class JoinWorkload(Workload):
@@ -318,18 +319,18 @@ class JoinWorkload(Workload):
         from spatialflink_amd import synth
         bj = synth.BEIJING
         cg = cref.grid(bj[0], bj[2], (bj[1] - bj[0]) / self.grid_n, self.grid_n)
-        n = 1_000_000  # data slice; all queries (the per-pair work scales with the data slice)
+        n = 2_000_000  # data slice of the C3 window; all 10k queries
         qx, qy = synth.gaussian_clusters(self.nq, 4, sigma=self.sigma)
+        x, y = synth.gaussian_clusters(n, 3, sigma=self.sigma)
 
         def one(i):
-            x, y = synth.gaussian_clusters(n, 3000 + i, sigma=self.sigma)
             t0 = time.perf_counter()
-            cref.join_pp(cg, cg, x, y, qx, qy, self.radius, cap=80_000_000)  # one pass, as the reference
+            cref.join_pp_hash(cg, cg, x, y, qx, qy, self.radius)  # one pass, as the reference
             return time.perf_counter() - t0
-        wins, t = _timed_loop(one, seconds, 20)
-        return {"value": wins * n / t, "unit": "points/sec", "cores": 1, "kind": "port",
-                "sample": f"{wins} x ({n} Gaussian data points x {self.nq} queries) (C3 shape), "
-                          f"oracle/geohip_oracle.c single thread, {t:.1f} s"}
+        wins, t = _timed_loop(one, seconds, 200)
+        return {"value": wins * n / t, "unit": "points/sec", "cores": cref.threads(), "kind": "port",
+                "sample": f"{wins} x ({n} Gaussian data points x {self.nq} queries) (C3 shape, pairs counted and "
+                          f"hashed, not stored), oracle/geohip_oracle.c, OpenMP {cref.threads()} threads, {t:.1f} s"}
 
 
 class PpolyWorkload(Workload):
@@ -377,23 +378,18 @@ class PpolyWorkload(Workload):
         from spatialflink_amd import synth
         bj = synth.BEIJING
         cg = cref.grid(bj[0], bj[2], (bj[1] - bj[0]) / self.grid_n, self.grid_n)
-        n, npoly = 2_000_000, 10  # the reference scans the window once per polygon query
+        n = 5_000_000  # a 5M-point slice of the C4 window, all 1k polygons
+        x, y = synth.uniform(n, 5)
 
         def one(i):
-            x, y = synth.uniform(n, 5000 + i)
-            sl = slice(10 * i % self.npoly, 10 * i % self.npoly + npoly + 1)
-            off = self.off[sl] - self.off[sl][0]
-            vx = self.vx[self.off[sl][0]:self.off[sl][-1]]
-            vy = self.vy[self.off[sl][0]:self.off[sl][-1]]
             t0 = time.perf_counter()
-            cref.range_ppoly(cg, x, y, off, vx, vy, self.radius)
+            cref.range_ppoly_hash(cg, x, y, self.off, self.vx, self.vy, self.radius)
             return time.perf_counter() - t0
-        reps, t = _timed_loop(one, seconds, 50)
-        # point x polygon evaluations per second, expressed as windows of n points x 1k polygons
-        pp_rate = reps * n * npoly / t
-        return {"value": pp_rate / self.npoly, "unit": "points/sec", "cores": 1, "kind": "port",
-                "sample": f"{reps} x ({n} uniform points x {npoly} polygons) (C4 shape), oracle/geohip_oracle.c single "
-                          f"thread, {t:.1f} s; value = point-polygon evaluations/s / {self.npoly} polygons"}
+        reps, t = _timed_loop(one, seconds, 200)
+        return {"value": reps * n / t, "unit": "points/sec", "cores": cref.threads(), "kind": "port",
+                "sample": f"{reps} x ({n} uniform points x {self.npoly} polygons) (C4 shape), oracle/geohip_oracle.c "
+                          f"(polygons in parallel over OpenMP {cref.threads()} threads, each visiting its G u C "
+                          f"cells), {t:.1f} s"}
 
 
 class PpJoinWorkload(PpolyWorkload):
@@ -434,22 +430,17 @@ class PpJoinWorkload(PpolyWorkload):
         from spatialflink_amd import synth
         bj = synth.BEIJING
         cg = cref.grid(bj[0], bj[2], (bj[1] - bj[0]) / self.grid_n, self.grid_n)
-        n, npoly = 2_000_000, 10
+        n = 5_000_000
+        x, y = synth.uniform(n, 5)
 
         def one(i):
-            x, y = synth.uniform(n, 5000 + i)
-            sl = slice(10 * i % self.npoly, 10 * i % self.npoly + npoly + 1)
-            off = self.off[sl] - self.off[sl][0]
-            vx = self.vx[self.off[sl][0]:self.off[sl][-1]]
-            vy = self.vy[self.off[sl][0]:self.off[sl][-1]]
             t0 = time.perf_counter()
-            cref.join_ppoly(cg, cg, x, y, off, vx, vy, self.radius)
+            cref.join_ppoly_hash(cg, cg, x, y, self.off, self.vx, self.vy, self.radius)
             return time.perf_counter() - t0
-        reps, t = _timed_loop(one, seconds, 50)
-        pp_rate = reps * n * npoly / t
-        return {"value": pp_rate / self.npoly, "unit": "points/sec", "cores": 1, "kind": "port",
-                "sample": f"{reps} x ({n} uniform points x {npoly} polygons), oracle/geohip_oracle.c join_ppoly single "
-                          f"thread, {t:.1f} s; value = point-polygon evaluations/s / {self.npoly} polygons"}
+        reps, t = _timed_loop(one, seconds, 200)
+        return {"value": reps * n / t, "unit": "points/sec", "cores": cref.threads(), "kind": "port",
+                "sample": f"{reps} x ({n} uniform points x {self.npoly} polygons), oracle/geohip_oracle.c join_ppoly, "
+                          f"OpenMP {cref.threads()} threads, {t:.1f} s"}
 
 
 class PpKnnWorkload(Workload):
@@ -493,17 +484,17 @@ class PpKnnWorkload(Workload):
         from spatialflink_amd import synth
         bj = synth.BEIJING
         cg = cref.grid(bj[0], bj[2], (bj[1] - bj[0]) / self.grid_n, self.grid_n)
-        n = 5_000_000
+        n = 10_000_000
+        x, y = synth.uniform(n, 5)
 
         def one(i):
-            x, y = synth.uniform(n, 6000 + i)
             t0 = time.perf_counter()
             cref.knn_ppoly(cg, x, y, self.vx, self.vy, self.radius, self.k)
             return time.perf_counter() - t0
-        reps, t = _timed_loop(one, seconds, 20)
-        return {"value": reps * n / t, "unit": "points/sec", "cores": 1, "kind": "port",
+        reps, t = _timed_loop(one, seconds, 500)
+        return {"value": reps * n / t, "unit": "points/sec", "cores": cref.threads(), "kind": "port",
                 "sample": f"{reps} windows x {n} uniform points (same polygon, k, grid, r), oracle/geohip_oracle.c "
-                          f"knn_ppoly single thread, {t:.1f} s"}
+                          f"knn_ppoly, OpenMP {cref.threads()} threads, {t:.1f} s"}
 
 
 class PpolyIncrWorkload(PpolyWorkload):
@@ -597,7 +588,23 @@ class C5Workload(KnnWorkload):
         return c
 
     def cpu_baseline(self, seconds):
-        return None
+        cref = _oracle()
+        from spatialflink_amd import synth
+        bj, q = synth.BEIJING, synth.README_QUERY
+        cg = cref.grid(bj[0], bj[2], (bj[1] - bj[0]) / self.grid_n, self.grid_n)
+        n = self.n
+        x, y = synth.uniform(n, self.seed0)  # rank 0's shard of the C5 window
+
+        def one(i):
+            t0 = time.perf_counter()
+            cref.knn_pp(cg, x, y, q[0], q[1], self.radius, self.k)
+            cref.range_pp_hash(cg, x, y, q[0], q[1], self.radius)
+            return time.perf_counter() - t0
+        wins, t = _timed_loop(one, seconds, 1000)
+        return {"value": wins * n / t, "unit": "points/sec", "cores": cref.threads(), "kind": "port",
+                "sample": f"{wins} x one {n}-point C5 shard (kNN k={self.k} + range r={self.radius}, "
+                          f"{self.grid_n}x{self.grid_n}), oracle/geohip_oracle.c, OpenMP {cref.threads()} threads, "
+                          f"{t:.1f} s"}
 
 
 class IngestWorkload(Workload):
@@ -689,7 +696,7 @@ def main():
     ctx = Context(local)
     _abi.debug_set_knn_fused(args.knn_final == "fused")
     stream = torch.cuda.current_stream(dev)
-    ctx.set_stream(stream.cuda_stream)  # kernels and RCCL ordered on one stream
+    ctx.set_stream(stream.cuda_stream)  # kernels and RCCL ordered on one stream (0 = the null stream)
     wl = WORKLOADS[args.workload](args, ctx, dev, rank, world, dist)
 
     torch.cuda.synchronize(dev)

@@ -94,8 +94,12 @@ int geohip_ctx_create(uint32_t device_mask, geohip_ctx** out_ctx);
 int geohip_ctx_destroy(geohip_ctx* ctx);
 const char* geohip_last_error(const geohip_ctx* ctx);
 int geohip_ctx_set_mem(geohip_ctx* ctx, int mem_kind);
-/* Use the caller's hipStream_t (NULL = the ctx's own stream). */
+/* Enqueue on the caller's hipStream_t from now on (NULL = the HIP null stream, e.g. PyTorch's
+   default stream): work the caller queued on that stream before a call is ordered before the
+   call's kernels, and the *_async results are ordered before later work on it. */
 int geohip_ctx_set_stream(geohip_ctx* ctx, void* hip_stream);
+/* Back to the ctx's own (non-blocking) stream, the state after geohip_ctx_create. */
+int geohip_ctx_reset_stream(geohip_ctx* ctx);
 void* geohip_ctx_stream(geohip_ctx* ctx);
 /* Per-launch HIP-event timing of each query's dominant kernel (the scan kernel). */
 int geohip_ctx_set_timing(geohip_ctx* ctx, int enable);

@@ -42,22 +42,31 @@ def _load():
         "geohip_oracle_key_roundtrip": (c_int, [c_int32, c_int32, POINTER(c_int32), POINTER(c_int32)]),
         "geohip_oracle_key_matches": (c_int, [c_int32, c_int32, c_void_p, c_int]),
         "geohip_oracle_range_pp": (c_int64, [POINTER(Grid), c_void_p, c_void_p, c_uint64, c_double, c_double,
-                                             c_double, c_int, c_void_p, c_uint64]),
+                                             c_double, c_int, c_void_p, c_uint64, POINTER(c_uint64)]),
         "geohip_oracle_knn_pp": (c_int, [POINTER(Grid), c_void_p, c_void_p, c_uint64, c_double, c_double, c_double,
                                          c_uint32, c_void_p, c_void_p, POINTER(c_uint32)]),
         "geohip_oracle_join_pp": (c_int64, [POINTER(Grid), POINTER(Grid), c_void_p, c_void_p, c_uint64, c_void_p,
-                                            c_void_p, c_uint64, c_double, c_int, c_void_p, c_uint64]),
+                                            c_void_p, c_uint64, c_double, c_int, c_void_p, c_uint64,
+                                            POINTER(c_uint64)]),
         "geohip_oracle_ingest_record": (c_int, [POINTER(IngestSpec), POINTER(Grid), ctypes.c_char_p, c_uint64,
                                                 POINTER(c_double), POINTER(c_double), POINTER(c_int64),
                                                 POINTER(c_uint32)]),
         "geohip_oracle_ingest": (c_int64, [POINTER(IngestSpec), POINTER(Grid), c_void_p, c_uint64, c_void_p,
                                            c_void_p, c_void_p, c_void_p, c_uint64]),
         "geohip_oracle_range_ppoly": (c_int64, [POINTER(Grid), c_void_p, c_void_p, c_uint64, c_void_p, c_void_p,
-                                                c_void_p, c_uint32, c_double, c_int, c_void_p, c_uint64]),
+                                                c_void_p, c_void_p, c_uint32, c_double, c_int, c_void_p, c_uint64,
+                                                POINTER(c_uint64)]),
         "geohip_oracle_join_ppoly": (c_int64, [POINTER(Grid), POINTER(Grid), c_void_p, c_void_p, c_uint64, c_void_p,
-                                               c_void_p, c_void_p, c_uint32, c_double, c_int, c_void_p, c_uint64]),
-        "geohip_oracle_knn_ppoly": (c_int, [POINTER(Grid), c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32,
-                                            c_double, c_uint32, c_int, c_void_p, c_void_p, POINTER(c_uint32)]),
+                                               c_void_p, c_void_p, c_void_p, c_uint32, c_double, c_int, c_void_p,
+                                               c_uint64, POINTER(c_uint64)]),
+        "geohip_oracle_knn_ppoly": (c_int, [POINTER(Grid), c_void_p, c_void_p, c_uint64, c_void_p, c_uint32, c_void_p,
+                                            c_void_p, c_double, c_uint32, c_int, c_void_p, c_void_p,
+                                            POINTER(c_uint32)]),
+        "geohip_oracle_point_polygon_rings": (c_double, [c_double, c_double, c_void_p, c_uint32, c_void_p, c_void_p,
+                                                         POINTER(c_int)]),
+        "geohip_oracle_set_threads": (None, [c_int]),
+        "geohip_oracle_threads": (c_int, []),
+        "geohip_oracle_mix64": (c_uint64, [c_uint64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -99,10 +108,23 @@ def range_pp(g: Grid, x, y, qx, qy, r, approximate=False) -> np.ndarray:
     x = np.ascontiguousarray(x, np.float64)
     y = np.ascontiguousarray(y, np.float64)
     out = np.empty(max(len(x), 1), np.uint32)
-    c = lib.geohip_oracle_range_pp(ctypes.byref(g), _p(x), _p(y), len(x), qx, qy, r, int(approximate), _p(out), len(out))
+    c = lib.geohip_oracle_range_pp(ctypes.byref(g), _p(x), _p(y), len(x), qx, qy, r, int(approximate), _p(out), len(out),
+                                   None)
     if c < 0:
         raise OracleError(f"oracle range_pp error {c}")
     return out[:c].copy()
+
+
+def range_pp_hash(g: Grid, x, y, qx, qy, r, approximate=False):
+    """(hit count, sum of mix64(idx) mod 2^64) without materialising the hits."""
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    h = c_uint64(0)
+    c = lib.geohip_oracle_range_pp(ctypes.byref(g), _p(x), _p(y), len(x), qx, qy, r, int(approximate), None, 0,
+                                   ctypes.byref(h))
+    if c < 0:
+        raise OracleError(f"oracle range_pp error {c}")
+    return c, h.value
 
 
 def knn_pp(g: Grid, x, y, qx, qy, r, k):
@@ -125,74 +147,133 @@ def join_pp(gd: Grid, gq: Grid, dx, dy, qx, qy, r, approximate=False, cap=None) 
     qy = np.ascontiguousarray(qy, np.float64)
     if cap is None:
         c = lib.geohip_oracle_join_pp(ctypes.byref(gd), ctypes.byref(gq), _p(dx), _p(dy), len(dx), _p(qx), _p(qy),
-                                      len(qx), r, int(approximate), None, 0)
+                                      len(qx), r, int(approximate), None, 0, None)
         if c < 0:
             raise OracleError(f"oracle join_pp error {c}")
         cap = c
     out = np.empty((max(cap, 1), 2), np.uint32)
     c = lib.geohip_oracle_join_pp(ctypes.byref(gd), ctypes.byref(gq), _p(dx), _p(dy), len(dx), _p(qx), _p(qy),
-                                  len(qx), r, int(approximate), _p(out), cap)
+                                  len(qx), r, int(approximate), _p(out), cap, None)
     if c < 0:
         raise OracleError(f"oracle join_pp error {c}")
     return out[:c].copy()
 
 
-def range_ppoly(g: Grid, x, y, ring_off, vx, vy, r, approximate=False) -> np.ndarray:
-    x = np.ascontiguousarray(x, np.float64)
-    y = np.ascontiguousarray(y, np.float64)
-    ring_off = np.ascontiguousarray(ring_off, np.uint32)
-    vx = np.ascontiguousarray(vx, np.float64)
-    vy = np.ascontiguousarray(vy, np.float64)
-    npoly = len(ring_off) - 1
-    c = lib.geohip_oracle_range_ppoly(ctypes.byref(g), _p(x), _p(y), len(x), _p(ring_off), _p(vx), _p(vy), npoly,
-                                      r, int(approximate), None, 0)
+def join_pp_hash(gd: Grid, gq: Grid, dx, dy, qx, qy, r, approximate=False):
+    """(pair count, sum of mix64(p << 32 | q) mod 2^64) without materialising the pairs."""
+    dx = np.ascontiguousarray(dx, np.float64)
+    dy = np.ascontiguousarray(dy, np.float64)
+    qx = np.ascontiguousarray(qx, np.float64)
+    qy = np.ascontiguousarray(qy, np.float64)
+    h = c_uint64(0)
+    c = lib.geohip_oracle_join_pp(ctypes.byref(gd), ctypes.byref(gq), _p(dx), _p(dy), len(dx), _p(qx), _p(qy),
+                                  len(qx), r, int(approximate), None, 0, ctypes.byref(h))
     if c < 0:
-        raise OracleError(f"oracle range_ppoly error {c}")
-    out = np.empty((max(c, 1), 2), np.uint32)
-    c2 = lib.geohip_oracle_range_ppoly(ctypes.byref(g), _p(x), _p(y), len(x), _p(ring_off), _p(vx), _p(vy), npoly,
-                                       r, int(approximate), _p(out), c)
-    assert c2 == c
-    return out[:c].copy()
+        raise OracleError(f"oracle join_pp error {c}")
+    return c, h.value
 
 
-def join_ppoly(gp: Grid, gq: Grid, x, y, ring_off, vx, vy, r, approximate=False) -> np.ndarray:
-    """PointPolygonJoinQuery window join: pairs (point, polygon), oracle order."""
-    x = np.ascontiguousarray(x, np.float64)
-    y = np.ascontiguousarray(y, np.float64)
+def _rings(ring_off, vx, vy, poly_rings):
     ring_off = np.ascontiguousarray(ring_off, np.uint32)
     vx = np.ascontiguousarray(vx, np.float64)
     vy = np.ascontiguousarray(vy, np.float64)
-    npoly = len(ring_off) - 1
-    args = (ctypes.byref(gp), ctypes.byref(gq), _p(x), _p(y), len(x), _p(ring_off), _p(vx), _p(vy), npoly, r,
+    if poly_rings is None:
+        return ring_off, vx, vy, None, len(ring_off) - 1
+    pr = np.ascontiguousarray(poly_rings, np.uint32)
+    return ring_off, vx, vy, pr, len(pr) - 1
+
+
+def _ppoly(fn, grids, x, y, ring_off, vx, vy, r, approximate, poly_rings, want_hash):
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    ring_off, vx, vy, pr, npoly = _rings(ring_off, vx, vy, poly_rings)
+    args = (*grids, _p(x), _p(y), len(x), None if pr is None else _p(pr), _p(ring_off), _p(vx), _p(vy), npoly, r,
             int(approximate))
-    c = lib.geohip_oracle_join_ppoly(*args, None, 0)
+    if want_hash:
+        h = c_uint64(0)
+        c = fn(*args, None, 0, ctypes.byref(h))
+        if c < 0:
+            raise OracleError(f"oracle polygon query error {c}")
+        return c, h.value
+    c = fn(*args, None, 0, None)
     if c < 0:
-        raise OracleError(f"oracle join_ppoly error {c}")
+        raise OracleError(f"oracle polygon query error {c}")
     out = np.empty((max(c, 1), 2), np.uint32)
-    assert lib.geohip_oracle_join_ppoly(*args, _p(out), c) == c
+    assert fn(*args, _p(out), c, None) == c
     return out[:c].copy()
 
 
-def knn_ppoly(g: Grid, x, y, vx, vy, r, k, approximate=False):
-    """PointPolygonKNNQuery window body: (idx, dist) ascending by (dist bits, idx)."""
+def range_ppoly(g: Grid, x, y, ring_off, vx, vy, r, approximate=False, poly_rings=None) -> np.ndarray:
+    """PointPolygonRangeQuery window body: pairs (polygon, point).  Ring j = vertices
+    [ring_off[j], ring_off[j+1]); polygon p = rings [poly_rings[p], poly_rings[p+1])
+    (poly_rings None: one ring per polygon)."""
+    return _ppoly(lib.geohip_oracle_range_ppoly, (ctypes.byref(g),), x, y, ring_off, vx, vy, r, approximate,
+                  poly_rings, False)
+
+
+def range_ppoly_hash(g: Grid, x, y, ring_off, vx, vy, r, approximate=False, poly_rings=None):
+    """(pair count, sum of mix64(poly << 32 | point) mod 2^64)."""
+    return _ppoly(lib.geohip_oracle_range_ppoly, (ctypes.byref(g),), x, y, ring_off, vx, vy, r, approximate,
+                  poly_rings, True)
+
+
+def join_ppoly(gp: Grid, gq: Grid, x, y, ring_off, vx, vy, r, approximate=False, poly_rings=None) -> np.ndarray:
+    """PointPolygonJoinQuery window join: pairs (point, polygon), oracle order."""
+    return _ppoly(lib.geohip_oracle_join_ppoly, (ctypes.byref(gp), ctypes.byref(gq)), x, y, ring_off, vx, vy, r,
+                  approximate, poly_rings, False)
+
+
+def join_ppoly_hash(gp: Grid, gq: Grid, x, y, ring_off, vx, vy, r, approximate=False, poly_rings=None):
+    """(pair count, sum of mix64(point << 32 | poly) mod 2^64)."""
+    return _ppoly(lib.geohip_oracle_join_ppoly, (ctypes.byref(gp), ctypes.byref(gq)), x, y, ring_off, vx, vy, r,
+                  approximate, poly_rings, True)
+
+
+def knn_ppoly(g: Grid, x, y, vx, vy, r, k, approximate=False, ring_off=None):
+    """PointPolygonKNNQuery window body: (idx, dist) ascending by (dist bits, idx).  One query
+    polygon: rings ring_off[0..] of vx/vy (None: vx/vy is one ring)."""
     x = np.ascontiguousarray(x, np.float64)
     y = np.ascontiguousarray(y, np.float64)
     vx = np.ascontiguousarray(vx, np.float64)
     vy = np.ascontiguousarray(vy, np.float64)
+    ro = np.array([0, len(vx)], np.uint32) if ring_off is None else np.ascontiguousarray(ring_off, np.uint32)
     oi = np.empty(k, np.uint32)
     od = np.empty(k, np.float64)
     cnt = c_uint32(0)
-    rc = lib.geohip_oracle_knn_ppoly(ctypes.byref(g), _p(x), _p(y), len(x), _p(vx), _p(vy), len(vx), r, k,
+    rc = lib.geohip_oracle_knn_ppoly(ctypes.byref(g), _p(x), _p(y), len(x), _p(ro), len(ro) - 1, _p(vx), _p(vy), r, k,
                                      int(approximate), _p(oi), _p(od), ctypes.byref(cnt))
     if rc != 0:
         raise OracleError(f"oracle knn_ppoly error {rc}")
     return oi[:cnt.value].copy(), od[:cnt.value].copy()
 
 
-def point_polygon(px, py, vx, vy):
+def point_polygon(px, py, vx, vy, ring_off=None):
+    """JTS point.distance(polygon): one closed ring, or the polygon built from rings ring_off."""
     vx = np.ascontiguousarray(vx, np.float64)
     vy = np.ascontiguousarray(vy, np.float64)
-    return lib.geohip_oracle_point_polygon(px, py, _p(vx), _p(vy), len(vx))
+    if ring_off is None:
+        return lib.geohip_oracle_point_polygon(px, py, _p(vx), _p(vy), len(vx))
+    ro = np.ascontiguousarray(ring_off, np.uint32)
+    st = c_int(0)
+    d = lib.geohip_oracle_point_polygon_rings(px, py, _p(ro), len(ro) - 1, _p(vx), _p(vy), ctypes.byref(st))
+    if st.value:
+        raise OracleError(f"oracle polygon error {st.value}")
+    return d
+
+
+def set_threads(t: int) -> None:
+    lib.geohip_oracle_set_threads(int(t))
+
+
+def threads() -> int:
+    return lib.geohip_oracle_threads()
+
+
+MASK64 = (1 << 64) - 1
+
+
+def mix64(z: int) -> int:
+    return lib.geohip_oracle_mix64(z & MASK64)
 
 
 # ---- ingest codec (oracle/ingest_oracle.c) -------------------------------------------------

@@ -292,21 +292,69 @@ def ring_envelope(ring):
     return minx, miny, maxx, maxy
 
 
-def jts_point_polygon_distance(px, py, ring) -> float:
-    """``p.point.distance(polygon)`` (DistanceFunctions.java:33-36) via JTS DistanceOp:
-    containment (PointLocator: envelope test, then ray crossing) first, then the
-    minimum over ring segments with MAX_VALUE start and strict ``<``."""
-    minx, miny, maxx, maxy = ring_envelope(ring)
-    inside_env = not (px > maxx or px < minx or py > maxy or py < miny)
-    if inside_env and locate_point_in_ring(px, py, ring) != EXTERIOR:
+def env_point_distance(env, px, py) -> float:
+    """JTS Envelope.distance(Envelope) of a ring envelope to a point's (1.16.1), the skip test
+    of DistanceOp.computeMinDistance(LineString, Point)."""
+    minx, miny, maxx, maxy = env
+    if not (px > maxx or px < minx or py > maxy or py < miny):
         return 0.0
+    dx = 0.0
+    if maxx < px:
+        dx = px - maxx
+    elif minx > px:
+        dx = minx - px
+    dy = 0.0
+    if maxy < py:
+        dy = py - maxy
+    elif miny > py:
+        dy = miny - py
+    if dx == 0.0:
+        return dy
+    if dy == 0.0:
+        return dx
+    return math.sqrt(dx * dx + dy * dy)
+
+
+def _ring_location(px, py, ring) -> int:
+    """PointLocator.locateInPolygonRing: envelope test, then RayCrossingCounter."""
+    minx, miny, maxx, maxy = ring_envelope(ring)
+    if px > maxx or px < minx or py > maxy or py < miny:
+        return EXTERIOR
+    return locate_point_in_ring(px, py, ring)
+
+
+def jts_point_polygon_distance(px, py, poly) -> float:
+    """``p.point.distance(polygon)`` (DistanceFunctions.java:33-36) via JTS DistanceOp.
+    ``poly`` is a closed ring (shell only) or a Polygon from ``make_polygon`` (shell, holes).
+    Containment first (PointLocator.locateInPolygon: shell EXTERIOR -> exterior, shell
+    BOUNDARY -> boundary, then each hole in order: INTERIOR -> exterior, BOUNDARY ->
+    boundary); not exterior -> 0.  Else the minimum over the rings' segments (shell, then
+    holes), a ring skipped when its envelope is farther than the current minimum, MAX_VALUE
+    start, strict ``<``, stop at 0."""
+    rings = [poly] if poly and isinstance(poly[0][0], float) else list(poly)
+    loc = _ring_location(px, py, rings[0])
+    if loc == BOUNDARY:
+        return 0.0
+    if loc == INTERIOR:
+        for hole in rings[1:]:
+            h = _ring_location(px, py, hole)
+            if h == INTERIOR:
+                loc = EXTERIOR
+                break
+            if h == BOUNDARY:
+                return 0.0
+        if loc == INTERIOR:
+            return 0.0
     md = DBL_MAX
-    for i in range(len(ring) - 1):
-        d = point_to_segment(px, py, ring[i][0], ring[i][1], ring[i + 1][0], ring[i + 1][1])
-        if d < md:
-            md = d
-        if md <= 0.0:
-            return md
+    for ring in rings:
+        if env_point_distance(ring_envelope(ring), px, py) > md:
+            continue
+        for i in range(len(ring) - 1):
+            d = point_to_segment(px, py, ring[i][0], ring[i][1], ring[i + 1][0], ring[i + 1][1])
+            if d < md:
+                md = d
+            if md <= 0.0:
+                return md
     return md
 
 
@@ -478,6 +526,65 @@ def close_ring(coords):
     if not (ring[0][0] == ring[-1][0] and ring[0][1] == ring[-1][1]):
         ring.append(ring[0])
     return ring
+
+
+def ring_area(ring) -> float:
+    """JTS 1.16.1 Polygon.getArea of a shell-only polygon: |Area.ofRingSigned| (shoelace with
+    the first x subtracted)."""
+    n = len(ring)
+    if n < 3:
+        return 0.0
+    x0 = ring[0][0]
+    s = 0.0
+    for i in range(1, n - 1):
+        s += (ring[i][0] - x0) * (ring[i - 1][1] - ring[i + 1][1])
+    return abs(s / 2.0)
+
+
+def make_polygon(rings_in):
+    """Polygon(List<List<Coordinate>>, UniformGrid).createPolygon (Polygon.java:52-66, 115-165):
+    one ring -> closed shell; several -> every ring padded (1-3 coords: first coordinate appended
+    4 times) and closed, then ordered by area, largest first, with createPolygonArray's insertion
+    rule (ties at the tail go after, in the middle before; a NaN area is never inserted); shell =
+    first, holes = the rest.  Returns the list of closed rings [shell, holes...] or None when the
+    constructor leaves polygon null (first ring <= 3 coords); ValueError where JTS throws
+    (an empty ring, a ring whose first coordinate is NaN: not closed)."""
+    rings = [[(float(x), float(y)) for x, y in r] for r in rings_in]
+    if not rings or len(rings[0]) <= 3:
+        return None
+    if len(rings) == 1:
+        ring = rings[0]
+        if not (ring[0][0] == ring[-1][0] and ring[0][1] == ring[-1][1]):
+            ring.append(ring[0])
+        if not (ring[0][0] == ring[-1][0] and ring[0][1] == ring[-1][1]):
+            raise ValueError("Points of LinearRing do not form a closed linestring")
+        return [ring]
+    ordered = []  # (area, ring)
+    for ring in rings:
+        if not ring:
+            raise ValueError("IndexOutOfBoundsException: empty ring")
+        if len(ring) < 4:
+            ring = ring + [ring[0]] * 4
+        if not (ring[0][0] == ring[-1][0] and ring[0][1] == ring[-1][1]):
+            ring.append(ring[0])
+        if not (ring[0][0] == ring[-1][0] and ring[0][1] == ring[-1][1]):
+            raise ValueError("Points of LinearRing do not form a closed linestring")
+        a = ring_area(ring)
+        if not ordered or ordered[-1][0] >= a:
+            ordered.append((a, ring))
+        else:
+            for i in range(len(ordered)):
+                if ordered[i][0] <= a:
+                    ordered.insert(i, (a, ring))
+                    break
+    return [r for _, r in ordered]
+
+
+def polygon_of(coords):
+    """A query polygon given as one ring (list of (x, y)) or as rings (list of lists)."""
+    if coords and isinstance(coords[0][0], (list, tuple)):
+        return make_polygon(coords)
+    return make_polygon([coords])
 
 
 # --------------------------------------------------------------------------------------
@@ -683,10 +790,10 @@ def range_ppoly(grid, xs, ys, rings, r, approximate=False):
     independent query per polygon; returns (poly_idx, point_idx) pairs."""
     out = []
     for pi, coords in enumerate(rings):
-        ring = close_ring(coords)
+        ring = polygon_of(coords)
         if ring is None:
             raise ValueError("polygon needs more than 3 coordinates (Polygon.java:53)")
-        bbox = ring_envelope(ring)
+        bbox = ring_envelope(ring[0])
         ids = bbox_grid_ids(grid, bbox)
         G = grid.guaranteed_cells_poly(r, ids)
         C = grid.candidate_cells_poly(r, ids, G)
@@ -710,10 +817,10 @@ def join_ppoly(ugrid, qgrid, xs, ys, rings, r, approximate=False):
     approximate or JTS distance <= r (no guaranteed shortcut).  Returns (point_idx, poly_idx)."""
     out = []
     for pi, coords in enumerate(rings):
-        ring = close_ring(coords)
+        ring = polygon_of(coords)
         if ring is None:
             raise ValueError("polygon needs more than 3 coordinates (Polygon.java:53)")
-        ids = bbox_grid_ids(qgrid, ring_envelope(ring))
+        ids = bbox_grid_ids(qgrid, ring_envelope(ring[0]))
         G = qgrid.guaranteed_cells_poly(r, ids)
         C = qgrid.candidate_cells_poly(r, ids, G)
         replicated = G | C  # disjoint sets: one copy per key
@@ -730,10 +837,10 @@ def knn_ppoly(grid, xs, ys, coords, r, k, approximate=False):
     contract of knn_pp: per-cell max-heaps of size k (replace only when the head is larger,
     :199-221) over the points of G u C, then the k smallest (distance, idx) over all cells,
     ascending.  A NaN (approximate bbox distance of a NaN coordinate) ranks last."""
-    ring = close_ring(coords)
+    ring = polygon_of(coords)
     if ring is None:
         raise ValueError("polygon needs more than 3 coordinates (Polygon.java:53)")
-    bbox = ring_envelope(ring)
+    bbox = ring_envelope(ring[0])
     ids = bbox_grid_ids(grid, bbox)
     G = grid.guaranteed_cells_poly(r, ids)
     C = grid.candidate_cells_poly(r, ids, G)

@@ -6,6 +6,7 @@ device is present ``Context()`` raises ``GeohipDeviceError``.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_uint32, c_uint64, c_void_p
@@ -98,6 +99,7 @@ _SIGS = {
     "geohip_last_error": (c_char_p, [_P]),
     "geohip_ctx_set_mem": (c_int, [_P, c_int]),
     "geohip_ctx_set_stream": (c_int, [_P, _P]),
+    "geohip_ctx_reset_stream": (c_int, [_P]),
     "geohip_ctx_stream": (c_void_p, [_P]),
     "geohip_ctx_set_timing": (c_int, [_P, c_int]),
     "geohip_ctx_timing": (c_int, [_P, POINTER(c_double), POINTER(c_uint64), c_int]),
@@ -235,7 +237,7 @@ def _ptr(a):
         return None
     if isinstance(a, np.ndarray):
         return a.ctypes.data_as(c_void_p)
-    return c_void_p(a.data_ptr())  # torch tensor on the ctx device
+    return c_void_p(a.data_ptr())  # torch tensor on the ctx device (checked by Context._dev)
 
 
 def _is_device(a) -> bool:
@@ -246,6 +248,13 @@ def _f64(a):
     if isinstance(a, np.ndarray):
         return np.ascontiguousarray(a, dtype=np.float64)
     return a
+
+
+def _host(a, dtype):
+    """Host array of dtype (polygon rings and other planning inputs are host memory)."""
+    if a is not None and not isinstance(a, np.ndarray) and hasattr(a, "detach"):
+        a = a.detach().cpu().numpy()
+    return np.ascontiguousarray(a, dtype=dtype)
 
 
 class Context:
@@ -260,6 +269,8 @@ class Context:
         self.h = h
         self.device = device
         self._mem = MEM_HOST
+        self._follow = True   # device calls enqueue on torch's current stream of the inputs' device
+        self._bound = None    # stream handle the C ctx enqueues on (None: its own stream)
 
     def close(self):
         if self.h:
@@ -283,10 +294,53 @@ class Context:
             self._mem = kind
 
     def set_stream(self, stream_ptr: int | None):
-        self._check(lib.geohip_ctx_set_stream(self.h, c_void_p(stream_ptr) if stream_ptr else None), "set_stream")
+        """Enqueue on this hipStream_t (0 = the null stream, PyTorch's default); None = the ctx's
+        own stream.  Stops following torch's current stream (follow_torch_stream)."""
+        self._follow = False
+        self._bind(stream_ptr)
+
+    def _bind(self, stream_ptr):
+        if stream_ptr is None:
+            self._check(lib.geohip_ctx_reset_stream(self.h), "reset_stream")
+        else:
+            self._check(lib.geohip_ctx_set_stream(self.h, c_void_p(stream_ptr) if stream_ptr else None), "set_stream")
+        self._bound = stream_ptr
+
+    def follow_torch_stream(self, on: bool = True):
+        """Default: calls on device tensors run on torch.cuda.current_stream() of their device, so
+        torch kernels that produced the inputs finish first and torch work queued after an
+        *_async call sees its results."""
+        self._follow = bool(on)
 
     def stream(self) -> int:
         return lib.geohip_ctx_stream(self.h) or 0
+
+    @contextlib.contextmanager
+    def using_stream(self, stream_ptr):
+        """Bind a stream for a block, then restore the previous binding and follow mode."""
+        prev, follow = self._bound, self._follow
+        self._follow = False
+        self._bind(stream_ptr)
+        try:
+            yield self
+        finally:
+            self._bind(prev)
+            self._follow = follow
+
+    def _dev(self, t, what="array", dtype="float64"):
+        """Validate a device tensor argument (dtype, contiguity, ctx device) and, in follow mode,
+        bind torch's current stream of its device."""
+        import torch
+        if t.dtype != getattr(torch, dtype):
+            raise GeohipArgumentError(f"{what}: expected a {dtype} tensor, got {t.dtype}")
+        if not t.is_contiguous():
+            raise GeohipArgumentError(f"{what}: tensor must be contiguous")
+        if t.device.index != self.device:
+            raise GeohipArgumentError(f"{what}: tensor on {t.device}, ctx on cuda:{self.device}")
+        if self._follow:
+            s = torch.cuda.current_stream(t.device).cuda_stream
+            if s != self._bound:
+                self._bind(s)
 
     def set_timing(self, on: bool):
         self._check(lib.geohip_ctx_set_timing(self.h, int(on)), "set_timing")
@@ -296,12 +350,17 @@ class Context:
         self._check(lib.geohip_ctx_timing(self.h, ctypes.byref(ms), ctypes.byref(n), int(reset)), "timing")
         return ms.value, n.value
 
-    def _mem_for(self, *arrays):
+    def _mem_for(self, *arrays, dtype="float64"):
         dev = [_is_device(a) for a in arrays if a is not None]
         if any(dev) and not all(dev):
             raise GeohipArgumentError("mix of host and device arrays")
-        self.set_mem(MEM_DEVICE if dev and dev[0] else MEM_HOST)
-        return bool(dev and dev[0])
+        on_dev = bool(dev and dev[0])
+        if on_dev:
+            for a in arrays:
+                if a is not None:
+                    self._dev(a, dtype=dtype)
+        self.set_mem(MEM_DEVICE if on_dev else MEM_HOST)
+        return on_dev
 
     # ---- queries -------------------------------------------------------------------------
     def range_pp(self, grid: Grid, x, y, qx, qy, r, approximate=False, cap=None):
@@ -341,6 +400,10 @@ class Context:
     # async forms: device tensors only, no host sync; the hot per-window path, so the pointers
     # go to ctypes as plain ints (argtypes c_void_p) without wrapper objects
     def knn_pp_async(self, grid: Grid, x, y, qx, qy, r, k, out_idx, out_dist, out_count):
+        self._dev(x, "x")
+        self._dev(y, "y")
+        self._dev(out_idx, "out_idx", "int32")
+        self._dev(out_dist, "out_dist")
         if self._mem != MEM_DEVICE:
             self.set_mem(MEM_DEVICE)
         rc = lib.geohip_knn_pp_async(self.h, ctypes.byref(grid), x.data_ptr(), y.data_ptr(), x.numel(), qx, qy, r, k,
@@ -349,6 +412,10 @@ class Context:
             self._check(rc, "knn_pp_async")
 
     def knn_merge_async(self, dist, idx, nlists, list_len, k, out_idx, out_dist, out_count):
+        self._dev(dist, "dist")
+        self._dev(idx, "idx", "int32")
+        if dist.numel() < nlists * list_len or idx.numel() < nlists * list_len:
+            raise GeohipArgumentError("knn_merge_async: lists shorter than nlists * list_len")
         if self._mem != MEM_DEVICE:
             self.set_mem(MEM_DEVICE)
         rc = lib.geohip_knn_merge_async(self.h, dist.data_ptr(), idx.data_ptr(), nlists, list_len, k,
@@ -357,6 +424,11 @@ class Context:
             self._check(rc, "knn_merge_async")
 
     def range_pp_async(self, grid: Grid, x, y, qx, qy, r, approximate, out_idx, cap, out_count):
+        self._dev(x, "x")
+        self._dev(y, "y")
+        self._dev(out_idx, "out_idx", "int32")
+        if out_idx.numel() < cap:
+            raise GeohipArgumentError("range_pp_async: out_idx shorter than cap")
         if self._mem != MEM_DEVICE:
             self.set_mem(MEM_DEVICE)
         rc = lib.geohip_range_pp_async(self.h, ctypes.byref(grid), x.data_ptr(), y.data_ptr(), x.numel(), qx, qy, r,
@@ -403,9 +475,9 @@ class Context:
         """Pairs (polygon idx, point idx).  ``out``: optional preallocated [cap, 2] buffer."""
         x, y = _f64(x), _f64(y)
         self._mem_for(x, y)
-        ring_off = np.ascontiguousarray(ring_off, dtype=np.uint32)
-        vx = np.ascontiguousarray(vx, dtype=np.float64)
-        vy = np.ascontiguousarray(vy, dtype=np.float64)
+        ring_off = _host(ring_off, np.uint32)
+        vx = _host(vx, np.float64)
+        vy = _host(vy, np.float64)
         npoly = len(ring_off) - 1
         cnt = c_uint64(0)
         if out is not None:
@@ -433,9 +505,9 @@ class Context:
         """Point-polygon join: pairs (point idx, polygon idx).  ``out``: optional [cap, 2] buffer."""
         x, y = _f64(x), _f64(y)
         self._mem_for(x, y)
-        ring_off = np.ascontiguousarray(ring_off, dtype=np.uint32)
-        vx = np.ascontiguousarray(vx, dtype=np.float64)
-        vy = np.ascontiguousarray(vy, dtype=np.float64)
+        ring_off = _host(ring_off, np.uint32)
+        vx = _host(vx, np.float64)
+        vy = _host(vy, np.float64)
         npoly = len(ring_off) - 1
         cnt = c_uint64(0)
         args = (self.h, ctypes.byref(grid_points), ctypes.byref(grid_query), _ptr(x), _ptr(y), len(x), _ptr(ring_off),
@@ -461,8 +533,8 @@ class Context:
         """Point-polygon kNN of one polygon ring: (idx, dist) ascending by (dist, idx)."""
         x, y = _f64(x), _f64(y)
         dev = self._mem_for(x, y)
-        vx = np.ascontiguousarray(vx, dtype=np.float64)
-        vy = np.ascontiguousarray(vy, dtype=np.float64)
+        vx = _host(vx, np.float64)
+        vy = _host(vy, np.float64)
         if dev:
             import torch
             oi = torch.empty(k, dtype=torch.int32, device=x.device)
@@ -514,6 +586,8 @@ class Context:
         return {k: v[:cnt.value] for k, v in out.items()}
 
     def synth_uniform_async(self, x, y, base, seed, bbox):
+        self._dev(x, "x")
+        self._dev(y, "y")
         min_x, max_x, min_y, max_y = bbox
         rc = lib.geohip_synth_uniform_async(self.h, _ptr(x), _ptr(y), len(x), base, seed, min_x, max_x, min_y, max_y)
         self._check(rc, "synth_uniform_async")

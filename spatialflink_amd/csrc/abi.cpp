@@ -352,7 +352,13 @@ int geohip_ctx_set_mem(geohip_ctx* ctx, int mem_kind) {
 
 int geohip_ctx_set_stream(geohip_ctx* ctx, void* hip_stream) {
     if (!ctx) return GEOHIP_ERR_ARG;
-    ctx->stream = hip_stream ? (hipStream_t)hip_stream : ctx->own;
+    ctx->stream = (hipStream_t)hip_stream;  // NULL: the HIP null stream (e.g. PyTorch's default stream)
+    return GEOHIP_OK;
+}
+
+int geohip_ctx_reset_stream(geohip_ctx* ctx) {
+    if (!ctx) return GEOHIP_ERR_ARG;
+    ctx->stream = ctx->own;
     return GEOHIP_OK;
 }
 

@@ -21,6 +21,8 @@ before the first element do.  Panes are device-resident (x, y float64 tensors) o
 """
 from __future__ import annotations
 
+import collections
+
 from collections import deque
 
 from . import _abi
@@ -100,7 +102,7 @@ class IncrementalKNN:
         self.stream = torch.cuda.Stream()
         self.sizes = deque(maxlen=self.p)  # sizes of the panes in the ring, oldest first
         self.count = 0                     # panes pushed so far
-        self._offs = {}                    # (slot order, offsets) -> device tensors
+        self._offs = collections.OrderedDict()  # (slot order, offsets) -> device tensors (LRU)
         self._dev = None
 
     def _alloc(self, dev):
@@ -121,31 +123,30 @@ class IncrementalKNN:
             self._alloc(x.device)
         caller = torch.cuda.current_stream()
         self.stream.wait_stream(caller)  # the pane's x, y are ready
-        prev = self.ctx.stream()
-        self.ctx.set_stream(self.stream.cuda_stream)
-        try:
-            with torch.cuda.stream(self.stream):
-                slot = self.count % self.p
-                self.ctx.knn_pp_async(self.grid, x, y, self.q[0], self.q[1], self.r, self.k, self.ring_i[slot],
-                                      self.ring_d[slot], self.cnt[0:1])
-                self.count += 1
-                self.sizes.append(len(x))
-                n = len(self.sizes)
-                order = tuple((self.count - n + j) % self.p for j in range(n))  # oldest first
-                offs = [0]
-                for size in list(self.sizes)[:-1]:
-                    offs.append(offs[-1] + size)
-                key = (order, tuple(offs))
-                if key not in self._offs:
-                    self._offs[key] = (torch.tensor(order, dtype=torch.int64, device=x.device),
-                                       torch.tensor(offs, dtype=torch.int32, device=x.device).view(-1, 1))
-                oidx, otens = self._offs[key]
-                li = self.ring_i.index_select(0, oidx)
-                wi = torch.where(li >= 0, li + otens, li)
-                wd = self.ring_d.index_select(0, oidx)
-                self.ctx.knn_merge_async(wd, wi, n, self.k, self.k, self.mi, self.md, self.cnt[1:2])
-        finally:
-            self.ctx.set_stream(prev)
+        with self.ctx.using_stream(self.stream.cuda_stream), torch.cuda.stream(self.stream):
+            slot = self.count % self.p
+            self.ctx.knn_pp_async(self.grid, x, y, self.q[0], self.q[1], self.r, self.k, self.ring_i[slot],
+                                  self.ring_d[slot], self.cnt[0:1])
+            self.count += 1
+            self.sizes.append(len(x))
+            n = len(self.sizes)
+            order = tuple((self.count - n + j) % self.p for j in range(n))  # oldest first
+            offs = [0]
+            for size in list(self.sizes)[:-1]:
+                offs.append(offs[-1] + size)
+            key = (order, tuple(offs))
+            if key in self._offs:
+                self._offs.move_to_end(key)
+            else:  # a small LRU: pane sizes vary window to window in a time-based stream
+                self._offs[key] = (torch.tensor(order, dtype=torch.int64, device=x.device),
+                                   torch.tensor(offs, dtype=torch.int32, device=x.device).view(-1, 1))
+                while len(self._offs) > 8:
+                    self._offs.popitem(last=False)
+            oidx, otens = self._offs[key]
+            li = self.ring_i.index_select(0, oidx)
+            wi = torch.where(li >= 0, li + otens, li)
+            wd = self.ring_d.index_select(0, oidx)
+            self.ctx.knn_merge_async(wd, wi, n, self.k, self.k, self.mi, self.md, self.cnt[1:2])
         caller.wait_stream(self.stream)
         if not sync:
             return self.mi, self.md

@@ -1,0 +1,153 @@
+"""Full-scale parity: BASELINE.json configs C3, C4 and the C5 shard at their own sizes.
+
+The HIP path (through the C ABI, device-resident windows) against the multithreaded C oracle
+(oracle/geohip_oracle.c, OpenMP; test infrastructure only).  Pair sets of up to 4.4e8 pairs are
+compared by their exact count and an order-independent 64-bit digest (sum over pairs of
+mix64(first << 32 | second) mod 2^64, computed on the device by torch for the product output
+and by the oracle for the reference semantics), so no pair list needs sorting or copying.
+  C3  point-point join, 10k queries x 10M Gaussian data points (32 centres, sigma 0.1), 500x500,
+      r = 0.05  (PointPointJoinQuery.java:113-172)
+  C4  point-polygon range, 1k star polygons x 50M uniform points, 500x500, r = 0.005
+      (PointPolygonRangeQuery.java:76-124); the join form of the same shape
+      (PointPolygonJoinQuery.java:162-201)
+  C5  one 25M-point shard, 1000x1000, kNN k = 100 + range r = 0.05 of the README query
+      (PointPointKNNQuery.java:125-191, PointPointRangeQuery.java:86-137)
+"""
+import numpy as np
+import pytest
+
+import cref
+from spatialflink_amd import _abi, synth
+
+pytestmark = pytest.mark.gpu
+
+BJ = synth.BEIJING
+Q = synth.README_QUERY
+MASK = (1 << 64) - 1
+
+
+def agrid(n):
+    l = (BJ[1] - BJ[0]) / n
+    return _abi.make_grid(BJ[0], BJ[2], l, n), cref.grid(BJ[0], BJ[2], l, n)
+
+
+def _s64(c):  # an unsigned 64-bit constant as the int64 torch holds it
+    return c - (1 << 64) if c >= 1 << 63 else c
+
+
+def _lsr(z, s):  # logical right shift of int64 lanes
+    import torch
+    return torch.bitwise_and(torch.bitwise_right_shift(z, s), (1 << (64 - s)) - 1)
+
+
+def mix64_torch(v):
+    """splitmix64 finaliser on int64 lanes (wrapping arithmetic), = cref.mix64 bit for bit."""
+    import torch
+    z = v + _s64(0x9E3779B97F4A7C15)
+    z = torch.bitwise_xor(z, _lsr(z, 30)) * _s64(0xBF58476D1CE4E5B9)
+    z = torch.bitwise_xor(z, _lsr(z, 27)) * _s64(0x94D049BB133111EB)
+    return torch.bitwise_xor(z, _lsr(z, 31))
+
+
+def pair_digest(pairs, chunk=1 << 26):
+    """(count, sum of mix64(a << 32 | b) mod 2^64) of an [m, 2] int32 device tensor of pairs."""
+    import torch
+    m = int(pairs.shape[0])
+    h = 0
+    for s in range(0, m, chunk):
+        p = pairs[s:s + chunk].to(torch.int64)
+        v = torch.bitwise_or(torch.bitwise_left_shift(torch.bitwise_and(p[:, 0], 0xFFFFFFFF), 32),
+                             torch.bitwise_and(p[:, 1], 0xFFFFFFFF))
+        # int64 sums wrap like the oracle's uint64 sum; add the halves exactly in Python
+        z = mix64_torch(v)
+        lo = int(torch.bitwise_and(z, 0xFFFFFFFF).sum().item())
+        hi = int(_lsr(z, 32).sum().item())
+        h = (h + lo + (hi << 32)) & MASK
+    return m, h
+
+
+def test_digest_matches_oracle_mix(ctx):
+    """The torch digest is the oracle's mix64, including wrap-around and the top bit."""
+    import torch
+    rng = np.random.default_rng(7)
+    a = rng.integers(0, 1 << 32, 5000, dtype=np.uint64)
+    b = rng.integers(0, 1 << 32, 5000, dtype=np.uint64)
+    a[:3] = [0, 0xFFFFFFFF, 0x80000000]
+    b[:3] = [0, 0xFFFFFFFF, 1]
+    want = sum(cref.mix64(int(p) << 32 | int(q)) for p, q in zip(a, b)) & MASK
+    t = torch.from_numpy(np.stack([a, b], 1).astype(np.uint32).view(np.int32)).cuda()
+    assert pair_digest(t, chunk=1024) == (5000, want)
+
+
+def _device_uniform(ctx, n, seed):
+    import torch
+    x = torch.empty(n, dtype=torch.float64, device="cuda")
+    y = torch.empty(n, dtype=torch.float64, device="cuda")
+    ctx.synth_uniform_async(x, y, 0, seed, BJ)
+    torch.cuda.synchronize()
+    return x, y
+
+
+def test_c3_join_full_scale(ctx):
+    """C3 at its own size: 10k queries x 10M Gaussian data points, sigma 0.1, 500x500, r = 0.05."""
+    import torch
+    hx, hy = synth.gaussian_clusters(10_000_000, 3, sigma=0.1)
+    hqx, hqy = synth.gaussian_clusters(10_000, 4, sigma=0.1)
+    ag, cg = agrid(500)
+    want = cref.join_pp_hash(cg, cg, hx, hy, hqx, hqy, 0.05)
+    assert want[0] > 4e8  # ~4.4e8 pairs at sigma 0.1
+    dx, dy = torch.from_numpy(hx).cuda(), torch.from_numpy(hy).cuda()
+    qx, qy = torch.from_numpy(hqx).cuda(), torch.from_numpy(hqy).cuda()
+    out = torch.empty((want[0] + 16, 2), dtype=torch.int32, device="cuda")
+    got = ctx.join_pp(ag, ag, dx, dy, qx, qy, 0.05, out=out)
+    assert pair_digest(got) == want
+    del out, got
+    assert ctx.join_pp_count(ag, ag, dx, dy, qx, qy, 0.05) == want[0]
+
+
+@pytest.fixture(scope="module")
+def c4_window(ctx):
+    x, y = _device_uniform(ctx, 50_000_000, 5)
+    hx, hy = x.cpu().numpy(), y.cpu().numpy()
+    off, vx, vy = synth.star_polygons(1000, 6)
+    return x, y, hx, hy, off, vx, vy
+
+
+def test_c4_range_ppoly_full_scale(ctx, c4_window):
+    """C4 at its own size: all 1k polygons (50 vertices) x 50M uniform points, 500x500, r = 0.005."""
+    import torch
+    x, y, hx, hy, off, vx, vy = c4_window
+    ag, cg = agrid(500)
+    want = cref.range_ppoly_hash(cg, hx, hy, off, vx, vy, 0.005)
+    assert want[0] > 1e7
+    out = torch.empty((want[0] + 16, 2), dtype=torch.int32, device="cuda")
+    got = ctx.range_ppoly(ag, x, y, off, vx, vy, 0.005, out=out)
+    assert pair_digest(got) == want
+
+
+def test_c4_join_ppoly_full_scale(ctx, c4_window):
+    """The join form of C4 (PointPolygonJoinQuery): every G u C pair distance-checked."""
+    import torch
+    x, y, hx, hy, off, vx, vy = c4_window
+    ag, cg = agrid(500)
+    want = cref.join_ppoly_hash(cg, cg, hx, hy, off, vx, vy, 0.005)
+    out = torch.empty((want[0] + 16, 2), dtype=torch.int32, device="cuda")
+    got = ctx.join_ppoly(ag, ag, x, y, off, vx, vy, 0.005, out=out)
+    assert pair_digest(got) == want
+
+
+def test_c5_shard_knn_and_range_full_scale(ctx):
+    """C5 shard: 25M uniform points (rank 0's slice of the 200M window), 1000x1000, kNN k = 100
+    and range r = 0.05 of the README query: exact (idx, distance bits) and the exact hit list."""
+    x, y = _device_uniform(ctx, 25_000_000, 7)
+    hx, hy = x.cpu().numpy(), y.cpu().numpy()
+    ag, cg = agrid(1000)
+    oi, od = ctx.knn_pp(ag, x, y, Q[0], Q[1], 0.05, 100)
+    wi, wd = cref.knn_pp(cg, hx, hy, Q[0], Q[1], 0.05, 100)
+    assert len(wi) == 100
+    assert oi.cpu().numpy().astype(np.uint32).tolist() == wi.tolist()
+    assert np.array_equal(od.cpu().numpy().view(np.uint64), wd.view(np.uint64))
+    got = ctx.range_pp(ag, x, y, Q[0], Q[1], 0.05)
+    want = cref.range_pp(cg, hx, hy, Q[0], Q[1], 0.05)
+    assert got.cpu().numpy().astype(np.uint32).tolist() == want.tolist()
+    assert len(want) > 5e4
