@@ -555,7 +555,7 @@ class Context:
         (attribute ``bad`` = first rejected record) where the device grammar rejects a record."""
         if isinstance(text, (bytes, bytearray)):
             text = np.frombuffer(text, dtype=np.uint8)
-        dev = self._mem_for(text)
+        dev = self._mem_for(text, dtype="uint8")
         nbytes = int(text.numel()) if dev else int(text.size)
         if cap is None:
             cap = nbytes // 2 + 1  # a record has at least one byte plus its '\n'
