@@ -2,7 +2,7 @@
 
 Default workload (the headline, BASELINE.json configs[1] = C2): one step = one window of
 point-point kNN (k = 50) of the README query over 10M uniform points per GPU (100x100 Beijing
-grid, r = 0.5): the scan kernel and the final selection (knn_final) and, for N > 1, the RCCL
+grid, r = 0.5): one knn_pass launch (scan + the last block's final selection) and, for N > 1, the RCCL
 all-gather of each rank's top-k plus the device merge (weak scaling: every rank holds its own
 10M-point shard of the window; ranks shard by arrival order, which gives the identical result
 for a single-query kNN).
@@ -58,8 +58,6 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--time-every", type=int, default=8,
                    help="bracket every N-th timed step's kernels with HIP events (1 = all)")
-    p.add_argument("--knn-final", choices=("fused", "separate"), default="separate",
-                   help="final selection in the scan's last block, or a separate knn_final launch")
     return p.parse_args()
 
 
@@ -134,7 +132,7 @@ def _uniform_windows(ctx, dev, n, rank, seeds, bbox):
 class KnnWorkload(Workload):
     """C2 (BASELINE.json configs[1]): kNN k=50, 100x100, r=0.5, 10M uniform points per GPU."""
     tag = "knn_scan"
-    kernel = "geohip::knn_scan<1> + geohip::knn_final<1> (one window's scan and final selection)"
+    kernel = "geohip::knn_pass<16> (one launch per window: scan, block lists, last block's final selection)"
     grid_n, k, radius, n_default, seed0 = 100, 50, 0.5, 10_000_000, 2
     label = "C2: point-point kNN k=50, 100x100 Beijing UniformGrid, r=0.5, README query"
 
@@ -181,7 +179,7 @@ class KnnWorkload(Workload):
     def config(self):
         return {"workload": f"{self.label}, {self.n} uniform points per window per GPU (BASELINE.json configs[1])",
                 "points_per_window_per_gpu": self.n, "grid": self.grid_n, "k": self.k, "radius": self.radius,
-                "windows_resident": self.windows, "final_selection": self.args.knn_final,
+                "windows_resident": self.windows,
                 "parallelism": f"shard{self.world}"}
 
     def cpu_baseline(self, seconds):
@@ -534,7 +532,7 @@ class KnnIncrWorkload(KnnWorkload):
     top-k merged from its two panes' top-k lists (spatialflink_amd.incremental.IncrementalKNN).
     value = stream points/sec (each point is evaluated once, not once per window)."""
     tag = "knn_incr"
-    kernel = "geohip::knn_scan<1> + knn_final<1> on one pane (+ a 2-list knn_merge)"
+    kernel = "geohip::knn_pass<16> on one pane (+ a 2-list knn_merge)"
     n_default = 5_000_000
     label = "C2 over 10s/5s sliding windows with pane reuse: kNN k=50, 100x100 Beijing UniformGrid, r=0.5"
 
@@ -694,7 +692,6 @@ def main():
 
     dev = torch.device("cuda", local)
     ctx = Context(local)
-    _abi.debug_set_knn_fused(args.knn_final == "fused")
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)  # kernels and RCCL ordered on one stream (0 = the null stream)
     wl = WORKLOADS[args.workload](args, ctx, dev, rank, world, dist)

@@ -69,8 +69,10 @@ extern "C" {
 #define GEOHIP_MEM_HOST 0
 #define GEOHIP_MEM_DEVICE 1
 
-/* Largest k served by the wave-select kNN path (PointPointKNNQuery's k). */
-#define GEOHIP_KNN_MAX_K 256
+/* Largest k of the point kNN (PointPointKNNQuery's k) and of the rank merge. */
+#define GEOHIP_KNN_MAX_K 1024
+/* Largest k of the point-polygon kNN (PointPolygonKNNQuery's k). */
+#define GEOHIP_KNN_PPOLY_MAX_K 256
 
 typedef struct geohip_ctx geohip_ctx;
 
@@ -162,7 +164,8 @@ int geohip_knn_pp_async(geohip_ctx* ctx, const geohip_grid* grid, const double* 
                         uint32_t* out_idx, double* out_dist, uint32_t* out_count_dev);
 /* Merge nlists sorted (dist, idx) lists of list_len entries (e.g. the all-gathered per-shard
    kNN results) into the k smallest; same output convention as geohip_knn_pp_async.
-   idx values are taken as global ids (shards add their base offset before the gather). */
+   idx values are taken as global ids (shards add their base offset before the gather).
+   k <= GEOHIP_KNN_MAX_K; above 256, nlists * list_len <= 8192. */
 int geohip_knn_merge_async(geohip_ctx* ctx, const double* dist, const uint32_t* idx, uint32_t nlists,
                            uint32_t list_len, uint32_t k, uint32_t* out_idx, double* out_dist,
                            uint32_t* out_count_dev);

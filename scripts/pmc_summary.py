@@ -15,7 +15,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 # workload -> (profiles tag, kernel-name substrings of the bench's timed region, timed launches per step)
-TAGS = {"knn": ("knn_scan", ("knn_scan", "knn_final"), 1),
+TAGS = {"knn": ("knn_scan", ("knn_pass",), 1),
         "range": ("range", ("range_fused", "range_scan", "scan_units", "range_emit"), 1),
         "join": ("join_probe", ("join_tile", "join_emit", "scan_seg_totals<unsigned long long>", "scan_totals<unsigned long long>",
                                  "scan_apply<unsigned long long>"), 1),
@@ -24,7 +24,7 @@ TAGS = {"knn": ("knn_scan", ("knn_scan", "knn_final"), 1),
         "ingest": ("ingest", ("ingest_count", "ingest_scan", "ingest_parse"), 1),
         "ppjoin": ("ppjoin", ("ppoly_eval", "ppoly_emit", "ppoly_outside"), 1),
         "ppknn": ("ppknn", ("rsel_", "ppknn_"), 1),
-        "knn_incr": ("knn_incr", ("knn_scan", "knn_final"), 1),
+        "knn_incr": ("knn_incr", ("knn_pass", "knn_final"), 1),
         "ppoly_incr": ("ppoly_incr", ("ppoly_eval", "ppoly_emit", "ppoly_outside"), 1)}
 
 

@@ -1,0 +1,45 @@
+"""Phase timeline of one kNN pass launch (100 MHz timestamps): per-block start, stream end,
+flush (block barrier), stores drained, arrived; the last block's acquire, gather and write.
+Percentiles in microseconds relative to the earliest block start (GPU box measurement)."""
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from spatialflink_amd import Context, _abi, synth  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
+K = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+R = float(sys.argv[3]) if len(sys.argv) > 3 else 0.5
+GN = int(sys.argv[4]) if len(sys.argv) > 4 else 100
+ABL = int(sys.argv[5]) if len(sys.argv) > 5 else 0
+W = 4
+ctx = Context(0)
+bj, q = synth.BEIJING, synth.README_QUERY
+grid = _abi.make_grid(bj[0], bj[2], (bj[1] - bj[0]) / GN, GN)
+xs, ys = [], []
+for w in range(W):
+    x = torch.empty(n, dtype=torch.float64, device="cuda")
+    y = torch.empty(n, dtype=torch.float64, device="cuda")
+    ctx.synth_uniform_async(x, y, 0, 2 + 7919 * w, bj)
+    xs.append(x)
+    ys.append(y)
+torch.cuda.synchronize()
+names = ["start", "stream_end", "flush", "drained", "arrived"]
+out = {}
+for rep in range(4):
+    for w in range(W):  # warm the path, cycle windows
+        ctx.knn_pp(grid, xs[w], ys[w], q[0], q[1], R, K)
+    tr = ctx.debug_knn_pass_trace(grid, xs[rep % W], ys[rep % W], q[0], q[1], R, K, ABL).astype(np.int64)
+    t0 = tr[:, 0].min()
+    rel = (tr - t0) / 100.0
+    row = {nm: [round(float(np.percentile(rel[:, j], p)), 2) for p in (0, 10, 50, 90, 100)] for j, nm in enumerate(names)}
+    last = int(np.argmax(tr[:, 7]))
+    row["final"] = {nm: round(float(rel[last, j]), 2) for nm, j in (("acquired", 5), ("gathered", 6), ("written", 7))}
+    row["last_block"] = last
+    row["stats"] = ctx.debug_knn_pass_stats()
+    out[f"rep{rep}"] = row
+print(json.dumps({"shape": dict(n=n, k=K, r=R, grid=GN, ablation=ABL), **out}))

@@ -18,7 +18,8 @@ LIB_PATH = Path(os.environ.get("GEOHIP_LIB", Path(__file__).resolve().parent / "
 
 OK, ERR_ARG, ERR_CAPACITY, ERR_DEVICE, ERR_OOM, ERR_UNSUPPORTED = 0, 1, 2, 3, 4, 5
 MEM_HOST, MEM_DEVICE = 0, 1
-KNN_MAX_K = 256
+KNN_MAX_K = 1024
+KNN_PPOLY_MAX_K = 256
 SENTINEL_IDX = 0xFFFFFFFF
 
 
@@ -133,13 +134,10 @@ _SIGS = {
                                            POINTER(c_double), POINTER(ctypes.c_int64)]),
     "geohip_debug_selftest_fp64": (c_int, [_P, _P, _P, c_uint64, _P, _P, _P, _P]),
     "geohip_debug_classify": (c_int, [POINTER(Grid), c_double, c_double, c_double, _P, _P, c_uint64, _P]),
-    "geohip_debug_set_knn_fused": (None, [c_int]),
-    "geohip_debug_set_join_mask_budget": (None, [c_uint64]),
-    "geohip_debug_set_range_mode": (None, [c_int]),
-    "geohip_debug_set_knn_config": (c_int, [c_int, c_int, c_int, c_int, c_int]),
-    "geohip_debug_knn_trace": (c_int, [_P, _P, c_uint64, POINTER(c_uint32)]),
-    "geohip_debug_knn_scan_variant": (c_int, [_P, c_int, POINTER(Grid), _P, _P, c_uint64, c_int, c_double,
-                                              c_double, c_double, c_uint32, c_int, _P]),
+    "geohip_debug_knn_pass_stats": (c_int, [_P, _P]),
+    "geohip_debug_knn_pass_trace": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_double, c_double, c_double,
+                                            c_uint32, c_int, _P, c_uint64, POINTER(c_uint32)]),
+    "geohip_debug_ctx_join_mask_budget": (c_int, [_P, c_uint64]),
 }
 for _name, (_res, _args) in _SIGS.items():
     _f = getattr(lib, _name)
@@ -189,31 +187,6 @@ def debug_classify(grid: Grid, qx: float, qy: float, r: float, x: np.ndarray, y:
     if rc:
         raise _ERRORS.get(rc, GeohipError)(f"debug_classify failed ({rc})")
     return out
-
-
-def debug_set_knn_fused(fused: bool) -> None:
-    """Test/measurement hook: kNN final selection inside the scan's last block (default) or
-    as a separate knn_final launch."""
-    lib.geohip_debug_set_knn_fused(1 if fused else 0)
-
-
-def debug_set_range_mode(mode: int = 0) -> None:
-    """Measurement hook: fused range pass ablation (0 full, 1 counts only, 2 loads only)."""
-    lib.geohip_debug_set_range_mode(mode)
-
-
-def debug_set_join_mask_budget(nbytes: int = 4 << 30) -> None:
-    """Test hook: byte budget of the join's hit masks; beyond it the write pass recomputes."""
-    lib.geohip_debug_set_join_mask_budget(nbytes)
-
-
-def debug_set_knn_config(waves_per_block: int = 16, prefetch: int = 1, ticket_groups: int = 16,
-                         epi_sort: int = 0, interleave: int = 0) -> None:
-    """Measurement hook: kNN scan launch shape (waves per block 4/8/16, load pipeline depth
-    1/2, arrival-ticket groups 1..64, block list by register sort (1) or rank placement (0),
-    iterations in contiguous block chunks (0) or interleaved over the blocks (1))."""
-    if lib.geohip_debug_set_knn_config(waves_per_block, prefetch, ticket_groups, epi_sort, interleave):
-        raise GeohipArgumentError(f"unsupported kNN shape {waves_per_block}/{prefetch}/{ticket_groups}/{epi_sort}")
 
 
 def plan_cell(grid: Grid, x: float, y: float):
@@ -592,22 +565,26 @@ class Context:
         rc = lib.geohip_synth_uniform_async(self.h, _ptr(x), _ptr(y), len(x), base, seed, min_x, max_x, min_y, max_y)
         self._check(rc, "synth_uniform_async")
 
-    def debug_knn_scan_variant(self, mode, grid, x, y, n, nwin, qx, qy, r, k, reps=20):
-        """x, y: [nwin * n] device arrays; launch i scans window i % nwin."""
-        ms = (c_double * 3)()
-        self.set_mem(MEM_DEVICE)
-        rc = lib.geohip_debug_knn_scan_variant(self.h, mode, ctypes.byref(grid), _ptr(x), _ptr(y), n, nwin, qx, qy,
-                                               r, k, reps, ms)
-        self._check(rc, "debug_knn_scan_variant")
-        return ms[0] if mode != 5 else (ms[0], ms[1], ms[2])
+    def debug_join_mask_budget(self, nbytes: int = 4 << 30):
+        """Test hook: byte budget of this ctx's join hit masks; beyond it the write pass recomputes."""
+        self._check(lib.geohip_debug_ctx_join_mask_budget(self.h, nbytes), "debug_join_mask_budget")
 
-    def debug_knn_trace(self, cap_blocks=4096):
-        """Phase timestamps (100 MHz) of the last MODE 6 scan: array [nblocks + 1, 8]."""
-        buf = np.zeros(8 * (cap_blocks + 1), dtype=np.uint64)
+    def debug_knn_pass_stats(self):
+        """(entries gathered, of them spilled, kept at or below the k-th bin) of the last kNN pass."""
+        out = np.zeros(3, dtype=np.uint32)
+        self._check(lib.geohip_debug_knn_pass_stats(self.h, out.ctypes.data_as(c_void_p)), "debug_knn_pass_stats")
+        return tuple(int(v) for v in out)
+
+    def debug_knn_pass_trace(self, grid, x, y, qx, qy, r, k, ablation=0):
+        """One traced kNN pass on device x/y: [nblocks, 8] timestamps (100 MHz, 0 = not reached)."""
+        buf = np.zeros(8 * 1024, dtype=np.uint64)
         nb = c_uint32(0)
-        rc = lib.geohip_debug_knn_trace(self.h, buf.ctypes.data_as(c_void_p), len(buf), ctypes.byref(nb))
-        self._check(rc, "debug_knn_trace")
-        return buf[:8 * (nb.value + 1)].reshape(nb.value + 1, 8)
+        self._dev(x, "x")
+        self.set_mem(MEM_DEVICE)
+        rc = lib.geohip_debug_knn_pass_trace(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), x.numel(), qx, qy, r, k,
+                                             ablation, buf.ctypes.data_as(c_void_p), len(buf), ctypes.byref(nb))
+        self._check(rc, "debug_knn_pass_trace")
+        return buf[:8 * nb.value].reshape(nb.value, 8)
 
     def selftest_fp64(self, a, b):
         """Device fp64 primitive bits (test hook): returns (sqrt|a|, a/b, hypot(a,b), a*b-b*b)."""

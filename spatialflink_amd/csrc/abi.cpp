@@ -23,7 +23,7 @@ using namespace geohip;
 
 enum Slot {
     S_X, S_Y, S_QX, S_QY, S_GTHR, S_PART_D, S_PART_I, S_OUT_D, S_OUT_I, S_OUT_CNT,
-    S_MASK, S_UCNT, S_OFFS, S_TOTAL, S_OUT_IDX, S_OUT_PAIRS, S_SPILL_D, S_SPILL_I, S_SPILL_CNT, S_RLB,
+    S_MASK, S_UCNT, S_OFFS, S_TOTAL, S_OUT_IDX, S_OUT_PAIRS, S_SPILL_D, S_SPILL_I, S_SPILL_CNT, S_RLB, S_TRACE,
     S_J0, S_J1, S_J2, S_J3, S_J4, S_J5, S_J6, S_J7, S_J8, S_J9, S_J10, S_J11, S_J12, S_J13, S_J14, S_J15,
     S_J16, S_J17, S_J18, S_J19, S_J20, S_J21, S_J22, S_J23,
     S_I0, S_I1, S_I2, S_I3, S_I4, S_I5, S_I6, S_I7,
@@ -50,6 +50,7 @@ struct geohip_ctx {
     double plan_q[3] = {0, 0, 0};
     PointPlan plan{};
     unsigned long long range_epoch = 0;  // fused range pass: status words of this launch carry it
+    uint64_t join_mask_budget = 4ull << 30;  // join hit masks kept between the passes up to this
 };
 
 namespace {
@@ -177,8 +178,6 @@ int plan_or_fail(geohip_ctx* ctx, const geohip_grid* grid, double qx, double qy,
     return GEOHIP_OK;
 }
 
-int kpl_for(uint32_t k) { return k <= 64 ? 1 : k <= 128 ? 2 : 4; }
-
 KnnArgs make_knn_args(const PointPlan& plan, uint32_t k, double qx, double qy) {
     KnnArgs a;
     memset(&a, 0, sizeof a);
@@ -220,23 +219,21 @@ int knn_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const
     const double *dx, *dy;
     rc = stage_xy(ctx, x, y, n, S_X, S_Y, &dx, &dy);
     if (rc) return rc;
-    const int kpl = kpl_for(k);
-    unsigned geo_blocks = 0;
-    uint64_t chunk = 0;
-    knn_geometry(n, &geo_blocks, &chunk);
-    const uint64_t nblocks = a.nu > 0 ? geo_blocks : 0;  // empty G u C: no candidates
-    const uint64_t N = 64ull * kpl;
-    rc = ensure(ctx, S_PART_D, nblocks * (N + 4) * 8);  // block lists, then the packed heads (kHeads = 4)
-    if (!rc) rc = ensure(ctx, S_PART_I, nblocks * (N + 4) * 4);
+    unsigned nb = 0;
+    uint64_t ch = 0;
+    knn_pass_geometry(n, &nb, &ch);
+    const size_t ents = knn_pass_list_entries(nb ? nb : 1);
+    rc = ensure(ctx, S_PART_D, ents * 8);
+    if (!rc) rc = ensure(ctx, S_PART_I, ents * 4);
     if (!rc) rc = ensure(ctx, S_SPILL_D, n * 8);  // worst case: every point survives
     if (!rc) rc = ensure(ctx, S_SPILL_I, n * 4);
     if (!rc) rc = ensure_zeroed(ctx, S_SPILL_CNT, kKnnCounterBytes);
     if (rc) return rc;
     hipEvent_t e0, e1;
     timing_events(ctx, &e0, &e1);
-    hipError_t e = launch_knn(dx, dy, n, a, kpl, B<unsigned long long>(ctx, S_PART_D), B<unsigned>(ctx, S_PART_I),
-                              (unsigned)nblocks, chunk, out_d, out_i, out_cnt, B<unsigned long long>(ctx, S_SPILL_D),
-                              B<unsigned>(ctx, S_SPILL_I), B<unsigned>(ctx, S_SPILL_CNT), ctx->stream, e0, e1);
+    hipError_t e = launch_knn_pass(dx, dy, n, a, B<unsigned long long>(ctx, S_PART_D), B<unsigned>(ctx, S_PART_I),
+                                   B<unsigned long long>(ctx, S_SPILL_D), B<unsigned>(ctx, S_SPILL_I),
+                                   B<unsigned>(ctx, S_SPILL_CNT), out_d, out_i, out_cnt, ctx->stream, e0, e1);
     if (e != hipSuccess) return hip_fail(ctx, e, "knn launch");
     return GEOHIP_OK;
 }
@@ -483,7 +480,10 @@ int geohip_knn_merge_async(geohip_ctx* ctx, const double* dist, const uint32_t* 
     int rc = begin(ctx);
     if (rc) return rc;
     if (ctx->mem != GEOHIP_MEM_DEVICE) return fail(ctx, GEOHIP_ERR_ARG, "async forms need GEOHIP_MEM_DEVICE");
-    if (k == 0 || k > GEOHIP_KNN_MAX_K) return fail(ctx, GEOHIP_ERR_ARG, "bad k");
+    if (k == 0) return fail(ctx, GEOHIP_ERR_ARG, "k must be > 0");
+    if (k > GEOHIP_KNN_MAX_K) return fail(ctx, GEOHIP_ERR_UNSUPPORTED, "k > GEOHIP_KNN_MAX_K");
+    if (k > 256 && (uint64_t)nlists * list_len > 8192)
+        return fail(ctx, GEOHIP_ERR_UNSUPPORTED, "merge of more than 8192 entries with k > 256");
     if (!dist || !idx || !out_idx || !out_dist || !out_count_dev) return fail(ctx, GEOHIP_ERR_ARG, "null pointer");
     hipError_t e = launch_knn_merge(reinterpret_cast<const unsigned long long*>(dist), idx, nlists, list_len, k,
                                     out_dist, out_idx, out_count_dev, ctx->stream);
@@ -567,99 +567,6 @@ int geohip_synth_uniform_async(geohip_ctx* ctx, double* x, double* y, uint64_t n
     return GEOHIP_OK;
 }
 
-static unsigned long long* g_trace_dev = nullptr;  // MODE 6 phase timestamps (debug only)
-static size_t g_trace_words = 0;
-static unsigned g_trace_blocks = 0;
-
-// Measurement hook: the phase timestamps of the last MODE 6 launch (8 u64 per block, then the
-// final selection's 8), 100 MHz clock; *nblocks = blocks of that launch.
-int geohip_debug_knn_trace(geohip_ctx* ctx, uint64_t* host, uint64_t cap_words, unsigned* nblocks) {
-    int rc = begin(ctx);
-    if (rc) return rc;
-    if (!g_trace_dev) return fail(ctx, GEOHIP_ERR_ARG, "no traced launch");
-    const size_t words = 8 * ((size_t)g_trace_blocks + 1);
-    if (cap_words < words) return fail(ctx, GEOHIP_ERR_CAPACITY, "trace buffer too small");
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    HIPCHK(hipMemcpy(host, g_trace_dev, words * 8, hipMemcpyDeviceToHost));
-    *nblocks = g_trace_blocks;
-    return GEOHIP_OK;
-}
-
-// Measurement hook (not part of the operator surface): time `reps` launches of a kNN scan
-// ablation variant (0 full .. 3, see knn_scan) with events on the ctx stream; device memory.
-int geohip_debug_knn_scan_variant(geohip_ctx* ctx, int mode, const geohip_grid* grid, const double* x,
-                                  const double* y, uint64_t n, int nwin, double qx, double qy, double r, uint32_t k,
-                                  int reps, double* ms_per_launch) {
-    int rc = begin(ctx);
-    if (rc) return rc;
-    PointPlan plan;
-    rc = plan_or_fail(ctx, grid, qx, qy, r, &plan);
-    if (rc) return rc;
-    KnnArgs a = make_knn_args(plan, k, qx, qy);
-    unsigned nblocks = 0;
-    uint64_t chunk = 0;
-    knn_geometry(n, &nblocks, &chunk);
-    rc = ensure(ctx, S_PART_D, nblocks * (64 + 4) * 8);
-    if (!rc) rc = ensure(ctx, S_PART_I, nblocks * (64 + 4) * 4);
-    if (!rc) rc = ensure(ctx, S_SPILL_D, n * 8);
-    if (!rc) rc = ensure(ctx, S_SPILL_I, n * 4);
-    if (!rc) rc = ensure_zeroed(ctx, S_SPILL_CNT, kKnnCounterBytes);
-    if (!rc) rc = ensure(ctx, S_OUT_D, (size_t)(k ? k : 1) * 8);
-    if (!rc) rc = ensure(ctx, S_OUT_I, (size_t)(k ? k : 1) * 4);
-    if (!rc) rc = ensure(ctx, S_OUT_CNT, 8);
-    if (rc) return rc;
-    if (mode == 6) {  // phase timestamps: trace buffer for this launch shape
-        const size_t words = 8 * ((size_t)nblocks + 1);
-        if (words > g_trace_words) {
-            if (g_trace_dev) (void)hipFree(g_trace_dev);
-            g_trace_dev = nullptr;
-            g_trace_words = 0;
-            HIPCHK(hipMalloc(&g_trace_dev, words * 8));
-            g_trace_words = words;
-        }
-        HIPCHK(hipMemsetAsync(g_trace_dev, 0, words * 8, ctx->stream));
-        HIPCHK(set_knn_trace(g_trace_dev));
-        g_trace_blocks = nblocks;
-    }
-    unsigned long long* sd = B<unsigned long long>(ctx, S_SPILL_D);
-    unsigned* si = B<unsigned>(ctx, S_SPILL_I);
-    unsigned* sc = B<unsigned>(ctx, S_SPILL_CNT);
-    double* od = B<double>(ctx, S_OUT_D);
-    unsigned* oi = B<unsigned>(ctx, S_OUT_I);
-    unsigned* oc = B<unsigned>(ctx, S_OUT_CNT);
-    hipEvent_t e0, e1;
-    HIPCHK(hipEventCreate(&e0));
-    HIPCHK(hipEventCreate(&e1));
-    HIPCHK(launch_knn_scan_variant(mode, x, y, n, a, B<unsigned long long>(ctx, S_PART_D), B<unsigned>(ctx, S_PART_I),
-                                   (unsigned)nblocks, chunk, sd, si, sc, od, oi, oc, ctx->stream));
-    HIPCHK(hipEventRecord(e0, ctx->stream));
-    for (int i = 0; i < reps; i++) {
-        const uint64_t w = (uint64_t)(i % (nwin > 0 ? nwin : 1)) * n;  // cycle windows: no Infinity-Cache reuse
-        HIPCHK(launch_knn_scan_variant(mode, x + w, y + w, n, a, B<unsigned long long>(ctx, S_PART_D),
-                                       B<unsigned>(ctx, S_PART_I), (unsigned)nblocks, chunk, sd, si, sc, od, oi, oc, ctx->stream));
-    }
-    HIPCHK(hipEventRecord(e1, ctx->stream));
-    HIPCHK(hipEventSynchronize(e1));
-    float ms = 0.f;
-    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
-    *ms_per_launch = ms / (reps > 0 ? reps : 1);
-    HIPCHK(hipMemsetAsync(sc, 0, kKnnCounterBytes, ctx->stream));  // list-only modes leave spill counts behind
-    if (mode == 5) {  // counters of one extra launch: sorts and passing candidates, summed
-        HIPCHK(hipMemsetAsync(ctx->buf[S_PART_I], 0, 8, ctx->stream));
-        HIPCHK(launch_knn_scan_variant(mode, x, y, n, a, B<unsigned long long>(ctx, S_PART_D),
-                                       B<unsigned>(ctx, S_PART_I), (unsigned)nblocks, chunk, sd, si, sc, od, oi, oc, ctx->stream));
-        unsigned c[2];
-        HIPCHK(hipMemcpy(&c[1], sc, 4, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemsetAsync(sc, 0, 4, ctx->stream));
-        HIPCHK(hipMemcpy(c, ctx->buf[S_PART_I], 4, hipMemcpyDeviceToHost));
-        ms_per_launch[1] = c[0];
-        ms_per_launch[2] = c[1];
-    }
-    return GEOHIP_OK;
-}
-
 // Test hook (host only): classify points with the planner's exact boxes, exactly as the
 // kernels do: out[i] = inG | inC << 1 | inU << 2.
 static inline bool host_in_box(const Box& b, double x, double y) {
@@ -697,12 +604,62 @@ int geohip_debug_selftest_fp64(geohip_ctx* ctx, const double* a, const double* b
     return GEOHIP_OK;
 }
 
-// Debug hook: 1 = final selection fused into the scan (default), 0 = separate knn_final launch.
-void geohip_debug_set_knn_fused(int fused) { set_knn_fused(fused); }
-void geohip_debug_set_range_mode(int mode) { set_range_mode(mode); }
-void geohip_debug_set_join_mask_budget(uint64_t bytes) { set_join_mask_budget(bytes); }
-int geohip_debug_set_knn_config(int waves_per_block, int prefetch, int ticket_groups, int epi_sort, int interleave) {
-    return set_knn_config(waves_per_block, prefetch, ticket_groups, epi_sort, interleave) ? GEOHIP_ERR_ARG : GEOHIP_OK;
+// Measurement hook: counters of the last kNN pass's final selection (entries gathered, spilled,
+// kept at or below the k-th bin), read back after a synchronise.
+int geohip_debug_knn_pass_stats(geohip_ctx* ctx, uint32_t* out3) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    if (!ctx->buf[S_SPILL_CNT]) return fail(ctx, GEOHIP_ERR_ARG, "no kNN pass ran");
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipMemcpy(out3, B<char>(ctx, S_SPILL_CNT) + kKnnCounterBytes - 64, 12, hipMemcpyDeviceToHost));
+    return GEOHIP_OK;
+}
+
+// Measurement hook: one kNN pass (device memory) with per-block phase timestamps (100 MHz):
+// host[8 b + s], s = start, stream end, flush, stores drained, arrived; the last block also
+// acquired, gathered, written.  *nblocks = blocks of the launch.
+int geohip_debug_knn_pass_trace(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
+                                uint64_t n, double qx, double qy, double r, uint32_t k, int ablation, uint64_t* host,
+                                uint64_t cap_words, unsigned* nblocks) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    PointPlan plan;
+    rc = plan_or_fail(ctx, grid, qx, qy, r, &plan);
+    if (rc) return rc;
+    KnnArgs a = make_knn_args(plan, k, qx, qy);
+    unsigned nb = 0;
+    uint64_t ch = 0;
+    knn_pass_geometry(n, &nb, &ch);
+    if (cap_words < 8ull * nb) return fail(ctx, GEOHIP_ERR_CAPACITY, "trace buffer too small");
+    const size_t ents = knn_pass_list_entries(nb ? nb : 1);
+    rc = ensure(ctx, S_PART_D, ents * 8);
+    if (!rc) rc = ensure(ctx, S_PART_I, ents * 4);
+    if (!rc) rc = ensure(ctx, S_SPILL_D, n * 8);
+    if (!rc) rc = ensure(ctx, S_SPILL_I, n * 4);
+    if (!rc) rc = ensure_zeroed(ctx, S_SPILL_CNT, kKnnCounterBytes);
+    if (!rc) rc = ensure(ctx, S_OUT_D, (size_t)k * 8);
+    if (!rc) rc = ensure(ctx, S_OUT_I, (size_t)k * 4);
+    if (!rc) rc = ensure(ctx, S_OUT_CNT, 8);
+    if (!rc) rc = ensure(ctx, S_TRACE, 8ull * nb * 8);
+    if (rc) return rc;
+    unsigned long long* tr = B<unsigned long long>(ctx, S_TRACE);
+    HIPCHK(hipMemsetAsync(tr, 0, 8ull * nb * 8, ctx->stream));
+    hipError_t e = launch_knn_pass(x, y, n, a, B<unsigned long long>(ctx, S_PART_D), B<unsigned>(ctx, S_PART_I),
+                                   B<unsigned long long>(ctx, S_SPILL_D), B<unsigned>(ctx, S_SPILL_I),
+                                   B<unsigned>(ctx, S_SPILL_CNT), B<double>(ctx, S_OUT_D), B<unsigned>(ctx, S_OUT_I),
+                                   B<unsigned>(ctx, S_OUT_CNT), ctx->stream, nullptr, nullptr, tr, ablation);
+    if (e != hipSuccess) return hip_fail(ctx, e, "knn pass launch");
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipMemcpy(host, tr, 8ull * nb * 8, hipMemcpyDeviceToHost));
+    *nblocks = nb;
+    return GEOHIP_OK;
+}
+
+// Test hook: byte budget of this ctx's join hit masks (beyond it the write pass recomputes).
+int geohip_debug_ctx_join_mask_budget(geohip_ctx* ctx, uint64_t bytes) {
+    if (!ctx) return GEOHIP_ERR_ARG;
+    ctx->join_mask_budget = bytes;
+    return GEOHIP_OK;
 }
 
 }  // extern "C"
@@ -721,6 +678,7 @@ int ctx_ensure_ingest(geohip_ctx* ctx, int slot, size_t bytes, void** out) {
     return rc;
 }
 int ctx_begin(geohip_ctx* ctx) { return begin(ctx); }
+uint64_t ctx_join_mask_budget(geohip_ctx* ctx) { return ctx->join_mask_budget; }
 hipStream_t ctx_stream(geohip_ctx* ctx) { return ctx->stream; }
 int ctx_mem(geohip_ctx* ctx) { return ctx->mem; }
 uint64_t* ctx_pinned(geohip_ctx* ctx) { return ctx->pinned; }

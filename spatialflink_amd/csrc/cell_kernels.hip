@@ -1878,7 +1878,6 @@ enum JSlot {
 };
 
 // join hit masks larger than this fall back to a recomputing write pass (debug hook: settable)
-uint64_t g_join_mask_budget = 4ull << 30;
 
 // J_MISC words: [0] outside count, [1] outside cursor, [2] scan grand total, [3] global
 // query count, [8..9] pair total (u64)
@@ -2046,7 +2045,6 @@ void screen_bounds(double r, double* r2lo, double* r2hi) {
 }  // namespace
 
 void pp_screen_bounds(double r, double* r2lo, double* r2hi) { screen_bounds(r, r2lo, r2hi); }
-void set_join_mask_budget(uint64_t bytes) { g_join_mask_budget = bytes; }
 
 int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, const double* dx, const double* dy,
                  uint64_t nd, const double* qx, const double* qy, uint64_t nq, double r, int approximate,
@@ -2165,7 +2163,7 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
         uint64_t nwords = 0;
         rc = read_total(ctx, moff + geo.ntiles, &nwords);
         if (rc) return rc;
-        if (nwords * 8 <= g_join_mask_budget) {
+        if (nwords * 8 <= ctx_join_mask_budget(ctx)) {
             mask = S.get<unsigned long long>(J_PMASK, nwords * 8 + 8);
             if (S.rc) return S.rc;
         }
@@ -2569,7 +2567,8 @@ int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, co
                    uint32_t* out_idx, double* out_dist, uint32_t* out_count) {
     if (!out_idx || !out_dist || !out_count) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null output");
     *out_count = 0;
-    if (k == 0 || k > GEOHIP_KNN_MAX_K) return ctx_fail(ctx, GEOHIP_ERR_ARG, "k must be in [1, 256]");
+    if (k == 0) return ctx_fail(ctx, GEOHIP_ERR_ARG, "k must be > 0");
+    if (k > GEOHIP_KNN_PPOLY_MAX_K) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "k > GEOHIP_KNN_PPOLY_MAX_K");
     int rc = check_grid_basic(ctx, grid, "grid");
     if (rc) return rc;
     if (n >= 0xffffffffull) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "window larger than 2^32-1 points");

@@ -317,6 +317,24 @@ __device__ __forceinline__ void rank_place(const unsigned long long* d, const un
         if (g == 0 && t < m && r < limit) put(r, kd, ki);
         return;
     }
+    if (NT >= 1024 && m <= 256) {
+        // 4 lanes per key (one DPP quad), each counting the smaller keys among every 4th
+        constexpr int G = 4;
+        const unsigned t = threadIdx.x / G, g = threadIdx.x % G;
+        unsigned r = 0;
+        unsigned long long kd = 0;
+        unsigned ki = 0;
+        if (t < m) {
+            kd = d[t];
+            ki = ix[t];
+#pragma unroll 8
+            for (unsigned j = g; j < m; j += G) r += rank_less(d[j], ix[j], j, kd, ki, t);
+        }
+        r += xor_lane(r, 1);
+        r += xor_lane(r, 2);
+        if (g == 0 && t < m && r < limit) put(r, kd, ki);
+        return;
+    }
     for (unsigned t = threadIdx.x; t < m; t += NT) {
         const unsigned long long kd = d[t];
         const unsigned ki = ix[t];
@@ -656,26 +674,6 @@ __global__ __launch_bounds__(kFinalThreads) void knn_final(FinalIo io) {
     final_select<KPL, kFinalThreads, 1>(io, s);
 }
 
-// Where a scan writes its result.  ticket != null: the block lists are stored write-through
-// (sc1) and the last block to arrive runs final_select into out_* (one launch per window);
-// ticket == null: only the block lists are written (knn_final merges them).
-// Arrival is counted in two levels so no counter sees more than ~max(G, nblocks/G) atomics
-// (one device-scope counter taking every block's atomic costs ~11-13 ns per arrival,
-// MI355X_MICROARCH.md "fanin"): block b counts on group counter b % G; the last arriver of
-// a group counts on the top counter; the last of those runs the final selection.  Counters
-// sit 128 B apart (ticket[32 g], top at ticket[32 G]) and are re-zeroed by their last user.
-struct KnnOut {
-    double* out_d;
-    unsigned* out_i;
-    unsigned* out_count;
-    unsigned* ticket;  // zero before the first launch
-    unsigned groups;   // G >= 1
-    unsigned* ghist;   // head histogram of the final selection (zero before the launch)
-    int epi_sort;      // block list by a register sort (fc <= 64, KPL 1) instead of rank placement
-};
-static_assert(kTicketStride * (kMaxTicketGroups + 2) <= kGhistWord, "counter scratch layout");
-static_assert((kGhistWord + kGhistCopies * kHistBins) * 4 <= kKnnCounterBytes, "counter scratch layout");
-
 __device__ __forceinline__ unsigned ticket_add(unsigned* p) {
     return __hip_atomic_fetch_add(((gu32*)(p)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -683,72 +681,370 @@ __device__ __forceinline__ void ticket_zero(unsigned* p) {
     __hip_atomic_store(((gu32*)(p)), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// one lane: true for the block that arrives last
-__device__ __forceinline__ bool arrive_last(const KnnOut& out) {
-    const unsigned G = out.groups;
+
+// ======================================================================== kNN pass ========
+// One launch per window (PointPointKNNQuery.java:125-191 + the windowAll
+// merge KNNQuery.java:204-272).  The stream phase is knn_scan's: exact box classification,
+// squared screen against the block bound, LDS-staged fdlibm distances, survivors and a 512-bin
+// distance histogram in LDS (B = upper edge of the bin where the block's cumulative count
+// reaches k: at least k real points at or below it).  At its end a block
+//  * writes its survivors <= B to its list slot unsorted (ballot + LDS cursor, write-through),
+//  * writes its 4 smallest sorted (heads, packed for coalesced reads) and its list length,
+// and takes a 2-level arrival ticket.  The last block to arrive (Guideline 16 counter hand-off)
+// loads the 4 heads of every block, takes T = upper edge of the bin where their cumulative count
+// reaches k (>= k real points at or below it, so T bounds the window's k-th key), keeps the
+// heads <= T, reads the whole list of the rare block whose 4 heads all pass, places the kept
+// entries by rank and writes the k smallest.  No separate final launch, no sorted block lists.
+constexpr int kPassNW = 16;                     // waves per block
+constexpr unsigned kPassMaxBlocks = 256;        // one block per CU
+constexpr unsigned kPassHeads = 8;
+constexpr unsigned kLenWhole = 0x80000000u;     // list length flag: heads incomplete, read it whole
+constexpr unsigned kStatWord = (unsigned)(kKnnCounterBytes / 4) - 16;  // last final: entries, spilled, kept
+
+template <int NW>
+struct PassBlock {
+    static constexpr int kCap = 192 * NW;
+    unsigned hist[kHistBins];   // survivor distances (local bound)
+    unsigned long long bd[kCap];
+    unsigned bi[kCap];
+    unsigned long long bound;   // block bound, distance bits
+    unsigned long long top_d[kWave];  // kept survivors <= hcap (the head candidates)
+    unsigned top_i[kWave];
+    unsigned long long hcap;    // 4th bin edge: the block's 4 smallest lie at or below it
+    unsigned cnt;               // survivors appended (may exceed kCap: the rest spilled)
+    unsigned next_it;
+    unsigned nsmall;
+    unsigned cursor, last;
+    unsigned fin[4];            // the final's LDS words
+};
+
+struct PassIo {
+    unsigned long long* list_d;  // block b: [b * list_cap, b * list_cap + len[b])
+    unsigned* list_i;
+    unsigned list_cap;
+    unsigned long long* head_d;  // block b: [kPassHeads * b, + kPassHeads), sentinel-padded
+    unsigned* head_i;
+    unsigned* len;               // nblocks list lengths
+    unsigned long long* spill_d;
+    unsigned long long* spill_d_unused;
+    unsigned* spill_i;
+    unsigned* ctr;               // zeroed scratch: [0] spill count, tickets from kTicketStride
+    double* out_d;
+    unsigned* out_i;
+    unsigned* out_count;
+    unsigned groups;
+    unsigned long long* trace;   // measurement only: 8 timestamps per block (null in production)
+};
+#define PASS_TRACE(io, slot)                                                                      \
+    do {                                                                                          \
+        if ((io).trace && threadIdx.x == 0) (io).trace[8 * (size_t)blockIdx.x + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+
+// exact distances of up to 64 staged candidates; survivors (<= the block bound) appended to the
+// block buffer and its histogram
+template <class PB>
+__device__ __forceinline__ void pass_dist_batch(WaveStage& st, unsigned& ccnt, PB& kb, const KnnArgs& a,
+                                                const PassIo& io, unsigned& appended, bool partial) {
+    const int lane = lane_id();
+    while (ccnt >= 64 || (partial && ccnt > 0)) {
+        const unsigned take = ccnt >= 64 ? 64u : ccnt;
+        const unsigned from = ccnt - take;
+        bool ok = (unsigned)lane < take;
+        double px = 0.0, py = 0.0;
+        unsigned pi = 0;
+        if (ok) {
+            px = st.cx[from + lane];
+            py = st.cy[from + lane];
+            pi = st.ci[from + lane];
+        }
+        const unsigned long long B = lds_fresh(kb.bound);
+        wave_lds_sync();
+        ccnt = from;
+        const double d = jts_pp_distance(a.qx, a.qy, px, py);
+        const unsigned long long db = (unsigned long long)__double_as_longlong(d);
+        ok = ok && db <= B;
+        const unsigned long long m = __ballot(ok);
+        if (m) {
+            const unsigned nm = (unsigned)__popcll(m);
+            unsigned pos = 0;
+            if (lane == 0) pos = atomicAdd(&kb.cnt, nm);
+            pos = __shfl(pos, 0);
+            const unsigned slot = pos + lanes_below(m);
+            unsigned gbase = 0;
+            if (pos + nm > (unsigned)PB::kCap) {  // spill the overflow to global memory (rare)
+                const unsigned first = pos > (unsigned)PB::kCap ? pos : (unsigned)PB::kCap;
+                if (lane == 0) gbase = atomicAdd(&io.ctr[0], pos + nm - first);
+                gbase = __shfl(gbase, 0) - (first - pos);
+            }
+            if (ok) {
+                if (slot < (unsigned)PB::kCap) {
+                    kb.bd[slot] = db;
+                    kb.bi[slot] = pi;
+                } else {
+                    store_wt(&io.spill_d[gbase + (slot - pos)], db);
+                    store_wt(&io.spill_i[gbase + (slot - pos)], pi);
+                }
+                atomicAdd(&kb.hist[hist_bin(db, a.hist_base)], 1u);
+            }
+            appended += nm;
+        }
+        wave_lds_sync();
+    }
+}
+
+// wave min of (d, i) keys; every lane gets the result
+__device__ __forceinline__ void wave_kmin(unsigned long long& d, unsigned& i) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long od = xor_lane64(d, o);
+        const unsigned oi = xor_lane(i, o);
+        if (od < d || (od == d && oi < i)) {
+            d = od;
+            i = oi;
+        }
+    }
+}
+
+// The window's k smallest, run by the last block (NT = 1024 threads).  Latency-bound: every
+// dependent LDS round trip costs ~35 ns and a global one ~1 us, so the phases are few and wide:
+//   A  loads: every block's 8 packed heads (2 per thread), its list length and last head (thread
+//      b stands for block b), the spill count;
+//   B  the heads' distance histogram (LDS atomics) and, per block, "read whole": its 8th head
+//      beats T or its heads are flagged incomplete -- known only after T, so the blocks' last
+//      heads go to LDS;
+//   C  one wave: T = upper edge of the bin where the heads' cumulative count reaches k (k real
+//      points at or below it: T bounds the window's k-th key; none if fewer than k heads);
+//   D  gather the heads <= T of the blocks not read whole, the whole lists (rare), the spill
+//      (ballot + one LDS atomic per wave and batch), then rank placement and the k smallest.
+template <int NT>
+__device__ __forceinline__ void pass_final(const PassIo& io, const KnnArgs& a, unsigned long long* gd, unsigned* gi,
+                                           unsigned gcap, unsigned* hist, unsigned* sh,
+                                           unsigned long long* blast_sh, unsigned* lens, unsigned* wl) {
+    const unsigned k = a.k, nb = gridDim.x;
+    const int lane = lane_id(), wid = threadIdx.x / kWave;
+    constexpr unsigned kPer = kPassMaxBlocks * kPassHeads / NT;
+    static_assert(kPer == 2, "final: 2 heads per thread");
+    // ---- A: loads up front
+    const unsigned nspill = load_sc1(io.ctr);
+    unsigned long long hd[kPer];
+    unsigned hi[kPer];
+#pragma unroll
+    for (unsigned u = 0; u < kPer; u++) {
+        const unsigned t = threadIdx.x + u * NT;
+        const bool ok = t < kPassHeads * nb;
+        hd[u] = ok ? io.head_d[t] : kSentinelD;
+        hi[u] = ok ? io.head_i[t] : kSentinelI;
+    }
+    const bool blk = threadIdx.x < nb;  // thread b also stands for block b
+    const unsigned mylen = blk ? io.len[threadIdx.x] : 0u;
+    const unsigned long long blast = blk ? io.head_d[kPassHeads * threadIdx.x + kPassHeads - 1] : kSentinelD;
+    for (unsigned t = threadIdx.x; t < kHistBins; t += NT) hist[t] = 0;
+    if (threadIdx.x == 0) {
+        sh[0] = 0xffffffffu;  // T bin
+        sh[2] = 0;            // gather cursor
+        sh[3] = 0;            // whole lists
+    }
+    __syncthreads();
+    // ---- B
+#pragma unroll
+    for (unsigned u = 0; u < kPer; u++)
+        if (hd[u] != kSentinelD) atomicAdd(&hist[hist_bin(hd[u], a.hist_base)], 1u);
+    if (blk) {
+        blast_sh[threadIdx.x] = (mylen & kLenWhole) ? 0ull : blast;  // flagged: whole whatever T
+        lens[threadIdx.x] = mylen & ~kLenWhole;
+    }
+    __syncthreads();
+    // ---- C
+    if (wid == 0) {
+        const int bin = hist_kth_bin(hist, k);
+        if (lane == 0 && bin >= 0 && bin < kHistBins - 1) sh[0] = (unsigned)bin;
+    }
+    __syncthreads();
+    const unsigned long long T = sh[0] != 0xffffffffu ? hist_edge((int)sh[0], a.hist_base) : kSentinelD;
+    // ---- D
+    auto take = [&](bool ok, unsigned long long d, unsigned i) {
+        ok = ok && d != kSentinelD && d <= T;
+        const unsigned long long msk = __ballot(ok);
+        if (!msk) return;
+        unsigned base = 0;
+        if (lane == 0) base = atomicAdd(&sh[2], (unsigned)__popcll(msk));
+        base = __shfl(base, 0);
+        const unsigned p = base + lanes_below(msk);
+        if (ok && p < gcap) {
+            gd[p] = d;
+            gi[p] = i;
+        }
+    };
+    if (blk) {
+        const unsigned long long bl = blast_sh[threadIdx.x];
+        if (bl != kSentinelD && bl <= T) wl[atomicAdd(&sh[3], 1u)] = threadIdx.x;  // rare
+    }
+#pragma unroll
+    for (unsigned u = 0; u < kPer; u++) {
+        const unsigned t = threadIdx.x + u * NT;
+        const unsigned b = t / kPassHeads;
+        bool part = b < nb;
+        if (part) {
+            const unsigned long long bl = blast_sh[b];
+            part = !(bl != kSentinelD && bl <= T);
+        }
+        take(part, hd[u], hi[u]);
+    }
+    __syncthreads();
+    const unsigned nwhole = sh[3];
+    for (unsigned w = (unsigned)wid; w < nwhole; w += NT / kWave) {  // one wave per whole list
+        const unsigned b = wl[w];
+        const unsigned L = lens[b];
+        for (unsigned q0 = 0; q0 < L; q0 += kWave) {
+            const unsigned q = q0 + (unsigned)lane;
+            unsigned long long d = kSentinelD;
+            unsigned i = kSentinelI;
+            if (q < L) {
+                d = io.list_d[(size_t)b * io.list_cap + q];
+                i = io.list_i[(size_t)b * io.list_cap + q];
+            }
+            take(q < L, d, i);
+        }
+    }
+    for (unsigned t0 = 0; t0 < nspill; t0 += NT) {
+        const unsigned t = t0 + threadIdx.x;
+        unsigned long long d = kSentinelD;
+        unsigned i = kSentinelI;
+        if (t < nspill) {
+            d = io.spill_d[t];
+            i = io.spill_i[t];
+        }
+        take(t < nspill, d, i);
+    }
+    __syncthreads();
+    const unsigned m = sh[2];
+    if (threadIdx.x == 0) {
+        io.ctr[kStatWord] = nwhole;
+        io.ctr[kStatWord + 1] = nspill;
+        io.ctr[kStatWord + 2] = m;
+    }
+    PASS_TRACE(io, 6);
+    auto put = [&](unsigned pos, unsigned long long d, unsigned i) {
+        io.out_d[pos] = __longlong_as_double((long long)d);
+        io.out_i[pos] = i;
+    };
+    unsigned outn = m < k ? m : k;
+    if (m <= 2u * NT) {
+        rank_place<NT>(gd, gi, m, k, put);
+    } else if (m <= gcap) {  // many exact ties around T: bitonic sort in LDS
+        unsigned p2 = 1;
+        while (p2 < m) p2 <<= 1;
+        for (unsigned t = threadIdx.x + m; t < p2; t += NT) {
+            gd[t] = kSentinelD;
+            gi[t] = kSentinelI;
+        }
+        __syncthreads();
+        block_sort_lds(gd, gi, (int)p2);
+        for (unsigned t = threadIdx.x; t < outn; t += NT) put(t, gd[t], gi[t]);
+    } else {
+        // pathological (more entries at or below T than LDS holds, e.g. a window of identical
+        // points): k rounds of "smallest key above the previous one" over every list and the spill
+        const size_t nl = (size_t)nb * io.list_cap;
+        unsigned long long prev_d = 0;
+        unsigned prev_i = 0;
+        bool have_prev = false;
+        unsigned got = 0;
+        for (unsigned r = 0; r < k; r++) {
+            unsigned long long best_d = kSentinelD;
+            unsigned best_i = kSentinelI;
+            for (size_t t = threadIdx.x; t < nl + nspill; t += NT) {
+                unsigned long long ed = kSentinelD;
+                unsigned ei = kSentinelI;
+                if (t < nl) {
+                    if (t % io.list_cap < (io.len[t / io.list_cap] & ~kLenWhole)) {
+                        ed = io.list_d[t];
+                        ei = io.list_i[t];
+                    }
+                } else {
+                    ed = io.spill_d[t - nl];
+                    ei = io.spill_i[t - nl];
+                }
+                if (ed == kSentinelD) continue;
+                if (have_prev && !lds_kless(prev_d, prev_i, ed, ei)) continue;
+                if (lds_kless(ed, ei, best_d, best_i)) {
+                    best_d = ed;
+                    best_i = ei;
+                }
+            }
+            __syncthreads();
+            gd[threadIdx.x] = best_d;
+            gi[threadIdx.x] = best_i;
+            __syncthreads();
+            for (int h = NT / 2; h > 0; h >>= 1) {
+                if ((int)threadIdx.x < h && lds_kless(gd[threadIdx.x + h], gi[threadIdx.x + h], gd[threadIdx.x], gi[threadIdx.x])) {
+                    gd[threadIdx.x] = gd[threadIdx.x + h];
+                    gi[threadIdx.x] = gi[threadIdx.x + h];
+                }
+                __syncthreads();
+            }
+            prev_d = gd[0];
+            prev_i = gi[0];
+            if (prev_d == kSentinelD) break;
+            have_prev = true;
+            if (threadIdx.x == 0) put(r, prev_d, prev_i);
+            got = r + 1;
+        }
+        outn = got;
+    }
+    for (unsigned t = outn + threadIdx.x; t < k; t += NT) put(t, kSentinelD, kSentinelI);
+    if (threadIdx.x == 0) {
+        *io.out_count = outn;
+        store_wt(io.ctr, 0u);  // spill count re-armed for the next window on this stream
+    }
+}
+
+__device__ __forceinline__ bool pass_arrive_last(unsigned* tickets, unsigned G) {
     const unsigned nb = gridDim.x;
     if (G <= 1) {
-        const bool last = ticket_add(out.ticket) == nb - 1;
-        if (last) ticket_zero(out.ticket);
+        const bool last = ticket_add(tickets) == nb - 1;
+        if (last) ticket_zero(tickets);
         return last;
     }
     const unsigned g = blockIdx.x % G;
     const unsigned members = nb / G + (g < nb % G ? 1u : 0u);
-    unsigned* gc = out.ticket + (size_t)kTicketStride * g;
+    unsigned* gc = tickets + (size_t)kTicketStride * g;
     if (ticket_add(gc) != members - 1) return false;
     ticket_zero(gc);
     const unsigned geff = nb < G ? nb : G;
-    unsigned* top = out.ticket + (size_t)kTicketStride * G;
+    unsigned* top = tickets + (size_t)kTicketStride * G;
     const bool last = ticket_add(top) == geff - 1;
     if (last) ticket_zero(top);
     return last;
 }
 
-// MODE (ablation builds for measurement only; the product launches MODE 0):
-//   0 full, 1 loads only, 2 loads + classification, 3 + LDS staging and distances (no selection),
-//   5 full + counters (survivors, spilled), 6 full + phase timestamps (g_knn_trace),
-//   7 full without the end-of-block selection, 10 full without the final selection (arrival
-//   protocol only), 11 full without the final selection's output writes
-template <int KPL, int NW, int PF, int MODE = 0>
-__global__ __launch_bounds__(NW * 64) void knn_scan(const double* __restrict__ x, const double* __restrict__ y,
-                                                    uint64_t n, uint64_t chunk, KnnArgs args,
-                                                    unsigned long long* __restrict__ part_d,
-                                                    unsigned* __restrict__ part_i,
-                                                    unsigned long long* __restrict__ spill_d,
-                                                    unsigned* __restrict__ spill_i, unsigned* __restrict__ spill_cnt,
-                                                    KnnOut out) {
+// ABL (measurement builds only, 0 in the product): bit 0 skips the list stores, bit 1 the heads
+// (4 smallest), bit 2 the end-of-block bound refresh
+template <int NW, int ABL = 0>
+__global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x, const double* __restrict__ y,
+                                                    uint64_t n, uint64_t chunk, KnnArgs args, PassIo io) {
     constexpr int NT = NW * 64;
-    constexpr bool TR = MODE == 6;
-    GEOHIP_TRACE(TR, 8 * blockIdx.x);
-    if (TR && threadIdx.x == 0) {  // where the block runs: HW_ID (cu/sh/se) and XCC_ID
-        g_knn_trace[8 * blockIdx.x + 5] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
-        g_knn_trace[8 * blockIdx.x + 6] = (unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 20);
-    }
-    using KB = KnnBlock<NW>;
-    __shared__ WaveStage stage[NW];
-    __shared__ KB kb;
+    using PB = PassBlock<NW>;
+    __shared__ __attribute__((aligned(16))) WaveStage stage[NW];
+    __shared__ PB kb;
     const int lane = lane_id();
     const int wid = threadIdx.x / kWave;
     WaveStage& st = stage[wid];
-    // chunk > 0: block b owns [b chunk, (b + 1) chunk); chunk == 0: iterations interleaved
-    // over the blocks (block b takes the window's iterations b, b + nblocks, ...)
-    const bool inter = chunk == 0;
-    const uint64_t blk_begin = inter ? 0 : (uint64_t)blockIdx.x * chunk;
-    uint64_t blk_end = inter ? n : blk_begin + chunk;
+    const uint64_t blk_begin = (uint64_t)blockIdx.x * chunk;
+    uint64_t blk_end = blk_begin + chunk;
     if (blk_end > n) blk_end = n;
     for (int t = threadIdx.x; t < kHistBins; t += NT) kb.hist[t] = 0;
     if (threadIdx.x == 0) {
         kb.bound = kSentinelD;
         kb.cnt = 0;
+        kb.cursor = 0;
+        kb.nsmall = 0;
+        kb.next_it = 2 * NW;  // iterations wid and NW + wid start statically
     }
-
+    PASS_TRACE(io, 0);
     const unsigned k = args.k;
+    const unsigned niters = (unsigned)((blk_end - blk_begin + kPtsIter - 1) / kPtsIter);
     unsigned ccnt = 0;
     unsigned appended = 0, last_hist = 0;
-
-    double sink = 0.0;
-    // G u C is one box for a point query (the candidate square contains the guaranteed one),
-    // kept in registers; further boxes (unusual plans) are tested from the kernel arguments
     const Box b0 = args.u[0];
     const int nu = args.nu;
     auto in_union = [&](double px, double py) -> bool {
@@ -757,39 +1053,22 @@ __global__ __launch_bounds__(NW * 64) void knn_scan(const double* __restrict__ x
             for (int b = 1; b < nu; b++) c = c || in_box(args.u[b], px, py);
         return c;
     };
-    // one wave iteration over 256 points (4 per lane) already in registers; FULL: all valid
     auto iter = [&](auto full, const double (&px)[4], const double (&py)[4], const bool (&valid)[4], uint64_t ib) {
         constexpr bool FULL = decltype(full)::value;
-        if (MODE == 1) {
-#pragma unroll
-            for (int s = 0; s < 4; s++) sink += px[s] + py[s];
-            return;
-        }
-        // squared screen against the block bound: only candidates that may beat it reach the
-        // exact fdlibm distance
         double T2 = __builtin_huge_val();
-        if (MODE == 0 || MODE >= 5) {
-            const unsigned long long B = lds_fresh(kb.bound);
-            if (B != kSentinelD) {
-                const double t = __longlong_as_double((long long)B);
-                // below 2^-960 the square leaves the normal range and the margin fails: no screen
-                T2 = __builtin_fmax((t * t) * kSqHi, 0x1.0p-960);
-            }
+        const unsigned long long B = lds_fresh(kb.bound);
+        if (B != kSentinelD) {
+            const double t = __longlong_as_double((long long)B);
+            T2 = __builtin_fmax((t * t) * kSqHi, 0x1.0p-960);
         }
 #pragma unroll
         for (int s = 0; s < 4; s++) {
             bool c = in_union(px[s], py[s]);
             if (!FULL) c = c && valid[s];
-            if (MODE == 0 || MODE >= 5) {
-                const double dx = args.qx - px[s], dy = args.qy - py[s];
-                const double d2 = dx * dx + dy * dy;
-                c = c && !(d2 > T2);
-            }
+            const double dx = args.qx - px[s], dy = args.qy - py[s];
+            const double d2 = dx * dx + dy * dy;
+            c = c && !(d2 > T2);
             const unsigned long long m = __ballot(c);
-            if (MODE == 2) {
-                sink += (double)__popcll(m);
-                continue;
-            }
             if (c) {
                 const unsigned pos = ccnt + lanes_below(m);
                 st.cx[pos] = px[s];
@@ -798,43 +1077,20 @@ __global__ __launch_bounds__(NW * 64) void knn_scan(const double* __restrict__ x
             }
             ccnt += (unsigned)__popcll(m);
         }
-        if (MODE == 2) return;
         wave_lds_sync();
-        if (MODE == 3) {
-            while (ccnt >= 64) {
-                const unsigned from = ccnt - 64;
-                sink += jts_pp_distance(args.qx, args.qy, st.cx[from + lane], st.cy[from + lane]);
-                wave_lds_sync();
-                ccnt = from;
-            }
-            return;
-        }
         if (ccnt >= 64) {
-            knn_dist_batch(st, ccnt, kb, args, spill_d, spill_i, spill_cnt, appended, false);
-            // refresh the block bound once this wave has added survivors
+            pass_dist_batch(st, ccnt, kb, args, io, appended, false);
             if (appended != last_hist && lds_fresh(kb.cnt) >= k) {
                 hist_bound(kb, k, args.hist_base);
                 last_hist = appended;
             }
         }
     };
-    // Iterations (256 points) of the block's chunk are claimed dynamically from an LDS counter:
-    // the memory system serves the 16 waves of a CU unevenly (phase trace: a block's last wave
-    // ended up to 6 us after its first with static striding), so a wave that is served faster
-    // takes more.  Two register sets A and B alternate as a software pipeline: each is refilled
-    // (claim + loads issued) right after use, so two iterations per wave are in flight while
-    // one is classified.  Claims are monotone per wave, so a slot holding an index past the
-    // end stays empty.  A partial iteration (only the window's last one) loads bounds-checked.
     const std::integral_constant<bool, true> kFull;
     const std::integral_constant<bool, false> kPart;
     const bool all_valid[4] = {true, true, true, true};
     double ax[4], ay[4], bx[4], by[4];
-    const uint64_t n_it = (n + kPtsIter - 1) / kPtsIter;
-    const unsigned niters = inter ? (blockIdx.x < n_it ? (unsigned)((n_it - blockIdx.x + gridDim.x - 1) / gridDim.x) : 0u)
-                                  : (unsigned)((blk_end - blk_begin + kPtsIter - 1) / kPtsIter);
-    auto it_base = [&](unsigned it) {
-        return inter ? ((uint64_t)it * gridDim.x + blockIdx.x) * kPtsIter : blk_begin + (uint64_t)it * kPtsIter;
-    };
+    auto it_base = [&](unsigned it) { return blk_begin + (uint64_t)it * kPtsIter; };
     auto is_full = [&](unsigned it) { return it_base(it) + kPtsIter <= blk_end; };
     auto load_full = [&](unsigned it, double (&px)[4], double (&py)[4]) {
         const uint64_t i0 = it_base(it) + 2 * (uint64_t)lane;
@@ -860,138 +1116,122 @@ __global__ __launch_bounds__(NW * 64) void knn_scan(const double* __restrict__ x
             iter(kPart, qx4, qy4, valid, it_base(it));
         }
     };
-    if (threadIdx.x == 0) kb.next_it = 2 * NW;  // iterations wid and NW + wid start statically
-    unsigned ia = (unsigned)wid, ib = (unsigned)(NW + wid);
+    unsigned ia = (unsigned)wid, ibb = (unsigned)(NW + wid);
     if (ia < niters && is_full(ia)) load_full(ia, ax, ay);
-    if (ib < niters && is_full(ib)) load_full(ib, bx, by);
+    if (ibb < niters && is_full(ibb)) load_full(ibb, bx, by);
     __syncthreads();
-    while (ia < niters || ib < niters) {
+    while (ia < niters || ibb < niters) {
         if (ia < niters) {
             const unsigned na = claim();
             run(ia, ax, ay);
             ia = na;
             if (ia < niters && is_full(ia)) load_full(ia, ax, ay);
         }
-        if (ib < niters) {
+        if (ibb < niters) {
             const unsigned nb2 = claim();
-            run(ib, bx, by);
-            ib = nb2;
-            if (ib < niters && is_full(ib)) load_full(ib, bx, by);
+            run(ibb, bx, by);
+            ibb = nb2;
+            if (ibb < niters && is_full(ibb)) load_full(ibb, bx, by);
         }
     }
-    if (MODE >= 1 && MODE <= 3) {
-        if (sink == 12345.678) part_d[blockIdx.x] = 1;  // keep the ablated work alive
-        return;
-    }
-    GEOHIP_TRACE(TR, 8 * blockIdx.x + 1);
-    knn_dist_batch(st, ccnt, kb, args, spill_d, spill_i, spill_cnt, appended, true);
-    if (MODE == 5) {
-        if (lane == 0) atomicAdd(&part_i[0], appended);
-        return;
-    }
-    if (MODE == 7) {
-        if (appended == 12345) part_d[blockIdx.x] = 1;
-        return;
-    }
-
-    // ---- end of block: keep the survivors <= final bound, sort once, write the block list
-    constexpr int N = 64 * KPL;
+    PASS_TRACE(io, 1);
+    pass_dist_batch(st, ccnt, kb, args, io, appended, true);
     __syncthreads();
-    GEOHIP_TRACE(TR, 8 * blockIdx.x + 2);
-    if (wid == 0 && kb.cnt >= k) hist_bound(kb, k, args.hist_base);
-    if (threadIdx.x == 0) kb.final_cnt = 0;
+    PASS_TRACE(io, 2);
+    // ---- end of block: final local bound B (k-th bin edge) and H (4th bin edge); survivors <= B
+    // written unsorted to this block's list, those <= H (the block's smallest, usually 4-10)
+    // sorted by one wave: its 4 smallest are the block's heads.  A list whose heads may be
+    // incomplete (spilled survivors counted in the histogram, > 64 entries <= H) is flagged in
+    // its length word so the final reads it whole.
+    if (wid == 0) {
+        if (!(ABL & 4) && kb.cnt >= k) hist_bound(kb, k, args.hist_base);
+        const int hb = hist_kth_bin(kb.hist, kPassHeads);
+        if (lane == 0) kb.hcap = hb >= 0 && hb < kHistBins - 1 ? hist_edge(hb, args.hist_base) : kSentinelD;
+    }
     __syncthreads();
     const unsigned long long B = kb.bound;
-    const unsigned have = kb.cnt < (unsigned)KB::kCap ? kb.cnt : (unsigned)KB::kCap;
-    // compact survivors <= B into the (now idle) wave stages
-    // (the tie path below sorts up to the next power of two of kCap = 256 NW entries in place)
-    constexpr size_t kCdCap = 256 * NW;
-    static_assert(sizeof(stage) >= kCdCap * 12, "end-of-block compaction buffer");
-    unsigned long long* cd = reinterpret_cast<unsigned long long*>(&stage[0]);
-    unsigned* ci = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(&stage[0]) + kCdCap * 8);
+    const unsigned long long H = kb.hcap < B ? kb.hcap : B;
+    const unsigned have = kb.cnt < (unsigned)PB::kCap ? kb.cnt : (unsigned)PB::kCap;
+    const size_t lbase = (size_t)blockIdx.x * io.list_cap;
     for (unsigned t0 = 0; t0 < have; t0 += NT) {
         const unsigned t = t0 + threadIdx.x;
-        const bool keep = t < have && kb.bd[t] <= B;
+        unsigned long long d = kSentinelD;
+        unsigned i = kSentinelI;
+        if (t < have) {
+            d = kb.bd[t];
+            i = kb.bi[t];
+        }
+        const bool keep = d <= B && t < have;
         const unsigned long long m = __ballot(keep);
-        unsigned wbase = 0;
-        if (lane == 0 && m) wbase = atomicAdd(&kb.final_cnt, (unsigned)__popcll(m));
-        wbase = __shfl(wbase, 0);
-        if (keep) {
-            const unsigned pos = wbase + lanes_below(m);
-            cd[pos] = kb.bd[t];
-            ci[pos] = kb.bi[t];
+        unsigned wb = 0;
+        if (lane == 0 && m) wb = atomicAdd(&kb.cursor, (unsigned)__popcll(m));
+        wb = __shfl(wb, 0);
+        if (keep && !(ABL & 1)) {
+            const unsigned p = wb + lanes_below(m);
+            store_wt(&io.list_d[lbase + p], d);
+            store_wt(&io.list_i[lbase + p], i);
+        }
+        const bool small = keep && d <= H;
+        const unsigned long long ms = __ballot(small);
+        unsigned sb = 0;
+        if (lane == 0 && ms) sb = atomicAdd(&kb.nsmall, (unsigned)__popcll(ms));
+        sb = __shfl(sb, 0);
+        if (small) {
+            const unsigned p = sb + lanes_below(ms);
+            if (p < (unsigned)kWave) {
+                kb.top_d[p] = d;
+                kb.top_i[p] = i;
+            }
         }
     }
     __syncthreads();
-    const unsigned fc = kb.final_cnt;
-    const size_t off = (size_t)blockIdx.x * N;
-    // packed heads behind the lists (FinalIo::head_d)
-    unsigned long long* head_d = part_d + (size_t)gridDim.x * N;
-    unsigned* head_i = part_i + (size_t)gridDim.x * N;
-    auto put = [&](unsigned pos, unsigned long long d, unsigned i) {
-        store_wt(&part_d[off + pos], d);
-        store_wt(&part_i[off + pos], i);
-        if (pos < (unsigned)kHeads) {
-            store_wt(&head_d[kHeads * blockIdx.x + pos], d);
-            store_wt(&head_i[kHeads * blockIdx.x + pos], i);
+    if (wid == 0) {
+        const unsigned ns = kb.nsmall;
+        KE e = ksentinel();
+        if ((unsigned)lane < ns && lane < kWave) {
+            e.d = kb.top_d[lane];
+            e.i = kb.top_i[lane];
         }
-        // the block head joins the final selection's histogram as the block finishes
-        // (kGhistCopies copies so no bin counter takes more than ~nblocks / 8 arrivals)
-        if (pos == 0 && d != kSentinelD && out.ghist)
-            __hip_atomic_fetch_add(((gu32*)(out.ghist + (blockIdx.x % kGhistCopies) * kHistBins +
-                                            hist_bin(d, args.hist_base))),
-                                   1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    };
-    GEOHIP_TRACE(TR, 8 * blockIdx.x + 7);
-    if (KPL == 1 && fc <= 64u && out.epi_sort) {
-        if (wid == 0) {  // one 64-lane register bitonic sort
-            KE e = ksentinel();
-            if ((unsigned)lane < fc) { e.d = cd[lane]; e.i = ci[lane]; }
-            e = wave_sort64(e);
-            put((unsigned)lane, e.d, e.i);
+        if (!(ABL & 2)) e = wave_sort64(e);
+        if ((unsigned)lane < kPassHeads) {
+            store_wt(&io.head_d[kPassHeads * blockIdx.x + lane], e.d);
+            store_wt(&io.head_i[kPassHeads * blockIdx.x + lane], e.i);
         }
-    } else if (fc <= (unsigned)NT) {
-        // every kept survivor placed by rank (one pass over <= NT keys in LDS)
-        rank_place<NT>(cd, ci, fc, (unsigned)N, put);
-        for (unsigned p = fc + threadIdx.x; p < (unsigned)N; p += NT) put(p, kSentinelD, kSentinelI);
-    } else {
-        // many exact ties around the bound: sort all kept survivors in LDS (uniform branch)
-        int m2 = 1;
-        while (m2 < (int)fc) m2 <<= 1;
-        for (int t = threadIdx.x + fc; t < m2; t += NT) { cd[t] = kSentinelD; ci[t] = kSentinelI; }
-        __syncthreads();
-        block_sort_lds(cd, ci, m2);
-        for (int t = threadIdx.x; t < N; t += NT) put((unsigned)t, t < (int)fc ? cd[t] : kSentinelD, t < (int)fc ? ci[t] : kSentinelI);
+        // heads complete: every list entry <= H is among the sorted ones, and either 4 of them
+        // exist or the list holds nothing else
+        const bool complete = ns <= (unsigned)kWave && (ns >= kPassHeads || ns == kb.cursor);
+        if (lane == 0) store_wt(&io.len[blockIdx.x], kb.cursor | (complete ? 0u : kLenWhole));
     }
-    if (out.ticket == nullptr) return;
-
-    // ---- fused final selection (cdna_hip_programming.md §6 Guideline 16, counter form): the
-    // block list (and any spill) was stored sc1; every storing wave drains, the block meets,
-    // one lane takes a ticket; the last arriver acquires once and merges all block lists.
+    // ---- arrival (cdna_hip_programming.md §6 Guideline 16, counter form): every storing wave
+    // drains its write-through stores, the block meets, one lane takes a ticket
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    GEOHIP_TRACE(TR, 8 * blockIdx.x + 3);
-    if (threadIdx.x == 0) kb.final_cnt = arrive_last(out) ? 1u : 0u;
+    PASS_TRACE(io, 3);
+    if (threadIdx.x == 0) kb.last = pass_arrive_last(io.ctr + kTicketStride, io.groups) ? 1u : 0u;
     __syncthreads();
-    GEOHIP_TRACE(TR, 8 * blockIdx.x + 4);
-    if (kb.final_cnt == 0) return;
+    PASS_TRACE(io, 4);
+    if (kb.last == 0) return;
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    GEOHIP_TRACE(TR, 8 * (size_t)gridDim.x);
-    // LDS: gathered entries in the (idle) wave stages, tree exchange in kb.bd/kb.bi
-    static_assert(sizeof(stage) >= 2048 * 12, "fused final: gather buffer");
-    static_assert(sizeof(kb.bd) >= (size_t)(NW / 2 > 0 ? NW / 2 : 1) * N * 8, "fused final: tree exchange");
+    PASS_TRACE(io, 5);
+    // LDS for the final: the (idle) wave stages hold the gathered entries
+    constexpr unsigned kGcap = (unsigned)(sizeof(stage) / 12) < 8u * NT ? (unsigned)(sizeof(stage) / 12) : 8u * NT;
     char* sb = reinterpret_cast<char*>(&stage[0]);
-    const FinalLds fl{kb.bd, kb.bi, reinterpret_cast<unsigned long long*>(sb), reinterpret_cast<unsigned*>(sb + 2048 * 8),
-                      2048u, &kb.cnt, &kb.bound, &kb.final_cnt, kb.hist};
-    const FinalIo io{part_d, part_i, gridDim.x, (unsigned)N, k, out.out_d, out.out_i, out.out_count,
-                     spill_d, spill_i, spill_cnt, head_d, head_i, args.hist_base, out.ghist};
-    if (MODE == 10) return;  // ablation: arrival protocol without the final selection
-    // (MODE 11: the final selection without its output writes)
-    final_select<KPL, NT, (1024 / NT > 0 ? 1024 / NT : 1), TR, MODE == 11>(io, fl);
+    unsigned long long* gd = reinterpret_cast<unsigned long long*>(sb);
+    unsigned* gi = reinterpret_cast<unsigned*>(sb + (size_t)kGcap * 8);
+    if (ABL & 8) {  // measurement: a first (cold) run of the final, then the timed (warm) one
+        const unsigned long long sp = load_sc1(io.ctr);  // the spill count the final re-arms
+        pass_final<NT>(io, args, gd, gi, kGcap - (kGcap & 1u), kb.hist, kb.fin, kb.bd, kb.bi, kb.bi + kPassMaxBlocks);
+        __syncthreads();
+        if (threadIdx.x == 0) store_wt(io.ctr, (unsigned)sp);
+        __syncthreads();
+        PASS_TRACE(io, 5);
+    }
+    pass_final<NT>(io, args, gd, gi, kGcap - (kGcap & 1u), kb.hist, kb.fin, kb.bd, kb.bi, kb.bi + kPassMaxBlocks);
+    PASS_TRACE(io, 7);
 }
 
 // ============================================================================ range =======
@@ -1457,142 +1697,89 @@ __global__ void selftest_fp64(const double* __restrict__ a, const double* __rest
 }
 
 // ============================================================================ launchers ===
-static int g_knn_fused = 0;  // separate knn_final launch: measured faster than the fused tail (profiles/r01_knn_shape_sweep_dynamic.log, mode 9 vs 0)
-void set_knn_fused(int fused) { g_knn_fused = fused; }
-
-template <int KPL>
-static void launch_knn_final_heads(unsigned long long* part_d, unsigned* part_i, unsigned nblocks, unsigned k,
-                                   double* out_d, unsigned* out_i, unsigned* out_count,
-                                   unsigned long long* spill_d, unsigned* spill_i, unsigned* spill_cnt, int hist_base,
-                                   hipStream_t st) {
-    const unsigned L = 64u * KPL;
-    const FinalIo io{part_d, part_i, nblocks, L, k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt,
-                     part_d + (size_t)nblocks * L, part_i + (size_t)nblocks * L, hist_base, spill_cnt + kGhistWord};
-    knn_final<KPL><<<1, kFinalThreads, 0, st>>>(io);
-}
-
-static KnnConfig g_knn_cfg = {16, 1, 16, 0, 0};  // fastest measured shape (profiles/r01_knn_shape_sweep.log)
-
-hipError_t set_knn_trace(unsigned long long* buf) {
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_knn_trace), &buf, sizeof(buf));
-}
-
-int set_knn_config(int nw, int pf, int groups, int epi_sort, int interleave) {
-    if (!(nw == 4 || nw == 8 || nw == 16) || !(pf == 1 || pf == 2) || groups < 1 || groups > (int)kMaxTicketGroups)
-        return -1;
-    g_knn_cfg = KnnConfig{nw, pf, groups, epi_sort ? 1 : 0, interleave ? 1 : 0};
-    return 0;
-}
-KnnConfig knn_config() { return g_knn_cfg; }
-
-void knn_geometry(uint64_t n, unsigned* nblocks, uint64_t* chunk) {
-    // 16 waves per CU on all 256 CUs when n is large (equal work per block); an even chunk keeps
-    // the 16-byte double2 loads aligned
-    const uint64_t target = 256ull * (16 / (unsigned)g_knn_cfg.nw);
-    if (g_knn_cfg.interleave) {  // chunk 0: iterations interleaved over the blocks
-        const uint64_t n_it = (n + kPtsIter - 1) / kPtsIter;
-        *chunk = 0;
-        *nblocks = (unsigned)(n_it < target ? n_it : target);
-        return;
-    }
-    uint64_t c = (n + target - 1) / target;
-    c = (c + kPtsIter - 1) / kPtsIter * kPtsIter;  // whole wave iterations (aligned double2 loads)
+// kNN pass geometry: <= 256 blocks of 16 waves, block chunks of whole 256-point iterations
+void knn_pass_geometry(uint64_t n, unsigned* nblocks, uint64_t* chunk) {
+    uint64_t c = (n + kPassMaxBlocks - 1) / kPassMaxBlocks;
+    c = (c + kPtsIter - 1) / kPtsIter * kPtsIter;
     if (c < 1024) c = 1024;
     *chunk = c;
     *nblocks = (unsigned)((n + c - 1) / c);
 }
 
-template <int KPL, int MODE>
-static void knn_scan_launch(unsigned nblocks, hipStream_t st, const double* x, const double* y, uint64_t n,
-                            uint64_t chunk, const KnnArgs& args, unsigned long long* part_d, unsigned* part_i,
-                            unsigned long long* spill_d, unsigned* spill_i, unsigned* spill_cnt, KnnOut out) {
-    const KnnConfig c = g_knn_cfg;
-#define GEOHIP_SCAN(NW, PF) \
-    knn_scan<KPL, NW, PF, MODE><<<nblocks, NW * 64, 0, st>>>(x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, out)
-    switch (c.nw * 10 + c.pf) {
-        case 41: GEOHIP_SCAN(4, 1); break;
-        case 42: GEOHIP_SCAN(4, 2); break;
-        case 81: GEOHIP_SCAN(8, 1); break;
-        case 82: GEOHIP_SCAN(8, 2); break;
-        case 161: GEOHIP_SCAN(16, 1); break;
-        default: GEOHIP_SCAN(16, 2); break;
-    }
-#undef GEOHIP_SCAN
+size_t knn_pass_list_entries(unsigned nblocks) {
+    return (size_t)nblocks * (PassBlock<kPassNW>::kCap + kPassHeads) + nblocks;
 }
 
-static KnnOut knn_out(bool fused, double* out_d, unsigned* out_i, unsigned* out_count, unsigned* spill_cnt) {
-    if (!fused) return KnnOut{nullptr, nullptr, nullptr, nullptr, 1u, spill_cnt + kGhistWord, g_knn_cfg.epi_sort};
-    return KnnOut{out_d, out_i, out_count, spill_cnt + kTicketStride, (unsigned)g_knn_cfg.groups, spill_cnt + kGhistWord,
-                  g_knn_cfg.epi_sort};
-}
-
-hipError_t launch_knn(const double* x, const double* y, uint64_t n, const KnnArgs& args, int kpl,
-                      unsigned long long* part_d, unsigned* part_i, unsigned nblocks, uint64_t chunk, double* out_d,
-                      unsigned* out_i, unsigned* out_count, unsigned long long* spill_d, unsigned* spill_i,
-                      unsigned* spill_cnt, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
-    const unsigned k = args.k;
-    const unsigned L = 64u * (unsigned)kpl;
-    if (nblocks == 0) {  // empty window: the final selection alone writes the empty result
-        const FinalIo io{part_d, part_i, 0u, L, k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt, nullptr, nullptr, 0,
-                         nullptr};
-        if (k <= 64) knn_final<1><<<1, kFinalThreads, 0, st>>>(io);
-        else if (k <= 128) knn_final<2><<<1, kFinalThreads, 0, st>>>(io);
-        else knn_final<4><<<1, kFinalThreads, 0, st>>>(io);
+hipError_t launch_knn_pass(const double* x, const double* y, uint64_t n, const KnnArgs& args,
+                           unsigned long long* list_d, unsigned* list_i, unsigned long long* spill_d, unsigned* spill_i,
+                           unsigned* ctr, double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st,
+                           hipEvent_t ev0, hipEvent_t ev1, unsigned long long* trace, int abl) {
+    unsigned nblocks = 0;
+    uint64_t chunk = 0;
+    knn_pass_geometry(n, &nblocks, &chunk);
+    if (n == 0 || args.nu == 0) {  // no candidates: the empty result
+        const FinalIo io{list_d, list_i, 0u, 64u, args.k, out_d, out_i, out_count, nullptr, nullptr, nullptr, nullptr,
+                         nullptr, 0, nullptr};
+        knn_final<1><<<1, kFinalThreads, 0, st>>>(io);
         return hipGetLastError();
     }
-    const KnnOut out = knn_out(g_knn_fused, out_d, out_i, out_count, spill_cnt);
+    const unsigned cap = (unsigned)PassBlock<kPassNW>::kCap;
+    const size_t lists = (size_t)nblocks * cap;
+    // list entries, then the packed heads, then the list lengths (in the index array)
+    const PassIo io{list_d, list_i, cap, list_d + lists, list_i + lists, list_i + lists + (size_t)kPassHeads * nblocks,
+                    spill_d, nullptr, spill_i, ctr, out_d, out_i, out_count, 16u, trace};
     if (ev0) (void)hipEventRecord(ev0, st);
-    switch (kpl) {
-        case 1: knn_scan_launch<1, 0>(nblocks, st, x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, out); break;
-        case 2: knn_scan_launch<2, 0>(nblocks, st, x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, out); break;
-        case 4: knn_scan_launch<4, 0>(nblocks, st, x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, out); break;
-        default: return hipErrorInvalidValue;
+    switch (abl) {
+        case 1: knn_pass<kPassNW, 1><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io); break;
+        case 2: knn_pass<kPassNW, 2><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io); break;
+        case 3: knn_pass<kPassNW, 3><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io); break;
+        case 7: knn_pass<kPassNW, 7><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io); break;
+        case 8: knn_pass<kPassNW, 8><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io); break;
+        default: knn_pass<kPassNW><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io); break;
     }
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess || g_knn_fused) {
-        if (ev1) (void)hipEventRecord(ev1, st);
-        return e;
-    }
-    switch (kpl) {
-        case 1: launch_knn_final_heads<1>(part_d, part_i, nblocks, k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt, args.hist_base, st); break;
-        case 2: launch_knn_final_heads<2>(part_d, part_i, nblocks, k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt, args.hist_base, st); break;
-        default: launch_knn_final_heads<4>(part_d, part_i, nblocks, k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt, args.hist_base, st); break;
-    }
-    if (ev1) (void)hipEventRecord(ev1, st);  // timed region: the scan and the final selection
+    if (ev1) (void)hipEventRecord(ev1, st);
     return hipGetLastError();
 }
 
-hipError_t launch_knn_scan_variant(int mode, const double* x, const double* y, uint64_t n, const KnnArgs& args,
-                                   unsigned long long* part_d, unsigned* part_i, unsigned nblocks, uint64_t chunk,
-                                   unsigned long long* spill_d, unsigned* spill_i, unsigned* spill_cnt, double* out_d,
-                                   unsigned* out_i, unsigned* out_count, hipStream_t st) {
-    const KnnOut fused = knn_out(true, out_d, out_i, out_count, spill_cnt);
-    const KnnOut lists = knn_out(false, out_d, out_i, out_count, spill_cnt);
-#define GEOHIP_VAR(M, O) knn_scan_launch<1, M>(nblocks, st, x, y, n, chunk, args, part_d, part_i, spill_d, spill_i, spill_cnt, O)
-    switch (mode) {
-        case 0: GEOHIP_VAR(0, fused); break;
-        case 1: GEOHIP_VAR(1, lists); break;
-        case 2: GEOHIP_VAR(2, lists); break;
-        case 3: GEOHIP_VAR(3, lists); break;
-        case 5: GEOHIP_VAR(5, lists); break;
-        case 6: GEOHIP_VAR(6, fused); break;
-        case 10: GEOHIP_VAR(10, fused); break;
-        case 11: GEOHIP_VAR(11, fused); break;
-        case 7: GEOHIP_VAR(7, lists); break;
-        case 8: GEOHIP_VAR(0, lists); break;
-        case 9:
-            GEOHIP_VAR(0, lists);
-            launch_knn_final_heads<1>(part_d, part_i, nblocks, args.k, out_d, out_i, out_count, spill_d, spill_i, spill_cnt,
-                                      args.hist_base, st);
-            break;
-        default: return hipErrorInvalidValue;
+// Rank merge for k > 256: every entry of the (<= 8192) gathered lists sorted in LDS by one
+// workgroup (bitonic), the k smallest real entries written.
+constexpr unsigned kMergeCap = 8192;
+__global__ __launch_bounds__(1024) void knn_merge_sort(const unsigned long long* __restrict__ d,
+                                                       const unsigned* __restrict__ ix, unsigned m, unsigned k,
+                                                       double* __restrict__ out_d, unsigned* __restrict__ out_i,
+                                                       unsigned* __restrict__ out_count) {
+    __shared__ __attribute__((aligned(16))) unsigned long long sd[kMergeCap];
+    __shared__ unsigned si[kMergeCap];
+    __shared__ unsigned nreal;
+    unsigned p2 = 1;
+    while (p2 < m) p2 <<= 1;
+    if (threadIdx.x == 0) nreal = 0;
+    __syncthreads();
+    unsigned mine = 0;
+    for (unsigned t = threadIdx.x; t < p2; t += blockDim.x) {
+        sd[t] = t < m ? d[t] : kSentinelD;
+        si[t] = t < m ? ix[t] : kSentinelI;
+        mine += (t < m && sd[t] != kSentinelD) ? 1u : 0u;
     }
-#undef GEOHIP_VAR
-    return hipGetLastError();
+    if (mine) atomicAdd(&nreal, mine);
+    __syncthreads();
+    block_sort_lds(sd, si, (int)p2);
+    const unsigned outn = nreal < k ? nreal : k;
+    for (unsigned t = threadIdx.x; t < k; t += blockDim.x) {
+        out_d[t] = __longlong_as_double((long long)(t < outn ? sd[t] : kSentinelD));
+        out_i[t] = t < outn ? si[t] : kSentinelI;
+    }
+    if (threadIdx.x == 0) *out_count = outn;
 }
 
 hipError_t launch_knn_merge(const unsigned long long* d, const unsigned* i, unsigned nlists, unsigned list_len,
                             unsigned k, double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st) {
+    if (k > 256) {
+        const uint64_t m = (uint64_t)nlists * list_len;
+        if (m > kMergeCap) return hipErrorInvalidValue;
+        knn_merge_sort<<<1, 1024, 0, st>>>(d, i, (unsigned)m, k, out_d, out_i, out_count);
+        return hipGetLastError();
+    }
     const FinalIo io{d, i, nlists, list_len, k, out_d, out_i, out_count, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
                      nullptr};
     if (k <= 64) knn_final<1><<<1, kFinalThreads, 0, st>>>(io);
@@ -1601,8 +1788,6 @@ hipError_t launch_knn_merge(const unsigned long long* d, const unsigned* i, unsi
     return hipGetLastError();
 }
 
-static int g_range_mode = 0;
-void set_range_mode(int mode) { g_range_mode = mode; }
 
 hipError_t launch_range(const double* x, const double* y, uint64_t n, const RangeArgs& a, int approximate,
                         unsigned long long* bitmask, unsigned* unit_count, uint64_t* offs, uint64_t* total,
@@ -1617,10 +1802,6 @@ hipError_t launch_range(const double* x, const double* y, uint64_t n, const Rang
         const RangeLookback lb{lb_status, lb_ticket, epoch};
         if (ev0) (void)hipEventRecord(ev0, st);
         if (approximate) range_fused<true><<<nblocks, kRangeNW * kWave, 0, st>>>(x, y, n, a, upb, lb, out, cap, total);
-        else if (g_range_mode == 1) range_fused<false, 1><<<nblocks, kRangeNW * kWave, 0, st>>>(x, y, n, a, upb, lb, out, cap, total);
-        else if (g_range_mode == 2) range_fused<false, 2><<<nblocks, kRangeNW * kWave, 0, st>>>(x, y, n, a, upb, lb, out, cap, total);
-        else if (g_range_mode == 3) range_fused<false, 3><<<nblocks, kRangeNW * kWave, 0, st>>>(x, y, n, a, upb, lb, out, cap, total);
-        else if (g_range_mode == 4) range_fused<false, 4><<<nblocks, kRangeNW * kWave, 0, st>>>(x, y, n, a, upb, lb, out, cap, total);
         else range_fused<false><<<nblocks, kRangeNW * kWave, 0, st>>>(x, y, n, a, upb, lb, out, cap, total);
         if (ev1) (void)hipEventRecord(ev1, st);
         return hipGetLastError();

@@ -378,18 +378,12 @@ def test_knn_equal_distance_shell(ctx):
         assert oi.tolist() == wi.tolist() and np.array_equal(od.view(np.uint64), wd.view(np.uint64))
 
 
-@pytest.mark.parametrize("fused", [False, True])
-def test_knn_query_duplicates_spill_and_repeat(ctx, fused):
+def test_knn_query_duplicates_spill_and_repeat(ctx):
     """Thousands of exact copies of the query point in consecutive window slots: one scan
-    block keeps far more than its LDS survivor buffer (spill path), the head histogram's k-th
-    bin is the lowest (exact-T fallback) or the gather overflows (k-round fallback).  Every
-    call is repeated on the same context: the fused final's arrival ticket and the spill
-    count must be back at zero after each launch (both final-selection forms)."""
-    _abi.debug_set_knn_fused(fused)
-    try:
-        _dup_spill_repeat(ctx)
-    finally:
-        _abi.debug_set_knn_fused(False)
+    block keeps far more than its LDS survivor buffer (spill path), the heads' k-th bin is the
+    lowest and lists are read whole.  Every call is repeated on the same context: the arrival
+    tickets and the spill count must be back at zero after each launch."""
+    _dup_spill_repeat(ctx)
 
 
 def _dup_spill_repeat(ctx):
@@ -413,23 +407,33 @@ def _dup_spill_repeat(ctx):
     assert oi.tolist() == wi.tolist() and np.array_equal(od.view(np.uint64), wd.view(np.uint64))
 
 
-def test_knn_fused_final_select(ctx):
-    """The same results with the final selection fused into the scan's last-arriving block
-    (arrival tickets, sc1 lists) instead of the default separate knn_final launch."""
+def test_knn_nan_ties_and_suffixes(ctx):
+    """NaN points, a block of exact query copies and window suffixes that move it across
+    block boundaries, at k from 1 to 1000."""
     ag, cg = agrid(100)
     rng = np.random.default_rng(23)
     x, y = _window(rng, 1_500_000, nan_every=1009)
     x[400000:403000] = Q[0]
     y[400000:403000] = Q[1]
-    _abi.debug_set_knn_fused(True)
-    try:
-        for (xx, yy) in ((x, y), (x[3000:], y[3000:]), (x[403000:], y[403000:])):
-            for k in (1, 50, 129, 256):
-                wi, wd = cref.knn_pp(cg, xx, yy, Q[0], Q[1], 0.5, k)
-                oi, od = ctx.knn_pp(ag, xx, yy, Q[0], Q[1], 0.5, k)
-                assert oi.tolist() == wi.tolist() and np.array_equal(od.view(np.uint64), wd.view(np.uint64))
-    finally:
-        _abi.debug_set_knn_fused(False)
+    for (xx, yy) in ((x, y), (x[3000:], y[3000:]), (x[403000:], y[403000:])):
+        for k in (1, 50, 129, 256, 1000):
+            wi, wd = cref.knn_pp(cg, xx, yy, Q[0], Q[1], 0.5, k)
+            oi, od = ctx.knn_pp(ag, xx, yy, Q[0], Q[1], 0.5, k)
+            assert oi.tolist() == wi.tolist() and np.array_equal(od.view(np.uint64), wd.view(np.uint64))
+
+
+def test_knn_large_k(ctx):
+    """k beyond the round-1 limit of 256 (PointPointKNNQuery takes any Integer k): 512, 1000 and
+    GEOHIP_KNN_MAX_K over a 2M-point window; k above the limit is GEOHIP_ERR_UNSUPPORTED."""
+    ag, cg = agrid(100)
+    x, y = synth.uniform(2_000_000, 43)
+    for k in (512, 1000, _abi.KNN_MAX_K):
+        wi, wd = cref.knn_pp(cg, x, y, Q[0], Q[1], 0.5, k)
+        oi, od = ctx.knn_pp(ag, x, y, Q[0], Q[1], 0.5, k)
+        assert len(oi) == k
+        assert oi.tolist() == wi.tolist() and np.array_equal(od.view(np.uint64), wd.view(np.uint64))
+    with pytest.raises(_abi.GeohipUnsupportedError):
+        ctx.knn_pp(ag, x, y, Q[0], Q[1], 0.5, _abi.KNN_MAX_K + 1)
 
 
 # ------------------------------------------------------------------ less common kernel paths --
@@ -447,12 +451,12 @@ def test_join_dense_tiles_batches_and_recompute(ctx):
     assert len(want) > 100000
     got = ctx.join_pp(ag, ag, dx, dy, qx, qy, 0.01)
     assert pairs_sorted(got).tolist() == want
-    _abi.debug_set_join_mask_budget(0)
+    ctx.debug_join_mask_budget(0)
     try:
         got = ctx.join_pp(ag, ag, dx, dy, qx, qy, 0.01)
         assert pairs_sorted(got).tolist() == want
     finally:
-        _abi.debug_set_join_mask_budget()
+        ctx.debug_join_mask_budget()
 
 
 def test_ppoly_big_tile_and_long_ring(ctx):
@@ -478,15 +482,3 @@ def test_ppoly_big_tile_and_long_ring(ctx):
         assert pairs_sorted(got).tolist() == want
 
 
-def test_knn_interleaved_iterations(ctx):
-    """The kNN scan with the window's 256-point iterations interleaved over the blocks (launch
-    shape switch) gives the same result as the default contiguous chunks."""
-    ag, cg = agrid(100)
-    x, y = synth.uniform(3_000_001, 41)
-    want_i, want_d = cref.knn_pp(cg, x, y, Q[0], Q[1], 0.5, 50)
-    _abi.debug_set_knn_config(interleave=1)
-    try:
-        oi, od = ctx.knn_pp(ag, x, y, Q[0], Q[1], 0.5, 50)
-        assert oi.tolist() == want_i.tolist() and np.array_equal(od.view(np.uint64), want_d.view(np.uint64))
-    finally:
-        _abi.debug_set_knn_config()

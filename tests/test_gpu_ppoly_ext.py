@@ -137,9 +137,10 @@ def test_knn_ppoly_errors(ctx):
     ag, _ = agrid(500)
     x, y = synth.uniform(1000, 1)
     sq_x, sq_y = np.array([116.3, 116.4, 116.4, 116.3]), np.array([40.1, 40.1, 40.2, 40.2])
-    for k in (0, 257):
-        with pytest.raises(_abi.GeohipArgumentError):
-            ctx.knn_ppoly(ag, x, y, sq_x, sq_y, 0.01, k)
+    with pytest.raises(_abi.GeohipArgumentError):
+        ctx.knn_ppoly(ag, x, y, sq_x, sq_y, 0.01, 0)
+    with pytest.raises(_abi.GeohipUnsupportedError):
+        ctx.knn_ppoly(ag, x, y, sq_x, sq_y, 0.01, _abi.KNN_PPOLY_MAX_K + 1)
     with pytest.raises(_abi.GeohipArgumentError):
         ctx.knn_ppoly(ag, x, y, sq_x[:3], sq_y[:3], 0.01, 5)  # <= 3 coordinates (Polygon.java:53)
 
