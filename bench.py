@@ -555,9 +555,11 @@ class KnnIncrWorkload(KnnWorkload):
 
 class C5Workload(KnnWorkload):
     """C5 per shard (BASELINE.json configs[4]): 1000x1000 grid, 25M uniform points per GPU
-    (200M per window on 8 GPUs), kNN k=100 + range r=0.05 of the README query."""
+    (200M per window on 8 GPUs), kNN k=100 + range r=0.05 of the README query -- both queries in
+    one pass over the shard (geohip_knn_range_pp), then for N > 1 the RCCL all-gather of the
+    ranks' top-k + the device merge and the all-gather of the range hit counts."""
     tag = "knn_scan_c5"
-    kernel = "geohip::knn_scan<2> + knn_final<2>, range pass (two timed launches per step)"
+    kernel = "geohip::knn_pass<16, range> (kNN k=100 + range r=0.05 in one pass: one launch per step)"
     grid_n, k, radius, n_default, seed0 = 1000, 100, 0.05, 25_000_000, 7
     windows = 2
     label = "C5 shard: kNN k=100 + range r=0.05, 1000x1000 Beijing UniformGrid, README query"
@@ -568,21 +570,30 @@ class C5Workload(KnnWorkload):
         self.rout = torch.empty(self.n, dtype=torch.int32, device=self.dev)
         self.rcnt = torch.zeros(1, dtype=torch.int64, device=self.dev)
         self.counts = torch.zeros(self.world, dtype=torch.int64, device=self.dev)
+        self.hits = None
 
     def step(self, s):
+        import torch
         w = s % self.windows
-        self.knn_step(w)
-        self.ctx.range_pp_async(self.grid, self.xs[w], self.ys[w], self.q[0], self.q[1], self.radius, False,
-                                self.rout, self.n, self.rcnt)
+        self.ctx.knn_range_pp_async(self.grid, self.xs[w], self.ys[w], self.q[0], self.q[1], self.radius, self.k, False,
+                                    self.out_i, self.out_d, self.cnt[0:1], self.rout, self.n, self.rcnt)
         if self.world > 1:
+            gi = torch.where(self.out_i >= 0, (self.out_i.to(torch.int64) + self.base).to(torch.int32), self.out_i)
+            self.dist.all_gather_into_tensor(self.g_d.view(-1), self.out_d)
+            self.dist.all_gather_into_tensor(self.g_i.view(-1), gi)
+            self.ctx.knn_merge_async(self.g_d, self.g_i, self.world, self.k, self.k, self.m_i, self.m_d,
+                                     self.cnt[1:2])
             self.dist.all_gather_into_tensor(self.counts, self.rcnt)
 
-    def algorithmic_bytes(self):  # per timed launch: kNN scan and range pass each read the window once
-        return BYTES_PER_POINT * self.n
+    def algorithmic_bytes(self):  # per step: the shard read once (16 B/pt) + the range hits written
+        if self.hits is None:
+            self.hits = float(self.rcnt.item())
+        return BYTES_PER_POINT * self.n + 4 * self.hits
 
     def config(self):
         c = super().config()
         c["workload"] = f"{self.label}, {self.n} uniform points per window per GPU (BASELINE.json configs[4])"
+        c["range_hits_per_window_per_gpu"] = self.hits
         return c
 
     def cpu_baseline(self, seconds):

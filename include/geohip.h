@@ -119,6 +119,15 @@ int geohip_knn_pp(geohip_ctx* ctx, const geohip_grid* grid, const double* x, con
                   uint64_t n, double qx, double qy, double r, uint32_t k,
                   uint32_t* out_idx, double* out_dist, uint32_t* out_count);
 
+/* The kNN (k) and the range (radius r) of the same query point over one window -- two GeoFlink
+   continuous queries (PointPointKNNQuery.java:125-191 and PointPointRangeQuery.java:86-137) with
+   the same q and r over the same stream, as BASELINE.json configs[4] runs them -- evaluated in
+   one pass over the window: results identical to geohip_knn_pp and geohip_range_pp. */
+int geohip_knn_range_pp(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
+                        uint64_t n, double qx, double qy, double r, uint32_t k, int approximate,
+                        uint32_t* knn_idx, double* knn_dist, uint32_t* knn_count,
+                        uint32_t* range_idx, uint64_t range_cap, uint64_t* range_count);
+
 /* out_pairs: 2*cap uint32 (p_idx, q_idx) pairs. */
 int geohip_join_pp(geohip_ctx* ctx, const geohip_grid* grid_data, const geohip_grid* grid_query,
                    const double* dx, const double* dy, uint64_t nd,
@@ -169,6 +178,11 @@ int geohip_knn_pp_async(geohip_ctx* ctx, const geohip_grid* grid, const double* 
 int geohip_knn_merge_async(geohip_ctx* ctx, const double* dist, const uint32_t* idx, uint32_t nlists,
                            uint32_t list_len, uint32_t k, uint32_t* out_idx, double* out_dist,
                            uint32_t* out_count_dev);
+/* geohip_knn_range_pp into device buffers (counts on the device). */
+int geohip_knn_range_pp_async(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
+                              uint64_t n, double qx, double qy, double r, uint32_t k, int approximate,
+                              uint32_t* knn_idx, double* knn_dist, uint32_t* knn_count_dev,
+                              uint32_t* range_idx, uint64_t range_cap, uint64_t* range_count_dev);
 /* Range into device buffers: out_idx (cap entries), *out_count_dev = total hits. */
 int geohip_range_pp_async(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
                           uint64_t n, double qx, double qy, double r, int approximate,

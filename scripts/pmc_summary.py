@@ -20,7 +20,7 @@ TAGS = {"knn": ("knn_scan", ("knn_pass",), 1),
         "join": ("join_probe", ("join_tile", "join_emit", "scan_seg_totals<unsigned long long>", "scan_totals<unsigned long long>",
                                  "scan_apply<unsigned long long>"), 1),
         "ppoly": ("ppoly_probe", ("ppoly_eval", "ppoly_emit", "ppoly_outside"), 1),
-        "c5": ("knn_scan_c5", ("knn_scan", "knn_final", "range_fused", "range_scan", "scan_units", "range_emit"), 2),
+        "c5": ("knn_scan_c5", ("knn_pass",), 1),
         "ingest": ("ingest", ("ingest_count", "ingest_scan", "ingest_parse"), 1),
         "ppjoin": ("ppjoin", ("ppoly_eval", "ppoly_emit", "ppoly_outside"), 1),
         "ppknn": ("ppknn", ("rsel_", "ppknn_"), 1),

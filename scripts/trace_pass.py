@@ -28,7 +28,7 @@ for w in range(W):
     xs.append(x)
     ys.append(y)
 torch.cuda.synchronize()
-names = ["start", "stream_end", "flush", "drained", "arrived"]
+names = ["start", "stream_end", "flush", "drained", "arrived"] + (["lookback", "emitted"] if ABL < 0 else [])
 out = {}
 for rep in range(4):
     for w in range(W):  # warm the path, cycle windows
@@ -36,7 +36,8 @@ for rep in range(4):
     tr = ctx.debug_knn_pass_trace(grid, xs[rep % W], ys[rep % W], q[0], q[1], R, K, ABL).astype(np.int64)
     t0 = tr[:, 0].min()
     rel = (tr - t0) / 100.0
-    row = {nm: [round(float(np.percentile(rel[:, j], p)), 2) for p in (0, 10, 50, 90, 100)] for j, nm in enumerate(names)}
+    cols = [0, 1, 2, 3, 4, 5, 6]
+    row = {nm: [round(float(np.percentile(rel[:, cols[j]], p)), 2) for p in (0, 10, 50, 90, 100)] for j, nm in enumerate(names)}
     last = int(np.argmax(tr[:, 7]))
     row["final"] = {nm: round(float(rel[last, j]), 2) for nm, j in (("acquired", 5), ("gathered", 6), ("written", 7))}
     row["last_block"] = last

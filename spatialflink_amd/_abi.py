@@ -113,6 +113,10 @@ _SIGS = {
     "geohip_knn_pp_async": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_double, c_double, c_double, c_uint32,
                                     _P, _P, _P]),
     "geohip_knn_merge_async": (c_int, [_P, _P, _P, c_uint32, c_uint32, c_uint32, _P, _P, _P]),
+    "geohip_knn_range_pp": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_double, c_double, c_double, c_uint32,
+                                    c_int, _P, _P, POINTER(c_uint32), _P, c_uint64, POINTER(c_uint64)]),
+    "geohip_knn_range_pp_async": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_double, c_double, c_double,
+                                          c_uint32, c_int, _P, _P, _P, _P, c_uint64, _P]),
     "geohip_join_pp": (c_int, [_P, POINTER(Grid), POINTER(Grid), _P, _P, c_uint64, _P, _P, c_uint64, c_double,
                                c_int, _P, c_uint64, POINTER(c_uint64)]),
     "geohip_join_pp_count_only": (c_int, [_P, POINTER(Grid), POINTER(Grid), _P, _P, c_uint64, _P, _P, c_uint64,
@@ -369,6 +373,45 @@ class Context:
                                ctypes.byref(cnt))
         self._check(rc, "knn_pp")
         return oi[:cnt.value], od[:cnt.value]
+
+    def knn_range_pp(self, grid: Grid, x, y, qx, qy, r, k, approximate=False, cap=None):
+        """kNN (k) and range (r) of one query point over one window in one pass:
+        ((knn_idx, knn_dist), range_idx) -- the results of knn_pp and range_pp."""
+        x, y = _f64(x), _f64(y)
+        n = len(x)
+        dev = self._mem_for(x, y)
+        cap = n if cap is None else cap
+        if dev:
+            import torch
+            oi = torch.empty(k, dtype=torch.int32, device=x.device)
+            od = torch.empty(k, dtype=torch.float64, device=x.device)
+            ro = torch.empty(max(cap, 1), dtype=torch.int32, device=x.device)
+        else:
+            oi = np.empty(k, dtype=np.uint32)
+            od = np.empty(k, dtype=np.float64)
+            ro = np.empty(max(cap, 1), dtype=np.uint32)
+        kc, rc_ = c_uint32(0), c_uint64(0)
+        rc = lib.geohip_knn_range_pp(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), n, qx, qy, r, k, int(approximate),
+                                     _ptr(oi), _ptr(od), ctypes.byref(kc), _ptr(ro), cap, ctypes.byref(rc_))
+        self._check(rc, "knn_range_pp")
+        return (oi[:kc.value], od[:kc.value]), ro[:rc_.value]
+
+    def knn_range_pp_async(self, grid: Grid, x, y, qx, qy, r, k, approximate, knn_idx, knn_dist, knn_count,
+                           range_idx, cap, range_count):
+        self._dev(x, "x")
+        self._dev(y, "y")
+        self._dev(knn_idx, "knn_idx", "int32")
+        self._dev(knn_dist, "knn_dist")
+        self._dev(range_idx, "range_idx", "int32")
+        if range_idx.numel() < cap:
+            raise GeohipArgumentError("knn_range_pp_async: range_idx shorter than cap")
+        if self._mem != MEM_DEVICE:
+            self.set_mem(MEM_DEVICE)
+        rc = lib.geohip_knn_range_pp_async(self.h, ctypes.byref(grid), x.data_ptr(), y.data_ptr(), x.numel(), qx, qy, r,
+                                           k, int(approximate), knn_idx.data_ptr(), knn_dist.data_ptr(),
+                                           knn_count.data_ptr(), range_idx.data_ptr(), cap, range_count.data_ptr())
+        if rc:
+            self._check(rc, "knn_range_pp_async")
 
     # async forms: device tensors only, no host sync; the hot per-window path, so the pointers
     # go to ctypes as plain ints (argtypes c_void_p) without wrapper objects

@@ -203,6 +203,21 @@ KnnArgs make_knn_args(const PointPlan& plan, uint32_t k, double qx, double qy) {
     return a;
 }
 
+RangeArgs make_range_args(const PointPlan& plan, double qx, double qy, double r) {
+    RangeArgs a;
+    memset(&a, 0, sizeof a);
+    for (int i = 0; i < plan.ng; i++) a.g[i] = plan.g[i];
+    a.ng = plan.ng;
+    a.c = plan.c;
+    a.nc = plan.nc;
+    a.qx = qx;
+    a.qy = qy;
+    a.r = r;
+    // squared screens for the candidate cells (see device_common.h): a 2^-40 margin
+    pp_screen_bounds(r, &a.r2lo, &a.r2hi);
+    return a;
+}
+
 // scratch that must start zeroed (the final kernel re-zeroes it after each use)
 int ensure_zeroed(geohip_ctx* ctx, Slot s, size_t bytes);
 
@@ -244,17 +259,7 @@ int range_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x, con
     PointPlan plan;
     int rc = plan_or_fail(ctx, grid, qx, qy, r, &plan);
     if (rc) return rc;
-    RangeArgs a;
-    memset(&a, 0, sizeof a);
-    for (int i = 0; i < plan.ng; i++) a.g[i] = plan.g[i];
-    a.ng = plan.ng;
-    a.c = plan.c;
-    a.nc = plan.nc;
-    a.qx = qx;
-    a.qy = qy;
-    a.r = r;
-    // squared screens for the candidate cells (see device_common.h): a 2^-40 margin
-    pp_screen_bounds(r, &a.r2lo, &a.r2hi);
+    RangeArgs a = make_range_args(plan, qx, qy, r);
     const double *dx, *dy;
     rc = stage_xy(ctx, x, y, n, S_X, S_Y, &dx, &dy);
     if (rc) return rc;
@@ -274,6 +279,55 @@ int range_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x, con
                                 B<unsigned long long>(ctx, S_RLB), reinterpret_cast<unsigned*>(B<char>(ctx, S_RLB) + 256 * 8),
                                 ctx->range_epoch);
     if (e != hipSuccess) return hip_fail(ctx, e, "range launch");
+    return GEOHIP_OK;
+}
+
+// kNN (k) and range of the same point over one window: one fused pass when the window fits
+// (knn_pass_fuses_range), else the two passes back to back.
+int knn_range_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
+                      double qx, double qy, double r, uint32_t k, int approximate, double* kd, unsigned* ki,
+                      unsigned* kcnt, unsigned* rout, uint64_t rcap, uint64_t* rtotal) {
+    if (k == 0) return fail(ctx, GEOHIP_ERR_ARG, "k must be > 0");
+    if (k > GEOHIP_KNN_MAX_K) return fail(ctx, GEOHIP_ERR_UNSUPPORTED, "k > GEOHIP_KNN_MAX_K");
+    PointPlan plan;
+    int rc = plan_or_fail(ctx, grid, qx, qy, r, &plan);
+    if (rc) return rc;
+    if (n == 0 || plan.nu == 0 || !knn_pass_fuses_range(n)) {
+        rc = knn_enqueue(ctx, grid, x, y, n, qx, qy, r, k, kd, ki, kcnt);
+        if (!rc) rc = range_enqueue(ctx, grid, x, y, n, qx, qy, r, approximate, rout, rcap, rtotal);
+        return rc;
+    }
+    KnnArgs a = make_knn_args(plan, k, qx, qy);
+    const double *dx, *dy;
+    rc = stage_xy(ctx, x, y, n, S_X, S_Y, &dx, &dy);
+    if (rc) return rc;
+    unsigned nb = 0;
+    uint64_t ch = 0;
+    knn_pass_geometry(n, &nb, &ch);
+    const size_t ents = knn_pass_list_entries(nb ? nb : 1);
+    rc = ensure(ctx, S_PART_D, ents * 8);
+    if (!rc) rc = ensure(ctx, S_PART_I, ents * 4);
+    if (!rc) rc = ensure(ctx, S_SPILL_D, n * 8);
+    if (!rc) rc = ensure(ctx, S_SPILL_I, n * 4);
+    if (!rc) rc = ensure_zeroed(ctx, S_SPILL_CNT, kKnnCounterBytes);
+    if (!rc) rc = ensure_zeroed(ctx, S_RLB, 256 * 8 + 64);
+    if (rc) return rc;
+    ctx->range_epoch = ctx->range_epoch % ((1ull << 24) - 1) + 1;
+    PassRangeIo rio;
+    memset(&rio, 0, sizeof rio);
+    rio.a = make_range_args(plan, qx, qy, r);
+    rio.approximate = approximate;
+    rio.status = B<unsigned long long>(ctx, S_RLB);
+    rio.epoch = ctx->range_epoch;
+    rio.out = rout;
+    rio.cap = rcap;
+    rio.total = rtotal;
+    hipEvent_t e0, e1;
+    timing_events(ctx, &e0, &e1);
+    hipError_t e = launch_knn_pass(dx, dy, n, a, B<unsigned long long>(ctx, S_PART_D), B<unsigned>(ctx, S_PART_I),
+                                   B<unsigned long long>(ctx, S_SPILL_D), B<unsigned>(ctx, S_SPILL_I),
+                                   B<unsigned>(ctx, S_SPILL_CNT), kd, ki, kcnt, ctx->stream, e0, e1, nullptr, 0, &rio);
+    if (e != hipSuccess) return hip_fail(ctx, e, "knn+range launch");
     return GEOHIP_OK;
 }
 
@@ -491,6 +545,66 @@ int geohip_knn_merge_async(geohip_ctx* ctx, const double* dist, const uint32_t* 
     return GEOHIP_OK;
 }
 
+int geohip_knn_range_pp(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
+                        double qx, double qy, double r, uint32_t k, int approximate, uint32_t* knn_idx,
+                        double* knn_dist, uint32_t* knn_count, uint32_t* range_idx, uint64_t range_cap,
+                        uint64_t* range_count) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    if (!knn_idx || !knn_dist || !knn_count || !range_count || (range_cap && !range_idx))
+        return fail(ctx, GEOHIP_ERR_ARG, "null output");
+    double* od;
+    unsigned *oi, *ro;
+    if (ctx->mem == GEOHIP_MEM_DEVICE) {
+        od = knn_dist;
+        oi = knn_idx;
+        ro = range_idx;
+    } else {
+        rc = ensure(ctx, S_OUT_D, (size_t)k * 8);
+        if (!rc) rc = ensure(ctx, S_OUT_I, (size_t)k * 4);
+        if (!rc) rc = ensure(ctx, S_OUT_IDX, range_cap * 4);
+        if (rc) return rc;
+        od = B<double>(ctx, S_OUT_D);
+        oi = B<unsigned>(ctx, S_OUT_I);
+        ro = B<unsigned>(ctx, S_OUT_IDX);
+    }
+    rc = ensure(ctx, S_OUT_CNT, 8);
+    if (!rc) rc = ensure(ctx, S_TOTAL, 8);
+    if (rc) return rc;
+    rc = knn_range_enqueue(ctx, grid, x, y, n, qx, qy, r, k, approximate, od, oi, B<unsigned>(ctx, S_OUT_CNT), ro,
+                           range_cap, B<uint64_t>(ctx, S_TOTAL));
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(ctx->pinned, ctx->buf[S_OUT_CNT], 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->pinned + 1, ctx->buf[S_TOTAL], 8, hipMemcpyDeviceToHost, ctx->stream));
+    if (ctx->mem == GEOHIP_MEM_HOST) {
+        HIPCHK(hipMemcpyAsync(knn_dist, od, (size_t)k * 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipMemcpyAsync(knn_idx, oi, (size_t)k * 4, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    *knn_count = (uint32_t)(ctx->pinned[0] & 0xffffffffu);
+    const uint64_t total = ctx->pinned[1];
+    *range_count = total;
+    if (ctx->mem == GEOHIP_MEM_HOST) {
+        const uint64_t m = total < range_cap ? total : range_cap;
+        if (m) HIPCHK(hipMemcpy(range_idx, ro, m * 4, hipMemcpyDeviceToHost));
+    }
+    if (total > range_cap) return fail(ctx, GEOHIP_ERR_CAPACITY, "range capacity too small; *range_count = required");
+    return GEOHIP_OK;
+}
+
+int geohip_knn_range_pp_async(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
+                              double qx, double qy, double r, uint32_t k, int approximate, uint32_t* knn_idx,
+                              double* knn_dist, uint32_t* knn_count_dev, uint32_t* range_idx, uint64_t range_cap,
+                              uint64_t* range_count_dev) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    if (ctx->mem != GEOHIP_MEM_DEVICE) return fail(ctx, GEOHIP_ERR_ARG, "async forms need GEOHIP_MEM_DEVICE");
+    if (!knn_idx || !knn_dist || !knn_count_dev || !range_count_dev || (range_cap && !range_idx))
+        return fail(ctx, GEOHIP_ERR_ARG, "null output");
+    return knn_range_enqueue(ctx, grid, x, y, n, qx, qy, r, k, approximate, knn_dist, knn_idx, knn_count_dev, range_idx,
+                             range_cap, range_count_dev);
+}
+
 int geohip_join_pp(geohip_ctx* ctx, const geohip_grid* grid_data, const geohip_grid* grid_query, const double* dx,
                    const double* dy, uint64_t nd, const double* qx, const double* qy, uint64_t nq, double r,
                    int approximate, uint32_t* out_pairs, uint64_t cap, uint64_t* out_count) {
@@ -621,6 +735,8 @@ int geohip_debug_knn_pass_stats(geohip_ctx* ctx, uint32_t* out3) {
 int geohip_debug_knn_pass_trace(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
                                 uint64_t n, double qx, double qy, double r, uint32_t k, int ablation, uint64_t* host,
                                 uint64_t cap_words, unsigned* nblocks) {
+    const bool with_range = ablation < 0;  // measurement of the fused kNN + range pass
+    if (with_range) ablation = 0;
     int rc = begin(ctx);
     if (rc) return rc;
     PointPlan plan;
@@ -644,10 +760,27 @@ int geohip_debug_knn_pass_trace(geohip_ctx* ctx, const geohip_grid* grid, const 
     if (rc) return rc;
     unsigned long long* tr = B<unsigned long long>(ctx, S_TRACE);
     HIPCHK(hipMemsetAsync(tr, 0, 8ull * nb * 8, ctx->stream));
+    PassRangeIo rio;
+    memset(&rio, 0, sizeof rio);
+    if (with_range) {
+        rc = ensure_zeroed(ctx, S_RLB, 256 * 8 + 64);
+        if (!rc) rc = ensure(ctx, S_OUT_IDX, n * 4);
+        if (!rc) rc = ensure(ctx, S_TOTAL, 8);
+        if (rc) return rc;
+        ctx->range_epoch = ctx->range_epoch % ((1ull << 24) - 1) + 1;
+        rio.a = make_range_args(plan, qx, qy, r);
+        rio.status = B<unsigned long long>(ctx, S_RLB);
+        rio.epoch = ctx->range_epoch;
+        rio.out = B<unsigned>(ctx, S_OUT_IDX);
+        rio.cap = n;
+        rio.total = B<uint64_t>(ctx, S_TOTAL);
+        rio.trace = tr;
+    }
     hipError_t e = launch_knn_pass(x, y, n, a, B<unsigned long long>(ctx, S_PART_D), B<unsigned>(ctx, S_PART_I),
                                    B<unsigned long long>(ctx, S_SPILL_D), B<unsigned>(ctx, S_SPILL_I),
                                    B<unsigned>(ctx, S_SPILL_CNT), B<double>(ctx, S_OUT_D), B<unsigned>(ctx, S_OUT_I),
-                                   B<unsigned>(ctx, S_OUT_CNT), ctx->stream, nullptr, nullptr, tr, ablation);
+                                   B<unsigned>(ctx, S_OUT_CNT), ctx->stream, nullptr, nullptr, tr, ablation,
+                                   with_range ? &rio : nullptr);
     if (e != hipSuccess) return hip_fail(ctx, e, "knn pass launch");
     HIPCHK(hipStreamSynchronize(ctx->stream));
     HIPCHK(hipMemcpy(host, tr, 8ull * nb * 8, hipMemcpyDeviceToHost));

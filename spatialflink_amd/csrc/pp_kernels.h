@@ -36,10 +36,25 @@ constexpr size_t kKnnCounterBytes = 32768;
 // n entries, ctr is the kKnnCounterBytes zeroed counter scratch (re-armed by every launch).
 void knn_pass_geometry(uint64_t n, unsigned* nblocks, uint64_t* chunk);
 size_t knn_pass_list_entries(unsigned nblocks);
+// The range query of the same point fused into the pass (see knn_pass; status = kPassMaxBlocks
+// epoch-tagged look-back words shared with the range pass).
+struct PassRangeIo {
+    RangeArgs a;
+    int approximate;
+    unsigned long long* status;
+    unsigned long long epoch;
+    unsigned* out;
+    uint64_t cap;
+    uint64_t* total;
+    unsigned long long* trace;  // measurement only: look-back done / hits written at [8 b + 5, 6]
+};
+// whether a window of n points fits the fused kNN + range pass (block chunk <= 131072 points)
+bool knn_pass_fuses_range(uint64_t n);
 hipError_t launch_knn_pass(const double* x, const double* y, uint64_t n, const KnnArgs& args,
                            unsigned long long* list_d, unsigned* list_i, unsigned long long* spill_d, unsigned* spill_i,
                            unsigned* ctr, double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st,
-                           hipEvent_t ev0, hipEvent_t ev1, unsigned long long* trace = nullptr, int abl = 0);
+                           hipEvent_t ev0, hipEvent_t ev1, unsigned long long* trace = nullptr, int abl = 0,
+                           const PassRangeIo* range = nullptr);
 hipError_t launch_knn_merge(const unsigned long long* d, const unsigned* i, unsigned nlists, unsigned list_len,
                             unsigned k, double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st);
 // range: bitmask (16 words / 1024 pts), unit_count (units), offs (units) scratch.

@@ -17,6 +17,7 @@
 //   range_emit   bitmask -> ascending window indices.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 
 #include <type_traits>
 
@@ -168,59 +169,6 @@ template <class KB>
 __device__ __forceinline__ void hist_bound(KB& kb, unsigned k, int base) {
     const int bin = hist_kth_bin(kb.hist, k);
     if (bin >= 0 && bin < kHistBins - 1 && lane_id() == 0) atomicMin(&kb.bound, hist_edge(bin, base));
-}
-
-// exact distances of up to 64 staged candidates, survivors appended to the block buffer
-template <class KB>
-__device__ __forceinline__ void knn_dist_batch(WaveStage& st, unsigned& ccnt, KB& kb, const KnnArgs& a,
-                                               unsigned long long* __restrict__ spill_d,
-                                               unsigned* __restrict__ spill_i, unsigned* __restrict__ spill_cnt,
-                                               unsigned& appended, bool partial) {
-    const int lane = lane_id();
-    while (ccnt >= 64 || (partial && ccnt > 0)) {
-        const unsigned take = ccnt >= 64 ? 64u : ccnt;
-        const unsigned from = ccnt - take;
-        bool ok = (unsigned)lane < take;
-        double px = 0.0, py = 0.0;
-        unsigned pi = 0;
-        if (ok) {
-            px = st.cx[from + lane];
-            py = st.cy[from + lane];
-            pi = st.ci[from + lane];
-        }
-        const unsigned long long B = lds_fresh(kb.bound);
-        wave_lds_sync();
-        ccnt = from;
-        const double d = jts_pp_distance(a.qx, a.qy, px, py);
-        const unsigned long long db = (unsigned long long)__double_as_longlong(d);
-        ok = ok && db <= B;
-        const unsigned long long m = __ballot(ok);
-        if (m) {
-            const unsigned nm = (unsigned)__popcll(m);
-            unsigned pos = 0;
-            if (lane == 0) pos = atomicAdd(&kb.cnt, nm);
-            pos = __shfl(pos, 0);
-            const unsigned slot = pos + lanes_below(m);
-            unsigned gbase = 0;
-            if (pos + nm > (unsigned)KB::kCap) {  // spill the overflow to global memory (rare)
-                const unsigned first = pos > (unsigned)KB::kCap ? pos : (unsigned)KB::kCap;
-                if (lane == 0) gbase = atomicAdd(spill_cnt, pos + nm - first);
-                gbase = __shfl(gbase, 0) - (first - pos);
-            }
-            if (ok) {
-                if (slot < (unsigned)KB::kCap) {
-                    kb.bd[slot] = db;
-                    kb.bi[slot] = pi;
-                } else {
-                    store_wt(&spill_d[gbase + (slot - pos)], db);
-                    store_wt(&spill_i[gbase + (slot - pos)], pi);
-                }
-                atomicAdd(&kb.hist[hist_bin(db, a.hist_base)], 1u);
-            }
-            appended += nm;
-        }
-        wave_lds_sync();
-    }
 }
 
 // ---------------------------------------------------------------- final selection --------
@@ -700,6 +648,7 @@ constexpr unsigned kPassMaxBlocks = 256;        // one block per CU
 constexpr unsigned kPassHeads = 8;
 constexpr unsigned kLenWhole = 0x80000000u;     // list length flag: heads incomplete, read it whole
 constexpr unsigned kStatWord = (unsigned)(kKnnCounterBytes / 4) - 16;  // last final: entries, spilled, kept
+constexpr unsigned kVbWord = kTicketStride * (kMaxTicketGroups + 1);      // chunk ticket (fused range)
 
 template <int NW>
 struct PassBlock {
@@ -742,9 +691,19 @@ struct PassIo {
 
 // exact distances of up to 64 staged candidates; survivors (<= the block bound) appended to the
 // block buffer and its histogram
-template <class PB>
+// Fused range (knn_pass<.., RANGE>): staged indices carry kFlagKnn (a kNN candidate) and
+// kFlagBand (a range candidate in the exact-distance band); one distance serves both.
+constexpr unsigned kFlagKnn = 0x80000000u, kFlagBand = 0x40000000u, kIdxMask = 0x3fffffffu;
+struct RangeSide {
+    unsigned long long* mask;  // LDS hit bitmask of the block's chunk
+    uint64_t base;             // first point of the chunk
+    double r;
+};
+
+template <class PB, bool RANGE = false>
 __device__ __forceinline__ void pass_dist_batch(WaveStage& st, unsigned& ccnt, PB& kb, const KnnArgs& a,
-                                                const PassIo& io, unsigned& appended, bool partial) {
+                                                const PassIo& io, unsigned& appended, bool partial,
+                                                const RangeSide& rs = RangeSide{nullptr, 0, 0.0}) {
     const int lane = lane_id();
     while (ccnt >= 64 || (partial && ccnt > 0)) {
         const unsigned take = ccnt >= 64 ? 64u : ccnt;
@@ -762,6 +721,14 @@ __device__ __forceinline__ void pass_dist_batch(WaveStage& st, unsigned& ccnt, P
         ccnt = from;
         const double d = jts_pp_distance(a.qx, a.qy, px, py);
         const unsigned long long db = (unsigned long long)__double_as_longlong(d);
+        if (RANGE) {
+            if (ok && (pi & kFlagBand) && d <= rs.r) {
+                const unsigned off = (unsigned)((pi & kIdxMask) - rs.base);
+                atomicOr(&rs.mask[off >> 6], 1ull << (off & 63));
+            }
+            ok = ok && (pi & kFlagKnn);
+            pi &= kIdxMask;
+        }
         ok = ok && db <= B;
         const unsigned long long m = __ballot(ok);
         if (m) {
@@ -994,7 +961,8 @@ __device__ __forceinline__ void pass_final(const PassIo& io, const KnnArgs& a, u
     for (unsigned t = outn + threadIdx.x; t < k; t += NT) put(t, kSentinelD, kSentinelI);
     if (threadIdx.x == 0) {
         *io.out_count = outn;
-        store_wt(io.ctr, 0u);  // spill count re-armed for the next window on this stream
+        store_wt(io.ctr, 0u);            // spill count and the chunk ticket (fused range) re-armed
+        store_wt(io.ctr + kVbWord, 0u);  // for the next window on this stream
     }
 }
 
@@ -1019,20 +987,145 @@ __device__ __forceinline__ bool pass_arrive_last(unsigned* tickets, unsigned G) 
 
 // ABL (measurement builds only, 0 in the product): bit 0 skips the list stores, bit 1 the heads
 // (4 smallest), bit 2 the end-of-block bound refresh
-template <int NW, int ABL = 0>
+__device__ __forceinline__ unsigned long long spread32(unsigned v) {  // bit b -> bit 2b
+    unsigned long long x = v;
+    x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+    x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+    x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    x = (x | (x << 2)) & 0x3333333333333333ull;
+    x = (x | (x << 1)) & 0x5555555555555555ull;
+    return x;
+}
+
+// Range hits of a block chunk (LDS bitmask) written in ascending index order: the block
+// publishes its count (status word tagged with the launch epoch, atomic exchange: visible at the
+// device coherence point), sums the counts of every earlier chunk (wave 0, all loads in flight,
+// s_sleep back-off), and each wave stores the hits of a contiguous run of mask words.  The block
+// of the last chunk writes the total.  Earlier chunks were taken by blocks that started earlier,
+// so the wait always ends.
+template <int NW>
+__device__ __forceinline__ void pass_range_publish(const PassRangeIo& rio, const unsigned long long* bmask,
+                                                   unsigned& bcount, unsigned vb, uint64_t p0, uint64_t p1) {
+    constexpr int NT = NW * 64;
+    const unsigned nw = p1 > p0 ? (unsigned)((p1 - p0 + 63) / 64) : 0u;
+    unsigned my = 0;
+    for (unsigned t = threadIdx.x; t < nw; t += NT) my += (unsigned)__popcll(bmask[t]);
+    if (my) atomicAdd(&bcount, my);
+    __syncthreads();
+    if (threadIdx.x == 0)
+        (void)__hip_atomic_exchange(rio.status + vb, (rio.epoch << 40) | (unsigned long long)bcount, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int NW>
+__device__ __forceinline__ void pass_range_emit(const PassRangeIo& rio, const unsigned long long* bmask,
+                                                unsigned* wsum, unsigned& bcount, unsigned long long& excl_sh,
+                                                unsigned vb, uint64_t p0, uint64_t p1) {
+    const int lane = lane_id(), wid = threadIdx.x / kWave;
+    const unsigned nw = p1 > p0 ? (unsigned)((p1 - p0 + 63) / 64) : 0u;
+    const unsigned long long tag = rio.epoch << 40;
+    if (wid == 0) {
+        constexpr int kPer = kPassMaxBlocks / kWave;
+        unsigned long long v[kPer];
+        unsigned pending = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const unsigned j = (unsigned)lane + (unsigned)k * kWave;
+            v[k] = j < vb ? __hip_atomic_load(rio.status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tag;
+        }
+#pragma unroll
+        for (int k = 0; k < kPer; k++)
+            if ((v[k] >> 40) != rio.epoch) pending |= 1u << k;
+        while (pending) {
+            __builtin_amdgcn_s_sleep(8);
+#pragma unroll
+            for (int k = 0; k < kPer; k++) {
+                if (pending & (1u << k)) {
+                    v[k] = __hip_atomic_load(rio.status + lane + k * kWave, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if ((v[k] >> 40) == rio.epoch) pending &= ~(1u << k);
+                }
+            }
+        }
+        unsigned long long pre = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; k++) pre += v[k] & ((1ull << 40) - 1);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
+        if (lane == 0) excl_sh = pre;
+    }
+    if (rio.trace && threadIdx.x == 0) rio.trace[8 * (size_t)blockIdx.x + 5] = __builtin_amdgcn_s_memrealtime();
+    // per-wave word runs and their hit counts (prefix over waves)
+    const unsigned wpw = (nw + NW - 1) / NW;
+    const unsigned wb = (unsigned)wid * wpw;
+    const unsigned we = wb + wpw < nw ? wb + wpw : nw;
+    unsigned c = 0;
+    for (unsigned w = wb + (unsigned)lane; w < we; w += kWave) c += (unsigned)__popcll(bmask[w]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if (lane == 0) wsum[wid] = c;
+    __syncthreads();
+    unsigned long long obase = excl_sh;
+    for (int w = 0; w < wid; w++) obase += wsum[w];
+    const unsigned ibase = (unsigned)p0;
+    for (unsigned w0 = wb; w0 < we; w0 += kWave) {
+        const unsigned long long mine = w0 + lane < we ? bmask[w0 + lane] : 0ull;
+        const unsigned cc = (unsigned)__popcll(mine);
+        const unsigned incl = wave_incl_scan(cc);
+        const unsigned ex = incl - cc;
+        const unsigned m = we - w0 < (unsigned)kWave ? we - w0 : (unsigned)kWave;
+        for (unsigned j = 0; j < m; j++) {
+            const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)mine, (int)j);
+            const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(mine >> 32), (int)j);
+            const unsigned long long bits = ((unsigned long long)hi << 32) | lo;
+            if (!bits) continue;
+            const unsigned pj = (unsigned)__builtin_amdgcn_readlane((int)ex, (int)j);
+            if ((bits >> lane) & 1ull) {
+                const unsigned long long pos = obase + pj + lanes_below(bits);
+                if (pos < rio.cap) rio.out[pos] = ibase + (w0 + j) * 64u + (unsigned)lane;
+            }
+        }
+        obase += (unsigned)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+    }
+    if (threadIdx.x == 0 && vb == gridDim.x - 1) *rio.total = excl_sh + bcount;
+    if (rio.trace && threadIdx.x == 0) rio.trace[8 * (size_t)blockIdx.x + 6] = __builtin_amdgcn_s_memrealtime();
+}
+
+// The range query of the same point, fused into the kNN pass (C5: kNN k + range r of one query):
+// the point classification is shared, one fdlibm distance serves both, hits go to an LDS bitmask
+// of the block's chunk (chunks taken in start order from a ticket) and are written in ascending
+// index order behind a look-back over the earlier chunks' hit counts (as range_fused).
+constexpr unsigned kFusedMaskWords = 2048;  // 131072 points per block chunk at most
+
+template <int NW, int ABL = 0, bool RANGE = false>
 __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x, const double* __restrict__ y,
-                                                    uint64_t n, uint64_t chunk, KnnArgs args, PassIo io) {
+                                                    uint64_t n, uint64_t chunk, KnnArgs args, PassIo io,
+                                                    PassRangeIo rio) {
     constexpr int NT = NW * 64;
     using PB = PassBlock<NW>;
     __shared__ __attribute__((aligned(16))) WaveStage stage[NW];
     __shared__ PB kb;
+    __shared__ unsigned long long rmask[RANGE ? kFusedMaskWords : 1];
+    __shared__ unsigned rwsum[RANGE ? NW : 1];
+    __shared__ unsigned rvb, rcount;
+    __shared__ unsigned long long rexcl;
     const int lane = lane_id();
     const int wid = threadIdx.x / kWave;
     WaveStage& st = stage[wid];
-    const uint64_t blk_begin = (uint64_t)blockIdx.x * chunk;
+    if (RANGE) {
+        if (threadIdx.x == 0) {
+            rvb = atomicAdd(io.ctr + kVbWord, 1u);
+            rcount = 0;
+        }
+        __syncthreads();
+    }
+    const unsigned vb = RANGE ? rvb : blockIdx.x;
+    const uint64_t blk_begin = (uint64_t)vb * chunk;
     uint64_t blk_end = blk_begin + chunk;
     if (blk_end > n) blk_end = n;
+    const RangeSide rs{rmask, blk_begin, rio.a.r};
     for (int t = threadIdx.x; t < kHistBins; t += NT) kb.hist[t] = 0;
+    if (RANGE)
+        for (unsigned t = threadIdx.x; t < kFusedMaskWords; t += NT) rmask[t] = 0ull;
     if (threadIdx.x == 0) {
         kb.bound = kSentinelD;
         kb.cnt = 0;
@@ -1061,25 +1154,54 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
             const double t = __longlong_as_double((long long)B);
             T2 = __builtin_fmax((t * t) * kSqHi, 0x1.0p-960);
         }
+        unsigned long long hb[4];
 #pragma unroll
         for (int s = 0; s < 4; s++) {
             bool c = in_union(px[s], py[s]);
             if (!FULL) c = c && valid[s];
+            hb[s] = 0;
+            // G and C (range) lie inside the union U (kNN): a slot with no point of U in the wave
+            // is done after the box test (C5: 0.34% of the points lie in U)
+            if (!__ballot(c)) continue;
             const double dx = args.qx - px[s], dy = args.qy - py[s];
             const double d2 = dx * dx + dy * dy;
+            bool band = false;
+            if (RANGE) {
+                // PointPointRangeQuery.java:117-136: G -> hit; C -> dist <= r (squared screens first)
+                bool g = rio.a.ng > 0 && in_box(rio.a.g[0], px[s], py[s]);
+                for (int b = 1; b < rio.a.ng; b++) g = g || in_box(rio.a.g[b], px[s], py[s]);
+                const bool cbox = !g && rio.a.nc && in_box(rio.a.c, px[s], py[s]);
+                const bool ok = FULL || valid[s];
+                bool hit = ok && (g || (rio.approximate && cbox));
+                if (!rio.approximate && ok && cbox) {
+                    if (d2 < rio.a.r2lo) hit = true;
+                    else if (!(d2 > rio.a.r2hi)) band = true;
+                }
+                hb[s] = __ballot(hit);
+            }
             c = c && !(d2 > T2);
-            const unsigned long long m = __ballot(c);
-            if (c) {
+            const bool stg = c || band;
+            const unsigned long long m = __ballot(stg);
+            if (stg) {
                 const unsigned pos = ccnt + lanes_below(m);
                 st.cx[pos] = px[s];
                 st.cy[pos] = py[s];
-                st.ci[pos] = (unsigned)slot_index(ib, lane, s);
+                unsigned id = (unsigned)slot_index(ib, lane, s);
+                if (RANGE) id |= (c ? kFlagKnn : 0u) | (band ? kFlagBand : 0u);
+                st.ci[pos] = id;
             }
             ccnt += (unsigned)__popcll(m);
         }
+        if (RANGE && lane < 4) {  // word q of this iteration covers points ib + 64 q .. + 63
+            const int h = lane >> 1, half = lane & 1;
+            const unsigned e = (unsigned)(hb[2 * h] >> (32 * half));
+            const unsigned o = (unsigned)(hb[2 * h + 1] >> (32 * half));
+            const unsigned long long word = spread32(e) | (spread32(o) << 1);
+            if (word) atomicOr(&rmask[(unsigned)((ib - blk_begin) >> 6) + lane], word);
+        }
         wave_lds_sync();
         if (ccnt >= 64) {
-            pass_dist_batch(st, ccnt, kb, args, io, appended, false);
+            pass_dist_batch<PB, RANGE>(st, ccnt, kb, args, io, appended, false, rs);
             if (appended != last_hist && lds_fresh(kb.cnt) >= k) {
                 hist_bound(kb, k, args.hist_base);
                 last_hist = appended;
@@ -1135,9 +1257,12 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
         }
     }
     PASS_TRACE(io, 1);
-    pass_dist_batch(st, ccnt, kb, args, io, appended, true);
+    pass_dist_batch<PB, RANGE>(st, ccnt, kb, args, io, appended, true, rs);
     __syncthreads();
     PASS_TRACE(io, 2);
+    // the range hit count goes out first (later chunks wait for it); the hits themselves after
+    // the kNN part, so the look-back wait never delays the kNN final
+    if (RANGE) pass_range_publish<NW>(rio, rmask, rcount, vb, blk_begin, blk_end);
     // ---- end of block: final local bound B (k-th bin edge) and H (4th bin edge); survivors <= B
     // written unsorted to this block's list, those <= H (the block's smallest, usually 4-10)
     // sorted by one wave: its 4 smallest are the block's heads.  A list whose heads may be
@@ -1210,7 +1335,10 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
     if (threadIdx.x == 0) kb.last = pass_arrive_last(io.ctr + kTicketStride, io.groups) ? 1u : 0u;
     __syncthreads();
     PASS_TRACE(io, 4);
-    if (kb.last == 0) return;
+    if (kb.last == 0) {
+        if (RANGE) pass_range_emit<NW>(rio, rmask, rwsum, rcount, rexcl, vb, blk_begin, blk_end);
+        return;
+    }
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1232,20 +1360,15 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
     }
     pass_final<NT>(io, args, gd, gi, kGcap - (kGcap & 1u), kb.hist, kb.fin, kb.bd, kb.bi, kb.bi + kPassMaxBlocks);
     PASS_TRACE(io, 7);
+    if (RANGE) {
+        __syncthreads();
+        pass_range_emit<NW>(rio, rmask, rwsum, rcount, rexcl, vb, blk_begin, blk_end);
+    }
 }
 
 // ============================================================================ range =======
 constexpr int kUnitPts = 1024;  // one wave's unit: 4 iterations of 256 points; 16 mask words
 
-__device__ __forceinline__ unsigned long long spread32(unsigned v) {  // bit b -> bit 2b
-    unsigned long long x = v;
-    x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
-    x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
-    x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
-    x = (x | (x << 2)) & 0x3333333333333333ull;
-    x = (x | (x << 1)) & 0x5555555555555555ull;
-    return x;
-}
 
 struct RangeStage {
     double cx[kCandCap];
@@ -1710,10 +1833,18 @@ size_t knn_pass_list_entries(unsigned nblocks) {
     return (size_t)nblocks * (PassBlock<kPassNW>::kCap + kPassHeads) + nblocks;
 }
 
+bool knn_pass_fuses_range(uint64_t n) {
+    unsigned nb = 0;
+    uint64_t ch = 0;
+    knn_pass_geometry(n, &nb, &ch);
+    return ch <= 64ull * kFusedMaskWords && n < (1ull << 30);
+}
+
 hipError_t launch_knn_pass(const double* x, const double* y, uint64_t n, const KnnArgs& args,
                            unsigned long long* list_d, unsigned* list_i, unsigned long long* spill_d, unsigned* spill_i,
                            unsigned* ctr, double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st,
-                           hipEvent_t ev0, hipEvent_t ev1, unsigned long long* trace, int abl) {
+                           hipEvent_t ev0, hipEvent_t ev1, unsigned long long* trace, int abl,
+                           const PassRangeIo* range) {
     unsigned nblocks = 0;
     uint64_t chunk = 0;
     knn_pass_geometry(n, &nblocks, &chunk);
@@ -1729,13 +1860,19 @@ hipError_t launch_knn_pass(const double* x, const double* y, uint64_t n, const K
     const PassIo io{list_d, list_i, cap, list_d + lists, list_i + lists, list_i + lists + (size_t)kPassHeads * nblocks,
                     spill_d, nullptr, spill_i, ctr, out_d, out_i, out_count, 16u, trace};
     if (ev0) (void)hipEventRecord(ev0, st);
-    switch (abl) {
-        case 1: knn_pass<kPassNW, 1><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io); break;
-        case 2: knn_pass<kPassNW, 2><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io); break;
-        case 3: knn_pass<kPassNW, 3><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io); break;
-        case 7: knn_pass<kPassNW, 7><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io); break;
-        case 8: knn_pass<kPassNW, 8><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io); break;
-        default: knn_pass<kPassNW><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io); break;
+    PassRangeIo rio;
+    memset(&rio, 0, sizeof rio);
+    if (range) {
+        if (!knn_pass_fuses_range(n)) return hipErrorInvalidValue;
+        rio = *range;
+        knn_pass<kPassNW, 0, true><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io, rio);
+    } else {
+        switch (abl) {
+            case 1: knn_pass<kPassNW, 1><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io, rio); break;
+            case 2: knn_pass<kPassNW, 2><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io, rio); break;
+            case 8: knn_pass<kPassNW, 8><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io, rio); break;
+            default: knn_pass<kPassNW><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io, rio); break;
+        }
     }
     if (ev1) (void)hipEventRecord(ev1, st);
     return hipGetLastError();

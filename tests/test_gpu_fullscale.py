@@ -151,3 +151,8 @@ def test_c5_shard_knn_and_range_full_scale(ctx):
     want = cref.range_pp(cg, hx, hy, Q[0], Q[1], 0.05)
     assert got.cpu().numpy().astype(np.uint32).tolist() == want.tolist()
     assert len(want) > 5e4
+    # the fused one-pass form of the C5 step (geohip_knn_range_pp)
+    (fi, fd), fr = ctx.knn_range_pp(ag, x, y, Q[0], Q[1], 0.05, 100)
+    assert fi.cpu().numpy().astype(np.uint32).tolist() == wi.tolist()
+    assert np.array_equal(fd.cpu().numpy().view(np.uint64), wd.view(np.uint64))
+    assert fr.cpu().numpy().astype(np.uint32).tolist() == want.tolist()

@@ -141,6 +141,52 @@ def test_knn_random(ctx, case):
     assert np.array_equal(od.view(np.uint64), wd.view(np.uint64))
 
 
+KR_CASES = [(1000, 0.05, Q, 100, False), (100, 0.5, Q, 50, False), (500, 0.05, (116.3, 40.2), 64, False),
+            (100, 0.5, Q, 50, True), (37, 0.3, (115.45, 39.55), 10, False), (100, 0.0, Q, 5, False),
+            (100, math.nan, Q, 7, False), (100, 0.03, (117.7, 41.3), 3, False), (100, 0.2, (116.0, 40.5), 1000, False)]
+
+
+@pytest.mark.parametrize("case", range(len(KR_CASES)))
+@pytest.mark.parametrize("n", [300000, 1025, 0])
+def test_knn_range_fused(ctx, case, n):
+    """geohip_knn_range_pp (the C5 step: kNN k + range r of one query in one pass) returns exactly
+    the kNN and range results of the oracle (and so of geohip_knn_pp / geohip_range_pp)."""
+    gn, r, q, k, approx = KR_CASES[case]
+    rng = np.random.default_rng(300 + case)
+    x, y = _window(rng, n, nan_every=1009)
+    ag, cg = agrid(gn)
+    (oi, od), got = ctx.knn_range_pp(ag, x, y, q[0], q[1], r, k, approx)
+    wi, wd = cref.knn_pp(cg, x, y, q[0], q[1], r, k)
+    assert oi.tolist() == wi.tolist()
+    assert np.array_equal(od.view(np.uint64), wd.view(np.uint64))
+    assert got.tolist() == cref.range_pp(cg, x, y, q[0], q[1], r, approx).tolist()
+
+
+def test_knn_range_fused_device_repeat_and_fallback(ctx):
+    """Device buffers, the async form, repeated launches on one context (chunk ticket and
+    look-back words re-armed), and a window too large for the fused pass (two passes)."""
+    import torch
+    ag, cg = agrid(1000)
+    for n, seed in ((5_000_001, 61), (5_000_001, 62), (34_000_000, 63)):
+        x = torch.empty(n, dtype=torch.float64, device="cuda")
+        y = torch.empty(n, dtype=torch.float64, device="cuda")
+        ctx.synth_uniform_async(x, y, 0, seed, BJ)
+        hx, hy = synth.uniform(n, seed)
+        wi, wd = cref.knn_pp(cg, hx, hy, Q[0], Q[1], 0.05, 100)
+        want = cref.range_pp(cg, hx, hy, Q[0], Q[1], 0.05)
+        ki = torch.empty(100, dtype=torch.int32, device="cuda")
+        kd = torch.empty(100, dtype=torch.float64, device="cuda")
+        kc = torch.zeros(1, dtype=torch.int32, device="cuda")
+        ro = torch.empty(n, dtype=torch.int32, device="cuda")
+        rc = torch.zeros(1, dtype=torch.int64, device="cuda")
+        for _ in range(2):
+            ctx.knn_range_pp_async(ag, x, y, Q[0], Q[1], 0.05, 100, False, ki, kd, kc, ro, n, rc)
+            assert int(kc.item()) == 100 and int(rc.item()) == len(want)
+            assert ki.cpu().numpy().astype(np.uint32).tolist() == wi.tolist()
+            assert np.array_equal(kd.cpu().numpy().view(np.uint64), wd.view(np.uint64))
+            assert ro[:len(want)].cpu().numpy().astype(np.uint32).tolist() == want.tolist()
+
+
 @pytest.mark.parametrize("n", [0, 1, 3, 1000, 4097])
 def test_knn_small_windows(ctx, n):
     rng = np.random.default_rng(n + 7)
