@@ -138,32 +138,44 @@ int geohip_join_pp_count_only(geohip_ctx* ctx, const geohip_grid* grid_data, con
                               const double* qx, const double* qy, uint64_t nq, double r,
                               int approximate, uint64_t* out_count);
 
-/* npoly single-ring polygons: vertices vx/vy[ring_off[i] .. ring_off[i+1]) as given to
-   Polygon(List<List<Coordinate>>, UniformGrid) (ring closed here if open; > 3 coords).
+/* Query polygons, always in HOST memory (whatever the ctx's mem kind: they are planned on the
+   host and cached per ctx; only the points and the outputs follow GEOHIP_MEM_DEVICE).
+   Polygon i = rings [poly_rings[i], poly_rings[i+1]) (poly_rings NULL: ring i alone), ring j =
+   vertices vx/vy[ring_off[j] .. ring_off[j+1]) -- the List<List<Coordinate>> given to
+   Polygon(List<List<Coordinate>>, UniformGrid) (Polygon.java:52-66, 115-165): one ring is closed
+   here if open and needs > 3 coords; several rings are padded and closed each, the largest JTS
+   area becomes the shell and the others its holes, in createPolygonArray's order.  At most 64
+   rings per polygon (GEOHIP_ERR_UNSUPPORTED).  Where the reference throws (an empty ring, a ring
+   whose first coordinate is NaN: LinearRing not closed) or leaves the polygon null (first ring
+   with <= 3 coords): GEOHIP_ERR_ARG.  npoly == 0: no pairs, the polygon arrays may be NULL.
+   Distances: JTS point.distance(polygon) -- 0 inside the shell and outside every hole, or on any
+   ring; else the minimum over every ring's segments.
    out_pairs: 2*cap uint32 (poly_idx, point_idx), unordered. */
 int geohip_range_ppoly(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
-                       uint64_t n, const uint32_t* ring_off, const double* vx, const double* vy,
-                       uint32_t npoly, double r, int approximate,
+                       uint64_t n, const uint32_t* poly_rings, const uint32_t* ring_off, const double* vx,
+                       const double* vy, uint32_t npoly, double r, int approximate,
                        uint32_t* out_pairs, uint64_t cap, uint64_t* out_count);
 
 /* Point-polygon window join: the polygon stream replicated to its guaranteed and candidate
    cells on grid_query (UniformGrid.java:193-206, 398-410), joined with the points' gridIDs on
    grid_points; emits (point_idx, poly_idx) iff approximate or JTS point.distance(polygon) <= r
-   (no guaranteed-cell shortcut, PointPolygonJoinQuery.java:183-195).  Rings as for
+   (no guaranteed-cell shortcut, PointPolygonJoinQuery.java:183-195).  Polygons as for
    geohip_range_ppoly (host arrays).  out_pairs: 2*cap uint32 (point_idx, poly_idx), unordered. */
 int geohip_join_ppoly(geohip_ctx* ctx, const geohip_grid* grid_points, const geohip_grid* grid_query,
-                      const double* x, const double* y, uint64_t n, const uint32_t* ring_off,
-                      const double* vx, const double* vy, uint32_t npoly, double r, int approximate,
-                      uint32_t* out_pairs, uint64_t cap, uint64_t* out_count);
+                      const double* x, const double* y, uint64_t n, const uint32_t* poly_rings,
+                      const uint32_t* ring_off, const double* vx, const double* vy, uint32_t npoly,
+                      double r, int approximate, uint32_t* out_pairs, uint64_t cap, uint64_t* out_count);
 
-/* Point-polygon kNN of one query polygon (vx/vy[nv], host arrays, ring closed here): candidates
-   are the points of the polygon's G u C cells (no radius filter); distance = JTS
-   point.distance(polygon), or the bbox distance (DistanceFunctions.java:150-200) when
-   approximate.  Output: the min(k, candidates) smallest (distance, idx) ascending by distance
-   bits then idx (a NaN bbox distance ranks after +Infinity); 1 <= k <= GEOHIP_KNN_MAX_K. */
+/* Point-polygon kNN of one query polygon of nring rings (ring j = vx/vy[ring_off[j] ..
+   ring_off[j+1]), host arrays, built as for geohip_range_ppoly): candidates are the points of
+   the polygon's G u C cells (no radius filter); distance = JTS point.distance(polygon), or the
+   bbox distance (DistanceFunctions.java:150-200) when approximate.  Output: the
+   min(k, candidates) smallest (distance, idx) ascending by distance bits then idx (a NaN bbox
+   distance ranks after +Infinity); 1 <= k <= GEOHIP_KNN_PPOLY_MAX_K. */
 int geohip_knn_ppoly(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
-                     uint64_t n, const double* vx, const double* vy, uint32_t nv, double r, uint32_t k,
-                     int approximate, uint32_t* out_idx, double* out_dist, uint32_t* out_count);
+                     uint64_t n, const uint32_t* ring_off, uint32_t nring, const double* vx,
+                     const double* vy, double r, uint32_t k, int approximate,
+                     uint32_t* out_idx, double* out_dist, uint32_t* out_count);
 
 /* ---- device-resident pipeline forms (GEOHIP_MEM_DEVICE pointers; enqueue only) -------- */
 /* Writes k (dist, idx) ascending to out_dist/out_idx (device), entries past the candidate

@@ -121,12 +121,12 @@ _SIGS = {
                                c_int, _P, c_uint64, POINTER(c_uint64)]),
     "geohip_join_pp_count_only": (c_int, [_P, POINTER(Grid), POINTER(Grid), _P, _P, c_uint64, _P, _P, c_uint64,
                                           c_double, c_int, POINTER(c_uint64)]),
-    "geohip_range_ppoly": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, _P, _P, _P, c_uint32, c_double, c_int, _P,
-                                   c_uint64, POINTER(c_uint64)]),
-    "geohip_join_ppoly": (c_int, [_P, POINTER(Grid), POINTER(Grid), _P, _P, c_uint64, _P, _P, _P, c_uint32, c_double,
-                                  c_int, _P, c_uint64, POINTER(c_uint64)]),
-    "geohip_knn_ppoly": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, _P, _P, c_uint32, c_double, c_uint32, c_int, _P,
-                                 _P, POINTER(c_uint32)]),
+    "geohip_range_ppoly": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, _P, _P, _P, _P, c_uint32, c_double, c_int,
+                                   _P, c_uint64, POINTER(c_uint64)]),
+    "geohip_join_ppoly": (c_int, [_P, POINTER(Grid), POINTER(Grid), _P, _P, c_uint64, _P, _P, _P, _P, c_uint32,
+                                  c_double, c_int, _P, c_uint64, POINTER(c_uint64)]),
+    "geohip_knn_ppoly": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, _P, c_uint32, _P, _P, c_double, c_uint32, c_int,
+                                 _P, _P, POINTER(c_uint32)]),
     "geohip_plan_point": (c_int, [POINTER(Grid), c_double, c_double, c_double, POINTER(Rect), POINTER(c_uint32),
                                   POINTER(Rect), POINTER(c_uint32), POINTER(c_int32), POINTER(c_int32)]),
     "geohip_plan_cell": (c_int, [POINTER(Grid), c_double, c_double, POINTER(c_int32), POINTER(c_int32)]),
@@ -232,6 +232,16 @@ def _host(a, dtype):
     if a is not None and not isinstance(a, np.ndarray) and hasattr(a, "detach"):
         a = a.detach().cpu().numpy()
     return np.ascontiguousarray(a, dtype=dtype)
+
+
+def _poly_arrays(poly_rings, ring_off, vx, vy):
+    """(poly_rings or None, ring_off, vx, vy, npoly) as host arrays for the point-polygon calls."""
+    ring_off = _host(ring_off, np.uint32)
+    pr = None if poly_rings is None else _host(poly_rings, np.uint32)
+    npoly = (len(ring_off) if pr is None else len(pr)) - 1
+    if npoly < 0:
+        raise GeohipArgumentError("ring_off / poly_rings need at least one entry")
+    return pr, ring_off, _host(vx, np.float64), _host(vy, np.float64), npoly
 
 
 class Context:
@@ -487,20 +497,21 @@ class Context:
         self._check(rc, "join_pp_count_only")
         return cnt.value
 
-    def range_ppoly(self, grid: Grid, x, y, ring_off, vx, vy, r, approximate=False, cap=None, out=None):
-        """Pairs (polygon idx, point idx).  ``out``: optional preallocated [cap, 2] buffer."""
+    def range_ppoly(self, grid: Grid, x, y, ring_off, vx, vy, r, approximate=False, cap=None, out=None,
+                    poly_rings=None):
+        """Pairs (polygon idx, point idx).  ``out``: optional preallocated [cap, 2] buffer.
+        ``poly_rings``: polygon i = rings [poly_rings[i], poly_rings[i+1]) of ``ring_off``
+        (shell and holes, Polygon.createPolygon); None = one ring per polygon."""
         x, y = _f64(x), _f64(y)
         self._mem_for(x, y)
-        ring_off = _host(ring_off, np.uint32)
-        vx = _host(vx, np.float64)
-        vy = _host(vy, np.float64)
-        npoly = len(ring_off) - 1
+        pr, ring_off, vx, vy, npoly = _poly_arrays(poly_rings, ring_off, vx, vy)
         cnt = c_uint64(0)
         if out is not None:
             cap = len(out) if cap is None else min(cap, len(out))
         if cap is None:
-            rc = lib.geohip_range_ppoly(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), len(x), _ptr(ring_off),
-                                        _ptr(vx), _ptr(vy), npoly, r, int(approximate), None, 0, ctypes.byref(cnt))
+            rc = lib.geohip_range_ppoly(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), len(x), _ptr(pr),
+                                        _ptr(ring_off), _ptr(vx), _ptr(vy), npoly, r, int(approximate), None, 0,
+                                        ctypes.byref(cnt))
             if rc not in (OK, ERR_CAPACITY):
                 self._check(rc, "range_ppoly")
             cap = cnt.value
@@ -511,23 +522,21 @@ class Context:
             out = torch.empty((max(cap, 1), 2), dtype=torch.int32, device=x.device)
         else:
             out = np.empty((max(cap, 1), 2), dtype=np.uint32)
-        rc = lib.geohip_range_ppoly(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), len(x), _ptr(ring_off), _ptr(vx),
-                                    _ptr(vy), npoly, r, int(approximate), _ptr(out), cap, ctypes.byref(cnt))
+        rc = lib.geohip_range_ppoly(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), len(x), _ptr(pr), _ptr(ring_off),
+                                    _ptr(vx), _ptr(vy), npoly, r, int(approximate), _ptr(out), cap, ctypes.byref(cnt))
         self._check(rc, "range_ppoly")
         return out[:cnt.value]
 
     def join_ppoly(self, grid_points: Grid, grid_query: Grid, x, y, ring_off, vx, vy, r, approximate=False, cap=None,
-                   out=None):
-        """Point-polygon join: pairs (point idx, polygon idx).  ``out``: optional [cap, 2] buffer."""
+                   out=None, poly_rings=None):
+        """Point-polygon join: pairs (point idx, polygon idx).  ``out``: optional [cap, 2] buffer.
+        ``poly_rings`` as for range_ppoly."""
         x, y = _f64(x), _f64(y)
         self._mem_for(x, y)
-        ring_off = _host(ring_off, np.uint32)
-        vx = _host(vx, np.float64)
-        vy = _host(vy, np.float64)
-        npoly = len(ring_off) - 1
+        pr, ring_off, vx, vy, npoly = _poly_arrays(poly_rings, ring_off, vx, vy)
         cnt = c_uint64(0)
-        args = (self.h, ctypes.byref(grid_points), ctypes.byref(grid_query), _ptr(x), _ptr(y), len(x), _ptr(ring_off),
-                _ptr(vx), _ptr(vy), npoly, r, int(approximate))
+        args = (self.h, ctypes.byref(grid_points), ctypes.byref(grid_query), _ptr(x), _ptr(y), len(x), _ptr(pr),
+                _ptr(ring_off), _ptr(vx), _ptr(vy), npoly, r, int(approximate))
         if out is not None:
             cap = len(out) if cap is None else min(cap, len(out))
         if cap is None:
@@ -545,12 +554,14 @@ class Context:
         self._check(rc, "join_ppoly")
         return out[:cnt.value]
 
-    def knn_ppoly(self, grid: Grid, x, y, vx, vy, r, k, approximate=False):
-        """Point-polygon kNN of one polygon ring: (idx, dist) ascending by (dist, idx)."""
+    def knn_ppoly(self, grid: Grid, x, y, vx, vy, r, k, approximate=False, ring_off=None):
+        """Point-polygon kNN of one polygon: (idx, dist) ascending by (dist, idx).  ``ring_off``:
+        its rings (shell and holes) as vertex offsets into vx/vy; None = one ring."""
         x, y = _f64(x), _f64(y)
         dev = self._mem_for(x, y)
         vx = _host(vx, np.float64)
         vy = _host(vy, np.float64)
+        ring_off = _host([0, len(vx)] if ring_off is None else ring_off, np.uint32)
         if dev:
             import torch
             oi = torch.empty(k, dtype=torch.int32, device=x.device)
@@ -559,8 +570,9 @@ class Context:
             oi = np.empty(k, dtype=np.uint32)
             od = np.empty(k, dtype=np.float64)
         cnt = c_uint32(0)
-        rc = lib.geohip_knn_ppoly(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), len(x), _ptr(vx), _ptr(vy), len(vx), r,
-                                  k, int(approximate), _ptr(oi), _ptr(od), ctypes.byref(cnt))
+        rc = lib.geohip_knn_ppoly(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), len(x), _ptr(ring_off),
+                                  len(ring_off) - 1, _ptr(vx), _ptr(vy), r, k, int(approximate), _ptr(oi), _ptr(od),
+                                  ctypes.byref(cnt))
         self._check(rc, "knn_ppoly")
         return oi[:cnt.value], od[:cnt.value]
 

@@ -624,30 +624,32 @@ int geohip_join_pp_count_only(geohip_ctx* ctx, const geohip_grid* grid_data, con
 }
 
 int geohip_range_ppoly(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
-                       const uint32_t* ring_off, const double* vx, const double* vy, uint32_t npoly, double r,
-                       int approximate, uint32_t* out_pairs, uint64_t cap, uint64_t* out_count) {
+                       const uint32_t* poly_rings, const uint32_t* ring_off, const double* vx, const double* vy,
+                       uint32_t npoly, double r, int approximate, uint32_t* out_pairs, uint64_t cap,
+                       uint64_t* out_count) {
     int rc = begin(ctx);
     if (rc) return rc;
-    return ppoly_impl(ctx, grid, nullptr, 0, x, y, n, ring_off, vx, vy, npoly, r, approximate, out_pairs, cap,
-                      out_count);
-}
-
-int geohip_join_ppoly(geohip_ctx* ctx, const geohip_grid* grid_points, const geohip_grid* grid_query, const double* x,
-                      const double* y, uint64_t n, const uint32_t* ring_off, const double* vx, const double* vy,
-                      uint32_t npoly, double r, int approximate, uint32_t* out_pairs, uint64_t cap,
-                      uint64_t* out_count) {
-    int rc = begin(ctx);
-    if (rc) return rc;
-    return ppoly_impl(ctx, grid_points, grid_query, 1, x, y, n, ring_off, vx, vy, npoly, r, approximate, out_pairs,
+    return ppoly_impl(ctx, grid, nullptr, 0, x, y, n, poly_rings, ring_off, vx, vy, npoly, r, approximate, out_pairs,
                       cap, out_count);
 }
 
-int geohip_knn_ppoly(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
-                     const double* vx, const double* vy, uint32_t nv, double r, uint32_t k, int approximate,
-                     uint32_t* out_idx, double* out_dist, uint32_t* out_count) {
+int geohip_join_ppoly(geohip_ctx* ctx, const geohip_grid* grid_points, const geohip_grid* grid_query, const double* x,
+                      const double* y, uint64_t n, const uint32_t* poly_rings, const uint32_t* ring_off,
+                      const double* vx, const double* vy, uint32_t npoly, double r, int approximate,
+                      uint32_t* out_pairs, uint64_t cap, uint64_t* out_count) {
     int rc = begin(ctx);
     if (rc) return rc;
-    return knn_ppoly_impl(ctx, grid, x, y, n, vx, vy, nv, r, k, approximate, out_idx, out_dist, out_count);
+    return ppoly_impl(ctx, grid_points, grid_query, 1, x, y, n, poly_rings, ring_off, vx, vy, npoly, r, approximate,
+                      out_pairs, cap, out_count);
+}
+
+int geohip_knn_ppoly(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
+                     const uint32_t* ring_off, uint32_t nring, const double* vx, const double* vy, double r,
+                     uint32_t k, int approximate, uint32_t* out_idx, double* out_dist, uint32_t* out_count) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    return knn_ppoly_impl(ctx, grid, x, y, n, ring_off, nring, vx, vy, r, k, approximate, out_idx, out_dist,
+                          out_count);
 }
 
 int geohip_plan_point(const geohip_grid* grid, double qx, double qy, double r, geohip_rect* g_rects, uint32_t* n_g,

@@ -776,7 +776,17 @@ struct PolyDev {
     double sy0, sinv;       // slab of y = clamp(floor((y - sy0) * sinv), 0, ns - 1)
     double E;               // distance lists hold every segment within E of the slab in y
     uint32_t loff, llen;    // slab block in the u16 list blob (SlabView)
+    uint32_t nring;         // closed rings in the vertex run: shell first, then the holes
+    uint32_t eoff;          // nring > 1: ring envelopes at renv[4 * eoff ...] (minx, miny, maxx, maxy)
+    double gb[4];           // box of every ring (= bb unless a hole leaves the shell's envelope):
+                            // the distance screens and slab lists are built on it
 };
+
+// Polygons with holes: rings are stored back to back in one vertex run, with a ring id per
+// vertex (u8, < kMaxRings); segment (v[e], v[e+1]) exists iff both ends carry the same id (the
+// junction between two rings is not an edge).  Crossing parity and boundary flags are kept per
+// ring as 64-bit masks, so segments may still be visited in any order.
+constexpr uint32_t kMaxRings = 64;
 
 // A polygon's y-slab index (u16): cbeg[ns + 1] | dbeg[ns + 1] | segment ids.  Crossing list of
 // slab s: segments (v[e], v[e+1]) whose y-range meets the slab (padded) -- every segment that
@@ -902,7 +912,7 @@ __device__ __forceinline__ bool point_polygon_within(double px, double py, const
         }
         if (boundary || (crossings & 1)) return true;  // distance 0
     }
-    const double lim2 = screen_lim2(px, py, P.bb, r);
+    const double lim2 = screen_lim2(px, py, P.gb, r);
     if (sv.ns && lim2 <= P.E * P.E) {
         const uint32_t k1 = sv.dbeg(s + 1);
         uint32_t k = sv.dbeg(s);
@@ -922,6 +932,71 @@ __device__ __forceinline__ bool point_polygon_within(double px, double py, const
     }
     for (int i = 0; i < nv - 1; i++)
         if (segment_within(px, py, vx[i], vy[i], vx[i + 1], vy[i + 1], r, lim2)) return true;
+    return false;
+}
+
+// PointLocator.locateInPolygon (JTS 1.16.1) from per-ring masks: bit j of bnd = some segment of
+// ring j flags the point as on it, bit j of par = odd crossing count of ring j.  Shell boundary
+// -> on the polygon; even shell parity -> outside; else the holes in order: a hole whose envelope
+// excludes the point is EXTERIOR to it (locateInPolygonRing's envelope test), boundary -> on the
+// polygon, interior -> outside; no hole claims the point -> inside.  true = distance 0.
+__device__ __forceinline__ bool rings_locate_inside(double px, double py, unsigned long long bnd,
+                                                    unsigned long long par, const double* __restrict__ renv) {
+    if (bnd & 1ull) return true;
+    if (!(par & 1ull)) return false;
+    unsigned long long m = (bnd | par) & ~1ull;
+    while (m) {
+        const int h = __builtin_ctzll(m);
+        m &= m - 1;
+        const double* e = renv + 4 * h;
+        if (px > e[2] || px < e[0] || py > e[3] || py < e[1]) continue;
+        if ((bnd >> h) & 1ull) return true;
+        return false;  // odd parity of hole h: inside the hole
+    }
+    return true;
+}
+
+// point_polygon_within for a polygon with holes (P.nring > 1): the same crossing and distance
+// lists (plan_slabs leaves the ring junctions out of them), crossings kept per ring.  Distance:
+// any segment of any ring within r (DistanceOp's per-ring envelope skip only drops rings whose
+// envelope is farther than the running minimum, which never holds a segment within r of p
+// except through a rounding tie between the envelope and segment distances).
+__device__ __forceinline__ bool point_polygon_within_rings(double px, double py, const double* __restrict__ vx,
+                                                        const double* __restrict__ vy,
+                                                        const uint8_t* __restrict__ vr,
+                                                        const double* __restrict__ renv, const PolyDev& P,
+                                                        const SlabView& sv, double r) {
+    const int nv = (int)P.nv;
+    const bool in_env = !(px > P.bb[2] || px < P.bb[0] || py > P.bb[3] || py < P.bb[1]);
+    const uint32_t s = sv.ns ? slab_of(py, P.sy0, P.sinv, sv.ns) : 0u;
+    if (in_env) {
+        unsigned long long bnd = 0, par = 0;
+        auto seg = [&](uint32_t e) {
+            bool b = false;
+            int c = 0;
+            count_segment(px, py, vx[e + 1], vy[e + 1], vx[e], vy[e], b, c);
+            const unsigned long long bit = 1ull << vr[e];
+            bnd |= b ? bit : 0ull;
+            par ^= (c & 1) ? bit : 0ull;
+        };
+        if (sv.ns) {
+            for (uint32_t k = sv.cbeg(s); k < sv.cbeg(s + 1); k++) seg(sv.id(k));
+        } else {
+            for (int e = 0; e < nv - 1; e++)
+                if (vr[e] == vr[e + 1]) seg((uint32_t)e);
+        }
+        if (rings_locate_inside(px, py, bnd, par, renv)) return true;
+    }
+    const double lim2 = screen_lim2(px, py, P.gb, r);
+    if (sv.ns && lim2 <= P.E * P.E) {
+        for (uint32_t k = sv.dbeg(s); k < sv.dbeg(s + 1); k++) {
+            const uint32_t e = sv.id(k);
+            if (segment_within(px, py, vx[e], vy[e], vx[e + 1], vy[e + 1], r, lim2)) return true;
+        }
+        return false;
+    }
+    for (int e = 0; e < nv - 1; e++)
+        if (vr[e] == vr[e + 1] && segment_within(px, py, vx[e], vy[e], vx[e + 1], vy[e + 1], r, lim2)) return true;
     return false;
 }
 
@@ -992,13 +1067,15 @@ __global__ void ppoly_words(const PolyWork* __restrict__ work, uint32_t nwork, c
 template <bool APPROX>
 __global__ __launch_bounds__(kTB) void ppoly_eval(TileBins tb, const PolyWork* __restrict__ work,
                                                   const PolyDev* __restrict__ polys, const double* __restrict__ vx,
-                                                  const double* __restrict__ vy, const int32_t* __restrict__ rects,
+                                                  const double* __restrict__ vy, const uint8_t* __restrict__ vring,
+                                                  const double* __restrict__ renv, const int32_t* __restrict__ rects,
                                                   const uint16_t* __restrict__ slabs, double r, int r_is_max,
                                                   const unsigned long long* __restrict__ wofs,
                                                   unsigned long long* __restrict__ mask,
                                                   unsigned long long* __restrict__ bcount) {
     __shared__ double lvx[kMaxLdsVerts];
     __shared__ double lvy[kMaxLdsVerts];
+    __shared__ uint8_t lvr[kMaxLdsVerts];
     __shared__ uint16_t lsl[kMaxLdsSlab];
     __shared__ unsigned long long lmask[kMaskWords];
     __shared__ CandQueue cq[kTB / kWave];
@@ -1011,10 +1088,12 @@ __global__ __launch_bounds__(kTB) void ppoly_eval(TileBins tb, const PolyWork* _
     unsigned long long* gm = mask + wofs[blockIdx.x];
     const bool v_lds = P.nv <= (uint32_t)kMaxLdsVerts;
     const bool s_lds = P.llen <= (uint32_t)kMaxLdsSlab;
+    const bool holes = P.nring > 1;
     if (v_lds)
         for (uint32_t t = threadIdx.x; t < P.nv; t += kTB) {
             lvx[t] = vx[P.voff + t];
             lvy[t] = vy[P.voff + t];
+            if (holes) lvr[t] = vring[P.voff + t];
         }
     if (s_lds)
         for (uint32_t t = threadIdx.x; t < P.llen; t += kTB) lsl[t] = slabs[P.loff + t];
@@ -1024,6 +1103,8 @@ __global__ __launch_bounds__(kTB) void ppoly_eval(TileBins tb, const PolyWork* _
     __syncthreads();
     const double* rvx = v_lds ? lvx : vx + P.voff;
     const double* rvy = v_lds ? lvy : vy + P.voff;
+    const uint8_t* rvr = v_lds ? lvr : vring + P.voff;
+    const double* rre = renv + 4 * (size_t)P.eoff;
     const SlabView sv{s_lds ? lsl : slabs + P.loff, P.ns};
     unsigned long long* mk = lds_mask ? lmask : gm;  // global words: zeroed by the host, atomics only
     const int wid = threadIdx.x / kWave, lane = lane_id();
@@ -1037,7 +1118,9 @@ __global__ __launch_bounds__(kTB) void ppoly_eval(TileBins tb, const PolyWork* _
         if ((unsigned)lane < take) {
             const double px = Q.x[from + lane], py = Q.y[from + lane];
             const unsigned pos = Q.pos[from + lane];
-            if (point_polygon_within(px, py, rvx, rvy, P, sv, r)) atomicOr(&mk[pos >> 6], 1ull << (pos & 63));
+            const bool in = holes ? point_polygon_within_rings(px, py, rvx, rvy, rvr, rre, P, sv, r)
+                                  : point_polygon_within(px, py, rvx, rvy, P, sv, r);
+            if (in) atomicOr(&mk[pos >> 6], 1ull << (pos & 63));
         }
         wave_lds_sync();
         qn = from;
@@ -1074,7 +1157,7 @@ __global__ __launch_bounds__(kTB) void ppoly_eval(TileBins tb, const PolyWork* _
             if (g || c) {
                 if (g || r_is_max) hit = true;
                 else if (APPROX) hit = bbox_distance(px, py, P.bb) <= r;
-                else need = !(box_dist2(px, py, P.bb[0], P.bb[1], P.bb[2], P.bb[3]) > screen_lim2(px, py, P.bb, r));
+                else need = !(box_dist2(px, py, P.gb[0], P.gb[1], P.gb[2], P.gb[3]) > screen_lim2(px, py, P.gb, r));
             }
         }
         const unsigned long long m = __ballot(hit);
@@ -1147,7 +1230,9 @@ __global__ __launch_bounds__(kTB) void ppoly_outside(const double* __restrict__ 
                                                      uint32_t npoly, const int32_t* __restrict__ rects, PairSink sink,
                                                      const double* __restrict__ vx = nullptr,
                                                      const double* __restrict__ vy = nullptr,
-                                                     const uint16_t* __restrict__ slabs = nullptr, double r = 0.0) {
+                                                     const uint16_t* __restrict__ slabs = nullptr, double r = 0.0,
+                                                     const uint8_t* __restrict__ vring = nullptr,
+                                                     const double* __restrict__ renv = nullptr) {
     __shared__ uint2 pbuf[WRITE ? kTB / kWave : 1][WRITE ? kPolyPairs : 1];
     __shared__ unsigned long long bsh;
     const int wid = threadIdx.x / kWave;
@@ -1167,8 +1252,12 @@ __global__ __launch_bounds__(kTB) void ppoly_outside(const double* __restrict__ 
                 const double px = x[pid], py = y[pid];
                 const int32_t cx = d_axis_cell(px, mnx, l), cy = d_axis_cell(py, mny, l);
                 hit = DIST ? in_rects(rects + 4 * P.coff, P.nc, cx, cy) : in_rects(rects + 4 * P.goff, P.ng, cx, cy);
-                if (DIST && hit)
-                    hit = point_polygon_within(px, py, vx + P.voff, vy + P.voff, P, SlabView{slabs + P.loff, P.ns}, r);
+                if (DIST && hit) {
+                    const SlabView sv{slabs + P.loff, P.ns};
+                    hit = P.nring > 1 ? point_polygon_within_rings(px, py, vx + P.voff, vy + P.voff, vring + P.voff,
+                                                                   renv + 4 * (size_t)P.eoff, P, sv, r)
+                                      : point_polygon_within(px, py, vx + P.voff, vy + P.voff, P, sv, r);
+                }
             }
             pairs_push<WRITE, kPolyPairs>(buf, cnt, hit, p, pid, &bsh, sink);
         }
@@ -1252,7 +1341,8 @@ __device__ __forceinline__ void hist_add(unsigned* h, unsigned dg) {
 
 struct PpknnPoly {
     double bb[4];
-    uint32_t nv, nrect;  // closed ring length; G rects then C rects (cell space)
+    uint32_t nv, nrect;  // closed rings' total length; G rects then C rects (cell space)
+    uint32_t nring, pad;  // rings (shell first); > 1: ring ids per vertex + ring envelopes
 };
 
 __global__ __launch_bounds__(1024) void rsel_init(RselState* __restrict__ st, unsigned k, unsigned small_max) {
@@ -1400,20 +1490,25 @@ template <bool APPROX>
 __global__ __launch_bounds__(kTB) void ppknn_dist(const double* __restrict__ x, const double* __restrict__ y,
                                                   const unsigned* __restrict__ cand, RselState* __restrict__ st,
                                                   const double* __restrict__ vx, const double* __restrict__ vy,
+                                                  const uint8_t* __restrict__ vring, const double* __restrict__ renv,
                                                   PpknnPoly P, unsigned long long* __restrict__ key) {
     __shared__ double lvx[kMaxLdsVerts];
     __shared__ double lvy[kMaxLdsVerts];
+    __shared__ uint8_t lvr[kMaxLdsVerts];
     __shared__ unsigned lh[kRselBins];  // round-0 digits of this block's keys (-> st->hist0)
     for (int t = threadIdx.x; t < kRselBins; t += kTB) lh[t] = 0;
     const bool v_lds = P.nv <= (uint32_t)kMaxLdsVerts;
+    const bool holes = P.nring > 1;
     if (!APPROX && v_lds)
         for (uint32_t t = threadIdx.x; t < P.nv; t += kTB) {
             lvx[t] = vx[t];
             lvy[t] = vy[t];
+            if (holes) lvr[t] = vring[t];
         }
     __syncthreads();
     const double* rvx = v_lds ? lvx : vx;
     const double* rvy = v_lds ? lvy : vy;
+    const uint8_t* rvr = v_lds ? lvr : vring;
     const unsigned m = st->ncand;
     if (APPROX) {
         for (unsigned t = blockIdx.x * kTB + threadIdx.x; t < m; t += gridDim.x * kTB) {
@@ -1443,20 +1538,50 @@ __global__ __launch_bounds__(kTB) void ppknn_dist(const double* __restrict__ x, 
         bool boundary = false;
         int crossings = 0;
         double md = 1.7976931348623157e308;
-        for (int e = (int)sub; e < nv - 1; e += (int)kG) {
-            const double ax = rvx[e], ay = rvy[e], bx = rvx[e + 1], by = rvy[e + 1];
-            if (in_env) count_segment(px, py, bx, by, ax, ay, boundary, crossings);
-            const double d = point_segment(px, py, ax, ay, bx, by);
-            md = d < md ? d : md;
-        }
+        double d;
+        if (!holes) {
+            for (int e = (int)sub; e < nv - 1; e += (int)kG) {
+                const double ax = rvx[e], ay = rvy[e], bx = rvx[e + 1], by = rvy[e + 1];
+                if (in_env) count_segment(px, py, bx, by, ax, ay, boundary, crossings);
+                const double sd = point_segment(px, py, ax, ay, bx, by);
+                md = sd < md ? sd : md;
+            }
 #pragma unroll
-        for (unsigned o = 1; o < kG; o <<= 1) {
-            crossings += __shfl_xor(crossings, (int)o);
-            boundary = (__shfl_xor((int)boundary, (int)o) != 0) || boundary;
-            const double od = __shfl_xor(md, (int)o);
-            md = od < md ? od : md;
+            for (unsigned o = 1; o < kG; o <<= 1) {
+                crossings += __shfl_xor(crossings, (int)o);
+                boundary = (__shfl_xor((int)boundary, (int)o) != 0) || boundary;
+                const double od = __shfl_xor(md, (int)o);
+                md = od < md ? od : md;
+            }
+            d = (in_env && (boundary || (crossings & 1))) ? 0.0 : md;
+        } else {
+            // per-ring boundary / parity masks (rings_locate_inside); the minimum covers every
+            // ring's segments (DistanceOp's envelope skip drops only rings farther than the
+            // running minimum)
+            unsigned long long bnd = 0, par = 0;
+            for (int e = (int)sub; e < nv - 1; e += (int)kG) {
+                const unsigned rid = rvr[e];
+                if (rid != rvr[e + 1]) continue;  // junction between two rings
+                const double ax = rvx[e], ay = rvy[e], bx = rvx[e + 1], by = rvy[e + 1];
+                if (in_env) {
+                    bool b = false;
+                    int c = 0;
+                    count_segment(px, py, bx, by, ax, ay, b, c);
+                    bnd |= b ? 1ull << rid : 0ull;
+                    par ^= (c & 1) ? 1ull << rid : 0ull;
+                }
+                const double sd = point_segment(px, py, ax, ay, bx, by);
+                md = sd < md ? sd : md;
+            }
+#pragma unroll
+            for (unsigned o = 1; o < kG; o <<= 1) {
+                bnd |= __shfl_xor(bnd, (int)o);
+                par ^= __shfl_xor(par, (int)o);
+                const double od = __shfl_xor(md, (int)o);
+                md = od < md ? od : md;
+            }
+            d = (in_env && rings_locate_inside(px, py, bnd, par, renv)) ? 0.0 : md;
         }
-        const double d = (in_env && (boundary || (crossings & 1))) ? 0.0 : md;
         if (sub == 0) {
             const unsigned long long bits = (unsigned long long)__double_as_longlong(d);
             key[t0] = bits;
@@ -2204,7 +2329,9 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
 
 // y-slab lists of one polygon (SlabView), appended to blob; P.ns = 0 when they cannot be built
 // (few or very many segments, non-finite extent): the device then visits every segment.
-void plan_slabs(PolyDev& P, const double* ry, double r, double cell_len, std::vector<uint16_t>& blob) {
+// rid (nullable): ring id per vertex; a ring junction (rid[e] != rid[e+1]) is no segment.
+void plan_slabs(PolyDev& P, const double* ry, const uint8_t* rid, double r, double cell_len,
+                std::vector<uint16_t>& blob) {
     P.ns = 0;
     P.sy0 = 0.0;
     P.sinv = 0.0;
@@ -2213,12 +2340,12 @@ void plan_slabs(PolyDev& P, const double* ry, double r, double cell_len, std::ve
     P.llen = 0;
     const uint32_t nseg = P.nv >= 2 ? P.nv - 1 : 0;
     if (nseg < 8 || nseg > 30000) return;
-    const double ext = (P.bb[2] - P.bb[0]) + (P.bb[3] - P.bb[1]);
+    const double ext = (P.gb[2] - P.gb[0]) + (P.gb[3] - P.gb[1]);
     // E bounds the screen radius of every point a work item evaluates (C cells lie within
     // r + 2 cells of the envelope); a point with a larger screen radius takes the full loop
     const double E = r + 0x1.0p-40 * 4.0 * (ext + std::fabs(r) + cell_len);
     if (!(E >= 0.0) || !std::isfinite(E) || !std::isfinite(ext)) return;
-    const double y0 = P.bb[1] - E, y1 = P.bb[3] + E;
+    const double y0 = P.gb[1] - E, y1 = P.gb[3] + E;
     const uint32_t ns = std::min<uint32_t>(64, nseg);
     const double span = y1 - y0;
     if (!(span > 0.0) || !std::isfinite(span)) return;
@@ -2230,6 +2357,7 @@ void plan_slabs(PolyDev& P, const double* ry, double r, double cell_len, std::ve
     auto ranges = [&](uint32_t e, uint32_t& c0, uint32_t& c1, uint32_t& d0, uint32_t& d1) -> bool {
         const double a = ry[e], b = ry[e + 1];
         if (a != a || b != b) return false;
+        if (rid && rid[e] != rid[e + 1]) return false;
         const double lo = std::min(a, b), hi = std::max(a, b);
         c0 = slab_of(lo - pad, y0, sinv, ns);
         c1 = slab_of(hi + pad, y0, sinv, ns);
@@ -2278,10 +2406,12 @@ struct PolyCache {
     geohip_grid grid{}, gq{};
     int jmode = 0;
     double r = 0.0;
-    std::vector<uint32_t> ring_off;
-    std::vector<double> vx, vy;
+    std::vector<uint32_t> poly_rings;  // as given, or the identity when the caller passed none
+    std::vector<uint32_t> ring_off;    // ring_off[R0 .. R1] (absolute vertex offsets)
+    std::vector<double> vx, vy;        // vx/vy[ring_off[R0] .. ring_off[R1])
     std::vector<PolyDev> pd;
-    std::vector<double> hvx, hvy;
+    std::vector<double> hvx, hvy, henv;
+    std::vector<uint8_t> hvr;
     std::vector<int32_t> hrects;
     std::vector<PolyWork> hwork;
     std::vector<uint16_t> hslab;
@@ -2293,12 +2423,19 @@ struct PolyCache {
 std::mutex g_pcache_mu;
 std::unordered_map<const geohip_ctx*, PolyCache> g_pcache;
 
-bool same_inputs(const PolyCache& c, const geohip_grid& g, double r, const uint32_t* ring_off, uint32_t npoly,
-                 const double* vx, const double* vy) {
+// ring range of polygon p: [poly_rings[p], poly_rings[p+1]) (poly_rings null: ring p)
+inline uint32_t ring_of(const uint32_t* poly_rings, uint32_t p) { return poly_rings ? poly_rings[p] : p; }
+
+bool same_inputs(const PolyCache& c, const geohip_grid& g, double r, const uint32_t* poly_rings,
+                 const uint32_t* ring_off, uint32_t npoly, const double* vx, const double* vy) {
     if (c.grid.min_x != g.min_x || c.grid.min_y != g.min_y || c.grid.cell_len != g.cell_len || c.grid.n != g.n) return false;
-    if (memcmp(&c.r, &r, sizeof r) != 0 || c.ring_off.size() != (size_t)npoly + 1) return false;
-    if (memcmp(c.ring_off.data(), ring_off, ((size_t)npoly + 1) * 4) != 0) return false;
-    const size_t v0 = npoly ? ring_off[0] : 0, v1 = npoly ? ring_off[npoly] : 0;
+    if (memcmp(&c.r, &r, sizeof r) != 0 || c.poly_rings.size() != (size_t)npoly + 1) return false;
+    for (uint32_t p = 0; p <= npoly; p++)
+        if (c.poly_rings[p] != ring_of(poly_rings, p)) return false;
+    const uint32_t R0 = c.poly_rings[0], R1 = c.poly_rings[npoly];
+    if (c.ring_off.size() != (size_t)(R1 - R0) + 1) return false;
+    if (memcmp(c.ring_off.data(), ring_off + R0, ((size_t)(R1 - R0) + 1) * 4) != 0) return false;
+    const size_t v0 = ring_off[R0], v1 = ring_off[R1];
     if (v1 < v0 || c.vx.size() != v1 - v0) return false;
     return memcmp(c.vx.data(), vx + v0, (v1 - v0) * 8) == 0 && memcmp(c.vy.data(), vy + v0, (v1 - v0) * 8) == 0;
 }
@@ -2308,9 +2445,34 @@ void ppoly_cache_drop(geohip_ctx* ctx) {
     g_pcache.erase(ctx);
 }
 
+// Ring ids, ring envelopes and the box of every ring of a planned polygon (PolyPlan rings).
+// Envelopes as JTS computes them (Envelope.expandToInclude: NaN coordinates never enter).
+static void ring_tables(const PolyPlan& pl, std::vector<uint8_t>& vr, std::vector<double>& env, double gb[4]) {
+    const size_t nring = pl.ring_start.size() - 1;
+    for (size_t j = 0; j < nring; j++) {
+        const uint32_t a = pl.ring_start[j], b = pl.ring_start[j + 1];
+        double mnx = pl.rx[a], mxx = pl.rx[a], mny = pl.ry[a], mxy = pl.ry[a];
+        for (uint32_t i = a; i < b; i++) {
+            vr.push_back((uint8_t)j);
+            const double x = pl.rx[i], y = pl.ry[i];
+            if (x < mnx) mnx = x;
+            if (x > mxx) mxx = x;
+            if (y < mny) mny = y;
+            if (y > mxy) mxy = y;
+        }
+        if (nring > 1) env.insert(env.end(), {mnx, mny, mxx, mxy});
+        if (j == 0) { gb[0] = mnx; gb[1] = mny; gb[2] = mxx; gb[3] = mxy; }
+        else {
+            gb[0] = std::min(gb[0], mnx); gb[1] = std::min(gb[1], mny);
+            gb[2] = std::max(gb[2], mxx); gb[3] = std::max(gb[3], mxy);
+        }
+    }
+}
+
 int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, int join, const double* x,
-               const double* y, uint64_t n, const uint32_t* ring_off, const double* vx, const double* vy, uint32_t npoly,
-               double r, int approximate, uint32_t* out_pairs, uint64_t cap, uint64_t* out_count) {
+               const double* y, uint64_t n, const uint32_t* poly_rings, const uint32_t* ring_off, const double* vx,
+               const double* vy, uint32_t npoly, double r, int approximate, uint32_t* out_pairs, uint64_t cap,
+               uint64_t* out_count) {
     if (!out_count) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null out_count");
     *out_count = 0;
     int rc = check_grid_basic(ctx, grid, join ? "point grid" : "grid");
@@ -2321,8 +2483,9 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     // (exact) or emitted (approximate); the range query's guaranteed shortcut does not apply
     const int jmode = join ? (approximate ? 2 : 1) : 0;
     if (n >= 0xffffffffull) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "window larger than 2^32-1 points");
-    if (npoly && (!ring_off || !vx || !vy)) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null polygon arrays");
     if (cap && !out_pairs) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null out_pairs");
+    if (npoly == 0) return GEOHIP_OK;  // no polygon: no pair (the polygon arrays may be null)
+    if (!ring_off || !vx || !vy) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null polygon arrays");
     hipStream_t st = ctx_stream(ctx);
     const bool dev = ctx_mem(ctx) == GEOHIP_MEM_DEVICE;
     const int32_t nb = gq->n;  // key space: the polygons' (query) grid; point cells on `grid`
@@ -2330,7 +2493,13 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     static const bool prof = getenv("GEOHIP_HOST_PROFILE") != nullptr;  // measurement only
     auto now = [] { return std::chrono::steady_clock::now(); };
     const auto t_start = now();
-    // polygon planning (host): ring closure, envelope, G / C rectangles (plan.cpp), the
+    for (uint32_t p = 0; p < npoly; p++)
+        if (ring_of(poly_rings, p + 1) <= ring_of(poly_rings, p))
+            return ctx_fail(ctx, GEOHIP_ERR_ARG, "poly_rings not strictly ascending (a polygon needs a ring)");
+    const uint32_t R0 = ring_of(poly_rings, 0), R1 = ring_of(poly_rings, npoly);
+    for (uint32_t j = R0; j < R1; j++)
+        if (ring_off[j + 1] < ring_off[j]) return ctx_fail(ctx, GEOHIP_ERR_ARG, "ring_off not ascending");
+    // polygon planning (host): rings (createPolygon), envelope, G / C rectangles (plan.cpp), the
     // (polygon, tile) work items of each polygon's walk region and the slab lists -- or the
     // cached plan of the same inputs
     PolyCache* pc = nullptr;
@@ -2338,11 +2507,9 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
         std::lock_guard<std::mutex> lk(g_pcache_mu);
         pc = &g_pcache[ctx];
     }
-    bool cached = same_inputs(*pc, *grid, r, ring_off, npoly, vx, vy) && pc->jmode == jmode &&
+    bool cached = same_inputs(*pc, *grid, r, poly_rings, ring_off, npoly, vx, vy) && pc->jmode == jmode &&
                   memcmp(&pc->gq, gq, sizeof *gq) == 0;
     if (!cached) {
-        for (uint32_t p = 0; p < npoly; p++)
-            if (ring_off[p + 1] < ring_off[p]) return ctx_fail(ctx, GEOHIP_ERR_ARG, "ring_off not ascending");
         PolyCache fresh;
         std::vector<PolyDev>& pd = fresh.pd;
         std::vector<double>& hvx = fresh.hvx;
@@ -2355,16 +2522,19 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
         for (uint32_t p = 0; p < npoly; p++) {
             PolyPlan pl;
             std::string err;
-            const uint32_t b = ring_off[p], e = ring_off[p + 1];
-            if (e < b) return ctx_fail(ctx, GEOHIP_ERR_ARG, "ring_off not ascending");
-            rc = plan_polygon(*gq, vx + b, vy + b, e - b, r, &pl, &err);
+            const uint32_t r0 = ring_of(poly_rings, p), r1 = ring_of(poly_rings, p + 1);
+            if (r1 - r0 > kMaxRings) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "polygon with more than 64 rings");
+            rc = plan_polygon_rings(*gq, ring_off + r0, r1 - r0, vx, vy, r, &pl, &err);
             if (rc) return ctx_fail(ctx, rc, err);
             PolyDev& P = pd[p];
             memset(&P, 0, sizeof P);
             P.voff = (uint32_t)hvx.size();
             P.nv = (uint32_t)pl.rx.size();
+            P.nring = (uint32_t)pl.ring_start.size() - 1;
+            P.eoff = (uint32_t)(fresh.henv.size() / 4);
             hvx.insert(hvx.end(), pl.rx.begin(), pl.rx.end());
             hvy.insert(hvy.end(), pl.ry.begin(), pl.ry.end());
+            ring_tables(pl, fresh.hvr, fresh.henv, P.gb);
             for (int i = 0; i < 4; i++) P.bb[i] = pl.bbox[i];
             P.goff = (uint32_t)(hrects.size() / 4);
             P.ng = (uint32_t)pl.g.size();
@@ -2386,7 +2556,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             // the C rects follow the G rects: the join sees one list, all checked or all emitted
             if (jmode == 1) { P.coff = P.goff; P.nc += P.ng; P.ng = 0; }
             if (jmode == 2) { P.ng += P.nc; P.nc = 0; }
-            plan_slabs(P, pl.ry.data(), r, gq->cell_len, hslab);
+            plan_slabs(P, pl.ry.data(), P.nring > 1 ? fresh.hvr.data() + P.voff : nullptr, r, gq->cell_len, hslab);
             if (wx0 <= wx1 && wy0 <= wy1)
                 for (int32_t a = wx0 / geo.ts; a <= wx1 / geo.ts; a++)
                     for (int32_t c = wy0 / geo.ts; c <= wy1 / geo.ts; c++)
@@ -2415,10 +2585,11 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
         fresh.gq = *gq;
         fresh.jmode = jmode;
         fresh.r = r;
-        fresh.ring_off.assign(ring_off, ring_off + npoly + 1);
-        const size_t v0 = npoly ? ring_off[0] : 0, v1 = npoly ? ring_off[npoly] : 0;
-        fresh.vx.assign(vx + v0, vx + v1);
-        fresh.vy.assign(vy + v0, vy + v1);
+        fresh.poly_rings.resize((size_t)npoly + 1);
+        for (uint32_t p = 0; p <= npoly; p++) fresh.poly_rings[p] = ring_of(poly_rings, p);
+        fresh.ring_off.assign(ring_off + R0, ring_off + R1 + 1);
+        fresh.vx.assign(vx + ring_off[R0], vx + ring_off[R1]);
+        fresh.vy.assign(vy + ring_off[R0], vy + ring_off[R1]);
         *pc = std::move(fresh);
     }
     const std::vector<PolyDev>& pd = pc->pd;
@@ -2427,6 +2598,8 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     const std::vector<int32_t>& hrects = pc->hrects;
     const std::vector<PolyWork>& hwork = pc->hwork;
     const std::vector<uint16_t>& hslab = pc->hslab;
+    const std::vector<uint8_t>& hvr = pc->hvr;
+    const std::vector<double>& henv = pc->henv;
     const bool any_outside = pc->any_outside;
     const std::vector<uint32_t>& keep = pc->keep;
     Scratch S{ctx};
@@ -2434,18 +2607,23 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     rc = ctx_stage_xy(ctx, x, y, n, 0, &dx, &dy);
     if (rc) return rc;
     const auto t_planned = now();
-    // polygon tables in one device blob: PolyDev[] | vx | vy | rects | work | slab lists
+    // polygon tables in one device blob:
+    //   PolyDev[] | vx | vy | ring envelopes | rects | work | slab lists | keep | ring ids
     const size_t sz_p = npoly * sizeof(PolyDev), sz_v = hvx.size() * 8, sz_r = hrects.size() * 4;
     const size_t sz_w = hwork.size() * sizeof(PolyWork), sz_s = hslab.size() * 2, sz_k = keep.size() * 4;
+    const size_t sz_e = henv.size() * 8, sz_vr = hvr.size();
     const size_t off_v = (sz_p + 15) & ~(size_t)15;
-    const size_t off_r = off_v + 2 * sz_v;
+    const size_t off_e = off_v + 2 * sz_v;
+    const size_t off_r = off_e + sz_e;
     const size_t off_w = (off_r + sz_r + 15) & ~(size_t)15;
     const size_t off_s = (off_w + sz_w + 15) & ~(size_t)15;
     const size_t off_k = (off_s + sz_s + 15) & ~(size_t)15;
+    const size_t off_vr = (off_k + sz_k + 15) & ~(size_t)15;
+    const size_t blob_end = off_vr + sz_vr;
     void* pblob = nullptr;
-    rc = ctx_ensure(ctx, J_POLY, off_k + sz_k + 64, &pblob);
+    rc = ctx_ensure(ctx, J_POLY, blob_end + 64, &pblob);
     if (rc) return rc;
-    const bool upload = !(cached && pc->dev_blob == pblob && pc->blob_bytes == off_k + sz_k);
+    const bool upload = !(cached && pc->dev_blob == pblob && pc->blob_bytes == blob_end);
     char* bp = reinterpret_cast<char*>(pblob);
     PolyDev* dpoly = reinterpret_cast<PolyDev*>(bp);
     double* dvx = reinterpret_cast<double*>(bp + off_v);
@@ -2454,6 +2632,8 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     PolyWork* dwork = reinterpret_cast<PolyWork*>(bp + off_w);
     uint16_t* dslab = reinterpret_cast<uint16_t*>(bp + off_s);
     unsigned* dkeep = sz_k ? reinterpret_cast<unsigned*>(bp + off_k) : nullptr;
+    double* denv = reinterpret_cast<double*>(bp + off_e);
+    uint8_t* dvr = reinterpret_cast<uint8_t*>(bp + off_vr);
     if (upload) {
         pc->dev_blob = nullptr;  // until the copies are issued
         if ((sz_p && hipMemcpyAsync(dpoly, pd.data(), sz_p, hipMemcpyHostToDevice, st) != hipSuccess) ||
@@ -2462,10 +2642,12 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             (sz_r && hipMemcpyAsync(drects, hrects.data(), sz_r, hipMemcpyHostToDevice, st) != hipSuccess) ||
             (sz_w && hipMemcpyAsync(dwork, hwork.data(), sz_w, hipMemcpyHostToDevice, st) != hipSuccess) ||
             (sz_s && hipMemcpyAsync(dslab, hslab.data(), sz_s, hipMemcpyHostToDevice, st) != hipSuccess) ||
-            (sz_k && hipMemcpyAsync(dkeep, keep.data(), sz_k, hipMemcpyHostToDevice, st) != hipSuccess))
+            (sz_k && hipMemcpyAsync(dkeep, keep.data(), sz_k, hipMemcpyHostToDevice, st) != hipSuccess) ||
+            (sz_e && hipMemcpyAsync(denv, henv.data(), sz_e, hipMemcpyHostToDevice, st) != hipSuccess) ||
+            (sz_vr && hipMemcpyAsync(dvr, hvr.data(), sz_vr, hipMemcpyHostToDevice, st) != hipSuccess))
             return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "polygon upload failed");
         pc->dev_blob = pblob;
-        pc->blob_bytes = off_k + sz_k;
+        pc->blob_bytes = blob_end;
     }
     TileBins tb;
     unsigned* oidx = nullptr;
@@ -2522,13 +2704,13 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     // count pass: hit masks + per-work-item counts; out-of-grid points counted separately
     if (nwork) {
         if (approximate)
-            ppoly_eval<true><<<nwork, kTB, 0, st>>>(tb, dwork, dpoly, dvx, dvy, drects, dslab, r, r_is_max, wofs, mask, bcount);
+            ppoly_eval<true><<<nwork, kTB, 0, st>>>(tb, dwork, dpoly, dvx, dvy, dvr, denv, drects, dslab, r, r_is_max, wofs, mask, bcount);
         else
-            ppoly_eval<false><<<nwork, kTB, 0, st>>>(tb, dwork, dpoly, dvx, dvy, drects, dslab, r, r_is_max, wofs, mask, bcount);
+            ppoly_eval<false><<<nwork, kTB, 0, st>>>(tb, dwork, dpoly, dvx, dvy, dvr, denv, drects, dslab, r, r_is_max, wofs, mask, bcount);
     }
     if (nob && jmode == 1)
         ppoly_outside<false, true><<<nob, kTB, 0, st>>>(dx, dy, oidx, n_out, grid->min_x, grid->min_y, grid->cell_len,
-                                                        dpoly, npoly, drects, osink, dvx, dvy, dslab, r);
+                                                        dpoly, npoly, drects, osink, dvx, dvy, dslab, r, dvr, denv);
     else if (nob)
         ppoly_outside<false><<<nob, kTB, 0, st>>>(dx, dy, oidx, n_out, grid->min_x, grid->min_y, grid->cell_len, dpoly,
                                                   npoly, drects, osink);
@@ -2539,7 +2721,8 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
         if (nwork) ppoly_emit<<<nwork, kTB, 0, st>>>(tb, dwork, wofs, mask, sink);
         if (nob && jmode == 1)
             ppoly_outside<true, true><<<nob, kTB, 0, st>>>(dx, dy, oidx, n_out, grid->min_x, grid->min_y,
-                                                           grid->cell_len, dpoly, npoly, drects, osink, dvx, dvy, dslab, r);
+                                                           grid->cell_len, dpoly, npoly, drects, osink, dvx, dvy, dslab, r,
+                                                           dvr, denv);
         else if (nob)
             ppoly_outside<true><<<nob, kTB, 0, st>>>(dx, dy, oidx, n_out, grid->min_x, grid->min_y, grid->cell_len, dpoly,
                                                      npoly, drects, osink);
@@ -2563,8 +2746,8 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
 
 // Point-polygon kNN of one query polygon over one window (host side of the kernels above).
 int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
-                   const double* vx, const double* vy, uint32_t nv, double r, uint32_t k, int approximate,
-                   uint32_t* out_idx, double* out_dist, uint32_t* out_count) {
+                   const uint32_t* ring_off, uint32_t nring, const double* vx, const double* vy, double r, uint32_t k,
+                   int approximate, uint32_t* out_idx, double* out_dist, uint32_t* out_count) {
     if (!out_idx || !out_dist || !out_count) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null output");
     *out_count = 0;
     if (k == 0) return ctx_fail(ctx, GEOHIP_ERR_ARG, "k must be > 0");
@@ -2572,11 +2755,18 @@ int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, co
     int rc = check_grid_basic(ctx, grid, "grid");
     if (rc) return rc;
     if (n >= 0xffffffffull) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "window larger than 2^32-1 points");
-    if (!vx || !vy) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null polygon arrays");
+    if (!ring_off || !vx || !vy) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null polygon arrays");
+    if (nring > kMaxRings) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "polygon with more than 64 rings");
+    for (uint32_t j = 0; j < nring; j++)
+        if (ring_off[j + 1] < ring_off[j]) return ctx_fail(ctx, GEOHIP_ERR_ARG, "ring_off not ascending");
     PolyPlan pl;
     std::string err;
-    rc = plan_polygon(*grid, vx, vy, nv, r, &pl, &err);
+    rc = plan_polygon_rings(*grid, ring_off, nring, vx, vy, r, &pl, &err);
     if (rc) return ctx_fail(ctx, rc, err);
+    std::vector<uint8_t> hvr;
+    std::vector<double> henv;
+    double gb[4];
+    ring_tables(pl, hvr, henv, gb);
     std::vector<int32_t> hrect;
     for (auto& q : pl.g) hrect.insert(hrect.end(), {q.x0, q.x1, q.y0, q.y1});
     for (auto& q : pl.c) hrect.insert(hrect.end(), {q.x0, q.x1, q.y0, q.y1});
@@ -2596,6 +2786,8 @@ int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, co
     for (int i = 0; i < 4; i++) P.bb[i] = pl.bbox[i];
     P.nv = (uint32_t)pl.rx.size();
     P.nrect = nrect;
+    P.nring = (uint32_t)pl.ring_start.size() - 1;
+    P.pad = 0;
     hipStream_t st = ctx_stream(ctx);
     const bool dev = ctx_mem(ctx) == GEOHIP_MEM_DEVICE;
     const double *dx, *dy;
@@ -2608,8 +2800,10 @@ int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, co
     const size_t off_sel_i = off_sel_d + 256 * 8;
     const size_t off_out = off_sel_i + 256 * 4;
     const size_t off_vx = (off_out + 256 * 12 + 16 + 15) & ~(size_t)15;
-    const size_t off_rect = off_vx + 2 * 8 * (size_t)P.nv;
-    char* sbuf = S.get<char>(23, off_rect + 16 * (size_t)nrect + 64);
+    const size_t off_env = off_vx + 2 * 8 * (size_t)P.nv;
+    const size_t off_rect = off_env + 8 * henv.size();
+    const size_t off_vr = off_rect + 16 * (size_t)nrect;
+    char* sbuf = S.get<char>(23, off_vr + hvr.size() + 64);
     if (S.rc) return S.rc;
     unsigned long long* key = reinterpret_cast<unsigned long long*>(cbuf);
     unsigned* cand = reinterpret_cast<unsigned*>(cbuf + ncap * 8);
@@ -2622,9 +2816,14 @@ int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, co
     double* dvx = reinterpret_cast<double*>(sbuf + off_vx);
     double* dvy = dvx + P.nv;
     int32_t* drect = reinterpret_cast<int32_t*>(sbuf + off_rect);
+    double* denv = reinterpret_cast<double*>(sbuf + off_env);
+    uint8_t* dvr = reinterpret_cast<uint8_t*>(sbuf + off_vr);
     if ((P.nv && (hipMemcpyAsync(dvx, pl.rx.data(), 8 * (size_t)P.nv, hipMemcpyHostToDevice, st) != hipSuccess ||
                   hipMemcpyAsync(dvy, pl.ry.data(), 8 * (size_t)P.nv, hipMemcpyHostToDevice, st) != hipSuccess)) ||
-        (nrect && hipMemcpyAsync(drect, hrect.data(), 16 * (size_t)nrect, hipMemcpyHostToDevice, st) != hipSuccess))
+        (nrect && hipMemcpyAsync(drect, hrect.data(), 16 * (size_t)nrect, hipMemcpyHostToDevice, st) != hipSuccess) ||
+        (P.nring > 1 &&
+         (hipMemcpyAsync(denv, henv.data(), 8 * henv.size(), hipMemcpyHostToDevice, st) != hipSuccess ||
+          hipMemcpyAsync(dvr, hvr.data(), hvr.size(), hipMemcpyHostToDevice, st) != hipSuccess)))
         return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "polygon upload failed");
     hipEvent_t e0, e1;
     ctx_timing_events(ctx, &e0, &e1);
@@ -2649,8 +2848,8 @@ int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, co
             ppknn_scan<<<(unsigned)nb, kTB, 0, st>>>(dx, dy, n, grid->min_x, grid->min_y, grid->cell_len, drect, nrect,
                                                      cand, rs);
         }
-        if (approximate) ppknn_dist<true><<<1024, kTB, 0, st>>>(dx, dy, cand, rs, dvx, dvy, P, key);
-        else ppknn_dist<false><<<1024, kTB, 0, st>>>(dx, dy, cand, rs, dvx, dvy, P, key);
+        if (approximate) ppknn_dist<true><<<1024, kTB, 0, st>>>(dx, dy, cand, rs, dvx, dvy, dvr, denv, P, key);
+        else ppknn_dist<false><<<1024, kTB, 0, st>>>(dx, dy, cand, rs, dvx, dvy, dvr, denv, P, key);
     }
     rsel_small<<<1, 1024, 0, st>>>(key, cand, rs, k, od, oi, ocnt);  // M <= kRselSmall (also M = 0)
     if (e1) hipEventRecord(e1, st);  // re-recorded below when the multi-block rounds run

@@ -52,13 +52,18 @@ bool key_roundtrip(int32_t cx, int32_t cy, int32_t* ox, int32_t* oy);
 // All (a,b) whose "%05d%05d" key equals the key of (cx,cy).
 int key_matches(int32_t cx, int32_t cy, int32_t* pairs, int max_pairs);
 
-// Polygon plan (one single-ring polygon of the point-polygon range query).
+// Polygon plan (one query polygon of the point-polygon queries).
 struct PolyPlan {
-    std::vector<geohip_rect> g, c;  // G = union g; C = union c minus G
-    double bbox[4];                 // minx, miny, maxx, maxy (JTS envelope)
-    std::vector<double> rx, ry;     // closed ring
+    std::vector<geohip_rect> g, c;   // G = union g; C = union c minus G
+    double bbox[4];                  // minx, miny, maxx, maxy (JTS envelope: the shell's)
+    std::vector<double> rx, ry;      // closed rings, shell first, then the holes
+    std::vector<uint32_t> ring_start;  // ring j = [ring_start[j], ring_start[j+1]) of rx/ry
 };
 int plan_polygon(const geohip_grid& g, const double* vx, const double* vy, uint32_t nv, double r,
                  PolyPlan* out, std::string* err);
+int plan_polygon_rings(const geohip_grid& g, const uint32_t* ring_off, uint32_t nring, const double* vx,
+                       const double* vy, double r, PolyPlan* out, std::string* err);
+int build_polygon_rings(const uint32_t* ring_off, uint32_t nring, const double* vx, const double* vy,
+                        PolyPlan* out, std::string* err);
 
 }  // namespace geohip

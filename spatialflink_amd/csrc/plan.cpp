@@ -289,20 +289,86 @@ int plan_point(const geohip_grid& g, double qx, double qy, double r, PointPlan* 
     return GEOHIP_OK;
 }
 
+// JTS 1.16.1 Polygon.getArea of a shell-only polygon: |Area.ofRingSigned| (shoelace with the
+// first x subtracted), evaluated in source order.
+static double jts_ring_area(const double* x, const double* y, size_t n) {
+    if (n < 3) return 0.0;
+    double sum = 0.0;
+    const double x0 = x[0];
+    for (size_t i = 1; i + 1 < n; i++) sum += (x[i] - x0) * (y[i - 1] - y[i + 1]);
+    return std::fabs(sum / 2.0);
+}
+
+// Polygon(List<List<Coordinate>>, UniformGrid).createPolygon (Polygon.java:52-66, 115-165):
+// rings [ring_off[j], ring_off[j+1]) of vx/vy.  One ring: closed if open (:149-153).  Several:
+// createPolygonArray (:115-145) -- each ring padded (1..3 coords: its first coordinate appended
+// 4 times) and closed, then ordered by JTS area, largest first, with that method's insertion
+// rule (a tie with the tail goes after it, a larger area goes before the first ring whose area is
+// <= it; a NaN area is never inserted), shell = first, holes = the rest.  Where the reference
+// leaves polygon null (first ring <= 3 coords) or JTS throws (an empty ring; a ring whose first
+// coordinate is NaN: LinearRing not closed; no ring left) -> GEOHIP_ERR_ARG.
+int build_polygon_rings(const uint32_t* ring_off, uint32_t nring, const double* vx, const double* vy,
+                        PolyPlan* out, std::string* err) {
+    out->rx.clear();
+    out->ry.clear();
+    out->ring_start.assign(1, 0u);
+    if (nring == 0) { *err = "polygon without rings"; return GEOHIP_ERR_ARG; }
+    if (ring_off[1] < ring_off[0] || ring_off[1] - ring_off[0] <= 3) {
+        *err = "Polygon needs more than 3 coordinates in its first ring (Polygon.java:53)";
+        return GEOHIP_ERR_ARG;
+    }
+    std::vector<std::vector<double>> rxs(nring), rys(nring);
+    std::vector<double> area(nring, 0.0);
+    std::vector<uint32_t> order;
+    for (uint32_t j = 0; j < nring; j++) {
+        if (ring_off[j + 1] < ring_off[j]) { *err = "ring_off not ascending"; return GEOHIP_ERR_ARG; }
+        const uint32_t a = ring_off[j], m = ring_off[j + 1] - ring_off[j];
+        if (m == 0) { *err = "empty ring (IndexOutOfBoundsException in Polygon.createPolygonArray)"; return GEOHIP_ERR_ARG; }
+        std::vector<double>& X = rxs[j];
+        std::vector<double>& Y = rys[j];
+        X.assign(vx + a, vx + a + m);
+        Y.assign(vy + a, vy + a + m);
+        if (nring > 1 && m < 4)
+            for (int t = 0; t < 4; t++) { X.push_back(X[0]); Y.push_back(Y[0]); }
+        if (!(X.front() == X.back() && Y.front() == Y.back())) { X.push_back(X[0]); Y.push_back(Y[0]); }
+        if (!(X.front() == X.back() && Y.front() == Y.back())) {
+            *err = "LinearRing not closed (NaN first coordinate): JTS IllegalArgumentException";
+            return GEOHIP_ERR_ARG;
+        }
+        if (nring == 1) { order.push_back(0); break; }
+        area[j] = jts_ring_area(X.data(), Y.data(), X.size());
+        if (order.empty() || area[order.back()] >= area[j]) {
+            order.push_back(j);
+        } else {
+            for (size_t i = 0; i < order.size(); i++)
+                if (area[order[i]] <= area[j]) { order.insert(order.begin() + i, j); break; }
+        }
+    }
+    if (order.empty()) { *err = "no ring with a comparable area (createPolygonArray)"; return GEOHIP_ERR_ARG; }
+    for (uint32_t j : order) {
+        out->rx.insert(out->rx.end(), rxs[j].begin(), rxs[j].end());
+        out->ry.insert(out->ry.end(), rys[j].begin(), rys[j].end());
+        out->ring_start.push_back((uint32_t)out->rx.size());
+    }
+    return GEOHIP_OK;
+}
+
 int plan_polygon(const geohip_grid& g, const double* vx, const double* vy, uint32_t nv, double r,
                  PolyPlan* out, std::string* err) {
+    const uint32_t ro[2] = {0, nv};
+    return plan_polygon_rings(g, ro, 1, vx, vy, r, out, err);
+}
+
+int plan_polygon_rings(const geohip_grid& g, const uint32_t* ring_off, uint32_t nring, const double* vx,
+                       const double* vy, double r, PolyPlan* out, std::string* err) {
     int rc = check_grid(g, err);
     if (rc) return rc;
-    if (nv <= 3) { *err = "Polygon needs more than 3 coordinates (Polygon.java:53)"; return GEOHIP_ERR_ARG; }
-    out->rx.assign(vx, vx + nv);
-    out->ry.assign(vy, vy + nv);
-    if (!(vx[0] == vx[nv - 1] && vy[0] == vy[nv - 1])) {  // Polygon.java:151-153
-        out->rx.push_back(vx[0]);
-        out->ry.push_back(vy[0]);
-    }
-    // JTS envelope (Envelope.expandToInclude over the shell)
+    rc = build_polygon_rings(ring_off, nring, vx, vy, out, err);
+    if (rc) return rc;
+    const size_t nshell = out->ring_start[1];
+    // JTS envelope (Polygon envelope = the shell's: Envelope.expandToInclude over the shell)
     double minx = out->rx[0], maxx = out->rx[0], miny = out->ry[0], maxy = out->ry[0];
-    for (size_t i = 1; i < out->rx.size(); i++) {
+    for (size_t i = 1; i < nshell; i++) {
         double x = out->rx[i], y = out->ry[i];
         if (x < minx) minx = x;
         if (x > maxx) maxx = x;

@@ -11,10 +11,11 @@ void ppoly_cache_drop(geohip_ctx* ctx);
 // range (join = 0: gq ignored, pairs (polygon, point)) or join (join = 1: polygons planned on gq,
 // point cells on grid, pairs (point, polygon), PointPolygonJoinQuery.java:162-201)
 int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, int join, const double* x,
-               const double* y, uint64_t n, const uint32_t* ring_off, const double* vx, const double* vy,
-               uint32_t npoly, double r, int approximate, uint32_t* out_pairs, uint64_t cap, uint64_t* out_count);
+               const double* y, uint64_t n, const uint32_t* poly_rings, const uint32_t* ring_off, const double* vx,
+               const double* vy, uint32_t npoly, double r, int approximate, uint32_t* out_pairs, uint64_t cap,
+               uint64_t* out_count);
 // point-polygon kNN of one polygon (PointPolygonKNNQuery.java:162-236)
 int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
-                   const double* vx, const double* vy, uint32_t nv, double r, uint32_t k, int approximate,
-                   uint32_t* out_idx, double* out_dist, uint32_t* out_count);
+                   const uint32_t* ring_off, uint32_t nring, const double* vx, const double* vy, double r, uint32_t k,
+                   int approximate, uint32_t* out_idx, double* out_dist, uint32_t* out_count);
 }  // namespace geohip

@@ -116,13 +116,23 @@ class Point:
 
 @dataclass
 class Polygon:
-    """Query polygon: one exterior ring as given to Polygon(List<List<Coordinate>>, UniformGrid)."""
-    coordinates: Sequence[Sequence[float]]
+    """Query polygon as given to Polygon(List<List<Coordinate>>, UniformGrid): either one ring
+    ([(x, y), ...]) or a list of rings ([[(x, y), ...], ...]; the largest JTS area becomes the
+    shell, the others its holes -- Polygon.createPolygon, Polygon.java:115-165)."""
+    coordinates: Sequence
     objID: Optional[str] = None
 
     def __post_init__(self):
-        if len(self.coordinates) <= 3:  # Polygon.java:53 leaves polygon == null
+        rings = self.rings
+        if not rings or len(rings[0]) <= 3:  # Polygon.java:53 leaves polygon == null
             raise _abi.GeohipArgumentError("Polygon needs more than 3 coordinates (Polygon.java:53)")
+
+    @property
+    def rings(self):
+        c = self.coordinates
+        if len(c) and len(c[0]) and isinstance(c[0][0], (list, tuple, np.ndarray)):
+            return [list(r) for r in c]
+        return [list(c)]
 
 
 @dataclass
@@ -237,26 +247,23 @@ class PointPolygonRangeQuery(_Operator):
     def run(self, window: PointWindow, query_polygons, query_radius: float):
         self._check_type()
         polys = [query_polygons] if isinstance(query_polygons, Polygon) else list(query_polygons)
-        off = [0]
-        vx, vy = [], []
-        for p in polys:
-            for c in p.coordinates:
-                vx.append(float(c[0]))
-                vy.append(float(c[1]))
-            off.append(len(vx))
-        return self._ctx().range_ppoly(self.index.abi(), window.x, window.y, np.array(off, np.uint32),
-                                       np.array(vx), np.array(vy), float(query_radius),
-                                       self.conf.approximate_query)
+        pr, off, vx, vy = _rings(polys)
+        return self._ctx().range_ppoly(self.index.abi(), window.x, window.y, off, vx, vy, float(query_radius),
+                                       self.conf.approximate_query, poly_rings=pr)
 
 
 def _rings(polys):
-    off, vx, vy = [0], [], []
+    """(poly_rings, ring_off, vx, vy) of a polygon list: polygon i = rings
+    [poly_rings[i], poly_rings[i+1]), ring j = vertices [ring_off[j], ring_off[j+1])."""
+    pr, off, vx, vy = [0], [0], [], []
     for p in polys:
-        for c in p.coordinates:
-            vx.append(float(c[0]))
-            vy.append(float(c[1]))
-        off.append(len(vx))
-    return np.array(off, np.uint32), np.array(vx), np.array(vy)
+        for ring in p.rings:
+            for c in ring:
+                vx.append(float(c[0]))
+                vy.append(float(c[1]))
+            off.append(len(vx))
+        pr.append(len(off) - 1)
+    return np.array(pr, np.uint32), np.array(off, np.uint32), np.array(vx), np.array(vy)
 
 
 class PointPolygonJoinQuery(_Operator):
@@ -274,9 +281,9 @@ class PointPolygonJoinQuery(_Operator):
     def run(self, points: PointWindow, query_polygons, query_radius: float):
         self._check_type()
         polys = [query_polygons] if isinstance(query_polygons, Polygon) else list(query_polygons)
-        off, vx, vy = _rings(polys)
+        pr, off, vx, vy = _rings(polys)
         return self._ctx().join_ppoly(self.index.abi(), self.index2.abi(), points.x, points.y, off, vx, vy,
-                                      float(query_radius), self.conf.approximate_query)
+                                      float(query_radius), self.conf.approximate_query, poly_rings=pr)
 
 
 class PointPolygonKNNQuery(_Operator):
@@ -287,6 +294,6 @@ class PointPolygonKNNQuery(_Operator):
 
     def run(self, window: PointWindow, query_polygon: Polygon, query_radius: float, k: int):
         self._check_type()
-        _, vx, vy = _rings([query_polygon])
+        _, off, vx, vy = _rings([query_polygon])
         return self._ctx().knn_ppoly(self.index.abi(), window.x, window.y, vx, vy, float(query_radius), int(k),
-                                     self.conf.approximate_query)
+                                     self.conf.approximate_query, ring_off=off)

@@ -83,6 +83,59 @@ def star_polygons(n_poly: int, seed: int, n_vert: int = 50, bbox=BEIJING, r_min=
     return np.array(off, np.uint32), np.array(vx), np.array(vy)
 
 
+def _star(rng, cx, cy, R, nv, closed=True, clockwise=False):
+    ang = np.arange(nv) * (2 * np.pi / nv)
+    if clockwise:
+        ang = -ang
+    rad = R * (1 + 0.3 * rng.uniform(0, 1, nv))
+    x = (cx + rad * np.cos(ang)).tolist()
+    y = (cy + rad * np.sin(ang)).tolist()
+    if closed:
+        x.append(x[0])
+        y.append(y[0])
+    return list(zip(x, y))
+
+
+def holed_polygons(n_poly: int, seed: int, n_vert: int = 40, bbox=BEIJING, r_min=0.005, r_max=0.02):
+    """n_poly polygons with holes (Polygon(List<List<Coordinate>>) input: rings in the caller's
+    order, the largest area becomes the shell).  Star shell of radius R plus 1-3 star holes of
+    radius 0.12-0.25 R inside it; by p % 6 the variant: 0 plain, 1 holes listed before the
+    shell, 2 an extra degenerate 2-coordinate hole (padded by createPolygonArray), 3 a hole
+    crossing the shell's boundary, 4 a "hole" outside the shell (JTS does not validate), 5
+    clockwise holes and an open shell.  Returns (poly_rings, ring_off, vx, vy, rings) with
+    rings[p] = the list of rings of polygon p."""
+    min_x, max_x, min_y, max_y = bbox
+    rng = np.random.default_rng(seed)
+    polys = []
+    for p in range(n_poly):
+        v = p % 6
+        cx = rng.uniform(min_x + 0.05, max_x - 0.05)
+        cy = rng.uniform(min_y + 0.05, max_y - 0.05)
+        R = rng.uniform(r_min, r_max)
+        shell = _star(rng, cx, cy, R, n_vert, closed=(v != 5))
+        holes = []
+        for _ in range(int(rng.integers(1, 4))):
+            a = rng.uniform(0, 2 * np.pi)
+            d = R * rng.uniform(0.0, 0.45)
+            holes.append(_star(rng, cx + d * np.cos(a), cy + d * np.sin(a), R * rng.uniform(0.12, 0.25),
+                               int(rng.integers(6, 16)), closed=bool(rng.integers(0, 2)), clockwise=(v == 5)))
+        if v == 2:
+            holes.append([(cx + 0.5 * R, cy), (cx + 0.55 * R, cy + 0.05 * R)])
+        if v == 3:
+            holes.append(_star(rng, cx + 0.95 * R, cy, 0.2 * R, 10))
+        if v == 4:
+            holes.append(_star(rng, cx + 1.6 * R, cy + 0.3 * R, 0.2 * R, 10))
+        polys.append(holes + [shell] if v == 1 else [shell] + holes)
+    pr, off, vx, vy = [0], [0], [], []
+    for rings in polys:
+        for ring in rings:
+            vx.extend(c[0] for c in ring)
+            vy.extend(c[1] for c in ring)
+            off.append(len(vx))
+        pr.append(len(off) - 1)
+    return np.array(pr, np.uint32), np.array(off, np.uint32), np.array(vx), np.array(vy), polys
+
+
 def _digits(v: np.ndarray, width: int) -> np.ndarray:
     """ASCII digits of non-negative int64 v, zero-padded to width: uint8 [len(v), width]."""
     p = np.int64(10) ** np.arange(width - 1, -1, -1, dtype=np.int64)

@@ -1,4 +1,6 @@
 """Shared helpers for the parity tests."""
+import math
+
 import numpy as np
 
 
@@ -20,3 +22,27 @@ def pairs_sorted(p):
         return p
     o = np.lexsort((p[:, 1], p[:, 0]))
     return p[o]
+
+
+def holed_window(rng, n, polys, r):
+    """Uniform points plus points around each polygon: its vertices, edge midpoints, hole
+    centres, points just inside / outside each hole ring and within r of it."""
+    from spatialflink_amd import synth
+    x, y = synth.uniform(n, int(rng.integers(1 << 30)))
+    xs, ys = [x], [y]
+    for rings in polys:
+        allv = np.array([c for ring in rings for c in ring])
+        lo, hi = allv.min(0), allv.max(0)
+        xs.append(rng.uniform(lo[0] - 2 * r, hi[0] + 2 * r, 400))
+        ys.append(rng.uniform(lo[1] - 2 * r, hi[1] + 2 * r, 400))
+        for ring in rings:
+            a = np.array(ring)
+            xs += [a[:, 0], (a[:-1, 0] + a[1:, 0]) / 2]
+            ys += [a[:, 1], (a[:-1, 1] + a[1:, 1]) / 2]
+            c = a.mean(0)
+            for f in (0.0, 0.5, 0.97, 1.03, 1.3):
+                xs.append(c[0] + f * (a[:, 0] - c[0]))
+                ys.append(c[1] + f * (a[:, 1] - c[1]))
+    xs.append(np.array([math.nan, 116.0]))
+    ys.append(np.array([40.0, math.nan]))
+    return np.concatenate(xs), np.concatenate(ys)

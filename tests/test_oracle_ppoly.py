@@ -12,6 +12,7 @@ import pytest
 
 import cref
 import restate as R
+from helpers import holed_window
 
 BJ = (115.5, 117.6, 39.6, 41.1)
 
@@ -113,3 +114,51 @@ def test_knn_ppoly_errors():
     with pytest.raises(cref.OracleError):
         cref.knn_ppoly(cg, np.zeros(3), np.zeros(3), np.array([116.0, 116.1, 116.1, 116.0]),
                        np.array([40.0, 40.0, 40.1, 40.1]), 0.01, 0)  # k = 0
+
+
+HOLE_CASES = [(500, 0.0005, False), (500, 0.003, False), (100, 0.01, False), (500, 0.003, True)]
+
+
+@pytest.mark.parametrize("case", range(len(HOLE_CASES)))
+def test_holed_polygons_oracles_agree(case):
+    """Polygons with holes (createPolygonArray ordering, padding, hole crossing / outside the
+    shell): the C oracle's range, join and kNN against the literal restatement."""
+    from spatialflink_amd import synth
+    n, r, approx = HOLE_CASES[case]
+    rng = np.random.default_rng(300 + case)
+    pr, off, vx, vy, polys = synth.holed_polygons(6, 310 + case)
+    x, y = holed_window(rng, 2000, polys, r)
+    g, cg = grids(n)
+    want = sorted(R.range_ppoly(g, x.tolist(), y.tolist(), polys, r, approx))
+    got = sorted(map(tuple, cref.range_ppoly(cg, x, y, off, vx, vy, r, approx, poly_rings=pr).tolist()))
+    assert got == want
+    assert len(want) > 500
+    want = sorted(R.join_ppoly(g, g, x.tolist(), y.tolist(), polys, r, approx))
+    got = sorted(map(tuple, cref.join_ppoly(cg, cg, x, y, off, vx, vy, r, approx, poly_rings=pr).tolist()))
+    assert got == want
+    for p in (0, 3, 4):
+        w = R.knn_ppoly(g, x.tolist(), y.tolist(), polys[p], r, 50, approx)
+        a, b = pr[p], pr[p + 1]
+        ro = off[a:b + 1] - off[a]
+        gi, gd = cref.knn_ppoly(cg, x, y, vx[off[a]:off[b]], vy[off[a]:off[b]], r, 50, approx, ring_off=ro)
+        assert gi.tolist() == [i for i, _ in w]
+        assert np.array_equal(gd.view(np.uint64), np.array([d for _, d in w]).view(np.uint64))
+
+
+def test_holed_point_distance_cases():
+    """JTS point.distance(polygon) with holes: inside a hole (distance to the hole ring), on a
+    hole edge / vertex (0), in the shell outside the holes (0), outside the shell."""
+    shell = [(0.0, 0.0), (10.0, 0.0), (10.0, 10.0), (0.0, 10.0)]
+    hole = [(4.0, 4.0), (6.0, 4.0), (6.0, 6.0), (4.0, 6.0)]
+    off = np.array([0, 4, 8], np.uint32)
+    vx = np.array([c[0] for c in shell + hole])
+    vy = np.array([c[1] for c in shell + hole])
+    for (px, py), want in [((5.0, 5.0), 1.0), ((4.5, 5.0), 0.5), ((6.0, 5.0), 0.0), ((4.0, 4.0), 0.0),
+                           ((2.0, 2.0), 0.0), ((12.0, 5.0), 2.0), ((5.0, 4.25), 0.25)]:
+        assert cref.point_polygon(px, py, vx, vy, ring_off=off) == want
+        assert R.jts_point_polygon_distance(px, py, R.make_polygon([shell, hole])) == want
+    # ring order does not matter: the larger ring becomes the shell
+    off2 = np.array([0, 4, 8], np.uint32)
+    vx2 = np.array([c[0] for c in hole + shell])
+    vy2 = np.array([c[1] for c in hole + shell])
+    assert cref.point_polygon(5.0, 5.0, vx2, vy2, ring_off=off2) == 1.0
