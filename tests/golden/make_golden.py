@@ -173,6 +173,54 @@ def main():
                    "approximate": approx, "expect": sorted([list(p) for p in pairs])})
     fixtures["range_ppoly"] = pc
 
+    # polygons with holes (Polygon.createPolygonArray ordering): range, join and kNN of the
+    # restatement; points on every ring's vertices and edge midpoints, hole centres, points
+    # just inside / outside each hole ring
+    hc = []
+    for n, r, approx, k in [(100, 0.01, False, 20), (500, 0.004, False, 40), (500, 0.004, True, 10)]:
+        g = R.UniformGrid(n, *BJ)
+        xs, ys = window(rng, g, 200, edge=False)
+        polys = []
+        for p in range(3):
+            cx, cy = rng.uniform(115.7, 117.4), rng.uniform(39.8, 40.9)
+            rad = rng.uniform(0.02, 0.06)
+
+            def star(ccx, ccy, rr, m, cw=False):
+                sgn = -1.0 if cw else 1.0
+                return [(ccx + rr * (1 + 0.3 * rng.random()) * math.cos(sgn * 2 * math.pi * t / m),
+                         ccy + rr * (1 + 0.3 * rng.random()) * math.sin(sgn * 2 * math.pi * t / m)) for t in range(m)]
+            shell = star(cx, cy, rad, rng.randint(6, 14))
+            holes = [star(cx + 0.3 * rad, cy, 0.2 * rad, rng.randint(4, 8), cw=p == 1),
+                     star(cx - 0.4 * rad, cy + 0.1 * rad, 0.15 * rad, rng.randint(4, 8))]
+            if p == 2:
+                holes.append([(cx, cy - 0.5 * rad), (cx + 0.05 * rad, cy - 0.45 * rad)])  # padded (2 coords)
+            rings = holes + [shell] if p == 1 else [shell] + holes
+            polys.append(rings)
+            for ring in rings:
+                for t in range(min(3, len(ring))):
+                    xs.append(ring[t][0])
+                    ys.append(ring[t][1])
+                if len(ring) > 1:
+                    xs.append((ring[0][0] + ring[1][0]) / 2)
+                    ys.append((ring[0][1] + ring[1][1]) / 2)
+                mx = sum(c[0] for c in ring) / len(ring)
+                my = sum(c[1] for c in ring) / len(ring)
+                for f in (0.0, 0.9, 1.1):
+                    xs.append(mx + f * (ring[0][0] - mx))
+                    ys.append(my + f * (ring[0][1] - my))
+            for _ in range(40):
+                xs.append(rng.uniform(cx - 1.3 * rad, cx + 1.3 * rad))
+                ys.append(rng.uniform(cy - 1.3 * rad, cy + 1.3 * rad))
+        rp = R.range_ppoly(g, xs, ys, polys, r, approx)
+        jp = R.join_ppoly(g, g, xs, ys, polys, r, approx)
+        kn = R.knn_ppoly(g, xs, ys, polys[0], r, k, approx)
+        hc.append({"grid": grid_dict(g), "x": [hx(v) for v in xs], "y": [hx(v) for v in ys],
+                   "polygons": [[[[hx(a), hx(b)] for a, b in ring] for ring in rings] for rings in polys],
+                   "r": hx(r), "approximate": approx, "k": k,
+                   "expect_range": sorted([list(p) for p in rp]), "expect_join": sorted([list(p) for p in jp]),
+                   "expect_knn_idx": [i for i, _ in kn], "expect_knn_dist": [hx(d) for _, d in kn]})
+    fixtures["ppoly_holes"] = hc
+
     (HERE / "golden.json").write_text(json.dumps(fixtures, indent=0))
     print("wrote", HERE / "golden.json")
 

@@ -46,3 +46,16 @@ def holed_window(rng, n, polys, r):
     xs.append(np.array([math.nan, 116.0]))
     ys.append(np.array([40.0, math.nan]))
     return np.concatenate(xs), np.concatenate(ys)
+
+
+def golden_polygons(polys_hex):
+    """(poly_rings, ring_off, vx, vy) of a fixture's polygons (rings of [x, y] hex pairs)."""
+    pr, off, vx, vy = [0], [0], [], []
+    for rings in polys_hex:
+        for ring in rings:
+            vx += [fx(a) for a, _ in ring]
+            vy += [fx(b) for _, b in ring]
+            off.append(len(vx))
+        pr.append(len(off) - 1)
+    return (np.array(pr, np.uint32), np.array(off, np.uint32), np.array(vx, np.float64),
+            np.array(vy, np.float64))

@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 import cref
-from helpers import holed_window, pairs_sorted
+from helpers import arr, fx, golden_polygons, grid_vals, holed_window, pairs_sorted
 from spatialflink_amd import _abi, synth
 
 pytestmark = pytest.mark.gpu
@@ -175,3 +175,22 @@ def test_holes_errors_and_empty(ctx):
     rc = _abi.lib.geohip_join_ppoly(ctx.h, ctypes.byref(ag), ctypes.byref(ag), _abi._ptr(x), _abi._ptr(y), len(x),
                                     None, None, None, None, 0, 0.01, 0, None, 0, ctypes.byref(cnt))
     assert rc == _abi.OK and cnt.value == 0
+
+
+def test_holes_golden(ctx, golden):
+    """The device path against the restatement's holed-polygon vectors (tests/golden)."""
+    for c in golden["ppoly_holes"]:
+        mx, my, l, n = grid_vals(c["grid"])
+        g = _abi.make_grid(mx, my, l, n)
+        x, y = arr(c["x"]), arr(c["y"])
+        pr, off, vx, vy = golden_polygons(c["polygons"])
+        r, approx = fx(c["r"]), c["approximate"]
+        assert pairs_sorted(ctx.range_ppoly(g, x, y, off, vx, vy, r, approx, poly_rings=pr)).tolist() == \
+            c["expect_range"]
+        assert pairs_sorted(ctx.join_ppoly(g, g, x, y, off, vx, vy, r, approx, poly_rings=pr)).tolist() == \
+            c["expect_join"]
+        a, b = pr[0], pr[1]
+        oi, od = ctx.knn_ppoly(g, x, y, vx[off[a]:off[b]], vy[off[a]:off[b]], r, c["k"], approx,
+                               ring_off=off[a:b + 1] - off[a])
+        assert oi.tolist() == c["expect_knn_idx"]
+        assert [v.hex() for v in od.tolist()] == c["expect_knn_dist"]
