@@ -200,6 +200,17 @@ int geohip_range_pp_async(geohip_ctx* ctx, const geohip_grid* grid, const double
                           uint64_t n, double qx, double qy, double r, int approximate,
                           uint32_t* out_idx, uint64_t cap, uint64_t* out_count_dev);
 
+/* Key-band partition of one window shard for the multi-GPU join (the device form of the
+   reference's keyBy(gridID) shuffle, PointPointJoinQuery.java:137-150): a point whose key
+   (HelperClass.java:104-116 on grid_data) is a cell (cx, cy) of the nb x nb key space belongs to
+   rank cx * world / nb; other points match no neighbour block and are dropped.  Writes the kept
+   points grouped by owner rank, in arrival order inside a group -- out_x / out_y and out_idx =
+   base + window position -- and out_counts_dev[world] = points per owner (device uint64), ready
+   for one all-to-all.  Outputs need n entries.  1 <= world <= 64; device memory only. */
+int geohip_band_pack_async(geohip_ctx* ctx, const geohip_grid* grid_data, int32_t nb, uint32_t world,
+                           const double* x, const double* y, uint64_t n, int64_t base, double* out_x,
+                           double* out_y, int64_t* out_idx, uint64_t* out_counts_dev);
+
 /* ---- ingest codec ---------------------------------------------- */
 /* A batch of '\n'-separated text records, as a Flink source hands them to the map functions of
    Deserialization.PointStream / TrajectoryStream (spatialStreams/Deserialization.java:47-80),

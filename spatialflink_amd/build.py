@@ -31,6 +31,7 @@ SOURCES = {
     "pp_kernels.hip": ["-x", "hip", f"--offload-arch={ARCH}"],
     "cell_kernels.hip": ["-x", "hip", f"--offload-arch={ARCH}"],
     "ingest.hip": ["-x", "hip", f"--offload-arch={ARCH}"],
+    "band.hip": ["-x", "hip", f"--offload-arch={ARCH}"],
 }
 
 

@@ -28,4 +28,8 @@ void pp_screen_bounds(double r, double* r2lo, double* r2hi);
 int join_pp_impl(geohip_ctx* ctx, const geohip_grid* grid_data, const geohip_grid* grid_query, const double* dx,
                  const double* dy, uint64_t nd, const double* qx, const double* qy, uint64_t nq, double r,
                  int approximate, uint32_t* out_pairs, uint64_t cap, uint64_t* out_count, bool count_only);
+// key-band owner partition of a window (band.hip; geohip_band_pack_async)
+int band_pack_impl(geohip_ctx* ctx, const geohip_grid* grid, int32_t nb, uint32_t world, const double* x,
+                   const double* y, uint64_t n, int64_t base, double* out_x, double* out_y, int64_t* out_idx,
+                   uint64_t* out_counts);
 }  // namespace geohip

@@ -75,8 +75,8 @@ def knn_sharded(x_local, y_local, base: int, qx: float, qy: float, r: float, k: 
     all_d = torch.empty((world, k), dtype=gd.dtype, device=gd.device)
     all_i = torch.empty((world, k), dtype=gi.dtype, device=gi.device)
     if world > 1:
-        dist.all_gather_into_tensor(all_d.view(-1), gd, group=group)
-        dist.all_gather_into_tensor(all_i.view(-1), gi, group=group)
+        all_gather_into(all_d.view(-1), gd, group)
+        all_gather_into(all_i.view(-1), gi, group)
     else:
         all_d[0] = gd
         all_i[0] = gi
@@ -110,17 +110,39 @@ def _java_cell(v, mn: float, l: float):
     return t.clamp(-2147483648.0, 2147483647.0).to(torch.int64)
 
 
+def torch_band_pack(grid_data):
+    """band_pack written with torch ops (CPU orchestration tests; the product engine is
+    geohip_band_pack_async): same owners, same arrival order inside each owner group."""
+    import torch
+
+    def f(x, y, base, nb, world):
+        cx = _java_cell(x, grid_data.min_x, grid_data.cell_len)
+        cy = _java_cell(y, grid_data.min_y, grid_data.cell_len)
+        valid = (cx >= 0) & (cx < nb) & (cy >= 0) & (cy < nb)  # other keys match no Nbr block
+        gidx = torch.arange(len(x), dtype=torch.int64, device=x.device) + base
+        owner = (cx * world) // nb
+        sel = torch.nonzero(valid).flatten()
+        order = sel[torch.argsort(owner[sel], stable=True)]
+        counts = torch.bincount(owner[order], minlength=world).to(torch.int64)
+        return x[order], y[order], gidx[order], counts
+
+    return f
+
+
 def key_band(world: int, rank: int, nb: int):
     """Grid columns [lo, hi) owned by `rank` when column cx belongs to rank cx * world // nb."""
     return (rank * nb + world - 1) // world, ((rank + 1) * nb + world - 1) // world
 
 
 def join_sharded(dx_local, dy_local, dbase: int, qx, qy, r: float, approximate: bool = False, *, grid_data,
-                 grid_query, ctx=None, group=None, partition: str = "arrival", local_join: Optional[Callable] = None):
+                 grid_query, ctx=None, group=None, partition: str = "arrival", local_join: Optional[Callable] = None,
+                 band_pack: Optional[Callable] = None):
     """Point-point join of one window over the group.  dx/dy_local: this rank's data shard
     (window indices dbase + local position); qx/qy: the whole query window (every rank).
     Returns (pairs int64 [m, 2] = (data window idx, query idx) of this rank, output offset,
-    total pairs); the per-rank pair sets are disjoint and their union is the window's join."""
+    total pairs); the per-rank pair sets are disjoint and their union is the window's join.
+    partition="cells": band_pack(x, y, base, nb, world) -> (x, y, window idx, counts[world])
+    groups the shard's valid-key points by owner (default: geohip_band_pack_async)."""
     import torch
     import torch.distributed as dist
 
@@ -133,25 +155,20 @@ def join_sharded(dx_local, dy_local, dbase: int, qx, qy, r: float, approximate: 
         pairs[:, 0] += dbase
     elif partition == "cells":
         nb = int(grid_query.n)
-        cx = _java_cell(dx_local, grid_data.min_x, grid_data.cell_len)
-        cy = _java_cell(dy_local, grid_data.min_y, grid_data.cell_len)
-        valid = (cx >= 0) & (cx < nb) & (cy >= 0) & (cy < nb)  # other keys match no Nbr block
-        gidx = torch.arange(len(dx_local), dtype=torch.int64, device=dx_local.device) + dbase
-        owner = (cx * world) // nb
-        sel = torch.nonzero(valid).flatten()
-        order = sel[torch.argsort(owner[sel], stable=True)]
-        send_counts = torch.bincount(owner[order], minlength=world).to(torch.int64)
+        if band_pack is None:
+            band_pack = _device_band_pack(ctx, grid_data)
+        px, py, pg, send_counts = band_pack(dx_local, dy_local, dbase, nb, world)
         recv_counts = torch.empty_like(send_counts)
-        dist.all_to_all_single(recv_counts, send_counts, group=group)
+        all_to_all(recv_counts, send_counts, group=group)
         sc, rc = send_counts.tolist(), recv_counts.tolist()
-        nrecv = sum(rc)
+        nrecv, nsend = sum(rc), sum(sc)
 
         def exchange(t):
             out = torch.empty(nrecv, dtype=t.dtype, device=t.device)
-            dist.all_to_all_single(out, t[order].contiguous(), rc, sc, group=group)
+            all_to_all(out, t[:nsend], rc, sc, group)
             return out
 
-        rx, ry, rg = exchange(dx_local), exchange(dy_local), exchange(gidx)
+        rx, ry, rg = exchange(px), exchange(py), exchange(pg)
         lo, hi = key_band(world, rank, nb)
         lq = float(grid_query.cell_len)
         qcx = _java_cell(qx, grid_query.min_x, lq)
@@ -171,15 +188,20 @@ def join_sharded(dx_local, dy_local, dbase: int, qx, qy, r: float, approximate: 
     return pairs, offset, total
 
 
+def _poly_kw(poly_rings):
+    return {} if poly_rings is None else {"poly_rings": poly_rings}
+
+
 def ppoly_sharded(x_local, y_local, base: int, ring_off, vx, vy, r: float, approximate: bool = False, *, grid=None,
-                  ctx=None, group=None, local_ppoly: Optional[Callable] = None):
+                  ctx=None, group=None, local_ppoly: Optional[Callable] = None, poly_rings=None):
     """Point-polygon range of one window over the group (polygons on every rank, points by
-    arrival): returns (pairs int64 [m, 2] = (polygon, point window idx), offset, total)."""
+    arrival): returns (pairs int64 [m, 2] = (polygon, point window idx), offset, total).
+    poly_rings: rings per polygon (shell + holes), as for Context.range_ppoly."""
     import torch
 
     if local_ppoly is None:
         local_ppoly = _device_local_ppoly(ctx, grid)
-    pairs = local_ppoly(x_local, y_local, ring_off, vx, vy, r, approximate).to(torch.int64)
+    pairs = local_ppoly(x_local, y_local, ring_off, vx, vy, r, approximate, **_poly_kw(poly_rings)).to(torch.int64)
     if len(pairs):
         pairs[:, 1] += base
     offset, total = gather_counts(len(pairs), pairs.device, group)
@@ -188,7 +210,7 @@ def ppoly_sharded(x_local, y_local, base: int, ring_off, vx, vy, r: float, appro
 
 def join_ppoly_sharded(x_local, y_local, base: int, ring_off, vx, vy, r: float, approximate: bool = False, *,
                        grid_points=None, grid_query=None, ctx=None, group=None,
-                       local_join: Optional[Callable] = None):
+                       local_join: Optional[Callable] = None, poly_rings=None):
     """Point-polygon join of one window over the group (PointPolygonJoinQuery.java:162-201):
     the polygon stream on every rank, points by arrival; returns (pairs int64 [m, 2] =
     (point window idx, polygon), offset, total).  Per-rank pair sets are disjoint (each point
@@ -197,7 +219,7 @@ def join_ppoly_sharded(x_local, y_local, base: int, ring_off, vx, vy, r: float, 
 
     if local_join is None:
         local_join = _device_local_join_ppoly(ctx, grid_points, grid_query)
-    pairs = local_join(x_local, y_local, ring_off, vx, vy, r, approximate).to(torch.int64)
+    pairs = local_join(x_local, y_local, ring_off, vx, vy, r, approximate, **_poly_kw(poly_rings)).to(torch.int64)
     if len(pairs):
         pairs[:, 0] += base
     offset, total = gather_counts(len(pairs), pairs.device, group)
@@ -206,7 +228,7 @@ def join_ppoly_sharded(x_local, y_local, base: int, ring_off, vx, vy, r: float, 
 
 def knn_ppoly_sharded(x_local, y_local, base: int, vx, vy, r: float, k: int, approximate: bool = False, *,
                       grid=None, ctx=None, group=None, local_knn: Optional[Callable] = None,
-                      merge: Optional[Callable] = None) -> KnnResult:
+                      merge: Optional[Callable] = None, ring_off=None) -> KnnResult:
     """Point-polygon kNN of one window over the group (PointPolygonKNNQuery.java:162-236 with the
     windowAll merge of KNNQuery.java:204-272 replaced by one all-gather of each rank's top-k):
     local_knn(x, y, vx, vy, r, k, approximate) -> (idx int32[k], dist f64[k]) padded with
@@ -219,15 +241,15 @@ def knn_ppoly_sharded(x_local, y_local, base: int, vx, vy, r: float, k: int, app
         local_knn = _device_local_knn_ppoly(ctx, grid)
     if merge is None:
         merge = _device_merge(ctx)
-    li, ld = local_knn(x_local, y_local, vx, vy, r, k, approximate)
+    li, ld = local_knn(x_local, y_local, vx, vy, r, k, approximate, **({} if ring_off is None else {"ring_off": ring_off}))
     li = li.to(torch.int64)
     gi = torch.where(li >= 0, li + base, torch.full_like(li, -1)).to(torch.int32)
     gd = ld.contiguous()
     all_d = torch.empty((world, k), dtype=gd.dtype, device=gd.device)
     all_i = torch.empty((world, k), dtype=gi.dtype, device=gi.device)
     if world > 1:
-        dist.all_gather_into_tensor(all_d.view(-1), gd, group=group)
-        dist.all_gather_into_tensor(all_i.view(-1), gi, group=group)
+        all_gather_into(all_d.view(-1), gd, group)
+        all_gather_into(all_i.view(-1), gi, group)
     else:
         all_d[0] = gd
         all_i[0] = gi
@@ -245,11 +267,43 @@ def gather_counts(count: int, device, group=None):
     t = torch.tensor([count], dtype=torch.int64, device=device)
     allc = torch.empty(world, dtype=torch.int64, device=device)
     if world > 1:
-        dist.all_gather_into_tensor(allc, t, group=group)
+        all_gather_into(allc, t, group)
     else:
         allc[0] = t[0]
     allc = allc.cpu().tolist()
     return sum(allc[:rank]), sum(allc)
+
+
+def _host_staged(t, group) -> bool:
+    """gloo moves CPU tensors only: device tensors are staged through host memory (the
+    multi-process-on-one-GPU test rig); RCCL (backend "nccl") takes them as they are."""
+    import torch.distributed as dist
+
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def all_gather_into(out, inp, group=None):
+    """dist.all_gather_into_tensor(out, inp), staged through host for gloo."""
+    import torch.distributed as dist
+
+    if _host_staged(inp, group):
+        o = out.cpu()
+        dist.all_gather_into_tensor(o, inp.cpu(), group=group)
+        out.copy_(o)
+    else:
+        dist.all_gather_into_tensor(out, inp, group=group)
+
+
+def all_to_all(out, inp, out_splits=None, in_splits=None, group=None):
+    """dist.all_to_all_single, staged through host for gloo."""
+    import torch.distributed as dist
+
+    if _host_staged(inp, group):
+        o = out.cpu()
+        dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=group)
+        out.copy_(o)
+    else:
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
 
 
 # ------------------------------------------------------------------ default device engine --
@@ -280,6 +334,13 @@ def _device_merge(ctx):
     return f
 
 
+def _device_band_pack(ctx, grid_data):
+    def f(x, y, base, nb, world):
+        return ctx.band_pack_async(grid_data, nb, world, x, y, base)
+
+    return f
+
+
 def _device_local_join(ctx, grid_data, grid_query):
     def f(x, y, qx, qy, r, approximate):
         return ctx.join_pp(grid_data, grid_query, x, y, qx, qy, r, approximate).reshape(-1, 2)
@@ -288,15 +349,16 @@ def _device_local_join(ctx, grid_data, grid_query):
 
 
 def _device_local_ppoly(ctx, grid):
-    def f(x, y, ring_off, vx, vy, r, approximate):
-        return ctx.range_ppoly(grid, x, y, ring_off, vx, vy, r, approximate).reshape(-1, 2)
+    def f(x, y, ring_off, vx, vy, r, approximate, poly_rings=None):
+        return ctx.range_ppoly(grid, x, y, ring_off, vx, vy, r, approximate, poly_rings=poly_rings).reshape(-1, 2)
 
     return f
 
 
 def _device_local_join_ppoly(ctx, grid_points, grid_query):
-    def f(x, y, ring_off, vx, vy, r, approximate):
-        return ctx.join_ppoly(grid_points, grid_query, x, y, ring_off, vx, vy, r, approximate).reshape(-1, 2)
+    def f(x, y, ring_off, vx, vy, r, approximate, poly_rings=None):
+        return ctx.join_ppoly(grid_points, grid_query, x, y, ring_off, vx, vy, r, approximate,
+                              poly_rings=poly_rings).reshape(-1, 2)
 
     return f
 
@@ -304,8 +366,8 @@ def _device_local_join_ppoly(ctx, grid_points, grid_query):
 def _device_local_knn_ppoly(ctx, grid):
     import torch
 
-    def f(x, y, vx, vy, r, k, approximate):
-        ii, dd = ctx.knn_ppoly(grid, x, y, vx, vy, r, k, approximate)
+    def f(x, y, vx, vy, r, k, approximate, ring_off=None):
+        ii, dd = ctx.knn_ppoly(grid, x, y, vx, vy, r, k, approximate, ring_off=ring_off)
         oi = torch.full((k,), -1, dtype=torch.int32, device=x.device)
         od = torch.full((k,), -1, dtype=torch.int64, device=x.device).view(torch.float64)  # all-ones bits
         oi[:len(ii)] = ii

@@ -135,7 +135,8 @@ def _join_worker(rank, world, port, out_path):
 
         for part in ("arrival", "cells"):
             pairs, off, total = D.join_sharded(xl, yl, lo, tqx, tqy, r, grid_data=cg, grid_query=cg,
-                                               partition=part, local_join=local_join)
+                                               partition=part, local_join=local_join,
+                                               band_pack=D.torch_band_pack(cg))
             got = [None] * world
             dist.all_gather_object(got, (rank, pairs.numpy().tolist(), off, total))
             out[f"{gn}_{r}_{part}"] = got
