@@ -267,7 +267,8 @@ class JoinWorkload(Workload):
     """C3 (BASELINE.json configs[2]): 10k queries x 10M Gaussian-clustered data points per
     window, 500x500, r = 0.05 (32 shared centres, sigma 0.1)."""
     tag = "join_probe"
-    kernel = "geohip::join_tile count + write passes (tile binning before the timed region)"
+    kernel = ("geohip join step: tile binning + query block lists + join_fused (one pass: work items, "
+              "decoupled look-back, staged pair runs); the whole device step is timed")
     grid_n, radius, n_default, nq, sigma = 500, 0.05, 10_000_000, 10_000, 0.1
     windows = 2
 

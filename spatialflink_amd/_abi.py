@@ -143,7 +143,6 @@ _SIGS = {
     "geohip_debug_knn_pass_stats": (c_int, [_P, _P]),
     "geohip_debug_knn_pass_trace": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_double, c_double, c_double,
                                             c_uint32, c_int, _P, c_uint64, POINTER(c_uint32)]),
-    "geohip_debug_ctx_join_mask_budget": (c_int, [_P, c_uint64]),
 }
 for _name, (_res, _args) in _SIGS.items():
     _f = getattr(lib, _name)
@@ -645,10 +644,6 @@ class Context:
         min_x, max_x, min_y, max_y = bbox
         rc = lib.geohip_synth_uniform_async(self.h, _ptr(x), _ptr(y), len(x), base, seed, min_x, max_x, min_y, max_y)
         self._check(rc, "synth_uniform_async")
-
-    def debug_join_mask_budget(self, nbytes: int = 4 << 30):
-        """Test hook: byte budget of this ctx's join hit masks; beyond it the write pass recomputes."""
-        self._check(lib.geohip_debug_ctx_join_mask_budget(self.h, nbytes), "debug_join_mask_budget")
 
     def debug_knn_pass_stats(self):
         """(entries gathered, of them spilled, kept at or below the k-th bin) of the last kNN pass."""

@@ -50,7 +50,6 @@ struct geohip_ctx {
     double plan_q[3] = {0, 0, 0};
     PointPlan plan{};
     unsigned long long range_epoch = 0;  // fused range pass: status words of this launch carry it
-    uint64_t join_mask_budget = 4ull << 30;  // join hit masks kept between the passes up to this
 };
 
 namespace {
@@ -799,12 +798,6 @@ int geohip_debug_knn_pass_trace(geohip_ctx* ctx, const geohip_grid* grid, const 
 }
 
 // Test hook: byte budget of this ctx's join hit masks (beyond it the write pass recomputes).
-int geohip_debug_ctx_join_mask_budget(geohip_ctx* ctx, uint64_t bytes) {
-    if (!ctx) return GEOHIP_ERR_ARG;
-    ctx->join_mask_budget = bytes;
-    return GEOHIP_OK;
-}
-
 }  // extern "C"
 
 // ------------------------------------------------------------------ shared with join/ppoly --
@@ -821,7 +814,6 @@ int ctx_ensure_ingest(geohip_ctx* ctx, int slot, size_t bytes, void** out) {
     return rc;
 }
 int ctx_begin(geohip_ctx* ctx) { return begin(ctx); }
-uint64_t ctx_join_mask_budget(geohip_ctx* ctx) { return ctx->join_mask_budget; }
 hipStream_t ctx_stream(geohip_ctx* ctx) { return ctx->stream; }
 int ctx_mem(geohip_ctx* ctx) { return ctx->mem; }
 uint64_t* ctx_pinned(geohip_ctx* ctx) { return ctx->pinned; }

@@ -13,7 +13,6 @@ int ctx_fail(geohip_ctx* ctx, int code, const std::string& msg);
 int ctx_ensure(geohip_ctx* ctx, int slot, size_t bytes, void** out);  // slot 0..23
 int ctx_ensure_ingest(geohip_ctx* ctx, int slot, size_t bytes, void** out);  // slot 0..7
 int ctx_begin(geohip_ctx* ctx);  // clears the error, selects the ctx's device
-uint64_t ctx_join_mask_budget(geohip_ctx* ctx);  // test hook geohip_debug_ctx_join_mask_budget
 hipStream_t ctx_stream(geohip_ctx* ctx);
 int ctx_mem(geohip_ctx* ctx);
 uint64_t* ctx_pinned(geohip_ctx* ctx);
@@ -23,7 +22,6 @@ int ctx_stage_xy(geohip_ctx* ctx, const double* x, const double* y, uint64_t n, 
 
 // squared-distance screen bounds for "dist <= r" (r2lo < 0 / r2hi = inf where they cannot hold)
 void pp_screen_bounds(double r, double* r2lo, double* r2hi);
-// measurement/test hook: byte budget of the join's hit masks (beyond it the write pass recomputes)
 
 int join_pp_impl(geohip_ctx* ctx, const geohip_grid* grid_data, const geohip_grid* grid_query, const double* dx,
                  const double* dy, uint64_t nd, const double* qx, const double* qy, uint64_t nq, double r,

@@ -483,10 +483,11 @@ def test_knn_large_k(ctx):
 
 
 # ------------------------------------------------------------------ less common kernel paths --
-def test_join_dense_tiles_batches_and_recompute(ctx):
-    """Join beyond the common case: > 256 candidate queries per tile (several LDS query batches)
-    and thousands of points per tile; then the same join with a zero mask budget (the write pass
-    recomputes instead of reading the count pass's hit masks)."""
+def test_join_dense_tiles_many_items(ctx):
+    """Join beyond the common case: > 256 candidate queries per tile (several query chunks per
+    tile) and thousands of points per tile (several point chunks): one tile becomes many work
+    items, each finding its output offset by the look-back; repeated calls agree exactly (the
+    item order, and so the pair order, is fixed by the tile lists)."""
     ag, cg = agrid(100)
     rng = np.random.default_rng(31)
     dx = 116.40 + rng.uniform(0, 0.03, 30000)
@@ -497,12 +498,9 @@ def test_join_dense_tiles_batches_and_recompute(ctx):
     assert len(want) > 100000
     got = ctx.join_pp(ag, ag, dx, dy, qx, qy, 0.01)
     assert pairs_sorted(got).tolist() == want
-    ctx.debug_join_mask_budget(0)
-    try:
-        got = ctx.join_pp(ag, ag, dx, dy, qx, qy, 0.01)
-        assert pairs_sorted(got).tolist() == want
-    finally:
-        ctx.debug_join_mask_budget()
+    assert ctx.join_pp_count(ag, ag, dx, dy, qx, qy, 0.01) == len(want)
+    got2 = ctx.join_pp(ag, ag, dx, dy, qx, qy, 0.01)
+    assert pairs_sorted(got2).tolist() == want
 
 
 def test_ppoly_big_tile_and_long_ring(ctx):
@@ -528,3 +526,30 @@ def test_ppoly_big_tile_and_long_ring(ctx):
         assert pairs_sorted(got).tolist() == want
 
 
+
+
+def test_binning_cell_boundaries(ctx):
+    """Tile binning computes cells by a multiply with an exact-division fallback near integers
+    (d_axis_cell_fast): points on and one ulp either side of many cell boundaries, through the
+    join and the point-polygon range, must land in the cells the reference's division gives."""
+    rng = np.random.default_rng(77)
+    for gn in (100, 500, 997):
+        ag, cg = agrid(gn)
+        l = (BJ[1] - BJ[0]) / gn
+        k = rng.integers(0, gn + 1, 4000)
+        bx = BJ[0] + k * l
+        by = BJ[2] + rng.integers(0, gn + 1, 4000) * l
+        xs = np.concatenate([bx, np.nextafter(bx, -np.inf), np.nextafter(bx, np.inf), bx])
+        ys = np.concatenate([by, by, by, np.nextafter(by, np.inf)])
+        # the boundary values (v - min) / l lands on exactly, or the division rounds to
+        xs = np.concatenate([xs, BJ[0] + (k + 1e-17) * l, rng.uniform(BJ[0], BJ[1], 20000)])
+        ys = np.concatenate([ys, BJ[2] + (k + 1e-17) * l, rng.uniform(BJ[2], BJ[3], 20000)])
+        qx, qy = rng.uniform(BJ[0], BJ[1], 300), rng.uniform(BJ[2], BJ[3], 300)
+        r = 3.5 * l
+        want = pairs_sorted(cref.join_pp(cg, cg, xs, ys, qx, qy, r)).tolist()
+        assert pairs_sorted(ctx.join_pp(ag, ag, xs, ys, qx, qy, r)).tolist() == want
+        want = pairs_sorted(cref.join_pp(cg, cg, xs, ys, qx, qy, r, True)).tolist()
+        assert pairs_sorted(ctx.join_pp(ag, ag, xs, ys, qx, qy, r, True)).tolist() == want
+        off, vx, vy = synth.star_polygons(40, 78, bbox=BJ, r_min=2 * l, r_max=6 * l)
+        want = pairs_sorted(cref.range_ppoly(cg, xs, ys, off, vx, vy, l)).tolist()
+        assert pairs_sorted(ctx.range_ppoly(ag, xs, ys, off, vx, vy, l)).tolist() == want
