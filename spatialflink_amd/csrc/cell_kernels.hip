@@ -135,6 +135,22 @@ __global__ void scan_apply(const T* __restrict__ in, uint64_t n, const T* __rest
 }
 
 // ------------------------------------------------------------------ tile binning ---------
+// Unsigned division by a launch constant d >= 1 without the ~30-instruction integer division
+// sequence: q = trunc(n * fl(1/d)) in fp64 is off by at most one (n < 2^32), and one multiply
+// corrects it.  Exact for every 32-bit n.
+struct FastDiv {
+    double inv;
+    unsigned d;
+    __device__ __forceinline__ unsigned div(unsigned n) const {
+        unsigned q = (unsigned)((double)n * inv);
+        const long long r = (long long)n - (long long)q * (long long)d;
+        if (r < 0) q--;
+        else if (r >= (long long)d) q++;
+        return q;
+    }
+};
+inline FastDiv make_fastdiv(unsigned d) { return FastDiv{1.0 / (double)d, d}; }
+
 struct TileGeom {
     double mnx, mny, l;  // grid the point cells are computed on
     double il;           // fl(1 / l) (d_axis_cell_fast)
@@ -142,6 +158,7 @@ struct TileGeom {
     int32_t ts;          // cells per tile side
     int32_t nt;          // tiles per side
     uint32_t ntiles;     // nt * nt <= kMaxTiles
+    FastDiv dts, dnb;    // / ts, / nb
 };
 
 __device__ __forceinline__ bool point_cell(const TileGeom& g, double x, double y, int32_t& cx, int32_t& cy) {
@@ -150,7 +167,7 @@ __device__ __forceinline__ bool point_cell(const TileGeom& g, double x, double y
     return cx >= 0 && cy >= 0 && cx < g.nb && cy < g.nb;
 }
 __device__ __forceinline__ unsigned tile_of(const TileGeom& g, int32_t cx, int32_t cy) {
-    return (unsigned)(cx / g.ts) * (unsigned)g.nt + (unsigned)(cy / g.ts);
+    return g.dts.div((unsigned)cx) * (unsigned)g.nt + g.dts.div((unsigned)cy);
 }
 
 // Two binning levels, each a local LDS counting sort so every store leaves in runs: level 1
@@ -187,23 +204,32 @@ struct BinPass {
 
 __device__ __forceinline__ unsigned key_tile(const TileGeom& g, unsigned key) {
     const unsigned nb = (unsigned)g.nb;
-    const unsigned cx = key / nb, cy = key - cx * nb;
-    return (cx / (unsigned)g.ts) * (unsigned)g.nt + cy / (unsigned)g.ts;
+    const unsigned cx = g.dnb.div(key), cy = key - cx * nb;
+    return g.dts.div(cx) * (unsigned)g.nt + g.dts.div(cy);
 }
 
-// level-1 point j: coordinates, key (kNoKey when out of the grid), bin: its band, nbands when
-// out of the grid, nbands + 1 when its cell is not in the keep bitmap (dropped)
-__device__ __forceinline__ unsigned l1_point(const BinPass& a, uint64_t i, double& px, double& py, unsigned& key) {
-    px = a.x[i];
-    py = a.y[i];
+// level-1 point: key (kNoKey when out of the grid); bin: its band, nbands when out of the grid,
+// nbands + 1 when its cell is not in the keep bitmap (dropped).  Two steps so the keep-bitmap
+// loads of several points go out together (and ahead of any prefetch).
+__device__ __forceinline__ unsigned l1_key(const BinPass& a, double px, double py) {
     int32_t cx, cy;
-    if (point_cell(a.g, px, py, cx, cy)) {
-        key = (unsigned)cx * (unsigned)a.g.nb + (unsigned)cy;
-        if (a.keep && !((a.keep[key >> 5] >> (key & 31u)) & 1u)) return a.nbands + 1;
-        return tile_of(a.g, cx, cy) >> kBandBits;
-    }
-    key = kNoKey;
-    return a.nbands;
+    if (point_cell(a.g, px, py, cx, cy)) return (unsigned)cx * (unsigned)a.g.nb + (unsigned)cy;
+    return kNoKey;
+}
+__device__ __forceinline__ unsigned l1_keepword(const BinPass& a, unsigned key) {
+    return (a.keep && key != kNoKey) ? a.keep[key >> 5] : ~0u;
+}
+__device__ __forceinline__ unsigned l1_bin(const BinPass& a, unsigned key, unsigned kw) {
+    if (key == kNoKey) return a.nbands;
+    if (!((kw >> (key & 31u)) & 1u)) return a.nbands + 1;
+    return key_tile(a.g, key) >> kBandBits;
+}
+
+// Workgroup barrier that orders LDS only: waits for this wave's LDS operations, not for its
+// outstanding global loads (__syncthreads' workgroup fence would drain those too).  For phases
+// whose cross-wave traffic is LDS alone.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 // the range of points a block bins: level 1 a chunk of the window, level 2 one work item
@@ -235,16 +261,40 @@ __global__ __launch_bounds__(kBinThreads) void bin_count(BinPass a) {
     const int wid = threadIdx.x / kWave;
     for (unsigned t = threadIdx.x; t < (kBinThreads / kWave) * kLocalBins; t += kBinThreads) (&h[0][0])[t] = 0;
     __syncthreads();
-    for (uint64_t i = b0 + threadIdx.x; i < b1; i += kBinThreads) {
-        unsigned bin;
-        if (LEVEL == 1) {
-            double px, py;
-            unsigned key;
-            bin = l1_point(a, i, px, py, key);
-        } else {
-            bin = key_tile(a.g, a.src.key[i]) - (band << kBandBits);
+    // 4 points per thread with all their loads issued first (a single load pair per thread in
+    // flight left the pass latency-bound at 2.5 TB/s)
+    constexpr unsigned kU = 4;
+    for (uint64_t i0 = b0 + threadIdx.x; i0 < b1; i0 += kU * kBinThreads) {
+        double px[kU], py[kU];
+        unsigned key[kU];
+#pragma unroll
+        for (unsigned k = 0; k < kU; k++) {
+            const uint64_t i = i0 + (uint64_t)k * kBinThreads;
+            if (i < b1) {
+                if (LEVEL == 1) {
+                    px[k] = a.x[i];
+                    py[k] = a.y[i];
+                } else {
+                    key[k] = a.src.key[i];
+                }
+            }
         }
-        atomicAdd(&h[wid][bin], 1u);
+        unsigned kw[kU];
+        if (LEVEL == 1) {
+#pragma unroll
+            for (unsigned k = 0; k < kU; k++) {
+                key[k] = l1_key(a, px[k], py[k]);
+                kw[k] = i0 + (uint64_t)k * kBinThreads < b1 ? l1_keepword(a, key[k]) : ~0u;
+            }
+        }
+#pragma unroll
+        for (unsigned k = 0; k < kU; k++) {
+            const uint64_t i = i0 + (uint64_t)k * kBinThreads;
+            if (i < b1) {
+                const unsigned bin = LEVEL == 1 ? l1_bin(a, key[k], kw[k]) : key_tile(a.g, key[k]) - (band << kBandBits);
+                atomicAdd(&h[wid][bin], 1u);
+            }
+        }
     }
     __syncthreads();
     if (threadIdx.x < nbins) {
@@ -365,29 +415,52 @@ __global__ __launch_bounds__(kBinThreads) void bin_scatter(BinPass a) {
         lh[t] = 0;
     }
     __syncthreads();
+    // the next sub-chunk's points are loaded while this one is sorted: the barriers below
+    // order LDS only (lds_barrier), so those loads stay in flight across them
+    double nx[2], ny[2];
+    unsigned nidx[2], nkey[2];
+    auto fetch = [&](uint64_t sb) {
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const uint64_t i = sb + threadIdx.x + (uint64_t)k * kBinThreads;
+            if (i < b1) {
+                if (LEVEL == 1) {
+                    nx[k] = a.x[i];
+                    ny[k] = a.y[i];
+                } else {
+                    nx[k] = a.src.x[i];
+                    ny[k] = a.src.y[i];
+                    nidx[k] = a.src.idx[i];
+                    nkey[k] = a.src.key[i];
+                }
+            }
+        }
+    };
+    if (b0 < b1) fetch(b0);
     for (uint64_t sb = b0; sb < b1; sb += kSub) {
         const unsigned m = b1 - sb < (uint64_t)kSub ? (unsigned)(b1 - sb) : (unsigned)kSub;
         double px[2], py[2];
         unsigned idx[2], key[2], bin[2], rk[2];
+        unsigned kw[2];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const unsigned j = threadIdx.x + k * kBinThreads;
+            px[k] = nx[k];
+            py[k] = ny[k];
+            idx[k] = LEVEL == 1 ? (unsigned)(sb + j) : nidx[k];
+            key[k] = LEVEL == 1 ? l1_key(a, px[k], py[k]) : nkey[k];
+            kw[k] = (LEVEL == 1 && j < m) ? l1_keepword(a, key[k]) : ~0u;  // issued before the prefetch
+        }
+        if (sb + kSub < b1) fetch(sb + kSub);
 #pragma unroll
         for (int k = 0; k < 2; k++) {
             const unsigned j = threadIdx.x + k * kBinThreads;
             if (j < m) {
-                const uint64_t i = sb + j;
-                if (LEVEL == 1) {
-                    bin[k] = l1_point(a, i, px[k], py[k], key[k]);
-                    idx[k] = (unsigned)i;
-                } else {
-                    px[k] = a.src.x[i];
-                    py[k] = a.src.y[i];
-                    idx[k] = a.src.idx[i];
-                    key[k] = a.src.key[i];
-                    bin[k] = key_tile(a.g, key[k]) - (band << kBandBits);
-                }
+                bin[k] = LEVEL == 1 ? l1_bin(a, key[k], kw[k]) : key_tile(a.g, key[k]) - (band << kBandBits);
                 rk[k] = atomicAdd(&lh[bin[k]], 1u);
             }
         }
-        __syncthreads();
+        lds_barrier();
         if (threadIdx.x < kWave) {  // exclusive scan of lh over <= 192 bins (3 per lane)
             const int l = threadIdx.x;
             const unsigned v0 = lh[l], v1 = lh[kWave + l], v2 = 2 * kWave + l < kLocalBins ? lh[2 * kWave + l] : 0u;
@@ -400,7 +473,7 @@ __global__ __launch_bounds__(kBinThreads) void bin_scatter(BinPass a) {
             ls[kWave + l] = i1 - v1;
             if (2 * kWave + l < kLocalBins) ls[2 * kWave + l] = i2 - v2;
         }
-        __syncthreads();
+        lds_barrier();
 #pragma unroll
         for (int k = 0; k < 2; k++) {
             const unsigned j = threadIdx.x + k * kBinThreads;
@@ -413,7 +486,7 @@ __global__ __launch_bounds__(kBinThreads) void bin_scatter(BinPass a) {
                 st.bin[slot] = (unsigned char)bin[k];
             }
         }
-        __syncthreads();
+        lds_barrier();
 #pragma unroll
         for (int k = 0; k < 2; k++) {
             const unsigned j = threadIdx.x + k * kBinThreads;
@@ -426,12 +499,12 @@ __global__ __launch_bounds__(kBinThreads) void bin_scatter(BinPass a) {
                 a.dst.key[g] = st.key[j];
             }
         }
-        __syncthreads();
+        lds_barrier();
         for (unsigned t = threadIdx.x; t < nbins; t += kBinThreads) {
             cur[t] += lh[t];
             lh[t] = 0;
         }
-        __syncthreads();
+        lds_barrier();
     }
 }
 
@@ -442,6 +515,7 @@ struct TileBins {
     const unsigned* skey;
     const unsigned* start;  // ntiles + 1
     int32_t nb;
+    FastDiv dnb;            // / nb (key -> cx)
 };
 
 // ------------------------------------------------------------------ pair output ----------
@@ -919,7 +993,7 @@ __global__ __launch_bounds__(kTB) void join_fused(JoinRun a) {
                 px = a.tb.sx[i];
                 py = a.tb.sy[i];
                 const unsigned key = a.tb.skey[i];
-                cx = (int32_t)(key / nb);
+                cx = (int32_t)g.dnb.div(key);
                 cy = (int32_t)(key - (unsigned)cx * nb);
             }
             const float ax = (float)(px - ox), ay = (float)(py - oy);
@@ -955,7 +1029,7 @@ __global__ __launch_bounds__(kTB) void join_fused(JoinRun a) {
                     py = a.tb.sy[i];
                     pid = a.tb.sidx[i];
                     const unsigned key = a.tb.skey[i];
-                    cx = (int32_t)(key / nb);
+                    cx = (int32_t)g.dnb.div(key);
                     cy = (int32_t)(key - (unsigned)cx * nb);
                 }
                 const float ax = (float)(px - ox), ay = (float)(py - oy);
@@ -1401,7 +1475,7 @@ __global__ __launch_bounds__(kTB) void ppoly_eval(TileBins tb, const PolyWork* _
         if (base + kTB < de) fetch(base + kTB);
         bool hit = false, need = false;
         if (i < de) {
-            const int32_t cx = (int32_t)(key / nb), cy = (int32_t)(key - (unsigned)cx * nb);
+            const int32_t cx = (int32_t)tb.dnb.div(key), cy = (int32_t)(key - (unsigned)cx * nb);
             bool g = in_r(g0, cx, cy);
             if (P.ng > 1 && !g) g = in_rects(grect + 4, P.ng - 1, cx, cy);
             bool c = !g && in_r(c0, cx, cy);
@@ -2290,6 +2364,8 @@ TileGeom tile_geom(const geohip_grid& g, int32_t nb) {
     if (t.ts < 1) t.ts = 1;
     t.nt = (nb + t.ts - 1) / t.ts;
     t.ntiles = (uint32_t)t.nt * (uint32_t)t.nt;
+    t.dts = make_fastdiv((unsigned)t.ts);
+    t.dnb = make_fastdiv((unsigned)(nb > 0 ? nb : 1));
     return t;
 }
 
@@ -2389,6 +2465,7 @@ int bin_tiles(geohip_ctx* ctx, Scratch& S, const double* dx, const double* dy, u
     tb->skey = a.dst.key;
     tb->start = start;
     tb->nb = geo.nb;
+    tb->dnb = geo.dnb;
     return GEOHIP_OK;
 }
 
