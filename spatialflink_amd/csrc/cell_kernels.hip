@@ -55,13 +55,23 @@ __device__ __forceinline__ int32_t d_axis_cell(double v, double mn, double l) {
 // The same cell through a multiply by il = fl(1/l): q = fl(t * il) is within |q| 2^-51 of the
 // exact quotient t / l, so when q lies farther than |q| 2^-49 from every integer, floor(q) is
 // floor(fl(t / l)); otherwise (and for NaN / inf / |q| >= 2^49) the division decides.
+// (int) of a double as Java casts it -- NaN -> 0, out of range saturates -- which is what
+// v_cvt_i32_f64 does: one instruction instead of d_java_d2i's compare chain.
+__device__ __forceinline__ int32_t d_cvt_java(double f) {
+    int32_t r;
+    asm("v_cvt_i32_f64 %0, %1" : "=v"(r) : "v"(f));
+    return r;
+}
 __device__ __forceinline__ int32_t d_axis_cell_fast(double v, double mn, double l, double il) {
     const double t = v - mn;
     const double q = t * il;
-    const double f = __builtin_floor(q);
+    double f = __builtin_floor(q);
     const double e = __builtin_fabs(q) * 0x1.0p-49 + 0x1.0p-1000;
-    if (q - f > e && (f + 1.0) - q > e) return d_java_d2i(f);
-    return d_java_d2i(__builtin_floor(t / l));
+    const bool ok = (q - f > e) & ((f + 1.0) - q > e);
+    if (__ballot(!ok)) {  // wave-uniform, rare: the division decides near integers, NaN, inf
+        if (!ok) f = __builtin_floor(t / l);
+    }
+    return d_cvt_java(f);
 }
 
 // ------------------------------------------------------------------ scans ----------------
@@ -292,7 +302,7 @@ __global__ __launch_bounds__(kBinThreads) void bin_count(BinPass a) {
             const uint64_t i = i0 + (uint64_t)k * kBinThreads;
             if (i < b1) {
                 const unsigned bin = LEVEL == 1 ? l1_bin(a, key[k], kw[k]) : key_tile(a.g, key[k]) - (band << kBandBits);
-                atomicAdd(&h[wid][bin], 1u);
+                if (LEVEL == 2 || bin != a.nbands + 1) atomicAdd(&h[wid][bin], 1u);  // dropped: not counted
             }
         }
     }
@@ -455,9 +465,10 @@ __global__ __launch_bounds__(kBinThreads) void bin_scatter(BinPass a) {
 #pragma unroll
         for (int k = 0; k < 2; k++) {
             const unsigned j = threadIdx.x + k * kBinThreads;
+            bin[k] = a.nbands + 1;  // level 1: dropped unless binned below
             if (j < m) {
                 bin[k] = LEVEL == 1 ? l1_bin(a, key[k], kw[k]) : key_tile(a.g, key[k]) - (band << kBandBits);
-                rk[k] = atomicAdd(&lh[bin[k]], 1u);
+                if (LEVEL == 2 || bin[k] != a.nbands + 1) rk[k] = atomicAdd(&lh[bin[k]], 1u);
             }
         }
         lds_barrier();
@@ -477,7 +488,7 @@ __global__ __launch_bounds__(kBinThreads) void bin_scatter(BinPass a) {
 #pragma unroll
         for (int k = 0; k < 2; k++) {
             const unsigned j = threadIdx.x + k * kBinThreads;
-            if (j < m) {
+            if (j < m && (LEVEL == 2 || bin[k] != a.nbands + 1)) {  // dropped points are not staged
                 const unsigned slot = ls[bin[k]] + rk[k];
                 st.x[slot] = px[k];
                 st.y[slot] = py[k];
@@ -490,7 +501,7 @@ __global__ __launch_bounds__(kBinThreads) void bin_scatter(BinPass a) {
 #pragma unroll
         for (int k = 0; k < 2; k++) {
             const unsigned j = threadIdx.x + k * kBinThreads;
-            if (j < m && (LEVEL == 2 || st.bin[j] <= a.nbands)) {  // dropped points stay here
+            if (j < (LEVEL == 2 ? m : ls[a.nbands + 1])) {  // the staged points: every bin before "dropped"
                 const unsigned b = st.bin[j];
                 const unsigned g = cur[b] + (j - ls[b]);
                 a.dst.x[g] = st.x[j];
