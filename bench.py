@@ -56,6 +56,7 @@ def parse():
     p.add_argument("--points", type=int, default=None, help="points per window per GPU (default: the config's)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-e2e", action="store_true", help="skip the host-resident end-to-end line")
     p.add_argument("--time-every", type=int, default=8,
                    help="bracket every N-th timed step's kernels with HIP events (1 = all)")
     return p.parse_args()
@@ -114,6 +115,9 @@ class Workload:
 
     def roofline_extra(self) -> dict:
         return {}
+
+    def e2e(self) -> dict | None:  # host-resident window -> results on host (rank 0, N = 1)
+        return None
 
 
 def _uniform_windows(ctx, dev, n, rank, seeds, bbox):
@@ -181,6 +185,32 @@ class KnnWorkload(Workload):
                 "points_per_window_per_gpu": self.n, "grid": self.grid_n, "k": self.k, "radius": self.radius,
                 "windows_resident": self.windows,
                 "parallelism": f"shard{self.world}"}
+
+    def e2e(self):
+        """The C2 window as a host (pageable numpy) array through geohip_knn_pp in
+        GEOHIP_MEM_HOST mode: pinned two-slot staging in 1M-point chunks, each chunk's knn_pass
+        launched as its DMA lands (overlapping the later copies), chunk lists merged, k results
+        copied back.  Wall clock per window, results on the host."""
+        import torch
+        from spatialflink_amd import Context
+        hx = self.xs[0].cpu().numpy()
+        hy = self.ys[0].cpu().numpy()
+        ctx = Context(self.dev.index)
+        want = self.ctx.knn_pp(self.grid, self.xs[0], self.ys[0], self.q[0], self.q[1], self.radius, self.k)
+        torch.cuda.synchronize(self.dev)
+        gi, gd = ctx.knn_pp(self.grid, hx, hy, self.q[0], self.q[1], self.radius, self.k)  # warm-up, check
+        same = gi.tolist() == want[0].cpu().numpy().astype(np.uint32).tolist()
+        reps = 5
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            ctx.knn_pp(self.grid, hx, hy, self.q[0], self.q[1], self.radius, self.k)
+        t = (time.perf_counter() - t0) / reps
+        ctx.close()
+        return {"value": self.n / t, "unit": "points/sec", "ms_per_window": t * 1e3,
+                "h2d_GBps": BYTES_PER_POINT * self.n / t / 1e9, "matches_device_path": same, "windows_timed": reps,
+                "path": "pageable host x/y -> ctx-owned pinned 2-slot staging (1M-point chunks, persistent copy workers) -> "
+                        "per-chunk knn_pass as each chunk lands (copy stream / compute stream overlap) -> "
+                        "rebase + merge -> k results to host"}
 
     def cpu_baseline(self, seconds):
         cref = _oracle()
@@ -759,6 +789,10 @@ def main():
                      "algorithmic_bytes_per_launch": abytes, **wl.roofline_extra()},
         "cpu_baseline": None,
     }
+    if rank == 0 and world == 1 and not args.no_e2e:
+        e2e = wl.e2e()
+        if e2e is not None:
+            result["e2e"] = e2e
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = wl.cpu_baseline(args.cpu_seconds)
     if rank == 0:

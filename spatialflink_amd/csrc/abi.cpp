@@ -11,6 +11,11 @@
 #include <algorithm>
 #include <cmath>
 #include <string>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <tuple>
 #include <utility>
 #include <vector>
 
@@ -28,6 +33,56 @@ enum Slot {
     S_J16, S_J17, S_J18, S_J19, S_J20, S_J21, S_J22, S_J23,
     S_I0, S_I1, S_I2, S_I3, S_I4, S_I5, S_I6, S_I7,
     S_COUNT
+};
+
+// Persistent copy workers of one ctx (host staging): a job is a list of (dst, src, bytes)
+// slices, one per worker; the caller waits until every slice is done.
+struct CopyPool {
+    std::vector<std::thread> th;
+    std::mutex mu;
+    std::condition_variable cv, done_cv;
+    std::vector<std::tuple<char*, const char*, size_t>> work;
+    uint64_t gen = 0;
+    unsigned pending = 0;
+    bool stop = false;
+    explicit CopyPool(unsigned n) {
+        for (unsigned t = 0; t < n; t++)
+            th.emplace_back([this, t] {
+                uint64_t seen = 0;
+                for (;;) {
+                    std::tuple<char*, const char*, size_t> w{nullptr, nullptr, 0};
+                    {
+                        std::unique_lock<std::mutex> lk(mu);
+                        cv.wait(lk, [&] { return stop || gen != seen; });
+                        if (stop) return;
+                        seen = gen;
+                        if (t < work.size()) w = work[t];
+                    }
+                    if (std::get<2>(w)) memcpy(std::get<0>(w), std::get<1>(w), std::get<2>(w));
+                    {
+                        std::lock_guard<std::mutex> lk(mu);
+                        if (--pending == 0) done_cv.notify_one();
+                    }
+                }
+            });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv.notify_all();
+        for (auto& h : th) h.join();
+    }
+    // copy the slices in parallel (at most one per worker) and wait
+    void run(const std::vector<std::tuple<char*, const char*, size_t>>& slices) {
+        std::unique_lock<std::mutex> lk(mu);
+        work = slices;
+        pending = (unsigned)th.size();
+        gen++;
+        cv.notify_all();
+        done_cv.wait(lk, [&] { return pending == 0; });
+    }
 };
 
 struct geohip_ctx {
@@ -50,6 +105,13 @@ struct geohip_ctx {
     double plan_q[3] = {0, 0, 0};
     PointPlan plan{};
     unsigned long long range_epoch = 0;  // fused range pass: status words of this launch carry it
+    // host windows (GEOHIP_MEM_HOST): two pinned staging slots; the DMA of one slot runs on the
+    // copy stream while the host fills the other (host_stage)
+    hipStream_t cstream = nullptr;
+    char* stg[2] = {nullptr, nullptr};
+    hipEvent_t stg_ev[2] = {nullptr, nullptr};
+    bool stg_used[2] = {false, false};
+    std::unique_ptr<CopyPool> copy_pool;
 };
 
 namespace {
@@ -137,6 +199,75 @@ void timing_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1) {
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 // Stage x/y for the kernels: host pointers are copied into ctx scratch, device pointers used.
+// ---- host windows: chunked staging through ctx-owned pinned slots ------------------------
+// A pageable host window reaches the device in chunks of kStagePts points: the host copies chunk
+// c into pinned slot c % 2 (kStageThreads threads) while the DMA of chunk c - 1 runs on the copy
+// stream; each chunk's arrival is an event the compute stream can wait on, so kernels over
+// landed chunks overlap the copies of later ones (the kNN pipelines this way).
+constexpr uint64_t kStagePts = 1ull << 20;      // 16 MB of x + y per slot
+constexpr unsigned kStageThreads = 16;
+
+
+int stage_init(geohip_ctx* ctx) {
+    if (ctx->cstream) return GEOHIP_OK;
+    HIPCHK(hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking));
+    const unsigned hw = std::thread::hardware_concurrency();
+    const unsigned nw = std::max(2u, std::min(kStageThreads, hw ? hw : 2u));
+    ctx->copy_pool = std::make_unique<CopyPool>(nw);
+    for (int k = 0; k < 2; k++) {
+        HIPCHK(hipHostMalloc((void**)&ctx->stg[k], kStagePts * 16, hipHostMallocDefault));
+        HIPCHK(hipEventCreateWithFlags(&ctx->stg_ev[k], hipEventDisableTiming));
+        ctx->stg_used[k] = false;
+    }
+    return GEOHIP_OK;
+}
+
+// x and y of one chunk into a pinned slot, split over the ctx's copy workers
+void stage_copy(geohip_ctx* ctx, char* dx, const char* sx, char* dy, const char* sy, size_t bytes) {
+    if (bytes < (1u << 18) || !ctx->copy_pool) {
+        memcpy(dx, sx, bytes);
+        memcpy(dy, sy, bytes);
+        return;
+    }
+    const unsigned nw = (unsigned)ctx->copy_pool->th.size();
+    const unsigned half = nw / 2 ? nw / 2 : 1;
+    std::vector<std::tuple<char*, const char*, size_t>> sl;
+    const size_t per = ((bytes + half - 1) / half + 63) & ~(size_t)63;
+    for (int a = 0; a < 2; a++)
+        for (unsigned t = 0; t < half; t++) {
+            const size_t b = t * per, e = std::min(bytes, b + per);
+            if (b < e) sl.emplace_back((a ? dy : dx) + b, (a ? sy : sx) + b, e - b);
+        }
+    ctx->copy_pool->run(sl);
+}
+
+// Copies host x/y[0, n) to device dx/dy; after chunk c is enqueued, on_chunk(c, first, count,
+// arrival event) runs (it may make ctx->stream wait on the event and launch work on the chunk).
+// On return ctx->stream is ordered after every chunk's DMA.
+template <typename F>
+int host_stage(geohip_ctx* ctx, const double* x, const double* y, uint64_t n, double* dx, double* dy, F&& on_chunk) {
+    int rc = stage_init(ctx);
+    if (rc) return rc;
+    const uint64_t nch = (n + kStagePts - 1) / kStagePts;
+    for (uint64_t c = 0; c < nch; c++) {
+        const int slot = (int)(c & 1);
+        const uint64_t b = c * kStagePts, m = std::min<uint64_t>(kStagePts, n - b);
+        if (ctx->stg_used[slot]) HIPCHK(hipEventSynchronize(ctx->stg_ev[slot]));  // slot's last DMA done
+        char* sp = ctx->stg[slot];
+        stage_copy(ctx, sp, reinterpret_cast<const char*>(x + b), sp + kStagePts * 8, reinterpret_cast<const char*>(y + b),
+                   m * 8);
+        HIPCHK(hipMemcpyAsync(dx + b, sp, m * 8, hipMemcpyHostToDevice, ctx->cstream));
+        HIPCHK(hipMemcpyAsync(dy + b, sp + kStagePts * 8, m * 8, hipMemcpyHostToDevice, ctx->cstream));
+        HIPCHK(hipEventRecord(ctx->stg_ev[slot], ctx->cstream));
+        ctx->stg_used[slot] = true;
+        rc = on_chunk(c, b, m, ctx->stg_ev[slot]);
+        if (rc) return rc;
+    }
+    for (int k = 0; k < 2; k++)
+        if (ctx->stg_used[k]) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->stg_ev[k], 0));
+    return GEOHIP_OK;
+}
+
 int stage_xy(geohip_ctx* ctx, const double* x, const double* y, uint64_t n, Slot sx, Slot sy,
              const double** dx, const double** dy) {
     if (n == 0) {
@@ -153,8 +284,17 @@ int stage_xy(geohip_ctx* ctx, const double* x, const double* y, uint64_t n, Slot
     int rc = ensure(ctx, sx, n * 8);
     if (!rc) rc = ensure(ctx, sy, n * 8);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(ctx->buf[sx], x, n * 8, hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(hipMemcpyAsync(ctx->buf[sy], y, n * 8, hipMemcpyHostToDevice, ctx->stream));
+    // the device buffers may still be read by work queued earlier on ctx->stream (the copy
+    // stream does not follow it): order the copies after it
+    hipEvent_t prior = nullptr;
+    HIPCHK(hipEventCreateWithFlags(&prior, hipEventDisableTiming));
+    hipError_t e = hipEventRecord(prior, ctx->stream);
+    if (e == hipSuccess) e = stage_init(ctx) ? hipErrorUnknown : hipStreamWaitEvent(ctx->cstream, prior, 0);
+    hipEventDestroy(prior);
+    if (e != hipSuccess) return hip_fail(ctx, e, "staging order");
+    rc = host_stage(ctx, x, y, n, B<double>(ctx, sx), B<double>(ctx, sy),
+                    [](uint64_t, uint64_t, uint64_t, hipEvent_t) { return GEOHIP_OK; });
+    if (rc) return rc;
     *dx = B<double>(ctx, sx);
     *dy = B<double>(ctx, sy);
     return GEOHIP_OK;
@@ -249,6 +389,72 @@ int knn_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const
                                    B<unsigned long long>(ctx, S_SPILL_D), B<unsigned>(ctx, S_SPILL_I),
                                    B<unsigned>(ctx, S_SPILL_CNT), out_d, out_i, out_cnt, ctx->stream, e0, e1);
     if (e != hipSuccess) return hip_fail(ctx, e, "knn launch");
+    return GEOHIP_OK;
+}
+
+// kNN of a host window staged in chunks (GEOHIP_MEM_HOST, >= 2 chunks): each chunk's pass
+// starts as soon as its DMA has landed (overlapping the copies of the later chunks), the chunk
+// lists are rebased to window indices and merged -- the k smallest of the union of per-chunk k
+// smallest is the window's k smallest (PointPointKNNQuery.java:125-191's windowAll merge).
+int knn_host_pipelined(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
+                       double qx, double qy, double r, uint32_t k, double* out_d, unsigned* out_i, unsigned* out_cnt,
+                       bool* done) {
+    *done = false;
+    const uint64_t nch = (n + kStagePts - 1) / kStagePts;
+    if (ctx->mem != GEOHIP_MEM_HOST || nch < 2 || n >= 0xffffffffull || k == 0 || k > GEOHIP_KNN_MAX_K ||
+        (k > 256 && nch * k > 8192) || nch > 4096)
+        return GEOHIP_OK;  // the one-pass path
+    if (!x || !y) return fail(ctx, GEOHIP_ERR_ARG, "null coordinate array");
+    PointPlan plan;
+    int rc = plan_or_fail(ctx, grid, qx, qy, r, &plan);
+    if (rc) return rc;
+    KnnArgs a = make_knn_args(plan, k, qx, qy);
+    unsigned nb = 0;
+    uint64_t chp = 0;
+    knn_pass_geometry(kStagePts, &nb, &chp);
+    const size_t ents = knn_pass_list_entries(nb ? nb : 1);
+    rc = ensure(ctx, S_X, n * 8);
+    if (!rc) rc = ensure(ctx, S_Y, n * 8);
+    if (!rc) rc = ensure(ctx, S_PART_D, ents * 8);
+    if (!rc) rc = ensure(ctx, S_PART_I, ents * 4);
+    if (!rc) rc = ensure(ctx, S_SPILL_D, kStagePts * 8);
+    if (!rc) rc = ensure(ctx, S_SPILL_I, kStagePts * 4);
+    if (!rc) rc = ensure_zeroed(ctx, S_SPILL_CNT, kKnnCounterBytes);
+    if (!rc) rc = ensure(ctx, S_QX, nch * k * 8);   // chunk lists (distance bits)
+    if (!rc) rc = ensure(ctx, S_QY, nch * k * 4);   // chunk lists (indices)
+    if (!rc) rc = ensure(ctx, S_UCNT, nch * 4);     // chunk list counts
+    if (!rc) rc = stage_init(ctx);
+    if (rc) return rc;
+    hipEvent_t prior = nullptr;
+    HIPCHK(hipEventCreateWithFlags(&prior, hipEventDisableTiming));
+    hipError_t e = hipEventRecord(prior, ctx->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(ctx->cstream, prior, 0);
+    hipEventDestroy(prior);
+    if (e != hipSuccess) return hip_fail(ctx, e, "staging order");
+    double* dx = B<double>(ctx, S_X);
+    double* dy = B<double>(ctx, S_Y);
+    double* ld = B<double>(ctx, S_QX);
+    unsigned* li = B<unsigned>(ctx, S_QY);
+    unsigned* lc = B<unsigned>(ctx, S_UCNT);
+    hipEvent_t e0, e1;
+    timing_events(ctx, &e0, &e1);  // timed: the first chunk's pass to the merge
+    rc = host_stage(ctx, x, y, n, dx, dy, [&](uint64_t c, uint64_t b, uint64_t m, hipEvent_t ev) -> int {
+        HIPCHK(hipStreamWaitEvent(ctx->stream, ev, 0));
+        hipError_t le = launch_knn_pass(dx + b, dy + b, m, a, B<unsigned long long>(ctx, S_PART_D),
+                                        B<unsigned>(ctx, S_PART_I), B<unsigned long long>(ctx, S_SPILL_D),
+                                        B<unsigned>(ctx, S_SPILL_I), B<unsigned>(ctx, S_SPILL_CNT), ld + c * k,
+                                        li + c * k, lc + c, ctx->stream, c == 0 ? e0 : nullptr, nullptr);
+        if (le != hipSuccess) return hip_fail(ctx, le, "knn chunk launch");
+        return GEOHIP_OK;
+    });
+    if (rc) return rc;
+    e = launch_knn_rebase(li, (unsigned)nch, k, kStagePts, ctx->stream);
+    if (e == hipSuccess)
+        e = launch_knn_merge(reinterpret_cast<const unsigned long long*>(ld), li, (unsigned)nch, k, k, out_d, out_i,
+                             out_cnt, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "knn merge launch");
+    if (e1) HIPCHK(hipEventRecord(e1, ctx->stream));
+    *done = true;
     return GEOHIP_OK;
 }
 
@@ -387,6 +593,12 @@ int geohip_ctx_destroy(geohip_ctx* ctx) {
     }
     for (auto ev : ctx->pool) hipEventDestroy(ev);
     if (ctx->pinned) hipHostFree(ctx->pinned);
+    if (ctx->cstream) hipStreamSynchronize(ctx->cstream);
+    for (int k = 0; k < 2; k++) {
+        if (ctx->stg[k]) hipHostFree(ctx->stg[k]);
+        if (ctx->stg_ev[k]) hipEventDestroy(ctx->stg_ev[k]);
+    }
+    if (ctx->cstream) hipStreamDestroy(ctx->cstream);
     if (ctx->own) hipStreamDestroy(ctx->own);
     delete ctx;
     return GEOHIP_OK;
@@ -505,7 +717,9 @@ int geohip_knn_pp(geohip_ctx* ctx, const geohip_grid* grid, const double* x, con
     }
     rc = ensure(ctx, S_OUT_CNT, 8);
     if (rc) return rc;
-    rc = knn_enqueue(ctx, grid, x, y, n, qx, qy, r, k, od, oi, B<unsigned>(ctx, S_OUT_CNT));
+    bool done = false;
+    rc = knn_host_pipelined(ctx, grid, x, y, n, qx, qy, r, k, od, oi, B<unsigned>(ctx, S_OUT_CNT), &done);
+    if (!rc && !done) rc = knn_enqueue(ctx, grid, x, y, n, qx, qy, r, k, od, oi, B<unsigned>(ctx, S_OUT_CNT));
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(ctx->pinned, ctx->buf[S_OUT_CNT], 4, hipMemcpyDeviceToHost, ctx->stream));
     if (ctx->mem == GEOHIP_MEM_HOST) {

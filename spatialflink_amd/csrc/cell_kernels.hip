@@ -1008,7 +1008,11 @@ __global__ __launch_bounds__(kTB) void join_fused(JoinRun a) {
                 cy = (int32_t)(key - (unsigned)cx * nb);
             }
             const float ax = (float)(px - ox), ay = (float)(py - oy);
-            cnt += (unsigned long long)nall * (unsigned)__popcll(__ballot(valid));
+            // ALL queries pair every point of the chunk whose coordinates lie in the tile box: a
+            // NaN coordinate is keyed to cell 0 by the (int) cast yet has no distance <= r
+            // (the approximate join pairs it by cell alone)
+            const bool in_box = valid && (APPROX || (px == px && py == py));
+            cnt += (unsigned long long)nall * (unsigned)__popcll(__ballot(in_box));
             for (unsigned j = 0; j < npart; j += 2) {
                 unsigned long long m0, m1;
                 jpart_pair<APPROX>(a, lpr, lpb, lpq, j, cx, cy, ax, ay, px, py, valid, lo, hi, m0, m1);
@@ -1044,11 +1048,12 @@ __global__ __launch_bounds__(kTB) void join_fused(JoinRun a) {
                     cy = (int32_t)(key - (unsigned)cx * nb);
                 }
                 const float ax = (float)(px - ox), ay = (float)(py - oy);
-                const unsigned long long vm = __ballot(valid);
+                const bool in_box = valid && (APPROX || (px == px && py == py));
+                const unsigned long long vm = __ballot(in_box);
                 const unsigned vrank = lanes_below(vm), vcnt = (unsigned)__popcll(vm);
                 // the stage has room for 2 x 64 pairs at the top of every step (flushed above 384)
                 for (unsigned j = 0; j < nall; j++) {
-                    if (valid) st[sc + vrank] = make_uint2(pid, lall[j]);
+                    if (in_box) st[sc + vrank] = make_uint2(pid, lall[j]);
                     sc += vcnt;
                     if (sc > kJStage - 2 * kWave) jstage_flush<WRITE>(a, st, sc, pos);
                 }

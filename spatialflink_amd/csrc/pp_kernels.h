@@ -55,6 +55,8 @@ hipError_t launch_knn_pass(const double* x, const double* y, uint64_t n, const K
                            unsigned* ctr, double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st,
                            hipEvent_t ev0, hipEvent_t ev1, unsigned long long* trace = nullptr, int abl = 0,
                            const PassRangeIo* range = nullptr);
+// add chunk * chunk_pts to every valid index of nlists lists of k (host windows staged in chunks)
+hipError_t launch_knn_rebase(unsigned* idx, unsigned nlists, unsigned k, uint64_t chunk_pts, hipStream_t st);
 hipError_t launch_knn_merge(const unsigned long long* d, const unsigned* i, unsigned nlists, unsigned list_len,
                             unsigned k, double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st);
 // range: bitmask (16 words / 1024 pts), unit_count (units), offs (units) scratch.

@@ -1909,6 +1909,19 @@ __global__ __launch_bounds__(1024) void knn_merge_sort(const unsigned long long*
     if (threadIdx.x == 0) *out_count = outn;
 }
 
+// per-chunk kNN lists of a host window staged in chunks: window index = chunk * chunk_pts + local
+__global__ void knn_rebase(unsigned* __restrict__ idx, unsigned nlists, unsigned k, uint64_t chunk_pts) {
+    const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nlists * k) return;
+    const unsigned v = idx[t];
+    if (v != kSentinelI) idx[t] = v + (unsigned)((uint64_t)(t / k) * chunk_pts);
+}
+hipError_t launch_knn_rebase(unsigned* idx, unsigned nlists, unsigned k, uint64_t chunk_pts, hipStream_t st) {
+    const unsigned m = nlists * k;
+    if (m) knn_rebase<<<(m + 255) / 256, 256, 0, st>>>(idx, nlists, k, chunk_pts);
+    return hipGetLastError();
+}
+
 hipError_t launch_knn_merge(const unsigned long long* d, const unsigned* i, unsigned nlists, unsigned list_len,
                             unsigned k, double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st) {
     if (k > 256) {

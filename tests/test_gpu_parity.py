@@ -553,3 +553,25 @@ def test_binning_cell_boundaries(ctx):
         off, vx, vy = synth.star_polygons(40, 78, bbox=BJ, r_min=2 * l, r_max=6 * l)
         want = pairs_sorted(cref.range_ppoly(cg, xs, ys, off, vx, vy, l)).tolist()
         assert pairs_sorted(ctx.range_ppoly(ag, xs, ys, off, vx, vy, l)).tolist() == want
+
+
+def test_host_window_chunked_staging(ctx):
+    """Host (pageable) windows larger than one staging chunk (2^20 points): the kNN runs one pass
+    per chunk as its DMA lands, then rebases and merges the chunk lists; range and join read the
+    chunk-staged window.  NaN points and exact ties straddle chunk boundaries."""
+    ag, cg = agrid(100)
+    rng = np.random.default_rng(57)
+    n = 3 * (1 << 20) + 12345
+    x, y = _window(rng, n, nan_every=4099)
+    for b in (1 << 20, 2 << 20):  # query copies across both boundaries
+        x[b - 700:b + 700] = Q[0]
+        y[b - 700:b + 700] = Q[1]
+    for k in (1, 100, 1000):
+        wi, wd = cref.knn_pp(cg, x, y, Q[0], Q[1], 0.5, k)
+        oi, od = ctx.knn_pp(ag, x, y, Q[0], Q[1], 0.5, k)
+        assert oi.tolist() == wi.tolist() and np.array_equal(od.view(np.uint64), wd.view(np.uint64))
+    want = cref.range_pp(cg, x, y, Q[0], Q[1], 0.05)
+    assert ctx.range_pp(ag, x, y, Q[0], Q[1], 0.05).tolist() == want.tolist()
+    qx, qy = synth.uniform(200, 58)
+    want = pairs_sorted(cref.join_pp(cg, cg, x, y, qx, qy, 0.02)).tolist()
+    assert pairs_sorted(ctx.join_pp(ag, ag, x, y, qx, qy, 0.02)).tolist() == want
