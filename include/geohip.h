@@ -211,6 +211,27 @@ int geohip_band_pack_async(geohip_ctx* ctx, const geohip_grid* grid_data, int32_
                            const double* x, const double* y, uint64_t n, int64_t base, double* out_x,
                            double* out_y, int64_t* out_idx, uint64_t* out_counts_dev);
 
+/* ---- output codec ------------------------------------------------ */
+/* Serialization.PointToCSVTSVOutputSchema.serialize (spatialStreams/Serialization.java:98-152) for
+   m result points, as one text buffer: record j (point p = idx[j], or j when idx is NULL) is the
+   fields at positions 0..max(attr) -- objID (bytes oid_text[oid_off[p] .. oid_off[p+1]), or
+   "null" when oid_text is NULL), timeStampMillisec (Long.toString of ts[p], 0 when ts is NULL),
+   Double.toString(x[p]), Double.toString(y[p]) (JDK 8 FloatingDecimal), "0" at positions no
+   field names, a later attr winning a shared position -- each followed by delim, the last
+   character deleted, then '\n'.  rec_off (nullable, m + 1 entries) receives the record offsets.
+   Device memory only; *out_len (host) = the total bytes; GEOHIP_ERR_CAPACITY when above cap
+   (records that do not fit entirely are not written). */
+typedef struct geohip_csv_out_spec {
+    int32_t attr_oid, attr_ts, attr_x, attr_y; /* csvTsvSchemaAttr[0..3], each 0..63 */
+    int32_t delim_len;                         /* 1..8 */
+    char delim[8];
+    int32_t reserved;
+} geohip_csv_out_spec;
+int geohip_format_points_csv(geohip_ctx* ctx, const geohip_csv_out_spec* spec, const double* x,
+                             const double* y, const int64_t* ts, const uint8_t* oid_text,
+                             const uint64_t* oid_off, const uint32_t* idx, uint64_t m, uint8_t* out,
+                             uint64_t cap, uint64_t* out_len, uint64_t* rec_off);
+
 /* ---- ingest codec ---------------------------------------------- */
 /* A batch of '\n'-separated text records, as a Flink source hands them to the map functions of
    Deserialization.PointStream / TrajectoryStream (spatialStreams/Deserialization.java:47-80),

@@ -73,6 +73,19 @@ def make_ingest_spec(fmt: int, delimiter: str = ",", attr_x: int = 0, attr_y: in
     return IngestSpec(fmt, d[0], attr_x, attr_y, attr_ts, 0)
 
 
+class CsvOutSpec(ctypes.Structure):
+    """geohip_csv_out_spec: csvTsvSchemaAttr positions of objID, ts, x, y and the delimiter."""
+    _fields_ = [("attr_oid", c_int32), ("attr_ts", c_int32), ("attr_x", c_int32), ("attr_y", c_int32),
+                ("delim_len", c_int32), ("delim", ctypes.c_char * 8), ("reserved", c_int32)]
+
+
+def make_csv_out_spec(attrs=(0, 1, 2, 3), delimiter: str = ",") -> CsvOutSpec:
+    d = delimiter.encode()
+    if not 1 <= len(d) <= 8:
+        raise GeohipUnsupportedError("delimiter must be 1..8 bytes")
+    return CsvOutSpec(attrs[0], attrs[1], attrs[2], attrs[3], len(d), d, 0)
+
+
 class Rect(ctypes.Structure):
     _fields_ = [("x0", c_int32), ("x1", c_int32), ("y0", c_int32), ("y1", c_int32)]
 
@@ -113,6 +126,8 @@ _SIGS = {
     "geohip_knn_pp_async": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_double, c_double, c_double, c_uint32,
                                     _P, _P, _P]),
     "geohip_knn_merge_async": (c_int, [_P, _P, _P, c_uint32, c_uint32, c_uint32, _P, _P, _P]),
+    "geohip_format_points_csv": (c_int, [_P, POINTER(CsvOutSpec), _P, _P, _P, _P, _P, _P, c_uint64, _P, c_uint64,
+                                         POINTER(c_uint64), _P]),
     "geohip_band_pack_async": (c_int, [_P, POINTER(Grid), c_int32, c_uint32, _P, _P, c_uint64, ctypes.c_int64, _P, _P,
                                        _P, _P]),
     "geohip_knn_range_pp": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_double, c_double, c_double, c_uint32,
@@ -449,6 +464,42 @@ class Context:
                                         out_idx.data_ptr(), out_dist.data_ptr(), out_count.data_ptr())
         if rc:
             self._check(rc, "knn_merge_async")
+
+    def format_points_csv(self, spec: CsvOutSpec, x, y, ts=None, oid_text=None, oid_off=None, idx=None, cap=None):
+        """geohip_format_points_csv (Serialization.PointToCSVTSVOutputSchema over result points):
+        device tensors in (x, y float64; ts int64; oid_text uint8 + oid_off int64 [n + 1]; idx
+        int32 record -> point), -> (text uint8 device tensor, record offsets int64 [m + 1])."""
+        import torch
+        self._dev(x, "x")
+        self._dev(y, "y")
+        if ts is not None:
+            self._dev(ts, "ts", "int64")
+        if (oid_text is None) != (oid_off is None):
+            raise GeohipArgumentError("oid_text and oid_off go together")
+        if oid_text is not None:
+            self._dev(oid_text, "oid_text", "uint8")
+            self._dev(oid_off, "oid_off", "int64")
+        if idx is not None:
+            self._dev(idx, "idx", "int32")
+        m = idx.numel() if idx is not None else x.numel()
+        if self._mem != MEM_DEVICE:
+            self.set_mem(MEM_DEVICE)
+        off = torch.empty(m + 1, dtype=torch.int64, device=x.device)
+        n = c_uint64(0)
+        ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+        if cap is None:  # size pass
+            rc = lib.geohip_format_points_csv(self.h, ctypes.byref(spec), x.data_ptr(), y.data_ptr(), ptr(ts),
+                                              ptr(oid_text), ptr(oid_off), ptr(idx), m, None, 0, ctypes.byref(n),
+                                              off.data_ptr())
+            if rc not in (OK, ERR_CAPACITY):
+                self._check(rc, "format_points_csv")
+            cap = n.value
+        out = torch.empty(max(cap, 1), dtype=torch.uint8, device=x.device)
+        rc = lib.geohip_format_points_csv(self.h, ctypes.byref(spec), x.data_ptr(), y.data_ptr(), ptr(ts),
+                                          ptr(oid_text), ptr(oid_off), ptr(idx), m, out.data_ptr(), cap,
+                                          ctypes.byref(n), off.data_ptr())
+        self._check(rc, "format_points_csv")
+        return out[:n.value], off
 
     def band_pack_async(self, grid_data: Grid, nb: int, world: int, x, y, base: int = 0):
         """geohip_band_pack_async: this shard's valid-key points grouped by key-band owner rank

@@ -32,6 +32,7 @@ SOURCES = {
     "cell_kernels.hip": ["-x", "hip", f"--offload-arch={ARCH}"],
     "ingest.hip": ["-x", "hip", f"--offload-arch={ARCH}"],
     "band.hip": ["-x", "hip", f"--offload-arch={ARCH}"],
+    "format.hip": ["-x", "hip", f"--offload-arch={ARCH}"],
 }
 
 

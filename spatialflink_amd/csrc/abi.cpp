@@ -741,6 +741,14 @@ int geohip_knn_pp_async(geohip_ctx* ctx, const geohip_grid* grid, const double* 
     return knn_enqueue(ctx, grid, x, y, n, qx, qy, r, k, out_dist, out_idx, out_count_dev);
 }
 
+int geohip_format_points_csv(geohip_ctx* ctx, const geohip_csv_out_spec* spec, const double* x, const double* y,
+                             const int64_t* ts, const uint8_t* oid_text, const uint64_t* oid_off, const uint32_t* idx,
+                             uint64_t m, uint8_t* out, uint64_t cap, uint64_t* out_len, uint64_t* rec_off) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    return format_csv_impl(ctx, spec, x, y, ts, oid_text, oid_off, idx, m, out, cap, out_len, rec_off);
+}
+
 int geohip_band_pack_async(geohip_ctx* ctx, const geohip_grid* grid_data, int32_t nb, uint32_t world,
                            const double* x, const double* y, uint64_t n, int64_t base, double* out_x,
                            double* out_y, int64_t* out_idx, uint64_t* out_counts_dev) {

@@ -30,4 +30,8 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* grid_data, const geohip_gri
 int band_pack_impl(geohip_ctx* ctx, const geohip_grid* grid, int32_t nb, uint32_t world, const double* x,
                    const double* y, uint64_t n, int64_t base, double* out_x, double* out_y, int64_t* out_idx,
                    uint64_t* out_counts);
+// point CSV/TSV output codec (format.hip; geohip_format_points_csv)
+int format_csv_impl(geohip_ctx* ctx, const geohip_csv_out_spec* spec, const double* x, const double* y,
+                    const int64_t* ts, const uint8_t* oid_text, const uint64_t* oid_off, const uint32_t* idx,
+                    uint64_t m, uint8_t* out, uint64_t cap, uint64_t* out_len, uint64_t* rec_off);
 }  // namespace geohip
