@@ -44,6 +44,9 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "points/sec (whole node) for windowed range/kNN/join at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# FP64 vector peak: half the FP32 vector rate of MI355X_MICROARCH.md (157.3 TFLOP/s; a wave64
+# FP64 FMA issues over 4 cycles on the SIMD-32 units), 78.6 TFLOP/s
+FP64_PEAK_TFLOPS = 78.6
 BYTES_PER_POINT = 16  # algorithmic: x + y fp64 read once
 
 
@@ -77,12 +80,13 @@ def _timed_loop(fn, seconds, max_iter):
     return i, t_total
 
 
-def pmc_traffic(kernel_tag: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/pmc_<tag>.json)."""
+def pmc_traffic(kernel_tag: str, key: str = "hbm_bytes_per_launch"):
+    """Per-launch value from the committed rocprofv3 PMC passes (profiles/pmc_<tag>.json): HBM
+    bytes (FETCH_SIZE x 2 + WRITE_SIZE) or FP64 FLOPs (SQ_INSTS_VALU_FLOPS_FP64)."""
     f = ROOT / "profiles" / f"pmc_{kernel_tag}.json"
     if f.exists():
         try:
-            return json.loads(f.read_text()).get("hbm_bytes_per_launch")
+            return json.loads(f.read_text()).get(key)
         except Exception:
             return None
     return None
@@ -366,7 +370,8 @@ class PpolyWorkload(Workload):
     """C4 (BASELINE.json configs[3]): 1k star polygons (50 vertices) over 50M uniform points per
     window, 500x500, r = 0.005 (conf/geoflink-conf.yml:52)."""
     tag = "ppoly_probe"
-    kernel = "geohip::ppoly_eval + ppoly_emit (tile binning before the timed region)"
+    kernel = ("geohip point-polygon step: tile binning (cells of no polygon dropped) + ppoly_eval + ppoly_emit; "
+              "the whole device step is timed")
     grid_n, radius, n_default, npoly = 500, 0.005, 50_000_000, 1000
     windows = 2
 
@@ -425,7 +430,8 @@ class PpJoinWorkload(PpolyWorkload):
     """the C4 shape as a point-polygon join (PointPolygonJoinQuery,
     polygon stream replicated to its G/C cells, every candidate distance-checked)."""
     tag = "ppjoin"
-    kernel = "geohip::ppoly_eval + ppoly_emit in join mode (tile binning before the timed region)"
+    kernel = ("geohip point-polygon join step: tile binning + ppoly_eval + ppoly_emit in join mode; "
+              "the whole device step is timed")
 
     def __init__(self, *a):
         Workload.__init__(self, *a)
@@ -532,7 +538,7 @@ class PpolyIncrWorkload(PpolyWorkload):
     once against the 1k polygons, the window's pairs assembled from its two panes
     (spatialflink_amd.incremental.IncrementalPPolyRange).  value = stream points/sec."""
     tag = "ppoly_incr"
-    kernel = "geohip::ppoly_eval + ppoly_emit on one pane (tile binning before the timed region)"
+    kernel = "geohip point-polygon step on one pane (binning + ppoly_eval + ppoly_emit, timed)"
     n_default = 25_000_000
     windows = 4
 
@@ -789,6 +795,13 @@ def main():
                      "algorithmic_bytes_per_launch": abytes, **wl.roofline_extra()},
         "cpu_baseline": None,
     }
+    flops = pmc_traffic(wl.tag, "fp64_flops_per_launch")
+    if flops and avg_s > 0:  # the point-polygon steps are FP64-VALU bound (crossings, distances)
+        tf = flops / avg_s / 1e12
+        result["roofline_fp64"] = {"bound": "fp64", "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                   "frac": tf / FP64_PEAK_TFLOPS, "flops": flops,
+                                   "source": "rocprofv3 SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes of the timed kernels per step "
+                                             "(profiles/pmc_" + wl.tag + ".json) / the live average step time"}
     if rank == 0 and world == 1 and not args.no_e2e:
         e2e = wl.e2e()
         if e2e is not None:

@@ -2961,6 +2961,9 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
         pc->dev_blob = pblob;
         pc->blob_bytes = blob_end;
     }
+    hipEvent_t e0, e1;
+    ctx_timing_events(ctx, &e0, &e1);
+    if (e0) hipEventRecord(e0, st);  // the whole device step: binning, mask sizing, count and write passes
     TileBins tb;
     unsigned* oidx = nullptr;
     unsigned n_out = 0;
@@ -3010,9 +3013,6 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     osink.slot0 = nwork;
     const int r_is_max = r >= 1.7976931348623157e308;
     if (hipMemsetAsync(bcount, 0, (nslots + 1) * 8, st) != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
-    hipEvent_t e0, e1;
-    ctx_timing_events(ctx, &e0, &e1);
-    if (e0) hipEventRecord(e0, st);
     // count pass: hit masks + per-work-item counts; out-of-grid points counted separately
     if (nwork) {
         if (approximate)
