@@ -29,6 +29,8 @@ for w in range(W):
     ys.append(y)
 torch.cuda.synchronize()
 names = ["start", "stream_end", "flush", "drained", "arrived"] + (["lookback", "emitted"] if ABL < 0 else [])
+blk = {"hist": 8, "listed": 9, "heads": 10}
+fin = {"acquired": 5, "loaded": 11, "T": 12, "taken": 13, "gathered": 6, "written": 7}
 out = {}
 for rep in range(4):
     for w in range(W):  # warm the path, cycle windows
@@ -36,10 +38,10 @@ for rep in range(4):
     tr = ctx.debug_knn_pass_trace(grid, xs[rep % W], ys[rep % W], q[0], q[1], R, K, ABL).astype(np.int64)
     t0 = tr[:, 0].min()
     rel = (tr - t0) / 100.0
-    cols = [0, 1, 2, 3, 4, 5, 6]
-    row = {nm: [round(float(np.percentile(rel[:, cols[j]], p)), 2) for p in (0, 10, 50, 90, 100)] for j, nm in enumerate(names)}
+    row = {nm: [round(float(np.percentile(rel[:, j], p)), 2) for p in (0, 10, 50, 90, 100)] for j, nm in enumerate(names)}
+    row["block_median"] = {nm: round(float(np.median(rel[:, j])), 2) for nm, j in blk.items()}
     last = int(np.argmax(tr[:, 7]))
-    row["final"] = {nm: round(float(rel[last, j]), 2) for nm, j in (("acquired", 5), ("gathered", 6), ("written", 7))}
+    row["final"] = {nm: round(float(rel[last, j]), 2) for nm, j in fin.items()}
     row["last_block"] = last
     row["stats"] = ctx.debug_knn_pass_stats()
     out[f"rep{rep}"] = row

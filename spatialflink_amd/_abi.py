@@ -704,14 +704,14 @@ class Context:
 
     def debug_knn_pass_trace(self, grid, x, y, qx, qy, r, k, ablation=0):
         """One traced kNN pass on device x/y: [nblocks, 8] timestamps (100 MHz, 0 = not reached)."""
-        buf = np.zeros(8 * 1024, dtype=np.uint64)
+        buf = np.zeros(16 * 1024, dtype=np.uint64)
         nb = c_uint32(0)
         self._dev(x, "x")
         self.set_mem(MEM_DEVICE)
         rc = lib.geohip_debug_knn_pass_trace(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), x.numel(), qx, qy, r, k,
                                              ablation, buf.ctypes.data_as(c_void_p), len(buf), ctypes.byref(nb))
         self._check(rc, "debug_knn_pass_trace")
-        return buf[:8 * nb.value].reshape(nb.value, 8)
+        return buf[:16 * nb.value].reshape(nb.value, 16)
 
     def selftest_fp64(self, a, b):
         """Device fp64 primitive bits (test hook): returns (sqrt|a|, a/b, hypot(a,b), a*b-b*b)."""

@@ -961,7 +961,7 @@ int geohip_debug_knn_pass_stats(geohip_ctx* ctx, uint32_t* out3) {
 }
 
 // Measurement hook: one kNN pass (device memory) with per-block phase timestamps (100 MHz):
-// host[8 b + s], s = start, stream end, flush, stores drained, arrived; the last block also
+// host[16 b + s], s = start, stream end, flush, stores drained, arrived; the last block also
 // acquired, gathered, written.  *nblocks = blocks of the launch.
 int geohip_debug_knn_pass_trace(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
                                 uint64_t n, double qx, double qy, double r, uint32_t k, int ablation, uint64_t* host,
@@ -977,7 +977,7 @@ int geohip_debug_knn_pass_trace(geohip_ctx* ctx, const geohip_grid* grid, const 
     unsigned nb = 0;
     uint64_t ch = 0;
     knn_pass_geometry(n, &nb, &ch);
-    if (cap_words < 8ull * nb) return fail(ctx, GEOHIP_ERR_CAPACITY, "trace buffer too small");
+    if (cap_words < 16ull * nb) return fail(ctx, GEOHIP_ERR_CAPACITY, "trace buffer too small");
     const size_t ents = knn_pass_list_entries(nb ? nb : 1);
     rc = ensure(ctx, S_PART_D, ents * 8);
     if (!rc) rc = ensure(ctx, S_PART_I, ents * 4);
@@ -987,10 +987,10 @@ int geohip_debug_knn_pass_trace(geohip_ctx* ctx, const geohip_grid* grid, const 
     if (!rc) rc = ensure(ctx, S_OUT_D, (size_t)k * 8);
     if (!rc) rc = ensure(ctx, S_OUT_I, (size_t)k * 4);
     if (!rc) rc = ensure(ctx, S_OUT_CNT, 8);
-    if (!rc) rc = ensure(ctx, S_TRACE, 8ull * nb * 8);
+    if (!rc) rc = ensure(ctx, S_TRACE, 16ull * nb * 8);
     if (rc) return rc;
     unsigned long long* tr = B<unsigned long long>(ctx, S_TRACE);
-    HIPCHK(hipMemsetAsync(tr, 0, 8ull * nb * 8, ctx->stream));
+    HIPCHK(hipMemsetAsync(tr, 0, 16ull * nb * 8, ctx->stream));
     PassRangeIo rio;
     memset(&rio, 0, sizeof rio);
     if (with_range) {
@@ -1014,7 +1014,7 @@ int geohip_debug_knn_pass_trace(geohip_ctx* ctx, const geohip_grid* grid, const 
                                    with_range ? &rio : nullptr);
     if (e != hipSuccess) return hip_fail(ctx, e, "knn pass launch");
     HIPCHK(hipStreamSynchronize(ctx->stream));
-    HIPCHK(hipMemcpy(host, tr, 8ull * nb * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(host, tr, 16ull * nb * 8, hipMemcpyDeviceToHost));
     *nblocks = nb;
     return GEOHIP_OK;
 }

@@ -159,6 +159,49 @@ __device__ __forceinline__ int hist_kth_bin(const unsigned* hist, unsigned k) {
     return __builtin_amdgcn_readlane(bin, first);
 }
 
+// One wave, one scan: the crossing bins of two counts (as hist_kth_bin).
+__device__ __forceinline__ void hist_kth_bins2(const unsigned* hist, unsigned k1, unsigned k2, int& b1, int& b2) {
+    const int lane = lane_id();
+    unsigned c[8];
+    unsigned tot = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        c[j] = hist[lane * 8 + j];
+        tot += c[j];
+    }
+    const unsigned incl = wave_incl_scan(tot);
+    auto cross = [&](unsigned kk) -> int {
+        const unsigned long long m = __ballot(incl >= kk);
+        if (m == 0) return -1;
+        int bin = kHistBins - 1;
+        unsigned run = incl - tot;
+        bool found = false;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            run += c[j];
+            if (!found && run >= kk) { bin = lane * 8 + j; found = true; }
+        }
+        return __builtin_amdgcn_readlane(bin, __builtin_ctzll(m));
+    };
+    b1 = cross(k1);
+    b2 = cross(k2);
+}
+
+// rank of this lane's (d, i) key among the keys of the lanes in `mask` (keys unique: indices are)
+__device__ __forceinline__ unsigned wave_rank_in(unsigned long long mask, unsigned long long d, unsigned i) {
+    unsigned r = 0;
+    while (mask) {
+        const int j = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)d, j);
+        const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(d >> 32), j);
+        const unsigned ij = (unsigned)__builtin_amdgcn_readlane((int)i, j);
+        const unsigned long long dj = ((unsigned long long)hi << 32) | lo;
+        r += (dj < d || (dj == d && ij < i)) ? 1u : 0u;
+    }
+    return r;
+}
+
 // upper edge (distance bits) of histogram bin `bin`
 __device__ __forceinline__ unsigned long long hist_edge(int bin, int base) {
     return ((unsigned long long)(bin + base + 1) << 48) - 1ull;
@@ -686,7 +729,7 @@ struct PassIo {
 };
 #define PASS_TRACE(io, slot)                                                                      \
     do {                                                                                          \
-        if ((io).trace && threadIdx.x == 0) (io).trace[8 * (size_t)blockIdx.x + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+        if ((io).trace && threadIdx.x == 0) (io).trace[16 * (size_t)blockIdx.x + (slot)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 
 // exact distances of up to 64 staged candidates; survivors (<= the block bound) appended to the
@@ -812,6 +855,7 @@ __device__ __forceinline__ void pass_final(const PassIo& io, const KnnArgs& a, u
         sh[3] = 0;            // whole lists
     }
     __syncthreads();
+    PASS_TRACE(io, 11);
     // ---- B
 #pragma unroll
     for (unsigned u = 0; u < kPer; u++)
@@ -827,6 +871,7 @@ __device__ __forceinline__ void pass_final(const PassIo& io, const KnnArgs& a, u
         if (lane == 0 && bin >= 0 && bin < kHistBins - 1) sh[0] = (unsigned)bin;
     }
     __syncthreads();
+    PASS_TRACE(io, 12);
     const unsigned long long T = sh[0] != 0xffffffffu ? hist_edge((int)sh[0], a.hist_base) : kSentinelD;
     // ---- D
     auto take = [&](bool ok, unsigned long long d, unsigned i) {
@@ -858,6 +903,7 @@ __device__ __forceinline__ void pass_final(const PassIo& io, const KnnArgs& a, u
         take(part, hd[u], hi[u]);
     }
     __syncthreads();
+    PASS_TRACE(io, 13);
     const unsigned nwhole = sh[3];
     for (unsigned w = (unsigned)wid; w < nwhole; w += NT / kWave) {  // one wave per whole list
         const unsigned b = wl[w];
@@ -1053,7 +1099,7 @@ __device__ __forceinline__ void pass_range_emit(const PassRangeIo& rio, const un
         for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
         if (lane == 0) excl_sh = pre;
     }
-    if (rio.trace && threadIdx.x == 0) rio.trace[8 * (size_t)blockIdx.x + 5] = __builtin_amdgcn_s_memrealtime();
+    if (rio.trace && threadIdx.x == 0) rio.trace[16 * (size_t)blockIdx.x + 5] = __builtin_amdgcn_s_memrealtime();
     // per-wave word runs and their hit counts (prefix over waves)
     const unsigned wpw = (nw + NW - 1) / NW;
     const unsigned wb = (unsigned)wid * wpw;
@@ -1087,7 +1133,7 @@ __device__ __forceinline__ void pass_range_emit(const PassRangeIo& rio, const un
         obase += (unsigned)__builtin_amdgcn_readlane((int)incl, kWave - 1);
     }
     if (threadIdx.x == 0 && vb == gridDim.x - 1) *rio.total = excl_sh + bcount;
-    if (rio.trace && threadIdx.x == 0) rio.trace[8 * (size_t)blockIdx.x + 6] = __builtin_amdgcn_s_memrealtime();
+    if (rio.trace && threadIdx.x == 0) rio.trace[16 * (size_t)blockIdx.x + 6] = __builtin_amdgcn_s_memrealtime();
 }
 
 // The range query of the same point, fused into the kNN pass (C5: kNN k + range r of one query):
@@ -1135,7 +1181,18 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
     }
     PASS_TRACE(io, 0);
     const unsigned k = args.k;
-    const unsigned niters = (unsigned)((blk_end - blk_begin + kPtsIter - 1) / kPtsIter);
+    // Iteration order.  kNN alone: the block's iterations interleave with every other block's
+    // (global iteration it * nblocks + block), so the grid sweeps the window as one front and
+    // the blocks' stream ends bunch up (a chunk per block leaves a 4-7 us spread between the
+    // first and the last block, measured by the phase trace).  The fused range keeps a contiguous
+    // chunk per block (its hit bitmask covers the chunk).  ABL bit 4: chunks (measurement).
+    constexpr bool kInterleave = !RANGE && !(ABL & 16);
+    const uint64_t total_iters = (n + kPtsIter - 1) / kPtsIter;
+    const unsigned niters = kInterleave ? (unsigned)(blockIdx.x < total_iters
+                                                         ? (total_iters - blockIdx.x + gridDim.x - 1) / gridDim.x
+                                                         : 0)
+                                        : (unsigned)((blk_end - blk_begin + kPtsIter - 1) / kPtsIter);
+    if (kInterleave) blk_end = n;
     unsigned ccnt = 0;
     unsigned appended = 0, last_hist = 0;
     const Box b0 = args.u[0];
@@ -1212,7 +1269,9 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
     const std::integral_constant<bool, false> kPart;
     const bool all_valid[4] = {true, true, true, true};
     double ax[4], ay[4], bx[4], by[4];
-    auto it_base = [&](unsigned it) { return blk_begin + (uint64_t)it * kPtsIter; };
+    auto it_base = [&](unsigned it) {
+        return kInterleave ? ((uint64_t)it * gridDim.x + blockIdx.x) * kPtsIter : blk_begin + (uint64_t)it * kPtsIter;
+    };
     auto is_full = [&](unsigned it) { return it_base(it) + kPtsIter <= blk_end; };
     auto load_full = [&](unsigned it, double (&px)[4], double (&py)[4]) {
         const uint64_t i0 = it_base(it) + 2 * (uint64_t)lane;
@@ -1258,81 +1317,135 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
     }
     PASS_TRACE(io, 1);
     pass_dist_batch<PB, RANGE>(st, ccnt, kb, args, io, appended, true, rs);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // spilled survivors drained before the ticket
     __syncthreads();
     PASS_TRACE(io, 2);
     // the range hit count goes out first (later chunks wait for it); the hits themselves after
     // the kNN part, so the look-back wait never delays the kNN final
     if (RANGE) pass_range_publish<NW>(rio, rmask, rcount, vb, blk_begin, blk_end);
-    // ---- end of block: final local bound B (k-th bin edge) and H (4th bin edge); survivors <= B
-    // written unsorted to this block's list, those <= H (the block's smallest, usually 4-10)
-    // sorted by one wave: its 4 smallest are the block's heads.  A list whose heads may be
-    // incomplete (spilled survivors counted in the histogram, > 64 entries <= H) is flagged in
-    // its length word so the final reads it whole.
-    if (wid == 0) {
-        if (!(ABL & 4) && kb.cnt >= k) hist_bound(kb, k, args.hist_base);
-        const int hb = hist_kth_bin(kb.hist, kPassHeads);
-        if (lane == 0) kb.hcap = hb >= 0 && hb < kHistBins - 1 ? hist_edge(hb, args.hist_base) : kSentinelD;
-    }
-    __syncthreads();
-    const unsigned long long B = kb.bound;
-    const unsigned long long H = kb.hcap < B ? kb.hcap : B;
-    const unsigned have = kb.cnt < (unsigned)PB::kCap ? kb.cnt : (unsigned)PB::kCap;
+    // ---- end of block: B (k-th bin edge) and H (kPassHeads-th bin edge) from one scan of the
+    // survivor histogram; survivors <= B written unsorted to this block's list; those <= H (the
+    // block's smallest, usually 8-12) placed by rank: the kPassHeads smallest are the block's
+    // heads, in order.  A list whose heads may be incomplete (spilled survivors counted in the
+    // histogram, > 64 entries <= H) is flagged in its length word so the final reads it whole.
+    // Then the arrival (cdna_hip_programming.md §6 Guideline 16, counter form): the storing wave
+    // drains its write-through stores and takes the ticket.  Common case (<= 64 survivors): wave
+    // 0 alone, in registers, behind no further barrier; else every wave through LDS.
+    const unsigned have = kb.cnt < (unsigned)PB::kCap ? kb.cnt : (unsigned)PB::kCap;  // block-uniform
     const size_t lbase = (size_t)blockIdx.x * io.list_cap;
-    for (unsigned t0 = 0; t0 < have; t0 += NT) {
-        const unsigned t = t0 + threadIdx.x;
-        unsigned long long d = kSentinelD;
-        unsigned i = kSentinelI;
-        if (t < have) {
-            d = kb.bd[t];
-            i = kb.bi[t];
+    auto bounds = [&](unsigned long long& Bv, unsigned long long& Hv) {  // wave 0
+        int bb, hb;
+        hist_kth_bins2(kb.hist, k, kPassHeads, bb, hb);
+        Bv = kb.bound;
+        if (!(ABL & 4) && kb.cnt >= k && bb >= 0 && bb < kHistBins - 1) {
+            const unsigned long long e = hist_edge(bb, args.hist_base);
+            if (e < Bv) Bv = e;
         }
-        const bool keep = d <= B && t < have;
-        const unsigned long long m = __ballot(keep);
-        unsigned wb = 0;
-        if (lane == 0 && m) wb = atomicAdd(&kb.cursor, (unsigned)__popcll(m));
-        wb = __shfl(wb, 0);
-        if (keep && !(ABL & 1)) {
-            const unsigned p = wb + lanes_below(m);
-            store_wt(&io.list_d[lbase + p], d);
-            store_wt(&io.list_i[lbase + p], i);
+        Hv = hb >= 0 && hb < kHistBins - 1 ? hist_edge(hb, args.hist_base) : kSentinelD;
+        if (Hv > Bv) Hv = Bv;
+    };
+    // heads of the ns entries <= H held by the lanes of `ms` (wave 0), then the list length
+    auto heads = [&](unsigned long long ms, unsigned long long d, unsigned i, unsigned ns, unsigned listed) {
+        const bool small = (ms >> lane) & 1ull;
+        const unsigned r = wave_rank_in(ms, d, i);
+        if (small && r < kPassHeads) {
+            store_wt(&io.head_d[kPassHeads * blockIdx.x + r], d);
+            store_wt(&io.head_i[kPassHeads * blockIdx.x + r], i);
         }
-        const bool small = keep && d <= H;
-        const unsigned long long ms = __ballot(small);
-        unsigned sb = 0;
-        if (lane == 0 && ms) sb = atomicAdd(&kb.nsmall, (unsigned)__popcll(ms));
-        sb = __shfl(sb, 0);
-        if (small) {
-            const unsigned p = sb + lanes_below(ms);
-            if (p < (unsigned)kWave) {
-                kb.top_d[p] = d;
-                kb.top_i[p] = i;
+        if ((unsigned)lane >= ns && (unsigned)lane < kPassHeads) {
+            store_wt(&io.head_d[kPassHeads * blockIdx.x + lane], kSentinelD);
+            store_wt(&io.head_i[kPassHeads * blockIdx.x + lane], kSentinelI);
+        }
+        // heads complete: every list entry <= H is among the ranked ones, and either kPassHeads
+        // of them exist or the list holds nothing else
+        const bool complete = ns <= (unsigned)kWave && (ns >= kPassHeads || ns == listed);
+        if (lane == 0) store_wt(&io.len[blockIdx.x], listed | (complete ? 0u : kLenWhole));
+        PASS_TRACE(io, 10);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        PASS_TRACE(io, 3);
+        if (lane == 0) kb.last = pass_arrive_last(io.ctr + kTicketStride, io.groups) ? 1u : 0u;
+    };
+    if (have <= (unsigned)kWave) {
+        if (wid == 0) {
+            unsigned long long Bv, Hv;
+            bounds(Bv, Hv);
+            PASS_TRACE(io, 8);
+            unsigned long long d = kSentinelD;
+            unsigned i = kSentinelI;
+            if ((unsigned)lane < have) {
+                d = kb.bd[lane];
+                i = kb.bi[lane];
+            }
+            const bool keep = (unsigned)lane < have && d <= Bv;
+            const unsigned long long m = __ballot(keep);
+            if (keep && !(ABL & 1)) {
+                const unsigned p = lanes_below(m);
+                store_wt(&io.list_d[lbase + p], d);
+                store_wt(&io.list_i[lbase + p], i);
+            }
+            const unsigned long long ms = __ballot(keep && d <= Hv);
+            PASS_TRACE(io, 9);
+            heads(ms, d, i, (unsigned)__popcll(ms), (unsigned)__popcll(m));
+        }
+    } else {
+        if (wid == 0) {
+            unsigned long long Bv, Hv;
+            bounds(Bv, Hv);
+            if (lane == 0) {
+                kb.bound = Bv;
+                kb.hcap = Hv;
             }
         }
-    }
-    __syncthreads();
-    if (wid == 0) {
-        const unsigned ns = kb.nsmall;
-        KE e = ksentinel();
-        if ((unsigned)lane < ns && lane < kWave) {
-            e.d = kb.top_d[lane];
-            e.i = kb.top_i[lane];
+        __syncthreads();
+        PASS_TRACE(io, 8);
+        const unsigned long long B = kb.bound;
+        const unsigned long long H = kb.hcap;
+        for (unsigned t0 = 0; t0 < have; t0 += NT) {
+            const unsigned t = t0 + threadIdx.x;
+            unsigned long long d = kSentinelD;
+            unsigned i = kSentinelI;
+            if (t < have) {
+                d = kb.bd[t];
+                i = kb.bi[t];
+            }
+            const bool keep = d <= B && t < have;
+            const unsigned long long m = __ballot(keep);
+            unsigned wb = 0;
+            if (lane == 0 && m) wb = atomicAdd(&kb.cursor, (unsigned)__popcll(m));
+            wb = __shfl(wb, 0);
+            if (keep && !(ABL & 1)) {
+                const unsigned p = wb + lanes_below(m);
+                store_wt(&io.list_d[lbase + p], d);
+                store_wt(&io.list_i[lbase + p], i);
+            }
+            const bool small = keep && d <= H;
+            const unsigned long long ms = __ballot(small);
+            unsigned sb = 0;
+            if (lane == 0 && ms) sb = atomicAdd(&kb.nsmall, (unsigned)__popcll(ms));
+            sb = __shfl(sb, 0);
+            if (small) {
+                const unsigned p = sb + lanes_below(ms);
+                if (p < (unsigned)kWave) {
+                    kb.top_d[p] = d;
+                    kb.top_i[p] = i;
+                }
+            }
         }
-        if (!(ABL & 2)) e = wave_sort64(e);
-        if ((unsigned)lane < kPassHeads) {
-            store_wt(&io.head_d[kPassHeads * blockIdx.x + lane], e.d);
-            store_wt(&io.head_i[kPassHeads * blockIdx.x + lane], e.i);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the list stores, before the ticket
+        __syncthreads();
+        PASS_TRACE(io, 9);
+        if (wid == 0) {
+            const unsigned ns = kb.nsmall;
+            const unsigned nl = ns < (unsigned)kWave ? ns : (unsigned)kWave;
+            unsigned long long d = kSentinelD;
+            unsigned i = kSentinelI;
+            if ((unsigned)lane < nl) {
+                d = kb.top_d[lane];
+                i = kb.top_i[lane];
+            }
+            heads(__ballot((unsigned)lane < nl), d, i, ns, kb.cursor);
         }
-        // heads complete: every list entry <= H is among the sorted ones, and either 4 of them
-        // exist or the list holds nothing else
-        const bool complete = ns <= (unsigned)kWave && (ns >= kPassHeads || ns == kb.cursor);
-        if (lane == 0) store_wt(&io.len[blockIdx.x], kb.cursor | (complete ? 0u : kLenWhole));
     }
-    // ---- arrival (cdna_hip_programming.md §6 Guideline 16, counter form): every storing wave
-    // drains its write-through stores, the block meets, one lane takes a ticket
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    PASS_TRACE(io, 3);
-    if (threadIdx.x == 0) kb.last = pass_arrive_last(io.ctr + kTicketStride, io.groups) ? 1u : 0u;
     __syncthreads();
     PASS_TRACE(io, 4);
     if (kb.last == 0) {
@@ -1871,6 +1984,7 @@ hipError_t launch_knn_pass(const double* x, const double* y, uint64_t n, const K
             case 1: knn_pass<kPassNW, 1><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io, rio); break;
             case 2: knn_pass<kPassNW, 2><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io, rio); break;
             case 8: knn_pass<kPassNW, 8><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io, rio); break;
+            case 16: knn_pass<kPassNW, 16><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io, rio); break;
             default: knn_pass<kPassNW><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io, rio); break;
         }
     }
