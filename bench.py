@@ -60,6 +60,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true", help="skip the host-resident end-to-end line")
+    p.add_argument("--no-pipelined", action="store_true", help="skip the multi-stream pipelined line")
+    p.add_argument("--pipeline-streams", type=int, default=2, help="contexts / HIP streams of the pipelined line")
     p.add_argument("--time-every", type=int, default=8,
                    help="bracket every N-th timed step's kernels with HIP events (1 = all)")
     return p.parse_args()
@@ -215,6 +217,53 @@ class KnnWorkload(Workload):
                 "path": "pageable host x/y -> ctx-owned pinned 2-slot staging (1M-point chunks, persistent copy workers) -> "
                         "per-chunk knn_pass as each chunk lands (copy stream / compute stream overlap) -> "
                         "rebase + merge -> k results to host"}
+
+    def pipelined(self, windows=400, nstreams=2):
+        """Consecutive windows on nstreams contexts / HIP streams (as Flink task slots sharing
+        the GPU would run them): window i+1's scan starts on the CUs window i's blocks free, so
+        the per-window tail (block lists, the last block's final selection) overlaps the next
+        stream.  Reported beside the strict one-window-per-step line, not as `value`."""
+        import torch
+        from spatialflink_amd import Context
+        ctxs = [self.ctx] + [Context(self.dev.index) for _ in range(nstreams - 1)]
+        streams = [torch.cuda.Stream(self.dev) for _ in ctxs]
+        outs = [(torch.empty(self.k, dtype=torch.int32, device=self.dev),
+                 torch.empty(self.k, dtype=torch.float64, device=self.dev),
+                 torch.zeros(1, dtype=torch.int32, device=self.dev)) for _ in ctxs]
+        old = self.ctx._bound
+        try:
+            for c in ctxs:
+                c.follow_torch_stream(True)
+
+            def run(nw):
+                for i in range(nw):
+                    j = i % nstreams
+                    with torch.cuda.stream(streams[j]):
+                        ctxs[j].knn_pp_async(self.grid, self.xs[i % self.windows], self.ys[i % self.windows],
+                                             self.q[0], self.q[1], self.radius, self.k, *outs[j])
+            torch.cuda.synchronize(self.dev)
+            run(16)
+            torch.cuda.synchronize(self.dev)
+            t0 = time.perf_counter()
+            run(windows)
+            torch.cuda.synchronize(self.dev)
+            t = (time.perf_counter() - t0) / windows
+            # the last window of each context against the sequential path
+            same = True
+            for j in range(nstreams):
+                i = windows - nstreams + j
+                wi, _ = self.ctx.knn_pp(self.grid, self.xs[i % self.windows], self.ys[i % self.windows],
+                                        self.q[0], self.q[1], self.radius, self.k)
+                same = same and outs[j][0].cpu().numpy().astype(np.uint32).tolist() == \
+                    wi.cpu().numpy().astype(np.uint32).tolist()
+        finally:
+            for c in ctxs[1:]:
+                c.close()
+            self.ctx.set_stream(old)
+        return {"value": self.n / t, "unit": "points/sec", "us_per_window": t * 1e6,
+                "hbm_GBps": BYTES_PER_POINT * self.n / t / 1e9,
+                "hbm_frac": BYTES_PER_POINT * self.n / t / 1e9 / HBM_PEAK_GBS, "streams": nstreams, "windows": windows,
+                "matches_sequential": same}
 
     def cpu_baseline(self, seconds):
         cref = _oracle()
@@ -806,6 +855,8 @@ def main():
         e2e = wl.e2e()
         if e2e is not None:
             result["e2e"] = e2e
+    if rank == 0 and world == 1 and hasattr(wl, "pipelined") and not args.no_pipelined:
+        result["pipelined"] = wl.pipelined(nstreams=args.pipeline_streams)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = wl.cpu_baseline(args.cpu_seconds)
     if rank == 0:
