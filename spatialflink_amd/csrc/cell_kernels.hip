@@ -145,21 +145,25 @@ __global__ void scan_apply(const T* __restrict__ in, uint64_t n, const T* __rest
 }
 
 // ------------------------------------------------------------------ tile binning ---------
-// Unsigned division by a launch constant d >= 1 without the ~30-instruction integer division
-// sequence: q = trunc(n * fl(1/d)) in fp64 is off by at most one (n < 2^32), and one multiply
-// corrects it.  Exact for every 32-bit n.
+// Unsigned division by a launch constant 1 <= d < 2^31 without the ~30-instruction integer
+// division sequence: round-up multiplier m = floor(2^32 (2^l - d) / d) + 1, l = ceil(log2 d),
+// q = (t + ((n - t) >> 1)) >> (l - 1), t = mulhi(m, n) (Granlund-Montgomery; exact for every
+// 32-bit n).  Five integer instructions; the fp64 reciprocal form it replaces cost ~12 VALU
+// with three fp64 ones per division, and the binning passes were VALU-issue-bound.
 struct FastDiv {
-    double inv;
-    unsigned d;
+    unsigned m, d;
+    unsigned s1, s2;
     __device__ __forceinline__ unsigned div(unsigned n) const {
-        unsigned q = (unsigned)((double)n * inv);
-        const long long r = (long long)n - (long long)q * (long long)d;
-        if (r < 0) q--;
-        else if (r >= (long long)d) q++;
-        return q;
+        const unsigned t = __umulhi(m, n);
+        return (t + ((n - t) >> s1)) >> s2;
     }
 };
-inline FastDiv make_fastdiv(unsigned d) { return FastDiv{1.0 / (double)d, d}; }
+inline FastDiv make_fastdiv(unsigned d) {
+    unsigned l = 0;
+    while ((1ull << l) < d) l++;
+    const unsigned m = (unsigned)(((1ull << 32) * ((1ull << l) - d)) / d + 1);
+    return FastDiv{m, d, l ? 1u : 0u, l ? l - 1 : 0u};
+}
 
 struct TileGeom {
     double mnx, mny, l;  // grid the point cells are computed on
@@ -186,7 +190,6 @@ __device__ __forceinline__ unsigned tile_of(const TileGeom& g, int32_t cx, int32
 // every block (measured 0.3 TB/s on 50M uniform points).
 constexpr int kBandBits = 7;
 constexpr unsigned kBandTiles = 1u << kBandBits;
-constexpr int kSub = 2048;        // points per local sort (2 per thread of a 1024-thread block)
 constexpr int kLocalBins = 132;   // >= bands + 1 (level 1), >= kBandTiles (level 2)
 constexpr unsigned kL2Items = 32768;  // points per level-2 work item
 constexpr unsigned kNoKey = 0xffffffffu;
@@ -221,18 +224,22 @@ __device__ __forceinline__ unsigned key_tile(const TileGeom& g, unsigned key) {
 // level-1 point: key (kNoKey when out of the grid); bin: its band, nbands when out of the grid,
 // nbands + 1 when its cell is not in the keep bitmap (dropped).  Two steps so the keep-bitmap
 // loads of several points go out together (and ahead of any prefetch).
-__device__ __forceinline__ unsigned l1_key(const BinPass& a, double px, double py) {
+__device__ __forceinline__ unsigned l1_key(const BinPass& a, double px, double py, unsigned& tile) {
     int32_t cx, cy;
-    if (point_cell(a.g, px, py, cx, cy)) return (unsigned)cx * (unsigned)a.g.nb + (unsigned)cy;
+    tile = 0;
+    if (point_cell(a.g, px, py, cx, cy)) {
+        tile = tile_of(a.g, cx, cy);  // from the cell itself: no division of the key
+        return (unsigned)cx * (unsigned)a.g.nb + (unsigned)cy;
+    }
     return kNoKey;
 }
 __device__ __forceinline__ unsigned l1_keepword(const BinPass& a, unsigned key) {
     return (a.keep && key != kNoKey) ? a.keep[key >> 5] : ~0u;
 }
-__device__ __forceinline__ unsigned l1_bin(const BinPass& a, unsigned key, unsigned kw) {
+__device__ __forceinline__ unsigned l1_bin(const BinPass& a, unsigned key, unsigned kw, unsigned tile) {
     if (key == kNoKey) return a.nbands;
     if (!((kw >> (key & 31u)) & 1u)) return a.nbands + 1;
-    return key_tile(a.g, key) >> kBandBits;
+    return tile >> kBandBits;
 }
 
 // Workgroup barrier that orders LDS only: waits for this wave's LDS operations, not for its
@@ -271,12 +278,12 @@ __global__ __launch_bounds__(kBinThreads) void bin_count(BinPass a) {
     const int wid = threadIdx.x / kWave;
     for (unsigned t = threadIdx.x; t < (kBinThreads / kWave) * kLocalBins; t += kBinThreads) (&h[0][0])[t] = 0;
     __syncthreads();
-    // 4 points per thread with all their loads issued first (a single load pair per thread in
-    // flight left the pass latency-bound at 2.5 TB/s)
-    constexpr unsigned kU = 4;
+    // kU points per thread with all their loads issued first (a single load pair per thread in
+    // flight left the pass latency-bound at 2.5 TB/s; level 1 runs one block per CU: 8)
+    constexpr unsigned kU = LEVEL == 1 ? 8 : 4;
     for (uint64_t i0 = b0 + threadIdx.x; i0 < b1; i0 += kU * kBinThreads) {
         double px[kU], py[kU];
-        unsigned key[kU];
+        unsigned key[kU], tl[kU];
 #pragma unroll
         for (unsigned k = 0; k < kU; k++) {
             const uint64_t i = i0 + (uint64_t)k * kBinThreads;
@@ -293,7 +300,7 @@ __global__ __launch_bounds__(kBinThreads) void bin_count(BinPass a) {
         if (LEVEL == 1) {
 #pragma unroll
             for (unsigned k = 0; k < kU; k++) {
-                key[k] = l1_key(a, px[k], py[k]);
+                key[k] = l1_key(a, px[k], py[k], tl[k]);
                 kw[k] = i0 + (uint64_t)k * kBinThreads < b1 ? l1_keepword(a, key[k]) : ~0u;
             }
         }
@@ -301,7 +308,7 @@ __global__ __launch_bounds__(kBinThreads) void bin_count(BinPass a) {
         for (unsigned k = 0; k < kU; k++) {
             const uint64_t i = i0 + (uint64_t)k * kBinThreads;
             if (i < b1) {
-                const unsigned bin = LEVEL == 1 ? l1_bin(a, key[k], kw[k]) : key_tile(a.g, key[k]) - (band << kBandBits);
+                const unsigned bin = LEVEL == 1 ? l1_bin(a, key[k], kw[k], tl[k]) : key_tile(a.g, key[k]) - (band << kBandBits);
                 if (LEVEL == 2 || bin != a.nbands + 1) atomicAdd(&h[wid][bin], 1u);  // dropped: not counted
             }
         }
@@ -402,19 +409,24 @@ __global__ void bin2_tiles(unsigned* __restrict__ hist, const unsigned* __restri
     }
 }
 
+template <int N>
 struct SortStage {
-    double x[kSub];
-    double y[kSub];
-    unsigned idx[kSub];
-    unsigned key[kSub];
-    unsigned char bin[kSub];
+    double x[N];
+    double y[N];
+    unsigned idx[N];
+    unsigned key[N];
+    unsigned char bin[N];
 };
 
-// Local-sort scatter: kSub points at a time are counted by bin in LDS, staged in bin order,
-// and stored so consecutive threads write consecutive addresses of one bin's run.
+// Local-sort scatter: SUB points at a time are counted by bin in LDS, staged in bin order,
+// and stored so consecutive threads write consecutive addresses of one bin's run.  Level 1 runs
+// one block per CU over the raw window: 4 points per thread per sub-chunk (64 KB of loads in
+// flight per CU; 2 per thread left it latency-bound at ~3 TB/s); level 2 has many more blocks.
 template <int LEVEL>
 __global__ __launch_bounds__(kBinThreads) void bin_scatter(BinPass a) {
-    __shared__ SortStage st;
+    constexpr int PPT = LEVEL == 1 ? 4 : 2;
+    constexpr int SUB = PPT * kBinThreads;
+    __shared__ SortStage<SUB> st;
     __shared__ unsigned cur[kLocalBins], lh[kLocalBins], ls[kLocalBins];
     uint64_t b0, b1;
     unsigned nbins, band;
@@ -427,11 +439,11 @@ __global__ __launch_bounds__(kBinThreads) void bin_scatter(BinPass a) {
     __syncthreads();
     // the next sub-chunk's points are loaded while this one is sorted: the barriers below
     // order LDS only (lds_barrier), so those loads stay in flight across them
-    double nx[2], ny[2];
-    unsigned nidx[2], nkey[2];
+    double nx[PPT], ny[PPT];
+    unsigned nidx[PPT], nkey[PPT];
     auto fetch = [&](uint64_t sb) {
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
+        for (int k = 0; k < PPT; k++) {
             const uint64_t i = sb + threadIdx.x + (uint64_t)k * kBinThreads;
             if (i < b1) {
                 if (LEVEL == 1) {
@@ -447,27 +459,27 @@ __global__ __launch_bounds__(kBinThreads) void bin_scatter(BinPass a) {
         }
     };
     if (b0 < b1) fetch(b0);
-    for (uint64_t sb = b0; sb < b1; sb += kSub) {
-        const unsigned m = b1 - sb < (uint64_t)kSub ? (unsigned)(b1 - sb) : (unsigned)kSub;
-        double px[2], py[2];
-        unsigned idx[2], key[2], bin[2], rk[2];
-        unsigned kw[2];
+    for (uint64_t sb = b0; sb < b1; sb += SUB) {
+        const unsigned m = b1 - sb < (uint64_t)SUB ? (unsigned)(b1 - sb) : (unsigned)SUB;
+        double px[PPT], py[PPT];
+        unsigned idx[PPT], key[PPT], bin[PPT], rk[PPT];
+        unsigned kw[PPT], tl[PPT];
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
+        for (int k = 0; k < PPT; k++) {
             const unsigned j = threadIdx.x + k * kBinThreads;
             px[k] = nx[k];
             py[k] = ny[k];
             idx[k] = LEVEL == 1 ? (unsigned)(sb + j) : nidx[k];
-            key[k] = LEVEL == 1 ? l1_key(a, px[k], py[k]) : nkey[k];
+            key[k] = LEVEL == 1 ? l1_key(a, px[k], py[k], tl[k]) : nkey[k];
             kw[k] = (LEVEL == 1 && j < m) ? l1_keepword(a, key[k]) : ~0u;  // issued before the prefetch
         }
-        if (sb + kSub < b1) fetch(sb + kSub);
+        if (sb + SUB < b1) fetch(sb + SUB);
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
+        for (int k = 0; k < PPT; k++) {
             const unsigned j = threadIdx.x + k * kBinThreads;
             bin[k] = a.nbands + 1;  // level 1: dropped unless binned below
             if (j < m) {
-                bin[k] = LEVEL == 1 ? l1_bin(a, key[k], kw[k]) : key_tile(a.g, key[k]) - (band << kBandBits);
+                bin[k] = LEVEL == 1 ? l1_bin(a, key[k], kw[k], tl[k]) : key_tile(a.g, key[k]) - (band << kBandBits);
                 if (LEVEL == 2 || bin[k] != a.nbands + 1) rk[k] = atomicAdd(&lh[bin[k]], 1u);
             }
         }
@@ -486,7 +498,7 @@ __global__ __launch_bounds__(kBinThreads) void bin_scatter(BinPass a) {
         }
         lds_barrier();
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
+        for (int k = 0; k < PPT; k++) {
             const unsigned j = threadIdx.x + k * kBinThreads;
             if (j < m && (LEVEL == 2 || bin[k] != a.nbands + 1)) {  // dropped points are not staged
                 const unsigned slot = ls[bin[k]] + rk[k];
@@ -499,7 +511,7 @@ __global__ __launch_bounds__(kBinThreads) void bin_scatter(BinPass a) {
         }
         lds_barrier();
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
+        for (int k = 0; k < PPT; k++) {
             const unsigned j = threadIdx.x + k * kBinThreads;
             if (j < (LEVEL == 2 ? m : ls[a.nbands + 1])) {  // the staged points: every bin before "dropped"
                 const unsigned b = st.bin[j];
