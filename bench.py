@@ -851,11 +851,11 @@ def main():
                                    "frac": tf / FP64_PEAK_TFLOPS, "flops": flops,
                                    "source": "rocprofv3 SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes of the timed kernels per step "
                                              "(profiles/pmc_" + wl.tag + ".json) / the live average step time"}
-    if rank == 0 and world == 1 and not args.no_e2e:
+    if rank == 0 and world == 1 and not args.no_e2e and args.workload == "knn":  # the C2 host path
         e2e = wl.e2e()
         if e2e is not None:
             result["e2e"] = e2e
-    if rank == 0 and world == 1 and hasattr(wl, "pipelined") and not args.no_pipelined:
+    if rank == 0 and world == 1 and args.workload == "knn" and not args.no_pipelined:
         result["pipelined"] = wl.pipelined(nstreams=args.pipeline_streams)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = wl.cpu_baseline(args.cpu_seconds)

@@ -20,13 +20,13 @@ for w in $WORKLOADS; do
   grep '^{' gpurun_out/bench_$w.log
   if [ "${PROF:-1}" = "1" ]; then
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o $w -- \
-        python3 bench.py --workload "$w" --steps $steps --warmup 3 --no-cpu-baseline ${BENCH_ARGS:-} \
+        python3 bench.py --workload "$w" --steps $steps --warmup 3 --no-cpu-baseline --no-e2e --no-pipelined ${BENCH_ARGS:-} \
         > gpurun_out/prof/bench_$w.log 2>&1 || { echo "rocprof $w failed"; tail -20 gpurun_out/prof/bench_$w.log; exit 3; }
   fi
   if [ "${PMC:-1}" = "1" ]; then
     for c in FETCH_SIZE WRITE_SIZE; do
       timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc -o ${w}_$c -- \
-          python3 bench.py --workload "$w" --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} \
+          python3 bench.py --workload "$w" --steps 5 --warmup 1 --no-cpu-baseline --no-e2e --no-pipelined ${BENCH_ARGS:-} \
           > gpurun_out/pmc/${w}_$c.log 2>&1 || { echo "pmc $w $c failed"; tail -20 gpurun_out/pmc/${w}_$c.log; exit 4; }
     done
   fi

@@ -12,7 +12,7 @@ for w in ${WLS:-knn c5 range join ppoly ppjoin ppknn ingest}; do
   case $w in ppoly|ppjoin|ppknn) passes="$passes SQ_INSTS_VALU_FLOPS_FP64";; esac
   for c in $passes; do
     timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc -o ${w}_$c -- \
-        python3 bench.py --workload $w --steps 5 --warmup 2 --no-cpu-baseline --no-e2e > gpurun_out/pmc/${w}_$c.log 2>&1 \
+        python3 bench.py --workload $w --steps 5 --warmup 2 --no-cpu-baseline --no-e2e --no-pipelined > gpurun_out/pmc/${w}_$c.log 2>&1 \
         || { echo "pass $w $c failed"; exit 1; }
     echo "$w $c ok"
   done
