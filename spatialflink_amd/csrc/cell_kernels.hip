@@ -1216,6 +1216,35 @@ __device__ __forceinline__ bool segment_within(double px, double py, double ax, 
     if (box_dist2(px, py, __builtin_fmin(ax, bx), __builtin_fmin(ay, by), __builtin_fmax(ax, bx),
                   __builtin_fmax(ay, by)) > lim2)
         return false;
+    // Certified screens without division or square root.  D = true distance from p to the
+    // segment; the JTS value d is within dJ = 2^-50 (|p-A|_1 + |B-A|_1) + 2^-51 D of it (see
+    // screen_lim2), so D < r - dl decides "d <= r" and D > r + dl decides "d > r", dl >= 4 dJ.
+    // Bounds on D: <= |p-A|, |p-B|; = the line distance |cross| / |B-A| when the projection is
+    // certainly interior; >= the line distance always.  Every product below is of terms <= M
+    // (M = |p-A|_1 + |B-A|_1), so each computed quantity is within 2^-50 M^2 of its value: E =
+    // 2^-45 M^2 covers it, and the (1 -/+ 2^-45) factors cover the roundings of the squared
+    // bounds.  NaN or an infinity anywhere fails every decision (the exact path runs).
+    {
+        const double dax = px - ax, day = py - ay, dbx = px - bx, dby = py - by;
+        const double ex = bx - ax, ey = by - ay;
+        const double M = __builtin_fabs(dax) + __builtin_fabs(day) + __builtin_fabs(ex) + __builtin_fabs(ey);
+        const double E = M * M * 0x1.0p-45;
+        const double dl = M * 0x1.0p-48 + __builtin_fabs(r) * 0x1.0p-49;
+        const double rl = r - dl, rh = r + dl;
+        const double rl2 = rl * rl * (1.0 - 0x1.0p-45), rh2 = rh * rh * (1.0 + 0x1.0p-45);
+        const double da2 = dax * dax + day * day, db2 = dbx * dbx + dby * dby;
+        const double len2 = ex * ex + ey * ey;
+        const double dot = dax * ex + day * ey;
+        const double crs = __builtin_fabs(day * ex - dax * ey);
+        const bool interior = dot - E > 0.0 && dot + E < len2 - E;
+        if (rl > 0.0) {
+            if (da2 + E < rl2 || db2 + E < rl2) return true;  // an endpoint is closer than r
+            if (interior && (crs + E) * (crs + E) < rl2 * (len2 - E) * (1.0 - 0x1.0p-50)) return true;
+        }
+        if (crs > E && (crs - E) * (crs - E) > rh2 * (len2 + E) * (1.0 + 0x1.0p-50)) return false;  // line
+        if (dot + E < 0.0 && da2 - E > rh2) return false;        // nearest point A
+        if (dot - E > len2 + E && db2 - E > rh2) return false;   // nearest point B
+    }
     double d;
     if (ax == bx && ay == by) {
         d = coord_distance(px, py, ax, ay);
@@ -1232,13 +1261,47 @@ __device__ __forceinline__ bool segment_within(double px, double py, double ax, 
     return d <= r;
 }
 
+// fp32 segment boxes for the distance pre-screen: box of segment (v[e], v[e+1]) relative to
+// the polygon's origin o = (gb[0], gb[1]), each coordinate rounded to fp32 once (error <=
+// 2^-24 |c - o| + 2^-53 |c - o|: IEEE subtraction and conversion are each within half an ulp of
+// their result).  The last vertex has no segment: an all-NaN box, which never rejects.
+__device__ __forceinline__ float4 seg_box32(const double* __restrict__ vx, const double* __restrict__ vy, uint32_t e,
+                                            uint32_t nv, double ox, double oy) {
+    if (e + 1 >= nv) return make_float4(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
+    const double ax = vx[e], ay = vy[e], bx = vx[e + 1], by = vy[e + 1];
+    return make_float4((float)(__builtin_fmin(ax, bx) - ox), (float)(__builtin_fmin(ay, by) - oy),
+                       (float)(__builtin_fmax(ax, bx) - ox), (float)(__builtin_fmax(ay, by) - oy));
+}
+// The point's side of that screen.  u = p - o and every box coordinate carry at most ~2^-23.9 of
+// their magnitude, the fp32 subtractions 2^-24 of theirs, so the fp32 box distance is within
+// S = 2^-18 (|u| + |v| + ext) (+ an absolute term for fp32 underflow) of the true box distance,
+// ext = the polygon box's half-perimeter >= every |box coordinate|.  Rejected: fp32 distance^2 >
+// (lim + S)^2 (1 + 2^-19) -- the squares' own fp32 rounding (<= 2^-22) is inside that factor.
+// NaN anywhere never rejects (fmaxf drops one NaN operand, a NaN bound compares false).
+struct Fp32Screen {
+    float u, v, lim2;
+    __device__ __forceinline__ bool rejects(const float4 b) const {
+        const float ex = __builtin_fmaxf(__builtin_fmaxf(b.x - u, u - b.z), 0.0f);
+        const float ey = __builtin_fmaxf(__builtin_fmaxf(b.y - v, v - b.w), 0.0f);
+        return ex * ex + ey * ey > lim2;
+    }
+};
+__device__ __forceinline__ Fp32Screen fp32_screen(double px, double py, const double gb[4], double lim2) {
+    const double u = px - gb[0], v = py - gb[1];
+    const double ext = (gb[2] - gb[0]) + (gb[3] - gb[1]);
+    const double S = (__builtin_fabs(u) + __builtin_fabs(v) + ext) * 0x1.0p-18 + 0x1.0p-100;
+    const double ls = __builtin_sqrt(lim2) * (1.0 + 0x1.0p-40) + S;
+    return Fp32Screen{(float)u, (float)v, (float)(ls * ls * (1.0 + 0x1.0p-19))};
+}
+
 // JTS DistanceOp(point, polygon) predicate "distance <= r" (r < MAX_VALUE):
 // PointLocator (envelope, RayCrossingCounter over the ring) -> 0 when not EXTERIOR; else the
 // min over segments of Distance.pointToSegment.  A boundary hit anywhere makes the answer true
 // whatever the other segments count, so segments are visited in any order and only those of
 // the point's slab lists; boolean-equivalent early exit on the first segment within r.
 __device__ __forceinline__ bool point_polygon_within(double px, double py, const double* __restrict__ vx,
-                                     const double* __restrict__ vy, const PolyDev& P, const SlabView& sv, double r) {
+                                     const double* __restrict__ vy, const PolyDev& P, const SlabView& sv, double r,
+                                     const float4* __restrict__ sb = nullptr) {
     const int nv = (int)P.nv;
     const bool in_env = !(px > P.bb[2] || px < P.bb[0] || py > P.bb[3] || py < P.bb[1]);
     const uint32_t s = sv.ns ? slab_of(py, P.sy0, P.sinv, sv.ns) : 0u;
@@ -1270,6 +1333,26 @@ __device__ __forceinline__ bool point_polygon_within(double px, double py, const
     if (sv.ns && lim2 <= P.E * P.E) {
         const uint32_t k1 = sv.dbeg(s + 1);
         uint32_t k = sv.dbeg(s);
+        if (sb) {
+            // fp32 pre-screen (sb: segment boxes relative to (gb[0], gb[1]), see seg_box32): the
+            // box distance of the fp32 point and box is within S of the true box distance, so
+            // "fp32 box distance > lim + S" rejects only segments the fp64 screen rejects too;
+            // the survivors (usually none or one per point) take the fp64 path unchanged
+            const float4* __restrict__ sbb = sb;
+            const Fp32Screen f = fp32_screen(px, py, P.gb, lim2);
+            for (; k + 2 <= k1; k += 2) {
+                const uint32_t e0 = sv.id(k), e1 = sv.id(k + 1);
+                const bool r0 = f.rejects(sbb[e0]), r1 = f.rejects(sbb[e1]);
+                if (!r0 && segment_within(px, py, vx[e0], vy[e0], vx[e0 + 1], vy[e0 + 1], r, lim2)) return true;
+                if (!r1 && segment_within(px, py, vx[e1], vy[e1], vx[e1 + 1], vy[e1 + 1], r, lim2)) return true;
+            }
+            if (k < k1) {
+                const uint32_t e = sv.id(k);
+                if (!f.rejects(sbb[e]) && segment_within(px, py, vx[e], vy[e], vx[e + 1], vy[e + 1], r, lim2))
+                    return true;
+            }
+            return false;
+        }
         for (; k + 2 <= k1; k += 2) {  // "any segment within r": pairs, same answer
             const uint32_t e0 = sv.id(k), e1 = sv.id(k + 1);
             const double a0x = vx[e0], a0y = vy[e0], b0x = vx[e0 + 1], b0y = vy[e0 + 1];
@@ -1430,6 +1513,7 @@ __global__ __launch_bounds__(kTB) void ppoly_eval(TileBins tb, const PolyWork* _
     __shared__ double lvx[kMaxLdsVerts];
     __shared__ double lvy[kMaxLdsVerts];
     __shared__ uint8_t lvr[kMaxLdsVerts];
+    __shared__ float4 lsb[kMaxLdsVerts];  // fp32 segment boxes (single-ring polygons staged in LDS)
     __shared__ uint16_t lsl[kMaxLdsSlab];
     __shared__ unsigned long long lmask[kMaskWords];
     __shared__ CandQueue cq[kTB / kWave];
@@ -1448,6 +1532,7 @@ __global__ __launch_bounds__(kTB) void ppoly_eval(TileBins tb, const PolyWork* _
             lvx[t] = vx[P.voff + t];
             lvy[t] = vy[P.voff + t];
             if (holes) lvr[t] = vring[P.voff + t];
+            else if (!APPROX) lsb[t] = seg_box32(vx + P.voff, vy + P.voff, t, P.nv, P.gb[0], P.gb[1]);
         }
     if (s_lds)
         for (uint32_t t = threadIdx.x; t < P.llen; t += kTB) lsl[t] = slabs[P.loff + t];
@@ -1473,7 +1558,7 @@ __global__ __launch_bounds__(kTB) void ppoly_eval(TileBins tb, const PolyWork* _
             const double px = Q.x[from + lane], py = Q.y[from + lane];
             const unsigned pos = Q.pos[from + lane];
             const bool in = holes ? point_polygon_within_rings(px, py, rvx, rvy, rvr, rre, P, sv, r)
-                                  : point_polygon_within(px, py, rvx, rvy, P, sv, r);
+                                  : point_polygon_within(px, py, rvx, rvy, P, sv, r, v_lds ? lsb : nullptr);
             if (in) atomicOr(&mk[pos >> 6], 1ull << (pos & 63));
         }
         wave_lds_sync();

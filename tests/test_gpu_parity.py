@@ -389,6 +389,42 @@ def test_ppoly_boundary_and_outside(ctx):
         assert pairs_sorted(got).tolist() == pairs_sorted(want).tolist()
 
 
+def test_ppoly_distance_band(ctx):
+    """Points a few ulps either side of distance r from star-polygon segments (perpendicular
+    offsets of edge interiors, offsets from vertices, points near the projection's ends): the
+    fp32 segment-box screen and the division-free certified screens of segment_within may only
+    decide outside that band; inside it the JTS expression decides (bit-exact vs the oracle)."""
+    ag, cg = agrid(500)
+    off, vx, vy = synth.star_polygons(12, 77)
+    rng = np.random.default_rng(77)
+    r = 0.005
+    xs, ys = [], []
+    for p in range(12):
+        a, b = int(off[p]), int(off[p + 1])
+        for e in range(a, b - 1):
+            ax, ay, bx, by = vx[e], vy[e], vx[e + 1], vy[e + 1]
+            ex, ey = bx - ax, by - ay
+            L = math.hypot(ex, ey)
+            nx, ny = -ey / L, ex / L
+            for t in rng.uniform(-0.05, 1.05, 6).tolist() + [0.0, 1.0, 1e-9, 1 - 1e-9]:
+                for side in (1.0, -1.0):
+                    for d in (r, r * (1 + 1e-15), r * (1 - 1e-15), r * (1 + 1e-9), r * (1 - 1e-9)):
+                        xs.append(ax + t * ex + side * d * nx)
+                        ys.append(ay + t * ey + side * d * ny)
+            th = rng.uniform(0, 2 * np.pi, 4)
+            for d in (r, r * (1 + 2e-16), r * (1 - 2e-16)):
+                xs.extend((ax + d * np.cos(th)).tolist())
+                ys.extend((ay + d * np.sin(th)).tolist())
+    x = np.array(xs)
+    y = np.array(ys)
+    x = np.concatenate([x, np.nextafter(x, np.inf), np.nextafter(x, -np.inf)])
+    y = np.concatenate([y, y, np.nextafter(y, np.inf)])
+    for rr in (r, np.nextafter(r, 0), np.nextafter(r, 1)):
+        got = ctx.range_ppoly(ag, x, y, off, vx, vy, rr)
+        want = cref.range_ppoly(cg, x, y, off, vx, vy, rr)
+        assert pairs_sorted(got).tolist() == pairs_sorted(want).tolist()
+
+
 def test_range_circle_band(ctx):
     """Points within a few ulps of the query circle exercise the exact-distance band behind the
     squared screens (fast accept / fast reject must never decide these)."""
