@@ -1043,6 +1043,29 @@ __device__ __forceinline__ unsigned long long spread32(unsigned v) {  // bit b -
     return x;
 }
 
+// Hits of 64 consecutive mask words (word j held by lane j, ex = exclusive prefix of the
+// words' hit counts) stored in ascending index order from output position obase: the wave walks
+// only the nonzero words (ballot + find-first-set) and each word's hits go out from its lanes at
+// consecutive positions (coalesced for dense words; sparse words cost one step each).
+__device__ __forceinline__ void emit_words(unsigned long long mine, unsigned ex, unsigned long long obase,
+                                           unsigned first_point, unsigned* __restrict__ out,
+                                           unsigned long long cap) {
+    const int lane = lane_id();
+    unsigned long long nz = __ballot(mine != 0ull);
+    while (nz) {
+        const int j = __builtin_ctzll(nz);
+        nz &= nz - 1;
+        const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)mine, j);
+        const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(mine >> 32), j);
+        const unsigned long long bits = ((unsigned long long)hi << 32) | lo;
+        const unsigned pj = (unsigned)__builtin_amdgcn_readlane((int)ex, j);
+        if ((bits >> lane) & 1ull) {
+            const unsigned long long pos = obase + pj + lanes_below(bits);
+            if (pos < cap) out[pos] = first_point + (unsigned)j * 64u + (unsigned)lane;
+        }
+    }
+}
+
 // Range hits of a block chunk (LDS bitmask) written in ascending index order: the block
 // publishes its count (status word tagged with the launch epoch, atomic exchange: visible at the
 // device coherence point), sums the counts of every earlier chunk (wave 0, all loads in flight,
@@ -1117,19 +1140,7 @@ __device__ __forceinline__ void pass_range_emit(const PassRangeIo& rio, const un
         const unsigned long long mine = w0 + lane < we ? bmask[w0 + lane] : 0ull;
         const unsigned cc = (unsigned)__popcll(mine);
         const unsigned incl = wave_incl_scan(cc);
-        const unsigned ex = incl - cc;
-        const unsigned m = we - w0 < (unsigned)kWave ? we - w0 : (unsigned)kWave;
-        for (unsigned j = 0; j < m; j++) {
-            const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)mine, (int)j);
-            const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(mine >> 32), (int)j);
-            const unsigned long long bits = ((unsigned long long)hi << 32) | lo;
-            if (!bits) continue;
-            const unsigned pj = (unsigned)__builtin_amdgcn_readlane((int)ex, (int)j);
-            if ((bits >> lane) & 1ull) {
-                const unsigned long long pos = obase + pj + lanes_below(bits);
-                if (pos < rio.cap) rio.out[pos] = ibase + (w0 + j) * 64u + (unsigned)lane;
-            }
-        }
+        emit_words(mine, incl - cc, obase, ibase + w0 * 64u, rio.out, rio.cap);
         obase += (unsigned)__builtin_amdgcn_readlane((int)incl, kWave - 1);
     }
     if (threadIdx.x == 0 && vb == gridDim.x - 1) *rio.total = excl_sh + bcount;
@@ -1329,7 +1340,7 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
     // heads, in order.  A list whose heads may be incomplete (spilled survivors counted in the
     // histogram, > 64 entries <= H) is flagged in its length word so the final reads it whole.
     // Then the arrival (cdna_hip_programming.md §6 Guideline 16, counter form): the storing wave
-    // drains its write-through stores and takes the ticket.  Common case (<= 64 survivors): wave
+    // drains its write-through stores and takes the ticket.  Common case (<= 256 survivors): wave
     // 0 alone, in registers, behind no further barrier; else every wave through LDS.
     const unsigned have = kb.cnt < (unsigned)PB::kCap ? kb.cnt : (unsigned)PB::kCap;  // block-uniform
     const size_t lbase = (size_t)blockIdx.x * io.list_cap;
@@ -1365,27 +1376,49 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
         PASS_TRACE(io, 3);
         if (lane == 0) kb.last = pass_arrive_last(io.ctr + kTicketStride, io.groups) ? 1u : 0u;
     };
-    if (have <= (unsigned)kWave) {
-        if (wid == 0) {
+    if (have <= 4u * kWave) {
+        if (wid == 0) {  // up to 4 survivors per lane: list offsets by ballot prefix, no atomics
             unsigned long long Bv, Hv;
             bounds(Bv, Hv);
             PASS_TRACE(io, 8);
+            unsigned listed = 0, ns = 0;
+            for (unsigned s0 = 0; s0 < have; s0 += kWave) {
+                const unsigned t = s0 + (unsigned)lane;
+                unsigned long long d = kSentinelD;
+                unsigned i = kSentinelI;
+                if (t < have) {
+                    d = kb.bd[t];
+                    i = kb.bi[t];
+                }
+                const bool keep = t < have && d <= Bv;
+                const unsigned long long m = __ballot(keep);
+                if (keep && !(ABL & 1)) {
+                    const unsigned p = listed + lanes_below(m);
+                    store_wt(&io.list_d[lbase + p], d);
+                    store_wt(&io.list_i[lbase + p], i);
+                }
+                listed += (unsigned)__popcll(m);
+                const bool small = keep && d <= Hv;
+                const unsigned long long ms = __ballot(small);
+                if (small) {
+                    const unsigned p = ns + lanes_below(ms);
+                    if (p < (unsigned)kWave) {
+                        kb.top_d[p] = d;
+                        kb.top_i[p] = i;
+                    }
+                }
+                ns += (unsigned)__popcll(ms);
+            }
+            wave_lds_sync();
+            PASS_TRACE(io, 9);
+            const unsigned nl = ns < (unsigned)kWave ? ns : (unsigned)kWave;
             unsigned long long d = kSentinelD;
             unsigned i = kSentinelI;
-            if ((unsigned)lane < have) {
-                d = kb.bd[lane];
-                i = kb.bi[lane];
+            if ((unsigned)lane < nl) {
+                d = kb.top_d[lane];
+                i = kb.top_i[lane];
             }
-            const bool keep = (unsigned)lane < have && d <= Bv;
-            const unsigned long long m = __ballot(keep);
-            if (keep && !(ABL & 1)) {
-                const unsigned p = lanes_below(m);
-                store_wt(&io.list_d[lbase + p], d);
-                store_wt(&io.list_i[lbase + p], i);
-            }
-            const unsigned long long ms = __ballot(keep && d <= Hv);
-            PASS_TRACE(io, 9);
-            heads(ms, d, i, (unsigned)__popcll(ms), (unsigned)__popcll(m));
+            heads(__ballot((unsigned)lane < nl), d, i, ns, listed);
         }
     } else {
         if (wid == 0) {
@@ -1825,18 +1858,7 @@ __global__ __launch_bounds__(kRangeNW * kWave) void range_fused(const double* __
             const unsigned c = (unsigned)__popcll(mine);
             const unsigned incl = wave_incl_scan(c);
             const unsigned ex = incl - c;
-            const unsigned m = we - w0 < (unsigned)kWave ? we - w0 : (unsigned)kWave;
-            for (unsigned j = 0; j < m; j++) {
-                const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)mine, (int)j);
-                const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(mine >> 32), (int)j);
-                const unsigned long long bits = ((unsigned long long)hi << 32) | lo;
-                if (!bits) continue;
-                const unsigned pj = (unsigned)__builtin_amdgcn_readlane((int)ex, (int)j);
-                if ((bits >> lane) & 1ull) {
-                    const unsigned long long pos = obase + pj + lanes_below(bits);
-                    if (pos < cap) out[pos] = ibase + (w0 + j) * 64u + (unsigned)lane;
-                }
-            }
+            emit_words(mine, ex, obase, ibase + w0 * 64u, out, cap);
             obase += (unsigned)__builtin_amdgcn_readlane((int)incl, kWave - 1);
         }
     }
