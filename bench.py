@@ -62,6 +62,7 @@ def parse():
     p.add_argument("--no-e2e", action="store_true", help="skip the host-resident end-to-end line")
     p.add_argument("--no-pipelined", action="store_true", help="skip the multi-stream pipelined line")
     p.add_argument("--pipeline-streams", type=int, default=2, help="contexts / HIP streams of the pipelined line")
+    p.add_argument("--check", action="store_true", help="N > 1 kNN / C5: check the merged top-k against rank 0's full window")
     p.add_argument("--time-every", type=int, default=8,
                    help="bracket every N-th timed step's kernels with HIP events (1 = all)")
     return p.parse_args()
@@ -145,6 +146,7 @@ class KnnWorkload(Workload):
     kernel = "geohip::knn_pass<16> (one launch per window: scan, block lists, last block's final selection)"
     grid_n, k, radius, n_default, seed0 = 100, 50, 0.5, 10_000_000, 2
     label = "C2: point-point kNN k=50, 100x100 Beijing UniformGrid, r=0.5, README query"
+    has_range = False
 
     def __init__(self, *a):
         super().__init__(*a)
@@ -157,31 +159,91 @@ class KnnWorkload(Workload):
         self.xs, self.ys = _uniform_windows(self.ctx, self.dev, self.n, self.rank,
                                             [self.seed0 + 7919 * w for w in range(self.windows)], bj)
         K, W, dev = self.k, self.world, self.dev
-        self.out_i = torch.empty(K, dtype=torch.int32, device=dev)
-        self.out_d = torch.empty(K, dtype=torch.float64, device=dev)
+        # Per step, rank r's result goes out in ONE packed all-gather row: [k dist (f64 as 2k
+        # int32) | k idx (int32) | range count (int64 as 2 int32, C5)]; the kNN pass writes straight
+        # into views of the row.  Two rows alternate so the all-gather + merge of window i (on the
+        # communication stream) overlaps the scan of window i + 1 (on the compute stream).
+        self.row = 3 * K + 2 + (K & 1)
+        self.pack = [torch.zeros(self.row, dtype=torch.int32, device=dev) for _ in range(2)]
+        self.out_d = [p[:2 * K].view(torch.float64) for p in self.pack]
+        self.out_i = [p[2 * K:3 * K] for p in self.pack]
+        self.out_rc = [p[3 * K + (K & 1):].view(torch.int64) for p in self.pack]
         self.cnt = torch.zeros(2, dtype=torch.int32, device=dev)
-        self.g_d = torch.empty((W, K), dtype=torch.float64, device=dev)
-        self.g_i = torch.empty((W, K), dtype=torch.int32, device=dev)
         self.m_i = torch.empty(K, dtype=torch.int32, device=dev)
         self.m_d = torch.empty(K, dtype=torch.float64, device=dev)
-        self.base = torch.tensor(self.rank * self.n, dtype=torch.int64, device=dev)
+        self.mcnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.counts = torch.zeros(W, dtype=torch.int64, device=dev)
+        self.host_staged = W > 1 and self.dist.get_backend() == "gloo"
+        if W > 1:
+            from spatialflink_amd import Context
+            self.g = [torch.empty(W * self.row, dtype=torch.int32, device=dev) for _ in range(2)]
+            self.offs = (torch.arange(W, dtype=torch.int32, device=dev) * self.n).view(W, 1)  # shard bases
+            self.cs = torch.cuda.Stream(dev)
+            self.mctx = Context(dev.index)  # merges on the communication stream
+            self.ev_scan = [torch.cuda.Event() for _ in range(2)]
+            self.ev_done = [None, None]
 
     def units_per_step(self):
         return self.n
 
-    def knn_step(self, w):
-        import torch
+    def scan(self, w, j):
         self.ctx.knn_pp_async(self.grid, self.xs[w], self.ys[w], self.q[0], self.q[1], self.radius, self.k,
-                              self.out_i, self.out_d, self.cnt[0:1])
-        if self.world > 1:
-            gi = torch.where(self.out_i >= 0, (self.out_i.to(torch.int64) + self.base).to(torch.int32), self.out_i)
-            self.dist.all_gather_into_tensor(self.g_d.view(-1), self.out_d)
-            self.dist.all_gather_into_tensor(self.g_i.view(-1), gi)
-            self.ctx.knn_merge_async(self.g_d, self.g_i, self.world, self.k, self.k, self.m_i, self.m_d,
-                                     self.cnt[1:2])
+                              self.out_i[j], self.out_d[j], self.cnt[0:1])
+
+    def gather_merge(self, j):
+        """All-gather of the ranks' packed rows, then every rank merges the W top-k lists
+        (geohip_knn_merge_async; the reference's parallelism-1 windowAll funnel,
+        PointPointKNNQuery.java:188-190) -- all on the communication stream."""
+        import torch
+        K, W = self.k, self.world
+        if self.host_staged:  # gloo (functional rehearsal of the N > 1 path on one GPU): via host
+            gh = torch.empty(W * self.row, dtype=torch.int32)
+            self.dist.all_gather_into_tensor(gh, self.pack[j].cpu())
+            self.g[j].copy_(gh)
+        else:
+            self.dist.all_gather_into_tensor(self.g[j], self.pack[j])
+        g = self.g[j].view(W, self.row)
+        gd = g[:, :2 * K].contiguous().view(torch.float64)
+        gi = g[:, 2 * K:3 * K]
+        gi = torch.where(gi >= 0, gi + self.offs, gi).contiguous()  # window ids; -1 sentinels stay
+        self.mctx.knn_merge_async(gd, gi, W, K, K, self.m_i, self.m_d, self.mcnt)
+        if self.has_range:
+            self.counts.copy_(g[:, 3 * K + (K & 1):].contiguous().view(torch.int64).view(-1))
+
+    def check_merged(self, last_step):
+        """N > 1 (--check): the last step's merged top-k against the kNN of the whole
+        W * n-point window evaluated on rank 0 alone (the counter-based generator makes the
+        concatenated shards).  True / False on rank 0, None elsewhere."""
+        import torch
+        from spatialflink_amd import synth
+        torch.cuda.synchronize(self.dev)
+        if self.rank != 0:
+            return None
+        w = last_step % self.windows
+        N = self.n * self.world
+        x = torch.empty(N, dtype=torch.float64, device=self.dev)
+        y = torch.empty(N, dtype=torch.float64, device=self.dev)
+        self.ctx.synth_uniform_async(x, y, 0, self.seed0 + 7919 * w, synth.BEIJING)
+        wi, wd = self.ctx.knn_pp(self.grid, x, y, self.q[0], self.q[1], self.radius, self.k)
+        m = int(self.mcnt.item())
+        return (m == len(wi) and self.m_i[:m].cpu().numpy().astype(np.uint32).tolist() ==
+                wi.cpu().numpy().astype(np.uint32).tolist() and
+                torch.equal(self.m_d[:m].cpu().view(torch.int64), wd.cpu().view(torch.int64)))
 
     def step(self, s):
-        self.knn_step(s % self.windows)
+        import torch
+        j = s & 1
+        if self.world > 1 and self.ev_done[j] is not None:
+            torch.cuda.current_stream(self.dev).wait_event(self.ev_done[j])  # row j free again
+        self.scan(s % self.windows, j)
+        if self.world > 1:
+            self.ev_scan[j].record(torch.cuda.current_stream(self.dev))
+            with torch.cuda.stream(self.cs):
+                self.cs.wait_event(self.ev_scan[j])
+                self.gather_merge(j)
+                ev = torch.cuda.Event()
+                ev.record(self.cs)
+                self.ev_done[j] = ev
 
     def algorithmic_bytes(self):
         return BYTES_PER_POINT * self.n
@@ -305,16 +367,33 @@ class RangeWorkload(Workload):
         self.cnt = torch.zeros(self.windows, dtype=torch.int64, device=self.dev)
         self.counts = torch.zeros(self.world, dtype=torch.int64, device=self.dev)
         self.hits = None
+        self.cs = torch.cuda.Stream(self.dev) if self.world > 1 else None
+        self.done = [None] * self.windows
 
     def units_per_step(self):
         return self.n
 
     def step(self, s):
+        import torch
         w = s % self.windows
+        cur = torch.cuda.current_stream(self.dev)
+        if self.world > 1 and self.done[w] is not None:
+            cur.wait_event(self.done[w])  # window w's count slot gathered
         self.ctx.range_pp_async(self.grid, self.xs[w], self.ys[w], self.q[0], self.q[1], self.radius, False,
                                 self.out, self.n, self.cnt[w:w + 1])
-        if self.world > 1:  # result gather: every rank learns each shard's hit count (offsets)
-            self.dist.all_gather_into_tensor(self.counts, self.cnt[w:w + 1])
+        if self.world > 1:  # result gather: every rank learns each shard's hit count (offsets), on the
+            ev = torch.cuda.Event()  # communication stream, overlapping the next window's pass
+            ev.record(cur)
+            with torch.cuda.stream(self.cs):
+                self.cs.wait_event(ev)
+                if self.dist.get_backend() == "gloo":
+                    ch = torch.empty(self.world, dtype=torch.int64)
+                    self.dist.all_gather_into_tensor(ch, self.cnt[w:w + 1].cpu())
+                    self.counts.copy_(ch)
+                else:
+                    self.dist.all_gather_into_tensor(self.counts, self.cnt[w:w + 1])
+                self.done[w] = torch.cuda.Event()
+                self.done[w].record(self.cs)
 
     def algorithmic_bytes(self):
         if self.hits is None:
@@ -648,32 +727,24 @@ class C5Workload(KnnWorkload):
     kernel = "geohip::knn_pass<16, range> (kNN k=100 + range r=0.05 in one pass: one launch per step)"
     grid_n, k, radius, n_default, seed0 = 1000, 100, 0.05, 25_000_000, 7
     windows = 2
+    has_range = True
     label = "C5 shard: kNN k=100 + range r=0.05, 1000x1000 Beijing UniformGrid, README query"
 
     def __init__(self, *a):
         super().__init__(*a)
         import torch
         self.rout = torch.empty(self.n, dtype=torch.int32, device=self.dev)
-        self.rcnt = torch.zeros(1, dtype=torch.int64, device=self.dev)
-        self.counts = torch.zeros(self.world, dtype=torch.int64, device=self.dev)
         self.hits = None
 
-    def step(self, s):
-        import torch
-        w = s % self.windows
+    def scan(self, w, j):
+        # the range hit count rides in the packed row: one all-gather carries the top-k and the
+        # counts (the ranks' output offsets of the concatenated range result)
         self.ctx.knn_range_pp_async(self.grid, self.xs[w], self.ys[w], self.q[0], self.q[1], self.radius, self.k, False,
-                                    self.out_i, self.out_d, self.cnt[0:1], self.rout, self.n, self.rcnt)
-        if self.world > 1:
-            gi = torch.where(self.out_i >= 0, (self.out_i.to(torch.int64) + self.base).to(torch.int32), self.out_i)
-            self.dist.all_gather_into_tensor(self.g_d.view(-1), self.out_d)
-            self.dist.all_gather_into_tensor(self.g_i.view(-1), gi)
-            self.ctx.knn_merge_async(self.g_d, self.g_i, self.world, self.k, self.k, self.m_i, self.m_d,
-                                     self.cnt[1:2])
-            self.dist.all_gather_into_tensor(self.counts, self.rcnt)
+                                    self.out_i[j], self.out_d[j], self.cnt[0:1], self.rout, self.n, self.out_rc[j])
 
     def algorithmic_bytes(self):  # per step: the shard read once (16 B/pt) + the range hits written
         if self.hits is None:
-            self.hits = float(self.rcnt.item())
+            self.hits = float(self.out_rc[0].item())
         return BYTES_PER_POINT * self.n + 4 * self.hits
 
     def config(self):
@@ -777,11 +848,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # GEOHIP_BENCH_ONE_DEVICE=1 + GEOHIP_BENCH_BACKEND=gloo: every rank on cuda:0 with host-staged
+    # collectives -- a functional rehearsal of the N > 1 path on a one-GPU box (not a measurement)
+    if os.environ.get("GEOHIP_BENCH_ONE_DEVICE") == "1":
+        local = 0
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("GEOHIP_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(local)
 
@@ -815,7 +894,7 @@ def main():
     ctx.set_timing(False)
     kern_ms, launches = ctx.timing(reset=True)
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -851,6 +930,10 @@ def main():
                                    "frac": tf / FP64_PEAK_TFLOPS, "flops": flops,
                                    "source": "rocprofv3 SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes of the timed kernels per step "
                                              "(profiles/pmc_" + wl.tag + ".json) / the live average step time"}
+    if args.check and world > 1 and hasattr(wl, "check_merged"):
+        ok = wl.check_merged(args.warmup + args.steps - 1)
+        if rank == 0:
+            result["merged_matches_full_window"] = ok
     if rank == 0 and world == 1 and not args.no_e2e and args.workload == "knn":  # the C2 host path
         e2e = wl.e2e()
         if e2e is not None:
