@@ -224,6 +224,141 @@ __device__ __forceinline__ int fast_csv(const uint8_t* __restrict__ s, uint32_t 
     return ingest::kFallback;
 }
 
+// ---- SWAR form of fast_csv: a field is read as one 24-byte window (three u64 words from the
+// staged LDS bytes), its digits / delimiter found from per-byte masks and its value converted
+// eight digits at a time, instead of a per-lane loop with a dependent LDS read and a branch per
+// byte.  It accepts a subset of fast_csv's records (fields within their 24-byte windows, at most
+// 19 digits per number counting leading zeros, the record starting 112 bytes or more before the
+// staged end) and gives the same (w, q) decimal -- so the same Eisel-Lemire bits -- and the same
+// Long; anything else returns kSwarNo and fast_csv (then the general parser) decides as before.
+constexpr int kSwarNo = 2;
+constexpr uint32_t kSwarRecordSpan = 112;  // staged bytes a record start needs ahead of it (72 + 32 + 8)
+constexpr uint32_t kSwarFieldSpan = 72;    // the last field start within a record's span
+
+struct Win24 {
+    uint64_t v[3];
+    __device__ __forceinline__ uint32_t byte(uint32_t k) const {
+        const uint64_t w = k < 8 ? v[0] : (k < 16 ? v[1] : v[2]);
+        return (uint32_t)(w >> ((k & 7u) * 8u)) & 0xffu;
+    }
+    // 8 bytes starting at window offset off (0 <= off <= 16; bytes past the window read as 0)
+    __device__ __forceinline__ uint64_t get8(uint32_t off) const {
+        const uint64_t lo = off < 8 ? v[0] : (off < 16 ? v[1] : v[2]);
+        const uint64_t hi = off < 8 ? v[1] : (off < 16 ? v[2] : 0ull);
+        const uint32_t sh = (off & 7u) * 8u;
+        return (lo >> sh) | ((hi << 1) << (63u - sh));
+    }
+};
+
+__device__ __forceinline__ Win24 lds_win24(const uint8_t* __restrict__ s, uint32_t p) {
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(s + (p & ~7u));
+    const uint64_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
+    const uint32_t sh = (p & 7u) * 8u;
+    Win24 r;
+    r.v[0] = (w0 >> sh) | ((w1 << 1) << (63u - sh));
+    r.v[1] = (w1 >> sh) | ((w2 << 1) << (63u - sh));
+    r.v[2] = (w2 >> sh) | ((w3 << 1) << (63u - sh));
+    return r;
+}
+
+// bit 7 of every byte -> one bit per byte (byte i -> bit i)
+__device__ __forceinline__ uint32_t byte_bits(uint64_t m) {
+    return (uint32_t)((((m >> 7) & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
+}
+// per-byte masks, exact for every byte (no carry or borrow crosses a byte)
+__device__ __forceinline__ uint64_t nondigit_m(uint64_t v) {
+    const uint64_t x = v ^ 0x3030303030303030ull;
+    return (((x & 0x7f7f7f7f7f7f7f7full) + 0x7676767676767676ull) | x) & 0x8080808080808080ull;
+}
+__device__ __forceinline__ uint64_t eq_m(uint64_t v, uint32_t c) {  // byte == c
+    const uint64_t x = v ^ (0x0101010101010101ull * c);
+    return ~((((x & 0x7f7f7f7f7f7f7f7full) + 0x7f7f7f7f7f7f7f7full) | x)) & 0x8080808080808080ull;
+}
+__device__ __forceinline__ uint64_t le20_m(uint64_t v) {  // byte <= 0x20
+    return ~((((v & 0x7f7f7f7f7f7f7f7full) + 0x5f5f5f5f5f5f5f5full) | v)) & 0x8080808080808080ull;
+}
+__device__ __forceinline__ uint32_t mask24(uint64_t a, uint64_t b, uint64_t c) {
+    return byte_bits(a) | (byte_bits(b) << 8) | (byte_bits(c) << 16);
+}
+// value of m <= 8 ASCII digits starting at window offset off
+__device__ __forceinline__ uint64_t digits8(const Win24& W, uint32_t off, uint32_t m) {
+    uint64_t x = W.get8(off) - 0x3030303030303030ull;  // digit bytes are the low m: no borrow into them
+    x = m ? (x << (8u * (8u - m))) : 0ull;
+    x = ((x & 0x0f0f0f0f0f0f0f0full) * 2561ull) >> 8;
+    x = ((x & 0x00ff00ff00ff00ffull) * 6553601ull) >> 16;
+    return ((x & 0x0000ffff0000ffffull) * 42949672960001ull) >> 32;
+}
+__device__ __forceinline__ uint64_t digits_n(const Win24& W, uint32_t off, uint32_t n) {  // n <= 19
+    constexpr uint64_t p8 = 100000000ull;
+    if (n <= 8) return digits8(W, off, n);
+    if (n <= 16) return digits8(W, off, n - 8) * p8 + digits8(W, off + n - 8, 8);
+    return (digits8(W, off, n - 16) * p8 + digits8(W, off + n - 16, 8)) * p8 + digits8(W, off + n - 8, 8);
+}
+__device__ const uint64_t kPow10u[20] = {1ull, 10ull, 100ull, 1000ull, 10000ull, 100000ull, 1000000ull,
+                                         10000000ull, 100000000ull, 1000000000ull, 10000000000ull,
+                                         100000000000ull, 1000000000000ull, 10000000000000ull,
+                                         100000000000000ull, 1000000000000000ull, 10000000000000000ull,
+                                         100000000000000000ull, 1000000000000000000ull,
+                                         10000000000000000000ull};
+
+__device__ __forceinline__ int swar_csv(const uint8_t* __restrict__ s, uint32_t p, uint32_t lim,
+                                        const ingest::Spec& sp, ingest::Parsed* o) {
+    if (p + kSwarRecordSpan > lim) return kSwarNo;
+    const uint32_t p0 = p;
+    const uint32_t d = (uint32_t)(uint8_t)sp.delim;
+    int need = sp.fx > sp.fy ? sp.fx : sp.fy;
+    if (sp.fts > need) need = sp.fts;
+    for (int f = 0; f <= need; f++) {
+        if (p - p0 > kSwarFieldSpan) return kSwarNo;
+        const Win24 W = lds_win24(s, p);
+        const bool isx = f == sp.fx, isy = f == sp.fy, ist = f == sp.fts;
+        uint32_t term;
+        if (isx || isy || ist) {
+            if ((isx || isy) && ist) return kSwarNo;
+            const uint32_t st = W.byte(0) == '-' ? 1u : 0u;
+            const uint32_t nd = mask24(nondigit_m(W.v[0]), nondigit_m(W.v[1]), nondigit_m(W.v[2]));
+            const uint32_t m1 = nd >> st;
+            if (!m1) return kSwarNo;
+            const uint32_t e1 = st + (uint32_t)__builtin_ctz(m1);
+            const uint32_t ni = e1 - st;
+            uint32_t nf = 0;
+            term = e1;
+            if (!ist && W.byte(e1) == '.') {
+                const uint32_t m2 = e1 + 1 < 24 ? nd >> (e1 + 1) : 0u;
+                if (!m2) return kSwarNo;
+                term = e1 + 1 + (uint32_t)__builtin_ctz(m2);
+                nf = term - e1 - 1;
+                if (nf == 0) return kSwarNo;
+            }
+            if (ni == 0 || ni + nf > 19 || (ist && ni > 18)) return kSwarNo;
+            const uint64_t iv = digits_n(W, st, ni);
+            if (ist) {
+                o->ts = st ? -(int64_t)iv : (int64_t)iv;
+            } else {
+                const uint64_t w = nf ? iv * kPow10u[nf] + digits_n(W, e1 + 1, nf) : iv;
+                const uint64_t bits = ingest::decimal_to_bits(w, -(int32_t)nf) | (st ? 1ull << 63 : 0ull);
+                const double v = __builtin_bit_cast(double, bits);
+                if (isx) o->x = v;
+                if (isy) o->y = v;
+            }
+        } else {
+            const uint32_t stop = mask24(eq_m(W.v[0], d) | le20_m(W.v[0]) | eq_m(W.v[0], '"'),
+                                         eq_m(W.v[1], d) | le20_m(W.v[1]) | eq_m(W.v[1], '"'),
+                                         eq_m(W.v[2], d) | le20_m(W.v[2]) | eq_m(W.v[2], '"'));
+            if (!stop) return kSwarNo;
+            term = (uint32_t)__builtin_ctz(stop);
+        }
+        const uint32_t c = W.byte(term);
+        if (c == d && f < need) {
+            p += term + 1;
+            continue;
+        }
+        if (f == need && (c == d || c == '\n')) return ingest::kOk;
+        return kSwarNo;
+    }
+    return kSwarNo;
+}
+
 __global__ __launch_bounds__(kThreads) void ingest_parse(const uint8_t* __restrict__ text, uint64_t nbytes,
                                                         IngestArgs a, const unsigned long long* __restrict__ chunk_base,
                                                         double* __restrict__ x, double* __restrict__ y,
@@ -267,8 +402,12 @@ __global__ __launch_bounds__(kThreads) void ingest_parse(const uint8_t* __restri
             o.x = o.y = (double)s_start[i];
             rc = ingest::kOk;
         } else {
-            rc = fast ? fast_csv(reinterpret_cast<const uint8_t*>(s_text4), s_start[i], stage_len, a.spec, &o, a.pad)
-                      : ingest::kFallback;
+            const uint8_t* st8 = reinterpret_cast<const uint8_t*>(s_text4);
+            rc = ingest::kFallback;
+            if (fast) {
+                rc = a.pad == 0 ? swar_csv(st8, s_start[i], stage_len, a.spec, &o) : kSwarNo;
+                if (rc == kSwarNo) rc = fast_csv(st8, s_start[i], stage_len, a.spec, &o, a.pad);
+            }
             if (rc != ingest::kOk) rc = ingest::parse_record(rd, c0 + s_start[i], a.spec, &o);
         }
         if (rc != ingest::kOk) {

@@ -80,6 +80,57 @@ def _ragged_csv(n, seed):
     return "\n".join(lines).encode()
 
 
+def _fast_forms_csv(n, seed):
+    """Records the CSV fast paths take (no blanks or quotes): numbers of every length around the
+    SWAR window (19 / 20 digits, 23-25 chars), leading zeros, signs, a bare integer, '-0.0',
+    timestamps up to 18 digits (19 are outside the device grammar), object ids of 1 to 30
+    characters; plus a few the fast paths hand on (exponent, trailing 'd')."""
+    rng = random.Random(seed)
+    lines = []
+    for i in range(n):
+        x = rng.uniform(115.4, 117.7)
+        y = rng.uniform(39.5, 41.2)
+        k = rng.randrange(14)
+        if k == 0:
+            xs, ys = repr(x), repr(-y)
+        elif k == 1:
+            nd = rng.randrange(0, 21)
+            xs, ys = f"{x:.{nd}f}", f"{y:.{rng.randrange(0, 21)}f}"
+        elif k == 2:
+            xs, ys = "00" + f"{x:.10f}", "0.000" + str(rng.randrange(10 ** 12))
+        elif k == 3:
+            xs, ys = "-0.0", "0"
+        elif k == 4:
+            xs, ys = f"{x:.16f}", f"{y:.17f}"  # 19 and 19 digits
+        elif k == 5:
+            xs, ys = f"{x:.17f}", f"{y:.18f}"  # 20 digits: past the SWAR limit
+        elif k == 6:
+            xs, ys = "1" * rng.randrange(1, 20), "9" * rng.randrange(1, 20)
+        elif k == 7:
+            xs, ys = f"{x:.22f}", f"{y:.21f}"  # 25 / 23 characters
+        elif k == 8:
+            xs, ys = f"{x:e}", f"{y!r}"
+        elif k == 9:
+            xs, ys = f"{x!r}d", f"{y:E}"
+        else:
+            xs, ys = repr(x), repr(y)
+        tsv = rng.choice([1611022449423 + i, -(10 ** 17) - i, 10 ** 17 + i, 10 ** 18 - 1 - i, 0])  # <= 18 digits
+        oid = "".join(rng.choice("abcdef0123456789") for _ in range(rng.randrange(1, 31)))
+        lines.append(f"{oid},{tsv},{xs},{ys}")
+    return "\n".join(lines).encode()
+
+
+def test_csv_fast_path_forms(ctx):
+    text = _fast_forms_csv(60000, 5)
+    g, cg = _grids()
+    spec = cref.ingest_spec(cref.CSV, ",", 2, 3, 1)
+    want = cref.ingest(spec, text, cg)
+    got = ctx.ingest_points(_abi.make_ingest_spec(cref.CSV, ",", 2, 3, 1), text, g, with_ts=True, with_cell=True)
+    assert np.array_equal(got["x"].view(np.uint64), want["x"].view(np.uint64))
+    assert np.array_equal(got["y"].view(np.uint64), want["y"].view(np.uint64))
+    assert np.array_equal(got["ts"], want["ts"])
+
+
 def test_csv_ragged(ctx):
     assert _check(ctx, cref.CSV, _ragged_csv(50000, 1)) == 50000
 
