@@ -13,7 +13,7 @@ namespace geohip {
 
 // Bytes of text owned by one block (its records are those whose preceding '\n' lies in the
 // chunk), and the LDS bytes staged past the chunk for records that straddle its end.
-constexpr uint32_t kIngestChunk = 8192;
+constexpr uint32_t kIngestChunk = 16384;
 constexpr uint32_t kIngestTail = 4096;
 
 struct IngestArgs {

@@ -8,7 +8,7 @@
 // (spatialObjects/Point.java:60-66 -> utils/HelperClass.java:104-116).
 //
 // Three launches per batch, all HBM-streaming:
-//   ingest_count  every block counts the record starts its 8 KB chunk owns (SWAR '\n' test on
+//   ingest_count  every block counts the record starts its 16 KB chunk owns (SWAR '\n' test on
 //                 16-byte loads);
 //   ingest_scan   one block turns the per-chunk counts into record bases (the record index of
 //                 a record is its position in the batch, as in the arrival-ordered stream);
@@ -25,7 +25,7 @@
 namespace geohip {
 namespace {
 
-constexpr int kThreads = 256;
+constexpr int kThreads = (int)(kIngestChunk / 32);  // 512: 32 bytes per thread
 constexpr uint32_t kBytesPerThread = kIngestChunk / kThreads;  // 32: two 16-byte loads
 static_assert(kBytesPerThread == 32, "chunk layout");
 
