@@ -823,8 +823,10 @@ __device__ __forceinline__ void jstage_flush(const JoinRun& a, uint2* st, unsign
     for (unsigned t = (unsigned)lane_id(); t < cnt; t += kWave) {
         const unsigned long long p = pos + t;
         if (p < a.cap) {
-            if (a.aligned8) {
-                reinterpret_cast<uint2*>(a.out)[p] = st[t];
+            if (a.aligned8) {  // streaming pair stores: nontemporal (no reuse on this device)
+                const uint2 v = st[t];
+                __builtin_nontemporal_store(((unsigned long long)v.y << 32) | v.x,
+                                            reinterpret_cast<unsigned long long*>(a.out) + p);
             } else {
                 a.out[2 * p] = st[t].x;
                 a.out[2 * p + 1] = st[t].y;
