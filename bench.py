@@ -313,7 +313,7 @@ class KnnWorkload(Workload):
             # the last window of each context against the sequential path
             same = True
             for j in range(nstreams):
-                i = windows - nstreams + j
+                i = windows - 1 - ((windows - 1 - j) % nstreams)  # context j's last window
                 wi, _ = self.ctx.knn_pp(self.grid, self.xs[i % self.windows], self.ys[i % self.windows],
                                         self.q[0], self.q[1], self.radius, self.k)
                 same = same and outs[j][0].cpu().numpy().astype(np.uint32).tolist() == \
