@@ -61,7 +61,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true", help="skip the host-resident end-to-end line")
     p.add_argument("--no-pipelined", action="store_true", help="skip the multi-stream pipelined line")
-    p.add_argument("--pipeline-streams", type=int, default=2, help="contexts / HIP streams of the pipelined line")
+    p.add_argument("--pipeline-streams", type=int, default=3, help="contexts / HIP streams of the pipelined line")
     p.add_argument("--check", action="store_true", help="N > 1 kNN / C5: check the merged top-k against rank 0's full window")
     p.add_argument("--time-every", type=int, default=8,
                    help="bracket every N-th timed step's kernels with HIP events (1 = all)")
