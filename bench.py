@@ -289,9 +289,10 @@ class KnnWorkload(Workload):
         from spatialflink_amd import Context
         ctxs = [self.ctx] + [Context(self.dev.index) for _ in range(nstreams - 1)]
         streams = [torch.cuda.Stream(self.dev) for _ in ctxs]
-        outs = [(torch.empty(self.k, dtype=torch.int32, device=self.dev),
-                 torch.empty(self.k, dtype=torch.float64, device=self.dev),
-                 torch.zeros(1, dtype=torch.int32, device=self.dev)) for _ in ctxs]
+        # every window writes its own result slot, so every window is checked afterwards
+        oi = torch.empty((windows, self.k), dtype=torch.int32, device=self.dev)
+        od = torch.empty((windows, self.k), dtype=torch.float64, device=self.dev)
+        oc = torch.zeros(windows, dtype=torch.int32, device=self.dev)
         old = self.ctx._bound
         try:
             for c in ctxs:
@@ -302,22 +303,25 @@ class KnnWorkload(Workload):
                     j = i % nstreams
                     with torch.cuda.stream(streams[j]):
                         ctxs[j].knn_pp_async(self.grid, self.xs[i % self.windows], self.ys[i % self.windows],
-                                             self.q[0], self.q[1], self.radius, self.k, *outs[j])
+                                             self.q[0], self.q[1], self.radius, self.k, oi[i], od[i], oc[i:i + 1])
             torch.cuda.synchronize(self.dev)
             run(16)
             torch.cuda.synchronize(self.dev)
+            oi.fill_(-7)
+            od.fill_(-7.0)
             t0 = time.perf_counter()
             run(windows)
             torch.cuda.synchronize(self.dev)
             t = (time.perf_counter() - t0) / windows
-            # the last window of each context against the sequential path
-            same = True
-            for j in range(nstreams):
-                i = windows - 1 - ((windows - 1 - j) % nstreams)  # context j's last window
-                wi, _ = self.ctx.knn_pp(self.grid, self.xs[i % self.windows], self.ys[i % self.windows],
-                                        self.q[0], self.q[1], self.radius, self.k)
-                same = same and outs[j][0].cpu().numpy().astype(np.uint32).tolist() == \
-                    wi.cpu().numpy().astype(np.uint32).tolist()
+            # every window against the sequential path of the same window: indices and distance bits
+            ref = []
+            for w in range(self.windows):
+                wi, wd = self.ctx.knn_pp(self.grid, self.xs[w], self.ys[w], self.q[0], self.q[1], self.radius, self.k)
+                ref.append((wi.cpu().numpy().astype(np.uint32), wd.cpu().numpy().view(np.uint64)))
+            gi = oi.cpu().numpy().astype(np.uint32)
+            gd = od.cpu().numpy().view(np.uint64)
+            same = all(np.array_equal(gi[i], ref[i % self.windows][0]) and np.array_equal(gd[i], ref[i % self.windows][1])
+                       for i in range(windows))
         finally:
             for c in ctxs[1:]:
                 c.close()
@@ -325,7 +329,7 @@ class KnnWorkload(Workload):
         return {"value": self.n / t, "unit": "points/sec", "us_per_window": t * 1e6,
                 "hbm_GBps": BYTES_PER_POINT * self.n / t / 1e9,
                 "hbm_frac": BYTES_PER_POINT * self.n / t / 1e9 / HBM_PEAK_GBS, "streams": nstreams, "windows": windows,
-                "matches_sequential": same}
+                "matches_sequential": same, "checked": "every window: indices and distance bits"}
 
     def cpu_baseline(self, seconds):
         cref = _oracle()

@@ -69,9 +69,10 @@ extern "C" {
 #define GEOHIP_MEM_HOST 0
 #define GEOHIP_MEM_DEVICE 1
 
-/* Largest k of the point kNN (PointPointKNNQuery's k) and of the rank merge. */
+/* Every k >= 1 is served (PointPointKNNQuery.java:33 / PointPolygonKNNQuery.java:34 take any
+   Integer k).  Up to these values one pass selects the k nearest in one workgroup's LDS; above
+   them the candidates are compacted, radix-selected and sorted (the large-k form). */
 #define GEOHIP_KNN_MAX_K 1024
-/* Largest k of the point-polygon kNN (PointPolygonKNNQuery's k). */
 #define GEOHIP_KNN_PPOLY_MAX_K 256
 
 typedef struct geohip_ctx geohip_ctx;
@@ -144,8 +145,8 @@ int geohip_join_pp_count_only(geohip_ctx* ctx, const geohip_grid* grid_data, con
    vertices vx/vy[ring_off[j] .. ring_off[j+1]) -- the List<List<Coordinate>> given to
    Polygon(List<List<Coordinate>>, UniformGrid) (Polygon.java:52-66, 115-165): one ring is closed
    here if open and needs > 3 coords; several rings are padded and closed each, the largest JTS
-   area becomes the shell and the others its holes, in createPolygonArray's order.  At most 64
-   rings per polygon (GEOHIP_ERR_UNSUPPORTED).  Where the reference throws (an empty ring, a ring
+   area becomes the shell and the others its holes, in createPolygonArray's order.  Up to 65535
+   rings per polygon.  Where the reference throws (an empty ring, a ring
    whose first coordinate is NaN: LinearRing not closed) or leaves the polygon null (first ring
    with <= 3 coords): GEOHIP_ERR_ARG.  npoly == 0: no pairs, the polygon arrays may be NULL.
    Distances: JTS point.distance(polygon) -- 0 inside the shell and outside every hole, or on any
@@ -171,7 +172,7 @@ int geohip_join_ppoly(geohip_ctx* ctx, const geohip_grid* grid_points, const geo
    the polygon's G u C cells (no radius filter); distance = JTS point.distance(polygon), or the
    bbox distance (DistanceFunctions.java:150-200) when approximate.  Output: the
    min(k, candidates) smallest (distance, idx) ascending by distance bits then idx (a NaN bbox
-   distance ranks after +Infinity); 1 <= k <= GEOHIP_KNN_PPOLY_MAX_K. */
+   distance ranks after +Infinity); any k >= 1. */
 int geohip_knn_ppoly(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
                      uint64_t n, const uint32_t* ring_off, uint32_t nring, const double* vx,
                      const double* vy, double r, uint32_t k, int approximate,
@@ -186,7 +187,7 @@ int geohip_knn_pp_async(geohip_ctx* ctx, const geohip_grid* grid, const double* 
 /* Merge nlists sorted (dist, idx) lists of list_len entries (e.g. the all-gathered per-shard
    kNN results) into the k smallest; same output convention as geohip_knn_pp_async.
    idx values are taken as global ids (shards add their base offset before the gather).
-   k <= GEOHIP_KNN_MAX_K; above 256, nlists * list_len <= 8192. */
+   Any k >= 1 and list count (fewer than 2^32 entries in all). */
 int geohip_knn_merge_async(geohip_ctx* ctx, const double* dist, const uint32_t* idx, uint32_t nlists,
                            uint32_t list_len, uint32_t k, uint32_t* out_idx, double* out_dist,
                            uint32_t* out_count_dev);
@@ -211,16 +212,50 @@ int geohip_band_pack_async(geohip_ctx* ctx, const geohip_grid* grid_data, int32_
                            const double* x, const double* y, uint64_t n, int64_t base, double* out_x,
                            double* out_y, int64_t* out_idx, uint64_t* out_counts_dev);
 
-/* ---- output codec ------------------------------------------------ */
-/* Serialization.PointToCSVTSVOutputSchema.serialize (spatialStreams/Serialization.java:98-152) for
-   m result points, as one text buffer: record j (point p = idx[j], or j when idx is NULL) is the
-   fields at positions 0..max(attr) -- objID (bytes oid_text[oid_off[p] .. oid_off[p+1]), or
-   "null" when oid_text is NULL), timeStampMillisec (Long.toString of ts[p], 0 when ts is NULL),
-   Double.toString(x[p]), Double.toString(y[p]) (JDK 8 FloatingDecimal), "0" at positions no
-   field names, a later attr winning a shared position -- each followed by delim, the last
-   character deleted, then '\n'.  rec_off (nullable, m + 1 entries) receives the record offsets.
-   Device memory only; *out_len (host) = the total bytes; GEOHIP_ERR_CAPACITY when above cap
-   (records that do not fit entirely are not written). */
+/* ---- output codecs ----------------------------------------------- */
+/* The point output schemas of spatialStreams/Serialization.java for m result points, as one text
+   buffer: record j is point p = idx[j] (or j when idx is NULL; p >= n is GEOHIP_ERR_ARG, e.g. a
+   padded kNN list's 0xffffffff sentinel), each record followed by '\n'.  The Point's fields:
+   objID = bytes oid_text[oid_off[p] .. oid_off[p+1]) (UTF-8; oid_text NULL: objID == null),
+   timeStampMillisec = ts[p] (ts NULL: 0), point.getX()/getY() = x[p]/y[p], doubles through JDK 8
+   Double.toString (FloatingDecimal).
+     GEOHIP_FMT_CSV     <- PointToCSVTSVOutputSchema.serialize  Serialization.java:125-150: the
+                           fields at positions 0..max(attr) (objID as "null" when null, Long.toString
+                           of the timestamp, "0" where no field is), each followed by delim, then
+                           deleteCharAt(length - 1) (one UTF-16 unit of the delimiter).
+     GEOHIP_FMT_WKT     <- PointToWKTOutputSchema.serialize     Serialization.java:72-92:
+                           "<objID><delim> POINT(<x> <y>)<delim> <date>"<delim>  (objID part only
+                           when not null, date part only when the timestamp is not 0).
+     GEOHIP_FMT_GEOJSON <- PointToGeoJSONOutputSchema.serialize Serialization.java:28-50: org.json
+                           20200518 (pom.xml:87-89) JSONObject.toString -- Java 8 HashMap key order,
+                           numberToString, quote -- i.e.
+                           {"geometry":{"coordinates":[x,y],"type":"Point"},"type":"Feature",
+                            "properties":{"oID":"..","timestamp":".."}}  (properties only when
+                           objID is not null or the timestamp is not 0).  A NaN / infinite
+                           coordinate is GEOHIP_ERR_ARG (JSONObject.toString returns null there).
+   The WKT / GeoJSON date is the caller's DateFormat: GEOHIP_DATE_YMD_HMS restates
+   SimpleDateFormat("yyyy-MM-dd HH:mm:ss") (conf/geoflink-conf.yml:15) in a zone of fixed offset
+   utc_offset_min; GEOHIP_DATE_NONE, or a year outside 1583..9999, makes a nonzero timestamp
+   GEOHIP_ERR_UNSUPPORTED.  The delimiter is the schema's effective SEPARATION (the `\\t` config
+   string is already mapped to the two characters `\t`, Serialization.java:62-66).
+   rec_off (nullable, m + 1 entries) receives the record offsets.  Device memory only; *out_len
+   (host) = the total bytes; GEOHIP_ERR_CAPACITY when above cap (records that do not fit entirely
+   are not written). */
+#define GEOHIP_DATE_NONE 0
+#define GEOHIP_DATE_YMD_HMS 1
+typedef struct geohip_text_out_spec {
+    int32_t format;                            /* GEOHIP_FMT_CSV / _WKT / _GEOJSON */
+    int32_t attr_oid, attr_ts, attr_x, attr_y; /* CSV: csvTsvSchemaAttr[0..3], each 0..63 */
+    int32_t delim_len;                         /* CSV / WKT: 1..8 bytes (UTF-8) */
+    char delim[8];
+    int32_t date_format;                       /* GEOHIP_DATE_* (WKT / GeoJSON) */
+    int32_t utc_offset_min;                    /* the DateFormat's zone: minutes east of UTC */
+} geohip_text_out_spec;
+int geohip_format_points(geohip_ctx* ctx, const geohip_text_out_spec* spec, const double* x,
+                         const double* y, uint64_t n, const int64_t* ts, const uint8_t* oid_text,
+                         const uint64_t* oid_off, const uint32_t* idx, uint64_t m, uint8_t* out,
+                         uint64_t cap, uint64_t* out_len, uint64_t* rec_off);
+/* The CSV/TSV schema alone (geohip_format_points with format GEOHIP_FMT_CSV). */
 typedef struct geohip_csv_out_spec {
     int32_t attr_oid, attr_ts, attr_x, attr_y; /* csvTsvSchemaAttr[0..3], each 0..63 */
     int32_t delim_len;                         /* 1..8 */
@@ -228,7 +263,7 @@ typedef struct geohip_csv_out_spec {
     int32_t reserved;
 } geohip_csv_out_spec;
 int geohip_format_points_csv(geohip_ctx* ctx, const geohip_csv_out_spec* spec, const double* x,
-                             const double* y, const int64_t* ts, const uint8_t* oid_text,
+                             const double* y, uint64_t n, const int64_t* ts, const uint8_t* oid_text,
                              const uint64_t* oid_off, const uint32_t* idx, uint64_t m, uint8_t* out,
                              uint64_t cap, uint64_t* out_len, uint64_t* rec_off);
 

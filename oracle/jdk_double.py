@@ -13,6 +13,8 @@ the big-integer test is not (10 S <= B + M), and a carry in roundup keeps the di
 """
 from __future__ import annotations
 
+import math
+
 import struct
 
 EXP_SHIFT = 52
@@ -280,4 +282,125 @@ def format_point_csv(oid, ts: int, x: float, y: float, attrs, delim: str) -> str
             parts.append("0")
         parts.append(delim)
     s = "".join(parts)
-    return s[:-1]
+    # StringBuffer.deleteCharAt(length - 1) removes one UTF-16 unit: a supplementary last
+    # character leaves its high surrogate, which String.getBytes(UTF_8) writes as '?'
+    return s[:-1] + ("?" if ord(s[-1]) > 0xFFFF else "")
+
+
+# ---------------------------------------------------------------- WKT / GeoJSON schemas ----
+def java_date_ymd_hms(ms: int, utc_offset_min: int = 0) -> str:
+    """SimpleDateFormat("yyyy-MM-dd HH:mm:ss").format(new Date(ms)) in a fixed-offset zone
+    (the proleptic Gregorian calendar of datetime equals GregorianCalendar from 1583 on)."""
+    import datetime
+    t = datetime.datetime(1970, 1, 1) + datetime.timedelta(milliseconds=ms + utc_offset_min * 60000)
+    if not 1583 <= t.year <= 9999:
+        raise ValueError("outside the supported years")
+    return t.strftime("%Y-%m-%d %H:%M:%S")
+
+
+def format_point_wkt(oid, ts: int, x: float, y: float, delim: str, utc_offset_min: int = 0) -> str:
+    """PointToWKTOutputSchema.serialize (Serialization.java:72-92)."""
+    buf = ['"']
+    if oid is not None:
+        buf += [oid, delim + " "]
+    buf += ["POINT(", java_double_to_string(x), " ", java_double_to_string(y), ")"]
+    if ts != 0:
+        buf += [delim + " ", java_date_ymd_hms(ts, utc_offset_min)]
+    buf += ['"', delim]
+    return "".join(buf)
+
+
+def java_string_hash(s: str) -> int:
+    """String.hashCode over the UTF-16 units."""
+    h = 0
+    for u in _utf16_units(s):
+        h = (31 * h + u) & 0xFFFFFFFF
+    return h
+
+
+def _utf16_units(s: str):
+    b = s.encode("utf-16-be")
+    return [int.from_bytes(b[i:i + 2], "big") for i in range(0, len(b), 2)]
+
+
+def java8_hashmap_order(keys):
+    """Iteration order of a java.util.HashMap (Java 8) after putting `keys` in order into a
+    default-constructed map: table of 16 buckets (no resize below 13 entries), bucket index
+    (h ^ (h >>> 16)) & 15, insertion order inside a bucket."""
+    assert len(keys) <= 12
+    buckets = {}
+    for k in keys:
+        h = java_string_hash(k)
+        buckets.setdefault((h ^ (h >> 16)) & 15, []).append(k)
+    return [k for b in sorted(buckets) for k in buckets[b]]
+
+
+def json_number_to_string(d: float) -> str:
+    """org.json JSONObject.numberToString(Double) (20200518): non-finite throws; Double.toString
+    with trailing zeros and then a trailing '.' shaved when it has a '.' and no exponent."""
+    if math.isnan(d) or math.isinf(d):
+        raise ValueError("JSON does not allow non-finite numbers.")
+    s = java_double_to_string(d)
+    if s.find(".") > 0 and "e" not in s and "E" not in s:
+        s = s.rstrip("0")
+        if s.endswith("."):
+            s = s[:-1]
+    return s
+
+
+def json_quote(s: str) -> str:
+    """org.json JSONObject.quote over the UTF-16 units of s."""
+    if not s:
+        return '""'
+    out = ['"']
+    prev = 0
+    # code points; a supplementary one is a surrogate pair in Java, never in an escaped range
+    for ch in s:
+        c = ord(ch)
+        if ch in ('\\', '"'):
+            out.append("\\" + ch)
+        elif ch == "/":
+            out.append("\\/" if prev == ord("<") else "/")
+        elif ch == "\b":
+            out.append("\\b")
+        elif ch == "\t":
+            out.append("\\t")
+        elif ch == "\n":
+            out.append("\\n")
+        elif ch == "\f":
+            out.append("\\f")
+        elif ch == "\r":
+            out.append("\\r")
+        elif c < 0x20 or 0x80 <= c < 0xA0 or 0x2000 <= c < 0x2100:
+            out.append("\\u%04x" % c)
+        else:
+            out.append(ch)
+        prev = c if c <= 0xFFFF else 0xDC00  # the low surrogate precedes the next unit
+    out.append('"')
+    return "".join(out)
+
+
+def _json_write(v) -> str:
+    if isinstance(v, dict):
+        return "{" + ",".join(json_quote(k) + ":" + _json_write(v[k]) for k in java8_hashmap_order(list(v))) + "}"
+    if isinstance(v, (list, tuple)):
+        return "[" + ",".join(_json_write(e) for e in v) + "]"
+    if isinstance(v, float):
+        return json_number_to_string(v)
+    return json_quote(v)
+
+
+def format_point_geojson(oid, ts: int, x: float, y: float, utc_offset_min: int = 0) -> str:
+    """PointToGeoJSONOutputSchema.serialize (Serialization.java:28-50) with org.json 20200518:
+    keys put in source order into HashMap-backed JSONObjects, written in HashMap order."""
+    geometry = {"coordinates": [float(x), float(y)], "type": "Point"}
+    props = {}
+    if oid is not None:  # put("oID", null) removes the key
+        props["oID"] = oid
+    if ts != 0:
+        props["timestamp"] = java_date_ymd_hms(ts, utc_offset_min)
+    obj = {"geometry": geometry}
+    if props:
+        obj["properties"] = props
+    obj["type"] = "Feature"
+    return _json_write(obj)

@@ -79,11 +79,40 @@ class CsvOutSpec(ctypes.Structure):
                 ("delim_len", c_int32), ("delim", ctypes.c_char * 8), ("reserved", c_int32)]
 
 
-def make_csv_out_spec(attrs=(0, 1, 2, 3), delimiter: str = ",") -> CsvOutSpec:
+def _separation(delimiter: str) -> bytes:
+    """The schemas' SEPARATION: the config string `\\\\t` (backslash, backslash, t) becomes the two
+    characters `\\t` (Serialization.java:62-66, 110-114); UTF-8, 1..8 bytes."""
+    if delimiter == "\\\\t":
+        delimiter = "\\t"
     d = delimiter.encode()
     if not 1 <= len(d) <= 8:
         raise GeohipUnsupportedError("delimiter must be 1..8 bytes")
+    return d
+
+
+def make_csv_out_spec(attrs=(0, 1, 2, 3), delimiter: str = ",") -> CsvOutSpec:
+    d = _separation(delimiter)
     return CsvOutSpec(attrs[0], attrs[1], attrs[2], attrs[3], len(d), d, 0)
+
+
+DATE_NONE, DATE_YMD_HMS = 0, 1
+
+
+class TextOutSpec(ctypes.Structure):
+    """geohip_text_out_spec: output schema (FMT_CSV / FMT_WKT / FMT_GEOJSON), CSV positions,
+    delimiter, date formatter and its zone offset."""
+    _fields_ = [("format", c_int32), ("attr_oid", c_int32), ("attr_ts", c_int32), ("attr_x", c_int32),
+                ("attr_y", c_int32), ("delim_len", c_int32), ("delim", ctypes.c_char * 8), ("date_format", c_int32),
+                ("utc_offset_min", c_int32)]
+
+
+def make_text_out_spec(fmt: int, attrs=(0, 1, 2, 3), delimiter: str = ",", date_format: int = DATE_NONE,
+                       utc_offset_min: int = 0) -> TextOutSpec:
+    """Serialization.PointToCSVTSVOutputSchema / PointToWKTOutputSchema / PointToGeoJSONOutputSchema
+    (Serialization.java:17-152); date_format DATE_YMD_HMS = SimpleDateFormat("yyyy-MM-dd HH:mm:ss")
+    in a fixed-offset zone."""
+    d = _separation(delimiter) if fmt != FMT_GEOJSON else b","
+    return TextOutSpec(fmt, attrs[0], attrs[1], attrs[2], attrs[3], len(d), d, date_format, utc_offset_min)
 
 
 class Rect(ctypes.Structure):
@@ -126,8 +155,10 @@ _SIGS = {
     "geohip_knn_pp_async": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_double, c_double, c_double, c_uint32,
                                     _P, _P, _P]),
     "geohip_knn_merge_async": (c_int, [_P, _P, _P, c_uint32, c_uint32, c_uint32, _P, _P, _P]),
-    "geohip_format_points_csv": (c_int, [_P, POINTER(CsvOutSpec), _P, _P, _P, _P, _P, _P, c_uint64, _P, c_uint64,
-                                         POINTER(c_uint64), _P]),
+    "geohip_format_points_csv": (c_int, [_P, POINTER(CsvOutSpec), _P, _P, c_uint64, _P, _P, _P, _P, c_uint64, _P,
+                                         c_uint64, POINTER(c_uint64), _P]),
+    "geohip_format_points": (c_int, [_P, POINTER(TextOutSpec), _P, _P, c_uint64, _P, _P, _P, _P, c_uint64, _P, c_uint64,
+                                     POINTER(c_uint64), _P]),
     "geohip_band_pack_async": (c_int, [_P, POINTER(Grid), c_int32, c_uint32, _P, _P, c_uint64, ctypes.c_int64, _P, _P,
                                        _P, _P]),
     "geohip_knn_range_pp": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_double, c_double, c_double, c_uint32,
@@ -257,7 +288,19 @@ def _poly_arrays(poly_rings, ring_off, vx, vy):
     npoly = (len(ring_off) if pr is None else len(pr)) - 1
     if npoly < 0:
         raise GeohipArgumentError("ring_off / poly_rings need at least one entry")
-    return pr, ring_off, _host(vx, np.float64), _host(vy, np.float64), npoly
+    vx, vy = _host(vx, np.float64), _host(vy, np.float64)
+    _check_rings(ring_off, vx, vy)
+    if pr is not None and npoly and (int(pr[-1]) >= len(ring_off) or int(pr.max()) >= len(ring_off)):
+        raise GeohipArgumentError("poly_rings refers past the end of ring_off")
+    return pr, ring_off, vx, vy, npoly
+
+
+def _check_rings(ring_off, vx, vy):
+    """The C ABI takes no vertex count: ring offsets past the vertex arrays are caught here."""
+    if len(vx) != len(vy):
+        raise GeohipArgumentError(f"vx and vy differ in length ({len(vx)} vs {len(vy)})")
+    if len(ring_off) and int(ring_off.max()) > len(vx):
+        raise GeohipArgumentError(f"ring_off refers past the end of vx/vy ({int(ring_off.max())} > {len(vx)})")
 
 
 class Context:
@@ -428,9 +471,13 @@ class Context:
         self._dev(y, "y")
         self._dev(knn_idx, "knn_idx", "int32")
         self._dev(knn_dist, "knn_dist")
+        self._dev(knn_count, "knn_count", "int32")
         self._dev(range_idx, "range_idx", "int32")
+        self._dev(range_count, "range_count", "int64")
         if range_idx.numel() < cap:
             raise GeohipArgumentError("knn_range_pp_async: range_idx shorter than cap")
+        if knn_idx.numel() < k or knn_dist.numel() < k:
+            raise GeohipArgumentError("knn_range_pp_async: knn_idx / knn_dist shorter than k")
         if self._mem != MEM_DEVICE:
             self.set_mem(MEM_DEVICE)
         rc = lib.geohip_knn_range_pp_async(self.h, ctypes.byref(grid), x.data_ptr(), y.data_ptr(), x.numel(), qx, qy, r,
@@ -446,6 +493,9 @@ class Context:
         self._dev(y, "y")
         self._dev(out_idx, "out_idx", "int32")
         self._dev(out_dist, "out_dist")
+        self._dev(out_count, "out_count", "int32")
+        if out_idx.numel() < k or out_dist.numel() < k:
+            raise GeohipArgumentError("knn_pp_async: out_idx / out_dist shorter than k")
         if self._mem != MEM_DEVICE:
             self.set_mem(MEM_DEVICE)
         rc = lib.geohip_knn_pp_async(self.h, ctypes.byref(grid), x.data_ptr(), y.data_ptr(), x.numel(), qx, qy, r, k,
@@ -458,6 +508,11 @@ class Context:
         self._dev(idx, "idx", "int32")
         if dist.numel() < nlists * list_len or idx.numel() < nlists * list_len:
             raise GeohipArgumentError("knn_merge_async: lists shorter than nlists * list_len")
+        self._dev(out_idx, "out_idx", "int32")
+        self._dev(out_dist, "out_dist")
+        self._dev(out_count, "out_count", "int32")
+        if out_idx.numel() < k or out_dist.numel() < k:
+            raise GeohipArgumentError("knn_merge_async: out_idx / out_dist shorter than k")
         if self._mem != MEM_DEVICE:
             self.set_mem(MEM_DEVICE)
         rc = lib.geohip_knn_merge_async(self.h, dist.data_ptr(), idx.data_ptr(), nlists, list_len, k,
@@ -469,37 +524,50 @@ class Context:
         """geohip_format_points_csv (Serialization.PointToCSVTSVOutputSchema over result points):
         device tensors in (x, y float64; ts int64; oid_text uint8 + oid_off int64 [n + 1]; idx
         int32 record -> point), -> (text uint8 device tensor, record offsets int64 [m + 1])."""
+        return self._format(lib.geohip_format_points_csv, spec, x, y, ts, oid_text, oid_off, idx, cap)
+
+    def format_points(self, spec: TextOutSpec, x, y, ts=None, oid_text=None, oid_off=None, idx=None, cap=None):
+        """geohip_format_points: the CSV/TSV, WKT or GeoJSON point schema (spec.format), arguments
+        as for format_points_csv."""
+        return self._format(lib.geohip_format_points, spec, x, y, ts, oid_text, oid_off, idx, cap)
+
+    def _format(self, fn, spec, x, y, ts, oid_text, oid_off, idx, cap):
         import torch
         self._dev(x, "x")
         self._dev(y, "y")
+        if y.numel() != x.numel():
+            raise GeohipArgumentError("format: x and y differ in length")
         if ts is not None:
             self._dev(ts, "ts", "int64")
+            if ts.numel() < x.numel():
+                raise GeohipArgumentError("format: ts shorter than x")
         if (oid_text is None) != (oid_off is None):
             raise GeohipArgumentError("oid_text and oid_off go together")
         if oid_text is not None:
             self._dev(oid_text, "oid_text", "uint8")
             self._dev(oid_off, "oid_off", "int64")
+            if oid_off.numel() < x.numel() + 1:
+                raise GeohipArgumentError("format: oid_off needs n + 1 entries")
         if idx is not None:
             self._dev(idx, "idx", "int32")
-        m = idx.numel() if idx is not None else x.numel()
+        n = x.numel()
+        m = idx.numel() if idx is not None else n
         if self._mem != MEM_DEVICE:
             self.set_mem(MEM_DEVICE)
         off = torch.empty(m + 1, dtype=torch.int64, device=x.device)
-        n = c_uint64(0)
+        ln = c_uint64(0)
         ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
         if cap is None:  # size pass
-            rc = lib.geohip_format_points_csv(self.h, ctypes.byref(spec), x.data_ptr(), y.data_ptr(), ptr(ts),
-                                              ptr(oid_text), ptr(oid_off), ptr(idx), m, None, 0, ctypes.byref(n),
-                                              off.data_ptr())
+            rc = fn(self.h, ctypes.byref(spec), x.data_ptr(), y.data_ptr(), n, ptr(ts), ptr(oid_text), ptr(oid_off),
+                    ptr(idx), m, None, 0, ctypes.byref(ln), off.data_ptr())
             if rc not in (OK, ERR_CAPACITY):
-                self._check(rc, "format_points_csv")
-            cap = n.value
+                self._check(rc, "format_points")
+            cap = ln.value
         out = torch.empty(max(cap, 1), dtype=torch.uint8, device=x.device)
-        rc = lib.geohip_format_points_csv(self.h, ctypes.byref(spec), x.data_ptr(), y.data_ptr(), ptr(ts),
-                                          ptr(oid_text), ptr(oid_off), ptr(idx), m, out.data_ptr(), cap,
-                                          ctypes.byref(n), off.data_ptr())
-        self._check(rc, "format_points_csv")
-        return out[:n.value], off
+        rc = fn(self.h, ctypes.byref(spec), x.data_ptr(), y.data_ptr(), n, ptr(ts), ptr(oid_text), ptr(oid_off),
+                ptr(idx), m, out.data_ptr(), cap, ctypes.byref(ln), off.data_ptr())
+        self._check(rc, "format_points")
+        return out[:ln.value], off
 
     def band_pack_async(self, grid_data: Grid, nb: int, world: int, x, y, base: int = 0):
         """geohip_band_pack_async: this shard's valid-key points grouped by key-band owner rank
@@ -529,6 +597,7 @@ class Context:
         self._dev(x, "x")
         self._dev(y, "y")
         self._dev(out_idx, "out_idx", "int32")
+        self._dev(out_count, "out_count", "int64")
         if out_idx.numel() < cap:
             raise GeohipArgumentError("range_pp_async: out_idx shorter than cap")
         if self._mem != MEM_DEVICE:
@@ -638,6 +707,7 @@ class Context:
         vx = _host(vx, np.float64)
         vy = _host(vy, np.float64)
         ring_off = _host([0, len(vx)] if ring_off is None else ring_off, np.uint32)
+        _check_rings(ring_off, vx, vy)
         if dev:
             import torch
             oi = torch.empty(k, dtype=torch.int32, device=x.device)

@@ -33,6 +33,7 @@ SOURCES = {
     "ingest.hip": ["-x", "hip", f"--offload-arch={ARCH}"],
     "band.hip": ["-x", "hip", f"--offload-arch={ARCH}"],
     "format.hip": ["-x", "hip", f"--offload-arch={ARCH}"],
+    "sort.hip": ["-x", "hip", f"--offload-arch={ARCH}"],
 }
 
 

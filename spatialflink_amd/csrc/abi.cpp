@@ -112,6 +112,8 @@ struct geohip_ctx {
     hipEvent_t stg_ev[2] = {nullptr, nullptr};
     bool stg_used[2] = {false, false};
     std::unique_ptr<CopyPool> copy_pool;
+    hipEvent_t switch_ev = nullptr;  // orders a stream rebinding after the old stream's work
+    void* pcache = nullptr;          // point-polygon plan cache (cell_kernels.hip owns the type)
 };
 
 namespace {
@@ -364,15 +366,16 @@ int ensure_zeroed(geohip_ctx* ctx, Slot s, size_t bytes);
 int knn_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
                 double qx, double qy, double r, uint32_t k, double* out_d, unsigned* out_i, unsigned* out_cnt) {
     if (k == 0) return fail(ctx, GEOHIP_ERR_ARG, "k must be > 0");
-    if (k > GEOHIP_KNN_MAX_K) return fail(ctx, GEOHIP_ERR_UNSUPPORTED, "k > GEOHIP_KNN_MAX_K");
     if (n >= 0xffffffffull) return fail(ctx, GEOHIP_ERR_UNSUPPORTED, "window larger than 2^32-1 points");
     PointPlan plan;
     int rc = plan_or_fail(ctx, grid, qx, qy, r, &plan);
     if (rc) return rc;
-    KnnArgs a = make_knn_args(plan, k, qx, qy);
     const double *dx, *dy;
     rc = stage_xy(ctx, x, y, n, S_X, S_Y, &dx, &dy);
     if (rc) return rc;
+    // k beyond the one-pass selection: candidates, radix select and sort (any k)
+    if (k > GEOHIP_KNN_MAX_K) return knn_pp_large_impl(ctx, plan, dx, dy, n, qx, qy, k, out_d, out_i, out_cnt);
+    KnnArgs a = make_knn_args(plan, k, qx, qy);
     unsigned nb = 0;
     uint64_t ch = 0;
     knn_pass_geometry(n, &nb, &ch);
@@ -493,11 +496,10 @@ int knn_range_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x,
                       double qx, double qy, double r, uint32_t k, int approximate, double* kd, unsigned* ki,
                       unsigned* kcnt, unsigned* rout, uint64_t rcap, uint64_t* rtotal) {
     if (k == 0) return fail(ctx, GEOHIP_ERR_ARG, "k must be > 0");
-    if (k > GEOHIP_KNN_MAX_K) return fail(ctx, GEOHIP_ERR_UNSUPPORTED, "k > GEOHIP_KNN_MAX_K");
     PointPlan plan;
     int rc = plan_or_fail(ctx, grid, qx, qy, r, &plan);
     if (rc) return rc;
-    if (n == 0 || plan.nu == 0 || !knn_pass_fuses_range(n)) {
+    if (n == 0 || plan.nu == 0 || !knn_pass_fuses_range(n) || k > GEOHIP_KNN_MAX_K) {
         rc = knn_enqueue(ctx, grid, x, y, n, qx, qy, r, k, kd, ki, kcnt);
         if (!rc) rc = range_enqueue(ctx, grid, x, y, n, qx, qy, r, approximate, rout, rcap, rtotal);
         return rc;
@@ -599,6 +601,7 @@ int geohip_ctx_destroy(geohip_ctx* ctx) {
         if (ctx->stg_ev[k]) hipEventDestroy(ctx->stg_ev[k]);
     }
     if (ctx->cstream) hipStreamDestroy(ctx->cstream);
+    if (ctx->switch_ev) hipEventDestroy(ctx->switch_ev);
     if (ctx->own) hipStreamDestroy(ctx->own);
     delete ctx;
     return GEOHIP_OK;
@@ -612,16 +615,29 @@ int geohip_ctx_set_mem(geohip_ctx* ctx, int mem_kind) {
     return GEOHIP_OK;
 }
 
+// Rebinding the ctx to another stream: the ctx's scratch (block lists, spill counter, look-back
+// words, staging slots) is shared by every call, so work still queued on the old stream must
+// finish before the new stream's kernels touch it -- the new stream waits on an event recorded
+// on the old one.
+static int switch_stream(geohip_ctx* ctx, hipStream_t next) {
+    if (next == ctx->stream) return GEOHIP_OK;
+    int rc = begin(ctx);
+    if (rc) return rc;
+    if (!ctx->switch_ev) HIPCHK(hipEventCreateWithFlags(&ctx->switch_ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(ctx->switch_ev, ctx->stream));
+    HIPCHK(hipStreamWaitEvent(next, ctx->switch_ev, 0));
+    ctx->stream = next;
+    return GEOHIP_OK;
+}
+
 int geohip_ctx_set_stream(geohip_ctx* ctx, void* hip_stream) {
     if (!ctx) return GEOHIP_ERR_ARG;
-    ctx->stream = (hipStream_t)hip_stream;  // NULL: the HIP null stream (e.g. PyTorch's default stream)
-    return GEOHIP_OK;
+    return switch_stream(ctx, (hipStream_t)hip_stream);  // NULL: the HIP null stream (PyTorch's default)
 }
 
 int geohip_ctx_reset_stream(geohip_ctx* ctx) {
     if (!ctx) return GEOHIP_ERR_ARG;
-    ctx->stream = ctx->own;
-    return GEOHIP_OK;
+    return switch_stream(ctx, ctx->own);
 }
 
 void* geohip_ctx_stream(geohip_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
@@ -742,11 +758,21 @@ int geohip_knn_pp_async(geohip_ctx* ctx, const geohip_grid* grid, const double* 
 }
 
 int geohip_format_points_csv(geohip_ctx* ctx, const geohip_csv_out_spec* spec, const double* x, const double* y,
-                             const int64_t* ts, const uint8_t* oid_text, const uint64_t* oid_off, const uint32_t* idx,
-                             uint64_t m, uint8_t* out, uint64_t cap, uint64_t* out_len, uint64_t* rec_off) {
+                             uint64_t n, const int64_t* ts, const uint8_t* oid_text, const uint64_t* oid_off,
+                             const uint32_t* idx, uint64_t m, uint8_t* out, uint64_t cap, uint64_t* out_len,
+                             uint64_t* rec_off) {
     int rc = begin(ctx);
     if (rc) return rc;
-    return format_csv_impl(ctx, spec, x, y, ts, oid_text, oid_off, idx, m, out, cap, out_len, rec_off);
+    return format_csv_impl(ctx, spec, x, y, n, ts, oid_text, oid_off, idx, m, out, cap, out_len, rec_off);
+}
+
+int geohip_format_points(geohip_ctx* ctx, const geohip_text_out_spec* spec, const double* x, const double* y,
+                         uint64_t n, const int64_t* ts, const uint8_t* oid_text, const uint64_t* oid_off,
+                         const uint32_t* idx, uint64_t m, uint8_t* out, uint64_t cap, uint64_t* out_len,
+                         uint64_t* rec_off) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    return format_points_impl(ctx, spec, x, y, n, ts, oid_text, oid_off, idx, m, out, cap, out_len, rec_off);
 }
 
 int geohip_band_pack_async(geohip_ctx* ctx, const geohip_grid* grid_data, int32_t nb, uint32_t world,
@@ -764,10 +790,10 @@ int geohip_knn_merge_async(geohip_ctx* ctx, const double* dist, const uint32_t* 
     if (rc) return rc;
     if (ctx->mem != GEOHIP_MEM_DEVICE) return fail(ctx, GEOHIP_ERR_ARG, "async forms need GEOHIP_MEM_DEVICE");
     if (k == 0) return fail(ctx, GEOHIP_ERR_ARG, "k must be > 0");
-    if (k > GEOHIP_KNN_MAX_K) return fail(ctx, GEOHIP_ERR_UNSUPPORTED, "k > GEOHIP_KNN_MAX_K");
-    if (k > 256 && (uint64_t)nlists * list_len > 8192)
-        return fail(ctx, GEOHIP_ERR_UNSUPPORTED, "merge of more than 8192 entries with k > 256");
     if (!dist || !idx || !out_idx || !out_dist || !out_count_dev) return fail(ctx, GEOHIP_ERR_ARG, "null pointer");
+    if (k > 256 && (uint64_t)nlists * list_len > 8192)  // beyond one workgroup's LDS sort
+        return knn_merge_large_impl(ctx, reinterpret_cast<const unsigned long long*>(dist), idx, nlists, list_len, k,
+                                    out_dist, out_idx, out_count_dev);
     hipError_t e = launch_knn_merge(reinterpret_cast<const unsigned long long*>(dist), idx, nlists, list_len, k,
                                     out_dist, out_idx, out_count_dev, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "knn merge launch");
@@ -1039,6 +1065,7 @@ int ctx_begin(geohip_ctx* ctx) { return begin(ctx); }
 hipStream_t ctx_stream(geohip_ctx* ctx) { return ctx->stream; }
 int ctx_mem(geohip_ctx* ctx) { return ctx->mem; }
 uint64_t* ctx_pinned(geohip_ctx* ctx) { return ctx->pinned; }
+void** ctx_pcache_slot(geohip_ctx* ctx) { return &ctx->pcache; }
 void ctx_timing_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1) { timing_events(ctx, e0, e1); }
 int ctx_stage_xy(geohip_ctx* ctx, const double* x, const double* y, uint64_t n, int which, const double** dx,
                  const double** dy) {

@@ -32,6 +32,7 @@
 #include "device_common.h"
 #include "join.h"
 #include "ppoly.h"
+#include "sort.h"
 
 namespace geohip {
 
@@ -1139,10 +1140,13 @@ struct PolyDev {
 };
 
 // Polygons with holes: rings are stored back to back in one vertex run, with a ring id per
-// vertex (u8, < kMaxRings); segment (v[e], v[e+1]) exists iff both ends carry the same id (the
+// vertex (u16, < kMaxRings); segment (v[e], v[e+1]) exists iff both ends carry the same id (the
 // junction between two rings is not an edge).  Crossing parity and boundary flags are kept per
-// ring as 64-bit masks, so segments may still be visited in any order.
-constexpr uint32_t kMaxRings = 64;
+// ring as 64-bit masks over a chunk of 64 rings (ring = 64 c + bit), so segments may still be
+// visited in any order; a polygon of more than 64 rings takes one pass per chunk until a chunk
+// decides (rings_locate_chunk).
+constexpr uint32_t kMaxRings = 65535;
+typedef uint16_t ring_id_t;
 
 // A polygon's y-slab index (u16): cbeg[ns + 1] | dbeg[ns + 1] | segment ids.  Crossing list of
 // slab s: segments (v[e], v[e+1]) whose y-range meets the slab (padded) -- every segment that
@@ -1374,25 +1378,29 @@ __device__ __forceinline__ bool point_polygon_within(double px, double py, const
     return false;
 }
 
-// PointLocator.locateInPolygon (JTS 1.16.1) from per-ring masks: bit j of bnd = some segment of
-// ring j flags the point as on it, bit j of par = odd crossing count of ring j.  Shell boundary
-// -> on the polygon; even shell parity -> outside; else the holes in order: a hole whose envelope
-// excludes the point is EXTERIOR to it (locateInPolygonRing's envelope test), boundary -> on the
-// polygon, interior -> outside; no hole claims the point -> inside.  true = distance 0.
-__device__ __forceinline__ bool rings_locate_inside(double px, double py, unsigned long long bnd,
-                                                    unsigned long long par, const double* __restrict__ renv) {
-    if (bnd & 1ull) return true;
-    if (!(par & 1ull)) return false;
-    unsigned long long m = (bnd | par) & ~1ull;
+// PointLocator.locateInPolygon (JTS 1.16.1) from per-ring masks of the rings [64 c, 64 c + 64):
+// bit j of bnd = some segment of ring 64 c + j flags the point as on it, bit j of par = odd
+// crossing count of that ring.  Chunk 0 holds the shell (bit 0): shell boundary -> on the polygon;
+// even shell parity -> outside.  Then the holes in order: a hole whose envelope excludes the point
+// is EXTERIOR to it (locateInPolygonRing's envelope test), boundary -> on the polygon, interior ->
+// outside.  Returns 1 (distance 0), 0 (outside), or -1: no ring of the chunk decides (the next
+// chunk's holes go on; after the last chunk the point is inside).
+__device__ __forceinline__ int rings_locate_chunk(double px, double py, unsigned long long bnd, unsigned long long par,
+                                                  const double* __restrict__ renv, uint32_t c) {
+    unsigned long long m = bnd | par;
+    if (c == 0) {
+        if (bnd & 1ull) return 1;
+        if (!(par & 1ull)) return 0;
+        m &= ~1ull;
+    }
     while (m) {
         const int h = __builtin_ctzll(m);
         m &= m - 1;
-        const double* e = renv + 4 * h;
+        const double* e = renv + 4 * (64 * (size_t)c + h);
         if (px > e[2] || px < e[0] || py > e[3] || py < e[1]) continue;
-        if ((bnd >> h) & 1ull) return true;
-        return false;  // odd parity of hole h: inside the hole
+        return ((bnd >> h) & 1ull) ? 1 : 0;  // on hole h / inside hole h
     }
-    return true;
+    return -1;
 }
 
 // point_polygon_within for a polygon with holes (P.nring > 1): the same crossing and distance
@@ -1402,29 +1410,36 @@ __device__ __forceinline__ bool rings_locate_inside(double px, double py, unsign
 // except through a rounding tie between the envelope and segment distances).
 __device__ __forceinline__ bool point_polygon_within_rings(double px, double py, const double* __restrict__ vx,
                                                         const double* __restrict__ vy,
-                                                        const uint8_t* __restrict__ vr,
+                                                        const ring_id_t* __restrict__ vr,
                                                         const double* __restrict__ renv, const PolyDev& P,
                                                         const SlabView& sv, double r) {
     const int nv = (int)P.nv;
     const bool in_env = !(px > P.bb[2] || px < P.bb[0] || py > P.bb[3] || py < P.bb[1]);
     const uint32_t s = sv.ns ? slab_of(py, P.sy0, P.sinv, sv.ns) : 0u;
     if (in_env) {
-        unsigned long long bnd = 0, par = 0;
-        auto seg = [&](uint32_t e) {
-            bool b = false;
-            int c = 0;
-            count_segment(px, py, vx[e + 1], vy[e + 1], vx[e], vy[e], b, c);
-            const unsigned long long bit = 1ull << vr[e];
-            bnd |= b ? bit : 0ull;
-            par ^= (c & 1) ? bit : 0ull;
-        };
-        if (sv.ns) {
-            for (uint32_t k = sv.cbeg(s); k < sv.cbeg(s + 1); k++) seg(sv.id(k));
-        } else {
-            for (int e = 0; e < nv - 1; e++)
-                if (vr[e] == vr[e + 1]) seg((uint32_t)e);
+        const uint32_t nch = (P.nring + 63) / 64;
+        int loc = -1;
+        for (uint32_t c = 0; c < nch && loc < 0; c++) {
+            unsigned long long bnd = 0, par = 0;
+            auto seg = [&](uint32_t e) {
+                const uint32_t rid = vr[e];
+                if ((rid >> 6) != c) return;
+                bool b = false;
+                int cr = 0;
+                count_segment(px, py, vx[e + 1], vy[e + 1], vx[e], vy[e], b, cr);
+                const unsigned long long bit = 1ull << (rid & 63);
+                bnd |= b ? bit : 0ull;
+                par ^= (cr & 1) ? bit : 0ull;
+            };
+            if (sv.ns) {
+                for (uint32_t k = sv.cbeg(s); k < sv.cbeg(s + 1); k++) seg(sv.id(k));
+            } else {
+                for (int e = 0; e < nv - 1; e++)
+                    if (vr[e] == vr[e + 1]) seg((uint32_t)e);
+            }
+            loc = rings_locate_chunk(px, py, bnd, par, renv, c);
         }
-        if (rings_locate_inside(px, py, bnd, par, renv)) return true;
+        if (loc != 0) return true;  // on a ring, or inside with no hole claiming the point
     }
     const double lim2 = screen_lim2(px, py, P.gb, r);
     if (sv.ns && lim2 <= P.E * P.E) {
@@ -1506,7 +1521,7 @@ __global__ void ppoly_words(const PolyWork* __restrict__ work, uint32_t nwork, c
 template <bool APPROX>
 __global__ __launch_bounds__(kTB) void ppoly_eval(TileBins tb, const PolyWork* __restrict__ work,
                                                   const PolyDev* __restrict__ polys, const double* __restrict__ vx,
-                                                  const double* __restrict__ vy, const uint8_t* __restrict__ vring,
+                                                  const double* __restrict__ vy, const ring_id_t* __restrict__ vring,
                                                   const double* __restrict__ renv, const int32_t* __restrict__ rects,
                                                   const uint16_t* __restrict__ slabs, double r, int r_is_max,
                                                   const unsigned long long* __restrict__ wofs,
@@ -1514,7 +1529,7 @@ __global__ __launch_bounds__(kTB) void ppoly_eval(TileBins tb, const PolyWork* _
                                                   unsigned long long* __restrict__ bcount) {
     __shared__ double lvx[kMaxLdsVerts];
     __shared__ double lvy[kMaxLdsVerts];
-    __shared__ uint8_t lvr[kMaxLdsVerts];
+    __shared__ ring_id_t lvr[kMaxLdsVerts];
     __shared__ float4 lsb[kMaxLdsVerts];  // fp32 segment boxes (single-ring polygons staged in LDS)
     __shared__ uint16_t lsl[kMaxLdsSlab];
     __shared__ unsigned long long lmask[kMaskWords];
@@ -1544,7 +1559,7 @@ __global__ __launch_bounds__(kTB) void ppoly_eval(TileBins tb, const PolyWork* _
     __syncthreads();
     const double* rvx = v_lds ? lvx : vx + P.voff;
     const double* rvy = v_lds ? lvy : vy + P.voff;
-    const uint8_t* rvr = v_lds ? lvr : vring + P.voff;
+    const ring_id_t* rvr = v_lds ? lvr : vring + P.voff;
     const double* rre = renv + 4 * (size_t)P.eoff;
     const SlabView sv{s_lds ? lsl : slabs + P.loff, P.ns};
     unsigned long long* mk = lds_mask ? lmask : gm;  // global words: zeroed by the host, atomics only
@@ -1672,7 +1687,7 @@ __global__ __launch_bounds__(kTB) void ppoly_outside(const double* __restrict__ 
                                                      const double* __restrict__ vx = nullptr,
                                                      const double* __restrict__ vy = nullptr,
                                                      const uint16_t* __restrict__ slabs = nullptr, double r = 0.0,
-                                                     const uint8_t* __restrict__ vring = nullptr,
+                                                     const ring_id_t* __restrict__ vring = nullptr,
                                                      const double* __restrict__ renv = nullptr) {
     __shared__ uint2 pbuf[WRITE ? kTB / kWave : 1][WRITE ? kPolyPairs : 1];
     __shared__ unsigned long long bsh;
@@ -1823,7 +1838,7 @@ __global__ __launch_bounds__(kTB) void ppknn_scan(const double* __restrict__ x, 
 }
 
 // G u C rects as exact coordinate boxes (planner: rect_to_box), classification by compares
-constexpr int kPpBoxes = 16;
+constexpr int kPpBoxes = kMaxPointBoxes + 1;  // a point plan's G u C boxes fit too
 constexpr unsigned kPpBuf = 1024;  // wave-private candidate buffer (u32 window indices)
 struct PpknnBoxes {
     Box b[kPpBoxes];
@@ -1931,11 +1946,11 @@ template <bool APPROX>
 __global__ __launch_bounds__(kTB) void ppknn_dist(const double* __restrict__ x, const double* __restrict__ y,
                                                   const unsigned* __restrict__ cand, RselState* __restrict__ st,
                                                   const double* __restrict__ vx, const double* __restrict__ vy,
-                                                  const uint8_t* __restrict__ vring, const double* __restrict__ renv,
+                                                  const ring_id_t* __restrict__ vring, const double* __restrict__ renv,
                                                   PpknnPoly P, unsigned long long* __restrict__ key) {
     __shared__ double lvx[kMaxLdsVerts];
     __shared__ double lvy[kMaxLdsVerts];
-    __shared__ uint8_t lvr[kMaxLdsVerts];
+    __shared__ ring_id_t lvr[kMaxLdsVerts];
     __shared__ unsigned lh[kRselBins];  // round-0 digits of this block's keys (-> st->hist0)
     for (int t = threadIdx.x; t < kRselBins; t += kTB) lh[t] = 0;
     const bool v_lds = P.nv <= (uint32_t)kMaxLdsVerts;
@@ -1949,7 +1964,7 @@ __global__ __launch_bounds__(kTB) void ppknn_dist(const double* __restrict__ x, 
     __syncthreads();
     const double* rvx = v_lds ? lvx : vx;
     const double* rvy = v_lds ? lvy : vy;
-    const uint8_t* rvr = v_lds ? lvr : vring;
+    const ring_id_t* rvr = v_lds ? lvr : vring;
     const unsigned m = st->ncand;
     if (APPROX) {
         for (unsigned t = blockIdx.x * kTB + threadIdx.x; t < m; t += gridDim.x * kTB) {
@@ -1996,32 +2011,40 @@ __global__ __launch_bounds__(kTB) void ppknn_dist(const double* __restrict__ x, 
             }
             d = (in_env && (boundary || (crossings & 1))) ? 0.0 : md;
         } else {
-            // per-ring boundary / parity masks (rings_locate_inside); the minimum covers every
+            // per-ring boundary / parity masks (rings_locate_chunk); the minimum covers every
             // ring's segments (DistanceOp's envelope skip drops only rings farther than the
             // running minimum)
-            unsigned long long bnd = 0, par = 0;
             for (int e = (int)sub; e < nv - 1; e += (int)kG) {
-                const unsigned rid = rvr[e];
-                if (rid != rvr[e + 1]) continue;  // junction between two rings
-                const double ax = rvx[e], ay = rvy[e], bx = rvx[e + 1], by = rvy[e + 1];
-                if (in_env) {
-                    bool b = false;
-                    int c = 0;
-                    count_segment(px, py, bx, by, ax, ay, b, c);
-                    bnd |= b ? 1ull << rid : 0ull;
-                    par ^= (c & 1) ? 1ull << rid : 0ull;
-                }
-                const double sd = point_segment(px, py, ax, ay, bx, by);
+                if (rvr[e] != rvr[e + 1]) continue;  // junction between two rings
+                const double sd = point_segment(px, py, rvx[e], rvy[e], rvx[e + 1], rvy[e + 1]);
                 md = sd < md ? sd : md;
             }
 #pragma unroll
             for (unsigned o = 1; o < kG; o <<= 1) {
-                bnd |= __shfl_xor(bnd, (int)o);
-                par ^= __shfl_xor(par, (int)o);
                 const double od = __shfl_xor(md, (int)o);
                 md = od < md ? od : md;
             }
-            d = (in_env && rings_locate_inside(px, py, bnd, par, renv)) ? 0.0 : md;
+            int loc = in_env ? -1 : 0;  // the 8 lanes of a candidate decide together
+            const uint32_t nch = (P.nring + 63) / 64;
+            for (uint32_t c = 0; c < nch && loc < 0; c++) {
+                unsigned long long bnd = 0, par = 0;
+                for (int e = (int)sub; e < nv - 1; e += (int)kG) {
+                    const unsigned rid = rvr[e];
+                    if (rid != rvr[e + 1] || (rid >> 6) != c) continue;
+                    bool b = false;
+                    int cr = 0;
+                    count_segment(px, py, rvx[e + 1], rvy[e + 1], rvx[e], rvy[e], b, cr);
+                    bnd |= b ? 1ull << (rid & 63) : 0ull;
+                    par ^= (cr & 1) ? 1ull << (rid & 63) : 0ull;
+                }
+#pragma unroll
+                for (unsigned o = 1; o < kG; o <<= 1) {
+                    bnd |= __shfl_xor(bnd, (int)o);
+                    par ^= __shfl_xor(par, (int)o);
+                }
+                loc = rings_locate_chunk(px, py, bnd, par, renv, c);
+            }
+            d = loc != 0 ? 0.0 : md;
         }
         if (sub == 0) {
             const unsigned long long bits = (unsigned long long)__double_as_longlong(d);
@@ -2435,6 +2458,49 @@ __global__ __launch_bounds__(256) void rsel_sort(const unsigned long long* __res
     if (t == 0) out_count[0] = m;
 }
 
+// ---- large-k forms (k above what the one-workgroup selections rank in LDS) ----------------
+// Point kNN keys: JTS point.distance of every candidate as raw bits, the order the one-pass kNN
+// (knn_pass) ranks them in.
+__global__ __launch_bounds__(kTB) void ppknn_pp_keys(const double* __restrict__ x, const double* __restrict__ y,
+                                                     const unsigned* __restrict__ cand,
+                                                     const RselState* __restrict__ st, double qx, double qy,
+                                                     unsigned long long* __restrict__ key) {
+    const unsigned m = st->ncand;
+    for (unsigned t = blockIdx.x * kTB + threadIdx.x; t < m; t += gridDim.x * kTB) {
+        const unsigned i = cand[t];
+        key[t] = (unsigned long long)__double_as_longlong(jts_pp_distance(qx, qy, x[i], y[i]));
+    }
+}
+
+// result count of a large-k selection: min(candidates, k)
+__global__ void rsel_count(const RselState* __restrict__ st, unsigned k, unsigned* __restrict__ out_count) {
+    if (threadIdx.x == 0) {
+        const unsigned m = st->ncand;
+        out_count[0] = m < k ? m : k;
+    }
+}
+
+// the first k of m sorted (dist, idx) entries (sentinels sort last), the rest sentinels; count =
+// real entries among them
+__global__ __launch_bounds__(1024) void topk_take(const unsigned long long* __restrict__ sd,
+                                                  const unsigned* __restrict__ si, unsigned m, unsigned k,
+                                                  double* __restrict__ out_d, unsigned* __restrict__ out_i,
+                                                  unsigned* __restrict__ out_count) {
+    __shared__ unsigned cnt;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    unsigned mine = 0;
+    for (unsigned t = threadIdx.x; t < k; t += 1024) {
+        const unsigned long long d = t < m ? sd[t] : kSentinelD;
+        out_d[t] = __longlong_as_double((long long)d);
+        out_i[t] = t < m ? si[t] : kSentinelI;
+        mine += d != kSentinelD ? 1u : 0u;
+    }
+    if (mine) atomicAdd(&cnt, mine);
+    __syncthreads();
+    if (threadIdx.x == 0) out_count[0] = cnt;
+}
+
 // ================================================================== host side =============
 namespace {
 
@@ -2741,7 +2807,7 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
 // y-slab lists of one polygon (SlabView), appended to blob; P.ns = 0 when they cannot be built
 // (few or very many segments, non-finite extent): the device then visits every segment.
 // rid (nullable): ring id per vertex; a ring junction (rid[e] != rid[e+1]) is no segment.
-void plan_slabs(PolyDev& P, const double* ry, const uint8_t* rid, double r, double cell_len,
+void plan_slabs(PolyDev& P, const double* ry, const ring_id_t* rid, double r, double cell_len,
                 std::vector<uint16_t>& blob) {
     P.ns = 0;
     P.sy0 = 0.0;
@@ -2822,7 +2888,7 @@ struct PolyCache {
     std::vector<double> vx, vy;        // vx/vy[ring_off[R0] .. ring_off[R1])
     std::vector<PolyDev> pd;
     std::vector<double> hvx, hvy, henv;
-    std::vector<uint8_t> hvr;
+    std::vector<ring_id_t> hvr;
     std::vector<int32_t> hrects;
     std::vector<PolyWork> hwork;
     std::vector<uint16_t> hslab;
@@ -2831,8 +2897,12 @@ struct PolyCache {
     void* dev_blob = nullptr;  // J_POLY buffer holding the uploaded tables
     size_t blob_bytes = 0;
 };
-std::mutex g_pcache_mu;
-std::unordered_map<const geohip_ctx*, PolyCache> g_pcache;
+// the cache lives in the ctx (one ctx per calling thread: no lock)
+PolyCache* ctx_pcache(geohip_ctx* ctx) {
+    void** slot = ctx_pcache_slot(ctx);
+    if (!*slot) *slot = new PolyCache();
+    return static_cast<PolyCache*>(*slot);
+}
 
 // ring range of polygon p: [poly_rings[p], poly_rings[p+1]) (poly_rings null: ring p)
 inline uint32_t ring_of(const uint32_t* poly_rings, uint32_t p) { return poly_rings ? poly_rings[p] : p; }
@@ -2852,19 +2922,20 @@ bool same_inputs(const PolyCache& c, const geohip_grid& g, double r, const uint3
 }
 
 void ppoly_cache_drop(geohip_ctx* ctx) {
-    std::lock_guard<std::mutex> lk(g_pcache_mu);
-    g_pcache.erase(ctx);
+    void** slot = ctx_pcache_slot(ctx);
+    delete static_cast<PolyCache*>(*slot);
+    *slot = nullptr;
 }
 
 // Ring ids, ring envelopes and the box of every ring of a planned polygon (PolyPlan rings).
 // Envelopes as JTS computes them (Envelope.expandToInclude: NaN coordinates never enter).
-static void ring_tables(const PolyPlan& pl, std::vector<uint8_t>& vr, std::vector<double>& env, double gb[4]) {
+static void ring_tables(const PolyPlan& pl, std::vector<ring_id_t>& vr, std::vector<double>& env, double gb[4]) {
     const size_t nring = pl.ring_start.size() - 1;
     for (size_t j = 0; j < nring; j++) {
         const uint32_t a = pl.ring_start[j], b = pl.ring_start[j + 1];
         double mnx = pl.rx[a], mxx = pl.rx[a], mny = pl.ry[a], mxy = pl.ry[a];
         for (uint32_t i = a; i < b; i++) {
-            vr.push_back((uint8_t)j);
+            vr.push_back((ring_id_t)j);
             const double x = pl.rx[i], y = pl.ry[i];
             if (x < mnx) mnx = x;
             if (x > mxx) mxx = x;
@@ -2913,11 +2984,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     // polygon planning (host): rings (createPolygon), envelope, G / C rectangles (plan.cpp), the
     // (polygon, tile) work items of each polygon's walk region and the slab lists -- or the
     // cached plan of the same inputs
-    PolyCache* pc = nullptr;
-    {
-        std::lock_guard<std::mutex> lk(g_pcache_mu);
-        pc = &g_pcache[ctx];
-    }
+    PolyCache* pc = ctx_pcache(ctx);
     bool cached = same_inputs(*pc, *grid, r, poly_rings, ring_off, npoly, vx, vy) && pc->jmode == jmode &&
                   memcmp(&pc->gq, gq, sizeof *gq) == 0;
     if (!cached) {
@@ -2934,7 +3001,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             PolyPlan pl;
             std::string err;
             const uint32_t r0 = ring_of(poly_rings, p), r1 = ring_of(poly_rings, p + 1);
-            if (r1 - r0 > kMaxRings) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "polygon with more than 64 rings");
+            if (r1 - r0 > kMaxRings) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "polygon with more than 65535 rings");
             rc = plan_polygon_rings(*gq, ring_off + r0, r1 - r0, vx, vy, r, &pl, &err);
             if (rc) return ctx_fail(ctx, rc, err);
             PolyDev& P = pd[p];
@@ -3009,7 +3076,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     const std::vector<int32_t>& hrects = pc->hrects;
     const std::vector<PolyWork>& hwork = pc->hwork;
     const std::vector<uint16_t>& hslab = pc->hslab;
-    const std::vector<uint8_t>& hvr = pc->hvr;
+    const std::vector<ring_id_t>& hvr = pc->hvr;
     const std::vector<double>& henv = pc->henv;
     const bool any_outside = pc->any_outside;
     const std::vector<uint32_t>& keep = pc->keep;
@@ -3022,7 +3089,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     //   PolyDev[] | vx | vy | ring envelopes | rects | work | slab lists | keep | ring ids
     const size_t sz_p = npoly * sizeof(PolyDev), sz_v = hvx.size() * 8, sz_r = hrects.size() * 4;
     const size_t sz_w = hwork.size() * sizeof(PolyWork), sz_s = hslab.size() * 2, sz_k = keep.size() * 4;
-    const size_t sz_e = henv.size() * 8, sz_vr = hvr.size();
+    const size_t sz_e = henv.size() * 8, sz_vr = hvr.size() * sizeof(ring_id_t);
     const size_t off_v = (sz_p + 15) & ~(size_t)15;
     const size_t off_e = off_v + 2 * sz_v;
     const size_t off_r = off_e + sz_e;
@@ -3044,7 +3111,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     uint16_t* dslab = reinterpret_cast<uint16_t*>(bp + off_s);
     unsigned* dkeep = sz_k ? reinterpret_cast<unsigned*>(bp + off_k) : nullptr;
     double* denv = reinterpret_cast<double*>(bp + off_e);
-    uint8_t* dvr = reinterpret_cast<uint8_t*>(bp + off_vr);
+    ring_id_t* dvr = reinterpret_cast<ring_id_t*>(bp + off_vr);
     if (upload) {
         pc->dev_blob = nullptr;  // until the copies are issued
         if ((sz_p && hipMemcpyAsync(dpoly, pd.data(), sz_p, hipMemcpyHostToDevice, st) != hipSuccess) ||
@@ -3155,6 +3222,124 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     return GEOHIP_OK;
 }
 
+// Large-k selection tail shared by the point and point-polygon kNN: the 9 radix rounds over the
+// candidate keys, the gather of exactly min(k, M) keys into sel (pre-filled with sentinels), the
+// (dist, idx) sort of the k entries into od / oi, and the count.  The candidate scan and key
+// kernels ran before on st.
+int rsel_large_tail(hipStream_t st, const unsigned long long* key, const unsigned* cand, RselState* rs, unsigned k,
+                    unsigned long long* sel_d, unsigned* sel_i, unsigned long long* tmp_d, unsigned* tmp_i, void* temp,
+                    size_t temp_bytes, double* od, unsigned* oi, unsigned* ocnt) {
+    for (int t = 0; t < kRselRounds; t++) {
+        rsel_hist<<<512, kTB, 0, st>>>(key, cand, rs, t, k);
+        rsel_pick<<<1, 1024, 0, st>>>(rs, t, k);
+    }
+    rsel_gather<<<512, kTB, 0, st>>>(key, cand, rs, k, sel_d, sel_i);
+    hipError_t e = sort_dist_idx(temp, temp_bytes, sel_d, sel_i, tmp_d, tmp_i,
+                                 reinterpret_cast<unsigned long long*>(od), oi, k, st);
+    if (e != hipSuccess) return GEOHIP_ERR_DEVICE;
+    rsel_count<<<1, 64, 0, st>>>(rs, k, ocnt);
+    return hipGetLastError() == hipSuccess ? GEOHIP_OK : GEOHIP_ERR_DEVICE;
+}
+
+// Scratch of a large-k selection in slot 23: RselState | sel (k) | tmp (k) | sort temp.
+struct LargeK {
+    RselState* rs;
+    unsigned long long *sel_d, *tmp_d;
+    unsigned *sel_i, *tmp_i;
+    void* temp;
+    size_t temp_bytes;
+    char* extra;  // caller's area after the sort temp (extra_bytes)
+};
+int large_k_scratch(geohip_ctx* ctx, unsigned k, size_t extra_bytes, LargeK* L) {
+    const size_t a16 = 255;
+    L->temp_bytes = sort_dist_idx_temp_bytes(k);
+    if (!L->temp_bytes) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "sort temp size query failed");
+    const size_t off_sel = (sizeof(RselState) + a16) & ~a16;
+    const size_t off_tmp = (off_sel + (size_t)k * 12 + a16) & ~a16;
+    const size_t off_temp = (off_tmp + (size_t)k * 12 + a16) & ~a16;
+    const size_t off_extra = (off_temp + L->temp_bytes + a16) & ~a16;
+    void* p = nullptr;
+    int rc = ctx_ensure(ctx, 23, off_extra + extra_bytes + 64, &p);
+    if (rc) return rc;
+    char* b = reinterpret_cast<char*>(p);
+    L->rs = reinterpret_cast<RselState*>(b);
+    L->sel_d = reinterpret_cast<unsigned long long*>(b + off_sel);
+    L->sel_i = reinterpret_cast<unsigned*>(b + off_sel + (size_t)k * 8);
+    L->tmp_d = reinterpret_cast<unsigned long long*>(b + off_tmp);
+    L->tmp_i = reinterpret_cast<unsigned*>(b + off_tmp + (size_t)k * 8);
+    L->temp = b + off_temp;
+    L->extra = b + off_extra;
+    return GEOHIP_OK;
+}
+
+// Point kNN with k > GEOHIP_KNN_MAX_K (PointPointKNNQuery.java:33 takes any Integer k): the
+// candidates of G u C compacted by one box-classifying pass, their keys, then the radix-select
+// tail.  Same result as the one-pass kNN: the min(k, M) smallest (dist bits, idx), ascending.
+int knn_pp_large_impl(geohip_ctx* ctx, const PointPlan& plan, const double* dx, const double* dy, uint64_t n,
+                      double qx, double qy, uint32_t k, double* od, unsigned* oi, unsigned* ocnt) {
+    hipStream_t st = ctx_stream(ctx);
+    const uint64_t ncap = n ? n : 1;
+    void* pc = nullptr;
+    int rc = ctx_ensure(ctx, 22, ncap * 12 + 64, &pc);
+    LargeK L;
+    if (!rc) rc = large_k_scratch(ctx, k, 0, &L);
+    if (rc) return rc;
+    unsigned long long* key = reinterpret_cast<unsigned long long*>(pc);
+    unsigned* cand = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(pc) + ncap * 8);
+    hipEvent_t e0, e1;
+    ctx_timing_events(ctx, &e0, &e1);
+    if (e0) hipEventRecord(e0, st);
+    rsel_init<<<1, 1024, 0, st>>>(L.rs, k, 0u);
+    if (hipMemsetAsync(L.sel_d, 0xff, (size_t)k * 12, st) != hipSuccess)
+        return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
+    if (n && plan.nu) {
+        PpknnBoxes PB;
+        memset(&PB, 0, sizeof PB);
+        for (int q = 0; q < plan.nu; q++) PB.b[q] = plan.u[q];
+        PB.nb = plan.nu;
+        const uint64_t nb = std::max<uint64_t>(1, std::min<uint64_t>(((n + 255) / 256 + 3) / 4, 2048));
+        switch (PB.nb) {
+            case 1: ppknn_scan_boxes<1><<<(unsigned)nb, kTB, 0, st>>>(dx, dy, n, PB, cand, L.rs); break;
+            case 2: ppknn_scan_boxes<2><<<(unsigned)nb, kTB, 0, st>>>(dx, dy, n, PB, cand, L.rs); break;
+            default: ppknn_scan_boxes<0><<<(unsigned)nb, kTB, 0, st>>>(dx, dy, n, PB, cand, L.rs); break;
+        }
+        ppknn_pp_keys<<<1024, kTB, 0, st>>>(dx, dy, cand, L.rs, qx, qy, key);
+    }
+    rc = rsel_large_tail(st, key, cand, L.rs, k, L.sel_d, L.sel_i, L.tmp_d, L.tmp_i, L.temp, L.temp_bytes, od, oi, ocnt);
+    if (rc) return ctx_fail(ctx, rc, "large-k kNN launch failed");
+    if (e1) hipEventRecord(e1, st);
+    return GEOHIP_OK;
+}
+
+// Rank merge of nlists sorted lists when k > 256 and the lists hold more than one workgroup
+// sorts in LDS (KNNQuery.java:204-272 over any number of per-cell or per-rank results): every
+// entry sorted by (dist, idx), the first k taken.
+int knn_merge_large_impl(geohip_ctx* ctx, const unsigned long long* d, const unsigned* i, unsigned nlists,
+                         unsigned list_len, unsigned k, double* od, unsigned* oi, unsigned* ocnt) {
+    const uint64_t m64 = (uint64_t)nlists * list_len;
+    if (m64 >= 0xffffffffull) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "merge of 2^32 or more entries");
+    const unsigned m = (unsigned)m64;
+    hipStream_t st = ctx_stream(ctx);
+    const size_t tb = sort_dist_idx_temp_bytes(m ? m : 1);
+    if (!tb) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "sort temp size query failed");
+    const size_t mcap = (size_t)(m ? m : 1);
+    void* p = nullptr;
+    int rc = ctx_ensure(ctx, 22, mcap * 24 + tb + 512, &p);
+    if (rc) return rc;
+    char* b = reinterpret_cast<char*>(p);
+    unsigned long long* tmp_d = reinterpret_cast<unsigned long long*>(b);
+    unsigned long long* srt_d = tmp_d + mcap;
+    unsigned* tmp_i = reinterpret_cast<unsigned*>(srt_d + mcap);
+    unsigned* srt_i = tmp_i + mcap;
+    void* temp = reinterpret_cast<void*>((reinterpret_cast<uintptr_t>(srt_i + mcap) + 255) & ~(uintptr_t)255);
+    if (sort_dist_idx(temp, tb, d, i, tmp_d, tmp_i, srt_d, srt_i, m, st) != hipSuccess)
+        return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "merge sort launch failed");
+    topk_take<<<1, 1024, 0, st>>>(srt_d, srt_i, m, k, od, oi, ocnt);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, std::string("merge launch: ") + hipGetErrorString(e));
+    return GEOHIP_OK;
+}
+
 // Point-polygon kNN of one query polygon over one window (host side of the kernels above).
 int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
                    const uint32_t* ring_off, uint32_t nring, const double* vx, const double* vy, double r, uint32_t k,
@@ -3162,19 +3347,21 @@ int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, co
     if (!out_idx || !out_dist || !out_count) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null output");
     *out_count = 0;
     if (k == 0) return ctx_fail(ctx, GEOHIP_ERR_ARG, "k must be > 0");
-    if (k > GEOHIP_KNN_PPOLY_MAX_K) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "k > GEOHIP_KNN_PPOLY_MAX_K");
+    // k above one workgroup's LDS sort (GEOHIP_KNN_PPOLY_MAX_K): the radix rounds always run,
+    // the k selected keys are gathered and sorted (PointPolygonKNNQuery.java:34 takes any k)
+    const bool big_k = k > GEOHIP_KNN_PPOLY_MAX_K;
     int rc = check_grid_basic(ctx, grid, "grid");
     if (rc) return rc;
     if (n >= 0xffffffffull) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "window larger than 2^32-1 points");
     if (!ring_off || !vx || !vy) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null polygon arrays");
-    if (nring > kMaxRings) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "polygon with more than 64 rings");
+    if (nring > kMaxRings) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "polygon with more than 65535 rings");
     for (uint32_t j = 0; j < nring; j++)
         if (ring_off[j + 1] < ring_off[j]) return ctx_fail(ctx, GEOHIP_ERR_ARG, "ring_off not ascending");
     PolyPlan pl;
     std::string err;
     rc = plan_polygon_rings(*grid, ring_off, nring, vx, vy, r, &pl, &err);
     if (rc) return ctx_fail(ctx, rc, err);
-    std::vector<uint8_t> hvr;
+    std::vector<ring_id_t> hvr;
     std::vector<double> henv;
     double gb[4];
     ring_tables(pl, hvr, henv, gb);
@@ -3207,41 +3394,47 @@ int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, co
     Scratch S{ctx};
     const uint64_t ncap = n ? n : 1;
     char* cbuf = S.get<char>(22, ncap * 12 + 64);
-    const size_t off_sel_d = (sizeof(RselState) + 15) & ~(size_t)15;
-    const size_t off_sel_i = off_sel_d + 256 * 8;
-    const size_t off_out = off_sel_i + 256 * 4;
-    const size_t off_vx = (off_out + 256 * 12 + 16 + 15) & ~(size_t)15;
+    if (S.rc) return S.rc;
+    // slot 23: RselState, selection and sort areas (large_k_scratch), then the output staging
+    // (host windows), polygon tables
+    const size_t kout = std::max<size_t>(k, 256);
+    const size_t off_out = 0;
+    const size_t off_vx = (off_out + kout * 12 + 16 + 15) & ~(size_t)15;
     const size_t off_env = off_vx + 2 * 8 * (size_t)P.nv;
     const size_t off_rect = off_env + 8 * henv.size();
     const size_t off_vr = off_rect + 16 * (size_t)nrect;
-    char* sbuf = S.get<char>(23, off_vr + hvr.size() + 64);
-    if (S.rc) return S.rc;
+    LargeK L;
+    rc = large_k_scratch(ctx, (unsigned)kout, off_vr + hvr.size() * sizeof(ring_id_t), &L);
+    if (rc) return rc;
+    char* xbuf = L.extra;
     unsigned long long* key = reinterpret_cast<unsigned long long*>(cbuf);
     unsigned* cand = reinterpret_cast<unsigned*>(cbuf + ncap * 8);
-    RselState* rs = reinterpret_cast<RselState*>(sbuf);
-    unsigned long long* sel_d = reinterpret_cast<unsigned long long*>(sbuf + off_sel_d);
-    unsigned* sel_i = reinterpret_cast<unsigned*>(sbuf + off_sel_i);
-    double* od = dev ? out_dist : reinterpret_cast<double*>(sbuf + off_out);
-    unsigned* oi = dev ? out_idx : reinterpret_cast<unsigned*>(sbuf + off_out + 256 * 8);
-    unsigned* ocnt = reinterpret_cast<unsigned*>(sbuf + off_out + 256 * 12);
-    double* dvx = reinterpret_cast<double*>(sbuf + off_vx);
+    RselState* rs = L.rs;
+    double* od = dev ? out_dist : reinterpret_cast<double*>(xbuf + off_out);
+    unsigned* oi = dev ? out_idx : reinterpret_cast<unsigned*>(xbuf + off_out + kout * 8);
+    unsigned* ocnt = reinterpret_cast<unsigned*>(xbuf + off_out + kout * 12);
+    double* dvx = reinterpret_cast<double*>(xbuf + off_vx);
     double* dvy = dvx + P.nv;
-    int32_t* drect = reinterpret_cast<int32_t*>(sbuf + off_rect);
-    double* denv = reinterpret_cast<double*>(sbuf + off_env);
-    uint8_t* dvr = reinterpret_cast<uint8_t*>(sbuf + off_vr);
+    int32_t* drect = reinterpret_cast<int32_t*>(xbuf + off_rect);
+    double* denv = reinterpret_cast<double*>(xbuf + off_env);
+    ring_id_t* dvr = reinterpret_cast<ring_id_t*>(xbuf + off_vr);
     if ((P.nv && (hipMemcpyAsync(dvx, pl.rx.data(), 8 * (size_t)P.nv, hipMemcpyHostToDevice, st) != hipSuccess ||
                   hipMemcpyAsync(dvy, pl.ry.data(), 8 * (size_t)P.nv, hipMemcpyHostToDevice, st) != hipSuccess)) ||
         (nrect && hipMemcpyAsync(drect, hrect.data(), 16 * (size_t)nrect, hipMemcpyHostToDevice, st) != hipSuccess) ||
         (P.nring > 1 &&
          (hipMemcpyAsync(denv, henv.data(), 8 * henv.size(), hipMemcpyHostToDevice, st) != hipSuccess ||
-          hipMemcpyAsync(dvr, hvr.data(), hvr.size(), hipMemcpyHostToDevice, st) != hipSuccess)))
+          hipMemcpyAsync(dvr, hvr.data(), hvr.size() * sizeof(ring_id_t), hipMemcpyHostToDevice, st) != hipSuccess)))
         return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "polygon upload failed");
     hipEvent_t e0, e1;
     ctx_timing_events(ctx, &e0, &e1);
     if (e0) hipEventRecord(e0, st);
-    // single-workgroup select up to kRselSmall candidates (GEOHIP_RSEL_SMALL: test hook)
-    static const unsigned small_max = getenv("GEOHIP_RSEL_SMALL") ? (unsigned)atol(getenv("GEOHIP_RSEL_SMALL")) : kRselSmall;
+    // single-workgroup select up to kRselSmall candidates (GEOHIP_RSEL_SMALL: test hook); none
+    // for the large-k form
+    static const unsigned small_env = getenv("GEOHIP_RSEL_SMALL") ? (unsigned)atol(getenv("GEOHIP_RSEL_SMALL")) : kRselSmall;
+    const unsigned small_max = big_k ? 0u : small_env;
     rsel_init<<<1, 1024, 0, st>>>(rs, k, small_max);
+    if (big_k && hipMemsetAsync(L.sel_d, 0xff, (size_t)kout * 12, st) != hipSuccess)
+        return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
     if (n && nrect) {
         if (boxed) {
             const uint64_t iters = (n + 255) / 256;
@@ -3262,26 +3455,33 @@ int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, co
         if (approximate) ppknn_dist<true><<<1024, kTB, 0, st>>>(dx, dy, cand, rs, dvx, dvy, dvr, denv, P, key);
         else ppknn_dist<false><<<1024, kTB, 0, st>>>(dx, dy, cand, rs, dvx, dvy, dvr, denv, P, key);
     }
-    rsel_small<<<1, 1024, 0, st>>>(key, cand, rs, k, od, oi, ocnt);  // M <= kRselSmall (also M = 0)
-    if (e1) hipEventRecord(e1, st);  // re-recorded below when the multi-block rounds run
-    // the multi-block rounds only when the candidate count needs them (one count readback
-    // instead of 20 no-op launches, ~80 us)
-    bool big = false;
-    if (n && nrect) {
-        uint64_t* pin = ctx_pinned(ctx);
-        if (hipMemcpyAsync(pin, &rs->ncand, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess)
-            return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "candidate count readback failed");
-        big = (uint32_t)(pin[0] & 0xffffffffu) > small_max;
-    }
-    if (big) {
-        for (int t = 0; t < kRselRounds; t++) {
-            rsel_hist<<<512, kTB, 0, st>>>(key, cand, rs, t, k);
-            rsel_pick<<<1, 1024, 0, st>>>(rs, t, k);
-        }
-        rsel_gather<<<512, kTB, 0, st>>>(key, cand, rs, k, sel_d, sel_i);
-        rsel_sort<<<1, 256, 0, st>>>(sel_d, sel_i, rs, k, od, oi, ocnt);
+    if (big_k) {
+        rc = rsel_large_tail(st, key, cand, rs, k, L.sel_d, L.sel_i, L.tmp_d, L.tmp_i, L.temp, L.temp_bytes, od, oi,
+                             ocnt);
+        if (rc) return ctx_fail(ctx, rc, "large-k kNN launch failed");
         if (e1) hipEventRecord(e1, st);
+    } else {
+        rsel_small<<<1, 1024, 0, st>>>(key, cand, rs, k, od, oi, ocnt);  // M <= kRselSmall (also M = 0)
+        if (e1) hipEventRecord(e1, st);  // re-recorded below when the multi-block rounds run
+        // the multi-block rounds only when the candidate count needs them (one count readback
+        // instead of 20 no-op launches, ~80 us)
+        bool big = false;
+        if (n && nrect) {
+            uint64_t* pin = ctx_pinned(ctx);
+            if (hipMemcpyAsync(pin, &rs->ncand, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess)
+                return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "candidate count readback failed");
+            big = (uint32_t)(pin[0] & 0xffffffffu) > small_max;
+        }
+        if (big) {
+            for (int t = 0; t < kRselRounds; t++) {
+                rsel_hist<<<512, kTB, 0, st>>>(key, cand, rs, t, k);
+                rsel_pick<<<1, 1024, 0, st>>>(rs, t, k);
+            }
+            rsel_gather<<<512, kTB, 0, st>>>(key, cand, rs, k, L.sel_d, L.sel_i);
+            rsel_sort<<<1, 256, 0, st>>>(L.sel_d, L.sel_i, rs, k, od, oi, ocnt);
+            if (e1) hipEventRecord(e1, st);
+        }
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, std::string("knn_ppoly launch: ") + hipGetErrorString(e));

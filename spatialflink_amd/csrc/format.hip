@@ -413,65 +413,271 @@ __device__ int java_long_to_string(long long v, char* out) {
 }
 
 constexpr int kMaxPos = 64;
+// record flags raised by the formatting kernels (the host turns them into status codes)
+constexpr unsigned kFlagIdx = 1u;       // idx[j] >= n: no such point (GEOHIP_ERR_ARG)
+constexpr unsigned kFlagNonFinite = 2u; // GeoJSON of a NaN / infinite coordinate: the reference's
+                                        // JSONObject.toString returns null (GEOHIP_ERR_ARG)
+constexpr unsigned kFlagDate = 4u;      // a nonzero timestamp the date formatter cannot render
+                                        // (no formatter named, or outside years 1583..9999)
 struct FmtArgs {
     const double* x;
     const double* y;
+    uint64_t n;                   // points: idx[j] < n
     const long long* ts;          // nullable: 0
-    const unsigned char* oid;     // nullable: "null"
+    const unsigned char* oid;     // nullable: objID == null
     const unsigned long long* oid_off;
     const unsigned* idx;          // nullable: record j = point j
     uint64_t m;
-    int8_t field[kMaxPos];        // per position: 0 objID, 1 ts, 2 x, 3 y, -1 "0"
+    int format;                   // GEOHIP_FMT_CSV / _GEOJSON / _WKT
+    int8_t field[kMaxPos];        // CSV: per position 0 objID, 1 ts, 2 x, 3 y, -1 "0"
     int npos;
-    char delim[8];
+    char delim[8];                // the SEPARATION string (UTF-8)
     int dlen;
+    int csv_tail;                 // CSV: bytes of the last delimiter kept by deleteCharAt
+    int csv_tail_q;               //      1: a '?' follows them (a lone high surrogate, UTF-8 encoded)
+    int date;                     // GEOHIP_DATE_*
+    long long off_ms;             // the formatter's fixed zone offset
+    unsigned* flags;
 };
 
-// the record of point p: WRITE = false returns its length; true also stores it at dst
+// byte sink: WRITE = false only counts
+template <bool WRITE>
+struct Sink {
+    unsigned char* dst;
+    uint64_t len;
+    __device__ void put(char c) {
+        if (WRITE) dst[len] = (unsigned char)c;
+        len++;
+    }
+    __device__ void put(const char* s, int n) {
+        for (int t = 0; t < n; t++) put(s[t]);
+    }
+    __device__ void lit(const char* s) {
+        while (*s) put(*s++);
+    }
+};
+
+// SimpleDateFormat("yyyy-MM-dd HH:mm:ss") of a Date in a fixed-offset zone (proleptic Gregorian
+// civil date, exact from the 1582-10-15 cutover on; callers keep to years 1583..9999)
+__device__ bool format_ymd_hms(long long ms, long long off_ms, char* out) {
+    const long long t = ms + off_ms;
+    long long sec = t / 1000;
+    if (t % 1000 < 0) sec--;
+    long long days = sec / 86400;
+    long long sod = sec - days * 86400;
+    if (sod < 0) {
+        sod += 86400;
+        days--;
+    }
+    // civil_from_days (H. Hinnant)
+    const long long z = days + 719468;
+    const long long era = (z >= 0 ? z : z - 146096) / 146097;
+    const long long doe = z - era * 146097;
+    const long long yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+    long long yr = yoe + era * 400;
+    const long long doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
+    const long long mp = (5 * doy + 2) / 153;
+    const long long d = doy - (153 * mp + 2) / 5 + 1;
+    const long long mo = mp < 10 ? mp + 3 : mp - 9;
+    if (mo <= 2) yr++;
+    if (yr < 1583 || yr > 9999) return false;
+    const long long hh = sod / 3600, mi = (sod / 60) % 60, ss = sod % 60;
+    const long long v[6] = {yr, mo, d, hh, mi, ss};
+    const char sep[6] = {'-', '-', ' ', ':', ':', 0};
+    int i = 0;
+    for (int f = 0; f < 6; f++) {
+        if (f == 0) {
+            out[i++] = (char)('0' + yr / 1000);
+            out[i++] = (char)('0' + (yr / 100) % 10);
+        }
+        out[i++] = (char)('0' + (v[f] / 10) % 10);
+        out[i++] = (char)('0' + v[f] % 10);
+        if (sep[f]) out[i++] = sep[f];
+    }
+    return true;  // 19 characters
+}
+
+// org.json JSONObject.numberToString(Double): Double.toString, trailing zeros (and then the
+// point) shaved when there is a '.' and no exponent
+__device__ int json_number(double v, char* out) {
+    int n = java_double_to_string(v, out);
+    bool dot = false, ex = false;
+    for (int t = 0; t < n; t++) {
+        dot = dot || out[t] == '.';
+        ex = ex || out[t] == 'E' || out[t] == 'e';
+    }
+    if (dot && !ex) {
+        while (out[n - 1] == '0') n--;
+        if (out[n - 1] == '.') n--;
+    }
+    return n;
+}
+
+// org.json JSONObject.quote of a String given as UTF-8 bytes (decoded to the UTF-16 units it
+// compares): \\ \" and </ escaped, \b \t \n \f \r, \\u00XX below ' ', in [U+0080, U+00A0) and
+// \\u20XX in [U+2000, U+2100), lowercase hex; every other byte as is
+template <bool WRITE>
+__device__ void json_quote(Sink<WRITE>& s, const unsigned char* b, uint64_t n) {
+    s.put('"');
+    unsigned prev = 0;
+    const char* hx = "0123456789abcdef";
+    for (uint64_t t = 0; t < n;) {
+        const unsigned c0 = b[t];
+        unsigned cp = c0;
+        int len = 1;
+        if (c0 >= 0xC0 && c0 < 0xE0 && t + 1 < n) {
+            cp = ((c0 & 0x1Fu) << 6) | (b[t + 1] & 0x3Fu);
+            len = 2;
+        } else if (c0 >= 0xE0 && c0 < 0xF0 && t + 2 < n) {
+            cp = ((c0 & 0x0Fu) << 12) | ((b[t + 1] & 0x3Fu) << 6) | (b[t + 2] & 0x3Fu);
+            len = 3;
+        } else if (c0 >= 0xF0 && t + 3 < n) {
+            cp = 0x10000u;  // a surrogate pair in Java: never escaped
+            len = 4;
+        }
+        if (cp == '\\' || cp == '"') {
+            s.put('\\');
+            s.put((char)cp);
+        } else if (cp == '/') {
+            if (prev == '<') s.put('\\');
+            s.put('/');
+        } else if (cp == '\b') {
+            s.lit("\\b");
+        } else if (cp == '\t') {
+            s.lit("\\t");
+        } else if (cp == '\n') {
+            s.lit("\\n");
+        } else if (cp == '\f') {
+            s.lit("\\f");
+        } else if (cp == '\r') {
+            s.lit("\\r");
+        } else if (cp < 0x20 || (cp >= 0x80 && cp < 0xA0) || (cp >= 0x2000 && cp < 0x2100)) {
+            s.lit("\\u");
+            s.put(hx[(cp >> 12) & 15]);
+            s.put(hx[(cp >> 8) & 15]);
+            s.put(hx[(cp >> 4) & 15]);
+            s.put(hx[cp & 15]);
+        } else {
+            for (int q = 0; q < len; q++) s.put((char)b[t + q]);
+        }
+        prev = cp;
+        t += (uint64_t)len;
+    }
+    s.put('"');
+}
+
+// the record of point p; returns its length (0 and a flag where the reference would throw)
 template <bool WRITE>
 __device__ uint64_t fmt_record(const FmtArgs& a, uint64_t p, unsigned char* dst) {
-    uint64_t len = 0;
+    Sink<WRITE> s{dst, 0};
     char buf[32];
-    for (int pos = 0; pos < a.npos; pos++) {
-        const int f = a.field[pos];
-        int n = 0;
-        if (f == 0) {
-            if (a.oid) {
-                const uint64_t b = a.oid_off[p], e = a.oid_off[p + 1];
-                if (WRITE)
-                    for (uint64_t t = b; t < e; t++) dst[len + (t - b)] = a.oid[t];
-                len += e - b;
-            } else {
-                buf[0] = 'n'; buf[1] = 'u'; buf[2] = 'l'; buf[3] = 'l';
-                n = 4;
-            }
-        } else if (f == 1) {
-            n = java_long_to_string(a.ts ? a.ts[p] : 0ll, buf);
-        } else if (f == 2) {
-            n = java_double_to_string(a.x[p], buf);
-        } else if (f == 3) {
-            n = java_double_to_string(a.y[p], buf);
-        } else {
-            buf[0] = '0';
-            n = 1;
+    const long long ts = a.ts ? a.ts[p] : 0ll;
+    const bool has_oid = a.oid != nullptr;
+    const uint64_t ob = has_oid ? a.oid_off[p] : 0, oe = has_oid ? a.oid_off[p + 1] : 0;
+    char date[20];
+    if (a.format != GEOHIP_FMT_CSV && ts != 0) {
+        if (a.date != GEOHIP_DATE_YMD_HMS || !format_ymd_hms(ts, a.off_ms, date)) {
+            if (!WRITE) atomicOr(a.flags, kFlagDate);
+            return 0;
         }
-        if (WRITE)
-            for (int t = 0; t < n; t++) dst[len + t] = (unsigned char)buf[t];
-        len += (uint64_t)n;
-        // the delimiter after every field, the record's last character deleted (deleteCharAt)
-        const int dl = pos + 1 == a.npos ? a.dlen - 1 : a.dlen;
-        if (WRITE)
-            for (int t = 0; t < dl; t++) dst[len + t] = (unsigned char)a.delim[t];
-        len += (uint64_t)dl;
     }
-    if (WRITE) dst[len] = '\n';
-    return len + 1;
+    if (a.format == GEOHIP_FMT_WKT) {
+        // PointToWKTOutputSchema.serialize (Serialization.java:72-92)
+        s.put('"');
+        if (has_oid) {
+            for (uint64_t t = ob; t < oe; t++) s.put((char)a.oid[t]);
+            s.put(a.delim, a.dlen);
+            s.put(' ');
+        }
+        s.lit("POINT(");
+        s.put(buf, java_double_to_string(a.x[p], buf));
+        s.put(' ');
+        s.put(buf, java_double_to_string(a.y[p], buf));
+        s.put(')');
+        if (ts != 0) {
+            s.put(a.delim, a.dlen);
+            s.put(' ');
+            s.put(date, 19);
+        }
+        s.put('"');
+        s.put(a.delim, a.dlen);
+    } else if (a.format == GEOHIP_FMT_GEOJSON) {
+        // PointToGeoJSONOutputSchema.serialize (Serialization.java:28-50): org.json HashMap
+        // iteration order of the fixed keys (Java 8, 16 buckets, (h ^ h >>> 16) & 15):
+        // geometry 10, type 12, properties 14; coordinates 8, type 12; oID 11, timestamp 15
+        const double px = a.x[p], py = a.y[p];
+        if (!__builtin_isfinite(px) || !__builtin_isfinite(py)) {
+            if (!WRITE) atomicOr(a.flags, kFlagNonFinite);
+            return 0;
+        }
+        s.lit("{\"geometry\":{\"coordinates\":[");
+        s.put(buf, json_number(px, buf));
+        s.put(',');
+        s.put(buf, json_number(py, buf));
+        s.lit("],\"type\":\"Point\"},\"type\":\"Feature\"");
+        if (has_oid || ts != 0) {
+            s.lit(",\"properties\":{");
+            if (has_oid) {
+                s.lit("\"oID\":");
+                json_quote(s, a.oid + ob, oe - ob);
+            }
+            if (ts != 0) {
+                if (has_oid) s.put(',');
+                s.lit("\"timestamp\":\"");
+                s.put(date, 19);
+                s.put('"');
+            }
+            s.put('}');
+        }
+        s.put('}');
+    } else {
+        // PointToCSVTSVOutputSchema.serialize (Serialization.java:125-150)
+        for (int pos = 0; pos < a.npos; pos++) {
+            const int f = a.field[pos];
+            if (f == 0) {
+                if (has_oid) {
+                    for (uint64_t t = ob; t < oe; t++) s.put((char)a.oid[t]);
+                } else {
+                    s.lit("null");
+                }
+            } else if (f == 1) {
+                s.put(buf, java_long_to_string(ts, buf));
+            } else if (f == 2) {
+                s.put(buf, java_double_to_string(a.x[p], buf));
+            } else if (f == 3) {
+                s.put(buf, java_double_to_string(a.y[p], buf));
+            } else {
+                s.put('0');
+            }
+            // the delimiter after every field; deleteCharAt(length - 1) drops the record's last
+            // UTF-16 unit: the last delimiter's last character (a '?' stays for the high half
+            // of a supplementary one)
+            if (pos + 1 < a.npos) {
+                s.put(a.delim, a.dlen);
+            } else {
+                s.put(a.delim, a.csv_tail);
+                if (a.csv_tail_q) s.put('?');
+            }
+        }
+    }
+    s.put('\n');
+    return s.len;
+}
+
+__device__ __forceinline__ bool fmt_point(const FmtArgs& a, uint64_t j, uint64_t* p) {
+    *p = a.idx ? a.idx[j] : j;
+    return *p < a.n;
 }
 
 __global__ __launch_bounds__(kFmtTB) void fmt_len(FmtArgs a, unsigned long long* __restrict__ len) {
     const uint64_t j = (uint64_t)blockIdx.x * kFmtTB + threadIdx.x;
     if (j >= a.m) return;
-    const uint64_t p = a.idx ? a.idx[j] : j;
+    uint64_t p;
+    if (!fmt_point(a, j, &p)) {  // e.g. a padded kNN list's sentinel: no such point
+        atomicOr(a.flags, kFlagIdx);
+        len[j] = 0;
+        return;
+    }
     len[j] = fmt_record<false>(a, p, nullptr);
 }
 
@@ -521,39 +727,69 @@ __global__ __launch_bounds__(kFmtTB) void fmt_write(FmtArgs a, const unsigned lo
                                                     unsigned char* __restrict__ out, uint64_t cap) {
     const uint64_t j = (uint64_t)blockIdx.x * kFmtTB + threadIdx.x;
     if (j >= a.m) return;
-    if (off[j + 1] > cap) return;  // the whole record must fit
-    const uint64_t p = a.idx ? a.idx[j] : j;
+    if (off[j + 1] > cap || off[j + 1] == off[j]) return;  // the whole record must fit; flagged ones are empty
+    uint64_t p;
+    if (!fmt_point(a, j, &p)) return;
     (void)fmt_record<true>(a, p, out + off[j]);
+}
+
+// bytes of the last UTF-8 sequence of s[0, n) (0: malformed)
+int utf8_last_len(const char* s, int n) {
+    int b = n - 1;
+    while (b > 0 && ((unsigned char)s[b] & 0xC0u) == 0x80u) b--;
+    const unsigned c = (unsigned char)s[b];
+    const int want = c < 0x80 ? 1 : (c >= 0xC0 && c < 0xE0) ? 2 : (c >= 0xE0 && c < 0xF0) ? 3 : (c >= 0xF0 && c < 0xF8) ? 4 : 0;
+    return want == n - b ? want : 0;
 }
 
 }  // namespace
 
-int format_csv_impl(geohip_ctx* ctx, const geohip_csv_out_spec* spec, const double* x, const double* y,
-                    const int64_t* ts, const uint8_t* oid_text, const uint64_t* oid_off, const uint32_t* idx,
-                    uint64_t m, uint8_t* out, uint64_t cap, uint64_t* out_len, uint64_t* rec_off) {
+int format_points_impl(geohip_ctx* ctx, const geohip_text_out_spec* spec, const double* x, const double* y, uint64_t n,
+                       const int64_t* ts, const uint8_t* oid_text, const uint64_t* oid_off, const uint32_t* idx,
+                       uint64_t m, uint8_t* out, uint64_t cap, uint64_t* out_len, uint64_t* rec_off) {
     if (!spec || !out_len) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null spec / out_len");
     *out_len = 0;
-    if (ctx_mem(ctx) != GEOHIP_MEM_DEVICE) return ctx_fail(ctx, GEOHIP_ERR_ARG, "format_points_csv needs GEOHIP_MEM_DEVICE");
-    if (spec->delim_len < 1 || spec->delim_len > 8) return ctx_fail(ctx, GEOHIP_ERR_ARG, "delimiter length must be 1..8");
+    if (ctx_mem(ctx) != GEOHIP_MEM_DEVICE) return ctx_fail(ctx, GEOHIP_ERR_ARG, "format_points needs GEOHIP_MEM_DEVICE");
+    if (spec->format != GEOHIP_FMT_CSV && spec->format != GEOHIP_FMT_GEOJSON && spec->format != GEOHIP_FMT_WKT)
+        return ctx_fail(ctx, GEOHIP_ERR_ARG, "unknown output format");
+    if (spec->format != GEOHIP_FMT_GEOJSON && (spec->delim_len < 1 || spec->delim_len > 8))
+        return ctx_fail(ctx, GEOHIP_ERR_ARG, "delimiter length must be 1..8");
+    if (spec->date_format != GEOHIP_DATE_NONE && spec->date_format != GEOHIP_DATE_YMD_HMS)
+        return ctx_fail(ctx, GEOHIP_ERR_ARG, "unknown date format");
+    if (spec->utc_offset_min < -24 * 60 || spec->utc_offset_min > 24 * 60)
+        return ctx_fail(ctx, GEOHIP_ERR_ARG, "utc offset outside +-24 h");
     if (m && (!x || !y)) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null x / y");
     if ((oid_text == nullptr) != (oid_off == nullptr)) return ctx_fail(ctx, GEOHIP_ERR_ARG, "oid_text and oid_off go together");
     if (cap && !out) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null out");
+    if (!idx && m > n) return ctx_fail(ctx, GEOHIP_ERR_ARG, "m > n without idx");
     FmtArgs a;
     memset(&a, 0, sizeof a);
-    // positionMap (Serialization.java:117-120): later fields win a shared position
-    const int32_t attrs[4] = {spec->attr_oid, spec->attr_ts, spec->attr_x, spec->attr_y};
-    int maxp = -1;
-    for (int k = 0; k < 4; k++) {
-        if (attrs[k] < 0 || attrs[k] >= kMaxPos) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "schema positions must be 0..63");
-        maxp = attrs[k] > maxp ? attrs[k] : maxp;
+    a.format = spec->format;
+    if (spec->format == GEOHIP_FMT_CSV) {
+        // positionMap (Serialization.java:117-120): later fields win a shared position
+        const int32_t attrs[4] = {spec->attr_oid, spec->attr_ts, spec->attr_x, spec->attr_y};
+        int maxp = -1;
+        for (int k = 0; k < 4; k++) {
+            if (attrs[k] < 0 || attrs[k] >= kMaxPos) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "schema positions must be 0..63");
+            maxp = attrs[k] > maxp ? attrs[k] : maxp;
+        }
+        for (int p = 0; p < kMaxPos; p++) a.field[p] = -1;
+        for (int k = 0; k < 4; k++) a.field[attrs[k]] = (int8_t)k;
+        a.npos = maxp + 1;
+        const int last = utf8_last_len(spec->delim, spec->delim_len);
+        if (!last) return ctx_fail(ctx, GEOHIP_ERR_ARG, "delimiter is not UTF-8");
+        a.csv_tail = spec->delim_len - last;
+        a.csv_tail_q = last == 4 ? 1 : 0;
     }
-    for (int p = 0; p < kMaxPos; p++) a.field[p] = -1;
-    for (int k = 0; k < 4; k++) a.field[attrs[k]] = (int8_t)k;
-    a.npos = maxp + 1;
-    memcpy(a.delim, spec->delim, 8);
-    a.dlen = spec->delim_len;
+    if (spec->format != GEOHIP_FMT_GEOJSON) {
+        memcpy(a.delim, spec->delim, 8);
+        a.dlen = spec->delim_len;
+    }
+    a.date = spec->date_format;
+    a.off_ms = (long long)spec->utc_offset_min * 60000ll;
     a.x = x;
     a.y = y;
+    a.n = n;
     a.ts = reinterpret_cast<const long long*>(ts);
     a.oid = oid_text;
     a.oid_off = reinterpret_cast<const unsigned long long*>(oid_off);
@@ -564,29 +800,53 @@ int format_csv_impl(geohip_ctx* ctx, const geohip_csv_out_spec* spec, const doub
     void *pl = nullptr, *po = nullptr, *pb = nullptr;
     int rc = ctx_ensure(ctx, 0, 8 * (m + 1), &pl);
     if (!rc) rc = ctx_ensure(ctx, 1, 8 * (m + 2), &po);
-    if (!rc) rc = ctx_ensure(ctx, 2, 8 * (nb + 2), &pb);
+    if (!rc) rc = ctx_ensure(ctx, 2, 8 * (nb + 4), &pb);
     if (rc) return rc;
     unsigned long long* len = reinterpret_cast<unsigned long long*>(pl);
     unsigned long long* off = rec_off ? reinterpret_cast<unsigned long long*>(rec_off) : reinterpret_cast<unsigned long long*>(po);
     unsigned long long* bsum = reinterpret_cast<unsigned long long*>(pb);
-    unsigned long long* total = bsum + nb + 1;
+    unsigned long long* total = bsum + nb + 1;  // total, then the flags word
+    a.flags = reinterpret_cast<unsigned*>(total + 1);
+    if (hipMemsetAsync(total, 0, 16, st) != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
     if (m) {
         fmt_len<<<(unsigned)nb, kFmtTB, 0, st>>>(a, len);
         fmt_scan_blocks<<<(unsigned)nb, kFmtTB, 0, st>>>(len, m, bsum);
         fmt_scan_top<<<1, 1, 0, st>>>(bsum, nb, total);
         fmt_scan_apply<<<(unsigned)nb, kFmtTB, 0, st>>>(len, m, bsum, total, off);
         if (cap) fmt_write<<<(unsigned)nb, kFmtTB, 0, st>>>(a, off, out, cap);
-    } else if (hipMemsetAsync(off, 0, 8, st) != hipSuccess || hipMemsetAsync(total, 0, 8, st) != hipSuccess) {
+    } else if (hipMemsetAsync(off, 0, 8, st) != hipSuccess) {
         return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, std::string("format launch: ") + hipGetErrorString(e));
     uint64_t* pin = ctx_pinned(ctx);
-    if (hipMemcpyAsync(pin, total, 8, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+    if (hipMemcpyAsync(pin, total, 16, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
         return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "length readback failed");
+    const unsigned flags = (unsigned)(pin[1] & 0xffffffffu);
     *out_len = pin[0];
+    if (flags & kFlagIdx) return ctx_fail(ctx, GEOHIP_ERR_ARG, "idx entry >= n (no such point; e.g. a kNN sentinel)");
+    if (flags & kFlagNonFinite)
+        return ctx_fail(ctx, GEOHIP_ERR_ARG, "GeoJSON of a non-finite coordinate (JSONObject.toString throws)");
+    if (flags & kFlagDate)
+        return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "a nonzero timestamp needs GEOHIP_DATE_YMD_HMS and years 1583..9999");
     if (pin[0] > cap) return ctx_fail(ctx, GEOHIP_ERR_CAPACITY, "output capacity too small; *out_len = required");
     return GEOHIP_OK;
+}
+
+int format_csv_impl(geohip_ctx* ctx, const geohip_csv_out_spec* spec, const double* x, const double* y, uint64_t n,
+                    const int64_t* ts, const uint8_t* oid_text, const uint64_t* oid_off, const uint32_t* idx,
+                    uint64_t m, uint8_t* out, uint64_t cap, uint64_t* out_len, uint64_t* rec_off) {
+    if (!spec || !out_len) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null spec / out_len");
+    geohip_text_out_spec t;
+    memset(&t, 0, sizeof t);
+    t.format = GEOHIP_FMT_CSV;
+    t.attr_oid = spec->attr_oid;
+    t.attr_ts = spec->attr_ts;
+    t.attr_x = spec->attr_x;
+    t.attr_y = spec->attr_y;
+    t.delim_len = spec->delim_len;
+    memcpy(t.delim, spec->delim, 8);
+    return format_points_impl(ctx, &t, x, y, n, ts, oid_text, oid_off, idx, m, out, cap, out_len, rec_off);
 }
 
 }  // namespace geohip

@@ -19,6 +19,7 @@ uint64_t* ctx_pinned(geohip_ctx* ctx);
 void ctx_timing_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1);
 int ctx_stage_xy(geohip_ctx* ctx, const double* x, const double* y, uint64_t n, int which, const double** dx,
                  const double** dy);
+void** ctx_pcache_slot(geohip_ctx* ctx);  // the ctx's point-polygon plan cache (owned by cell_kernels)
 
 // squared-distance screen bounds for "dist <= r" (r2lo < 0 / r2hi = inf where they cannot hold)
 void pp_screen_bounds(double r, double* r2lo, double* r2hi);
@@ -30,8 +31,11 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* grid_data, const geohip_gri
 int band_pack_impl(geohip_ctx* ctx, const geohip_grid* grid, int32_t nb, uint32_t world, const double* x,
                    const double* y, uint64_t n, int64_t base, double* out_x, double* out_y, int64_t* out_idx,
                    uint64_t* out_counts);
-// point CSV/TSV output codec (format.hip; geohip_format_points_csv)
-int format_csv_impl(geohip_ctx* ctx, const geohip_csv_out_spec* spec, const double* x, const double* y,
+// point output codecs (format.hip; geohip_format_points, geohip_format_points_csv)
+int format_points_impl(geohip_ctx* ctx, const geohip_text_out_spec* spec, const double* x, const double* y, uint64_t n,
+                       const int64_t* ts, const uint8_t* oid_text, const uint64_t* oid_off, const uint32_t* idx,
+                       uint64_t m, uint8_t* out, uint64_t cap, uint64_t* out_len, uint64_t* rec_off);
+int format_csv_impl(geohip_ctx* ctx, const geohip_csv_out_spec* spec, const double* x, const double* y, uint64_t n,
                     const int64_t* ts, const uint8_t* oid_text, const uint64_t* oid_off, const uint32_t* idx,
                     uint64_t m, uint8_t* out, uint64_t cap, uint64_t* out_len, uint64_t* rec_off);
 }  // namespace geohip

@@ -18,4 +18,10 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
 int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
                    const uint32_t* ring_off, uint32_t nring, const double* vx, const double* vy, double r, uint32_t k,
                    int approximate, uint32_t* out_idx, double* out_dist, uint32_t* out_count);
+// point kNN with k > GEOHIP_KNN_MAX_K: candidate scan, keys, radix select, sort (device outputs)
+int knn_pp_large_impl(geohip_ctx* ctx, const PointPlan& plan, const double* dx, const double* dy, uint64_t n,
+                      double qx, double qy, uint32_t k, double* od, unsigned* oi, unsigned* ocnt);
+// rank merge of nlists * list_len (> 8192) entries with k > 256 (device pointers)
+int knn_merge_large_impl(geohip_ctx* ctx, const unsigned long long* d, const unsigned* i, unsigned nlists,
+                         unsigned list_len, unsigned k, double* od, unsigned* oi, unsigned* ocnt);
 }  // namespace geohip

@@ -43,3 +43,43 @@ def test_csv_record_layout():
     assert J.format_point_csv(None, 0, 1.0, 2.0, (0, 1, 2, 2), ";") == "null;0;2.0"
     # a two-character delimiter keeps its first character at the end
     assert J.format_point_csv("x", 1, 3.0, 4.0, (0, 1, 2, 3), "||") == "x||1||3.0||4.0|"
+
+
+def test_csv_delete_char_is_one_utf16_unit():
+    # a BMP delimiter character goes whole; a supplementary one leaves its high surrogate ('?')
+    assert J.format_point_csv("x", 1, 3.0, 4.0, (0, 1, 2, 3), "é") == "xé1é3.0é4.0"
+    assert J.format_point_csv("x", 1, 3.0, 4.0, (0, 1, 2, 3), "\U0001F600") == "x\U0001F6001\U0001F6003.0\U0001F6004.0?"
+
+
+def test_java8_hashmap_order_of_the_schema_keys():
+    # String.hashCode by hand: "type" = 't'*31^3 + 'y'*31^2 + 'p'*31 + 'e' = 3575610 = 0x368f3a;
+    # (h ^ h >>> 16) & 15 = (0x368f3a ^ 0x36) & 15 = 0xc = 12
+    assert J.java_string_hash("type") == 3575610
+    assert J.java8_hashmap_order(["geometry", "properties", "type"]) == ["geometry", "type", "properties"]
+    assert J.java8_hashmap_order(["coordinates", "type"]) == ["coordinates", "type"]
+    assert J.java8_hashmap_order(["oID", "timestamp"]) == ["oID", "timestamp"]
+
+
+def test_json_number_and_quote():
+    assert J.json_number_to_string(116.0) == "116"
+    assert J.json_number_to_string(116.5) == "116.5"
+    assert J.json_number_to_string(-0.0) == "-0"
+    assert J.json_number_to_string(1e-5) == "1.0E-5"  # an exponent: nothing shaved
+    assert J.json_number_to_string(100.0) == "100"
+    assert J.json_quote("") == '""'
+    assert J.json_quote('a"b\\c</d/e') == '"a\\"b\\\\c<\\/d/e"'
+    assert J.json_quote("\x01\t\u0085  ") == '"\\u0001\\t\\u0085\\u2028 "'
+
+
+def test_wkt_and_geojson_layout():
+    # 2021-01-19 02:14:09.423 UTC
+    ts = 1611022449423
+    assert J.java_date_ymd_hms(ts) == "2021-01-19 02:14:09"
+    assert J.java_date_ymd_hms(ts, 480) == "2021-01-19 10:14:09"
+    assert J.java_date_ymd_hms(-1) == "1969-12-31 23:59:59"
+    assert J.format_point_wkt("17", ts, 116.5, 40.25, ",") == '"17, POINT(116.5 40.25), 2021-01-19 02:14:09",'
+    assert J.format_point_wkt(None, 0, 116.5, 40.0, "\t") == '"POINT(116.5 40.0)"\t'
+    assert (J.format_point_geojson("17", ts, 116.5, 40.0) ==
+            '{"geometry":{"coordinates":[116.5,40],"type":"Point"},"type":"Feature",'
+            '"properties":{"oID":"17","timestamp":"2021-01-19 02:14:09"}}')
+    assert J.format_point_geojson(None, 0, 1.0, 2.0) == '{"geometry":{"coordinates":[1,2],"type":"Point"},"type":"Feature"}'

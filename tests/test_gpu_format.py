@@ -81,3 +81,114 @@ def test_csv_records_fields_and_subsets(ctx):
     assert bytes(text.cpu().numpy()).decode().split("\n")[0].startswith("null,0,")
     with pytest.raises(_abi.GeohipCapacityError):
         ctx.format_points_csv(spec, tx, ty, cap=100)
+
+
+def _oid_tensors(oids):
+    import torch
+    enc = [o.encode() for o in oids]
+    off = np.zeros(len(enc) + 1, np.int64)
+    off[1:] = np.cumsum([len(e) for e in enc])
+    text = np.frombuffer(b"".join(enc) or b"\0", np.uint8).copy()
+    return torch.from_numpy(text).cuda(), torch.from_numpy(off).cuda()
+
+
+_ODD_OIDS = ["", "plain", 'q"uote', "back\\slash", "</tag>", "a/b", "tab\there", "nl\nx", "\x01\x1f", "\x7f",
+             "\u0080\u0085\u009f ", "  ⃿℀", "café", "\U0001F600 smile", "\b\f\r"]
+
+
+@pytest.mark.parametrize("delim", [",", "\t", ";", "<->", "é", "\\\\t"])
+def test_wkt_records(ctx, delim):
+    """PointToWKTOutputSchema (Serialization.java:72-92) byte for byte vs the restatement."""
+    import torch
+    rng = np.random.default_rng(11)
+    n = 3000
+    x = _doubles(rng, 400)[:n]
+    x = np.concatenate([x, rng.uniform(115.5, 117.6, n - len(x))])
+    y = rng.permutation(x)
+    ts = rng.integers(-(1 << 40), 1 << 44, n).astype(np.int64)  # 1935 .. 2527
+    ts[::5] = 0
+    oids = [_ODD_OIDS[i % len(_ODD_OIDS)] + str(i) for i in range(n)]
+    toid, toff = _oid_tensors(oids)
+    tx, ty, tts = (torch.from_numpy(a).cuda() for a in (x, y, ts))
+    idx = rng.permutation(n)[:1001].astype(np.int32)
+    sep = "\\t" if delim == "\\\\t" else delim
+    for off_min in (0, 480, -300):
+        spec = _abi.make_text_out_spec(_abi.FMT_WKT, delimiter=delim, date_format=_abi.DATE_YMD_HMS,
+                                       utc_offset_min=off_min)
+        for use_idx, with_oid in ((False, True), (True, True), (True, False)):
+            text, off = ctx.format_points(spec, tx, ty, tts, toid if with_oid else None, toff if with_oid else None,
+                                          torch.from_numpy(idx).cuda() if use_idx else None)
+            pts = idx.tolist() if use_idx else range(n)
+            want = "".join(J.format_point_wkt(oids[p] if with_oid else None, int(ts[p]), float(x[p]), float(y[p]), sep,
+                                              off_min) + "\n" for p in pts)
+            assert bytes(text.cpu().numpy()).decode() == want
+            assert int(off[-1]) == len(want.encode())
+
+
+def test_geojson_records(ctx):
+    """PointToGeoJSONOutputSchema (Serialization.java:28-50) with org.json's HashMap key order,
+    numberToString and quote, byte for byte vs the restatement."""
+    import torch
+    rng = np.random.default_rng(12)
+    v = _doubles(rng, 4000)
+    v = v[np.isfinite(v)]
+    n = len(v)
+    x, y = v, rng.permutation(v)
+    ts = rng.integers(-(1 << 40), 1 << 44, n).astype(np.int64)
+    ts[::3] = 0
+    oids = [_ODD_OIDS[i % len(_ODD_OIDS)] + ("" if i % 7 else str(i)) for i in range(n)]
+    toid, toff = _oid_tensors(oids)
+    tx, ty, tts = (torch.from_numpy(a).cuda() for a in (x, y, ts))
+    for off_min, with_oid, with_ts in ((0, True, True), (330, True, True), (0, False, True), (0, False, False)):
+        spec = _abi.make_text_out_spec(_abi.FMT_GEOJSON, date_format=_abi.DATE_YMD_HMS, utc_offset_min=off_min)
+        text, off = ctx.format_points(spec, tx, ty, tts if with_ts else None, toid if with_oid else None,
+                                      toff if with_oid else None)
+        got = bytes(text.cpu().numpy()).decode().split("\n")[:-1]
+        assert len(got) == n
+        for p in range(n):
+            want = J.format_point_geojson(oids[p] if with_oid else None, int(ts[p]) if with_ts else 0, float(x[p]),
+                                          float(y[p]), off_min)
+            assert got[p] == want, (p, got[p], want)
+
+
+def test_codec_errors_where_the_reference_throws(ctx):
+    import torch
+    x = torch.tensor([116.0, math.nan, 117.0], dtype=torch.float64, device="cuda")
+    y = torch.tensor([40.0, 40.5, math.inf], dtype=torch.float64, device="cuda")
+    gj = _abi.make_text_out_spec(_abi.FMT_GEOJSON)
+    with pytest.raises(_abi.GeohipArgumentError):  # JSONObject.toString -> null -> NPE
+        ctx.format_points(gj, x, y)
+    text, _ = ctx.format_points(gj, x, y, idx=torch.tensor([0], dtype=torch.int32, device="cuda"))
+    assert bytes(text.cpu().numpy()).decode() == '{"geometry":{"coordinates":[116,40],"type":"Point"},"type":"Feature"}\n'
+    # a padded kNN list (sentinel -1 = 0xffffffff) names no point
+    csv = _abi.make_csv_out_spec()
+    with pytest.raises(_abi.GeohipArgumentError):
+        ctx.format_points_csv(csv, x, y, idx=torch.tensor([0, -1], dtype=torch.int32, device="cuda"))
+    with pytest.raises(_abi.GeohipArgumentError):
+        ctx.format_points(_abi.make_text_out_spec(_abi.FMT_WKT), x, y, idx=torch.tensor([3], dtype=torch.int32,
+                                                                                         device="cuda"))
+    # a nonzero timestamp without the caller's DateFormat, or outside the supported years
+    ts = torch.tensor([0, 1, 0], dtype=torch.int64, device="cuda")
+    with pytest.raises(_abi.GeohipUnsupportedError):
+        ctx.format_points(_abi.make_text_out_spec(_abi.FMT_WKT), x, y, ts)
+    far = torch.tensor([0, 1 << 60, 0], dtype=torch.int64, device="cuda")
+    with pytest.raises(_abi.GeohipUnsupportedError):
+        ctx.format_points(_abi.make_text_out_spec(_abi.FMT_WKT, date_format=_abi.DATE_YMD_HMS), x, y, far)
+    # the CSV codec never formats dates: its timestamps are Long.toString
+    text, _ = ctx.format_points(_abi.make_text_out_spec(_abi.FMT_CSV), x, y, far)
+    assert bytes(text.cpu().numpy()).decode().split("\n")[1] == "null,%d,NaN,40.5" % (1 << 60)
+
+
+@pytest.mark.parametrize("delim", ["é", "€", "\U0001F600", "a\U0001F600", "\\\\t"])
+def test_csv_multibyte_delimiter_delete_char(ctx, delim):
+    """deleteCharAt(length - 1) drops one UTF-16 unit of the last delimiter: the whole of a BMP
+    character, the low half of a supplementary one (its high half is written as '?')."""
+    import torch
+    x = torch.tensor([116.5, 117.25], dtype=torch.float64, device="cuda")
+    y = torch.tensor([40.0, 39.75], dtype=torch.float64, device="cuda")
+    spec = _abi.make_csv_out_spec((0, 1, 2, 3), delim)
+    text, _ = ctx.format_points_csv(spec, x, y)
+    sep = "\\t" if delim == "\\\\t" else delim
+    want = "".join(J.format_point_csv(None, 0, float(a), float(b), (0, 1, 2, 3), sep) + "\n"
+                   for a, b in ((116.5, 40.0), (117.25, 39.75)))
+    assert bytes(text.cpu().numpy()).decode() == want

@@ -156,3 +156,47 @@ def test_c5_shard_knn_and_range_full_scale(ctx):
     assert fi.cpu().numpy().astype(np.uint32).tolist() == wi.tolist()
     assert np.array_equal(fd.cpu().numpy().view(np.uint64), wd.view(np.uint64))
     assert fr.cpu().numpy().astype(np.uint32).tolist() == want.tolist()
+
+
+def test_c5_as_configured_200m_window_eight_shards(ctx):
+    """BASELINE configs[4] as configured: one 200M-point window (3.2 GB, on one device) split into
+    eight 25M-point shards, each evaluated by the fused kNN (k = 100) + range (r = 0.05) pass
+    (geohip_knn_range_pp_async, the per-GPU step of the 8-GPU job), the eight top-k lists merged
+    by geohip_knn_merge_async (the windowAll merge, KNNQuery.java:204-272) and the range hits
+    concatenated in shard order -- against the oracle over the whole window: kNN indices and
+    distance bits, the exact range hit list."""
+    import torch
+    n, S, k, r = 200_000_000, 8, 100, 0.05
+    per = n // S
+    x = torch.empty(n, dtype=torch.float64, device="cuda")
+    y = torch.empty(n, dtype=torch.float64, device="cuda")
+    ctx.synth_uniform_async(x, y, 0, 7, BJ)
+    ag, cg = agrid(1000)
+    ki = torch.empty((S, k), dtype=torch.int32, device="cuda")
+    kd = torch.empty((S, k), dtype=torch.float64, device="cuda")
+    kc = torch.zeros(S + 1, dtype=torch.int32, device="cuda")
+    cap = 1 << 21
+    ro = torch.empty((S, cap), dtype=torch.int32, device="cuda")
+    rc = torch.zeros(S, dtype=torch.int64, device="cuda")
+    for s in range(S):
+        xs, ys = x[s * per:(s + 1) * per], y[s * per:(s + 1) * per]
+        ctx.knn_range_pp_async(ag, xs, ys, Q[0], Q[1], r, k, False, ki[s], kd[s], kc[s:s + 1], ro[s], cap,
+                               rc[s:s + 1])
+    base = (torch.arange(S, dtype=torch.int32, device="cuda") * per).view(S, 1)
+    ki = torch.where(ki >= 0, ki + base, ki).contiguous()
+    mi = torch.empty(k, dtype=torch.int32, device="cuda")
+    md = torch.empty(k, dtype=torch.float64, device="cuda")
+    ctx.knn_merge_async(kd, ki, S, k, k, mi, md, kc[S:])
+    counts = rc.cpu().tolist()
+    assert max(counts) <= cap
+    hits = torch.cat([ro[s, :counts[s]].to(torch.int64) + s * per for s in range(S)]).cpu().numpy()
+    got_i, got_d = mi.cpu().numpy().astype(np.uint32), md.cpu().numpy()
+    assert int(kc[S].item()) == k
+    hx, hy = x.cpu().numpy(), y.cpu().numpy()
+    del x, y
+    wi, wd = cref.knn_pp(cg, hx, hy, Q[0], Q[1], r, k)
+    assert got_i.tolist() == wi.tolist()
+    assert np.array_equal(got_d.view(np.uint64), wd.view(np.uint64))
+    want = cref.range_pp(cg, hx, hy, Q[0], Q[1], r)
+    assert len(want) > 4e5
+    assert hits.tolist() == want.astype(np.int64).tolist()

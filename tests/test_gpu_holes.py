@@ -3,8 +3,9 @@ through the C ABI: geohip_range_ppoly / geohip_join_ppoly with poly_rings and ge
 with ring_off, against the C oracle (itself checked against the literal restatement in
 tests/test_oracle_ppoly.py and the golden holes fixtures).  Points in holes, on hole edges and
 vertices, within r of a hole ring, NaN points; holes listed before the shell, padded
-degenerate holes, holes crossing or outside the shell, clockwise holes, an open shell; 64
-rings; rings too long for LDS and too many segments for slab lists; the reference's errors.
+degenerate holes, holes crossing or outside the shell, clockwise holes, an open shell; 64, 65
+and 201 rings (ring masks in chunks of 64); rings too long for LDS and too many segments for
+slab lists; the reference's errors.
 Parity unpinned beyond the restatement: the reference ships no holed-polygon test.
 """
 import math
@@ -111,6 +112,58 @@ def test_many_and_long_rings(ctx):
         assert gi.tolist() == wi.tolist() and np.array_equal(gd.view(np.uint64), wd.view(np.uint64))
 
 
+def _lattice_polygon(cx, cy, R, nh, rng):
+    """A square shell with nh small holes: a lattice, every 7th hole overlapping its neighbour
+    (a point in both is decided by the first in ring order), a few clockwise, some listed
+    before the shell is the largest ring anyway."""
+    sq = [(cx - R, cy - R), (cx + R, cy - R), (cx + R, cy + R), (cx - R, cy + R)]
+    side = int(math.ceil(math.sqrt(nh)))
+    step = 1.8 * R / side
+    holes = []
+    for i in range(nh):
+        hx_, hy_ = cx - 0.9 * R + (i % side) * step, cy - 0.9 * R + (i // side) * step
+        w = step * (0.9 if i % 7 == 3 else 0.5)
+        h = [(hx_, hy_), (hx_ + w, hy_), (hx_ + w, hy_ + w), (hx_, hy_ + w)]
+        holes.append(h[::-1] if i % 5 == 1 else h)
+    return holes[:3] + [sq] + holes[3:]
+
+
+def test_two_hundred_holes(ctx):
+    """A polygon of 201 rings (4 mask chunks) and one of 130 with a long shell, through range,
+    join and kNN (k = 1, 100, 256) against the oracle, with points on hole edges and vertices."""
+    rng = np.random.default_rng(21)
+    p1 = _lattice_polygon(116.4, 40.3, 0.05, 200, rng)
+    big = synth._star(rng, 116.8, 40.6, 0.04, 700)
+    p2 = [big] + [synth._star(rng, 116.8 + 0.025 * math.cos(a), 40.6 + 0.025 * math.sin(a), 0.0015, 8)
+                  for a in np.linspace(0, 2 * math.pi, 129, endpoint=False)]
+    polys = [p1, p2]
+    pr = np.array([0, len(p1), len(p1) + len(p2)], np.uint32)
+    off, vx, vy = _flat([ring for rings in polys for ring in rings])
+    x, y = holed_window(rng, 150000, polys, 0.002)
+    # points exactly on hole vertices and edge midpoints of the 200-hole polygon
+    hv = np.array([c for ring in p1 for c in ring])
+    mid = (hv[:-1] + hv[1:]) / 2
+    x = np.concatenate([x, hv[:, 0], mid[:, 0]])
+    y = np.concatenate([y, hv[:, 1], mid[:, 1]])
+    ag, cg = agrid(500)
+    for r in (0.0004, 0.002):
+        got = ctx.range_ppoly(ag, x, y, off, vx, vy, r, poly_rings=pr)
+        want = cref.range_ppoly(cg, x, y, off, vx, vy, r, poly_rings=pr)
+        assert len(want) > 1000
+        assert pairs_sorted(got).tolist() == pairs_sorted(want).tolist()
+        got = ctx.join_ppoly(ag, ag, x, y, off, vx, vy, r, poly_rings=pr)
+        want = cref.join_ppoly(cg, cg, x, y, off, vx, vy, r, poly_rings=pr)
+        assert pairs_sorted(got).tolist() == pairs_sorted(want).tolist()
+    for p in range(2):
+        a, b = pr[p], pr[p + 1]
+        ro = off[a:b + 1] - off[a]
+        px, py = vx[off[a]:off[b]], vy[off[a]:off[b]]
+        for k in (1, 100, 256):
+            gi, gd = ctx.knn_ppoly(ag, x, y, px, py, 0.002, k, ring_off=ro)
+            wi, wd = cref.knn_ppoly(cg, x, y, px, py, 0.002, k, ring_off=ro)
+            assert gi.tolist() == wi.tolist() and np.array_equal(gd.view(np.uint64), wd.view(np.uint64))
+
+
 def test_holes_device_window_and_repeat(ctx):
     """Device-resident points; the cached plan is reused on a repeat call and replaced when
     only the ring grouping changes (same vertices, other poly_rings)."""
@@ -159,13 +212,15 @@ def test_holes_errors_and_empty(ctx):
     # a polygon without rings
     with pytest.raises(_abi.GeohipArgumentError):
         ctx.range_ppoly(ag, x, y, off, vx, vy, 0.01, poly_rings=np.array([0, 0, 2], np.uint32))
-    # 65 rings
+    # 65 rings (one past a mask chunk): accepted like any ring count (Polygon.java:115-165)
     rings = [shell] + [hole] * 64
     off4, vx4, vy4 = _flat(rings)
-    with pytest.raises(_abi.GeohipUnsupportedError):
-        ctx.range_ppoly(ag, x, y, off4, vx4, vy4, 0.01, poly_rings=np.array([0, 65], np.uint32))
-    with pytest.raises(_abi.GeohipUnsupportedError):
-        ctx.knn_ppoly(ag, x, y, vx4, vy4, 0.01, 5, ring_off=off4)
+    got = ctx.range_ppoly(ag, x, y, off4, vx4, vy4, 0.01, poly_rings=np.array([0, 65], np.uint32))
+    want = cref.range_ppoly(cg, x, y, off4, vx4, vy4, 0.01, poly_rings=np.array([0, 65], np.uint32))
+    assert pairs_sorted(got).tolist() == pairs_sorted(want).tolist()
+    gi, gd = ctx.knn_ppoly(ag, x, y, vx4, vy4, 0.01, 5, ring_off=off4)
+    wi, wd = cref.knn_ppoly(cg, x, y, vx4, vy4, 0.01, 5, ring_off=off4)
+    assert gi.tolist() == wi.tolist() and np.array_equal(gd.view(np.uint64), wd.view(np.uint64))
     # zero polygons, null arrays
     cnt = _abi.c_uint64(0)
     import ctypes

@@ -505,17 +505,75 @@ def test_knn_nan_ties_and_suffixes(ctx):
 
 
 def test_knn_large_k(ctx):
-    """k beyond the round-1 limit of 256 (PointPointKNNQuery takes any Integer k): 512, 1000 and
-    GEOHIP_KNN_MAX_K over a 2M-point window; k above the limit is GEOHIP_ERR_UNSUPPORTED."""
+    """Any k (PointPointKNNQuery.java:33 takes any Integer k): 512, 1000 and GEOHIP_KNN_MAX_K in
+    the one-pass selection, then the large-k form (candidates, radix select, sort) at 1025, 5000,
+    65536 and a k above the candidate count, over a 2M-point window with duplicates and NaN
+    points; host and device windows, the fused kNN + range form."""
+    import torch
     ag, cg = agrid(100)
     x, y = synth.uniform(2_000_000, 43)
-    for k in (512, 1000, _abi.KNN_MAX_K):
+    x[1000:1400] = x[0]  # exact duplicates: ties broken by index
+    y[1000:1400] = y[0]
+    x[5000:5010] = math.nan
+    for k in (512, 1000, _abi.KNN_MAX_K, _abi.KNN_MAX_K + 1, 5000, 65536, 1_500_000):
         wi, wd = cref.knn_pp(cg, x, y, Q[0], Q[1], 0.5, k)
         oi, od = ctx.knn_pp(ag, x, y, Q[0], Q[1], 0.5, k)
-        assert len(oi) == k
+        assert len(oi) == min(k, len(wi)) and (k < 1_000_000 or len(wi) < k)
         assert oi.tolist() == wi.tolist() and np.array_equal(od.view(np.uint64), wd.view(np.uint64))
-    with pytest.raises(_abi.GeohipUnsupportedError):
-        ctx.knn_pp(ag, x, y, Q[0], Q[1], 0.5, _abi.KNN_MAX_K + 1)
+    tx, ty = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+    k = 5000
+    wi, wd = cref.knn_pp(cg, x, y, Q[0], Q[1], 0.05, k)
+    oi, od = ctx.knn_pp(ag, tx, ty, Q[0], Q[1], 0.05, k)
+    assert oi.cpu().numpy().astype(np.uint32).tolist() == wi.tolist()
+    assert np.array_equal(od.cpu().numpy().view(np.uint64), wd.view(np.uint64))
+    (ki, kd), ro = ctx.knn_range_pp(ag, tx, ty, Q[0], Q[1], 0.05, k)
+    assert ki.cpu().numpy().astype(np.uint32).tolist() == wi.tolist()
+    assert sorted(ro.cpu().numpy().tolist()) == sorted(cref.range_pp(cg, x, y, Q[0], Q[1], 0.05).tolist())
+    # the async form pads past the candidate count with sentinels
+    oi = torch.empty(k, dtype=torch.int32, device="cuda")
+    od = torch.empty(k, dtype=torch.float64, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ctx.knn_pp_async(ag, tx[:20000], ty[:20000], Q[0], Q[1], 0.5, k, oi, od, cnt)
+    wi, wd = cref.knn_pp(cg, x[:20000], y[:20000], Q[0], Q[1], 0.5, k)
+    m = int(cnt.item())
+    assert m == len(wi) < k
+    assert oi[:m].cpu().numpy().astype(np.uint32).tolist() == wi.tolist()
+    assert (oi[m:] == -1).all() and (od[m:].view(torch.int64) == -1).all()
+
+
+@pytest.mark.parametrize("nlists,k", [(8, 100), (8, 1024), (9, 1024), (64, 300), (3, 5000)])
+def test_knn_merge_many_lists(ctx, nlists, k):
+    """geohip_knn_merge_async over nlists per-shard top-k lists (KNNQuery.java:204-272's merge,
+    one list per rank): 8 x 100 is the C5 form, 8 x 1024 fills one workgroup's LDS sort (8192
+    entries), 9 x 1024, 64 x 300 and 3 x 5000 take the large-k sort.  Shards of unequal length,
+    one shard shorter than k (sentinel-padded list)."""
+    import torch
+    rng = np.random.default_rng(nlists * 7 + k)
+    hx, hy = _window(rng, 600000)
+    hx[77:90] = hx[5]  # ties across shards
+    hy[77:90] = hy[5]
+    ag, cg = agrid(100)
+    cuts = np.sort(rng.choice(np.arange(1, len(hx)), nlists - 1, replace=False))
+    cuts[0] = 300  # a shard with fewer candidates than k
+    bounds = [0, *cuts.tolist(), len(hx)]
+    d_all = torch.empty((nlists, k), dtype=torch.float64, device="cuda")
+    i_all = torch.empty((nlists, k), dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(nlists + 1, dtype=torch.int32, device="cuda")
+    for s in range(nlists):
+        a, b = bounds[s], bounds[s + 1]
+        xs = torch.from_numpy(hx[a:b].copy()).cuda()
+        ys = torch.from_numpy(hy[a:b].copy()).cuda()
+        ctx.knn_pp_async(ag, xs, ys, Q[0], Q[1], 0.5, k, i_all[s], d_all[s], cnt[s:s + 1])
+        torch.cuda.synchronize()
+        i_all[s] = torch.where(i_all[s] != -1, i_all[s] + a, i_all[s])
+    oi = torch.empty(k, dtype=torch.int32, device="cuda")
+    od = torch.empty(k, dtype=torch.float64, device="cuda")
+    ctx.knn_merge_async(d_all, i_all, nlists, k, k, oi, od, cnt[nlists:])
+    torch.cuda.synchronize()
+    wi, wd = cref.knn_pp(cg, hx, hy, Q[0], Q[1], 0.5, k)
+    assert int(cnt[nlists].item()) == len(wi)
+    assert oi[:len(wi)].cpu().numpy().astype(np.uint32).tolist() == wi.tolist()
+    assert np.array_equal(od[:len(wi)].cpu().numpy().view(np.uint64), wd.view(np.uint64))
 
 
 # ------------------------------------------------------------------ less common kernel paths --

@@ -139,10 +139,26 @@ def test_knn_ppoly_errors(ctx):
     sq_x, sq_y = np.array([116.3, 116.4, 116.4, 116.3]), np.array([40.1, 40.1, 40.2, 40.2])
     with pytest.raises(_abi.GeohipArgumentError):
         ctx.knn_ppoly(ag, x, y, sq_x, sq_y, 0.01, 0)
-    with pytest.raises(_abi.GeohipUnsupportedError):
-        ctx.knn_ppoly(ag, x, y, sq_x, sq_y, 0.01, _abi.KNN_PPOLY_MAX_K + 1)
     with pytest.raises(_abi.GeohipArgumentError):
         ctx.knn_ppoly(ag, x, y, sq_x[:3], sq_y[:3], 0.01, 5)  # <= 3 coordinates (Polygon.java:53)
+
+
+@pytest.mark.parametrize("approx", [False, True])
+def test_knn_ppoly_large_k(ctx, approx):
+    """Any k (PointPolygonKNNQuery.java:34): GEOHIP_KNN_PPOLY_MAX_K + 1, 2000 and 60000 take the
+    large-k form (radix rounds, gather, sort); a k above the candidate count returns them all.
+    Points inside the polygon tie at distance 0 (ordered by index)."""
+    ag, cg = agrid(500)
+    rng = np.random.default_rng(77)
+    x, y = synth.uniform(1_000_000, 78)
+    star = np.array(synth._star(rng, 116.4, 40.2, 0.02, 50))
+    ring_x, ring_y = star[:, 0].copy(), star[:, 1].copy()
+    for k in (_abi.KNN_PPOLY_MAX_K + 1, 2000, 60000):
+        gi, gd = ctx.knn_ppoly(ag, x, y, ring_x, ring_y, 0.005, k, approx)
+        wi, wd = cref.knn_ppoly(cg, x, y, ring_x, ring_y, 0.005, k, approx)
+        assert len(wi) <= k and (k < 50000 or len(wi) < k)
+        assert gi.tolist() == wi.tolist()
+        assert np.array_equal(gd.view(np.uint64), wd.view(np.uint64))
 
 
 def test_knn_ppoly_c4_size(ctx):

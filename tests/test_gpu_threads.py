@@ -66,3 +66,45 @@ def test_four_threads_four_contexts():
         h.join(timeout=240)
     assert not any(h.is_alive() for h in th), "a worker thread did not finish"
     assert not errors, errors
+
+
+def test_one_ctx_alternating_torch_streams(ctx):
+    """One ctx following torch's current stream while the caller alternates two streams: the ctx
+    scratch (block lists, spill counter, look-back words) is shared by every call, so a rebinding
+    orders the new stream after the old one's queued work (geohip_ctx_set_stream).  kNN and range
+    calls alternate streams with no synchronisation in between; every result matches the oracle."""
+    import torch
+    from spatialflink_amd import synth
+    import cref
+    bj, q = synth.BEIJING, synth.README_QUERY
+    l = (bj[1] - bj[0]) / 100
+    ag, cg = _abi.make_grid(bj[0], bj[2], l, 100), cref.grid(bj[0], bj[2], l, 100)
+    wins = [synth.uniform(600_000 + 1000 * i, 900 + i) for i in range(3)]
+    dev = [(torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()) for a, b in wins]
+    s = [torch.cuda.Stream(), torch.cuda.Stream()]
+    ctx.follow_torch_stream(True)
+    R = 24
+    ki = torch.empty((R, 50), dtype=torch.int32, device="cuda")
+    kd = torch.empty((R, 50), dtype=torch.float64, device="cuda")
+    kc = torch.zeros(R, dtype=torch.int32, device="cuda")
+    ro = torch.empty((R, 700_000), dtype=torch.int32, device="cuda")
+    rc = torch.zeros(R, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    for i in range(R):
+        x, y = dev[i % 3]
+        with torch.cuda.stream(s[i % 2]):
+            if i % 4 < 2:
+                ctx.knn_pp_async(ag, x, y, q[0], q[1], 0.5, 50, ki[i], kd[i], kc[i:i + 1])
+            else:
+                ctx.range_pp_async(ag, x, y, q[0], q[1], 0.5, False, ro[i], 700_000, rc[i:i + 1])
+    torch.cuda.synchronize()
+    for i in range(R):
+        hx, hy = wins[i % 3]
+        if i % 4 < 2:
+            wi, wd = cref.knn_pp(cg, hx, hy, q[0], q[1], 0.5, 50)
+            assert ki[i].cpu().numpy().astype(np.uint32).tolist() == wi.tolist(), i
+            assert np.array_equal(kd[i].cpu().numpy().view(np.uint64), wd.view(np.uint64)), i
+        else:
+            want = sorted(cref.range_pp(cg, hx, hy, q[0], q[1], 0.5).tolist())
+            m = int(rc[i].item())
+            assert ro[i, :m].cpu().numpy().tolist() == want, i
