@@ -533,8 +533,8 @@ def test_knn_large_k(ctx):
     oi = torch.empty(k, dtype=torch.int32, device="cuda")
     od = torch.empty(k, dtype=torch.float64, device="cuda")
     cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
-    ctx.knn_pp_async(ag, tx[:20000], ty[:20000], Q[0], Q[1], 0.5, k, oi, od, cnt)
-    wi, wd = cref.knn_pp(cg, x[:20000], y[:20000], Q[0], Q[1], 0.5, k)
+    ctx.knn_pp_async(ag, tx[:10000], ty[:10000], Q[0], Q[1], 0.5, k, oi, od, cnt)
+    wi, wd = cref.knn_pp(cg, x[:10000], y[:10000], Q[0], Q[1], 0.5, k)
     m = int(cnt.item())
     assert m == len(wi) < k
     assert oi[:m].cpu().numpy().astype(np.uint32).tolist() == wi.tolist()
