@@ -63,6 +63,11 @@ def parse():
     p.add_argument("--no-pipelined", action="store_true", help="skip the multi-stream pipelined line")
     p.add_argument("--pipeline-streams", type=int, default=3, help="contexts / HIP streams of the pipelined line")
     p.add_argument("--check", action="store_true", help="N > 1 kNN / C5: check the merged top-k against rank 0's full window")
+    p.add_argument("--partition", choices=("arrival", "cells"), default="arrival",
+                   help="knn / c5 / join: the timed step's layout -- arrival-order shards (default) or the north-star "
+                        "grid-cell key bands (filter, keyBy(gridID) as one all-to-all, halo queries for the join)")
+    p.add_argument("--no-cells-line", action="store_true", help="skip the key-band layout side line (knn / c5 / join)")
+    p.add_argument("--cells-steps", type=int, default=10, help="timed steps of the key-band side line")
     p.add_argument("--time-every", type=int, default=8,
                    help="bracket every N-th timed step's kernels with HIP events (1 = all)")
     return p.parse_args()
@@ -125,6 +130,40 @@ class Workload:
 
     def e2e(self) -> dict | None:  # host-resident window -> results on host (rank 0, N = 1)
         return None
+
+    def cells_partition(self, steps: int) -> dict | None:  # the key-band layout side line
+        return None
+
+    def _timed_side(self, fn, steps):
+        """Max-over-ranks wall time of `steps` calls of fn(s) (barrier + synchronize around)."""
+        import torch
+        fn(0)
+        torch.cuda.synchronize(self.dev)
+        if self.dist:
+            self.dist.barrier()
+        t0 = time.perf_counter()
+        out = None
+        for s in range(steps):
+            out = fn(s)
+        torch.cuda.synchronize(self.dev)
+        if self.dist:
+            self.dist.barrier()
+        t = time.perf_counter() - t0
+        if self.dist:
+            tt = torch.tensor([t], dtype=torch.float64, device=self.dev if self.dist.get_backend() == "nccl" else "cpu")
+            self.dist.all_reduce(tt, op=self.dist.ReduceOp.MAX)
+            t = float(tt.item())
+        return t, out
+
+    def _gather_ints(self, v):
+        import torch
+        if not self.dist:
+            return [int(v)]
+        from spatialflink_amd import distributed as D
+        t = torch.tensor([int(v)], dtype=torch.int64, device=self.dev)
+        allv = torch.empty(self.world, dtype=torch.int64, device=self.dev)
+        D.all_gather_into(allv, t)
+        return [int(a) for a in allv.cpu().tolist()]
 
 
 def _uniform_windows(ctx, dev, n, rank, seeds, bbox):
@@ -230,8 +269,60 @@ class KnnWorkload(Workload):
                 wi.cpu().numpy().astype(np.uint32).tolist() and
                 torch.equal(self.m_d[:m].cpu().view(torch.int64), wd.cpu().view(torch.int64)))
 
+    def cells_window(self, w):
+        """One window in the north-star layout: the points of this rank's shard in the query's
+        G u C cells packed by key band (geohip_band_pack_query_async), one all-to-all to their
+        owner, the owner's kNN (+ range) of its band, one all-gather of the top-k + merge
+        (distributed.knn_range_cells)."""
+        import torch
+        from spatialflink_amd import distributed as D
+
+        def local(xs, ys, qx, qy, r, k, approximate):
+            oi = torch.full((k,), -1, dtype=torch.int32, device=self.dev)
+            od = torch.full((k,), -1, dtype=torch.int64, device=self.dev).view(torch.float64)
+            if self.has_range:
+                (ki, kd), ro = self.ctx.knn_range_pp(self.grid, xs, ys, qx, qy, r, k, approximate)
+            else:
+                ki, kd = self.ctx.knn_pp(self.grid, xs, ys, qx, qy, r, k)
+                ro = torch.zeros(0, dtype=torch.int32, device=self.dev)
+            oi[:len(ki)] = ki
+            od[:len(kd)] = kd
+            return oi, od, ro
+
+        return D.knn_range_cells(self.xs[w], self.ys[w], self.rank * self.n, self.q[0], self.q[1], self.radius,
+                                 self.k, grid=self.grid, ctx=self.ctx, local=local)
+
+    def cells_partition(self, steps):
+        """Side line: the key-band layout timed per window (max over ranks), per-rank skew of the
+        points each band owner receives, and a check against the arrival-sharded result."""
+        import torch
+        from spatialflink_amd import distributed as D
+        t, out = self._timed_side(lambda s: self.cells_window(s % self.windows), steps)
+        res, (hits, _, total), nrecv = out
+        w = (steps - 1) % self.windows
+        ref = D.knn_sharded(self.xs[w], self.ys[w], self.rank * self.n, self.q[0], self.q[1], self.radius, self.k,
+                            grid=self.grid, ctx=self.ctx)
+        same = (res.count == ref.count and torch.equal(res.idx.cpu(), ref.idx.cpu()) and
+                torch.equal(res.dist.cpu().view(torch.int64), ref.dist.cpu().view(torch.int64)))
+        if self.has_range:
+            _, _, rtotal = D.range_sharded(self.xs[w], self.ys[w], self.rank * self.n, self.q[0], self.q[1],
+                                           self.radius, grid=self.grid, ctx=self.ctx)
+            same = same and rtotal == total
+        ok = self._gather_ints(1 if same else 0)
+        recv = self._gather_ints(nrecv)
+        mean = sum(recv) / len(recv)
+        return {"value": self.n * self.world * steps / t, "unit": "points/sec", "ms_per_step": t / steps * 1e3,
+                "steps": steps, "layout": "grid-cell key bands (column cx -> rank cx*W/n): G u C filter + pack by owner "
+                "(geohip_band_pack_query_async), all_to_all, owner's kNN" + (" + range" if self.has_range else "") +
+                ", all_gather of top-k + geohip_knn_merge_async", "points_received_per_rank": recv,
+                "skew_max_over_mean": (max(recv) / mean) if mean else None,
+                "matches_arrival_sharding": all(ok)}
+
     def step(self, s):
         import torch
+        if self.args.partition == "cells":
+            self.cells_window(s % self.windows)
+            return
         j = s & 1
         if self.world > 1 and self.ev_done[j] is not None:
             torch.cuda.current_stream(self.dev).wait_event(self.ev_done[j])  # row j free again
@@ -461,9 +552,36 @@ class JoinWorkload(Workload):
     def units_per_step(self):
         return self.n
 
+    def cells_window(self, w):
+        """One window in the north-star layout (PointPointJoinQuery.java:137-150): data points
+        packed by owner key band (geohip_band_pack_async), one all-to-all, each owner joins its
+        band against the queries whose Nbr block meets it (halo replication)."""
+        from spatialflink_amd import distributed as D
+        return D.join_sharded(self.dx[w], self.dy[w], self.rank * self.n, self.qx, self.qy, self.radius,
+                              grid_data=self.grid, grid_query=self.grid, ctx=self.ctx,
+                              partition="cells" if self.world > 1 else "arrival")
+
+    def cells_partition(self, steps):
+        if self.world == 1:
+            return None  # one band: the arrival line itself
+        t, out = self._timed_side(lambda s: self.cells_window(s % self.windows), steps)
+        pairs, _, total = out
+        w = (steps - 1) % self.windows
+        want = sum(self._gather_ints(self.pairs[w]))
+        pr = self._gather_ints(len(pairs))
+        mean = sum(pr) / len(pr)
+        return {"value": self.n * self.world * steps / t, "unit": "points/sec", "ms_per_step": t / steps * 1e3,
+                "steps": steps, "layout": "grid-cell key bands: data points packed by owner band "
+                "(geohip_band_pack_async), all_to_all, halo query selection, owner's join",
+                "pairs_per_rank": pr, "skew_max_over_mean": (max(pr) / mean) if mean else None,
+                "matches_arrival_sharding": total == want}
+
     def step(self, s):
         import torch
         w = s % self.windows
+        if self.args.partition == "cells":
+            self.cells_window(w)
+            return
         self.ctx.join_pp(self.grid, self.grid, self.dx[w], self.dy[w], self.qx, self.qy, self.radius, out=self.out)
         if self.world > 1:
             self.dist.all_gather_into_tensor(self.counts, torch.tensor([self.pairs[w]], device=self.dev))
@@ -705,6 +823,9 @@ class KnnIncrWorkload(KnnWorkload):
     n_default = 5_000_000
     label = "C2 over 10s/5s sliding windows with pane reuse: kNN k=50, 100x100 Beijing UniformGrid, r=0.5"
 
+    def cells_partition(self, steps):  # pane reuse is a single-GPU stream form
+        return None
+
     def __init__(self, *a):
         super().__init__(*a)
         from spatialflink_amd.incremental import IncrementalKNN
@@ -938,6 +1059,12 @@ def main():
         ok = wl.check_merged(args.warmup + args.steps - 1)
         if rank == 0:
             result["merged_matches_full_window"] = ok
+    if not args.no_cells_line and args.partition == "arrival":
+        cells = wl.cells_partition(args.cells_steps)
+        if cells is not None and rank == 0:
+            result["partition_cells"] = cells
+    if args.partition == "cells":
+        result["config"]["parallelism"] = f"key-band{world} (north-star layout)"
     if rank == 0 and world == 1 and not args.no_e2e and args.workload == "knn":  # the C2 host path
         e2e = wl.e2e()
         if e2e is not None:

@@ -212,6 +212,15 @@ int geohip_band_pack_async(geohip_ctx* ctx, const geohip_grid* grid_data, int32_
                            const double* x, const double* y, uint64_t n, int64_t base, double* out_x,
                            double* out_y, int64_t* out_idx, uint64_t* out_counts_dev);
 
+/* The same partition for a single point query (kNN / range of (qx, qy) with radius r on
+   grid_data): only the points of the query's guaranteed and candidate cells are kept -- the
+   reference filters them before its keyBy(gridID) (PointPointKNNQuery.java:137-151,
+   PointPointRangeQuery.java:102-116) -- then grouped by the owner of their key band as above. */
+int geohip_band_pack_query_async(geohip_ctx* ctx, const geohip_grid* grid_data, int32_t nb, uint32_t world,
+                                 double qx, double qy, double r, const double* x, const double* y, uint64_t n,
+                                 int64_t base, double* out_x, double* out_y, int64_t* out_idx,
+                                 uint64_t* out_counts_dev);
+
 /* ---- output codecs ----------------------------------------------- */
 /* The point output schemas of spatialStreams/Serialization.java for m result points, as one text
    buffer: record j is point p = idx[j] (or j when idx is NULL; p >= n is GEOHIP_ERR_ARG, e.g. a

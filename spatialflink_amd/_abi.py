@@ -161,6 +161,8 @@ _SIGS = {
                                      POINTER(c_uint64), _P]),
     "geohip_band_pack_async": (c_int, [_P, POINTER(Grid), c_int32, c_uint32, _P, _P, c_uint64, ctypes.c_int64, _P, _P,
                                        _P, _P]),
+    "geohip_band_pack_query_async": (c_int, [_P, POINTER(Grid), c_int32, c_uint32, c_double, c_double, c_double, _P, _P,
+                                             c_uint64, ctypes.c_int64, _P, _P, _P, _P]),
     "geohip_knn_range_pp": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_double, c_double, c_double, c_uint32,
                                     c_int, _P, _P, POINTER(c_uint32), _P, c_uint64, POINTER(c_uint64)]),
     "geohip_knn_range_pp_async": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_double, c_double, c_double,
@@ -591,6 +593,29 @@ class Context:
                                         cnt.data_ptr())
         if rc:
             self._check(rc, "band_pack_async")
+        return ox[:n], oy[:n], oi[:n], cnt[:world]
+
+    def band_pack_query_async(self, grid_data: Grid, nb: int, world: int, qx: float, qy: float, r: float, x, y,
+                              base: int = 0):
+        """geohip_band_pack_query_async: as band_pack_async, keeping only the points of the point
+        query's G u C cells (the reference's filter before keyBy(gridID))."""
+        import torch
+        self._dev(x, "x")
+        self._dev(y, "y")
+        n = x.numel()
+        if y.numel() != n:
+            raise GeohipArgumentError("band_pack_query_async: x and y differ in length")
+        ox = torch.empty(max(n, 1), dtype=torch.float64, device=x.device)
+        oy = torch.empty_like(ox)
+        oi = torch.empty(max(n, 1), dtype=torch.int64, device=x.device)
+        cnt = torch.empty(max(world, 1), dtype=torch.int64, device=x.device)
+        if self._mem != MEM_DEVICE:
+            self.set_mem(MEM_DEVICE)
+        rc = lib.geohip_band_pack_query_async(self.h, ctypes.byref(grid_data), int(nb), int(world), qx, qy, r,
+                                              x.data_ptr(), y.data_ptr(), n, int(base), ox.data_ptr(), oy.data_ptr(),
+                                              oi.data_ptr(), cnt.data_ptr())
+        if rc:
+            self._check(rc, "band_pack_query_async")
         return ox[:n], oy[:n], oi[:n], cnt[:world]
 
     def range_pp_async(self, grid: Grid, x, y, qx, qy, r, approximate, out_idx, cap, out_count):

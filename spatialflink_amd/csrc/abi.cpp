@@ -783,6 +783,17 @@ int geohip_band_pack_async(geohip_ctx* ctx, const geohip_grid* grid_data, int32_
     return band_pack_impl(ctx, grid_data, nb, world, x, y, n, base, out_x, out_y, out_idx, out_counts_dev);
 }
 
+int geohip_band_pack_query_async(geohip_ctx* ctx, const geohip_grid* grid_data, int32_t nb, uint32_t world, double qx,
+                                 double qy, double r, const double* x, const double* y, uint64_t n, int64_t base,
+                                 double* out_x, double* out_y, int64_t* out_idx, uint64_t* out_counts_dev) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    PointPlan plan;
+    rc = plan_or_fail(ctx, grid_data, qx, qy, r, &plan);
+    if (rc) return rc;
+    return band_pack_impl(ctx, grid_data, nb, world, x, y, n, base, out_x, out_y, out_idx, out_counts_dev, &plan);
+}
+
 int geohip_knn_merge_async(geohip_ctx* ctx, const double* dist, const uint32_t* idx, uint32_t nlists,
                            uint32_t list_len, uint32_t k, uint32_t* out_idx, double* out_dist,
                            uint32_t* out_count_dev) {

@@ -17,6 +17,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string.h>
+
 #include <string>
 
 #include "device_common.h"
@@ -43,11 +45,19 @@ struct BandArgs {
     uint64_t n, chunk;
     double mnx, mny, l;
     int32_t nb, world;
+    Box u[kMaxPointBoxes + 1];  // nu > 0: only points of the query's G u C cells (planner boxes)
+    int32_t nu, pad;
 };
 
 // HelperClass.assignGridCellID (HelperClass.java:104-116) per axis, then the owner of the key's
-// column; -1 when the key is not a cell of the key space
+// column; -1 when the key is not a cell of the key space (or, with a query filter, when the
+// point lies in none of its guaranteed and candidate cells)
 __device__ __forceinline__ int band_owner(const BandArgs& a, uint64_t i) {
+    if (a.nu) {
+        bool in = false;
+        for (int b = 0; b < a.nu; b++) in = in || in_box(a.u[b], a.x[i], a.y[i]);
+        if (!in) return -1;
+    }
     const int32_t cx = band_d2i(__builtin_floor((a.x[i] - a.mnx) / a.l));
     const int32_t cy = band_d2i(__builtin_floor((a.y[i] - a.mny) / a.l));
     if (cx < 0 || cy < 0 || cx >= a.nb || cy >= a.nb) return -1;
@@ -146,7 +156,7 @@ __global__ __launch_bounds__(kBandTB) void band_scatter(BandArgs a, const unsign
 
 int band_pack_impl(geohip_ctx* ctx, const geohip_grid* grid, int32_t nb, uint32_t world, const double* x,
                    const double* y, uint64_t n, int64_t base, double* out_x, double* out_y, int64_t* out_idx,
-                   uint64_t* out_counts) {
+                   uint64_t* out_counts, const PointPlan* filter) {
     if (!grid || !out_counts) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null grid / out_counts");
     if (ctx_mem(ctx) != GEOHIP_MEM_DEVICE) return ctx_fail(ctx, GEOHIP_ERR_ARG, "band_pack_async needs GEOHIP_MEM_DEVICE");
     if (world == 0 || world > (uint32_t)kBandMaxWorld)
@@ -162,7 +172,26 @@ int band_pack_impl(geohip_ctx* ctx, const geohip_grid* grid, int32_t nb, uint32_
     }
     const uint64_t want_blocks = (n + 16ull * kBandTB - 1) / (16ull * kBandTB);
     const uint32_t nblk = (uint32_t)(want_blocks < (uint64_t)kBandMaxBlocks ? want_blocks : kBandMaxBlocks);
-    BandArgs a{x, y, n, (n + nblk - 1) / nblk, grid->min_x, grid->min_y, grid->cell_len, nb, (int32_t)world};
+    BandArgs a;
+    memset(&a, 0, sizeof a);
+    a.x = x;
+    a.y = y;
+    a.n = n;
+    a.chunk = (n + nblk - 1) / nblk;
+    a.mnx = grid->min_x;
+    a.mny = grid->min_y;
+    a.l = grid->cell_len;
+    a.nb = nb;
+    a.world = (int32_t)world;
+    if (filter) {
+        for (int b = 0; b < filter->nu; b++) a.u[b] = filter->u[b];
+        a.nu = filter->nu;
+        if (a.nu == 0) {  // no candidate cell at all (r <= 0): nothing to send
+            if (hipMemsetAsync(out_counts, 0, 8 * (size_t)world, st) != hipSuccess)
+                return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
+            return GEOHIP_OK;
+        }
+    }
     const uint32_t m = world * nblk;
     void* ph = nullptr;
     void* po = nullptr;

@@ -30,7 +30,7 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* grid_data, const geohip_gri
 // key-band owner partition of a window (band.hip; geohip_band_pack_async)
 int band_pack_impl(geohip_ctx* ctx, const geohip_grid* grid, int32_t nb, uint32_t world, const double* x,
                    const double* y, uint64_t n, int64_t base, double* out_x, double* out_y, int64_t* out_idx,
-                   uint64_t* out_counts);
+                   uint64_t* out_counts, const PointPlan* filter = nullptr);
 // point output codecs (format.hip; geohip_format_points, geohip_format_points_csv)
 int format_points_impl(geohip_ctx* ctx, const geohip_text_out_spec* spec, const double* x, const double* y, uint64_t n,
                        const int64_t* ts, const uint8_t* oid_text, const uint64_t* oid_off, const uint32_t* idx,

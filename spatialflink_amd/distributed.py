@@ -60,9 +60,8 @@ def knn_sharded(x_local, y_local, base: int, qx: float, qy: float, r: float, k: 
     (idx -1 / 0xffffffff, dist all-ones bits); merge(dist[W,k], idx[W,k], k) -> same shape.
     """
     import torch
-    import torch.distributed as dist
 
-    world = dist.get_world_size(group)
+    world, _ = _world_rank(group)
     if local_knn is None:
         local_knn = _device_local_knn(ctx, grid)
     if merge is None:
@@ -110,15 +109,18 @@ def _java_cell(v, mn: float, l: float):
     return t.clamp(-2147483648.0, 2147483647.0).to(torch.int64)
 
 
-def torch_band_pack(grid_data):
+def torch_band_pack(grid_data, keep=None):
     """band_pack written with torch ops (CPU orchestration tests; the product engine is
-    geohip_band_pack_async): same owners, same arrival order inside each owner group."""
+    geohip_band_pack_async): same owners, same arrival order inside each owner group.
+    keep(x, y) -> bool mask: an extra filter (the query's G u C cells for band_pack_query)."""
     import torch
 
     def f(x, y, base, nb, world):
         cx = _java_cell(x, grid_data.min_x, grid_data.cell_len)
         cy = _java_cell(y, grid_data.min_y, grid_data.cell_len)
         valid = (cx >= 0) & (cx < nb) & (cy >= 0) & (cy < nb)  # other keys match no Nbr block
+        if keep is not None:
+            valid = valid & keep(x, y)
         gidx = torch.arange(len(x), dtype=torch.int64, device=x.device) + base
         owner = (cx * world) // nb
         sel = torch.nonzero(valid).flatten()
@@ -127,6 +129,78 @@ def torch_band_pack(grid_data):
         return x[order], y[order], gidx[order], counts
 
     return f
+
+
+def torch_band_pack_query(grid_data, qx: float, qy: float, r: float):
+    """band_pack_query with torch ops (CPU tests): the query's G u C membership from the host
+    planner's exact boxes (geohip_debug_classify), then torch_band_pack."""
+    import torch
+
+    from . import _abi
+
+    def keep(x, y):
+        c = _abi.debug_classify(grid_data, qx, qy, r, x.cpu().numpy(), y.cpu().numpy())
+        return torch.from_numpy((c & 4) != 0).to(x.device)
+
+    return torch_band_pack(grid_data, keep)
+
+
+def knn_range_cells(x_local, y_local, base: int, qx: float, qy: float, r: float, k: int, approximate: bool = False,
+                    *, grid, ctx=None, group=None, band_pack: Optional[Callable] = None,
+                    local: Optional[Callable] = None, merge: Optional[Callable] = None):
+    """kNN (k) and range (r) of one point query over a window partitioned by grid-cell key band
+    (the north-star layout, mirroring the reference's filter + keyBy(gridID),
+    PointPointKNNQuery.java:137-151 / PointPointRangeQuery.java:102-116): every rank packs the
+    points of its arrival shard that lie in the query's G u C cells by owner band
+    (geohip_band_pack_query_async), one all-to-all moves them to their owner, each owner
+    evaluates its band, the top-k lists meet in one all-gather + merge (the windowAll funnel),
+    the range hits stay with their owner as window indices.
+    local(x, y, qx, qy, r, k, approximate) -> (idx int32 [k] sentinel -1, dist f64 [k], hits int
+    [m]), local indices.  Returns (KnnResult, (hits int64 window idx ascending, offset, total),
+    points received by this rank)."""
+    import torch
+
+    world, _ = _world_rank(group)
+    nb = int(grid.n)
+    if band_pack is None:
+        def band_pack(x, y, b, nb_, w):
+            return ctx.band_pack_query_async(grid, nb_, w, qx, qy, r, x, y, b)
+    if local is None:
+        local = _device_local_knn_range(ctx, grid)
+    if merge is None:
+        merge = _device_merge(ctx)
+    px, py, pg, send_counts = band_pack(x_local, y_local, base, nb, world)
+    if world > 1:
+        recv_counts = torch.empty_like(send_counts)
+        all_to_all(recv_counts, send_counts, group=group)
+        sc, rc = send_counts.tolist(), recv_counts.tolist()
+        nrecv, nsend = sum(rc), sum(sc)
+
+        def exchange(t):
+            out = torch.empty(nrecv, dtype=t.dtype, device=t.device)
+            all_to_all(out, t[:nsend], rc, sc, group)
+            return out
+
+        rx, ry, rg = exchange(px), exchange(py), exchange(pg)
+    else:
+        nrecv = int(send_counts.sum().item())
+        rx, ry, rg = px[:nrecv].contiguous(), py[:nrecv].contiguous(), pg[:nrecv]
+    li, ld, lh = local(rx, ry, qx, qy, r, k, approximate)
+    li64 = li.to(torch.int64)
+    gi = torch.where(li64 >= 0, rg[li64.clamp(min=0)] if nrecv else li64, torch.full_like(li64, -1)).to(torch.int32)
+    all_d = torch.empty((world, k), dtype=ld.dtype, device=ld.device)
+    all_i = torch.empty((world, k), dtype=torch.int32, device=ld.device)
+    if world > 1:
+        all_gather_into(all_d.view(-1), ld.contiguous(), group)
+        all_gather_into(all_i.view(-1), gi, group)
+    else:
+        all_d[0] = ld
+        all_i[0] = gi
+    mi, md = merge(all_d, all_i, k)
+    count = int((mi != -1).sum().item())
+    hits = rg[lh.to(torch.int64)] if len(lh) else torch.zeros(0, dtype=torch.int64, device=ld.device)
+    offset, total = gather_counts(len(hits), hits.device, group)
+    return KnnResult(mi[:count], md[:count], count), (hits, offset, total), nrecv
 
 
 def key_band(world: int, rank: int, nb: int):
@@ -258,12 +332,18 @@ def knn_ppoly_sharded(x_local, y_local, base: int, vx, vy, r: float, k: int, app
     return KnnResult(mi[:count], md[:count], count)
 
 
-def gather_counts(count: int, device, group=None):
-    import torch
+def _world_rank(group=None):
     import torch.distributed as dist
 
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
+    if not dist.is_available() or not dist.is_initialized():
+        return 1, 0  # a single process: the window is one shard
+    return dist.get_world_size(group), dist.get_rank(group)
+
+
+def gather_counts(count: int, device, group=None):
+    import torch
+
+    world, rank = _world_rank(group)
     t = torch.tensor([count], dtype=torch.int64, device=device)
     allc = torch.empty(world, dtype=torch.int64, device=device)
     if world > 1:
@@ -373,6 +453,20 @@ def _device_local_knn_ppoly(ctx, grid):
         oi[:len(ii)] = ii
         od[:len(dd)] = dd
         return oi, od
+
+    return f
+
+
+def _device_local_knn_range(ctx, grid):
+    import torch
+
+    def f(x, y, qx, qy, r, k, approximate):
+        (ki, kd), ro = ctx.knn_range_pp(grid, x, y, qx, qy, r, k, approximate)
+        oi = torch.full((k,), -1, dtype=torch.int32, device=x.device)
+        od = torch.full((k,), -1, dtype=torch.int64, device=x.device).view(torch.float64)  # all-ones bits
+        oi[:len(ki)] = ki
+        od[:len(kd)] = kd
+        return oi, od, ro
 
     return f
 

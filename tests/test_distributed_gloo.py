@@ -292,3 +292,94 @@ def test_sharded_ppoly_join_and_knn_gloo(tmp_path, world):
     assert res["knn_i"] == wi.astype(np.int64).tolist()
     assert [int(v) for v in res["knn_d"]] == wd.view(np.uint64).astype(np.int64).tolist() or \
         np.array_equal(np.array([int(v) for v in res["knn_d"]], dtype=np.uint64), wd.view(np.uint64))
+
+
+def _cells_worker(rank, world, port, out_path):
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "oracle"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import cref
+    from spatialflink_amd import _abi
+    from spatialflink_amd import distributed as D
+    from spatialflink_amd import synth
+
+    bj = synth.BEIJING
+    q = synth.README_QUERY
+    out = {}
+    for n_grid, r, k in ((100, 0.5, 50), (1000, 0.05, 100)):
+        l = (bj[1] - bj[0]) / n_grid
+        cg = cref.grid(bj[0], bj[2], l, n_grid)
+        ag = _abi.make_grid(bj[0], bj[2], l, n_grid)
+        n_total = 300_007
+        x, y = synth.uniform(n_total, 5 + n_grid)
+        x[:50] = q[0] + 1e-4 * np.arange(50)  # a dense clump at the query: one band owns it
+        y[:50] = q[1]
+        lo, hi = D.shard_bounds(n_total, world, rank)
+        xl, yl = torch.from_numpy(x[lo:hi].copy()), torch.from_numpy(y[lo:hi].copy())
+
+        def local(xs, ys, qx, qy, rr, kk, approximate):
+            oi, od = cref.knn_pp(cg, xs.numpy(), ys.numpy(), qx, qy, rr, kk)
+            ti = torch.full((kk,), -1, dtype=torch.int32)
+            td = _sentinel_d(kk)
+            ti[:len(oi)] = torch.from_numpy(oi.astype(np.int64)).to(torch.int32)
+            td[:len(od)] = torch.from_numpy(od)
+            hits = np.sort(cref.range_pp(cg, xs.numpy(), ys.numpy(), qx, qy, rr, approximate)).astype(np.int64)
+            return ti, td, torch.from_numpy(hits)
+
+        def merge(all_d, all_i, kk):
+            d = all_d.reshape(-1).view(torch.int64).numpy().astype(np.uint64)
+            i = all_i.reshape(-1).numpy().astype(np.int64) & 0xFFFFFFFF
+            keep = i != 0xFFFFFFFF
+            o = np.lexsort((i[keep], d[keep]))[:kk]
+            ti = torch.full((kk,), -1, dtype=torch.int32)
+            td = _sentinel_d(kk)
+            ti[:len(o)] = torch.from_numpy(i[keep][o].astype(np.int32))
+            td[:len(o)] = torch.from_numpy(d[keep][o].view(np.float64))
+            return ti, td
+
+        res, (hits, off, total), nrecv = D.knn_range_cells(
+            xl, yl, lo, q[0], q[1], r, k, grid=ag, band_pack=D.torch_band_pack_query(ag, q[0], q[1], r),
+            local=local, merge=merge)
+        gathered = [None] * world
+        dist.all_gather_object(gathered, (off, total, hits.numpy().tolist(), nrecv))
+        out[f"knn_i_{n_grid}"] = res.idx.numpy()
+        out[f"knn_d_{n_grid}"] = res.dist.numpy()
+        out[f"hits_{n_grid}"] = np.array(sorted(sum((g[2] for g in gathered), [])), dtype=np.int64)
+        out[f"totals_{n_grid}"] = np.array([g[1] for g in gathered])
+        out[f"recv_{n_grid}"] = np.array([g[3] for g in gathered])
+    if rank == 0:
+        np.savez(out_path, **out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_knn_range_key_band_partition_gloo(tmp_path, world):
+    """The north-star layout for point queries (filter to G u C, keyBy(gridID) as key bands,
+    PointPointKNNQuery.java:137-151): the merged kNN and the union of the owners' range hits equal
+    the unsharded oracle; every rank received only its band's candidates."""
+    out = tmp_path / "cells.npz"
+    mp.spawn(_cells_worker, args=(world, _free_port(), str(out)), nprocs=world, join=True)
+    r = np.load(out)
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import cref
+    from spatialflink_amd import synth
+
+    bj = synth.BEIJING
+    q = synth.README_QUERY
+    for n_grid, rad, k in ((100, 0.5, 50), (1000, 0.05, 100)):
+        l = (bj[1] - bj[0]) / n_grid
+        cg = cref.grid(bj[0], bj[2], l, n_grid)
+        x, y = synth.uniform(300_007, 5 + n_grid)
+        x[:50] = q[0] + 1e-4 * np.arange(50)
+        y[:50] = q[1]
+        wi, wd = cref.knn_pp(cg, x, y, q[0], q[1], rad, k)
+        assert r[f"knn_i_{n_grid}"].astype(np.uint32).tolist() == wi.tolist()
+        assert np.array_equal(r[f"knn_d_{n_grid}"].view(np.uint64), wd.view(np.uint64))
+        want = np.sort(cref.range_pp(cg, x, y, q[0], q[1], rad)).astype(np.int64)
+        assert r[f"hits_{n_grid}"].tolist() == want.tolist()
+        assert (r[f"totals_{n_grid}"] == len(want)).all()
+        # only G u C points moved; their total is the candidate count
+        assert r[f"recv_{n_grid}"].sum() < len(x) * 0.3
