@@ -690,6 +690,16 @@ constexpr int kPassNW = 16;                     // waves per block
 constexpr unsigned kPassMaxBlocks = 256;        // one block per CU
 constexpr unsigned kPassHeads = 8;
 constexpr unsigned kLenWhole = 0x80000000u;     // list length flag: heads incomplete, read it whole
+constexpr unsigned kLenSlots = 0x40000000u;     // list length flag: the block's slot set is complete (below)
+// Slot-complete blocks (k <= kSlotMaxK): every block publishes the lowest nonzero bin of its
+// survivor histogram (word kMinWord + block, bin + 1; 0 = none) -- the upper edge of that bin
+// bounds the distance of a real point of the block, distinct blocks hold distinct points, so the
+// upper edge of the bin where k of the published bins have accumulated bounds the window's k-th
+// distance.  A block whose survivors at or below that bound T_b fit kPassHeads slots writes
+// just those (its share of the window's k nearest is among them) and skips the list / head
+// ranking; the last block re-arms the words.
+constexpr unsigned kSlotMaxK = 256;
+constexpr unsigned kMinWord = 6400;
 constexpr unsigned kStatWord = (unsigned)(kKnnCounterBytes / 4) - 16;  // last final: entries, spilled, kept
 constexpr unsigned kVbWord = kTicketStride * (kMaxTicketGroups + 1);      // chunk ticket (fused range)
 
@@ -708,7 +718,21 @@ struct PassBlock {
     unsigned nsmall;
     unsigned cursor, last;
     unsigned fin[4];            // the final's LDS words
+    unsigned long long tslot;   // slot bound T_b (kSentinelD: none)
+    unsigned nslot;             // survivors at or below T_b
 };
+
+// One wave: the lowest bin holding a survivor, -1 if none (8 bins per lane).
+__device__ __forceinline__ int hist_low_bin(const unsigned* hist) {
+    const int lane = lane_id();
+    int f = -1;
+#pragma unroll
+    for (int j = 7; j >= 0; j--)
+        if (hist[lane * 8 + j]) f = lane * 8 + j;
+    const unsigned long long m = __ballot(f >= 0);
+    if (!m) return -1;
+    return __builtin_amdgcn_readlane(f, __builtin_ctzll(m));
+}
 
 struct PassIo {
     unsigned long long* list_d;  // block b: [b * list_cap, b * list_cap + len[b])
@@ -861,9 +885,11 @@ __device__ __forceinline__ void pass_final(const PassIo& io, const KnnArgs& a, u
     for (unsigned u = 0; u < kPer; u++)
         if (hd[u] != kSentinelD) atomicAdd(&hist[hist_bin(hd[u], a.hist_base)], 1u);
     if (blk) {
-        blast_sh[threadIdx.x] = (mylen & kLenWhole) ? 0ull : blast;  // flagged: whole whatever T
-        lens[threadIdx.x] = mylen & ~kLenWhole;
+        // flagged: whole whatever T; slot-complete: never (its slots hold all it contributes)
+        blast_sh[threadIdx.x] = (mylen & kLenWhole) ? 0ull : ((mylen & kLenSlots) ? kSentinelD : blast);
+        lens[threadIdx.x] = mylen & ~(kLenWhole | kLenSlots);
     }
+    if (blk) io.ctr[kMinWord + threadIdx.x] = 0u;  // slot-bound words re-armed for the next launch
     __syncthreads();
     // ---- C
     if (wid == 0) {
@@ -1312,21 +1338,41 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
     if (ia < niters && is_full(ia)) load_full(ia, ax, ay);
     if (ibb < niters && is_full(ibb)) load_full(ibb, bx, by);
     __syncthreads();
+    // slot bound publication (kSlotMaxK): the waves claiming these iterations publish the
+    // block's lowest survivor bin so far
+    const bool slots = k <= kSlotMaxK;
+    const unsigned pub1 = niters / 3, pub2 = 2 * niters / 3;
+    auto publish = [&](unsigned claimed) {
+        if (!slots || (claimed != pub1 && claimed != pub2)) return;
+        const int bin = hist_low_bin(kb.hist);
+        if (lane == 0 && bin >= 0 && bin < kHistBins - 1) store_wt(io.ctr + kMinWord + blockIdx.x, (unsigned)bin + 1u);
+    };
     while (ia < niters || ibb < niters) {
         if (ia < niters) {
             const unsigned na = claim();
             run(ia, ax, ay);
+            publish(na);
             ia = na;
             if (ia < niters && is_full(ia)) load_full(ia, ax, ay);
         }
         if (ibb < niters) {
             const unsigned nb2 = claim();
             run(ibb, bx, by);
+            publish(nb2);
             ibb = nb2;
             if (ibb < niters && is_full(ibb)) load_full(ibb, bx, by);
         }
     }
     PASS_TRACE(io, 1);
+    // the other blocks' published bins, in flight while the block's last batches finish
+    unsigned gv[kPassMaxBlocks / kWave] = {};
+    if (slots && wid == 0) {
+#pragma unroll
+        for (unsigned u = 0; u < kPassMaxBlocks / kWave; u++) {
+            const unsigned b = (unsigned)lane + u * kWave;
+            gv[u] = b < gridDim.x ? load_sc1(io.ctr + kMinWord + b) : 0u;
+        }
+    }
     pass_dist_batch<PB, RANGE>(st, ccnt, kb, args, io, appended, true, rs);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // spilled survivors drained before the ticket
     __syncthreads();
@@ -1344,6 +1390,68 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
     // 0 alone, in registers, behind no further barrier; else every wave through LDS.
     const unsigned have = kb.cnt < (unsigned)PB::kCap ? kb.cnt : (unsigned)PB::kCap;  // block-uniform
     const size_t lbase = (size_t)blockIdx.x * io.list_cap;
+    // ---- slot-complete end of block (k <= kSlotMaxK): T_b = upper edge of the bin where k of
+    // the blocks' lowest survivor bins (this block's current one, the others' as published)
+    // accumulate; the survivors <= T_b (the spill goes to the final on its own) into the slots
+    bool slotted = false;
+    if (slots && !(ABL & 7)) {
+        unsigned* mh = reinterpret_cast<unsigned*>(&stage[0]);  // 512 words: the stages are idle
+        if (wid == 0) {
+            const int own = hist_low_bin(kb.hist);
+#pragma unroll
+            for (int j = 0; j < 8; j++) mh[lane * 8 + j] = 0u;
+            wave_lds_sync();
+#pragma unroll
+            for (unsigned u = 0; u < kPassMaxBlocks / kWave; u++) {
+                const unsigned b = (unsigned)lane + u * kWave;
+                const int bin = b == blockIdx.x ? own : (int)gv[u] - 1;
+                if (b < gridDim.x && bin >= 0 && bin < kHistBins - 1) atomicAdd(&mh[bin], 1u);
+            }
+            if (lane == 0 && own >= 0 && own < kHistBins - 1) store_wt(io.ctr + kMinWord + blockIdx.x, (unsigned)own + 1u);
+            wave_lds_sync();
+            const int tb = hist_kth_bin(mh, k);
+            if (lane == 0) {
+                kb.tslot = (tb >= 0 && tb < kHistBins - 1) ? hist_edge(tb, args.hist_base) : kSentinelD;
+                kb.nslot = 0;
+            }
+        }
+        __syncthreads();
+        const unsigned long long T = kb.tslot;
+        if (T != kSentinelD) {
+            for (unsigned t = threadIdx.x; t < have; t += NT) {
+                const unsigned long long d = kb.bd[t];
+                if (d <= T) {
+                    const unsigned p = atomicAdd(&kb.nslot, 1u);
+                    if (p < kPassHeads) {
+                        kb.top_d[p] = d;
+                        kb.top_i[p] = kb.bi[t];
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        const unsigned ns = kb.nslot;
+        slotted = T != kSentinelD && ns <= kPassHeads;  // block-uniform
+        if (slotted && wid == 0) {
+            PASS_TRACE(io, 8);
+            if ((unsigned)lane < kPassHeads) {
+                const bool real = (unsigned)lane < ns;
+                const unsigned long long d = real ? kb.top_d[lane] : kSentinelD;
+                const unsigned i = real ? kb.top_i[lane] : kSentinelI;
+                store_wt(&io.head_d[kPassHeads * blockIdx.x + lane], d);
+                store_wt(&io.head_i[kPassHeads * blockIdx.x + lane], i);
+                if (real) {  // the list holds the same set (the final's fallback paths read lists)
+                    store_wt(&io.list_d[lbase + lane], d);
+                    store_wt(&io.list_i[lbase + lane], i);
+                }
+            }
+            if (lane == 0) store_wt(&io.len[blockIdx.x], ns | kLenSlots);
+            PASS_TRACE(io, 10);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            PASS_TRACE(io, 3);
+            if (lane == 0) kb.last = pass_arrive_last(io.ctr + kTicketStride, io.groups) ? 1u : 0u;
+        }
+    }
     auto bounds = [&](unsigned long long& Bv, unsigned long long& Hv) {  // wave 0
         int bb, hb;
         hist_kth_bins2(kb.hist, k, kPassHeads, bb, hb);
@@ -1376,7 +1484,9 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
         PASS_TRACE(io, 3);
         if (lane == 0) kb.last = pass_arrive_last(io.ctr + kTicketStride, io.groups) ? 1u : 0u;
     };
-    if (have <= 4u * kWave) {
+    if (slotted) {
+        // done above
+    } else if (have <= 4u * kWave) {
         if (wid == 0) {  // up to 4 survivors per lane: list offsets by ballot prefix, no atomics
             unsigned long long Bv, Hv;
             bounds(Bv, Hv);
