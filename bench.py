@@ -732,7 +732,7 @@ class PpKnnWorkload(Workload):
     """point-polygon kNN (PointPolygonKNNQuery) of one star polygon,
     k = 50, over the C4 window (50M uniform points per GPU, 500x500, r = 0.005)."""
     tag = "ppknn"
-    kernel = "geohip ppknn_scan + ppknn_dist + radix select (9 rounds) + rsel_sort"
+    kernel = "geohip ppknn_scan_boxes + ppknn_dist + one-workgroup radix select (rsel_small); plan cached, no host sync"
     grid_n, radius, n_default, k = 500, 0.005, 50_000_000, 50
     windows = 2
 
@@ -746,13 +746,18 @@ class PpKnnWorkload(Workload):
                                             [5 + 7919 * w for w in range(self.windows)], bj)
         off, vx, vy = synth.star_polygons(1, 6)
         self.vx, self.vy = vx, vy
+        import torch
+        self.oi = torch.empty(self.k, dtype=torch.int32, device=self.dev)
+        self.od = torch.empty(self.k, dtype=torch.float64, device=self.dev)
+        self.oc = torch.zeros(1, dtype=torch.int32, device=self.dev)
 
     def units_per_step(self):
         return self.n
 
     def step(self, s):
-        w = s % self.windows
-        self.ctx.knn_ppoly(self.grid, self.xs[w], self.ys[w], self.vx, self.vy, self.radius, self.k)
+        w = s % self.windows  # the device form: plan cached by the ctx, no host round trip
+        self.ctx.knn_ppoly_async(self.grid, self.xs[w], self.ys[w], self.vx, self.vy, self.radius, self.k, False,
+                                 self.oi, self.od, self.oc)
 
     def algorithmic_bytes(self):
         return BYTES_PER_POINT * self.n
@@ -819,7 +824,7 @@ class KnnIncrWorkload(KnnWorkload):
     top-k merged from its two panes' top-k lists (spatialflink_amd.incremental.IncrementalKNN).
     value = stream points/sec (each point is evaluated once, not once per window)."""
     tag = "knn_incr"
-    kernel = "geohip::knn_pass<16> on one pane (+ a 2-list knn_merge)"
+    kernel = "geohip::knn_pass<16> on one pane + one knn_merge_panes launch (2 panes, rebase folded in)"
     n_default = 5_000_000
     label = "C2 over 10s/5s sliding windows with pane reuse: kNN k=50, 100x100 Beijing UniformGrid, r=0.5"
 

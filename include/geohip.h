@@ -191,6 +191,17 @@ int geohip_knn_pp_async(geohip_ctx* ctx, const geohip_grid* grid, const double* 
 int geohip_knn_merge_async(geohip_ctx* ctx, const double* dist, const uint32_t* idx, uint32_t nlists,
                            uint32_t list_len, uint32_t k, uint32_t* out_idx, double* out_dist,
                            uint32_t* out_count_dev);
+/* Sliding-window kNN with pane reuse (the window = the last npanes panes,
+   PointPointKNNQuery's SlidingProcessingTimeWindows with size a multiple of the slide): the
+   window's k smallest from the panes' top-k lists (each ascending, sentinel-padded, as
+   geohip_knn_pp_async writes them) kept in a ring of list_len-entry slots (ring_dist/ring_idx,
+   device); slots[b] (host) names the slot of the b-th pane, oldest first, offsets[b] (host) its
+   first point's position in the window (indices are rebased by it).  One launch; output as
+   geohip_knn_merge_async.  1 <= npanes <= 16. */
+int geohip_knn_merge_panes_async(geohip_ctx* ctx, const double* ring_dist, const uint32_t* ring_idx,
+                                 uint32_t list_len, const uint32_t* slots, const uint64_t* offsets,
+                                 uint32_t npanes, uint32_t k, uint32_t* out_idx, double* out_dist,
+                                 uint32_t* out_count_dev);
 /* geohip_knn_range_pp into device buffers (counts on the device). */
 int geohip_knn_range_pp_async(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
                               uint64_t n, double qx, double qy, double r, uint32_t k, int approximate,

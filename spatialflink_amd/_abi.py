@@ -155,6 +155,7 @@ _SIGS = {
     "geohip_knn_pp_async": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_double, c_double, c_double, c_uint32,
                                     _P, _P, _P]),
     "geohip_knn_merge_async": (c_int, [_P, _P, _P, c_uint32, c_uint32, c_uint32, _P, _P, _P]),
+    "geohip_knn_merge_panes_async": (c_int, [_P, _P, _P, c_uint32, _P, _P, c_uint32, c_uint32, _P, _P, _P]),
     "geohip_format_points_csv": (c_int, [_P, POINTER(CsvOutSpec), _P, _P, c_uint64, _P, _P, _P, _P, c_uint64, _P,
                                          c_uint64, POINTER(c_uint64), _P]),
     "geohip_format_points": (c_int, [_P, POINTER(TextOutSpec), _P, _P, c_uint64, _P, _P, _P, _P, c_uint64, _P, c_uint64,
@@ -177,6 +178,8 @@ _SIGS = {
                                   c_double, c_int, _P, c_uint64, POINTER(c_uint64)]),
     "geohip_knn_ppoly": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, _P, c_uint32, _P, _P, c_double, c_uint32, c_int,
                                  _P, _P, POINTER(c_uint32)]),
+    "geohip_knn_ppoly_async": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, _P, c_uint32, _P, _P, c_double, c_uint32,
+                                       c_int, _P, _P, _P]),
     "geohip_plan_point": (c_int, [POINTER(Grid), c_double, c_double, c_double, POINTER(Rect), POINTER(c_uint32),
                                   POINTER(Rect), POINTER(c_uint32), POINTER(c_int32), POINTER(c_int32)]),
     "geohip_plan_cell": (c_int, [POINTER(Grid), c_double, c_double, POINTER(c_int32), POINTER(c_int32)]),
@@ -522,6 +525,31 @@ class Context:
         if rc:
             self._check(rc, "knn_merge_async")
 
+    def knn_merge_panes_async(self, ring_d, ring_i, slots, offsets, k, out_idx, out_dist, out_count):
+        """geohip_knn_merge_panes_async: the window's k smallest from the panes' top-k lists in a
+        ring (ring_d / ring_i: [slots, list_len] device tensors), pane b = ring slot slots[b]
+        (oldest first) rebased by offsets[b].  One launch, no host sync."""
+        self._dev(ring_d, "ring_d")
+        self._dev(ring_i, "ring_i", "int32")
+        self._dev(out_idx, "out_idx", "int32")
+        self._dev(out_dist, "out_dist")
+        self._dev(out_count, "out_count", "int32")
+        if ring_d.dim() != 2 or ring_d.shape != ring_i.shape:
+            raise GeohipArgumentError("knn_merge_panes_async: ring_d / ring_i must be [slots, list_len]")
+        if out_idx.numel() < k or out_dist.numel() < k:
+            raise GeohipArgumentError("knn_merge_panes_async: outputs shorter than k")
+        nslot, L = int(ring_d.shape[0]), int(ring_d.shape[1])
+        sl = (ctypes.c_uint32 * len(slots))(*[int(v) for v in slots])
+        of = (ctypes.c_uint64 * len(offsets))(*[int(v) for v in offsets])
+        if len(slots) != len(offsets) or any(not 0 <= int(v) < nslot for v in slots):
+            raise GeohipArgumentError("knn_merge_panes_async: bad slot list")
+        if self._mem != MEM_DEVICE:
+            self.set_mem(MEM_DEVICE)
+        rc = lib.geohip_knn_merge_panes_async(self.h, ring_d.data_ptr(), ring_i.data_ptr(), L, sl, of, len(slots), k,
+                                              out_idx.data_ptr(), out_dist.data_ptr(), out_count.data_ptr())
+        if rc:
+            self._check(rc, "knn_merge_panes_async")
+
     def format_points_csv(self, spec: CsvOutSpec, x, y, ts=None, oid_text=None, oid_off=None, idx=None, cap=None):
         """geohip_format_points_csv (Serialization.PointToCSVTSVOutputSchema over result points):
         device tensors in (x, y float64; ts int64; oid_text uint8 + oid_off int64 [n + 1]; idx
@@ -746,6 +774,28 @@ class Context:
                                   ctypes.byref(cnt))
         self._check(rc, "knn_ppoly")
         return oi[:cnt.value], od[:cnt.value]
+
+    def knn_ppoly_async(self, grid: Grid, x, y, vx, vy, r, k, approximate, out_idx, out_dist, out_count, ring_off=None):
+        """geohip_knn_ppoly_async: device window, k-long device outputs (sentinel-padded), count
+        on the device; no host synchronisation (the polygon plan is cached by the ctx)."""
+        self._dev(x, "x")
+        self._dev(y, "y")
+        self._dev(out_idx, "out_idx", "int32")
+        self._dev(out_dist, "out_dist")
+        self._dev(out_count, "out_count", "int32")
+        if out_idx.numel() < k or out_dist.numel() < k:
+            raise GeohipArgumentError("knn_ppoly_async: outputs shorter than k")
+        vx = _host(vx, np.float64)
+        vy = _host(vy, np.float64)
+        ring_off = _host([0, len(vx)] if ring_off is None else ring_off, np.uint32)
+        _check_rings(ring_off, vx, vy)
+        if self._mem != MEM_DEVICE:
+            self.set_mem(MEM_DEVICE)
+        rc = lib.geohip_knn_ppoly_async(self.h, ctypes.byref(grid), x.data_ptr(), y.data_ptr(), x.numel(),
+                                        _ptr(ring_off), len(ring_off) - 1, _ptr(vx), _ptr(vy), r, k, int(approximate),
+                                        out_idx.data_ptr(), out_dist.data_ptr(), out_count.data_ptr())
+        if rc:
+            self._check(rc, "knn_ppoly_async")
 
     def ingest_points(self, spec: IngestSpec, text, grid: Grid | None = None, with_ts=False, with_cell=False,
                       cap=None, out=None):

@@ -30,7 +30,7 @@ enum Slot {
     S_X, S_Y, S_QX, S_QY, S_GTHR, S_PART_D, S_PART_I, S_OUT_D, S_OUT_I, S_OUT_CNT,
     S_MASK, S_UCNT, S_OFFS, S_TOTAL, S_OUT_IDX, S_OUT_PAIRS, S_SPILL_D, S_SPILL_I, S_SPILL_CNT, S_RLB, S_TRACE,
     S_J0, S_J1, S_J2, S_J3, S_J4, S_J5, S_J6, S_J7, S_J8, S_J9, S_J10, S_J11, S_J12, S_J13, S_J14, S_J15,
-    S_J16, S_J17, S_J18, S_J19, S_J20, S_J21, S_J22, S_J23,
+    S_J16, S_J17, S_J18, S_J19, S_J20, S_J21, S_J22, S_J23, S_J24, S_J25,
     S_I0, S_I1, S_I2, S_I3, S_I4, S_I5, S_I6, S_I7,
     S_COUNT
 };
@@ -114,6 +114,7 @@ struct geohip_ctx {
     std::unique_ptr<CopyPool> copy_pool;
     hipEvent_t switch_ev = nullptr;  // orders a stream rebinding after the old stream's work
     void* pcache = nullptr;          // point-polygon plan cache (cell_kernels.hip owns the type)
+    void* kcache = nullptr;          // point-polygon kNN polygon cache (cell_kernels.hip owns the type)
 };
 
 namespace {
@@ -584,6 +585,7 @@ int geohip_ctx_create(uint32_t device_mask, geohip_ctx** out_ctx) {
 
 int geohip_ctx_destroy(geohip_ctx* ctx) {
     if (ctx) ppoly_cache_drop(ctx);
+    if (ctx) knn_poly_cache_drop(ctx);
     if (!ctx) return GEOHIP_ERR_ARG;
     hipSetDevice(ctx->device);
     hipStreamSynchronize(ctx->stream);
@@ -811,6 +813,33 @@ int geohip_knn_merge_async(geohip_ctx* ctx, const double* dist, const uint32_t* 
     return GEOHIP_OK;
 }
 
+int geohip_knn_merge_panes_async(geohip_ctx* ctx, const double* ring_dist, const uint32_t* ring_idx, uint32_t list_len,
+                                 const uint32_t* slots, const uint64_t* offsets, uint32_t npanes, uint32_t k,
+                                 uint32_t* out_idx, double* out_dist, uint32_t* out_count_dev) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    if (ctx->mem != GEOHIP_MEM_DEVICE) return fail(ctx, GEOHIP_ERR_ARG, "async forms need GEOHIP_MEM_DEVICE");
+    if (k == 0 || list_len == 0) return fail(ctx, GEOHIP_ERR_ARG, "k and list_len must be > 0");
+    if (npanes == 0 || npanes > kMaxPanes) return fail(ctx, GEOHIP_ERR_UNSUPPORTED, "1..16 panes per window");
+    if (!ring_dist || !ring_idx || !slots || !offsets || !out_idx || !out_dist || !out_count_dev)
+        return fail(ctx, GEOHIP_ERR_ARG, "null pointer");
+    if ((uint64_t)npanes * list_len > (1ull << 30)) return fail(ctx, GEOHIP_ERR_UNSUPPORTED, "panes too long");
+    PaneMerge pm;
+    memset(&pm, 0, sizeof pm);
+    for (uint32_t b = 0; b < npanes; b++) {
+        if (offsets[b] >= 0xffffffffull) return fail(ctx, GEOHIP_ERR_UNSUPPORTED, "window beyond 2^32-1 points");
+        pm.slot[b] = slots[b];
+        pm.off[b] = (unsigned)offsets[b];
+    }
+    pm.n = npanes;
+    pm.list_len = list_len;
+    pm.k = k;
+    hipError_t e = launch_knn_merge_panes(reinterpret_cast<const unsigned long long*>(ring_dist), ring_idx, pm,
+                                          out_dist, out_idx, out_count_dev, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "pane merge launch");
+    return GEOHIP_OK;
+}
+
 int geohip_knn_range_pp(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
                         double qx, double qy, double r, uint32_t k, int approximate, uint32_t* knn_idx,
                         double* knn_dist, uint32_t* knn_count, uint32_t* range_idx, uint64_t range_cap,
@@ -915,7 +944,17 @@ int geohip_knn_ppoly(geohip_ctx* ctx, const geohip_grid* grid, const double* x, 
     int rc = begin(ctx);
     if (rc) return rc;
     return knn_ppoly_impl(ctx, grid, x, y, n, ring_off, nring, vx, vy, r, k, approximate, out_idx, out_dist,
-                          out_count);
+                          out_count, false);
+}
+
+int geohip_knn_ppoly_async(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
+                           const uint32_t* ring_off, uint32_t nring, const double* vx, const double* vy, double r,
+                           uint32_t k, int approximate, uint32_t* out_idx, double* out_dist, uint32_t* out_count_dev) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    if (ctx->mem != GEOHIP_MEM_DEVICE) return fail(ctx, GEOHIP_ERR_ARG, "async forms need GEOHIP_MEM_DEVICE");
+    return knn_ppoly_impl(ctx, grid, x, y, n, ring_off, nring, vx, vy, r, k, approximate, out_idx, out_dist,
+                          out_count_dev, true);
 }
 
 int geohip_plan_point(const geohip_grid* grid, double qx, double qy, double r, geohip_rect* g_rects, uint32_t* n_g,
@@ -1077,6 +1116,7 @@ hipStream_t ctx_stream(geohip_ctx* ctx) { return ctx->stream; }
 int ctx_mem(geohip_ctx* ctx) { return ctx->mem; }
 uint64_t* ctx_pinned(geohip_ctx* ctx) { return ctx->pinned; }
 void** ctx_pcache_slot(geohip_ctx* ctx) { return &ctx->pcache; }
+void** ctx_kcache_slot(geohip_ctx* ctx) { return &ctx->kcache; }
 void ctx_timing_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1) { timing_events(ctx, e0, e1); }
 int ctx_stage_xy(geohip_ctx* ctx, const double* x, const double* y, uint64_t n, int which, const double** dx,
                  const double** dy) {

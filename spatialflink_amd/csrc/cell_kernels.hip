@@ -3340,12 +3340,55 @@ int knn_merge_large_impl(geohip_ctx* ctx, const unsigned long long* d, const uns
     return GEOHIP_OK;
 }
 
+// Point-polygon kNN polygon cache (one per ctx): a continuous PointPolygonKNNQuery evaluates the
+// same polygon on every window, so its plan (rings, envelopes, G/C rectangles, boxes) is built and
+// uploaded to a dedicated ctx slot once; later calls compare their inputs bitwise.  It also keeps
+// the previous window's candidate count, which picks the selection path of the next window without
+// a host round trip (either path is exact for any count; the guess only decides which is fast).
+struct KnnPolyCache {
+    bool valid = false;
+    geohip_grid grid{};
+    double r = 0.0;
+    std::vector<uint32_t> ring_off;  // ring offsets relative to ring_off[0]
+    std::vector<double> vx, vy;      // the rings' vertices as given
+    PpknnPoly P;
+    PpknnBoxes PB;
+    bool boxed = false;
+    uint32_t nrect = 0;
+    size_t off_vx = 0, off_env = 0, off_rect = 0, off_vr = 0, blob_bytes = 0;
+    size_t n_env = 0, n_vr = 0;
+    void* dev_blob = nullptr;
+    uint32_t* pin = nullptr;    // pinned: the last window's candidate count
+    hipEvent_t ev = nullptr;    // ... landed when this event completes
+    bool ev_pending = false;
+    uint32_t last_m = 0;
+};
+
+KnnPolyCache* ctx_kcache(geohip_ctx* ctx) {
+    void** slot = ctx_kcache_slot(ctx);
+    if (!*slot) *slot = new KnnPolyCache();
+    return static_cast<KnnPolyCache*>(*slot);
+}
+
+void knn_poly_cache_drop(geohip_ctx* ctx) {
+    void** slot = ctx_kcache_slot(ctx);
+    KnnPolyCache* c = static_cast<KnnPolyCache*>(*slot);
+    if (!c) return;
+    if (c->ev) {
+        hipEventSynchronize(c->ev);
+        hipEventDestroy(c->ev);
+    }
+    if (c->pin) hipHostFree(c->pin);
+    delete c;
+    *slot = nullptr;
+}
+
 // Point-polygon kNN of one query polygon over one window (host side of the kernels above).
 int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
                    const uint32_t* ring_off, uint32_t nring, const double* vx, const double* vy, double r, uint32_t k,
-                   int approximate, uint32_t* out_idx, double* out_dist, uint32_t* out_count) {
+                   int approximate, uint32_t* out_idx, double* out_dist, uint32_t* out_count, bool async) {
     if (!out_idx || !out_dist || !out_count) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null output");
-    *out_count = 0;
+    if (!async) *out_count = 0;
     if (k == 0) return ctx_fail(ctx, GEOHIP_ERR_ARG, "k must be > 0");
     // k above one workgroup's LDS sort (GEOHIP_KNN_PPOLY_MAX_K): the radix rounds always run,
     // the k selected keys are gathered and sorted (PointPolygonKNNQuery.java:34 takes any k)
@@ -3357,37 +3400,110 @@ int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, co
     if (nring > kMaxRings) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "polygon with more than 65535 rings");
     for (uint32_t j = 0; j < nring; j++)
         if (ring_off[j + 1] < ring_off[j]) return ctx_fail(ctx, GEOHIP_ERR_ARG, "ring_off not ascending");
-    PolyPlan pl;
-    std::string err;
-    rc = plan_polygon_rings(*grid, ring_off, nring, vx, vy, r, &pl, &err);
-    if (rc) return ctx_fail(ctx, rc, err);
-    std::vector<ring_id_t> hvr;
-    std::vector<double> henv;
-    double gb[4];
-    ring_tables(pl, hvr, henv, gb);
-    std::vector<int32_t> hrect;
-    for (auto& q : pl.g) hrect.insert(hrect.end(), {q.x0, q.x1, q.y0, q.y1});
-    for (auto& q : pl.c) hrect.insert(hrect.end(), {q.x0, q.x1, q.y0, q.y1});
-    const uint32_t nrect = (uint32_t)(hrect.size() / 4);
-    // exact coordinate boxes of the rects (no division in the scan) when they fit the kernel args
-    PpknnBoxes PB;
-    memset(&PB, 0, sizeof PB);
-    const bool boxed = nrect <= (uint32_t)kPpBoxes;
-    if (boxed) {
-        for (uint32_t q = 0; q < nrect; q++) {
-            const geohip_rect rr{hrect[4 * q], hrect[4 * q + 1], hrect[4 * q + 2], hrect[4 * q + 3]};
-            PB.b[q] = rect_to_box(*grid, rr);
-        }
-        PB.nb = (int32_t)nrect;
-    }
-    PpknnPoly P;
-    for (int i = 0; i < 4; i++) P.bb[i] = pl.bbox[i];
-    P.nv = (uint32_t)pl.rx.size();
-    P.nrect = nrect;
-    P.nring = (uint32_t)pl.ring_start.size() - 1;
-    P.pad = 0;
     hipStream_t st = ctx_stream(ctx);
     const bool dev = ctx_mem(ctx) == GEOHIP_MEM_DEVICE;
+    KnnPolyCache* kc = ctx_kcache(ctx);
+    // ---- the polygon's plan: cached, or built and uploaded once
+    const size_t v0 = nring ? ring_off[0] : 0, v1 = nring ? ring_off[nring] : 0;
+    bool same = kc->valid && memcmp(&kc->grid, grid, sizeof *grid) == 0 && memcmp(&kc->r, &r, sizeof r) == 0 &&
+                kc->ring_off.size() == (size_t)nring + 1 && kc->vx.size() == v1 - v0;
+    if (same)
+        for (uint32_t j = 0; j <= nring && same; j++) same = kc->ring_off[j] == ring_off[j] - ring_off[0];
+    if (same && v1 > v0)
+        same = memcmp(kc->vx.data(), vx + v0, (v1 - v0) * 8) == 0 && memcmp(kc->vy.data(), vy + v0, (v1 - v0) * 8) == 0;
+    if (!same) {
+        kc->valid = false;
+        PolyPlan pl;
+        std::string err;
+        rc = plan_polygon_rings(*grid, ring_off, nring, vx, vy, r, &pl, &err);
+        if (rc) return ctx_fail(ctx, rc, err);
+        std::vector<ring_id_t> hvr;
+        std::vector<double> henv;
+        double gb[4];
+        ring_tables(pl, hvr, henv, gb);
+        std::vector<int32_t> hrect;
+        for (auto& q : pl.g) hrect.insert(hrect.end(), {q.x0, q.x1, q.y0, q.y1});
+        for (auto& q : pl.c) hrect.insert(hrect.end(), {q.x0, q.x1, q.y0, q.y1});
+        const uint32_t nrect = (uint32_t)(hrect.size() / 4);
+        // exact coordinate boxes of the rects (no division in the scan) when they fit the kernel args
+        PpknnBoxes PB;
+        memset(&PB, 0, sizeof PB);
+        const bool boxed = nrect <= (uint32_t)kPpBoxes;
+        if (boxed) {
+            for (uint32_t q = 0; q < nrect; q++) {
+                const geohip_rect rr{hrect[4 * q], hrect[4 * q + 1], hrect[4 * q + 2], hrect[4 * q + 3]};
+                PB.b[q] = rect_to_box(*grid, rr);
+            }
+            PB.nb = (int32_t)nrect;
+        }
+        PpknnPoly P;
+        memset(&P, 0, sizeof P);
+        for (int i = 0; i < 4; i++) P.bb[i] = pl.bbox[i];
+        P.nv = (uint32_t)pl.rx.size();
+        P.nrect = nrect;
+        P.nring = (uint32_t)pl.ring_start.size() - 1;
+        // device tables in slot 24 (only this path writes it): vx | vy | ring envelopes | rects | ring ids
+        const size_t off_vx = 0;
+        const size_t off_env = off_vx + 2 * 8 * (size_t)P.nv;
+        const size_t off_rect = off_env + 8 * henv.size();
+        const size_t off_vr = off_rect + 16 * (size_t)nrect;
+        const size_t blob = off_vr + hvr.size() * sizeof(ring_id_t);
+        void* pb = nullptr;
+        rc = ctx_ensure(ctx, 24, blob + 64, &pb);
+        if (rc) return rc;
+        char* b = reinterpret_cast<char*>(pb);
+        if ((P.nv && (hipMemcpyAsync(b + off_vx, pl.rx.data(), 8 * (size_t)P.nv, hipMemcpyHostToDevice, st) != hipSuccess ||
+                      hipMemcpyAsync(b + off_vx + 8 * (size_t)P.nv, pl.ry.data(), 8 * (size_t)P.nv, hipMemcpyHostToDevice,
+                                     st) != hipSuccess)) ||
+            (nrect && hipMemcpyAsync(b + off_rect, hrect.data(), 16 * (size_t)nrect, hipMemcpyHostToDevice, st) != hipSuccess) ||
+            (P.nring > 1 &&
+             (hipMemcpyAsync(b + off_env, henv.data(), 8 * henv.size(), hipMemcpyHostToDevice, st) != hipSuccess ||
+              hipMemcpyAsync(b + off_vr, hvr.data(), hvr.size() * sizeof(ring_id_t), hipMemcpyHostToDevice, st) != hipSuccess)))
+            return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "polygon upload failed");
+        kc->grid = *grid;
+        kc->r = r;
+        kc->ring_off.resize((size_t)nring + 1);
+        for (uint32_t j = 0; j <= nring; j++) kc->ring_off[j] = ring_off[j] - ring_off[0];
+        kc->vx.assign(vx + v0, vx + v1);
+        kc->vy.assign(vy + v0, vy + v1);
+        kc->P = P;
+        kc->PB = PB;
+        kc->boxed = boxed;
+        kc->nrect = nrect;
+        kc->off_vx = off_vx;
+        kc->off_env = off_env;
+        kc->off_rect = off_rect;
+        kc->off_vr = off_vr;
+        kc->blob_bytes = blob;
+        kc->dev_blob = pb;
+        kc->valid = true;
+    } else {
+        void* pb = nullptr;  // the slot is this path's own: same pointer, same contents
+        rc = ctx_ensure(ctx, 24, kc->blob_bytes + 64, &pb);
+        if (rc) return rc;
+        if (pb != kc->dev_blob) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "polygon table slot moved");
+    }
+    const PpknnPoly& P = kc->P;
+    const PpknnBoxes& PB = kc->PB;
+    const uint32_t nrect = kc->nrect;
+    char* tb = reinterpret_cast<char*>(kc->dev_blob);
+    double* dvx = reinterpret_cast<double*>(tb + kc->off_vx);
+    double* dvy = dvx + P.nv;
+    int32_t* drect = reinterpret_cast<int32_t*>(tb + kc->off_rect);
+    double* denv = reinterpret_cast<double*>(tb + kc->off_env);
+    ring_id_t* dvr = reinterpret_cast<ring_id_t*>(tb + kc->off_vr);
+    // ---- the last window's candidate count, if it has landed: picks the selection path
+    if (!kc->pin) {
+        if (hipHostMalloc((void**)&kc->pin, 16, hipHostMallocDefault) != hipSuccess ||
+            hipEventCreateWithFlags(&kc->ev, hipEventDisableTiming) != hipSuccess)
+            return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "pinned count allocation failed");
+        kc->pin[0] = 0;
+    }
+    if (kc->ev_pending && hipEventQuery(kc->ev) == hipSuccess) {
+        kc->last_m = kc->pin[0];
+        kc->ev_pending = false;
+    }
+    (void)hipGetLastError();  // a not-ready query is no error
     const double *dx, *dy;
     rc = ctx_stage_xy(ctx, x, y, n, 0, &dx, &dy);
     if (rc) return rc;
@@ -3395,48 +3511,30 @@ int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, co
     const uint64_t ncap = n ? n : 1;
     char* cbuf = S.get<char>(22, ncap * 12 + 64);
     if (S.rc) return S.rc;
-    // slot 23: RselState, selection and sort areas (large_k_scratch), then the output staging
-    // (host windows), polygon tables
     const size_t kout = std::max<size_t>(k, 256);
-    const size_t off_out = 0;
-    const size_t off_vx = (off_out + kout * 12 + 16 + 15) & ~(size_t)15;
-    const size_t off_env = off_vx + 2 * 8 * (size_t)P.nv;
-    const size_t off_rect = off_env + 8 * henv.size();
-    const size_t off_vr = off_rect + 16 * (size_t)nrect;
     LargeK L;
-    rc = large_k_scratch(ctx, (unsigned)kout, off_vr + hvr.size() * sizeof(ring_id_t), &L);
+    rc = large_k_scratch(ctx, (unsigned)kout, kout * 12 + 64, &L);  // + output staging (host windows)
     if (rc) return rc;
-    char* xbuf = L.extra;
     unsigned long long* key = reinterpret_cast<unsigned long long*>(cbuf);
     unsigned* cand = reinterpret_cast<unsigned*>(cbuf + ncap * 8);
     RselState* rs = L.rs;
-    double* od = dev ? out_dist : reinterpret_cast<double*>(xbuf + off_out);
-    unsigned* oi = dev ? out_idx : reinterpret_cast<unsigned*>(xbuf + off_out + kout * 8);
-    unsigned* ocnt = reinterpret_cast<unsigned*>(xbuf + off_out + kout * 12);
-    double* dvx = reinterpret_cast<double*>(xbuf + off_vx);
-    double* dvy = dvx + P.nv;
-    int32_t* drect = reinterpret_cast<int32_t*>(xbuf + off_rect);
-    double* denv = reinterpret_cast<double*>(xbuf + off_env);
-    ring_id_t* dvr = reinterpret_cast<ring_id_t*>(xbuf + off_vr);
-    if ((P.nv && (hipMemcpyAsync(dvx, pl.rx.data(), 8 * (size_t)P.nv, hipMemcpyHostToDevice, st) != hipSuccess ||
-                  hipMemcpyAsync(dvy, pl.ry.data(), 8 * (size_t)P.nv, hipMemcpyHostToDevice, st) != hipSuccess)) ||
-        (nrect && hipMemcpyAsync(drect, hrect.data(), 16 * (size_t)nrect, hipMemcpyHostToDevice, st) != hipSuccess) ||
-        (P.nring > 1 &&
-         (hipMemcpyAsync(denv, henv.data(), 8 * henv.size(), hipMemcpyHostToDevice, st) != hipSuccess ||
-          hipMemcpyAsync(dvr, hvr.data(), hvr.size() * sizeof(ring_id_t), hipMemcpyHostToDevice, st) != hipSuccess)))
-        return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "polygon upload failed");
+    double* od = dev ? out_dist : reinterpret_cast<double*>(L.extra);
+    unsigned* oi = dev ? out_idx : reinterpret_cast<unsigned*>(L.extra + kout * 8);
+    unsigned* ocnt = async ? out_count : reinterpret_cast<unsigned*>(L.extra + kout * 12);
     hipEvent_t e0, e1;
     ctx_timing_events(ctx, &e0, &e1);
     if (e0) hipEventRecord(e0, st);
-    // single-workgroup select up to kRselSmall candidates (GEOHIP_RSEL_SMALL: test hook); none
-    // for the large-k form
-    static const unsigned small_env = getenv("GEOHIP_RSEL_SMALL") ? (unsigned)atol(getenv("GEOHIP_RSEL_SMALL")) : kRselSmall;
-    const unsigned small_max = big_k ? 0u : small_env;
+    // one workgroup selects (any candidate count, fast up to kRselSmall) unless the last window
+    // had more candidates than that: then the multi-block rounds (GEOHIP_RSEL_SMALL: test hook
+    // forcing them above the given count)
+    static const char* env_small = getenv("GEOHIP_RSEL_SMALL");
+    const bool multi = big_k || (env_small ? true : kc->last_m > kRselSmall);
+    const unsigned small_max = big_k ? 0u : (env_small ? (unsigned)atol(env_small) : (multi ? 0u : 0xffffffffu));
     rsel_init<<<1, 1024, 0, st>>>(rs, k, small_max);
     if (big_k && hipMemsetAsync(L.sel_d, 0xff, (size_t)kout * 12, st) != hipSuccess)
         return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
     if (n && nrect) {
-        if (boxed) {
+        if (kc->boxed) {
             const uint64_t iters = (n + 255) / 256;
             static const uint64_t max_blocks = getenv("GEOHIP_PPKNN_BLOCKS") ? (uint64_t)atol(getenv("GEOHIP_PPKNN_BLOCKS")) : 2048;
             const uint64_t nb = std::max<uint64_t>(1, std::min<uint64_t>((iters + 3) / 4, max_blocks));  // 4 waves per block
@@ -3459,35 +3557,31 @@ int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, co
         rc = rsel_large_tail(st, key, cand, rs, k, L.sel_d, L.sel_i, L.tmp_d, L.tmp_i, L.temp, L.temp_bytes, od, oi,
                              ocnt);
         if (rc) return ctx_fail(ctx, rc, "large-k kNN launch failed");
-        if (e1) hipEventRecord(e1, st);
     } else {
-        rsel_small<<<1, 1024, 0, st>>>(key, cand, rs, k, od, oi, ocnt);  // M <= kRselSmall (also M = 0)
-        if (e1) hipEventRecord(e1, st);  // re-recorded below when the multi-block rounds run
-        // the multi-block rounds only when the candidate count needs them (one count readback
-        // instead of 20 no-op launches, ~80 us)
-        bool big = false;
-        if (n && nrect) {
-            uint64_t* pin = ctx_pinned(ctx);
-            if (hipMemcpyAsync(pin, &rs->ncand, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                hipStreamSynchronize(st) != hipSuccess)
-                return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "candidate count readback failed");
-            big = (uint32_t)(pin[0] & 0xffffffffu) > small_max;
-        }
-        if (big) {
+        rsel_small<<<1, 1024, 0, st>>>(key, cand, rs, k, od, oi, ocnt);  // M <= small_max (and M = 0)
+        if (multi) {
             for (int t = 0; t < kRselRounds; t++) {
                 rsel_hist<<<512, kTB, 0, st>>>(key, cand, rs, t, k);
                 rsel_pick<<<1, 1024, 0, st>>>(rs, t, k);
             }
             rsel_gather<<<512, kTB, 0, st>>>(key, cand, rs, k, L.sel_d, L.sel_i);
             rsel_sort<<<1, 256, 0, st>>>(L.sel_d, L.sel_i, rs, k, od, oi, ocnt);
-            if (e1) hipEventRecord(e1, st);
         }
     }
+    if (e1) hipEventRecord(e1, st);
+    // this window's candidate count for the next call's choice (lands with the event)
+    if (hipMemcpyAsync(kc->pin, &rs->ncand, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipEventRecord(kc->ev, st) != hipSuccess)
+        return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "candidate count copy failed");
+    kc->ev_pending = true;
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, std::string("knn_ppoly launch: ") + hipGetErrorString(e));
+    if (async) return GEOHIP_OK;
     uint32_t m = 0;
     if (hipMemcpyAsync(&m, ocnt, 4, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
         return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "count readback failed");
+    kc->last_m = kc->pin[0];
+    kc->ev_pending = false;
     if (!dev && m &&
         (hipMemcpy(out_dist, od, 8 * (size_t)m, hipMemcpyDeviceToHost) != hipSuccess ||
          hipMemcpy(out_idx, oi, 4 * (size_t)m, hipMemcpyDeviceToHost) != hipSuccess))

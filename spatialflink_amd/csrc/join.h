@@ -10,7 +10,7 @@
 namespace geohip {
 // context services implemented in abi.cpp
 int ctx_fail(geohip_ctx* ctx, int code, const std::string& msg);
-int ctx_ensure(geohip_ctx* ctx, int slot, size_t bytes, void** out);  // slot 0..23
+int ctx_ensure(geohip_ctx* ctx, int slot, size_t bytes, void** out);  // slot 0..25
 int ctx_ensure_ingest(geohip_ctx* ctx, int slot, size_t bytes, void** out);  // slot 0..7
 int ctx_begin(geohip_ctx* ctx);  // clears the error, selects the ctx's device
 hipStream_t ctx_stream(geohip_ctx* ctx);
@@ -20,6 +20,7 @@ void ctx_timing_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1);
 int ctx_stage_xy(geohip_ctx* ctx, const double* x, const double* y, uint64_t n, int which, const double** dx,
                  const double** dy);
 void** ctx_pcache_slot(geohip_ctx* ctx);  // the ctx's point-polygon plan cache (owned by cell_kernels)
+void** ctx_kcache_slot(geohip_ctx* ctx);  // the ctx's point-polygon kNN polygon cache
 
 // squared-distance screen bounds for "dist <= r" (r2lo < 0 / r2hi = inf where they cannot hold)
 void pp_screen_bounds(double r, double* r2lo, double* r2hi);

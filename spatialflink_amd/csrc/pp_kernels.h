@@ -59,6 +59,15 @@ hipError_t launch_knn_pass(const double* x, const double* y, uint64_t n, const K
 hipError_t launch_knn_rebase(unsigned* idx, unsigned nlists, unsigned k, uint64_t chunk_pts, hipStream_t st);
 hipError_t launch_knn_merge(const unsigned long long* d, const unsigned* i, unsigned nlists, unsigned list_len,
                             unsigned k, double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st);
+// pane merge: n lists of list_len in ring slots slot[0..n) (oldest first), indices + off[b]
+constexpr unsigned kMaxPanes = 16;
+struct PaneMerge {
+    unsigned slot[kMaxPanes];
+    unsigned off[kMaxPanes];
+    unsigned n, list_len, k, pad;
+};
+hipError_t launch_knn_merge_panes(const unsigned long long* ring_d, const unsigned* ring_i, const PaneMerge& pm,
+                                  double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st);
 // range: bitmask (16 words / 1024 pts), unit_count (units), offs (units) scratch.
 hipError_t launch_range(const double* x, const double* y, uint64_t n, const RangeArgs& a, int approximate,
                         unsigned long long* bitmask, unsigned* unit_count, uint64_t* offs, uint64_t* total,

@@ -2168,6 +2168,77 @@ hipError_t launch_knn_rebase(unsigned* idx, unsigned nlists, unsigned k, uint64_
     return hipGetLastError();
 }
 
+// Pane merge (sliding windows with pane reuse): the window's k smallest
+// from n panes' sorted top-k lists held in a ring of slots, each pane's indices rebased by the
+// pane's offset in the window.  One launch, no sort: entry e of list a (position p) lands at
+// output rank p + sum over the other lists of the entries below it (binary search; keys are
+// unique after the rebase, panes being disjoint), which is its place in the merged order.
+__device__ __forceinline__ bool pane_less(unsigned long long ad, unsigned ai, unsigned long long bd, unsigned bi) {
+    return ad < bd || (ad == bd && ai < bi);
+}
+// entries of list (d, i)[0, len) below key (kd, ki), rebased by off (sentinels never below)
+__device__ __forceinline__ unsigned pane_below(const unsigned long long* d, const unsigned* i, unsigned len,
+                                               unsigned off, unsigned long long kd, unsigned ki) {
+    unsigned lo = 0, hi = len;
+    while (lo < hi) {
+        const unsigned mid = (lo + hi) >> 1;
+        const unsigned long long md = d[mid];
+        const unsigned mi = i[mid];
+        const bool below = md != kSentinelD && mi != kSentinelI && pane_less(md, mi + off, kd, ki);
+        if (below) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+__global__ __launch_bounds__(256) void knn_merge_panes(const unsigned long long* __restrict__ ring_d,
+                                                       const unsigned* __restrict__ ring_i, PaneMerge pm,
+                                                       double* __restrict__ out_d, unsigned* __restrict__ out_i,
+                                                       unsigned* __restrict__ out_count) {
+    const unsigned t = blockIdx.x * 256 + threadIdx.x;
+    const unsigned L = pm.list_len;
+    // real entries of every pane (a list is its real entries, then sentinels)
+    unsigned total = 0;
+    for (unsigned b = 0; b < pm.n; b++) {
+        const unsigned long long* d = ring_d + (size_t)pm.slot[b] * L;
+        const unsigned* ix = ring_i + (size_t)pm.slot[b] * L;
+        unsigned lo = 0, hi = L;
+        while (lo < hi) {
+            const unsigned mid = (lo + hi) >> 1;
+            if (d[mid] != kSentinelD && ix[mid] != kSentinelI) lo = mid + 1;
+            else hi = mid;
+        }
+        total += lo;
+    }
+    if (t < pm.k && t >= total) {
+        out_d[t] = __longlong_as_double((long long)kSentinelD);
+        out_i[t] = kSentinelI;
+    }
+    if (t == 0) *out_count = total < pm.k ? total : pm.k;
+    if (t >= pm.n * L) return;
+    const unsigned a = t / L, p = t % L;
+    const unsigned long long* da = ring_d + (size_t)pm.slot[a] * L;
+    const unsigned* ia = ring_i + (size_t)pm.slot[a] * L;
+    const unsigned long long kd = da[p];
+    const unsigned raw = ia[p];
+    if (kd == kSentinelD || raw == kSentinelI) return;
+    const unsigned ki = raw + pm.off[a];
+    unsigned rank = p;
+    for (unsigned b = 0; b < pm.n && rank < pm.k; b++)
+        if (b != a)
+            rank += pane_below(ring_d + (size_t)pm.slot[b] * L, ring_i + (size_t)pm.slot[b] * L, L, pm.off[b], kd, ki);
+    if (rank < pm.k) {
+        out_d[rank] = __longlong_as_double((long long)kd);
+        out_i[rank] = ki;
+    }
+}
+
+hipError_t launch_knn_merge_panes(const unsigned long long* ring_d, const unsigned* ring_i, const PaneMerge& pm,
+                                  double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st) {
+    const unsigned m = pm.n * pm.list_len > pm.k ? pm.n * pm.list_len : pm.k;
+    knn_merge_panes<<<(m + 255) / 256, 256, 0, st>>>(ring_d, ring_i, pm, out_d, out_i, out_count);
+    return hipGetLastError();
+}
+
 hipError_t launch_knn_merge(const unsigned long long* d, const unsigned* i, unsigned nlists, unsigned list_len,
                             unsigned k, double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st) {
     if (k > 256) {

@@ -14,10 +14,12 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
                const double* y, uint64_t n, const uint32_t* poly_rings, const uint32_t* ring_off, const double* vx,
                const double* vy, uint32_t npoly, double r, int approximate, uint32_t* out_pairs, uint64_t cap,
                uint64_t* out_count);
-// point-polygon kNN of one polygon (PointPolygonKNNQuery.java:162-236)
+// point-polygon kNN of one polygon (PointPolygonKNNQuery.java:162-236); async: device outputs and
+// count, no host synchronisation
 int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
                    const uint32_t* ring_off, uint32_t nring, const double* vx, const double* vy, double r, uint32_t k,
-                   int approximate, uint32_t* out_idx, double* out_dist, uint32_t* out_count);
+                   int approximate, uint32_t* out_idx, double* out_dist, uint32_t* out_count, bool async);
+void knn_poly_cache_drop(geohip_ctx* ctx);
 // point kNN with k > GEOHIP_KNN_MAX_K: candidate scan, keys, radix select, sort (device outputs)
 int knn_pp_large_impl(geohip_ctx* ctx, const PointPlan& plan, const double* dx, const double* dy, uint64_t n,
                       double qx, double qy, uint32_t k, double* od, unsigned* oi, unsigned* ocnt);

@@ -21,8 +21,6 @@ before the first element do.  Panes are device-resident (x, y float64 tensors) o
 """
 from __future__ import annotations
 
-import collections
-
 from collections import deque
 
 from . import _abi
@@ -92,17 +90,14 @@ class IncrementalPPolyRange:
 
 class IncrementalKNN:
     """Point-point kNN over sliding windows with pane reuse (device tensors).  Each pane's top-k
-    (k indices, -1 padded, and distances) lands in a ring of P slots; a window merges the P lists
-    after offsetting each pane's indices by the pane's position in the window.  The kernels and the
-    torch plumbing between them run on one private stream; the caller's stream waits for it."""
+    (k indices, -1 padded, and distances) lands in a ring of P slots; a window is one
+    geohip_knn_merge_panes_async launch over the ring (the panes' slots oldest first, each
+    rebased by its offset in the window) -- no torch kernels between the pass and the merge."""
 
     def __init__(self, ctx: _abi.Context, grid: _abi.Grid, qx: float, qy: float, r: float, k: int, panes: int = 2):
-        import torch
         self.ctx, self.grid, self.q, self.r, self.k, self.p = ctx, grid, (qx, qy), r, int(k), int(panes)
-        self.stream = torch.cuda.Stream()
         self.sizes = deque(maxlen=self.p)  # sizes of the panes in the ring, oldest first
         self.count = 0                     # panes pushed so far
-        self._offs = collections.OrderedDict()  # (slot order, offsets) -> device tensors (LRU)
         self._dev = None
 
     def _alloc(self, dev):
@@ -116,41 +111,25 @@ class IncrementalKNN:
         self._dev = dev
 
     def push(self, x, y, sync: bool = True):
-        """Evaluate the new pane and merge the window.  sync=True: (idx, dist) trimmed to the
-        count (one host sync); sync=False: the k-long device outputs (idx -1 padded), no sync."""
-        import torch
+        """Evaluate the new pane and merge the window (on torch's current stream, which the ctx
+        follows).  sync=True: (idx, dist) trimmed to the count (one host sync); sync=False: the
+        k-long device outputs (idx -1 padded), no sync."""
         if self._dev != x.device:
             self._alloc(x.device)
-        caller = torch.cuda.current_stream()
-        self.stream.wait_stream(caller)  # the pane's x, y are ready
-        with self.ctx.using_stream(self.stream.cuda_stream), torch.cuda.stream(self.stream):
-            slot = self.count % self.p
-            self.ctx.knn_pp_async(self.grid, x, y, self.q[0], self.q[1], self.r, self.k, self.ring_i[slot],
-                                  self.ring_d[slot], self.cnt[0:1])
-            self.count += 1
-            self.sizes.append(len(x))
-            n = len(self.sizes)
-            order = tuple((self.count - n + j) % self.p for j in range(n))  # oldest first
-            offs = [0]
-            for size in list(self.sizes)[:-1]:
-                offs.append(offs[-1] + size)
-            key = (order, tuple(offs))
-            if key in self._offs:
-                self._offs.move_to_end(key)
-            else:  # a small LRU: pane sizes vary window to window in a time-based stream
-                self._offs[key] = (torch.tensor(order, dtype=torch.int64, device=x.device),
-                                   torch.tensor(offs, dtype=torch.int32, device=x.device).view(-1, 1))
-                while len(self._offs) > 8:
-                    self._offs.popitem(last=False)
-            oidx, otens = self._offs[key]
-            li = self.ring_i.index_select(0, oidx)
-            wi = torch.where(li >= 0, li + otens, li)
-            wd = self.ring_d.index_select(0, oidx)
-            self.ctx.knn_merge_async(wd, wi, n, self.k, self.k, self.mi, self.md, self.cnt[1:2])
-        caller.wait_stream(self.stream)
+        slot = self.count % self.p
+        self.ctx.knn_pp_async(self.grid, x, y, self.q[0], self.q[1], self.r, self.k, self.ring_i[slot],
+                              self.ring_d[slot], self.cnt[0:1])
+        self.count += 1
+        self.sizes.append(len(x))
+        n = len(self.sizes)
+        slots = [(self.count - n + j) % self.p for j in range(n)]  # oldest first
+        offs = [0]
+        for size in list(self.sizes)[:-1]:
+            offs.append(offs[-1] + size)
+        self.ctx.knn_merge_panes_async(self.ring_d, self.ring_i, slots, offs, self.k, self.mi, self.md, self.cnt[1:2])
         if not sync:
             return self.mi, self.md
-        m = int((self.mi != -1).sum().item())
+        m = int(self.cnt[1].item())
         return self.mi[:m].clone(), self.md[:m].clone()
 
 

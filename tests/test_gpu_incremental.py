@@ -96,3 +96,30 @@ def test_incremental_ppoly_equals_full_window(ctx):
         wy = np.concatenate([w[1] for w in win])
         want = cref.range_ppoly(cg, wx, wy, off, vx, vy, 0.01)
         assert pairs_sorted(got).tolist() == pairs_sorted(want).tolist()
+
+
+@pytest.mark.parametrize("p,k", [(16, 40), (5, 300), (2, 2000)])
+def test_pane_merge_many_panes(ctx, p, k):
+    """geohip_knn_merge_panes_async over up to 16 panes of a ring (slots rotating, ties across
+    panes, panes with fewer candidates than k, the large-k pane pass): every window equals the
+    kNN of the window's concatenated panes."""
+    import torch
+    ag, cg = grids(100)
+    rng = np.random.default_rng(p * 31 + k)
+    panes = []
+    base = 0
+    for j in range(p + 4):
+        s = int(rng.integers(2000, 60000)) if j % 3 else 900
+        x, y = synth.uniform(s, 70 + j, base=base)
+        x[:5] = Q[0] + 1e-3  # exact ties across panes (ordered by window index)
+        y[:5] = Q[1]
+        panes.append((x, y))
+        base += s
+    inc = IncrementalKNN(ctx, ag, Q[0], Q[1], 0.5, k, p)
+    for j, (x, y) in enumerate(panes):
+        gi, gd = inc.push(torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda())
+        win = panes[max(0, j - p + 1):j + 1]
+        wi, wd = cref.knn_pp(cg, np.concatenate([w[0] for w in win]), np.concatenate([w[1] for w in win]),
+                             Q[0], Q[1], 0.5, k)
+        assert gi.cpu().numpy().tolist() == wi.tolist(), j
+        assert np.array_equal(gd.cpu().numpy().view(np.uint64), wd.view(np.uint64)), j

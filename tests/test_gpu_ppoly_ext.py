@@ -218,3 +218,28 @@ def test_sharded_device_paths_world1(ctx):
         assert np.array_equal(res.dist.cpu().numpy().view(np.uint64), wd.view(np.uint64))
     finally:
         dist.destroy_process_group()
+
+
+def test_knn_ppoly_async_cached_plan(ctx):
+    """geohip_knn_ppoly_async: the polygon plan cached by the ctx across windows and replaced when
+    the polygon changes; the selection path guessed from the previous window's candidate count
+    (a small window after a huge one and the reverse) -- every result exact vs the oracle."""
+    import torch
+    ag, cg = agrid(500)
+    rng = np.random.default_rng(91)
+    small = np.array(synth._star(rng, 116.4, 40.2, 0.01, 30))
+    huge = np.array(synth._star(rng, 116.5, 40.3, 0.35, 60))  # > 128K candidates in a 2M window
+    oi = torch.empty(64, dtype=torch.int32, device="cuda")
+    od = torch.empty(64, dtype=torch.float64, device="cuda")
+    oc = torch.zeros(1, dtype=torch.int32, device="cuda")
+    for j, (poly, n) in enumerate([(small, 300_000), (small, 2_000_000), (huge, 2_000_000), (huge, 300_000),
+                                   (small, 2_000_000), (huge, 2_000_000), (small, 0)]):
+        x, y = synth.uniform(n, 92 + j)
+        tx, ty = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+        for k in (50, 64):
+            ctx.knn_ppoly_async(ag, tx, ty, poly[:, 0].copy(), poly[:, 1].copy(), 0.005, k, False, oi, od, oc)
+            wi, wd = cref.knn_ppoly(cg, x, y, poly[:, 0].copy(), poly[:, 1].copy(), 0.005, k)
+            m = int(oc.item())
+            assert m == len(wi), (j, k)
+            assert oi[:m].cpu().numpy().astype(np.uint32).tolist() == wi.tolist(), (j, k)
+            assert np.array_equal(od[:m].cpu().numpy().view(np.uint64), wd.view(np.uint64)), (j, k)
