@@ -299,10 +299,12 @@ int geohip_format_points_csv(geohip_ctx* ctx, const geohip_csv_out_spec* spec, c
    as out_cell[i] = cx * grid->n + cy for a valid key (0 <= cx, cy < n), else 0xffffffff.
    Record i is the i-th line; a final empty line (text ending in '\n') is not a record.
    Every parsed value is the double Double.parseDouble / the JSON and WKT readers produce
-   (correctly rounded).  Records the device grammar cannot decide -- malformed ones, where the
-   reference throws, and rare valid forms (hex significands, 6+ digit exponents, quotes inside
-   a number, Z/M ordinates) -- make the call return GEOHIP_ERR_UNSUPPORTED with *out_bad = the
-   first such record; the caller hands that batch to the reference deserializer.
+   (correctly rounded), for the whole Java grammar: decimal and hex significands, exponents of any
+   length, type suffixes, quotes inside CSV tokens, 19-digit longs, a third WKT ordinate, NaN
+   words.  Records the device does not decide -- malformed ones, where the reference throws, and
+   forms whose Java behaviour is not restated (tokens of 100000+ characters, Z / M tags, POINT
+   EMPTY) -- make the call return GEOHIP_ERR_UNSUPPORTED with *out_bad = the first such record;
+   the caller hands that batch to the reference deserializer.
    GEOHIP_MEM_DEVICE: text (16-byte aligned) and outputs are device pointers.
    *out_count = number of records (GEOHIP_ERR_CAPACITY if > cap; outputs hold the first cap). */
 #define GEOHIP_FMT_CSV 0

@@ -11,14 +11,16 @@
 //       str.indexOf("POINT"), JTS WKTReader.read(substring), getCoordinate()
 //
 // The device parser accepts exactly what it can decide bit-exactly -- decimal tokens (any digit
-// count when the 19-digit truncation decides the rounding), NaN/Infinity, Java type suffixes
-// and the common record shapes -- and converts them with the Eisel-Lemire algorithm (correctly
-// rounded, ties to even: the value Double.parseDouble returns).  Everything else returns
-// kFallback and the batch call reports GEOHIP_ERR_UNSUPPORTED with the first such record:
-// malformed text (where the reference throws NumberFormatException / IndexOutOfBounds) and the
-// rare valid forms outside the device grammar (hex significands, 6+ digit exponents, quotes
-// inside a token, ...).  The library has no CPU parsing path; the caller hands
-// such a batch back to the reference's own Java deserializer, which parses it or throws.
+// count when the 19-digit truncation decides the rounding, exponents of any length), hex
+// significands (FloatingDecimal.parseHexString), NaN/Infinity, Java type suffixes, quotes inside
+// CSV tokens, 19-digit longs, a third WKT ordinate and the common record shapes -- and converts
+// decimals with the Eisel-Lemire algorithm (correctly rounded, ties to even: the value
+// Double.parseDouble returns).  Everything else returns kFallback and the batch call reports
+// GEOHIP_ERR_UNSUPPORTED with the first such record: malformed text (where the reference throws
+// NumberFormatException / IndexOutOfBounds / ParseException) and forms whose Java behaviour is
+// not restated here (tokens of 100000+ characters, a zero hex significand with an exponent past
+// int range, Z / M tags).  The library has no CPU parsing path; the caller
+// hands such a batch back to the reference's own Java deserializer, which parses it or throws.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -107,18 +109,120 @@ __host__ __device__ inline bool is_jspace(uint8_t c) {
     return c == ' ' || c == '\t' || c == '\n' || c == 0x0b || c == '\f' || c == '\r';
 }
 
+// A token this long could carry enough leading zeros to cancel a 10^6+ exponent, where
+// FloatingDecimal's exponent clamp (expLimit) is not restated: such tokens go to the host.
+constexpr uint64_t kMaxTokenLen = 100000;
+
+// Hex significand (FloatingDecimal.parseHexString): 0[xX](hex+[.]|hex*.hex+)[pP][+-]?digits
+// [fFdD]? after the sign, at p; the exact binary value correctly rounded (ties to even) to
+// binary64, subnormals included; an exponent past int range is +-Infinity / 0 (a zero
+// significand with one -> kFallback).
+template <class R>
+__host__ __device__ inline int parse_hex(const R& rd, uint64_t p, uint64_t e, bool neg, double* out) {
+    p += 2;  // "0x"
+    uint64_t m = 0;      // leading 60 significant bits
+    int64_t e2 = 0;      // value = (m + below) * 2^e2
+    bool sticky = false; // a nonzero bit below m
+    int nh = 0;
+    auto hv = [](uint8_t c) -> int {
+        if (c >= '0' && c <= '9') return c - '0';
+        if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+        if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+        return -1;
+    };
+    uint8_t c = p < e ? rd(p) : 0;
+    for (int v; p < e && (v = hv(c)) >= 0; c = ++p < e ? rd(p) : 0, nh++) {
+        if ((m >> 56) == 0) m = m * 16 + (uint64_t)v;
+        else {
+            sticky |= v != 0;
+            e2 += 4;
+        }
+    }
+    if (p < e && c == '.') {
+        c = ++p < e ? rd(p) : 0;
+        for (int v; p < e && (v = hv(c)) >= 0; c = ++p < e ? rd(p) : 0, nh++) {
+            if ((m >> 56) == 0) {
+                m = m * 16 + (uint64_t)v;
+                e2 -= 4;
+            } else {
+                sticky |= v != 0;
+            }
+        }
+    }
+    if (nh == 0 || p >= e || (c != 'p' && c != 'P')) return kFallback;
+    c = ++p < e ? rd(p) : 0;
+    bool eneg = false;
+    if (p < e && (c == '+' || c == '-')) {
+        eneg = c == '-';
+        c = ++p < e ? rd(p) : 0;
+    }
+    int64_t ev = 0;
+    int ne = 0;
+    bool big = false;  // past int range (Integer.parseInt of the exponent fails)
+    while (p < e && is_digit(c)) {
+        if (ev > 214748364 || (ev == 214748364 && c - '0' > 7)) big = true;
+        if (!big) ev = ev * 10 + (c - '0');
+        ne++;
+        c = ++p < e ? rd(p) : 0;
+    }
+    if (ne == 0) return kFallback;
+    if (p < e && (c == 'f' || c == 'F' || c == 'd' || c == 'D')) p++;
+    if (p != e) return kFallback;
+    const uint64_t sign = neg ? 1ull << 63 : 0ull;
+    if (m == 0) {
+        if (big) return kFallback;
+        *out = __builtin_bit_cast(double, sign);
+        return kOk;
+    }
+    uint64_t bits;
+    if (big) {
+        bits = eneg ? 0ull : 0x7ffull << 52;
+    } else {
+        const int lz = __builtin_clzll(m);
+        m <<= lz;  // value = 1.f * 2^ex
+        const int64_t ex = e2 + (eneg ? -ev : ev) + 63 - lz;
+        if (ex > 1023) {
+            bits = 0x7ffull << 52;
+        } else {
+            const int sh = ex >= -1022 ? 11 : (int)(11 + (-1022 - ex) < 70 ? 11 + (-1022 - ex) : 70);
+            uint64_t mant = 0;
+            bool up = false;
+            if (sh < 64) {
+                mant = m >> sh;
+                const uint64_t rem = m & ((1ull << sh) - 1), half = 1ull << (sh - 1);
+                up = rem > half || (rem == half && (sticky || (mant & 1)));
+            } else if (sh == 64) {
+                up = m > (1ull << 63) || (m == (1ull << 63) && sticky);
+            }
+            mant += up ? 1 : 0;
+            if (ex >= -1022) {
+                int64_t be = ex + 1023;
+                if (mant >> 53) {
+                    mant >>= 1;
+                    be++;
+                }
+                bits = be >= 0x7ff ? 0x7ffull << 52 : ((uint64_t)be << 52) | (mant & ((1ull << 52) - 1));
+            } else {
+                bits = mant;  // subnormal (a carry to 2^52 is the smallest normal)
+            }
+        }
+    }
+    *out = __builtin_bit_cast(double, bits | sign);
+    return kOk;
+}
+
 // Decimal token [s, e) -> double (correctly rounded, ties to even).
 // json: RFC 8259 number grammar as Jackson reads it (no '+', no leading zeros, digits on both
-//   sides of '.'); an integer token is an IntNode/LongNode, so "-0" is +0.0 and integers of
-//   more than 18 digits (LongNode overflow, BigIntegerNode) go to kFallback.
+//   sides of '.'); an integer token is an IntNode/LongNode, so "-0" is +0.0, and an integer
+//   outside long range (BigIntegerNode, which JTS's reader rejects) goes to kFallback.
 // else: FloatingDecimal.readJavaFormatString's grammar on an already trimmed token: [+-]?
-//   then "NaN" | "Infinity" | digits[.digits][(e|E)[+-]?digits][fFdD].  Hex significands and
-//   exponents of 6+ digits -> kFallback.
+//   then "NaN" | "Infinity" | hex (parse_hex) | digits[.digits][(e|E)[+-]?digits][fFdD].
+// Exponents of any length: beyond 10^8 the value is 0 or +-Infinity for a nonzero significand.
 // More than 19 significant digits: the token is truncated to 19 and converted at w and w + 1;
 // equal results decide it (the true value lies between them), unequal -> kFallback.
 template <class R>
 __host__ __device__ inline int parse_decimal(const R& rd, uint64_t s, uint64_t e, bool json, double* out) {
-    if (s >= e) return kFallback;
+    if (s >= e || e - s >= kMaxTokenLen) return kFallback;
     uint64_t p = s;
     uint8_t c = rd(p);
     bool neg = false;
@@ -127,6 +231,7 @@ __host__ __device__ inline int parse_decimal(const R& rd, uint64_t s, uint64_t e
         if (++p >= e) return kFallback;
         c = rd(p);
     }
+    if (!json && c == '0' && p + 1 < e && (rd(p + 1) == 'x' || rd(p + 1) == 'X')) return parse_hex(rd, p, e, neg, out);
     if (!json && (c == 'N' || c == 'I')) {
         const char* word = c == 'N' ? "NaN" : "Infinity";
         const uint64_t len = c == 'N' ? 3 : 8;
@@ -190,8 +295,7 @@ __host__ __device__ inline int parse_decimal(const R& rd, uint64_t s, uint64_t e
         int32_t ev = 0;
         int ne = 0;
         while (p < e && is_digit(c)) {
-            if (ne == 6) return kFallback;  // |exponent| >= 10^6: Java saturates; not decided here
-            ev = ev * 10 + (c - '0');
+            if (ev < 100000000) ev = ev * 10 + (c - '0');  // beyond: 0 or Infinity either way
             ne++;
             if (++p < e) c = rd(p);
         }
@@ -201,7 +305,8 @@ __host__ __device__ inline int parse_decimal(const R& rd, uint64_t s, uint64_t e
     if (p < e && !json && (c == 'f' || c == 'F' || c == 'd' || c == 'D')) p++;  // type suffix
     if (p != e) return kFallback;  // hex, stray characters
     if (json && !frac && !expo) {
-        if (nd > 18) return kFallback;
+        // IntNode / LongNode (then Long.valueOf of its text): within long range only
+        if (nd > 19 || (nd == 19 && w > (neg ? 9223372036854775808ull : 9223372036854775807ull))) return kFallback;
         if (w == 0) neg = false;  // IntNode 0
     }
     uint64_t bits = decimal_to_bits(w, q);
@@ -213,7 +318,7 @@ __host__ __device__ inline int parse_decimal(const R& rd, uint64_t s, uint64_t e
     return kOk;
 }
 
-// Long.valueOf: [+-]?digits, no trim; 18 digits at most here (longer -> host range check)
+// Long.valueOf: [+-]?digits, no trim, within [-2^63, 2^63 - 1] (else NumberFormatException)
 template <class R>
 __host__ __device__ inline int parse_long(const R& rd, uint64_t s, uint64_t e, int64_t* out) {
     if (s >= e) return kFallback;
@@ -221,15 +326,63 @@ __host__ __device__ inline int parse_long(const R& rd, uint64_t s, uint64_t e, i
     const uint8_t c0 = rd(p);
     const bool neg = c0 == '-';
     if (c0 == '+' || c0 == '-') p++;
-    if (p >= e || e - p > 18) return kFallback;
-    int64_t v = 0;
+    if (p >= e) return kFallback;
+    uint64_t v = 0;
+    const uint64_t lim = neg ? 9223372036854775808ull : 9223372036854775807ull;
     for (; p < e; p++) {
         const uint8_t c = rd(p);
         if (!is_digit(c)) return kFallback;
-        v = v * 10 + (c - '0');
+        const uint64_t d = (uint64_t)(c - '0');
+        if (v > (lim - d) / 10) return kFallback;  // beyond the long range
+        v = v * 10 + d;
     }
-    *out = neg ? -v : v;
+    *out = neg ? (int64_t)(0ull - v) : (int64_t)v;
     return kOk;
+}
+
+// A token with the quotes inside it deleted (str.replace("\"", "") before the split), copied
+// into a local buffer; tokens longer than kQuoteBuf -> kFallback.
+constexpr int kQuoteBuf = 96;
+struct BufReader {
+    const uint8_t* b;
+    __host__ __device__ uint8_t operator()(uint64_t p) const { return b[p]; }
+};
+template <class R>
+__host__ __device__ inline bool unquote(const R& rd, uint64_t t0, uint64_t t1, uint8_t* buf, uint64_t* len) {
+    uint64_t n = 0;
+    for (uint64_t p = t0; p < t1; p++) {
+        const uint8_t c = rd(p);
+        if (c == '"') continue;
+        if (n >= (uint64_t)kQuoteBuf) return false;
+        buf[n++] = c;
+    }
+    *len = n;
+    return true;
+}
+
+// A CSV field's number: quotes inside the token are deleted first (the reference deletes every
+// quote before the split)
+template <class R>
+__host__ __device__ inline bool has_quote(const R& rd, uint64_t t0, uint64_t t1) {
+    for (uint64_t p = t0; p < t1; p++)
+        if (rd(p) == '"') return true;
+    return false;
+}
+template <class R>
+__host__ __device__ inline int field_decimal(const R& rd, uint64_t t0, uint64_t t1, double* v) {
+    if (!has_quote(rd, t0, t1)) return parse_decimal(rd, t0, t1, false, v);
+    uint8_t buf[kQuoteBuf];
+    uint64_t n = 0;
+    if (!unquote(rd, t0, t1, buf, &n)) return kFallback;
+    return parse_decimal(BufReader{buf}, 0, n, false, v);
+}
+template <class R>
+__host__ __device__ inline int field_long(const R& rd, uint64_t t0, uint64_t t1, int64_t* v) {
+    if (!has_quote(rd, t0, t1)) return parse_long(rd, t0, t1, v);
+    uint8_t buf[kQuoteBuf];
+    uint64_t n = 0;
+    if (!unquote(rd, t0, t1, buf, &n)) return kFallback;
+    return parse_long(BufReader{buf}, 0, n, v);
 }
 
 // CSVTSVToSpatial / CSVTSVToTSpatial.  Quotes are deleted before the split, so they never end a
@@ -286,12 +439,12 @@ __host__ __device__ inline int parse_csv(const R& rd, uint64_t p, const Spec& sp
         }
         if (f == sp.fx || f == sp.fy) {
             double v;
-            if (t0 == ~0ull || parse_decimal(rd, t0, t1, false, &v) != kOk) return kFallback;
+            if (t0 == ~0ull || field_decimal(rd, t0, t1, &v) != kOk) return kFallback;
             if (f == sp.fx) o->x = v;
             if (f == sp.fy) o->y = v;
         }
         if (f == sp.fts && (ctrl || (f == 0 && lead) || (!sep && trail) || t0 == ~0ull ||
-                            parse_long(rd, t0, t1, &o->ts) != kOk))
+                            field_long(rd, t0, t1, &o->ts) != kOk))
             return kFallback;
         if (f == need) return kOk;
         if (!sep) return kFallback;  // fewer fields than the schema names: the reference throws
@@ -357,8 +510,19 @@ __host__ __device__ inline uint64_t wkt_skip(const R& rd, uint64_t p) {
     }
 }
 
-// WKTToSpatial: "POINT" (first occurrence) then "(" x y ")"; POINT EMPTY, Z / M tags, a third
-// ordinate and NaN words go to the host.
+// WKTReader.getNextNumber: a word equal to "NaN" ignoring case is NaN, else Double.parseDouble
+template <class R>
+__host__ __device__ inline int wkt_number(const R& rd, uint64_t s, uint64_t e, double* v) {
+    if (e - s == 3 && (rd(s) | 32) == 'n' && (rd(s + 1) | 32) == 'a' && (rd(s + 2) | 32) == 'n') {
+        *v = __builtin_bit_cast(double, 0x7ff8000000000000ull);
+        return kOk;
+    }
+    return parse_decimal(rd, s, e, false, v);
+}
+
+// WKTToSpatial: "POINT" (first occurrence) then "(" x y [z] ")" (getPreciseCoordinate reads a
+// third ordinate when a word follows; getCoordinate() keeps x and y).  POINT EMPTY and Z / M
+// tags go to the host.
 template <class R>
 __host__ __device__ inline int parse_wkt(const R& rd, uint64_t p, Parsed* o) {
     for (;; p++) {
@@ -373,13 +537,21 @@ __host__ __device__ inline int parse_wkt(const R& rd, uint64_t p, Parsed* o) {
     p = wkt_skip(rd, p + 1);
     uint64_t t = p;
     while (wkt_word(rd(t))) t++;
-    if (parse_decimal(rd, p, t, false, &o->x) != kOk) return kFallback;
+    if (p == t || wkt_number(rd, p, t, &o->x) != kOk) return kFallback;
     p = wkt_skip(rd, t);
     if (p == t) return kFallback;  // the next token is not separated by blanks: ',' or ')' -> error
     t = p;
     while (wkt_word(rd(t))) t++;
-    if (parse_decimal(rd, p, t, false, &o->y) != kOk) return kFallback;
+    if (p == t || wkt_number(rd, p, t, &o->y) != kOk) return kFallback;
     p = wkt_skip(rd, t);
+    if (wkt_word(rd(p))) {  // a third ordinate (z): read, validated, dropped
+        if (p == t) return kFallback;
+        t = p;
+        while (wkt_word(rd(t))) t++;
+        double z;
+        if (wkt_number(rd, p, t, &z) != kOk) return kFallback;
+        p = wkt_skip(rd, t);
+    }
     return rd(p) == ')' ? kOk : kFallback;
 }
 

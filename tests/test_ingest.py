@@ -62,8 +62,17 @@ KNOWN = [
     (CSV_T, b"7,12.0,1,2", None, False),  # Long.valueOf
     (CSV_T, b"7, 12\x01,1,2", None, False),  # Long.valueOf does not trim
     (CSV_T, b"7,9223372036854775808,1,2", None, False),  # Long overflow
-    (CSV_T, b"7,-9223372036854775808,1,2", (1.0, 2.0, -9223372036854775808), True),
-    (CSV_T, b"7,12,0x1.8p1,2", (3.0, 2.0, 12), True),  # hex significand
+    (CSV_T, b"7,-9223372036854775808,1,2", (1.0, 2.0, -9223372036854775808), False),
+    (CSV_T, b"7,9223372036854775807,1,2", (1.0, 2.0, 9223372036854775807), False),
+    (CSV_T, b"7,12,0x1.8p1,2", (3.0, 2.0, 12), False),  # hex significand
+    (CSV_T, b"7,12,-0X.8P-1d,0x1p-1074", (-0.25, 5e-324, 12), False),
+    (CSV_T, b"7,12,0x1p-1075,0x1.0000000000001p-1075", (0.0, 5e-324, 12), False),  # tie to even / just above
+    (CSV_T, b"7,12,0x1.fffffffffffff8p1023,0x1p99999999999", (INF, INF, 12), False),  # rounds past MAX / int range
+    (CSV_T, b"7,12,0x0.0p5,-0x1p-99999999999", (0.0, -0.0, 12), False),
+    (CSV_T, b"7,12,0x1.00000000000008p0,0x1.00000000000018p0", (1.0, 1.0000000000000004, 12), False),  # ties
+    (CSV_T, b"7,12,0x123456789abcdef0123p-70,2", (float.fromhex("0x123456789abcdef0123p-70"), 2.0, 12), False),
+    (CSV_T, b"7,12,0xp1,2", None, False),
+    (CSV_T, b"7,12,0x1.8p,2", None, False),
     (CSV_T, b"7,12,0x1.8,2", None, False),  # hex needs a binary exponent
     (CSV_T, b"7,12,1.5,2,extra", (1.5, 2.0, 12), False),
     (CSV_T, b",12,1,2", (1.0, 2.0, 12), False),  # leading "" field
@@ -73,8 +82,11 @@ KNOWN = [
     (CSV_T, b"7,12,2.2250738585072011e-308,4.9e-324", (2.225073858507201e-308, 5e-324, 12), False),
     (CSV_T, b"7,12,1e400,1e-400", (INF, 0.0, 12), False),
     (CSV_T, b"7,12,-0.0,0", (-0.0, 0.0, 12), False),
-    (CSV_T, b"7,12,1e1000000,2", (INF, 2.0, 12), True),  # 7-digit exponent
-    (CSV_T, b'7,12,1"5,2', (15.0, 2.0, 12), True),  # quotes deleted inside a token
+    (CSV_T, b"7,12,1e1000000,2", (INF, 2.0, 12), False),  # 7-digit exponent
+    (CSV_T, b"7,12,1e-99999999999999,0e99999999999", (0.0, 0.0, 12), False),
+    (CSV_T, b"7,12,-0.001e1000000002,2", (-INF, 2.0, 12), False),
+    (CSV_T, b'7,12,1"5,2', (15.0, 2.0, 12), False),  # quotes deleted inside a token
+    (CSV_T, b'7,1"2,-"1".5"e1,2', (-15.0, 2.0, 12), False),
     (CSV_T, b"7,12,1 5,2", None, False),
     (CSV, b"a,b,116.5,39.75", (116.5, 39.75, 0), False),
     (CSV, b"a,b,116.5,", None, False),  # trailing "" removed -> get(3) throws
@@ -90,7 +102,10 @@ KNOWN = [
     (WKT, b"POINT (116.5,39.75)", None, False),
     (WKT, b"POINT EMPTY", None, False),
     (WKT, b"MULTIPOINT ((1 2))", None, False),
-    (WKT, b"POINT (1 2 3)", (1.0, 2.0, 0), True),
+    (WKT, b"POINT (1 2 3)", (1.0, 2.0, 0), False),
+    (WKT, b"POINT (nan NaN 0x1p4)", (NAN, NAN, 0), False),  # WKTReader: NaN ignoring case
+    (WKT, b"POINT (1 2 3 4)", None, False),
+    (WKT, b"POINT (1 2 x)", None, False),
     (WKT, b"POINT (1.5d -2e1)", (1.5, -20.0, 0), False),
     (WKT, b"point (1 2)", None, False),
     (WKT, b"POINTZ (1 2)", None, False),
@@ -104,6 +119,9 @@ KNOWN = [
     (GEO, b'{"type":"Point","coordinates":[1.,2]}', None, False),
     (GEO, b'{"type":"LineString","coordinates":[[1,2],[3,4]]}', (1.0, 2.0, 0), False),
     (GEO, b'{"type":"Point","coordinates":[1e400,2]}', None, False),
+    (GEO, b'{"type":"Point","coordinates":[9223372036854775807,-9223372036854775808]}',
+     (9.223372036854776e18, -9.223372036854776e18, 0), False),  # LongNode
+    (GEO, b'{"type":"Point","coordinates":[9223372036854775808,1]}', None, False),  # BigIntegerNode
 ]
 
 
@@ -265,3 +283,39 @@ def test_spec_validation():
         _abi.debug_ingest_record(_abi.make_ingest_spec(cref.CSV, "|", 0, 1), b"1|2")  # regex metacharacter
     with pytest.raises(_abi.GeohipArgumentError):
         _abi.debug_ingest_record(_abi.make_ingest_spec(cref.CSV, ",", -1, 1), b"1,2")
+
+
+def test_hex_and_long_exponent_fuzz():
+    """Random hex significands (Double.parseDouble's parseHexString grammar) and decimal tokens with
+    long exponents: device parser == oracle (glibc strtod, correctly rounded) == Python."""
+    rng = random.Random(424242)
+    spec_d, spec_o = _spec_dev(TSV), _spec_oracle(TSV)
+    for _ in range(20000):
+        toks = []
+        for _t in range(2):
+            if rng.random() < 0.7:
+                ih = "".join(rng.choice("0123456789abcdefABCDEF") for _ in range(rng.choice([0, 1, 2, 7, 14, 16, 20])))
+                fh = "".join(rng.choice("0123456789abcdef") for _ in range(rng.choice([0, 1, 3, 13, 15, 20])))
+                if not ih and not fh:
+                    ih = "1"
+                body = ih + ("." + fh if fh or rng.random() < 0.2 else "")
+                ex = rng.choice([0, 1, -1, 52, -1022, -1074, -1075, -1080, 1023, 1024, -1100, 900, -990,
+                                 rng.randint(-1200, 1200)])
+                t = rng.choice(["", "-", "+"]) + rng.choice(["0x", "0X"]) + body + rng.choice("pP") + str(ex)
+                t += rng.choice(["", "", "d", "F"])
+                try:
+                    want = float.fromhex(t.rstrip("dF"))
+                except OverflowError:
+                    want = -INF if t.startswith("-") else INF
+            else:
+                m = rng.choice(["1", "0", "0.0", "7.25", "123456789", "0.000001"])
+                e = rng.choice([1000000, 99999999, 123456789012, -1000000, -99999999999])
+                t = rng.choice(["", "-"]) + m + "e" + str(e)
+                want = float(t)
+            toks.append((t, want))
+        rec = f"{toks[0][0]}\t{toks[1][0]}".encode()
+        o = cref.ingest_record(spec_o, rec)
+        d = _abi.debug_ingest_record(spec_d, rec)
+        assert o is not None and d is not None, rec
+        for k in range(2):
+            assert _same(o[k], toks[k][1]) and _same(d[k], toks[k][1]), (rec, o, d)
