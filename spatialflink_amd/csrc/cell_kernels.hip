@@ -214,7 +214,12 @@ struct BinPass {
     const uint4* items;    // level 2: (band, begin, end, -)
     const unsigned* nitems;
     const unsigned* keep;  // optional cell bitmap (nb * nb bits): points of other cells are dropped
+    unsigned keep_words;   // its words; level 1 copies it into LDS when it fits kKeepLds
 };
+
+// Level 1 reads the keep bitmap once per point at a random word: from LDS when the bitmap fits
+// (nb <= 512), so the per-lane gathers do not go through the vector L1 (bin_*<1, KL = true>).
+constexpr unsigned kKeepLds = 8192;
 
 __device__ __forceinline__ unsigned key_tile(const TileGeom& g, unsigned key) {
     const unsigned nb = (unsigned)g.nb;
@@ -234,8 +239,16 @@ __device__ __forceinline__ unsigned l1_key(const BinPass& a, double px, double p
     }
     return kNoKey;
 }
-__device__ __forceinline__ unsigned l1_keepword(const BinPass& a, unsigned key) {
-    return (a.keep && key != kNoKey) ? a.keep[key >> 5] : ~0u;
+// KL (a launch-time choice: one pointer that may be either would compile to flat loads)
+template <bool KL>
+__device__ __forceinline__ unsigned l1_keepword(const BinPass& a, const unsigned* kl, unsigned key) {
+    if (!a.keep || key == kNoKey) return ~0u;
+    return KL ? kl[key >> 5] : a.keep[key >> 5];
+}
+template <bool KL>
+__device__ __forceinline__ void keep_stage(const BinPass& a, unsigned* kl) {
+    if (KL)
+        for (unsigned t = threadIdx.x; t < a.keep_words; t += kBinThreads) kl[t] = a.keep[t];
 }
 __device__ __forceinline__ unsigned l1_bin(const BinPass& a, unsigned key, unsigned kw, unsigned tile) {
     if (key == kNoKey) return a.nbands;
@@ -270,25 +283,35 @@ __device__ __forceinline__ bool bin_range(const BinPass& a, uint64_t& b0, uint64
     return true;
 }
 
-template <int LEVEL>
+template <bool B>
+struct BoolC {
+    static constexpr bool value = B;
+};
+
+template <int LEVEL, bool KL = false>
 __global__ __launch_bounds__(kBinThreads) void bin_count(BinPass a) {
     __shared__ unsigned h[kBinThreads / kWave][kLocalBins];
+    __shared__ unsigned kl[KL ? kKeepLds : 1];
     uint64_t b0, b1;
     unsigned nbins, band;
     if (!bin_range<LEVEL>(a, b0, b1, nbins, band)) return;
+    keep_stage<KL>(a, kl);
     const int wid = threadIdx.x / kWave;
     for (unsigned t = threadIdx.x; t < (kBinThreads / kWave) * kLocalBins; t += kBinThreads) (&h[0][0])[t] = 0;
     __syncthreads();
     // kU points per thread with all their loads issued first (a single load pair per thread in
     // flight left the pass latency-bound at 2.5 TB/s; level 1 runs one block per CU: 8)
     constexpr unsigned kU = LEVEL == 1 ? 8 : 4;
-    for (uint64_t i0 = b0 + threadIdx.x; i0 < b1; i0 += kU * kBinThreads) {
+    // FULL: every thread's kU points are in range (all but the block's last step), so the loads
+    // carry no guards and their waits count down one at a time instead of vmcnt(0)
+    auto step = [&](uint64_t i0, auto full) {
+        constexpr bool FULL = decltype(full)::value;
         double px[kU], py[kU];
         unsigned key[kU], tl[kU];
 #pragma unroll
         for (unsigned k = 0; k < kU; k++) {
             const uint64_t i = i0 + (uint64_t)k * kBinThreads;
-            if (i < b1) {
+            if (FULL || i < b1) {
                 if (LEVEL == 1) {
                     px[k] = a.x[i];
                     py[k] = a.y[i];
@@ -302,18 +325,22 @@ __global__ __launch_bounds__(kBinThreads) void bin_count(BinPass a) {
 #pragma unroll
             for (unsigned k = 0; k < kU; k++) {
                 key[k] = l1_key(a, px[k], py[k], tl[k]);
-                kw[k] = i0 + (uint64_t)k * kBinThreads < b1 ? l1_keepword(a, key[k]) : ~0u;
+                kw[k] = (FULL || i0 + (uint64_t)k * kBinThreads < b1) ? l1_keepword<KL>(a, kl, key[k]) : ~0u;
             }
         }
 #pragma unroll
         for (unsigned k = 0; k < kU; k++) {
             const uint64_t i = i0 + (uint64_t)k * kBinThreads;
-            if (i < b1) {
+            if (FULL || i < b1) {
                 const unsigned bin = LEVEL == 1 ? l1_bin(a, key[k], kw[k], tl[k]) : key_tile(a.g, key[k]) - (band << kBandBits);
                 if (LEVEL == 2 || bin != a.nbands + 1) atomicAdd(&h[wid][bin], 1u);  // dropped: not counted
             }
         }
-    }
+    };
+    constexpr uint64_t kSpan = (uint64_t)kU * kBinThreads;
+    uint64_t s0 = b0;
+    for (; s0 + kSpan <= b1; s0 += kSpan) step(s0 + threadIdx.x, BoolC<true>{});
+    if (s0 < b1) step(s0 + threadIdx.x, BoolC<false>{});
     __syncthreads();
     if (threadIdx.x < nbins) {
         unsigned c = 0;
@@ -423,15 +450,17 @@ struct SortStage {
 // and stored so consecutive threads write consecutive addresses of one bin's run.  Level 1 runs
 // one block per CU over the raw window: 4 points per thread per sub-chunk (64 KB of loads in
 // flight per CU; 2 per thread left it latency-bound at ~3 TB/s); level 2 has many more blocks.
-template <int LEVEL>
+template <int LEVEL, bool KL = false>
 __global__ __launch_bounds__(kBinThreads) void bin_scatter(BinPass a) {
     constexpr int PPT = LEVEL == 1 ? 4 : 2;
     constexpr int SUB = PPT * kBinThreads;
     __shared__ SortStage<SUB> st;
     __shared__ unsigned cur[kLocalBins], lh[kLocalBins], ls[kLocalBins];
+    __shared__ unsigned kl[KL ? kKeepLds : 1];
     uint64_t b0, b1;
     unsigned nbins, band;
     if (!bin_range<LEVEL>(a, b0, b1, nbins, band)) return;
+    keep_stage<KL>(a, kl);
     const unsigned* row = a.hist + (size_t)blockIdx.x * nbins;
     for (unsigned t = threadIdx.x; t < kLocalBins; t += kBinThreads) {
         cur[t] = t < nbins ? row[t] : 0u;
@@ -472,7 +501,7 @@ __global__ __launch_bounds__(kBinThreads) void bin_scatter(BinPass a) {
             py[k] = ny[k];
             idx[k] = LEVEL == 1 ? (unsigned)(sb + j) : nidx[k];
             key[k] = LEVEL == 1 ? l1_key(a, px[k], py[k], tl[k]) : nkey[k];
-            kw[k] = (LEVEL == 1 && j < m) ? l1_keepword(a, key[k]) : ~0u;  // issued before the prefetch
+            kw[k] = (LEVEL == 1 && j < m) ? l1_keepword<KL>(a, kl, key[k]) : ~0u;  // issued before the prefetch
         }
         if (sb + SUB < b1) fetch(sb + SUB);
 #pragma unroll
@@ -2611,10 +2640,18 @@ int bin_tiles(geohip_ctx* ctx, Scratch& S, const double* dx, const double* dy, u
     a.hist = hist1;
     a.nitems = misc + 4;
     a.keep = keep;
+    a.keep_words = keep ? (unsigned)(((uint64_t)geo.nb * (uint64_t)geo.nb + 31) / 32) : 0u;
     // level 1: bands
-    bin_count<1><<<(unsigned)nblk, kBinThreads, 0, st>>>(a);
-    bin1_offsets<<<1, kTB, 0, st>>>(hist1, (unsigned)nblk, nbands + 2, start1);
-    bin_scatter<1><<<(unsigned)nblk, kBinThreads, 0, st>>>(a);
+    // (the keep bitmap in LDS when it fits: its per-point word reads are random gathers)
+    if (keep && a.keep_words <= kKeepLds) {
+        bin_count<1, true><<<(unsigned)nblk, kBinThreads, 0, st>>>(a);
+        bin1_offsets<<<1, kTB, 0, st>>>(hist1, (unsigned)nblk, nbands + 2, start1);
+        bin_scatter<1, true><<<(unsigned)nblk, kBinThreads, 0, st>>>(a);
+    } else {
+        bin_count<1><<<(unsigned)nblk, kBinThreads, 0, st>>>(a);
+        bin1_offsets<<<1, kTB, 0, st>>>(hist1, (unsigned)nblk, nbands + 2, start1);
+        bin_scatter<1><<<(unsigned)nblk, kBinThreads, 0, st>>>(a);
+    }
     // level 2: tiles within each band
     bin2_plan<<<1, kTB, 0, st>>>(start1, nbands, items, wfirst, misc + 4);
     a.dst = carve_soa(l2, n);
