@@ -569,6 +569,7 @@ struct TileBins {
     const unsigned* start;  // ntiles + 1
     int32_t nb;
     FastDiv dnb;            // / nb (key -> cx)
+    int32_t ts, nt;         // cells per tile side, tiles per side
 };
 
 // ------------------------------------------------------------------ pair output ----------
@@ -1166,7 +1167,16 @@ struct PolyDev {
     uint32_t eoff;          // nring > 1: ring envelopes at renv[4 * eoff ...] (minx, miny, maxx, maxy)
     double gb[4];           // box of every ring (= bb unless a hole leaves the shell's envelope):
                             // the distance screens and slab lists are built on it
+    uint32_t cls;           // per-cell classes of the walk region at pcls[cls ...] (x-major,
+                            // (wy1 - wy0 + 1) per column), kNoCls: none (classify_cells)
+    uint32_t pad_cls;
 };
+
+// Per-cell classes of a polygon's exact-evaluation cells, decided once on the host for every
+// point a cell's exact coordinate box can hold (classify_cells): kClsHit -- every such point is
+// within r of the polygon (JTS distance <= r), kClsMiss -- none is, kClsMixed -- per point.
+constexpr uint8_t kClsMixed = 0, kClsHit = 1, kClsMiss = 2;
+constexpr uint32_t kNoCls = 0xffffffffu;
 
 // Polygons with holes: rings are stored back to back in one vertex run, with a ring id per
 // vertex (u16, < kMaxRings); segment (v[e], v[e+1]) exists iff both ends carry the same id (the
@@ -1520,6 +1530,7 @@ constexpr int kMaxLdsSlab = 2048;   // u16 slab-list entries staged in LDS
 constexpr int kMaskWords = 512;     // hit-mask words kept in LDS (tiles up to 32768 points)
 constexpr int kCandQ = 128;         // per-wave queue of points needing the exact polygon distance
 constexpr int kPolyPairs = 512;     // per-wave pair buffer of the polygon kernels
+constexpr int kTileCls = 1024;      // tile cells whose classes ppoly_eval stages (ts <= 32)
 
 struct PolyWork {
     uint32_t poly, tile;
@@ -1552,10 +1563,11 @@ __global__ __launch_bounds__(kTB) void ppoly_eval(TileBins tb, const PolyWork* _
                                                   const PolyDev* __restrict__ polys, const double* __restrict__ vx,
                                                   const double* __restrict__ vy, const ring_id_t* __restrict__ vring,
                                                   const double* __restrict__ renv, const int32_t* __restrict__ rects,
-                                                  const uint16_t* __restrict__ slabs, double r, int r_is_max,
-                                                  const unsigned long long* __restrict__ wofs,
+                                                  const uint16_t* __restrict__ slabs, const uint8_t* __restrict__ pcls,
+                                                  double r, int r_is_max, const unsigned long long* __restrict__ wofs,
                                                   unsigned long long* __restrict__ mask,
                                                   unsigned long long* __restrict__ bcount) {
+    __shared__ uint8_t lcls[kTileCls];  // the cell classes of this tile (P.cls)
     __shared__ double lvx[kMaxLdsVerts];
     __shared__ double lvy[kMaxLdsVerts];
     __shared__ ring_id_t lvr[kMaxLdsVerts];
@@ -1585,6 +1597,18 @@ __global__ __launch_bounds__(kTB) void ppoly_eval(TileBins tb, const PolyWork* _
     if (lds_mask)
         for (uint32_t t = threadIdx.x; t < nwords; t += kTB) lmask[t] = 0;
     if (threadIdx.x == 0) bsh = 0;
+    const int32_t ts = tb.ts;
+    const int32_t tx0 = (int32_t)(w.tile / (uint32_t)tb.nt) * ts, ty0 = (int32_t)(w.tile % (uint32_t)tb.nt) * ts;
+    const bool use_cls = !APPROX && P.cls != kNoCls && ts * ts <= kTileCls;
+    if (use_cls) {
+        const int32_t ch = P.wy1 - P.wy0 + 1;
+        for (int32_t t = threadIdx.x; t < ts * ts; t += kTB) {
+            const int32_t cx = tx0 + t / ts, cy = ty0 + t % ts;
+            lcls[t] = (cx >= P.wx0 && cx <= P.wx1 && cy >= P.wy0 && cy <= P.wy1)
+                          ? pcls[P.cls + (uint32_t)((cx - P.wx0) * ch + (cy - P.wy0))]
+                          : kClsMixed;
+        }
+    }
     __syncthreads();
     const double* rvx = v_lds ? lvx : vx + P.voff;
     const double* rvy = v_lds ? lvy : vy + P.voff;
@@ -1640,9 +1664,13 @@ __global__ __launch_bounds__(kTB) void ppoly_eval(TileBins tb, const PolyWork* _
             bool c = !g && in_r(c0, cx, cy);
             if (P.nc > 1 && !g && !c) c = in_rects(crect + 4, P.nc - 1, cx, cy);
             if (g || c) {
-                if (g || r_is_max) hit = true;
+                // a decided cell class applies to every point in the cell's coordinate box: not
+                // to NaN coordinates (cell 0 by Java's (int) NaN)
+                const uint8_t k = (use_cls && !g && px == px && py == py) ? lcls[(cx - tx0) * ts + (cy - ty0)] : kClsMixed;
+                if (g || r_is_max || k == kClsHit) hit = true;
                 else if (APPROX) hit = bbox_distance(px, py, P.bb) <= r;
-                else need = !(box_dist2(px, py, P.gb[0], P.gb[1], P.gb[2], P.gb[3]) > screen_lim2(px, py, P.gb, r));
+                else if (k != kClsMiss)
+                    need = !(box_dist2(px, py, P.gb[0], P.gb[1], P.gb[2], P.gb[3]) > screen_lim2(px, py, P.gb, r));
             }
         }
         const unsigned long long m = __ballot(hit);
@@ -2684,6 +2712,8 @@ int bin_tiles(geohip_ctx* ctx, Scratch& S, const double* dx, const double* dy, u
     tb->start = start;
     tb->nb = geo.nb;
     tb->dnb = geo.dnb;
+    tb->ts = geo.ts;
+    tb->nt = geo.nt;
     return GEOHIP_OK;
 }
 
@@ -2912,6 +2942,174 @@ void plan_slabs(PolyDev& P, const double* ry, const ring_id_t* rid, double r, do
     P.llen = (uint32_t)(2 * (ns + 1) + total);
 }
 
+// ---------------------------------------------------------------- cell classes ------------
+// Host geometry for classify_cells.  Every decision below is conservative: a computed quantity
+// only decides when it clears its rounding by a wide relative margin; otherwise the cell stays
+// kClsMixed and its points take the exact per-point path on the device.
+namespace cls {
+struct Seg {
+    double ax, ay, bx, by;
+    uint32_t ring;
+};
+// distance from p to segment s in plain fp64 (error << the margins used)
+inline double pt_seg(double px, double py, const Seg& s) {
+    const double ex = s.bx - s.ax, ey = s.by - s.ay;
+    const double l2 = ex * ex + ey * ey;
+    double t = l2 > 0.0 ? ((px - s.ax) * ex + (py - s.ay) * ey) / l2 : 0.0;
+    t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
+    const double dx = px - (s.ax + t * ex), dy = py - (s.ay + t * ey);
+    return std::sqrt(dx * dx + dy * dy);
+}
+// does the segment meet the box [x0, x1] x [y0, y1] (Liang-Barsky clip; the caller inflates the
+// box, so a computed "no" is a true "no")
+inline bool seg_meets_box(const Seg& s, double x0, double x1, double y0, double y1) {
+    double t0 = 0.0, t1 = 1.0;
+    const double dx = s.bx - s.ax, dy = s.by - s.ay;
+    const double pv[4] = {-dx, dx, -dy, dy};
+    const double qv[4] = {s.ax - x0, x1 - s.ax, s.ay - y0, y1 - s.ay};
+    for (int i = 0; i < 4; i++) {
+        if (pv[i] == 0.0) {
+            if (qv[i] < 0.0) return false;
+        } else {
+            const double t = qv[i] / pv[i];
+            if (pv[i] < 0.0) { if (t > t1) return false; if (t > t0) t0 = t; }
+            else { if (t < t0) return false; if (t < t1) t1 = t; }
+        }
+    }
+    return true;
+}
+// distance from the box to a segment that does not meet it: attained at a box corner or a
+// segment end (two disjoint convex sets)
+inline double box_seg(double x0, double x1, double y0, double y1, const Seg& s) {
+    double d = std::min(std::min(pt_seg(x0, y0, s), pt_seg(x0, y1, s)), std::min(pt_seg(x1, y0, s), pt_seg(x1, y1, s)));
+    auto pb = [&](double px, double py) {
+        const double ex = std::max(std::max(x0 - px, px - x1), 0.0), ey = std::max(std::max(y0 - py, py - y1), 0.0);
+        return std::sqrt(ex * ex + ey * ey);
+    };
+    return std::min(d, std::min(pb(s.ax, s.ay), pb(s.bx, s.by)));
+}
+}  // namespace cls
+
+// Classes of the cells of P's walk region that the device evaluates exactly (C cells; the join's
+// G u C in exact mode).  For a cell's exact coordinate box B (plan.cpp axis bounds: every
+// non-NaN point of the cell lies in B):
+//  * HIT when one segment s has all four corners of B within r - m of it (distance to a segment
+//    is convex, so every p in B is within r - m of s and the JTS distance, 0 inside or the
+//    minimum over segments outside, is <= r), or when no segment meets B and B's centre is
+//    inside the polygon (no point of B is then on a ring, the crossing parities are the same
+//    for all of B: every point is interior, distance 0);
+//  * MISS when no segment meets B, the centre is outside (so all of B is) and every segment is
+//    farther than r + m from B;
+//  * MIXED otherwise.  m = 2^-36 (scale + r) covers JTS's rounding (<= 2^-49 of the magnitudes,
+//    segment_within) and this code's own.
+// Returns false (no classes) for r < 0 / NaN / inf, non-finite vertices or too large a region.
+bool classify_cells(const PolyDev& P, const std::vector<double>& hvx, const std::vector<double>& hvy,
+                    const ring_id_t* rid, const geohip_grid& pg, const int32_t* rects, uint32_t first_c,
+                    uint32_t nrect_c, uint32_t nring, double r, std::vector<uint8_t>& blob, uint32_t* off) {
+    using cls::Seg;
+    *off = kNoCls;
+    if (!(r >= 0.0) || !std::isfinite(r) || P.wx0 > P.wx1 || P.wy0 > P.wy1 || nrect_c == 0) return false;
+    const uint32_t nv = P.nv;
+    std::vector<Seg> segs;
+    double scale = std::fabs(r);
+    for (uint32_t i = 0; i + 1 < nv; i++) {
+        const double ax = hvx[P.voff + i], ay = hvy[P.voff + i], bx = hvx[P.voff + i + 1], by = hvy[P.voff + i + 1];
+        if (!std::isfinite(ax) || !std::isfinite(ay) || !std::isfinite(bx) || !std::isfinite(by)) return false;
+        scale = std::max(scale, std::max(std::max(std::fabs(ax), std::fabs(ay)), std::max(std::fabs(bx), std::fabs(by))));
+        if (rid && rid[i] != rid[i + 1]) continue;  // ring junction: no segment
+        segs.push_back(Seg{ax, ay, bx, by, rid ? (uint32_t)rid[i] : 0u});
+    }
+    if (segs.empty()) return false;
+    const int32_t w = P.wx1 - P.wx0 + 1, h = P.wy1 - P.wy0 + 1;
+    if ((uint64_t)w * (uint64_t)h * segs.size() > 8000000ull) return false;
+    std::vector<double> xl(w), xh(w), yl(h), yh(h);
+    std::vector<uint8_t> okx(w), oky(h);
+    for (int32_t a = 0; a < w; a++)
+        okx[a] = axis_lower(pg.min_x, pg.cell_len, P.wx0 + a, &xl[a]) && axis_upper(pg.min_x, pg.cell_len, P.wx0 + a, &xh[a]) &&
+                 std::isfinite(xl[a]) && std::isfinite(xh[a]) && xl[a] <= xh[a];
+    for (int32_t c = 0; c < h; c++)
+        oky[c] = axis_lower(pg.min_y, pg.cell_len, P.wy0 + c, &yl[c]) && axis_upper(pg.min_y, pg.cell_len, P.wy0 + c, &yh[c]) &&
+                 std::isfinite(yl[c]) && std::isfinite(yh[c]) && yl[c] <= yh[c];
+    std::vector<uint8_t> par(nring, 0);
+    const size_t base = blob.size();
+    blob.resize(base + (size_t)w * h, kClsMixed);
+    uint8_t* out = blob.data() + base;
+    for (int32_t a = 0; a < w; a++) {
+        if (!okx[a]) continue;
+        for (int32_t c = 0; c < h; c++) {
+            if (!oky[c]) continue;
+            const int32_t cx = P.wx0 + a, cy = P.wy0 + c;
+            bool in_c = false;
+            for (uint32_t q = 0; q < nrect_c && !in_c; q++) {
+                const int32_t* R = rects + 4 * (first_c + q);
+                in_c = cx >= R[0] && cx <= R[1] && cy >= R[2] && cy <= R[3];
+            }
+            if (!in_c) continue;
+            const double x0 = xl[a], x1 = xh[a], y0 = yl[c], y1 = yh[c];
+            const double sc = std::max(scale, std::max(std::max(std::fabs(x0), std::fabs(x1)), std::max(std::fabs(y0), std::fabs(y1))));
+            const double m = 0x1.0p-36 * (sc + r);
+            // one segment covering the whole box
+            bool hit = false;
+            for (const Seg& s : segs) {
+                // (only a segment whose box, grown by r, holds the cell box can cover it)
+                if (std::min(s.ax, s.bx) - r > x0 || std::max(s.ax, s.bx) + r < x1 || std::min(s.ay, s.by) - r > y0 ||
+                    std::max(s.ay, s.by) + r < y1)
+                    continue;
+                if (std::max(std::max(cls::pt_seg(x0, y0, s), cls::pt_seg(x0, y1, s)),
+                             std::max(cls::pt_seg(x1, y0, s), cls::pt_seg(x1, y1, s))) <= r - m) {
+                    hit = true;
+                    break;
+                }
+            }
+            if (hit) {
+                out[(size_t)a * h + c] = kClsHit;
+                continue;
+            }
+            const double d = 0x1.0p-30 * (sc + (x1 - x0) + (y1 - y0));  // inflation
+            bool touch = false;
+            for (const Seg& s : segs)
+                if (cls::seg_meets_box(s, x0 - d, x1 + d, y0 - d, y1 + d)) { touch = true; break; }
+            if (touch) continue;
+            // location of the centre: crossing parity per ring to the +x side (the device's
+            // RayCrossingCounter direction); no segment is near the centre, so the determinant
+            // signs are far from their rounding -- checked, else mixed
+            const double px = 0.5 * x0 + 0.5 * x1, py = 0.5 * y0 + 0.5 * y1;
+            std::fill(par.begin(), par.end(), (uint8_t)0);
+            bool sure = true;
+            for (const Seg& s : segs) {
+                const double p1x = s.bx, p1y = s.by, p2x = s.ax, p2y = s.ay;  // count_segment(p, v[e+1], v[e])
+                if (p1x < px && p2x < px) continue;
+                if (!((p1y > py && p2y <= py) || (p2y > py && p1y <= py))) continue;
+                const double x1r = p1x - px, y1r = p1y - py, x2r = p2x - px, y2r = p2y - py;
+                const double tl = x1r * y2r, tr = y1r * x2r, det = tl - tr;
+                if (!(std::fabs(det) > 1e-9 * (std::fabs(tl) + std::fabs(tr)))) { sure = false; break; }
+                int sg = det > 0.0 ? 1 : -1;
+                if (y2r < y1r) sg = -sg;
+                if (sg > 0) par[s.ring] ^= 1;
+            }
+            if (!sure) continue;
+            bool inside = par[0] != 0;
+            for (uint32_t j = 1; j < nring && inside; j++) inside = par[j] == 0;
+            if (inside) {
+                out[(size_t)a * h + c] = kClsHit;
+                continue;
+            }
+            double dmin = INFINITY;
+            const double rm = r + 2.0 * m;
+            for (const Seg& s : segs) {
+                // a segment whose box is farther than r + 2m from the cell box is farther still
+                if (std::min(s.ax, s.bx) > x1 + rm || std::max(s.ax, s.bx) < x0 - rm || std::min(s.ay, s.by) > y1 + rm ||
+                    std::max(s.ay, s.by) < y0 - rm)
+                    continue;
+                dmin = std::min(dmin, cls::box_seg(x0, x1, y0, y1, s));
+            }
+            if (dmin > r + m) out[(size_t)a * h + c] = kClsMiss;
+        }
+    }
+    *off = (uint32_t)base;
+    return true;
+}
+
 // Polygon plan cache, one entry per ctx: a continuous point-polygon query evaluates the same
 // polygons on every window, so the host planning (rings, envelopes, G/C rectangles, work items,
 // slab lists: ~2 ms for 1000 polygons) and the device upload are done once; later calls compare
@@ -2919,6 +3117,7 @@ void plan_slabs(PolyDev& P, const double* ry, const ring_id_t* rid, double r, do
 struct PolyCache {
     geohip_grid grid{}, gq{};
     int jmode = 0;
+    int approx = 0;  // the cell classes and the keep filter hold for exact distances only
     double r = 0.0;
     std::vector<uint32_t> poly_rings;  // as given, or the identity when the caller passed none
     std::vector<uint32_t> ring_off;    // ring_off[R0 .. R1] (absolute vertex offsets)
@@ -2929,6 +3128,7 @@ struct PolyCache {
     std::vector<int32_t> hrects;
     std::vector<PolyWork> hwork;
     std::vector<uint16_t> hslab;
+    std::vector<uint8_t> hcls;   // per-cell classes (classify_cells), PolyDev.cls offsets into it
     std::vector<uint32_t> keep;  // cells of any polygon's G or C rectangles (empty: no filter)
     bool any_outside = false;
     void* dev_blob = nullptr;  // J_POLY buffer holding the uploaded tables
@@ -3023,7 +3223,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     // cached plan of the same inputs
     PolyCache* pc = ctx_pcache(ctx);
     bool cached = same_inputs(*pc, *grid, r, poly_rings, ring_off, npoly, vx, vy) && pc->jmode == jmode &&
-                  memcmp(&pc->gq, gq, sizeof *gq) == 0;
+                  pc->approx == (approximate ? 1 : 0) && memcmp(&pc->gq, gq, sizeof *gq) == 0;
     if (!cached) {
         PolyCache fresh;
         std::vector<PolyDev>& pd = fresh.pd;
@@ -3072,6 +3272,10 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             if (jmode == 1) { P.coff = P.goff; P.nc += P.ng; P.ng = 0; }
             if (jmode == 2) { P.ng += P.nc; P.nc = 0; }
             plan_slabs(P, pl.ry.data(), P.nring > 1 ? fresh.hvr.data() + P.voff : nullptr, r, gq->cell_len, hslab);
+            P.cls = kNoCls;
+            if (!approximate)
+                classify_cells(P, hvx, hvy, P.nring > 1 ? fresh.hvr.data() + P.voff : nullptr, *grid, hrects.data(),
+                               P.coff, P.nc, P.nring, r, fresh.hcls, &P.cls);
             if (wx0 <= wx1 && wy0 <= wy1)
                 for (int32_t a = wx0 / geo.ts; a <= wx1 / geo.ts; a++)
                     for (int32_t c = wy0 / geo.ts; c <= wy1 / geo.ts; c++)
@@ -3084,12 +3288,18 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             fresh.keep.assign(((uint64_t)nb * nb + 31) / 32, 0u);
             for (uint32_t p = 0; p < npoly; p++) {
                 const PolyDev& P = pd[p];
+                const int32_t ch = P.wy1 - P.wy0 + 1;
                 for (uint32_t q = 0; q < P.ng + P.nc; q++) {
                     const int32_t* R = &hrects[4 * ((q < P.ng ? P.goff : P.coff) + (q < P.ng ? q : q - P.ng))];
                     const int32_t a0 = std::max(R[0], 0), a1 = std::min(R[1], nb - 1);
                     const int32_t c0 = std::max(R[2], 0), c1 = std::min(R[3], nb - 1);
                     for (int32_t a = a0; a <= a1; a++)
                         for (int32_t c = c0; c <= c1; c++) {
+                            // a C cell none of whose points can be within r is not needed by P
+                            // (a cell in P's G as well is kept by the G rectangle's own pass)
+                            if (q >= P.ng && P.cls != kNoCls &&
+                                fresh.hcls[P.cls + (size_t)(a - P.wx0) * ch + (c - P.wy0)] == kClsMiss)
+                                continue;
                             const uint64_t k = (uint64_t)a * nb + c;
                             fresh.keep[k >> 5] |= 1u << (k & 31);
                         }
@@ -3099,6 +3309,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
         fresh.grid = *grid;
         fresh.gq = *gq;
         fresh.jmode = jmode;
+        fresh.approx = approximate ? 1 : 0;
         fresh.r = r;
         fresh.poly_rings.resize((size_t)npoly + 1);
         for (uint32_t p = 0; p <= npoly; p++) fresh.poly_rings[p] = ring_of(poly_rings, p);
@@ -3117,13 +3328,14 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     const std::vector<double>& henv = pc->henv;
     const bool any_outside = pc->any_outside;
     const std::vector<uint32_t>& keep = pc->keep;
+    const std::vector<uint8_t>& hcls = pc->hcls;
     Scratch S{ctx};
     const double *dx, *dy;
     rc = ctx_stage_xy(ctx, x, y, n, 0, &dx, &dy);
     if (rc) return rc;
     const auto t_planned = now();
     // polygon tables in one device blob:
-    //   PolyDev[] | vx | vy | ring envelopes | rects | work | slab lists | keep | ring ids
+    //   PolyDev[] | vx | vy | ring envelopes | rects | work | slab lists | keep | ring ids | classes
     const size_t sz_p = npoly * sizeof(PolyDev), sz_v = hvx.size() * 8, sz_r = hrects.size() * 4;
     const size_t sz_w = hwork.size() * sizeof(PolyWork), sz_s = hslab.size() * 2, sz_k = keep.size() * 4;
     const size_t sz_e = henv.size() * 8, sz_vr = hvr.size() * sizeof(ring_id_t);
@@ -3134,7 +3346,8 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     const size_t off_s = (off_w + sz_w + 15) & ~(size_t)15;
     const size_t off_k = (off_s + sz_s + 15) & ~(size_t)15;
     const size_t off_vr = (off_k + sz_k + 15) & ~(size_t)15;
-    const size_t blob_end = off_vr + sz_vr;
+    const size_t off_cl = (off_vr + sz_vr + 15) & ~(size_t)15, sz_cl = hcls.size();
+    const size_t blob_end = off_cl + sz_cl;
     void* pblob = nullptr;
     rc = ctx_ensure(ctx, J_POLY, blob_end + 64, &pblob);
     if (rc) return rc;
@@ -3149,6 +3362,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     unsigned* dkeep = sz_k ? reinterpret_cast<unsigned*>(bp + off_k) : nullptr;
     double* denv = reinterpret_cast<double*>(bp + off_e);
     ring_id_t* dvr = reinterpret_cast<ring_id_t*>(bp + off_vr);
+    uint8_t* dcls = reinterpret_cast<uint8_t*>(bp + off_cl);
     if (upload) {
         pc->dev_blob = nullptr;  // until the copies are issued
         if ((sz_p && hipMemcpyAsync(dpoly, pd.data(), sz_p, hipMemcpyHostToDevice, st) != hipSuccess) ||
@@ -3159,7 +3373,8 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             (sz_s && hipMemcpyAsync(dslab, hslab.data(), sz_s, hipMemcpyHostToDevice, st) != hipSuccess) ||
             (sz_k && hipMemcpyAsync(dkeep, keep.data(), sz_k, hipMemcpyHostToDevice, st) != hipSuccess) ||
             (sz_e && hipMemcpyAsync(denv, henv.data(), sz_e, hipMemcpyHostToDevice, st) != hipSuccess) ||
-            (sz_vr && hipMemcpyAsync(dvr, hvr.data(), sz_vr, hipMemcpyHostToDevice, st) != hipSuccess))
+            (sz_vr && hipMemcpyAsync(dvr, hvr.data(), sz_vr, hipMemcpyHostToDevice, st) != hipSuccess) ||
+            (sz_cl && hipMemcpyAsync(dcls, hcls.data(), sz_cl, hipMemcpyHostToDevice, st) != hipSuccess))
             return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "polygon upload failed");
         pc->dev_blob = pblob;
         pc->blob_bytes = blob_end;
@@ -3187,6 +3402,11 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     // hit-mask layout: words per work item, scanned; the total sizes the mask (one readback)
     uint64_t nmask = 0;
     if (nwork) {
+        if (prof) {
+            size_t nc[3] = {0, 0, 0};
+            for (uint8_t v : hcls) nc[v < 3 ? v : 0]++;
+            fprintf(stderr, "ppoly host: cell classes mixed %zu hit %zu miss %zu (region cells incl. non-C)\n", nc[0], nc[1], nc[2]);
+        }
         if (prof) fprintf(stderr, "ppoly host: plan %.1f us (cached %d), bin launch %.1f us, upload %.1f us\n",
                           std::chrono::duration<double, std::micro>(t_planned - t_start).count(), (int)cached,
                           std::chrono::duration<double, std::micro>(t_binned - t_planned).count(),
@@ -3219,9 +3439,9 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     // count pass: hit masks + per-work-item counts; out-of-grid points counted separately
     if (nwork) {
         if (approximate)
-            ppoly_eval<true><<<nwork, kTB, 0, st>>>(tb, dwork, dpoly, dvx, dvy, dvr, denv, drects, dslab, r, r_is_max, wofs, mask, bcount);
+            ppoly_eval<true><<<nwork, kTB, 0, st>>>(tb, dwork, dpoly, dvx, dvy, dvr, denv, drects, dslab, dcls, r, r_is_max, wofs, mask, bcount);
         else
-            ppoly_eval<false><<<nwork, kTB, 0, st>>>(tb, dwork, dpoly, dvx, dvy, dvr, denv, drects, dslab, r, r_is_max, wofs, mask, bcount);
+            ppoly_eval<false><<<nwork, kTB, 0, st>>>(tb, dwork, dpoly, dvx, dvy, dvr, denv, drects, dslab, dcls, r, r_is_max, wofs, mask, bcount);
     }
     if (nob && jmode == 1)
         ppoly_outside<false, true><<<nob, kTB, 0, st>>>(dx, dy, oidx, n_out, grid->min_x, grid->min_y, grid->cell_len,

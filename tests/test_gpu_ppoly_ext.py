@@ -243,3 +243,64 @@ def test_knn_ppoly_async_cached_plan(ctx):
             assert m == len(wi), (j, k)
             assert oi[:m].cpu().numpy().astype(np.uint32).tolist() == wi.tolist(), (j, k)
             assert np.array_equal(od[:m].cpu().numpy().view(np.uint64), wd.view(np.uint64)), (j, k)
+
+
+def _cell_edges(lo, l, n):
+    """Per cell boundary k in 1..n-1 of one grid axis: the first double of cell k and the last
+    double of cell k - 1 under Java's (int) Math.floor((v - min) / l) (found by bisection on the
+    ordered doubles), plus both ends of the axis."""
+    def cell(v):
+        return int(math.floor((v - lo) / l))
+
+    def first_at_least(k):
+        a, b = lo + (k - 1) * l, lo + (k + 1) * l  # cell(a) < k <= cell(b)
+        while True:
+            m = (a + b) / 2
+            if m in (a, b):
+                return b
+            if cell(m) >= k:
+                b = m
+            else:
+                a = m
+
+    out = [lo, lo + n * l, np.nextafter(lo + n * l, -np.inf)]
+    for k in range(1, n):
+        v = first_at_least(k)
+        out += [v, np.nextafter(v, -np.inf)]
+    return np.array(out)
+
+
+@pytest.mark.parametrize("holes", [False, True])
+def test_ppoly_cell_class_box_edges(ctx, holes):
+    """Per-cell classes (classify_cells) decide whole cells from their exact coordinate boxes:
+    points at every cell's extreme doubles (both sides of each boundary, both axes), cell
+    centres, NaN coordinates (cell 0) and random points, for the range query and the exact join,
+    against the oracle."""
+    n = 500
+    l = (BJ[1] - BJ[0]) / n
+    ag, cg = agrid(n)
+    if holes:
+        pr, off, vx, vy, _ = synth.holed_polygons(25, 91)
+    else:
+        pr = None
+        off, vx, vy = synth.star_polygons(40, 90)
+    ex = _cell_edges(BJ[0], l, n)
+    ey = _cell_edges(BJ[2], l, n)
+    # boundary doubles near the polygons only (the full cross product is 1M points)
+    near_x = ex[(ex > vx.min() - 0.03) & (ex < vx.max() + 0.03)]
+    near_y = ey[(ey > vy.min() - 0.03) & (ey < vy.max() + 0.03)]
+    gx, gy = np.meshgrid(near_x, near_y, indexing="ij")
+    cx = BJ[0] + (np.arange(n) + 0.5) * l
+    cy = BJ[2] + (np.arange(n) + 0.5) * l
+    hx, hy = np.meshgrid(cx, cy, indexing="ij")
+    rng = np.random.default_rng(5)
+    rx, ry = synth.uniform(200000, 93)
+    x = np.concatenate([gx.ravel(), hx.ravel(), rx, [math.nan, BJ[0], math.nan], rng.uniform(BJ[0], BJ[1], 10)])
+    y = np.concatenate([gy.ravel(), hy.ravel(), ry, [BJ[2], math.nan, math.nan], np.full(10, math.nan)])
+    for r in (0.005, 0.012, 0.0):
+        got = ctx.range_ppoly(ag, x, y, off, vx, vy, r, poly_rings=pr)
+        want = cref.range_ppoly(cg, x, y, off, vx, vy, r, poly_rings=pr)
+        assert pairs_sorted(got).tolist() == pairs_sorted(want).tolist()
+        got = ctx.join_ppoly(ag, ag, x, y, off, vx, vy, r, poly_rings=pr)
+        want = cref.join_ppoly(cg, cg, x, y, off, vx, vy, r, poly_rings=pr)
+        assert pairs_sorted(got).tolist() == pairs_sorted(want).tolist()
