@@ -264,10 +264,18 @@ class KnnWorkload(Workload):
         y = torch.empty(N, dtype=torch.float64, device=self.dev)
         self.ctx.synth_uniform_async(x, y, 0, self.seed0 + 7919 * w, synth.BEIJING)
         wi, wd = self.ctx.knn_pp(self.grid, x, y, self.q[0], self.q[1], self.radius, self.k)
-        m = int(self.mcnt.item())
-        return (m == len(wi) and self.m_i[:m].cpu().numpy().astype(np.uint32).tolist() ==
+        if self.args.partition == "cells":  # the key-band step's own merged result
+            res, (_, _, total), _ = self.cells_last
+            m_i, m_d, m = res.idx, res.dist, int(res.count)
+            if self.has_range:
+                want = self.ctx.range_pp(self.grid, x, y, self.q[0], self.q[1], self.radius)
+                if int(total) != len(want):
+                    return False
+        else:
+            m_i, m_d, m = self.m_i, self.m_d, int(self.mcnt.item())
+        return (m == len(wi) and m_i[:m].cpu().numpy().astype(np.uint32).tolist() ==
                 wi.cpu().numpy().astype(np.uint32).tolist() and
-                torch.equal(self.m_d[:m].cpu().view(torch.int64), wd.cpu().view(torch.int64)))
+                torch.equal(m_d[:m].cpu().view(torch.int64), wd.cpu().view(torch.int64)))
 
     def cells_window(self, w):
         """One window in the north-star layout: the points of this rank's shard in the query's
@@ -321,7 +329,7 @@ class KnnWorkload(Workload):
     def step(self, s):
         import torch
         if self.args.partition == "cells":
-            self.cells_window(s % self.windows)
+            self.cells_last = self.cells_window(s % self.windows)  # (merged top-k, range hits, received)
             return
         j = s & 1
         if self.world > 1 and self.ev_done[j] is not None:
@@ -580,11 +588,19 @@ class JoinWorkload(Workload):
         import torch
         w = s % self.windows
         if self.args.partition == "cells":
-            self.cells_window(w)
+            self.cells_last = self.cells_window(w)  # (this rank's pairs, offset, window total)
             return
         self.ctx.join_pp(self.grid, self.grid, self.dx[w], self.dy[w], self.qx, self.qy, self.radius, out=self.out)
         if self.world > 1:
             self.dist.all_gather_into_tensor(self.counts, torch.tensor([self.pairs[w]], device=self.dev))
+
+    def check_merged(self, last_step):
+        """N > 1, key-band step (--check): the window's pair total over the band owners against the
+        arrival-sharded join's (every rank joins its own shard in __init__).  Rank 0 only."""
+        if self.args.partition != "cells":
+            return None
+        want = sum(self._gather_ints(self.pairs[last_step % self.windows]))
+        return (int(self.cells_last[2]) == want) if self.rank == 0 else None
 
     def algorithmic_bytes(self):
         return BYTES_PER_POINT * self.n + BYTES_PER_POINT * self.nq + 8 * float(np.mean(self.pairs))
@@ -874,7 +890,10 @@ class C5Workload(KnnWorkload):
 
     def algorithmic_bytes(self):  # per step: the shard read once (16 B/pt) + the range hits written
         if self.hits is None:
-            self.hits = float(self.out_rc[0].item())
+            if self.args.partition == "cells" and getattr(self, "cells_last", None) is not None:
+                self.hits = float(self.cells_last[1][2]) / self.world  # the window's hits, per GPU
+            else:
+                self.hits = float(self.out_rc[0].item())
         return BYTES_PER_POINT * self.n + 4 * self.hits
 
     def config(self):
@@ -1062,7 +1081,7 @@ def main():
                                              "(profiles/pmc_" + wl.tag + ".json) / the live average step time"}
     if args.check and world > 1 and hasattr(wl, "check_merged"):
         ok = wl.check_merged(args.warmup + args.steps - 1)
-        if rank == 0:
+        if rank == 0 and ok is not None:
             result["merged_matches_full_window"] = ok
     if not args.no_cells_line and args.partition == "arrival":
         cells = wl.cells_partition(args.cells_steps)

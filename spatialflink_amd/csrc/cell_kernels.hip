@@ -1533,8 +1533,9 @@ constexpr int kPolyPairs = 512;     // per-wave pair buffer of the polygon kerne
 constexpr int kTileCls = 1024;      // tile cells whose classes ppoly_eval stages (ts <= 32)
 
 struct PolyWork {
-    uint32_t poly, tile;
+    uint32_t poly, tile;  // tile | kWorkAllHit: every point of the tile is a hit (no point is read)
 };
+constexpr uint32_t kWorkAllHit = 0x80000000u;
 
 struct CandQueue {
     double x[kCandQ];
@@ -1547,7 +1548,7 @@ __global__ void ppoly_words(const PolyWork* __restrict__ work, uint32_t nwork, c
                             unsigned long long* __restrict__ words) {
     const uint32_t w = blockIdx.x * kTB + threadIdx.x;
     if (w >= nwork) return;
-    const uint32_t t = work[w].tile;
+    const uint32_t t = work[w].tile & ~kWorkAllHit;
     words[w] = (tstart[t + 1] - tstart[t] + 63) / 64;
 }
 
@@ -1578,7 +1579,9 @@ __global__ __launch_bounds__(kTB) void ppoly_eval(TileBins tb, const PolyWork* _
     __shared__ unsigned long long bsh;
     const PolyWork w = work[blockIdx.x];
     const PolyDev P = polys[w.poly];
-    const unsigned ds = tb.start[w.tile], de = tb.start[w.tile + 1];
+    const uint32_t tile = w.tile & ~kWorkAllHit;
+    const bool all_hit = (w.tile & kWorkAllHit) != 0;
+    const unsigned ds = tb.start[tile], de = tb.start[tile + 1];
     const unsigned nwords = (de - ds + 63) / 64;
     const bool lds_mask = nwords <= (unsigned)kMaskWords;
     unsigned long long* gm = mask + wofs[blockIdx.x];
@@ -1598,8 +1601,8 @@ __global__ __launch_bounds__(kTB) void ppoly_eval(TileBins tb, const PolyWork* _
         for (uint32_t t = threadIdx.x; t < nwords; t += kTB) lmask[t] = 0;
     if (threadIdx.x == 0) bsh = 0;
     const int32_t ts = tb.ts;
-    const int32_t tx0 = (int32_t)(w.tile / (uint32_t)tb.nt) * ts, ty0 = (int32_t)(w.tile % (uint32_t)tb.nt) * ts;
-    const bool use_cls = !APPROX && P.cls != kNoCls && ts * ts <= kTileCls;
+    const int32_t tx0 = (int32_t)(tile / (uint32_t)tb.nt) * ts, ty0 = (int32_t)(tile % (uint32_t)tb.nt) * ts;
+    const bool use_cls = !APPROX && !all_hit && P.cls != kNoCls && ts * ts <= kTileCls;
     if (use_cls) {
         const int32_t ch = P.wy1 - P.wy0 + 1;
         for (int32_t t = threadIdx.x; t < ts * ts; t += kTB) {
@@ -1650,8 +1653,18 @@ __global__ __launch_bounds__(kTB) void ppoly_eval(TileBins tb, const PolyWork* _
             py_n = tb.sy[i];
         }
     };
-    if (ds + wid * kWave < de) fetch(ds + wid * kWave);
-    for (unsigned base = ds + wid * kWave; base < de; base += kTB) {
+    if (all_hit) {
+        // every cell of the tile is guaranteed or a whole-cell hit (the plan checked cell 0
+        // rows/columns are guaranteed, so NaN points there are hits too): whole mask words
+        for (uint32_t t = threadIdx.x; t < nwords; t += kTB) {
+            const unsigned left = de - ds - 64 * t;
+            const unsigned long long v = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
+            if (lds_mask) lmask[t] = v;
+            else gm[t] = v;
+        }
+    }
+    if (!all_hit && ds + wid * kWave < de) fetch(ds + wid * kWave);
+    for (unsigned base = ds + wid * kWave; !all_hit && base < de; base += kTB) {
         const unsigned i = base + lane;
         const unsigned key = key_n;
         const double px = px_n, py = py_n;
@@ -1715,7 +1728,8 @@ __global__ __launch_bounds__(kTB) void ppoly_emit(TileBins tb, const PolyWork* _
     __shared__ uint2 pbuf[kTB / kWave][kPolyPairs];
     __shared__ unsigned long long bsh;
     const PolyWork w = work[blockIdx.x];
-    const unsigned ds = tb.start[w.tile], de = tb.start[w.tile + 1];
+    const uint32_t tile = w.tile & ~kWorkAllHit;
+    const unsigned ds = tb.start[tile], de = tb.start[tile + 1];
     const unsigned nwords = (de - ds + 63) / 64;
     const unsigned long long* gm = mask + wofs[blockIdx.x];
     if (threadIdx.x == 0) bsh = 0;
@@ -3110,6 +3124,37 @@ bool classify_cells(const PolyDev& P, const std::vector<double>& hvx, const std:
     return true;
 }
 
+// The work item of polygon P on tile (a, c): kNoWork when no point of the tile can be a hit
+// (every cell of the tile is outside P's rectangles or a kClsMiss C cell), kWorkAllHit when
+// every point is (every cell of the tile is in a G rectangle, or a C cell of class kClsHit or
+// with r = MAX_VALUE -- but NaN coordinates land in cell 0 of their axis, so a cell of row or
+// column 0 must be guaranteed), else 0.
+constexpr uint32_t kNoWork = 0xffffffffu;
+uint32_t tile_work(const PolyDev& P, const int32_t* rects, const std::vector<uint8_t>& hcls, const TileGeom& geo,
+                   int32_t a, int32_t c, bool r_is_max) {
+    auto in_list = [&](uint32_t off, uint32_t n, int32_t cx, int32_t cy) {
+        for (uint32_t q = 0; q < n; q++) {
+            const int32_t* R = rects + 4 * (off + q);
+            if (cx >= R[0] && cx <= R[1] && cy >= R[2] && cy <= R[3]) return true;
+        }
+        return false;
+    };
+    const int32_t ch = P.wy1 - P.wy0 + 1;
+    bool any = false, all = true;
+    for (int32_t cx = a * geo.ts; cx < std::min((a + 1) * geo.ts, geo.nb); cx++)
+        for (int32_t cy = c * geo.ts; cy < std::min((c + 1) * geo.ts, geo.nb); cy++) {
+            const bool g = in_list(P.goff, P.ng, cx, cy);
+            const bool cc = !g && in_list(P.coff, P.nc, cx, cy);
+            uint8_t k = kClsMixed;
+            if (cc && P.cls != kNoCls) k = hcls[P.cls + (size_t)(cx - P.wx0) * ch + (cy - P.wy0)];
+            any = any || g || (cc && k != kClsMiss);
+            const bool hit = g || (cc && (r_is_max || k == kClsHit) && cx > 0 && cy > 0);
+            all = all && hit;
+        }
+    if (!any) return kNoWork;
+    return all ? kWorkAllHit : 0u;
+}
+
 // Polygon plan cache, one entry per ctx: a continuous point-polygon query evaluates the same
 // polygons on every window, so the host planning (rings, envelopes, G/C rectangles, work items,
 // slab lists: ~2 ms for 1000 polygons) and the device upload are done once; later calls compare
@@ -3278,8 +3323,10 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
                                P.coff, P.nc, P.nring, r, fresh.hcls, &P.cls);
             if (wx0 <= wx1 && wy0 <= wy1)
                 for (int32_t a = wx0 / geo.ts; a <= wx1 / geo.ts; a++)
-                    for (int32_t c = wy0 / geo.ts; c <= wy1 / geo.ts; c++)
-                        hwork.push_back(PolyWork{p, (uint32_t)a * (uint32_t)geo.nt + (uint32_t)c});
+                    for (int32_t c = wy0 / geo.ts; c <= wy1 / geo.ts; c++) {
+                        const uint32_t t = tile_work(P, hrects.data(), fresh.hcls, geo, a, c, r >= 1.7976931348623157e308);
+                        if (t != kNoWork) hwork.push_back(PolyWork{p, (uint32_t)a * (uint32_t)geo.nt + (uint32_t)c | t});
+                    }
         }
 
         if (fresh.hwork.size() >= 0x7fffffffull) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "too many polygon work items");
