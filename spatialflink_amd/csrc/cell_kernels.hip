@@ -570,6 +570,7 @@ struct TileBins {
     int32_t nb;
     FastDiv dnb;            // / nb (key -> cx)
     int32_t ts, nt;         // cells per tile side, tiles per side
+    double mnx, mny, l;     // the point grid (subcell edges)
 };
 
 // ------------------------------------------------------------------ pair output ----------
@@ -1175,8 +1176,20 @@ struct PolyDev {
 // Per-cell classes of a polygon's exact-evaluation cells, decided once on the host for every
 // point a cell's exact coordinate box can hold (classify_cells): kClsHit -- every such point is
 // within r of the polygon (JTS distance <= r), kClsMiss -- none is, kClsMixed -- per point.
+// One u32 per cell: 2 bits per subcell of a 4 x 4 split (subcell 4 sx + sy at bits 2 (4 sx + sy));
+// a cell decided as a whole repeats its class in all 16 fields.
 constexpr uint8_t kClsMixed = 0, kClsHit = 1, kClsMiss = 2;
 constexpr uint32_t kNoCls = 0xffffffffu;
+constexpr uint32_t kWordHit = 0x55555555u, kWordMiss = 0xAAAAAAAAu;
+// Subcell split of cell c of an axis: edge i (1..3) = mn + (c + i / 4) l, evaluated identically on
+// host and device (no contraction); a point of the cell is in subcell #{i : v >= edge i}, so each
+// subcell is an exact interval of doubles.
+__host__ __device__ __forceinline__ double sub_edge(double mn, double l, int32_t c, int i) {
+    return mn + ((double)c + 0.25 * (double)i) * l;
+}
+__host__ __device__ __forceinline__ int sub_of(double v, double mn, double l, int32_t c) {
+    return (v >= sub_edge(mn, l, c, 1) ? 1 : 0) + (v >= sub_edge(mn, l, c, 2) ? 1 : 0) + (v >= sub_edge(mn, l, c, 3) ? 1 : 0);
+}
 
 // Polygons with holes: rings are stored back to back in one vertex run, with a ring id per
 // vertex (u16, < kMaxRings); segment (v[e], v[e+1]) exists iff both ends carry the same id (the
@@ -1564,11 +1577,11 @@ __global__ __launch_bounds__(kTB) void ppoly_eval(TileBins tb, const PolyWork* _
                                                   const PolyDev* __restrict__ polys, const double* __restrict__ vx,
                                                   const double* __restrict__ vy, const ring_id_t* __restrict__ vring,
                                                   const double* __restrict__ renv, const int32_t* __restrict__ rects,
-                                                  const uint16_t* __restrict__ slabs, const uint8_t* __restrict__ pcls,
+                                                  const uint16_t* __restrict__ slabs, const uint32_t* __restrict__ pcls,
                                                   double r, int r_is_max, const unsigned long long* __restrict__ wofs,
                                                   unsigned long long* __restrict__ mask,
                                                   unsigned long long* __restrict__ bcount) {
-    __shared__ uint8_t lcls[kTileCls];  // the cell classes of this tile (P.cls)
+    __shared__ uint32_t lcls[kTileCls];  // the cell class words of this tile (P.cls)
     __shared__ double lvx[kMaxLdsVerts];
     __shared__ double lvy[kMaxLdsVerts];
     __shared__ ring_id_t lvr[kMaxLdsVerts];
@@ -1609,7 +1622,7 @@ __global__ __launch_bounds__(kTB) void ppoly_eval(TileBins tb, const PolyWork* _
             const int32_t cx = tx0 + t / ts, cy = ty0 + t % ts;
             lcls[t] = (cx >= P.wx0 && cx <= P.wx1 && cy >= P.wy0 && cy <= P.wy1)
                           ? pcls[P.cls + (uint32_t)((cx - P.wx0) * ch + (cy - P.wy0))]
-                          : kClsMixed;
+                          : 0u;
         }
     }
     __syncthreads();
@@ -1679,7 +1692,16 @@ __global__ __launch_bounds__(kTB) void ppoly_eval(TileBins tb, const PolyWork* _
             if (g || c) {
                 // a decided cell class applies to every point in the cell's coordinate box: not
                 // to NaN coordinates (cell 0 by Java's (int) NaN)
-                const uint8_t k = (use_cls && !g && px == px && py == py) ? lcls[(cx - tx0) * ts + (cy - ty0)] : kClsMixed;
+                uint32_t k = kClsMixed;
+                if (use_cls && !g && px == px && py == py) {
+                    const uint32_t wd = lcls[(cx - tx0) * ts + (cy - ty0)];
+                    if (wd == kWordHit) k = kClsHit;
+                    else if (wd == kWordMiss) k = kClsMiss;
+                    else if (wd != 0u) {
+                        const int sx = sub_of(px, tb.mnx, tb.l, cx), sy = sub_of(py, tb.mny, tb.l, cy);
+                        k = (wd >> (2 * (4 * sx + sy))) & 3u;
+                    }
+                }
                 if (g || r_is_max || k == kClsHit) hit = true;
                 else if (APPROX) hit = bbox_distance(px, py, P.bb) <= r;
                 else if (k != kClsMiss)
@@ -2728,6 +2750,9 @@ int bin_tiles(geohip_ctx* ctx, Scratch& S, const double* dx, const double* dy, u
     tb->dnb = geo.dnb;
     tb->ts = geo.ts;
     tb->nt = geo.nt;
+    tb->mnx = geo.mnx;
+    tb->mny = geo.mny;
+    tb->l = geo.l;
     return GEOHIP_OK;
 }
 
@@ -3005,8 +3030,8 @@ inline double box_seg(double x0, double x1, double y0, double y1, const Seg& s) 
 }  // namespace cls
 
 // Classes of the cells of P's walk region that the device evaluates exactly (C cells; the join's
-// G u C in exact mode).  For a cell's exact coordinate box B (plan.cpp axis bounds: every
-// non-NaN point of the cell lies in B):
+// G u C in exact mode).  For a box B of doubles (a cell's exact coordinate box from plan.cpp's
+// axis bounds -- every non-NaN point of the cell lies in it -- or a subcell's):
 //  * HIT when one segment s has all four corners of B within r - m of it (distance to a segment
 //    is convex, so every p in B is within r - m of s and the JTS distance, 0 inside or the
 //    minimum over segments outside, is <= r), or when no segment meets B and B's centre is
@@ -3016,26 +3041,82 @@ inline double box_seg(double x0, double x1, double y0, double y1, const Seg& s) 
 //    farther than r + m from B;
 //  * MIXED otherwise.  m = 2^-36 (scale + r) covers JTS's rounding (<= 2^-49 of the magnitudes,
 //    segment_within) and this code's own.
+// A cell that stays MIXED is split into 4 x 4 subcells (sub_edge) classified the same way.
+struct BoxClassifier {
+    std::vector<cls::Seg> segs;
+    double scale = 0.0, r = 0.0;
+    uint32_t nring = 1;
+    std::vector<uint8_t> par;
+    uint8_t operator()(double x0, double x1, double y0, double y1) {
+        using cls::Seg;
+        if (!(x0 <= x1) || !(y0 <= y1)) return kClsMiss;  // an empty box holds no point
+        const double sc = std::max(scale, std::max(std::max(std::fabs(x0), std::fabs(x1)), std::max(std::fabs(y0), std::fabs(y1))));
+        const double m = 0x1.0p-36 * (sc + r);
+        for (const Seg& s : segs) {
+            // (only a segment whose box, grown by r, holds B can cover it)
+            if (std::min(s.ax, s.bx) - r > x0 || std::max(s.ax, s.bx) + r < x1 || std::min(s.ay, s.by) - r > y0 ||
+                std::max(s.ay, s.by) + r < y1)
+                continue;
+            if (std::max(std::max(cls::pt_seg(x0, y0, s), cls::pt_seg(x0, y1, s)),
+                         std::max(cls::pt_seg(x1, y0, s), cls::pt_seg(x1, y1, s))) <= r - m)
+                return kClsHit;
+        }
+        const double d = 0x1.0p-30 * (sc + (x1 - x0) + (y1 - y0));  // inflation
+        for (const Seg& s : segs)
+            if (cls::seg_meets_box(s, x0 - d, x1 + d, y0 - d, y1 + d)) return kClsMixed;
+        // location of the centre: crossing parity per ring to the +x side (the device's
+        // RayCrossingCounter direction); no segment is near the centre, so the determinant signs
+        // are far from their rounding -- checked, else mixed
+        const double px = 0.5 * x0 + 0.5 * x1, py = 0.5 * y0 + 0.5 * y1;
+        std::fill(par.begin(), par.end(), (uint8_t)0);
+        for (const Seg& s : segs) {
+            const double p1x = s.bx, p1y = s.by, p2x = s.ax, p2y = s.ay;  // count_segment(p, v[e+1], v[e])
+            if (p1x < px && p2x < px) continue;
+            if (!((p1y > py && p2y <= py) || (p2y > py && p1y <= py))) continue;
+            const double x1r = p1x - px, y1r = p1y - py, x2r = p2x - px, y2r = p2y - py;
+            const double tl = x1r * y2r, tr = y1r * x2r, det = tl - tr;
+            if (!(std::fabs(det) > 1e-9 * (std::fabs(tl) + std::fabs(tr)))) return kClsMixed;
+            int sg = det > 0.0 ? 1 : -1;
+            if (y2r < y1r) sg = -sg;
+            if (sg > 0) par[s.ring] ^= 1;
+        }
+        bool inside = par[0] != 0;
+        for (uint32_t j = 1; j < nring && inside; j++) inside = par[j] == 0;
+        if (inside) return kClsHit;
+        const double rm = r + 2.0 * m;
+        double dmin = INFINITY;
+        for (const Seg& s : segs) {
+            // a segment whose box is farther than r + 2m from B is farther still
+            if (std::min(s.ax, s.bx) > x1 + rm || std::max(s.ax, s.bx) < x0 - rm || std::min(s.ay, s.by) > y1 + rm ||
+                std::max(s.ay, s.by) < y0 - rm)
+                continue;
+            dmin = std::min(dmin, cls::box_seg(x0, x1, y0, y1, s));
+        }
+        return dmin > r + m ? kClsMiss : kClsMixed;
+    }
+};
+
 // Returns false (no classes) for r < 0 / NaN / inf, non-finite vertices or too large a region.
 bool classify_cells(const PolyDev& P, const std::vector<double>& hvx, const std::vector<double>& hvy,
                     const ring_id_t* rid, const geohip_grid& pg, const int32_t* rects, uint32_t first_c,
-                    uint32_t nrect_c, uint32_t nring, double r, std::vector<uint8_t>& blob, uint32_t* off) {
-    using cls::Seg;
+                    uint32_t nrect_c, uint32_t nring, double r, std::vector<uint32_t>& blob, uint32_t* off) {
     *off = kNoCls;
     if (!(r >= 0.0) || !std::isfinite(r) || P.wx0 > P.wx1 || P.wy0 > P.wy1 || nrect_c == 0) return false;
-    const uint32_t nv = P.nv;
-    std::vector<Seg> segs;
-    double scale = std::fabs(r);
-    for (uint32_t i = 0; i + 1 < nv; i++) {
+    BoxClassifier bc;
+    bc.r = r;
+    bc.scale = std::fabs(r);
+    bc.nring = nring;
+    bc.par.assign(nring, 0);
+    for (uint32_t i = 0; i + 1 < P.nv; i++) {
         const double ax = hvx[P.voff + i], ay = hvy[P.voff + i], bx = hvx[P.voff + i + 1], by = hvy[P.voff + i + 1];
         if (!std::isfinite(ax) || !std::isfinite(ay) || !std::isfinite(bx) || !std::isfinite(by)) return false;
-        scale = std::max(scale, std::max(std::max(std::fabs(ax), std::fabs(ay)), std::max(std::fabs(bx), std::fabs(by))));
+        bc.scale = std::max(bc.scale, std::max(std::max(std::fabs(ax), std::fabs(ay)), std::max(std::fabs(bx), std::fabs(by))));
         if (rid && rid[i] != rid[i + 1]) continue;  // ring junction: no segment
-        segs.push_back(Seg{ax, ay, bx, by, rid ? (uint32_t)rid[i] : 0u});
+        bc.segs.push_back(cls::Seg{ax, ay, bx, by, rid ? (uint32_t)rid[i] : 0u});
     }
-    if (segs.empty()) return false;
+    if (bc.segs.empty()) return false;
     const int32_t w = P.wx1 - P.wx0 + 1, h = P.wy1 - P.wy0 + 1;
-    if ((uint64_t)w * (uint64_t)h * segs.size() > 8000000ull) return false;
+    if ((uint64_t)w * (uint64_t)h * bc.segs.size() > 8000000ull) return false;
     std::vector<double> xl(w), xh(w), yl(h), yh(h);
     std::vector<uint8_t> okx(w), oky(h);
     for (int32_t a = 0; a < w; a++)
@@ -3044,10 +3125,14 @@ bool classify_cells(const PolyDev& P, const std::vector<double>& hvx, const std:
     for (int32_t c = 0; c < h; c++)
         oky[c] = axis_lower(pg.min_y, pg.cell_len, P.wy0 + c, &yl[c]) && axis_upper(pg.min_y, pg.cell_len, P.wy0 + c, &yh[c]) &&
                  std::isfinite(yl[c]) && std::isfinite(yh[c]) && yl[c] <= yh[c];
-    std::vector<uint8_t> par(nring, 0);
     const size_t base = blob.size();
-    blob.resize(base + (size_t)w * h, kClsMixed);
-    uint8_t* out = blob.data() + base;
+    blob.resize(base + (size_t)w * h, 0u);  // all mixed
+    uint32_t* out = blob.data() + base;
+    // subcell i of an axis: the doubles v of the cell box [bl, bh] with sub_of(v) == i
+    auto sub_iv = [](double mn, double l, int32_t c, double bl, double bh, int i, double& lo, double& hi) {
+        lo = i == 0 ? bl : std::max(bl, sub_edge(mn, l, c, i));
+        hi = i == 3 ? bh : std::min(bh, std::nextafter(sub_edge(mn, l, c, i + 1), -INFINITY));
+    };
     for (int32_t a = 0; a < w; a++) {
         if (!okx[a]) continue;
         for (int32_t c = 0; c < h; c++) {
@@ -3059,65 +3144,20 @@ bool classify_cells(const PolyDev& P, const std::vector<double>& hvx, const std:
                 in_c = cx >= R[0] && cx <= R[1] && cy >= R[2] && cy <= R[3];
             }
             if (!in_c) continue;
-            const double x0 = xl[a], x1 = xh[a], y0 = yl[c], y1 = yh[c];
-            const double sc = std::max(scale, std::max(std::max(std::fabs(x0), std::fabs(x1)), std::max(std::fabs(y0), std::fabs(y1))));
-            const double m = 0x1.0p-36 * (sc + r);
-            // one segment covering the whole box
-            bool hit = false;
-            for (const Seg& s : segs) {
-                // (only a segment whose box, grown by r, holds the cell box can cover it)
-                if (std::min(s.ax, s.bx) - r > x0 || std::max(s.ax, s.bx) + r < x1 || std::min(s.ay, s.by) - r > y0 ||
-                    std::max(s.ay, s.by) + r < y1)
-                    continue;
-                if (std::max(std::max(cls::pt_seg(x0, y0, s), cls::pt_seg(x0, y1, s)),
-                             std::max(cls::pt_seg(x1, y0, s), cls::pt_seg(x1, y1, s))) <= r - m) {
-                    hit = true;
-                    break;
+            const uint8_t k = bc(xl[a], xh[a], yl[c], yh[c]);
+            if (k == kClsHit) { out[(size_t)a * h + c] = kWordHit; continue; }
+            if (k == kClsMiss) { out[(size_t)a * h + c] = kWordMiss; continue; }
+            uint32_t word = 0;
+            for (int sx = 0; sx < 4; sx++) {
+                double sx0, sx1;
+                sub_iv(pg.min_x, pg.cell_len, cx, xl[a], xh[a], sx, sx0, sx1);
+                for (int sy = 0; sy < 4; sy++) {
+                    double sy0, sy1;
+                    sub_iv(pg.min_y, pg.cell_len, cy, yl[c], yh[c], sy, sy0, sy1);
+                    word |= (uint32_t)bc(sx0, sx1, sy0, sy1) << (2 * (4 * sx + sy));
                 }
             }
-            if (hit) {
-                out[(size_t)a * h + c] = kClsHit;
-                continue;
-            }
-            const double d = 0x1.0p-30 * (sc + (x1 - x0) + (y1 - y0));  // inflation
-            bool touch = false;
-            for (const Seg& s : segs)
-                if (cls::seg_meets_box(s, x0 - d, x1 + d, y0 - d, y1 + d)) { touch = true; break; }
-            if (touch) continue;
-            // location of the centre: crossing parity per ring to the +x side (the device's
-            // RayCrossingCounter direction); no segment is near the centre, so the determinant
-            // signs are far from their rounding -- checked, else mixed
-            const double px = 0.5 * x0 + 0.5 * x1, py = 0.5 * y0 + 0.5 * y1;
-            std::fill(par.begin(), par.end(), (uint8_t)0);
-            bool sure = true;
-            for (const Seg& s : segs) {
-                const double p1x = s.bx, p1y = s.by, p2x = s.ax, p2y = s.ay;  // count_segment(p, v[e+1], v[e])
-                if (p1x < px && p2x < px) continue;
-                if (!((p1y > py && p2y <= py) || (p2y > py && p1y <= py))) continue;
-                const double x1r = p1x - px, y1r = p1y - py, x2r = p2x - px, y2r = p2y - py;
-                const double tl = x1r * y2r, tr = y1r * x2r, det = tl - tr;
-                if (!(std::fabs(det) > 1e-9 * (std::fabs(tl) + std::fabs(tr)))) { sure = false; break; }
-                int sg = det > 0.0 ? 1 : -1;
-                if (y2r < y1r) sg = -sg;
-                if (sg > 0) par[s.ring] ^= 1;
-            }
-            if (!sure) continue;
-            bool inside = par[0] != 0;
-            for (uint32_t j = 1; j < nring && inside; j++) inside = par[j] == 0;
-            if (inside) {
-                out[(size_t)a * h + c] = kClsHit;
-                continue;
-            }
-            double dmin = INFINITY;
-            const double rm = r + 2.0 * m;
-            for (const Seg& s : segs) {
-                // a segment whose box is farther than r + 2m from the cell box is farther still
-                if (std::min(s.ax, s.bx) > x1 + rm || std::max(s.ax, s.bx) < x0 - rm || std::min(s.ay, s.by) > y1 + rm ||
-                    std::max(s.ay, s.by) < y0 - rm)
-                    continue;
-                dmin = std::min(dmin, cls::box_seg(x0, x1, y0, y1, s));
-            }
-            if (dmin > r + m) out[(size_t)a * h + c] = kClsMiss;
+            out[(size_t)a * h + c] = word;
         }
     }
     *off = (uint32_t)base;
@@ -3130,7 +3170,7 @@ bool classify_cells(const PolyDev& P, const std::vector<double>& hvx, const std:
 // with r = MAX_VALUE -- but NaN coordinates land in cell 0 of their axis, so a cell of row or
 // column 0 must be guaranteed), else 0.
 constexpr uint32_t kNoWork = 0xffffffffu;
-uint32_t tile_work(const PolyDev& P, const int32_t* rects, const std::vector<uint8_t>& hcls, const TileGeom& geo,
+uint32_t tile_work(const PolyDev& P, const int32_t* rects, const std::vector<uint32_t>& hcls, const TileGeom& geo,
                    int32_t a, int32_t c, bool r_is_max) {
     auto in_list = [&](uint32_t off, uint32_t n, int32_t cx, int32_t cy) {
         for (uint32_t q = 0; q < n; q++) {
@@ -3145,10 +3185,10 @@ uint32_t tile_work(const PolyDev& P, const int32_t* rects, const std::vector<uin
         for (int32_t cy = c * geo.ts; cy < std::min((c + 1) * geo.ts, geo.nb); cy++) {
             const bool g = in_list(P.goff, P.ng, cx, cy);
             const bool cc = !g && in_list(P.coff, P.nc, cx, cy);
-            uint8_t k = kClsMixed;
+            uint32_t k = 0;
             if (cc && P.cls != kNoCls) k = hcls[P.cls + (size_t)(cx - P.wx0) * ch + (cy - P.wy0)];
-            any = any || g || (cc && k != kClsMiss);
-            const bool hit = g || (cc && (r_is_max || k == kClsHit) && cx > 0 && cy > 0);
+            any = any || g || (cc && k != kWordMiss);
+            const bool hit = g || (cc && (r_is_max || k == kWordHit) && cx > 0 && cy > 0);
             all = all && hit;
         }
     if (!any) return kNoWork;
@@ -3173,7 +3213,7 @@ struct PolyCache {
     std::vector<int32_t> hrects;
     std::vector<PolyWork> hwork;
     std::vector<uint16_t> hslab;
-    std::vector<uint8_t> hcls;   // per-cell classes (classify_cells), PolyDev.cls offsets into it
+    std::vector<uint32_t> hcls;  // per-cell class words (classify_cells), PolyDev.cls offsets into it
     std::vector<uint32_t> keep;  // cells of any polygon's G or C rectangles (empty: no filter)
     bool any_outside = false;
     void* dev_blob = nullptr;  // J_POLY buffer holding the uploaded tables
@@ -3345,7 +3385,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
                             // a C cell none of whose points can be within r is not needed by P
                             // (a cell in P's G as well is kept by the G rectangle's own pass)
                             if (q >= P.ng && P.cls != kNoCls &&
-                                fresh.hcls[P.cls + (size_t)(a - P.wx0) * ch + (c - P.wy0)] == kClsMiss)
+                                fresh.hcls[P.cls + (size_t)(a - P.wx0) * ch + (c - P.wy0)] == kWordMiss)
                                 continue;
                             const uint64_t k = (uint64_t)a * nb + c;
                             fresh.keep[k >> 5] |= 1u << (k & 31);
@@ -3375,7 +3415,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     const std::vector<double>& henv = pc->henv;
     const bool any_outside = pc->any_outside;
     const std::vector<uint32_t>& keep = pc->keep;
-    const std::vector<uint8_t>& hcls = pc->hcls;
+    const std::vector<uint32_t>& hcls = pc->hcls;
     Scratch S{ctx};
     const double *dx, *dy;
     rc = ctx_stage_xy(ctx, x, y, n, 0, &dx, &dy);
@@ -3393,7 +3433,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     const size_t off_s = (off_w + sz_w + 15) & ~(size_t)15;
     const size_t off_k = (off_s + sz_s + 15) & ~(size_t)15;
     const size_t off_vr = (off_k + sz_k + 15) & ~(size_t)15;
-    const size_t off_cl = (off_vr + sz_vr + 15) & ~(size_t)15, sz_cl = hcls.size();
+    const size_t off_cl = (off_vr + sz_vr + 15) & ~(size_t)15, sz_cl = hcls.size() * 4;
     const size_t blob_end = off_cl + sz_cl;
     void* pblob = nullptr;
     rc = ctx_ensure(ctx, J_POLY, blob_end + 64, &pblob);
@@ -3409,7 +3449,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     unsigned* dkeep = sz_k ? reinterpret_cast<unsigned*>(bp + off_k) : nullptr;
     double* denv = reinterpret_cast<double*>(bp + off_e);
     ring_id_t* dvr = reinterpret_cast<ring_id_t*>(bp + off_vr);
-    uint8_t* dcls = reinterpret_cast<uint8_t*>(bp + off_cl);
+    uint32_t* dcls = reinterpret_cast<uint32_t*>(bp + off_cl);
     if (upload) {
         pc->dev_blob = nullptr;  // until the copies are issued
         if ((sz_p && hipMemcpyAsync(dpoly, pd.data(), sz_p, hipMemcpyHostToDevice, st) != hipSuccess) ||
@@ -3451,7 +3491,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     if (nwork) {
         if (prof) {
             size_t nc[3] = {0, 0, 0};
-            for (uint8_t v : hcls) nc[v < 3 ? v : 0]++;
+            for (uint32_t v : hcls) nc[v == kWordHit ? 1 : v == kWordMiss ? 2 : 0]++;
             fprintf(stderr, "ppoly host: cell classes mixed %zu hit %zu miss %zu (region cells incl. non-C)\n", nc[0], nc[1], nc[2]);
         }
         if (prof) fprintf(stderr, "ppoly host: plan %.1f us (cached %d), bin launch %.1f us, upload %.1f us\n",

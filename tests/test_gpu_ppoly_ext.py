@@ -267,15 +267,19 @@ def _cell_edges(lo, l, n):
     for k in range(1, n):
         v = first_at_least(k)
         out += [v, np.nextafter(v, -np.inf)]
+    for k in range(n):  # the device's 4 x 4 subcell edges (sub_edge: min + (c + i / 4) * l)
+        for i in (1, 2, 3):
+            v = lo + (k + 0.25 * i) * l
+            out += [v, np.nextafter(v, -np.inf)]
     return np.array(out)
 
 
 @pytest.mark.parametrize("holes", [False, True])
 def test_ppoly_cell_class_box_edges(ctx, holes):
-    """Per-cell classes (classify_cells) decide whole cells from their exact coordinate boxes:
-    points at every cell's extreme doubles (both sides of each boundary, both axes), cell
-    centres, NaN coordinates (cell 0) and random points, for the range query and the exact join,
-    against the oracle."""
+    """Per-cell classes (classify_cells) decide whole cells and 4 x 4 subcells from their exact
+    coordinate boxes: points at every cell's and subcell's extreme doubles (both sides of each
+    boundary, both axes), cell centres, NaN coordinates (cell 0) and random points, for the range
+    query and the exact join, against the oracle."""
     n = 500
     l = (BJ[1] - BJ[0]) / n
     ag, cg = agrid(n)
@@ -286,10 +290,16 @@ def test_ppoly_cell_class_box_edges(ctx, holes):
         off, vx, vy = synth.star_polygons(40, 90)
     ex = _cell_edges(BJ[0], l, n)
     ey = _cell_edges(BJ[2], l, n)
-    # boundary doubles near the polygons only (the full cross product is 1M points)
-    near_x = ex[(ex > vx.min() - 0.03) & (ex < vx.max() + 0.03)]
-    near_y = ey[(ey > vy.min() - 0.03) & (ey < vy.max() + 0.03)]
-    gx, gy = np.meshgrid(near_x, near_y, indexing="ij")
+    # boundary doubles around each polygon (within r_max of its box): their cross product
+    px, py = [], []
+    for p in range(len(off) - 1 if pr is None else len(pr) - 1):
+        a, b = (int(off[p]), int(off[p + 1])) if pr is None else (int(off[pr[p]]), int(off[pr[p + 1]]))
+        sx = ex[(ex > vx[a:b].min() - 0.013) & (ex < vx[a:b].max() + 0.013)]
+        sy = ey[(ey > vy[a:b].min() - 0.013) & (ey < vy[a:b].max() + 0.013)]
+        gx, gy = np.meshgrid(sx, sy, indexing="ij")
+        px.append(gx.ravel())
+        py.append(gy.ravel())
+    gx, gy = np.concatenate(px), np.concatenate(py)
     cx = BJ[0] + (np.arange(n) + 0.5) * l
     cy = BJ[2] + (np.arange(n) + 0.5) * l
     hx, hy = np.meshgrid(cx, cy, indexing="ij")
