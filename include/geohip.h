@@ -177,6 +177,14 @@ int geohip_knn_ppoly(geohip_ctx* ctx, const geohip_grid* grid, const double* x, 
                      uint64_t n, const uint32_t* ring_off, uint32_t nring, const double* vx,
                      const double* vy, double r, uint32_t k, int approximate,
                      uint32_t* out_idx, double* out_dist, uint32_t* out_count);
+/* Enqueue-only form of geohip_knn_ppoly (GEOHIP_MEM_DEVICE window and outputs; the polygon stays
+   host memory and is planned once per ctx): k (dist, idx) ascending, entries past the candidate
+   count are (+inf-bits sentinel, 0xffffffff); *out_count_dev = number of valid entries.  No host
+   round trip: the selection path is chosen from the previous call's candidate count. */
+int geohip_knn_ppoly_async(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
+                           uint64_t n, const uint32_t* ring_off, uint32_t nring, const double* vx,
+                           const double* vy, double r, uint32_t k, int approximate,
+                           uint32_t* out_idx, double* out_dist, uint32_t* out_count_dev);
 
 /* ---- device-resident pipeline forms (GEOHIP_MEM_DEVICE pointers; enqueue only) -------- */
 /* Writes k (dist, idx) ascending to out_dist/out_idx (device), entries past the candidate
