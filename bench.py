@@ -928,7 +928,7 @@ class IngestWorkload(Workload):
     (Point.java:91-100 -> HelperClass.java:104-116) on the device; the C2 window size (10M records)
     and grid (100x100).  Text is device-resident before the timed region."""
     tag = "ingest"
-    kernel = "geohip ingest: ingest_count + chunk scan + ingest_parse (one batch)"
+    kernel = "geohip ingest: ingest_fused (one launch per batch: chunk ticket, record split, look-back record base, parse)"
     grid_n, n_default = 100, 10_000_000
     windows = 1  # one batch of ~570 MB is > the 256 MiB Infinity Cache
 

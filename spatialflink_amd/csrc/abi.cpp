@@ -105,6 +105,7 @@ struct geohip_ctx {
     double plan_q[3] = {0, 0, 0};
     PointPlan plan{};
     unsigned long long range_epoch = 0;  // fused range pass: status words of this launch carry it
+    unsigned long long ingest_epoch = 0; // ingest look-back: status words of this launch carry it
     // host windows (GEOHIP_MEM_HOST): two pinned staging slots; the DMA of one slot runs on the
     // copy stream while the host fills the other (host_stage)
     hipStream_t cstream = nullptr;
@@ -1110,6 +1111,15 @@ int ctx_ensure_ingest(geohip_ctx* ctx, int slot, size_t bytes, void** out) {
     int rc = ensure(ctx, (Slot)(S_I0 + slot), bytes);
     if (!rc) *out = ctx->buf[S_I0 + slot];
     return rc;
+}
+int ctx_ensure_ingest_zeroed(geohip_ctx* ctx, int slot, size_t bytes, void** out) {
+    int rc = ensure_zeroed(ctx, (Slot)(S_I0 + slot), bytes);
+    if (!rc) *out = ctx->buf[S_I0 + slot];
+    return rc;
+}
+unsigned long long ctx_next_ingest_epoch(geohip_ctx* ctx) {
+    ctx->ingest_epoch = ctx->ingest_epoch % ((1ull << 22) - 1) + 1;
+    return ctx->ingest_epoch;
 }
 int ctx_begin(geohip_ctx* ctx) { return begin(ctx); }
 hipStream_t ctx_stream(geohip_ctx* ctx) { return ctx->stream; }

@@ -12,9 +12,10 @@
 namespace geohip {
 
 // Bytes of text owned by one block (its records are those whose preceding '\n' lies in the
-// chunk), and the LDS bytes staged past the chunk for records that straddle its end.
+// chunk), and the LDS bytes staged past the chunk for the record that straddles its end (a
+// longer record reads its remaining bytes from global memory through the general parser).
 constexpr uint32_t kIngestChunk = 16384;
-constexpr uint32_t kIngestTail = 4096;
+constexpr uint32_t kIngestTail = 512;
 
 struct IngestArgs {
     ingest::Spec spec;
@@ -25,12 +26,24 @@ struct IngestArgs {
 
 inline uint64_t ingest_chunks(uint64_t nbytes) { return (nbytes + kIngestChunk - 1) / kIngestChunk; }
 
-// Pass 1: records per chunk (chunk_cnt[nchunks]); pass 2: exclusive scan into chunk_base and
-// the record total (*total); pass 3: per-block record split + parse.  bad[0] = first rejected
-// record index (UINT64_MAX if none; must hold UINT64_MAX before the launch).
-hipError_t launch_ingest(const uint8_t* text, uint64_t nbytes, const IngestArgs& a, unsigned* chunk_cnt,
-                         unsigned long long* chunk_base, unsigned long long* total, double* x, double* y,
-                         int64_t* ts, uint32_t* cell, uint64_t cap, unsigned long long* bad, hipStream_t st,
-                         hipEvent_t ev0, hipEvent_t ev1);
+// Chunk-order look-back state: status[nchunks] words (any content before the first launch),
+// a ticket word (zero before the first launch; the last chunk re-arms it), the launch's epoch
+// (1 .. 2^22 - 1, new per launch); the chunks left to the general grammar: listed[nchunks]
+// (chunk, record base) and their count *nlisted (zero before the launch).
+struct IngestLookback {
+    unsigned long long* status;
+    unsigned* ticket;
+    unsigned long long epoch;
+    ulonglong2* listed;
+    unsigned* nlisted;
+};
+
+// Two launches: ingest_fused (per chunk record split + look-back record base + CSV fast-path
+// parse; *total = records in the batch) and ingest_general (the full grammar over the chunks the
+// first left undecided).  bad[0] = ~(first rejected record index), 0 if none (must hold 0
+// before the launch).
+hipError_t launch_ingest(const uint8_t* text, uint64_t nbytes, const IngestArgs& a, const IngestLookback& lb,
+                         unsigned long long* total, double* x, double* y, int64_t* ts, uint32_t* cell, uint64_t cap,
+                         unsigned long long* bad, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
 
 }  // namespace geohip

@@ -7,15 +7,15 @@
 // WKTToSpatial :223-228) and the cell assignment of the Point constructor
 // (spatialObjects/Point.java:60-66 -> utils/HelperClass.java:104-116).
 //
-// Three launches per batch, all HBM-streaming:
-//   ingest_count  every block counts the record starts its 16 KB chunk owns (SWAR '\n' test on
-//                 16-byte loads);
-//   ingest_scan   one block turns the per-chunk counts into record bases (the record index of
-//                 a record is its position in the batch, as in the arrival-ordered stream);
-//   ingest_parse  every block stages its chunk (+ a 4 KB tail for straddling records) in LDS
-//                 with 16-byte loads, lists its record starts in order (block scan), and parses
-//                 one record per lane with the ingest_parse.h functions (Eisel-Lemire fp64),
-//                 writing x/y/ts/cell coalesced by record index.
+// One launch per batch (ingest_fused), HBM-streaming: every block takes the next 16 KB chunk by
+// an arrival ticket, stages it (+ a 512-byte tail for the record straddling its end) in LDS with
+// 16-byte loads, lists the record starts it owns in order (SWAR '\n' test + block scan),
+// publishes its record count and finds its first record's index by a decoupled look-back over
+// the earlier chunks' published counts (the record index of a record is its position in the
+// batch, as in the arrival-ordered stream), then parses one record per lane with the
+// ingest_parse.h functions (Eisel-Lemire fp64) and writes x/y/ts/cell coalesced by record index.
+// The text is read once (+3 % for the tails); the count pass and scan launch of the earlier
+// three-launch form, which read the text twice, are gone.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -26,6 +26,7 @@ namespace geohip {
 namespace {
 
 constexpr int kThreads = (int)(kIngestChunk / 32);  // 512: 32 bytes per thread
+constexpr unsigned kGeneralBlocks = 256;               // ingest_general's grid (strides over its list)
 constexpr uint32_t kBytesPerThread = kIngestChunk / kThreads;  // 32: two 16-byte loads
 static_assert(kBytesPerThread == 32, "chunk layout");
 
@@ -78,64 +79,6 @@ __device__ __forceinline__ unsigned block_excl_scan(unsigned v, unsigned* s_wave
     }
     *total = sum;
     return base + incl - v;
-}
-
-__global__ __launch_bounds__(kThreads) void ingest_count(const uint8_t* __restrict__ text, uint64_t nbytes,
-                                                        unsigned* __restrict__ chunk_cnt) {
-    __shared__ unsigned s_wave[kThreads / kWave];
-    const uint64_t p = (uint64_t)blockIdx.x * kIngestChunk + threadIdx.x * kBytesPerThread;
-    unsigned c = 0;
-    if (p < nbytes) {
-        const uint4 a = load16(text, p, nbytes), b = load16(text, p + 16, nbytes);
-        c = __builtin_popcount(nl_mask32(a, b, p, nbytes - 1));  // a '\n' at nbytes-1 starts nothing
-    }
-    unsigned total;
-    block_excl_scan(c, s_wave, &total);
-    if (threadIdx.x == 0) chunk_cnt[blockIdx.x] = total + (blockIdx.x == 0 ? 1u : 0u);  // record 0 at byte 0
-}
-
-__global__ __launch_bounds__(1024) void ingest_scan(const unsigned* __restrict__ cnt, uint64_t nchunks,
-                                                    unsigned long long* __restrict__ base,
-                                                    unsigned long long* __restrict__ total) {
-    __shared__ unsigned long long s_part[1024];
-    const uint64_t per = (nchunks + 1023) / 1024;
-    const uint64_t b0 = threadIdx.x * per, b1 = b0 + per < nchunks ? b0 + per : nchunks;
-    // 8 independent loads in flight per thread (the serial sum paid one memory latency per count)
-    unsigned long long s = 0;
-    uint64_t b = b0;
-    for (; b + 8 <= b1; b += 8) {
-        unsigned v[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) v[u] = cnt[b + u];
-#pragma unroll
-        for (int u = 0; u < 8; u++) s += v[u];
-    }
-    for (; b < b1; b++) s += cnt[b];
-    s_part[threadIdx.x] = s;
-    __syncthreads();
-    // Hillis-Steele over 1024 partial sums (one launch per batch: not on the critical path)
-    for (int off = 1; off < 1024; off <<= 1) {
-        const unsigned long long v = threadIdx.x >= (unsigned)off ? s_part[threadIdx.x - off] : 0ull;
-        __syncthreads();
-        s_part[threadIdx.x] += v;
-        __syncthreads();
-    }
-    unsigned long long run = s_part[threadIdx.x] - s;
-    for (b = b0; b + 8 <= b1; b += 8) {
-        unsigned v[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) v[u] = cnt[b + u];
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            base[b + u] = run;
-            run += v[u];
-        }
-    }
-    for (; b < b1; b++) {
-        base[b] = run;
-        run += cnt[b];
-    }
-    if (threadIdx.x == 1023) *total = s_part[1023];
 }
 
 // byte reader for the parsers: the staged LDS window first, global memory past it, and '\n'
@@ -359,90 +302,216 @@ __device__ __forceinline__ int swar_csv(const uint8_t* __restrict__ s, uint32_t 
     return kSwarNo;
 }
 
-__global__ __launch_bounds__(kThreads) void ingest_parse(const uint8_t* __restrict__ text, uint64_t nbytes,
-                                                        IngestArgs a, const unsigned long long* __restrict__ chunk_base,
-                                                        double* __restrict__ x, double* __restrict__ y,
-                                                        int64_t* __restrict__ ts, uint32_t* __restrict__ cell,
-                                                        uint64_t cap, unsigned long long* __restrict__ bad) {
-    __shared__ uint4 s_text4[(kIngestChunk + kIngestTail) / 16];
-    __shared__ uint16_t s_start[kIngestChunk + 1];
-    __shared__ unsigned s_wave[kThreads / kWave];
-    const uint64_t c0 = (uint64_t)blockIdx.x * kIngestChunk;
-    const uint64_t stage_end = c0 + kIngestChunk + kIngestTail < nbytes ? c0 + kIngestChunk + kIngestTail : nbytes;
-    const uint32_t stage_len = (uint32_t)(stage_end - c0);
-    // stage: the chunk first (this thread's 32 bytes stay in registers for the '\n' scan)
+// Decoupled look-back status word of a chunk: (epoch << 42) | kPrefixBit? | value, value = the
+// chunk's record count (aggregate) or, with kPrefixBit, the records of every chunk up to and
+// including it (inclusive prefix).  Words of an earlier launch carry another epoch: not ready.
+constexpr unsigned long long kPrefixBit = 1ull << 41;
+constexpr unsigned long long kValueMask = kPrefixBit - 1;
+
+__device__ __forceinline__ void publish_status(unsigned long long* w, unsigned long long v) {
+    // an atomic exchange is performed at the device coherence point: the other XCDs' polling
+    // loads see it at once (a plain store may sit in this XCD's L2)
+    (void)__hip_atomic_exchange(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One wave: records of the chunks before vb.  Lane l inspects chunk j - l; the window of 64
+// is consumed up to its nearest inclusive prefix (or entirely), once every word in that span is
+// ready.  Chunks start in ticket order, so every chunk waited on is resident or done.
+__device__ __forceinline__ unsigned long long lookback_prefix(const unsigned long long* status, unsigned vb,
+                                                              unsigned long long epoch) {
+    const int lane = lane_id();
+    unsigned long long excl = 0;
+    long long j = (long long)vb - 1;
+    while (j >= 0) {
+        const long long t = j - lane;
+        unsigned long long v = t >= 0 ? __hip_atomic_load(status + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                      : (epoch << 42) | kPrefixBit;  // before chunk 0: prefix 0
+        const bool ready = (v >> 42) == epoch;
+        const unsigned long long pm = __ballot(ready && (v & kPrefixBit));
+        const unsigned long long span = pm ? (2ull << __builtin_ctzll(pm)) - 1ull : ~0ull;  // lanes 0 .. first prefix
+        if (__ballot(!ready) & span) {
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        unsigned long long c = ((span >> lane) & 1ull) ? (v & kValueMask) : 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+        excl += c;
+        if (pm) break;
+        j -= kWave;
+    }
+    return excl;
+}
+
+// Stage chunk vb (+ the tail) in LDS and list the record starts it owns, in order: byte 0 of the
+// batch, then q + 1 for each '\n' at q.  Returns the chunk's record count (block-uniform).
+struct ChunkLds {
+    uint4 text4[(kIngestChunk + kIngestTail) / 16];
+    uint16_t start[kIngestChunk + 1];
+    unsigned wave[kThreads / kWave];
+};
+__device__ __forceinline__ unsigned stage_chunk(const uint8_t* __restrict__ text, uint64_t nbytes, unsigned vb,
+                                                ChunkLds& L) {
+    const uint64_t c0 = (uint64_t)vb * kIngestChunk;
+    // the chunk first (this thread's 32 bytes stay in registers for the '\n' scan)
     const uint64_t p = c0 + threadIdx.x * kBytesPerThread;
-    const uint4 va = load16(text, p, nbytes), vb = load16(text, p + 16, nbytes);
-    s_text4[threadIdx.x * 2] = va;
-    s_text4[threadIdx.x * 2 + 1] = vb;
+    const uint4 va = load16(text, p, nbytes), vb4 = load16(text, p + 16, nbytes);
+    L.text4[threadIdx.x * 2] = va;
+    L.text4[threadIdx.x * 2 + 1] = vb4;
     for (uint32_t i = kIngestChunk / 16 + threadIdx.x; i < (kIngestChunk + kIngestTail) / 16; i += kThreads) {
         const uint64_t q = c0 + (uint64_t)i * 16;
-        if (q < nbytes) s_text4[i] = load16(text, q, nbytes);
+        if (q < nbytes) L.text4[i] = load16(text, q, nbytes);
     }
-    // record starts owned by this chunk, in order: byte 0 of the batch, then q + 1 for each '\n' at q
-    const uint32_t m = p < nbytes ? nl_mask32(va, vb, p, nbytes - 1) : 0u;
-    const bool first = blockIdx.x == 0 && threadIdx.x == 0 && nbytes > 0;
+    const uint32_t m = p < nbytes ? nl_mask32(va, vb4, p, nbytes - 1) : 0u;
+    const bool first = vb == 0 && threadIdx.x == 0 && nbytes > 0;
     const unsigned mine = __builtin_popcount(m) + (first ? 1u : 0u);
     unsigned nrec;
-    unsigned at = block_excl_scan(mine, s_wave, &nrec);
-    if (first) s_start[at++] = 0;
-    for (uint32_t mm = m; mm; mm &= mm - 1) s_start[at++] = (uint16_t)(threadIdx.x * kBytesPerThread + __builtin_ctz(mm) + 1);
+    unsigned at = block_excl_scan(mine, L.wave, &nrec);
+    if (first) L.start[at++] = 0;
+    for (uint32_t mm = m; mm; mm &= mm - 1) L.start[at++] = (uint16_t)(threadIdx.x * kBytesPerThread + __builtin_ctz(mm) + 1);
     __syncthreads();
-    const LdsReader rd{reinterpret_cast<const uint8_t*>(s_text4), c0, stage_len, text, nbytes};
-    const uint64_t rbase = chunk_base[blockIdx.x];
+    return nrec;
+}
+
+__device__ __forceinline__ void store_record(const IngestArgs& a, uint64_t idx, const ingest::Parsed& o,
+                                             double* __restrict__ x, double* __restrict__ y,
+                                             int64_t* __restrict__ ts, uint32_t* __restrict__ cell) {
+    x[idx] = o.x;
+    y[idx] = o.y;
+    if (ts) ts[idx] = o.ts;
+    if (cell && a.pad == 3) {
+        cell[idx] = 0u;
+    } else if (cell) {
+        const int32_t cx = ingest::java_cell(o.x, a.min_x, a.cell_len);
+        const int32_t cy = ingest::java_cell(o.y, a.min_y, a.cell_len);
+        const bool ok = cx >= 0 && cx < a.n && cy >= 0 && cy < a.n;
+        cell[idx] = ok ? (uint32_t)cx * (uint32_t)a.n + (uint32_t)cy : 0xffffffffu;
+    }
+}
+
+// The hot kernel: CSV fast paths only (swar_csv, then fast_csv), so no call, no scratch and 55
+// VGPRs -- with the general grammar inlined the kernel took 256 VGPRs + 880 B of scratch per
+// lane (2 waves per SIMD, 4.0 ms per batch), and as a call its scratch frame alone kept it at
+// 1.3 ms.  A chunk with a record the fast paths do not decide (or any chunk of a GeoJSON / WKT
+// batch) is listed for ingest_general, which re-parses all its records with the full grammar.
+// The first round of records is parsed before the look-back, so the wait for the earlier
+// chunks' counts overlaps the parse.
+__global__ __launch_bounds__(kThreads) void ingest_fused(const uint8_t* __restrict__ text, uint64_t nbytes,
+                                                        IngestArgs a, IngestLookback lb,
+                                                        double* __restrict__ x, double* __restrict__ y,
+                                                        int64_t* __restrict__ ts, uint32_t* __restrict__ cell,
+                                                        uint64_t cap, unsigned long long* __restrict__ total) {
+    __shared__ ChunkLds L;
+    __shared__ unsigned s_vb, s_flag;
+    __shared__ unsigned long long s_base;
+    if (threadIdx.x == 0) {
+        s_vb = atomicAdd(lb.ticket, 1u);
+        s_flag = 0;
+    }
+    __syncthreads();
+    const unsigned vb = s_vb;
+    const unsigned nrec = stage_chunk(text, nbytes, vb, L);
+    const unsigned long long tag = lb.epoch << 42;
+    if (threadIdx.x == 0) publish_status(lb.status + vb, tag | (vb == 0 ? kPrefixBit : 0ull) | nrec);
+    const uint64_t c0 = (uint64_t)vb * kIngestChunk;
+    const uint64_t stage_end = c0 + kIngestChunk + kIngestTail < nbytes ? c0 + kIngestChunk + kIngestTail : nbytes;
+    const uint32_t stage_len = (uint32_t)(stage_end - c0);
+    const uint8_t* st8 = reinterpret_cast<const uint8_t*>(L.text4);
     const uint8_t dl = (uint8_t)a.spec.delim;
     const bool fast = a.spec.format == ingest::kCsv && dl > ' ' && dl != '"' && dl != '.' && dl != '-' &&
                       (unsigned)(dl - '0') >= 10u;
-    for (unsigned i = threadIdx.x; i < nrec; i += kThreads) {
-        const uint64_t idx = rbase + i;
+    const unsigned rounds = nrec ? (nrec + kThreads - 1) / kThreads : 1u;  // block-uniform
+    uint64_t rbase = 0;
+    bool undecided = false;
+    for (unsigned r = 0; r < rounds; r++) {
+        const unsigned i = r * kThreads + threadIdx.x;
         ingest::Parsed o;
+        o.x = o.y = 0.0;
         o.ts = 0;
-        int rc;
-        if (a.pad == 1) {
-            o.x = o.y = (double)s_start[i];
-            rc = ingest::kOk;
-        } else {
-            const uint8_t* st8 = reinterpret_cast<const uint8_t*>(s_text4);
-            rc = ingest::kFallback;
-            if (fast) {
-                rc = a.pad == 0 ? swar_csv(st8, s_start[i], stage_len, a.spec, &o) : kSwarNo;
-                if (rc == kSwarNo) rc = fast_csv(st8, s_start[i], stage_len, a.spec, &o, a.pad);
+        int rc = ingest::kFallback;
+        if (i < nrec) {
+            if (a.pad == 1) {
+                o.x = o.y = (double)L.start[i];
+                rc = ingest::kOk;
+            } else if (fast) {
+                rc = a.pad == 0 ? swar_csv(st8, L.start[i], stage_len, a.spec, &o) : kSwarNo;
+                if (rc == kSwarNo) rc = fast_csv(st8, L.start[i], stage_len, a.spec, &o, a.pad);
             }
-            if (rc != ingest::kOk) rc = ingest::parse_record(rd, c0 + s_start[i], a.spec, &o);
+            undecided |= rc != ingest::kOk;
         }
-        if (rc != ingest::kOk) {
-            atomicMin(bad, (unsigned long long)idx);
-            continue;
+        if (r == 0) {  // the record base: look-back by wave 0, behind its first round's parse
+            if (threadIdx.x < kWave) {
+                const unsigned long long excl = vb == 0 ? 0ull : lookback_prefix(lb.status, vb, lb.epoch);
+                if (threadIdx.x == 0) {
+                    if (vb != 0) publish_status(lb.status + vb, tag | kPrefixBit | (excl + nrec));
+                    s_base = excl;
+                    if (vb == gridDim.x - 1) {
+                        *total = excl + nrec;
+                        __hip_atomic_store(lb.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+                    }
+                }
+            }
+            __syncthreads();
+            rbase = s_base;
         }
-        if (idx >= cap) continue;
-        x[idx] = o.x;
-        y[idx] = o.y;
-        if (ts) ts[idx] = o.ts;
-        if (cell && a.pad == 3) {
-            cell[idx] = 0u;
-        } else if (cell) {
-            const int32_t cx = ingest::java_cell(o.x, a.min_x, a.cell_len);
-            const int32_t cy = ingest::java_cell(o.y, a.min_y, a.cell_len);
-            const bool ok = cx >= 0 && cx < a.n && cy >= 0 && cy < a.n;
-            cell[idx] = ok ? (uint32_t)cx * (uint32_t)a.n + (uint32_t)cy : 0xffffffffu;
+        const uint64_t idx = rbase + i;
+        if (i < nrec && rc == ingest::kOk && idx < cap) store_record(a, idx, o, x, y, ts, cell);
+    }
+    if (__ballot(undecided) && lane_id() == 0) s_flag = 1u;
+    __syncthreads();
+    if (threadIdx.x == 0 && s_flag) {  // the chunk goes to ingest_general (rare for CSV)
+        const unsigned j = atomicAdd(lb.nlisted, 1u);
+        lb.listed[j] = make_ulonglong2(vb, rbase);
+    }
+}
+
+// The general grammar (ingest_parse.h: quoted tokens, hex significands, exponents of any length,
+// GeoJSON, WKT) over the chunks ingest_fused listed: every record of such a chunk is parsed again
+// (the fast paths give the same values on the records they accept) and the first rejected record
+// index is kept (bad holds its complement under atomicMax: zero = none).  A fixed grid that
+// strides over the list; with an empty list every block exits after one load.
+__global__ __launch_bounds__(kThreads) void ingest_general(const uint8_t* __restrict__ text, uint64_t nbytes,
+                                                          IngestArgs a, IngestLookback lb,
+                                                          double* __restrict__ x, double* __restrict__ y,
+                                                          int64_t* __restrict__ ts, uint32_t* __restrict__ cell,
+                                                          uint64_t cap, unsigned long long* __restrict__ bad) {
+    __shared__ ChunkLds L;
+    const unsigned nl = *lb.nlisted;
+    for (unsigned j = blockIdx.x; j < nl; j += gridDim.x) {
+        const ulonglong2 e = lb.listed[j];
+        const unsigned vb = (unsigned)e.x;
+        const uint64_t rbase = e.y;
+        const unsigned nrec = stage_chunk(text, nbytes, vb, L);
+        const uint64_t c0 = (uint64_t)vb * kIngestChunk;
+        const uint64_t stage_end = c0 + kIngestChunk + kIngestTail < nbytes ? c0 + kIngestChunk + kIngestTail : nbytes;
+        const LdsReader rd{reinterpret_cast<const uint8_t*>(L.text4), c0, (uint32_t)(stage_end - c0), text, nbytes};
+        for (unsigned i = threadIdx.x; i < nrec; i += kThreads) {
+            const uint64_t idx = rbase + i;
+            ingest::Parsed o;
+            o.ts = 0;
+            if (ingest::parse_record(rd, c0 + L.start[i], a.spec, &o) != ingest::kOk) {
+                atomicMax(bad, ~(unsigned long long)idx);
+                continue;
+            }
+            if (idx < cap) store_record(a, idx, o, x, y, ts, cell);
         }
+        __syncthreads();  // L is restaged for the next listed chunk
     }
 }
 
 }  // namespace
 
-hipError_t launch_ingest(const uint8_t* text, uint64_t nbytes, const IngestArgs& a, unsigned* chunk_cnt,
-                         unsigned long long* chunk_base, unsigned long long* total, double* x, double* y,
-                         int64_t* ts, uint32_t* cell, uint64_t cap, unsigned long long* bad, hipStream_t st,
-                         hipEvent_t ev0, hipEvent_t ev1) {
+hipError_t launch_ingest(const uint8_t* text, uint64_t nbytes, const IngestArgs& a, const IngestLookback& lb,
+                         unsigned long long* total, double* x, double* y, int64_t* ts, uint32_t* cell, uint64_t cap,
+                         unsigned long long* bad, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
     const uint64_t nchunks = ingest_chunks(nbytes);
     if (ev0) (void)hipEventRecord(ev0, st);
     if (nchunks == 0) {
         (void)hipMemsetAsync(total, 0, sizeof(unsigned long long), st);
     } else {
-        ingest_count<<<(unsigned)nchunks, kThreads, 0, st>>>(text, nbytes, chunk_cnt);
-        ingest_scan<<<1, 1024, 0, st>>>(chunk_cnt, nchunks, chunk_base, total);
-        ingest_parse<<<(unsigned)nchunks, kThreads, 0, st>>>(text, nbytes, a, chunk_base, x, y, ts, cell, cap, bad);
+        ingest_fused<<<(unsigned)nchunks, kThreads, 0, st>>>(text, nbytes, a, lb, x, y, ts, cell, cap, total);
+        const unsigned g = nchunks < kGeneralBlocks ? (unsigned)nchunks : kGeneralBlocks;
+        ingest_general<<<g, kThreads, 0, st>>>(text, nbytes, a, lb, x, y, ts, cell, cap, bad);
     }
     if (ev1) (void)hipEventRecord(ev1, st);
     return hipGetLastError();

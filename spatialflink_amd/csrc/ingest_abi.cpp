@@ -1,5 +1,5 @@
 // ingest_abi.cpp -- geohip_ingest_points (include/geohip.h): argument checks the way the
-// reference fails, scratch, the three ingest launches (ingest.hip) and the count readback.
+// reference fails, scratch, the ingest launch (ingest.hip) and the count readback.
 // Also the CPU test hook geohip_debug_ingest_record, which runs the very parser the kernels run
 // (ingest_parse.h, host-compiled) on one record so the CPU suite can check its decisions.
 #include <hip/hip_runtime.h>
@@ -23,7 +23,7 @@ namespace {
         if (e_ != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, std::string(#expr ": ") + hipGetErrorString(e_)); \
     } while (0)
 
-enum { I_TEXT, I_CNT, I_BASE, I_WORDS, I_X, I_Y, I_TS, I_CELL };
+enum { I_TEXT, I_STATUS, I_WORDS, I_X, I_Y, I_TS, I_CELL, I_LIST };
 
 // java.util.regex metacharacters: "\\s*" + delimiter + "\\s*" would not be a literal split
 bool delim_ok(int32_t d) {
@@ -91,10 +91,10 @@ int geohip_ingest_points(geohip_ctx* ctx, const geohip_grid* grid, const geohip_
     if (nchunks >= (1ull << 31)) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "batch too large");
     hipStream_t st = ctx_stream(ctx);
     const bool dev = ctx_mem(ctx) == GEOHIP_MEM_DEVICE;
-    void *cnt, *base, *words;
-    rc = ctx_ensure_ingest(ctx, I_CNT, nchunks * 4, &cnt);
-    if (!rc) rc = ctx_ensure_ingest(ctx, I_BASE, nchunks * 8, &base);
-    if (!rc) rc = ctx_ensure_ingest(ctx, I_WORDS, 64, &words);
+    void *status, *words, *list;
+    rc = ctx_ensure_ingest(ctx, I_STATUS, nchunks * 8, &status);
+    if (!rc) rc = ctx_ensure_ingest(ctx, I_LIST, nchunks * 16, &list);
+    if (!rc) rc = ctx_ensure_ingest_zeroed(ctx, I_WORDS, 64, &words);  // the ticket word starts at zero
     if (rc) return rc;
     const uint8_t* dtext = reinterpret_cast<const uint8_t*>(text);
     double *dx = out_x, *dy = out_y;
@@ -117,17 +117,19 @@ int geohip_ingest_points(geohip_ctx* ctx, const geohip_grid* grid, const geohip_
         dts = static_cast<int64_t*>(pts);
         dcell = static_cast<uint32_t*>(pc);
     }
-    unsigned long long* w = static_cast<unsigned long long*>(words);  // [0] total, [1] first rejected record
-    ICHK(hipMemsetAsync(w + 1, 0xff, 8, st));
+    // [0] total, [1] ticket (re-armed by the kernel), [2] ~first rejected record, [3] listed chunks
+    unsigned long long* w = static_cast<unsigned long long*>(words);
+    ICHK(hipMemsetAsync(w + 2, 0, 16, st));
     hipEvent_t e0, e1;
     ctx_timing_events(ctx, &e0, &e1);
-    hipError_t e = launch_ingest(dtext, nbytes, a, static_cast<unsigned*>(cnt), static_cast<unsigned long long*>(base),
-                                 w, dx, dy, dts, dcell, cap, w + 1, st, e0, e1);
+    const IngestLookback lb{static_cast<unsigned long long*>(status), reinterpret_cast<unsigned*>(w + 1),
+                            ctx_next_ingest_epoch(ctx), static_cast<ulonglong2*>(list), reinterpret_cast<unsigned*>(w + 3)};
+    hipError_t e = launch_ingest(dtext, nbytes, a, lb, w, dx, dy, dts, dcell, cap, w + 2, st, e0, e1);
     if (e != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, std::string("ingest launch: ") + hipGetErrorString(e));
     uint64_t* pinned = ctx_pinned(ctx);
-    ICHK(hipMemcpyAsync(pinned, w, 16, hipMemcpyDeviceToHost, st));
+    ICHK(hipMemcpyAsync(pinned, w, 24, hipMemcpyDeviceToHost, st));
     ICHK(hipStreamSynchronize(st));
-    const uint64_t total = pinned[0], bad = pinned[1];
+    const uint64_t total = pinned[0], bad = pinned[2] ? ~pinned[2] : UINT64_MAX;
     *out_count = total;
     *out_bad = bad;
     if (!dev) {
