@@ -32,6 +32,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -636,8 +637,9 @@ class PpolyWorkload(Workload):
     """C4 (BASELINE.json configs[3]): 1k star polygons (50 vertices) over 50M uniform points per
     window, 500x500, r = 0.005 (conf/geoflink-conf.yml:52)."""
     tag = "ppoly_probe"
-    kernel = ("geohip point-polygon step: tile binning (cells of no polygon dropped) + ppoly_eval + ppoly_emit; "
-              "the whole device step is timed")
+    kernel = ("geohip point-polygon step: ppoly_stream (one pass over the window: cell-table heads, decided pairs, "
+              "mixed-subcell candidates, chunk look-back offsets) + candidates grouped by polygon + ppoly_cand_eval "
+              "(exact JTS tests); the whole device step is timed")
     grid_n, radius, n_default, npoly = 500, 0.005, 50_000_000, 1000
     windows = 2
 
@@ -665,6 +667,39 @@ class PpolyWorkload(Workload):
 
     def algorithmic_bytes(self):
         return BYTES_PER_POINT * self.n + 16 * len(self.vx) + 8 * float(np.mean(self.hits))
+
+    def algorithmic_flops(self):
+        """candidate pairs x ~1.85 kflop (50 crossings + 50 segment distances per
+        JTS DistanceOp).  Candidate pairs = the window's points in each polygon's G u C cells (the
+        reference's per-candidate distance work): the bbox-cell rectangle (HelperClass.java:123-143)
+        dilated by Lc = ceil(r / l) (UniformGrid.java:398-444), clipped, counted from the window's
+        cell histogram (first window)."""
+        if getattr(self, "_alg_flops", None) is None:
+            from spatialflink_amd import synth
+            bj = synth.BEIJING
+            n_, l = self.grid_n, (bj[1] - bj[0]) / self.grid_n
+            x = self.xs[0].cpu().numpy()
+            y = self.ys[0].cpu().numpy()
+            cx = np.floor((x - bj[0]) / l)
+            cy = np.floor((y - bj[2]) / l)
+            ok = (cx >= 0) & (cx < n_) & (cy >= 0) & (cy < n_)
+            h = np.zeros((n_ + 1, n_ + 1), np.int64)
+            np.add.at(h, (cx[ok].astype(np.int64) + 1, cy[ok].astype(np.int64) + 1), 1)
+            S = h.cumsum(0).cumsum(1)  # S[a, b] = points in cells [0, a) x [0, b)
+            lc = int(math.ceil(self.radius / l))
+            cand = 0
+            for p in range(self.npoly):
+                a, b = int(self.off[p]), int(self.off[p + 1])
+                px, py = self.vx[a:b], self.vy[a:b]
+                x0 = max(int(math.floor((px.min() - bj[0]) / l)) - lc, 0)
+                x1 = min(int(math.floor((px.max() - bj[0]) / l)) + lc, n_ - 1)
+                y0 = max(int(math.floor((py.min() - bj[2]) / l)) - lc, 0)
+                y1 = min(int(math.floor((py.max() - bj[2]) / l)) + lc, n_ - 1)
+                if x0 <= x1 and y0 <= y1:
+                    cand += int(S[x1 + 1, y1 + 1] - S[x0, y1 + 1] - S[x1 + 1, y0] + S[x0, y0])
+            self._alg_cand = cand
+            self._alg_flops = cand * 1850.0
+        return self._alg_flops
 
     def config(self):
         return {"workload": f"C4: point-polygon range, {self.npoly} polygons x 50 vertices over {self.n} uniform "
@@ -696,7 +731,7 @@ class PpJoinWorkload(PpolyWorkload):
     """the C4 shape as a point-polygon join (PointPolygonJoinQuery,
     polygon stream replicated to its G/C cells, every candidate distance-checked)."""
     tag = "ppjoin"
-    kernel = ("geohip point-polygon join step: tile binning + ppoly_eval + ppoly_emit in join mode; "
+    kernel = ("geohip point-polygon join step: ppoly_stream + candidate grouping + ppoly_cand_eval in join mode; "
               "the whole device step is timed")
 
     def __init__(self, *a):
@@ -809,7 +844,7 @@ class PpolyIncrWorkload(PpolyWorkload):
     once against the 1k polygons, the window's pairs assembled from its two panes
     (spatialflink_amd.incremental.IncrementalPPolyRange).  value = stream points/sec."""
     tag = "ppoly_incr"
-    kernel = "geohip point-polygon step on one pane (binning + ppoly_eval + ppoly_emit, timed)"
+    kernel = "geohip point-polygon step on one pane (ppoly_stream + candidate grouping + ppoly_cand_eval, timed)"
     n_default = 25_000_000
     windows = 4
 
@@ -1072,13 +1107,19 @@ def main():
                      "algorithmic_bytes_per_launch": abytes, **wl.roofline_extra()},
         "cpu_baseline": None,
     }
-    flops = pmc_traffic(wl.tag, "fp64_flops_per_launch")
-    if flops and avg_s > 0:  # the point-polygon steps are FP64-VALU bound (crossings, distances)
-        tf = flops / avg_s / 1e12
+    alg_flops = wl.algorithmic_flops() if hasattr(wl, "algorithmic_flops") else None
+    if alg_flops and avg_s > 0:  # the point-polygon steps: the reference's FP64 work (crossings, distances)
+        tf = alg_flops / avg_s / 1e12
+        pmc_flops = pmc_traffic(wl.tag, "fp64_flops_per_launch")
         result["roofline_fp64"] = {"bound": "fp64", "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                                   "frac": tf / FP64_PEAK_TFLOPS, "flops": flops,
-                                   "source": "rocprofv3 SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes of the timed kernels per step "
-                                             "(profiles/pmc_" + wl.tag + ".json) / the live average step time"}
+                                   "frac": tf / FP64_PEAK_TFLOPS, "flops": alg_flops,
+                                   "candidate_pairs": wl._alg_cand,
+                                   "source": "SURVEY.md 8(d): candidate pairs (window points in each polygon's G u C "
+                                             "cells) x 1850 flop / the live average step time",
+                                   "pmc_flops": pmc_flops,
+                                   "pmc_source": "rocprofv3 SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes of the timed kernels per "
+                                                 "step (profiles/pmc_" + wl.tag + ".json): the executed flops, "
+                                                 "after the cell classes and screens removed most of the algorithmic work"}
     if args.check and world > 1 and hasattr(wl, "check_merged"):
         ok = wl.check_merged(args.warmup + args.steps - 1)
         if rank == 0 and ok is not None:

@@ -24,6 +24,8 @@ _BIN = {"bin_count<1>": 1, "bin_count<2>": 1, "bin_scatter<1>": 1, "bin_scatter<
 _PP = {**_BIN, "scan_seg_totals<unsigned int>": 1, "scan_totals<unsigned int>": 1, "scan_apply<unsigned int>": 1,
        "scan_seg_totals<unsigned long long>": 2, "scan_totals<unsigned long long>": 2,
        "scan_apply<unsigned long long>": 2, "ppoly_words": 1, "ppoly_eval": 1, "ppoly_emit": 1, "ppoly_outside": 1}
+# streaming point-polygon step (r03): one pass over the window + candidate grouping + exact tests
+_PS = {"ppoly_stream": 1, "ppoly_cand_count": 1, "ppoly_cand_plan": 1, "ppoly_cand_scatter": 1, "ppoly_cand_eval": 1}
 # SQ_INSTS_VALU_FLOPS_FP64 counts per wave instruction: calibrated on synth_uniform (6 fp64
 # add/mul per point in its ISA, 50M points -> 4,687,500 counted = 300M / 64), so lane FLOPs are
 # the counted value times 64 (issued lanes: a divergent wave's idle lanes are included).
@@ -33,13 +35,13 @@ TAGS = {"knn": ("knn_scan", {"knn_pass": 1}),
         "join": ("join_probe", {**_BIN, "scan_seg_totals<unsigned int>": 3, "scan_totals<unsigned int>": 3,
                                 "scan_apply<unsigned int>": 3, "jq_rect": 1, "jq_build<false>": 1, "jq_build<true>": 1,
                                 "join_items": 1, "join_item_fill": 1, "join_fused<false, true>": 1}),
-        "ppoly": ("ppoly_probe", _PP),
+        "ppoly": ("ppoly_probe", _PS),
         "c5": ("knn_scan_c5", {"knn_pass": 1}),
         "ingest": ("ingest", {"ingest_fused": 1}),
-        "ppjoin": ("ppjoin", _PP),
+        "ppjoin": ("ppjoin", _PS),
         "ppknn": ("ppknn", {"rsel_init": 1, "rsel_small": 1, "ppknn_scan_boxes": 1, "ppknn_dist": 1}),
         "knn_incr": ("knn_incr", {"knn_pass": 1, "knn_final": 1}),
-        "ppoly_incr": ("ppoly_incr", _PP)}
+        "ppoly_incr": ("ppoly_incr", _PS)}
 
 
 def per_kernel(path):

@@ -87,6 +87,7 @@ struct CopyPool {
 
 struct geohip_ctx {
     int device = 0;
+    int cus = 256;               // compute units of the device (persistent grids)
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
     int mem = GEOHIP_MEM_HOST;
@@ -105,7 +106,7 @@ struct geohip_ctx {
     double plan_q[3] = {0, 0, 0};
     PointPlan plan{};
     unsigned long long range_epoch = 0;  // fused range pass: status words of this launch carry it
-    unsigned long long ingest_epoch = 0; // ingest look-back: status words of this launch carry it
+    unsigned long long lb_epoch = 0;     // chunk look-backs (ingest, point-polygon stream): status words of a launch carry it
     // host windows (GEOHIP_MEM_HOST): two pinned staging slots; the DMA of one slot runs on the
     // copy stream while the host fills the other (host_stage)
     hipStream_t cstream = nullptr;
@@ -574,6 +575,10 @@ int geohip_ctx_create(uint32_t device_mask, geohip_ctx** out_ctx) {
     }
     geohip_ctx* ctx = new geohip_ctx();
     ctx->device = dev;
+    {
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0) ctx->cus = ncu;
+    }
     if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc((void**)&ctx->pinned, 64, hipHostMallocDefault) != hipSuccess) {
         delete ctx;
@@ -1117,10 +1122,12 @@ int ctx_ensure_ingest_zeroed(geohip_ctx* ctx, int slot, size_t bytes, void** out
     if (!rc) *out = ctx->buf[S_I0 + slot];
     return rc;
 }
-unsigned long long ctx_next_ingest_epoch(geohip_ctx* ctx) {
-    ctx->ingest_epoch = ctx->ingest_epoch % ((1ull << 22) - 1) + 1;
-    return ctx->ingest_epoch;
+unsigned long long ctx_next_epoch(geohip_ctx* ctx) {
+    ctx->lb_epoch = ctx->lb_epoch % ((1ull << 22) - 1) + 1;
+    return ctx->lb_epoch;
 }
+int ctx_cus(geohip_ctx* ctx) { return ctx->cus; }
+
 int ctx_begin(geohip_ctx* ctx) { return begin(ctx); }
 hipStream_t ctx_stream(geohip_ctx* ctx) { return ctx->stream; }
 int ctx_mem(geohip_ctx* ctx) { return ctx->mem; }

@@ -1814,6 +1814,601 @@ __global__ __launch_bounds__(kTB) void ppoly_outside(const double* __restrict__ 
     pairs_end<WRITE>(buf, cnt, &bsh, sink);
 }
 
+// ====================================================== point-polygon: streaming path =======
+// The window is read once, in arrival order, with no tile binning.  A host-built cell table
+// (PolyCache::cell_off / cell_ent, cached with the polygon plan) lists per key cell the
+// polygons whose rectangles hold it, C cells of class kClsMiss left out: entry (poly | kEntC?,
+// class word).  Per point, its cell's entries: a G entry (or, exact, a C entry whose subcell
+// class is kClsHit; approximate, a C entry whose bbox distance is <= r) is a pair at once; a C
+// entry of a mixed subcell is a candidate (point, polygon) for the exact JTS test.  Candidates
+// (a few % of the points for C4) are grouped by polygon (ppoly_cand_count / _plan / _scatter)
+// and evaluated with the polygon's rings in LDS (ppoly_cand_eval), as ppoly_eval does per tile.
+// Pairs and candidates leave through per-wave LDS buffers, one global atomic per buffer.
+// The same decisions as ppoly_eval (PointPolygonRangeQuery.java:105-121; the join's
+// PointPolygonJoinQuery.java:183-195 through jmode's rectangle lists).
+constexpr uint32_t kEntC = 0x80000000u;    // entry.x: C cell (class word in entry.y); else G
+constexpr int kStreamNW = 8;               // waves per block
+constexpr unsigned kStreamPts = 256;       // points per wave iteration (4 per lane)
+constexpr unsigned kStreamChunk = 8192;    // points per chunk (4 iterations per wave)
+constexpr unsigned kStreamBlocksPerCU = 2;
+constexpr unsigned kSPairCap = 8192;       // block-staged pairs per chunk (4 B each: poly << 13 | point)
+constexpr unsigned kSCandCap = 1024;       // block-staged candidates per chunk
+constexpr unsigned kLocalBits = 13;        // point within its chunk
+constexpr uint32_t kStreamMaxPolys = 1u << (32 - kLocalBits);
+constexpr unsigned kCandItem = 1024;       // candidates per evaluation work item
+constexpr unsigned kCandLdsPolys = 16384;  // polygons whose per-polygon counters fit LDS
+constexpr unsigned kEvalBlocks = 1024;     // grid of the evaluation pass (strides over its items)
+static_assert(kStreamChunk == (1u << kLocalBits), "chunk-local point ids");
+static_assert(kStreamChunk == kStreamNW * 4 * kStreamPts, "chunk = waves x iterations x points");
+
+// A cell's table head (8 B, one gather per point): x == kNoEntry -- no entry; x & kMulti -- x's
+// low 30 bits entries at cell_ent[y ...]; else the cell's only entry (x = poly | kEntC?, y = its
+// class word).  2 MB for 500 x 500 cells.
+constexpr uint32_t kNoEntry = 0xffffffffu;
+constexpr uint32_t kMulti = 0x40000000u;
+
+struct StreamOut {
+    unsigned* out;                  // pairs, u32 x 2 (swap: (point, polygon))
+    uint64_t cap;
+    int aligned8, swap;
+    unsigned long long* totals;     // [0] pairs, [1] candidates: reservation cursors (zero before)
+    uint64_t ccap;                  // candidates past it are counted only (the host regrows, re-runs)
+    unsigned* cpoly;                // candidates in chunk order: polygon, point, coordinates
+    unsigned* cidx;
+    double* cx;
+    double* cy;
+};
+
+struct StreamArgs {
+    const double* x;
+    const double* y;
+    uint64_t n;
+    TileGeom g;
+    const unsigned* keep;           // cells with entries (bitmap, keep_words words)
+    unsigned keep_words;
+    const uint2* head;              // nb * nb
+    const uint2* ent;
+    const PolyDev* polys;
+    const uint32_t* opoly;          // polygons whose rectangles reach outside the grid
+    uint32_t nopoly;
+    const int32_t* rects;
+    int jmode;                      // 0 range, 1 join exact, 2 join approximate
+    double r;
+    StreamOut o;
+};
+
+// one pair or candidate of the current chunk: staged in LDS (packed), or -- a chunk whose stage
+// overflowed, re-run once its bases are known -- stored straight to its global slot
+struct StreamSink {
+    unsigned* pk;                   // LDS: packed pairs / candidates
+    unsigned* cursor;               // LDS counter
+    unsigned cap;
+    bool direct;
+    unsigned long long base;        // direct: first global slot of the chunk
+    unsigned acc;                   // measurement only (GEOHIP_PS_ABL 3)
+};
+
+__device__ __forceinline__ void stream_emit_pair(const StreamOut& o, unsigned long long p, unsigned poly, unsigned idx) {
+    if (p >= o.cap) return;
+    const uint2 v = o.swap ? make_uint2(idx, poly) : make_uint2(poly, idx);
+    if (o.aligned8) {  // streaming pair stores: nothing on the device reads them again
+        __builtin_nontemporal_store(((unsigned long long)v.y << 32) | v.x, reinterpret_cast<unsigned long long*>(o.out) + p);
+    } else {
+        o.out[2 * p] = v.x;
+        o.out[2 * p + 1] = v.y;
+    }
+}
+__device__ __forceinline__ void stream_emit_cand(const StreamArgs& a, unsigned long long p, unsigned poly, unsigned idx) {
+    if (p >= a.o.ccap) return;
+    a.o.cpoly[p] = poly;
+    a.o.cidx[p] = idx;
+    a.o.cx[p] = a.x[idx];
+    a.o.cy[p] = a.y[idx];
+}
+
+#ifndef GEOHIP_PS_ABL
+#define GEOHIP_PS_ABL 0  // measurement builds only: 1 no staging pushes, 2 no cell-table reads,
+                          // 3 pushes folded into a register checksum, 4 no chunk write-out
+#endif
+// wave-uniform: the lanes with `hit` add (poly, chunk-local point) to the sink
+template <bool CAND>
+__device__ __forceinline__ void stream_push(const StreamArgs& a, StreamSink& k, bool hit, unsigned poly, unsigned loc,
+                                            uint64_t chunk0) {
+    if (GEOHIP_PS_ABL == 3) {
+        k.acc += hit ? (poly ^ loc) : 0u;
+        return;
+    }
+    const unsigned long long m = __ballot(hit);
+    if (!m || GEOHIP_PS_ABL == 1) return;
+    unsigned b = 0;
+    if (lane_id() == 0) b = atomicAdd(k.cursor, (unsigned)__popcll(m));
+    b = (unsigned)__shfl((int)b, 0) + lanes_below(m);
+    if (!hit) return;
+    if (k.direct) {
+        if (CAND) stream_emit_cand(a, k.base + b, poly, (unsigned)(chunk0 + loc));
+        else stream_emit_pair(a.o, k.base + b, poly, (unsigned)(chunk0 + loc));
+    } else if (b < k.cap) {
+        k.pk[b] = (poly << kLocalBits) | loc;
+    }
+}
+
+// One chunk's points (all waves of the block): their cells, table heads and entries.  A wave's
+// next iteration's coordinates load while the current one is decided (a two-deep pipeline that
+// also held the next table heads in flight spilled registers and measured slower: 630 -> 720 us).
+template <bool APPROX>
+__device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned* kl, bool kl_ok, uint64_t c0,
+                                             uint64_t c1, StreamSink& ps, StreamSink& cs) {
+    const int wid = threadIdx.x / kWave, lane = lane_id();
+    const TileGeom& g = a.g;
+    const unsigned nb = (unsigned)g.nb;
+    constexpr unsigned kIters = kStreamChunk / (kStreamNW * kStreamPts);
+    auto load = [&](unsigned t, double (&qx)[4], double (&qy)[4]) {
+        const uint64_t base = c0 + (uint64_t)(t * kStreamNW + wid) * kStreamPts;
+        const uint64_t i0 = base + 2 * (uint64_t)lane, i1 = i0 + 128;
+        if (base + kStreamPts <= c1) {
+            const double2 ax = *reinterpret_cast<const double2*>(a.x + i0);
+            const double2 bx = *reinterpret_cast<const double2*>(a.x + i1);
+            const double2 ay = *reinterpret_cast<const double2*>(a.y + i0);
+            const double2 by = *reinterpret_cast<const double2*>(a.y + i1);
+            qx[0] = ax.x; qx[1] = ax.y; qx[2] = bx.x; qx[3] = bx.y;
+            qy[0] = ay.x; qy[1] = ay.y; qy[2] = by.x; qy[3] = by.y;
+        } else {
+            const uint64_t id[4] = {i0, i0 + 1, i1, i1 + 1};
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                qx[s] = id[s] < c1 ? a.x[id[s]] : 0.0;
+                qy[s] = id[s] < c1 ? a.y[id[s]] : 0.0;
+            }
+        }
+    };
+    double nx[4], ny[4];
+    load(0, nx, ny);
+#pragma unroll 1
+    for (unsigned t = 0; t < kIters; t++) {
+        double cxv[4], cyv[4];
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            cxv[s] = nx[s];
+            cyv[s] = ny[s];
+        }
+        if (t + 1 < kIters) load(t + 1, nx, ny);
+        const unsigned lb = (t * kStreamNW + (unsigned)wid) * kStreamPts + 2u * (unsigned)lane;
+        const unsigned loc[4] = {lb, lb + 1, lb + 128, lb + 129};
+        uint2 h[4];
+        int32_t ccx[4], ccy[4];
+        bool outside[4];
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const bool v = c0 + loc[s] < c1;
+            int32_t cx = 0, cy = 0;
+            const bool in = v && point_cell(g, cxv[s], cyv[s], cx, cy);
+            outside[s] = v && !in;
+            ccx[s] = cx;
+            ccy[s] = cy;
+            h[s] = make_uint2(kNoEntry, 0u);
+            if (in) {
+                const unsigned key = (unsigned)cx * nb + (unsigned)cy;
+                bool has = true;
+                if (a.keep) has = ((kl_ok ? kl[key >> 5] : a.keep[key >> 5]) >> (key & 31u)) & 1u;
+                if (has && GEOHIP_PS_ABL != 2) h[s] = a.head[key];
+                if (GEOHIP_PS_ABL == 2 && has && key == 0xfffffffu) h[s].x = 0;
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const double qx = cxv[s], qy = cyv[s];
+            const bool nan = !(qx == qx && qy == qy);
+            int sx = -1, sy = 0;  // subcell, computed on the first mixed word
+            // entry cursor: the head's entry (single) or cell_ent[e, e1) (multi)
+            uint32_t ex = h[s].x, word = h[s].y;
+            unsigned e = 0, e1 = 0;
+            if (ex != kNoEntry && (ex & kMulti)) {
+                e = word;
+                e1 = e + (ex & ~kMulti);
+                const uint2 en = a.ent[e++];
+                ex = en.x;
+                word = en.y;
+            }
+            while (__ballot(ex != kNoEntry)) {
+                bool hit = false, need = false;
+                unsigned poly = 0;
+                if (ex != kNoEntry) {
+                    poly = ex & ~kEntC;
+                    if (!(ex & kEntC)) {
+                        hit = true;
+                    } else if (APPROX) {
+                        hit = bbox_distance(qx, qy, a.polys[poly].bb) <= a.r;
+                    } else {
+                        // a decided class holds for every point in the cell's coordinate box: not
+                        // for NaN coordinates (cell 0 by Java's (int) NaN)
+                        uint32_t k = kClsMixed;
+                        if (!nan) {
+                            if (word == kWordHit) k = kClsHit;
+                            else if (word == kWordMiss) k = kClsMiss;
+                            else if (word != 0u) {
+                                if (sx < 0) {
+                                    sx = sub_of(qx, g.mnx, g.l, ccx[s]);
+                                    sy = sub_of(qy, g.mny, g.l, ccy[s]);
+                                }
+                                k = (word >> (2 * (4 * sx + sy))) & 3u;
+                            }
+                        }
+                        hit = k == kClsHit;
+                        need = k == kClsMixed;
+                    }
+                    if (e < e1) {  // the cell's next entry
+                        const uint2 en = a.ent[e++];
+                        ex = en.x;
+                        word = en.y;
+                    } else {
+                        ex = kNoEntry;
+                    }
+                }
+                stream_push<false>(a, ps, hit, poly, loc[s], c0);
+                if (!APPROX) stream_push<true>(a, cs, need, poly, loc[s], c0);
+            }
+        }
+        // points outside the grid against the polygons whose rectangles reach outside it (rare)
+        if (a.nopoly && __ballot(outside[0] || outside[1] || outside[2] || outside[3])) {
+            for (int s = 0; s < 4; s++) {
+                int32_t cx = 0, cy = 0;
+                if (outside[s]) {
+                    cx = d_axis_cell(cxv[s], g.mnx, g.l);
+                    cy = d_axis_cell(cyv[s], g.mny, g.l);
+                }
+                for (uint32_t j = 0; j < a.nopoly; j++) {
+                    const uint32_t p = a.opoly[j];
+                    const PolyDev& P = a.polys[p];
+                    // range: the guaranteed rectangles; join exact: the checked list (+ the exact
+                    // test); join approximate: every rectangle is in the G list
+                    bool in = false;
+                    if (outside[s])
+                        in = a.jmode == 1 ? in_rects(a.rects + 4 * P.coff, P.nc, cx, cy)
+                                          : in_rects(a.rects + 4 * P.goff, P.ng, cx, cy);
+                    const bool dist = !APPROX && a.jmode == 1;
+                    stream_push<false>(a, ps, in && !dist, p, loc[s], c0);
+                    if (!APPROX) stream_push<true>(a, cs, in && dist, p, loc[s], c0);
+                }
+            }
+        }
+    }
+}
+
+// Persistent blocks take the 8192-point chunks blockIdx.x, + gridDim.x, ...  Per chunk: pairs
+// and candidates staged in LDS (4 B each), then one atomic reservation each on the pair and
+// candidate totals (the output is unordered: no look-back, no chunk waits for another) and
+// coalesced stores.  A chunk whose stage overflowed runs again with its reservations made from
+// the counts, storing every pair / candidate straight to its slot.
+template <bool APPROX>
+#ifndef GEOHIP_PS_WPE
+#define GEOHIP_PS_WPE 4  // waves per SIMD the register budget is held to (LDS allows 4)
+#endif
+__global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_eu(GEOHIP_PS_WPE))) void ppoly_stream(StreamArgs a) {
+    __shared__ unsigned kl[kKeepLds];
+    __shared__ unsigned ppk[kSPairCap];
+    __shared__ unsigned cpk[APPROX ? 1 : kSCandCap];
+    __shared__ unsigned s_np, s_nc;
+    __shared__ unsigned long long s_pb, s_cb;
+    const bool kl_ok = a.keep && a.keep_words <= kKeepLds;
+    if (kl_ok)
+        for (unsigned t = threadIdx.x; t < a.keep_words; t += kStreamNW * kWave) kl[t] = a.keep[t];
+    const unsigned nchunks = (unsigned)((a.n + kStreamChunk - 1) / kStreamChunk);
+    for (unsigned vb = blockIdx.x; vb < nchunks; vb += gridDim.x) {
+        __syncthreads();  // the previous chunk's stage is drained (and the bitmap staged)
+        if (threadIdx.x == 0) {
+            s_np = 0;
+            s_nc = 0;
+        }
+        __syncthreads();
+        const uint64_t c0 = (uint64_t)vb * kStreamChunk;
+        const uint64_t c1 = c0 + kStreamChunk < a.n ? c0 + kStreamChunk : a.n;
+        StreamSink ps{ppk, &s_np, kSPairCap, false, 0, 0u};
+        StreamSink cs{cpk, &s_nc, APPROX ? 0u : kSCandCap, false, 0, 0u};
+        stream_chunk<APPROX>(a, kl, kl_ok, c0, c1, ps, cs);
+        if (GEOHIP_PS_ABL == 3 && ps.acc + cs.acc == 0x9e3779b9u) a.o.totals[0] = 1;
+        __syncthreads();
+        const unsigned np = s_np, nc = s_nc;
+        if (threadIdx.x == 0) {
+            s_pb = np ? atomicAdd(a.o.totals, (unsigned long long)np) : 0ull;
+            s_cb = nc ? atomicAdd(a.o.totals + 1, (unsigned long long)nc) : 0ull;
+        }
+        __syncthreads();
+        const unsigned long long pb = s_pb, cb = s_cb;
+        if (GEOHIP_PS_ABL == 4) continue;
+        if (np <= kSPairCap && nc <= cs.cap) {
+            for (unsigned t = threadIdx.x; t < np; t += kStreamNW * kWave) {
+                const unsigned v = ppk[t];
+                stream_emit_pair(a.o, pb + t, v >> kLocalBits, (unsigned)(c0 + (v & (kStreamChunk - 1))));
+            }
+            if (!APPROX)
+                for (unsigned t = threadIdx.x; t < nc; t += kStreamNW * kWave) {
+                    const unsigned v = cpk[t];
+                    stream_emit_cand(a, cb + t, v >> kLocalBits, (unsigned)(c0 + (v & (kStreamChunk - 1))));
+                }
+        } else {  // overflow (many polygons per cell): the chunk again, straight to its slots
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                s_np = 0;
+                s_nc = 0;
+            }
+            __syncthreads();
+            StreamSink pd{ppk, &s_np, kSPairCap, true, pb, 0u};
+            StreamSink cd{cpk, &s_nc, cs.cap, true, cb, 0u};
+            stream_chunk<APPROX>(a, kl, kl_ok, c0, c1, pd, cd);
+        }
+    }
+}
+
+// Pairs of the exact tests: per-wave LDS buffers appended behind the stream's pairs, one global
+// atomic per buffer on the pair total (the stream's last chunk wrote it before this launch).
+constexpr int kSPairs = 512;
+__device__ __forceinline__ void spairs_flush(uint2* buf, unsigned& cnt, const StreamOut& o) {
+    wave_lds_sync();
+    unsigned lo = 0, hi = 0;
+    if (lane_id() == 0) {
+        const unsigned long long b = atomicAdd(o.totals, (unsigned long long)cnt);
+        lo = (unsigned)b;
+        hi = (unsigned)(b >> 32);
+    }
+    const unsigned long long base = ((unsigned long long)__shfl(hi, 0) << 32) | __shfl(lo, 0);
+    for (unsigned t = lane_id(); t < cnt; t += kWave) stream_emit_pair(o, base + t, buf[t].x, buf[t].y);
+    wave_lds_sync();
+    cnt = 0;
+}
+__device__ __forceinline__ void spairs_push(uint2* buf, unsigned& cnt, bool hit, unsigned poly, unsigned idx,
+                                            const StreamOut& o) {
+    const unsigned long long m = __ballot(hit);
+    if (!m) return;
+    if (hit) buf[cnt + lanes_below(m)] = make_uint2(poly, idx);
+    cnt += (unsigned)__popcll(m);
+    if (cnt > (unsigned)(kSPairs - kWave)) spairs_flush(buf, cnt, o);
+}
+
+// Grouping of the candidates by polygon: a counting sort with no global atomics.  kCandGroups
+// blocks each own a contiguous range of the candidates: per-polygon counts of the range in LDS
+// -> row b of a [kCandGroups][npoly] matrix (ppoly_cand_hist); one block turns the matrix into
+// per-(range, polygon) write bases, the polygons' runs and the work items (ppoly_cand_plan); the
+// same ranges scatter (point, x, y) into the runs from their rows (ppoly_cand_scatter).
+constexpr unsigned kCandGroups = 128;
+constexpr unsigned kCandThreads = 1024;
+constexpr unsigned kCandPer = 4;  // candidates per thread per round (loads in flight together)
+struct CandGroup {
+    const unsigned long long* ccount;  // candidate total (StreamOut::totals + 1)
+    uint64_t ccap;
+    const unsigned* cpoly;
+    const unsigned* cidx;
+    const double* cx;
+    const double* cy;
+    unsigned* mat;          // [kCandGroups][npoly]: counts, then write bases
+    uint32_t npoly;         // <= kCandLdsPolys
+    uint4* items;           // (poly, begin, end, -)
+    unsigned* nitems;
+    unsigned* sidx;         // sorted runs
+    double* sx;
+    double* sy;
+};
+
+__device__ __forceinline__ uint64_t cand_n(const CandGroup& c) {
+    const unsigned long long n = *c.ccount;
+    return n < c.ccap ? n : c.ccap;
+}
+__device__ __forceinline__ void cand_range(const CandGroup& c, uint64_t& b0, uint64_t& b1) {
+    const uint64_t n = cand_n(c);
+    const uint64_t per = (n + kCandGroups - 1) / kCandGroups;
+    b0 = (uint64_t)blockIdx.x * per < n ? (uint64_t)blockIdx.x * per : n;
+    b1 = b0 + per < n ? b0 + per : n;
+}
+
+__global__ __launch_bounds__(kCandThreads) void ppoly_cand_hist(CandGroup c) {
+    __shared__ unsigned h[kCandLdsPolys];
+    uint64_t b0, b1;
+    cand_range(c, b0, b1);
+    for (unsigned t = threadIdx.x; t < c.npoly; t += kCandThreads) h[t] = 0;
+    __syncthreads();
+    for (uint64_t i0 = b0 + threadIdx.x; i0 < b1; i0 += (uint64_t)kCandPer * kCandThreads) {
+        unsigned p[kCandPer];
+#pragma unroll
+        for (unsigned u = 0; u < kCandPer; u++) {
+            const uint64_t i = i0 + (uint64_t)u * kCandThreads;
+            p[u] = i < b1 ? c.cpoly[i] : 0xffffffffu;
+        }
+#pragma unroll
+        for (unsigned u = 0; u < kCandPer; u++)
+            if (p[u] != 0xffffffffu) atomicAdd(&h[p[u]], 1u);
+    }
+    __syncthreads();
+    unsigned* row = c.mat + (size_t)blockIdx.x * c.npoly;
+    for (unsigned t = threadIdx.x; t < c.npoly; t += kCandThreads) row[t] = h[t];
+}
+
+// one block: column sums (a polygon's run length), their scan (run starts), the columns' scans
+// (each range's base inside each run) and the kCandItem work items
+__global__ __launch_bounds__(kCandThreads) void ppoly_cand_plan(CandGroup c) {
+    __shared__ unsigned sc[kCandThreads], si[kCandThreads];
+    __shared__ unsigned carry_c, carry_i;
+    constexpr unsigned kB = 16;
+    if (threadIdx.x == 0) {
+        carry_c = 0;
+        carry_i = 0;
+    }
+    for (unsigned p0 = 0; p0 < c.npoly; p0 += kCandThreads) {
+        const unsigned p = p0 + threadIdx.x;
+        unsigned tot = 0;
+        if (p < c.npoly)
+            for (unsigned g0 = 0; g0 < kCandGroups; g0 += kB) {
+                unsigned v[kB];
+#pragma unroll
+                for (unsigned u = 0; u < kB; u++) v[u] = c.mat[(size_t)(g0 + u) * c.npoly + p];
+#pragma unroll
+                for (unsigned u = 0; u < kB; u++) tot += v[u];
+            }
+        const unsigned nit = (tot + kCandItem - 1) / kCandItem;
+        sc[threadIdx.x] = tot;
+        si[threadIdx.x] = nit;
+        __syncthreads();
+        for (unsigned o = 1; o < kCandThreads; o <<= 1) {
+            const unsigned a = threadIdx.x >= o ? sc[threadIdx.x - o] : 0u;
+            const unsigned b = threadIdx.x >= o ? si[threadIdx.x - o] : 0u;
+            __syncthreads();
+            sc[threadIdx.x] += a;
+            si[threadIdx.x] += b;
+            __syncthreads();
+        }
+        const unsigned start = carry_c + sc[threadIdx.x] - tot, item0 = carry_i + si[threadIdx.x] - nit;
+        if (p < c.npoly) {
+            unsigned run = start;
+            for (unsigned g0 = 0; g0 < kCandGroups; g0 += kB) {
+                unsigned v[kB];
+#pragma unroll
+                for (unsigned u = 0; u < kB; u++) v[u] = c.mat[(size_t)(g0 + u) * c.npoly + p];
+#pragma unroll
+                for (unsigned u = 0; u < kB; u++) {
+                    c.mat[(size_t)(g0 + u) * c.npoly + p] = run;
+                    run += v[u];
+                }
+            }
+            for (unsigned k = 0; k < nit; k++) {
+                const unsigned lo = start + k * kCandItem;
+                c.items[item0 + k] = make_uint4(p, lo, tot - k * kCandItem > kCandItem ? lo + kCandItem : start + tot, 0u);
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == kCandThreads - 1) {
+            carry_c += sc[kCandThreads - 1];
+            carry_i += si[kCandThreads - 1];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *c.nitems = carry_i;
+}
+
+__global__ __launch_bounds__(kCandThreads) void ppoly_cand_scatter(CandGroup c) {
+    __shared__ unsigned h[kCandLdsPolys];
+    uint64_t b0, b1;
+    cand_range(c, b0, b1);
+    const unsigned* row = c.mat + (size_t)blockIdx.x * c.npoly;
+    for (unsigned t = threadIdx.x; t < c.npoly; t += kCandThreads) h[t] = row[t];
+    __syncthreads();
+    for (uint64_t i0 = b0 + threadIdx.x; i0 < b1; i0 += (uint64_t)kCandPer * kCandThreads) {
+        unsigned p[kCandPer], q[kCandPer];
+        double x[kCandPer], y[kCandPer];
+#pragma unroll
+        for (unsigned u = 0; u < kCandPer; u++) {
+            const uint64_t i = i0 + (uint64_t)u * kCandThreads;
+            p[u] = 0xffffffffu;
+            if (i < b1) {
+                p[u] = c.cpoly[i];
+                q[u] = c.cidx[i];
+                x[u] = c.cx[i];
+                y[u] = c.cy[i];
+            }
+        }
+#pragma unroll
+        for (unsigned u = 0; u < kCandPer; u++)
+            if (p[u] != 0xffffffffu) {
+                const unsigned pos = atomicAdd(&h[p[u]], 1u);
+                c.sidx[pos] = q[u];
+                c.sx[pos] = x[u];
+                c.sy[pos] = y[u];
+            }
+    }
+}
+
+// Exact test of each grouped candidate: one work item = one polygon's run slice, its rings,
+// ring ids, fp32 segment boxes and slab lists staged in LDS as in ppoly_eval.  The slice is
+// ordered by y slab in LDS first (counting sort, 64 bins), so the lanes of a wave mostly walk
+// the same crossing and distance lists (equal trip counts, broadcast LDS reads).
+__global__ __launch_bounds__(kTB) void ppoly_cand_eval(CandGroup c, const PolyDev* __restrict__ polys,
+                                                       const double* __restrict__ vx, const double* __restrict__ vy,
+                                                       const ring_id_t* __restrict__ vring,
+                                                       const double* __restrict__ renv,
+                                                       const uint16_t* __restrict__ slabs, double r, StreamOut o) {
+    __shared__ double lvx[kMaxLdsVerts];
+    __shared__ double lvy[kMaxLdsVerts];
+    __shared__ ring_id_t lvr[kMaxLdsVerts];
+    __shared__ float4 lsb[kMaxLdsVerts];
+    __shared__ uint16_t lsl[kMaxLdsSlab];
+    __shared__ uint2 pbuf[kTB / kWave][kSPairs];
+    __shared__ double lqx[kCandItem], lqy[kCandItem];
+    __shared__ unsigned lqi[kCandItem];
+    __shared__ unsigned scnt[64];
+    constexpr unsigned kPer = kCandItem / kTB;
+    const int wid = threadIdx.x / kWave, lane = lane_id();
+    uint2* pb = pbuf[wid];
+    unsigned pc = 0;
+    const unsigned ni = *c.nitems;
+    for (unsigned it = blockIdx.x; it < ni; it += gridDim.x) {
+        const uint4 w = c.items[it];
+        const unsigned poly = w.x, m = w.z - w.y;
+        const PolyDev P = polys[poly];
+        const bool v_lds = P.nv <= (uint32_t)kMaxLdsVerts;
+        const bool s_lds = P.llen <= (uint32_t)kMaxLdsSlab;
+        const bool holes = P.nring > 1;
+        __syncthreads();  // the previous item's LDS reads are done
+        if (v_lds)
+            for (uint32_t t = threadIdx.x; t < P.nv; t += kTB) {
+                lvx[t] = vx[P.voff + t];
+                lvy[t] = vy[P.voff + t];
+                if (holes) lvr[t] = vring[P.voff + t];
+                else lsb[t] = seg_box32(vx + P.voff, vy + P.voff, t, P.nv, P.gb[0], P.gb[1]);
+            }
+        if (s_lds)
+            for (uint32_t t = threadIdx.x; t < P.llen; t += kTB) lsl[t] = slabs[P.loff + t];
+        if (threadIdx.x < 64) scnt[threadIdx.x] = 0;
+        // the slice (<= kCandItem) in registers, its slab histogram in LDS
+        double qx[kPer], qy[kPer];
+        unsigned qi[kPer], qs[kPer];
+#pragma unroll
+        for (unsigned u = 0; u < kPer; u++) {
+            const unsigned t = threadIdx.x + u * kTB;
+            qs[u] = 0;
+            if (t < m) {
+                qx[u] = c.sx[w.y + t];
+                qy[u] = c.sy[w.y + t];
+                qi[u] = c.sidx[w.y + t];
+                if (P.ns) qs[u] = slab_of(qy[u], P.sy0, P.sinv, P.ns);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (unsigned u = 0; u < kPer; u++)
+            if (threadIdx.x + u * kTB < m) atomicAdd(&scnt[qs[u]], 1u);
+        __syncthreads();
+        if (threadIdx.x < kWave) {  // exclusive scan of the 64 bins: slab starts
+            const unsigned v = scnt[threadIdx.x];
+            scnt[threadIdx.x] = wave_incl_scan(v) - v;
+        }
+        __syncthreads();
+#pragma unroll
+        for (unsigned u = 0; u < kPer; u++)
+            if (threadIdx.x + u * kTB < m) {
+                const unsigned at = atomicAdd(&scnt[qs[u]], 1u);
+                lqx[at] = qx[u];
+                lqy[at] = qy[u];
+                lqi[at] = qi[u];
+            }
+        __syncthreads();
+        const double* rvx = v_lds ? lvx : vx + P.voff;
+        const double* rvy = v_lds ? lvy : vy + P.voff;
+        const ring_id_t* rvr = v_lds ? lvr : vring + P.voff;
+        const double* rre = renv + 4 * (size_t)P.eoff;
+        const SlabView sv{s_lds ? lsl : slabs + P.loff, P.ns};
+        for (unsigned b = (unsigned)wid * kWave; b < m; b += kTB) {
+            const unsigned i = b + (unsigned)lane;
+            bool in = false;
+            unsigned pid = 0;
+            if (i < m) {
+                const double px = lqx[i], py = lqy[i];
+                pid = lqi[i];
+                in = holes ? point_polygon_within_rings(px, py, rvx, rvy, rvr, rre, P, sv, r)
+                           : point_polygon_within(px, py, rvx, rvy, P, sv, r, v_lds ? lsb : nullptr);
+            }
+            spairs_push(pb, pc, in, poly, pid, o);
+        }
+    }
+    if (pc) spairs_flush(pb, pc, o);
+}
+
 // ============================================================ point-polygon kNN ===========
 // PointPolygonKNNQuery window body (PointPolygonKNNQuery.java:162-236): candidates = points of
 // the polygon's G u C cells; key = (distance bits, window index), distance = JTS
@@ -3216,6 +3811,16 @@ struct PolyCache {
     std::vector<uint32_t> hcls;  // per-cell class words (classify_cells), PolyDev.cls offsets into it
     std::vector<uint32_t> keep;  // cells of any polygon's G or C rectangles (empty: no filter)
     bool any_outside = false;
+    // streaming path (ppoly_stream): per key cell its polygon entries, the cells holding any
+    // (bitmap), the polygons whose rectangles reach outside the grid; stream_ok = false when the
+    // key space or the table is too large (the tile-binned path runs instead)
+    bool stream_ok = false;
+    std::vector<uint32_t> cell_off;   // nb * nb + 1 (host only)
+    std::vector<uint32_t> cell_ent;   // 2 per entry: poly | kEntC, class word
+    std::vector<uint32_t> cell_head;  // 2 per cell (see kMulti)
+    std::vector<uint32_t> skeep;
+    std::vector<uint32_t> opoly;
+    uint64_t last_cand = 0;           // candidates of the previous step (sizes the buffer)
     void* dev_blob = nullptr;  // J_POLY buffer holding the uploaded tables
     size_t blob_bytes = 0;
 };
@@ -3271,6 +3876,87 @@ static void ring_tables(const PolyPlan& pl, std::vector<ring_id_t>& vr, std::vec
             gb[2] = std::max(gb[2], mxx); gb[3] = std::max(gb[3], mxy);
         }
     }
+}
+
+// The streaming path's cell table (see ppoly_stream): for every polygon and every cell of its
+// walk region in one of its rectangles, one entry -- G (its G list, or r = MAX_VALUE) or C with
+// the cell's class word (0 = every subcell mixed when the polygon has no classes); C cells of
+// class kClsMiss hold no point within r and get no entry.
+void build_stream_table(PolyCache& c, uint32_t npoly, int32_t nb, bool r_is_max) {
+    c.stream_ok = false;
+    c.cell_off.clear();
+    c.cell_ent.clear();
+    c.cell_head.clear();
+    c.skeep.clear();
+    c.opoly.clear();
+    if (nb <= 0 || (uint64_t)nb * (uint64_t)nb > (1ull << 24)) return;
+    const size_t ncell = (size_t)nb * (size_t)nb;
+    auto in_list = [&](uint32_t off, uint32_t n, int32_t cx, int32_t cy) {
+        for (uint32_t q = 0; q < n; q++) {
+            const int32_t* R = &c.hrects[4 * (size_t)(off + q)];
+            if (cx >= R[0] && cx <= R[1] && cy >= R[2] && cy <= R[3]) return true;
+        }
+        return false;
+    };
+    // pass 0 counts per cell, pass 1 fills
+    std::vector<uint32_t> cur;
+    for (int pass = 0; pass < 2; pass++) {
+        if (pass == 0) c.cell_off.assign(ncell + 1, 0u);
+        for (uint32_t p = 0; p < npoly; p++) {
+            const PolyDev& P = c.pd[p];
+            if (P.wx0 > P.wx1 || P.wy0 > P.wy1) continue;
+            const int32_t ch = P.wy1 - P.wy0 + 1;
+            for (int32_t cx = P.wx0; cx <= P.wx1; cx++)
+                for (int32_t cy = P.wy0; cy <= P.wy1; cy++) {
+                    const bool g = in_list(P.goff, P.ng, cx, cy);
+                    const bool cc = !g && in_list(P.coff, P.nc, cx, cy);
+                    if (!g && !cc) continue;
+                    uint32_t ex = p, word = 0;
+                    if (cc && !r_is_max) {
+                        if (P.cls != kNoCls) word = c.hcls[P.cls + (size_t)(cx - P.wx0) * ch + (cy - P.wy0)];
+                        if (word == kWordMiss) continue;
+                        ex |= kEntC;
+                    }
+                    const size_t k = (size_t)cx * nb + cy;
+                    if (pass == 0) {
+                        c.cell_off[k + 1]++;
+                    } else {
+                        const uint32_t at = cur[k]++;
+                        c.cell_ent[2 * (size_t)at] = ex;
+                        c.cell_ent[2 * (size_t)at + 1] = word;
+                    }
+                }
+        }
+        if (pass == 0) {
+            for (size_t k = 0; k < ncell; k++) c.cell_off[k + 1] += c.cell_off[k];
+            if (c.cell_off[ncell] >= (1u << 28)) {
+                c.cell_off.clear();
+                return;
+            }
+            c.cell_ent.assign(2 * (size_t)c.cell_off[ncell], 0u);
+            cur.assign(c.cell_off.begin(), c.cell_off.end() - 1);
+        }
+    }
+    // packed stage words; LDS per-polygon counts; entry words (bits 30, 31 are flags)
+    if (npoly >= kStreamMaxPolys || npoly > kCandLdsPolys || c.cell_off[ncell] >= kMulti) return;
+    c.skeep.assign((ncell + 31) / 32, 0u);
+    c.cell_head.assign(2 * ncell, 0u);
+    for (size_t k = 0; k < ncell; k++) {
+        const uint32_t b = c.cell_off[k], e = c.cell_off[k + 1];
+        c.cell_head[2 * k] = kNoEntry;
+        if (e == b) continue;
+        c.skeep[k >> 5] |= 1u << (k & 31);
+        if (e - b == 1) {
+            c.cell_head[2 * k] = c.cell_ent[2 * (size_t)b];
+            c.cell_head[2 * k + 1] = c.cell_ent[2 * (size_t)b + 1];
+        } else {
+            c.cell_head[2 * k] = kMulti | (e - b);
+            c.cell_head[2 * k + 1] = b;
+        }
+    }
+    for (uint32_t p = 0; p < npoly; p++)
+        if (c.pd[p].outside) c.opoly.push_back(p);
+    c.stream_ok = true;
 }
 
 int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, int join, const double* x,
@@ -3393,6 +4079,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
                 }
             }
         }
+        build_stream_table(fresh, npoly, nb, r >= 1.7976931348623157e308);
         fresh.grid = *grid;
         fresh.gq = *gq;
         fresh.jmode = jmode;
@@ -3434,7 +4121,12 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     const size_t off_k = (off_s + sz_s + 15) & ~(size_t)15;
     const size_t off_vr = (off_k + sz_k + 15) & ~(size_t)15;
     const size_t off_cl = (off_vr + sz_vr + 15) & ~(size_t)15, sz_cl = hcls.size() * 4;
-    const size_t blob_end = off_cl + sz_cl;
+    // streaming-path tables (empty unless stream_ok)
+    const size_t off_co = (off_cl + sz_cl + 15) & ~(size_t)15, sz_co = pc->cell_head.size() * 4;
+    const size_t off_ce = (off_co + sz_co + 15) & ~(size_t)15, sz_ce = pc->cell_ent.size() * 4;
+    const size_t off_sk = (off_ce + sz_ce + 15) & ~(size_t)15, sz_sk = pc->skeep.size() * 4;
+    const size_t off_op = (off_sk + sz_sk + 15) & ~(size_t)15, sz_op = pc->opoly.size() * 4;
+    const size_t blob_end = off_op + sz_op;
     void* pblob = nullptr;
     rc = ctx_ensure(ctx, J_POLY, blob_end + 64, &pblob);
     if (rc) return rc;
@@ -3450,6 +4142,10 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     double* denv = reinterpret_cast<double*>(bp + off_e);
     ring_id_t* dvr = reinterpret_cast<ring_id_t*>(bp + off_vr);
     uint32_t* dcls = reinterpret_cast<uint32_t*>(bp + off_cl);
+    uint2* dchead = reinterpret_cast<uint2*>(bp + off_co);
+    uint2* dcent = reinterpret_cast<uint2*>(bp + off_ce);
+    unsigned* dskeep = reinterpret_cast<unsigned*>(bp + off_sk);
+    uint32_t* dopoly = reinterpret_cast<uint32_t*>(bp + off_op);
     if (upload) {
         pc->dev_blob = nullptr;  // until the copies are issued
         if ((sz_p && hipMemcpyAsync(dpoly, pd.data(), sz_p, hipMemcpyHostToDevice, st) != hipSuccess) ||
@@ -3461,10 +4157,121 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             (sz_k && hipMemcpyAsync(dkeep, keep.data(), sz_k, hipMemcpyHostToDevice, st) != hipSuccess) ||
             (sz_e && hipMemcpyAsync(denv, henv.data(), sz_e, hipMemcpyHostToDevice, st) != hipSuccess) ||
             (sz_vr && hipMemcpyAsync(dvr, hvr.data(), sz_vr, hipMemcpyHostToDevice, st) != hipSuccess) ||
-            (sz_cl && hipMemcpyAsync(dcls, hcls.data(), sz_cl, hipMemcpyHostToDevice, st) != hipSuccess))
+            (sz_cl && hipMemcpyAsync(dcls, hcls.data(), sz_cl, hipMemcpyHostToDevice, st) != hipSuccess) ||
+            (sz_co && hipMemcpyAsync(dchead, pc->cell_head.data(), sz_co, hipMemcpyHostToDevice, st) != hipSuccess) ||
+            (sz_ce && hipMemcpyAsync(dcent, pc->cell_ent.data(), sz_ce, hipMemcpyHostToDevice, st) != hipSuccess) ||
+            (sz_sk && hipMemcpyAsync(dskeep, pc->skeep.data(), sz_sk, hipMemcpyHostToDevice, st) != hipSuccess) ||
+            (sz_op && hipMemcpyAsync(dopoly, pc->opoly.data(), sz_op, hipMemcpyHostToDevice, st) != hipSuccess))
             return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "polygon upload failed");
         pc->dev_blob = pblob;
         pc->blob_bytes = blob_end;
+    }
+    static const int force_tiles = getenv("GEOHIP_PPOLY_TILES") ? atoi(getenv("GEOHIP_PPOLY_TILES")) : 0;  // A/B only
+    if (pc->stream_ok && !force_tiles) {
+        unsigned* out = nullptr;
+        if (cap) {
+            if (dev) {
+                out = out_pairs;
+            } else {
+                void* p = nullptr;
+                rc = ctx_ensure(ctx, J_OUT, cap * 8, &p);
+                if (rc) return rc;
+                out = reinterpret_cast<unsigned*>(p);
+            }
+        }
+        const bool cands = !approximate && jmode != 2;
+        uint64_t ccap = std::max<uint64_t>(std::max<uint64_t>(65536, n / 16), pc->last_cand + pc->last_cand / 4);
+        uint64_t tot = 0;
+        const uint64_t nchunks = (n + kStreamChunk - 1) / kStreamChunk;
+        for (int attempt = 0; attempt < 3; attempt++) {
+            // J_MISC: [0..1] pair total, [2..3] candidate total, [4] work items
+            unsigned* misc = S.get<unsigned>(J_MISC, kMiscWords * 4);
+            unsigned* mat = cands ? S.get<unsigned>(J_HIST, (size_t)kCandGroups * npoly * 4 + 16) : nullptr;
+            void* cbuf = cands ? S.get<void>(J_SY, ccap * 24 + 64) : nullptr;
+            void* sbuf = cands ? S.get<void>(J_SX, ccap * 20 + 64) : nullptr;
+            uint4* items = cands ? S.get<uint4>(J_SKEY, (ccap / kCandItem + npoly + 1) * sizeof(uint4)) : nullptr;
+            if (S.rc) return S.rc;
+            hipEvent_t e0, e1;
+            ctx_timing_events(ctx, &e0, &e1);
+            if (e0) hipEventRecord(e0, st);  // the whole device step
+            if (hipMemsetAsync(misc, 0, 32, st) != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
+            StreamOut so;
+            so.out = out;
+            so.cap = out ? cap : 0;
+            so.aligned8 = ((uintptr_t)out & 7u) == 0;
+            so.swap = join ? 1 : 0;
+            so.totals = reinterpret_cast<unsigned long long*>(misc);
+            so.ccap = cands ? ccap : 0;
+            char* cb = reinterpret_cast<char*>(cbuf);
+            so.cpoly = cands ? reinterpret_cast<unsigned*>(cb) : nullptr;
+            so.cidx = cands ? reinterpret_cast<unsigned*>(cb + ccap * 4) : nullptr;
+            so.cx = cands ? reinterpret_cast<double*>(cb + ccap * 8) : nullptr;
+            so.cy = cands ? reinterpret_cast<double*>(cb + ccap * 16) : nullptr;
+            StreamArgs sa;
+            sa.x = dx;
+            sa.y = dy;
+            sa.n = n;
+            sa.g = geo;
+            sa.keep = sz_sk ? dskeep : nullptr;
+            sa.keep_words = (unsigned)pc->skeep.size();
+            sa.head = dchead;
+            sa.ent = dcent;
+            sa.polys = dpoly;
+            sa.opoly = dopoly;
+            sa.nopoly = (uint32_t)pc->opoly.size();
+            sa.rects = drects;
+            sa.jmode = jmode;
+            sa.r = r;
+            sa.o = so;
+            if (nchunks) {
+                const unsigned nblk = (unsigned)std::min<uint64_t>(nchunks, (uint64_t)ctx_cus(ctx) * kStreamBlocksPerCU);
+                if (approximate) ppoly_stream<true><<<nblk, kStreamNW * kWave, 0, st>>>(sa);
+                else ppoly_stream<false><<<nblk, kStreamNW * kWave, 0, st>>>(sa);
+            }
+            if (cands) {
+                char* sb = reinterpret_cast<char*>(sbuf);
+                CandGroup cg;
+                cg.ccount = so.totals + 1;
+                cg.ccap = ccap;
+                cg.cpoly = so.cpoly;
+                cg.cidx = so.cidx;
+                cg.cx = so.cx;
+                cg.cy = so.cy;
+                cg.mat = mat;
+                cg.npoly = npoly;
+                cg.items = items;
+                cg.nitems = misc + 4;
+                cg.sidx = reinterpret_cast<unsigned*>(sb);
+                cg.sx = reinterpret_cast<double*>(sb + ((ccap * 4 + 15) & ~(uint64_t)15));
+                cg.sy = cg.sx + ccap;
+                ppoly_cand_hist<<<kCandGroups, kCandThreads, 0, st>>>(cg);
+                ppoly_cand_plan<<<1, kCandThreads, 0, st>>>(cg);
+                ppoly_cand_scatter<<<kCandGroups, kCandThreads, 0, st>>>(cg);
+                ppoly_cand_eval<<<kEvalBlocks, kTB, 0, st>>>(cg, dpoly, dvx, dvy, dvr, denv, dslab, r, so);
+            }
+            if (e1) hipEventRecord(e1, st);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, std::string("ppoly stream launch: ") + hipGetErrorString(e));
+            uint64_t* pin = ctx_pinned(ctx);
+            if (hipMemcpyAsync(pin, misc, 32, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+                return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "count readback failed");
+            tot = pin[0];
+            const uint64_t ncand = pin[1];
+            pc->last_cand = ncand;
+            if (prof) fprintf(stderr, "ppoly stream: %llu pairs, %llu candidates (capacity %llu)\n",
+                              (unsigned long long)tot, (unsigned long long)ncand, (unsigned long long)ccap);
+            if (ncand <= ccap) break;
+            if (attempt == 2) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "candidate buffer did not converge");
+            ccap = ncand + ncand / 4 + 1024;  // grown to the counted need: the step runs again
+        }
+        *out_count = tot;
+        if (!dev && cap) {
+            const uint64_t m = std::min<uint64_t>(tot, cap);
+            if (m && hipMemcpy(out_pairs, out, m * 8, hipMemcpyDeviceToHost) != hipSuccess)
+                return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "pair readback failed");
+        }
+        if (tot > cap) return ctx_fail(ctx, GEOHIP_ERR_CAPACITY, "output capacity too small; *out_count = required");
+        return GEOHIP_OK;
     }
     hipEvent_t e0, e1;
     ctx_timing_events(ctx, &e0, &e1);

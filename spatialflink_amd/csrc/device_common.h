@@ -301,4 +301,55 @@ __device__ __forceinline__ KE wave_list_get(const WList<KPL>& L, int e) {  // e 
     return o;
 }
 
+// ---------------------------------------------------------------- decoupled look-back -----
+// Status word of a chunk processed in ticket order: (epoch << 42) | kPrefixBit? | value, value =
+// the chunk's own count (aggregate) or, with kPrefixBit, the counts of every chunk up to and
+// including it (inclusive prefix).  Words of an earlier launch carry another epoch: not ready.
+// (The ingest record bases and the streaming point-polygon pair / candidate offsets.)
+constexpr unsigned long long kPrefixBit = 1ull << 41;
+constexpr unsigned long long kValueMask = kPrefixBit - 1;
+
+__device__ __forceinline__ void publish_status(unsigned long long* w, unsigned long long v) {
+    // an atomic exchange is performed at the device coherence point: the other XCDs' polling
+    // loads see it at once (a plain store may sit in this XCD's L2)
+    (void)__hip_atomic_exchange(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One wave: the sum of the counts of the chunks before vb.  Lane l inspects chunk j - l; the
+// window of 64 is consumed up to its nearest inclusive prefix (or entirely), once every word in
+// that span is ready.  Chunks start in ticket order, so every chunk waited on is resident or
+// done.  A wait past kLookbackSpins polls (seconds: a broken invariant, never a slow chunk) sets
+// *fault and returns, so a bug ends the kernel with an error instead of hanging the device.
+constexpr unsigned kLookbackSpins = 1u << 22;
+__device__ __forceinline__ unsigned long long lookback_prefix(const unsigned long long* status, unsigned vb,
+                                                              unsigned long long epoch, unsigned* fault) {
+    const int lane = lane_id();
+    unsigned long long excl = 0;
+    long long j = (long long)vb - 1;
+    unsigned spins = 0;
+    while (j >= 0) {
+        const long long t = j - lane;
+        unsigned long long v = t >= 0 ? __hip_atomic_load(status + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                      : (epoch << 42) | kPrefixBit;  // before chunk 0: prefix 0
+        const bool ready = (v >> 42) == epoch;
+        const unsigned long long pm = __ballot(ready && (v & kPrefixBit));
+        const unsigned long long span = pm ? (2ull << __builtin_ctzll(pm)) - 1ull : ~0ull;  // lanes 0 .. first prefix
+        if (__ballot(!ready) & span) {
+            if (++spins > kLookbackSpins) {
+                if (lane == 0) *fault = 1u;
+                return excl;
+            }
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        unsigned long long c = ((span >> lane) & 1ull) ? (v & kValueMask) : 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+        excl += c;
+        if (pm) break;
+        j -= kWave;
+    }
+    return excl;
+}
+
 }  // namespace geohip

@@ -29,7 +29,8 @@ inline uint64_t ingest_chunks(uint64_t nbytes) { return (nbytes + kIngestChunk -
 // Chunk-order look-back state: status[nchunks] words (any content before the first launch),
 // a ticket word (zero before the first launch; the last chunk re-arms it), the launch's epoch
 // (1 .. 2^22 - 1, new per launch); the chunks left to the general grammar: listed[nchunks]
-// (chunk, record base) and their count *nlisted (zero before the launch).
+// (chunk, record base) and their count *nlisted (zero before the launch); nlisted[1] = 1 when a
+// look-back gave up (zero before the launch).
 struct IngestLookback {
     unsigned long long* status;
     unsigned* ticket;

@@ -302,47 +302,6 @@ __device__ __forceinline__ int swar_csv(const uint8_t* __restrict__ s, uint32_t 
     return kSwarNo;
 }
 
-// Decoupled look-back status word of a chunk: (epoch << 42) | kPrefixBit? | value, value = the
-// chunk's record count (aggregate) or, with kPrefixBit, the records of every chunk up to and
-// including it (inclusive prefix).  Words of an earlier launch carry another epoch: not ready.
-constexpr unsigned long long kPrefixBit = 1ull << 41;
-constexpr unsigned long long kValueMask = kPrefixBit - 1;
-
-__device__ __forceinline__ void publish_status(unsigned long long* w, unsigned long long v) {
-    // an atomic exchange is performed at the device coherence point: the other XCDs' polling
-    // loads see it at once (a plain store may sit in this XCD's L2)
-    (void)__hip_atomic_exchange(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// One wave: records of the chunks before vb.  Lane l inspects chunk j - l; the window of 64
-// is consumed up to its nearest inclusive prefix (or entirely), once every word in that span is
-// ready.  Chunks start in ticket order, so every chunk waited on is resident or done.
-__device__ __forceinline__ unsigned long long lookback_prefix(const unsigned long long* status, unsigned vb,
-                                                              unsigned long long epoch) {
-    const int lane = lane_id();
-    unsigned long long excl = 0;
-    long long j = (long long)vb - 1;
-    while (j >= 0) {
-        const long long t = j - lane;
-        unsigned long long v = t >= 0 ? __hip_atomic_load(status + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                      : (epoch << 42) | kPrefixBit;  // before chunk 0: prefix 0
-        const bool ready = (v >> 42) == epoch;
-        const unsigned long long pm = __ballot(ready && (v & kPrefixBit));
-        const unsigned long long span = pm ? (2ull << __builtin_ctzll(pm)) - 1ull : ~0ull;  // lanes 0 .. first prefix
-        if (__ballot(!ready) & span) {
-            __builtin_amdgcn_s_sleep(2);
-            continue;
-        }
-        unsigned long long c = ((span >> lane) & 1ull) ? (v & kValueMask) : 0ull;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-        excl += c;
-        if (pm) break;
-        j -= kWave;
-    }
-    return excl;
-}
-
 // Stage chunk vb (+ the tail) in LDS and list the record starts it owns, in order: byte 0 of the
 // batch, then q + 1 for each '\n' at q.  Returns the chunk's record count (block-uniform).
 struct ChunkLds {
@@ -441,7 +400,7 @@ __global__ __launch_bounds__(kThreads) void ingest_fused(const uint8_t* __restri
         }
         if (r == 0) {  // the record base: look-back by wave 0, behind its first round's parse
             if (threadIdx.x < kWave) {
-                const unsigned long long excl = vb == 0 ? 0ull : lookback_prefix(lb.status, vb, lb.epoch);
+                const unsigned long long excl = vb == 0 ? 0ull : lookback_prefix(lb.status, vb, lb.epoch, lb.nlisted + 1);
                 if (threadIdx.x == 0) {
                     if (vb != 0) publish_status(lb.status + vb, tag | kPrefixBit | (excl + nrec));
                     s_base = excl;

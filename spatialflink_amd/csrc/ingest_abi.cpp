@@ -123,12 +123,13 @@ int geohip_ingest_points(geohip_ctx* ctx, const geohip_grid* grid, const geohip_
     hipEvent_t e0, e1;
     ctx_timing_events(ctx, &e0, &e1);
     const IngestLookback lb{static_cast<unsigned long long*>(status), reinterpret_cast<unsigned*>(w + 1),
-                            ctx_next_ingest_epoch(ctx), static_cast<ulonglong2*>(list), reinterpret_cast<unsigned*>(w + 3)};
+                            ctx_next_epoch(ctx), static_cast<ulonglong2*>(list), reinterpret_cast<unsigned*>(w + 3)};
     hipError_t e = launch_ingest(dtext, nbytes, a, lb, w, dx, dy, dts, dcell, cap, w + 2, st, e0, e1);
     if (e != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, std::string("ingest launch: ") + hipGetErrorString(e));
     uint64_t* pinned = ctx_pinned(ctx);
-    ICHK(hipMemcpyAsync(pinned, w, 24, hipMemcpyDeviceToHost, st));
+    ICHK(hipMemcpyAsync(pinned, w, 32, hipMemcpyDeviceToHost, st));
     ICHK(hipStreamSynchronize(st));
+    if (pinned[3] >> 32) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "ingest: record-base look-back gave up");
     const uint64_t total = pinned[0], bad = pinned[2] ? ~pinned[2] : UINT64_MAX;
     *out_count = total;
     *out_bad = bad;

@@ -13,7 +13,8 @@ int ctx_fail(geohip_ctx* ctx, int code, const std::string& msg);
 int ctx_ensure(geohip_ctx* ctx, int slot, size_t bytes, void** out);  // slot 0..25
 int ctx_ensure_ingest(geohip_ctx* ctx, int slot, size_t bytes, void** out);  // slot 0..7
 int ctx_ensure_ingest_zeroed(geohip_ctx* ctx, int slot, size_t bytes, void** out);  // zeroed when (re)allocated
-unsigned long long ctx_next_ingest_epoch(geohip_ctx* ctx);  // 1 .. 2^22 - 1, new per call
+unsigned long long ctx_next_epoch(geohip_ctx* ctx);  // look-back epoch: 1 .. 2^22 - 1, new per call
+int ctx_cus(geohip_ctx* ctx);                       // compute units of the ctx's device
 int ctx_begin(geohip_ctx* ctx);  // clears the error, selects the ctx's device
 hipStream_t ctx_stream(geohip_ctx* ctx);
 int ctx_mem(geohip_ctx* ctx);

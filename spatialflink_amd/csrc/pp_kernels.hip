@@ -2268,8 +2268,11 @@ hipError_t launch_range(const double* x, const double* y, uint64_t n, const Rang
         const unsigned nblocks = (unsigned)((units + upb - 1) / upb);
         const RangeLookback lb{lb_status, lb_ticket, epoch};
         if (ev0) (void)hipEventRecord(ev0, st);
+#ifndef GEOHIP_RANGE_MODE
+#define GEOHIP_RANGE_MODE 0  // measurement builds only (range_fused MODE)
+#endif
         if (approximate) range_fused<true><<<nblocks, kRangeNW * kWave, 0, st>>>(x, y, n, a, upb, lb, out, cap, total);
-        else range_fused<false><<<nblocks, kRangeNW * kWave, 0, st>>>(x, y, n, a, upb, lb, out, cap, total);
+        else range_fused<false, GEOHIP_RANGE_MODE><<<nblocks, kRangeNW * kWave, 0, st>>>(x, y, n, a, upb, lb, out, cap, total);
         if (ev1) (void)hipEventRecord(ev1, st);
         return hipGetLastError();
     }
