@@ -1829,17 +1829,23 @@ __global__ __launch_bounds__(kTB) void ppoly_outside(const double* __restrict__ 
 constexpr uint32_t kEntC = 0x80000000u;    // entry.x: C cell (class word in entry.y); else G
 constexpr int kStreamNW = 8;               // waves per block
 constexpr unsigned kStreamPts = 256;       // points per wave iteration (4 per lane)
-constexpr unsigned kStreamChunk = 8192;    // points per chunk (4 iterations per wave)
-constexpr unsigned kStreamBlocksPerCU = 2;
-constexpr unsigned kSPairCap = 8192;       // block-staged pairs per chunk (4 B each: poly << 13 | point)
-constexpr unsigned kSCandCap = 1024;       // block-staged candidates per chunk
-constexpr unsigned kLocalBits = 13;        // point within its chunk
+#ifndef GEOHIP_PS_CHUNK_BITS
+#define GEOHIP_PS_CHUNK_BITS 12  // 2 iterations per wave: 13 (4) spilled 33 VGPRs in the two-phase chunk
+#endif
+constexpr unsigned kStreamChunk = 1u << GEOHIP_PS_CHUNK_BITS;  // points per chunk
+#ifndef GEOHIP_PS_BPC
+#define GEOHIP_PS_BPC 2
+#endif
+constexpr unsigned kStreamBlocksPerCU = GEOHIP_PS_BPC;  // resident blocks per CU (LDS, registers)
+constexpr unsigned kSPairCap = kStreamChunk;      // block-staged pairs per chunk (4 B each: poly << 13 | point)
+constexpr unsigned kSCandCap = kStreamChunk / 8;  // block-staged candidates per chunk
+constexpr unsigned kLocalBits = GEOHIP_PS_CHUNK_BITS;  // point within its chunk
 constexpr uint32_t kStreamMaxPolys = 1u << (32 - kLocalBits);
 constexpr unsigned kCandItem = 1024;       // candidates per evaluation work item
 constexpr unsigned kCandLdsPolys = 16384;  // polygons whose per-polygon counters fit LDS
 constexpr unsigned kEvalBlocks = 1024;     // grid of the evaluation pass (strides over its items)
 static_assert(kStreamChunk == (1u << kLocalBits), "chunk-local point ids");
-static_assert(kStreamChunk == kStreamNW * 4 * kStreamPts, "chunk = waves x iterations x points");
+static_assert(kStreamChunk % (kStreamNW * kStreamPts) == 0, "chunk = waves x iterations x points");
 
 // A cell's table head (8 B, one gather per point): x == kNoEntry -- no entry; x & kMulti -- x's
 // low 30 bits entries at cell_ent[y ...]; else the cell's only entry (x = poly | kEntC?, y = its
@@ -1921,8 +1927,8 @@ __device__ __forceinline__ void stream_push(const StreamArgs& a, StreamSink& k, 
     const unsigned long long m = __ballot(hit);
     if (!m || GEOHIP_PS_ABL == 1) return;
     unsigned b = 0;
-    if (lane_id() == 0) b = atomicAdd(k.cursor, (unsigned)__popcll(m));
-    b = (unsigned)__shfl((int)b, 0) + lanes_below(m);
+    if (lane_id() == 0) b = atomicAdd(k.cursor, (unsigned)__popcll(m));  // every lane is active here
+    b = (unsigned)__builtin_amdgcn_readfirstlane((int)b) + lanes_below(m);
     if (!hit) return;
     if (k.direct) {
         if (CAND) stream_emit_cand(a, k.base + b, poly, (unsigned)(chunk0 + loc));
@@ -1932,12 +1938,15 @@ __device__ __forceinline__ void stream_push(const StreamArgs& a, StreamSink& k, 
     }
 }
 
-// One chunk's points (all waves of the block): their cells, table heads and entries.  A wave's
-// next iteration's coordinates load while the current one is decided (a two-deep pipeline that
-// also held the next table heads in flight spilled registers and measured slower: 630 -> 720 us).
-template <bool APPROX>
-__device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned* kl, bool kl_ok, uint64_t c0,
-                                             uint64_t c1, StreamSink& ps, StreamSink& cs) {
+// One chunk's points (all waves of the block).  Phase A: every point of the wave's iterations --
+// coordinates (next iteration's in flight), cell, subcell, and its table head gather issued;
+// phase B: the entries, with all the wave's heads already in flight from phase A (a head gather
+// per iteration waited on at once cost ~1 us of latency per iteration under the streaming
+// traffic).  Phase B needs no coordinates except for the approximate bbox test and the rare
+// out-of-grid polygons (reloaded).
+template <bool APPROX, bool KL>
+__device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned* kl, uint64_t c0, uint64_t c1,
+                                             StreamSink& ps, StreamSink& cs) {
     const int wid = threadIdx.x / kWave, lane = lane_id();
     const TileGeom& g = a.g;
     const unsigned nb = (unsigned)g.nb;
@@ -1961,46 +1970,59 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
             }
         }
     };
+    auto loc_of = [&](unsigned t, int s) {
+        return (t * kStreamNW + (unsigned)wid) * kStreamPts + 2u * (unsigned)lane + (unsigned)(s & 1) +
+               128u * (unsigned)(s >> 1);
+    };
+    // point state for phase B: bits 0-3 subcell (4 sx + sy), 4 NaN coordinate, 5 outside the grid
+    constexpr unsigned kNanBit = 16u, kOutBit = 32u;
+    uint2 hd[kIters][4];
+    unsigned st[kIters];  // one byte per point
     double nx[4], ny[4];
     load(0, nx, ny);
-#pragma unroll 1
+#pragma unroll
     for (unsigned t = 0; t < kIters; t++) {
-        double cxv[4], cyv[4];
+        double qx[4], qy[4];
 #pragma unroll
         for (int s = 0; s < 4; s++) {
-            cxv[s] = nx[s];
-            cyv[s] = ny[s];
+            qx[s] = nx[s];
+            qy[s] = ny[s];
         }
         if (t + 1 < kIters) load(t + 1, nx, ny);
-        const unsigned lb = (t * kStreamNW + (unsigned)wid) * kStreamPts + 2u * (unsigned)lane;
-        const unsigned loc[4] = {lb, lb + 1, lb + 128, lb + 129};
-        uint2 h[4];
-        int32_t ccx[4], ccy[4];
-        bool outside[4];
 #pragma unroll
         for (int s = 0; s < 4; s++) {
-            const bool v = c0 + loc[s] < c1;
+            const bool v = c0 + loc_of(t, s) < c1;
             int32_t cx = 0, cy = 0;
-            const bool in = v && point_cell(g, cxv[s], cyv[s], cx, cy);
-            outside[s] = v && !in;
-            ccx[s] = cx;
-            ccy[s] = cy;
-            h[s] = make_uint2(kNoEntry, 0u);
+            const bool in = v && point_cell(g, qx[s], qy[s], cx, cy);
+            const bool nan = !(qx[s] == qx[s] && qy[s] == qy[s]);
+            unsigned w = (nan ? kNanBit : 0u) | ((v && !in) ? kOutBit : 0u);
+            hd[t][s] = make_uint2(kNoEntry, 0u);
             if (in) {
                 const unsigned key = (unsigned)cx * nb + (unsigned)cy;
                 bool has = true;
-                if (a.keep) has = ((kl_ok ? kl[key >> 5] : a.keep[key >> 5]) >> (key & 31u)) & 1u;
-                if (has && GEOHIP_PS_ABL != 2) h[s] = a.head[key];
-                if (GEOHIP_PS_ABL == 2 && has && key == 0xfffffffu) h[s].x = 0;
+                if (KL) has = (kl[key >> 5] >> (key & 31u)) & 1u;
+                else if (a.keep) has = (a.keep[key >> 5] >> (key & 31u)) & 1u;
+                if (has && GEOHIP_PS_ABL != 2) hd[t][s] = a.head[key];
+                if (GEOHIP_PS_ABL == 2 && has && key == 0xfffffffu) hd[t][s].x = 0;
+                if (has && !nan && !APPROX)
+                    w |= (unsigned)(4 * sub_of(qx[s], g.mnx, g.l, cx) + sub_of(qy[s], g.mny, g.l, cy));
             }
+            st[t] = s == 0 ? w : (st[t] | (w << (8 * s)));
         }
+    }
+#pragma unroll
+    for (unsigned t = 0; t < kIters; t++) {
+        double qx[4] = {0.0, 0.0, 0.0, 0.0}, qy[4] = {0.0, 0.0, 0.0, 0.0};
+        const bool any_out = __ballot((st[t] & (kOutBit * 0x01010101u)) != 0) != 0;
+        if (APPROX || (a.nopoly && any_out)) load(t, qx, qy);  // reloaded (L2): bbox test, outside points
 #pragma unroll
         for (int s = 0; s < 4; s++) {
-            const double qx = cxv[s], qy = cyv[s];
-            const bool nan = !(qx == qx && qy == qy);
-            int sx = -1, sy = 0;  // subcell, computed on the first mixed word
+            const unsigned loc = loc_of(t, s);
+            const unsigned sw = st[t] >> (8 * s);
+            const bool nan = sw & kNanBit;
+            const unsigned sub = sw & 15u;
             // entry cursor: the head's entry (single) or cell_ent[e, e1) (multi)
-            uint32_t ex = h[s].x, word = h[s].y;
+            uint32_t ex = hd[t][s].x, word = hd[t][s].y;
             unsigned e = 0, e1 = 0;
             if (ex != kNoEntry && (ex & kMulti)) {
                 e = word;
@@ -2017,7 +2039,7 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
                     if (!(ex & kEntC)) {
                         hit = true;
                     } else if (APPROX) {
-                        hit = bbox_distance(qx, qy, a.polys[poly].bb) <= a.r;
+                        hit = bbox_distance(qx[s], qy[s], a.polys[poly].bb) <= a.r;
                     } else {
                         // a decided class holds for every point in the cell's coordinate box: not
                         // for NaN coordinates (cell 0 by Java's (int) NaN)
@@ -2025,13 +2047,7 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
                         if (!nan) {
                             if (word == kWordHit) k = kClsHit;
                             else if (word == kWordMiss) k = kClsMiss;
-                            else if (word != 0u) {
-                                if (sx < 0) {
-                                    sx = sub_of(qx, g.mnx, g.l, ccx[s]);
-                                    sy = sub_of(qy, g.mny, g.l, ccy[s]);
-                                }
-                                k = (word >> (2 * (4 * sx + sy))) & 3u;
-                            }
+                            else k = (word >> (2 * sub)) & 3u;
                         }
                         hit = k == kClsHit;
                         need = k == kClsMixed;
@@ -2044,17 +2060,18 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
                         ex = kNoEntry;
                     }
                 }
-                stream_push<false>(a, ps, hit, poly, loc[s], c0);
-                if (!APPROX) stream_push<true>(a, cs, need, poly, loc[s], c0);
+                stream_push<false>(a, ps, hit, poly, loc, c0);
+                if (!APPROX) stream_push<true>(a, cs, need, poly, loc, c0);
             }
         }
         // points outside the grid against the polygons whose rectangles reach outside it (rare)
-        if (a.nopoly && __ballot(outside[0] || outside[1] || outside[2] || outside[3])) {
+        if (a.nopoly && any_out) {
             for (int s = 0; s < 4; s++) {
+                const bool o = (st[t] >> (8 * s)) & kOutBit;
                 int32_t cx = 0, cy = 0;
-                if (outside[s]) {
-                    cx = d_axis_cell(cxv[s], g.mnx, g.l);
-                    cy = d_axis_cell(cyv[s], g.mny, g.l);
+                if (o) {
+                    cx = d_axis_cell(qx[s], g.mnx, g.l);
+                    cy = d_axis_cell(qy[s], g.mny, g.l);
                 }
                 for (uint32_t j = 0; j < a.nopoly; j++) {
                     const uint32_t p = a.opoly[j];
@@ -2062,35 +2079,34 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
                     // range: the guaranteed rectangles; join exact: the checked list (+ the exact
                     // test); join approximate: every rectangle is in the G list
                     bool in = false;
-                    if (outside[s])
+                    if (o)
                         in = a.jmode == 1 ? in_rects(a.rects + 4 * P.coff, P.nc, cx, cy)
                                           : in_rects(a.rects + 4 * P.goff, P.ng, cx, cy);
                     const bool dist = !APPROX && a.jmode == 1;
-                    stream_push<false>(a, ps, in && !dist, p, loc[s], c0);
-                    if (!APPROX) stream_push<true>(a, cs, in && dist, p, loc[s], c0);
+                    stream_push<false>(a, ps, in && !dist, p, loc_of(t, s), c0);
+                    if (!APPROX) stream_push<true>(a, cs, in && dist, p, loc_of(t, s), c0);
                 }
             }
         }
     }
 }
 
-// Persistent blocks take the 8192-point chunks blockIdx.x, + gridDim.x, ...  Per chunk: pairs
+// Persistent blocks take the kStreamChunk-point chunks blockIdx.x, + gridDim.x, ...  Per chunk: pairs
 // and candidates staged in LDS (4 B each), then one atomic reservation each on the pair and
 // candidate totals (the output is unordered: no look-back, no chunk waits for another) and
 // coalesced stores.  A chunk whose stage overflowed runs again with its reservations made from
 // the counts, storing every pair / candidate straight to its slot.
-template <bool APPROX>
 #ifndef GEOHIP_PS_WPE
 #define GEOHIP_PS_WPE 4  // waves per SIMD the register budget is held to (LDS allows 4)
 #endif
+template <bool APPROX, bool KL>
 __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_eu(GEOHIP_PS_WPE))) void ppoly_stream(StreamArgs a) {
-    __shared__ unsigned kl[kKeepLds];
+    __shared__ unsigned kl[KL ? kKeepLds : 1];
     __shared__ unsigned ppk[kSPairCap];
     __shared__ unsigned cpk[APPROX ? 1 : kSCandCap];
     __shared__ unsigned s_np, s_nc;
     __shared__ unsigned long long s_pb, s_cb;
-    const bool kl_ok = a.keep && a.keep_words <= kKeepLds;
-    if (kl_ok)
+    if (KL)
         for (unsigned t = threadIdx.x; t < a.keep_words; t += kStreamNW * kWave) kl[t] = a.keep[t];
     const unsigned nchunks = (unsigned)((a.n + kStreamChunk - 1) / kStreamChunk);
     for (unsigned vb = blockIdx.x; vb < nchunks; vb += gridDim.x) {
@@ -2104,7 +2120,7 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
         const uint64_t c1 = c0 + kStreamChunk < a.n ? c0 + kStreamChunk : a.n;
         StreamSink ps{ppk, &s_np, kSPairCap, false, 0, 0u};
         StreamSink cs{cpk, &s_nc, APPROX ? 0u : kSCandCap, false, 0, 0u};
-        stream_chunk<APPROX>(a, kl, kl_ok, c0, c1, ps, cs);
+        stream_chunk<APPROX, KL>(a, kl, c0, c1, ps, cs);
         if (GEOHIP_PS_ABL == 3 && ps.acc + cs.acc == 0x9e3779b9u) a.o.totals[0] = 1;
         __syncthreads();
         const unsigned np = s_np, nc = s_nc;
@@ -2134,7 +2150,7 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
             __syncthreads();
             StreamSink pd{ppk, &s_np, kSPairCap, true, pb, 0u};
             StreamSink cd{cpk, &s_nc, cs.cap, true, cb, 0u};
-            stream_chunk<APPROX>(a, kl, kl_ok, c0, c1, pd, cd);
+            stream_chunk<APPROX, KL>(a, kl, c0, c1, pd, cd);
         }
     }
 }
@@ -2183,9 +2199,7 @@ struct CandGroup {
     uint32_t npoly;         // <= kCandLdsPolys
     uint4* items;           // (poly, begin, end, -)
     unsigned* nitems;
-    unsigned* sidx;         // sorted runs
-    double* sx;
-    double* sy;
+    unsigned* sidx;         // sorted runs: slots of the unsorted candidate arrays
 };
 
 __device__ __forceinline__ uint64_t cand_n(const CandGroup& c) {
@@ -2282,6 +2296,8 @@ __global__ __launch_bounds__(kCandThreads) void ppoly_cand_plan(CandGroup c) {
     if (threadIdx.x == 0) *c.nitems = carry_i;
 }
 
+// Only the 4-byte slot of each candidate moves (a random scatter of its 20 bytes cost 3x the
+// time); the evaluation gathers the coordinates from the unsorted arrays.
 __global__ __launch_bounds__(kCandThreads) void ppoly_cand_scatter(CandGroup c) {
     __shared__ unsigned h[kCandLdsPolys];
     uint64_t b0, b1;
@@ -2290,27 +2306,15 @@ __global__ __launch_bounds__(kCandThreads) void ppoly_cand_scatter(CandGroup c) 
     for (unsigned t = threadIdx.x; t < c.npoly; t += kCandThreads) h[t] = row[t];
     __syncthreads();
     for (uint64_t i0 = b0 + threadIdx.x; i0 < b1; i0 += (uint64_t)kCandPer * kCandThreads) {
-        unsigned p[kCandPer], q[kCandPer];
-        double x[kCandPer], y[kCandPer];
+        unsigned p[kCandPer];
 #pragma unroll
         for (unsigned u = 0; u < kCandPer; u++) {
             const uint64_t i = i0 + (uint64_t)u * kCandThreads;
-            p[u] = 0xffffffffu;
-            if (i < b1) {
-                p[u] = c.cpoly[i];
-                q[u] = c.cidx[i];
-                x[u] = c.cx[i];
-                y[u] = c.cy[i];
-            }
+            p[u] = i < b1 ? c.cpoly[i] : 0xffffffffu;
         }
 #pragma unroll
         for (unsigned u = 0; u < kCandPer; u++)
-            if (p[u] != 0xffffffffu) {
-                const unsigned pos = atomicAdd(&h[p[u]], 1u);
-                c.sidx[pos] = q[u];
-                c.sx[pos] = x[u];
-                c.sy[pos] = y[u];
-            }
+            if (p[u] != 0xffffffffu) c.sidx[atomicAdd(&h[p[u]], 1u)] = (unsigned)(i0 + (uint64_t)u * kCandThreads);
     }
 }
 
@@ -2363,9 +2367,10 @@ __global__ __launch_bounds__(kTB) void ppoly_cand_eval(CandGroup c, const PolyDe
             const unsigned t = threadIdx.x + u * kTB;
             qs[u] = 0;
             if (t < m) {
-                qx[u] = c.sx[w.y + t];
-                qy[u] = c.sy[w.y + t];
-                qi[u] = c.sidx[w.y + t];
+                const unsigned slot = c.sidx[w.y + t];
+                qx[u] = c.cx[slot];
+                qy[u] = c.cy[slot];
+                qi[u] = c.cidx[slot];
                 if (P.ns) qs[u] = slab_of(qy[u], P.sy0, P.sinv, P.ns);
             }
         }
@@ -4188,7 +4193,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             unsigned* misc = S.get<unsigned>(J_MISC, kMiscWords * 4);
             unsigned* mat = cands ? S.get<unsigned>(J_HIST, (size_t)kCandGroups * npoly * 4 + 16) : nullptr;
             void* cbuf = cands ? S.get<void>(J_SY, ccap * 24 + 64) : nullptr;
-            void* sbuf = cands ? S.get<void>(J_SX, ccap * 20 + 64) : nullptr;
+            void* sbuf = cands ? S.get<void>(J_SX, ccap * 4 + 64) : nullptr;
             uint4* items = cands ? S.get<uint4>(J_SKEY, (ccap / kCandItem + npoly + 1) * sizeof(uint4)) : nullptr;
             if (S.rc) return S.rc;
             hipEvent_t e0, e1;
@@ -4225,8 +4230,14 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             sa.o = so;
             if (nchunks) {
                 const unsigned nblk = (unsigned)std::min<uint64_t>(nchunks, (uint64_t)ctx_cus(ctx) * kStreamBlocksPerCU);
-                if (approximate) ppoly_stream<true><<<nblk, kStreamNW * kWave, 0, st>>>(sa);
-                else ppoly_stream<false><<<nblk, kStreamNW * kWave, 0, st>>>(sa);
+                const bool kl = sa.keep && sa.keep_words <= kKeepLds;
+                if (approximate) {
+                    if (kl) ppoly_stream<true, true><<<nblk, kStreamNW * kWave, 0, st>>>(sa);
+                    else ppoly_stream<true, false><<<nblk, kStreamNW * kWave, 0, st>>>(sa);
+                } else {
+                    if (kl) ppoly_stream<false, true><<<nblk, kStreamNW * kWave, 0, st>>>(sa);
+                    else ppoly_stream<false, false><<<nblk, kStreamNW * kWave, 0, st>>>(sa);
+                }
             }
             if (cands) {
                 char* sb = reinterpret_cast<char*>(sbuf);
@@ -4242,8 +4253,6 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
                 cg.items = items;
                 cg.nitems = misc + 4;
                 cg.sidx = reinterpret_cast<unsigned*>(sb);
-                cg.sx = reinterpret_cast<double*>(sb + ((ccap * 4 + 15) & ~(uint64_t)15));
-                cg.sy = cg.sx + ccap;
                 ppoly_cand_hist<<<kCandGroups, kCandThreads, 0, st>>>(cg);
                 ppoly_cand_plan<<<1, kCandThreads, 0, st>>>(cg);
                 ppoly_cand_scatter<<<kCandGroups, kCandThreads, 0, st>>>(cg);
