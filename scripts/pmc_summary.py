@@ -37,7 +37,7 @@ TAGS = {"knn": ("knn_scan", {"knn_pass": 1}),
                                 "join_items": 1, "join_item_fill": 1, "join_fused<false, true>": 1}),
         "ppoly": ("ppoly_probe", _PS),
         "c5": ("knn_scan_c5", {"knn_pass": 1}),
-        "ingest": ("ingest", {"ingest_fused": 1}),
+        "ingest": ("ingest", {"ingest_fused": 1, "ingest_general": 1}),
         "ppjoin": ("ppjoin", _PS),
         "ppknn": ("ppknn", {"rsel_init": 1, "rsel_small": 1, "ppknn_scan_boxes": 1, "ppknn_dist": 1}),
         "knn_incr": ("knn_incr", {"knn_pass": 1, "knn_final": 1}),
