@@ -1859,10 +1859,8 @@ struct StreamOut {
     int aligned8, swap;
     unsigned long long* totals;     // [0] pairs, [1] candidates: reservation cursors (zero before)
     uint64_t ccap;                  // candidates past it are counted only (the host regrows, re-runs)
-    unsigned* cpoly;                // candidates in chunk order: polygon, point, coordinates
-    unsigned* cidx;
-    double* cx;
-    double* cy;
+    unsigned* cpoly;                // candidates in chunk order: polygon (the grouping reads these),
+    double4* crec;                  // and (x, y, point bits, -) -- one 32-byte sector per gather
 };
 
 struct StreamArgs {
@@ -1907,9 +1905,7 @@ __device__ __forceinline__ void stream_emit_pair(const StreamOut& o, unsigned lo
 __device__ __forceinline__ void stream_emit_cand(const StreamArgs& a, unsigned long long p, unsigned poly, unsigned idx) {
     if (p >= a.o.ccap) return;
     a.o.cpoly[p] = poly;
-    a.o.cidx[p] = idx;
-    a.o.cx[p] = a.x[idx];
-    a.o.cy[p] = a.y[idx];
+    a.o.crec[p] = make_double4(a.x[idx], a.y[idx], __longlong_as_double((long long)idx), 0.0);
 }
 
 #ifndef GEOHIP_PS_ABL
@@ -2192,9 +2188,7 @@ struct CandGroup {
     const unsigned long long* ccount;  // candidate total (StreamOut::totals + 1)
     uint64_t ccap;
     const unsigned* cpoly;
-    const unsigned* cidx;
-    const double* cx;
-    const double* cy;
+    const double4* crec;
     unsigned* mat;          // [kCandGroups][npoly]: counts, then write bases
     uint32_t npoly;         // <= kCandLdsPolys
     uint4* items;           // (poly, begin, end, -)
@@ -2367,10 +2361,10 @@ __global__ __launch_bounds__(kTB) void ppoly_cand_eval(CandGroup c, const PolyDe
             const unsigned t = threadIdx.x + u * kTB;
             qs[u] = 0;
             if (t < m) {
-                const unsigned slot = c.sidx[w.y + t];
-                qx[u] = c.cx[slot];
-                qy[u] = c.cy[slot];
-                qi[u] = c.cidx[slot];
+                const double4 rc = c.crec[c.sidx[w.y + t]];
+                qx[u] = rc.x;
+                qy[u] = rc.y;
+                qi[u] = (unsigned)__double_as_longlong(rc.z);
                 if (P.ns) qs[u] = slab_of(qy[u], P.sy0, P.sinv, P.ns);
             }
         }
@@ -4192,7 +4186,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             // J_MISC: [0..1] pair total, [2..3] candidate total, [4] work items
             unsigned* misc = S.get<unsigned>(J_MISC, kMiscWords * 4);
             unsigned* mat = cands ? S.get<unsigned>(J_HIST, (size_t)kCandGroups * npoly * 4 + 16) : nullptr;
-            void* cbuf = cands ? S.get<void>(J_SY, ccap * 24 + 64) : nullptr;
+            void* cbuf = cands ? S.get<void>(J_SY, ccap * 36 + 64) : nullptr;
             void* sbuf = cands ? S.get<void>(J_SX, ccap * 4 + 64) : nullptr;
             uint4* items = cands ? S.get<uint4>(J_SKEY, (ccap / kCandItem + npoly + 1) * sizeof(uint4)) : nullptr;
             if (S.rc) return S.rc;
@@ -4209,9 +4203,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             so.ccap = cands ? ccap : 0;
             char* cb = reinterpret_cast<char*>(cbuf);
             so.cpoly = cands ? reinterpret_cast<unsigned*>(cb) : nullptr;
-            so.cidx = cands ? reinterpret_cast<unsigned*>(cb + ccap * 4) : nullptr;
-            so.cx = cands ? reinterpret_cast<double*>(cb + ccap * 8) : nullptr;
-            so.cy = cands ? reinterpret_cast<double*>(cb + ccap * 16) : nullptr;
+            so.crec = cands ? reinterpret_cast<double4*>(cb + ((ccap * 4 + 31) & ~(uint64_t)31)) : nullptr;
             StreamArgs sa;
             sa.x = dx;
             sa.y = dy;
@@ -4245,9 +4237,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
                 cg.ccount = so.totals + 1;
                 cg.ccap = ccap;
                 cg.cpoly = so.cpoly;
-                cg.cidx = so.cidx;
-                cg.cx = so.cx;
-                cg.cy = so.cy;
+                cg.crec = so.crec;
                 cg.mat = mat;
                 cg.npoly = npoly;
                 cg.items = items;
