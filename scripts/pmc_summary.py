@@ -19,7 +19,7 @@ ROOT = Path(__file__).resolve().parents[1]
 # point-polygon timed regions are the whole device step (binning included, r02); the bench's
 # setup calls (count-only joins) run some of these kernels too, so per-step totals are the
 # per-dispatch averages times these multiplicities, not dispatch totals over the run.
-_BIN = {"bin_count<1>": 1, "bin_count<2>": 1, "bin_scatter<1>": 1, "bin_scatter<2>": 1, "bin1_offsets": 1,
+_BIN = {"bin_count<1,": 1, "bin_count<2,": 1, "bin_scatter<1,": 1, "bin_scatter<2,": 1, "bin1_offsets": 1,
         "bin2_plan": 1, "bin2_tiles<false>": 1, "bin2_tiles<true>": 1}
 _PP = {**_BIN, "scan_seg_totals<unsigned int>": 1, "scan_totals<unsigned int>": 1, "scan_apply<unsigned int>": 1,
        "scan_seg_totals<unsigned long long>": 2, "scan_totals<unsigned long long>": 2,
