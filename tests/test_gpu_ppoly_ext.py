@@ -314,3 +314,32 @@ def test_ppoly_cell_class_box_edges(ctx, holes):
         got = ctx.join_ppoly(ag, ag, x, y, off, vx, vy, r, poly_rings=pr)
         want = cref.join_ppoly(cg, cg, x, y, off, vx, vy, r, poly_rings=pr)
         assert pairs_sorted(got).tolist() == pairs_sorted(want).tolist()
+
+
+def test_ppoly_stream_overflow_and_regrow(ctx):
+    """The streaming point-polygon path's rare branches: 96 concentric star polygons put ~96
+    entries in each central cell, so a 4096-point chunk stages more pairs (and mixed-subcell
+    candidates) than its LDS holds and reruns with its reservations known; the candidates of the
+    first call exceed the initial candidate buffer (n / 16) and the step runs again with the
+    buffer regrown.  Range, exact and approximate, and join vs the oracle; a second call reuses
+    the cached plan and the grown buffer."""
+    ag, cg = agrid(100)
+    rng = np.random.default_rng(123)
+    off, vx, vy = [0], [], []
+    for p in range(96):
+        ring = synth._star(rng, 116.4, 40.2, 0.03 + 0.0004 * p, 50)
+        vx += [a for a, _ in ring]
+        vy += [b for _, b in ring]
+        off.append(len(vx))
+    off, vx, vy = np.array(off, np.uint32), np.array(vx), np.array(vy)
+    x = rng.uniform(116.3, 116.5, 200000)
+    y = rng.uniform(40.1, 40.3, 200000)
+    x, y = with_edges(x, y, off, vx, vy)
+    for r, approx in ((0.01, False), (0.02, True), (0.01, False)):
+        got = ctx.range_ppoly(ag, x, y, off, vx, vy, r, approx)
+        want = cref.range_ppoly(cg, x, y, off, vx, vy, r, approx)
+        assert len(want) > 4096 * 2
+        assert pairs_sorted(got).tolist() == pairs_sorted(want).tolist()
+    got = ctx.join_ppoly(ag, ag, x, y, off, vx, vy, 0.01)
+    want = cref.join_ppoly(cg, cg, x, y, off, vx, vy, 0.01)
+    assert pairs_sorted(got).tolist() == pairs_sorted(want).tolist()
