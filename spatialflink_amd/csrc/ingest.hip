@@ -204,9 +204,13 @@ __device__ __forceinline__ Win24 lds_win24(const uint8_t* __restrict__ s, uint32
     return r;
 }
 
-// bit 7 of every byte -> one bit per byte (byte i -> bit i)
+// bit 7 of every byte -> one bit per byte (byte i -> bit i); per 32-bit half, one 32-bit multiply
+// gathers the four bits (shifted copies land on distinct positions, so no carries)
+__device__ __forceinline__ uint32_t byte_bits4(uint32_t m) {
+    return ((((m >> 7) & 0x01010101u) * 0x00204081u) >> 21) & 0xfu;
+}
 __device__ __forceinline__ uint32_t byte_bits(uint64_t m) {
-    return (uint32_t)((((m >> 7) & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
+    return byte_bits4((uint32_t)m) | (byte_bits4((uint32_t)(m >> 32)) << 4);
 }
 // per-byte masks, exact for every byte (no carry or borrow crosses a byte)
 __device__ __forceinline__ uint64_t nondigit_m(uint64_t v) {
@@ -223,18 +227,23 @@ __device__ __forceinline__ uint64_t le20_m(uint64_t v) {  // byte <= 0x20
 __device__ __forceinline__ uint32_t mask24(uint64_t a, uint64_t b, uint64_t c) {
     return byte_bits(a) | (byte_bits(b) << 8) | (byte_bits(c) << 16);
 }
+// value of four digit values b0..b3 (bytes of v, b0 most significant): two byte dot products
+// and a 24-bit multiply-add, all full rate (the 64-bit SWAR multiplies they replace are built
+// of quarter-rate 32-bit multiplies)
+__device__ __forceinline__ uint32_t digits4(uint32_t v) {
+    const uint32_t hi = __builtin_amdgcn_udot4(v, 0x0000010au, 0u, false);  // b0 * 10 + b1
+    return __builtin_amdgcn_udot4(v, 0x010a0000u, __umul24(hi, 100u), false);  // .. * 100 + b2 * 10 + b3
+}
 // value of m <= 8 ASCII digits starting at window offset off
 __device__ __forceinline__ uint64_t digits8(const Win24& W, uint32_t off, uint32_t m) {
     uint64_t x = W.get8(off) - 0x3030303030303030ull;  // digit bytes are the low m: no borrow into them
-    x = m ? (x << (8u * (8u - m))) : 0ull;
-    x = ((x & 0x0f0f0f0f0f0f0f0full) * 2561ull) >> 8;
-    x = ((x & 0x00ff00ff00ff00ffull) * 6553601ull) >> 16;
-    return ((x & 0x0000ffff0000ffffull) * 42949672960001ull) >> 32;
+    x = m ? (x << (8u * (8u - m))) : 0ull;  // the m digits in bytes 8 - m .. 7 (weights 10^(7 - byte))
+    return __umul24(digits4((uint32_t)x), 10000u) + digits4((uint32_t)(x >> 32));
 }
 __device__ __forceinline__ uint64_t digits_n(const Win24& W, uint32_t off, uint32_t n) {  // n <= 19
     constexpr uint64_t p8 = 100000000ull;
     if (n <= 8) return digits8(W, off, n);
-    if (n <= 16) return digits8(W, off, n - 8) * p8 + digits8(W, off + n - 8, 8);
+    if (n <= 16) return (uint64_t)(uint32_t)digits8(W, off, n - 8) * (uint32_t)p8 + digits8(W, off + n - 8, 8);
     return (digits8(W, off, n - 16) * p8 + digits8(W, off + n - 16, 8)) * p8 + digits8(W, off + n - 8, 8);
 }
 __device__ const uint64_t kPow10u[20] = {1ull, 10ull, 100ull, 1000ull, 10000ull, 100000ull, 1000000ull,
@@ -304,13 +313,19 @@ __device__ __forceinline__ int swar_csv(const uint8_t* __restrict__ s, uint32_t 
 
 // Stage chunk vb (+ the tail) in LDS and list the record starts it owns, in order: byte 0 of the
 // batch, then q + 1 for each '\n' at q.  Returns the chunk's record count (block-uniform).
+// The record-start list holds CAP entries (the hot kernel: 4096, so its LDS is 25 KB; a chunk
+// with more records -- shorter than 4 bytes on average, i.e. blank lines the reference rejects --
+// goes to ingest_general, whose list holds every possible start).
+constexpr unsigned kFastStarts = 4096;
+template <unsigned CAP>
 struct ChunkLds {
     uint4 text4[(kIngestChunk + kIngestTail) / 16];
-    uint16_t start[kIngestChunk + 1];
+    uint16_t start[CAP + 1];
     unsigned wave[kThreads / kWave];
 };
+template <unsigned CAP>
 __device__ __forceinline__ unsigned stage_chunk(const uint8_t* __restrict__ text, uint64_t nbytes, unsigned vb,
-                                                ChunkLds& L) {
+                                                ChunkLds<CAP>& L) {
     const uint64_t c0 = (uint64_t)vb * kIngestChunk;
     // the chunk first (this thread's 32 bytes stay in registers for the '\n' scan)
     const uint64_t p = c0 + threadIdx.x * kBytesPerThread;
@@ -327,7 +342,10 @@ __device__ __forceinline__ unsigned stage_chunk(const uint8_t* __restrict__ text
     unsigned nrec;
     unsigned at = block_excl_scan(mine, L.wave, &nrec);
     if (first) L.start[at++] = 0;
-    for (uint32_t mm = m; mm; mm &= mm - 1) L.start[at++] = (uint16_t)(threadIdx.x * kBytesPerThread + __builtin_ctz(mm) + 1);
+    for (uint32_t mm = m; mm; mm &= mm - 1) {
+        if (at < CAP) L.start[at] = (uint16_t)(threadIdx.x * kBytesPerThread + __builtin_ctz(mm) + 1);
+        at++;
+    }
     __syncthreads();
     return nrec;
 }
@@ -355,16 +373,23 @@ __device__ __forceinline__ void store_record(const IngestArgs& a, uint64_t idx, 
 // batch) is listed for ingest_general, which re-parses all its records with the full grammar.
 // The first round of records is parsed before the look-back, so the wait for the earlier
 // chunks' counts overlaps the parse.
-__global__ __launch_bounds__(kThreads) void ingest_fused(const uint8_t* __restrict__ text, uint64_t nbytes,
+#ifndef GEOHIP_ING_WPE
+#define GEOHIP_ING_WPE 8
+#endif
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(GEOHIP_ING_WPE))) void ingest_fused(const uint8_t* __restrict__ text, uint64_t nbytes,
                                                         IngestArgs a, IngestLookback lb,
                                                         double* __restrict__ x, double* __restrict__ y,
                                                         int64_t* __restrict__ ts, uint32_t* __restrict__ cell,
                                                         uint64_t cap, unsigned long long* __restrict__ total) {
-    __shared__ ChunkLds L;
+    __shared__ ChunkLds<kFastStarts> L;
     __shared__ unsigned s_vb, s_flag;
     __shared__ unsigned long long s_base;
     if (threadIdx.x == 0) {
+#ifdef GEOHIP_ING_NOTICKET
+        s_vb = blockIdx.x;  // measurement only: in-order dispatch assumed
+#else
         s_vb = atomicAdd(lb.ticket, 1u);
+#endif
         s_flag = 0;
     }
     __syncthreads();
@@ -379,16 +404,17 @@ __global__ __launch_bounds__(kThreads) void ingest_fused(const uint8_t* __restri
     const uint8_t dl = (uint8_t)a.spec.delim;
     const bool fast = a.spec.format == ingest::kCsv && dl > ' ' && dl != '"' && dl != '.' && dl != '-' &&
                       (unsigned)(dl - '0') >= 10u;
-    const unsigned rounds = nrec ? (nrec + kThreads - 1) / kThreads : 1u;  // block-uniform
+    const bool listed_all = nrec <= kFastStarts;  // else the whole chunk goes to ingest_general
+    const unsigned rounds = (nrec && listed_all) ? (nrec + kThreads - 1) / kThreads : 1u;  // block-uniform
+    bool undecided = !listed_all;
     uint64_t rbase = 0;
-    bool undecided = false;
     for (unsigned r = 0; r < rounds; r++) {
         const unsigned i = r * kThreads + threadIdx.x;
         ingest::Parsed o;
         o.x = o.y = 0.0;
         o.ts = 0;
         int rc = ingest::kFallback;
-        if (i < nrec) {
+        if (i < nrec && listed_all) {
             if (a.pad == 1) {
                 o.x = o.y = (double)L.start[i];
                 rc = ingest::kOk;
@@ -400,12 +426,20 @@ __global__ __launch_bounds__(kThreads) void ingest_fused(const uint8_t* __restri
         }
         if (r == 0) {  // the record base: look-back by wave 0, behind its first round's parse
             if (threadIdx.x < kWave) {
+#ifdef GEOHIP_ING_NOLB
+                const unsigned long long excl = (unsigned long long)vb * 287u;  // measurement only
+#else
                 const unsigned long long excl = vb == 0 ? 0ull : lookback_prefix(lb.status, vb, lb.epoch, lb.nlisted + 1);
+#endif
                 if (threadIdx.x == 0) {
                     if (vb != 0) publish_status(lb.status + vb, tag | kPrefixBit | (excl + nrec));
                     s_base = excl;
                     if (vb == gridDim.x - 1) {
+#ifdef GEOHIP_ING_NOLB
+                        *total = cap;
+#else
                         *total = excl + nrec;
+#endif
                         __hip_atomic_store(lb.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
                     }
                 }
@@ -414,7 +448,11 @@ __global__ __launch_bounds__(kThreads) void ingest_fused(const uint8_t* __restri
             rbase = s_base;
         }
         const uint64_t idx = rbase + i;
-        if (i < nrec && rc == ingest::kOk && idx < cap) store_record(a, idx, o, x, y, ts, cell);
+#ifndef GEOHIP_ING_NOSTORE
+        if (i < nrec && listed_all && rc == ingest::kOk && idx < cap) store_record(a, idx, o, x, y, ts, cell);
+#else
+        if (i < nrec && listed_all && rc == ingest::kOk && idx < cap && o.x == 12345.0) store_record(a, idx, o, x, y, ts, cell);
+#endif
     }
     if (__ballot(undecided) && lane_id() == 0) s_flag = 1u;
     __syncthreads();
@@ -434,7 +472,7 @@ __global__ __launch_bounds__(kThreads) void ingest_general(const uint8_t* __rest
                                                           double* __restrict__ x, double* __restrict__ y,
                                                           int64_t* __restrict__ ts, uint32_t* __restrict__ cell,
                                                           uint64_t cap, unsigned long long* __restrict__ bad) {
-    __shared__ ChunkLds L;
+    __shared__ ChunkLds<kIngestChunk> L;
     const unsigned nl = *lb.nlisted;
     for (unsigned j = blockIdx.x; j < nl; j += gridDim.x) {
         const ulonglong2 e = lb.listed[j];

@@ -197,6 +197,21 @@ def test_rejection_names_first_bad_record(ctx):
         assert d.value.bad == bad_at
 
 
+def test_rejection_in_overfull_chunk(ctx):
+    """A run of blank lines (records the reference rejects) puts more record starts in one chunk
+    than the hot kernel lists; the chunk goes whole to the general kernel, which must still name
+    the first blank line and keep the good records around it."""
+    good = _ragged_csv(20000, 12).split(b"\n")
+    for at, run in ((0, 9000), (7000, 5000), (19999, 20000)):
+        text = b"\n".join(good[:at] + [b""] * run + good[at:])
+        with pytest.raises(cref.IngestRejected) as e:
+            cref.ingest(cref.ingest_spec(cref.CSV, ",", 2, 3, 1), text)
+        assert e.value.bad == at
+        with pytest.raises(_abi.GeohipUnsupportedError) as d:
+            ctx.ingest_points(_abi.make_ingest_spec(cref.CSV, ",", 2, 3, 1), text)
+        assert d.value.bad == at
+
+
 def test_capacity(ctx):
     text = _ragged_csv(1000, 9)
     with pytest.raises(_abi.GeohipCapacityError):
