@@ -283,12 +283,23 @@ __device__ __forceinline__ int swar_csv(const uint8_t* __restrict__ s, uint32_t 
                 if (nf == 0) return kSwarNo;
             }
             if (ni == 0 || ni + nf > 19 || (ist && ni > 18)) return kSwarNo;
+#ifdef GEOHIP_ING_NODIG
+            const uint64_t iv = W.v[0] ^ ni;  // measurement only
+#else
             const uint64_t iv = digits_n(W, st, ni);
+#endif
             if (ist) {
                 o->ts = st ? -(int64_t)iv : (int64_t)iv;
             } else {
+#if defined(GEOHIP_ING_NODIG)
+                const uint64_t bits = iv ^ W.v[1] ^ nf;  // measurement only
+#elif defined(GEOHIP_ING_NOEL)
+                const uint64_t w = nf ? iv * kPow10u[nf] + digits_n(W, e1 + 1, nf) : iv;
+                const uint64_t bits = w ^ nf;  // measurement only
+#else
                 const uint64_t w = nf ? iv * kPow10u[nf] + digits_n(W, e1 + 1, nf) : iv;
                 const uint64_t bits = ingest::decimal_to_bits(w, -(int32_t)nf) | (st ? 1ull << 63 : 0ull);
+#endif
                 const double v = __builtin_bit_cast(double, bits);
                 if (isx) o->x = v;
                 if (isy) o->y = v;
