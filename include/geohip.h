@@ -101,13 +101,28 @@ int geohip_ctx_set_mem(geohip_ctx* ctx, int mem_kind);
    default stream): work the caller queued on that stream before a call is ordered before the
    call's kernels, and the *_async results are ordered before later work on it. */
 int geohip_ctx_set_stream(geohip_ctx* ctx, void* hip_stream);
+/* Rebinding (set_stream / reset_stream) orders the new stream after the work already queued on
+   the previously bound one (an event recorded on it at the switch), so a caller's stream must stay
+   alive until the ctx is bound to another stream or destroyed. */
 /* Back to the ctx's own (non-blocking) stream, the state after geohip_ctx_create. */
 int geohip_ctx_reset_stream(geohip_ctx* ctx);
 void* geohip_ctx_stream(geohip_ctx* ctx);
-/* Per-launch HIP-event timing of each query's dominant kernel (the scan kernel). */
+/* Device timing of each call's step (measurement): while enabled, every query call's device work
+   is timed with HIP events on the ctx stream. */
 int geohip_ctx_set_timing(geohip_ctx* ctx, int enable);
-/* Synchronises, then reports the summed duration and launch count since the last reset. */
+/* Synchronises, then reports the summed step duration and step count since the last reset (a
+   one-kernel step: the kernel's own dispatch timestamps; a multi-launch step: first launch to
+   last, gaps included). */
 int geohip_ctx_timing(geohip_ctx* ctx, double* total_ms, uint64_t* launches, int reset);
+/* As geohip_ctx_timing, plus the summed duration and count of the steps' kernels, each stamped by
+   its own dispatch (hipExtLaunchKernel: the begin / end timestamps rocprofv3 reports), so
+   kernel_ms / steps is a step's kernel time without the gaps between its launches. */
+int geohip_ctx_timing_kernels(geohip_ctx* ctx, double* step_ms, uint64_t* steps, double* kernel_ms,
+                              uint64_t* kernels, int reset);
+/* Waits for the ctx's enqueued work; GEOHIP_ERR_DEVICE if one of its kernels gave up a look-back
+   wait since the last check (a device-side invariant broken: the results of the *_async calls
+   since then are invalid).  The synchronous calls check this themselves. */
+int geohip_ctx_sync(geohip_ctx* ctx);
 int geohip_device_count(int* out_count);
 const char* geohip_version(void);
 

@@ -145,7 +145,11 @@ _SIGS = {
     "geohip_ctx_reset_stream": (c_int, [_P]),
     "geohip_ctx_stream": (c_void_p, [_P]),
     "geohip_ctx_set_timing": (c_int, [_P, c_int]),
+    "geohip_ctx_sync": (c_int, [_P]),
+    "geohip_debug_lookback_inject": (c_int, [_P, c_int]),
     "geohip_ctx_timing": (c_int, [_P, POINTER(c_double), POINTER(c_uint64), c_int]),
+    "geohip_ctx_timing_kernels": (c_int, [_P, POINTER(c_double), POINTER(c_uint64), POINTER(c_double),
+                                          POINTER(c_uint64), c_int]),
     "geohip_range_pp": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_double, c_double, c_double, c_int, _P,
                                 c_uint64, POINTER(c_uint64)]),
     "geohip_range_pp_async": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_double, c_double, c_double, c_int,
@@ -393,6 +397,15 @@ class Context:
             if s != self._bound:
                 self._bind(s)
 
+    def sync(self):
+        """Wait for this ctx's queued work; raises GeohipDeviceError if a kernel gave up a look-back
+        wait since the last check (geohip_ctx_sync)."""
+        self._check(lib.geohip_ctx_sync(self.h), "sync")
+
+    def debug_lookback_inject(self, on: bool):
+        """Test knob: range look-back waits give up (the fault path)."""
+        self._check(lib.geohip_debug_lookback_inject(self.h, int(on)), "debug_lookback_inject")
+
     def set_timing(self, on: bool):
         self._check(lib.geohip_ctx_set_timing(self.h, int(on)), "set_timing")
 
@@ -400,6 +413,15 @@ class Context:
         ms, n = c_double(0), c_uint64(0)
         self._check(lib.geohip_ctx_timing(self.h, ctypes.byref(ms), ctypes.byref(n), int(reset)), "timing")
         return ms.value, n.value
+
+    def timing_kernels(self, reset: bool = True):
+        """(step_ms, steps, kernel_ms, kernels) since the last reset: step_ms sums the timed steps
+        (a multi-launch step from its first launch to its last, gaps included), kernel_ms the
+        kernels of those steps as their own dispatches stamp them (what rocprofv3 reports)."""
+        sm, sn, km, kn = c_double(0), c_uint64(0), c_double(0), c_uint64(0)
+        self._check(lib.geohip_ctx_timing_kernels(self.h, ctypes.byref(sm), ctypes.byref(sn), ctypes.byref(km),
+                                                  ctypes.byref(kn), int(reset)), "timing_kernels")
+        return sm.value, sn.value, km.value, kn.value
 
     def _mem_for(self, *arrays, dtype="float64"):
         dev = [_is_device(a) for a in arrays if a is not None]

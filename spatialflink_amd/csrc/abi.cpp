@@ -96,16 +96,27 @@ struct geohip_ctx {
     size_t cap[S_COUNT] = {};
     uint64_t* pinned = nullptr;  // 8 words of pinned host memory for count readback
     bool timing = false;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+    // timed event pairs since the last readout: kind 0 = a step bracketed by hipEventRecord (its
+    // kernels and the gaps between them), 1 = one kernel of such a step, 2 = a step that is one
+    // kernel; kinds 1 and 2 are stamped by the kernel's own dispatch (hipExtLaunchKernel), the
+    // begin/end timestamps rocprofv3 reports
+    struct TimedPair {
+        hipEvent_t a, b;
+        int kind;
+    };
+    std::vector<TimedPair> pending;
     std::vector<hipEvent_t> pool;
-    double acc_ms = 0.0;
-    uint64_t launches = 0;
+    double acc_ms = 0.0;      // steps (kinds 0, 2)
+    uint64_t launches = 0;    // steps
+    double kern_ms = 0.0;     // kernels (kinds 1, 2)
+    uint64_t kernels = 0;
     // last point plan: a continuous query plans the same (grid, q, r) for every window
     bool plan_valid = false;
     geohip_grid plan_grid{};
     double plan_q[3] = {0, 0, 0};
     PointPlan plan{};
     unsigned long long range_epoch = 0;  // fused range pass: status words of this launch carry it
+    bool lb_inject = false;              // test knob: range look-back waits give up (geohip_debug_lookback_inject)
     unsigned long long lb_epoch = 0;     // chunk look-backs (ingest, point-polygon stream): status words of a launch carry it
     // host windows (GEOHIP_MEM_HOST): two pinned staging slots; the DMA of one slot runs on the
     // copy stream while the host fills the other (host_stage)
@@ -173,6 +184,45 @@ int ensure_zeroed(geohip_ctx* ctx, Slot s, size_t bytes) {
     return GEOHIP_OK;
 }
 
+// The range look-back words (S_RLB): 256 block-count status words, then the arrival ticket, then
+// the fault word a wait that gives up sets.  Zeroed on allocation; the status words again when the
+// 24-bit epoch wraps (a word last written 2^24 - 1 launches ago must not read as ready).
+constexpr size_t kRlbBytes = 256 * 8 + 64;
+struct RangeLb {
+    unsigned long long* status;
+    unsigned* ticket;
+    unsigned* fault;
+    unsigned long long epoch;
+    unsigned spins, inject;
+};
+int range_lookback(geohip_ctx* ctx, RangeLb* lb) {
+    int rc = ensure_zeroed(ctx, S_RLB, kRlbBytes);
+    if (rc) return rc;
+    ctx->range_epoch = ctx->range_epoch % ((1ull << 24) - 1) + 1;
+    char* base = B<char>(ctx, S_RLB);
+    if (ctx->range_epoch == 1 && hipMemsetAsync(base, 0, 256 * 8, ctx->stream) != hipSuccess)
+        return fail(ctx, GEOHIP_ERR_DEVICE, "look-back status reset failed");
+    lb->status = reinterpret_cast<unsigned long long*>(base);
+    lb->ticket = reinterpret_cast<unsigned*>(base + 256 * 8);
+    lb->fault = reinterpret_cast<unsigned*>(base + 256 * 8 + 16);
+    lb->epoch = ctx->range_epoch;
+    lb->spins = ctx->lb_inject ? 4096u : (1u << 22);  // kLookbackSpins (device_common.h): seconds
+    lb->inject = ctx->lb_inject ? 1u : 0u;
+    return GEOHIP_OK;
+}
+
+// After a synchronisation: GEOHIP_ERR_DEVICE if a look-back wait of this ctx gave up since the
+// last check (the word is cleared).
+int check_lookback_fault(geohip_ctx* ctx) {
+    if (!ctx->buf[S_RLB]) return GEOHIP_OK;
+    unsigned* fw = reinterpret_cast<unsigned*>(B<char>(ctx, S_RLB) + 256 * 8 + 16);
+    unsigned v = 0;
+    HIPCHK(hipMemcpy(&v, fw, 4, hipMemcpyDeviceToHost));
+    if (!v) return GEOHIP_OK;
+    HIPCHK(hipMemset(fw, 0, 4));
+    return fail(ctx, GEOHIP_ERR_DEVICE, "range look-back wait gave up (a block count never arrived); results invalid");
+}
+
 int begin(geohip_ctx* ctx) {
     if (!ctx) return GEOHIP_ERR_ARG;
     ctx->err.clear();
@@ -185,21 +235,28 @@ int begin(geohip_ctx* ctx) {
     return GEOHIP_OK;
 }
 
-void timing_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1) {
+void timed_pair(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1, int kind) {
     *e0 = *e1 = nullptr;
     if (!ctx->timing) return;
+    hipEvent_t ev[2] = {nullptr, nullptr};
     for (int t = 0; t < 2; t++) {
-        hipEvent_t ev = nullptr;
         if (!ctx->pool.empty()) {
-            ev = ctx->pool.back();
+            ev[t] = ctx->pool.back();
             ctx->pool.pop_back();
-        } else if (hipEventCreate(&ev) != hipSuccess) {
+        } else if (hipEventCreate(&ev[t]) != hipSuccess) {
+            if (t) ctx->pool.push_back(ev[0]);
             return;
         }
-        (t == 0 ? *e0 : *e1) = ev;
     }
-    ctx->pending.push_back({*e0, *e1});
+    *e0 = ev[0];
+    *e1 = ev[1];
+    ctx->pending.push_back({ev[0], ev[1], kind});
 }
+
+// a step of several launches: the caller records e0 / e1 around them (hipEventRecord)
+void timing_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1) { timed_pair(ctx, e0, e1, 0); }
+// a step that is one kernel: e0 / e1 go to hipExtLaunchKernel (the kernel's own timestamps)
+void kernel_step_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1) { timed_pair(ctx, e0, e1, 2); }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
@@ -390,7 +447,7 @@ int knn_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const
     if (!rc) rc = ensure_zeroed(ctx, S_SPILL_CNT, kKnnCounterBytes);
     if (rc) return rc;
     hipEvent_t e0, e1;
-    timing_events(ctx, &e0, &e1);
+    kernel_step_events(ctx, &e0, &e1);
     hipError_t e = launch_knn_pass(dx, dy, n, a, B<unsigned long long>(ctx, S_PART_D), B<unsigned>(ctx, S_PART_I),
                                    B<unsigned long long>(ctx, S_SPILL_D), B<unsigned>(ctx, S_SPILL_I),
                                    B<unsigned>(ctx, S_SPILL_CNT), out_d, out_i, out_cnt, ctx->stream, e0, e1);
@@ -480,15 +537,15 @@ int range_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x, con
     if (!rc) rc = ensure(ctx, S_OFFS, units * 8);
     if (rc) return rc;
     // fused pass: 256 status words + the arrival ticket (zeroed once; re-armed by each launch)
-    rc = ensure_zeroed(ctx, S_RLB, 256 * 8 + 64);
+    RangeLb lb;
+    rc = range_lookback(ctx, &lb);
     if (rc) return rc;
-    ctx->range_epoch = ctx->range_epoch % ((1ull << 24) - 1) + 1;
     hipEvent_t e0, e1;
-    timing_events(ctx, &e0, &e1);
+    if (range_is_one_kernel(n)) kernel_step_events(ctx, &e0, &e1);
+    else timing_events(ctx, &e0, &e1);
     hipError_t e = launch_range(dx, dy, n, a, approximate, B<unsigned long long>(ctx, S_MASK), B<unsigned>(ctx, S_UCNT),
-                                B<uint64_t>(ctx, S_OFFS), total, out, cap, ctx->stream, e0, e1,
-                                B<unsigned long long>(ctx, S_RLB), reinterpret_cast<unsigned*>(B<char>(ctx, S_RLB) + 256 * 8),
-                                ctx->range_epoch);
+                                B<uint64_t>(ctx, S_OFFS), total, out, cap, ctx->stream, e0, e1, lb.status, lb.ticket,
+                                lb.epoch, lb.fault, lb.spins, lb.inject);
     if (e != hipSuccess) return hip_fail(ctx, e, "range launch");
     return GEOHIP_OK;
 }
@@ -520,20 +577,23 @@ int knn_range_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x,
     if (!rc) rc = ensure(ctx, S_SPILL_D, n * 8);
     if (!rc) rc = ensure(ctx, S_SPILL_I, n * 4);
     if (!rc) rc = ensure_zeroed(ctx, S_SPILL_CNT, kKnnCounterBytes);
-    if (!rc) rc = ensure_zeroed(ctx, S_RLB, 256 * 8 + 64);
+    RangeLb lb;
+    if (!rc) rc = range_lookback(ctx, &lb);
     if (rc) return rc;
-    ctx->range_epoch = ctx->range_epoch % ((1ull << 24) - 1) + 1;
     PassRangeIo rio;
     memset(&rio, 0, sizeof rio);
     rio.a = make_range_args(plan, qx, qy, r);
     rio.approximate = approximate;
-    rio.status = B<unsigned long long>(ctx, S_RLB);
-    rio.epoch = ctx->range_epoch;
+    rio.status = lb.status;
+    rio.epoch = lb.epoch;
+    rio.fault = lb.fault;
+    rio.spin_limit = lb.spins;
+    rio.inject = lb.inject;
     rio.out = rout;
     rio.cap = rcap;
     rio.total = rtotal;
     hipEvent_t e0, e1;
-    timing_events(ctx, &e0, &e1);
+    kernel_step_events(ctx, &e0, &e1);
     hipError_t e = launch_knn_pass(dx, dy, n, a, B<unsigned long long>(ctx, S_PART_D), B<unsigned>(ctx, S_PART_I),
                                    B<unsigned long long>(ctx, S_SPILL_D), B<unsigned>(ctx, S_SPILL_I),
                                    B<unsigned>(ctx, S_SPILL_CNT), kd, ki, kcnt, ctx->stream, e0, e1, nullptr, 0, &rio);
@@ -598,8 +658,8 @@ int geohip_ctx_destroy(geohip_ctx* ctx) {
     for (int s = 0; s < S_COUNT; s++)
         if (ctx->buf[s]) hipFree(ctx->buf[s]);
     for (auto& p : ctx->pending) {
-        hipEventDestroy(p.first);
-        hipEventDestroy(p.second);
+        hipEventDestroy(p.a);
+        hipEventDestroy(p.b);
     }
     for (auto ev : ctx->pool) hipEventDestroy(ev);
     if (ctx->pinned) hipHostFree(ctx->pinned);
@@ -662,14 +722,20 @@ int geohip_ctx_timing(geohip_ctx* ctx, double* total_ms, uint64_t* launches, int
     HIPCHK(hipStreamSynchronize(ctx->stream));
     for (auto& p : ctx->pending) {
         float ms = 0.f;
-        if (hipEventElapsedTime(&ms, p.first, p.second) == hipSuccess) {
-            ctx->acc_ms += ms;
-            ctx->launches++;
+        if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            if (p.kind != 1) {
+                ctx->acc_ms += ms;
+                ctx->launches++;
+            }
+            if (p.kind != 0) {
+                ctx->kern_ms += ms;
+                ctx->kernels++;
+            }
         } else {
             (void)hipGetLastError();
         }
-        ctx->pool.push_back(p.first);
-        ctx->pool.push_back(p.second);
+        ctx->pool.push_back(p.a);
+        ctx->pool.push_back(p.b);
     }
     ctx->pending.clear();
     if (total_ms) *total_ms = ctx->acc_ms;
@@ -677,7 +743,38 @@ int geohip_ctx_timing(geohip_ctx* ctx, double* total_ms, uint64_t* launches, int
     if (reset) {
         ctx->acc_ms = 0.0;
         ctx->launches = 0;
+        ctx->kern_ms = 0.0;
+        ctx->kernels = 0;
     }
+    return GEOHIP_OK;
+}
+
+int geohip_ctx_sync(geohip_ctx* ctx) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return check_lookback_fault(ctx);
+}
+
+// Test knob: while on, the range look-back waits (range_fused, the kNN pass's fused range) wait
+// for an epoch no block publishes and give up after 4096 polls -- the fault path, exercised.
+int geohip_debug_lookback_inject(geohip_ctx* ctx, int on) {
+    if (!ctx) return GEOHIP_ERR_ARG;
+    ctx->lb_inject = on != 0;
+    return GEOHIP_OK;
+}
+
+int geohip_ctx_timing_kernels(geohip_ctx* ctx, double* step_ms, uint64_t* steps, double* kernel_ms,
+                              uint64_t* kernels, int reset) {
+    double km = 0.0;
+    uint64_t kn = 0;
+    int rc = geohip_ctx_timing(ctx, step_ms, steps, 0);
+    if (rc) return rc;
+    km = ctx->kern_ms;
+    kn = ctx->kernels;
+    if (kernel_ms) *kernel_ms = km;
+    if (kernels) *kernels = kn;
+    if (reset) geohip_ctx_timing(ctx, nullptr, nullptr, 1);
     return GEOHIP_OK;
 }
 
@@ -701,6 +798,8 @@ int geohip_range_pp(geohip_ctx* ctx, const geohip_grid* grid, const double* x, c
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(ctx->pinned, ctx->buf[S_TOTAL], 8, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    rc = check_lookback_fault(ctx);
+    if (rc) return rc;
     const uint64_t total = ctx->pinned[0];
     *out_count = total;
     if (ctx->mem == GEOHIP_MEM_HOST) {
@@ -882,6 +981,8 @@ int geohip_knn_range_pp(geohip_ctx* ctx, const geohip_grid* grid, const double* 
         HIPCHK(hipMemcpyAsync(knn_idx, oi, (size_t)k * 4, hipMemcpyDeviceToHost, ctx->stream));
     }
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    rc = check_lookback_fault(ctx);
+    if (rc) return rc;
     *knn_count = (uint32_t)(ctx->pinned[0] & 0xffffffffu);
     const uint64_t total = ctx->pinned[1];
     *range_count = total;
@@ -1076,14 +1177,17 @@ int geohip_debug_knn_pass_trace(geohip_ctx* ctx, const geohip_grid* grid, const 
     PassRangeIo rio;
     memset(&rio, 0, sizeof rio);
     if (with_range) {
-        rc = ensure_zeroed(ctx, S_RLB, 256 * 8 + 64);
+        RangeLb lb;
+        rc = range_lookback(ctx, &lb);
         if (!rc) rc = ensure(ctx, S_OUT_IDX, n * 4);
         if (!rc) rc = ensure(ctx, S_TOTAL, 8);
         if (rc) return rc;
-        ctx->range_epoch = ctx->range_epoch % ((1ull << 24) - 1) + 1;
         rio.a = make_range_args(plan, qx, qy, r);
-        rio.status = B<unsigned long long>(ctx, S_RLB);
-        rio.epoch = ctx->range_epoch;
+        rio.status = lb.status;
+        rio.epoch = lb.epoch;
+        rio.fault = lb.fault;
+        rio.spin_limit = lb.spins;
+        rio.inject = lb.inject;
         rio.out = B<unsigned>(ctx, S_OUT_IDX);
         rio.cap = n;
         rio.total = B<uint64_t>(ctx, S_TOTAL);
@@ -1126,6 +1230,21 @@ unsigned long long ctx_next_epoch(geohip_ctx* ctx) {
     ctx->lb_epoch = ctx->lb_epoch % ((1ull << 22) - 1) + 1;
     return ctx->lb_epoch;
 }
+// Look-back status words of a launch carry its epoch in their top bits, so they need no reset
+// between launches -- provided no word can hold the epoch of the current launch unless this
+// launch wrote it: the slot is zeroed whenever it is (re)allocated (epoch 0 is never issued), and
+// all of it again when the epoch counter wraps (a word last written 2^22 - 1 launches ago by a
+// larger batch would otherwise read as ready).
+int ctx_lookback_status(geohip_ctx* ctx, int slot, size_t bytes, void** out, unsigned long long* epoch) {
+    const Slot s = (Slot)(S_I0 + slot);
+    int rc = ensure_zeroed(ctx, s, bytes);
+    if (rc) return rc;
+    *epoch = ctx_next_epoch(ctx);
+    if (*epoch == 1 && hipMemsetAsync(ctx->buf[s], 0, ctx->cap[s], ctx->stream) != hipSuccess)
+        return fail(ctx, GEOHIP_ERR_DEVICE, "look-back status reset failed");
+    *out = ctx->buf[s];
+    return GEOHIP_OK;
+}
 int ctx_cus(geohip_ctx* ctx) { return ctx->cus; }
 
 int ctx_begin(geohip_ctx* ctx) { return begin(ctx); }
@@ -1135,6 +1254,8 @@ uint64_t* ctx_pinned(geohip_ctx* ctx) { return ctx->pinned; }
 void** ctx_pcache_slot(geohip_ctx* ctx) { return &ctx->pcache; }
 void** ctx_kcache_slot(geohip_ctx* ctx) { return &ctx->kcache; }
 void ctx_timing_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1) { timing_events(ctx, e0, e1); }
+void ctx_kernel_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1) { timed_pair(ctx, e0, e1, 1); }
+void ctx_kernel_step_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1) { timed_pair(ctx, e0, e1, 2); }
 int ctx_stage_xy(geohip_ctx* ctx, const double* x, const double* y, uint64_t n, int which, const double** dx,
                  const double** dy) {
     return which == 0 ? stage_xy(ctx, x, y, n, S_X, S_Y, dx, dy) : stage_xy(ctx, x, y, n, S_QX, S_QY, dx, dy);

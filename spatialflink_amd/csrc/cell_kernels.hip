@@ -75,6 +75,11 @@ __device__ __forceinline__ int32_t d_axis_cell_fast(double v, double mn, double 
     return d_cvt_java(f);
 }
 
+// small zero-fills inside timed steps (a kernel, so its time is stamped like the others)
+__global__ void fill_words(unsigned* __restrict__ p, unsigned n, unsigned v) {
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = v;
+}
+
 // ------------------------------------------------------------------ scans ----------------
 // exclusive scan, 3 phases: per-block totals, scan of totals, per-block rescan + offset
 constexpr int kScanPer = 16;
@@ -4193,7 +4198,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             hipEvent_t e0, e1;
             ctx_timing_events(ctx, &e0, &e1);
             if (e0) hipEventRecord(e0, st);  // the whole device step
-            if (hipMemsetAsync(misc, 0, 32, st) != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
+            tlaunch(ctx, fill_words, 1, 64, 0, st, misc, 8u, 0u);  // totals and the item count
             StreamOut so;
             so.out = out;
             so.cap = out ? cap : 0;
@@ -4224,11 +4229,11 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
                 const unsigned nblk = (unsigned)std::min<uint64_t>(nchunks, (uint64_t)ctx_cus(ctx) * kStreamBlocksPerCU);
                 const bool kl = sa.keep && sa.keep_words <= kKeepLds;
                 if (approximate) {
-                    if (kl) ppoly_stream<true, true><<<nblk, kStreamNW * kWave, 0, st>>>(sa);
-                    else ppoly_stream<true, false><<<nblk, kStreamNW * kWave, 0, st>>>(sa);
+                    if (kl) tlaunch(ctx, ppoly_stream<true, true>, nblk, kStreamNW * kWave, 0, st, sa);
+                    else tlaunch(ctx, ppoly_stream<true, false>, nblk, kStreamNW * kWave, 0, st, sa);
                 } else {
-                    if (kl) ppoly_stream<false, true><<<nblk, kStreamNW * kWave, 0, st>>>(sa);
-                    else ppoly_stream<false, false><<<nblk, kStreamNW * kWave, 0, st>>>(sa);
+                    if (kl) tlaunch(ctx, ppoly_stream<false, true>, nblk, kStreamNW * kWave, 0, st, sa);
+                    else tlaunch(ctx, ppoly_stream<false, false>, nblk, kStreamNW * kWave, 0, st, sa);
                 }
             }
             if (cands) {
@@ -4243,10 +4248,10 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
                 cg.items = items;
                 cg.nitems = misc + 4;
                 cg.sidx = reinterpret_cast<unsigned*>(sb);
-                ppoly_cand_hist<<<kCandGroups, kCandThreads, 0, st>>>(cg);
-                ppoly_cand_plan<<<1, kCandThreads, 0, st>>>(cg);
-                ppoly_cand_scatter<<<kCandGroups, kCandThreads, 0, st>>>(cg);
-                ppoly_cand_eval<<<kEvalBlocks, kTB, 0, st>>>(cg, dpoly, dvx, dvy, dvr, denv, dslab, r, so);
+                tlaunch(ctx, ppoly_cand_hist, kCandGroups, kCandThreads, 0, st, cg);
+                tlaunch(ctx, ppoly_cand_plan, 1, kCandThreads, 0, st, cg);
+                tlaunch(ctx, ppoly_cand_scatter, kCandGroups, kCandThreads, 0, st, cg);
+                tlaunch(ctx, ppoly_cand_eval, kEvalBlocks, kTB, 0, st, cg, dpoly, dvx, dvy, dvr, denv, dslab, r, so);
             }
             if (e1) hipEventRecord(e1, st);
             hipError_t e = hipGetLastError();

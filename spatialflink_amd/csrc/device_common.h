@@ -352,4 +352,50 @@ __device__ __forceinline__ unsigned long long lookback_prefix(const unsigned lon
     return excl;
 }
 
+// The exclusive prefix of the per-block counts of blocks 0 .. vb - 1 (status words (epoch << 40)
+// | count, published by blocks that took their tickets earlier, so every block waited on is
+// resident or done): one wave, lane l polls words l, l + 64, ... with all loads in flight, s_sleep
+// back-off between rounds.  A wait past spin_limit rounds (seconds at kLookbackSpins: a broken
+// invariant, never a slow block) sets *fault and returns what it has -- the kernel then ends with
+// an error the host reports instead of hanging the device.  inject (measurement / tests only)
+// waits for an epoch no block writes, to exercise that path.
+template <int kPer>
+__device__ __forceinline__ unsigned long long poll_block_counts(const unsigned long long* status, unsigned vb,
+                                                                unsigned long long epoch, unsigned spin_limit,
+                                                                unsigned inject, unsigned* fault) {
+    const int lane = lane_id();
+    const unsigned long long want = inject && vb ? (epoch ^ 0x800000ull) : epoch;
+    unsigned long long v[kPer];
+    unsigned pending = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        const unsigned j = (unsigned)lane + (unsigned)k * kWave;
+        v[k] = j < vb ? __hip_atomic_load(status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (want << 40);
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; k++)
+        if ((v[k] >> 40) != want) pending |= 1u << k;
+    unsigned spins = 0;
+    while (__ballot(pending != 0)) {
+        if (++spins > spin_limit) {
+            if (lane == 0) __hip_atomic_store(fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(8);
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            if (pending & (1u << k)) {
+                v[k] = __hip_atomic_load(status + lane + k * kWave, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((v[k] >> 40) == want) pending &= ~(1u << k);
+            }
+        }
+    }
+    unsigned long long pre = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) pre += v[k] & ((1ull << 40) - 1);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
+    return pre;
+}
+
 }  // namespace geohip

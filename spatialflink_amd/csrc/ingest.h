@@ -43,8 +43,8 @@ struct IngestLookback {
 // parse; *total = records in the batch) and ingest_general (the full grammar over the chunks the
 // first left undecided).  bad[0] = ~(first rejected record index), 0 if none (must hold 0
 // before the launch).
-hipError_t launch_ingest(const uint8_t* text, uint64_t nbytes, const IngestArgs& a, const IngestLookback& lb,
-                         unsigned long long* total, double* x, double* y, int64_t* ts, uint32_t* cell, uint64_t cap,
-                         unsigned long long* bad, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
+hipError_t launch_ingest(geohip_ctx* ctx, const uint8_t* text, uint64_t nbytes, const IngestArgs& a,
+                         const IngestLookback& lb, unsigned long long* total, double* x, double* y, int64_t* ts,
+                         uint32_t* cell, uint64_t cap, unsigned long long* bad, hipStream_t st);
 
 }  // namespace geohip

@@ -21,6 +21,7 @@
 
 #include "device_common.h"
 #include "ingest.h"
+#include "join.h"
 
 namespace geohip {
 namespace {
@@ -509,18 +510,17 @@ __global__ __launch_bounds__(kThreads) void ingest_general(const uint8_t* __rest
 
 }  // namespace
 
-hipError_t launch_ingest(const uint8_t* text, uint64_t nbytes, const IngestArgs& a, const IngestLookback& lb,
-                         unsigned long long* total, double* x, double* y, int64_t* ts, uint32_t* cell, uint64_t cap,
-                         unsigned long long* bad, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+hipError_t launch_ingest(geohip_ctx* ctx, const uint8_t* text, uint64_t nbytes, const IngestArgs& a,
+                         const IngestLookback& lb, unsigned long long* total, double* x, double* y, int64_t* ts,
+                         uint32_t* cell, uint64_t cap, unsigned long long* bad, hipStream_t st) {
     const uint64_t nchunks = ingest_chunks(nbytes);
+    if (nchunks == 0) return hipMemsetAsync(total, 0, sizeof(unsigned long long), st);
+    hipEvent_t ev0, ev1;
+    ctx_timing_events(ctx, &ev0, &ev1);  // the step: both kernels (each also stamped by tlaunch)
     if (ev0) (void)hipEventRecord(ev0, st);
-    if (nchunks == 0) {
-        (void)hipMemsetAsync(total, 0, sizeof(unsigned long long), st);
-    } else {
-        ingest_fused<<<(unsigned)nchunks, kThreads, 0, st>>>(text, nbytes, a, lb, x, y, ts, cell, cap, total);
-        const unsigned g = nchunks < kGeneralBlocks ? (unsigned)nchunks : kGeneralBlocks;
-        ingest_general<<<g, kThreads, 0, st>>>(text, nbytes, a, lb, x, y, ts, cell, cap, bad);
-    }
+    tlaunch(ctx, ingest_fused, (unsigned)nchunks, kThreads, 0, st, text, nbytes, a, lb, x, y, ts, cell, cap, total);
+    const unsigned g = nchunks < kGeneralBlocks ? (unsigned)nchunks : kGeneralBlocks;
+    tlaunch(ctx, ingest_general, g, kThreads, 0, st, text, nbytes, a, lb, x, y, ts, cell, cap, bad);
     if (ev1) (void)hipEventRecord(ev1, st);
     return hipGetLastError();
 }

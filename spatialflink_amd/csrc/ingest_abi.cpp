@@ -92,7 +92,8 @@ int geohip_ingest_points(geohip_ctx* ctx, const geohip_grid* grid, const geohip_
     hipStream_t st = ctx_stream(ctx);
     const bool dev = ctx_mem(ctx) == GEOHIP_MEM_DEVICE;
     void *status, *words, *list;
-    rc = ctx_ensure_ingest(ctx, I_STATUS, nchunks * 8, &status);
+    unsigned long long epoch = 0;
+    rc = ctx_lookback_status(ctx, I_STATUS, nchunks * 8, &status, &epoch);
     if (!rc) rc = ctx_ensure_ingest(ctx, I_LIST, nchunks * 16, &list);
     if (!rc) rc = ctx_ensure_ingest_zeroed(ctx, I_WORDS, 64, &words);  // the ticket word starts at zero
     if (rc) return rc;
@@ -120,11 +121,9 @@ int geohip_ingest_points(geohip_ctx* ctx, const geohip_grid* grid, const geohip_
     // [0] total, [1] ticket (re-armed by the kernel), [2] ~first rejected record, [3] listed chunks
     unsigned long long* w = static_cast<unsigned long long*>(words);
     ICHK(hipMemsetAsync(w + 2, 0, 16, st));
-    hipEvent_t e0, e1;
-    ctx_timing_events(ctx, &e0, &e1);
     const IngestLookback lb{static_cast<unsigned long long*>(status), reinterpret_cast<unsigned*>(w + 1),
-                            ctx_next_epoch(ctx), static_cast<ulonglong2*>(list), reinterpret_cast<unsigned*>(w + 3)};
-    hipError_t e = launch_ingest(dtext, nbytes, a, lb, w, dx, dy, dts, dcell, cap, w + 2, st, e0, e1);
+                            epoch, static_cast<ulonglong2*>(list), reinterpret_cast<unsigned*>(w + 3)};
+    hipError_t e = launch_ingest(ctx, dtext, nbytes, a, lb, w, dx, dy, dts, dcell, cap, w + 2, st);
     if (e != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, std::string("ingest launch: ") + hipGetErrorString(e));
     uint64_t* pinned = ctx_pinned(ctx);
     ICHK(hipMemcpyAsync(pinned, w, 32, hipMemcpyDeviceToHost, st));

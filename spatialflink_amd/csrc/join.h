@@ -1,5 +1,6 @@
 // join.h -- point-point window join (PointPointJoinQuery.java:113-172).
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -14,12 +15,26 @@ int ctx_ensure(geohip_ctx* ctx, int slot, size_t bytes, void** out);  // slot 0.
 int ctx_ensure_ingest(geohip_ctx* ctx, int slot, size_t bytes, void** out);  // slot 0..7
 int ctx_ensure_ingest_zeroed(geohip_ctx* ctx, int slot, size_t bytes, void** out);  // zeroed when (re)allocated
 unsigned long long ctx_next_epoch(geohip_ctx* ctx);  // look-back epoch: 1 .. 2^22 - 1, new per call
+// the ingest look-back status slot (zeroed on allocation and on epoch wrap) and this call's epoch
+int ctx_lookback_status(geohip_ctx* ctx, int slot, size_t bytes, void** out, unsigned long long* epoch);
 int ctx_cus(geohip_ctx* ctx);                       // compute units of the ctx's device
 int ctx_begin(geohip_ctx* ctx);  // clears the error, selects the ctx's device
 hipStream_t ctx_stream(geohip_ctx* ctx);
 int ctx_mem(geohip_ctx* ctx);
 uint64_t* ctx_pinned(geohip_ctx* ctx);
-void ctx_timing_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1);
+void ctx_timing_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1);      // a step of several launches
+void ctx_kernel_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1);      // one kernel inside such a step
+void ctx_kernel_step_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1); // a step that is one kernel
+
+// A kernel of a timed step: while the ctx's timing is on, launched with a fresh event pair that
+// its own dispatch stamps (begin / end, the durations rocprofv3 reports), so a step's kernel time
+// is the sum of its kernels without the gaps between them.
+template <typename F, typename... A>
+inline void tlaunch(geohip_ctx* ctx, F kernel, dim3 grid, dim3 block, uint32_t shm, hipStream_t st, A... a) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (ctx) ctx_kernel_events(ctx, &e0, &e1);
+    hipExtLaunchKernelGGL(kernel, grid, block, shm, st, e0, e1, 0, a...);
+}
 int ctx_stage_xy(geohip_ctx* ctx, const double* x, const double* y, uint64_t n, int which, const double** dx,
                  const double** dy);
 void** ctx_pcache_slot(geohip_ctx* ctx);  // the ctx's point-polygon plan cache (owned by cell_kernels)

@@ -47,6 +47,8 @@ struct PassRangeIo {
     uint64_t cap;
     uint64_t* total;
     unsigned long long* trace;  // measurement only: look-back done / hits written at [8 b + 5, 6]
+    unsigned* fault;            // set when the look-back wait gives up (poll_block_counts)
+    unsigned spin_limit, inject;
 };
 // whether a window of n points fits the fused kNN + range pass (block chunk <= 131072 points)
 bool knn_pass_fuses_range(uint64_t n);
@@ -69,10 +71,13 @@ struct PaneMerge {
 hipError_t launch_knn_merge_panes(const unsigned long long* ring_d, const unsigned* ring_i, const PaneMerge& pm,
                                   double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st);
 // range: bitmask (16 words / 1024 pts), unit_count (units), offs (units) scratch.
+// the range runs as one fused kernel at this window size (else three launches)
+bool range_is_one_kernel(uint64_t n);
 hipError_t launch_range(const double* x, const double* y, uint64_t n, const RangeArgs& a, int approximate,
                         unsigned long long* bitmask, unsigned* unit_count, uint64_t* offs, uint64_t* total,
                         unsigned* out, uint64_t cap, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1,
-                        unsigned long long* lb_status, unsigned* lb_ticket, unsigned long long epoch);
+                        unsigned long long* lb_status, unsigned* lb_ticket, unsigned long long epoch,
+                        unsigned* lb_fault, unsigned lb_spins, unsigned lb_inject);
 hipError_t launch_synth_uniform(double* x, double* y, uint64_t n, uint64_t base, uint64_t seed, double min_x,
                                 double max_x, double min_y, double max_y, hipStream_t st);
 hipError_t launch_selftest_fp64(const double* a, const double* b, uint64_t n, double* o_sqrt, double* o_div,

@@ -15,6 +15,7 @@
 //                compacted distance batches; hits kept as a bitmask per 1024-point unit.
 //   scan_units   exclusive scan of per-unit hit counts.
 //   range_emit   bitmask -> ascending window indices.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -1120,32 +1121,8 @@ __device__ __forceinline__ void pass_range_emit(const PassRangeIo& rio, const un
     const unsigned nw = p1 > p0 ? (unsigned)((p1 - p0 + 63) / 64) : 0u;
     const unsigned long long tag = rio.epoch << 40;
     if (wid == 0) {
-        constexpr int kPer = kPassMaxBlocks / kWave;
-        unsigned long long v[kPer];
-        unsigned pending = 0;
-#pragma unroll
-        for (int k = 0; k < kPer; k++) {
-            const unsigned j = (unsigned)lane + (unsigned)k * kWave;
-            v[k] = j < vb ? __hip_atomic_load(rio.status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tag;
-        }
-#pragma unroll
-        for (int k = 0; k < kPer; k++)
-            if ((v[k] >> 40) != rio.epoch) pending |= 1u << k;
-        while (pending) {
-            __builtin_amdgcn_s_sleep(8);
-#pragma unroll
-            for (int k = 0; k < kPer; k++) {
-                if (pending & (1u << k)) {
-                    v[k] = __hip_atomic_load(rio.status + lane + k * kWave, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if ((v[k] >> 40) == rio.epoch) pending &= ~(1u << k);
-                }
-            }
-        }
-        unsigned long long pre = 0;
-#pragma unroll
-        for (int k = 0; k < kPer; k++) pre += v[k] & ((1ull << 40) - 1);
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
+        const unsigned long long pre = poll_block_counts<kPassMaxBlocks / kWave>(rio.status, vb, rio.epoch, rio.spin_limit,
+                                                                                  rio.inject, rio.fault);
         if (lane == 0) excl_sh = pre;
     }
     if (rio.trace && threadIdx.x == 0) rio.trace[16 * (size_t)blockIdx.x + 5] = __builtin_amdgcn_s_memrealtime();
@@ -1744,6 +1721,8 @@ struct RangeLookback {
     unsigned long long* status;  // kRangeMaxBlocks words: (epoch << 40) | count
     unsigned* ticket;            // zero before the first launch; re-armed by the last block
     unsigned long long epoch;    // 1 .. 2^24 - 1, new per launch
+    unsigned* fault;             // set when a look-back wait gives up (poll_block_counts)
+    unsigned spin_limit, inject;
 };
 
 // MODE (measurement only): 0 full; 1 no look-back/emission (counts only); 2 loads only;
@@ -1923,32 +1902,8 @@ __global__ __launch_bounds__(kRangeNW * kWave) void range_fused(const double* __
     if (wid == 0 && MODE != 4) {
         // lane l reads predecessors l, l + 64, l + 128, l + 192 with all four loads in flight
         // (a dependent chain of device-scope loads costs a memory round trip each)
-        constexpr int kPer = kRangeMaxBlocks / kWave;
-        unsigned long long v[kPer];
-        unsigned pending = 0;
-#pragma unroll
-        for (int k = 0; k < kPer; k++) {
-            const unsigned j = (unsigned)lane + (unsigned)k * kWave;
-            v[k] = j < vb ? __hip_atomic_load(lb.status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tag;
-        }
-#pragma unroll
-        for (int k = 0; k < kPer; k++)
-            if ((v[k] >> 40) != lb.epoch) pending |= 1u << k;
-        while (pending) {
-            __builtin_amdgcn_s_sleep(8);
-#pragma unroll
-            for (int k = 0; k < kPer; k++) {
-                if (pending & (1u << k)) {
-                    v[k] = __hip_atomic_load(lb.status + lane + k * kWave, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if ((v[k] >> 40) == lb.epoch) pending &= ~(1u << k);
-                }
-            }
-        }
-        unsigned long long pre = 0;
-#pragma unroll
-        for (int k = 0; k < kPer; k++) pre += v[k] & ((1ull << 40) - 1);
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
+        const unsigned long long pre = poll_block_counts<kRangeMaxBlocks / kWave>(lb.status, vb, lb.epoch, lb.spin_limit,
+                                                                                   lb.inject, lb.fault);
         if (lane == 0) excl_sh = pre;
     }
     __syncthreads();
@@ -2104,23 +2059,23 @@ hipError_t launch_knn_pass(const double* x, const double* y, uint64_t n, const K
     // list entries, then the packed heads, then the list lengths (in the index array)
     const PassIo io{list_d, list_i, cap, list_d + lists, list_i + lists, list_i + lists + (size_t)kPassHeads * nblocks,
                     spill_d, nullptr, spill_i, ctr, out_d, out_i, out_count, 16u, trace};
-    if (ev0) (void)hipEventRecord(ev0, st);
     PassRangeIo rio;
     memset(&rio, 0, sizeof rio);
+    // ev0 / ev1 (timing on): stamped by the kernel's own dispatch begin / end
+    const dim3 g(nblocks), b(kPassNW * 64);
     if (range) {
         if (!knn_pass_fuses_range(n)) return hipErrorInvalidValue;
         rio = *range;
-        knn_pass<kPassNW, 0, true><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io, rio);
+        hipExtLaunchKernelGGL(knn_pass<kPassNW, 0, true>, g, b, 0, st, ev0, ev1, 0, x, y, n, chunk, args, io, rio);
     } else {
         switch (abl) {
-            case 1: knn_pass<kPassNW, 1><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io, rio); break;
-            case 2: knn_pass<kPassNW, 2><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io, rio); break;
-            case 8: knn_pass<kPassNW, 8><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io, rio); break;
-            case 16: knn_pass<kPassNW, 16><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io, rio); break;
-            default: knn_pass<kPassNW><<<nblocks, kPassNW * 64, 0, st>>>(x, y, n, chunk, args, io, rio); break;
+            case 1: hipExtLaunchKernelGGL(knn_pass<kPassNW, 1>, g, b, 0, st, ev0, ev1, 0, x, y, n, chunk, args, io, rio); break;
+            case 2: hipExtLaunchKernelGGL(knn_pass<kPassNW, 2>, g, b, 0, st, ev0, ev1, 0, x, y, n, chunk, args, io, rio); break;
+            case 8: hipExtLaunchKernelGGL(knn_pass<kPassNW, 8>, g, b, 0, st, ev0, ev1, 0, x, y, n, chunk, args, io, rio); break;
+            case 16: hipExtLaunchKernelGGL(knn_pass<kPassNW, 16>, g, b, 0, st, ev0, ev1, 0, x, y, n, chunk, args, io, rio); break;
+            default: hipExtLaunchKernelGGL(knn_pass<kPassNW>, g, b, 0, st, ev0, ev1, 0, x, y, n, chunk, args, io, rio); break;
         }
     }
-    if (ev1) (void)hipEventRecord(ev1, st);
     return hipGetLastError();
 }
 
@@ -2256,24 +2211,33 @@ hipError_t launch_knn_merge(const unsigned long long* d, const unsigned* i, unsi
 }
 
 
+bool range_is_one_kernel(uint64_t n) {
+    const uint64_t units = (n + kUnitPts - 1) / kUnitPts;
+    return units > 0 && units <= (uint64_t)kRangeMaxBlocks * kRangeMaxUnits;
+}
+
 hipError_t launch_range(const double* x, const double* y, uint64_t n, const RangeArgs& a, int approximate,
                         unsigned long long* bitmask, unsigned* unit_count, uint64_t* offs, uint64_t* total,
                         unsigned* out, uint64_t cap, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1,
-                        unsigned long long* lb_status, unsigned* lb_ticket, unsigned long long epoch) {
+                        unsigned long long* lb_status, unsigned* lb_ticket, unsigned long long epoch,
+                        unsigned* lb_fault, unsigned lb_spins, unsigned lb_inject) {
     const uint64_t units = (n + kUnitPts - 1) / kUnitPts;
     if (units == 0) return hipMemsetAsync(total, 0, sizeof(uint64_t), st);
     if (lb_status && units <= (uint64_t)kRangeMaxBlocks * kRangeMaxUnits) {
         // one fused launch: <= 256 blocks of upb units
         const unsigned upb = (unsigned)((units + kRangeMaxBlocks - 1) / kRangeMaxBlocks);
         const unsigned nblocks = (unsigned)((units + upb - 1) / upb);
-        const RangeLookback lb{lb_status, lb_ticket, epoch};
-        if (ev0) (void)hipEventRecord(ev0, st);
+        const RangeLookback lb{lb_status, lb_ticket, epoch, lb_fault, lb_spins, lb_inject};
 #ifndef GEOHIP_RANGE_MODE
 #define GEOHIP_RANGE_MODE 0  // measurement builds only (range_fused MODE)
 #endif
-        if (approximate) range_fused<true><<<nblocks, kRangeNW * kWave, 0, st>>>(x, y, n, a, upb, lb, out, cap, total);
-        else range_fused<false, GEOHIP_RANGE_MODE><<<nblocks, kRangeNW * kWave, 0, st>>>(x, y, n, a, upb, lb, out, cap, total);
-        if (ev1) (void)hipEventRecord(ev1, st);
+        // one kernel: ev0 / ev1 stamped by its dispatch
+        const dim3 g(nblocks), b(kRangeNW * kWave);
+        if (approximate)
+            hipExtLaunchKernelGGL(range_fused<true>, g, b, 0, st, ev0, ev1, 0, x, y, n, a, upb, lb, out, cap, total);
+        else
+            hipExtLaunchKernelGGL(range_fused<false, GEOHIP_RANGE_MODE>, g, b, 0, st, ev0, ev1, 0, x, y, n, a, upb, lb,
+                                  out, cap, total);
         return hipGetLastError();
     }
     const uint64_t blocks = (units + 3) / 4;

@@ -95,6 +95,8 @@ class IncrementalKNN:
     rebased by its offset in the window) -- no torch kernels between the pass and the merge."""
 
     def __init__(self, ctx: _abi.Context, grid: _abi.Grid, qx: float, qy: float, r: float, k: int, panes: int = 2):
+        if not 1 <= int(panes) <= 16:  # one geohip_knn_merge_panes_async launch merges at most 16 lists
+            raise _abi.GeohipArgumentError(f"IncrementalKNN merges 1..16 panes per window, got {panes}")
         self.ctx, self.grid, self.q, self.r, self.k, self.p = ctx, grid, (qx, qy), r, int(k), int(panes)
         self.sizes = deque(maxlen=self.p)  # sizes of the panes in the ring, oldest first
         self.count = 0                     # panes pushed so far
