@@ -259,7 +259,8 @@ int geohip_band_pack_query_async(geohip_ctx* ctx, const geohip_grid* grid_data, 
 /* The point output schemas of spatialStreams/Serialization.java for m result points, as one text
    buffer: record j is point p = idx[j] (or j when idx is NULL; p >= n is GEOHIP_ERR_ARG, e.g. a
    padded kNN list's 0xffffffff sentinel), each record followed by '\n'.  The Point's fields:
-   objID = bytes oid_text[oid_off[p] .. oid_off[p+1]) (UTF-8; oid_text NULL: objID == null),
+   objID = bytes oid_text[oid_off[p] .. oid_off[p+1]) (UTF-8; oid_text NULL: objID == null; bit 63
+   of oid_off[p] set: point p's objID is null, offsets are the low 63 bits),
    timeStampMillisec = ts[p] (ts NULL: 0), point.getX()/getY() = x[p]/y[p], doubles through JDK 8
    Double.toString (FloatingDecimal).
      GEOHIP_FMT_CSV     <- PointToCSVTSVOutputSchema.serialize  Serialization.java:125-150: the
@@ -339,12 +340,51 @@ typedef struct geohip_ingest_spec {
     int32_t attr_x;  /* csvTsvSchemaAttr.get(2) */
     int32_t attr_y;  /* csvTsvSchemaAttr.get(3) */
     int32_t attr_ts; /* csvTsvSchemaAttr.get(1) for CSVTSVToTSpatial (Long.valueOf), -1: none */
-    int32_t reserved;
+    int32_t attr_oid; /* csvTsvSchemaAttr.get(0), the objID field: read only by geohip_ingest_trajectory
+                         with out_oid (geohip_ingest_points ignores it) */
 } geohip_ingest_spec;
 int geohip_ingest_points(geohip_ctx* ctx, const geohip_grid* grid, const geohip_ingest_spec* spec,
                          const char* text, uint64_t nbytes, double* out_x, double* out_y,
                          int64_t* out_ts /* nullable */, uint32_t* out_cell /* nullable */,
                          uint64_t cap, uint64_t* out_count, uint64_t* out_bad);
+
+/* TrajectoryStream (Deserialization.java:64-80): every field of the Point the reference builds,
+   Point(objID, x, y, timeStampMillisec, uGrid) (spatialObjects/Point.java:91-100):
+     GEOHIP_FMT_CSV     <- CSVTSVToTSpatial.map Deserialization.java:306-321: objID = field attr_oid,
+                           timestamp = Long.valueOf(field attr_ts) (attr_ts -1: 0);
+     GEOHIP_FMT_GEOJSON <- GeoJSONToTSpatial.map Deserialization.java:149-208: timestamp =
+                           traj->date_format's parse of properties[prop_ts] (GEOHIP_DATE_YMD_HMS:
+                           SimpleDateFormat("yyyy-MM-dd HH:mm:ss"), conf/geoflink-conf.yml, in a zone
+                           of fixed offset utc_offset_min; GEOHIP_DATE_NONE: 0), 0 where the reference
+                           catches a ParseException; objID = properties[prop_oid].toString() with every
+                           '"' deleted, null where properties or the key are absent;
+     GEOHIP_FMT_WKT     <- WKTToTSpatial.map Deserialization.java:258-284: objID null, timestamp 0.
+   out_oid[i] = record i's objID as a span of the text: (offset << 24) | length -- the bytes of the
+   reference's String once the '"' among them are deleted -- or 0xffffff (length field all ones)
+   for a null objID; geohip_ingest_oid_compact turns the spans into the (oid_text, oid_off) form
+   the output codecs take.  Records whose objID or date form is not restated here (non-ASCII or
+   escaped JSON strings, JSON numbers with fractions, lenient date forms such as one-digit
+   fields, empty or control-character CSV objIDs) are GEOHIP_ERR_UNSUPPORTED like any record the
+   device does not decide.  Other arguments and errors as geohip_ingest_points. */
+typedef struct geohip_traj_spec {
+    int32_t date_format;    /* GEOHIP_DATE_NONE / GEOHIP_DATE_YMD_HMS (GeoJSON) */
+    int32_t utc_offset_min; /* the DateFormat's zone: minutes east of UTC */
+    char prop_ts[60];       /* propertyTimeStamp (GeoJSON), NUL-terminated, <= 59 bytes */
+    char prop_oid[60];      /* propertyObjID (GeoJSON), NUL-terminated, <= 59 bytes */
+} geohip_traj_spec;
+int geohip_ingest_trajectory(geohip_ctx* ctx, const geohip_grid* grid, const geohip_ingest_spec* spec,
+                             const geohip_traj_spec* traj /* nullable for CSV / WKT */, const char* text,
+                             uint64_t nbytes, double* out_x, double* out_y, int64_t* out_ts /* nullable */,
+                             uint32_t* out_cell /* nullable */, uint64_t* out_oid /* nullable */,
+                             uint64_t cap, uint64_t* out_count, uint64_t* out_bad);
+/* objID spans (geohip_ingest_trajectory's out_oid, m records) over the same text -> the strings:
+   out_text = their bytes with every '"' deleted, concatenated; out_off[0..m] = each record's start
+   in out_text (out_off[m] = the total), bit 63 of out_off[i] set where record i's objID is null.
+   The layout geohip_format_points / _csv take as (oid_text, oid_off).  Device memory only;
+   *out_len (host) = total bytes, GEOHIP_ERR_CAPACITY when above cap (out_off written, out_text
+   untouched). */
+int geohip_ingest_oid_compact(geohip_ctx* ctx, const char* text, uint64_t nbytes, const uint64_t* oid_spans,
+                              uint64_t m, uint8_t* out_text, uint64_t cap, uint64_t* out_off, uint64_t* out_len);
 
 /* ---- host-side planning introspection (no device needed) ------------------------------ */
 /* Query-cell sets of a point query as rectangles: point in G iff in any g rect; point in C

@@ -21,7 +21,12 @@ class Grid(ctypes.Structure):
 
 class IngestSpec(ctypes.Structure):
     _fields_ = [("format", c_int32), ("delim", c_int32), ("fx", c_int32), ("fy", c_int32), ("fts", c_int32),
-                ("reserved", c_int32)]
+                ("foid", c_int32)]
+
+
+class TrajSpec(ctypes.Structure):
+    _fields_ = [("date_format", c_int32), ("utc_offset_min", c_int32), ("prop_ts", ctypes.c_char * 60),
+                ("prop_oid", ctypes.c_char * 60)]
 
 
 def _load():
@@ -53,6 +58,9 @@ def _load():
                                                 POINTER(c_uint32)]),
         "geohip_oracle_ingest": (c_int64, [POINTER(IngestSpec), POINTER(Grid), c_void_p, c_uint64, c_void_p,
                                            c_void_p, c_void_p, c_void_p, c_uint64]),
+        "geohip_oracle_ingest_traj": (c_int64, [POINTER(IngestSpec), POINTER(TrajSpec), POINTER(Grid), c_void_p,
+                                                c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64,
+                                                c_void_p, c_uint64]),
         "geohip_oracle_range_ppoly": (c_int64, [POINTER(Grid), c_void_p, c_void_p, c_uint64, c_void_p, c_void_p,
                                                 c_void_p, c_void_p, c_uint32, c_double, c_int, c_void_p, c_uint64,
                                                 POINTER(c_uint64)]),
@@ -288,8 +296,36 @@ class IngestRejected(OracleError):
         self.bad = bad
 
 
-def ingest_spec(fmt, delimiter=",", fx=0, fy=1, fts=-1) -> IngestSpec:
-    return IngestSpec(fmt, delimiter.encode()[0] if delimiter else 0, fx, fy, fts, 0)
+def ingest_spec(fmt, delimiter=",", fx=0, fy=1, fts=-1, foid=-1) -> IngestSpec:
+    return IngestSpec(fmt, delimiter.encode()[0] if delimiter else 0, fx, fy, fts, foid)
+
+
+def traj_spec(prop_ts="timestamp", prop_oid="oID", date_format=1, utc_offset_min=0) -> TrajSpec:
+    return TrajSpec(date_format, utc_offset_min, prop_ts.encode(), prop_oid.encode())
+
+
+def ingest_traj(spec: IngestSpec, traj: TrajSpec | None, text: bytes, g: Grid | None = None):
+    """TrajectoryStream batch -> dict(x, y, ts, cell, oid): oid = list of bytes / None per record
+    (quotes deleted); IngestRejected(bad) for the first record thrown or not restated."""
+    g = g if g is not None else grid(0.0, 0.0, 1.0, 1)
+    cap = text.count(b"\n") + 1
+    x, y = np.empty(cap), np.empty(cap)
+    ts, cell = np.empty(cap, dtype=np.int64), np.empty(cap, dtype=np.uint32)
+    off = np.empty(cap + 1, dtype=np.uint64)
+    ob = np.empty(len(text) + 1, dtype=np.uint8)
+    buf = np.frombuffer(text, dtype=np.uint8) if len(text) else np.zeros(1, dtype=np.uint8)
+    n = lib.geohip_oracle_ingest_traj(ctypes.byref(spec), ctypes.byref(traj) if traj is not None else None,
+                                      ctypes.byref(g), _p(buf), len(text), _p(x), _p(y), _p(ts), _p(cell), _p(ob),
+                                      len(ob), _p(off), cap)
+    if n < 0:
+        raise IngestRejected(-n - 1)
+    mask = (1 << 63) - 1
+    oids = []
+    for i in range(n):
+        o = int(off[i])
+        oids.append(None if o >> 63 else bytes(ob[o & mask:int(off[i + 1]) & mask]))
+    return {"x": x[:n], "y": y[:n], "ts": ts[:n], "cell": cell[:n], "oid": oids,
+            "oid_text": bytes(ob[:int(off[n]) & mask]), "oid_off": off[:n + 1]}
 
 
 def ingest_record(spec: IngestSpec, rec: bytes, g: Grid | None = None):

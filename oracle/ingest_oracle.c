@@ -28,20 +28,37 @@
  * Records are the '\n'-separated lines of a text batch; a final empty line (text ending in
  * '\n') is not a record.
  */
+#define _GNU_SOURCE
 #include <errno.h>
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #define ING_OK 0
 #define ING_ERR -1 /* the reference throws (NumberFormatException, IndexOutOfBounds, ParseException) */
+#define ING_UNDECIDED -2 /* valid for the reference, but a form libgeohip does not restate (it hands
+                            such records back to the host): the batch is rejected all the same */
 
 enum { FMT_CSV = 0, FMT_GEOJSON = 1, FMT_WKT = 2 };
 
 typedef struct {
-    int32_t format, delim, fx, fy, fts, reserved;
+    int32_t format, delim, fx, fy, fts, foid; /* foid: csvTsvSchemaAttr.get(0) (trajectory batches) */
 } ing_spec;
+
+/* TrajectoryStream's GeoJSON parameters (include/geohip.h geohip_traj_spec) */
+typedef struct {
+    int32_t date_format, utc_offset_min;
+    char prop_ts[60], prop_oid[60];
+} ing_traj;
+
+/* a record's objID: bytes [a, b) of buf (the quote-free record copy or the record), or null */
+typedef struct {
+    int null;
+    const char* buf;
+    size_t a, b;
+} ing_oid;
 
 typedef struct {
     double min_x, min_y, cell_len;
@@ -191,7 +208,10 @@ static int j_csv_field(const char* t, size_t n, unsigned char d, int want, size_
     return ING_OK;
 }
 
-static int csv_record(const char* r, size_t n, const ing_spec* sp, double* x, double* y, int64_t* ts) {
+/* oid (nullable): CSVTSVToTSpatial's strOId = strArrayList.get(csvTsvSchemaAttr.get(0)),
+   Deserialization.java:313-314 -- copied out of the quote-free record into *oidbuf (malloc'd). */
+static int csv_record(const char* r, size_t n, const ing_spec* sp, double* x, double* y, int64_t* ts,
+                      ing_oid* oid, char** oidbuf) {
     char* t = (char*)malloc(n + 1);
     size_t m = 0;
     for (size_t i = 0; i < n; i++)
@@ -199,7 +219,24 @@ static int csv_record(const char* r, size_t n, const ing_spec* sp, double* x, do
     size_t a, b;
     int rc = ING_OK;
     /* CSVTSVToTSpatial evaluates get(0), then Long.valueOf(get(1)), then x, then y */
-    if (sp->fts >= 0) {
+    if (oid && sp->foid >= 0) {
+        rc = j_csv_field(t, m, (unsigned char)sp->delim, sp->foid, &a, &b);
+        if (!rc) {
+            /* libgeohip restates non-empty objIDs without control characters (other than \s) */
+            if (a == b) rc = ING_UNDECIDED;
+            for (size_t i = a; !rc && i < b; i++)
+                if ((unsigned char)t[i] < 0x20 && !jspace((unsigned char)t[i])) rc = ING_UNDECIDED;
+        }
+        if (!rc) {
+            *oidbuf = (char*)malloc(b - a + 1);
+            memcpy(*oidbuf, t + a, b - a);
+            oid->null = 0;
+            oid->buf = *oidbuf;
+            oid->a = 0;
+            oid->b = b - a;
+        }
+    }
+    if (!rc && sp->fts >= 0) {
         rc = j_csv_field(t, m, (unsigned char)sp->delim, sp->fts, &a, &b);
         if (!rc) rc = j_parse_long(t + a, b - a, ts);
     }
@@ -383,6 +420,129 @@ static int geojson_record(const char* s, size_t n, double* x, double* y) {
     return ING_OK;
 }
 
+/* ---- GeoJSONToTSpatial (Deserialization.java:149-208) -------------------------------------- */
+/* the keys of the object at obj hold no backslash (libgeohip compares keys as written) */
+static int jkeys_plain(const char* s, size_t n, size_t obj) {
+    jr r = {s, n, obj};
+    jws(&r);
+    if (r.p >= n || s[r.p] != '{') return 1;
+    r.p++;
+    jws(&r);
+    if (r.p < n && s[r.p] == '}') return 1;
+    for (;;) {
+        size_t a, b;
+        jws(&r);
+        if (jstring(&r, &a, &b)) return 0;
+        if (memchr(s + a, '\\', b - a)) return 0;
+        jws(&r);
+        r.p++; /* ':' */
+        if (jskip(&r, 1)) return 0;
+        jws(&r);
+        if (r.p < n && s[r.p] == ',') {
+            r.p++;
+            continue;
+        }
+        return 1;
+    }
+}
+
+/* SimpleDateFormat("yyyy-MM-dd HH:mm:ss").parse(text) (lenient) then getTime() in a zone of fixed
+   offset off_min.  Restated here: the 'yyyy-MM-dd HH:mm:ss' digit counts after blanks, year
+   1583..9999, fields carried over by timegm's normalisation (the lenient calendar's arithmetic);
+   no parse at all (ParseException, caught by the reference) -> 0.  Other forms -> ING_UNDECIDED. */
+static int j_date_parse(const char* s, size_t n, int32_t off_min, int64_t* ms) {
+    size_t i = 0;
+    while (i < n && (s[i] == ' ' || s[i] == '\t')) i++;
+    if (i == n) {
+        *ms = 0;
+        return ING_OK;
+    }
+    unsigned char c = (unsigned char)s[i];
+    if (c < 0x80 && !isdig(c) && c != '-' && c != '+' && c != 'N') { /* DecimalFormat parses nothing */
+        *ms = 0;
+        return ING_OK;
+    }
+    const char* t = s + i;
+    size_t L = n - i;
+    static const int digit_at[] = {0, 1, 2, 3, 5, 6, 8, 9, 11, 12, 14, 15, 17, 18};
+    if (L < 19 || t[4] != '-' || t[7] != '-' || t[10] != ' ' || t[13] != ':' || t[16] != ':') return ING_UNDECIDED;
+    for (int k = 0; k < 14; k++)
+        if (!isdig((unsigned char)t[digit_at[k]])) return ING_UNDECIDED;
+    if (L > 19) {
+        unsigned char e = (unsigned char)t[19];
+        if (e >= 0x80 || isdig(e) || strchr("Ee.,", e)) return ING_UNDECIDED;
+    }
+    int Y = atoi((char[]){t[0], t[1], t[2], t[3], 0});
+    if (Y < 1583) return ING_UNDECIDED;
+    struct tm tm;
+    memset(&tm, 0, sizeof tm);
+    tm.tm_year = Y - 1900;
+    tm.tm_mon = (t[5] - '0') * 10 + (t[6] - '0') - 1;
+    tm.tm_mday = (t[8] - '0') * 10 + (t[9] - '0');
+    tm.tm_hour = (t[11] - '0') * 10 + (t[12] - '0');
+    tm.tm_min = (t[14] - '0') * 10 + (t[15] - '0');
+    tm.tm_sec = (t[17] - '0') * 10 + (t[18] - '0');
+    const time_t secs = timegm(&tm);
+    *ms = ((int64_t)secs - (int64_t)off_min * 60) * 1000;
+    return ING_OK;
+}
+
+static int geojson_traj_record(const char* s, size_t n, const ing_traj* tr, double* x, double* y, int64_t* ts,
+                               ing_oid* oid) {
+    int rc = geojson_record(s, n, x, y);
+    if (rc) return rc;
+    *ts = 0;
+    oid->null = 1;
+    if (!jkeys_plain(s, n, 0)) return ING_UNDECIDED;
+    /* trailing text after the value: Jackson ignores it, libgeohip does not restate that */
+    {
+        jr w = {s, n, 0};
+        jskip(&w, 0);
+        jws(&w);
+        if (w.p != n) return ING_UNDECIDED;
+    }
+    size_t props;
+    if (jmember(s, n, 0, "properties", &props)) return ING_OK; /* nodeProperties == null */
+    if (!jkeys_plain(s, n, props)) return ING_UNDECIDED;
+    size_t at;
+    if (tr->date_format != 0 && !jmember(s, n, props, tr->prop_ts, &at)) {
+        /* dateFormat.parse(nodeTime.textValue()): a non-string node has no text -> NPE */
+        jr r = {s, n, at};
+        size_t a, b;
+        if (s[at] != '"' || jstring(&r, &a, &b)) return ING_ERR;
+        if (memchr(s + a, '\\', b - a)) return ING_UNDECIDED;
+        rc = j_date_parse(s + a, b - a, tr->utc_offset_min, ts);
+        if (rc) return rc;
+    }
+    if (!jmember(s, n, props, tr->prop_oid, &at)) {
+        /* nodeOId.toString().replaceAll("\"", ""): Jackson's text of the node, quotes deleted */
+        jr r = {s, n, at};
+        size_t a = at, b;
+        if (s[at] == '"') {
+            size_t sa, sb;
+            if (jstring(&r, &sa, &sb)) return ING_ERR;
+            for (size_t i = sa; i < sb; i++)
+                if ((unsigned char)s[i] < 0x20 || (unsigned char)s[i] >= 0x7f || s[i] == '\\') return ING_UNDECIDED;
+            a = sa;
+            b = sb;
+        } else {
+            if (jskip(&r, 1)) return ING_ERR;
+            b = r.p;
+            int lit = (b - a == 4 && !memcmp(s + a, "true", 4)) || (b - a == 5 && !memcmp(s + a, "false", 5)) ||
+                      (b - a == 4 && !memcmp(s + a, "null", 4));
+            int integer = b > a && (isdig((unsigned char)s[a]) || s[a] == '-');
+            for (size_t i = a + (s[a] == '-'); integer && i < b; i++) integer = isdig((unsigned char)s[i]);
+            if (integer && b - a == 2 && s[a] == '-' && s[a + 1] == '0') integer = 0; /* IntNode(0): "0" */
+            if (!lit && !integer) return ING_UNDECIDED;
+        }
+        oid->null = 0;
+        oid->buf = s;
+        oid->a = a;
+        oid->b = b;
+    }
+    return ING_OK;
+}
+
 /* ---- WKT: JTS WKTReader on str.substring(str.indexOf("POINT")) ----------------------------- */
 static int wword(unsigned char c) {
     return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || isdig(c) || c == '-' || c == '+' || c == '.' || c >= 160;
@@ -444,17 +604,19 @@ static int32_t j_d2i(double v) {
     return (int32_t)v;
 }
 
+static int any_record(const ing_spec* sp, const ing_traj* tr, const char* r, size_t n, double* x, double* y,
+                      int64_t* ts, ing_oid* oid, char** oidbuf) {
+    *ts = 0;
+    if (oid) oid->null = 1;
+    if (sp->format == FMT_CSV) return csv_record(r, n, sp, x, y, ts, oid, oidbuf);
+    if (sp->format == FMT_GEOJSON) return tr ? geojson_traj_record(r, n, tr, x, y, ts, oid) : geojson_record(r, n, x, y);
+    return wkt_record(r, n, x, y); /* WKTToTSpatial: objID null, timestamp 0 */
+}
+
 /* One record -> (x, y, ts, cell).  cell = cx * n + cy for a valid key, else 0xffffffff. */
 int geohip_oracle_ingest_record(const ing_spec* sp, const ing_grid* g, const char* r, size_t n, double* x,
                                 double* y, int64_t* ts, uint32_t* cell) {
-    int rc;
-    *ts = 0;
-    if (sp->format == FMT_CSV)
-        rc = csv_record(r, n, sp, x, y, ts);
-    else if (sp->format == FMT_GEOJSON)
-        rc = geojson_record(r, n, x, y);
-    else
-        rc = wkt_record(r, n, x, y);
+    int rc = any_record(sp, NULL, r, n, x, y, ts, NULL, NULL);
     if (rc) return rc;
     const int32_t cx = j_d2i(floor((*x - g->min_x) / g->cell_len));
     const int32_t cy = j_d2i(floor((*y - g->min_y) / g->cell_len));
@@ -483,5 +645,53 @@ int64_t geohip_oracle_ingest(const ing_spec* sp, const ing_grid* g, const char* 
         rec++;
         p = e + 1;
     }
+    return (int64_t)rec;
+}
+
+/* TrajectoryStream batch (CSVTSVToTSpatial / GeoJSONToTSpatial / WKTToTSpatial): as
+   geohip_oracle_ingest plus the objID strings -- oid_buf (oid_cap bytes) and oid_off[rec + 1]
+   (bit 63: null objID).  Returns the record count, -(1 + i) for the first record i rejected
+   (thrown or not restated), or INT64_MIN when oid_cap is too small. */
+int64_t geohip_oracle_ingest_traj(const ing_spec* sp, const ing_traj* tr, const ing_grid* g, const char* text,
+                                  uint64_t nbytes, double* x, double* y, int64_t* ts, uint32_t* cell, char* oid_buf,
+                                  uint64_t oid_cap, uint64_t* oid_off, uint64_t cap) {
+    uint64_t p = 0, rec = 0, ob = 0;
+    while (p < nbytes) {
+        const char* nl = memchr(text + p, '\n', nbytes - p);
+        uint64_t e = nl ? (uint64_t)(nl - text) : nbytes;
+        double xv, yv;
+        int64_t tv;
+        ing_oid oid = {1, NULL, 0, 0};
+        char* own = NULL;
+        int rc = any_record(sp, sp->format == FMT_GEOJSON ? tr : NULL, text + p, e - p, &xv, &yv, &tv, &oid, &own);
+        if (rc) {
+            free(own);
+            return -(int64_t)(rec + 1);
+        }
+        if (rec < cap) {
+            x[rec] = xv;
+            y[rec] = yv;
+            ts[rec] = tv;
+            const int32_t cx = j_d2i(floor((xv - g->min_x) / g->cell_len));
+            const int32_t cy = j_d2i(floor((yv - g->min_y) / g->cell_len));
+            cell[rec] = (cx >= 0 && cx < g->n && cy >= 0 && cy < g->n) ? (uint32_t)cx * (uint32_t)g->n + (uint32_t)cy
+                                                                       : 0xffffffffu;
+            oid_off[rec] = ob | (oid.null ? 1ull << 63 : 0ull);
+            if (!oid.null) {
+                for (size_t i = oid.a; i < oid.b; i++) {
+                    if (oid.buf[i] == '"') continue;
+                    if (ob >= oid_cap) {
+                        free(own);
+                        return INT64_MIN;
+                    }
+                    oid_buf[ob++] = oid.buf[i];
+                }
+            }
+        }
+        free(own);
+        rec++;
+        p = e + 1;
+    }
+    if (rec <= cap) oid_off[rec] = ob;
     return (int64_t)rec;
 }

@@ -61,16 +61,45 @@ FMT_CSV, FMT_GEOJSON, FMT_WKT = 0, 1, 2
 
 
 class IngestSpec(ctypes.Structure):
-    """geohip_ingest_spec: format, delimiter byte, csvTsvSchemaAttr x/y/ts indices."""
+    """geohip_ingest_spec: format, delimiter byte, csvTsvSchemaAttr x/y/ts/objID indices."""
     _fields_ = [("format", c_int32), ("delim", c_int32), ("attr_x", c_int32), ("attr_y", c_int32),
-                ("attr_ts", c_int32), ("reserved", c_int32)]
+                ("attr_ts", c_int32), ("attr_oid", c_int32)]
 
 
-def make_ingest_spec(fmt: int, delimiter: str = ",", attr_x: int = 0, attr_y: int = 1, attr_ts: int = -1) -> IngestSpec:
+def make_ingest_spec(fmt: int, delimiter: str = ",", attr_x: int = 0, attr_y: int = 1, attr_ts: int = -1,
+                     attr_oid: int = 0) -> IngestSpec:
     d = delimiter.encode() if delimiter else b"\0"
     if len(d) != 1:
         raise GeohipUnsupportedError("delimiter must be one byte")
-    return IngestSpec(fmt, d[0], attr_x, attr_y, attr_ts, 0)
+    return IngestSpec(fmt, d[0], attr_x, attr_y, attr_ts, attr_oid)
+
+
+class TrajSpec(ctypes.Structure):
+    """geohip_traj_spec: the TrajectoryStream's DateFormat and GeoJSON property names."""
+    _fields_ = [("date_format", c_int32), ("utc_offset_min", c_int32), ("prop_ts", ctypes.c_char * 60),
+                ("prop_oid", ctypes.c_char * 60)]
+
+
+def make_traj_spec(prop_ts: str = "timestamp", prop_oid: str = "oID", date_format: int = 1,
+                   utc_offset_min: int = 0) -> TrajSpec:
+    """Defaults: conf/geoflink-conf.yml's propertyTimeStamp / propertyObjID and
+    "yyyy-MM-dd HH:mm:ss" (GEOHIP_DATE_YMD_HMS) in UTC."""
+    a, b = prop_ts.encode(), prop_oid.encode()
+    if len(a) > 59 or len(b) > 59:
+        raise GeohipArgumentError("property names of at most 59 bytes")
+    return TrajSpec(date_format, utc_offset_min, a, b)
+
+
+OID_NULL = (1 << 24) - 1  # the length field of a null objID span
+
+
+def oid_spans_to_strings(text: bytes, spans) -> list:
+    """Host view of objID spans (tests, small batches): the str / None per record, quotes deleted."""
+    out = []
+    for v in (int(s) for s in spans):
+        off, ln = v >> 24, v & OID_NULL
+        out.append(None if ln == OID_NULL else text[off:off + ln].replace(b'"', b"").decode("utf-8", "replace"))
+    return out
 
 
 class CsvOutSpec(ctypes.Structure):
@@ -193,6 +222,12 @@ _SIGS = {
                                      POINTER(c_uint64), POINTER(c_uint64)]),
     "geohip_debug_ingest_record": (c_int, [POINTER(IngestSpec), c_char_p, c_uint64, POINTER(c_double),
                                            POINTER(c_double), POINTER(ctypes.c_int64)]),
+    "geohip_debug_ingest_traj_record": (c_int, [POINTER(IngestSpec), POINTER(TrajSpec), c_char_p, c_uint64,
+                                                POINTER(c_double), POINTER(c_double), POINTER(ctypes.c_int64),
+                                                POINTER(c_uint64)]),
+    "geohip_ingest_trajectory": (c_int, [_P, POINTER(Grid), POINTER(IngestSpec), POINTER(TrajSpec), _P, c_uint64, _P,
+                                         _P, _P, _P, _P, c_uint64, POINTER(c_uint64), POINTER(c_uint64)]),
+    "geohip_ingest_oid_compact": (c_int, [_P, _P, c_uint64, _P, c_uint64, _P, c_uint64, _P, POINTER(c_uint64)]),
     "geohip_debug_selftest_fp64": (c_int, [_P, _P, _P, c_uint64, _P, _P, _P, _P]),
     "geohip_debug_classify": (c_int, [POINTER(Grid), c_double, c_double, c_double, _P, _P, c_uint64, _P]),
     "geohip_debug_knn_pass_stats": (c_int, [_P, _P]),
@@ -263,6 +298,18 @@ def debug_ingest_record(spec: IngestSpec, rec: bytes):
     if rc == ERR_ARG:
         raise GeohipArgumentError("bad ingest spec")
     return None if rc else (x.value, y.value, ts.value)
+
+
+def debug_ingest_traj_record(spec: IngestSpec, traj: TrajSpec | None, rec: bytes):
+    """The device trajectory parse on the host: (x, y, ts, oid span relative to rec) or None if
+    rejected."""
+    x, y, ts, oid = c_double(), c_double(), ctypes.c_int64(), c_uint64()
+    rc = lib.geohip_debug_ingest_traj_record(ctypes.byref(spec), ctypes.byref(traj) if traj is not None else None, rec,
+                                             len(rec), ctypes.byref(x), ctypes.byref(y), ctypes.byref(ts),
+                                             ctypes.byref(oid))
+    if rc == ERR_ARG:
+        raise GeohipArgumentError("bad ingest spec")
+    return None if rc else (x.value, y.value, ts.value, oid.value)
 
 
 def _ptr(a):
@@ -855,6 +902,64 @@ class Context:
             raise err
         self._check(rc, "ingest_points")
         return {k: v[:cnt.value] for k, v in out.items()}
+
+    def ingest_trajectory(self, spec: IngestSpec, text, grid: Grid | None = None, traj: TrajSpec | None = None,
+                          with_ts=True, with_cell=False, with_oid=True, cap=None):
+        """geohip_ingest_trajectory (TrajectoryStream: the Point's objID, x, y, timestamp, cell):
+        dict(x, y[, ts][, cell][, oid]) trimmed to the record count; ``oid`` = the objID spans
+        (ingest_oid_compact / oid_spans_to_strings read them)."""
+        if isinstance(text, (bytes, bytearray)):
+            text = np.frombuffer(text, dtype=np.uint8)
+        dev = self._mem_for(text, dtype="uint8")
+        nbytes = int(text.numel()) if dev else int(text.size)
+        if cap is None:
+            cap = nbytes // 2 + 1
+        if dev:
+            import torch
+            mk = lambda dt: torch.empty(max(cap, 1), dtype=dt, device=text.device)  # noqa: E731
+            i64, i32, f64 = torch.int64, torch.int32, torch.float64
+        else:
+            mk = lambda dt: np.empty(max(cap, 1), dtype=dt)  # noqa: E731
+            i64, i32, f64 = np.int64, np.uint32, np.float64
+        out = {"x": mk(f64), "y": mk(f64)}
+        if with_ts:
+            out["ts"] = mk(i64)
+        if with_cell:
+            out["cell"] = mk(i32)
+        if with_oid:
+            out["oid"] = mk(i64)
+        cnt, bad = c_uint64(0), c_uint64(0)
+        rc = lib.geohip_ingest_trajectory(self.h, ctypes.byref(grid) if grid is not None else None, ctypes.byref(spec),
+                                          ctypes.byref(traj) if traj is not None else None, _ptr(text), nbytes,
+                                          _ptr(out["x"]), _ptr(out["y"]), _ptr(out.get("ts")), _ptr(out.get("cell")),
+                                          _ptr(out.get("oid")), cap, ctypes.byref(cnt), ctypes.byref(bad))
+        if rc == ERR_UNSUPPORTED and bad.value != 2**64 - 1:
+            err = GeohipUnsupportedError(f"ingest_trajectory: {lib.geohip_last_error(self.h).decode(errors='replace')}")
+            err.bad = bad.value
+            raise err
+        self._check(rc, "ingest_trajectory")
+        return {k: v[:cnt.value] for k, v in out.items()}
+
+    def ingest_oid_compact(self, text, spans):
+        """geohip_ingest_oid_compact (device tensors): (oid_text uint8, oid_off int64 [m + 1], bit 63 =
+        null) -- the form format_points takes."""
+        import torch
+        self._dev(text, "text", "uint8")
+        self._dev(spans, "spans", "int64")
+        if self._mem != MEM_DEVICE:
+            self.set_mem(MEM_DEVICE)
+        m = spans.numel()
+        off = torch.empty(m + 1, dtype=torch.int64, device=text.device)
+        ln = c_uint64(0)
+        rc = lib.geohip_ingest_oid_compact(self.h, text.data_ptr(), text.numel(), spans.data_ptr(), m, None, 0,
+                                           off.data_ptr(), ctypes.byref(ln))
+        if rc not in (OK, ERR_CAPACITY):
+            self._check(rc, "ingest_oid_compact")
+        out = torch.empty(max(ln.value, 1), dtype=torch.uint8, device=text.device)
+        rc = lib.geohip_ingest_oid_compact(self.h, text.data_ptr(), text.numel(), spans.data_ptr(), m, out.data_ptr(),
+                                           ln.value, off.data_ptr(), ctypes.byref(ln))
+        self._check(rc, "ingest_oid_compact")
+        return out[:ln.value], off
 
     def synth_uniform_async(self, x, y, base, seed, bbox):
         self._dev(x, "x")

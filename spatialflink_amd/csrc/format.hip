@@ -572,8 +572,10 @@ __device__ uint64_t fmt_record(const FmtArgs& a, uint64_t p, unsigned char* dst)
     Sink<WRITE> s{dst, 0};
     char buf[32];
     const long long ts = a.ts ? a.ts[p] : 0ll;
-    const bool has_oid = a.oid != nullptr;
-    const uint64_t ob = has_oid ? a.oid_off[p] : 0, oe = has_oid ? a.oid_off[p + 1] : 0;
+    // bit 63 of oid_off[p]: this point's objID is null (offsets are the low 63 bits)
+    constexpr unsigned long long kOffMask = ~(1ull << 63);
+    const bool has_oid = a.oid != nullptr && !(a.oid_off[p] >> 63);
+    const uint64_t ob = has_oid ? (a.oid_off[p] & kOffMask) : 0, oe = has_oid ? (a.oid_off[p + 1] & kOffMask) : 0;
     char date[20];
     if (a.format != GEOHIP_FMT_CSV && ts != 0) {
         if (a.date != GEOHIP_DATE_YMD_HMS || !format_ymd_hms(ts, a.off_ms, date)) {

@@ -22,6 +22,7 @@ struct IngestArgs {
     double min_x, min_y, cell_len;
     int32_t n;
     int32_t pad;
+    uint64_t* oid;  // nullable: per-record objID spans (ingest::kOidLenBits packing)
 };
 
 inline uint64_t ingest_chunks(uint64_t nbytes) { return (nbytes + kIngestChunk - 1) / kIngestChunk; }
@@ -46,5 +47,13 @@ struct IngestLookback {
 hipError_t launch_ingest(geohip_ctx* ctx, const uint8_t* text, uint64_t nbytes, const IngestArgs& a,
                          const IngestLookback& lb, unsigned long long* total, double* x, double* y, int64_t* ts,
                          uint32_t* cell, uint64_t cap, unsigned long long* bad, hipStream_t st);
+
+// objID spans -> strings: launch_oid_compact without out_text writes the lengths, the scan and
+// out_off (seg[nseg] = the total bytes, seg[nseg + 1] != 0: a span outside the text); with
+// out_text, the bytes (the same len / seg / out_off).  seg holds oid_segments(m) + 2 words.
+uint64_t oid_segments(uint64_t m);
+hipError_t launch_oid_compact(geohip_ctx* ctx, const uint8_t* text, uint64_t nbytes, const uint64_t* spans, uint64_t m,
+                              uint64_t* len, uint64_t* seg, uint64_t* out_off, uint8_t* out_text, uint64_t cap,
+                              hipStream_t st);
 
 }  // namespace geohip

@@ -105,15 +105,19 @@ struct LdsReader {
 // or a record running past the staged bytes -- returns kFallback and takes the general parser.
 // One pass, 32-bit offsets and few branches per byte: the general parser is SALU-bound on
 // divergent per-byte control flow.
+// The objID field (foid, not one of the number fields) is its bytes up to the delimiter: no
+// blanks or quotes, so the span is the field as staged; empty -> kFallback.  c0: the chunk's text
+// offset (spans are batch offsets).
 __device__ __forceinline__ int fast_csv(const uint8_t* __restrict__ s, uint32_t p, uint32_t lim,
-                                        const ingest::Spec& sp, ingest::Parsed* o, int ablate = 0) {
+                                        const ingest::Spec& sp, ingest::Parsed* o, uint64_t c0, int ablate = 0) {
     const uint8_t d = (uint8_t)sp.delim;
     int need = sp.fx > sp.fy ? sp.fx : sp.fy;
     if (sp.fts > need) need = sp.fts;
+    if (sp.foid > need) need = sp.foid;
     for (int f = 0; f <= need; f++) {
         const bool isx = f == sp.fx, isy = f == sp.fy, ist = f == sp.fts;
         if (isx || isy || ist) {
-            if (p >= lim || ((isx || isy) && ist)) return ingest::kFallback;
+            if (p >= lim || ((isx || isy) && ist) || f == sp.foid) return ingest::kFallback;
             const bool neg = s[p] == '-';
             p += neg ? 1u : 0u;
             uint64_t w = 0;
@@ -151,11 +155,16 @@ __device__ __forceinline__ int fast_csv(const uint8_t* __restrict__ s, uint32_t 
                 if (isy) o->y = v;
             }
         } else {
+            const uint32_t fs = p;
             for (; p < lim; p++) {
                 const uint8_t c = s[p];
                 if (c == d || c <= ' ' || c == '"') break;
             }
             if (p >= lim) return ingest::kFallback;
+            if (f == sp.foid) {
+                if (p == fs) return ingest::kFallback;
+                o->oid = ((c0 + fs) << ingest::kOidLenBits) | (uint64_t)(p - fs);
+            }
         }
         const uint8_t c = s[p];
         if (c == d && f < need) {
@@ -255,19 +264,20 @@ __device__ const uint64_t kPow10u[20] = {1ull, 10ull, 100ull, 1000ull, 10000ull,
                                          10000000000000000000ull};
 
 __device__ __forceinline__ int swar_csv(const uint8_t* __restrict__ s, uint32_t p, uint32_t lim,
-                                        const ingest::Spec& sp, ingest::Parsed* o) {
+                                        const ingest::Spec& sp, ingest::Parsed* o, uint64_t c0) {
     if (p + kSwarRecordSpan > lim) return kSwarNo;
     const uint32_t p0 = p;
     const uint32_t d = (uint32_t)(uint8_t)sp.delim;
     int need = sp.fx > sp.fy ? sp.fx : sp.fy;
     if (sp.fts > need) need = sp.fts;
+    if (sp.foid > need) need = sp.foid;
     for (int f = 0; f <= need; f++) {
         if (p - p0 > kSwarFieldSpan) return kSwarNo;
         const Win24 W = lds_win24(s, p);
         const bool isx = f == sp.fx, isy = f == sp.fy, ist = f == sp.fts;
         uint32_t term;
         if (isx || isy || ist) {
-            if ((isx || isy) && ist) return kSwarNo;
+            if (((isx || isy) && ist) || f == sp.foid) return kSwarNo;
             const uint32_t st = W.byte(0) == '-' ? 1u : 0u;
             const uint32_t nd = mask24(nondigit_m(W.v[0]), nondigit_m(W.v[1]), nondigit_m(W.v[2]));
             const uint32_t m1 = nd >> st;
@@ -311,6 +321,10 @@ __device__ __forceinline__ int swar_csv(const uint8_t* __restrict__ s, uint32_t 
                                          eq_m(W.v[2], d) | le20_m(W.v[2]) | eq_m(W.v[2], '"'));
             if (!stop) return kSwarNo;
             term = (uint32_t)__builtin_ctz(stop);
+            if (f == sp.foid) {
+                if (term == 0) return kSwarNo;
+                o->oid = ((c0 + p) << ingest::kOidLenBits) | term;
+            }
         }
         const uint32_t c = W.byte(term);
         if (c == d && f < need) {
@@ -368,6 +382,7 @@ __device__ __forceinline__ void store_record(const IngestArgs& a, uint64_t idx, 
     x[idx] = o.x;
     y[idx] = o.y;
     if (ts) ts[idx] = o.ts;
+    if (a.oid) a.oid[idx] = o.oid;
     if (cell && a.pad == 3) {
         cell[idx] = 0u;
     } else if (cell) {
@@ -425,14 +440,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(GEOHIP
         ingest::Parsed o;
         o.x = o.y = 0.0;
         o.ts = 0;
+        o.oid = ingest::kOidNull;
         int rc = ingest::kFallback;
         if (i < nrec && listed_all) {
             if (a.pad == 1) {
                 o.x = o.y = (double)L.start[i];
                 rc = ingest::kOk;
             } else if (fast) {
-                rc = a.pad == 0 ? swar_csv(st8, L.start[i], stage_len, a.spec, &o) : kSwarNo;
-                if (rc == kSwarNo) rc = fast_csv(st8, L.start[i], stage_len, a.spec, &o, a.pad);
+                rc = a.pad == 0 ? swar_csv(st8, L.start[i], stage_len, a.spec, &o, c0) : kSwarNo;
+                if (rc == kSwarNo) rc = fast_csv(st8, L.start[i], stage_len, a.spec, &o, c0, a.pad);
             }
             undecided |= rc != ingest::kOk;
         }
@@ -508,7 +524,145 @@ __global__ __launch_bounds__(kThreads) void ingest_general(const uint8_t* __rest
     }
 }
 
+// ---- objID spans -> strings (geohip_ingest_oid_compact) --------------------------------------
+// Per record: the span's bytes without '"' (the reference deletes every quote of a CSV record
+// before the split; a GeoJSON objID span holds none).  Lengths, a segmented exclusive scan into
+// out_off (bit 63 = null objID), then the copy.
+constexpr unsigned kOidTB = 256;
+constexpr unsigned kOidPer = 8;                  // records per thread
+constexpr unsigned kOidSeg = kOidTB * kOidPer;   // records per block
+
+__device__ __forceinline__ bool oid_span(uint64_t v, uint64_t* off, uint64_t* len) {
+    *len = v & ((1ull << ingest::kOidLenBits) - 1);
+    *off = v >> ingest::kOidLenBits;
+    return *len != ingest::kOidNull;
+}
+
+__global__ __launch_bounds__(kOidTB) void oid_len(const uint8_t* __restrict__ text, uint64_t nbytes,
+                                                 const uint64_t* __restrict__ spans, uint64_t m,
+                                                 uint64_t* __restrict__ len, uint64_t* __restrict__ seg, uint64_t nseg) {
+    uint64_t sum = 0;
+    for (unsigned k = 0; k < kOidPer; k++) {
+        const uint64_t i = (uint64_t)blockIdx.x * kOidSeg + (uint64_t)k * kOidTB + threadIdx.x;
+        if (i >= m) break;
+        uint64_t off, n, c = 0;
+        if (oid_span(spans[i], &off, &n)) {
+            if (off > nbytes || n > nbytes - off) {
+                atomicOr(reinterpret_cast<unsigned long long*>(seg + nseg + 1), 1ull);
+                n = 0;
+            }
+            for (uint64_t t = 0; t < n; t++) c += text[off + t] != '"' ? 1u : 0u;
+        }
+        len[i] = c;
+        sum += c;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    __shared__ uint64_t s_sum[kOidTB / kWave];
+    if (lane_id() == 0) s_sum[threadIdx.x / kWave] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+        for (unsigned w = 0; w < kOidTB / kWave; w++) t += s_sum[w];
+        seg[blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(1024) void oid_scan_segs(uint64_t* __restrict__ seg, uint64_t nseg) {
+    __shared__ uint64_t part[1024];
+    const uint64_t per = (nseg + 1023) / 1024;
+    const uint64_t b = threadIdx.x * per, e = b + per < nseg ? b + per : nseg;
+    uint64_t s = 0;
+    for (uint64_t u = b; u < e; u++) s += seg[u];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const uint64_t v = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint64_t run = part[threadIdx.x] - s;
+    for (uint64_t u = b; u < e; u++) {
+        const uint64_t c = seg[u];
+        seg[u] = run;
+        run += c;
+    }
+    if (threadIdx.x == 1023) seg[nseg] = part[1023];
+}
+
+__global__ __launch_bounds__(kOidTB) void oid_offsets(const uint64_t* __restrict__ spans, uint64_t m,
+                                                     const uint64_t* __restrict__ len, const uint64_t* __restrict__ seg,
+                                                     uint64_t nseg, uint64_t* __restrict__ out_off) {
+    // thread t owns records b0 + t * kOidPer .. + kOidPer (contiguous), a block scan of their sums
+    __shared__ uint64_t s_tot[kOidTB];
+    const uint64_t b0 = (uint64_t)blockIdx.x * kOidSeg + (uint64_t)threadIdx.x * kOidPer;
+    uint64_t mine = 0;
+    for (unsigned k = 0; k < kOidPer; k++)
+        if (b0 + k < m) mine += len[b0 + k];
+    s_tot[threadIdx.x] = mine;
+    __syncthreads();
+    for (unsigned o = 1; o < kOidTB; o <<= 1) {
+        const uint64_t v = threadIdx.x >= o ? s_tot[threadIdx.x - o] : 0;
+        __syncthreads();
+        s_tot[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint64_t run = seg[blockIdx.x] + s_tot[threadIdx.x] - mine;
+    for (unsigned k = 0; k < kOidPer; k++) {
+        const uint64_t i = b0 + k;
+        if (i >= m) break;
+        uint64_t off, n;
+        const bool real = oid_span(spans[i], &off, &n);
+        out_off[i] = run | (real ? 0ull : 1ull << 63);
+        run += len[i];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) out_off[m] = seg[nseg];
+}
+
+__global__ __launch_bounds__(kOidTB) void oid_write(const uint8_t* __restrict__ text, const uint64_t* __restrict__ spans,
+                                                   uint64_t m, const uint64_t* __restrict__ out_off,
+                                                   uint8_t* __restrict__ out, uint64_t cap) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kOidTB + threadIdx.x; i < m; i += (uint64_t)gridDim.x * kOidTB) {
+        uint64_t off, n;
+        if (!oid_span(spans[i], &off, &n)) continue;
+        uint64_t o = out_off[i] & ~(1ull << 63);
+        for (uint64_t t = 0; t < n; t++) {
+            const uint8_t c = text[off + t];
+            if (c != '"' && o < cap) out[o++] = c;
+        }
+    }
+}
+
 }  // namespace
+
+uint64_t oid_segments(uint64_t m) { return (m + kOidSeg - 1) / kOidSeg; }
+
+hipError_t launch_oid_compact(geohip_ctx* ctx, const uint8_t* text, uint64_t nbytes, const uint64_t* spans, uint64_t m,
+                              uint64_t* len, uint64_t* seg, uint64_t* out_off, uint8_t* out_text, uint64_t cap,
+                              hipStream_t st) {
+    const uint64_t nseg = oid_segments(m);
+    if (out_text) {  // second call: the copy
+        if (m) {
+            const uint64_t g = (m + kOidTB - 1) / kOidTB;
+            tlaunch(ctx, oid_write, (unsigned)(g < 65536 ? g : 65536), kOidTB, 0, st, text, spans, m,
+                    (const uint64_t*)out_off, out_text, cap);
+        }
+        return hipGetLastError();
+    }
+    hipError_t e = hipMemsetAsync(seg + nseg, 0, 16, st);
+    if (e != hipSuccess) return e;
+    if (m) {
+        tlaunch(ctx, oid_len, (unsigned)nseg, kOidTB, 0, st, text, nbytes, spans, m, len, seg, nseg);
+        tlaunch(ctx, oid_scan_segs, 1, 1024, 0, st, seg, nseg);
+        tlaunch(ctx, oid_offsets, (unsigned)nseg, kOidTB, 0, st, spans, m, (const uint64_t*)len, (const uint64_t*)seg,
+                nseg, out_off);
+    } else {
+        e = hipMemsetAsync(out_off, 0, 8, st);
+        if (e != hipSuccess) return e;
+    }
+    return hipGetLastError();
+}
 
 hipError_t launch_ingest(geohip_ctx* ctx, const uint8_t* text, uint64_t nbytes, const IngestArgs& a,
                          const IngestLookback& lb, unsigned long long* total, double* x, double* y, int64_t* ts,

@@ -35,16 +35,30 @@ constexpr int kFallback = 1;
 
 enum Format { kCsv = 0, kGeoJson = 1, kWkt = 2 };
 
+// The objID of a record as a span of the batch text: (offset << kOidLenBits) | length, the bytes
+// the reference's String holds once the quotes in them are deleted (CSV) -- or kOidNull for a
+// null objID.  Offsets below 2^40 (batches are < 1 TiB), lengths below kMaxTokenLen.
+constexpr int kOidLenBits = 24;
+constexpr uint64_t kOidNull = (1ull << kOidLenBits) - 1;
+constexpr int kPropKeyMax = 60;
+
 struct Spec {
     int32_t format;
     int32_t delim;  // CSV/TSV delimiter byte
     int32_t fx, fy;  // csvTsvSchemaAttr[2], [3]
     int32_t fts;     // csvTsvSchemaAttr[1] (Long.valueOf timestamp), < 0: not parsed
+    int32_t foid;    // csvTsvSchemaAttr[0] (the objID span), < 0: not produced
+    // GeoJSONToTSpatial (traj != 0): properties[kts] parsed by the DateFormat (date_fmt: 0 none,
+    // 1 "yyyy-MM-dd HH:mm:ss" in a zone of fixed offset utc_off_min), properties[koid] the objID
+    int32_t traj, date_fmt, utc_off_min;
+    int32_t kts_len, koid_len;
+    char kts[kPropKeyMax], koid[kPropKeyMax];
 };
 
 struct Parsed {
     double x, y;
     int64_t ts;
+    uint64_t oid;  // span (kOidNull: null); only when the spec asks for it
 };
 
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -391,10 +405,18 @@ __host__ __device__ inline int field_long(const R& rd, uint64_t t0, uint64_t t1,
 // number token is its text without surrounding chars <= ' ' or quotes (Double.valueOf trims).
 // Long.valueOf does not trim: the timestamp field is rejected if \s survives the split around it
 // (before field 0, after the last field) or if it holds any other control character.
+//
+// The objID (CSVTSVToTSpatial's strArrayList.get(csvTsvSchemaAttr.get(0)), Deserialization.java:
+// 313-314) is the field's raw bytes between its separators: the \s / quote runs the split consumes
+// around the delimiter are outside it, the leading \s of field 0 and the trailing \s of the last
+// field stay (no separator match there), and the quotes inside it are deleted when the span is
+// read (geohip_ingest_oid_compact).  An empty or control-character objID goes to the host.
 template <class R>
 __host__ __device__ inline int parse_csv(const R& rd, uint64_t p, const Spec& sp, Parsed* o) {
     int need = sp.fx > sp.fy ? sp.fx : sp.fy;
     if (sp.fts > need) need = sp.fts;
+    if (sp.foid > need) need = sp.foid;
+    const uint64_t rec0 = p;
     const uint8_t d = (uint8_t)sp.delim;
     const bool wsd = is_jspace(d);
     for (int f = 0;; f++) {
@@ -446,6 +468,12 @@ __host__ __device__ inline int parse_csv(const R& rd, uint64_t p, const Spec& sp
         if (f == sp.fts && (ctrl || (f == 0 && lead) || (!sep && trail) || t0 == ~0ull ||
                             field_long(rd, t0, t1, &o->ts) != kOk))
             return kFallback;
+        if (f == sp.foid) {
+            if (ctrl || t0 == ~0ull) return kFallback;
+            const uint64_t a = f == 0 ? rec0 : t0, b = sep ? t1 : p;  // p: the record's '\n'
+            if (b - a >= kMaxTokenLen) return kFallback;
+            o->oid = (a << kOidLenBits) | (b - a);
+        }
         if (f == need) return kOk;
         if (!sep) return kFallback;  // fewer fields than the schema names: the reference throws
     }
@@ -494,6 +522,234 @@ __host__ __device__ inline int parse_geojson(const R& rd, uint64_t p, Parsed* o)
     while (json_space(rd(p))) p++;
     const uint8_t c = rd(p);
     return (c == ']' || c == ',') ? kOk : kFallback;
+}
+
+// ---- GeoJSONToTSpatial (Deserialization.java:149-208): properties[propertyTimeStamp] through the
+// DateFormat, properties[propertyObjID] as nodeOId.toString().replaceAll("\"", "").
+// The record is the Kafka value object; Jackson's ObjectNode keeps the LAST member of a repeated
+// key, so a later "properties" (or a later key inside it) replaces an earlier one.
+
+// one JSON string at p ('"'): the end (past the closing quote) and whether it holds a backslash
+template <class R>
+__host__ __device__ inline bool json_string_end(const R& rd, uint64_t p, uint64_t* end, bool* esc) {
+    *esc = false;
+    for (p++;; p++) {
+        const uint8_t c = rd(p);
+        if (c == '\n') return false;
+        if (c == '"') break;
+        if (c == '\\') {
+            *esc = true;
+            if (rd(++p) == '\n') return false;
+        }
+    }
+    *end = p + 1;
+    return true;
+}
+// any JSON value at p: its end (nested containers by a depth count, strings skipped whole)
+template <class R>
+__host__ __device__ inline bool json_skip_value(const R& rd, uint64_t p, uint64_t* end) {
+    const uint64_t p0 = p;
+    int depth = 0;
+    for (;;) {
+        const uint8_t c = rd(p);
+        if (c == '\n') return false;
+        if (c == '"') {
+            bool esc;
+            if (!json_string_end(rd, p, &p, &esc)) return false;
+        } else if (c == '{' || c == '[') {
+            depth++;
+            p++;
+        } else if (c == '}' || c == ']') {
+            if (depth == 0) break;  // the enclosing container's end
+            depth--;
+            p++;
+        } else if (c == ',' && depth == 0) {
+            break;
+        } else {
+            p++;
+        }
+        if (depth == 0 && (rd(p) == ',' || rd(p) == '}' || rd(p) == ']' || json_space(rd(p)))) break;
+    }
+    *end = p;
+    return p != p0;  // an empty value is not JSON
+}
+template <class R>
+__host__ __device__ inline uint64_t json_ws(const R& rd, uint64_t p) {
+    while (json_space(rd(p))) p++;
+    return p;
+}
+template <class R>
+__host__ __device__ inline bool key_is(const R& rd, uint64_t a, uint64_t b, const char* k, int klen) {
+    if (b - a != (uint64_t)klen) return false;
+    for (int i = 0; i < klen; i++)
+        if (rd(a + (uint64_t)i) != (uint8_t)k[i]) return false;
+    return true;
+}
+
+// SimpleDateFormat("yyyy-MM-dd HH:mm:ss").parse (lenient, zone of fixed offset off_min) of the
+// string s[a, b) (no escapes), as DateFormat.parse(String) then Date.getTime():
+//   * 'yyyy-MM-dd HH:mm:ss' with exactly those digit counts (after ' ' / '\t', which subParse
+//     skips), year 1583..9999 (Gregorian throughout), any 2-digit month / day / hour / minute /
+//     second (the lenient calendar carries them over linearly), followed by the end or by an
+//     ASCII character that cannot continue the seconds number -> the epoch milliseconds;
+//   * nothing parseable at all (empty, or a first character that starts no number: ASCII, not a
+//     digit, '-' or '+') -> ParseException, caught by the reference: 0;
+//   * anything else (other digit counts, signs, non-ASCII, the other fields' leniencies) -> the
+//     host.
+__host__ __device__ inline int64_t days_from_civil(int64_t y, int64_t m, int64_t d) {
+    y -= m <= 2 ? 1 : 0;
+    const int64_t era = (y >= 0 ? y : y - 399) / 400;
+    const int64_t yoe = y - era * 400;
+    const int64_t doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+    const int64_t doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+    return era * 146097 + doe - 719468;
+}
+template <class R>
+__host__ __device__ inline int parse_date_ymd_hms(const R& rd, uint64_t a, uint64_t b, int32_t off_min, int64_t* ms) {
+    while (a < b && (rd(a) == ' ' || rd(a) == '\t')) a++;
+    if (a == b) {
+        *ms = 0;
+        return kOk;
+    }
+    const uint8_t c0 = rd(a);
+    // ('N' could begin a NaN symbol DecimalFormat accepts: the host decides)
+    if (c0 < 0x80 && !is_digit(c0) && c0 != '-' && c0 != '+' && c0 != 'N') {
+        *ms = 0;
+        return kOk;
+    }
+    const char pat[] = "dddd-dd-dd dd:dd:dd";
+    if (b - a < 19) return kFallback;
+    int64_t v[6] = {0, 0, 0, 0, 0, 0};
+    int k = 0;
+    for (int i = 0; i < 19; i++) {
+        const uint8_t c = rd(a + (uint64_t)i);
+        if (pat[i] == 'd') {
+            if (!is_digit(c)) return kFallback;
+            v[k] = v[k] * 10 + (c - '0');
+        } else {
+            if (c != (uint8_t)pat[i]) return kFallback;
+            k++;
+        }
+    }
+    if (b - a > 19) {
+        const uint8_t c = rd(a + 19);
+        if (c >= 0x80 || is_digit(c) || c == 'E' || c == 'e' || c == '.' || c == ',') return kFallback;
+    }
+    if (v[0] < 1583) return kFallback;
+    // month carried into the year (month 0 = December of the year before), day 0 = the last day
+    // of the month before, hours / minutes / seconds past their range carried forward
+    const int64_t m0 = v[1] - 1;
+    const int64_t y = v[0] + (m0 >= 0 ? m0 / 12 : -1);
+    const int64_t m = (m0 % 12 + 12) % 12 + 1;
+    const int64_t days = days_from_civil(y, m, 1) + v[2] - 1;
+    const int64_t secs = ((days * 24 + v[3]) * 60 + v[4]) * 60 + v[5] - (int64_t)off_min * 60;
+    *ms = secs * 1000;
+    return kOk;
+}
+
+template <class R>
+__host__ __device__ inline int parse_geojson_traj(const R& rd, uint64_t p, const Spec& sp, Parsed* o) {
+    if (parse_geojson(rd, p, o) != kOk) return kFallback;
+    o->ts = 0;
+    o->oid = kOidNull;
+    p = json_ws(rd, p);
+    if (rd(p) != '{') return kFallback;
+    p = json_ws(rd, p + 1);
+    uint64_t ts_a = 0, ts_b = 0, oid_a = 0, oid_b = 0;  // value spans of the last "properties"
+    bool ts_found = false, oid_found = false;
+    for (;;) {
+        if (rd(p) != '"') return kFallback;
+        uint64_t ke;
+        bool esc;
+        if (!json_string_end(rd, p, &ke, &esc) || esc) return kFallback;  // escaped keys: the host
+        const bool props = key_is(rd, p + 1, ke - 1, "properties", 10);
+        p = json_ws(rd, ke);
+        if (rd(p) != ':') return kFallback;
+        p = json_ws(rd, p + 1);
+        uint64_t ve;
+        if (props) {
+            ts_found = oid_found = false;  // this "properties" replaces any earlier one
+            if (rd(p) == '{') {
+                uint64_t q = json_ws(rd, p + 1);
+                if (rd(q) != '}') {
+                    for (;;) {
+                        if (rd(q) != '"') return kFallback;
+                        uint64_t k2;
+                        if (!json_string_end(rd, q, &k2, &esc) || esc) return kFallback;
+                        const bool is_ts = key_is(rd, q + 1, k2 - 1, sp.kts, sp.kts_len);
+                        const bool is_oid = key_is(rd, q + 1, k2 - 1, sp.koid, sp.koid_len);
+                        q = json_ws(rd, k2);
+                        if (rd(q) != ':') return kFallback;
+                        q = json_ws(rd, q + 1);
+                        uint64_t e2;
+                        if (!json_skip_value(rd, q, &e2)) return kFallback;
+                        if (is_ts) {
+                            ts_found = true;
+                            ts_a = q;
+                            ts_b = e2;
+                        }
+                        if (is_oid) {
+                            oid_found = true;
+                            oid_a = q;
+                            oid_b = e2;
+                        }
+                        q = json_ws(rd, e2);
+                        if (rd(q) == ',') {
+                            q = json_ws(rd, q + 1);
+                            continue;
+                        }
+                        if (rd(q) != '}') return kFallback;
+                        break;
+                    }
+                }
+                ve = q + 1;
+            } else if (!json_skip_value(rd, p, &ve)) {
+                return kFallback;
+            }
+        } else if (!json_skip_value(rd, p, &ve)) {
+            return kFallback;
+        }
+        p = json_ws(rd, ve);
+        if (rd(p) == ',') {
+            p = json_ws(rd, p + 1);
+            continue;
+        }
+        if (rd(p) != '}') return kFallback;
+        break;
+    }
+    if (rd(json_ws(rd, p + 1)) != '\n') return kFallback;  // trailing text after the value
+    if (ts_found && sp.date_fmt != 0) {
+        // nodeTime.textValue(): a string's text, null (-> NullPointerException) for other nodes
+        if (rd(ts_a) != '"') return kFallback;
+        uint64_t e;
+        bool esc;
+        if (!json_string_end(rd, ts_a, &e, &esc) || esc || e != ts_b) return kFallback;
+        if (parse_date_ymd_hms(rd, ts_a + 1, ts_b - 1, sp.utc_off_min, &o->ts) != kOk) return kFallback;
+    }
+    if (oid_found) {
+        // toString() then every '"' deleted: a string's characters (no escapes, printable ASCII
+        // here), an integer's digits, true / false / null as written; others -> the host
+        const uint8_t c = rd(oid_a);
+        uint64_t a = oid_a, b = oid_b;
+        if (c == '"') {
+            a++;
+            b--;
+            for (uint64_t t = a; t < b; t++) {
+                const uint8_t ch = rd(t);
+                if (ch < 0x20 || ch >= 0x7f || ch == '\\') return kFallback;
+            }
+        } else if (c == '-' || is_digit(c)) {
+            uint64_t t = a + (c == '-' ? 1 : 0);
+            if (t >= b || (rd(t) == '0' && (b - t > 1 || c == '-'))) return kFallback;  // "-0", leading zeros
+            for (; t < b; t++)
+                if (!is_digit(rd(t))) return kFallback;  // fractions, exponents: DoubleNode text differs
+        } else if (!(key_is(rd, a, b, "true", 4) || key_is(rd, a, b, "false", 5) || key_is(rd, a, b, "null", 4))) {
+            return kFallback;
+        }
+        if (b - a >= kMaxTokenLen) return kFallback;
+        o->oid = (a << kOidLenBits) | (b - a);
+    }
+    return kOk;
 }
 
 // JTS WKTReader tokenizer word characters (a-z A-Z 0-9 - + . and 160-255)
@@ -557,9 +813,10 @@ __host__ __device__ inline int parse_wkt(const R& rd, uint64_t p, Parsed* o) {
 
 template <class R>
 __host__ __device__ inline int parse_record(const R& rd, uint64_t start, const Spec& sp, Parsed* o) {
+    o->oid = kOidNull;
     if (sp.format == kCsv) return parse_csv(rd, start, sp, o);
-    if (sp.format == kGeoJson) return parse_geojson(rd, start, o);
-    return parse_wkt(rd, start, o);
+    if (sp.format == kGeoJson) return sp.traj ? parse_geojson_traj(rd, start, sp, o) : parse_geojson(rd, start, o);
+    return parse_wkt(rd, start, o);  // WKTToTSpatial: objID null, timestamp 0 as WKTToSpatial
 }
 
 // HelperClass.assignGridCellID axis index: (int)Math.floor((v - min) / cellLength)
