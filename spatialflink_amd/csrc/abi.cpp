@@ -31,7 +31,7 @@ enum Slot {
     S_MASK, S_UCNT, S_OFFS, S_TOTAL, S_OUT_IDX, S_OUT_PAIRS, S_SPILL_D, S_SPILL_I, S_SPILL_CNT, S_RLB, S_TRACE,
     S_J0, S_J1, S_J2, S_J3, S_J4, S_J5, S_J6, S_J7, S_J8, S_J9, S_J10, S_J11, S_J12, S_J13, S_J14, S_J15,
     S_J16, S_J17, S_J18, S_J19, S_J20, S_J21, S_J22, S_J23, S_J24, S_J25,
-    S_I0, S_I1, S_I2, S_I3, S_I4, S_I5, S_I6, S_I7,
+    S_I0, S_I1, S_I2, S_I3, S_I4, S_I5, S_I6, S_I7, S_I8, S_I9, S_I10, S_I11,
     S_COUNT
 };
 
@@ -1212,16 +1212,19 @@ int geohip_debug_knn_pass_trace(geohip_ctx* ctx, const geohip_grid* grid, const 
 namespace geohip {
 int ctx_fail(geohip_ctx* ctx, int code, const std::string& msg) { return fail(ctx, code, msg); }
 int ctx_ensure(geohip_ctx* ctx, int slot, size_t bytes, void** out) {
+    if (slot < 0 || S_J0 + slot > S_J25) return fail(ctx, GEOHIP_ERR_DEVICE, "internal: scratch slot out of range");
     int rc = ensure(ctx, (Slot)(S_J0 + slot), bytes);
     if (!rc) *out = ctx->buf[S_J0 + slot];
     return rc;
 }
 int ctx_ensure_ingest(geohip_ctx* ctx, int slot, size_t bytes, void** out) {
+    if (slot < 0 || S_I0 + slot >= S_COUNT) return fail(ctx, GEOHIP_ERR_DEVICE, "internal: scratch slot out of range");
     int rc = ensure(ctx, (Slot)(S_I0 + slot), bytes);
     if (!rc) *out = ctx->buf[S_I0 + slot];
     return rc;
 }
 int ctx_ensure_ingest_zeroed(geohip_ctx* ctx, int slot, size_t bytes, void** out) {
+    if (slot < 0 || S_I0 + slot >= S_COUNT) return fail(ctx, GEOHIP_ERR_DEVICE, "internal: scratch slot out of range");
     int rc = ensure_zeroed(ctx, (Slot)(S_I0 + slot), bytes);
     if (!rc) *out = ctx->buf[S_I0 + slot];
     return rc;
@@ -1236,6 +1239,7 @@ unsigned long long ctx_next_epoch(geohip_ctx* ctx) {
 // all of it again when the epoch counter wraps (a word last written 2^22 - 1 launches ago by a
 // larger batch would otherwise read as ready).
 int ctx_lookback_status(geohip_ctx* ctx, int slot, size_t bytes, void** out, unsigned long long* epoch) {
+    if (slot < 0 || S_I0 + slot >= S_COUNT) return fail(ctx, GEOHIP_ERR_DEVICE, "internal: scratch slot out of range");
     const Slot s = (Slot)(S_I0 + slot);
     int rc = ensure_zeroed(ctx, s, bytes);
     if (rc) return rc;
