@@ -166,11 +166,22 @@ int geohip_join_pp_count_only(geohip_ctx* ctx, const geohip_grid* grid_data, con
    with <= 3 coords): GEOHIP_ERR_ARG.  npoly == 0: no pairs, the polygon arrays may be NULL.
    Distances: JTS point.distance(polygon) -- 0 inside the shell and outside every hole, or on any
    ring; else the minimum over every ring's segments.
+   nv = the length of vx / vy: every ring offset the polygons use must be <= nv (GEOHIP_ERR_ARG
+   otherwise -- the library reads no vertex past it).
    out_pairs: 2*cap uint32 (poly_idx, point_idx), unordered. */
 int geohip_range_ppoly(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
                        uint64_t n, const uint32_t* poly_rings, const uint32_t* ring_off, const double* vx,
-                       const double* vy, uint32_t npoly, double r, int approximate,
+                       const double* vy, uint64_t nv, uint32_t npoly, double r, int approximate,
                        uint32_t* out_pairs, uint64_t cap, uint64_t* out_count);
+
+/* geohip_range_ppoly over one pane of a sliding window (pane reuse): point
+   indices are point_base + the position in the pane (mod 2^32), i.e. stream positions when
+   point_base is the pane's first one -- a pane is evaluated once and its pairs serve every window
+   that holds it unchanged (a window's local index = stream position - its first position). */
+int geohip_range_ppoly_pane(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
+                            uint64_t n, uint32_t point_base, const uint32_t* poly_rings, const uint32_t* ring_off,
+                            const double* vx, const double* vy, uint64_t nv, uint32_t npoly, double r,
+                            int approximate, uint32_t* out_pairs, uint64_t cap, uint64_t* out_count);
 
 /* Point-polygon window join: the polygon stream replicated to its guaranteed and candidate
    cells on grid_query (UniformGrid.java:193-206, 398-410), joined with the points' gridIDs on
@@ -179,18 +190,19 @@ int geohip_range_ppoly(geohip_ctx* ctx, const geohip_grid* grid, const double* x
    geohip_range_ppoly (host arrays).  out_pairs: 2*cap uint32 (point_idx, poly_idx), unordered. */
 int geohip_join_ppoly(geohip_ctx* ctx, const geohip_grid* grid_points, const geohip_grid* grid_query,
                       const double* x, const double* y, uint64_t n, const uint32_t* poly_rings,
-                      const uint32_t* ring_off, const double* vx, const double* vy, uint32_t npoly,
-                      double r, int approximate, uint32_t* out_pairs, uint64_t cap, uint64_t* out_count);
+                      const uint32_t* ring_off, const double* vx, const double* vy, uint64_t nv,
+                      uint32_t npoly, double r, int approximate, uint32_t* out_pairs, uint64_t cap,
+                      uint64_t* out_count);
 
 /* Point-polygon kNN of one query polygon of nring rings (ring j = vx/vy[ring_off[j] ..
-   ring_off[j+1]), host arrays, built as for geohip_range_ppoly): candidates are the points of
+   ring_off[j+1]), host arrays of nv vertices, built as for geohip_range_ppoly): candidates are the points of
    the polygon's G u C cells (no radius filter); distance = JTS point.distance(polygon), or the
    bbox distance (DistanceFunctions.java:150-200) when approximate.  Output: the
    min(k, candidates) smallest (distance, idx) ascending by distance bits then idx (a NaN bbox
    distance ranks after +Infinity); any k >= 1. */
 int geohip_knn_ppoly(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
                      uint64_t n, const uint32_t* ring_off, uint32_t nring, const double* vx,
-                     const double* vy, double r, uint32_t k, int approximate,
+                     const double* vy, uint64_t nv, double r, uint32_t k, int approximate,
                      uint32_t* out_idx, double* out_dist, uint32_t* out_count);
 /* Enqueue-only form of geohip_knn_ppoly (GEOHIP_MEM_DEVICE window and outputs; the polygon stays
    host memory and is planned once per ctx): k (dist, idx) ascending, entries past the candidate
@@ -198,7 +210,7 @@ int geohip_knn_ppoly(geohip_ctx* ctx, const geohip_grid* grid, const double* x, 
    round trip: the selection path is chosen from the previous call's candidate count. */
 int geohip_knn_ppoly_async(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
                            uint64_t n, const uint32_t* ring_off, uint32_t nring, const double* vx,
-                           const double* vy, double r, uint32_t k, int approximate,
+                           const double* vy, uint64_t nv, double r, uint32_t k, int approximate,
                            uint32_t* out_idx, double* out_dist, uint32_t* out_count_dev);
 
 /* ---- device-resident pipeline forms (GEOHIP_MEM_DEVICE pointers; enqueue only) -------- */

@@ -205,13 +205,15 @@ _SIGS = {
                                c_int, _P, c_uint64, POINTER(c_uint64)]),
     "geohip_join_pp_count_only": (c_int, [_P, POINTER(Grid), POINTER(Grid), _P, _P, c_uint64, _P, _P, c_uint64,
                                           c_double, c_int, POINTER(c_uint64)]),
-    "geohip_range_ppoly": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, _P, _P, _P, _P, c_uint32, c_double, c_int,
+    "geohip_range_ppoly": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, _P, _P, _P, _P, c_uint64, c_uint32, c_double, c_int,
                                    _P, c_uint64, POINTER(c_uint64)]),
-    "geohip_join_ppoly": (c_int, [_P, POINTER(Grid), POINTER(Grid), _P, _P, c_uint64, _P, _P, _P, _P, c_uint32,
+    "geohip_range_ppoly_pane": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_uint32, _P, _P, _P, _P, c_uint64, c_uint32,
+                                        c_double, c_int, _P, c_uint64, POINTER(c_uint64)]),
+    "geohip_join_ppoly": (c_int, [_P, POINTER(Grid), POINTER(Grid), _P, _P, c_uint64, _P, _P, _P, _P, c_uint64, c_uint32,
                                   c_double, c_int, _P, c_uint64, POINTER(c_uint64)]),
-    "geohip_knn_ppoly": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, _P, c_uint32, _P, _P, c_double, c_uint32, c_int,
+    "geohip_knn_ppoly": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, _P, c_uint32, _P, _P, c_uint64, c_double, c_uint32, c_int,
                                  _P, _P, POINTER(c_uint32)]),
-    "geohip_knn_ppoly_async": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, _P, c_uint32, _P, _P, c_double, c_uint32,
+    "geohip_knn_ppoly_async": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, _P, c_uint32, _P, _P, c_uint64, c_double, c_uint32,
                                        c_int, _P, _P, _P]),
     "geohip_plan_point": (c_int, [POINTER(Grid), c_double, c_double, c_double, POINTER(Rect), POINTER(c_uint32),
                                   POINTER(Rect), POINTER(c_uint32), POINTER(c_int32), POINTER(c_int32)]),
@@ -352,7 +354,7 @@ def _poly_arrays(poly_rings, ring_off, vx, vy):
 
 
 def _check_rings(ring_off, vx, vy):
-    """The C ABI takes no vertex count: ring offsets past the vertex arrays are caught here."""
+    """Python-side argument check (the C side checks ring offsets against the vertex count too)."""
     if len(vx) != len(vy):
         raise GeohipArgumentError(f"vx and vy differ in length ({len(vx)} vs {len(vy)})")
     if len(ring_off) and int(ring_off.max()) > len(vx):
@@ -765,20 +767,26 @@ class Context:
         return cnt.value
 
     def range_ppoly(self, grid: Grid, x, y, ring_off, vx, vy, r, approximate=False, cap=None, out=None,
-                    poly_rings=None):
+                    poly_rings=None, point_base=None):
         """Pairs (polygon idx, point idx).  ``out``: optional preallocated [cap, 2] buffer.
         ``poly_rings``: polygon i = rings [poly_rings[i], poly_rings[i+1]) of ``ring_off``
-        (shell and holes, Polygon.createPolygon); None = one ring per polygon."""
+        (shell and holes, Polygon.createPolygon); None = one ring per polygon.  ``point_base``
+        (geohip_range_ppoly_pane): point indices are point_base + position (mod 2^32)."""
         x, y = _f64(x), _f64(y)
         self._mem_for(x, y)
         pr, ring_off, vx, vy, npoly = _poly_arrays(poly_rings, ring_off, vx, vy)
         cnt = c_uint64(0)
+        if point_base is None:
+            call = lib.geohip_range_ppoly
+        else:
+            base = int(point_base) & 0xFFFFFFFF
+            call = lambda h, g, px, py, n, *rest: lib.geohip_range_ppoly_pane(h, g, px, py, n, base, *rest)  # noqa: E731
         if out is not None:
             cap = len(out) if cap is None else min(cap, len(out))
         if cap is None:
-            rc = lib.geohip_range_ppoly(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), len(x), _ptr(pr),
-                                        _ptr(ring_off), _ptr(vx), _ptr(vy), npoly, r, int(approximate), None, 0,
-                                        ctypes.byref(cnt))
+            rc = call(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), len(x), _ptr(pr),
+                      _ptr(ring_off), _ptr(vx), _ptr(vy), len(vx), npoly, r, int(approximate), None, 0,
+                      ctypes.byref(cnt))
             if rc not in (OK, ERR_CAPACITY):
                 self._check(rc, "range_ppoly")
             cap = cnt.value
@@ -789,8 +797,8 @@ class Context:
             out = torch.empty((max(cap, 1), 2), dtype=torch.int32, device=x.device)
         else:
             out = np.empty((max(cap, 1), 2), dtype=np.uint32)
-        rc = lib.geohip_range_ppoly(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), len(x), _ptr(pr), _ptr(ring_off),
-                                    _ptr(vx), _ptr(vy), npoly, r, int(approximate), _ptr(out), cap, ctypes.byref(cnt))
+        rc = call(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), len(x), _ptr(pr), _ptr(ring_off),
+                  _ptr(vx), _ptr(vy), len(vx), npoly, r, int(approximate), _ptr(out), cap, ctypes.byref(cnt))
         self._check(rc, "range_ppoly")
         return out[:cnt.value]
 
@@ -803,7 +811,7 @@ class Context:
         pr, ring_off, vx, vy, npoly = _poly_arrays(poly_rings, ring_off, vx, vy)
         cnt = c_uint64(0)
         args = (self.h, ctypes.byref(grid_points), ctypes.byref(grid_query), _ptr(x), _ptr(y), len(x), _ptr(pr),
-                _ptr(ring_off), _ptr(vx), _ptr(vy), npoly, r, int(approximate))
+                _ptr(ring_off), _ptr(vx), _ptr(vy), len(vx), npoly, r, int(approximate))
         if out is not None:
             cap = len(out) if cap is None else min(cap, len(out))
         if cap is None:
@@ -839,7 +847,7 @@ class Context:
             od = np.empty(k, dtype=np.float64)
         cnt = c_uint32(0)
         rc = lib.geohip_knn_ppoly(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), len(x), _ptr(ring_off),
-                                  len(ring_off) - 1, _ptr(vx), _ptr(vy), r, k, int(approximate), _ptr(oi), _ptr(od),
+                                  len(ring_off) - 1, _ptr(vx), _ptr(vy), len(vx), r, k, int(approximate), _ptr(oi), _ptr(od),
                                   ctypes.byref(cnt))
         self._check(rc, "knn_ppoly")
         return oi[:cnt.value], od[:cnt.value]
@@ -861,7 +869,7 @@ class Context:
         if self._mem != MEM_DEVICE:
             self.set_mem(MEM_DEVICE)
         rc = lib.geohip_knn_ppoly_async(self.h, ctypes.byref(grid), x.data_ptr(), y.data_ptr(), x.numel(),
-                                        _ptr(ring_off), len(ring_off) - 1, _ptr(vx), _ptr(vy), r, k, int(approximate),
+                                        _ptr(ring_off), len(ring_off) - 1, _ptr(vx), _ptr(vy), len(vx), r, k, int(approximate),
                                         out_idx.data_ptr(), out_dist.data_ptr(), out_count.data_ptr())
         if rc:
             self._check(rc, "knn_ppoly_async")

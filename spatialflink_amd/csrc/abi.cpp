@@ -1027,40 +1027,51 @@ int geohip_join_pp_count_only(geohip_ctx* ctx, const geohip_grid* grid_data, con
 
 int geohip_range_ppoly(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
                        const uint32_t* poly_rings, const uint32_t* ring_off, const double* vx, const double* vy,
-                       uint32_t npoly, double r, int approximate, uint32_t* out_pairs, uint64_t cap,
+                       uint64_t nv, uint32_t npoly, double r, int approximate, uint32_t* out_pairs, uint64_t cap,
                        uint64_t* out_count) {
     int rc = begin(ctx);
     if (rc) return rc;
-    return ppoly_impl(ctx, grid, nullptr, 0, x, y, n, poly_rings, ring_off, vx, vy, npoly, r, approximate, out_pairs,
+    return ppoly_impl(ctx, grid, nullptr, 0, x, y, n, poly_rings, ring_off, vx, vy, nv, npoly, r, approximate, out_pairs,
                       cap, out_count);
+}
+
+int geohip_range_ppoly_pane(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
+                            uint32_t point_base, const uint32_t* poly_rings, const uint32_t* ring_off, const double* vx,
+                            const double* vy, uint64_t nv, uint32_t npoly, double r, int approximate,
+                            uint32_t* out_pairs, uint64_t cap, uint64_t* out_count) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    return ppoly_impl(ctx, grid, nullptr, 0, x, y, n, poly_rings, ring_off, vx, vy, nv, npoly, r, approximate, out_pairs,
+                      cap, out_count, point_base);
 }
 
 int geohip_join_ppoly(geohip_ctx* ctx, const geohip_grid* grid_points, const geohip_grid* grid_query, const double* x,
                       const double* y, uint64_t n, const uint32_t* poly_rings, const uint32_t* ring_off,
-                      const double* vx, const double* vy, uint32_t npoly, double r, int approximate,
+                      const double* vx, const double* vy, uint64_t nv, uint32_t npoly, double r, int approximate,
                       uint32_t* out_pairs, uint64_t cap, uint64_t* out_count) {
     int rc = begin(ctx);
     if (rc) return rc;
-    return ppoly_impl(ctx, grid_points, grid_query, 1, x, y, n, poly_rings, ring_off, vx, vy, npoly, r, approximate,
+    return ppoly_impl(ctx, grid_points, grid_query, 1, x, y, n, poly_rings, ring_off, vx, vy, nv, npoly, r, approximate,
                       out_pairs, cap, out_count);
 }
 
 int geohip_knn_ppoly(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
-                     const uint32_t* ring_off, uint32_t nring, const double* vx, const double* vy, double r,
-                     uint32_t k, int approximate, uint32_t* out_idx, double* out_dist, uint32_t* out_count) {
+                     const uint32_t* ring_off, uint32_t nring, const double* vx, const double* vy, uint64_t nv,
+                     double r, uint32_t k, int approximate, uint32_t* out_idx, double* out_dist, uint32_t* out_count) {
     int rc = begin(ctx);
     if (rc) return rc;
-    return knn_ppoly_impl(ctx, grid, x, y, n, ring_off, nring, vx, vy, r, k, approximate, out_idx, out_dist,
+    return knn_ppoly_impl(ctx, grid, x, y, n, ring_off, nring, vx, vy, nv, r, k, approximate, out_idx, out_dist,
                           out_count, false);
 }
 
 int geohip_knn_ppoly_async(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
-                           const uint32_t* ring_off, uint32_t nring, const double* vx, const double* vy, double r,
-                           uint32_t k, int approximate, uint32_t* out_idx, double* out_dist, uint32_t* out_count_dev) {
+                           const uint32_t* ring_off, uint32_t nring, const double* vx, const double* vy, uint64_t nv,
+                           double r, uint32_t k, int approximate, uint32_t* out_idx, double* out_dist,
+                           uint32_t* out_count_dev) {
     int rc = begin(ctx);
     if (rc) return rc;
     if (ctx->mem != GEOHIP_MEM_DEVICE) return fail(ctx, GEOHIP_ERR_ARG, "async forms need GEOHIP_MEM_DEVICE");
-    return knn_ppoly_impl(ctx, grid, x, y, n, ring_off, nring, vx, vy, r, k, approximate, out_idx, out_dist,
+    return knn_ppoly_impl(ctx, grid, x, y, n, ring_off, nring, vx, vy, nv, r, k, approximate, out_idx, out_dist,
                           out_count_dev, true);
 }
 

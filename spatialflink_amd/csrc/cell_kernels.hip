@@ -591,6 +591,7 @@ struct PairSink {
     uint64_t cap;                     // pairs at or beyond cap are dropped (size reported by the scan)
     int aligned8;                     // out is 8-byte aligned: one 8-byte store per pair
     int swap;                         // store (b, a): the point-polygon join emits (point, polygon)
+    unsigned point_base;              // added to every point index (pane stream positions)
 };
 
 template <bool WRITE>
@@ -608,7 +609,7 @@ __device__ __forceinline__ void pairs_flush(uint2* buf, unsigned long long& cnt,
     for (unsigned t = lane_id(); t < (unsigned)cnt; t += kWave) {
         const unsigned long long p = base + t;
         if (p < s.cap) {
-            const uint2 b = buf[t];
+            const uint2 b = make_uint2(buf[t].x, buf[t].y + s.point_base);  // (polygon, point)
             const uint2 v = s.swap ? make_uint2(b.y, b.x) : b;
             if (s.aligned8) {
                 reinterpret_cast<uint2*>(s.out)[p] = v;
@@ -1862,6 +1863,7 @@ struct StreamOut {
     unsigned* out;                  // pairs, u32 x 2 (swap: (point, polygon))
     uint64_t cap;
     int aligned8, swap;
+    unsigned point_base;            // added to every point index of a pair (pane stream positions)
     unsigned long long* totals;     // [0] pairs, [1] candidates: reservation cursors (zero before)
     uint64_t ccap;                  // candidates past it are counted only (the host regrows, re-runs)
     unsigned* cpoly;                // candidates in chunk order: polygon (the grouping reads these),
@@ -1899,6 +1901,7 @@ struct StreamSink {
 
 __device__ __forceinline__ void stream_emit_pair(const StreamOut& o, unsigned long long p, unsigned poly, unsigned idx) {
     if (p >= o.cap) return;
+    idx += o.point_base;
     const uint2 v = o.swap ? make_uint2(idx, poly) : make_uint2(poly, idx);
     if (o.aligned8) {  // streaming pair stores: nothing on the device reads them again
         __builtin_nontemporal_store(((unsigned long long)v.y << 32) | v.x, reinterpret_cast<unsigned long long*>(o.out) + p);
@@ -3965,8 +3968,8 @@ void build_stream_table(PolyCache& c, uint32_t npoly, int32_t nb, bool r_is_max)
 
 int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, int join, const double* x,
                const double* y, uint64_t n, const uint32_t* poly_rings, const uint32_t* ring_off, const double* vx,
-               const double* vy, uint32_t npoly, double r, int approximate, uint32_t* out_pairs, uint64_t cap,
-               uint64_t* out_count) {
+               const double* vy, uint64_t nv, uint32_t npoly, double r, int approximate, uint32_t* out_pairs,
+               uint64_t cap, uint64_t* out_count, uint32_t point_base) {
     if (!out_count) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null out_count");
     *out_count = 0;
     int rc = check_grid_basic(ctx, grid, join ? "point grid" : "grid");
@@ -3993,6 +3996,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     const uint32_t R0 = ring_of(poly_rings, 0), R1 = ring_of(poly_rings, npoly);
     for (uint32_t j = R0; j < R1; j++)
         if (ring_off[j + 1] < ring_off[j]) return ctx_fail(ctx, GEOHIP_ERR_ARG, "ring_off not ascending");
+    if (ring_off[R1] > nv) return ctx_fail(ctx, GEOHIP_ERR_ARG, "ring_off refers past the nv vertices of vx / vy");
     // polygon planning (host): rings (createPolygon), envelope, G / C rectangles (plan.cpp), the
     // (polygon, tile) work items of each polygon's walk region and the slab lists -- or the
     // cached plan of the same inputs
@@ -4204,6 +4208,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             so.cap = out ? cap : 0;
             so.aligned8 = ((uintptr_t)out & 7u) == 0;
             so.swap = join ? 1 : 0;
+            so.point_base = point_base;
             so.totals = reinterpret_cast<unsigned long long*>(misc);
             so.ccap = cands ? ccap : 0;
             char* cb = reinterpret_cast<char*>(cbuf);
@@ -4329,7 +4334,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             out = reinterpret_cast<unsigned*>(p);
         }
     }
-    PairSink sink{bcount, boff, 0u, out, out ? cap : 0, ((uintptr_t)out & 7u) == 0, join ? 1 : 0};
+    PairSink sink{bcount, boff, 0u, out, out ? cap : 0, ((uintptr_t)out & 7u) == 0, join ? 1 : 0, point_base};
     PairSink osink = sink;
     osink.slot0 = nwork;
     const int r_is_max = r >= 1.7976931348623157e308;
@@ -4540,8 +4545,8 @@ void knn_poly_cache_drop(geohip_ctx* ctx) {
 
 // Point-polygon kNN of one query polygon over one window (host side of the kernels above).
 int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
-                   const uint32_t* ring_off, uint32_t nring, const double* vx, const double* vy, double r, uint32_t k,
-                   int approximate, uint32_t* out_idx, double* out_dist, uint32_t* out_count, bool async) {
+                   const uint32_t* ring_off, uint32_t nring, const double* vx, const double* vy, uint64_t nv, double r,
+                   uint32_t k, int approximate, uint32_t* out_idx, double* out_dist, uint32_t* out_count, bool async) {
     if (!out_idx || !out_dist || !out_count) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null output");
     if (!async) *out_count = 0;
     if (k == 0) return ctx_fail(ctx, GEOHIP_ERR_ARG, "k must be > 0");
@@ -4555,6 +4560,7 @@ int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, co
     if (nring > kMaxRings) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "polygon with more than 65535 rings");
     for (uint32_t j = 0; j < nring; j++)
         if (ring_off[j + 1] < ring_off[j]) return ctx_fail(ctx, GEOHIP_ERR_ARG, "ring_off not ascending");
+    if (ring_off[nring] > nv) return ctx_fail(ctx, GEOHIP_ERR_ARG, "ring_off refers past the nv vertices of vx / vy");
     hipStream_t st = ctx_stream(ctx);
     const bool dev = ctx_mem(ctx) == GEOHIP_MEM_DEVICE;
     KnnPolyCache* kc = ctx_kcache(ctx);

@@ -12,13 +12,13 @@ void ppoly_cache_drop(geohip_ctx* ctx);
 // point cells on grid, pairs (point, polygon), PointPolygonJoinQuery.java:162-201)
 int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, int join, const double* x,
                const double* y, uint64_t n, const uint32_t* poly_rings, const uint32_t* ring_off, const double* vx,
-               const double* vy, uint32_t npoly, double r, int approximate, uint32_t* out_pairs, uint64_t cap,
-               uint64_t* out_count);
+               const double* vy, uint64_t nv, uint32_t npoly, double r, int approximate, uint32_t* out_pairs,
+               uint64_t cap, uint64_t* out_count, uint32_t point_base = 0);
 // point-polygon kNN of one polygon (PointPolygonKNNQuery.java:162-236); async: device outputs and
 // count, no host synchronisation
 int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
-                   const uint32_t* ring_off, uint32_t nring, const double* vx, const double* vy, double r, uint32_t k,
-                   int approximate, uint32_t* out_idx, double* out_dist, uint32_t* out_count, bool async);
+                   const uint32_t* ring_off, uint32_t nring, const double* vx, const double* vy, uint64_t nv, double r,
+                   uint32_t k, int approximate, uint32_t* out_idx, double* out_dist, uint32_t* out_count, bool async);
 void knn_poly_cache_drop(geohip_ctx* ctx);
 // point kNN with k > GEOHIP_KNN_MAX_K: candidate scan, keys, radix select, sort (device outputs)
 int knn_pp_large_impl(geohip_ctx* ctx, const PointPlan& plan, const double* dx, const double* dy, uint64_t n,

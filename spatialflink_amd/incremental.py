@@ -58,34 +58,36 @@ class IncrementalRange:
 
 class IncrementalPPolyRange:
     """Point-polygon range (many query polygons) over sliding windows with pane reuse: each pane's
-    (polygon, point) pairs are computed once; a window's pairs are the panes' pairs with the
-    point index offset by the pane's position in the window (PointPolygonRangeQuery's per-point
-    predicate, PointPolygonRangeQuery.java:104-124, makes pane results independent).  The polygon
+    (polygon, point) pairs are computed once, by geohip_range_ppoly_pane with the pane's stream
+    position as the point-index base, so the pairs carry stream positions and serve every window
+    that holds the pane unchanged -- no per-window pass over them (PointPolygonRangeQuery's
+    per-point predicate, PointPolygonRangeQuery.java:104-124, makes pane results independent).
+    A window's local point index = stream position - ``window_start`` (mod 2^32).  The polygon
     plan is cached by the context, so panes after the first skip planning and upload."""
 
     def __init__(self, ctx: _abi.Context, grid: _abi.Grid, ring_off, vx, vy, r: float, approximate: bool = False,
                  panes: int = 2, out_cap: int = 0):
         self.ctx, self.grid, self.r, self.approx = ctx, grid, r, approximate
         self.rings = (ring_off, vx, vy)
-        self.panes = deque(maxlen=panes)  # (pane size, pairs [m, 2] (polygon, point))
+        self.panes = deque(maxlen=panes)  # (first stream position, pane size, pairs [m, 2] (polygon, position))
         self.out_cap = out_cap
+        self.pos = 0  # stream position of the next pane's first point
 
     def push(self, x, y, out=None):
-        pairs = self.ctx.range_ppoly(self.grid, x, y, *self.rings, self.r, self.approx, out=out)
-        self.panes.append((len(x), pairs))
+        pairs = self.ctx.range_ppoly(self.grid, x, y, *self.rings, self.r, self.approx, out=out, point_base=self.pos)
+        self.panes.append((self.pos, len(x), pairs))
+        self.pos = (self.pos + len(x)) & 0xFFFFFFFF
         return self.window()
 
+    @property
+    def window_start(self) -> int:
+        """Stream position of the window's first point (its local index 0)."""
+        return self.panes[0][0] if self.panes else self.pos
+
     def window(self):
-        """Pairs of the window (polygon, window-local point index), pane by pane (a list: the
-        caller concatenates if it needs one array)."""
-        out, off = [], 0
-        for size, pairs in self.panes:
-            if off:
-                pairs = pairs.clone() if _abi._is_device(pairs) else pairs.copy()
-                pairs[:, 1] += off
-            out.append(pairs)
-            off += size
-        return out
+        """Pairs of the window (polygon, stream position), pane by pane (a list: the caller
+        concatenates if it needs one array)."""
+        return [pairs for _, _, pairs in self.panes]
 
 
 class IncrementalKNN:

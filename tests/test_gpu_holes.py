@@ -225,11 +225,31 @@ def test_holes_errors_and_empty(ctx):
     cnt = _abi.c_uint64(0)
     import ctypes
     rc = _abi.lib.geohip_range_ppoly(ctx.h, ctypes.byref(ag), _abi._ptr(x), _abi._ptr(y), len(x), None, None, None,
-                                     None, 0, 0.01, 0, None, 0, ctypes.byref(cnt))
+                                     None, 0, 0, 0.01, 0, None, 0, ctypes.byref(cnt))
     assert rc == _abi.OK and cnt.value == 0
     rc = _abi.lib.geohip_join_ppoly(ctx.h, ctypes.byref(ag), ctypes.byref(ag), _abi._ptr(x), _abi._ptr(y), len(x),
-                                    None, None, None, None, 0, 0.01, 0, None, 0, ctypes.byref(cnt))
+                                    None, None, None, None, 0, 0, 0.01, 0, None, 0, ctypes.byref(cnt))
     assert rc == _abi.OK and cnt.value == 0
+    # ring offsets past the vertex count nv: GEOHIP_ERR_ARG from the C side itself (no host read
+    # past the caller's arrays), for every polygon entry point
+    off = np.ascontiguousarray(off4, np.uint32)
+    vxc, vyc = np.ascontiguousarray(vx4, np.float64), np.ascontiguousarray(vy4, np.float64)
+    short = len(vxc) - 1
+    rc = _abi.lib.geohip_range_ppoly(ctx.h, ctypes.byref(ag), _abi._ptr(x), _abi._ptr(y), len(x), None, _abi._ptr(off),
+                                     _abi._ptr(vxc), _abi._ptr(vyc), short, len(off) - 1, 0.01, 0, None, 0,
+                                     ctypes.byref(cnt))
+    assert rc == _abi.ERR_ARG and b"past" in _abi.lib.geohip_last_error(ctx.h)
+    rc = _abi.lib.geohip_join_ppoly(ctx.h, ctypes.byref(ag), ctypes.byref(ag), _abi._ptr(x), _abi._ptr(y), len(x), None,
+                                    _abi._ptr(off), _abi._ptr(vxc), _abi._ptr(vyc), short, len(off) - 1, 0.01, 0, None, 0,
+                                    ctypes.byref(cnt))
+    assert rc == _abi.ERR_ARG
+    k_i = np.zeros(5, np.uint32)
+    k_d = np.zeros(5, np.float64)
+    kc = _abi.c_uint32(0)
+    rc = _abi.lib.geohip_knn_ppoly(ctx.h, ctypes.byref(ag), _abi._ptr(x), _abi._ptr(y), len(x), _abi._ptr(off),
+                                   len(off) - 1, _abi._ptr(vxc), _abi._ptr(vyc), short, 0.01, 5, 0, _abi._ptr(k_i),
+                                   _abi._ptr(k_d), ctypes.byref(kc))
+    assert rc == _abi.ERR_ARG
 
 
 def test_holes_golden(ctx, golden):

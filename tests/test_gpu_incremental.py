@@ -90,7 +90,8 @@ def test_incremental_ppoly_equals_full_window(ctx):
     inc = IncrementalPPolyRange(ctx, ag, off, vx, vy, 0.01, False, 2)
     for j, (x, y) in enumerate(panes):
         got = inc.push(torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda())
-        got = np.concatenate([g.cpu().numpy().astype(np.int64).reshape(-1, 2) for g in got])
+        got = np.concatenate([g.cpu().numpy().astype(np.int64).reshape(-1, 2) & 0xFFFFFFFF for g in got])
+        got[:, 1] = (got[:, 1] - inc.window_start) & 0xFFFFFFFF  # stream positions -> window-local
         win = panes[max(0, j - 1):j + 1]
         wx = np.concatenate([w[0] for w in win])
         wy = np.concatenate([w[1] for w in win])
