@@ -1,6 +1,6 @@
-"""Per-XCD view of the kNN pass phase trace: block b runs on XCD b % 8 (round-robin dispatch).
-Prints, per XCD, the median / max stream-end and arrival times (us from the earliest start), to
-tell XCD-level imbalance from CU-level imbalance (GPU box measurement)."""
+"""Per-XCD view of the kNN pass phase trace: each block records its XCD (HW_REG_XCC_ID, trace
+slot 15).  Prints, per XCD, the median / max stream-end and arrival times (us from the earliest
+start), to tell XCD-level imbalance from CU-level imbalance (GPU box measurement)."""
 import sys
 from pathlib import Path
 
@@ -22,7 +22,7 @@ for w in range(4):
     xs.append(x)
     ys.append(y)
 torch.cuda.synchronize()
-acc_se, acc_ar = [], []
+acc_se, acc_ar, acc_x = [], [], []
 for rep in range(8):
     for w in range(4):
         ctx.knn_pp(grid, xs[w], ys[w], q[0], q[1], R, K)
@@ -31,14 +31,20 @@ for rep in range(8):
     rel = (tr - t0) / 100.0
     acc_se.append(rel[:, 1])
     acc_ar.append(rel[:, 4])
+    acc_x.append(tr[:, 15] & 0xF)
 se = np.stack(acc_se)  # [rep, block]
 ar = np.stack(acc_ar)
 nb = se.shape[1]
 print("blocks", nb)
+xid = np.stack(acc_x)
+print("block -> XCC id consistent across reps:", bool((xid == xid[0]).all()), "| b % 8 == id (up to a rotation):",
+      len({int((xid[0, b] - b) % 8) for b in range(nb)}) == 1)
 for x in range(8):
-    b = np.arange(x, nb, 8)
-    print(f"xcd {x}: stream_end med {np.median(se[:, b]):6.2f} max {se[:, b].max(1).mean():6.2f}  "
-          f"arrived med {np.median(ar[:, b]):6.2f} max {ar[:, b].max(1).mean():6.2f}")
+    sel = xid == x
+    se_x = np.where(sel, se, np.nan)
+    ar_x = np.where(sel, ar, np.nan)
+    print(f"xcc {x}: blocks {int(sel[0].sum()):3d} stream_end med {np.nanmedian(se_x):6.2f} max "
+          f"{np.nanmax(se_x, 1).mean():6.2f}  arrived med {np.nanmedian(ar_x):6.2f} max {np.nanmax(ar_x, 1).mean():6.2f}")
 # correlation of a block's lateness across reps (a slow CU stays slow?)
 z = se - se.mean(1, keepdims=True)
 c = np.corrcoef(z)

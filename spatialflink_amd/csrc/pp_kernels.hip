@@ -1119,7 +1119,6 @@ __device__ __forceinline__ void pass_range_emit(const PassRangeIo& rio, const un
                                                 unsigned vb, uint64_t p0, uint64_t p1) {
     const int lane = lane_id(), wid = threadIdx.x / kWave;
     const unsigned nw = p1 > p0 ? (unsigned)((p1 - p0 + 63) / 64) : 0u;
-    const unsigned long long tag = rio.epoch << 40;
     if (wid == 0) {
         const unsigned long long pre = poll_block_counts<kPassMaxBlocks / kWave>(rio.status, vb, rio.epoch, rio.spin_limit,
                                                                                   rio.inject, rio.fault);
@@ -1194,6 +1193,11 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
         kb.next_it = 2 * NW;  // iterations wid and NW + wid start statically
     }
     PASS_TRACE(io, 0);
+    if (io.trace && threadIdx.x == 0) {  // measurement only: the XCD this block runs on
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        io.trace[16 * (size_t)blockIdx.x + 15] = xcc & 0xfu;
+    }
     const unsigned k = args.k;
     // Iteration order.  kNN alone: the block's iterations interleave with every other block's
     // (global iteration it * nblocks + block), so the grid sweeps the window as one front and
@@ -1201,11 +1205,19 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
     // first and the last block, measured by the phase trace).  The fused range keeps a contiguous
     // chunk per block (its hit bitmask covers the chunk).  ABL bit 4: chunks (measurement).
     constexpr bool kInterleave = !RANGE && !(ABL & 16);
+    // Front rotation (GEOHIP_KNN_ROT): block b takes slot (b + it * ROT) mod nblocks of front it, so
+    // the blocks of one XCD (b mod 8) do not always read the same 2 KB position mod 16 KB of the
+    // window (with ROT 0 they do: a fixed slice of the address bits per XCD).
+#ifndef GEOHIP_KNN_ROT
+#define GEOHIP_KNN_ROT 0
+#endif
+    constexpr unsigned kRot = GEOHIP_KNN_ROT;
     const uint64_t total_iters = (n + kPtsIter - 1) / kPtsIter;
-    const unsigned niters = kInterleave ? (unsigned)(blockIdx.x < total_iters
-                                                         ? (total_iters - blockIdx.x + gridDim.x - 1) / gridDim.x
-                                                         : 0)
-                                        : (unsigned)((blk_end - blk_begin + kPtsIter - 1) / kPtsIter);
+    const uint64_t full_fronts = total_iters / gridDim.x, rem_front = total_iters % gridDim.x;
+    const unsigned niters =
+        kInterleave ? (unsigned)(full_fronts + ((rem_front && (blockIdx.x + full_fronts * kRot) % gridDim.x < rem_front)
+                                                    ? 1u : 0u))
+                    : (unsigned)((blk_end - blk_begin + kPtsIter - 1) / kPtsIter);
     if (kInterleave) blk_end = n;
     unsigned ccnt = 0;
     unsigned appended = 0, last_hist = 0;
@@ -1284,7 +1296,8 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
     const bool all_valid[4] = {true, true, true, true};
     double ax[4], ay[4], bx[4], by[4];
     auto it_base = [&](unsigned it) {
-        return kInterleave ? ((uint64_t)it * gridDim.x + blockIdx.x) * kPtsIter : blk_begin + (uint64_t)it * kPtsIter;
+        return kInterleave ? ((uint64_t)it * gridDim.x + (blockIdx.x + (uint64_t)it * kRot) % gridDim.x) * kPtsIter
+                           : blk_begin + (uint64_t)it * kPtsIter;
     };
     auto is_full = [&](unsigned it) { return it_base(it) + kPtsIter <= blk_end; };
     auto load_full = [&](unsigned it, double (&px)[4], double (&py)[4]) {
