@@ -1843,8 +1843,9 @@ constexpr unsigned kStreamChunk = 1u << GEOHIP_PS_CHUNK_BITS;  // points per chu
 #define GEOHIP_PS_BPC 2
 #endif
 constexpr unsigned kStreamBlocksPerCU = GEOHIP_PS_BPC;  // resident blocks per CU (LDS, registers)
-constexpr unsigned kSPairCap = kStreamChunk;      // block-staged pairs per chunk (4 B each: poly << 13 | point)
-constexpr unsigned kSCandCap = kStreamChunk / 8;  // block-staged candidates per chunk
+constexpr unsigned kSPairCap = 2 * kStreamChunk;  // block-staged pairs per chunk (4 B each: poly << 12 | point),
+                                                  // kSPairCap / kStreamNW per wave
+constexpr unsigned kSCandCap = kStreamChunk / 4;  // block-staged candidates per chunk (per wave likewise)
 constexpr unsigned kLocalBits = GEOHIP_PS_CHUNK_BITS;  // point within its chunk
 constexpr uint32_t kStreamMaxPolys = 1u << (32 - kLocalBits);
 constexpr unsigned kCandItem = 1024;       // candidates per evaluation work item
@@ -1890,12 +1891,16 @@ struct StreamArgs {
 
 // one pair or candidate of the current chunk: staged in LDS (packed), or -- a chunk whose stage
 // overflowed, re-run once its bases are known -- stored straight to its global slot
+// Staged (the common case): each wave owns a region of the block's LDS stage and counts its
+// entries in a wave-uniform register -- no LDS atomic per push; the block sums the waves' counts at
+// the end of the chunk.  Direct (the overflow re-run): one LDS cursor for the block, global slots.
 struct StreamSink {
-    unsigned* pk;                   // LDS: packed pairs / candidates
-    unsigned* cursor;               // LDS counter
-    unsigned cap;
+    unsigned* pk;                   // staged: this wave's LDS region
+    unsigned* cursor;               // direct: the block's LDS counter
+    unsigned cap;                   // staged: region capacity (entries past it: overflow, counted)
     bool direct;
     unsigned long long base;        // direct: first global slot of the chunk
+    unsigned n;                     // staged: entries pushed by this wave (wave-uniform)
     unsigned acc;                   // measurement only (GEOHIP_PS_ABL 3)
 };
 
@@ -1930,16 +1935,18 @@ __device__ __forceinline__ void stream_push(const StreamArgs& a, StreamSink& k, 
     }
     const unsigned long long m = __ballot(hit);
     if (!m || GEOHIP_PS_ABL == 1) return;
+    if (!k.direct) {
+        const unsigned b = k.n + lanes_below(m);
+        if (hit && b < k.cap) k.pk[b] = (poly << kLocalBits) | loc;
+        k.n += (unsigned)__popcll(m);
+        return;
+    }
     unsigned b = 0;
     if (lane_id() == 0) b = atomicAdd(k.cursor, (unsigned)__popcll(m));  // every lane is active here
     b = (unsigned)__builtin_amdgcn_readfirstlane((int)b) + lanes_below(m);
     if (!hit) return;
-    if (k.direct) {
-        if (CAND) stream_emit_cand(a, k.base + b, poly, (unsigned)(chunk0 + loc));
-        else stream_emit_pair(a.o, k.base + b, poly, (unsigned)(chunk0 + loc));
-    } else if (b < k.cap) {
-        k.pk[b] = (poly << kLocalBits) | loc;
-    }
+    if (CAND) stream_emit_cand(a, k.base + b, poly, (unsigned)(chunk0 + loc));
+    else stream_emit_pair(a.o, k.base + b, poly, (unsigned)(chunk0 + loc));
 }
 
 // One chunk's points (all waves of the block).  Phase A: every point of the wave's iterations --
@@ -2014,6 +2021,74 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
             st[t] = s == 0 ? w : (st[t] | (w << (8 * s)));
         }
     }
+    if (!APPROX) {
+        // Phase B (exact): each lane walks the entries of its kIters * 4 points as ONE list, slot
+        // after slot (the heads queue in registers, shifted as slots are taken), so a wave step
+        // costs the lanes' largest TOTAL entry count, not the sum over the slots of each slot's
+        // largest count (every slot had some lane with a multi-entry cell: ~3.5 steps per slot).
+        constexpr unsigned kSlots = kIters * 4;
+        uint2 q[kSlots];
+#pragma unroll
+        for (unsigned j = 0; j < kSlots; j++) q[j] = hd[j >> 2][j & 3];
+        unsigned c = 0, cur = 0;  // slots taken; slot of the current entry
+        uint32_t ex = kNoEntry, word = 0;
+        unsigned e = 0, e1 = 0;
+        auto take = [&]() {  // the next slot holding an entry (a multi cell: its first entry loaded)
+            ex = kNoEntry;
+            while (c < kSlots) {
+                const uint2 h = q[0];
+#pragma unroll
+                for (unsigned j = 0; j + 1 < kSlots; j++) q[j] = q[j + 1];
+                cur = c++;
+                if (h.x == kNoEntry) continue;
+                ex = h.x;
+                word = h.y;
+                e = e1 = 0;
+                if (ex & kMulti) {
+                    e = word;
+                    e1 = e + (ex & ~kMulti);
+                    const uint2 en = a.ent[e++];
+                    ex = en.x;
+                    word = en.y;
+                }
+                return;
+            }
+        };
+        take();
+        while (__ballot(ex != kNoEntry)) {
+            bool hit = false, need = false;
+            unsigned poly = 0, loc = 0;
+            if (ex != kNoEntry) {
+                const unsigned t = cur >> 2, sl = cur & 3;
+                loc = (t * kStreamNW + (unsigned)wid) * kStreamPts + 2u * (unsigned)lane + (sl & 1u) + 128u * (sl >> 1);
+                const unsigned sw = (kIters > 1 && t ? st[kIters > 1 ? 1 : 0] : st[0]) >> (8 * sl);
+                poly = ex & ~kEntC;
+                if (!(ex & kEntC)) {
+                    hit = true;
+                } else {
+                    // a decided class holds for every point in the cell's coordinate box: not for
+                    // NaN coordinates (cell 0 by Java's (int) NaN)
+                    uint32_t k = kClsMixed;
+                    if (!(sw & kNanBit)) {
+                        if (word == kWordHit) k = kClsHit;
+                        else if (word == kWordMiss) k = kClsMiss;
+                        else k = (word >> (2 * (sw & 15u))) & 3u;
+                    }
+                    hit = k == kClsHit;
+                    need = k == kClsMixed;
+                }
+                if (e < e1) {  // the cell's next entry
+                    const uint2 en = a.ent[e++];
+                    ex = en.x;
+                    word = en.y;
+                } else {
+                    take();
+                }
+            }
+            stream_push<false>(a, ps, hit, poly, loc, c0);
+            stream_push<true>(a, cs, need, poly, loc, c0);
+        }
+    }
 #pragma unroll
     for (unsigned t = 0; t < kIters; t++) {
         double qx[4] = {0.0, 0.0, 0.0, 0.0}, qy[4] = {0.0, 0.0, 0.0, 0.0};
@@ -2021,6 +2096,7 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
         if (APPROX || (a.nopoly && any_out)) load(t, qx, qy);  // reloaded (L2): bbox test, outside points
 #pragma unroll
         for (int s = 0; s < 4; s++) {
+            if (!APPROX) break;  // exact: the worklist above walked the entries
             const unsigned loc = loc_of(t, s);
             const unsigned sw = st[t] >> (8 * s);
             const bool nan = sw & kNanBit;
@@ -2109,25 +2185,37 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
     __shared__ unsigned ppk[kSPairCap];
     __shared__ unsigned cpk[APPROX ? 1 : kSCandCap];
     __shared__ unsigned s_np, s_nc;
+    __shared__ unsigned s_wp[kStreamNW], s_wc[kStreamNW];  // per-wave staged counts
     __shared__ unsigned long long s_pb, s_cb;
+    constexpr unsigned kWPair = kSPairCap / kStreamNW, kWCand = kSCandCap / kStreamNW;
+    const int wid = threadIdx.x / kWave, lane = lane_id();
     if (KL)
         for (unsigned t = threadIdx.x; t < a.keep_words; t += kStreamNW * kWave) kl[t] = a.keep[t];
     const unsigned nchunks = (unsigned)((a.n + kStreamChunk - 1) / kStreamChunk);
     for (unsigned vb = blockIdx.x; vb < nchunks; vb += gridDim.x) {
         __syncthreads();  // the previous chunk's stage is drained (and the bitmap staged)
-        if (threadIdx.x == 0) {
-            s_np = 0;
-            s_nc = 0;
-        }
-        __syncthreads();
         const uint64_t c0 = (uint64_t)vb * kStreamChunk;
         const uint64_t c1 = c0 + kStreamChunk < a.n ? c0 + kStreamChunk : a.n;
-        StreamSink ps{ppk, &s_np, kSPairCap, false, 0, 0u};
-        StreamSink cs{cpk, &s_nc, APPROX ? 0u : kSCandCap, false, 0, 0u};
+        StreamSink ps{ppk + wid * kWPair, &s_np, kWPair, false, 0, 0u, 0u};
+        StreamSink cs{cpk + (APPROX ? 0 : wid * kWCand), &s_nc, APPROX ? 0u : kWCand, false, 0, 0u, 0u};
         stream_chunk<APPROX, KL>(a, kl, c0, c1, ps, cs);
         if (GEOHIP_PS_ABL == 3 && ps.acc + cs.acc == 0x9e3779b9u) a.o.totals[0] = 1;
+        if (lane == 0) {
+            s_wp[wid] = ps.n;
+            s_wc[wid] = cs.n;
+        }
         __syncthreads();
-        const unsigned np = s_np, nc = s_nc;
+        unsigned np = 0, nc = 0, pex = 0, cex = 0;  // totals; this wave's offsets in the chunk
+        bool over = false;
+#pragma unroll
+        for (int w = 0; w < kStreamNW; w++) {
+            const unsigned wp = s_wp[w], wc = s_wc[w];
+            over |= wp > kWPair || wc > (APPROX ? 0u : kWCand);
+            pex += w < wid ? wp : 0u;
+            cex += w < wid ? wc : 0u;
+            np += wp;
+            nc += wc;
+        }
         if (threadIdx.x == 0) {
             s_pb = np ? atomicAdd(a.o.totals, (unsigned long long)np) : 0ull;
             s_cb = nc ? atomicAdd(a.o.totals + 1, (unsigned long long)nc) : 0ull;
@@ -2135,16 +2223,19 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
         __syncthreads();
         const unsigned long long pb = s_pb, cb = s_cb;
         if (GEOHIP_PS_ABL == 4) continue;
-        if (np <= kSPairCap && nc <= cs.cap) {
-            for (unsigned t = threadIdx.x; t < np; t += kStreamNW * kWave) {
-                const unsigned v = ppk[t];
-                stream_emit_pair(a.o, pb + t, v >> kLocalBits, (unsigned)(c0 + (v & (kStreamChunk - 1))));
+        if (!over) {  // each wave stores its own region: coalesced runs of the output
+            const unsigned* wpk = ppk + wid * kWPair;
+            for (unsigned t = (unsigned)lane; t < ps.n; t += kWave) {
+                const unsigned v = wpk[t];
+                stream_emit_pair(a.o, pb + pex + t, v >> kLocalBits, (unsigned)(c0 + (v & (kStreamChunk - 1))));
             }
-            if (!APPROX)
-                for (unsigned t = threadIdx.x; t < nc; t += kStreamNW * kWave) {
-                    const unsigned v = cpk[t];
-                    stream_emit_cand(a, cb + t, v >> kLocalBits, (unsigned)(c0 + (v & (kStreamChunk - 1))));
+            if (!APPROX) {
+                const unsigned* wck = cpk + wid * kWCand;
+                for (unsigned t = (unsigned)lane; t < cs.n; t += kWave) {
+                    const unsigned v = wck[t];
+                    stream_emit_cand(a, cb + cex + t, v >> kLocalBits, (unsigned)(c0 + (v & (kStreamChunk - 1))));
                 }
+            }
         } else {  // overflow (many polygons per cell): the chunk again, straight to its slots
             __syncthreads();
             if (threadIdx.x == 0) {
@@ -2152,8 +2243,8 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
                 s_nc = 0;
             }
             __syncthreads();
-            StreamSink pd{ppk, &s_np, kSPairCap, true, pb, 0u};
-            StreamSink cd{cpk, &s_nc, cs.cap, true, cb, 0u};
+            StreamSink pd{ppk, &s_np, kSPairCap, true, pb, 0u, 0u};
+            StreamSink cd{cpk, &s_nc, kSCandCap, true, cb, 0u, 0u};
             stream_chunk<APPROX, KL>(a, kl, c0, c1, pd, cd);
         }
     }

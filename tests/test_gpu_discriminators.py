@@ -35,12 +35,14 @@ def test_q1_point_point_distances_and_knn(ctx):
     x = np.array([f(c["p"][0]) for c in P["cases"]])
     y = np.array([f(c["p"][1]) for c in P["cases"]])
     kn = FIX["Q1"]["knn"]
-    g = _grid(kn["grid"])
-    idx, dist = ctx.knn_pp(g, _dev(x), _dev(y), q[0], q[1], 0.5, len(x))  # every point: its distance
+    # a grid around every pair point (the Beijing grid clips the query's cells at its south edge)
+    gp = _abi.make_grid(115.0, 39.0, 0.03, 100)
+    idx, dist = ctx.knn_pp(gp, _dev(x), _dev(y), q[0], q[1], 0.5, len(x))  # every point: its distance
     got = {int(i): float(d).hex() for i, d in zip(idx.cpu().numpy(), dist.cpu().numpy())}
     assert len(got) == len(x)
     for j, c in enumerate(P["cases"]):
         assert got[j] == c["A"] != c["B"]
+    g = _grid(kn["grid"])
     xw = np.array([f(v) for v in kn["x"]])
     yw = np.array([f(v) for v in kn["y"]])
     qq = [f(v) for v in kn["query"]]
