@@ -1228,6 +1228,12 @@ int ctx_ensure(geohip_ctx* ctx, int slot, size_t bytes, void** out) {
     if (!rc) *out = ctx->buf[S_J0 + slot];
     return rc;
 }
+int ctx_ensure_zeroed(geohip_ctx* ctx, int slot, size_t bytes, void** out) {
+    if (slot < 0 || S_J0 + slot > S_J25) return fail(ctx, GEOHIP_ERR_DEVICE, "internal: scratch slot out of range");
+    int rc = ensure_zeroed(ctx, (Slot)(S_J0 + slot), bytes);
+    if (!rc) *out = ctx->buf[S_J0 + slot];
+    return rc;
+}
 int ctx_ensure_ingest(geohip_ctx* ctx, int slot, size_t bytes, void** out) {
     if (slot < 0 || S_I0 + slot >= S_COUNT) return fail(ctx, GEOHIP_ERR_DEVICE, "internal: scratch slot out of range");
     int rc = ensure(ctx, (Slot)(S_I0 + slot), bytes);

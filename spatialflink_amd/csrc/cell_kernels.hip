@@ -39,7 +39,6 @@ namespace geohip {
 constexpr int kTB = 256;             // threads per block (probe kernels, scans)
 constexpr int kBinThreads = 1024;    // binning kernels
 constexpr unsigned kMaxTiles = 16384;
-constexpr int kWavePairs = 1024;     // per-wave LDS pair buffer (8 KB)
 constexpr unsigned kGlobalTiles = 4096;  // queries touching more tiles go to every tile's list
 
 __device__ __forceinline__ int32_t d_java_d2i(double v) {
@@ -762,6 +761,7 @@ template <bool FILL>
 __global__ __launch_bounds__(kTB) void jq_build(const QRect* __restrict__ rect, uint64_t nq, TileGeom g,
                                                 unsigned* __restrict__ tcnt, const unsigned* __restrict__ qstart,
                                                 unsigned* __restrict__ qlist) {
+    // FILL: tcnt = the per-tile cursors (zeroed like the counts, a separate array)
     const uint64_t q = (uint64_t)blockIdx.x * (kTB / kWave) + threadIdx.x / kWave;
     if (q >= nq) return;  // wave-uniform
     const unsigned lane = (unsigned)lane_id();
@@ -782,6 +782,382 @@ __global__ void jq_global(uint64_t nq, unsigned* __restrict__ glist, unsigned* _
     const uint64_t i = (uint64_t)blockIdx.x * kTB + threadIdx.x;
     if (i < nq) glist[i] = (unsigned)i;
     if (i == 0) *gcnt = (unsigned)nq;
+}
+
+// ---- join binning: 16-B point records in two data passes, no count pass ------------------
+// The join reads, per point, only what its decisions use: the fp32 coordinates relative to the
+// tile origin (the fp32 screen's operands, computed once here exactly as the screen defines
+// them), the window index, and the cell inside the tile; the fp64 coordinates are gathered from
+// the window by index for the rare exact decisions.  Record = uint4 {fl32(x - ox), fl32(y - oy),
+// idx, lcx | lcy << 10 | (tile & 127) << 20} (ts <= 782 < 1024: grids of <= 99999 cells).
+//   jb_bands  (one block per CU, its contiguous chunk of the window): each sub-chunk of kJbSub
+//             points is sorted by band (128 consecutive tiles) in LDS and written back in place
+//             (the same positions: one contiguous 64-KB store per sub-chunk); the sub-chunk's band
+//             offsets go to soff; a block-wide LDS tile histogram is added to the tile counts once.
+//   jb_scan   tile counts -> tile starts and per-tile cursors (one block); re-zeroes the counts.
+//   jb_tiles  one block per (band, group of kJbGroup level-1 blocks): the band's segments of
+//             those blocks' sub-chunks, sorted by tile in LDS; each tile's run reserved with one
+//             global atomic on its cursor, written contiguously.
+// 16 + 16 B per point for level 1, 16 + 16 for level 2 (the SoA form moved 16 + 24 and 24 + 24,
+// after two count passes).  The order of a tile's points depends on the cursor atomics -- the
+// join's decisions are per point, and its pair order was never fixed.
+constexpr unsigned kJbSub = 4096;     // points per local sort round (4 per thread)
+constexpr unsigned kJbBlocks = 256;   // level-1 blocks
+constexpr unsigned kJbL2Threads = 512;  // level 2: rounds of kJbRound records, 4 blocks per CU
+constexpr unsigned kJbRound = 2048;
+constexpr unsigned kJbL2Blocks = 1024;
+
+struct JBin {
+    const double* x;
+    const double* y;
+    uint64_t n, chunk;  // points; points per level-1 block
+    TileGeom g;
+    unsigned nbands, nsub, nblk;
+    uint4* l1;          // level-1 records (block chunks, band-sorted per sub-chunk)
+    unsigned* soff;     // [(block * nsub + sub) * (nbands + 1) + band] band starts inside the sub-chunk
+    unsigned* tcnt;     // [ntiles] tile counts (zero on entry; jb_scan re-zeroes)
+    unsigned* tstart;   // [ntiles + 1]
+    unsigned* tcur;     // [ntiles] level-2 cursors
+    unsigned* spre;     // [nbands][nblk * nsub + 1] record prefix of each band's non-empty segments
+    unsigned* sst;      // [nbands][nblk * nsub] their positions in l1
+    unsigned* nne;      // [nbands] non-empty segments
+    uint4* rinfo;       // level-2 rounds: (band, first segment, first record, end record)
+    unsigned* nround;   // [1]
+    uint4* recs;        // tile-sorted records
+};
+
+__device__ __forceinline__ uint4 jb_record(const TileGeom& g, double x, double y, unsigned idx, bool& in, unsigned& tile) {
+    int32_t cx, cy;
+    in = point_cell(g, x, y, cx, cy);
+    tile = 0;
+    if (!in) return make_uint4(0u, 0u, 0u, 0u);
+    const unsigned tx = g.dts.div((unsigned)cx), ty = g.dts.div((unsigned)cy);
+    tile = tx * (unsigned)g.nt + ty;
+    const int32_t X0 = (int32_t)tx * g.ts, Y0 = (int32_t)ty * g.ts;
+    // the tile origin exactly as join_fused forms it
+    const double ox = g.mnx + (double)X0 * g.l, oy = g.mny + (double)Y0 * g.l;
+    const float ax = (float)(x - ox), ay = (float)(y - oy);
+    const unsigned meta = (unsigned)(cx - X0) | ((unsigned)(cy - Y0) << 10) | ((tile & (kBandTiles - 1)) << 20);
+    return make_uint4(__float_as_uint(ax), __float_as_uint(ay), idx, meta);
+}
+
+// exclusive scan of lh[0..nbins) (nbins <= 192) into ls by wave 0
+__device__ __forceinline__ void lds_bins_scan(const unsigned* lh, unsigned* ls, unsigned nbins) {
+    if (threadIdx.x < kWave) {
+        const unsigned l = threadIdx.x;
+        const unsigned v0 = l < nbins ? lh[l] : 0u, v1 = kWave + l < nbins ? lh[kWave + l] : 0u;
+        const unsigned v2 = 2 * kWave + l < nbins ? lh[2 * kWave + l] : 0u;
+        const unsigned i0 = wave_incl_scan(v0);
+        const unsigned t0 = (unsigned)__builtin_amdgcn_readlane((int)i0, kWave - 1);
+        const unsigned i1 = wave_incl_scan(v1) + t0;
+        const unsigned t1 = (unsigned)__builtin_amdgcn_readlane((int)i1, kWave - 1);
+        const unsigned i2 = wave_incl_scan(v2) + t1;
+        if (l < nbins) ls[l] = i0 - v0;
+        if (kWave + l < nbins) ls[kWave + l] = i1 - v1;
+        if (2 * kWave + l < nbins) ls[2 * kWave + l] = i2 - v2;
+        if (l == kWave - 1) ls[nbins] = i2;
+    }
+}
+
+__global__ __launch_bounds__(kBinThreads) void jb_bands(JBin a) {
+    constexpr int PPT = kJbSub / kBinThreads;
+    __shared__ uint4 st[kJbSub];
+    __shared__ unsigned th[kMaxTiles];
+    __shared__ unsigned lh[kLocalBins], ls[kLocalBins + 1];
+    const uint64_t b0 = (uint64_t)blockIdx.x * a.chunk;
+    const uint64_t b1 = b0 + a.chunk < a.n ? b0 + a.chunk : a.n;
+    const unsigned nbins = a.nbands + 1;  // + out of the key space (dropped)
+    for (unsigned t = threadIdx.x; t < a.g.ntiles; t += kBinThreads) th[t] = 0;
+    for (unsigned t = threadIdx.x; t < kLocalBins; t += kBinThreads) lh[t] = 0;
+    __syncthreads();
+    // the next sub-chunk's coordinates are loaded while this one is sorted (lds_barrier: LDS only)
+    double nx[PPT], ny[PPT];
+    auto fetch = [&](uint64_t sb) {
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            const uint64_t i = sb + threadIdx.x + (uint64_t)k * kBinThreads;
+            if (i < b1) {
+                nx[k] = a.x[i];
+                ny[k] = a.y[i];
+            }
+        }
+    };
+    if (b0 < b1) fetch(b0);
+    for (unsigned s = 0; s < a.nsub; s++) {
+        const uint64_t sb = b0 + (uint64_t)s * kJbSub;
+        const unsigned m = sb < b1 ? (b1 - sb < (uint64_t)kJbSub ? (unsigned)(b1 - sb) : kJbSub) : 0u;
+        uint4 rec[PPT];
+        unsigned bin[PPT], rk[PPT];
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            const unsigned j = threadIdx.x + k * kBinThreads;
+            bin[k] = a.nbands;
+            if (j < m) {
+                bool in;
+                unsigned tile;
+                rec[k] = jb_record(a.g, nx[k], ny[k], (unsigned)(sb + j), in, tile);
+                if (in) {
+                    bin[k] = tile >> kBandBits;
+                    atomicAdd(&th[tile], 1u);
+                }
+                rk[k] = atomicAdd(&lh[bin[k]], 1u);
+            }
+        }
+        if (sb + kJbSub < b1) fetch(sb + kJbSub);
+        lds_barrier();
+        lds_bins_scan(lh, ls, nbins);
+        lds_barrier();
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            const unsigned j = threadIdx.x + k * kBinThreads;
+            if (j < m && bin[k] < a.nbands) st[ls[bin[k]] + rk[k]] = rec[k];
+        }
+        if (threadIdx.x < nbins) a.soff[((size_t)blockIdx.x * a.nsub + s) * nbins + threadIdx.x] = ls[threadIdx.x];
+        lds_barrier();
+        const unsigned kept = ls[a.nbands];
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            const unsigned j = threadIdx.x + k * kBinThreads;
+            if (j < kept) a.l1[sb + j] = st[j];
+        }
+        lds_barrier();
+        for (unsigned t = threadIdx.x; t < nbins; t += kBinThreads) lh[t] = 0;
+        lds_barrier();
+    }
+    __syncthreads();
+    for (unsigned t = threadIdx.x; t < a.g.ntiles; t += kBinThreads) {
+        const unsigned c = th[t];
+        if (c) atomicAdd(&a.tcnt[t], c);
+    }
+}
+
+// Exclusive scan of n <= kMaxTiles words by one block of kBinThreads: every value loaded up front
+// (one global round trip: a pass-by-pass scan waited for one per pass, ~1 us each), then 16
+// coalesced passes scanned together -- wave scans, one 256-entry scan of the (pass, wave) sums.
+// store(i, v, exclusive prefix) per element; returns the total.  wsum: 256 words of LDS.
+constexpr unsigned kScanPasses = kMaxTiles / kBinThreads;
+template <typename L, typename S>
+__device__ __forceinline__ unsigned block_scan_passes(unsigned n, unsigned* wsum, L&& load, S&& store) {
+    constexpr unsigned kW = kBinThreads / kWave;  // 16 waves
+    const unsigned wid = threadIdx.x / kWave, lane = (unsigned)lane_id();
+    unsigned v[kScanPasses], incl[kScanPasses];
+#pragma unroll
+    for (unsigned p = 0; p < kScanPasses; p++) {
+        const unsigned t = p * kBinThreads + threadIdx.x;
+        v[p] = t < n ? load(t) : 0u;
+    }
+#pragma unroll
+    for (unsigned p = 0; p < kScanPasses; p++) {
+        incl[p] = wave_incl_scan(v[p]);
+        if (lane == kWave - 1) wsum[p * kW + wid] = incl[p];
+    }
+    __syncthreads();
+    // (pass, wave) sums in pass-major order: exclusive scan over 256 entries by 4 waves
+    unsigned x = 0, xi = 0;
+    if (threadIdx.x < kScanPasses * kW) {
+        x = wsum[threadIdx.x];
+        xi = wave_incl_scan(x);
+    }
+    __syncthreads();
+    __shared__ unsigned wtot[kScanPasses * kW / kWave];
+    if (threadIdx.x < kScanPasses * kW && lane == kWave - 1) wtot[wid] = xi;
+    __syncthreads();
+    if (threadIdx.x < kScanPasses * kW) {
+        unsigned b = 0;
+        for (unsigned w = 0; w < wid; w++) b += wtot[w];
+        wsum[threadIdx.x] = b + xi - x;
+    }
+    __syncthreads();
+    unsigned total = 0;
+    for (unsigned w = 0; w < kScanPasses * kW / kWave; w++) total += wtot[w];
+#pragma unroll
+    for (unsigned p = 0; p < kScanPasses; p++) {
+        const unsigned t = p * kBinThreads + threadIdx.x;
+        if (t < n) store(t, v[p], wsum[p * kW + wid] + incl[p] - v[p]);
+    }
+    return total;
+}
+
+// Tile starts and cursors from the tile counts (one block; re-zeroes the counts for the next
+// launch).  Also zeroes the join's per-call counters (the query list counts and cursors, the
+// error / ticket words, the pair total): one launch instead of five memsets.
+__global__ __launch_bounds__(kBinThreads) void jb_scan(JBin a, unsigned* __restrict__ zero, unsigned nzero) {
+    __shared__ unsigned wsum[kScanPasses * (kBinThreads / kWave)];
+    for (unsigned t = threadIdx.x; t < nzero; t += kBinThreads) zero[t] = 0u;
+    const unsigned total = block_scan_passes(
+        a.g.ntiles, wsum, [&](unsigned t) { return a.tcnt[t]; },
+        [&](unsigned t, unsigned, unsigned ex) {
+            a.tstart[t] = ex;
+            a.tcur[t] = ex;
+            a.tcnt[t] = 0u;
+        });
+    if (threadIdx.x == 0) a.tstart[a.g.ntiles] = total;
+}
+
+// Level-2 rounds: each band's records, in (level-1 block, sub-chunk) order, cut into rounds of
+// kJbSub; per band the non-empty segments (a sub-chunk's run of the band) with their record
+// prefix and window position.  One block per band: its round base from the band totals (the
+// tile starts), its segments scanned and compacted, a descriptor per round
+// (band, first segment, first record, end record).
+__global__ __launch_bounds__(kBinThreads) void jb_segs(JBin a) {
+    __shared__ unsigned wsum[2][kBinThreads / kWave];
+    __shared__ unsigned sh_rbase;
+    const unsigned b = blockIdx.x, nbins = a.nbands + 1, nseg = a.nblk * a.nsub;
+    const int wid = threadIdx.x / kWave, lane = lane_id();
+    auto band_total = [&](unsigned t) {
+        const unsigned e = (t + 1) * kBandTiles < a.g.ntiles ? (t + 1) * kBandTiles : a.g.ntiles;
+        return a.tstart[e] - a.tstart[t * kBandTiles];
+    };
+    // round base: the rounds of bands < b (b <= 128 bands: one per thread of the first waves)
+    if (threadIdx.x == 0) sh_rbase = 0;
+    __syncthreads();
+    if (threadIdx.x < b) {
+        const unsigned rb = (band_total(threadIdx.x) + kJbRound - 1) / kJbRound;
+        if (rb) atomicAdd(&sh_rbase, rb);
+    }
+    __syncthreads();
+    const unsigned rbase = sh_rbase, T = band_total(b);
+    if (b == a.nbands - 1 && threadIdx.x == 0) a.nround[0] = rbase + (T + kJbRound - 1) / kJbRound;
+    unsigned* spre = a.spre + (size_t)b * (nseg + 1);
+    unsigned* sst = a.sst + (size_t)b * nseg;
+    unsigned carry_len = 0, carry_ne = 0;
+    constexpr unsigned kG = 4;  // passes whose segment rows are loaded together (one round trip)
+    for (unsigned g0 = 0; g0 < nseg; g0 += kG * kBinThreads) {
+        unsigned len[kG], gst[kG];
+#pragma unroll
+        for (unsigned u = 0; u < kG; u++) {
+            const unsigned sg = g0 + u * kBinThreads + threadIdx.x;
+            len[u] = 0;
+            gst[u] = 0;
+            if (sg < nseg) {
+                const unsigned blk = sg / a.nsub, sub = sg - blk * a.nsub;
+                const unsigned* row = a.soff + (size_t)sg * nbins;
+                const unsigned lo = row[b], hi = row[b + 1];
+                len[u] = hi - lo;
+                gst[u] = (unsigned)((uint64_t)blk * a.chunk + (uint64_t)sub * kJbSub) + lo;
+            }
+        }
+#pragma unroll
+        for (unsigned u = 0; u < kG; u++) {
+            if (g0 + u * kBinThreads >= nseg) break;  // block-uniform
+            const unsigned ne = len[u] ? 1u : 0u;
+            const unsigned il = wave_incl_scan(len[u]), in = wave_incl_scan(ne);
+            if (lane == kWave - 1) {
+                wsum[0][wid] = il;
+                wsum[1][wid] = in;
+            }
+            __syncthreads();
+            unsigned bl = carry_len, bn = carry_ne, tl = 0, tn = 0;
+            for (int w = 0; w < kBinThreads / kWave; w++) {
+                if (w < wid) {
+                    bl += wsum[0][w];
+                    bn += wsum[1][w];
+                }
+                tl += wsum[0][w];
+                tn += wsum[1][w];
+            }
+            if (ne) {
+                const unsigned pre = bl + il - len[u], idx = bn + in - ne;
+                spre[idx] = pre;
+                sst[idx] = gst[u];
+                // the rounds whose first record lies in this segment
+                for (unsigned k = (pre + kJbRound - 1) / kJbRound; (uint64_t)k * kJbRound < (uint64_t)pre + len[u]; k++) {
+                    const unsigned v0 = k * kJbRound;
+                    a.rinfo[rbase + k] = make_uint4(b, idx, v0, T - v0 < kJbRound ? T : v0 + kJbRound);
+                }
+            }
+            carry_len += tl;
+            carry_ne += tn;
+            __syncthreads();
+        }
+    }
+    if (threadIdx.x == 0) {
+        spre[carry_ne] = carry_len;  // = T: the end of the last segment
+        a.nne[b] = carry_ne;
+    }
+}
+
+// Level 2: persistent blocks over the rounds (static stride: every round holds <= kJbRound records).
+// A round's segments come into LDS in windows of kJbSegBatch; each record finds its segment by a
+// wave-uniform binary search and a per-lane forward step; the round is sorted by tile in LDS and
+// each tile's run reserved with one atomic on its cursor.
+__global__ __launch_bounds__(kJbL2Threads) void jb_tiles(JBin a) {
+    constexpr int PPT = kJbRound / kJbL2Threads;
+    constexpr unsigned kWin = kJbL2Threads;  // segments per window
+    __shared__ uint4 st[kJbRound];
+    __shared__ unsigned wst[kWin], wpre[kWin + 1];
+    __shared__ unsigned lh[kBandTiles], ls[kBandTiles + 1], base[kBandTiles];
+    const unsigned nseg = a.nblk * a.nsub;
+    const unsigned nround = a.nround[0];
+    const int wid = threadIdx.x / kWave;
+    for (unsigned t = threadIdx.x; t < kBandTiles; t += kJbL2Threads) lh[t] = 0;
+    for (unsigned r = blockIdx.x; r < nround; r += gridDim.x) {
+        const uint4 info = a.rinfo[r];
+        const unsigned b = info.x, v0 = info.z, v1 = info.w;
+        const unsigned nne = a.nne[b];
+        const unsigned* spre = a.spre + (size_t)b * (nseg + 1);
+        const unsigned* sst = a.sst + (size_t)b * nseg;
+        uint4 rec[PPT];
+        unsigned bin[PPT], rk[PPT];
+        unsigned wb = info.y;  // the window's first segment
+        for (;;) {
+            const unsigned wl = nne - wb < kWin ? nne - wb : kWin;
+            __syncthreads();  // the previous window is no longer read
+            if (threadIdx.x < wl) {
+                wst[threadIdx.x] = sst[wb + threadIdx.x];
+                wpre[threadIdx.x] = spre[wb + threadIdx.x];
+            }
+            if (threadIdx.x == 0) wpre[wl] = spre[wb + wl];
+            __syncthreads();
+            const unsigned wlo = wpre[0], whi = wpre[wl];
+#pragma unroll
+            for (int k = 0; k < PPT; k++) {
+                const unsigned v = v0 + threadIdx.x + k * kJbL2Threads;
+                const unsigned vw = v0 + (unsigned)(wid * kWave) + k * kJbL2Threads;  // the wave's first
+                if (vw + kWave > wlo && vw < whi && vw < v1) {  // wave-uniform: some lane in this window
+                    const unsigned key = vw > wlo ? vw : wlo;
+                    unsigned lo = 0, hi = wl;  // largest j with wpre[j] <= key
+                    while (hi - lo > 1) {
+                        const unsigned mid = (lo + hi) >> 1;
+                        if (wpre[mid] <= key) lo = mid;
+                        else hi = mid;
+                    }
+                    if (v >= wlo && v < whi && v < v1) {
+                        unsigned j = lo;
+                        while (wpre[j + 1] <= v) j++;
+                        rec[k] = a.l1[wst[j] + (v - wpre[j])];
+                        bin[k] = (rec[k].w >> 20) & (kBandTiles - 1);
+                        rk[k] = atomicAdd(&lh[bin[k]], 1u);
+                    }
+                }
+            }
+            if (whi >= v1 || wb + wl >= nne) break;
+            wb += wl;
+        }
+        __syncthreads();
+        lds_bins_scan(lh, ls, kBandTiles);
+        if (threadIdx.x < kBandTiles && lh[threadIdx.x])
+            base[threadIdx.x] = atomicAdd(&a.tcur[b * kBandTiles + threadIdx.x], lh[threadIdx.x]);
+        __syncthreads();
+        const unsigned m = v1 - v0;
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            const unsigned j = threadIdx.x + k * kJbL2Threads;
+            if (j < m) st[ls[bin[k]] + rk[k]] = rec[k];
+        }
+        lds_barrier();
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            const unsigned j = threadIdx.x + k * kJbL2Threads;
+            if (j < m) {
+                const uint4 q = st[j];
+                const unsigned bq = (q.w >> 20) & (kBandTiles - 1);
+                a.recs[base[bq] + (j - ls[bq])] = q;
+            }
+        }
+        lds_barrier();
+        for (unsigned t = threadIdx.x; t < kBandTiles; t += kJbL2Threads) lh[t] = 0;
+    }
 }
 
 // ---- single-pass join: balanced work items, decoupled look-back, staged pair runs ---------
@@ -807,20 +1183,39 @@ __global__ void jq_global(uint64_t nq, unsigned* __restrict__ glist, unsigned* _
 // |dx' - dx| <= e = 2.05 u A, so |d2' - d2| <= 4 e A + 2 e^2 + 3 u d2'.  d2' below lo (above hi)
 // puts the true d2 below r2lo (above r2hi), where the fp64 screens already decide (kSqLo/kSqHi).
 constexpr unsigned kJP = 1024;      // points per item (4 waves x 4 chunks of 64)
-constexpr unsigned kJQ = 256;       // queries per item
-constexpr unsigned kJStage = 512;   // per-wave pair stage (4 KB)
-constexpr unsigned kJBlocks = 1280; // persistent grid (5 blocks per CU)
+constexpr unsigned kJQ = 128;       // queries per item
+constexpr unsigned kJCh = kJP / kWave / (kTB / kWave);  // chunks per wave and item
+constexpr unsigned kJBlocksW = 1024;  // persistent grid, write pass (37 KB LDS: 4 blocks per CU)
+constexpr unsigned kJBlocksC = 1280;  // count pass (4 KB LDS, 83 VGPRs: 5 blocks per CU)
 
-// work items per tile
-__global__ void join_items(const unsigned* __restrict__ tstart, const unsigned* __restrict__ qstart,
-                           const unsigned* __restrict__ gcnt, uint32_t ntiles, unsigned* __restrict__ icnt) {
-    const unsigned t = blockIdx.x * kTB + threadIdx.x;
-    if (t >= ntiles) return;
-    const unsigned np = tstart[t + 1] - tstart[t];
-    const unsigned nq = qstart[t + 1] - qstart[t] + *gcnt;
-    icnt[t] = (np == 0 || nq == 0) ? 0u : ((np + kJP - 1) / kJP) * ((nq + kJQ - 1) / kJQ);
+// query list starts per tile (one block)
+__global__ __launch_bounds__(kBinThreads) void jq_starts(const unsigned* __restrict__ qcnt, uint32_t ntiles,
+                                                          unsigned* __restrict__ qstart) {
+    __shared__ unsigned wsum[kScanPasses * (kBinThreads / kWave)];
+    const unsigned total = block_scan_passes(
+        ntiles, wsum, [&](unsigned t) { return qcnt[t]; }, [&](unsigned t, unsigned, unsigned ex) { qstart[t] = ex; });
+    if (threadIdx.x == 0) qstart[ntiles] = total;
 }
-// item descriptors (tile, index inside the tile)
+
+// Work items (one block): per tile ceil(points / kJP) * ceil(queries / kJQ) and their starts
+__global__ __launch_bounds__(kBinThreads) void join_plan(const unsigned* __restrict__ tstart,
+                                                          const unsigned* __restrict__ qstart,
+                                                          const unsigned* __restrict__ gcnt, uint32_t ntiles,
+                                                          unsigned* __restrict__ istart) {
+    __shared__ unsigned wsum[kScanPasses * (kBinThreads / kWave)];
+    const unsigned gq = *gcnt;
+    const unsigned total = block_scan_passes(
+        ntiles, wsum,
+        [&](unsigned t) {
+            const unsigned np = tstart[t + 1] - tstart[t];
+            const unsigned nq = qstart[t + 1] - qstart[t] + gq;
+            return (np == 0 || nq == 0) ? 0u : ((np + kJP - 1) / kJP) * ((nq + kJQ - 1) / kJQ);
+        },
+        [&](unsigned t, unsigned, unsigned ex) { istart[t] = ex; });
+    if (threadIdx.x == 0) istart[ntiles] = total;
+}
+
+// item descriptors (tile, index inside the tile), one thread per tile
 __global__ void join_item_fill(const unsigned* __restrict__ istart, uint32_t ntiles, uint2* __restrict__ items) {
     const unsigned t = blockIdx.x * kTB + threadIdx.x;
     if (t >= ntiles) return;
@@ -829,7 +1224,10 @@ __global__ void join_item_fill(const unsigned* __restrict__ istart, uint32_t nti
 }
 
 struct JoinRun {
-    TileBins tb;
+    const uint4* recs;       // tile-sorted point records (jb_tiles)
+    const unsigned* tstart;  // [ntiles + 1]
+    const double* px;        // the window (fp64 coordinates of the exact decisions, by index)
+    const double* py;
     TileGeom geo;
     const unsigned* qstart;
     const unsigned* qlist;
@@ -851,24 +1249,84 @@ struct JoinRun {
 
 typedef float jf2 __attribute__((ext_vector_type(2)));
 
+// a jb_record: tile-relative fp32 coordinates, window index, cell (tile origin X0, Y0 + local)
+__device__ __forceinline__ void jrec_load(const uint4 r, int32_t X0, int32_t Y0, float& ax, float& ay, unsigned& pid,
+                                          int32_t& cx, int32_t& cy) {
+    ax = __uint_as_float(r.x);
+    ay = __uint_as_float(r.y);
+    pid = r.z;
+    cx = X0 + (int32_t)(r.w & 1023u);
+    cy = Y0 + (int32_t)((r.w >> 10) & 1023u);
+}
+
 struct JPart {  // a PART query: block as (x0, x1 - x0, y0, y1 - y0), tile-relative fp32 coordinates
     int32_t x0, wx, y0, wy;
 };
 
-template <bool WRITE>
+// pair (point, query) at output position p (< cap)
+__device__ __forceinline__ void jpair_store(const JoinRun& a, unsigned long long p, unsigned pid, unsigned q) {
+#ifndef JX_NOSTORE
+    if (a.aligned8) {  // streaming pair stores: nontemporal (no reuse on this device)
+        __builtin_nontemporal_store(((unsigned long long)q << 32) | pid, reinterpret_cast<unsigned long long*>(a.out) + p);
+    } else {
+        a.out[2 * p] = pid;
+        a.out[2 * p + 1] = q;
+    }
+#endif
+}
+
+
+// hit ballots of one point chunk against PART queries j .. j + 3 (padded past the count): the
+// four blocks and screen operands read together, one wave-uniform branch for the rare band
+template <bool APPROX>
+__device__ __forceinline__ void jpart_quad(const JoinRun& a, const JPart* __restrict__ pr, const jf2* __restrict__ pb,
+                                           const unsigned* __restrict__ pq, unsigned j, int32_t cx, int32_t cy,
+                                           float ax, float ay, unsigned pid, float lo, float hi,
+                                           unsigned long long (&m)[4]) {
+    // branch-free: every block is read whatever the lane (invalid lanes carry cx = -1 and fail)
+    const unsigned ux = (unsigned)cx, uy = (unsigned)cy;
+    bool h[4], band[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const JPart R = pr[j + u];
+        const bool in = (ux - (unsigned)R.x0 <= (unsigned)R.wx) & (uy - (unsigned)R.y0 <= (unsigned)R.wy);
+        if (APPROX) {
+            h[u] = in;
+            band[u] = false;
+        } else {
+            const jf2 b = pb[j + u];
+            const float dx = ax - b.x, dy = ay - b.y;
+            const float d2 = dx * dx + dy * dy;
+            h[u] = in && d2 < lo;
+            band[u] = in && !(d2 < lo) && !(d2 > hi);
+        }
+    }
+    if (!APPROX && __ballot(band[0] || band[1] || band[2] || band[3])) {  // rare: fp64 screens, then JTS
+        const double px = a.px[pid], py = a.py[pid];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (band[u]) {
+                const unsigned q = pq[j + u];
+                const double ox = a.qx[q], oy = a.qy[q];
+                const double ex = px - ox, ey = py - oy, e2 = ex * ex + ey * ey;
+                h[u] = e2 <= a.r2lo || (!(e2 > a.r2hi) && jts_pp_distance(px, py, ox, oy) <= a.r);
+            }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) m[u] = __ballot(h[u]);
+}
+
+// A wave's pair stage: pairs leave in contiguous runs of full 512-B wave stores.  (One store per
+// (chunk, query) straight from the ballots -- no stage -- measured slower: 1.13 ms against 1.04 ms
+// for C3's write pass; the partial-wave stores are ~3x as many instructions for the same bytes.)
+constexpr unsigned kJStage = 512;   // pairs per wave (4 KB)
 __device__ __forceinline__ void jstage_flush(const JoinRun& a, uint2* st, unsigned& cnt, unsigned long long& pos) {
     wave_lds_sync();
     for (unsigned t = (unsigned)lane_id(); t < cnt; t += kWave) {
         const unsigned long long p = pos + t;
         if (p < a.cap) {
-            if (a.aligned8) {  // streaming pair stores: nontemporal (no reuse on this device)
-                const uint2 v = st[t];
-                __builtin_nontemporal_store(((unsigned long long)v.y << 32) | v.x,
-                                            reinterpret_cast<unsigned long long*>(a.out) + p);
-            } else {
-                a.out[2 * p] = st[t].x;
-                a.out[2 * p + 1] = st[t].y;
-            }
+            const uint2 v = st[t];
+            jpair_store(a, p, v.x, v.y);
         }
     }
     wave_lds_sync();
@@ -876,59 +1334,72 @@ __device__ __forceinline__ void jstage_flush(const JoinRun& a, uint2* st, unsign
     cnt = 0;
 }
 
-// hit ballots of one point chunk against PART queries j, j + 1 (j + 1 < n or padded)
-template <bool APPROX>
-__device__ __forceinline__ void jpart_pair(const JoinRun& a, const JPart* __restrict__ pr, const jf2* __restrict__ pb,
-                                           const unsigned* __restrict__ pq, unsigned j, int32_t cx, int32_t cy,
-                                           float ax, float ay, double px, double py, bool valid, float lo, float hi,
-                                           unsigned long long& m0, unsigned long long& m1) {
-    const JPart R0 = pr[j], R1 = pr[j + 1];
-    // branch-free: both blocks are read whatever the lane (invalid lanes carry cx = -1 and fail)
-    const unsigned ux = (unsigned)cx, uy = (unsigned)cy;
-    const bool in0 = (ux - (unsigned)R0.x0 <= (unsigned)R0.wx) & (uy - (unsigned)R0.y0 <= (unsigned)R0.wy);
-    const bool in1 = (ux - (unsigned)R1.x0 <= (unsigned)R1.wx) & (uy - (unsigned)R1.y0 <= (unsigned)R1.wy);
-    if (APPROX) {
-        m0 = __ballot(in0);
-        m1 = __ballot(in1);
-        return;
-    }
-    const jf2 b0 = pb[j], b1 = pb[j + 1];
-    const jf2 dx = jf2{ax, ax} - jf2{b0.x, b1.x};
-    const jf2 dy = jf2{ay, ay} - jf2{b0.y, b1.y};
-    const jf2 d2 = dx * dx + dy * dy;
-    bool h0 = in0 && d2.x < lo, h1 = in1 && d2.y < lo;
-    const bool band0 = in0 && !(d2.x < lo) && !(d2.x > hi);
-    const bool band1 = in1 && !(d2.y < lo) && !(d2.y > hi);
-    if (__ballot(band0 || band1)) {  // rare: the fp64 screens, then the JTS distance
-        if (band0) {
-            const unsigned q = pq[j];
-            const double ox = a.qx[q], oy = a.qy[q];
-            const double ex = px - ox, ey = py - oy, e2 = ex * ex + ey * ey;
-            h0 = e2 <= a.r2lo || (!(e2 > a.r2hi) && jts_pp_distance(px, py, ox, oy) <= a.r);
+// The pairs of one chunk of 64 points: ALL queries (the in-box ballot vm) and PART queries (the
+// kept hit ballots), from position pos on (advanced).  A full chunk's ALL pairs go straight out as
+// 512-B wave stores; the rest through the stage (st, sc), flushed when fewer than 4 x 64 slots
+// remain (the most one step adds).
+__device__ __forceinline__ void jemit_chunk(const JoinRun& a, unsigned long long vm, unsigned pid,
+                                            const unsigned* __restrict__ lall, unsigned nall,
+                                            const unsigned* __restrict__ lpq, unsigned npart,
+                                            const ulonglong2* __restrict__ masks, uint2* st, unsigned& sc,
+                                            unsigned long long& pos) {
+    const unsigned lane = (unsigned)lane_id();
+    const bool in_box = (vm >> lane) & 1ull;
+    const unsigned vrank = lanes_below(vm), vcnt = (unsigned)__popcll(vm);
+#ifdef JX_NOALL
+    pos += (unsigned long long)nall * vcnt;
+#else
+    if (vcnt == kWave) {
+        unsigned j = 0;
+        for (; j + 4 <= nall; j += 4) {  // four queries' ids in one LDS read
+            const uint4 q4 = *reinterpret_cast<const uint4*>(&lall[j]);
+            const unsigned long long p = pos + lane;
+            if (p < a.cap) jpair_store(a, p, pid, q4.x);
+            if (p + kWave < a.cap) jpair_store(a, p + kWave, pid, q4.y);
+            if (p + 2 * kWave < a.cap) jpair_store(a, p + 2 * kWave, pid, q4.z);
+            if (p + 3 * kWave < a.cap) jpair_store(a, p + 3 * kWave, pid, q4.w);
+            pos += 4 * kWave;
         }
-        if (band1) {
-            const unsigned q = pq[j + 1];
-            const double ox = a.qx[q], oy = a.qy[q];
-            const double ex = px - ox, ey = py - oy, e2 = ex * ex + ey * ey;
-            h1 = e2 <= a.r2lo || (!(e2 > a.r2hi) && jts_pp_distance(px, py, ox, oy) <= a.r);
+        for (; j < nall; j++) {
+            const unsigned long long p = pos + lane;
+            if (p < a.cap) jpair_store(a, p, pid, lall[j]);
+            pos += kWave;
+        }
+    } else {
+        for (unsigned j = 0; j < nall; j++) {
+            if (in_box) st[sc + vrank] = make_uint2(pid, lall[j]);
+            sc += vcnt;
+            if (sc > kJStage - 4 * kWave) jstage_flush(a, st, sc, pos);
         }
     }
-    m0 = __ballot(h0);
-    m1 = __ballot(h1);
+#endif
+#ifndef JX_NOPART
+    for (unsigned j = 0; j < npart; j += 4) {  // four queries per step, reads first
+        const ulonglong2 ma = masks[j / 2], mb = masks[j / 2 + 1];
+        const unsigned long long mq[4] = {ma.x, ma.y, mb.x, mb.y};
+        const unsigned qq[4] = {lpq[j], lpq[j + 1], lpq[j + 2], lpq[j + 3]};
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            if ((mq[u] >> lane) & 1ull) st[sc + lanes_below(mq[u])] = make_uint2(pid, qq[u]);
+            sc += (unsigned)__popcll(mq[u]);
+        }
+        if (sc > kJStage - 4 * kWave) jstage_flush(a, st, sc, pos);
+    }
+#endif
 }
 
 template <bool APPROX, bool WRITE>
 __global__ __launch_bounds__(kTB) void join_fused(JoinRun a) {
-    __shared__ unsigned lall[kJQ];       // ALL queries
-    __shared__ unsigned lpq[kJQ + 2];    // PART queries (+ padding)
-    __shared__ JPart lpr[kJQ + 2];
-    __shared__ jf2 lpb[kJQ + 2];
+    __shared__ __attribute__((aligned(16))) unsigned lall[kJQ];  // ALL queries
+    __shared__ unsigned lpq[kJQ + 4];    // PART queries (+ padding to a multiple of 4)
+    __shared__ JPart lpr[kJQ + 4];
+    __shared__ jf2 lpb[kJQ + 4];
     __shared__ uint2 stage[WRITE ? kTB / kWave : 1][WRITE ? kJStage : 1];
+    __shared__ ulonglong2 lmask[WRITE ? kTB / kWave : 1][WRITE ? kJCh : 1][WRITE ? kJQ / 2 : 1];  // PART ballots
     __shared__ unsigned sh_item, sh_nall, sh_npart, sh_amax, sh_wc[2][kTB / kWave];
     __shared__ unsigned long long sh_wcnt[kTB / kWave], sh_off;
     const int wid = threadIdx.x / kWave, lane = lane_id();
     const unsigned nitems = a.istart[a.ntiles];
-    const unsigned nb = (unsigned)a.tb.nb;
     const unsigned gq = *a.gcnt;
     const TileGeom& g = a.geo;
     const double slack = 0x1.0p-30 * (__builtin_fabs(g.mnx) + __builtin_fabs(g.mny) + ((double)g.nb + 2.0) * g.l);
@@ -947,8 +1418,8 @@ __global__ __launch_bounds__(kTB) void join_fused(JoinRun a) {
         const unsigned qs = a.qstart[tile], nql = a.qstart[tile + 1] - qs, nqt = nql + gq;
         const unsigned nqc = (nqt + kJQ - 1) / kJQ;
         const unsigned pc = d.y / nqc, qc = d.y - pc * nqc;
-        const unsigned ds = a.tb.start[tile] + pc * kJP;
-        const unsigned de0 = a.tb.start[tile + 1];
+        const unsigned ds = a.tstart[tile] + pc * kJP;
+        const unsigned de0 = a.tstart[tile + 1];
         const unsigned de = ds + kJP < de0 ? ds + kJP : de0;
         const unsigned q0 = qc * kJQ;
         const unsigned nbq = nqt - q0 < kJQ ? nqt - q0 : kJQ;
@@ -1017,11 +1488,11 @@ __global__ __launch_bounds__(kTB) void join_fused(JoinRun a) {
             if (threadIdx.x == 0) {
                 sh_nall = ta;
                 sh_npart = tp;
-                lpr[tp] = JPart{INT32_MAX, 0, INT32_MAX, 0};  // padding: never inside
-                lpr[tp + 1] = JPart{INT32_MAX, 0, INT32_MAX, 0};
-                lpb[tp] = jf2{0.f, 0.f};
-                lpb[tp + 1] = jf2{0.f, 0.f};
-                lpq[tp] = lpq[tp + 1] = 0;
+                for (unsigned u = tp; u < tp + 4; u++) {  // padding: never inside
+                    lpr[u] = JPart{INT32_MAX, 0, INT32_MAX, 0};
+                    lpb[u] = jf2{0.f, 0.f};
+                    lpq[u] = 0;
+                }
             }
         }
         __syncthreads();
@@ -1044,31 +1515,52 @@ __global__ __launch_bounds__(kTB) void join_fused(JoinRun a) {
                 hi = __builtin_nanf("");
             }
         }
-        // 2. count: the wave's chunks w, w + 4, ... of 64 points
+        // 2. count: the wave's chunks w, w + 4, ... of 64 points.  The write pass keeps every
+        //    decision of this phase -- each chunk's window indices and in-box ballot in registers,
+        //    the PART hit ballots in LDS -- so the emission issues no global load: on gfx9 a load's
+        //    wait also waits for every store issued before it, so a load in the emission would hold
+        //    the wave until its previous pair stores had drained.
         const unsigned nch = (de - ds + 63) / 64;
         unsigned long long cnt = 0;
-        for (unsigned c = (unsigned)wid; c < nch; c += kTB / kWave) {
+        uint4 rk[kJCh];
+        unsigned pidk[kJCh];
+        unsigned long long vmk[kJCh];
+#pragma unroll
+        for (unsigned k = 0; k < kJCh; k++) {  // the wave's records first: their loads in flight together
+            const unsigned c = (unsigned)wid + k * (kTB / kWave);
+            const unsigned i = ds + c * 64 + (unsigned)lane;
+            rk[k] = make_uint4(0u, 0u, 0u, 0u);
+            if (c < nch && i < de) rk[k] = a.recs[i];
+        }
+#pragma unroll
+        for (unsigned k = 0; k < kJCh; k++) {
+            const unsigned c = (unsigned)wid + k * (kTB / kWave);
+            vmk[k] = 0;
+            pidk[k] = 0;
+            if (c >= nch) continue;  // wave-uniform
             const unsigned i = ds + c * 64 + (unsigned)lane;
             const bool valid = i < de;
-            double px = 0.0, py = 0.0;
+            float ax = 0.f, ay = 0.f;
+            unsigned pid = 0;
             int32_t cx = -1, cy = -1;
-            if (valid) {
-                px = a.tb.sx[i];
-                py = a.tb.sy[i];
-                const unsigned key = a.tb.skey[i];
-                cx = (int32_t)g.dnb.div(key);
-                cy = (int32_t)(key - (unsigned)cx * nb);
-            }
-            const float ax = (float)(px - ox), ay = (float)(py - oy);
+            if (valid) jrec_load(rk[k], X0, Y0, ax, ay, pid, cx, cy);
             // ALL queries pair every point of the chunk whose coordinates lie in the tile box: a
             // NaN coordinate is keyed to cell 0 by the (int) cast yet has no distance <= r
-            // (the approximate join pairs it by cell alone)
-            const bool in_box = valid && (APPROX || (px == px && py == py));
-            cnt += (unsigned long long)nall * (unsigned)__popcll(__ballot(in_box));
-            for (unsigned j = 0; j < npart; j += 2) {
-                unsigned long long m0, m1;
-                jpart_pair<APPROX>(a, lpr, lpb, lpq, j, cx, cy, ax, ay, px, py, valid, lo, hi, m0, m1);
-                cnt += (unsigned)__popcll(m0) + (unsigned)__popcll(m1);
+            // (the approximate join pairs it by cell alone; fl32 of NaN - o is NaN, of a finite
+            // difference never)
+            const bool in_box = valid && (APPROX || (ax == ax && ay == ay));
+            const unsigned long long vm = __ballot(in_box);
+            vmk[k] = vm;
+            pidk[k] = pid;
+            cnt += (unsigned long long)nall * (unsigned)__popcll(vm);
+            for (unsigned j = 0; j < npart; j += 4) {
+                unsigned long long m[4];
+                jpart_quad<APPROX>(a, lpr, lpb, lpq, j, cx, cy, ax, ay, pid, lo, hi, m);
+                if (WRITE && lane == 0) {
+                    lmask[WRITE ? wid : 0][WRITE ? k : 0][WRITE ? j / 2 : 0] = make_ulonglong2(m[0], m[1]);
+                    lmask[WRITE ? wid : 0][WRITE ? k : 0][WRITE ? j / 2 + 1 : 0] = make_ulonglong2(m[2], m[3]);
+                }
+                cnt += (unsigned)(__popcll(m[0]) + __popcll(m[1]) + __popcll(m[2]) + __popcll(m[3]));
             }
         }
         if (lane == 0) sh_wcnt[wid] = cnt;
@@ -1079,49 +1571,288 @@ __global__ __launch_bounds__(kTB) void join_fused(JoinRun a) {
         //    every item wait for the count phase of all earlier ones: +0.25 ms on C3, measured)
         if (threadIdx.x == 0) sh_off = tot ? atomicAdd(a.total, tot) : 0ull;
         if (WRITE) __syncthreads();
-        // 4. emit: the same decisions, pairs staged per wave
+        // 4. emit the kept decisions (LDS reads and global stores only)
         if (WRITE && cnt) {
             unsigned long long pos = sh_off;
             for (int w = 0; w < wid; w++) pos += sh_wcnt[w];
             uint2* st = stage[WRITE ? wid : 0];
             unsigned sc = 0;
-            for (unsigned c = (unsigned)wid; c < nch; c += kTB / kWave) {
-                const unsigned i = ds + c * 64 + (unsigned)lane;
-                const bool valid = i < de;
-                double px = 0.0, py = 0.0;
-                int32_t cx = -1, cy = -1;
-                unsigned pid = 0;
-                if (valid) {
-                    px = a.tb.sx[i];
-                    py = a.tb.sy[i];
-                    pid = a.tb.sidx[i];
-                    const unsigned key = a.tb.skey[i];
-                    cx = (int32_t)g.dnb.div(key);
-                    cy = (int32_t)(key - (unsigned)cx * nb);
-                }
-                const float ax = (float)(px - ox), ay = (float)(py - oy);
-                const bool in_box = valid && (APPROX || (px == px && py == py));
-                const unsigned long long vm = __ballot(in_box);
-                const unsigned vrank = lanes_below(vm), vcnt = (unsigned)__popcll(vm);
-                // the stage has room for 2 x 64 pairs at the top of every step (flushed above 384)
-                for (unsigned j = 0; j < nall; j++) {
-                    if (in_box) st[sc + vrank] = make_uint2(pid, lall[j]);
-                    sc += vcnt;
-                    if (sc > kJStage - 2 * kWave) jstage_flush<WRITE>(a, st, sc, pos);
-                }
-                for (unsigned j = 0; j < npart; j += 2) {
-                    unsigned long long m0, m1;
-                    jpart_pair<APPROX>(a, lpr, lpb, lpq, j, cx, cy, ax, ay, px, py, valid, lo, hi, m0, m1);
-                    if ((m0 >> lane) & 1ull) st[sc + lanes_below(m0)] = make_uint2(pid, lpq[j]);
-                    sc += (unsigned)__popcll(m0);
-                    if ((m1 >> lane) & 1ull) st[sc + lanes_below(m1)] = make_uint2(pid, lpq[j + 1]);
-                    sc += (unsigned)__popcll(m1);
-                    if (sc > kJStage - 2 * kWave) jstage_flush<WRITE>(a, st, sc, pos);
-                }
+#pragma unroll
+            for (unsigned k = 0; k < kJCh; k++) {
+                const unsigned c = (unsigned)wid + k * (kTB / kWave);
+                if (c >= nch) continue;
+                jemit_chunk(a, vmk[k], pidk[k], lall, nall, lpq, npart, lmask[WRITE ? wid : 0][WRITE ? k : 0], st, sc,
+                            pos);
             }
-            if (sc) jstage_flush<WRITE>(a, st, sc, pos);
+            if (sc) jstage_flush(a, st, sc, pos);
         }
         __syncthreads();  // every wave leaves the item together (LDS reuse, uniform loop)
+    }
+}
+
+// ---- join write pass: decision waves and store waves ------------------------------------
+// On gfx9 a wave's load wait also waits for every store the wave issued before that load
+// (one in-order vmcnt), so a wave that both decides (loads) and stores pairs alternates between
+// the two: the one-role write pass measured 1.03 ms against 0.47 ms with its stores removed and
+// 0.65 ms for the pair bytes alone at the measured store rate.  Here each workgroup has kJCW
+// decision waves that never store to global memory and kJEW store waves that never load from it:
+// the decision waves classify, count and keep the decisions of item g in LDS set g % 2 (the
+// chunks' window indices and in-box ballots, the PART hit ballots, the query lists), reserve the
+// item's output run and hand the set over; the store waves turn the set into pairs while the
+// decision waves work on item g + 1.  The roles synchronise through LDS counters only (the
+// decision waves' barrier included), so neither role waits on the other's memory traffic.
+#ifndef GEOHIP_JOIN_PIPE
+#define GEOHIP_JOIN_PIPE 0  // 1: the two-role write pass (measured slower with LDS-staged emission)
+#endif
+constexpr int kJCW = kTB / kWave;           // decision waves (the classification's 256 threads)
+constexpr int kJEW = 2;                     // store waves (each the chunks of kJCW / kJEW decision waves)
+constexpr int kJPipeThreads = (kJCW + kJEW) * kWave;
+constexpr unsigned kJPipeBlocks = 512;      // 2 per CU (55 KB LDS)
+
+struct JSet {
+    unsigned lall[kJQ];
+    unsigned lpq[kJQ + 4];
+    ulonglong2 mask[kJCW][kJCh][kJQ / 2];
+    unsigned pid[kJCW][kJCh][kWave];
+    unsigned long long vm[kJCW][kJCh];
+    unsigned long long wcnt[kJCW];
+    unsigned long long base;
+    unsigned nall, npart, nch;
+};
+
+__device__ __forceinline__ unsigned lds_peek(const unsigned* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// this wave's LDS operations done, then +1 (relaxed: no global-memory fence, which would wait
+// for the store waves' pair stores)
+__device__ __forceinline__ void lds_signal(unsigned* p) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane_id() == 0) __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_wait_geq(const unsigned* p, unsigned target) {
+    while (lds_peek(p) < target) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+}
+
+template <bool APPROX>
+__global__ __launch_bounds__(kJPipeThreads) void join_pipe(JoinRun a) {
+    __shared__ JSet set[2];
+    __shared__ JPart lpr[kJQ + 4];
+    __shared__ jf2 lpb[kJQ + 4];
+    __shared__ uint2 stage[kJEW][kJStage];
+    __shared__ unsigned c_bar, produced, done, sh_item, sh_amax, sh_wc[2][kJCW];
+    __shared__ unsigned consumed[kJEW];  // items emitted, per store wave (they run at their own pace)
+    const int wid = threadIdx.x / kWave, lane = lane_id();
+    if (threadIdx.x == 0) {
+        c_bar = 0;
+        produced = 0;
+        for (int e = 0; e < kJEW; e++) consumed[e] = 0;
+        done = 0;
+    }
+    __syncthreads();  // the only workgroup barrier: below, each role waits on LDS counters
+    if (wid >= kJCW) {
+        // ---------------- store waves: no global loads
+        const int e = wid - kJCW;
+        uint2* st = stage[e];
+        for (unsigned g = 0;; g++) {
+            while (lds_peek(&produced) <= g) {
+                if (lds_peek(&done) && lds_peek(&produced) <= g) return;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            asm volatile("" ::: "memory");
+            const JSet& S = set[g & 1];
+            const unsigned nall = S.nall, npart = S.npart, nch = S.nch;
+            for (int cw = e * (kJCW / kJEW); cw < (e + 1) * (kJCW / kJEW); cw++) {
+                unsigned long long pos = S.base;
+                for (int w = 0; w < cw; w++) pos += S.wcnt[w];
+                if (S.wcnt[cw] == 0) continue;
+                unsigned sc = 0;
+#pragma unroll
+                for (unsigned k = 0; k < kJCh; k++) {
+                    const unsigned c = (unsigned)cw + k * kJCW;
+                    if (c >= nch) continue;
+                    jemit_chunk(a, S.vm[cw][k], S.pid[cw][k][lane], S.lall, nall, S.lpq, npart, S.mask[cw][k], st, sc,
+                                pos);
+                }
+                if (sc) jstage_flush(a, st, sc, pos);
+            }
+            lds_signal(&consumed[e]);  // the set's reads are done (in-order LDS)
+        }
+    }
+    // ---------------- decision waves: no global stores
+    const unsigned nitems = a.istart[a.ntiles];
+    const unsigned gq = *a.gcnt;
+    const TileGeom& g = a.geo;
+    const double slack = 0x1.0p-30 * (__builtin_fabs(g.mnx) + __builtin_fabs(g.mny) + ((double)g.nb + 2.0) * g.l);
+    unsigned phase = 0;
+    auto cbar = [&]() {  // barrier of the decision waves
+        phase += kJCW;
+        lds_signal(&c_bar);
+        lds_wait_geq(&c_bar, phase);
+    };
+    for (unsigned gi = 0;; gi++) {
+        if (threadIdx.x == 0) {
+            sh_item = atomicAdd(a.ticket, 1u);
+            sh_amax = 0;
+        }
+        cbar();
+        const unsigned it = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_peek(&sh_item));
+        if (it >= nitems) break;
+        JSet& S = set[gi & 1];
+        if (gi >= 2)  // item gi - 2 emitted by every store wave: its set is free
+            for (int e = 0; e < kJEW; e++) lds_wait_geq(&consumed[e], gi - 1);
+        const uint2 d = a.items[it];
+        const unsigned tile = d.x;
+        const unsigned qs = a.qstart[tile], nql = a.qstart[tile + 1] - qs, nqt = nql + gq;
+        const unsigned nqc = (nqt + kJQ - 1) / kJQ;
+        const unsigned pc = d.y / nqc, qc = d.y - pc * nqc;
+        const unsigned ds = a.tstart[tile] + pc * kJP;
+        const unsigned de0 = a.tstart[tile + 1];
+        const unsigned de = ds + kJP < de0 ? ds + kJP : de0;
+        const unsigned q0 = qc * kJQ;
+        const unsigned nbq = nqt - q0 < kJQ ? nqt - q0 : kJQ;
+        const int32_t tx = (int32_t)(tile / (unsigned)g.nt), ty = (int32_t)(tile % (unsigned)g.nt);
+        const int32_t X0 = tx * g.ts, Y0 = ty * g.ts;
+        const int32_t X1 = X0 + g.ts - 1 < g.nb - 1 ? X0 + g.ts - 1 : g.nb - 1;
+        const int32_t Y1 = Y0 + g.ts - 1 < g.nb - 1 ? Y0 + g.ts - 1 : g.nb - 1;
+        const double ox = g.mnx + (double)X0 * g.l, oy = g.mny + (double)Y0 * g.l;
+        const double bx0 = ox - slack, by0 = oy - slack;
+        const double bx1 = g.mnx + (double)(X1 + 1) * g.l + slack, by1 = g.mny + (double)(Y1 + 1) * g.l + slack;
+        // the wave's records, in flight during the classification
+        const unsigned nch = (de - ds + 63) / 64;
+        uint4 rk[kJCh];
+#pragma unroll
+        for (unsigned k = 0; k < kJCh; k++) {
+            const unsigned c = (unsigned)wid + k * kJCW;
+            const unsigned i = ds + c * 64 + (unsigned)lane;
+            rk[k] = make_uint4(0u, 0u, 0u, 0u);
+            if (c < nch && i < de) rk[k] = a.recs[i];
+        }
+        // 1. classify the item's queries (as join_fused)
+        int cls = 0;
+        unsigned q = 0;
+        QRect R{1, 0, 1, 0};
+        double qxv = 0.0, qyv = 0.0;
+        if (threadIdx.x < nbq) {
+            const unsigned t = q0 + threadIdx.x;
+            q = t < nql ? a.qlist[qs + t] : a.glist[t - nql];
+            R = a.rect[q];
+            qxv = a.qx[q];
+            qyv = a.qy[q];
+            const bool inter = R.x0 <= R.x1 && R.y0 <= R.y1 && R.x0 <= X1 && R.x1 >= X0 && R.y0 <= Y1 && R.y1 >= Y0;
+            const bool cover = R.x0 <= X0 && R.x1 >= X1 && R.y0 <= Y0 && R.y1 >= Y1;
+            if (APPROX) {
+                cls = !inter ? 0 : (cover ? 1 : 2);
+            } else if (inter) {
+                const double ex0 = __builtin_fmax(__builtin_fmax(bx0 - qxv, qxv - bx1), 0.0);
+                const double ey0 = __builtin_fmax(__builtin_fmax(by0 - qyv, qyv - by1), 0.0);
+                const double dmin2 = ex0 * ex0 + ey0 * ey0;
+                const double ex1 = __builtin_fmax(__builtin_fabs(qxv - bx0), __builtin_fabs(qxv - bx1));
+                const double ey1 = __builtin_fmax(__builtin_fabs(qyv - by0), __builtin_fabs(qyv - by1));
+                const double dmax2 = ex1 * ex1 + ey1 * ey1;
+                if (dmin2 * (1.0 - 0x1.0p-40) > a.r2hi) cls = 0;
+                else if (cover && dmax2 * (1.0 + 0x1.0p-40) < a.r2lo) cls = 1;
+                else cls = 2;
+            }
+        }
+        {
+            const unsigned long long ma = __ballot(cls == 1), mp = __ballot(cls == 2);
+            if (lane == 0) {
+                sh_wc[0][wid] = (unsigned)__popcll(ma);
+                sh_wc[1][wid] = (unsigned)__popcll(mp);
+            }
+            cbar();
+            unsigned ba = 0, bp = 0, ta = 0, tp = 0;
+            for (int w = 0; w < kJCW; w++) {
+                if (w < wid) {
+                    ba += sh_wc[0][w];
+                    bp += sh_wc[1][w];
+                }
+                ta += sh_wc[0][w];
+                tp += sh_wc[1][w];
+            }
+            if (cls == 1) S.lall[ba + lanes_below(ma)] = q;
+            if (cls == 2) {
+                const unsigned k = bp + lanes_below(mp);
+                S.lpq[k] = q;
+                lpr[k] = JPart{R.x0, R.x1 - R.x0, R.y0, R.y1 - R.y0};
+                const float fx = (float)(qxv - ox), fy = (float)(qyv - oy);
+                lpb[k] = jf2{fx, fy};
+                const float m = __builtin_fmaxf(__builtin_fabsf(fx), __builtin_fabsf(fy));
+                atomicMax(&sh_amax, m == m ? __float_as_uint(m) : 0x7f800000u);  // NaN -> no fp32 screen
+            }
+            if (threadIdx.x == 0) {
+                S.nall = ta;
+                S.npart = tp;
+                S.nch = nch;
+                for (unsigned u = tp; u < tp + 4; u++) {  // padding: never inside
+                    lpr[u] = JPart{INT32_MAX, 0, INT32_MAX, 0};
+                    lpb[u] = jf2{0.f, 0.f};
+                    S.lpq[u] = 0;
+                }
+            }
+        }
+        cbar();
+        const unsigned nall = S.nall, npart = S.npart;
+        float lo = -1.0f, hi = __builtin_inff();
+        if (!APPROX) {
+            const double pa = (bx1 - bx0) + (by1 - by0);
+            const double A = pa + 2.0 * (double)__uint_as_float(lds_peek(&sh_amax)) * (1.0 + 0x1.0p-20);
+            const double e = 2.05 * 0x1.0p-24 * A;
+            const double err = 4.0 * e * A + 2.0 * e * e;
+            if (err == err && err < 0x1.0p100) {
+                if (a.r2lo > 0.0) {
+                    const double l = (a.r2lo - err) * (1.0 - 0x1.0p-21);
+                    lo = l > 0.0 ? __double2float_rd(l) : -1.0f;
+                }
+                if (a.r2hi < 0x1.0p100) hi = __double2float_ru((a.r2hi + err) * (1.0 + 0x1.0p-21));
+            } else {
+                lo = -1.0f;
+                hi = __builtin_nanf("");
+            }
+        }
+        // 2. count, keeping every decision in the set
+        unsigned long long cnt = 0;
+#pragma unroll
+        for (unsigned k = 0; k < kJCh; k++) {
+            const unsigned c = (unsigned)wid + k * kJCW;
+            if (c >= nch) continue;
+            const unsigned i = ds + c * 64 + (unsigned)lane;
+            const bool valid = i < de;
+            float ax = 0.f, ay = 0.f;
+            unsigned pid = 0;
+            int32_t cx = -1, cy = -1;
+            if (valid) jrec_load(rk[k], X0, Y0, ax, ay, pid, cx, cy);
+            const bool in_box = valid && (APPROX || (ax == ax && ay == ay));
+            const unsigned long long vm = __ballot(in_box);
+            S.pid[wid][k][lane] = pid;
+            if (lane == 0) S.vm[wid][k] = vm;
+            cnt += (unsigned long long)nall * (unsigned)__popcll(vm);
+            for (unsigned j = 0; j < npart; j += 4) {
+                unsigned long long m[4];
+                jpart_quad<APPROX>(a, lpr, lpb, S.lpq, j, cx, cy, ax, ay, pid, lo, hi, m);
+                if (lane == 0) {
+                    S.mask[wid][k][j / 2] = make_ulonglong2(m[0], m[1]);
+                    S.mask[wid][k][j / 2 + 1] = make_ulonglong2(m[2], m[3]);
+                }
+                cnt += (unsigned)(__popcll(m[0]) + __popcll(m[1]) + __popcll(m[2]) + __popcll(m[3]));
+            }
+        }
+        if (lane == 0) S.wcnt[wid] = cnt;
+        cbar();
+        // 3. the item's output run, then the hand-over
+        if (wid == 0) {
+            unsigned long long tot = 0;
+            for (int w = 0; w < kJCW; w++) tot += S.wcnt[w];
+            unsigned long long b = 0;
+            if (lane == 0 && tot) b = atomicAdd(a.total, tot);
+            if (lane == 0) S.base = b;
+            lds_signal(&produced);
+        }
+    }
+    if (wid == 0) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(&done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 }
 
@@ -3292,7 +4023,7 @@ namespace {
 
 enum JSlot {
     J_HIST, J_TTOT, J_TSTART, J_SEG, J_SX, J_SY, J_SIDX, J_SKEY, J_MISC, J_AUX, J_POLY, J_OUT, J_RECT, J_QSTART,
-    J_QLIST, J_GLIST, J_QCNT, J_BCNT, J_BOFF, J_PMASK, J_MWORDS, J_MOFF
+    J_QLIST, J_GLIST, J_QCNT, J_BCNT, J_BOFF, J_PMASK, J_MWORDS, J_MOFF, J_TCNT, J_TCUR
 };
 
 // J_MISC words: [0] outside count, [1] outside cursor, [2] scan grand total, [3] global
@@ -3449,6 +4180,57 @@ int bin_tiles(geohip_ctx* ctx, Scratch& S, const double* dx, const double* dy, u
     return GEOHIP_OK;
 }
 
+// Join binning (jb_bands / jb_scan / jb_tiles): the window's in-grid points as tile-sorted
+// 16-B records; *recs and *tstart (ntiles + 1) on the device.  jb_scan also zeroes zero[nzero).
+int join_bin(geohip_ctx* ctx, Scratch& S, const double* dx, const double* dy, uint64_t n, const TileGeom& geo,
+             const uint4** recs, const unsigned** tstart, unsigned* zero, unsigned nzero) {
+    hipStream_t st = ctx_stream(ctx);
+    uint64_t nblk = (n + 16383) / 16384;
+    if (nblk > kJbBlocks) nblk = kJbBlocks;
+    if (nblk < 1) nblk = 1;
+    JBin a;
+    memset(&a, 0, sizeof a);
+    a.x = dx;
+    a.y = dy;
+    a.n = n;
+    a.chunk = (n + nblk - 1) / nblk;
+    a.g = geo;
+    a.nbands = (unsigned)((geo.ntiles + kBandTiles - 1) / kBandTiles);
+    a.nsub = (unsigned)((a.chunk + kJbSub - 1) / kJbSub);
+    if (a.nsub < 1) a.nsub = 1;
+    a.nblk = (unsigned)nblk;
+    const uint64_t nt = geo.ntiles;
+    const uint64_t nseg = (uint64_t)a.nblk * a.nsub;
+    const uint64_t maxround = n / kJbRound + a.nbands + 1;
+    a.l1 = S.get<uint4>(J_SY, n * 16 + 64);
+    a.recs = S.get<uint4>(J_SX, n * 16 + 64);
+    a.soff = S.get<unsigned>(J_HIST, (size_t)nblk * a.nsub * (a.nbands + 1) * 4 + 16);
+    a.tstart = S.get<unsigned>(J_TSTART, (nt + 1) * 4);
+    a.tcur = S.get<unsigned>(J_TCUR, (nt + 1) * 4);
+    char* seg = S.get<char>(J_SEG, (size_t)a.nbands * (2 * nseg + 1) * 4 + a.nbands * 4 + 16 + maxround * 16 + 64);
+    if (S.rc) return S.rc;
+    a.rinfo = reinterpret_cast<uint4*>(seg);
+    a.spre = reinterpret_cast<unsigned*>(seg + maxround * 16);
+    a.sst = a.spre + (size_t)a.nbands * (nseg + 1);
+    a.nne = a.sst + (size_t)a.nbands * nseg;
+    a.nround = a.nne + a.nbands;
+    void* tc = nullptr;
+    int rc = ctx_ensure_zeroed(ctx, J_TCNT, kMaxTiles * 4, &tc);  // jb_scan leaves it zero
+    if (rc) return rc;
+    a.tcnt = reinterpret_cast<unsigned*>(tc);
+    if (n) jb_bands<<<(unsigned)nblk, kBinThreads, 0, st>>>(a);
+    jb_scan<<<1, kBinThreads, 0, st>>>(a, zero, nzero);
+    if (n) {
+        jb_segs<<<a.nbands, kBinThreads, 0, st>>>(a);
+        jb_tiles<<<(unsigned)std::min<uint64_t>(kJbL2Blocks, maxround), kJbL2Threads, 0, st>>>(a);
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, std::string("join binning: ") + hipGetErrorString(e));
+    *recs = a.recs;
+    *tstart = a.tstart;
+    return GEOHIP_OK;
+}
+
 int read_total(geohip_ctx* ctx, unsigned long long* dev_total, uint64_t* out) {
     hipStream_t st = ctx_stream(ctx);
     uint64_t* pin = ctx_pinned(ctx);
@@ -3509,32 +4291,32 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
     rc = ctx_stage_xy(ctx, dx, dy, nd, 0, &ddx, &ddy);
     if (!rc) rc = ctx_stage_xy(ctx, qx, qy, nq, 1, &dqx, &dqy);
     if (rc) return rc;
-    hipEvent_t e0, e1;
-    ctx_timing_events(ctx, &e0, &e1);
-    if (e0) hipEventRecord(e0, st);  // the whole device step: binning, replication, join
-    TileBins tb;
-    rc = bin_tiles(ctx, S, ddx, ddy, nd, geo, false, &tb, nullptr, nullptr);
-    if (rc) return rc;
     const uint64_t ntl = geo.ntiles;
     // item bound: per tile ceil(points / kJP) * ceil(queries / kJQ)
     const uint64_t qpt = global_mode ? nq : std::min<uint64_t>(nq, list_cap);
     const uint64_t item_cap = ((nd + kJP - 1) / kJP + ntl) * ((qpt + kJQ - 1) / kJQ) + 1;
     QRect* drect = S.get<QRect>(J_RECT, nq * sizeof(QRect) + 16);
-    unsigned* qcnt = S.get<unsigned>(J_QCNT, (ntl + 1) * 4);
+    // per-call counters, zeroed by one launch (jb_scan): query counts | query cursors | misc words
+    // ([0] jq_rect error, [4] ticket, [5] global query count) | the pair total (u64)
+    const unsigned nzero = (unsigned)(2 * (ntl + 1) + kMiscWords + 2 + 1) & ~1u;
+    unsigned* zero = S.get<unsigned>(J_QCNT, (size_t)nzero * 4 + 16);
     unsigned* qstart = S.get<unsigned>(J_QSTART, (ntl + 1) * 4);
     unsigned* qlist = S.get<unsigned>(J_QLIST, list_cap * 4 + 16);
     unsigned* glist = S.get<unsigned>(J_GLIST, nq * 4 + 16);
-    unsigned* misc = S.get<unsigned>(J_MISC, kMiscWords * 4);
-    unsigned* seg = S.get<unsigned>(J_SEG, ((ntl + kScanSeg - 1) / kScanSeg + 1) * 8 + 64);
-    unsigned* icnt = S.get<unsigned>(J_BCNT, (ntl + 1) * 4);
     unsigned* istart = S.get<unsigned>(J_BOFF, (ntl + 1) * 4);
     uint2* items = S.get<uint2>(J_MWORDS, item_cap * 8);
-    unsigned long long* total = S.get<unsigned long long>(J_MOFF, 64);
     if (S.rc) return S.rc;
-    // misc: [0] jq_rect error, [2..3] scan totals, [4] ticket, [5] global query count
-    if (hipMemsetAsync(qcnt, 0, (ntl + 1) * 4, st) != hipSuccess || hipMemsetAsync(misc + 4, 0, 8, st) != hipSuccess ||
-        hipMemsetAsync(misc, 0, 4, st) != hipSuccess || hipMemsetAsync(total, 0, 8, st) != hipSuccess)
-        return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
+    unsigned* qcnt = zero;
+    unsigned* qcur = zero + (ntl + 1);
+    unsigned* misc = zero + 2 * (ntl + 1);
+    unsigned long long* total = reinterpret_cast<unsigned long long*>(zero + ((2 * (ntl + 1) + kMiscWords + 1) & ~(uint64_t)1));
+    hipEvent_t e0, e1;
+    ctx_timing_events(ctx, &e0, &e1);
+    if (e0) hipEventRecord(e0, st);  // the whole device step: binning, replication, join
+    const uint4* recs = nullptr;
+    const unsigned* tstart = nullptr;
+    rc = join_bin(ctx, S, ddx, ddy, nd, geo, &recs, &tstart, zero, nzero);
+    if (rc) return rc;
     const unsigned qb = (unsigned)((nq + kTB - 1) / kTB);
     if (nq) {
         JqGeom jg{gq->min_x, gq->min_y, gq->cell_len, nb, lc, all_cells ? 1 : 0};
@@ -3542,19 +4324,15 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
     }
     if (global_mode) {
         if (nq) jq_global<<<qb, kTB, 0, st>>>(nq, glist, misc + 5);
-        scan_launch<unsigned>(st, qcnt, ntl, seg, misc + 2, qstart);  // all zero: no per-tile lists
+        jq_starts<<<1, kBinThreads, 0, st>>>(qcnt, geo.ntiles, qstart);  // all zero: no per-tile lists
     } else {
         const unsigned qg = (unsigned)((nq + kTB / kWave - 1) / (kTB / kWave));  // one wave per query
         if (nq) jq_build<false><<<qg, kTB, 0, st>>>(drect, nq, geo, qcnt, nullptr, nullptr);
-        scan_launch<unsigned>(st, qcnt, ntl, seg, misc + 2, qstart);
-        if (hipMemsetAsync(qcnt, 0, (ntl + 1) * 4, st) != hipSuccess)
-            return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
-        if (nq) jq_build<true><<<qg, kTB, 0, st>>>(drect, nq, geo, qcnt, qstart, qlist);
+        jq_starts<<<1, kBinThreads, 0, st>>>(qcnt, geo.ntiles, qstart);
+        if (nq) jq_build<true><<<qg, kTB, 0, st>>>(drect, nq, geo, qcur, qstart, qlist);
     }
-    const unsigned tg = (unsigned)((ntl + kTB - 1) / kTB);
-    join_items<<<tg, kTB, 0, st>>>(tb.start, qstart, misc + 5, geo.ntiles, icnt);
-    scan_launch<unsigned>(st, icnt, ntl, seg, misc + 3, istart);
-    join_item_fill<<<tg, kTB, 0, st>>>(istart, geo.ntiles, items);
+    join_plan<<<1, kBinThreads, 0, st>>>(tstart, qstart, misc + 5, geo.ntiles, istart);
+    join_item_fill<<<(unsigned)((ntl + kTB - 1) / kTB), kTB, 0, st>>>(istart, geo.ntiles, items);
     // output: device pointer directly, or a device staging buffer for host output
     unsigned* out = nullptr;
     if (!count_only && cap) {
@@ -3570,15 +4348,17 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
     double r2lo, r2hi;
     screen_bounds(r, &r2lo, &r2hi);
     const bool write = !count_only;
-    JoinRun jr{tb, geo, qstart, qlist, glist, misc + 5, dqx, dqy, drect, r, r2lo, r2hi, istart, items, geo.ntiles,
+    JoinRun jr{recs, tstart, ddx, ddy, geo, qstart, qlist, glist, misc + 5, dqx, dqy, drect, r, r2lo, r2hi, istart, items, geo.ntiles,
                misc + 4, total, out, out ? cap : 0, ((uintptr_t)out & 7u) == 0};
     if (nq && nd) {
         if (approximate) {
-            if (write) join_fused<true, true><<<kJBlocks, kTB, 0, st>>>(jr);
-            else join_fused<true, false><<<kJBlocks, kTB, 0, st>>>(jr);
+            if (write && GEOHIP_JOIN_PIPE) join_pipe<true><<<kJPipeBlocks, kJPipeThreads, 0, st>>>(jr);
+            else if (write) join_fused<true, true><<<kJBlocksW, kTB, 0, st>>>(jr);
+            else join_fused<true, false><<<kJBlocksC, kTB, 0, st>>>(jr);
         } else {
-            if (write) join_fused<false, true><<<kJBlocks, kTB, 0, st>>>(jr);
-            else join_fused<false, false><<<kJBlocks, kTB, 0, st>>>(jr);
+            if (write && GEOHIP_JOIN_PIPE) join_pipe<false><<<kJPipeBlocks, kJPipeThreads, 0, st>>>(jr);
+            else if (write) join_fused<false, true><<<kJBlocksW, kTB, 0, st>>>(jr);
+            else join_fused<false, false><<<kJBlocksC, kTB, 0, st>>>(jr);
         }
     }
     if (e1) hipEventRecord(e1, st);

@@ -12,6 +12,7 @@ namespace geohip {
 // context services implemented in abi.cpp
 int ctx_fail(geohip_ctx* ctx, int code, const std::string& msg);
 int ctx_ensure(geohip_ctx* ctx, int slot, size_t bytes, void** out);  // slot 0..25
+int ctx_ensure_zeroed(geohip_ctx* ctx, int slot, size_t bytes, void** out);  // zeroed when (re)allocated
 int ctx_ensure_ingest(geohip_ctx* ctx, int slot, size_t bytes, void** out);  // slot 0..11
 int ctx_ensure_ingest_zeroed(geohip_ctx* ctx, int slot, size_t bytes, void** out);  // zeroed when (re)allocated
 unsigned long long ctx_next_epoch(geohip_ctx* ctx);  // look-back epoch: 1 .. 2^22 - 1, new per call

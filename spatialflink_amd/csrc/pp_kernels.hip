@@ -18,7 +18,6 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <stdlib.h>
 #include <string.h>
 
 #include <type_traits>
@@ -704,16 +703,6 @@ constexpr unsigned kSlotMaxK = 256;
 constexpr unsigned kMinWord = 6400;
 constexpr unsigned kStatWord = (unsigned)(kKnnCounterBytes / 4) - 16;  // last final: entries, spilled, kept
 constexpr unsigned kVbWord = kTicketStride * (kMaxTicketGroups + 1);      // chunk ticket (fused range)
-// Tail pools (GEOHIP_KNN_TAIL > 0): the last GEOHIP_KNN_TAIL % of the fronts are not dealt to the
-// blocks statically but claimed one iteration at a time from 8 pools -- pool x holds the tail
-// iterations of the blocks b with b % 8 == x (one XCD under round-robin dispatch) -- own pool first,
-// then the others', so an XCD whose stream runs slower hands its last iterations to faster ones.
-// Counters at word kPoolWord + kTicketStride * x, re-armed by the final.
-#ifndef GEOHIP_KNN_TAIL
-#define GEOHIP_KNN_TAIL 0
-#endif
-constexpr unsigned kPoolWord = 7000;
-constexpr unsigned kNoIter = 0xffffffffu, kTailIter = 0x80000000u;
 
 template <int NW>
 struct PassBlock {
@@ -732,7 +721,6 @@ struct PassBlock {
     unsigned fin[4];            // the final's LDS words
     unsigned long long tslot;   // slot bound T_b (kSentinelD: none)
     unsigned nslot;             // survivors at or below T_b
-    unsigned pool_dead;         // tail pools found empty (bit x)
 };
 
 // One wave: the lowest bin holding a survivor, -1 if none (8 bins per lane).
@@ -891,33 +879,25 @@ __device__ __forceinline__ void pass_final(const PassIo& io, const KnnArgs& a, u
         sh[2] = 0;            // gather cursor
         sh[3] = 0;            // whole lists
     }
-    // every block slot-complete (the usual case for k <= kSlotMaxK): the union of the blocks' slots
-    // already holds the window's k nearest and only a few more -- no bound T is needed, every slot
-    // entry goes to the rank placement
-    const bool all_slots = __syncthreads_and(!blk || (mylen & kLenSlots)) != 0;
+    __syncthreads();
     PASS_TRACE(io, 11);
     // ---- B
-    if (!all_slots) {
 #pragma unroll
-        for (unsigned u = 0; u < kPer; u++)
-            if (hd[u] != kSentinelD) atomicAdd(&hist[hist_bin(hd[u], a.hist_base)], 1u);
-    }
+    for (unsigned u = 0; u < kPer; u++)
+        if (hd[u] != kSentinelD) atomicAdd(&hist[hist_bin(hd[u], a.hist_base)], 1u);
     if (blk) {
         // flagged: whole whatever T; slot-complete: never (its slots hold all it contributes)
         blast_sh[threadIdx.x] = (mylen & kLenWhole) ? 0ull : ((mylen & kLenSlots) ? kSentinelD : blast);
         lens[threadIdx.x] = mylen & ~(kLenWhole | kLenSlots);
     }
     if (blk) io.ctr[kMinWord + threadIdx.x] = 0u;  // slot-bound words re-armed for the next launch
-    if (GEOHIP_KNN_TAIL > 0 && threadIdx.x < 8) store_wt(io.ctr + kPoolWord + kTicketStride * threadIdx.x, 0u);
     __syncthreads();
     // ---- C
-    if (!all_slots) {
-        if (wid == 0) {
-            const int bin = hist_kth_bin(hist, k);
-            if (lane == 0 && bin >= 0 && bin < kHistBins - 1) sh[0] = (unsigned)bin;
-        }
-        __syncthreads();
+    if (wid == 0) {
+        const int bin = hist_kth_bin(hist, k);
+        if (lane == 0 && bin >= 0 && bin < kHistBins - 1) sh[0] = (unsigned)bin;
     }
+    __syncthreads();
     PASS_TRACE(io, 12);
     const unsigned long long T = sh[0] != 0xffffffffu ? hist_edge((int)sh[0], a.hist_base) : kSentinelD;
     // ---- D
@@ -1211,7 +1191,6 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
         kb.cursor = 0;
         kb.nsmall = 0;
         kb.next_it = 2 * NW;  // iterations wid and NW + wid start statically
-        kb.pool_dead = 0;
     }
     PASS_TRACE(io, 0);
     if (io.trace && threadIdx.x == 0) {  // measurement only: the XCD this block runs on
@@ -1235,15 +1214,10 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
     constexpr unsigned kRot = GEOHIP_KNN_ROT;
     const uint64_t total_iters = (n + kPtsIter - 1) / kPtsIter;
     const uint64_t full_fronts = total_iters / gridDim.x, rem_front = total_iters % gridDim.x;
-    const unsigned niters_all =
+    const unsigned niters =
         kInterleave ? (unsigned)(full_fronts + ((rem_front && (blockIdx.x + full_fronts * kRot) % gridDim.x < rem_front)
                                                     ? 1u : 0u))
                     : (unsigned)((blk_end - blk_begin + kPtsIter - 1) / kPtsIter);
-    // static iterations of this block; with tail pools the fronts from S on are claimed dynamically
-    const unsigned S_tail = (unsigned)(full_fronts * (100u - GEOHIP_KNN_TAIL) / 100u);
-    const bool tail = GEOHIP_KNN_TAIL > 0 && kInterleave && kRot == 0 && S_tail >= 2u * NW && S_tail < full_fronts;
-    const unsigned niters = tail ? S_tail : niters_all;
-    const unsigned nfronts = (unsigned)((total_iters + gridDim.x - 1) / gridDim.x);
     if (kInterleave) blk_end = n;
     unsigned ccnt = 0;
     unsigned appended = 0, last_hist = 0;
@@ -1322,7 +1296,6 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
     const bool all_valid[4] = {true, true, true, true};
     double ax[4], ay[4], bx[4], by[4];
     auto it_base = [&](unsigned it) {
-        if (it & kTailIter) return (uint64_t)(it & ~kTailIter) * kPtsIter;  // a claimed global iteration
         return kInterleave ? ((uint64_t)it * gridDim.x + (blockIdx.x + (uint64_t)it * kRot) % gridDim.x) * kPtsIter
                            : blk_begin + (uint64_t)it * kPtsIter;
     };
@@ -1336,29 +1309,9 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
         px[0] = u0.x; px[1] = u0.y; px[2] = u1.x; px[3] = u1.y;
         py[0] = v0.x; py[1] = v0.y; py[2] = v1.x; py[3] = v1.y;
     };
-    unsigned pool_k = 0;  // tail pools tried by this wave (lane 0)
     auto claim = [&]() -> unsigned {
         unsigned v = 0;
-        if (lane == 0) {
-            v = atomicAdd(&kb.next_it, 1u);
-            if (tail && v >= niters) {
-                v = kNoIter;
-                const unsigned nb = gridDim.x, x0 = blockIdx.x & 7u;
-                for (; pool_k < 8u; pool_k++) {
-                    const unsigned px = (x0 + pool_k) & 7u;
-                    if (px >= nb || (lds_fresh(kb.pool_dead) >> px) & 1u) continue;
-                    const unsigned gsz = (nb - px + 7u) / 8u;  // blocks b with b % 8 == px
-                    const unsigned j = atomicAdd(io.ctr + kPoolWord + kTicketStride * px, 1u);
-                    const unsigned f = niters + j / gsz;
-                    const uint64_t g = (uint64_t)f * nb + px + 8u * (j % gsz);
-                    if (f < nfronts && g < total_iters) {
-                        v = kTailIter | (unsigned)g;
-                        break;
-                    }
-                    atomicOr(&kb.pool_dead, 1u << px);  // past the pool's end: exhausted
-                }
-            }
-        }
+        if (lane == 0) v = atomicAdd(&kb.next_it, 1u);
         return (unsigned)__builtin_amdgcn_readfirstlane((int)v);
     };
     auto run = [&](unsigned it, double (&px)[4], double (&py)[4]) {
@@ -1371,12 +1324,9 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
             iter(kPart, qx4, qy4, valid, it_base(it));
         }
     };
-    // ia / ibb: the iteration each of the wave's two slots holds (kNoIter: none); static it < niters,
-    // or a claimed tail iteration (kTailIter | global iteration)
-    unsigned ia = (unsigned)wid < niters ? (unsigned)wid : kNoIter;
-    unsigned ibb = (unsigned)(NW + wid) < niters ? (unsigned)(NW + wid) : kNoIter;
-    if (ia != kNoIter && is_full(ia)) load_full(ia, ax, ay);
-    if (ibb != kNoIter && is_full(ibb)) load_full(ibb, bx, by);
+    unsigned ia = (unsigned)wid, ibb = (unsigned)(NW + wid);
+    if (ia < niters && is_full(ia)) load_full(ia, ax, ay);
+    if (ibb < niters && is_full(ibb)) load_full(ibb, bx, by);
     __syncthreads();
     // slot bound publication (kSlotMaxK): the waves claiming these iterations publish the
     // block's lowest survivor bin so far
@@ -1387,23 +1337,20 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
         const int bin = hist_low_bin(kb.hist);
         if (lane == 0 && bin >= 0 && bin < kHistBins - 1) store_wt(io.ctr + kMinWord + blockIdx.x, (unsigned)bin + 1u);
     };
-    auto valid_it = [&](unsigned v) { return (v & kTailIter) ? v != kNoIter : v < niters; };
-    while (ia != kNoIter || ibb != kNoIter) {
-        if (ia != kNoIter) {
-            unsigned na = claim();
-            if (!valid_it(na)) na = kNoIter;
+    while (ia < niters || ibb < niters) {
+        if (ia < niters) {
+            const unsigned na = claim();
             run(ia, ax, ay);
             publish(na);
             ia = na;
-            if (ia != kNoIter && is_full(ia)) load_full(ia, ax, ay);
+            if (ia < niters && is_full(ia)) load_full(ia, ax, ay);
         }
-        if (ibb != kNoIter) {
-            unsigned nb2 = claim();
-            if (!valid_it(nb2)) nb2 = kNoIter;
+        if (ibb < niters) {
+            const unsigned nb2 = claim();
             run(ibb, bx, by);
             publish(nb2);
             ibb = nb2;
-            if (ibb != kNoIter && is_full(ibb)) load_full(ibb, bx, by);
+            if (ibb < niters && is_full(ibb)) load_full(ibb, bx, by);
         }
     }
     PASS_TRACE(io, 1);
@@ -2106,16 +2053,6 @@ bool knn_pass_fuses_range(uint64_t n) {
     return ch <= 64ull * kFusedMaskWords && n < (1ull << 30);
 }
 
-// arrival-ticket groups of the kNN pass (2-level counter; GEOHIP_KNN_GROUPS: measurement A/B only)
-static unsigned knn_ticket_groups() {
-    static const unsigned g = [] {
-        const char* e = getenv("GEOHIP_KNN_GROUPS");
-        const int v = e ? atoi(e) : 16;
-        return (unsigned)(v >= 1 && v <= (int)kMaxTicketGroups ? v : 16);
-    }();
-    return g;
-}
-
 hipError_t launch_knn_pass(const double* x, const double* y, uint64_t n, const KnnArgs& args,
                            unsigned long long* list_d, unsigned* list_i, unsigned long long* spill_d, unsigned* spill_i,
                            unsigned* ctr, double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st,
@@ -2134,7 +2071,7 @@ hipError_t launch_knn_pass(const double* x, const double* y, uint64_t n, const K
     const size_t lists = (size_t)nblocks * cap;
     // list entries, then the packed heads, then the list lengths (in the index array)
     const PassIo io{list_d, list_i, cap, list_d + lists, list_i + lists, list_i + lists + (size_t)kPassHeads * nblocks,
-                    spill_d, nullptr, spill_i, ctr, out_d, out_i, out_count, knn_ticket_groups(), trace};
+                    spill_d, nullptr, spill_i, ctr, out_d, out_i, out_count, 16u, trace};
     PassRangeIo rio;
     memset(&rio, 0, sizeof rio);
     // ev0 / ev1 (timing on): stamped by the kernel's own dispatch begin / end

@@ -145,6 +145,23 @@ def torch_band_pack_query(grid_data, qx: float, qy: float, r: float):
     return torch_band_pack(grid_data, keep)
 
 
+def _exchange_records(px, py, pg, send_counts, group):
+    """The key-band shuffle: counts exchanged on the device and read once (the only host round
+    trip -- all_to_all needs the split sizes), then x, y and the window index as one [m, 3] fp64
+    record array in a single all_to_all.  Returns the owner's (x, y, window idx)."""
+    import torch
+
+    recv_counts = torch.empty_like(send_counts)
+    all_to_all(recv_counts, send_counts, group=group)
+    both = torch.stack([send_counts, recv_counts]).cpu().tolist()
+    sc, rc = both[0], both[1]
+    nrecv, nsend = sum(rc), sum(sc)
+    rec = torch.stack([px[:nsend], py[:nsend], pg[:nsend].view(torch.float64)], dim=1).contiguous()
+    got = torch.empty((nrecv, 3), dtype=torch.float64, device=rec.device)
+    all_to_all(got, rec, rc, sc, group)
+    return got[:, 0].contiguous(), got[:, 1].contiguous(), got[:, 2].contiguous().view(torch.int64)
+
+
 def knn_range_cells(x_local, y_local, base: int, qx: float, qy: float, r: float, k: int, approximate: bool = False,
                     *, grid, ctx=None, group=None, band_pack: Optional[Callable] = None,
                     local: Optional[Callable] = None, merge: Optional[Callable] = None):
@@ -169,25 +186,22 @@ def knn_range_cells(x_local, y_local, base: int, qx: float, qy: float, r: float,
         local = _device_local_knn_range(ctx, grid)
     if merge is None:
         merge = _device_merge(ctx)
-    px, py, pg, send_counts = band_pack(x_local, y_local, base, nb, world)
-    if world > 1:
-        recv_counts = torch.empty_like(send_counts)
-        all_to_all(recv_counts, send_counts, group=group)
-        sc, rc = send_counts.tolist(), recv_counts.tolist()
-        nrecv, nsend = sum(rc), sum(sc)
-
-        def exchange(t):
-            out = torch.empty(nrecv, dtype=t.dtype, device=t.device)
-            all_to_all(out, t[:nsend], rc, sc, group)
-            return out
-
-        rx, ry, rg = exchange(px), exchange(py), exchange(pg)
+    if world == 1:
+        # one owner holds every key band: the filter + keyBy shuffle is the identity (the local
+        # kernel applies the G u C filter itself), so the shard is evaluated where it lies
+        rx, ry = x_local, y_local
+        rg = None
+        nrecv = len(x_local)
     else:
-        nrecv = int(send_counts.sum().item())
-        rx, ry, rg = px[:nrecv].contiguous(), py[:nrecv].contiguous(), pg[:nrecv]
+        px, py, pg, send_counts = band_pack(x_local, y_local, base, nb, world)
+        rx, ry, rg = _exchange_records(px, py, pg, send_counts, group)
+        nrecv = len(rx)
     li, ld, lh = local(rx, ry, qx, qy, r, k, approximate)
     li64 = li.to(torch.int64)
-    gi = torch.where(li64 >= 0, rg[li64.clamp(min=0)] if nrecv else li64, torch.full_like(li64, -1)).to(torch.int32)
+    if rg is None:
+        gi = torch.where(li64 >= 0, li64 + base, torch.full_like(li64, -1)).to(torch.int32)
+    else:
+        gi = torch.where(li64 >= 0, rg[li64.clamp(min=0)] if nrecv else li64, torch.full_like(li64, -1)).to(torch.int32)
     all_d = torch.empty((world, k), dtype=ld.dtype, device=ld.device)
     all_i = torch.empty((world, k), dtype=torch.int32, device=ld.device)
     if world > 1:
@@ -198,7 +212,10 @@ def knn_range_cells(x_local, y_local, base: int, qx: float, qy: float, r: float,
         all_i[0] = gi
     mi, md = merge(all_d, all_i, k)
     count = int((mi != -1).sum().item())
-    hits = rg[lh.to(torch.int64)] if len(lh) else torch.zeros(0, dtype=torch.int64, device=ld.device)
+    if rg is None:
+        hits = lh.to(torch.int64) + base
+    else:
+        hits = rg[lh.to(torch.int64)] if len(lh) else torch.zeros(0, dtype=torch.int64, device=ld.device)
     offset, total = gather_counts(len(hits), hits.device, group)
     return KnnResult(mi[:count], md[:count], count), (hits, offset, total), nrecv
 
@@ -232,17 +249,7 @@ def join_sharded(dx_local, dy_local, dbase: int, qx, qy, r: float, approximate: 
         if band_pack is None:
             band_pack = _device_band_pack(ctx, grid_data)
         px, py, pg, send_counts = band_pack(dx_local, dy_local, dbase, nb, world)
-        recv_counts = torch.empty_like(send_counts)
-        all_to_all(recv_counts, send_counts, group=group)
-        sc, rc = send_counts.tolist(), recv_counts.tolist()
-        nrecv, nsend = sum(rc), sum(sc)
-
-        def exchange(t):
-            out = torch.empty(nrecv, dtype=t.dtype, device=t.device)
-            all_to_all(out, t[:nsend], rc, sc, group)
-            return out
-
-        rx, ry, rg = exchange(px), exchange(py), exchange(pg)
+        rx, ry, rg = _exchange_records(px, py, pg, send_counts, group)
         lo, hi = key_band(world, rank, nb)
         lq = float(grid_query.cell_len)
         qcx = _java_cell(qx, grid_query.min_x, lq)
