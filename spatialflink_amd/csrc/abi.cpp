@@ -126,6 +126,9 @@ struct geohip_ctx {
     bool stg_used[2] = {false, false};
     std::unique_ptr<CopyPool> copy_pool;
     hipEvent_t switch_ev = nullptr;  // orders a stream rebinding after the old stream's work
+    // side stream of a step's independent chain (ctx_fork / ctx_join): created on first use
+    hipStream_t side = nullptr;
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
     void* pcache = nullptr;          // point-polygon plan cache (cell_kernels.hip owns the type)
     void* kcache = nullptr;          // point-polygon kNN polygon cache (cell_kernels.hip owns the type)
 };
@@ -670,6 +673,12 @@ int geohip_ctx_destroy(geohip_ctx* ctx) {
     }
     if (ctx->cstream) hipStreamDestroy(ctx->cstream);
     if (ctx->switch_ev) hipEventDestroy(ctx->switch_ev);
+    if (ctx->side) {
+        hipStreamSynchronize(ctx->side);
+        hipStreamDestroy(ctx->side);
+    }
+    if (ctx->fork_ev) hipEventDestroy(ctx->fork_ev);
+    if (ctx->join_ev) hipEventDestroy(ctx->join_ev);
     if (ctx->own) hipStreamDestroy(ctx->own);
     delete ctx;
     return GEOHIP_OK;
@@ -1270,6 +1279,25 @@ int ctx_cus(geohip_ctx* ctx) { return ctx->cus; }
 
 int ctx_begin(geohip_ctx* ctx) { return begin(ctx); }
 hipStream_t ctx_stream(geohip_ctx* ctx) { return ctx->stream; }
+// Fork: work enqueued on *side after this call runs after everything enqueued on the ctx stream so
+// far, concurrently with what follows there; ctx_join orders the ctx stream after it again.
+int ctx_fork(geohip_ctx* ctx, hipStream_t* side) {
+    if (!ctx->side) {
+        if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ctx->join_ev, hipEventDisableTiming) != hipSuccess)
+            return fail(ctx, GEOHIP_ERR_DEVICE, "side stream creation failed");
+    }
+    if (hipEventRecord(ctx->fork_ev, ctx->stream) != hipSuccess || hipStreamWaitEvent(ctx->side, ctx->fork_ev, 0) != hipSuccess)
+        return fail(ctx, GEOHIP_ERR_DEVICE, "side stream fork failed");
+    *side = ctx->side;
+    return GEOHIP_OK;
+}
+int ctx_join(geohip_ctx* ctx) {
+    if (hipEventRecord(ctx->join_ev, ctx->side) != hipSuccess || hipStreamWaitEvent(ctx->stream, ctx->join_ev, 0) != hipSuccess)
+        return fail(ctx, GEOHIP_ERR_DEVICE, "side stream join failed");
+    return GEOHIP_OK;
+}
 int ctx_mem(geohip_ctx* ctx) { return ctx->mem; }
 uint64_t* ctx_pinned(geohip_ctx* ctx) { return ctx->pinned; }
 void** ctx_pcache_slot(geohip_ctx* ctx) { return &ctx->pcache; }

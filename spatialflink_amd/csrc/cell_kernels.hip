@@ -979,11 +979,9 @@ __device__ __forceinline__ unsigned block_scan_passes(unsigned n, unsigned* wsum
 }
 
 // Tile starts and cursors from the tile counts (one block; re-zeroes the counts for the next
-// launch).  Also zeroes the join's per-call counters (the query list counts and cursors, the
-// error / ticket words, the pair total): one launch instead of five memsets.
-__global__ __launch_bounds__(kBinThreads) void jb_scan(JBin a, unsigned* __restrict__ zero, unsigned nzero) {
+// launch).
+__global__ __launch_bounds__(kBinThreads) void jb_scan(JBin a) {
     __shared__ unsigned wsum[kScanPasses * (kBinThreads / kWave)];
-    for (unsigned t = threadIdx.x; t < nzero; t += kBinThreads) zero[t] = 0u;
     const unsigned total = block_scan_passes(
         a.g.ntiles, wsum, [&](unsigned t) { return a.tcnt[t]; },
         [&](unsigned t, unsigned, unsigned ex) {
@@ -1587,272 +1585,6 @@ __global__ __launch_bounds__(kTB) void join_fused(JoinRun a) {
             if (sc) jstage_flush(a, st, sc, pos);
         }
         __syncthreads();  // every wave leaves the item together (LDS reuse, uniform loop)
-    }
-}
-
-// ---- join write pass: decision waves and store waves ------------------------------------
-// On gfx9 a wave's load wait also waits for every store the wave issued before that load
-// (one in-order vmcnt), so a wave that both decides (loads) and stores pairs alternates between
-// the two: the one-role write pass measured 1.03 ms against 0.47 ms with its stores removed and
-// 0.65 ms for the pair bytes alone at the measured store rate.  Here each workgroup has kJCW
-// decision waves that never store to global memory and kJEW store waves that never load from it:
-// the decision waves classify, count and keep the decisions of item g in LDS set g % 2 (the
-// chunks' window indices and in-box ballots, the PART hit ballots, the query lists), reserve the
-// item's output run and hand the set over; the store waves turn the set into pairs while the
-// decision waves work on item g + 1.  The roles synchronise through LDS counters only (the
-// decision waves' barrier included), so neither role waits on the other's memory traffic.
-#ifndef GEOHIP_JOIN_PIPE
-#define GEOHIP_JOIN_PIPE 0  // 1: the two-role write pass (measured slower with LDS-staged emission)
-#endif
-constexpr int kJCW = kTB / kWave;           // decision waves (the classification's 256 threads)
-constexpr int kJEW = 2;                     // store waves (each the chunks of kJCW / kJEW decision waves)
-constexpr int kJPipeThreads = (kJCW + kJEW) * kWave;
-constexpr unsigned kJPipeBlocks = 512;      // 2 per CU (55 KB LDS)
-
-struct JSet {
-    unsigned lall[kJQ];
-    unsigned lpq[kJQ + 4];
-    ulonglong2 mask[kJCW][kJCh][kJQ / 2];
-    unsigned pid[kJCW][kJCh][kWave];
-    unsigned long long vm[kJCW][kJCh];
-    unsigned long long wcnt[kJCW];
-    unsigned long long base;
-    unsigned nall, npart, nch;
-};
-
-__device__ __forceinline__ unsigned lds_peek(const unsigned* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// this wave's LDS operations done, then +1 (relaxed: no global-memory fence, which would wait
-// for the store waves' pair stores)
-__device__ __forceinline__ void lds_signal(unsigned* p) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane_id() == 0) __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_wait_geq(const unsigned* p, unsigned target) {
-    while (lds_peek(p) < target) __builtin_amdgcn_s_sleep(1);
-    asm volatile("" ::: "memory");
-}
-
-template <bool APPROX>
-__global__ __launch_bounds__(kJPipeThreads) void join_pipe(JoinRun a) {
-    __shared__ JSet set[2];
-    __shared__ JPart lpr[kJQ + 4];
-    __shared__ jf2 lpb[kJQ + 4];
-    __shared__ uint2 stage[kJEW][kJStage];
-    __shared__ unsigned c_bar, produced, done, sh_item, sh_amax, sh_wc[2][kJCW];
-    __shared__ unsigned consumed[kJEW];  // items emitted, per store wave (they run at their own pace)
-    const int wid = threadIdx.x / kWave, lane = lane_id();
-    if (threadIdx.x == 0) {
-        c_bar = 0;
-        produced = 0;
-        for (int e = 0; e < kJEW; e++) consumed[e] = 0;
-        done = 0;
-    }
-    __syncthreads();  // the only workgroup barrier: below, each role waits on LDS counters
-    if (wid >= kJCW) {
-        // ---------------- store waves: no global loads
-        const int e = wid - kJCW;
-        uint2* st = stage[e];
-        for (unsigned g = 0;; g++) {
-            while (lds_peek(&produced) <= g) {
-                if (lds_peek(&done) && lds_peek(&produced) <= g) return;
-                __builtin_amdgcn_s_sleep(1);
-            }
-            asm volatile("" ::: "memory");
-            const JSet& S = set[g & 1];
-            const unsigned nall = S.nall, npart = S.npart, nch = S.nch;
-            for (int cw = e * (kJCW / kJEW); cw < (e + 1) * (kJCW / kJEW); cw++) {
-                unsigned long long pos = S.base;
-                for (int w = 0; w < cw; w++) pos += S.wcnt[w];
-                if (S.wcnt[cw] == 0) continue;
-                unsigned sc = 0;
-#pragma unroll
-                for (unsigned k = 0; k < kJCh; k++) {
-                    const unsigned c = (unsigned)cw + k * kJCW;
-                    if (c >= nch) continue;
-                    jemit_chunk(a, S.vm[cw][k], S.pid[cw][k][lane], S.lall, nall, S.lpq, npart, S.mask[cw][k], st, sc,
-                                pos);
-                }
-                if (sc) jstage_flush(a, st, sc, pos);
-            }
-            lds_signal(&consumed[e]);  // the set's reads are done (in-order LDS)
-        }
-    }
-    // ---------------- decision waves: no global stores
-    const unsigned nitems = a.istart[a.ntiles];
-    const unsigned gq = *a.gcnt;
-    const TileGeom& g = a.geo;
-    const double slack = 0x1.0p-30 * (__builtin_fabs(g.mnx) + __builtin_fabs(g.mny) + ((double)g.nb + 2.0) * g.l);
-    unsigned phase = 0;
-    auto cbar = [&]() {  // barrier of the decision waves
-        phase += kJCW;
-        lds_signal(&c_bar);
-        lds_wait_geq(&c_bar, phase);
-    };
-    for (unsigned gi = 0;; gi++) {
-        if (threadIdx.x == 0) {
-            sh_item = atomicAdd(a.ticket, 1u);
-            sh_amax = 0;
-        }
-        cbar();
-        const unsigned it = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_peek(&sh_item));
-        if (it >= nitems) break;
-        JSet& S = set[gi & 1];
-        if (gi >= 2)  // item gi - 2 emitted by every store wave: its set is free
-            for (int e = 0; e < kJEW; e++) lds_wait_geq(&consumed[e], gi - 1);
-        const uint2 d = a.items[it];
-        const unsigned tile = d.x;
-        const unsigned qs = a.qstart[tile], nql = a.qstart[tile + 1] - qs, nqt = nql + gq;
-        const unsigned nqc = (nqt + kJQ - 1) / kJQ;
-        const unsigned pc = d.y / nqc, qc = d.y - pc * nqc;
-        const unsigned ds = a.tstart[tile] + pc * kJP;
-        const unsigned de0 = a.tstart[tile + 1];
-        const unsigned de = ds + kJP < de0 ? ds + kJP : de0;
-        const unsigned q0 = qc * kJQ;
-        const unsigned nbq = nqt - q0 < kJQ ? nqt - q0 : kJQ;
-        const int32_t tx = (int32_t)(tile / (unsigned)g.nt), ty = (int32_t)(tile % (unsigned)g.nt);
-        const int32_t X0 = tx * g.ts, Y0 = ty * g.ts;
-        const int32_t X1 = X0 + g.ts - 1 < g.nb - 1 ? X0 + g.ts - 1 : g.nb - 1;
-        const int32_t Y1 = Y0 + g.ts - 1 < g.nb - 1 ? Y0 + g.ts - 1 : g.nb - 1;
-        const double ox = g.mnx + (double)X0 * g.l, oy = g.mny + (double)Y0 * g.l;
-        const double bx0 = ox - slack, by0 = oy - slack;
-        const double bx1 = g.mnx + (double)(X1 + 1) * g.l + slack, by1 = g.mny + (double)(Y1 + 1) * g.l + slack;
-        // the wave's records, in flight during the classification
-        const unsigned nch = (de - ds + 63) / 64;
-        uint4 rk[kJCh];
-#pragma unroll
-        for (unsigned k = 0; k < kJCh; k++) {
-            const unsigned c = (unsigned)wid + k * kJCW;
-            const unsigned i = ds + c * 64 + (unsigned)lane;
-            rk[k] = make_uint4(0u, 0u, 0u, 0u);
-            if (c < nch && i < de) rk[k] = a.recs[i];
-        }
-        // 1. classify the item's queries (as join_fused)
-        int cls = 0;
-        unsigned q = 0;
-        QRect R{1, 0, 1, 0};
-        double qxv = 0.0, qyv = 0.0;
-        if (threadIdx.x < nbq) {
-            const unsigned t = q0 + threadIdx.x;
-            q = t < nql ? a.qlist[qs + t] : a.glist[t - nql];
-            R = a.rect[q];
-            qxv = a.qx[q];
-            qyv = a.qy[q];
-            const bool inter = R.x0 <= R.x1 && R.y0 <= R.y1 && R.x0 <= X1 && R.x1 >= X0 && R.y0 <= Y1 && R.y1 >= Y0;
-            const bool cover = R.x0 <= X0 && R.x1 >= X1 && R.y0 <= Y0 && R.y1 >= Y1;
-            if (APPROX) {
-                cls = !inter ? 0 : (cover ? 1 : 2);
-            } else if (inter) {
-                const double ex0 = __builtin_fmax(__builtin_fmax(bx0 - qxv, qxv - bx1), 0.0);
-                const double ey0 = __builtin_fmax(__builtin_fmax(by0 - qyv, qyv - by1), 0.0);
-                const double dmin2 = ex0 * ex0 + ey0 * ey0;
-                const double ex1 = __builtin_fmax(__builtin_fabs(qxv - bx0), __builtin_fabs(qxv - bx1));
-                const double ey1 = __builtin_fmax(__builtin_fabs(qyv - by0), __builtin_fabs(qyv - by1));
-                const double dmax2 = ex1 * ex1 + ey1 * ey1;
-                if (dmin2 * (1.0 - 0x1.0p-40) > a.r2hi) cls = 0;
-                else if (cover && dmax2 * (1.0 + 0x1.0p-40) < a.r2lo) cls = 1;
-                else cls = 2;
-            }
-        }
-        {
-            const unsigned long long ma = __ballot(cls == 1), mp = __ballot(cls == 2);
-            if (lane == 0) {
-                sh_wc[0][wid] = (unsigned)__popcll(ma);
-                sh_wc[1][wid] = (unsigned)__popcll(mp);
-            }
-            cbar();
-            unsigned ba = 0, bp = 0, ta = 0, tp = 0;
-            for (int w = 0; w < kJCW; w++) {
-                if (w < wid) {
-                    ba += sh_wc[0][w];
-                    bp += sh_wc[1][w];
-                }
-                ta += sh_wc[0][w];
-                tp += sh_wc[1][w];
-            }
-            if (cls == 1) S.lall[ba + lanes_below(ma)] = q;
-            if (cls == 2) {
-                const unsigned k = bp + lanes_below(mp);
-                S.lpq[k] = q;
-                lpr[k] = JPart{R.x0, R.x1 - R.x0, R.y0, R.y1 - R.y0};
-                const float fx = (float)(qxv - ox), fy = (float)(qyv - oy);
-                lpb[k] = jf2{fx, fy};
-                const float m = __builtin_fmaxf(__builtin_fabsf(fx), __builtin_fabsf(fy));
-                atomicMax(&sh_amax, m == m ? __float_as_uint(m) : 0x7f800000u);  // NaN -> no fp32 screen
-            }
-            if (threadIdx.x == 0) {
-                S.nall = ta;
-                S.npart = tp;
-                S.nch = nch;
-                for (unsigned u = tp; u < tp + 4; u++) {  // padding: never inside
-                    lpr[u] = JPart{INT32_MAX, 0, INT32_MAX, 0};
-                    lpb[u] = jf2{0.f, 0.f};
-                    S.lpq[u] = 0;
-                }
-            }
-        }
-        cbar();
-        const unsigned nall = S.nall, npart = S.npart;
-        float lo = -1.0f, hi = __builtin_inff();
-        if (!APPROX) {
-            const double pa = (bx1 - bx0) + (by1 - by0);
-            const double A = pa + 2.0 * (double)__uint_as_float(lds_peek(&sh_amax)) * (1.0 + 0x1.0p-20);
-            const double e = 2.05 * 0x1.0p-24 * A;
-            const double err = 4.0 * e * A + 2.0 * e * e;
-            if (err == err && err < 0x1.0p100) {
-                if (a.r2lo > 0.0) {
-                    const double l = (a.r2lo - err) * (1.0 - 0x1.0p-21);
-                    lo = l > 0.0 ? __double2float_rd(l) : -1.0f;
-                }
-                if (a.r2hi < 0x1.0p100) hi = __double2float_ru((a.r2hi + err) * (1.0 + 0x1.0p-21));
-            } else {
-                lo = -1.0f;
-                hi = __builtin_nanf("");
-            }
-        }
-        // 2. count, keeping every decision in the set
-        unsigned long long cnt = 0;
-#pragma unroll
-        for (unsigned k = 0; k < kJCh; k++) {
-            const unsigned c = (unsigned)wid + k * kJCW;
-            if (c >= nch) continue;
-            const unsigned i = ds + c * 64 + (unsigned)lane;
-            const bool valid = i < de;
-            float ax = 0.f, ay = 0.f;
-            unsigned pid = 0;
-            int32_t cx = -1, cy = -1;
-            if (valid) jrec_load(rk[k], X0, Y0, ax, ay, pid, cx, cy);
-            const bool in_box = valid && (APPROX || (ax == ax && ay == ay));
-            const unsigned long long vm = __ballot(in_box);
-            S.pid[wid][k][lane] = pid;
-            if (lane == 0) S.vm[wid][k] = vm;
-            cnt += (unsigned long long)nall * (unsigned)__popcll(vm);
-            for (unsigned j = 0; j < npart; j += 4) {
-                unsigned long long m[4];
-                jpart_quad<APPROX>(a, lpr, lpb, S.lpq, j, cx, cy, ax, ay, pid, lo, hi, m);
-                if (lane == 0) {
-                    S.mask[wid][k][j / 2] = make_ulonglong2(m[0], m[1]);
-                    S.mask[wid][k][j / 2 + 1] = make_ulonglong2(m[2], m[3]);
-                }
-                cnt += (unsigned)(__popcll(m[0]) + __popcll(m[1]) + __popcll(m[2]) + __popcll(m[3]));
-            }
-        }
-        if (lane == 0) S.wcnt[wid] = cnt;
-        cbar();
-        // 3. the item's output run, then the hand-over
-        if (wid == 0) {
-            unsigned long long tot = 0;
-            for (int w = 0; w < kJCW; w++) tot += S.wcnt[w];
-            unsigned long long b = 0;
-            if (lane == 0 && tot) b = atomicAdd(a.total, tot);
-            if (lane == 0) S.base = b;
-            lds_signal(&produced);
-        }
-    }
-    if (wid == 0) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_store(&done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 }
 
@@ -4180,10 +3912,10 @@ int bin_tiles(geohip_ctx* ctx, Scratch& S, const double* dx, const double* dy, u
     return GEOHIP_OK;
 }
 
-// Join binning (jb_bands / jb_scan / jb_tiles): the window's in-grid points as tile-sorted
-// 16-B records; *recs and *tstart (ntiles + 1) on the device.  jb_scan also zeroes zero[nzero).
+// Join binning (jb_bands / jb_scan / jb_segs / jb_tiles): the window's in-grid points as
+// tile-sorted 16-B records; *recs and *tstart (ntiles + 1) on the device.
 int join_bin(geohip_ctx* ctx, Scratch& S, const double* dx, const double* dy, uint64_t n, const TileGeom& geo,
-             const uint4** recs, const unsigned** tstart, unsigned* zero, unsigned nzero) {
+             const uint4** recs, const unsigned** tstart) {
     hipStream_t st = ctx_stream(ctx);
     uint64_t nblk = (n + 16383) / 16384;
     if (nblk > kJbBlocks) nblk = kJbBlocks;
@@ -4219,7 +3951,7 @@ int join_bin(geohip_ctx* ctx, Scratch& S, const double* dx, const double* dy, ui
     if (rc) return rc;
     a.tcnt = reinterpret_cast<unsigned*>(tc);
     if (n) jb_bands<<<(unsigned)nblk, kBinThreads, 0, st>>>(a);
-    jb_scan<<<1, kBinThreads, 0, st>>>(a, zero, nzero);
+    jb_scan<<<1, kBinThreads, 0, st>>>(a);
     if (n) {
         jb_segs<<<a.nbands, kBinThreads, 0, st>>>(a);
         jb_tiles<<<(unsigned)std::min<uint64_t>(kJbL2Blocks, maxround), kJbL2Threads, 0, st>>>(a);
@@ -4296,7 +4028,7 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
     const uint64_t qpt = global_mode ? nq : std::min<uint64_t>(nq, list_cap);
     const uint64_t item_cap = ((nd + kJP - 1) / kJP + ntl) * ((qpt + kJQ - 1) / kJQ) + 1;
     QRect* drect = S.get<QRect>(J_RECT, nq * sizeof(QRect) + 16);
-    // per-call counters, zeroed by one launch (jb_scan): query counts | query cursors | misc words
+    // per-call counters, zeroed by one launch (fill_words): query counts | query cursors | misc words
     // ([0] jq_rect error, [4] ticket, [5] global query count) | the pair total (u64)
     const unsigned nzero = (unsigned)(2 * (ntl + 1) + kMiscWords + 2 + 1) & ~1u;
     unsigned* zero = S.get<unsigned>(J_QCNT, (size_t)nzero * 4 + 16);
@@ -4313,24 +4045,32 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
     hipEvent_t e0, e1;
     ctx_timing_events(ctx, &e0, &e1);
     if (e0) hipEventRecord(e0, st);  // the whole device step: binning, replication, join
-    const uint4* recs = nullptr;
-    const unsigned* tstart = nullptr;
-    rc = join_bin(ctx, S, ddx, ddy, nd, geo, &recs, &tstart, zero, nzero);
+    // the query side (counters zeroed, query blocks, per-tile lists) on the ctx's side stream,
+    // concurrently with the data binning; the join waits for both
+    hipStream_t qs = nullptr;
+    rc = ctx_fork(ctx, &qs);
     if (rc) return rc;
+    fill_words<<<(nzero + kTB - 1) / kTB, kTB, 0, qs>>>(zero, nzero, 0u);
     const unsigned qb = (unsigned)((nq + kTB - 1) / kTB);
     if (nq) {
         JqGeom jg{gq->min_x, gq->min_y, gq->cell_len, nb, lc, all_cells ? 1 : 0};
-        jq_rect<<<qb, kTB, 0, st>>>(dqx, dqy, nq, jg, drect, misc);
+        jq_rect<<<qb, kTB, 0, qs>>>(dqx, dqy, nq, jg, drect, misc);
     }
     if (global_mode) {
-        if (nq) jq_global<<<qb, kTB, 0, st>>>(nq, glist, misc + 5);
-        jq_starts<<<1, kBinThreads, 0, st>>>(qcnt, geo.ntiles, qstart);  // all zero: no per-tile lists
+        if (nq) jq_global<<<qb, kTB, 0, qs>>>(nq, glist, misc + 5);
+        jq_starts<<<1, kBinThreads, 0, qs>>>(qcnt, geo.ntiles, qstart);  // all zero: no per-tile lists
     } else {
         const unsigned qg = (unsigned)((nq + kTB / kWave - 1) / (kTB / kWave));  // one wave per query
-        if (nq) jq_build<false><<<qg, kTB, 0, st>>>(drect, nq, geo, qcnt, nullptr, nullptr);
-        jq_starts<<<1, kBinThreads, 0, st>>>(qcnt, geo.ntiles, qstart);
-        if (nq) jq_build<true><<<qg, kTB, 0, st>>>(drect, nq, geo, qcur, qstart, qlist);
+        if (nq) jq_build<false><<<qg, kTB, 0, qs>>>(drect, nq, geo, qcnt, nullptr, nullptr);
+        jq_starts<<<1, kBinThreads, 0, qs>>>(qcnt, geo.ntiles, qstart);
+        if (nq) jq_build<true><<<qg, kTB, 0, qs>>>(drect, nq, geo, qcur, qstart, qlist);
     }
+    const uint4* recs = nullptr;
+    const unsigned* tstart = nullptr;
+    rc = join_bin(ctx, S, ddx, ddy, nd, geo, &recs, &tstart);
+    if (rc) return rc;
+    rc = ctx_join(ctx);
+    if (rc) return rc;
     join_plan<<<1, kBinThreads, 0, st>>>(tstart, qstart, misc + 5, geo.ntiles, istart);
     join_item_fill<<<(unsigned)((ntl + kTB - 1) / kTB), kTB, 0, st>>>(istart, geo.ntiles, items);
     // output: device pointer directly, or a device staging buffer for host output
@@ -4352,12 +4092,10 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
                misc + 4, total, out, out ? cap : 0, ((uintptr_t)out & 7u) == 0};
     if (nq && nd) {
         if (approximate) {
-            if (write && GEOHIP_JOIN_PIPE) join_pipe<true><<<kJPipeBlocks, kJPipeThreads, 0, st>>>(jr);
-            else if (write) join_fused<true, true><<<kJBlocksW, kTB, 0, st>>>(jr);
+            if (write) join_fused<true, true><<<kJBlocksW, kTB, 0, st>>>(jr);
             else join_fused<true, false><<<kJBlocksC, kTB, 0, st>>>(jr);
         } else {
-            if (write && GEOHIP_JOIN_PIPE) join_pipe<false><<<kJPipeBlocks, kJPipeThreads, 0, st>>>(jr);
-            else if (write) join_fused<false, true><<<kJBlocksW, kTB, 0, st>>>(jr);
+            if (write) join_fused<false, true><<<kJBlocksW, kTB, 0, st>>>(jr);
             else join_fused<false, false><<<kJBlocksC, kTB, 0, st>>>(jr);
         }
     }

@@ -21,6 +21,8 @@ int ctx_lookback_status(geohip_ctx* ctx, int slot, size_t bytes, void** out, uns
 int ctx_cus(geohip_ctx* ctx);                       // compute units of the ctx's device
 int ctx_begin(geohip_ctx* ctx);  // clears the error, selects the ctx's device
 hipStream_t ctx_stream(geohip_ctx* ctx);
+int ctx_fork(geohip_ctx* ctx, hipStream_t* side);  // a side stream ordered after the ctx stream's work so far
+int ctx_join(geohip_ctx* ctx);                     // the ctx stream ordered after the side stream's work
 int ctx_mem(geohip_ctx* ctx);
 uint64_t* ctx_pinned(geohip_ctx* ctx);
 void ctx_timing_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1);      // a step of several launches
