@@ -1074,9 +1074,24 @@ __device__ __forceinline__ unsigned long long spread32(unsigned v) {  // bit b -
 // words' hit counts) stored in ascending index order from output position obase: the wave walks
 // only the nonzero words (ballot + find-first-set) and each word's hits go out from its lanes at
 // consecutive positions (coalesced for dense words; sparse words cost one step each).
-__device__ __forceinline__ void emit_words(unsigned long long mine, unsigned ex, unsigned long long obase,
-                                           unsigned first_point, unsigned* __restrict__ out,
+// Hits of 64 mask words (lane l holds word l, first point first_point) in ascending order from
+// output position obase (advanced): each word's hits go to the wave's LDS stage (one ds_write per
+// word), and the stage leaves as full 64-lane stores when it fills and at the end (emit_flush).
+// One store instruction per word straight from the bits (partial waves, ~14 lanes for C1) made
+// the emission store-issue-bound: ~8 us of the range pass's tail.
+constexpr unsigned kEmitStage = 512;  // u32 entries per wave (the wave's idle candidate stage)
+static_assert(kEmitStage * 4 <= kCandCap * 8, "the emission stage fits a wave's candidate stage");
+__device__ __forceinline__ void emit_flush(unsigned* stg, unsigned& sc, unsigned long long& obase, unsigned* __restrict__ out,
                                            unsigned long long cap) {
+    wave_lds_sync();
+    for (unsigned t = (unsigned)lane_id(); t < sc; t += kWave)
+        if (obase + t < cap) out[obase + t] = stg[t];
+    wave_lds_sync();
+    obase += sc;
+    sc = 0;
+}
+__device__ __forceinline__ void emit_words(unsigned long long mine, unsigned first_point, unsigned* stg, unsigned& sc,
+                                           unsigned long long& obase, unsigned* __restrict__ out, unsigned long long cap) {
     const int lane = lane_id();
     unsigned long long nz = __ballot(mine != 0ull);
     while (nz) {
@@ -1085,11 +1100,9 @@ __device__ __forceinline__ void emit_words(unsigned long long mine, unsigned ex,
         const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)mine, j);
         const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(mine >> 32), j);
         const unsigned long long bits = ((unsigned long long)hi << 32) | lo;
-        const unsigned pj = (unsigned)__builtin_amdgcn_readlane((int)ex, j);
-        if ((bits >> lane) & 1ull) {
-            const unsigned long long pos = obase + pj + lanes_below(bits);
-            if (pos < cap) out[pos] = first_point + (unsigned)j * 64u + (unsigned)lane;
-        }
+        if ((bits >> lane) & 1ull) stg[sc + lanes_below(bits)] = first_point + (unsigned)j * 64u + (unsigned)lane;
+        sc += (unsigned)__popcll(bits);
+        if (sc > kEmitStage - kWave) emit_flush(stg, sc, obase, out, cap);
     }
 }
 
@@ -1116,7 +1129,7 @@ __device__ __forceinline__ void pass_range_publish(const PassRangeIo& rio, const
 template <int NW>
 __device__ __forceinline__ void pass_range_emit(const PassRangeIo& rio, const unsigned long long* bmask,
                                                 unsigned* wsum, unsigned& bcount, unsigned long long& excl_sh,
-                                                unsigned vb, uint64_t p0, uint64_t p1) {
+                                                unsigned vb, uint64_t p0, uint64_t p1, unsigned* stg) {
     const int lane = lane_id(), wid = threadIdx.x / kWave;
     const unsigned nw = p1 > p0 ? (unsigned)((p1 - p0 + 63) / 64) : 0u;
     if (wid == 0) {
@@ -1138,13 +1151,12 @@ __device__ __forceinline__ void pass_range_emit(const PassRangeIo& rio, const un
     unsigned long long obase = excl_sh;
     for (int w = 0; w < wid; w++) obase += wsum[w];
     const unsigned ibase = (unsigned)p0;
+    unsigned sc = 0;
     for (unsigned w0 = wb; w0 < we; w0 += kWave) {
         const unsigned long long mine = w0 + lane < we ? bmask[w0 + lane] : 0ull;
-        const unsigned cc = (unsigned)__popcll(mine);
-        const unsigned incl = wave_incl_scan(cc);
-        emit_words(mine, incl - cc, obase, ibase + w0 * 64u, rio.out, rio.cap);
-        obase += (unsigned)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+        emit_words(mine, ibase + w0 * 64u, stg, sc, obase, rio.out, rio.cap);
     }
+    if (sc) emit_flush(stg, sc, obase, rio.out, rio.cap);
     if (threadIdx.x == 0 && vb == gridDim.x - 1) *rio.total = excl_sh + bcount;
     if (rio.trace && threadIdx.x == 0) rio.trace[16 * (size_t)blockIdx.x + 6] = __builtin_amdgcn_s_memrealtime();
 }
@@ -1582,7 +1594,8 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
     __syncthreads();
     PASS_TRACE(io, 4);
     if (kb.last == 0) {
-        if (RANGE) pass_range_emit<NW>(rio, rmask, rwsum, rcount, rexcl, vb, blk_begin, blk_end);
+        if (RANGE)
+            pass_range_emit<NW>(rio, rmask, rwsum, rcount, rexcl, vb, blk_begin, blk_end, reinterpret_cast<unsigned*>(st.cx));
         return;
     }
     if (threadIdx.x == 0) {
@@ -1608,7 +1621,7 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
     PASS_TRACE(io, 7);
     if (RANGE) {
         __syncthreads();
-        pass_range_emit<NW>(rio, rmask, rwsum, rcount, rexcl, vb, blk_begin, blk_end);
+        pass_range_emit<NW>(rio, rmask, rwsum, rcount, rexcl, vb, blk_begin, blk_end, reinterpret_cast<unsigned*>(st.cx));
     }
 }
 
@@ -1931,14 +1944,13 @@ __global__ __launch_bounds__(kRangeNW * kWave) void range_fused(const double* __
         const unsigned we = wb + wpw < nw ? wb + wpw : nw;
         unsigned long long obase = excl + (wb < we ? wpre[wb] : 0u);
         const unsigned ibase = (unsigned)(u0 * kUnitPts);
+        unsigned* stg = reinterpret_cast<unsigned*>(st.cx);  // the wave's idle candidate stage
+        unsigned sc = 0;
         for (unsigned w0 = wb; w0 < we; w0 += kWave) {
             const unsigned long long mine = w0 + lane < we ? bmask[w0 + lane] : 0ull;
-            const unsigned c = (unsigned)__popcll(mine);
-            const unsigned incl = wave_incl_scan(c);
-            const unsigned ex = incl - c;
-            emit_words(mine, ex, obase, ibase + w0 * 64u, out, cap);
-            obase += (unsigned)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+            emit_words(mine, ibase + w0 * 64u, stg, sc, obase, out, cap);
         }
+        if (sc) emit_flush(stg, sc, obase, out, cap);
     }
     if (threadIdx.x == 0 && vb == gridDim.x - 1) {
         *total = excl + bcount;
