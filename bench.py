@@ -534,8 +534,9 @@ class JoinWorkload(Workload):
     """C3 (BASELINE.json configs[2]): 10k queries x 10M Gaussian-clustered data points per
     window, 500x500, r = 0.05 (32 shared centres, sigma 0.1)."""
     tag = "join_probe"
-    kernel = ("geohip join step: tile binning + query block lists + join_fused (one pass: work items, "
-              "decoupled look-back, staged pair runs); the whole device step is timed")
+    kernel = ("geohip join step: query block lists (jq_rect / jq_build / jq_starts), tile binning into 16-B "
+              "records (jb_bands / jb_scan / jb_segs / jb_tiles), join_plan / join_item_fill, join_fused (work "
+              "items, decoupled look-back, LDS-staged 512-B pair stores); every kernel timed by its dispatch stamps")
     grid_n, radius, n_default, nq, sigma = 500, 0.05, 10_000_000, 10_000, 0.1
     windows = 2
 

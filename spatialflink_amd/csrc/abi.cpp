@@ -30,7 +30,7 @@ enum Slot {
     S_X, S_Y, S_QX, S_QY, S_GTHR, S_PART_D, S_PART_I, S_OUT_D, S_OUT_I, S_OUT_CNT,
     S_MASK, S_UCNT, S_OFFS, S_TOTAL, S_OUT_IDX, S_OUT_PAIRS, S_SPILL_D, S_SPILL_I, S_SPILL_CNT, S_RLB, S_TRACE,
     S_J0, S_J1, S_J2, S_J3, S_J4, S_J5, S_J6, S_J7, S_J8, S_J9, S_J10, S_J11, S_J12, S_J13, S_J14, S_J15,
-    S_J16, S_J17, S_J18, S_J19, S_J20, S_J21, S_J22, S_J23, S_J24, S_J25,
+    S_J16, S_J17, S_J18, S_J19, S_J20, S_J21, S_J22, S_J23, S_J24, S_J25, S_J26, S_J27,
     S_I0, S_I1, S_I2, S_I3, S_I4, S_I5, S_I6, S_I7, S_I8, S_I9, S_I10, S_I11,
     S_COUNT
 };
@@ -126,9 +126,6 @@ struct geohip_ctx {
     bool stg_used[2] = {false, false};
     std::unique_ptr<CopyPool> copy_pool;
     hipEvent_t switch_ev = nullptr;  // orders a stream rebinding after the old stream's work
-    // side stream of a step's independent chain (ctx_fork / ctx_join): created on first use
-    hipStream_t side = nullptr;
-    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
     void* pcache = nullptr;          // point-polygon plan cache (cell_kernels.hip owns the type)
     void* kcache = nullptr;          // point-polygon kNN polygon cache (cell_kernels.hip owns the type)
 };
@@ -673,12 +670,6 @@ int geohip_ctx_destroy(geohip_ctx* ctx) {
     }
     if (ctx->cstream) hipStreamDestroy(ctx->cstream);
     if (ctx->switch_ev) hipEventDestroy(ctx->switch_ev);
-    if (ctx->side) {
-        hipStreamSynchronize(ctx->side);
-        hipStreamDestroy(ctx->side);
-    }
-    if (ctx->fork_ev) hipEventDestroy(ctx->fork_ev);
-    if (ctx->join_ev) hipEventDestroy(ctx->join_ev);
     if (ctx->own) hipStreamDestroy(ctx->own);
     delete ctx;
     return GEOHIP_OK;
@@ -1232,13 +1223,13 @@ int geohip_debug_knn_pass_trace(geohip_ctx* ctx, const geohip_grid* grid, const 
 namespace geohip {
 int ctx_fail(geohip_ctx* ctx, int code, const std::string& msg) { return fail(ctx, code, msg); }
 int ctx_ensure(geohip_ctx* ctx, int slot, size_t bytes, void** out) {
-    if (slot < 0 || S_J0 + slot > S_J25) return fail(ctx, GEOHIP_ERR_DEVICE, "internal: scratch slot out of range");
+    if (slot < 0 || S_J0 + slot > S_J27) return fail(ctx, GEOHIP_ERR_DEVICE, "internal: scratch slot out of range");
     int rc = ensure(ctx, (Slot)(S_J0 + slot), bytes);
     if (!rc) *out = ctx->buf[S_J0 + slot];
     return rc;
 }
 int ctx_ensure_zeroed(geohip_ctx* ctx, int slot, size_t bytes, void** out) {
-    if (slot < 0 || S_J0 + slot > S_J25) return fail(ctx, GEOHIP_ERR_DEVICE, "internal: scratch slot out of range");
+    if (slot < 0 || S_J0 + slot > S_J27) return fail(ctx, GEOHIP_ERR_DEVICE, "internal: scratch slot out of range");
     int rc = ensure_zeroed(ctx, (Slot)(S_J0 + slot), bytes);
     if (!rc) *out = ctx->buf[S_J0 + slot];
     return rc;
@@ -1279,25 +1270,6 @@ int ctx_cus(geohip_ctx* ctx) { return ctx->cus; }
 
 int ctx_begin(geohip_ctx* ctx) { return begin(ctx); }
 hipStream_t ctx_stream(geohip_ctx* ctx) { return ctx->stream; }
-// Fork: work enqueued on *side after this call runs after everything enqueued on the ctx stream so
-// far, concurrently with what follows there; ctx_join orders the ctx stream after it again.
-int ctx_fork(geohip_ctx* ctx, hipStream_t* side) {
-    if (!ctx->side) {
-        if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&ctx->join_ev, hipEventDisableTiming) != hipSuccess)
-            return fail(ctx, GEOHIP_ERR_DEVICE, "side stream creation failed");
-    }
-    if (hipEventRecord(ctx->fork_ev, ctx->stream) != hipSuccess || hipStreamWaitEvent(ctx->side, ctx->fork_ev, 0) != hipSuccess)
-        return fail(ctx, GEOHIP_ERR_DEVICE, "side stream fork failed");
-    *side = ctx->side;
-    return GEOHIP_OK;
-}
-int ctx_join(geohip_ctx* ctx) {
-    if (hipEventRecord(ctx->join_ev, ctx->side) != hipSuccess || hipStreamWaitEvent(ctx->stream, ctx->join_ev, 0) != hipSuccess)
-        return fail(ctx, GEOHIP_ERR_DEVICE, "side stream join failed");
-    return GEOHIP_OK;
-}
 int ctx_mem(geohip_ctx* ctx) { return ctx->mem; }
 uint64_t* ctx_pinned(geohip_ctx* ctx) { return ctx->pinned; }
 void** ctx_pcache_slot(geohip_ctx* ctx) { return &ctx->pcache; }

@@ -74,6 +74,30 @@ __device__ __forceinline__ int32_t d_axis_cell_fast(double v, double mn, double 
     return d_cvt_java(f);
 }
 
+// d_axis_cell_fast plus the point's subcell (0..3: which quarter of the cell, sub_of's edges):
+// from q, the quotient the cell came from -- 4 (q - floor q) is exact in fp64, and it differs
+// from the subcell edges' own arithmetic (sub_edge: mn + (c + i / 4) l, rounded twice) by at most
+// 2^-51 (6 |q| + |mn| / l + 2) in those units, so outside the margin E below floor(4 (q - f)) is
+// sub_of's answer; inside it (or when the cell itself took the division) sub_ok is false and the
+// caller evaluates sub_of.
+__device__ __forceinline__ int32_t d_axis_cell_sub(double v, double mn, double l, double il, double mnl, unsigned& sub,
+                                                   bool& sub_ok) {
+    const double t = v - mn;
+    const double q = t * il;
+    double f = __builtin_floor(q);
+    const double e = __builtin_fabs(q) * 0x1.0p-49 + 0x1.0p-1000;
+    const bool ok = (q - f > e) & ((f + 1.0) - q > e);
+    const double t4 = (q - f) * 4.0;
+    const double sf = __builtin_floor(t4);
+    const double E = (__builtin_fabs(q) + mnl + 4.0) * 0x1.0p-44;
+    sub_ok = ok && (sf < 1.0 || t4 - sf > E) && (sf > 2.0 || (sf + 1.0) - t4 > E);
+    sub = sub_ok ? (unsigned)(int)sf : 0u;
+    if (__ballot(!ok)) {  // wave-uniform, rare: the division decides near integers, NaN, inf
+        if (!ok) f = __builtin_floor(t / l);
+    }
+    return d_cvt_java(f);
+}
+
 // small zero-fills inside timed steps (a kernel, so its time is stamped like the others)
 __global__ void fill_words(unsigned* __restrict__ p, unsigned n, unsigned v) {
     for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = v;
@@ -815,7 +839,7 @@ struct JBin {
     unsigned nbands, nsub, nblk;
     uint4* l1;          // level-1 records (block chunks, band-sorted per sub-chunk)
     unsigned* soff;     // [(block * nsub + sub) * (nbands + 1) + band] band starts inside the sub-chunk
-    unsigned* tcnt;     // [ntiles] tile counts (zero on entry; jb_scan re-zeroes)
+    unsigned* tcnt;     // [ntiles] tile counts (zeroed by the step's fill_words launch)
     unsigned* tstart;   // [ntiles + 1]
     unsigned* tcur;     // [ntiles] level-2 cursors
     unsigned* spre;     // [nbands][nblk * nsub + 1] record prefix of each band's non-empty segments
@@ -978,8 +1002,7 @@ __device__ __forceinline__ unsigned block_scan_passes(unsigned n, unsigned* wsum
     return total;
 }
 
-// Tile starts and cursors from the tile counts (one block; re-zeroes the counts for the next
-// launch).
+// Tile starts and cursors from the tile counts (one block).
 __global__ __launch_bounds__(kBinThreads) void jb_scan(JBin a) {
     __shared__ unsigned wsum[kScanPasses * (kBinThreads / kWave)];
     const unsigned total = block_scan_passes(
@@ -987,7 +1010,6 @@ __global__ __launch_bounds__(kBinThreads) void jb_scan(JBin a) {
         [&](unsigned t, unsigned, unsigned ex) {
             a.tstart[t] = ex;
             a.tcur[t] = ex;
-            a.tcnt[t] = 0u;
         });
     if (threadIdx.x == 0) a.tstart[a.g.ntiles] = total;
 }
@@ -1150,7 +1172,8 @@ __global__ __launch_bounds__(kJbL2Threads) void jb_tiles(JBin a) {
             if (j < m) {
                 const uint4 q = st[j];
                 const unsigned bq = (q.w >> 20) & (kBandTiles - 1);
-                a.recs[base[bq] + (j - ls[bq])] = q;
+                const unsigned p = base[bq] + (j - ls[bq]);
+                if (p < a.n) a.recs[p] = q;  // bounded even if the counts were not the binning's own
             }
         }
         lds_barrier();
@@ -2448,6 +2471,7 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
         return (t * kStreamNW + (unsigned)wid) * kStreamPts + 2u * (unsigned)lane + (unsigned)(s & 1) +
                128u * (unsigned)(s >> 1);
     };
+    const double mnlx = __builtin_fabs(g.mnx) * g.il, mnly = __builtin_fabs(g.mny) * g.il;
     // point state for phase B: bits 0-3 subcell (4 sx + sy), 4 NaN coordinate, 5 outside the grid
     constexpr unsigned kNanBit = 16u, kOutBit = 32u;
     uint2 hd[kIters][4];
@@ -2466,8 +2490,11 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
 #pragma unroll
         for (int s = 0; s < 4; s++) {
             const bool v = c0 + loc_of(t, s) < c1;
-            int32_t cx = 0, cy = 0;
-            const bool in = v && point_cell(g, qx[s], qy[s], cx, cy);
+            unsigned sx = 0, sy = 0;
+            bool okx = false, oky = false;
+            const int32_t cx = d_axis_cell_sub(qx[s], g.mnx, g.l, g.il, mnlx, sx, okx);
+            const int32_t cy = d_axis_cell_sub(qy[s], g.mny, g.l, g.il, mnly, sy, oky);
+            const bool in = v && cx >= 0 && cy >= 0 && cx < g.nb && cy < g.nb;
             const bool nan = !(qx[s] == qx[s] && qy[s] == qy[s]);
             unsigned w = (nan ? kNanBit : 0u) | ((v && !in) ? kOutBit : 0u);
             hd[t][s] = make_uint2(kNoEntry, 0u);
@@ -2478,8 +2505,15 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
                 else if (a.keep) has = (a.keep[key >> 5] >> (key & 31u)) & 1u;
                 if (has && GEOHIP_PS_ABL != 2) hd[t][s] = a.head[key];
                 if (GEOHIP_PS_ABL == 2 && has && key == 0xfffffffu) hd[t][s].x = 0;
-                if (has && !nan && !APPROX)
-                    w |= (unsigned)(4 * sub_of(qx[s], g.mnx, g.l, cx) + sub_of(qy[s], g.mny, g.l, cy));
+                if (has && !nan && !APPROX) {
+                    // the subcell from the cell computation's quotient, exact outside a margin
+                    // around the subcell edges; the edges' own arithmetic inside it (rare)
+                    if (__ballot(!(okx && oky))) {
+                        if (!okx) sx = (unsigned)sub_of(qx[s], g.mnx, g.l, cx);
+                        if (!oky) sy = (unsigned)sub_of(qy[s], g.mny, g.l, cy);
+                    }
+                    w |= 4u * sx + sy;
+                }
             }
             st[t] = s == 0 ? w : (st[t] | (w << (8 * s)));
         }
@@ -3755,8 +3789,10 @@ namespace {
 
 enum JSlot {
     J_HIST, J_TTOT, J_TSTART, J_SEG, J_SX, J_SY, J_SIDX, J_SKEY, J_MISC, J_AUX, J_POLY, J_OUT, J_RECT, J_QSTART,
-    J_QLIST, J_GLIST, J_QCNT, J_BCNT, J_BOFF, J_PMASK, J_MWORDS, J_MOFF, J_TCNT, J_TCUR
+    J_QLIST, J_GLIST, J_QCNT, J_BCNT, J_BOFF, J_PMASK, J_MWORDS, J_MOFF, J_TCUR,
+    J_KCAND, J_KTEMP, J_KBLOB  // point kNN (large k) and point-polygon kNN scratch
 };
+static_assert(J_KBLOB <= 27, "scratch slots (abi.cpp S_J0 .. S_J27)");
 
 // J_MISC words: [0] outside count, [1] outside cursor, [2] scan grand total, [3] global
 // query count, [8..9] pair total (u64)
@@ -3766,7 +3802,7 @@ struct Scratch {
     geohip_ctx* ctx;
     int rc = GEOHIP_OK;
     template <typename T>
-    T* get(int slot, size_t bytes) {
+    T* get(JSlot slot, size_t bytes) {
         void* p = nullptr;
         if (rc) return nullptr;
         rc = ctx_ensure(ctx, slot, bytes, &p);
@@ -3915,7 +3951,7 @@ int bin_tiles(geohip_ctx* ctx, Scratch& S, const double* dx, const double* dy, u
 // Join binning (jb_bands / jb_scan / jb_segs / jb_tiles): the window's in-grid points as
 // tile-sorted 16-B records; *recs and *tstart (ntiles + 1) on the device.
 int join_bin(geohip_ctx* ctx, Scratch& S, const double* dx, const double* dy, uint64_t n, const TileGeom& geo,
-             const uint4** recs, const unsigned** tstart) {
+             unsigned* tcnt, const uint4** recs, const unsigned** tstart) {
     hipStream_t st = ctx_stream(ctx);
     uint64_t nblk = (n + 16383) / 16384;
     if (nblk > kJbBlocks) nblk = kJbBlocks;
@@ -3946,15 +3982,12 @@ int join_bin(geohip_ctx* ctx, Scratch& S, const double* dx, const double* dy, ui
     a.sst = a.spre + (size_t)a.nbands * (nseg + 1);
     a.nne = a.sst + (size_t)a.nbands * nseg;
     a.nround = a.nne + a.nbands;
-    void* tc = nullptr;
-    int rc = ctx_ensure_zeroed(ctx, J_TCNT, kMaxTiles * 4, &tc);  // jb_scan leaves it zero
-    if (rc) return rc;
-    a.tcnt = reinterpret_cast<unsigned*>(tc);
-    if (n) jb_bands<<<(unsigned)nblk, kBinThreads, 0, st>>>(a);
-    jb_scan<<<1, kBinThreads, 0, st>>>(a);
+    a.tcnt = tcnt;  // zero on entry: part of the step's zero block, no state carried between calls
+    if (n) tlaunch(ctx, jb_bands, (unsigned)nblk, kBinThreads, 0, st, a);
+    tlaunch(ctx, jb_scan, 1, kBinThreads, 0, st, a);
     if (n) {
-        jb_segs<<<a.nbands, kBinThreads, 0, st>>>(a);
-        jb_tiles<<<(unsigned)std::min<uint64_t>(kJbL2Blocks, maxround), kJbL2Threads, 0, st>>>(a);
+        tlaunch(ctx, jb_segs, a.nbands, kBinThreads, 0, st, a);
+        tlaunch(ctx, jb_tiles, (unsigned)std::min<uint64_t>(kJbL2Blocks, maxround), kJbL2Threads, 0, st, a);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, std::string("join binning: ") + hipGetErrorString(e));
@@ -4029,8 +4062,9 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
     const uint64_t item_cap = ((nd + kJP - 1) / kJP + ntl) * ((qpt + kJQ - 1) / kJQ) + 1;
     QRect* drect = S.get<QRect>(J_RECT, nq * sizeof(QRect) + 16);
     // per-call counters, zeroed by one launch (fill_words): query counts | query cursors | misc words
-    // ([0] jq_rect error, [4] ticket, [5] global query count) | the pair total (u64)
-    const unsigned nzero = (unsigned)(2 * (ntl + 1) + kMiscWords + 2 + 1) & ~1u;
+    // ([0] jq_rect error, [4] ticket, [5] global query count) | the pair total (u64) | tile counts
+    const uint64_t ztot = (2 * (ntl + 1) + kMiscWords + 1) & ~(uint64_t)1;  // word offset of the total
+    const unsigned nzero = (unsigned)(ztot + 2 + ntl + 1);
     unsigned* zero = S.get<unsigned>(J_QCNT, (size_t)nzero * 4 + 16);
     unsigned* qstart = S.get<unsigned>(J_QSTART, (ntl + 1) * 4);
     unsigned* qlist = S.get<unsigned>(J_QLIST, list_cap * 4 + 16);
@@ -4041,38 +4075,36 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
     unsigned* qcnt = zero;
     unsigned* qcur = zero + (ntl + 1);
     unsigned* misc = zero + 2 * (ntl + 1);
-    unsigned long long* total = reinterpret_cast<unsigned long long*>(zero + ((2 * (ntl + 1) + kMiscWords + 1) & ~(uint64_t)1));
+    unsigned long long* total = reinterpret_cast<unsigned long long*>(zero + ztot);
+    unsigned* tcnt = zero + ztot + 2;
     hipEvent_t e0, e1;
     ctx_timing_events(ctx, &e0, &e1);
     if (e0) hipEventRecord(e0, st);  // the whole device step: binning, replication, join
-    // the query side (counters zeroed, query blocks, per-tile lists) on the ctx's side stream,
-    // concurrently with the data binning; the join waits for both
-    hipStream_t qs = nullptr;
-    rc = ctx_fork(ctx, &qs);
-    if (rc) return rc;
-    fill_words<<<(nzero + kTB - 1) / kTB, kTB, 0, qs>>>(zero, nzero, 0u);
+    // every kernel of the step is timed on its own (tlaunch: the dispatch's begin / end stamps)
+    tlaunch(ctx, fill_words, (nzero + kTB - 1) / kTB, kTB, 0, st, zero, nzero, 0u);
     const unsigned qb = (unsigned)((nq + kTB - 1) / kTB);
     if (nq) {
         JqGeom jg{gq->min_x, gq->min_y, gq->cell_len, nb, lc, all_cells ? 1 : 0};
-        jq_rect<<<qb, kTB, 0, qs>>>(dqx, dqy, nq, jg, drect, misc);
+        tlaunch(ctx, jq_rect, qb, kTB, 0, st, dqx, dqy, nq, jg, drect, misc);
     }
     if (global_mode) {
-        if (nq) jq_global<<<qb, kTB, 0, qs>>>(nq, glist, misc + 5);
-        jq_starts<<<1, kBinThreads, 0, qs>>>(qcnt, geo.ntiles, qstart);  // all zero: no per-tile lists
+        if (nq) tlaunch(ctx, jq_global, qb, kTB, 0, st, nq, glist, misc + 5);
+        tlaunch(ctx, jq_starts, 1, kBinThreads, 0, st, (const unsigned*)qcnt, geo.ntiles, qstart);  // all zero
     } else {
         const unsigned qg = (unsigned)((nq + kTB / kWave - 1) / (kTB / kWave));  // one wave per query
-        if (nq) jq_build<false><<<qg, kTB, 0, qs>>>(drect, nq, geo, qcnt, nullptr, nullptr);
-        jq_starts<<<1, kBinThreads, 0, qs>>>(qcnt, geo.ntiles, qstart);
-        if (nq) jq_build<true><<<qg, kTB, 0, qs>>>(drect, nq, geo, qcur, qstart, qlist);
+        if (nq) tlaunch(ctx, jq_build<false>, qg, kTB, 0, st, (const QRect*)drect, nq, geo, qcnt, (const unsigned*)nullptr,
+                        (unsigned*)nullptr);
+        tlaunch(ctx, jq_starts, 1, kBinThreads, 0, st, (const unsigned*)qcnt, geo.ntiles, qstart);
+        if (nq) tlaunch(ctx, jq_build<true>, qg, kTB, 0, st, (const QRect*)drect, nq, geo, qcur, (const unsigned*)qstart,
+                        qlist);
     }
     const uint4* recs = nullptr;
     const unsigned* tstart = nullptr;
-    rc = join_bin(ctx, S, ddx, ddy, nd, geo, &recs, &tstart);
+    rc = join_bin(ctx, S, ddx, ddy, nd, geo, tcnt, &recs, &tstart);
     if (rc) return rc;
-    rc = ctx_join(ctx);
-    if (rc) return rc;
-    join_plan<<<1, kBinThreads, 0, st>>>(tstart, qstart, misc + 5, geo.ntiles, istart);
-    join_item_fill<<<(unsigned)((ntl + kTB - 1) / kTB), kTB, 0, st>>>(istart, geo.ntiles, items);
+    tlaunch(ctx, join_plan, 1, kBinThreads, 0, st, tstart, (const unsigned*)qstart, (const unsigned*)(misc + 5), geo.ntiles,
+            istart);
+    tlaunch(ctx, join_item_fill, (unsigned)((ntl + kTB - 1) / kTB), kTB, 0, st, (const unsigned*)istart, geo.ntiles, items);
     // output: device pointer directly, or a device staging buffer for host output
     unsigned* out = nullptr;
     if (!count_only && cap) {
@@ -4092,11 +4124,11 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
                misc + 4, total, out, out ? cap : 0, ((uintptr_t)out & 7u) == 0};
     if (nq && nd) {
         if (approximate) {
-            if (write) join_fused<true, true><<<kJBlocksW, kTB, 0, st>>>(jr);
-            else join_fused<true, false><<<kJBlocksC, kTB, 0, st>>>(jr);
+            if (write) tlaunch(ctx, join_fused<true, true>, kJBlocksW, kTB, 0, st, jr);
+            else tlaunch(ctx, join_fused<true, false>, kJBlocksC, kTB, 0, st, jr);
         } else {
-            if (write) join_fused<false, true><<<kJBlocksW, kTB, 0, st>>>(jr);
-            else join_fused<false, false><<<kJBlocksC, kTB, 0, st>>>(jr);
+            if (write) tlaunch(ctx, join_fused<false, true>, kJBlocksW, kTB, 0, st, jr);
+            else tlaunch(ctx, join_fused<false, false>, kJBlocksC, kTB, 0, st, jr);
         }
     }
     if (e1) hipEventRecord(e1, st);
@@ -5028,7 +5060,7 @@ int large_k_scratch(geohip_ctx* ctx, unsigned k, size_t extra_bytes, LargeK* L) 
     const size_t off_temp = (off_tmp + (size_t)k * 12 + a16) & ~a16;
     const size_t off_extra = (off_temp + L->temp_bytes + a16) & ~a16;
     void* p = nullptr;
-    int rc = ctx_ensure(ctx, 23, off_extra + extra_bytes + 64, &p);
+    int rc = ctx_ensure(ctx, J_KTEMP, off_extra + extra_bytes + 64, &p);
     if (rc) return rc;
     char* b = reinterpret_cast<char*>(p);
     L->rs = reinterpret_cast<RselState*>(b);
@@ -5049,7 +5081,7 @@ int knn_pp_large_impl(geohip_ctx* ctx, const PointPlan& plan, const double* dx, 
     hipStream_t st = ctx_stream(ctx);
     const uint64_t ncap = n ? n : 1;
     void* pc = nullptr;
-    int rc = ctx_ensure(ctx, 22, ncap * 12 + 64, &pc);
+    int rc = ctx_ensure(ctx, J_KCAND, ncap * 12 + 64, &pc);
     LargeK L;
     if (!rc) rc = large_k_scratch(ctx, k, 0, &L);
     if (rc) return rc;
@@ -5093,7 +5125,7 @@ int knn_merge_large_impl(geohip_ctx* ctx, const unsigned long long* d, const uns
     if (!tb) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "sort temp size query failed");
     const size_t mcap = (size_t)(m ? m : 1);
     void* p = nullptr;
-    int rc = ctx_ensure(ctx, 22, mcap * 24 + tb + 512, &p);
+    int rc = ctx_ensure(ctx, J_KCAND, mcap * 24 + tb + 512, &p);
     if (rc) return rc;
     char* b = reinterpret_cast<char*>(p);
     unsigned long long* tmp_d = reinterpret_cast<unsigned long long*>(b);
@@ -5219,7 +5251,7 @@ int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, co
         const size_t off_vr = off_rect + 16 * (size_t)nrect;
         const size_t blob = off_vr + hvr.size() * sizeof(ring_id_t);
         void* pb = nullptr;
-        rc = ctx_ensure(ctx, 24, blob + 64, &pb);
+        rc = ctx_ensure(ctx, J_KBLOB, blob + 64, &pb);
         if (rc) return rc;
         char* b = reinterpret_cast<char*>(pb);
         if ((P.nv && (hipMemcpyAsync(b + off_vx, pl.rx.data(), 8 * (size_t)P.nv, hipMemcpyHostToDevice, st) != hipSuccess ||
@@ -5249,7 +5281,7 @@ int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, co
         kc->valid = true;
     } else {
         void* pb = nullptr;  // the slot is this path's own: same pointer, same contents
-        rc = ctx_ensure(ctx, 24, kc->blob_bytes + 64, &pb);
+        rc = ctx_ensure(ctx, J_KBLOB, kc->blob_bytes + 64, &pb);
         if (rc) return rc;
         if (pb != kc->dev_blob) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "polygon table slot moved");
     }
@@ -5279,7 +5311,7 @@ int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, co
     if (rc) return rc;
     Scratch S{ctx};
     const uint64_t ncap = n ? n : 1;
-    char* cbuf = S.get<char>(22, ncap * 12 + 64);
+    char* cbuf = S.get<char>(J_KCAND, ncap * 12 + 64);
     if (S.rc) return S.rc;
     const size_t kout = std::max<size_t>(k, 256);
     LargeK L;

@@ -242,6 +242,8 @@ int geohip_debug_ingest_record(const geohip_ingest_spec* spec, const char* rec, 
                                int64_t* ts) {
     ingest::Spec sp;
     if (!spec || spec->format < 0 || spec->format > 2) return GEOHIP_ERR_ARG;
+    memset(&sp, 0, sizeof sp);  // no trajectory fields: point records only
+    sp.foid = -1;
     sp.format = spec->format;
     sp.delim = spec->delim;
     sp.fx = spec->attr_x;

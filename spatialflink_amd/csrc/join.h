@@ -1,5 +1,6 @@
 // join.h -- point-point window join (PointPointJoinQuery.java:113-172).
 #pragma once
+#include <type_traits>
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -11,7 +12,7 @@
 namespace geohip {
 // context services implemented in abi.cpp
 int ctx_fail(geohip_ctx* ctx, int code, const std::string& msg);
-int ctx_ensure(geohip_ctx* ctx, int slot, size_t bytes, void** out);  // slot 0..25
+int ctx_ensure(geohip_ctx* ctx, int slot, size_t bytes, void** out);  // slot 0..27 (JSlot, cell_kernels.hip)
 int ctx_ensure_zeroed(geohip_ctx* ctx, int slot, size_t bytes, void** out);  // zeroed when (re)allocated
 int ctx_ensure_ingest(geohip_ctx* ctx, int slot, size_t bytes, void** out);  // slot 0..11
 int ctx_ensure_ingest_zeroed(geohip_ctx* ctx, int slot, size_t bytes, void** out);  // zeroed when (re)allocated
@@ -21,8 +22,6 @@ int ctx_lookback_status(geohip_ctx* ctx, int slot, size_t bytes, void** out, uns
 int ctx_cus(geohip_ctx* ctx);                       // compute units of the ctx's device
 int ctx_begin(geohip_ctx* ctx);  // clears the error, selects the ctx's device
 hipStream_t ctx_stream(geohip_ctx* ctx);
-int ctx_fork(geohip_ctx* ctx, hipStream_t* side);  // a side stream ordered after the ctx stream's work so far
-int ctx_join(geohip_ctx* ctx);                     // the ctx stream ordered after the side stream's work
 int ctx_mem(geohip_ctx* ctx);
 uint64_t* ctx_pinned(geohip_ctx* ctx);
 void ctx_timing_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1);      // a step of several launches
@@ -32,8 +31,15 @@ void ctx_kernel_step_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1); //
 // A kernel of a timed step: while the ctx's timing is on, launched with a fresh event pair that
 // its own dispatch stamps (begin / end, the durations rocprofv3 reports), so a step's kernel time
 // is the sum of its kernels without the gaps between them.
-template <typename F, typename... A>
-inline void tlaunch(geohip_ctx* ctx, F kernel, dim3 grid, dim3 block, uint32_t shm, hipStream_t st, A... a) {
+// The arguments are packed as given (no conversion to the kernel's parameter types), so they must
+// match those types in size and kind (a pointer may gain const): checked at compile time.
+template <typename... P, typename... A>
+inline void tlaunch(geohip_ctx* ctx, void (*kernel)(P...), dim3 grid, dim3 block, uint32_t shm, hipStream_t st, A... a) {
+    static_assert(sizeof...(P) == sizeof...(A), "tlaunch: argument count");
+    static_assert(((sizeof(typename std::decay<P>::type) == sizeof(A) &&
+                    std::is_convertible<A, typename std::decay<P>::type>::value &&
+                    std::is_floating_point<typename std::decay<P>::type>::value == std::is_floating_point<A>::value) && ...),
+                  "tlaunch: argument types must match the kernel's (same size and kind)");
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (ctx) ctx_kernel_events(ctx, &e0, &e1);
     hipExtLaunchKernelGGL(kernel, grid, block, shm, st, e0, e1, 0, a...);

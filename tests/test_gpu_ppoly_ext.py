@@ -343,3 +343,22 @@ def test_ppoly_stream_overflow_and_regrow(ctx):
     got = ctx.join_ppoly(ag, ag, x, y, off, vx, vy, 0.01)
     want = cref.join_ppoly(cg, cg, x, y, off, vx, vy, 0.01)
     assert pairs_sorted(got).tolist() == pairs_sorted(want).tolist()
+
+
+def test_join_after_knn_ppoly_scratch(ctx):
+    """Regression: the point-polygon kNN's candidate buffer once shared a scratch slot with the
+    join's tile counts, so a point join after a large point-polygon kNN on the same ctx read
+    leftover counts.  kNN first (a window larger than any tile-count array), then the join."""
+    x, y = synth.uniform(400000, 140)
+    off, vx, vy = synth.star_polygons(1, 141)
+    ag, cg = agrid(500)
+    gi, gd = ctx.knn_ppoly(ag, x, y, vx, vy, 0.02, 256)
+    wi, wd = cref.knn_ppoly(cg, x, y, vx, vy, 0.02, 256)
+    assert gi.tolist() == wi.tolist()
+    dx, dy = synth.uniform(200000, 142)
+    qx, qy = synth.uniform(2000, 143)
+    for _ in range(2):
+        got = ctx.join_pp(ag, ag, dx, dy, qx, qy, 0.01, False)
+        want = cref.join_pp(cg, cg, dx, dy, qx, qy, 0.01)
+        assert pairs_sorted(got).tolist() == pairs_sorted(want).tolist()
+        ctx.knn_ppoly(ag, x, y, vx, vy, 0.02, 256)
