@@ -2407,6 +2407,14 @@ __device__ __forceinline__ void stream_emit_cand(const StreamArgs& a, unsigned l
     a.o.crec[p] = make_double4(a.x[idx], a.y[idx], __longlong_as_double((long long)idx), 0.0);
 }
 
+#ifndef GEOHIP_PS_BATCH
+#define GEOHIP_PS_BATCH 2  // entries whose loads a wave step of the exact walk issues together (0: one
+                           // dependent gather per step; measurement builds).  C4 kernel sums, one
+                           // box: 0 -> 925 us, 1 -> 809, 2 -> 812, 3 -> 822, 4 -> 828, 8 -> 906
+#endif
+#ifndef GEOHIP_PS_NTLOAD
+#define GEOHIP_PS_NTLOAD 0
+#endif
 #ifndef GEOHIP_PS_ABL
 #define GEOHIP_PS_ABL 0  // measurement builds only: 1 no staging pushes, 2 no cell-table reads,
                           // 3 pushes folded into a register checksum, 4 no chunk write-out
@@ -2452,10 +2460,18 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
         const uint64_t base = c0 + (uint64_t)(t * kStreamNW + wid) * kStreamPts;
         const uint64_t i0 = base + 2 * (uint64_t)lane, i1 = i0 + 128;
         if (base + kStreamPts <= c1) {
+#if GEOHIP_PS_NTLOAD  // measurement builds: the window read past L2 (the cell table stays resident)
+            typedef double d2v __attribute__((ext_vector_type(2)));
+            const d2v ax = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(a.x + i0));
+            const d2v bx = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(a.x + i1));
+            const d2v ay = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(a.y + i0));
+            const d2v by = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(a.y + i1));
+#else
             const double2 ax = *reinterpret_cast<const double2*>(a.x + i0);
             const double2 bx = *reinterpret_cast<const double2*>(a.x + i1);
             const double2 ay = *reinterpret_cast<const double2*>(a.y + i0);
             const double2 by = *reinterpret_cast<const double2*>(a.y + i1);
+#endif
             qx[0] = ax.x; qx[1] = ax.y; qx[2] = bx.x; qx[3] = bx.y;
             qy[0] = ay.x; qy[1] = ay.y; qy[2] = by.x; qy[3] = by.y;
         } else {
@@ -2518,7 +2534,72 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
             st[t] = s == 0 ? w : (st[t] | (w << (8 * s)));
         }
     }
-    if (!APPROX) {
+    if (!APPROX && GEOHIP_PS_BATCH > 0) {
+        // Phase B (exact): each lane's entries of its kIters * 4 points form ONE list, numbered
+        // 0 .. tot-1 slot after slot; entry k's address follows from the heads alone (slot = the
+        // last slot whose list start is <= k; a multi cell's entries are consecutive in cell_ent),
+        // so a wave step issues the loads of kPsBatch entries at once instead of a chain of
+        // dependent gathers (each entry's load waited on before the next one was known).
+        constexpr unsigned kSlots = kIters * 4;
+        constexpr unsigned kB = GEOHIP_PS_BATCH > 0 ? GEOHIP_PS_BATCH : 1;
+        unsigned pre[kSlots];
+        unsigned tot = 0;
+#pragma unroll
+        for (unsigned j = 0; j < kSlots; j++) {
+            const uint2 h = hd[j >> 2][j & 3];
+            pre[j] = tot;
+            tot += h.x == kNoEntry ? 0u : ((h.x & kMulti) ? (h.x & ~kMulti) : 1u);
+        }
+        for (unsigned k0 = 0; __ballot(k0 < tot); k0 += kB) {
+            uint2 en[kB];
+            unsigned sj[kB];
+#pragma unroll
+            for (unsigned u = 0; u < kB; u++) {
+                const unsigned k = k0 + u;
+                unsigned j = 0, pj = 0;
+                uint2 h = hd[0][0];
+#pragma unroll
+                for (unsigned i = 1; i < kSlots; i++) {
+                    if (pre[i] <= k) {
+                        j = i;
+                        pj = pre[i];
+                        h = hd[i >> 2][i & 3];
+                    }
+                }
+                sj[u] = j;
+                en[u] = make_uint2(kNoEntry, 0u);
+                if (k < tot) en[u] = (h.x & kMulti) ? a.ent[h.y + (k - pj)] : h;
+            }
+#pragma unroll
+            for (unsigned u = 0; u < kB; u++) {
+                const unsigned j = sj[u];
+                const uint32_t ex = en[u].x, word = en[u].y;
+                bool hit = false, need = false;
+                const unsigned poly = ex & ~kEntC;
+                const unsigned t = j >> 2, sl = j & 3;
+                const unsigned loc = (t * kStreamNW + (unsigned)wid) * kStreamPts + 2u * (unsigned)lane + (sl & 1u) + 128u * (sl >> 1);
+                if (ex != kNoEntry) {
+                    const unsigned sw = (kIters > 1 && t ? st[kIters > 1 ? 1 : 0] : st[0]) >> (8 * sl);
+                    if (!(ex & kEntC)) {
+                        hit = true;
+                    } else {
+                        // a decided class holds for every point in the cell's coordinate box: not for
+                        // NaN coordinates (cell 0 by Java's (int) NaN)
+                        uint32_t kc = kClsMixed;
+                        if (!(sw & kNanBit)) {
+                            if (word == kWordHit) kc = kClsHit;
+                            else if (word == kWordMiss) kc = kClsMiss;
+                            else kc = (word >> (2 * (sw & 15u))) & 3u;
+                        }
+                        hit = kc == kClsHit;
+                        need = kc == kClsMixed;
+                    }
+                }
+                stream_push<false>(a, ps, hit, poly, loc, c0);
+                stream_push<true>(a, cs, need, poly, loc, c0);
+            }
+        }
+    } else if (!APPROX) {
         // Phase B (exact): each lane walks the entries of its kIters * 4 points as ONE list, slot
         // after slot (the heads queue in registers, shifted as slots are taken), so a wave step
         // costs the lanes' largest TOTAL entry count, not the sum over the slots of each slot's
