@@ -896,14 +896,15 @@ __global__ __launch_bounds__(kBinThreads) void jb_bands(JBin a) {
     __syncthreads();
     // the next sub-chunk's coordinates are loaded while this one is sorted (lds_barrier: LDS only)
     double nx[PPT], ny[PPT];
+    // unconditional loads (index clamped into the chunk): a branch per load left the compiler a
+    // wait for every earlier memory operation in front of each one
     auto fetch = [&](uint64_t sb) {
 #pragma unroll
         for (int k = 0; k < PPT; k++) {
             const uint64_t i = sb + threadIdx.x + (uint64_t)k * kBinThreads;
-            if (i < b1) {
-                nx[k] = a.x[i];
-                ny[k] = a.y[i];
-            }
+            const uint64_t ic = i < b1 ? i : b1 - 1;
+            nx[k] = a.x[ic];
+            ny[k] = a.y[ic];
         }
     };
     if (b0 < b1) fetch(b0);
@@ -1101,6 +1102,10 @@ __global__ __launch_bounds__(kBinThreads) void jb_segs(JBin a) {
 // A round's segments come into LDS in windows of kJbSegBatch; each record finds its segment by a
 // wave-uniform binary search and a per-lane forward step; the round is sorted by tile in LDS and
 // each tile's run reserved with one atomic on its cursor.
+#ifndef GEOHIP_JB_ABL
+#define GEOHIP_JB_ABL 0  // measurement builds only: 1 no record stores, 2 no tile-cursor atomics (each
+                         // round's records kept in place), 4 the join step ends after the binning
+#endif
 __global__ __launch_bounds__(kJbL2Threads) void jb_tiles(JBin a) {
     constexpr int PPT = kJbRound / kJbL2Threads;
     constexpr unsigned kWin = kJbL2Threads;  // segments per window
@@ -1111,14 +1116,21 @@ __global__ __launch_bounds__(kJbL2Threads) void jb_tiles(JBin a) {
     const unsigned nround = a.nround[0];
     const int wid = threadIdx.x / kWave;
     for (unsigned t = threadIdx.x; t < kBandTiles; t += kJbL2Threads) lh[t] = 0;
+    uint4 ninfo = blockIdx.x < nround ? a.rinfo[blockIdx.x] : make_uint4(0u, 0u, 0u, 0u);
     for (unsigned r = blockIdx.x; r < nround; r += gridDim.x) {
-        const uint4 info = a.rinfo[r];
+        const uint4 info = ninfo;
+        if (r + gridDim.x < nround) ninfo = a.rinfo[r + gridDim.x];  // the next round's, in flight meanwhile
         const unsigned b = info.x, v0 = info.z, v1 = info.w;
         const unsigned nne = a.nne[b];
         const unsigned* spre = a.spre + (size_t)b * (nseg + 1);
         const unsigned* sst = a.sst + (size_t)b * nseg;
         uint4 rec[PPT];
         unsigned bin[PPT], rk[PPT];
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            rec[k] = make_uint4(0u, 0u, 0u, 0u);
+            bin[k] = rk[k] = 0u;
+        }
         unsigned wb = info.y;  // the window's first segment
         for (;;) {
             const unsigned wl = nne - wb < kWin ? nne - wb : kWin;
@@ -1130,10 +1142,17 @@ __global__ __launch_bounds__(kJbL2Threads) void jb_tiles(JBin a) {
             if (threadIdx.x == 0) wpre[wl] = spre[wb + wl];
             __syncthreads();
             const unsigned wlo = wpre[0], whi = wpre[wl];
+            // the PPT record addresses first, then their loads together, then the bins: one
+            // global round trip per window instead of one per record (each bin's LDS atomic
+            // used to wait for its record before the next load was issued)
+            unsigned src[PPT];
+            bool has[PPT];
 #pragma unroll
             for (int k = 0; k < PPT; k++) {
                 const unsigned v = v0 + threadIdx.x + k * kJbL2Threads;
                 const unsigned vw = v0 + (unsigned)(wid * kWave) + k * kJbL2Threads;  // the wave's first
+                has[k] = false;
+                src[k] = 0;
                 if (vw + kWave > wlo && vw < whi && vw < v1) {  // wave-uniform: some lane in this window
                     const unsigned key = vw > wlo ? vw : wlo;
                     unsigned lo = 0, hi = wl;  // largest j with wpre[j] <= key
@@ -1145,19 +1164,33 @@ __global__ __launch_bounds__(kJbL2Threads) void jb_tiles(JBin a) {
                     if (v >= wlo && v < whi && v < v1) {
                         unsigned j = lo;
                         while (wpre[j + 1] <= v) j++;
-                        rec[k] = a.l1[wst[j] + (v - wpre[j])];
-                        bin[k] = (rec[k].w >> 20) & (kBandTiles - 1);
-                        rk[k] = atomicAdd(&lh[bin[k]], 1u);
+                        has[k] = true;
+                        src[k] = wst[j] + (v - wpre[j]);
                     }
                 }
+            }
+            uint4 got[PPT];
+#pragma unroll
+            for (int k = 0; k < PPT; k++) got[k] = a.l1[src[k]];  // unconditional (src 0 when none): no branch per load
+#pragma unroll
+            for (int k = 0; k < PPT; k++) {
+                rec[k].x = has[k] ? got[k].x : rec[k].x;  // selects, not stores under a branch (kept in VGPRs)
+                rec[k].y = has[k] ? got[k].y : rec[k].y;
+                rec[k].z = has[k] ? got[k].z : rec[k].z;
+                rec[k].w = has[k] ? got[k].w : rec[k].w;
+                const unsigned bk = (got[k].w >> 20) & (kBandTiles - 1);
+                bin[k] = has[k] ? bk : bin[k];
+                if (has[k]) rk[k] = atomicAdd(&lh[bk], 1u);
             }
             if (whi >= v1 || wb + wl >= nne) break;
             wb += wl;
         }
         __syncthreads();
         lds_bins_scan(lh, ls, kBandTiles);
-        if (threadIdx.x < kBandTiles && lh[threadIdx.x])
-            base[threadIdx.x] = atomicAdd(&a.tcur[b * kBandTiles + threadIdx.x], lh[threadIdx.x]);
+        if (threadIdx.x < kBandTiles && lh[threadIdx.x]) {
+            if (GEOHIP_JB_ABL & 2) base[threadIdx.x] = v0 + ls[threadIdx.x];
+            else base[threadIdx.x] = atomicAdd(&a.tcur[b * kBandTiles + threadIdx.x], lh[threadIdx.x]);
+        }
         __syncthreads();
         const unsigned m = v1 - v0;
 #pragma unroll
@@ -1173,7 +1206,7 @@ __global__ __launch_bounds__(kJbL2Threads) void jb_tiles(JBin a) {
                 const uint4 q = st[j];
                 const unsigned bq = (q.w >> 20) & (kBandTiles - 1);
                 const unsigned p = base[bq] + (j - ls[bq]);
-                if (p < a.n) a.recs[p] = q;  // bounded even if the counts were not the binning's own
+                if (p < a.n && !(GEOHIP_JB_ABL & 1)) a.recs[p] = q;  // bounded even if the counts were not the binning's own
             }
         }
         lds_barrier();
@@ -4183,6 +4216,7 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
     const unsigned* tstart = nullptr;
     rc = join_bin(ctx, S, ddx, ddy, nd, geo, tcnt, &recs, &tstart);
     if (rc) return rc;
+    if (GEOHIP_JB_ABL) nq = 0;  // measurement builds: no join over ablated records
     tlaunch(ctx, join_plan, 1, kBinThreads, 0, st, tstart, (const unsigned*)qstart, (const unsigned*)(misc + 5), geo.ntiles,
             istart);
     tlaunch(ctx, join_item_fill, (unsigned)((ntl + kTB - 1) / kTB), kTB, 0, st, (const unsigned*)istart, geo.ntiles, items);
