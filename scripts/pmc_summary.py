@@ -30,17 +30,19 @@ _PS = {"ppoly_stream": 1, "ppoly_cand_hist": 1, "ppoly_cand_plan": 1, "ppoly_can
 # add/mul per point in its ISA, 50M points -> 4,687,500 counted = 300M / 64), so lane FLOPs are
 # the counted value times 64 (issued lanes: a divergent wave's idle lanes are included).
 FP64_LANES = 64
+# r04 join step: query lists, two binning passes into 16-B records, plan, one join pass
+_JOIN = {"fill_words": 1, "jq_rect": 1, "jq_build<false>": 1, "jq_build<true>": 1, "jq_starts": 1, "jb_bands": 1,
+         "jb_scan": 1, "jb_segs": 1, "jb_tiles": 1, "join_plan": 1, "join_item_fill": 1, "join_fused<false, true>": 1}
+_PS = {**_PS, "fill_words": 1}
 TAGS = {"knn": ("knn_scan", {"knn_pass": 1}),
         "range": ("range", {"range_fused": 1, "range_scan": 1, "scan_units": 1, "range_emit": 1}),
-        "join": ("join_probe", {**_BIN, "scan_seg_totals<unsigned int>": 3, "scan_totals<unsigned int>": 3,
-                                "scan_apply<unsigned int>": 3, "jq_rect": 1, "jq_build<false>": 1, "jq_build<true>": 1,
-                                "join_items": 1, "join_item_fill": 1, "join_fused<false, true>": 1}),
+        "join": ("join_probe", _JOIN),
         "ppoly": ("ppoly_probe", _PS),
         "c5": ("knn_scan_c5", {"knn_pass": 1}),
         "ingest": ("ingest", {"ingest_fused": 1, "ingest_general": 1}),
         "ppjoin": ("ppjoin", _PS),
         "ppknn": ("ppknn", {"rsel_init": 1, "rsel_small": 1, "ppknn_scan_boxes": 1, "ppknn_dist": 1}),
-        "knn_incr": ("knn_incr", {"knn_pass": 1, "knn_final": 1}),
+        "knn_incr": ("knn_incr", {"knn_pass": 1, "knn_merge_panes": 1}),
         "ppoly_incr": ("ppoly_incr", _PS)}
 
 

@@ -939,8 +939,10 @@ int geohip_knn_merge_panes_async(geohip_ctx* ctx, const double* ring_dist, const
     pm.n = npanes;
     pm.list_len = list_len;
     pm.k = k;
+    hipEvent_t ev0, ev1;
+    timed_pair(ctx, &ev0, &ev1, 1);  // one kernel of the pane step (the pane's scan is the other)
     hipError_t e = launch_knn_merge_panes(reinterpret_cast<const unsigned long long*>(ring_dist), ring_idx, pm,
-                                          out_dist, out_idx, out_count_dev, ctx->stream);
+                                          out_dist, out_idx, out_count_dev, ctx->stream, ev0, ev1);
     if (e != hipSuccess) return hip_fail(ctx, e, "pane merge launch");
     return GEOHIP_OK;
 }

@@ -5447,7 +5447,7 @@ int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, co
     static const char* env_small = getenv("GEOHIP_RSEL_SMALL");
     const bool multi = big_k || (env_small ? true : kc->last_m > kRselSmall);
     const unsigned small_max = big_k ? 0u : (env_small ? (unsigned)atol(env_small) : (multi ? 0u : 0xffffffffu));
-    rsel_init<<<1, 1024, 0, st>>>(rs, k, small_max);
+    tlaunch(ctx, rsel_init, 1, 1024, 0, st, rs, k, small_max);
     if (big_k && hipMemsetAsync(L.sel_d, 0xff, (size_t)kout * 12, st) != hipSuccess)
         return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");
     if (n && nrect) {
@@ -5456,33 +5456,33 @@ int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, co
             static const uint64_t max_blocks = getenv("GEOHIP_PPKNN_BLOCKS") ? (uint64_t)atol(getenv("GEOHIP_PPKNN_BLOCKS")) : 2048;
             const uint64_t nb = std::max<uint64_t>(1, std::min<uint64_t>((iters + 3) / 4, max_blocks));  // 4 waves per block
             switch (PB.nb) {
-                case 1: ppknn_scan_boxes<1><<<(unsigned)nb, kTB, 0, st>>>(dx, dy, n, PB, cand, rs); break;
-                case 2: ppknn_scan_boxes<2><<<(unsigned)nb, kTB, 0, st>>>(dx, dy, n, PB, cand, rs); break;
-                case 3: ppknn_scan_boxes<3><<<(unsigned)nb, kTB, 0, st>>>(dx, dy, n, PB, cand, rs); break;
-                case 4: ppknn_scan_boxes<4><<<(unsigned)nb, kTB, 0, st>>>(dx, dy, n, PB, cand, rs); break;
-                default: ppknn_scan_boxes<0><<<(unsigned)nb, kTB, 0, st>>>(dx, dy, n, PB, cand, rs); break;
+                case 1: tlaunch(ctx, ppknn_scan_boxes<1>, (unsigned)nb, kTB, 0, st, dx, dy, n, PB, cand, rs); break;
+                case 2: tlaunch(ctx, ppknn_scan_boxes<2>, (unsigned)nb, kTB, 0, st, dx, dy, n, PB, cand, rs); break;
+                case 3: tlaunch(ctx, ppknn_scan_boxes<3>, (unsigned)nb, kTB, 0, st, dx, dy, n, PB, cand, rs); break;
+                case 4: tlaunch(ctx, ppknn_scan_boxes<4>, (unsigned)nb, kTB, 0, st, dx, dy, n, PB, cand, rs); break;
+                default: tlaunch(ctx, ppknn_scan_boxes<0>, (unsigned)nb, kTB, 0, st, dx, dy, n, PB, cand, rs); break;
             }
         } else {
             const uint64_t nb = std::min<uint64_t>((n + kTB - 1) / kTB, 4096);
-            ppknn_scan<<<(unsigned)nb, kTB, 0, st>>>(dx, dy, n, grid->min_x, grid->min_y, grid->cell_len, drect, nrect,
+            tlaunch(ctx, ppknn_scan, (unsigned)nb, kTB, 0, st, dx, dy, n, grid->min_x, grid->min_y, grid->cell_len, drect, nrect,
                                                      cand, rs);
         }
-        if (approximate) ppknn_dist<true><<<1024, kTB, 0, st>>>(dx, dy, cand, rs, dvx, dvy, dvr, denv, P, key);
-        else ppknn_dist<false><<<1024, kTB, 0, st>>>(dx, dy, cand, rs, dvx, dvy, dvr, denv, P, key);
+        if (approximate) tlaunch(ctx, ppknn_dist<true>, 1024, kTB, 0, st, dx, dy, cand, rs, dvx, dvy, dvr, denv, P, key);
+        else tlaunch(ctx, ppknn_dist<false>, 1024, kTB, 0, st, dx, dy, cand, rs, dvx, dvy, dvr, denv, P, key);
     }
     if (big_k) {
         rc = rsel_large_tail(st, key, cand, rs, k, L.sel_d, L.sel_i, L.tmp_d, L.tmp_i, L.temp, L.temp_bytes, od, oi,
                              ocnt);
         if (rc) return ctx_fail(ctx, rc, "large-k kNN launch failed");
     } else {
-        rsel_small<<<1, 1024, 0, st>>>(key, cand, rs, k, od, oi, ocnt);  // M <= small_max (and M = 0)
+        tlaunch(ctx, rsel_small, 1, 1024, 0, st, key, cand, rs, k, od, oi, ocnt);  // M <= small_max (and M = 0)
         if (multi) {
             for (int t = 0; t < kRselRounds; t++) {
-                rsel_hist<<<512, kTB, 0, st>>>(key, cand, rs, t, k);
-                rsel_pick<<<1, 1024, 0, st>>>(rs, t, k);
+                tlaunch(ctx, rsel_hist, 512, kTB, 0, st, key, cand, rs, t, k);
+                tlaunch(ctx, rsel_pick, 1, 1024, 0, st, rs, t, k);
             }
-            rsel_gather<<<512, kTB, 0, st>>>(key, cand, rs, k, L.sel_d, L.sel_i);
-            rsel_sort<<<1, 256, 0, st>>>(L.sel_d, L.sel_i, rs, k, od, oi, ocnt);
+            tlaunch(ctx, rsel_gather, 512, kTB, 0, st, key, cand, rs, k, L.sel_d, L.sel_i);
+            tlaunch(ctx, rsel_sort, 1, 256, 0, st, L.sel_d, L.sel_i, rs, k, od, oi, ocnt);
         }
     }
     if (e1) hipEventRecord(e1, st);

@@ -69,7 +69,8 @@ struct PaneMerge {
     unsigned n, list_len, k, pad;
 };
 hipError_t launch_knn_merge_panes(const unsigned long long* ring_d, const unsigned* ring_i, const PaneMerge& pm,
-                                  double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st);
+                                  double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st,
+                                  hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);  // timed: the kernel's stamps
 // range: bitmask (16 words / 1024 pts), unit_count (units), offs (units) scratch.
 // the range runs as one fused kernel at this window size (else three launches)
 bool range_is_one_kernel(uint64_t n);

@@ -2213,9 +2213,11 @@ __global__ __launch_bounds__(256) void knn_merge_panes(const unsigned long long*
 }
 
 hipError_t launch_knn_merge_panes(const unsigned long long* ring_d, const unsigned* ring_i, const PaneMerge& pm,
-                                  double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st) {
+                                  double* out_d, unsigned* out_i, unsigned* out_count, hipStream_t st, hipEvent_t ev0,
+                                  hipEvent_t ev1) {
     const unsigned m = pm.n * pm.list_len > pm.k ? pm.n * pm.list_len : pm.k;
-    knn_merge_panes<<<(m + 255) / 256, 256, 0, st>>>(ring_d, ring_i, pm, out_d, out_i, out_count);
+    hipExtLaunchKernelGGL(knn_merge_panes, dim3((m + 255) / 256), dim3(256), 0, st, ev0, ev1, 0, ring_d, ring_i, pm, out_d,
+                          out_i, out_count);
     return hipGetLastError();
 }
 
