@@ -848,6 +848,12 @@ struct JBin {
     uint4* rinfo;       // level-2 rounds: (band, first segment, first record, end record)
     unsigned* nround;   // [1]
     uint4* recs;        // tile-sorted records
+    // the join's work items, planned by the same launches: per tile ceil(points / kJP) x
+    // ceil(queries / kJQ) items (istart by jb_scan, the item list by jb_segs)
+    const unsigned* qstart;  // [ntiles + 1] per-tile query list starts
+    const unsigned* gcnt;    // [1] queries every tile checks (global mode)
+    unsigned* istart;        // [ntiles + 1]
+    uint2* items;            // (tile, item within the tile)
 };
 
 __device__ __forceinline__ uint4 jb_record(const TileGeom& g, double x, double y, unsigned idx, bool& in, unsigned& tile) {
@@ -1003,7 +1009,10 @@ __device__ __forceinline__ unsigned block_scan_passes(unsigned n, unsigned* wsum
     return total;
 }
 
-// Tile starts and cursors from the tile counts (one block).
+// Tile starts and cursors from the tile counts, then the join's item starts from the same counts
+// and the query list starts (one block; was a separate join_plan launch).
+constexpr unsigned kJP = 1024;      // points per join work item (4 waves x 4 chunks of 64)
+constexpr unsigned kJQ = 128;       // queries per join work item
 __global__ __launch_bounds__(kBinThreads) void jb_scan(JBin a) {
     __shared__ unsigned wsum[kScanPasses * (kBinThreads / kWave)];
     const unsigned total = block_scan_passes(
@@ -1013,6 +1022,17 @@ __global__ __launch_bounds__(kBinThreads) void jb_scan(JBin a) {
             a.tcur[t] = ex;
         });
     if (threadIdx.x == 0) a.tstart[a.g.ntiles] = total;
+    __syncthreads();  // wsum is reused
+    const unsigned gq = *a.gcnt;
+    const unsigned items = block_scan_passes(
+        a.g.ntiles, wsum,
+        [&](unsigned t) {
+            const unsigned np = a.tcnt[t];
+            const unsigned nq = a.qstart[t + 1] - a.qstart[t] + gq;
+            return (np == 0 || nq == 0) ? 0u : ((np + kJP - 1) / kJP) * ((nq + kJQ - 1) / kJQ);
+        },
+        [&](unsigned t, unsigned, unsigned ex) { a.istart[t] = ex; });
+    if (threadIdx.x == 0) a.istart[a.g.ntiles] = items;
 }
 
 // Level-2 rounds: each band's records, in (level-1 block, sub-chunk) order, cut into rounds of
@@ -1095,6 +1115,12 @@ __global__ __launch_bounds__(kBinThreads) void jb_segs(JBin a) {
     if (threadIdx.x == 0) {
         spre[carry_ne] = carry_len;  // = T: the end of the last segment
         a.nne[b] = carry_ne;
+    }
+    // the join's work items of this band's tiles (was a separate join_item_fill launch)
+    const unsigned t0 = b * kBandTiles, t1 = t0 + kBandTiles < a.g.ntiles ? t0 + kBandTiles : a.g.ntiles;
+    for (unsigned t = t0 + (unsigned)wid; t < t1; t += kBinThreads / kWave) {
+        const unsigned ib = a.istart[t], ie = a.istart[t + 1];
+        for (unsigned k = ib + (unsigned)lane; k < ie; k += kWave) a.items[k] = make_uint2(t, k - ib);
     }
 }
 
@@ -1236,10 +1262,14 @@ __global__ __launch_bounds__(kJbL2Threads) void jb_tiles(JBin a) {
 // in fp32.  With A >= |p - o| + |q - o| on both axes over the item and u = 2^-24,
 // |dx' - dx| <= e = 2.05 u A, so |d2' - d2| <= 4 e A + 2 e^2 + 3 u d2'.  d2' below lo (above hi)
 // puts the true d2 below r2lo (above r2hi), where the fp64 screens already decide (kSqLo/kSqHi).
-constexpr unsigned kJP = 1024;      // points per item (4 waves x 4 chunks of 64)
-constexpr unsigned kJQ = 128;       // queries per item
 constexpr unsigned kJCh = kJP / kWave / (kTB / kWave);  // chunks per wave and item
-constexpr unsigned kJBlocksW = 1024;  // persistent grid, write pass (37 KB LDS: 4 blocks per CU)
+#ifndef GEOHIP_JBLOCKSW
+#define GEOHIP_JBLOCKSW 1024
+#endif
+#ifndef GEOHIP_JSTAGE
+#define GEOHIP_JSTAGE 512
+#endif
+constexpr unsigned kJBlocksW = GEOHIP_JBLOCKSW;  // persistent grid, write pass (37 KB LDS: 4 blocks per CU)
 constexpr unsigned kJBlocksC = 1280;  // count pass (4 KB LDS, 83 VGPRs: 5 blocks per CU)
 
 // query list starts per tile (one block)
@@ -1251,31 +1281,6 @@ __global__ __launch_bounds__(kBinThreads) void jq_starts(const unsigned* __restr
     if (threadIdx.x == 0) qstart[ntiles] = total;
 }
 
-// Work items (one block): per tile ceil(points / kJP) * ceil(queries / kJQ) and their starts
-__global__ __launch_bounds__(kBinThreads) void join_plan(const unsigned* __restrict__ tstart,
-                                                          const unsigned* __restrict__ qstart,
-                                                          const unsigned* __restrict__ gcnt, uint32_t ntiles,
-                                                          unsigned* __restrict__ istart) {
-    __shared__ unsigned wsum[kScanPasses * (kBinThreads / kWave)];
-    const unsigned gq = *gcnt;
-    const unsigned total = block_scan_passes(
-        ntiles, wsum,
-        [&](unsigned t) {
-            const unsigned np = tstart[t + 1] - tstart[t];
-            const unsigned nq = qstart[t + 1] - qstart[t] + gq;
-            return (np == 0 || nq == 0) ? 0u : ((np + kJP - 1) / kJP) * ((nq + kJQ - 1) / kJQ);
-        },
-        [&](unsigned t, unsigned, unsigned ex) { istart[t] = ex; });
-    if (threadIdx.x == 0) istart[ntiles] = total;
-}
-
-// item descriptors (tile, index inside the tile), one thread per tile
-__global__ void join_item_fill(const unsigned* __restrict__ istart, uint32_t ntiles, uint2* __restrict__ items) {
-    const unsigned t = blockIdx.x * kTB + threadIdx.x;
-    if (t >= ntiles) return;
-    const unsigned b = istart[t], e = istart[t + 1];
-    for (unsigned k = b; k < e; k++) items[k] = make_uint2(t, k - b);
-}
 
 struct JoinRun {
     const uint4* recs;       // tile-sorted point records (jb_tiles)
@@ -1373,7 +1378,7 @@ __device__ __forceinline__ void jpart_quad(const JoinRun& a, const JPart* __rest
 // A wave's pair stage: pairs leave in contiguous runs of full 512-B wave stores.  (One store per
 // (chunk, query) straight from the ballots -- no stage -- measured slower: 1.13 ms against 1.04 ms
 // for C3's write pass; the partial-wave stores are ~3x as many instructions for the same bytes.)
-constexpr unsigned kJStage = 512;   // pairs per wave (4 KB)
+constexpr unsigned kJStage = GEOHIP_JSTAGE;   // pairs per wave (4 KB)
 __device__ __forceinline__ void jstage_flush(const JoinRun& a, uint2* st, unsigned& cnt, unsigned long long& pos) {
     wave_lds_sync();
     for (unsigned t = (unsigned)lane_id(); t < cnt; t += kWave) {
@@ -4065,7 +4070,8 @@ int bin_tiles(geohip_ctx* ctx, Scratch& S, const double* dx, const double* dy, u
 // Join binning (jb_bands / jb_scan / jb_segs / jb_tiles): the window's in-grid points as
 // tile-sorted 16-B records; *recs and *tstart (ntiles + 1) on the device.
 int join_bin(geohip_ctx* ctx, Scratch& S, const double* dx, const double* dy, uint64_t n, const TileGeom& geo,
-             unsigned* tcnt, const uint4** recs, const unsigned** tstart) {
+             unsigned* tcnt, const unsigned* qstart, const unsigned* gcnt, unsigned* istart, uint2* items,
+             const uint4** recs, const unsigned** tstart) {
     hipStream_t st = ctx_stream(ctx);
     uint64_t nblk = (n + 16383) / 16384;
     if (nblk > kJbBlocks) nblk = kJbBlocks;
@@ -4097,6 +4103,10 @@ int join_bin(geohip_ctx* ctx, Scratch& S, const double* dx, const double* dy, ui
     a.nne = a.sst + (size_t)a.nbands * nseg;
     a.nround = a.nne + a.nbands;
     a.tcnt = tcnt;  // zero on entry: part of the step's zero block, no state carried between calls
+    a.qstart = qstart;
+    a.gcnt = gcnt;
+    a.istart = istart;
+    a.items = items;
     if (n) tlaunch(ctx, jb_bands, (unsigned)nblk, kBinThreads, 0, st, a);
     tlaunch(ctx, jb_scan, 1, kBinThreads, 0, st, a);
     if (n) {
@@ -4214,12 +4224,9 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
     }
     const uint4* recs = nullptr;
     const unsigned* tstart = nullptr;
-    rc = join_bin(ctx, S, ddx, ddy, nd, geo, tcnt, &recs, &tstart);
+    rc = join_bin(ctx, S, ddx, ddy, nd, geo, tcnt, qstart, misc + 5, istart, items, &recs, &tstart);
     if (rc) return rc;
     if (GEOHIP_JB_ABL) nq = 0;  // measurement builds: no join over ablated records
-    tlaunch(ctx, join_plan, 1, kBinThreads, 0, st, tstart, (const unsigned*)qstart, (const unsigned*)(misc + 5), geo.ntiles,
-            istart);
-    tlaunch(ctx, join_item_fill, (unsigned)((ntl + kTB - 1) / kTB), kTB, 0, st, (const unsigned*)istart, geo.ntiles, items);
     // output: device pointer directly, or a device staging buffer for host output
     unsigned* out = nullptr;
     if (!count_only && cap) {
