@@ -1264,12 +1264,15 @@ __global__ __launch_bounds__(kJbL2Threads) void jb_tiles(JBin a) {
 // puts the true d2 below r2lo (above r2hi), where the fp64 screens already decide (kSqLo/kSqHi).
 constexpr unsigned kJCh = kJP / kWave / (kTB / kWave);  // chunks per wave and item
 #ifndef GEOHIP_JBLOCKSW
-#define GEOHIP_JBLOCKSW 1024
+#define GEOHIP_JBLOCKSW 768
 #endif
 #ifndef GEOHIP_JSTAGE
-#define GEOHIP_JSTAGE 512
+#define GEOHIP_JSTAGE 768
 #endif
-constexpr unsigned kJBlocksW = GEOHIP_JBLOCKSW;  // persistent grid, write pass (37 KB LDS: 4 blocks per CU)
+// persistent grid of the write pass: 45 KB of LDS with 768-pair stages, 3 blocks per CU.  C3 kernel
+// sums, one box: stage 512 at 4 blocks per CU 1278 us; 640 / 768 / 896 at 3: 1265 / 1262 / 1262;
+// 1024 at 2: 1360; 320 at 5: 1333
+constexpr unsigned kJBlocksW = GEOHIP_JBLOCKSW;
 constexpr unsigned kJBlocksC = 1280;  // count pass (4 KB LDS, 83 VGPRs: 5 blocks per CU)
 
 // query list starts per tile (one block)
@@ -1378,7 +1381,7 @@ __device__ __forceinline__ void jpart_quad(const JoinRun& a, const JPart* __rest
 // A wave's pair stage: pairs leave in contiguous runs of full 512-B wave stores.  (One store per
 // (chunk, query) straight from the ballots -- no stage -- measured slower: 1.13 ms against 1.04 ms
 // for C3's write pass; the partial-wave stores are ~3x as many instructions for the same bytes.)
-constexpr unsigned kJStage = GEOHIP_JSTAGE;   // pairs per wave (4 KB)
+constexpr unsigned kJStage = GEOHIP_JSTAGE;   // pairs per wave (6 KB)
 __device__ __forceinline__ void jstage_flush(const JoinRun& a, uint2* st, unsigned& cnt, unsigned long long& pos) {
     wave_lds_sync();
     for (unsigned t = (unsigned)lane_id(); t < cnt; t += kWave) {
