@@ -827,9 +827,15 @@ __global__ void jq_global(uint64_t nq, unsigned* __restrict__ glist, unsigned* _
 // join's decisions are per point, and its pair order was never fixed.
 constexpr unsigned kJbSub = 4096;     // points per local sort round (4 per thread)
 constexpr unsigned kJbBlocks = 256;   // level-1 blocks
+#ifndef GEOHIP_JB_ROUND
+#define GEOHIP_JB_ROUND 2048
+#endif
+#ifndef GEOHIP_JB_L2BLOCKS
+#define GEOHIP_JB_L2BLOCKS 1024
+#endif
 constexpr unsigned kJbL2Threads = 512;  // level 2: rounds of kJbRound records, 4 blocks per CU
-constexpr unsigned kJbRound = 2048;
-constexpr unsigned kJbL2Blocks = 1024;
+constexpr unsigned kJbRound = GEOHIP_JB_ROUND;
+constexpr unsigned kJbL2Blocks = GEOHIP_JB_L2BLOCKS;
 
 struct JBin {
     const double* x;
