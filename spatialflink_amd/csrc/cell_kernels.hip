@@ -1021,23 +1021,24 @@ constexpr unsigned kJP = 1024;      // points per join work item (4 waves x 4 ch
 constexpr unsigned kJQ = 128;       // queries per join work item
 __global__ __launch_bounds__(kBinThreads) void jb_scan(JBin a) {
     __shared__ unsigned wsum[kScanPasses * (kBinThreads / kWave)];
+    __shared__ unsigned sitems[kMaxTiles];  // item counts, formed while the tile counts load
+    const unsigned gq = *a.gcnt;
     const unsigned total = block_scan_passes(
-        a.g.ntiles, wsum, [&](unsigned t) { return a.tcnt[t]; },
+        a.g.ntiles, wsum,
+        [&](unsigned t) {
+            const unsigned np = a.tcnt[t];
+            const unsigned nq = a.qstart[t + 1] - a.qstart[t] + gq;
+            sitems[t] = (np == 0 || nq == 0) ? 0u : ((np + kJP - 1) / kJP) * ((nq + kJQ - 1) / kJQ);
+            return np;
+        },
         [&](unsigned t, unsigned, unsigned ex) {
             a.tstart[t] = ex;
             a.tcur[t] = ex;
         });
     if (threadIdx.x == 0) a.tstart[a.g.ntiles] = total;
-    __syncthreads();  // wsum is reused
-    const unsigned gq = *a.gcnt;
+    __syncthreads();  // wsum is reused; sitems complete
     const unsigned items = block_scan_passes(
-        a.g.ntiles, wsum,
-        [&](unsigned t) {
-            const unsigned np = a.tcnt[t];
-            const unsigned nq = a.qstart[t + 1] - a.qstart[t] + gq;
-            return (np == 0 || nq == 0) ? 0u : ((np + kJP - 1) / kJP) * ((nq + kJQ - 1) / kJQ);
-        },
-        [&](unsigned t, unsigned, unsigned ex) { a.istart[t] = ex; });
+        a.g.ntiles, wsum, [&](unsigned t) { return sitems[t]; }, [&](unsigned t, unsigned, unsigned ex) { a.istart[t] = ex; });
     if (threadIdx.x == 0) a.istart[a.g.ntiles] = items;
 }
 
