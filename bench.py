@@ -538,7 +538,7 @@ class JoinWorkload(Workload):
     window, 500x500, r = 0.05 (32 shared centres, sigma 0.1)."""
     tag = "join_probe"
     kernel = ("geohip join step: query block lists (jq_rect / jq_build / jq_starts), tile binning into 16-B "
-              "records (jb_bands / jb_scan / jb_segs / jb_tiles), join_plan / join_item_fill, join_fused (work "
+              "records with the work-item plan (jb_bands / jb_scan / jb_segs / jb_tiles), join_fused (work "
               "items, decoupled look-back, LDS-staged 512-B pair stores); every kernel timed by its dispatch stamps")
     grid_n, radius, n_default, nq, sigma = 500, 0.05, 10_000_000, 10_000, 0.1
     windows = 2

@@ -32,7 +32,7 @@ _PS = {"ppoly_stream": 1, "ppoly_cand_hist": 1, "ppoly_cand_plan": 1, "ppoly_can
 FP64_LANES = 64
 # r04 join step: query lists, two binning passes into 16-B records, plan, one join pass
 _JOIN = {"fill_words": 1, "jq_rect": 1, "jq_build<false>": 1, "jq_build<true>": 1, "jq_starts": 1, "jb_bands": 1,
-         "jb_scan": 1, "jb_segs": 1, "jb_tiles": 1, "join_plan": 1, "join_item_fill": 1, "join_fused<false, true>": 1}
+         "jb_scan": 1, "jb_segs": 1, "jb_tiles": 1, "join_fused<false, true>": 1}
 _PS = {**_PS, "fill_words": 1}
 TAGS = {"knn": ("knn_scan", {"knn_pass": 1}),
         "range": ("range", {"range_fused": 1, "range_scan": 1, "scan_units": 1, "range_emit": 1}),
