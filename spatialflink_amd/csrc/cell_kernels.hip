@@ -3081,17 +3081,26 @@ __global__ __launch_bounds__(kTB) void ppoly_cand_eval(CandGroup c, const PolyDe
         // the slice (<= kCandItem) in registers, its slab histogram in LDS
         double qx[kPer], qy[kPer];
         unsigned qi[kPer], qs[kPer];
+        // slot indices for every u first, then every record, then the slabs: two global round
+        // trips per item instead of two per u (a load under a branch made the compiler wait for it
+        // before issuing the next); lanes past the slice read the item's first slot
+        unsigned sid[kPer];
+#pragma unroll
+        for (unsigned u = 0; u < kPer; u++) {
+            const unsigned t = threadIdx.x + u * kTB;
+            sid[u] = c.sidx[w.y + (t < m ? t : 0u)];
+        }
+        double4 rcs[kPer];
+#pragma unroll
+        for (unsigned u = 0; u < kPer; u++) rcs[u] = c.crec[sid[u]];
 #pragma unroll
         for (unsigned u = 0; u < kPer; u++) {
             const unsigned t = threadIdx.x + u * kTB;
             qs[u] = 0;
-            if (t < m) {
-                const double4 rc = c.crec[c.sidx[w.y + t]];
-                qx[u] = rc.x;
-                qy[u] = rc.y;
-                qi[u] = (unsigned)__double_as_longlong(rc.z);
-                if (P.ns) qs[u] = slab_of(qy[u], P.sy0, P.sinv, P.ns);
-            }
+            qx[u] = rcs[u].x;
+            qy[u] = rcs[u].y;
+            qi[u] = (unsigned)__double_as_longlong(rcs[u].z);
+            if (t < m && P.ns) qs[u] = slab_of(qy[u], P.sy0, P.sinv, P.ns);
         }
         __syncthreads();
 #pragma unroll
