@@ -17,53 +17,18 @@ import numpy as np
 import pytest
 
 import cref
+from helpers import MASK, pair_digest
 from spatialflink_amd import _abi, synth
 
 pytestmark = pytest.mark.gpu
 
 BJ = synth.BEIJING
 Q = synth.README_QUERY
-MASK = (1 << 64) - 1
 
 
 def agrid(n):
     l = (BJ[1] - BJ[0]) / n
     return _abi.make_grid(BJ[0], BJ[2], l, n), cref.grid(BJ[0], BJ[2], l, n)
-
-
-def _s64(c):  # an unsigned 64-bit constant as the int64 torch holds it
-    return c - (1 << 64) if c >= 1 << 63 else c
-
-
-def _lsr(z, s):  # logical right shift of int64 lanes
-    import torch
-    return torch.bitwise_and(torch.bitwise_right_shift(z, s), (1 << (64 - s)) - 1)
-
-
-def mix64_torch(v):
-    """splitmix64 finaliser on int64 lanes (wrapping arithmetic), = cref.mix64 bit for bit."""
-    import torch
-    z = v + _s64(0x9E3779B97F4A7C15)
-    z = torch.bitwise_xor(z, _lsr(z, 30)) * _s64(0xBF58476D1CE4E5B9)
-    z = torch.bitwise_xor(z, _lsr(z, 27)) * _s64(0x94D049BB133111EB)
-    return torch.bitwise_xor(z, _lsr(z, 31))
-
-
-def pair_digest(pairs, chunk=1 << 26):
-    """(count, sum of mix64(a << 32 | b) mod 2^64) of an [m, 2] int32 device tensor of pairs."""
-    import torch
-    m = int(pairs.shape[0])
-    h = 0
-    for s in range(0, m, chunk):
-        p = pairs[s:s + chunk].to(torch.int64)
-        v = torch.bitwise_or(torch.bitwise_left_shift(torch.bitwise_and(p[:, 0], 0xFFFFFFFF), 32),
-                             torch.bitwise_and(p[:, 1], 0xFFFFFFFF))
-        # int64 sums wrap like the oracle's uint64 sum; add the halves exactly in Python
-        z = mix64_torch(v)
-        lo = int(torch.bitwise_and(z, 0xFFFFFFFF).sum().item())
-        hi = int(_lsr(z, 32).sum().item())
-        h = (h + lo + (hi << 32)) & MASK
-    return m, h
 
 
 def test_digest_matches_oracle_mix(ctx):

@@ -1,0 +1,124 @@
+"""Point-point join at a mid size that reaches the binning and emission shapes the small join
+tests do not (PointPointJoinQuery.java:113-172, JoinQuery.java:73-90).
+
+Round 4's full-scale C3 test once failed with the right pair count and the wrong digest while
+every smaller join test passed: the window sizes of those tests never reach
+  * tiles with more than one level-2 round of records (kJbRound = 2048 records per round),
+  * bands whose records come from more than one window of segments in jb_tiles (a band has one
+    segment per level-1 sub-chunk holding its points; jb_tiles reads kWin = 512 of them at a
+    time, and a window has 4096-point sub-chunks, so only windows above ~2.1M points have
+    bands with more than 512 non-empty segments),
+  * full 64-point chunks whose ALL queries (every point of the tile within r) leave as 512-B
+    wave stores straight from registers, not through the LDS pair stage.
+These windows have 4M Gaussian points with tight clusters.  The test asserts on the host that the
+window reaches each shape (the geometry below mirrors join_bin / tile_geom in
+csrc/cell_kernels.hip), then compares the pair count and the order-independent 64-bit digest of
+the pair set with the C oracle (oracle/geohip_oracle.c, test infrastructure), in exact and
+approximate mode and through the count-only entry point.
+"""
+import numpy as np
+import pytest
+
+import cref
+from helpers import pair_digest
+from spatialflink_amd import _abi, synth
+
+pytestmark = pytest.mark.gpu
+
+BJ = synth.BEIJING
+
+# (points, data sigma, queries, query sigma, r): tiles of > 2048 and > 10k records, bands of up
+# to 980 non-empty segments, 4.4e7 .. 1.5e8 pairs
+SHAPES = [(4_000_000, 0.03, 2000, 0.03, 0.05), (4_000_000, 0.01, 1000, 0.02, 0.02)]
+
+
+def agrid(n):
+    l = (BJ[1] - BJ[0]) / n
+    return _abi.make_grid(BJ[0], BJ[2], l, n), cref.grid(BJ[0], BJ[2], l, n)
+
+
+def binning_shape(x, y, nb=500):
+    """(largest tile, tiles over one round, largest non-empty segment count of a band) of the
+    join binning for this window (join_bin: <= 256 level-1 blocks of >= 16384 points, 4096-point
+    sub-chunks, tiles of ceil(nb / 128) cells, 128 tiles per band)."""
+    n = len(x)
+    l = (BJ[1] - BJ[0]) / nb
+    ts = (nb + 127) // 128
+    nt = (nb + ts - 1) // ts
+    cx = np.floor((x - BJ[0]) / l).astype(np.int64)
+    cy = np.floor((y - BJ[2]) / l).astype(np.int64)
+    ok = (cx >= 0) & (cx < nb) & (cy >= 0) & (cy < nb)
+    tile = (cx // ts) * nt + cy // ts
+    cnt = np.bincount(tile[ok], minlength=nt * nt)
+    nblk = min(256, max(1, (n + 16383) // 16384))
+    chunk = (n + nblk - 1) // nblk
+    nsub = (chunk + 4095) // 4096
+    i = np.arange(n)
+    seg = (i // chunk) * nsub + (i % chunk) // 4096
+    key = (tile[ok] >> 7) * (nblk * nsub) + seg[ok]
+    band_of = np.unique(key) // (nblk * nsub)
+    return int(cnt.max()), int((cnt > 2048).sum()), int(np.bincount(band_of).max())
+
+
+def full_all_chunks(x, y, qx, qy, r, nb=500):
+    """Lower bound on the (tile, query) pairs whose query covers the whole tile (ALL) and whose
+    tile has at least 64 points: the full-chunk ALL emission runs for each."""
+    l = (BJ[1] - BJ[0]) / nb
+    ts = (nb + 127) // 128
+    nt = (nb + ts - 1) // ts
+    cx = np.floor((x - BJ[0]) / l).astype(np.int64) // ts
+    cy = np.floor((y - BJ[2]) / l).astype(np.int64) // ts
+    ok = (cx >= 0) & (cx < nt) & (cy >= 0) & (cy < nt)
+    cnt = np.bincount(cx[ok] * nt + cy[ok], minlength=nt * nt)
+    dense = np.nonzero(cnt >= 64)[0]
+    tx0 = BJ[0] + (dense // nt) * ts * l
+    ty0 = BJ[2] + (dense % nt) * ts * l
+    w = ts * l
+    hits = 0
+    for a, b in zip(qx, qy):  # farthest corner within r (with a margin): every point pairs
+        fx = np.maximum(np.abs(tx0 - a), np.abs(tx0 + w - a))
+        fy = np.maximum(np.abs(ty0 - b), np.abs(ty0 + w - b))
+        hits += int((fx * fx + fy * fy < (0.99 * r) ** 2).sum())
+    return hits
+
+
+@pytest.fixture(scope="module", params=range(len(SHAPES)), ids=["sigma0.03", "sigma0.01"])
+def mid_window(request):
+    import torch
+    n, sig, nq, qsig, r = SHAPES[request.param]
+    hx, hy = synth.gaussian_clusters(n, 11 + request.param, sigma=sig)
+    hqx, hqy = synth.gaussian_clusters(nq, 21 + request.param, sigma=qsig)
+    big, over, segs = binning_shape(hx, hy)
+    assert over > 0 and big > 2 * 2048, (big, over)   # tiles spanning several level-2 rounds
+    assert segs > 512, segs                          # bands read in several segment windows
+    assert full_all_chunks(hx, hy, hqx[:200], hqy[:200], r) > 0  # full-chunk ALL runs
+    d = [torch.from_numpy(a).cuda() for a in (hx, hy, hqx, hqy)]
+    return hx, hy, hqx, hqy, r, d
+
+
+@pytest.mark.parametrize("approximate", [False, True], ids=["exact", "approx"])
+def test_join_mid_gaussian(ctx, mid_window, approximate):
+    import torch
+    hx, hy, hqx, hqy, r, (dx, dy, qx, qy) = mid_window
+    ag, cg = agrid(500)
+    want = cref.join_pp_hash(cg, cg, hx, hy, hqx, hqy, r, approximate)
+    assert want[0] > 1e7
+    out = torch.empty((want[0] + 16, 2), dtype=torch.int32, device="cuda")
+    got = ctx.join_pp(ag, ag, dx, dy, qx, qy, r, approximate, out=out)
+    assert pair_digest(got) == want
+    assert ctx.join_pp_count(ag, ag, dx, dy, qx, qy, r, approximate) == want[0]
+
+
+def test_join_mid_capacity(ctx, mid_window):
+    """Two-phase output at this size: a short buffer raises the capacity error with the
+    required count, and a second call into a buffer of that size returns the full set."""
+    import torch
+    hx, hy, hqx, hqy, r, (dx, dy, qx, qy) = mid_window
+    ag, cg = agrid(500)
+    want = cref.join_pp_hash(cg, cg, hx, hy, hqx, hqy, r)
+    short = torch.empty((want[0] // 3, 2), dtype=torch.int32, device="cuda")
+    with pytest.raises(_abi.GeohipCapacityError):
+        ctx.join_pp(ag, ag, dx, dy, qx, qy, r, out=short)
+    del short
+    got = ctx.join_pp(ag, ag, dx, dy, qx, qy, r)  # count-only pass, then the write pass
+    assert pair_digest(got) == want
