@@ -138,6 +138,9 @@ class Workload:
     def cells_partition(self, steps: int) -> dict | None:  # the key-band layout side line
         return None
 
+    def verify(self) -> bool | None:  # after the timed region: the async steps' device counts
+        return None
+
     def _timed_side(self, fn, steps):
         """Max-over-ranks wall time of `steps` calls of fn(s) (barrier + synchronize around)."""
         import torch
@@ -562,6 +565,7 @@ class JoinWorkload(Workload):
                                              self.radius) for w in range(self.windows)]
         self.out = torch.empty((max(self.pairs) + 1, 2), dtype=torch.int32, device=self.dev)
         self.counts = torch.zeros(self.world, dtype=torch.int64, device=self.dev)
+        self.cnt = torch.zeros(self.windows, dtype=torch.int64, device=self.dev)  # async steps' pair totals
 
     def units_per_step(self):
         return self.n
@@ -596,9 +600,17 @@ class JoinWorkload(Workload):
         if self.args.partition == "cells":
             self.cells_last = self.cells_window(w)  # (this rank's pairs, offset, window total)
             return
-        res = self.ctx.join_pp(self.grid, self.grid, self.dx[w], self.dy[w], self.qx, self.qy, self.radius, out=self.out)
+        # enqueue-only (geohip_join_pp_async): the pair total stays on the device, no host round trip
+        self.ctx.join_pp_async(self.grid, self.grid, self.dx[w], self.dy[w], self.qx, self.qy, self.radius, False,
+                               self.out, self.cnt[w:w + 1])
         if self.world > 1:  # result gather: each rank's pair count of this step (output offsets)
-            self.dist.all_gather_into_tensor(self.counts, torch.tensor([len(res)], dtype=torch.int64, device=self.dev))
+            self.dist.all_gather_into_tensor(self.counts, self.cnt[w:w + 1])
+
+    def verify(self):
+        if self.args.partition == "cells":
+            return None
+        self.ctx.sync()  # faults of the async steps (query keys) raise here
+        return self.cnt.cpu().tolist() == self.pairs
 
     def check_merged(self, last_step):
         """N > 1, key-band step (--check): the window's pair total over the band owners against the
@@ -662,13 +674,20 @@ class PpolyWorkload(Workload):
         self.hits = [len(self.ctx.range_ppoly(self.grid, self.xs[w], self.ys[w], self.off, self.vx, self.vy,
                                               self.radius)) for w in range(self.windows)]
         self.out = torch.empty((max(self.hits) + 1, 2), dtype=torch.int32, device=self.dev)
+        self.cnt = torch.zeros(self.windows, dtype=torch.int64, device=self.dev)  # async steps' pair totals
 
     def units_per_step(self):
         return self.n
 
     def step(self, s):
         w = s % self.windows
-        self.ctx.range_ppoly(self.grid, self.xs[w], self.ys[w], self.off, self.vx, self.vy, self.radius, out=self.out)
+        # enqueue-only (geohip_range_ppoly_async): no end-of-step count readback
+        self.ctx.range_ppoly_async(self.grid, self.xs[w], self.ys[w], self.off, self.vx, self.vy, self.radius, False,
+                                   self.out, self.cnt[w:w + 1])
+
+    def verify(self):
+        self.ctx.sync()  # a candidate-buffer overflow of an async step raises here
+        return self.cnt.cpu().tolist() == self.hits
 
     def algorithmic_bytes(self):
         return BYTES_PER_POINT * self.n + 16 * len(self.vx) + 8 * float(np.mean(self.hits))
@@ -753,11 +772,12 @@ class PpJoinWorkload(PpolyWorkload):
         self.hits = [len(self.ctx.join_ppoly(self.grid, self.grid, self.xs[w], self.ys[w], self.off, self.vx, self.vy,
                                              self.radius)) for w in range(self.windows)]
         self.out = torch.empty((max(self.hits) + 1, 2), dtype=torch.int32, device=self.dev)
+        self.cnt = torch.zeros(self.windows, dtype=torch.int64, device=self.dev)
 
     def step(self, s):
         w = s % self.windows
-        self.ctx.join_ppoly(self.grid, self.grid, self.xs[w], self.ys[w], self.off, self.vx, self.vy, self.radius,
-                            out=self.out)
+        self.ctx.join_ppoly_async(self.grid, self.grid, self.xs[w], self.ys[w], self.off, self.vx, self.vy,
+                                  self.radius, False, self.out, self.cnt[w:w + 1])
 
     def config(self):
         c = super().config()
@@ -859,6 +879,9 @@ class PpolyIncrWorkload(PpolyWorkload):
         import torch
         self.inc = IncrementalPPolyRange(self.ctx, self.grid, self.off, self.vx, self.vy, self.radius, False, 2)
         self.outs = [torch.empty((max(self.hits) + 1, 2), dtype=torch.int32, device=self.dev) for _ in range(2)]
+
+    def verify(self):
+        return None  # synchronous pane calls
 
     def step(self, s):
         w = s % self.windows
@@ -1082,6 +1105,9 @@ def main():
     elapsed = time.perf_counter() - t0
     ctx.set_timing(False)
     step_ms, launches, kern_ms, kernels = ctx.timing_kernels(reset=True)
+    verified = wl.verify()  # the enqueue-only steps' device counts against the counts of __init__
+    if verified is False:
+        raise SystemExit(f"bench: {args.workload} steps returned counts that differ from the synchronous calls'")
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -1119,6 +1145,7 @@ def main():
         "dtype": "f64",
         "data": "synthetic",
         "config": wl.config(),
+        "counts_verified": verified,
         "roofline": roofline,
         "cpu_baseline": None,
     }

@@ -119,12 +119,27 @@ int geohip_ctx_timing(geohip_ctx* ctx, double* total_ms, uint64_t* launches, int
    kernel_ms / steps is a step's kernel time without the gaps between its launches. */
 int geohip_ctx_timing_kernels(geohip_ctx* ctx, double* step_ms, uint64_t* steps, double* kernel_ms,
                               uint64_t* kernels, int reset);
-/* Waits for the ctx's enqueued work; GEOHIP_ERR_DEVICE if one of its kernels gave up a look-back
-   wait since the last check (a device-side invariant broken: the results of the *_async calls
-   since then are invalid).  The synchronous calls check this themselves. */
+/* Waits for the ctx's enqueued work, then reports what its *_async calls since the last check
+   could not return as a status (the first that applies; all are cleared):
+     GEOHIP_ERR_DEVICE    a kernel gave up a look-back wait (a device-side invariant broken: the
+                          results of those calls are invalid),
+     GEOHIP_ERR_ARG       geohip_join_pp_async: a query key the reference cannot parse back
+                          (NumberFormatException) or whose neighbour loop never ends
+                          (UniformGrid.java:261-293) -- its results are incomplete,
+     GEOHIP_ERR_CAPACITY  geohip_range_ppoly_async / geohip_join_ppoly_async: the candidate buffer
+                          (sized from the previous call) overflowed; that call's pairs are
+                          incomplete and repeating it succeeds (the buffer is now sized for it).
+   The synchronous calls check the look-back themselves. */
 int geohip_ctx_sync(geohip_ctx* ctx);
 int geohip_device_count(int* out_count);
+/* "geohip 0.2 (gfx950)".  GEOHIP_ABI_VERSION / geohip_abi_version() change whenever an existing
+   entry point's signature changes, so a binding built against another header can refuse to run:
+     1  round 1-3 signatures
+     2  the polygon entry points take nv (the vertex count) after vy; the *_async join and
+        point-polygon forms and geohip_abi_version added */
+#define GEOHIP_ABI_VERSION 2
 const char* geohip_version(void);
+int geohip_abi_version(void);
 
 /* ---- queries (synchronous) ------------------------------------------------------------ */
 int geohip_range_pp(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
@@ -246,6 +261,28 @@ int geohip_knn_range_pp_async(geohip_ctx* ctx, const geohip_grid* grid, const do
 int geohip_range_pp_async(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
                           uint64_t n, double qx, double qy, double r, int approximate,
                           uint32_t* out_idx, uint64_t cap, uint64_t* out_count_dev);
+/* geohip_join_pp into device buffers with no host round trip: out_pairs (cap pairs),
+   *out_count_dev (device uint64) = the window's pair total; pairs past cap are not written (the
+   caller compares the count with cap).  Query-key errors surface at geohip_ctx_sync. */
+int geohip_join_pp_async(geohip_ctx* ctx, const geohip_grid* grid_data, const geohip_grid* grid_query,
+                         const double* dx, const double* dy, uint64_t nd, const double* qx, const double* qy,
+                         uint64_t nq, double r, int approximate, uint32_t* out_pairs, uint64_t cap,
+                         uint64_t* out_count_dev);
+/* geohip_range_ppoly / geohip_join_ppoly into device buffers with no host round trip (points and
+   outputs in device memory, polygons host arrays as for the synchronous forms):
+   *out_count_dev = the pair total, pairs past cap not written.  The candidate buffer is sized
+   from the previous call on this ctx (or n / 16); an overflow surfaces at geohip_ctx_sync.  A
+   grid or polygon set the streaming path cannot take (n > 4096 cells per side, > 16384
+   polygons) runs the tile-binned path, which synchronises inside the call. */
+int geohip_range_ppoly_async(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
+                             uint64_t n, const uint32_t* poly_rings, const uint32_t* ring_off, const double* vx,
+                             const double* vy, uint64_t nv, uint32_t npoly, double r, int approximate,
+                             uint32_t* out_pairs, uint64_t cap, uint64_t* out_count_dev);
+int geohip_join_ppoly_async(geohip_ctx* ctx, const geohip_grid* grid_points, const geohip_grid* grid_query,
+                            const double* x, const double* y, uint64_t n, const uint32_t* poly_rings,
+                            const uint32_t* ring_off, const double* vx, const double* vy, uint64_t nv,
+                            uint32_t npoly, double r, int approximate, uint32_t* out_pairs, uint64_t cap,
+                            uint64_t* out_count_dev);
 
 /* Key-band partition of one window shard for the multi-GPU join (the device form of the
    reference's keyBy(gridID) shuffle, PointPointJoinQuery.java:137-150): a point whose key

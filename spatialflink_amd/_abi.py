@@ -165,6 +165,7 @@ lib = ctypes.CDLL(str(LIB_PATH))
 _P = c_void_p
 _SIGS = {
     "geohip_version": (c_char_p, []),
+    "geohip_abi_version": (c_int, []),
     "geohip_device_count": (c_int, [POINTER(c_int)]),
     "geohip_ctx_create": (c_int, [c_uint32, POINTER(c_void_p)]),
     "geohip_ctx_destroy": (c_int, [_P]),
@@ -205,6 +206,12 @@ _SIGS = {
                                c_int, _P, c_uint64, POINTER(c_uint64)]),
     "geohip_join_pp_count_only": (c_int, [_P, POINTER(Grid), POINTER(Grid), _P, _P, c_uint64, _P, _P, c_uint64,
                                           c_double, c_int, POINTER(c_uint64)]),
+    "geohip_join_pp_async": (c_int, [_P, POINTER(Grid), POINTER(Grid), _P, _P, c_uint64, _P, _P, c_uint64, c_double,
+                                     c_int, _P, c_uint64, _P]),
+    "geohip_range_ppoly_async": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, _P, _P, _P, _P, c_uint64, c_uint32,
+                                         c_double, c_int, _P, c_uint64, _P]),
+    "geohip_join_ppoly_async": (c_int, [_P, POINTER(Grid), POINTER(Grid), _P, _P, c_uint64, _P, _P, _P, _P, c_uint64,
+                                        c_uint32, c_double, c_int, _P, c_uint64, _P]),
     "geohip_range_ppoly": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, _P, _P, _P, _P, c_uint64, c_uint32, c_double, c_int,
                                    _P, c_uint64, POINTER(c_uint64)]),
     "geohip_range_ppoly_pane": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_uint32, _P, _P, _P, _P, c_uint64, c_uint32,
@@ -730,6 +737,53 @@ class Context:
                                        int(approximate), out_idx.data_ptr(), cap, out_count.data_ptr())
         if rc:
             self._check(rc, "range_pp_async")
+
+    def join_pp_async(self, grid_data: Grid, grid_query: Grid, dx, dy, qx, qy, r, approximate, out, out_count):
+        """geohip_join_pp_async: pairs into ``out`` ([cap, 2] int32, device), the pair total into
+        ``out_count`` (one int64, device); nothing is read back (pairs past cap are not written;
+        query-key errors surface at sync())."""
+        for t, nm in ((dx, "dx"), (dy, "dy"), (qx, "qx"), (qy, "qy")):
+            self._dev(t, nm)
+        self._dev(out, "out", "int32")
+        self._dev(out_count, "out_count", "int64")
+        if out.dim() != 2 or out.shape[1] != 2:
+            raise GeohipArgumentError("join_pp_async: out must be [cap, 2]")
+        if self._mem != MEM_DEVICE:
+            self.set_mem(MEM_DEVICE)
+        rc = lib.geohip_join_pp_async(self.h, ctypes.byref(grid_data), ctypes.byref(grid_query), dx.data_ptr(),
+                                      dy.data_ptr(), dx.numel(), qx.data_ptr(), qy.data_ptr(), qx.numel(), r,
+                                      int(approximate), out.data_ptr(), out.shape[0], out_count.data_ptr())
+        if rc:
+            self._check(rc, "join_pp_async")
+
+    def range_ppoly_async(self, grid: Grid, x, y, ring_off, vx, vy, r, approximate, out, out_count, poly_rings=None):
+        """geohip_range_ppoly_async: (polygon, point) pairs into ``out`` ([cap, 2] int32, device),
+        the pair total into ``out_count`` (one int64, device); a candidate-buffer overflow surfaces
+        at sync()."""
+        self._ppoly_async(lib.geohip_range_ppoly_async, "range_ppoly_async", (ctypes.byref(grid),), x, y, ring_off,
+                          vx, vy, r, approximate, out, out_count, poly_rings)
+
+    def join_ppoly_async(self, grid_points: Grid, grid_query: Grid, x, y, ring_off, vx, vy, r, approximate, out,
+                         out_count, poly_rings=None):
+        """geohip_join_ppoly_async: (point, polygon) pairs, as range_ppoly_async."""
+        self._ppoly_async(lib.geohip_join_ppoly_async, "join_ppoly_async",
+                          (ctypes.byref(grid_points), ctypes.byref(grid_query)), x, y, ring_off, vx, vy, r,
+                          approximate, out, out_count, poly_rings)
+
+    def _ppoly_async(self, fn, what, grids, x, y, ring_off, vx, vy, r, approximate, out, out_count, poly_rings):
+        self._dev(x, "x")
+        self._dev(y, "y")
+        self._dev(out, "out", "int32")
+        self._dev(out_count, "out_count", "int64")
+        if out.dim() != 2 or out.shape[1] != 2:
+            raise GeohipArgumentError(f"{what}: out must be [cap, 2]")
+        pr, ring_off, vx, vy, npoly = _poly_arrays(poly_rings, ring_off, vx, vy)
+        if self._mem != MEM_DEVICE:
+            self.set_mem(MEM_DEVICE)
+        rc = fn(self.h, *grids, x.data_ptr(), y.data_ptr(), x.numel(), _ptr(pr), _ptr(ring_off), _ptr(vx), _ptr(vy),
+                len(vx), npoly, r, int(approximate), out.data_ptr(), out.shape[0], out_count.data_ptr())
+        if rc:
+            self._check(rc, what)
 
     def join_pp(self, grid_data: Grid, grid_query: Grid, dx, dy, qx, qy, r, approximate=False, cap=None, out=None):
         """Pairs (data idx, query idx).  ``out`` (optional): a preallocated [cap, 2] u32/i32 buffer on

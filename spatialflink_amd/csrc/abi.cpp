@@ -211,16 +211,41 @@ int range_lookback(geohip_ctx* ctx, RangeLb* lb) {
     return GEOHIP_OK;
 }
 
-// After a synchronisation: GEOHIP_ERR_DEVICE if a look-back wait of this ctx gave up since the
-// last check (the word is cleared).
-int check_lookback_fault(geohip_ctx* ctx) {
-    if (!ctx->buf[S_RLB]) return GEOHIP_OK;
-    unsigned* fw = reinterpret_cast<unsigned*>(B<char>(ctx, S_RLB) + 256 * 8 + 16);
-    unsigned v = 0;
-    HIPCHK(hipMemcpy(&v, fw, 4, hipMemcpyDeviceToHost));
-    if (!v) return GEOHIP_OK;
-    HIPCHK(hipMemset(fw, 0, 4));
-    return fail(ctx, GEOHIP_ERR_DEVICE, "range look-back wait gave up (a block count never arrived); results invalid");
+// The fault block (the S_RLB tail, join.h kFault*): word 0 = fault bits, words 2..3 = the
+// candidate count an overflowing async point-polygon call needed.
+constexpr size_t kFaultOff = 256 * 8 + 16;
+unsigned* fault_block(geohip_ctx* ctx) {
+    return ctx->buf[S_RLB] ? reinterpret_cast<unsigned*>(B<char>(ctx, S_RLB) + kFaultOff) : nullptr;
+}
+constexpr int kPinFault = 6;  // pinned[6] = fault bits, pinned[7] = the candidate need
+
+// Queue the fault block's read into pinned[6..7] behind the call's own readback (one
+// synchronisation covers both; nothing to read before the block exists).
+int queue_fault_read(geohip_ctx* ctx) {
+    ctx->pinned[kPinFault] = 0;
+    ctx->pinned[kPinFault + 1] = 0;
+    unsigned* fw = fault_block(ctx);
+    if (fw) HIPCHK(hipMemcpyAsync(ctx->pinned + kPinFault, fw, 16, hipMemcpyDeviceToHost, ctx->stream));
+    return GEOHIP_OK;
+}
+
+// After the synchronisation that follows queue_fault_read: the faults since the last check as
+// one status (the block cleared on the ctx's stream, the candidate need kept for the next call).
+int report_faults(geohip_ctx* ctx) {
+    const unsigned bits = (unsigned)(ctx->pinned[kPinFault] & 0xffffffffu);
+    if (!bits) return GEOHIP_OK;
+    const uint64_t need = ctx->pinned[kPinFault + 1];
+    HIPCHK(hipMemsetAsync(fault_block(ctx), 0, 16, ctx->stream));
+    if (bits & kFaultCandOverflow) ppoly_note_cand_need(ctx, need);
+    if (bits & kFaultLookback)
+        return fail(ctx, GEOHIP_ERR_DEVICE, "range look-back wait gave up (a block count never arrived); results invalid");
+    if (bits & kFaultQueryKey)
+        return fail(ctx, GEOHIP_ERR_ARG, "async join: NumberFormatException in getIntCellIndices (query point key)");
+    if (bits & kFaultQueryLoop)
+        return fail(ctx, GEOHIP_ERR_ARG, "async join: reference neighbour loop does not terminate");
+    return fail(ctx, GEOHIP_ERR_CAPACITY, "async point-polygon call: candidate buffer overflow (" + std::to_string(need) +
+                                              " candidates), its pairs are incomplete; repeat the call (it now sizes "
+                                              "the buffer for them)");
 }
 
 int begin(geohip_ctx* ctx) {
@@ -605,7 +630,8 @@ int knn_range_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x,
 
 extern "C" {
 
-const char* geohip_version(void) { return "geohip 0.1 (gfx950)"; }
+const char* geohip_version(void) { return "geohip 0.2 (gfx950)"; }
+int geohip_abi_version(void) { return GEOHIP_ABI_VERSION; }
 
 int geohip_device_count(int* out_count) {
     int c = 0;
@@ -752,8 +778,10 @@ int geohip_ctx_timing(geohip_ctx* ctx, double* total_ms, uint64_t* launches, int
 int geohip_ctx_sync(geohip_ctx* ctx) {
     int rc = begin(ctx);
     if (rc) return rc;
+    rc = queue_fault_read(ctx);
+    if (rc) return rc;
     HIPCHK(hipStreamSynchronize(ctx->stream));
-    return check_lookback_fault(ctx);
+    return report_faults(ctx);
 }
 
 // Test knob: while on, the range look-back waits (range_fused, the kNN pass's fused range) wait
@@ -797,8 +825,10 @@ int geohip_range_pp(geohip_ctx* ctx, const geohip_grid* grid, const double* x, c
     rc = range_enqueue(ctx, grid, x, y, n, qx, qy, r, approximate, out, cap, B<uint64_t>(ctx, S_TOTAL));
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(ctx->pinned, ctx->buf[S_TOTAL], 8, hipMemcpyDeviceToHost, ctx->stream));
+    rc = queue_fault_read(ctx);
+    if (rc) return rc;
     HIPCHK(hipStreamSynchronize(ctx->stream));
-    rc = check_lookback_fault(ctx);
+    rc = report_faults(ctx);
     if (rc) return rc;
     const uint64_t total = ctx->pinned[0];
     *out_count = total;
@@ -982,8 +1012,10 @@ int geohip_knn_range_pp(geohip_ctx* ctx, const geohip_grid* grid, const double* 
         HIPCHK(hipMemcpyAsync(knn_dist, od, (size_t)k * 8, hipMemcpyDeviceToHost, ctx->stream));
         HIPCHK(hipMemcpyAsync(knn_idx, oi, (size_t)k * 4, hipMemcpyDeviceToHost, ctx->stream));
     }
+    rc = queue_fault_read(ctx);
+    if (rc) return rc;
     HIPCHK(hipStreamSynchronize(ctx->stream));
-    rc = check_lookback_fault(ctx);
+    rc = report_faults(ctx);
     if (rc) return rc;
     *knn_count = (uint32_t)(ctx->pinned[0] & 0xffffffffu);
     const uint64_t total = ctx->pinned[1];
@@ -1025,6 +1057,42 @@ int geohip_join_pp_count_only(geohip_ctx* ctx, const geohip_grid* grid_data, con
     if (rc) return rc;
     return join_pp_impl(ctx, grid_data, grid_query, dx, dy, nd, qx, qy, nq, r, approximate, nullptr, 0, out_count,
                         true);
+}
+
+int geohip_join_pp_async(geohip_ctx* ctx, const geohip_grid* grid_data, const geohip_grid* grid_query,
+                         const double* dx, const double* dy, uint64_t nd, const double* qx, const double* qy,
+                         uint64_t nq, double r, int approximate, uint32_t* out_pairs, uint64_t cap,
+                         uint64_t* out_count_dev) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    if (ctx->mem != GEOHIP_MEM_DEVICE) return fail(ctx, GEOHIP_ERR_ARG, "async forms need GEOHIP_MEM_DEVICE");
+    if (!out_count_dev || (cap && !out_pairs)) return fail(ctx, GEOHIP_ERR_ARG, "null output");
+    return join_pp_impl(ctx, grid_data, grid_query, dx, dy, nd, qx, qy, nq, r, approximate, out_pairs, cap, nullptr,
+                        false, out_count_dev);
+}
+
+int geohip_range_ppoly_async(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
+                             const uint32_t* poly_rings, const uint32_t* ring_off, const double* vx, const double* vy,
+                             uint64_t nv, uint32_t npoly, double r, int approximate, uint32_t* out_pairs, uint64_t cap,
+                             uint64_t* out_count_dev) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    if (ctx->mem != GEOHIP_MEM_DEVICE) return fail(ctx, GEOHIP_ERR_ARG, "async forms need GEOHIP_MEM_DEVICE");
+    if (!out_count_dev) return fail(ctx, GEOHIP_ERR_ARG, "null output");
+    return ppoly_impl(ctx, grid, nullptr, 0, x, y, n, poly_rings, ring_off, vx, vy, nv, npoly, r, approximate, out_pairs,
+                      cap, nullptr, 0, out_count_dev);
+}
+
+int geohip_join_ppoly_async(geohip_ctx* ctx, const geohip_grid* grid_points, const geohip_grid* grid_query,
+                            const double* x, const double* y, uint64_t n, const uint32_t* poly_rings,
+                            const uint32_t* ring_off, const double* vx, const double* vy, uint64_t nv, uint32_t npoly,
+                            double r, int approximate, uint32_t* out_pairs, uint64_t cap, uint64_t* out_count_dev) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    if (ctx->mem != GEOHIP_MEM_DEVICE) return fail(ctx, GEOHIP_ERR_ARG, "async forms need GEOHIP_MEM_DEVICE");
+    if (!out_count_dev) return fail(ctx, GEOHIP_ERR_ARG, "null output");
+    return ppoly_impl(ctx, grid_points, grid_query, 1, x, y, n, poly_rings, ring_off, vx, vy, nv, npoly, r, approximate,
+                      out_pairs, cap, nullptr, 0, out_count_dev);
 }
 
 int geohip_range_ppoly(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
@@ -1274,6 +1342,12 @@ int ctx_begin(geohip_ctx* ctx) { return begin(ctx); }
 hipStream_t ctx_stream(geohip_ctx* ctx) { return ctx->stream; }
 int ctx_mem(geohip_ctx* ctx) { return ctx->mem; }
 uint64_t* ctx_pinned(geohip_ctx* ctx) { return ctx->pinned; }
+int ctx_fault_block(geohip_ctx* ctx, unsigned** out) {
+    int rc = ensure_zeroed(ctx, S_RLB, kRlbBytes);
+    if (rc) return rc;
+    *out = fault_block(ctx);
+    return GEOHIP_OK;
+}
 void** ctx_pcache_slot(geohip_ctx* ctx) { return &ctx->pcache; }
 void** ctx_kcache_slot(geohip_ctx* ctx) { return &ctx->kcache; }
 void ctx_timing_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1) { timing_events(ctx, e0, e1); }

@@ -102,6 +102,12 @@ __device__ __forceinline__ int32_t d_axis_cell_sub(double v, double mn, double l
 __global__ void fill_words(unsigned* __restrict__ p, unsigned n, unsigned v) {
     for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = v;
 }
+// a step's zero block, and one more 64-bit word (an async call's device count) when z is not null
+__global__ void zero_step(unsigned* __restrict__ p, unsigned n, unsigned long long* __restrict__ z) {
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = 0u;
+    if (z && blockIdx.x == 0 && threadIdx.x == 0) *z = 0ull;
+}
+__global__ void set_u64(unsigned long long* __restrict__ p, unsigned long long v) { *p = v; }
 
 // ------------------------------------------------------------------ scans ----------------
 // exclusive scan, 3 phases: per-block totals, scan of totals, per-block rescan + offset
@@ -740,9 +746,10 @@ struct JqGeom {
     int all_cells;       // r == 0: every cell (UniformGrid.java:264-266)
 };
 
+// fault (async calls, else null): the ctx's fault word, kFaultQueryKey / kFaultQueryLoop
 __global__ __launch_bounds__(kTB) void jq_rect(const double* __restrict__ qx, const double* __restrict__ qy,
                                                uint64_t nq, JqGeom g, QRect* __restrict__ rect,
-                                               unsigned* __restrict__ err) {
+                                               unsigned* __restrict__ err, unsigned* __restrict__ fault) {
     const uint64_t i = (uint64_t)blockIdx.x * kTB + threadIdx.x;
     if (i >= nq) return;
     QRect R{0, g.nb - 1, 0, g.nb - 1};
@@ -758,6 +765,7 @@ __global__ __launch_bounds__(kTB) void jq_rect(const double* __restrict__ qx, co
         }
         if (!ok) {
             atomicMax(err, 1u);
+            if (fault) atomicOr(fault, kFaultQueryKey);
             R = QRect{1, 0, 1, 0};
         } else {
             const int32_t lo_i = (int32_t)(uint32_t)(uint64_t)((int64_t)ci - g.lc);
@@ -768,6 +776,7 @@ __global__ __launch_bounds__(kTB) void jq_rect(const double* __restrict__ qx, co
                 R = QRect{1, 0, 1, 0};
             } else if (hi_i == INT32_MAX || hi_j == INT32_MAX) {
                 atomicMax(err, 2u);
+                if (fault) atomicOr(fault, kFaultQueryLoop);
                 R = QRect{1, 0, 1, 0};
             } else {
                 R = QRect{lo_i > 0 ? lo_i : 0, hi_i < g.nb - 1 ? hi_i : g.nb - 1, lo_j > 0 ? lo_j : 0,
@@ -818,7 +827,8 @@ __global__ void jq_global(uint64_t nq, unsigned* __restrict__ glist, unsigned* _
 //             points is sorted by band (128 consecutive tiles) in LDS and written back in place
 //             (the same positions: one contiguous 64-KB store per sub-chunk); the sub-chunk's band
 //             offsets go to soff; a block-wide LDS tile histogram is added to the tile counts once.
-//   jb_scan   tile counts -> tile starts and per-tile cursors (one block); re-zeroes the counts.
+//   jb_scan   tile counts -> tile starts and per-tile cursors (one block); the counts are zeroed
+//             before the step by its zero_step launch (the zero block), not here.
 //   jb_tiles  one block per (band, group of kJbGroup level-1 blocks): the band's segments of
 //             those blocks' sub-chunks, sorted by tile in LDS; each tile's run reserved with one
 //             global atomic on its cursor, written contiguously.
@@ -2399,7 +2409,8 @@ struct StreamOut {
     uint64_t cap;
     int aligned8, swap;
     unsigned point_base;            // added to every point index of a pair (pane stream positions)
-    unsigned long long* totals;     // [0] pairs, [1] candidates: reservation cursors (zero before)
+    unsigned long long* ptotal;     // pairs: reservation cursor (zero before; an async call's count)
+    unsigned long long* ctotal;     // candidates: reservation cursor (zero before)
     uint64_t ccap;                  // candidates past it are counted only (the host regrows, re-runs)
     unsigned* cpoly;                // candidates in chunk order: polygon (the grouping reads these),
     double4* crec;                  // and (x, y, point bits, -) -- one 32-byte sector per gather
@@ -2825,7 +2836,7 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
         StreamSink ps{ppk + wid * kWPair, &s_np, kWPair, false, 0, 0u, 0u};
         StreamSink cs{cpk + (APPROX ? 0 : wid * kWCand), &s_nc, APPROX ? 0u : kWCand, false, 0, 0u, 0u};
         stream_chunk<APPROX, KL>(a, kl, c0, c1, ps, cs);
-        if (GEOHIP_PS_ABL == 3 && ps.acc + cs.acc == 0x9e3779b9u) a.o.totals[0] = 1;
+        if (GEOHIP_PS_ABL == 3 && ps.acc + cs.acc == 0x9e3779b9u) a.o.ptotal[0] = 1;
         if (lane == 0) {
             s_wp[wid] = ps.n;
             s_wc[wid] = cs.n;
@@ -2843,8 +2854,8 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
             nc += wc;
         }
         if (threadIdx.x == 0) {
-            s_pb = np ? atomicAdd(a.o.totals, (unsigned long long)np) : 0ull;
-            s_cb = nc ? atomicAdd(a.o.totals + 1, (unsigned long long)nc) : 0ull;
+            s_pb = np ? atomicAdd(a.o.ptotal, (unsigned long long)np) : 0ull;
+            s_cb = nc ? atomicAdd(a.o.ctotal, (unsigned long long)nc) : 0ull;
         }
         __syncthreads();
         const unsigned long long pb = s_pb, cb = s_cb;
@@ -2883,7 +2894,7 @@ __device__ __forceinline__ void spairs_flush(uint2* buf, unsigned& cnt, const St
     wave_lds_sync();
     unsigned lo = 0, hi = 0;
     if (lane_id() == 0) {
-        const unsigned long long b = atomicAdd(o.totals, (unsigned long long)cnt);
+        const unsigned long long b = atomicAdd(o.ptotal, (unsigned long long)cnt);
         lo = (unsigned)b;
         hi = (unsigned)(b >> 32);
     }
@@ -2910,8 +2921,10 @@ constexpr unsigned kCandGroups = 128;
 constexpr unsigned kCandThreads = 1024;
 constexpr unsigned kCandPer = 4;  // candidates per thread per round (loads in flight together)
 struct CandGroup {
-    const unsigned long long* ccount;  // candidate total (StreamOut::totals + 1)
+    const unsigned long long* ccount;  // candidate total (StreamOut::ctotal)
     uint64_t ccap;
+    unsigned* fault;                   // async calls: the ctx's fault word (kFaultCandOverflow), else null
+    unsigned long long* need;          // async calls: the candidate count an overflowing call needed
     const unsigned* cpoly;
     const double4* crec;
     unsigned* mat;          // [kCandGroups][npoly]: counts, then write bases
@@ -3012,7 +3025,16 @@ __global__ __launch_bounds__(kCandThreads) void ppoly_cand_plan(CandGroup c) {
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) *c.nitems = carry_i;
+    if (threadIdx.x == 0) {
+        *c.nitems = carry_i;
+        // an async call cannot rerun with a larger buffer: the overflow (the candidates past ccap
+        // are untested, the pairs incomplete) and the size it needed go to the ctx's fault block
+        const unsigned long long nc = *c.ccount;
+        if (c.fault && nc > c.ccap) {
+            atomicOr(c.fault, kFaultCandOverflow);
+            atomicMax(c.need, nc);
+        }
+    }
 }
 
 // Only the 4-byte slot of each candidate moves (a random scatter of its 20 bytes cost 3x the
@@ -4171,9 +4193,10 @@ void pp_screen_bounds(double r, double* r2lo, double* r2hi) { screen_bounds(r, r
 
 int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, const double* dx, const double* dy,
                  uint64_t nd, const double* qx, const double* qy, uint64_t nq, double r, int approximate,
-                 uint32_t* out_pairs, uint64_t cap, uint64_t* out_count, bool count_only) {
-    if (!out_count) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null out_count");
-    *out_count = 0;
+                 uint32_t* out_pairs, uint64_t cap, uint64_t* out_count, bool count_only, uint64_t* count_dev) {
+    const bool async = count_dev != nullptr;
+    if (!out_count && !async) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null out_count");
+    if (out_count) *out_count = 0;
     int rc = check_grid_basic(ctx, gd, "data grid");
     if (!rc) rc = check_grid_basic(ctx, gq, "query grid");
     if (rc) return rc;
@@ -4220,15 +4243,22 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
     unsigned* misc = zero + 2 * (ntl + 1);
     unsigned long long* total = reinterpret_cast<unsigned long long*>(zero + ztot);
     unsigned* tcnt = zero + ztot + 2;
+    unsigned* fault = nullptr;  // async: query-key errors surface at geohip_ctx_sync
+    if (async) {
+        rc = ctx_fault_block(ctx, &fault);
+        if (rc) return rc;
+        total = reinterpret_cast<unsigned long long*>(count_dev);  // the caller's device count word
+    }
     hipEvent_t e0, e1;
     ctx_timing_events(ctx, &e0, &e1);
     if (e0) hipEventRecord(e0, st);  // the whole device step: binning, replication, join
     // every kernel of the step is timed on its own (tlaunch: the dispatch's begin / end stamps)
-    tlaunch(ctx, fill_words, (nzero + kTB - 1) / kTB, kTB, 0, st, zero, nzero, 0u);
+    tlaunch(ctx, zero_step, (nzero + kTB - 1) / kTB, kTB, 0, st, zero, nzero,
+            async ? reinterpret_cast<unsigned long long*>(count_dev) : (unsigned long long*)nullptr);
     const unsigned qb = (unsigned)((nq + kTB - 1) / kTB);
     if (nq) {
         JqGeom jg{gq->min_x, gq->min_y, gq->cell_len, nb, lc, all_cells ? 1 : 0};
-        tlaunch(ctx, jq_rect, qb, kTB, 0, st, dqx, dqy, nq, jg, drect, misc);
+        tlaunch(ctx, jq_rect, qb, kTB, 0, st, dqx, dqy, nq, jg, drect, misc, fault);
     }
     if (global_mode) {
         if (nq) tlaunch(ctx, jq_global, qb, kTB, 0, st, nq, glist, misc + 5);
@@ -4275,6 +4305,7 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
     if (e1) hipEventRecord(e1, st);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, std::string("join launch: ") + hipGetErrorString(e));
+    if (async) return GEOHIP_OK;  // the total is in *count_dev; errors at geohip_ctx_sync
     // one readback: the pair total and the query-block error word
     uint64_t* pin = ctx_pinned(ctx);
     if (hipMemcpyAsync(pin, total, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -4637,6 +4668,11 @@ bool same_inputs(const PolyCache& c, const geohip_grid& g, double r, const uint3
     return memcmp(c.vx.data(), vx + v0, (v1 - v0) * 8) == 0 && memcmp(c.vy.data(), vy + v0, (v1 - v0) * 8) == 0;
 }
 
+void ppoly_note_cand_need(geohip_ctx* ctx, uint64_t need) {
+    PolyCache* pc = ctx_pcache(ctx);
+    if (need > pc->last_cand) pc->last_cand = need;
+}
+
 void ppoly_cache_drop(geohip_ctx* ctx) {
     void** slot = ctx_pcache_slot(ctx);
     delete static_cast<PolyCache*>(*slot);
@@ -4751,8 +4787,11 @@ void build_stream_table(PolyCache& c, uint32_t npoly, int32_t nb, bool r_is_max)
 int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, int join, const double* x,
                const double* y, uint64_t n, const uint32_t* poly_rings, const uint32_t* ring_off, const double* vx,
                const double* vy, uint64_t nv, uint32_t npoly, double r, int approximate, uint32_t* out_pairs,
-               uint64_t cap, uint64_t* out_count, uint32_t point_base) {
-    if (!out_count) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null out_count");
+               uint64_t cap, uint64_t* out_count, uint32_t point_base, uint64_t* count_dev) {
+    const bool async = count_dev != nullptr;
+    uint64_t count_local = 0;
+    if (!out_count && !async) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null out_count");
+    if (!out_count) out_count = &count_local;
     *out_count = 0;
     int rc = check_grid_basic(ctx, grid, join ? "point grid" : "grid");
     if (!rc && join) rc = check_grid_basic(ctx, gq, "query grid");
@@ -4763,7 +4802,13 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     const int jmode = join ? (approximate ? 2 : 1) : 0;
     if (n >= 0xffffffffull) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "window larger than 2^32-1 points");
     if (cap && !out_pairs) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null out_pairs");
-    if (npoly == 0) return GEOHIP_OK;  // no polygon: no pair (the polygon arrays may be null)
+    if (npoly == 0) {  // no polygon: no pair (the polygon arrays may be null)
+        if (async) {
+            set_u64<<<1, 1, 0, ctx_stream(ctx)>>>(reinterpret_cast<unsigned long long*>(count_dev), 0ull);
+            if (hipGetLastError() != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "count launch failed");
+        }
+        return GEOHIP_OK;
+    }
     if (!ring_off || !vx || !vy) return ctx_fail(ctx, GEOHIP_ERR_ARG, "null polygon arrays");
     hipStream_t st = ctx_stream(ctx);
     const bool dev = ctx_mem(ctx) == GEOHIP_MEM_DEVICE;
@@ -4973,6 +5018,11 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
         uint64_t ccap = std::max<uint64_t>(std::max<uint64_t>(65536, n / 16), pc->last_cand + pc->last_cand / 4);
         uint64_t tot = 0;
         const uint64_t nchunks = (n + kStreamChunk - 1) / kStreamChunk;
+        unsigned* fault = nullptr;  // async: a candidate overflow surfaces at geohip_ctx_sync
+        if (async) {
+            rc = ctx_fault_block(ctx, &fault);
+            if (rc) return rc;
+        }
         for (int attempt = 0; attempt < 3; attempt++) {
             // J_MISC: [0..1] pair total, [2..3] candidate total, [4] work items
             unsigned* misc = S.get<unsigned>(J_MISC, kMiscWords * 4);
@@ -4984,14 +5034,17 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             hipEvent_t e0, e1;
             ctx_timing_events(ctx, &e0, &e1);
             if (e0) hipEventRecord(e0, st);  // the whole device step
-            tlaunch(ctx, fill_words, 1, 64, 0, st, misc, 8u, 0u);  // totals and the item count
+            // totals and the item count (async: the pair total is the caller's device word)
+            tlaunch(ctx, zero_step, 1, 64, 0, st, misc, 8u,
+                    async ? reinterpret_cast<unsigned long long*>(count_dev) : (unsigned long long*)nullptr);
             StreamOut so;
             so.out = out;
             so.cap = out ? cap : 0;
             so.aligned8 = ((uintptr_t)out & 7u) == 0;
             so.swap = join ? 1 : 0;
             so.point_base = point_base;
-            so.totals = reinterpret_cast<unsigned long long*>(misc);
+            so.ptotal = async ? reinterpret_cast<unsigned long long*>(count_dev) : reinterpret_cast<unsigned long long*>(misc);
+            so.ctotal = reinterpret_cast<unsigned long long*>(misc) + 1;
             so.ccap = cands ? ccap : 0;
             char* cb = reinterpret_cast<char*>(cbuf);
             so.cpoly = cands ? reinterpret_cast<unsigned*>(cb) : nullptr;
@@ -5026,8 +5079,10 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             if (cands) {
                 char* sb = reinterpret_cast<char*>(sbuf);
                 CandGroup cg;
-                cg.ccount = so.totals + 1;
+                cg.ccount = so.ctotal;
                 cg.ccap = ccap;
+                cg.fault = fault;
+                cg.need = fault ? reinterpret_cast<unsigned long long*>(fault + 2) : nullptr;
                 cg.cpoly = so.cpoly;
                 cg.crec = so.crec;
                 cg.mat = mat;
@@ -5043,6 +5098,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             if (e1) hipEventRecord(e1, st);
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, std::string("ppoly stream launch: ") + hipGetErrorString(e));
+            if (async) return GEOHIP_OK;  // pairs counted into *count_dev; an overflow at geohip_ctx_sync
             uint64_t* pin = ctx_pinned(ctx);
             if (hipMemcpyAsync(pin, misc, 32, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
                 return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "count readback failed");
@@ -5151,6 +5207,11 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, std::string("ppoly launch: ") + hipGetErrorString(e));
     unsigned long long* total = boff + nslots;
+    if (async) {  // the tile-binned path read its mask size back already; the total stays on the device
+        if (hipMemcpyAsync(count_dev, total, 8, hipMemcpyDeviceToDevice, st) != hipSuccess)
+            return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "count copy failed");
+        return GEOHIP_OK;
+    }
     uint64_t tot = 0;
     rc = read_total(ctx, total, &tot);
     if (rc) return rc;

@@ -378,7 +378,7 @@ __device__ __forceinline__ unsigned long long poll_block_counts(const unsigned l
     unsigned spins = 0;
     while (__ballot(pending != 0)) {
         if (++spins > spin_limit) {
-            if (lane == 0) __hip_atomic_store(fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) __hip_atomic_fetch_or(fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // kFaultLookback
             break;
         }
         __builtin_amdgcn_s_sleep(8);

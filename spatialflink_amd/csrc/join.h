@@ -10,6 +10,13 @@
 #include "geohip_internal.h"
 
 namespace geohip {
+// The ctx's device fault word (bits; read, reported and cleared by geohip_ctx_sync and by the
+// synchronous calls): a device-side condition an enqueue-only call cannot return as a status.
+constexpr unsigned kFaultLookback = 1u;       // a look-back wait gave up (GEOHIP_ERR_DEVICE)
+constexpr unsigned kFaultQueryKey = 2u;       // join query key: NumberFormatException (GEOHIP_ERR_ARG)
+constexpr unsigned kFaultQueryLoop = 4u;      // join query block: a loop that never ends (GEOHIP_ERR_ARG)
+constexpr unsigned kFaultCandOverflow = 8u;   // point-polygon candidate buffer overflow (GEOHIP_ERR_CAPACITY)
+
 // context services implemented in abi.cpp
 int ctx_fail(geohip_ctx* ctx, int code, const std::string& msg);
 int ctx_ensure(geohip_ctx* ctx, int slot, size_t bytes, void** out);  // slot 0..27 (JSlot, cell_kernels.hip)
@@ -24,6 +31,9 @@ int ctx_begin(geohip_ctx* ctx);  // clears the error, selects the ctx's device
 hipStream_t ctx_stream(geohip_ctx* ctx);
 int ctx_mem(geohip_ctx* ctx);
 uint64_t* ctx_pinned(geohip_ctx* ctx);
+// the fault block on the device: word 0 = fault bits, words 2..3 = the u64 candidate count an
+// overflowing async point-polygon call needed (atomicMax); allocated zeroed on first use
+int ctx_fault_block(geohip_ctx* ctx, unsigned** out);
 void ctx_timing_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1);      // a step of several launches
 void ctx_kernel_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1);      // one kernel inside such a step
 void ctx_kernel_step_events(geohip_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1); // a step that is one kernel
@@ -52,9 +62,11 @@ void** ctx_kcache_slot(geohip_ctx* ctx);  // the ctx's point-polygon kNN polygon
 // squared-distance screen bounds for "dist <= r" (r2lo < 0 / r2hi = inf where they cannot hold)
 void pp_screen_bounds(double r, double* r2lo, double* r2hi);
 
+// count_dev (async, device window and outputs): the pair total goes there, nothing is read back
 int join_pp_impl(geohip_ctx* ctx, const geohip_grid* grid_data, const geohip_grid* grid_query, const double* dx,
                  const double* dy, uint64_t nd, const double* qx, const double* qy, uint64_t nq, double r,
-                 int approximate, uint32_t* out_pairs, uint64_t cap, uint64_t* out_count, bool count_only);
+                 int approximate, uint32_t* out_pairs, uint64_t cap, uint64_t* out_count, bool count_only,
+                 uint64_t* count_dev = nullptr);
 // key-band owner partition of a window (band.hip; geohip_band_pack_async)
 int band_pack_impl(geohip_ctx* ctx, const geohip_grid* grid, int32_t nb, uint32_t world, const double* x,
                    const double* y, uint64_t n, int64_t base, double* out_x, double* out_y, int64_t* out_idx,

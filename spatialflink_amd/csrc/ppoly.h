@@ -13,7 +13,9 @@ void ppoly_cache_drop(geohip_ctx* ctx);
 int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, int join, const double* x,
                const double* y, uint64_t n, const uint32_t* poly_rings, const uint32_t* ring_off, const double* vx,
                const double* vy, uint64_t nv, uint32_t npoly, double r, int approximate, uint32_t* out_pairs,
-               uint64_t cap, uint64_t* out_count, uint32_t point_base = 0);
+               uint64_t cap, uint64_t* out_count, uint32_t point_base = 0, uint64_t* count_dev = nullptr);
+// geohip_ctx_sync found an async call's candidate overflow: the next call sizes its buffer for need
+void ppoly_note_cand_need(geohip_ctx* ctx, uint64_t need);
 // point-polygon kNN of one polygon (PointPolygonKNNQuery.java:162-236); async: device outputs and
 // count, no host synchronisation
 int knn_ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
