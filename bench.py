@@ -272,7 +272,7 @@ class KnnWorkload(Workload):
         self.ctx.synth_uniform_async(x, y, 0, self.seed0 + 7919 * w, synth.BEIJING)
         wi, wd = self.ctx.knn_pp(self.grid, x, y, self.q[0], self.q[1], self.radius, self.k)
         if self.args.partition == "cells":  # the key-band step's own merged result
-            res, (_, _, total), _ = self.cells_last
+            res, (_, _, total), _ = self.cells_last.result()
             m_i, m_d, m = res.idx, res.dist, int(res.count)
             if self.has_range:
                 want = self.ctx.range_pp(self.grid, x, y, self.q[0], self.q[1], self.radius)
@@ -289,23 +289,12 @@ class KnnWorkload(Workload):
         G u C cells packed by key band (geohip_band_pack_query_async), one all-to-all to their
         owner, the owner's kNN (+ range) of its band, one all-gather of the top-k + merge
         (distributed.knn_range_cells)."""
-        import torch
         from spatialflink_amd import distributed as D
 
-        def local(xs, ys, qx, qy, r, k, approximate):
-            oi = torch.full((k,), -1, dtype=torch.int32, device=self.dev)
-            od = torch.full((k,), -1, dtype=torch.int64, device=self.dev).view(torch.float64)
-            if self.has_range:
-                (ki, kd), ro = self.ctx.knn_range_pp(self.grid, xs, ys, qx, qy, r, k, approximate)
-            else:
-                ki, kd = self.ctx.knn_pp(self.grid, xs, ys, qx, qy, r, k)
-                ro = torch.zeros(0, dtype=torch.int32, device=self.dev)
-            oi[:len(ki)] = ki
-            od[:len(kd)] = kd
-            return oi, od, ro
-
+        if getattr(self, "cbufs", None) is None:  # preallocated rows: the step enqueues only
+            self.cbufs = D.CellsBuffers(self.k, self.n, self.world, self.dev, with_range=self.has_range)
         return D.knn_range_cells(self.xs[w], self.ys[w], self.rank * self.n, self.q[0], self.q[1], self.radius,
-                                 self.k, grid=self.grid, ctx=self.ctx, local=local)
+                                 self.k, grid=self.grid, ctx=self.ctx, bufs=self.cbufs)
 
     def cells_partition(self, steps):
         """Side line: the key-band layout timed per window (max over ranks), per-rank skew of the
@@ -313,7 +302,7 @@ class KnnWorkload(Workload):
         import torch
         from spatialflink_amd import distributed as D
         t, out = self._timed_side(lambda s: self.cells_window(s % self.windows), steps)
-        res, (hits, _, total), nrecv = out
+        res, (hits, _, total), nrecv = out.result()
         w = (steps - 1) % self.windows
         ref = D.knn_sharded(self.xs[w], self.ys[w], self.rank * self.n, self.q[0], self.q[1], self.radius, self.k,
                             grid=self.grid, ctx=self.ctx)
@@ -954,7 +943,7 @@ class C5Workload(KnnWorkload):
     def algorithmic_bytes(self):  # per step: the shard read once (16 B/pt) + the range hits written
         if self.hits is None:
             if self.args.partition == "cells" and getattr(self, "cells_last", None) is not None:
-                self.hits = float(self.cells_last[1][2]) / self.world  # the window's hits, per GPU
+                self.hits = float(self.cells_last.result()[1][2]) / self.world  # the window's hits, per GPU
             else:
                 self.hits = float(self.out_rc[0].item())
         return BYTES_PER_POINT * self.n + 4 * self.hits

@@ -151,6 +151,9 @@ def _exchange_records(px, py, pg, send_counts, group):
     record array in a single all_to_all.  Returns the owner's (x, y, window idx)."""
     import torch
 
+    if _world_rank(group)[0] == 1:  # one owner: the packed points stay (no collective)
+        m = int(send_counts.sum().item())
+        return px[:m], py[:m], pg[:m]
     recv_counts = torch.empty_like(send_counts)
     all_to_all(recv_counts, send_counts, group=group)
     both = torch.stack([send_counts, recv_counts]).cpu().tolist()
@@ -162,9 +165,99 @@ def _exchange_records(px, py, pg, send_counts, group):
     return got[:, 0].contiguous(), got[:, 1].contiguous(), got[:, 2].contiguous().view(torch.int64)
 
 
+class CellsBuffers:
+    """Preallocated device rows of knn_range_cells' enqueue-only form (one set per window in
+    flight): the owner's top-k and range hits with their device counts, the all-gathered lists,
+    the merged top-k and the per-rank hit counts."""
+
+    def __init__(self, k: int, hit_cap: int, world: int, device, with_range: bool = True):
+        import torch
+        i32, i64, f64 = torch.int32, torch.int64, torch.float64
+        self.k, self.cap, self.with_range = k, hit_cap, with_range
+        self.ki = torch.empty(k, dtype=i32, device=device)
+        self.kd = torch.empty(k, dtype=f64, device=device)
+        self.kc = torch.zeros(1, dtype=i32, device=device)
+        self.hits = torch.empty(max(hit_cap, 1), dtype=i32, device=device)
+        self.hc = torch.zeros(1, dtype=i64, device=device)
+        self.all_d = torch.empty((world, k), dtype=f64, device=device)
+        self.all_i = torch.empty((world, k), dtype=i32, device=device)
+        self.mi = torch.empty(k, dtype=i32, device=device)
+        self.md = torch.empty(k, dtype=f64, device=device)
+        self.mc = torch.zeros(1, dtype=i32, device=device)
+        self.counts = torch.zeros(world, dtype=i64, device=device)
+
+
+@dataclass
+class CellsStep:
+    """knn_range_cells' enqueue-only result: device tensors, nothing read back yet.  idx / dist:
+    the merged top-k (k entries, -1 / sentinel padded), count: its int32 device count; hits: this
+    rank's hit buffer (local indices, hit_count of them), mapped to window indices by base or by
+    rg; counts: every rank's hit count (device).  result() reads it back as the synchronous form
+    returns it."""
+    idx: object
+    dist: object
+    count: object
+    hits: object
+    hit_count: object
+    base: int
+    rg: object
+    counts: object
+    rank: int
+    nrecv: int
+
+    def result(self):
+        import torch
+        m = int(self.count.item())
+        h = int(self.hit_count.item())
+        lh = self.hits[:h].to(torch.int64)
+        hits = lh + self.base if self.rg is None else (self.rg[lh] if h else lh)
+        allc = self.counts.cpu().tolist()
+        return (KnnResult(self.idx[:m], self.dist[:m], m), (hits, sum(allc[:self.rank]), sum(allc)), self.nrecv)
+
+
+def _knn_range_cells_enqueue(x_local, y_local, base, qx, qy, r, k, approximate, grid, ctx, group, band_pack,
+                             bufs: CellsBuffers) -> CellsStep:
+    """knn_range_cells with the device engine into preallocated rows and no host round trip
+    except the exchange's split sizes (world > 1; all_to_all takes them on the host)."""
+    import torch
+
+    world, rank = _world_rank(group)
+    b = bufs
+    if world == 1 and band_pack is None:  # one owner: the filter is fused into the kNN pass
+        rx, ry, rg, nrecv = x_local, y_local, None, len(x_local)
+    else:
+        if band_pack is None:
+            def band_pack(x, y, bb, nb_, w):
+                return ctx.band_pack_query_async(grid, nb_, w, qx, qy, r, x, y, bb)
+        px, py, pg, send_counts = band_pack(x_local, y_local, base, int(grid.n), world)
+        rx, ry, rg = _exchange_records(px, py, pg, send_counts, group)
+        nrecv = len(rx)
+    if b.with_range:
+        ctx.knn_range_pp_async(grid, rx, ry, qx, qy, r, k, approximate, b.ki, b.kd, b.kc, b.hits, b.cap, b.hc)
+    else:
+        ctx.knn_pp_async(grid, rx, ry, qx, qy, r, k, b.ki, b.kd, b.kc)
+        b.hc.zero_()
+    li = b.ki.to(torch.int64)
+    if rg is None:
+        gi = torch.where(li >= 0, li + base, li).to(torch.int32)
+    else:
+        gi = torch.where(li >= 0, rg[li.clamp(min=0, max=max(nrecv - 1, 0))] if nrecv else li, li).to(torch.int32)
+    if world == 1:  # one list: it is the merged result
+        idx, dist, count = gi, b.kd, b.kc
+        b.counts[0:1].copy_(b.hc)
+    else:
+        all_gather_into(b.all_d.view(-1), b.kd, group)
+        all_gather_into(b.all_i.view(-1), gi, group)
+        ctx.knn_merge_async(b.all_d, b.all_i, world, k, k, b.mi, b.md, b.mc)
+        idx, dist, count = b.mi, b.md, b.mc
+        all_gather_into(b.counts, b.hc, group)
+    return CellsStep(idx, dist, count, b.hits, b.hc, base, rg, b.counts, rank, nrecv)
+
+
 def knn_range_cells(x_local, y_local, base: int, qx: float, qy: float, r: float, k: int, approximate: bool = False,
                     *, grid, ctx=None, group=None, band_pack: Optional[Callable] = None,
-                    local: Optional[Callable] = None, merge: Optional[Callable] = None):
+                    local: Optional[Callable] = None, merge: Optional[Callable] = None,
+                    bufs: Optional[CellsBuffers] = None):
     """kNN (k) and range (r) of one point query over a window partitioned by grid-cell key band
     (the north-star layout, mirroring the reference's filter + keyBy(gridID),
     PointPointKNNQuery.java:137-151 / PointPointRangeQuery.java:102-116): every rank packs the
@@ -174,11 +267,21 @@ def knn_range_cells(x_local, y_local, base: int, qx: float, qy: float, r: float,
     the range hits stay with their owner as window indices.
     local(x, y, qx, qy, r, k, approximate) -> (idx int32 [k] sentinel -1, dist f64 [k], hits int
     [m]), local indices.  Returns (KnnResult, (hits int64 window idx ascending, offset, total),
-    points received by this rank)."""
+    points this rank evaluated: the band-packed candidates it received, or at world 1 with the
+    default packing its whole shard -- one owner holds every band, the shuffle is the identity and
+    the kNN pass applies the G u C filter itself).
+    bufs (device engine only: local and merge not given): the enqueue-only form into those
+    preallocated rows -- returns a CellsStep (device tensors; .result() reads it back)."""
     import torch
 
+    if bufs is not None:
+        if local is not None or merge is not None:
+            raise ValueError("knn_range_cells: bufs needs the device engine (no local / merge)")
+        return _knn_range_cells_enqueue(x_local, y_local, base, qx, qy, r, k, approximate, grid, ctx, group,
+                                        band_pack, bufs)
     world, _ = _world_rank(group)
     nb = int(grid.n)
+    shortcut = world == 1 and band_pack is None
     if band_pack is None:
         def band_pack(x, y, b, nb_, w):
             return ctx.band_pack_query_async(grid, nb_, w, qx, qy, r, x, y, b)
@@ -186,7 +289,7 @@ def knn_range_cells(x_local, y_local, base: int, qx: float, qy: float, r: float,
         local = _device_local_knn_range(ctx, grid)
     if merge is None:
         merge = _device_merge(ctx)
-    if world == 1:
+    if shortcut:
         # one owner holds every key band: the filter + keyBy shuffle is the identity (the local
         # kernel applies the G u C filter itself), so the shard is evaluated where it lies
         rx, ry = x_local, y_local

@@ -355,7 +355,7 @@ def _cells_worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [1, 2, 4])
 def test_knn_range_key_band_partition_gloo(tmp_path, world):
     """The north-star layout for point queries (filter to G u C, keyBy(gridID) as key bands,
     PointPointKNNQuery.java:137-151): the merged kNN and the union of the owners' range hits equal

@@ -95,3 +95,31 @@ def test_knn_range_cells_device_world1(ctx, grid_n, r, k):
     want = np.sort(cref.range_pp(cg, x, y, Q[0], Q[1], r)).astype(np.int64)
     assert off == 0 and total == len(want)
     assert np.array_equal(np.sort(hits.cpu().numpy().astype(np.int64)), want)
+
+
+@pytest.mark.parametrize("grid_n,r,k", [(100, 0.5, 50), (1000, 0.05, 100)])
+def test_knn_range_cells_world1_forms(ctx, grid_n, r, k):
+    """World 1: the default shortcut (no pack: the kNN pass filters), a caller's band pack (the
+    device pack, then the identity exchange) and the enqueue-only form into preallocated rows
+    (no host round trip until result()) all give the same top-k, distance bits and hits."""
+    import torch
+    l = (BJ[1] - BJ[0]) / grid_n
+    ag = _abi.make_grid(BJ[0], BJ[2], l, grid_n)
+    x, y = _window(300_007, 21 + grid_n, grid_n)
+    xd, yd = torch.from_numpy(x).to("cuda:0"), torch.from_numpy(y).to("cuda:0")
+    base = 1000
+
+    def packed(xs, ys, b, nb, w):
+        return ctx.band_pack_query_async(ag, nb, w, Q[0], Q[1], r, xs, ys, b)
+    a = D.knn_range_cells(xd, yd, base, Q[0], Q[1], r, k, grid=ag, ctx=ctx)
+    p = D.knn_range_cells(xd, yd, base, Q[0], Q[1], r, k, grid=ag, ctx=ctx, band_pack=packed)
+    bufs = D.CellsBuffers(k, len(x), 1, xd.device)
+    e = D.knn_range_cells(xd, yd, base, Q[0], Q[1], r, k, grid=ag, ctx=ctx, bufs=bufs).result()
+    ra, (ha, _, ta), na = a
+    for rb, (hb, _, tb), nbv in (p, e):
+        assert rb.count == ra.count
+        assert rb.idx.cpu().tolist() == ra.idx.cpu().tolist()
+        assert torch.equal(rb.dist.cpu().view(torch.int64), ra.dist.cpu().view(torch.int64))
+        assert tb == ta and sorted(hb.cpu().tolist()) == sorted(ha.cpu().tolist())
+    assert na == len(x) and e[2] == len(x)
+    assert p[2] < len(x)  # the pack kept the G u C candidates only
