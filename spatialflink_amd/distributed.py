@@ -237,14 +237,16 @@ def _knn_range_cells_enqueue(x_local, y_local, base, qx, qy, r, k, approximate, 
     else:
         ctx.knn_pp_async(grid, rx, ry, qx, qy, r, k, b.ki, b.kd, b.kc)
         b.hc.zero_()
-    li = b.ki.to(torch.int64)
-    if rg is None:
-        gi = torch.where(li >= 0, li + base, li).to(torch.int32)
+    if rg is None and base == 0:
+        gi = b.ki  # local positions are window indices: no pass
     else:
-        gi = torch.where(li >= 0, rg[li.clamp(min=0, max=max(nrecv - 1, 0))] if nrecv else li, li).to(torch.int32)
-    if world == 1:  # one list: it is the merged result
-        idx, dist, count = gi, b.kd, b.kc
-        b.counts[0:1].copy_(b.hc)
+        li = b.ki.to(torch.int64)
+        if rg is None:
+            gi = torch.where(li >= 0, li + base, li).to(torch.int32)
+        else:
+            gi = torch.where(li >= 0, rg[li.clamp(min=0, max=max(nrecv - 1, 0))] if nrecv else li, li).to(torch.int32)
+    if world == 1:  # one list: it is the merged result, its hit count the only count
+        return CellsStep(gi, b.kd, b.kc, b.hits, b.hc, base, rg, b.hc, rank, nrecv)
     else:
         all_gather_into(b.all_d.view(-1), b.kd, group)
         all_gather_into(b.all_i.view(-1), gi, group)
