@@ -145,6 +145,13 @@ int geohip_abi_version(void);
 int geohip_range_pp(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
                     uint64_t n, double qx, double qy, double r, int approximate,
                     uint32_t* out_idx, uint64_t cap, uint64_t* out_count);
+/* geohip_range_pp over one pane of a sliding window (pane reuse): the hit
+   indices are point_base + the position in the pane (mod 2^32) -- stream positions when
+   point_base is the pane's first one, ascending -- so a pane's hits serve every window that
+   holds it with no pass over them (PointPointRangeQuery.queryIncremental, :144-245). */
+int geohip_range_pp_pane(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
+                         uint64_t n, uint32_t point_base, double qx, double qy, double r, int approximate,
+                         uint32_t* out_idx, uint64_t cap, uint64_t* out_count);
 
 int geohip_knn_pp(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
                   uint64_t n, double qx, double qy, double r, uint32_t k,

@@ -182,6 +182,8 @@ _SIGS = {
                                           POINTER(c_uint64), c_int]),
     "geohip_range_pp": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_double, c_double, c_double, c_int, _P,
                                 c_uint64, POINTER(c_uint64)]),
+    "geohip_range_pp_pane": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_uint32, c_double, c_double, c_double, c_int,
+                                     _P, c_uint64, POINTER(c_uint64)]),
     "geohip_range_pp_async": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_double, c_double, c_double, c_int,
                                       _P, c_uint64, _P]),
     "geohip_knn_pp": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_double, c_double, c_double, c_uint32, _P, _P,
@@ -492,7 +494,9 @@ class Context:
         return on_dev
 
     # ---- queries -------------------------------------------------------------------------
-    def range_pp(self, grid: Grid, x, y, qx, qy, r, approximate=False, cap=None):
+    def range_pp(self, grid: Grid, x, y, qx, qy, r, approximate=False, cap=None, point_base=None):
+        """Hit indices, ascending.  ``point_base`` (geohip_range_pp_pane): indices are point_base +
+        position (mod 2^32), a pane's stream positions."""
         x, y = _f64(x), _f64(y)
         n = len(x)
         dev = self._mem_for(x, y)
@@ -504,8 +508,12 @@ class Context:
             cap = n if cap is None else cap
             out = np.empty(max(cap, 1), dtype=np.uint32)
         cnt = c_uint64(0)
-        rc = lib.geohip_range_pp(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), n, qx, qy, r, int(approximate),
-                                 _ptr(out), cap, ctypes.byref(cnt))
+        if point_base is None:
+            rc = lib.geohip_range_pp(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), n, qx, qy, r, int(approximate),
+                                     _ptr(out), cap, ctypes.byref(cnt))
+        else:
+            rc = lib.geohip_range_pp_pane(self.h, ctypes.byref(grid), _ptr(x), _ptr(y), n, int(point_base) & 0xFFFFFFFF,
+                                          qx, qy, r, int(approximate), _ptr(out), cap, ctypes.byref(cnt))
         self._check(rc, "range_pp")
         return out[:cnt.value]
 

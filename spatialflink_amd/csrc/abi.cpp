@@ -547,12 +547,14 @@ int knn_host_pipelined(geohip_ctx* ctx, const geohip_grid* grid, const double* x
 }
 
 int range_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n, double qx,
-                  double qy, double r, int approximate, unsigned* out, uint64_t cap, uint64_t* total) {
+                  double qy, double r, int approximate, unsigned* out, uint64_t cap, uint64_t* total,
+                  uint32_t point_base = 0) {
     if (n >= 0xffffffffull) return fail(ctx, GEOHIP_ERR_UNSUPPORTED, "window larger than 2^32-1 points");
     PointPlan plan;
     int rc = plan_or_fail(ctx, grid, qx, qy, r, &plan);
     if (rc) return rc;
     RangeArgs a = make_range_args(plan, qx, qy, r);
+    a.point_base = point_base;
     const double *dx, *dy;
     rc = stage_xy(ctx, x, y, n, S_X, S_Y, &dx, &dy);
     if (rc) return rc;
@@ -809,6 +811,12 @@ int geohip_ctx_timing_kernels(geohip_ctx* ctx, double* step_ms, uint64_t* steps,
 int geohip_range_pp(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
                     double qx, double qy, double r, int approximate, uint32_t* out_idx, uint64_t cap,
                     uint64_t* out_count) {
+    return geohip_range_pp_pane(ctx, grid, x, y, n, 0u, qx, qy, r, approximate, out_idx, cap, out_count);
+}
+
+int geohip_range_pp_pane(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y, uint64_t n,
+                         uint32_t point_base, double qx, double qy, double r, int approximate, uint32_t* out_idx,
+                         uint64_t cap, uint64_t* out_count) {
     int rc = begin(ctx);
     if (rc) return rc;
     if (!out_count || (cap && !out_idx)) return fail(ctx, GEOHIP_ERR_ARG, "null output");
@@ -822,7 +830,7 @@ int geohip_range_pp(geohip_ctx* ctx, const geohip_grid* grid, const double* x, c
     }
     rc = ensure(ctx, S_TOTAL, 8);
     if (rc) return rc;
-    rc = range_enqueue(ctx, grid, x, y, n, qx, qy, r, approximate, out, cap, B<uint64_t>(ctx, S_TOTAL));
+    rc = range_enqueue(ctx, grid, x, y, n, qx, qy, r, approximate, out, cap, B<uint64_t>(ctx, S_TOTAL), point_base);
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(ctx->pinned, ctx->buf[S_TOTAL], 8, hipMemcpyDeviceToHost, ctx->stream));
     rc = queue_fault_read(ctx);

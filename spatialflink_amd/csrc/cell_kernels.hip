@@ -2502,6 +2502,42 @@ __device__ __forceinline__ void stream_push(const StreamArgs& a, StreamSink& k, 
     else stream_emit_pair(a.o, k.base + b, poly, (unsigned)(chunk0 + loc));
 }
 
+#ifndef GEOHIP_PS_BAL
+#define GEOHIP_PS_BAL 1  // 0: each lane walks its own points' entries (measurement builds)
+#endif
+// Entry balance of the exact walk (GEOHIP_PS_BAL): per wave iteration, the multi-entry cells'
+// entries are numbered across the wave and every lane takes kBalItems of them per step, so a step
+// serves the wave's entries evenly (a lane's own list had ~7 entries on average and ~14 at the
+// wave's maximum: half of every step's lanes idle) and an iteration needs one round of entry
+// gathers, not one per entry of the longest list.  Per wave in LDS: one record per multi-entry
+// slot (kBalRecs) and a bitmap of the entries that start a record (kBalWords x 64 entries); an
+// iteration that exceeds either takes the per-lane walk.
+constexpr unsigned kBalRecs = 128;
+constexpr unsigned kBalWords = 16;
+constexpr unsigned kBalItems = 4;
+
+// the class decision of one entry (ex, word) for a point with subcell / NaN bits sw:
+// PointPolygonRangeQuery.java:105-121 -- G -> pair; C -> by the subcell class (mixed: candidate)
+__device__ __forceinline__ void stream_decide(uint32_t ex, uint32_t word, unsigned sw, bool& hit, bool& need) {
+    constexpr unsigned kNanBit = 16u;
+    hit = need = false;
+    if (ex == kNoEntry) return;
+    if (!(ex & kEntC)) {
+        hit = true;
+        return;
+    }
+    // a decided class holds for every point in the cell's coordinate box: not for NaN
+    // coordinates (cell 0 by Java's (int) NaN)
+    uint32_t kc = kClsMixed;
+    if (!(sw & kNanBit)) {
+        if (word == kWordHit) kc = kClsHit;
+        else if (word == kWordMiss) kc = kClsMiss;
+        else kc = (word >> (2 * (sw & 15u))) & 3u;
+    }
+    hit = kc == kClsHit;
+    need = kc == kClsMixed;
+}
+
 // One chunk's points (all waves of the block).  Phase A: every point of the wave's iterations --
 // coordinates (next iteration's in flight), cell, subcell, and its table head gather issued;
 // phase B: the entries, with all the wave's heads already in flight from phase A (a head gather
@@ -2510,7 +2546,7 @@ __device__ __forceinline__ void stream_push(const StreamArgs& a, StreamSink& k, 
 // out-of-grid polygons (reloaded).
 template <bool APPROX, bool KL>
 __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned* kl, uint64_t c0, uint64_t c1,
-                                             StreamSink& ps, StreamSink& cs) {
+                                             StreamSink& ps, StreamSink& cs, uint2* brec, unsigned long long* bbm) {
     const int wid = threadIdx.x / kWave, lane = lane_id();
     const TileGeom& g = a.g;
     const unsigned nb = (unsigned)g.nb;
@@ -2593,7 +2629,93 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
             st[t] = s == 0 ? w : (st[t] | (w << (8 * s)));
         }
     }
-    if (!APPROX && GEOHIP_PS_BATCH > 0) {
+    if (!APPROX && GEOHIP_PS_BAL) {
+        // Phase B (exact, balanced): per iteration, single-entry slots decided by their own lanes
+        // (the head is the entry: no gather), multi-entry slots recorded for the wave
+#pragma unroll
+        for (unsigned t = 0; t < kIters; t++) {
+            unsigned cnt[4], lc = 0, ln = 0;
+#pragma unroll
+            for (int sl = 0; sl < 4; sl++) {
+                const uint2 h = hd[t][sl];
+                const bool multi = h.x != kNoEntry && (h.x & kMulti);
+                cnt[sl] = multi ? (h.x & ~kMulti) : 0u;
+                lc += cnt[sl];
+                ln += multi ? 1u : 0u;
+                bool hit = false, need = false;
+                if (!multi) stream_decide(h.x, h.y, st[t] >> (8 * sl), hit, need);
+                const unsigned loc = loc_of(t, sl);
+                stream_push<false>(a, ps, hit, h.x & ~kEntC, loc, c0);
+                stream_push<true>(a, cs, need, h.x & ~kEntC, loc, c0);
+            }
+            const unsigned ic = wave_incl_scan(lc), in = wave_incl_scan(ln);
+            const unsigned T = (unsigned)__builtin_amdgcn_readlane((int)ic, kWave - 1);
+            const unsigned R = (unsigned)__builtin_amdgcn_readlane((int)in, kWave - 1);
+            if (T == 0) continue;
+            if (T > kBalWords * kWave || R > kBalRecs) {
+                // rare (cells of many polygons): each lane walks its own multi-entry slots
+#pragma unroll
+                for (int sl = 0; sl < 4; sl++) {
+                    unsigned e = cnt[sl] ? hd[t][sl].y : 0u;
+                    const unsigned e1 = e + cnt[sl];
+                    const unsigned sw = st[t] >> (8 * sl), loc = loc_of(t, sl);
+                    while (__ballot(e < e1)) {
+                        uint2 en = make_uint2(kNoEntry, 0u);
+                        if (e < e1) en = a.ent[e++];
+                        bool hit, need;
+                        stream_decide(en.x, en.y, sw, hit, need);
+                        stream_push<false>(a, ps, hit, en.x & ~kEntC, loc, c0);
+                        stream_push<true>(a, cs, need, en.x & ~kEntC, loc, c0);
+                    }
+                }
+                continue;
+            }
+            // records (first entry, loc | sw << 12 | start << 17) and the entry-start bitmap
+            if ((unsigned)lane < (T + kWave - 1) / kWave) bbm[lane] = 0ull;
+            wave_lds_sync();
+            unsigned p = ic - lc, r = in - ln;
+#pragma unroll
+            for (int sl = 0; sl < 4; sl++) {
+                if (cnt[sl]) {
+                    brec[r] = make_uint2(hd[t][sl].y, loc_of(t, sl) | (((st[t] >> (8 * sl)) & 31u) << 12) | (p << 17));
+                    atomicOr(&bbm[p >> 6], 1ull << (p & 63u));
+                    r++;
+                    p += cnt[sl];
+                }
+            }
+            wave_lds_sync();
+            // entries w = w0 + 64 u + lane: the record = starts at or below w, minus one
+            unsigned carry = 0;
+            const unsigned long long le = ~0ull >> (63 - lane);
+            for (unsigned w0 = 0; w0 < T; w0 += kBalItems * kWave) {  // wave-uniform
+                uint2 en[kBalItems];
+                unsigned ry[kBalItems];
+#pragma unroll
+                for (unsigned u = 0; u < kBalItems; u++) {
+                    const unsigned wb = w0 + u * kWave, w = wb + (unsigned)lane;
+                    const unsigned long long word = wb < T ? bbm[wb >> 6] : 0ull;
+                    const unsigned rr = carry + (unsigned)__popcll(word & le) - 1u;
+                    carry += (unsigned)__popcll(word);
+                    en[u] = make_uint2(kNoEntry, 0u);
+                    ry[u] = 0u;
+                    if (w < T) {
+                        const uint2 rec = brec[rr];
+                        ry[u] = rec.y;
+                        en[u] = a.ent[rec.x + (w - (rec.y >> 17))];
+                    }
+                }
+#pragma unroll
+                for (unsigned u = 0; u < kBalItems; u++) {
+                    bool hit, need;
+                    stream_decide(en[u].x, en[u].y, ry[u] >> 12, hit, need);
+                    const unsigned loc = ry[u] & (kStreamChunk - 1);
+                    stream_push<false>(a, ps, hit, en[u].x & ~kEntC, loc, c0);
+                    stream_push<true>(a, cs, need, en[u].x & ~kEntC, loc, c0);
+                }
+            }
+            wave_lds_sync();  // the records and bitmap are reused by the next iteration
+        }
+    } else if (!APPROX && GEOHIP_PS_BATCH > 0) {
         // Phase B (exact): each lane's entries of its kIters * 4 points form ONE list, numbered
         // 0 .. tot-1 slot after slot; entry k's address follows from the heads alone (slot = the
         // last slot whose list start is <= k; a multi cell's entries are consecutive in cell_ent),
@@ -2824,6 +2946,9 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
     __shared__ unsigned s_np, s_nc;
     __shared__ unsigned s_wp[kStreamNW], s_wc[kStreamNW];  // per-wave staged counts
     __shared__ unsigned long long s_pb, s_cb;
+    constexpr bool kBal = !APPROX && GEOHIP_PS_BAL;
+    __shared__ uint2 brec[kBal ? kStreamNW * kBalRecs : 1];             // balanced walk: records
+    __shared__ unsigned long long bbm[kBal ? kStreamNW * kBalWords : 1];  // and entry-start bitmaps
     constexpr unsigned kWPair = kSPairCap / kStreamNW, kWCand = kSCandCap / kStreamNW;
     const int wid = threadIdx.x / kWave, lane = lane_id();
     if (KL)
@@ -2835,7 +2960,9 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
         const uint64_t c1 = c0 + kStreamChunk < a.n ? c0 + kStreamChunk : a.n;
         StreamSink ps{ppk + wid * kWPair, &s_np, kWPair, false, 0, 0u, 0u};
         StreamSink cs{cpk + (APPROX ? 0 : wid * kWCand), &s_nc, APPROX ? 0u : kWCand, false, 0, 0u, 0u};
-        stream_chunk<APPROX, KL>(a, kl, c0, c1, ps, cs);
+        uint2* wrec = kBal ? brec + wid * kBalRecs : brec;
+        unsigned long long* wbm = kBal ? bbm + wid * kBalWords : bbm;
+        stream_chunk<APPROX, KL>(a, kl, c0, c1, ps, cs, wrec, wbm);
         if (GEOHIP_PS_ABL == 3 && ps.acc + cs.acc == 0x9e3779b9u) a.o.ptotal[0] = 1;
         if (lane == 0) {
             s_wp[wid] = ps.n;
@@ -2882,7 +3009,8 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
             __syncthreads();
             StreamSink pd{ppk, &s_np, kSPairCap, true, pb, 0u, 0u};
             StreamSink cd{cpk, &s_nc, kSCandCap, true, cb, 0u, 0u};
-            stream_chunk<APPROX, KL>(a, kl, c0, c1, pd, cd);
+            stream_chunk<APPROX, KL>(a, kl, c0, c1, pd, cd, kBal ? brec + wid * kBalRecs : brec,
+                                     kBal ? bbm + wid * kBalWords : bbm);
         }
     }
 }
@@ -5067,7 +5195,14 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             sa.o = so;
             if (nchunks) {
                 const unsigned nblk = (unsigned)std::min<uint64_t>(nchunks, (uint64_t)ctx_cus(ctx) * kStreamBlocksPerCU);
+#ifdef GEOHIP_PS_NOKEEP  // measurement builds: no cell bitmap (every in-grid point gathers its head)
+                sa.keep = nullptr;
+#endif
+#ifdef GEOHIP_PS_NOKL  // measurement builds: the cell bitmap read from global memory, not staged in LDS
+                const bool kl = false;
+#else
                 const bool kl = sa.keep && sa.keep_words <= kKeepLds;
+#endif
                 if (approximate) {
                     if (kl) tlaunch(ctx, ppoly_stream<true, true>, nblk, kStreamNW * kWave, 0, st, sa);
                     else tlaunch(ctx, ppoly_stream<true, false>, nblk, kStreamNW * kWave, 0, st, sa);

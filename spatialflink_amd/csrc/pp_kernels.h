@@ -22,6 +22,8 @@ struct RangeArgs {
     int32_t ng, nc;
     double qx, qy, r;
     double r2lo, r2hi;  // squared screens (device_common.h kSqLo/kSqHi); r2lo < 0 disables
+    uint32_t point_base;  // added to every hit index (mod 2^32): a pane's stream position
+    uint32_t pad;
 };
 
 // kNN counter scratch (zeroed once; every launch re-arms what it used): word 0 = spill count,

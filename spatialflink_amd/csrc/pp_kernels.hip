@@ -1150,7 +1150,7 @@ __device__ __forceinline__ void pass_range_emit(const PassRangeIo& rio, const un
     __syncthreads();
     unsigned long long obase = excl_sh;
     for (int w = 0; w < wid; w++) obase += wsum[w];
-    const unsigned ibase = (unsigned)p0;
+    const unsigned ibase = (unsigned)p0 + rio.a.point_base;
     unsigned sc = 0;
     for (unsigned w0 = wb; w0 < we; w0 += kWave) {
         const unsigned long long mine = w0 + lane < we ? bmask[w0 + lane] : 0ull;
@@ -1943,7 +1943,7 @@ __global__ __launch_bounds__(kRangeNW * kWave) void range_fused(const double* __
         const unsigned wb = (unsigned)wid * wpw;
         const unsigned we = wb + wpw < nw ? wb + wpw : nw;
         unsigned long long obase = excl + (wb < we ? wpre[wb] : 0u);
-        const unsigned ibase = (unsigned)(u0 * kUnitPts);
+        const unsigned ibase = (unsigned)(u0 * kUnitPts) + a.point_base;
         unsigned* stg = reinterpret_cast<unsigned*>(st.cx);  // the wave's idle candidate stage
         unsigned sc = 0;
         for (unsigned w0 = wb; w0 < we; w0 += kWave) {
@@ -1986,7 +1986,7 @@ __global__ __launch_bounds__(1024) void scan_units(const unsigned* __restrict__ 
 
 __global__ __launch_bounds__(kBlock) void range_emit(const unsigned long long* __restrict__ bitmask,
                                                      const uint64_t* __restrict__ offs, uint64_t units,
-                                                     unsigned* __restrict__ out, uint64_t cap) {
+                                                     unsigned* __restrict__ out, uint64_t cap, unsigned point_base) {
     const int lane = lane_id();
     const uint64_t unit = (uint64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
     if (unit >= units) return;
@@ -2000,7 +2000,7 @@ __global__ __launch_bounds__(kBlock) void range_emit(const unsigned long long* _
         if (lane >= o) incl += v;
     }
     uint64_t pos = offs[unit] + (incl - c);
-    const unsigned base = (unsigned)(unit * kUnitPts) + (unsigned)(wq * 64 + q * 16);
+    const unsigned base = (unsigned)(unit * kUnitPts) + (unsigned)(wq * 64 + q * 16) + point_base;
     while (bits) {
         const int b = __builtin_ctz(bits);
         bits &= bits - 1;
@@ -2276,7 +2276,7 @@ hipError_t launch_range(const double* x, const double* y, uint64_t n, const Rang
     scan_units<<<1, 1024, 0, st>>>(unit_count, units, offs, total);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    range_emit<<<(unsigned)blocks, kBlock, 0, st>>>(bitmask, offs, units, out, cap);
+    range_emit<<<(unsigned)blocks, kBlock, 0, st>>>(bitmask, offs, units, out, cap, a.point_base);
     if (ev1) (void)hipEventRecord(ev1, st);  // timed region: all three kernels
     return hipGetLastError();
 }

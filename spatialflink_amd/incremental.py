@@ -8,9 +8,10 @@ newest slide of each window (``point.timeStampMillisec >= timeWindow.getEnd() - 
 window (``>= timeWindow.getStart() + slideStep``, :201-208).  Here every pane is evaluated once
 on the GPU when it arrives; a window's result is assembled from the last P panes' results:
 
-* range: the concatenation of the panes' hit lists, each offset by the pane's position in the
-  window -- the window-local indices a full evaluation of the window returns (the range
-  predicate is per point, so it is the same set, and ascending);
+* range: the panes' hit lists, each computed once by geohip_range_pp_pane with the pane's stream
+  position as the index base -- stream positions, ascending; concatenated pane after pane they
+  are the window's hits (the range predicate is per point) with no pass over them per window
+  (window-local index = stream position - the window's first position);
 * kNN: the k smallest of the panes' top-k lists (geohip_knn_merge_async on the device) -- the
   top-k of a union is the top-k of the union of top-ks, so the same (dist, idx) list as a full
   evaluation of the window.
@@ -33,27 +34,43 @@ def panes_per_window(window_size: int, slide_step: int) -> int:
 
 
 class IncrementalRange:
-    """Point-point range over sliding windows with pane reuse."""
+    """Point-point range over sliding windows with pane reuse: each pane's hits are computed once,
+    by geohip_range_pp_pane with the pane's stream position as the index base, so they are stream
+    positions and serve every window that holds the pane unchanged -- no per-window pass over
+    them (the round-4 form added each pane's window offset with a torch pass per window)."""
 
     def __init__(self, ctx: _abi.Context, grid: _abi.Grid, qx: float, qy: float, r: float,
                  approximate: bool = False, panes: int = 2):
         self.ctx, self.grid, self.q, self.r, self.approx = ctx, grid, (qx, qy), r, approximate
-        self.panes = deque(maxlen=panes)  # (pane size, hits of the pane, pane-local indices)
+        self.panes = deque(maxlen=panes)  # (first stream position, pane size, hits as stream positions)
+        self.pos = 0  # stream position of the next pane's first point
 
     def push(self, x, y):
-        """Evaluate the new pane; returns the window result (window-local indices, ascending)."""
-        hits = self.ctx.range_pp(self.grid, x, y, self.q[0], self.q[1], self.r, self.approx)
-        self.panes.append((len(x), hits))
+        """Evaluate the new pane; returns the window's hits (window())."""
+        hits = self.ctx.range_pp(self.grid, x, y, self.q[0], self.q[1], self.r, self.approx, point_base=self.pos)
+        self.panes.append((self.pos, len(x), hits))
+        self.pos = (self.pos + len(x)) & 0xFFFFFFFF
         return self.window()
 
+    @property
+    def window_start(self) -> int:
+        """Stream position of the window's first point (its local index 0)."""
+        return self.panes[0][0] if self.panes else self.pos
+
     def window(self):
+        """The window's hits pane by pane (stream positions, ascending): a list of the panes' hit
+        arrays, nothing recomputed or copied."""
+        return [hits for _, _, hits in self.panes]
+
+    def window_local(self):
+        """The window's hits as window-local indices in one int64 array (a convenience: one pass
+        over the hits, (stream position - window_start) mod 2^32)."""
         import numpy as np
-        offs = np.cumsum([0] + [size for size, _ in self.panes])
-        if self.panes and _abi._is_device(self.panes[0][1]):
+        parts, s0 = self.window(), self.window_start
+        if parts and _abi._is_device(parts[0]):
             import torch
-            return torch.cat([hits.to(torch.int64) + int(o) for (_, hits), o in zip(self.panes, offs)])
-        return np.concatenate([np.zeros(0, np.int64)] +
-                              [hits.astype(np.int64) + o for (_, hits), o in zip(self.panes, offs)])
+            return (torch.cat([h.to(torch.int64) for h in parts]) - s0) & 0xFFFFFFFF
+        return (np.concatenate([np.zeros(0, np.int64)] + [np.asarray(h).astype(np.int64) for h in parts]) - s0) & 0xFFFFFFFF
 
 
 class IncrementalPPolyRange:
@@ -139,7 +156,8 @@ class IncrementalKNN:
 
 def run_incremental_range(ctx, grid, panes, qx, qy, r, approximate=False, window_size=10, slide_step=5):
     """Generator over windows: for each pane (x, y) of the stream, the result of the window that
-    ends with it (PointPointRangeQuery.queryIncremental semantics)."""
+    ends with it as window-local indices (PointPointRangeQuery.queryIncremental semantics)."""
     inc = IncrementalRange(ctx, grid, qx, qy, r, approximate, panes_per_window(window_size, slide_step))
     for x, y in panes:
-        yield inc.push(x, y)
+        inc.push(x, y)
+        yield inc.window_local()

@@ -200,7 +200,8 @@ class PointPointRangeQuery(_Operator):
                                self.conf.approximate_query,
                                panes_per_window(self.conf.window_size, self.conf.slide_step))
         for pane in panes:
-            yield inc.push(pane.x, pane.y)
+            inc.push(pane.x, pane.y)
+            yield inc.window_local()
 
 
 class PointPointKNNQuery(_Operator):

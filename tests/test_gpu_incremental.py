@@ -41,7 +41,9 @@ def test_incremental_range_equals_full_window(ctx, p):
     panes = pane_stream(11)
     inc = IncrementalRange(ctx, ag, Q[0], Q[1], 0.5, False, p)
     for j, (x, y) in enumerate(panes):
-        got = inc.push(torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()).cpu().numpy()
+        parts = inc.push(torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda())
+        # the panes' hits are stream positions (geohip_range_pp_pane): no per-window pass
+        got = torch.cat([h.to(torch.int64) for h in parts]).cpu().numpy() - inc.window_start
         win = panes[max(0, j - p + 1):j + 1]
         wx = np.concatenate([w[0] for w in win])
         wy = np.concatenate([w[1] for w in win])
@@ -124,3 +126,18 @@ def test_pane_merge_many_panes(ctx, p, k):
                              Q[0], Q[1], 0.5, k)
         assert gi.cpu().numpy().tolist() == wi.tolist(), j
         assert np.array_equal(gd.cpu().numpy().view(np.uint64), wd.view(np.uint64)), j
+
+
+@pytest.mark.parametrize("n", [300_000, 70_000_000])
+def test_range_pane_point_base(ctx, n):
+    """geohip_range_pp_pane: the hits of geohip_range_pp plus the base (mod 2^32), in the one-kernel
+    range path and (70M points) the multi-launch one; a base near 2^32 wraps."""
+    import torch
+    ag, _ = grids(100)
+    x = torch.empty(n, dtype=torch.float64, device="cuda")
+    y = torch.empty(n, dtype=torch.float64, device="cuda")
+    ctx.synth_uniform_async(x, y, 0, 41, BJ)
+    plain = ctx.range_pp(ag, x, y, Q[0], Q[1], 0.5).to(torch.int64)
+    for base in (12345, (1 << 32) - 1000):
+        got = ctx.range_pp(ag, x, y, Q[0], Q[1], 0.5, point_base=base).to(torch.int64) & 0xFFFFFFFF
+        assert torch.equal(got, (plain + base) & 0xFFFFFFFF)
