@@ -2411,10 +2411,15 @@ struct StreamOut {
     unsigned point_base;            // added to every point index of a pair (pane stream positions)
     unsigned long long* ptotal;     // pairs: reservation cursor (zero before; an async call's count)
     unsigned long long* ctotal;     // candidates: reservation cursor (zero before)
+    unsigned long long* both;       // non-null: one cursor for both, pairs in the low kPackBits bits
+                                    // (one atomic per chunk; ppoly_cand_plan unpacks it into the two)
     uint64_t ccap;                  // candidates past it are counted only (the host regrows, re-runs)
     unsigned* cpoly;                // candidates in chunk order: polygon (the grouping reads these),
     double4* crec;                  // and (x, y, point bits, -) -- one 32-byte sector per gather
 };
+
+constexpr unsigned kPackBits = 34;  // packed cursor: pairs < 2^34, candidates < 2^30 (host-checked)
+constexpr unsigned long long kPackMask = (1ull << kPackBits) - 1ull;
 
 struct StreamArgs {
     const double* x;
@@ -2544,9 +2549,15 @@ __device__ __forceinline__ void stream_decide(uint32_t ex, uint32_t word, unsign
 // per iteration waited on at once cost ~1 us of latency per iteration under the streaming
 // traffic).  Phase B needs no coordinates except for the approximate bbox test and the rare
 // out-of-grid polygons (reloaded).
+// Coordinates of the first wave iteration of chunk [c0, c1) (loaded by stream_chunk itself, or by the
+// kernel ahead of the previous chunk's write-out: its loads then return before those stores).
+struct StreamPre {
+    double x[4], y[4];
+};
 template <bool APPROX, bool KL>
 __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned* kl, uint64_t c0, uint64_t c1,
-                                             StreamSink& ps, StreamSink& cs, uint2* brec, unsigned long long* bbm) {
+                                             StreamSink& ps, StreamSink& cs, uint2* brec, unsigned long long* bbm,
+                                             const StreamPre* pre) {
     const int wid = threadIdx.x / kWave, lane = lane_id();
     const TileGeom& g = a.g;
     const unsigned nb = (unsigned)g.nb;
@@ -2588,7 +2599,15 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
     uint2 hd[kIters][4];
     unsigned st[kIters];  // one byte per point
     double nx[4], ny[4];
-    load(0, nx, ny);
+    if (pre) {
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            nx[s] = pre->x[s];
+            ny[s] = pre->y[s];
+        }
+    } else {
+        load(0, nx, ny);
+    }
 #pragma unroll
     for (unsigned t = 0; t < kIters; t++) {
         double qx[4], qy[4];
@@ -2954,6 +2973,31 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
     if (KL)
         for (unsigned t = threadIdx.x; t < a.keep_words; t += kStreamNW * kWave) kl[t] = a.keep[t];
     const unsigned nchunks = (unsigned)((a.n + kStreamChunk - 1) / kStreamChunk);
+    // the first wave iteration's coordinates of the block's next chunk, loaded before the current
+    // chunk's reservation and pair stores (gfx9: one vmcnt for loads and stores -- loads issued
+    // after the stores would wait for them to drain)
+    StreamPre pre;
+    auto prefetch = [&](unsigned v) {
+        const uint64_t b0 = (uint64_t)v * kStreamChunk + (uint64_t)wid * kStreamPts;
+        const uint64_t b1 = (uint64_t)v * kStreamChunk + kStreamChunk < a.n ? (uint64_t)v * kStreamChunk + kStreamChunk : a.n;
+        const uint64_t i0 = b0 + 2 * (uint64_t)lane, i1 = i0 + 128;
+        if (b0 + kStreamPts <= b1) {
+            const double2 ax = *reinterpret_cast<const double2*>(a.x + i0);
+            const double2 bx = *reinterpret_cast<const double2*>(a.x + i1);
+            const double2 ay = *reinterpret_cast<const double2*>(a.y + i0);
+            const double2 by = *reinterpret_cast<const double2*>(a.y + i1);
+            pre.x[0] = ax.x; pre.x[1] = ax.y; pre.x[2] = bx.x; pre.x[3] = bx.y;
+            pre.y[0] = ay.x; pre.y[1] = ay.y; pre.y[2] = by.x; pre.y[3] = by.y;
+        } else {
+            const uint64_t id[4] = {i0, i0 + 1, i1, i1 + 1};
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                pre.x[s] = id[s] < b1 ? a.x[id[s]] : 0.0;
+                pre.y[s] = id[s] < b1 ? a.y[id[s]] : 0.0;
+            }
+        }
+    };
+    if (blockIdx.x < nchunks) prefetch(blockIdx.x);
     for (unsigned vb = blockIdx.x; vb < nchunks; vb += gridDim.x) {
         __syncthreads();  // the previous chunk's stage is drained (and the bitmap staged)
         const uint64_t c0 = (uint64_t)vb * kStreamChunk;
@@ -2962,7 +3006,8 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
         StreamSink cs{cpk + (APPROX ? 0 : wid * kWCand), &s_nc, APPROX ? 0u : kWCand, false, 0, 0u, 0u};
         uint2* wrec = kBal ? brec + wid * kBalRecs : brec;
         unsigned long long* wbm = kBal ? bbm + wid * kBalWords : bbm;
-        stream_chunk<APPROX, KL>(a, kl, c0, c1, ps, cs, wrec, wbm);
+        stream_chunk<APPROX, KL>(a, kl, c0, c1, ps, cs, wrec, wbm, &pre);
+        if (vb + gridDim.x < nchunks) prefetch(vb + gridDim.x);
         if (GEOHIP_PS_ABL == 3 && ps.acc + cs.acc == 0x9e3779b9u) a.o.ptotal[0] = 1;
         if (lane == 0) {
             s_wp[wid] = ps.n;
@@ -2981,8 +3026,15 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
             nc += wc;
         }
         if (threadIdx.x == 0) {
-            s_pb = np ? atomicAdd(a.o.ptotal, (unsigned long long)np) : 0ull;
-            s_cb = nc ? atomicAdd(a.o.ctotal, (unsigned long long)nc) : 0ull;
+            if (a.o.both) {  // one reservation for the pairs and the candidates
+                const unsigned long long v =
+                    (np || nc) ? atomicAdd(a.o.both, (unsigned long long)np | ((unsigned long long)nc << kPackBits)) : 0ull;
+                s_pb = v & kPackMask;
+                s_cb = v >> kPackBits;
+            } else {
+                s_pb = np ? atomicAdd(a.o.ptotal, (unsigned long long)np) : 0ull;
+                s_cb = nc ? atomicAdd(a.o.ctotal, (unsigned long long)nc) : 0ull;
+            }
         }
         __syncthreads();
         const unsigned long long pb = s_pb, cb = s_cb;
@@ -3010,7 +3062,7 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
             StreamSink pd{ppk, &s_np, kSPairCap, true, pb, 0u, 0u};
             StreamSink cd{cpk, &s_nc, kSCandCap, true, cb, 0u, 0u};
             stream_chunk<APPROX, KL>(a, kl, c0, c1, pd, cd, kBal ? brec + wid * kBalRecs : brec,
-                                     kBal ? bbm + wid * kBalWords : bbm);
+                                     kBal ? bbm + wid * kBalWords : bbm, nullptr);
         }
     }
 }
@@ -3050,6 +3102,9 @@ constexpr unsigned kCandThreads = 1024;
 constexpr unsigned kCandPer = 4;  // candidates per thread per round (loads in flight together)
 struct CandGroup {
     const unsigned long long* ccount;  // candidate total (StreamOut::ctotal)
+    const unsigned long long* both;    // the stream's packed cursor (StreamOut::both) or null
+    unsigned long long* ptotal;        // with both: the pair and candidate totals ppoly_cand_plan
+    unsigned long long* ctotal;        // unpacks it into (ptotal, the exact tests' cursor, and ccount)
     uint64_t ccap;
     unsigned* fault;                   // async calls: the ctx's fault word (kFaultCandOverflow), else null
     unsigned long long* need;          // async calls: the candidate count an overflowing call needed
@@ -3063,7 +3118,7 @@ struct CandGroup {
 };
 
 __device__ __forceinline__ uint64_t cand_n(const CandGroup& c) {
-    const unsigned long long n = *c.ccount;
+    const unsigned long long n = c.both ? (*c.both >> kPackBits) : *c.ccount;
     return n < c.ccap ? n : c.ccap;
 }
 __device__ __forceinline__ void cand_range(const CandGroup& c, uint64_t& b0, uint64_t& b1) {
@@ -3155,9 +3210,14 @@ __global__ __launch_bounds__(kCandThreads) void ppoly_cand_plan(CandGroup c) {
     }
     if (threadIdx.x == 0) {
         *c.nitems = carry_i;
+        if (c.both) {  // the stream's packed cursor into the two totals (ppoly_cand_eval appends pairs)
+            const unsigned long long v = *c.both;
+            *c.ptotal = v & kPackMask;
+            *c.ctotal = v >> kPackBits;
+        }
         // an async call cannot rerun with a larger buffer: the overflow (the candidates past ccap
         // are untested, the pairs incomplete) and the size it needed go to the ctx's fault block
-        const unsigned long long nc = *c.ccount;
+        const unsigned long long nc = c.both ? (*c.both >> kPackBits) : *c.ccount;
         if (c.fault && nc > c.ccap) {
             atomicOr(c.fault, kFaultCandOverflow);
             atomicMax(c.need, nc);
@@ -4769,6 +4829,7 @@ struct PolyCache {
     std::vector<uint32_t> skeep;
     std::vector<uint32_t> opoly;
     uint64_t last_cand = 0;           // candidates of the previous step (sizes the buffer)
+    uint32_t max_ent = 0;             // most entries of one cell (bounds a point's pairs + candidates)
     void* dev_blob = nullptr;  // J_POLY buffer holding the uploaded tables
     size_t blob_bytes = 0;
 };
@@ -4899,6 +4960,7 @@ void build_stream_table(PolyCache& c, uint32_t npoly, int32_t nb, bool r_is_max)
         c.cell_head[2 * k] = kNoEntry;
         if (e == b) continue;
         c.skeep[k >> 5] |= 1u << (k & 31);
+        if (e - b > c.max_ent) c.max_ent = e - b;
         if (e - b == 1) {
             c.cell_head[2 * k] = c.cell_ent[2 * (size_t)b];
             c.cell_head[2 * k + 1] = c.cell_ent[2 * (size_t)b + 1];
@@ -5173,6 +5235,10 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             so.point_base = point_base;
             so.ptotal = async ? reinterpret_cast<unsigned long long*>(count_dev) : reinterpret_cast<unsigned long long*>(misc);
             so.ctotal = reinterpret_cast<unsigned long long*>(misc) + 1;
+            // one reservation atomic per chunk when both counts fit the packed fields (a point yields
+            // at most its cell's entries plus the out-of-grid polygons as pairs or candidates)
+            so.both = (cands && (uint64_t)n * (pc->max_ent + pc->opoly.size()) < (1ull << (64 - kPackBits)))
+                          ? reinterpret_cast<unsigned long long*>(misc) + 3 : nullptr;
             so.ccap = cands ? ccap : 0;
             char* cb = reinterpret_cast<char*>(cbuf);
             so.cpoly = cands ? reinterpret_cast<unsigned*>(cb) : nullptr;
@@ -5215,6 +5281,9 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
                 char* sb = reinterpret_cast<char*>(sbuf);
                 CandGroup cg;
                 cg.ccount = so.ctotal;
+                cg.both = so.both;
+                cg.ptotal = so.ptotal;
+                cg.ctotal = so.ctotal;
                 cg.ccap = ccap;
                 cg.fault = fault;
                 cg.need = fault ? reinterpret_cast<unsigned long long*>(fault + 2) : nullptr;
