@@ -3069,7 +3069,7 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
 
 // Pairs of the exact tests: per-wave LDS buffers appended behind the stream's pairs, one global
 // atomic per buffer on the pair total (the stream's last chunk wrote it before this launch).
-constexpr int kSPairs = 512;
+constexpr unsigned kSPairs = 512;
 __device__ __forceinline__ void spairs_flush(uint2* buf, unsigned& cnt, const StreamOut& o) {
     wave_lds_sync();
     unsigned lo = 0, hi = 0;
@@ -3083,13 +3083,14 @@ __device__ __forceinline__ void spairs_flush(uint2* buf, unsigned& cnt, const St
     wave_lds_sync();
     cnt = 0;
 }
+template <unsigned CAP = kSPairs>
 __device__ __forceinline__ void spairs_push(uint2* buf, unsigned& cnt, bool hit, unsigned poly, unsigned idx,
                                             const StreamOut& o) {
     const unsigned long long m = __ballot(hit);
     if (!m) return;
     if (hit) buf[cnt + lanes_below(m)] = make_uint2(poly, idx);
     cnt += (unsigned)__popcll(m);
-    if (cnt > (unsigned)(kSPairs - kWave)) spairs_flush(buf, cnt, o);
+    if (cnt > CAP - (unsigned)kWave) spairs_flush(buf, cnt, o);
 }
 
 // Grouping of the candidates by polygon: a counting sort with no global atomics.  kCandGroups
@@ -3251,17 +3252,33 @@ __global__ __launch_bounds__(kCandThreads) void ppoly_cand_scatter(CandGroup c) 
 // ring ids, fp32 segment boxes and slab lists staged in LDS as in ppoly_eval.  The slice is
 // ordered by y slab in LDS first (counting sort, 64 bins), so the lanes of a wave mostly walk
 // the same crossing and distance lists (equal trip counts, broadcast LDS reads).
+// LDS of the candidate evaluation, sized for 4 blocks per CU (<= 40 KB: 4 waves per SIMD; the
+// round-4 sizes -- 512 vertices, 2048 slab entries, 512 staged pairs per wave, 58.6 KB -- left 2
+// blocks per CU and this latency-bound pass at 2 waves per SIMD).  Larger rings and slab lists
+// are read from global memory (as ppoly_eval does past its limits).
+#ifndef GEOHIP_CE_VERTS
+#define GEOHIP_CE_VERTS 256
+#endif
+#ifndef GEOHIP_CE_SLAB
+#define GEOHIP_CE_SLAB 1024
+#endif
+#ifndef GEOHIP_CE_PAIRS
+#define GEOHIP_CE_PAIRS 256
+#endif
+constexpr int kEvalLdsVerts = GEOHIP_CE_VERTS;
+constexpr int kEvalLdsSlab = GEOHIP_CE_SLAB;
+constexpr unsigned kEvalPairs = GEOHIP_CE_PAIRS;
 __global__ __launch_bounds__(kTB) void ppoly_cand_eval(CandGroup c, const PolyDev* __restrict__ polys,
                                                        const double* __restrict__ vx, const double* __restrict__ vy,
                                                        const ring_id_t* __restrict__ vring,
                                                        const double* __restrict__ renv,
                                                        const uint16_t* __restrict__ slabs, double r, StreamOut o) {
-    __shared__ double lvx[kMaxLdsVerts];
-    __shared__ double lvy[kMaxLdsVerts];
-    __shared__ ring_id_t lvr[kMaxLdsVerts];
-    __shared__ float4 lsb[kMaxLdsVerts];
-    __shared__ uint16_t lsl[kMaxLdsSlab];
-    __shared__ uint2 pbuf[kTB / kWave][kSPairs];
+    __shared__ double lvx[kEvalLdsVerts];
+    __shared__ double lvy[kEvalLdsVerts];
+    __shared__ ring_id_t lvr[kEvalLdsVerts];
+    __shared__ float4 lsb[kEvalLdsVerts];
+    __shared__ uint16_t lsl[kEvalLdsSlab];
+    __shared__ uint2 pbuf[kTB / kWave][kEvalPairs];
     __shared__ double lqx[kCandItem], lqy[kCandItem];
     __shared__ unsigned lqi[kCandItem];
     __shared__ unsigned scnt[64];
@@ -3274,8 +3291,8 @@ __global__ __launch_bounds__(kTB) void ppoly_cand_eval(CandGroup c, const PolyDe
         const uint4 w = c.items[it];
         const unsigned poly = w.x, m = w.z - w.y;
         const PolyDev P = polys[poly];
-        const bool v_lds = P.nv <= (uint32_t)kMaxLdsVerts;
-        const bool s_lds = P.llen <= (uint32_t)kMaxLdsSlab;
+        const bool v_lds = P.nv <= (uint32_t)kEvalLdsVerts;
+        const bool s_lds = P.llen <= (uint32_t)kEvalLdsSlab;
         const bool holes = P.nring > 1;
         __syncthreads();  // the previous item's LDS reads are done
         if (v_lds)
@@ -3346,7 +3363,7 @@ __global__ __launch_bounds__(kTB) void ppoly_cand_eval(CandGroup c, const PolyDe
                 in = holes ? point_polygon_within_rings(px, py, rvx, rvy, rvr, rre, P, sv, r)
                            : point_polygon_within(px, py, rvx, rvy, P, sv, r, v_lds ? lsb : nullptr);
             }
-            spairs_push(pb, pc, in, poly, pid, o);
+            spairs_push<kEvalPairs>(pb, pc, in, poly, pid, o);
         }
     }
     if (pc) spairs_flush(pb, pc, o);
