@@ -2413,6 +2413,7 @@ struct StreamOut {
     unsigned long long* ctotal;     // candidates: reservation cursor (zero before)
     unsigned long long* both;       // non-null: one cursor for both, pairs in the low kPackBits bits
                                     // (one atomic per chunk; ppoly_cand_plan unpacks it into the two)
+    unsigned* reruns;               // chunks whose LDS stage overflowed (run again, direct stores)
     uint64_t ccap;                  // candidates past it are counted only (the host regrows, re-runs)
     unsigned* cpoly;                // candidates in chunk order: polygon (the grouping reads these),
     double4* crec;                  // and (x, y, point bits, -) -- one 32-byte sector per gather
@@ -3057,6 +3058,7 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
             if (threadIdx.x == 0) {
                 s_np = 0;
                 s_nc = 0;
+                atomicAdd(a.o.reruns, 1u);
             }
             __syncthreads();
             StreamSink pd{ppk, &s_np, kSPairCap, true, pb, 0u, 0u};
@@ -5250,6 +5252,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             so.aligned8 = ((uintptr_t)out & 7u) == 0;
             so.swap = join ? 1 : 0;
             so.point_base = point_base;
+            so.reruns = misc + 5;  // zeroed with the totals
             so.ptotal = async ? reinterpret_cast<unsigned long long*>(count_dev) : reinterpret_cast<unsigned long long*>(misc);
             so.ctotal = reinterpret_cast<unsigned long long*>(misc) + 1;
             // one reservation atomic per chunk when both counts fit the packed fields (a point yields
@@ -5326,8 +5329,9 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             tot = pin[0];
             const uint64_t ncand = pin[1];
             pc->last_cand = ncand;
-            if (prof) fprintf(stderr, "ppoly stream: %llu pairs, %llu candidates (capacity %llu)\n",
-                              (unsigned long long)tot, (unsigned long long)ncand, (unsigned long long)ccap);
+            if (prof) fprintf(stderr, "ppoly stream: %llu pairs, %llu candidates (capacity %llu), %u of %llu chunks re-run\n",
+                              (unsigned long long)tot, (unsigned long long)ncand, (unsigned long long)ccap,
+                              (unsigned)(pin[2] >> 32), (unsigned long long)nchunks);
             if (ncand <= ccap) break;
             if (attempt == 2) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "candidate buffer did not converge");
             ccap = ncand + ncand / 4 + 1024;  // grown to the counted need: the step runs again
