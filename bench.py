@@ -868,13 +868,16 @@ class PpolyIncrWorkload(PpolyWorkload):
         import torch
         self.inc = IncrementalPPolyRange(self.ctx, self.grid, self.off, self.vx, self.vy, self.radius, False, 2)
         self.outs = [torch.empty((max(self.hits) + 1, 2), dtype=torch.int32, device=self.dev) for _ in range(2)]
+        self.pcnt = torch.zeros((self.windows, 1), dtype=torch.int64, device=self.dev)  # per window slot
 
     def verify(self):
-        return None  # synchronous pane calls
+        self.ctx.sync()  # a candidate-buffer overflow of an async pane raises here
+        return self.pcnt.view(-1).cpu().tolist() == self.hits
 
     def step(self, s):
         w = s % self.windows
-        self.inc.push(self.xs[w], self.ys[w], out=self.outs[s % 2])
+        # enqueue-only pane (geohip_range_ppoly_pane_async): no end-of-step count readback
+        self.inc.push(self.xs[w], self.ys[w], out=self.outs[s % 2], count=self.pcnt[w])
 
     def config(self):
         c = super().config()

@@ -285,6 +285,12 @@ int geohip_range_ppoly_async(geohip_ctx* ctx, const geohip_grid* grid, const dou
                              uint64_t n, const uint32_t* poly_rings, const uint32_t* ring_off, const double* vx,
                              const double* vy, uint64_t nv, uint32_t npoly, double r, int approximate,
                              uint32_t* out_pairs, uint64_t cap, uint64_t* out_count_dev);
+/* geohip_range_ppoly_pane as an enqueue-only call (point indices point_base + position). */
+int geohip_range_ppoly_pane_async(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
+                                  uint64_t n, uint32_t point_base, const uint32_t* poly_rings,
+                                  const uint32_t* ring_off, const double* vx, const double* vy, uint64_t nv,
+                                  uint32_t npoly, double r, int approximate, uint32_t* out_pairs, uint64_t cap,
+                                  uint64_t* out_count_dev);
 int geohip_join_ppoly_async(geohip_ctx* ctx, const geohip_grid* grid_points, const geohip_grid* grid_query,
                             const double* x, const double* y, uint64_t n, const uint32_t* poly_rings,
                             const uint32_t* ring_off, const double* vx, const double* vy, uint64_t nv,

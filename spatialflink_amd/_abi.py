@@ -212,6 +212,8 @@ _SIGS = {
                                      c_int, _P, c_uint64, _P]),
     "geohip_range_ppoly_async": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, _P, _P, _P, _P, c_uint64, c_uint32,
                                          c_double, c_int, _P, c_uint64, _P]),
+    "geohip_range_ppoly_pane_async": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, c_uint32, _P, _P, _P, _P, c_uint64,
+                                              c_uint32, c_double, c_int, _P, c_uint64, _P]),
     "geohip_join_ppoly_async": (c_int, [_P, POINTER(Grid), POINTER(Grid), _P, _P, c_uint64, _P, _P, _P, _P, c_uint64,
                                         c_uint32, c_double, c_int, _P, c_uint64, _P]),
     "geohip_range_ppoly": (c_int, [_P, POINTER(Grid), _P, _P, c_uint64, _P, _P, _P, _P, c_uint64, c_uint32, c_double, c_int,
@@ -764,12 +766,20 @@ class Context:
         if rc:
             self._check(rc, "join_pp_async")
 
-    def range_ppoly_async(self, grid: Grid, x, y, ring_off, vx, vy, r, approximate, out, out_count, poly_rings=None):
+    def range_ppoly_async(self, grid: Grid, x, y, ring_off, vx, vy, r, approximate, out, out_count, poly_rings=None,
+                          point_base=None):
         """geohip_range_ppoly_async: (polygon, point) pairs into ``out`` ([cap, 2] int32, device),
         the pair total into ``out_count`` (one int64, device); a candidate-buffer overflow surfaces
-        at sync()."""
-        self._ppoly_async(lib.geohip_range_ppoly_async, "range_ppoly_async", (ctypes.byref(grid),), x, y, ring_off,
-                          vx, vy, r, approximate, out, out_count, poly_rings)
+        at sync().  ``point_base`` (geohip_range_ppoly_pane_async): point indices point_base +
+        position (mod 2^32)."""
+        if point_base is None:
+            self._ppoly_async(lib.geohip_range_ppoly_async, "range_ppoly_async", (ctypes.byref(grid),), x, y, ring_off,
+                              vx, vy, r, approximate, out, out_count, poly_rings)
+        else:
+            base = int(point_base) & 0xFFFFFFFF
+            fn = lambda h, g, px, py, n, *rest: lib.geohip_range_ppoly_pane_async(h, g, px, py, n, base, *rest)  # noqa: E731
+            self._ppoly_async(fn, "range_ppoly_pane_async", (ctypes.byref(grid),), x, y, ring_off, vx, vy, r,
+                              approximate, out, out_count, poly_rings)
 
     def join_ppoly_async(self, grid_points: Grid, grid_query: Grid, x, y, ring_off, vx, vy, r, approximate, out,
                          out_count, poly_rings=None):

@@ -1091,6 +1091,18 @@ int geohip_range_ppoly_async(geohip_ctx* ctx, const geohip_grid* grid, const dou
                       cap, nullptr, 0, out_count_dev);
 }
 
+int geohip_range_ppoly_pane_async(geohip_ctx* ctx, const geohip_grid* grid, const double* x, const double* y,
+                                  uint64_t n, uint32_t point_base, const uint32_t* poly_rings, const uint32_t* ring_off,
+                                  const double* vx, const double* vy, uint64_t nv, uint32_t npoly, double r,
+                                  int approximate, uint32_t* out_pairs, uint64_t cap, uint64_t* out_count_dev) {
+    int rc = begin(ctx);
+    if (rc) return rc;
+    if (ctx->mem != GEOHIP_MEM_DEVICE) return fail(ctx, GEOHIP_ERR_ARG, "async forms need GEOHIP_MEM_DEVICE");
+    if (!out_count_dev) return fail(ctx, GEOHIP_ERR_ARG, "null output");
+    return ppoly_impl(ctx, grid, nullptr, 0, x, y, n, poly_rings, ring_off, vx, vy, nv, npoly, r, approximate, out_pairs,
+                      cap, nullptr, point_base, out_count_dev);
+}
+
 int geohip_join_ppoly_async(geohip_ctx* ctx, const geohip_grid* grid_points, const geohip_grid* grid_query,
                             const double* x, const double* y, uint64_t n, const uint32_t* poly_rings,
                             const uint32_t* ring_off, const double* vx, const double* vy, uint64_t nv, uint32_t npoly,

@@ -90,8 +90,18 @@ class IncrementalPPolyRange:
         self.out_cap = out_cap
         self.pos = 0  # stream position of the next pane's first point
 
-    def push(self, x, y, out=None):
-        pairs = self.ctx.range_ppoly(self.grid, x, y, *self.rings, self.r, self.approx, out=out, point_base=self.pos)
+    def push(self, x, y, out=None, count=None):
+        """Evaluate the new pane; returns the window's pairs (window()).  With ``count`` (one int64
+        device tensor) and ``out`` ([cap, 2] int32, device): enqueue-only
+        (geohip_range_ppoly_pane_async) -- the pane's entry is (out, count), the pair count stays on
+        the device (faults at ctx.sync())."""
+        if count is not None:
+            self.ctx.range_ppoly_async(self.grid, x, y, *self.rings, self.r, self.approx, out, count,
+                                       point_base=self.pos)
+            pairs = (out, count)
+        else:
+            pairs = self.ctx.range_ppoly(self.grid, x, y, *self.rings, self.r, self.approx, out=out,
+                                         point_base=self.pos)
         self.panes.append((self.pos, len(x), pairs))
         self.pos = (self.pos + len(x)) & 0xFFFFFFFF
         return self.window()
@@ -103,7 +113,7 @@ class IncrementalPPolyRange:
 
     def window(self):
         """Pairs of the window (polygon, stream position), pane by pane (a list: the caller
-        concatenates if it needs one array)."""
+        concatenates if it needs one array; an enqueue-only pane's entry is its (out, count))."""
         return [pairs for _, _, pairs in self.panes]
 
 

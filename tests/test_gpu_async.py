@@ -140,3 +140,28 @@ def test_ppoly_async_candidate_overflow():
     c.range_ppoly_async(ag, x, y, off, vx, vy, 0.002, False, out, cnt)
     c.sync()
     assert (int(cnt.item()), pair_digest(out[:int(cnt.item())])[1]) == want
+
+
+def test_ppoly_pane_async(ctx):
+    """geohip_range_ppoly_pane_async: the synchronous pane call's pairs (polygon, base + position),
+    a base near 2^32 wrapping; IncrementalPPolyRange's enqueue-only pane."""
+    import torch
+    from spatialflink_amd.incremental import IncrementalPPolyRange
+    ag, cg = agrid(500)
+    off, vx, vy = synth.star_polygons(200, 91)
+    hx, hy = synth.uniform(1_000_000, 92)
+    x, y = _dev(hx, hy)
+    want = cref.range_ppoly(cg, hx, hy, off, vx, vy, 0.005)
+    base = (1 << 32) - 300_000
+    out = torch.empty((len(want) + 8, 2), dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ctx.range_ppoly_async(ag, x, y, off, vx, vy, 0.005, False, out, cnt, point_base=base)
+    ctx.sync()
+    m = int(cnt.item())
+    got = out[:m].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+    got[:, 1] = (got[:, 1] - base) & 0xFFFFFFFF
+    assert pairs_sorted(got).tolist() == pairs_sorted(want).tolist()
+    inc = IncrementalPPolyRange(ctx, ag, off, vx, vy, 0.005)
+    inc.push(x, y, out=out, count=cnt)
+    ctx.sync()
+    assert int(cnt.item()) == len(want)
