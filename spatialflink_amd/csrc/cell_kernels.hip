@@ -20,7 +20,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
+#include <thread>
 #include <unordered_map>
 #include <chrono>
 #include <cstdio>
@@ -1741,6 +1743,21 @@ __host__ __device__ __forceinline__ int sub_of(double v, double mn, double l, in
     return (v >= sub_edge(mn, l, c, 1) ? 1 : 0) + (v >= sub_edge(mn, l, c, 2) ? 1 : 0) + (v >= sub_edge(mn, l, c, 3) ? 1 : 0);
 }
 
+// Refinement of the mixed subcells (ppoly_cand_refine): a mixed subcell is split again 4 x 4 on
+// the sixteenth-cell edges sub16_edge (the subcell edges are every fourth of them, bit-identical:
+// 0.0625 * 4 i == 0.25 i), each part classified by the same BoxClassifier.  Per walk-region cell,
+// rf[cell] = the first of its 16 refinement words (one per subcell, 2 bits per part: 4 tx + ty),
+// or kNoRefine when the cell has no mixed subcell.
+constexpr uint32_t kNoRefine = 0xffffffffu;
+__host__ __device__ __forceinline__ double sub16_edge(double mn, double l, int32_t c, int j) {
+    return mn + ((double)c + 0.0625 * (double)j) * l;
+}
+// part t (0..3) of subcell s of cell c: #{i in 1..3 : v >= sub16_edge(4 s + i)}
+__host__ __device__ __forceinline__ int sub16_of(double v, double mn, double l, int32_t c, int s) {
+    return (v >= sub16_edge(mn, l, c, 4 * s + 1) ? 1 : 0) + (v >= sub16_edge(mn, l, c, 4 * s + 2) ? 1 : 0) +
+           (v >= sub16_edge(mn, l, c, 4 * s + 3) ? 1 : 0);
+}
+
 // Polygons with holes: rings are stored back to back in one vertex run, with a ring id per
 // vertex (u16, < kMaxRings); segment (v[e], v[e+1]) exists iff both ends carry the same id (the
 // junction between two rings is not an edge).  Crossing parity and boundary flags are kept per
@@ -2411,16 +2428,11 @@ struct StreamOut {
     unsigned point_base;            // added to every point index of a pair (pane stream positions)
     unsigned long long* ptotal;     // pairs: reservation cursor (zero before; an async call's count)
     unsigned long long* ctotal;     // candidates: reservation cursor (zero before)
-    unsigned long long* both;       // non-null: one cursor for both, pairs in the low kPackBits bits
-                                    // (one atomic per chunk; ppoly_cand_plan unpacks it into the two)
     unsigned* reruns;               // chunks whose LDS stage overflowed (run again, direct stores)
     uint64_t ccap;                  // candidates past it are counted only (the host regrows, re-runs)
     unsigned* cpoly;                // candidates in chunk order: polygon (the grouping reads these),
     double4* crec;                  // and (x, y, point bits, -) -- one 32-byte sector per gather
 };
-
-constexpr unsigned kPackBits = 34;  // packed cursor: pairs < 2^34, candidates < 2^30 (host-checked)
-constexpr unsigned long long kPackMask = (1ull << kPackBits) - 1ull;
 
 struct StreamArgs {
     const double* x;
@@ -3027,15 +3039,8 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
             nc += wc;
         }
         if (threadIdx.x == 0) {
-            if (a.o.both) {  // one reservation for the pairs and the candidates
-                const unsigned long long v =
-                    (np || nc) ? atomicAdd(a.o.both, (unsigned long long)np | ((unsigned long long)nc << kPackBits)) : 0ull;
-                s_pb = v & kPackMask;
-                s_cb = v >> kPackBits;
-            } else {
-                s_pb = np ? atomicAdd(a.o.ptotal, (unsigned long long)np) : 0ull;
-                s_cb = nc ? atomicAdd(a.o.ctotal, (unsigned long long)nc) : 0ull;
-            }
+            s_pb = np ? atomicAdd(a.o.ptotal, (unsigned long long)np) : 0ull;
+            s_cb = nc ? atomicAdd(a.o.ctotal, (unsigned long long)nc) : 0ull;
         }
         __syncthreads();
         const unsigned long long pb = s_pb, cb = s_cb;
@@ -3103,11 +3108,10 @@ __device__ __forceinline__ void spairs_push(uint2* buf, unsigned& cnt, bool hit,
 constexpr unsigned kCandGroups = 128;
 constexpr unsigned kCandThreads = 1024;
 constexpr unsigned kCandPer = 4;  // candidates per thread per round (loads in flight together)
+constexpr unsigned kCandGone = 0xffffffffu;  // a candidate slot decided by the refinement (and the range end)
 struct CandGroup {
-    const unsigned long long* ccount;  // candidate total (StreamOut::ctotal)
-    const unsigned long long* both;    // the stream's packed cursor (StreamOut::both) or null
-    unsigned long long* ptotal;        // with both: the pair and candidate totals ppoly_cand_plan
-    unsigned long long* ctotal;        // unpacks it into (ptotal, the exact tests' cursor, and ccount)
+    const unsigned long long* ccount;  // candidate total (StreamOut::ctotal, or the refined count)
+    const unsigned long long* cstream; // the stream's candidate total (the capacity check)
     uint64_t ccap;
     unsigned* fault;                   // async calls: the ctx's fault word (kFaultCandOverflow), else null
     unsigned long long* need;          // async calls: the candidate count an overflowing call needed
@@ -3121,7 +3125,7 @@ struct CandGroup {
 };
 
 __device__ __forceinline__ uint64_t cand_n(const CandGroup& c) {
-    const unsigned long long n = c.both ? (*c.both >> kPackBits) : *c.ccount;
+    const unsigned long long n = *c.ccount;
     return n < c.ccap ? n : c.ccap;
 }
 __device__ __forceinline__ void cand_range(const CandGroup& c, uint64_t& b0, uint64_t& b1) {
@@ -3142,11 +3146,11 @@ __global__ __launch_bounds__(kCandThreads) void ppoly_cand_hist(CandGroup c) {
 #pragma unroll
         for (unsigned u = 0; u < kCandPer; u++) {
             const uint64_t i = i0 + (uint64_t)u * kCandThreads;
-            p[u] = i < b1 ? c.cpoly[i] : 0xffffffffu;
+            p[u] = i < b1 ? c.cpoly[i] : kCandGone;
         }
 #pragma unroll
         for (unsigned u = 0; u < kCandPer; u++)
-            if (p[u] != 0xffffffffu) atomicAdd(&h[p[u]], 1u);
+            if (p[u] != kCandGone) atomicAdd(&h[p[u]], 1u);
     }
     __syncthreads();
     unsigned* row = c.mat + (size_t)blockIdx.x * c.npoly;
@@ -3213,14 +3217,9 @@ __global__ __launch_bounds__(kCandThreads) void ppoly_cand_plan(CandGroup c) {
     }
     if (threadIdx.x == 0) {
         *c.nitems = carry_i;
-        if (c.both) {  // the stream's packed cursor into the two totals (ppoly_cand_eval appends pairs)
-            const unsigned long long v = *c.both;
-            *c.ptotal = v & kPackMask;
-            *c.ctotal = v >> kPackBits;
-        }
         // an async call cannot rerun with a larger buffer: the overflow (the candidates past ccap
         // are untested, the pairs incomplete) and the size it needed go to the ctx's fault block
-        const unsigned long long nc = c.both ? (*c.both >> kPackBits) : *c.ccount;
+        const unsigned long long nc = *c.cstream;
         if (c.fault && nc > c.ccap) {
             atomicOr(c.fault, kFaultCandOverflow);
             atomicMax(c.need, nc);
@@ -3242,11 +3241,11 @@ __global__ __launch_bounds__(kCandThreads) void ppoly_cand_scatter(CandGroup c) 
 #pragma unroll
         for (unsigned u = 0; u < kCandPer; u++) {
             const uint64_t i = i0 + (uint64_t)u * kCandThreads;
-            p[u] = i < b1 ? c.cpoly[i] : 0xffffffffu;
+            p[u] = i < b1 ? c.cpoly[i] : kCandGone;
         }
 #pragma unroll
         for (unsigned u = 0; u < kCandPer; u++)
-            if (p[u] != 0xffffffffu) c.sidx[atomicAdd(&h[p[u]], 1u)] = (unsigned)(i0 + (uint64_t)u * kCandThreads);
+            if (p[u] != kCandGone) c.sidx[atomicAdd(&h[p[u]], 1u)] = (unsigned)(i0 + (uint64_t)u * kCandThreads);
     }
 }
 
@@ -3254,6 +3253,97 @@ __global__ __launch_bounds__(kCandThreads) void ppoly_cand_scatter(CandGroup c) 
 // ring ids, fp32 segment boxes and slab lists staged in LDS as in ppoly_eval.  The slice is
 // ordered by y slab in LDS first (counting sort, 64 bins), so the lanes of a wave mostly walk
 // the same crossing and distance lists (equal trip counts, broadcast LDS reads).
+// Refinement of the stream's candidates (round 5): a candidate's point lies in a mixed subcell of
+// its polygon's cell; the subcell's 4 x 4 parts were classified on the host (classify_cells), so
+// its part decides it as a pair (HIT), nothing (MISS) or still a candidate (MIXED, or NaN
+// coordinates, or no refinement).  A decided candidate's polygon slot becomes kCandGone, which
+// the grouping skips (its range-end sentinel): no compaction, no counter -- the survivors, about
+// a quarter for C4, go on to the grouping and the exact tests.  (Compacting survivors with a
+// per-wave reservation on one counter serialised ~44k atomics: 568 us for C4; in place per
+// grouping range, 128 blocks: 176 us; both measured.)  Pairs through per-wave LDS stages.
+struct CandRefine {
+    const unsigned long long* ccount;  // the stream's candidates (ctotal)
+    uint64_t ccap;
+    unsigned* cpoly;                   // decided candidates -> kCandGone
+    const double4* crec;
+    const PolyDev* polys;
+    const uint32_t* rf;                // per walk-region cell (PolyDev.cls indexing): refinement base
+    const uint32_t* rfw;
+    double mnx, mny, l;                // the point grid (cells as the stream computed them)
+};
+// Pairs go to a block-wide LDS stage (kRefineStage) reserved with one global atomic per flush --
+// about one per block (per-wave stages flushed every ~128 pairs cost 83 of the kernel's 148 us
+// for C4: same-address atomics); kRefinePer candidates per thread per round keep their gather
+// chains (slot -> polygon -> refinement base -> word) in flight together.
+constexpr unsigned kRefineBlocks = 1024, kRefinePer = 4, kRefineStage = 4096;
+__device__ __forceinline__ uint32_t refine_code(const CandRefine& c, unsigned poly, double2 xy) {
+    if (!(xy.x == xy.x && xy.y == xy.y)) return kClsMixed;  // NaN: the exact test decides
+    const PolyDev& P = c.polys[poly];
+    const uint32_t cls = P.cls;
+    const int32_t wx0 = P.wx0, wx1 = P.wx1, wy0 = P.wy0, wy1 = P.wy1;
+    const int32_t cx = d_axis_cell(xy.x, c.mnx, c.l), cy = d_axis_cell(xy.y, c.mny, c.l);
+    if (cls == kNoCls || cx < wx0 || cx > wx1 || cy < wy0 || cy > wy1) return kClsMixed;
+    const uint32_t rb = c.rf[cls + (size_t)(cx - wx0) * (uint32_t)(wy1 - wy0 + 1) + (uint32_t)(cy - wy0)];
+    if (rb == kNoRefine) return kClsMixed;
+    const int sx = sub_of(xy.x, c.mnx, c.l, cx), sy = sub_of(xy.y, c.mny, c.l, cy);
+    const int tx = sub16_of(xy.x, c.mnx, c.l, cx, sx), ty = sub16_of(xy.y, c.mny, c.l, cy, sy);
+    return (c.rfw[rb + 4 * sx + sy] >> (2 * (4 * tx + ty))) & 3u;
+}
+__global__ __launch_bounds__(kTB) void ppoly_cand_refine(CandRefine c, StreamOut o) {
+    __shared__ uint2 stage[kRefineStage];
+    __shared__ unsigned s_n;
+    __shared__ unsigned long long s_base;
+    const int lane = lane_id();
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    auto flush = [&]() {  // block-uniform
+        __syncthreads();
+        const unsigned n = s_n;
+        if (threadIdx.x == 0) s_base = atomicAdd(o.ptotal, (unsigned long long)n);
+        __syncthreads();
+        const unsigned long long base = s_base;
+        for (unsigned t = threadIdx.x; t < n; t += kTB) stream_emit_pair(o, base + t, stage[t].x, stage[t].y);
+        __syncthreads();
+        if (threadIdx.x == 0) s_n = 0;
+        __syncthreads();
+    };
+    const unsigned long long nt = *c.ccount;
+    const uint64_t n = nt < c.ccap ? nt : c.ccap;
+    constexpr unsigned kRound = kTB * kRefinePer;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * kRound; i0 < n; i0 += (uint64_t)gridDim.x * kRound) {  // block-uniform
+        unsigned poly[kRefinePer];
+        double2 xy[kRefinePer];
+#pragma unroll
+        for (unsigned u = 0; u < kRefinePer; u++) {
+            const uint64_t i = i0 + u * kTB + threadIdx.x;
+            poly[u] = kCandGone;
+            xy[u] = make_double2(0.0, 0.0);
+            if (i < n) {
+                poly[u] = c.cpoly[i];
+                xy[u] = *reinterpret_cast<const double2*>(&c.crec[i]);
+            }
+        }
+#pragma unroll
+        for (unsigned u = 0; u < kRefinePer; u++) {
+            const uint64_t i = i0 + u * kTB + threadIdx.x;
+            const uint32_t code = poly[u] != kCandGone ? refine_code(c, poly[u], xy[u]) : kClsMixed;
+            const bool hit = code == kClsHit;
+            const unsigned long long m = __ballot(hit);
+            if (m) {  // this wave's hits: one LDS reservation
+                unsigned wb = 0;
+                if (lane == 0) wb = atomicAdd(&s_n, (unsigned)__popcll(m));
+                wb = (unsigned)__shfl(wb, 0);
+                if (hit) stage[wb + lanes_below(m)] = make_uint2(poly[u], (unsigned)__double_as_longlong(c.crec[i].z));
+            }
+            if (poly[u] != kCandGone && code != kClsMixed) c.cpoly[i] = kCandGone;
+        }
+        __syncthreads();
+        if (s_n > kRefineStage - kRound) flush();
+    }
+    __syncthreads();
+    if (s_n) flush();
+}
+
 // LDS of the candidate evaluation, sized for 4 blocks per CU (<= 40 KB: 4 waves per SIMD; the
 // round-4 sizes -- 512 vertices, 2048 slab entries, 512 staged pairs per wave, 58.6 KB -- left 2
 // blocks per CU and this latency-bound pass at 2 waves per SIMD).  Larger rings and slab lists
@@ -4719,9 +4809,12 @@ struct BoxClassifier {
 };
 
 // Returns false (no classes) for r < 0 / NaN / inf, non-finite vertices or too large a region.
+// rf / rfw (may be null): the refinement table of the mixed subcells (kNoRefine entries otherwise),
+// rf parallel to blob.
 bool classify_cells(const PolyDev& P, const std::vector<double>& hvx, const std::vector<double>& hvy,
                     const ring_id_t* rid, const geohip_grid& pg, const int32_t* rects, uint32_t first_c,
-                    uint32_t nrect_c, uint32_t nring, double r, std::vector<uint32_t>& blob, uint32_t* off) {
+                    uint32_t nrect_c, uint32_t nring, double r, std::vector<uint32_t>& blob, uint32_t* off,
+                    std::vector<uint32_t>* rf = nullptr, std::vector<uint32_t>* rfw = nullptr) {
     *off = kNoCls;
     if (!(r >= 0.0) || !std::isfinite(r) || P.wx0 > P.wx1 || P.wy0 > P.wy1 || nrect_c == 0) return false;
     BoxClassifier bc;
@@ -4750,6 +4843,7 @@ bool classify_cells(const PolyDev& P, const std::vector<double>& hvx, const std:
     const size_t base = blob.size();
     blob.resize(base + (size_t)w * h, 0u);  // all mixed
     uint32_t* out = blob.data() + base;
+    if (rf) rf->resize(base + (size_t)w * h, kNoRefine);
     // subcell i of an axis: the doubles v of the cell box [bl, bh] with sub_of(v) == i
     auto sub_iv = [](double mn, double l, int32_t c, double bl, double bh, int i, double& lo, double& hi) {
         lo = i == 0 ? bl : std::max(bl, sub_edge(mn, l, c, i));
@@ -4770,16 +4864,38 @@ bool classify_cells(const PolyDev& P, const std::vector<double>& hvx, const std:
             if (k == kClsHit) { out[(size_t)a * h + c] = kWordHit; continue; }
             if (k == kClsMiss) { out[(size_t)a * h + c] = kWordMiss; continue; }
             uint32_t word = 0;
+            uint32_t rw[16];
+            bool refined = false;
             for (int sx = 0; sx < 4; sx++) {
                 double sx0, sx1;
                 sub_iv(pg.min_x, pg.cell_len, cx, xl[a], xh[a], sx, sx0, sx1);
                 for (int sy = 0; sy < 4; sy++) {
                     double sy0, sy1;
                     sub_iv(pg.min_y, pg.cell_len, cy, yl[c], yh[c], sy, sy0, sy1);
-                    word |= (uint32_t)bc(sx0, sx1, sy0, sy1) << (2 * (4 * sx + sy));
+                    const uint8_t ks = bc(sx0, sx1, sy0, sy1);
+                    word |= (uint32_t)ks << (2 * (4 * sx + sy));
+                    rw[4 * sx + sy] = 0u;
+                    if (ks != kClsMixed || !rf) continue;
+                    // the subcell's 4 x 4 parts: [sub16 edge, next edge) clipped to the subcell
+                    uint32_t pw = 0;
+                    for (int tx = 0; tx < 4; tx++) {
+                        const double px0 = tx == 0 ? sx0 : std::max(sx0, sub16_edge(pg.min_x, pg.cell_len, cx, 4 * sx + tx));
+                        const double px1 = tx == 3 ? sx1 : std::min(sx1, std::nextafter(sub16_edge(pg.min_x, pg.cell_len, cx, 4 * sx + tx + 1), -INFINITY));
+                        for (int ty = 0; ty < 4; ty++) {
+                            const double py0 = ty == 0 ? sy0 : std::max(sy0, sub16_edge(pg.min_y, pg.cell_len, cy, 4 * sy + ty));
+                            const double py1 = ty == 3 ? sy1 : std::min(sy1, std::nextafter(sub16_edge(pg.min_y, pg.cell_len, cy, 4 * sy + ty + 1), -INFINITY));
+                            pw |= (uint32_t)bc(px0, px1, py0, py1) << (2 * (4 * tx + ty));
+                        }
+                    }
+                    rw[4 * sx + sy] = pw;
+                    refined = refined || pw != 0u;  // some part decided
                 }
             }
             out[(size_t)a * h + c] = word;
+            if (refined) {
+                (*rf)[base + (size_t)a * h + c] = (uint32_t)rfw->size();
+                rfw->insert(rfw->end(), rw, rw + 16);
+            }
         }
     }
     *off = (uint32_t)base;
@@ -4836,6 +4952,8 @@ struct PolyCache {
     std::vector<PolyWork> hwork;
     std::vector<uint16_t> hslab;
     std::vector<uint32_t> hcls;  // per-cell class words (classify_cells), PolyDev.cls offsets into it
+    std::vector<uint32_t> hrf;   // parallel to hcls: first refinement word of the cell, or kNoRefine
+    std::vector<uint32_t> hrfw;  // refinement words (16 per refined cell)
     std::vector<uint32_t> keep;  // cells of any polygon's G or C rectangles (empty: no filter)
     bool any_outside = false;
     // streaming path (ppoly_stream): per key cell its polygon entries, the cells holding any
@@ -4848,7 +4966,6 @@ struct PolyCache {
     std::vector<uint32_t> skeep;
     std::vector<uint32_t> opoly;
     uint64_t last_cand = 0;           // candidates of the previous step (sizes the buffer)
-    uint32_t max_ent = 0;             // most entries of one cell (bounds a point's pairs + candidates)
     void* dev_blob = nullptr;  // J_POLY buffer holding the uploaded tables
     size_t blob_bytes = 0;
 };
@@ -4979,7 +5096,6 @@ void build_stream_table(PolyCache& c, uint32_t npoly, int32_t nb, bool r_is_max)
         c.cell_head[2 * k] = kNoEntry;
         if (e == b) continue;
         c.skeep[k >> 5] |= 1u << (k & 31);
-        if (e - b > c.max_ent) c.max_ent = e - b;
         if (e - b == 1) {
             c.cell_head[2 * k] = c.cell_ent[2 * (size_t)b];
             c.cell_head[2 * k + 1] = c.cell_ent[2 * (size_t)b + 1];
@@ -5088,12 +5204,46 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             if (jmode == 2) { P.ng += P.nc; P.nc = 0; }
             plan_slabs(P, pl.ry.data(), P.nring > 1 ? fresh.hvr.data() + P.voff : nullptr, r, gq->cell_len, hslab);
             P.cls = kNoCls;
-            if (!approximate)
-                classify_cells(P, hvx, hvy, P.nring > 1 ? fresh.hvr.data() + P.voff : nullptr, *grid, hrects.data(),
-                               P.coff, P.nc, P.nring, r, fresh.hcls, &P.cls);
-            if (wx0 <= wx1 && wy0 <= wy1)
-                for (int32_t a = wx0 / geo.ts; a <= wx1 / geo.ts; a++)
-                    for (int32_t c = wy0 / geo.ts; c <= wy1 / geo.ts; c++) {
+        }
+        // the cell classes (exact modes): polygons in parallel on the host's cores (the refined
+        // parts of a mixed subcell cost 16 box classifications each: 0.6 s on one core for C4's
+        // 3000 polygons), each into its own tables, then concatenated in polygon order
+        if (!approximate && npoly) {
+            struct Cls {
+                std::vector<uint32_t> blob, rf, rfw;
+                uint32_t off = kNoCls;
+            };
+            std::vector<Cls> part(npoly);
+            std::atomic<uint32_t> next{0};
+            auto work = [&]() {
+                for (uint32_t p; (p = next.fetch_add(1)) < npoly;) {
+                    const PolyDev& P = pd[p];
+                    classify_cells(P, hvx, hvy, P.nring > 1 ? fresh.hvr.data() + P.voff : nullptr, *grid, hrects.data(),
+                                   P.coff, P.nc, P.nring, r, part[p].blob, &part[p].off, &part[p].rf, &part[p].rfw);
+                }
+            };
+            const unsigned nth = std::min<unsigned>(std::max(1u, std::min(std::thread::hardware_concurrency(), 16u)),
+                                                    std::max<uint32_t>(1u, npoly / 8));
+            std::vector<std::thread> th;
+            for (unsigned t = 1; t < nth; t++) th.emplace_back(work);
+            work();
+            for (auto& t : th) t.join();
+            for (uint32_t p = 0; p < npoly; p++) {
+                Cls& q = part[p];
+                if (q.off == kNoCls) continue;
+                const uint32_t wbase = (uint32_t)fresh.hrfw.size();
+                pd[p].cls = (uint32_t)fresh.hcls.size();
+                fresh.hcls.insert(fresh.hcls.end(), q.blob.begin(), q.blob.end());
+                for (uint32_t v : q.rf) fresh.hrf.push_back(v == kNoRefine ? kNoRefine : v + wbase);
+                fresh.hrfw.insert(fresh.hrfw.end(), q.rfw.begin(), q.rfw.end());
+                std::vector<uint32_t>().swap(q.blob);
+            }
+        }
+        for (uint32_t p = 0; p < npoly; p++) {
+            const PolyDev& P = pd[p];
+            if (P.wx0 <= P.wx1 && P.wy0 <= P.wy1)
+                for (int32_t a = P.wx0 / geo.ts; a <= P.wx1 / geo.ts; a++)
+                    for (int32_t c = P.wy0 / geo.ts; c <= P.wy1 / geo.ts; c++) {
                         const uint32_t t = tile_work(P, hrects.data(), fresh.hcls, geo, a, c, r >= 1.7976931348623157e308);
                         if (t != kNoWork) hwork.push_back(PolyWork{p, (uint32_t)a * (uint32_t)geo.nt + (uint32_t)c | t});
                     }
@@ -5170,7 +5320,9 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     const size_t off_ce = (off_co + sz_co + 15) & ~(size_t)15, sz_ce = pc->cell_ent.size() * 4;
     const size_t off_sk = (off_ce + sz_ce + 15) & ~(size_t)15, sz_sk = pc->skeep.size() * 4;
     const size_t off_op = (off_sk + sz_sk + 15) & ~(size_t)15, sz_op = pc->opoly.size() * 4;
-    const size_t blob_end = off_op + sz_op;
+    const size_t off_rf = (off_op + sz_op + 15) & ~(size_t)15, sz_rf = pc->hrf.size() * 4;
+    const size_t off_rw = (off_rf + sz_rf + 15) & ~(size_t)15, sz_rw = pc->hrfw.size() * 4;
+    const size_t blob_end = off_rw + sz_rw;
     void* pblob = nullptr;
     rc = ctx_ensure(ctx, J_POLY, blob_end + 64, &pblob);
     if (rc) return rc;
@@ -5190,6 +5342,8 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     uint2* dcent = reinterpret_cast<uint2*>(bp + off_ce);
     unsigned* dskeep = reinterpret_cast<unsigned*>(bp + off_sk);
     uint32_t* dopoly = reinterpret_cast<uint32_t*>(bp + off_op);
+    uint32_t* drf = reinterpret_cast<uint32_t*>(bp + off_rf);
+    uint32_t* drfw = reinterpret_cast<uint32_t*>(bp + off_rw);
     if (upload) {
         pc->dev_blob = nullptr;  // until the copies are issued
         if ((sz_p && hipMemcpyAsync(dpoly, pd.data(), sz_p, hipMemcpyHostToDevice, st) != hipSuccess) ||
@@ -5205,7 +5359,9 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             (sz_co && hipMemcpyAsync(dchead, pc->cell_head.data(), sz_co, hipMemcpyHostToDevice, st) != hipSuccess) ||
             (sz_ce && hipMemcpyAsync(dcent, pc->cell_ent.data(), sz_ce, hipMemcpyHostToDevice, st) != hipSuccess) ||
             (sz_sk && hipMemcpyAsync(dskeep, pc->skeep.data(), sz_sk, hipMemcpyHostToDevice, st) != hipSuccess) ||
-            (sz_op && hipMemcpyAsync(dopoly, pc->opoly.data(), sz_op, hipMemcpyHostToDevice, st) != hipSuccess))
+            (sz_op && hipMemcpyAsync(dopoly, pc->opoly.data(), sz_op, hipMemcpyHostToDevice, st) != hipSuccess) ||
+            (sz_rf && hipMemcpyAsync(drf, pc->hrf.data(), sz_rf, hipMemcpyHostToDevice, st) != hipSuccess) ||
+            (sz_rw && hipMemcpyAsync(drfw, pc->hrfw.data(), sz_rw, hipMemcpyHostToDevice, st) != hipSuccess))
             return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "polygon upload failed");
         pc->dev_blob = pblob;
         pc->blob_bytes = blob_end;
@@ -5237,6 +5393,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             unsigned* misc = S.get<unsigned>(J_MISC, kMiscWords * 4);
             unsigned* mat = cands ? S.get<unsigned>(J_HIST, (size_t)kCandGroups * npoly * 4 + 16) : nullptr;
             void* cbuf = cands ? S.get<void>(J_SY, ccap * 36 + 64) : nullptr;
+            const bool refine = cands && !pc->hrfw.empty();
             void* sbuf = cands ? S.get<void>(J_SX, ccap * 4 + 64) : nullptr;
             uint4* items = cands ? S.get<uint4>(J_SKEY, (ccap / kCandItem + npoly + 1) * sizeof(uint4)) : nullptr;
             if (S.rc) return S.rc;
@@ -5255,10 +5412,6 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             so.reruns = misc + 5;  // zeroed with the totals
             so.ptotal = async ? reinterpret_cast<unsigned long long*>(count_dev) : reinterpret_cast<unsigned long long*>(misc);
             so.ctotal = reinterpret_cast<unsigned long long*>(misc) + 1;
-            // one reservation atomic per chunk when both counts fit the packed fields (a point yields
-            // at most its cell's entries plus the out-of-grid polygons as pairs or candidates)
-            so.both = (cands && (uint64_t)n * (pc->max_ent + pc->opoly.size()) < (1ull << (64 - kPackBits)))
-                          ? reinterpret_cast<unsigned long long*>(misc) + 3 : nullptr;
             so.ccap = cands ? ccap : 0;
             char* cb = reinterpret_cast<char*>(cbuf);
             so.cpoly = cands ? reinterpret_cast<unsigned*>(cb) : nullptr;
@@ -5301,14 +5454,26 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
                 char* sb = reinterpret_cast<char*>(sbuf);
                 CandGroup cg;
                 cg.ccount = so.ctotal;
-                cg.both = so.both;
-                cg.ptotal = so.ptotal;
-                cg.ctotal = so.ctotal;
+                cg.cstream = so.ctotal;
+                cg.cpoly = so.cpoly;
+                cg.crec = so.crec;
+                if (refine) {  // the candidates' refined parts first: decided ones leave the grouping
+                    CandRefine cr;
+                    cr.ccount = so.ctotal;
+                    cr.ccap = ccap;
+                    cr.cpoly = so.cpoly;
+                    cr.crec = so.crec;
+                    cr.polys = dpoly;
+                    cr.rf = drf;
+                    cr.rfw = drfw;
+                    cr.mnx = grid->min_x;
+                    cr.mny = grid->min_y;
+                    cr.l = grid->cell_len;
+                    tlaunch(ctx, ppoly_cand_refine, kRefineBlocks, kTB, 0, st, cr, so);
+                }
                 cg.ccap = ccap;
                 cg.fault = fault;
                 cg.need = fault ? reinterpret_cast<unsigned long long*>(fault + 2) : nullptr;
-                cg.cpoly = so.cpoly;
-                cg.crec = so.crec;
                 cg.mat = mat;
                 cg.npoly = npoly;
                 cg.items = items;
@@ -5329,9 +5494,13 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             tot = pin[0];
             const uint64_t ncand = pin[1];
             pc->last_cand = ncand;
+            if (prof && attempt == 0)
+                fprintf(stderr, "ppoly host: plan %.1f us (cached %d), %zu refined cells\n",
+                        std::chrono::duration<double, std::micro>(t_planned - t_start).count(), (int)cached,
+                        pc->hrfw.size() / 16);
             if (prof) fprintf(stderr, "ppoly stream: %llu pairs, %llu candidates (capacity %llu), %u of %llu chunks re-run\n",
-                              (unsigned long long)tot, (unsigned long long)ncand, (unsigned long long)ccap,
-                              (unsigned)(pin[2] >> 32), (unsigned long long)nchunks);
+                              (unsigned long long)tot, (unsigned long long)ncand, (unsigned long long)ccap, (unsigned)(pin[2] >> 32),
+                              (unsigned long long)nchunks);
             if (ncand <= ccap) break;
             if (attempt == 2) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "candidate buffer did not converge");
             ccap = ncand + ncand / 4 + 1024;  // grown to the counted need: the step runs again
