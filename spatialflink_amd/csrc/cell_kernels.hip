@@ -105,8 +105,10 @@ __global__ void fill_words(unsigned* __restrict__ p, unsigned n, unsigned v) {
     for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = v;
 }
 // a step's zero block, and one more 64-bit word (an async call's device count) when z is not null
-__global__ void zero_step(unsigned* __restrict__ p, unsigned n, unsigned long long* __restrict__ z) {
+__global__ void zero_step(unsigned* __restrict__ p, unsigned n, unsigned long long* __restrict__ z,
+                          unsigned* __restrict__ p2 = nullptr, unsigned n2 = 0) {
     for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = 0u;
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += gridDim.x * blockDim.x) p2[i] = 0u;
     if (z && blockIdx.x == 0 && threadIdx.x == 0) *z = 0ull;
 }
 __global__ void set_u64(unsigned long long* __restrict__ p, unsigned long long v) { *p = v; }
@@ -3100,11 +3102,14 @@ __device__ __forceinline__ void spairs_push(uint2* buf, unsigned& cnt, bool hit,
     if (cnt > CAP - (unsigned)kWave) spairs_flush(buf, cnt, o);
 }
 
-// Grouping of the candidates by polygon: a counting sort with no global atomics.  kCandGroups
-// blocks each own a contiguous range of the candidates: per-polygon counts of the range in LDS
-// -> row b of a [kCandGroups][npoly] matrix (ppoly_cand_hist); one block turns the matrix into
-// per-(range, polygon) write bases, the polygons' runs and the work items (ppoly_cand_plan); the
-// same ranges scatter (point, x, y) into the runs from their rows (ppoly_cand_scatter).
+// Grouping of the candidates by polygon: a counting sort.  kCandGroups blocks each own a
+// contiguous range of the candidates: per-polygon counts of the range in LDS -> row b of a
+// [kCandGroups][npoly] matrix and, one atomic per nonzero count, the polygons' totals
+// (ppoly_cand_hist); one block scans the totals into the polygons' runs, their cursors and the
+// work items (ppoly_cand_plan); the same ranges reserve their slice of each run from its cursor
+// (one atomic per nonzero count) and scatter into it (ppoly_cand_scatter).  (The plan block
+// summing the matrix's columns and scanning them per range took 21 us for C4's 1000 polygons;
+// the order of the ranges inside a run is free: the pairs are unordered.)
 constexpr unsigned kCandGroups = 128;
 constexpr unsigned kCandThreads = 1024;
 constexpr unsigned kCandPer = 4;  // candidates per thread per round (loads in flight together)
@@ -3117,7 +3122,9 @@ struct CandGroup {
     unsigned long long* need;          // async calls: the candidate count an overflowing call needed
     const unsigned* cpoly;
     const double4* crec;
-    unsigned* mat;          // [kCandGroups][npoly]: counts, then write bases
+    unsigned* mat;          // [kCandGroups][npoly]: each range's counts
+    unsigned* ptot;         // [npoly] candidates per polygon (zeroed with the step's totals)
+    unsigned* pcur;         // [npoly] run cursors: each range reserves its slice of a run
     uint32_t npoly;         // <= kCandLdsPolys
     uint4* items;           // (poly, begin, end, -)
     unsigned* nitems;
@@ -3154,30 +3161,25 @@ __global__ __launch_bounds__(kCandThreads) void ppoly_cand_hist(CandGroup c) {
     }
     __syncthreads();
     unsigned* row = c.mat + (size_t)blockIdx.x * c.npoly;
-    for (unsigned t = threadIdx.x; t < c.npoly; t += kCandThreads) row[t] = h[t];
+    for (unsigned t = threadIdx.x; t < c.npoly; t += kCandThreads) {
+        const unsigned v = h[t];
+        row[t] = v;
+        if (v) atomicAdd(&c.ptot[t], v);
+    }
 }
 
-// one block: column sums (a polygon's run length), their scan (run starts), the columns' scans
-// (each range's base inside each run) and the kCandItem work items
+// one block: the polygons' totals scanned into run starts (their cursors) and the kCandItem
+// work items
 __global__ __launch_bounds__(kCandThreads) void ppoly_cand_plan(CandGroup c) {
     __shared__ unsigned sc[kCandThreads], si[kCandThreads];
     __shared__ unsigned carry_c, carry_i;
-    constexpr unsigned kB = 16;
     if (threadIdx.x == 0) {
         carry_c = 0;
         carry_i = 0;
     }
     for (unsigned p0 = 0; p0 < c.npoly; p0 += kCandThreads) {
         const unsigned p = p0 + threadIdx.x;
-        unsigned tot = 0;
-        if (p < c.npoly)
-            for (unsigned g0 = 0; g0 < kCandGroups; g0 += kB) {
-                unsigned v[kB];
-#pragma unroll
-                for (unsigned u = 0; u < kB; u++) v[u] = c.mat[(size_t)(g0 + u) * c.npoly + p];
-#pragma unroll
-                for (unsigned u = 0; u < kB; u++) tot += v[u];
-            }
+        const unsigned tot = p < c.npoly ? c.ptot[p] : 0u;
         const unsigned nit = (tot + kCandItem - 1) / kCandItem;
         sc[threadIdx.x] = tot;
         si[threadIdx.x] = nit;
@@ -3192,17 +3194,7 @@ __global__ __launch_bounds__(kCandThreads) void ppoly_cand_plan(CandGroup c) {
         }
         const unsigned start = carry_c + sc[threadIdx.x] - tot, item0 = carry_i + si[threadIdx.x] - nit;
         if (p < c.npoly) {
-            unsigned run = start;
-            for (unsigned g0 = 0; g0 < kCandGroups; g0 += kB) {
-                unsigned v[kB];
-#pragma unroll
-                for (unsigned u = 0; u < kB; u++) v[u] = c.mat[(size_t)(g0 + u) * c.npoly + p];
-#pragma unroll
-                for (unsigned u = 0; u < kB; u++) {
-                    c.mat[(size_t)(g0 + u) * c.npoly + p] = run;
-                    run += v[u];
-                }
-            }
+            c.pcur[p] = start;
             for (unsigned k = 0; k < nit; k++) {
                 const unsigned lo = start + k * kCandItem;
                 c.items[item0 + k] = make_uint4(p, lo, tot - k * kCandItem > kCandItem ? lo + kCandItem : start + tot, 0u);
@@ -3234,7 +3226,10 @@ __global__ __launch_bounds__(kCandThreads) void ppoly_cand_scatter(CandGroup c) 
     uint64_t b0, b1;
     cand_range(c, b0, b1);
     const unsigned* row = c.mat + (size_t)blockIdx.x * c.npoly;
-    for (unsigned t = threadIdx.x; t < c.npoly; t += kCandThreads) h[t] = row[t];
+    for (unsigned t = threadIdx.x; t < c.npoly; t += kCandThreads) {
+        const unsigned v = row[t];
+        h[t] = v ? atomicAdd(&c.pcur[t], v) : 0u;  // this range's slice of the run
+    }
     __syncthreads();
     for (uint64_t i0 = b0 + threadIdx.x; i0 < b1; i0 += (uint64_t)kCandPer * kCandThreads) {
         unsigned p[kCandPer];
@@ -3275,20 +3270,10 @@ struct CandRefine {
 // about one per block (per-wave stages flushed every ~128 pairs cost 83 of the kernel's 148 us
 // for C4: same-address atomics); kRefinePer candidates per thread per round keep their gather
 // chains (slot -> polygon -> refinement base -> word) in flight together.
+#ifndef GEOHIP_RF_ABL
+#define GEOHIP_RF_ABL 0  // measurement builds: bit 0 no refinement-table gathers, bit 1 polygon 0's region only
+#endif
 constexpr unsigned kRefineBlocks = 1024, kRefinePer = 4, kRefineStage = 4096;
-__device__ __forceinline__ uint32_t refine_code(const CandRefine& c, unsigned poly, double2 xy) {
-    if (!(xy.x == xy.x && xy.y == xy.y)) return kClsMixed;  // NaN: the exact test decides
-    const PolyDev& P = c.polys[poly];
-    const uint32_t cls = P.cls;
-    const int32_t wx0 = P.wx0, wx1 = P.wx1, wy0 = P.wy0, wy1 = P.wy1;
-    const int32_t cx = d_axis_cell(xy.x, c.mnx, c.l), cy = d_axis_cell(xy.y, c.mny, c.l);
-    if (cls == kNoCls || cx < wx0 || cx > wx1 || cy < wy0 || cy > wy1) return kClsMixed;
-    const uint32_t rb = c.rf[cls + (size_t)(cx - wx0) * (uint32_t)(wy1 - wy0 + 1) + (uint32_t)(cy - wy0)];
-    if (rb == kNoRefine) return kClsMixed;
-    const int sx = sub_of(xy.x, c.mnx, c.l, cx), sy = sub_of(xy.y, c.mny, c.l, cy);
-    const int tx = sub16_of(xy.x, c.mnx, c.l, cx, sx), ty = sub16_of(xy.y, c.mny, c.l, cy, sy);
-    return (c.rfw[rb + 4 * sx + sy] >> (2 * (4 * tx + ty))) & 3u;
-}
 __global__ __launch_bounds__(kTB) void ppoly_cand_refine(CandRefine c, StreamOut o) {
     __shared__ uint2 stage[kRefineStage];
     __shared__ unsigned s_n;
@@ -3311,31 +3296,70 @@ __global__ __launch_bounds__(kTB) void ppoly_cand_refine(CandRefine c, StreamOut
     const uint64_t n = nt < c.ccap ? nt : c.ccap;
     constexpr unsigned kRound = kTB * kRefinePer;
     for (uint64_t i0 = (uint64_t)blockIdx.x * kRound; i0 < n; i0 += (uint64_t)gridDim.x * kRound) {  // block-uniform
-        unsigned poly[kRefinePer];
+        // the chain slot -> polygon region -> refinement base -> part word, each level's loads for
+        // the kRefinePer candidates issued together and unconditionally (clamped indices; the
+        // branchy form waited for each candidate's chain in turn: 4 x 4 round trips per round)
+        unsigned poly[kRefinePer], idx[kRefinePer];
         double2 xy[kRefinePer];
 #pragma unroll
         for (unsigned u = 0; u < kRefinePer; u++) {
             const uint64_t i = i0 + u * kTB + threadIdx.x;
-            poly[u] = kCandGone;
-            xy[u] = make_double2(0.0, 0.0);
-            if (i < n) {
-                poly[u] = c.cpoly[i];
-                xy[u] = *reinterpret_cast<const double2*>(&c.crec[i]);
-            }
+            const uint64_t ii = i < n ? i : 0;
+            poly[u] = c.cpoly[ii];
+            xy[u] = *reinterpret_cast<const double2*>(&c.crec[ii]);
+            idx[u] = reinterpret_cast<const unsigned*>(&c.crec[ii])[4];  // low word of the point bits
+            if (i >= n) poly[u] = kCandGone;
         }
+        uint32_t cls[kRefinePer];
+        int32_t wx0[kRefinePer], wx1[kRefinePer], wy0[kRefinePer], wy1[kRefinePer];
+#pragma unroll
+        for (unsigned u = 0; u < kRefinePer; u++) {
+            const PolyDev& P = c.polys[GEOHIP_RF_ABL & 2 ? 0u : (poly[u] != kCandGone ? poly[u] : 0u)];
+            cls[u] = P.cls;
+            wx0[u] = P.wx0;
+            wx1[u] = P.wx1;
+            wy0[u] = P.wy0;
+            wy1[u] = P.wy1;
+        }
+        size_t ri[kRefinePer];
+        bool go[kRefinePer];
+        int32_t cx[kRefinePer], cy[kRefinePer];
+#pragma unroll
+        for (unsigned u = 0; u < kRefinePer; u++) {
+            cx[u] = d_axis_cell(xy[u].x, c.mnx, c.l);
+            cy[u] = d_axis_cell(xy[u].y, c.mny, c.l);
+            go[u] = poly[u] != kCandGone && xy[u].x == xy[u].x && xy[u].y == xy[u].y && cls[u] != kNoCls &&
+                    cx[u] >= wx0[u] && cx[u] <= wx1[u] && cy[u] >= wy0[u] && cy[u] <= wy1[u];
+            ri[u] = go[u] ? cls[u] + (size_t)(cx[u] - wx0[u]) * (uint32_t)(wy1[u] - wy0[u] + 1) + (uint32_t)(cy[u] - wy0[u]) : 0;
+        }
+        uint32_t rb[kRefinePer];
+#pragma unroll
+        for (unsigned u = 0; u < kRefinePer; u++) rb[u] = GEOHIP_RF_ABL & 1 ? (uint32_t)ri[u] & 0xffffu : c.rf[ri[u]];
+        uint32_t wi[kRefinePer], sh[kRefinePer];
+#pragma unroll
+        for (unsigned u = 0; u < kRefinePer; u++) {
+            go[u] = go[u] && rb[u] != kNoRefine;
+            const int sx = sub_of(xy[u].x, c.mnx, c.l, cx[u]), sy = sub_of(xy[u].y, c.mny, c.l, cy[u]);
+            const int tx = sub16_of(xy[u].x, c.mnx, c.l, cx[u], sx), ty = sub16_of(xy[u].y, c.mny, c.l, cy[u], sy);
+            wi[u] = go[u] ? rb[u] + 4 * sx + sy : 0u;
+            sh[u] = 2 * (4 * tx + ty);
+        }
+        uint32_t wd[kRefinePer];
+#pragma unroll
+        for (unsigned u = 0; u < kRefinePer; u++) wd[u] = GEOHIP_RF_ABL & 1 ? wi[u] * 0x9E3779B1u : c.rfw[wi[u]];
 #pragma unroll
         for (unsigned u = 0; u < kRefinePer; u++) {
             const uint64_t i = i0 + u * kTB + threadIdx.x;
-            const uint32_t code = poly[u] != kCandGone ? refine_code(c, poly[u], xy[u]) : kClsMixed;
+            const uint32_t code = go[u] ? (wd[u] >> sh[u]) & 3u : kClsMixed;
             const bool hit = code == kClsHit;
             const unsigned long long m = __ballot(hit);
             if (m) {  // this wave's hits: one LDS reservation
                 unsigned wb = 0;
                 if (lane == 0) wb = atomicAdd(&s_n, (unsigned)__popcll(m));
                 wb = (unsigned)__shfl(wb, 0);
-                if (hit) stage[wb + lanes_below(m)] = make_uint2(poly[u], (unsigned)__double_as_longlong(c.crec[i].z));
+                if (hit) stage[wb + lanes_below(m)] = make_uint2(poly[u], idx[u]);
             }
-            if (poly[u] != kCandGone && code != kClsMixed) c.cpoly[i] = kCandGone;
+            if (code != kClsMixed) c.cpoly[i] = kCandGone;
         }
         __syncthreads();
         if (s_n > kRefineStage - kRound) flush();
@@ -4551,7 +4575,7 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
     if (e0) hipEventRecord(e0, st);  // the whole device step: binning, replication, join
     // every kernel of the step is timed on its own (tlaunch: the dispatch's begin / end stamps)
     tlaunch(ctx, zero_step, (nzero + kTB - 1) / kTB, kTB, 0, st, zero, nzero,
-            async ? reinterpret_cast<unsigned long long*>(count_dev) : (unsigned long long*)nullptr);
+            async ? reinterpret_cast<unsigned long long*>(count_dev) : (unsigned long long*)nullptr, (unsigned*)nullptr, 0u);
     const unsigned qb = (unsigned)((nq + kTB - 1) / kTB);
     if (nq) {
         JqGeom jg{gq->min_x, gq->min_y, gq->cell_len, nb, lc, all_cells ? 1 : 0};
@@ -5391,7 +5415,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
         for (int attempt = 0; attempt < 3; attempt++) {
             // J_MISC: [0..1] pair total, [2..3] candidate total, [4] work items
             unsigned* misc = S.get<unsigned>(J_MISC, kMiscWords * 4);
-            unsigned* mat = cands ? S.get<unsigned>(J_HIST, (size_t)kCandGroups * npoly * 4 + 16) : nullptr;
+            unsigned* mat = cands ? S.get<unsigned>(J_HIST, ((size_t)kCandGroups + 2) * npoly * 4 + 16) : nullptr;
             void* cbuf = cands ? S.get<void>(J_SY, ccap * 36 + 64) : nullptr;
             const bool refine = cands && !pc->hrfw.empty();
             void* sbuf = cands ? S.get<void>(J_SX, ccap * 4 + 64) : nullptr;
@@ -5401,8 +5425,10 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             ctx_timing_events(ctx, &e0, &e1);
             if (e0) hipEventRecord(e0, st);  // the whole device step
             // totals and the item count (async: the pair total is the caller's device word)
-            tlaunch(ctx, zero_step, 1, 64, 0, st, misc, 8u,
-                    async ? reinterpret_cast<unsigned long long*>(count_dev) : (unsigned long long*)nullptr);
+            unsigned* ptot = cands ? mat + (size_t)kCandGroups * npoly : nullptr;  // then pcur
+            tlaunch(ctx, zero_step, 1, kTB, 0, st, misc, 8u,
+                    async ? reinterpret_cast<unsigned long long*>(count_dev) : (unsigned long long*)nullptr, ptot,
+                    cands ? npoly : 0u);
             StreamOut so;
             so.out = out;
             so.cap = out ? cap : 0;
@@ -5475,6 +5501,8 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
                 cg.fault = fault;
                 cg.need = fault ? reinterpret_cast<unsigned long long*>(fault + 2) : nullptr;
                 cg.mat = mat;
+                cg.ptot = ptot;
+                cg.pcur = ptot + npoly;
                 cg.npoly = npoly;
                 cg.items = items;
                 cg.nitems = misc + 4;
@@ -5495,9 +5523,9 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             const uint64_t ncand = pin[1];
             pc->last_cand = ncand;
             if (prof && attempt == 0)
-                fprintf(stderr, "ppoly host: plan %.1f us (cached %d), %zu refined cells\n",
+                fprintf(stderr, "ppoly host: plan %.1f us (cached %d), %zu refined cells, class table %zu cells\n",
                         std::chrono::duration<double, std::micro>(t_planned - t_start).count(), (int)cached,
-                        pc->hrfw.size() / 16);
+                        pc->hrfw.size() / 16, pc->hcls.size());
             if (prof) fprintf(stderr, "ppoly stream: %llu pairs, %llu candidates (capacity %llu), %u of %llu chunks re-run\n",
                               (unsigned long long)tot, (unsigned long long)ncand, (unsigned long long)ccap, (unsigned)(pin[2] >> 32),
                               (unsigned long long)nchunks);
