@@ -3128,6 +3128,7 @@ struct CandGroup {
     uint32_t npoly;         // <= kCandLdsPolys
     uint4* items;           // (poly, begin, end, -)
     unsigned* nitems;
+    unsigned* eticket;      // the evaluation's item ticket (zeroed with the step's totals)
     unsigned* sidx;         // sorted runs: slots of the unsorted candidate arrays
 };
 
@@ -3169,44 +3170,63 @@ __global__ __launch_bounds__(kCandThreads) void ppoly_cand_hist(CandGroup c) {
 }
 
 // one block: the polygons' totals scanned into run starts (their cursors) and the kCandItem
-// work items
+// work items -- every polygon's full items first, then the partial ones (the evaluation claims
+// items in order, so the long items start first and the short ones fill in behind them)
 __global__ __launch_bounds__(kCandThreads) void ppoly_cand_plan(CandGroup c) {
-    __shared__ unsigned sc[kCandThreads], si[kCandThreads];
-    __shared__ unsigned carry_c, carry_i;
+    __shared__ unsigned sc[kCandThreads], sf[kCandThreads], sp[kCandThreads];
+    __shared__ unsigned carry_c, carry_f, carry_p, nfull;
     if (threadIdx.x == 0) {
         carry_c = 0;
-        carry_i = 0;
+        carry_f = 0;
+        carry_p = 0;
+        nfull = 0;
     }
+    __syncthreads();
+    {  // the full items' count (the partial items follow them)
+        unsigned f = 0;
+        for (unsigned p = threadIdx.x; p < c.npoly; p += kCandThreads) f += c.ptot[p] / kCandItem;
+        f = wave_incl_scan(f);
+        if (lane_id() == kWave - 1 && f) atomicAdd(&nfull, f);
+    }
+    __syncthreads();
+    const unsigned F = nfull;
     for (unsigned p0 = 0; p0 < c.npoly; p0 += kCandThreads) {
         const unsigned p = p0 + threadIdx.x;
         const unsigned tot = p < c.npoly ? c.ptot[p] : 0u;
-        const unsigned nit = (tot + kCandItem - 1) / kCandItem;
+        const unsigned nf = tot / kCandItem, np = tot % kCandItem ? 1u : 0u;
         sc[threadIdx.x] = tot;
-        si[threadIdx.x] = nit;
+        sf[threadIdx.x] = nf;
+        sp[threadIdx.x] = np;
         __syncthreads();
         for (unsigned o = 1; o < kCandThreads; o <<= 1) {
             const unsigned a = threadIdx.x >= o ? sc[threadIdx.x - o] : 0u;
-            const unsigned b = threadIdx.x >= o ? si[threadIdx.x - o] : 0u;
+            const unsigned b = threadIdx.x >= o ? sf[threadIdx.x - o] : 0u;
+            const unsigned d = threadIdx.x >= o ? sp[threadIdx.x - o] : 0u;
             __syncthreads();
             sc[threadIdx.x] += a;
-            si[threadIdx.x] += b;
+            sf[threadIdx.x] += b;
+            sp[threadIdx.x] += d;
             __syncthreads();
         }
-        const unsigned start = carry_c + sc[threadIdx.x] - tot, item0 = carry_i + si[threadIdx.x] - nit;
+        const unsigned start = carry_c + sc[threadIdx.x] - tot;
+        const unsigned f0 = carry_f + sf[threadIdx.x] - nf, p0i = F + carry_p + sp[threadIdx.x] - np;
         if (p < c.npoly) {
             c.pcur[p] = start;
-            for (unsigned k = 0; k < nit; k++) {
+            for (unsigned k = 0; k < nf; k++) {
                 const unsigned lo = start + k * kCandItem;
-                c.items[item0 + k] = make_uint4(p, lo, tot - k * kCandItem > kCandItem ? lo + kCandItem : start + tot, 0u);
+                c.items[f0 + k] = make_uint4(p, lo, lo + kCandItem, 0u);
             }
+            if (np) c.items[p0i] = make_uint4(p, start + nf * kCandItem, start + tot, 0u);
         }
         __syncthreads();
         if (threadIdx.x == kCandThreads - 1) {
             carry_c += sc[kCandThreads - 1];
-            carry_i += si[kCandThreads - 1];
+            carry_f += sf[kCandThreads - 1];
+            carry_p += sp[kCandThreads - 1];
         }
         __syncthreads();
     }
+    const unsigned carry_i = F + carry_p;
     if (threadIdx.x == 0) {
         *c.nitems = carry_i;
         // an async call cannot rerun with a larger buffer: the overflow (the candidates past ccap
@@ -3403,14 +3423,21 @@ __global__ __launch_bounds__(kTB) void ppoly_cand_eval(CandGroup c, const PolyDe
     uint2* pb = pbuf[wid];
     unsigned pc = 0;
     const unsigned ni = *c.nitems;
-    for (unsigned it = blockIdx.x; it < ni; it += gridDim.x) {
+    __shared__ unsigned s_it;
+    for (;;) {
+        // items claimed in order from a ticket: a block done with a short item takes the next
+        // (a static stride gave the blocks with two long items the whole pass's tail)
+        __syncthreads();  // the previous item's LDS reads are done
+        if (threadIdx.x == 0) s_it = atomicAdd(c.eticket, 1u);
+        __syncthreads();
+        const unsigned it = (unsigned)__builtin_amdgcn_readfirstlane((int)s_it);
+        if (it >= ni) break;
         const uint4 w = c.items[it];
         const unsigned poly = w.x, m = w.z - w.y;
         const PolyDev P = polys[poly];
         const bool v_lds = P.nv <= (uint32_t)kEvalLdsVerts;
         const bool s_lds = P.llen <= (uint32_t)kEvalLdsSlab;
         const bool holes = P.nring > 1;
-        __syncthreads();  // the previous item's LDS reads are done
         if (v_lds)
             for (uint32_t t = threadIdx.x; t < P.nv; t += kTB) {
                 lvx[t] = vx[P.voff + t];
@@ -5413,7 +5440,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             if (rc) return rc;
         }
         for (int attempt = 0; attempt < 3; attempt++) {
-            // J_MISC: [0..1] pair total, [2..3] candidate total, [4] work items
+            // J_MISC: [0..1] pair total, [2..3] candidate total, [4] work items, [5] re-runs, [6] eval ticket
             unsigned* misc = S.get<unsigned>(J_MISC, kMiscWords * 4);
             unsigned* mat = cands ? S.get<unsigned>(J_HIST, ((size_t)kCandGroups + 2) * npoly * 4 + 16) : nullptr;
             void* cbuf = cands ? S.get<void>(J_SY, ccap * 36 + 64) : nullptr;
@@ -5506,6 +5533,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
                 cg.npoly = npoly;
                 cg.items = items;
                 cg.nitems = misc + 4;
+                cg.eticket = misc + 6;
                 cg.sidx = reinterpret_cast<unsigned*>(sb);
                 tlaunch(ctx, ppoly_cand_hist, kCandGroups, kCandThreads, 0, st, cg);
                 tlaunch(ctx, ppoly_cand_plan, 1, kCandThreads, 0, st, cg);
