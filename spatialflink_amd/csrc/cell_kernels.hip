@@ -1747,10 +1747,18 @@ __host__ __device__ __forceinline__ int sub_of(double v, double mn, double l, in
 
 // Refinement of the mixed subcells (ppoly_cand_refine): a mixed subcell is split again 4 x 4 on
 // the sixteenth-cell edges sub16_edge (the subcell edges are every fourth of them, bit-identical:
-// 0.0625 * 4 i == 0.25 i), each part classified by the same BoxClassifier.  Per walk-region cell,
-// rf[cell] = the first of its 16 refinement words (one per subcell, 2 bits per part: 4 tx + ty),
-// or kNoRefine when the cell has no mixed subcell.
+// 0.0625 * 4 i == 0.25 i), each part classified by the same BoxClassifier.  Per walk-region cell
+// a pair rf[2 cell] = the first of its refinement words or kNoRefine (no part of a mixed subcell
+// decided), rf[2 cell + 1] = its class word; one word per MIXED subcell (2 bits per part: 4 tx +
+// ty), in subcell order, so subcell s's word is rank(s) words in, rank = the mixed subcells below s
+// in the class word (refine_rank).  (16 words per refined cell took 2.55 MB for C4 and its gathers
+// 24 of the refinement's 63 us.)
 constexpr uint32_t kNoRefine = 0xffffffffu;
+// mixed subcells of a class word below subcell s (fields of value kClsMixed = 0)
+__host__ __device__ __forceinline__ uint32_t refine_mixed(uint32_t word) { return ~(word | (word >> 1)) & 0x55555555u; }
+__host__ __device__ __forceinline__ uint32_t refine_rank(uint32_t word, int s) {
+    return (uint32_t)__builtin_popcount(refine_mixed(word) & ((1u << (2 * s)) - 1u));
+}
 __host__ __device__ __forceinline__ double sub16_edge(double mn, double l, int32_t c, int j) {
     return mn + ((double)c + 0.0625 * (double)j) * l;
 }
@@ -3282,7 +3290,7 @@ struct CandRefine {
     unsigned* cpoly;                   // decided candidates -> kCandGone
     const double4* crec;
     const PolyDev* polys;
-    const uint32_t* rf;                // per walk-region cell (PolyDev.cls indexing): refinement base
+    const uint2* rf;                   // per walk-region cell (PolyDev.cls indexing): (refinement base, class word)
     const uint32_t* rfw;
     double mnx, mny, l;                // the point grid (cells as the stream computed them)
 };
@@ -3290,9 +3298,6 @@ struct CandRefine {
 // about one per block (per-wave stages flushed every ~128 pairs cost 83 of the kernel's 148 us
 // for C4: same-address atomics); kRefinePer candidates per thread per round keep their gather
 // chains (slot -> polygon -> refinement base -> word) in flight together.
-#ifndef GEOHIP_RF_ABL
-#define GEOHIP_RF_ABL 0  // measurement builds: bit 0 no refinement-table gathers, bit 1 polygon 0's region only
-#endif
 constexpr unsigned kRefineBlocks = 1024, kRefinePer = 4, kRefineStage = 4096;
 __global__ __launch_bounds__(kTB) void ppoly_cand_refine(CandRefine c, StreamOut o) {
     __shared__ uint2 stage[kRefineStage];
@@ -3334,7 +3339,7 @@ __global__ __launch_bounds__(kTB) void ppoly_cand_refine(CandRefine c, StreamOut
         int32_t wx0[kRefinePer], wx1[kRefinePer], wy0[kRefinePer], wy1[kRefinePer];
 #pragma unroll
         for (unsigned u = 0; u < kRefinePer; u++) {
-            const PolyDev& P = c.polys[GEOHIP_RF_ABL & 2 ? 0u : (poly[u] != kCandGone ? poly[u] : 0u)];
+            const PolyDev& P = c.polys[poly[u] != kCandGone ? poly[u] : 0u];
             cls[u] = P.cls;
             wx0[u] = P.wx0;
             wx1[u] = P.wx1;
@@ -3352,21 +3357,23 @@ __global__ __launch_bounds__(kTB) void ppoly_cand_refine(CandRefine c, StreamOut
                     cx[u] >= wx0[u] && cx[u] <= wx1[u] && cy[u] >= wy0[u] && cy[u] <= wy1[u];
             ri[u] = go[u] ? cls[u] + (size_t)(cx[u] - wx0[u]) * (uint32_t)(wy1[u] - wy0[u] + 1) + (uint32_t)(cy[u] - wy0[u]) : 0;
         }
-        uint32_t rb[kRefinePer];
+        uint2 rb[kRefinePer];
 #pragma unroll
-        for (unsigned u = 0; u < kRefinePer; u++) rb[u] = GEOHIP_RF_ABL & 1 ? (uint32_t)ri[u] & 0xffffu : c.rf[ri[u]];
+        for (unsigned u = 0; u < kRefinePer; u++) rb[u] = c.rf[ri[u]];
         uint32_t wi[kRefinePer], sh[kRefinePer];
 #pragma unroll
         for (unsigned u = 0; u < kRefinePer; u++) {
-            go[u] = go[u] && rb[u] != kNoRefine;
             const int sx = sub_of(xy[u].x, c.mnx, c.l, cx[u]), sy = sub_of(xy[u].y, c.mny, c.l, cy[u]);
             const int tx = sub16_of(xy[u].x, c.mnx, c.l, cx[u], sx), ty = sub16_of(xy[u].y, c.mny, c.l, cy[u], sy);
-            wi[u] = go[u] ? rb[u] + 4 * sx + sy : 0u;
+            const int sub = 4 * sx + sy;
+            // the candidate's subcell is mixed (the stream emitted it for that); if not, it stays
+            go[u] = go[u] && rb[u].x != kNoRefine && ((refine_mixed(rb[u].y) >> (2 * sub)) & 1u);
+            wi[u] = go[u] ? rb[u].x + refine_rank(rb[u].y, sub) : 0u;
             sh[u] = 2 * (4 * tx + ty);
         }
         uint32_t wd[kRefinePer];
 #pragma unroll
-        for (unsigned u = 0; u < kRefinePer; u++) wd[u] = GEOHIP_RF_ABL & 1 ? wi[u] * 0x9E3779B1u : c.rfw[wi[u]];
+        for (unsigned u = 0; u < kRefinePer; u++) wd[u] = c.rfw[wi[u]];
 #pragma unroll
         for (unsigned u = 0; u < kRefinePer; u++) {
             const uint64_t i = i0 + u * kTB + threadIdx.x;
@@ -4894,7 +4901,7 @@ bool classify_cells(const PolyDev& P, const std::vector<double>& hvx, const std:
     const size_t base = blob.size();
     blob.resize(base + (size_t)w * h, 0u);  // all mixed
     uint32_t* out = blob.data() + base;
-    if (rf) rf->resize(base + (size_t)w * h, kNoRefine);
+    if (rf) rf->resize(2 * (base + (size_t)w * h), kNoRefine);
     // subcell i of an axis: the doubles v of the cell box [bl, bh] with sub_of(v) == i
     auto sub_iv = [](double mn, double l, int32_t c, double bl, double bh, int i, double& lo, double& hi) {
         lo = i == 0 ? bl : std::max(bl, sub_edge(mn, l, c, i));
@@ -4944,8 +4951,11 @@ bool classify_cells(const PolyDev& P, const std::vector<double>& hvx, const std:
             }
             out[(size_t)a * h + c] = word;
             if (refined) {
-                (*rf)[base + (size_t)a * h + c] = (uint32_t)rfw->size();
-                rfw->insert(rfw->end(), rw, rw + 16);
+                const size_t at = 2 * (base + (size_t)a * h + c);
+                (*rf)[at] = (uint32_t)rfw->size();
+                (*rf)[at + 1] = word;
+                for (int q = 0; q < 16; q++)
+                    if ((refine_mixed(word) >> (2 * q)) & 1u) rfw->push_back(rw[q]);
             }
         }
     }
@@ -5003,8 +5013,8 @@ struct PolyCache {
     std::vector<PolyWork> hwork;
     std::vector<uint16_t> hslab;
     std::vector<uint32_t> hcls;  // per-cell class words (classify_cells), PolyDev.cls offsets into it
-    std::vector<uint32_t> hrf;   // parallel to hcls: first refinement word of the cell, or kNoRefine
-    std::vector<uint32_t> hrfw;  // refinement words (16 per refined cell)
+    std::vector<uint32_t> hrf;   // 2 per hcls cell: first refinement word (or kNoRefine), class word
+    std::vector<uint32_t> hrfw;  // refinement words (one per mixed subcell of a refined cell)
     std::vector<uint32_t> keep;  // cells of any polygon's G or C rectangles (empty: no filter)
     bool any_outside = false;
     // streaming path (ppoly_stream): per key cell its polygon entries, the cells holding any
@@ -5285,7 +5295,10 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
                 const uint32_t wbase = (uint32_t)fresh.hrfw.size();
                 pd[p].cls = (uint32_t)fresh.hcls.size();
                 fresh.hcls.insert(fresh.hcls.end(), q.blob.begin(), q.blob.end());
-                for (uint32_t v : q.rf) fresh.hrf.push_back(v == kNoRefine ? kNoRefine : v + wbase);
+                for (size_t k = 0; k < q.rf.size(); k += 2) {  // (first word, class word) pairs
+                    fresh.hrf.push_back(q.rf[k] == kNoRefine ? kNoRefine : q.rf[k] + wbase);
+                    fresh.hrf.push_back(q.rf[k + 1]);
+                }
                 fresh.hrfw.insert(fresh.hrfw.end(), q.rfw.begin(), q.rfw.end());
                 std::vector<uint32_t>().swap(q.blob);
             }
@@ -5393,7 +5406,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     uint2* dcent = reinterpret_cast<uint2*>(bp + off_ce);
     unsigned* dskeep = reinterpret_cast<unsigned*>(bp + off_sk);
     uint32_t* dopoly = reinterpret_cast<uint32_t*>(bp + off_op);
-    uint32_t* drf = reinterpret_cast<uint32_t*>(bp + off_rf);
+    uint2* drf = reinterpret_cast<uint2*>(bp + off_rf);
     uint32_t* drfw = reinterpret_cast<uint32_t*>(bp + off_rw);
     if (upload) {
         pc->dev_blob = nullptr;  // until the copies are issued
@@ -5553,7 +5566,8 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             if (prof && attempt == 0)
                 fprintf(stderr, "ppoly host: plan %.1f us (cached %d), %zu refined cells, class table %zu cells\n",
                         std::chrono::duration<double, std::micro>(t_planned - t_start).count(), (int)cached,
-                        pc->hrfw.size() / 16, pc->hcls.size());
+                        (size_t)std::count_if(pc->hrf.begin(), pc->hrf.end(), [](uint32_t v) { return v != kNoRefine; }) / 2,
+                        pc->hcls.size());
             if (prof) fprintf(stderr, "ppoly stream: %llu pairs, %llu candidates (capacity %llu), %u of %llu chunks re-run\n",
                               (unsigned long long)tot, (unsigned long long)ncand, (unsigned long long)ccap, (unsigned)(pin[2] >> 32),
                               (unsigned long long)nchunks);
