@@ -644,8 +644,9 @@ class PpolyWorkload(Workload):
     window, 500x500, r = 0.005 (conf/geoflink-conf.yml:52)."""
     tag = "ppoly_probe"
     kernel = ("geohip point-polygon step: ppoly_stream (one pass over the window: cell-table heads, decided pairs, "
-              "mixed-subcell candidates, chunk look-back offsets) + candidates grouped by polygon + ppoly_cand_eval "
-              "(exact JTS tests); the whole device step is timed")
+              "mixed-subcell candidates, one reservation per chunk) + ppoly_cand_refine (4x4 parts of mixed "
+              "subcells) + candidates grouped by polygon + ppoly_cand_eval (exact JTS tests); the whole device "
+              "step is timed")
     grid_n, radius, n_default, npoly = 500, 0.005, 50_000_000, 1000
     windows = 2
 
@@ -744,7 +745,7 @@ class PpJoinWorkload(PpolyWorkload):
     """the C4 shape as a point-polygon join (PointPolygonJoinQuery,
     polygon stream replicated to its G/C cells, every candidate distance-checked)."""
     tag = "ppjoin"
-    kernel = ("geohip point-polygon join step: ppoly_stream + candidate grouping + ppoly_cand_eval in join mode; "
+    kernel = ("geohip point-polygon join step: ppoly_stream + refinement + candidate grouping + ppoly_cand_eval in join mode; "
               "the whole device step is timed")
 
     def __init__(self, *a):
@@ -858,7 +859,7 @@ class PpolyIncrWorkload(PpolyWorkload):
     once against the 1k polygons, the window's pairs assembled from its two panes
     (spatialflink_amd.incremental.IncrementalPPolyRange).  value = stream points/sec."""
     tag = "ppoly_incr"
-    kernel = "geohip point-polygon step on one pane (ppoly_stream + candidate grouping + ppoly_cand_eval, timed)"
+    kernel = "geohip point-polygon step on one pane (ppoly_stream + refinement + candidate grouping + ppoly_cand_eval, timed)"
     n_default = 25_000_000
     windows = 4
 

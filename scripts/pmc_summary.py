@@ -25,15 +25,16 @@ _PP = {**_BIN, "scan_seg_totals<unsigned int>": 1, "scan_totals<unsigned int>": 
        "scan_seg_totals<unsigned long long>": 2, "scan_totals<unsigned long long>": 2,
        "scan_apply<unsigned long long>": 2, "ppoly_words": 1, "ppoly_eval": 1, "ppoly_emit": 1, "ppoly_outside": 1}
 # streaming point-polygon step (r03): one pass over the window + candidate grouping + exact tests
-_PS = {"ppoly_stream": 1, "ppoly_cand_hist": 1, "ppoly_cand_plan": 1, "ppoly_cand_scatter": 1, "ppoly_cand_eval": 1}
+_PS = {"ppoly_stream": 1, "ppoly_cand_refine": 1, "ppoly_cand_hist": 1, "ppoly_cand_plan": 1, "ppoly_cand_scatter": 1,
+       "ppoly_cand_eval": 1}
 # SQ_INSTS_VALU_FLOPS_FP64 counts per wave instruction: calibrated on synth_uniform (6 fp64
 # add/mul per point in its ISA, 50M points -> 4,687,500 counted = 300M / 64), so lane FLOPs are
 # the counted value times 64 (issued lanes: a divergent wave's idle lanes are included).
 FP64_LANES = 64
 # r04 join step: query lists, two binning passes into 16-B records, plan, one join pass
-_JOIN = {"fill_words": 1, "jq_rect": 1, "jq_build<false>": 1, "jq_build<true>": 1, "jq_starts": 1, "jb_bands": 1,
+_JOIN = {"zero_step": 1, "jq_rect": 1, "jq_build<false>": 1, "jq_build<true>": 1, "jq_starts": 1, "jb_bands": 1,
          "jb_scan": 1, "jb_segs": 1, "jb_tiles": 1, "join_fused<false, true>": 1}
-_PS = {**_PS, "fill_words": 1}
+_PS = {**_PS, "zero_step": 1}
 TAGS = {"knn": ("knn_scan", {"knn_pass": 1}),
         "range": ("range", {"range_fused": 1, "range_scan": 1, "scan_units": 1, "range_emit": 1}),
         "join": ("join_probe", _JOIN),
