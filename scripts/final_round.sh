@@ -15,8 +15,13 @@ for w in ${WORKLOADS:-knn range c5 join ppoly ingest ppjoin ppknn knn_incr ppoly
   timeout -k 10 300 python -u bench.py --workload "$w" --steps $steps --warmup 3 \
       > gpurun_out/final/bench_$w.log 2>&1 || { echo "bench $w failed"; tail -20 gpurun_out/final/bench_$w.log; exit 2; }
   grep '^{' gpurun_out/final/bench_$w.log | cut -c1-160
+  [ "${PROF:-1}" = "1" ] || continue
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/final/prof -o $w -- \
       python3 bench.py --workload "$w" --steps $steps --warmup 3 --no-cpu-baseline --no-e2e --no-pipelined --no-cells-line \
       > gpurun_out/final/prof/bench_$w.log 2>&1 || { echo "rocprof $w failed"; tail -20 gpurun_out/final/prof/bench_$w.log; exit 3; }
 done
+if [ "${DEFAULT:-0}" = "1" ]; then  # the driver's own command: no flags
+  timeout -k 10 300 python -u bench.py > gpurun_out/final/bench_default.log 2>&1 || { echo "bench default failed"; exit 4; }
+  grep '^{' gpurun_out/final/bench_default.log | cut -c1-160
+fi
 echo done
