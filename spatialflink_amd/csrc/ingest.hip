@@ -26,10 +26,12 @@
 namespace geohip {
 namespace {
 
-constexpr int kThreads = (int)(kIngestChunk / 32);  // 512: 32 bytes per thread
+constexpr int kThreads = 512;
 constexpr unsigned kGeneralBlocks = 256;               // ingest_general's grid (strides over its list)
-constexpr uint32_t kBytesPerThread = kIngestChunk / kThreads;  // 32: two 16-byte loads
-static_assert(kBytesPerThread == 32, "chunk layout");
+constexpr uint32_t kBytesPerThread = kIngestChunk / kThreads;  // 16-byte loads per thread: kLoads
+constexpr int kLoads = (int)(kBytesPerThread / 16);
+static_assert(kBytesPerThread % 16 == 0 && kLoads >= 2 && kLoads <= 4, "chunk layout");
+static_assert(kIngestChunk + kIngestTail < 65536, "record starts are u16 offsets into the staged chunk");
 
 // bit 7 of each byte set iff that byte of w is '\n' (exact: no borrow between bytes)
 __device__ __forceinline__ uint32_t nl_bits(uint32_t w) {
@@ -50,18 +52,21 @@ __device__ __forceinline__ uint4 load16(const uint8_t* text, uint64_t p, uint64_
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-// '\n' mask of 32 bytes starting at p (bit i = byte p + i); only positions < lim count
-__device__ __forceinline__ uint32_t nl_mask32(const uint4& a, const uint4& b, uint64_t p, uint64_t lim) {
-    const uint32_t wv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    uint32_t m = 0;
+// '\n' mask of the kBytesPerThread bytes starting at p (bit i = byte p + i); only positions < lim count
+__device__ __forceinline__ uint64_t nl_mask(const uint4 (&v)[kLoads], uint64_t p, uint64_t lim) {
+    uint64_t m = 0;
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-        const uint32_t z = nl_bits(wv[k]);
-        // gather bits 7, 15, 23, 31 into bits 4k .. 4k+3
-        const uint32_t g = ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
-        m |= g << (4 * k);
+    for (int j = 0; j < kLoads; j++) {
+        const uint32_t wv[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t z = nl_bits(wv[k]);
+            // gather bits 7, 15, 23, 31 into bits 4k .. 4k+3 of this load's 16
+            const uint32_t g = ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+            m |= (uint64_t)g << (16 * j + 4 * k);
+        }
     }
-    if (p + 32 > lim) m &= p >= lim ? 0u : ((1u << (uint32_t)(lim - p)) - 1u);
+    if (p + kBytesPerThread > lim) m &= p >= lim ? 0ull : ((1ull << (uint32_t)(lim - p)) - 1ull);
     return m;
 }
 
@@ -355,21 +360,23 @@ __device__ __forceinline__ unsigned stage_chunk(const uint8_t* __restrict__ text
     const uint64_t c0 = (uint64_t)vb * kIngestChunk;
     // the chunk first (this thread's 32 bytes stay in registers for the '\n' scan)
     const uint64_t p = c0 + threadIdx.x * kBytesPerThread;
-    const uint4 va = load16(text, p, nbytes), vb4 = load16(text, p + 16, nbytes);
-    L.text4[threadIdx.x * 2] = va;
-    L.text4[threadIdx.x * 2 + 1] = vb4;
+    uint4 v[kLoads];
+#pragma unroll
+    for (int j = 0; j < kLoads; j++) v[j] = load16(text, p + 16 * j, nbytes);
+#pragma unroll
+    for (int j = 0; j < kLoads; j++) L.text4[threadIdx.x * kLoads + j] = v[j];
     for (uint32_t i = kIngestChunk / 16 + threadIdx.x; i < (kIngestChunk + kIngestTail) / 16; i += kThreads) {
         const uint64_t q = c0 + (uint64_t)i * 16;
         if (q < nbytes) L.text4[i] = load16(text, q, nbytes);
     }
-    const uint32_t m = p < nbytes ? nl_mask32(va, vb4, p, nbytes - 1) : 0u;
+    const uint64_t m = p < nbytes ? nl_mask(v, p, nbytes - 1) : 0ull;
     const bool first = vb == 0 && threadIdx.x == 0 && nbytes > 0;
-    const unsigned mine = __builtin_popcount(m) + (first ? 1u : 0u);
+    const unsigned mine = (unsigned)__popcll(m) + (first ? 1u : 0u);
     unsigned nrec;
     unsigned at = block_excl_scan(mine, L.wave, &nrec);
     if (first) L.start[at++] = 0;
-    for (uint32_t mm = m; mm; mm &= mm - 1) {
-        if (at < CAP) L.start[at] = (uint16_t)(threadIdx.x * kBytesPerThread + __builtin_ctz(mm) + 1);
+    for (uint64_t mm = m; mm; mm &= mm - 1) {
+        if (at < CAP) L.start[at] = (uint16_t)(threadIdx.x * kBytesPerThread + __builtin_ctzll(mm) + 1);
         at++;
     }
     __syncthreads();
