@@ -1752,7 +1752,8 @@ __host__ __device__ __forceinline__ int sub_of(double v, double mn, double l, in
 // decided), rf[2 cell + 1] = its class word; one word per MIXED subcell (2 bits per part: 4 tx +
 // ty), in subcell order, so subcell s's word is rank(s) words in, rank = the mixed subcells below s
 // in the class word (refine_rank).  (16 words per refined cell took 2.55 MB for C4 and its gathers
-// 24 of the refinement's 63 us.)
+// 24 of the refinement's 63 us.)  Each such word comes with the first of its second-level words
+// (one per mixed part, in part order, 2 bits per 64th-cell sub-part), or kNoRefine.
 constexpr uint32_t kNoRefine = 0xffffffffu;
 // mixed subcells of a class word below subcell s (fields of value kClsMixed = 0)
 __host__ __device__ __forceinline__ uint32_t refine_mixed(uint32_t word) { return ~(word | (word >> 1)) & 0x55555555u; }
@@ -1766,6 +1767,16 @@ __host__ __device__ __forceinline__ double sub16_edge(double mn, double l, int32
 __host__ __device__ __forceinline__ int sub16_of(double v, double mn, double l, int32_t c, int s) {
     return (v >= sub16_edge(mn, l, c, 4 * s + 1) ? 1 : 0) + (v >= sub16_edge(mn, l, c, 4 * s + 2) ? 1 : 0) +
            (v >= sub16_edge(mn, l, c, 4 * s + 3) ? 1 : 0);
+}
+// Second level: a mixed part is split 4 x 4 again on the 64th-cell edges (every fourth is a part
+// edge, bit-identical: 0.015625 * 4 j == 0.0625 j); sub-part u (0..3) of part q (0..15 along the
+// axis, q = 4 s + t) of cell c: #{i in 1..3 : v >= sub64_edge(4 q + i)}
+__host__ __device__ __forceinline__ double sub64_edge(double mn, double l, int32_t c, int j) {
+    return mn + ((double)c + 0.015625 * (double)j) * l;
+}
+__host__ __device__ __forceinline__ int sub64_of(double v, double mn, double l, int32_t c, int q) {
+    return (v >= sub64_edge(mn, l, c, 4 * q + 1) ? 1 : 0) + (v >= sub64_edge(mn, l, c, 4 * q + 2) ? 1 : 0) +
+           (v >= sub64_edge(mn, l, c, 4 * q + 3) ? 1 : 0);
 }
 
 // Polygons with holes: rings are stored back to back in one vertex run, with a ring id per
@@ -2419,7 +2430,10 @@ constexpr unsigned kSPairCap = 2 * kStreamChunk;  // block-staged pairs per chun
 constexpr unsigned kSCandCap = kStreamChunk / 4;  // block-staged candidates per chunk (per wave likewise)
 constexpr unsigned kLocalBits = GEOHIP_PS_CHUNK_BITS;  // point within its chunk
 constexpr uint32_t kStreamMaxPolys = 1u << (32 - kLocalBits);
-constexpr unsigned kCandItem = 1024;       // candidates per evaluation work item
+#ifndef GEOHIP_CAND_ITEM
+#define GEOHIP_CAND_ITEM 1024
+#endif
+constexpr unsigned kCandItem = GEOHIP_CAND_ITEM;  // candidates per evaluation work item
 constexpr unsigned kCandLdsPolys = 16384;  // polygons whose per-polygon counters fit LDS
 constexpr unsigned kEvalBlocks = 1024;     // grid of the evaluation pass (strides over its items)
 static_assert(kStreamChunk == (1u << kLocalBits), "chunk-local point ids");
@@ -3291,7 +3305,8 @@ struct CandRefine {
     const double4* crec;
     const PolyDev* polys;
     const uint2* rf;                   // per walk-region cell (PolyDev.cls indexing): (refinement base, class word)
-    const uint32_t* rfw;
+    const uint2* rfw;                  // per mixed subcell: (part word, first second-level word)
+    const uint32_t* rfw2;              // per mixed part: sub-part word
     double mnx, mny, l;                // the point grid (cells as the stream computed them)
 };
 // Pairs go to a block-wide LDS stage (kRefineStage) reserved with one global atomic per flush --
@@ -3360,24 +3375,37 @@ __global__ __launch_bounds__(kTB) void ppoly_cand_refine(CandRefine c, StreamOut
         uint2 rb[kRefinePer];
 #pragma unroll
         for (unsigned u = 0; u < kRefinePer; u++) rb[u] = c.rf[ri[u]];
-        uint32_t wi[kRefinePer], sh[kRefinePer];
+        uint32_t wi[kRefinePer], pt[kRefinePer], sh2[kRefinePer];
 #pragma unroll
         for (unsigned u = 0; u < kRefinePer; u++) {
             const int sx = sub_of(xy[u].x, c.mnx, c.l, cx[u]), sy = sub_of(xy[u].y, c.mny, c.l, cy[u]);
             const int tx = sub16_of(xy[u].x, c.mnx, c.l, cx[u], sx), ty = sub16_of(xy[u].y, c.mny, c.l, cy[u], sy);
+            const int vx2 = sub64_of(xy[u].x, c.mnx, c.l, cx[u], 4 * sx + tx), vy2 = sub64_of(xy[u].y, c.mny, c.l, cy[u], 4 * sy + ty);
             const int sub = 4 * sx + sy;
             // the candidate's subcell is mixed (the stream emitted it for that); if not, it stays
             go[u] = go[u] && rb[u].x != kNoRefine && ((refine_mixed(rb[u].y) >> (2 * sub)) & 1u);
             wi[u] = go[u] ? rb[u].x + refine_rank(rb[u].y, sub) : 0u;
-            sh[u] = 2 * (4 * tx + ty);
+            pt[u] = 4 * tx + ty;
+            sh2[u] = 2 * (4 * vx2 + vy2);
         }
-        uint32_t wd[kRefinePer];
+        uint2 wd[kRefinePer];
 #pragma unroll
         for (unsigned u = 0; u < kRefinePer; u++) wd[u] = c.rfw[wi[u]];
+        uint32_t code1[kRefinePer], w2i[kRefinePer];
+        bool go2[kRefinePer];
+#pragma unroll
+        for (unsigned u = 0; u < kRefinePer; u++) {
+            code1[u] = go[u] ? (wd[u].x >> (2 * pt[u])) & 3u : kClsMixed;
+            go2[u] = go[u] && code1[u] == kClsMixed && wd[u].y != kNoRefine;
+            w2i[u] = go2[u] ? wd[u].y + refine_rank(wd[u].x, (int)pt[u]) : 0u;
+        }
+        uint32_t wd2[kRefinePer];
+#pragma unroll
+        for (unsigned u = 0; u < kRefinePer; u++) wd2[u] = c.rfw2[w2i[u]];
 #pragma unroll
         for (unsigned u = 0; u < kRefinePer; u++) {
             const uint64_t i = i0 + u * kTB + threadIdx.x;
-            const uint32_t code = go[u] ? (wd[u] >> sh[u]) & 3u : kClsMixed;
+            const uint32_t code = go2[u] ? (wd2[u] >> sh2[u]) & 3u : code1[u];
             const bool hit = code == kClsHit;
             const unsigned long long m = __ballot(hit);
             if (m) {  // this wave's hits: one LDS reservation
@@ -3399,6 +3427,9 @@ __global__ __launch_bounds__(kTB) void ppoly_cand_refine(CandRefine c, StreamOut
 // round-4 sizes -- 512 vertices, 2048 slab entries, 512 staged pairs per wave, 58.6 KB -- left 2
 // blocks per CU and this latency-bound pass at 2 waves per SIMD).  Larger rings and slab lists
 // are read from global memory (as ppoly_eval does past its limits).
+#ifndef GEOHIP_CE_ABL
+#define GEOHIP_CE_ABL 0
+#endif
 #ifndef GEOHIP_CE_VERTS
 #define GEOHIP_CE_VERTS 256
 #endif
@@ -3510,8 +3541,12 @@ __global__ __launch_bounds__(kTB) void ppoly_cand_eval(CandGroup c, const PolyDe
             if (i < m) {
                 const double px = lqx[i], py = lqy[i];
                 pid = lqi[i];
+#if GEOHIP_CE_ABL  // measurement builds only: no exact tests (results wrong)
+                in = px == 1234.5;
+#else
                 in = holes ? point_polygon_within_rings(px, py, rvx, rvy, rvr, rre, P, sv, r)
                            : point_polygon_within(px, py, rvx, rvy, P, sv, r, v_lds ? lsb : nullptr);
+#endif
             }
             spairs_push<kEvalPairs>(pb, pc, in, poly, pid, o);
         }
@@ -4872,7 +4907,8 @@ struct BoxClassifier {
 bool classify_cells(const PolyDev& P, const std::vector<double>& hvx, const std::vector<double>& hvy,
                     const ring_id_t* rid, const geohip_grid& pg, const int32_t* rects, uint32_t first_c,
                     uint32_t nrect_c, uint32_t nring, double r, std::vector<uint32_t>& blob, uint32_t* off,
-                    std::vector<uint32_t>* rf = nullptr, std::vector<uint32_t>* rfw = nullptr) {
+                    std::vector<uint32_t>* rf = nullptr, std::vector<uint32_t>* rfw = nullptr,
+                    std::vector<uint32_t>* rfw2 = nullptr) {
     *off = kNoCls;
     if (!(r >= 0.0) || !std::isfinite(r) || P.wx0 > P.wx1 || P.wy0 > P.wy1 || nrect_c == 0) return false;
     BoxClassifier bc;
@@ -4923,6 +4959,7 @@ bool classify_cells(const PolyDev& P, const std::vector<double>& hvx, const std:
             if (k == kClsMiss) { out[(size_t)a * h + c] = kWordMiss; continue; }
             uint32_t word = 0;
             uint32_t rw[16];
+            uint32_t qw[16][16];  // [subcell][part]: second-level words of the mixed parts
             bool refined = false;
             for (int sx = 0; sx < 4; sx++) {
                 double sx0, sx1;
@@ -4934,15 +4971,32 @@ bool classify_cells(const PolyDev& P, const std::vector<double>& hvx, const std:
                     word |= (uint32_t)ks << (2 * (4 * sx + sy));
                     rw[4 * sx + sy] = 0u;
                     if (ks != kClsMixed || !rf) continue;
-                    // the subcell's 4 x 4 parts: [sub16 edge, next edge) clipped to the subcell
+                    // the subcell's 4 x 4 parts: [sub16 edge, next edge) clipped to the subcell; a
+                    // mixed part's 4 x 4 sub-parts likewise on the sub64 edges
                     uint32_t pw = 0;
                     for (int tx = 0; tx < 4; tx++) {
-                        const double px0 = tx == 0 ? sx0 : std::max(sx0, sub16_edge(pg.min_x, pg.cell_len, cx, 4 * sx + tx));
-                        const double px1 = tx == 3 ? sx1 : std::min(sx1, std::nextafter(sub16_edge(pg.min_x, pg.cell_len, cx, 4 * sx + tx + 1), -INFINITY));
+                        const int qx = 4 * sx + tx;
+                        const double px0 = tx == 0 ? sx0 : std::max(sx0, sub16_edge(pg.min_x, pg.cell_len, cx, qx));
+                        const double px1 = tx == 3 ? sx1 : std::min(sx1, std::nextafter(sub16_edge(pg.min_x, pg.cell_len, cx, qx + 1), -INFINITY));
                         for (int ty = 0; ty < 4; ty++) {
-                            const double py0 = ty == 0 ? sy0 : std::max(sy0, sub16_edge(pg.min_y, pg.cell_len, cy, 4 * sy + ty));
-                            const double py1 = ty == 3 ? sy1 : std::min(sy1, std::nextafter(sub16_edge(pg.min_y, pg.cell_len, cy, 4 * sy + ty + 1), -INFINITY));
-                            pw |= (uint32_t)bc(px0, px1, py0, py1) << (2 * (4 * tx + ty));
+                            const int qy = 4 * sy + ty;
+                            const double py0 = ty == 0 ? sy0 : std::max(sy0, sub16_edge(pg.min_y, pg.cell_len, cy, qy));
+                            const double py1 = ty == 3 ? sy1 : std::min(sy1, std::nextafter(sub16_edge(pg.min_y, pg.cell_len, cy, qy + 1), -INFINITY));
+                            const uint8_t kp = bc(px0, px1, py0, py1);
+                            pw |= (uint32_t)kp << (2 * (4 * tx + ty));
+                            uint32_t w2 = 0;
+                            if (kp == kClsMixed)
+                                for (int ux = 0; ux < 4; ux++) {
+                                    const double qx0 = ux == 0 ? px0 : std::max(px0, sub64_edge(pg.min_x, pg.cell_len, cx, 4 * qx + ux));
+                                    const double qx1 = ux == 3 ? px1 : std::min(px1, std::nextafter(sub64_edge(pg.min_x, pg.cell_len, cx, 4 * qx + ux + 1), -INFINITY));
+                                    for (int uy = 0; uy < 4; uy++) {
+                                        const double qy0 = uy == 0 ? py0 : std::max(py0, sub64_edge(pg.min_y, pg.cell_len, cy, 4 * qy + uy));
+                                        const double qy1 = uy == 3 ? py1 : std::min(py1, std::nextafter(sub64_edge(pg.min_y, pg.cell_len, cy, 4 * qy + uy + 1), -INFINITY));
+                                        w2 |= (uint32_t)bc(qx0, qx1, qy0, qy1) << (2 * (4 * ux + uy));
+                                    }
+                                }
+                            qw[4 * sx + sy][4 * tx + ty] = w2;
+                            refined = refined || w2 != 0u;  // some sub-part decided
                         }
                     }
                     rw[4 * sx + sy] = pw;
@@ -4952,10 +5006,16 @@ bool classify_cells(const PolyDev& P, const std::vector<double>& hvx, const std:
             out[(size_t)a * h + c] = word;
             if (refined) {
                 const size_t at = 2 * (base + (size_t)a * h + c);
-                (*rf)[at] = (uint32_t)rfw->size();
+                (*rf)[at] = (uint32_t)(rfw->size() / 2);
                 (*rf)[at + 1] = word;
-                for (int q = 0; q < 16; q++)
-                    if ((refine_mixed(word) >> (2 * q)) & 1u) rfw->push_back(rw[q]);
+                for (int q = 0; q < 16; q++) {
+                    if (!((refine_mixed(word) >> (2 * q)) & 1u)) continue;
+                    const uint32_t pw = rw[q];
+                    rfw->push_back(pw);
+                    rfw->push_back(refine_mixed(pw) ? (uint32_t)rfw2->size() : kNoRefine);
+                    for (int t = 0; t < 16; t++)
+                        if ((refine_mixed(pw) >> (2 * t)) & 1u) rfw2->push_back(qw[q][t]);
+                }
             }
         }
     }
@@ -5014,7 +5074,8 @@ struct PolyCache {
     std::vector<uint16_t> hslab;
     std::vector<uint32_t> hcls;  // per-cell class words (classify_cells), PolyDev.cls offsets into it
     std::vector<uint32_t> hrf;   // 2 per hcls cell: first refinement word (or kNoRefine), class word
-    std::vector<uint32_t> hrfw;  // refinement words (one per mixed subcell of a refined cell)
+    std::vector<uint32_t> hrfw;  // 2 per mixed subcell of a refined cell: part word, first second-level word
+    std::vector<uint32_t> hrfw2; // second-level words (one per mixed part of those subcells)
     std::vector<uint32_t> keep;  // cells of any polygon's G or C rectangles (empty: no filter)
     bool any_outside = false;
     // streaming path (ppoly_stream): per key cell its polygon entries, the cells holding any
@@ -5271,7 +5332,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
         // 3000 polygons), each into its own tables, then concatenated in polygon order
         if (!approximate && npoly) {
             struct Cls {
-                std::vector<uint32_t> blob, rf, rfw;
+                std::vector<uint32_t> blob, rf, rfw, rfw2;
                 uint32_t off = kNoCls;
             };
             std::vector<Cls> part(npoly);
@@ -5280,7 +5341,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
                 for (uint32_t p; (p = next.fetch_add(1)) < npoly;) {
                     const PolyDev& P = pd[p];
                     classify_cells(P, hvx, hvy, P.nring > 1 ? fresh.hvr.data() + P.voff : nullptr, *grid, hrects.data(),
-                                   P.coff, P.nc, P.nring, r, part[p].blob, &part[p].off, &part[p].rf, &part[p].rfw);
+                                   P.coff, P.nc, P.nring, r, part[p].blob, &part[p].off, &part[p].rf, &part[p].rfw, &part[p].rfw2);
                 }
             };
             const unsigned nth = std::min<unsigned>(std::max(1u, std::min(std::thread::hardware_concurrency(), 16u)),
@@ -5292,14 +5353,18 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             for (uint32_t p = 0; p < npoly; p++) {
                 Cls& q = part[p];
                 if (q.off == kNoCls) continue;
-                const uint32_t wbase = (uint32_t)fresh.hrfw.size();
+                const uint32_t wbase = (uint32_t)(fresh.hrfw.size() / 2), w2base = (uint32_t)fresh.hrfw2.size();
                 pd[p].cls = (uint32_t)fresh.hcls.size();
                 fresh.hcls.insert(fresh.hcls.end(), q.blob.begin(), q.blob.end());
                 for (size_t k = 0; k < q.rf.size(); k += 2) {  // (first word, class word) pairs
                     fresh.hrf.push_back(q.rf[k] == kNoRefine ? kNoRefine : q.rf[k] + wbase);
                     fresh.hrf.push_back(q.rf[k + 1]);
                 }
-                fresh.hrfw.insert(fresh.hrfw.end(), q.rfw.begin(), q.rfw.end());
+                for (size_t k = 0; k < q.rfw.size(); k += 2) {  // (part word, first second-level word) pairs
+                    fresh.hrfw.push_back(q.rfw[k]);
+                    fresh.hrfw.push_back(q.rfw[k + 1] == kNoRefine ? kNoRefine : q.rfw[k + 1] + w2base);
+                }
+                fresh.hrfw2.insert(fresh.hrfw2.end(), q.rfw2.begin(), q.rfw2.end());
                 std::vector<uint32_t>().swap(q.blob);
             }
         }
@@ -5386,7 +5451,8 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     const size_t off_op = (off_sk + sz_sk + 15) & ~(size_t)15, sz_op = pc->opoly.size() * 4;
     const size_t off_rf = (off_op + sz_op + 15) & ~(size_t)15, sz_rf = pc->hrf.size() * 4;
     const size_t off_rw = (off_rf + sz_rf + 15) & ~(size_t)15, sz_rw = pc->hrfw.size() * 4;
-    const size_t blob_end = off_rw + sz_rw;
+    const size_t off_r2 = (off_rw + sz_rw + 15) & ~(size_t)15, sz_r2 = pc->hrfw2.size() * 4;
+    const size_t blob_end = off_r2 + (sz_r2 ? sz_r2 : 16);  // >= one readable word (unconditional gathers)
     void* pblob = nullptr;
     rc = ctx_ensure(ctx, J_POLY, blob_end + 64, &pblob);
     if (rc) return rc;
@@ -5407,7 +5473,8 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
     unsigned* dskeep = reinterpret_cast<unsigned*>(bp + off_sk);
     uint32_t* dopoly = reinterpret_cast<uint32_t*>(bp + off_op);
     uint2* drf = reinterpret_cast<uint2*>(bp + off_rf);
-    uint32_t* drfw = reinterpret_cast<uint32_t*>(bp + off_rw);
+    uint2* drfw = reinterpret_cast<uint2*>(bp + off_rw);
+    uint32_t* drfw2 = reinterpret_cast<uint32_t*>(bp + off_r2);
     if (upload) {
         pc->dev_blob = nullptr;  // until the copies are issued
         if ((sz_p && hipMemcpyAsync(dpoly, pd.data(), sz_p, hipMemcpyHostToDevice, st) != hipSuccess) ||
@@ -5425,7 +5492,8 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             (sz_sk && hipMemcpyAsync(dskeep, pc->skeep.data(), sz_sk, hipMemcpyHostToDevice, st) != hipSuccess) ||
             (sz_op && hipMemcpyAsync(dopoly, pc->opoly.data(), sz_op, hipMemcpyHostToDevice, st) != hipSuccess) ||
             (sz_rf && hipMemcpyAsync(drf, pc->hrf.data(), sz_rf, hipMemcpyHostToDevice, st) != hipSuccess) ||
-            (sz_rw && hipMemcpyAsync(drfw, pc->hrfw.data(), sz_rw, hipMemcpyHostToDevice, st) != hipSuccess))
+            (sz_rw && hipMemcpyAsync(drfw, pc->hrfw.data(), sz_rw, hipMemcpyHostToDevice, st) != hipSuccess) ||
+            (sz_r2 && hipMemcpyAsync(drfw2, pc->hrfw2.data(), sz_r2, hipMemcpyHostToDevice, st) != hipSuccess))
             return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "polygon upload failed");
         pc->dev_blob = pblob;
         pc->blob_bytes = blob_end;
@@ -5532,6 +5600,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
                     cr.polys = dpoly;
                     cr.rf = drf;
                     cr.rfw = drfw;
+                    cr.rfw2 = drfw2;
                     cr.mnx = grid->min_x;
                     cr.mny = grid->min_y;
                     cr.l = grid->cell_len;
@@ -5568,6 +5637,9 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
                         std::chrono::duration<double, std::micro>(t_planned - t_start).count(), (int)cached,
                         (size_t)std::count_if(pc->hrf.begin(), pc->hrf.end(), [](uint32_t v) { return v != kNoRefine; }) / 2,
                         pc->hcls.size());
+            if (prof && attempt == 0)
+                fprintf(stderr, "ppoly host: refinement words %zu (parts) + %zu (sub-parts)\n", pc->hrfw.size() / 2,
+                        pc->hrfw2.size());
             if (prof) fprintf(stderr, "ppoly stream: %llu pairs, %llu candidates (capacity %llu), %u of %llu chunks re-run\n",
                               (unsigned long long)tot, (unsigned long long)ncand, (unsigned long long)ccap, (unsigned)(pin[2] >> 32),
                               (unsigned long long)nchunks);

@@ -319,26 +319,27 @@ def test_ppoly_cell_class_box_edges(ctx, holes):
 @pytest.mark.parametrize("holes", [False, True])
 def test_ppoly_refinement_part_edges(ctx, holes):
     """The candidate refinement (ppoly_cand_refine) decides a mixed subcell's candidates by the
-    4 x 4 parts the host classified (sub16_edge: min + (c + j / 16) * l): points at every part
-    edge double and the double below it, both axes, around each polygon (the parts straddling its
+    4 x 4 parts the host classified (sub16_edge: min + (c + j / 16) * l) and a mixed part's by its
+    4 x 4 sub-parts (sub64_edge: min + (c + j / 64) * l): points at every part and sub-part edge
+    double and the double below it, both axes, around each polygon (the parts straddling its
     boundary and its r-contour), for the range query and the exact join, against the oracle."""
     n = 500
     l = (BJ[1] - BJ[0]) / n
     ag, cg = agrid(n)
     if holes:
-        pr, off, vx, vy, _ = synth.holed_polygons(6, 95)
+        pr, off, vx, vy, _ = synth.holed_polygons(4, 95)
         rings = [(int(off[pr[p]]), int(off[pr[p + 1]])) for p in range(len(pr) - 1)]
     else:
         pr = None
-        off, vx, vy = synth.star_polygons(10, 94)
+        off, vx, vy = synth.star_polygons(6, 94)
         rings = [(int(off[p]), int(off[p + 1])) for p in range(len(off) - 1)]
 
     def part_edges(lo, a, b):
         k0, k1 = int(math.floor((a - lo) / l)) - 1, int(math.floor((b - lo) / l)) + 2
         out = []
         for k in range(max(k0, 0), min(k1, n)):
-            for j in range(1, 16):
-                v = lo + (k + 0.0625 * j) * l
+            for j in range(1, 64):
+                v = lo + (k + 0.015625 * j) * l
                 out += [v, np.nextafter(v, -np.inf)]
         return np.array(out)
 
@@ -346,10 +347,10 @@ def test_ppoly_refinement_part_edges(ctx, holes):
     for a, b in rings:
         sx = part_edges(BJ[0], vx[a:b].min() - 0.013, vx[a:b].max() + 0.013)
         sy = part_edges(BJ[2], vy[a:b].min() - 0.013, vy[a:b].max() + 0.013)
-        # every part edge of x against a thinned set of y edges, and the reverse (the full cross
-        # product of one polygon is ~2.5e5 points)
-        gx, gy = np.meshgrid(sx, sy[::7], indexing="ij")
-        hx, hy = np.meshgrid(sx[::7], sy, indexing="ij")
+        # every edge double of x against a thinned set of the y ones, and the reverse (the full
+        # cross product of one polygon is ~5e6 points)
+        gx, gy = np.meshgrid(sx, sy[::31], indexing="ij")
+        hx, hy = np.meshgrid(sx[::31], sy, indexing="ij")
         px += [gx.ravel(), hx.ravel()]
         py += [gy.ravel(), hy.ravel()]
     x, y = np.concatenate(px), np.concatenate(py)
