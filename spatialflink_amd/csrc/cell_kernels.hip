@@ -3464,11 +3464,13 @@ __global__ __launch_bounds__(kTB) void ppoly_cand_eval(CandGroup c, const PolyDe
     unsigned pc = 0;
     const unsigned ni = *c.nitems;
     __shared__ unsigned s_it;
-    for (;;) {
-        // items claimed in order from a ticket: a block done with a short item takes the next
-        // (a static stride gave the blocks with two long items the whole pass's tail)
+    for (bool first = true;; first = false) {
+        // items claimed in order: block b's first is item b, the rest from a ticket -- a block
+        // done with a short item takes the next (a static stride gave the blocks with two long
+        // items the whole pass's tail; a ticket for the first items too queued every block's
+        // start behind one counter)
         __syncthreads();  // the previous item's LDS reads are done
-        if (threadIdx.x == 0) s_it = atomicAdd(c.eticket, 1u);
+        if (threadIdx.x == 0) s_it = first ? blockIdx.x : gridDim.x + atomicAdd(c.eticket, 1u);
         __syncthreads();
         const unsigned it = (unsigned)__builtin_amdgcn_readfirstlane((int)s_it);
         if (it >= ni) break;
