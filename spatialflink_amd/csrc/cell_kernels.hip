@@ -1487,9 +1487,9 @@ __global__ __launch_bounds__(kTB) void join_fused(JoinRun a) {
     const unsigned gq = *a.gcnt;
     const TileGeom& g = a.geo;
     const double slack = 0x1.0p-30 * (__builtin_fabs(g.mnx) + __builtin_fabs(g.mny) + ((double)g.nb + 2.0) * g.l);
-    for (;;) {
-        if (threadIdx.x == 0) {
-            sh_item = atomicAdd(a.ticket, 1u);
+    for (bool first = true;; first = false) {
+        if (threadIdx.x == 0) {  // the block's first item by its index, the rest from the ticket
+            sh_item = first ? blockIdx.x : gridDim.x + atomicAdd(a.ticket, 1u);
             sh_amax = 0;
         }
         __syncthreads();
