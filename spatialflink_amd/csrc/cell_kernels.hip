@@ -1285,14 +1285,16 @@ __global__ __launch_bounds__(kJbL2Threads) void jb_tiles(JBin a) {
 // puts the true d2 below r2lo (above r2hi), where the fp64 screens already decide (kSqLo/kSqHi).
 constexpr unsigned kJCh = kJP / kWave / (kTB / kWave);  // chunks per wave and item
 #ifndef GEOHIP_JBLOCKSW
-#define GEOHIP_JBLOCKSW 768
+#define GEOHIP_JBLOCKSW 1280
 #endif
 #ifndef GEOHIP_JSTAGE
-#define GEOHIP_JSTAGE 768
+#define GEOHIP_JSTAGE 352
 #endif
-// persistent grid of the write pass: 45 KB of LDS with 768-pair stages, 3 blocks per CU.  C3 kernel
-// sums, one box: stage 512 at 4 blocks per CU 1278 us; 640 / 768 / 896 at 3: 1265 / 1262 / 1262;
-// 1024 at 2: 1360; 320 at 5: 1333
+// persistent grid of the write pass: 31.2 KB of LDS with 352-pair stages, 5 blocks per CU (89
+// VGPRs allow 5 waves per SIMD).  C3 kernel sums, one box, round 4 (nontemporal pair stores):
+// stage 512 at 4 blocks per CU 1278 us; 640 / 768 / 896 at 3: 1265 / 1262 / 1262; 1024 at 2: 1360;
+// 320 at 5: 1333.  Round 5, plain stores (same box, 2 reps): 768 at 3: 1176-1184; 512 at 4:
+// 1081-1089; 448 at 4: 1078-1091; 352 at 5: 1066-1067 -- with cached stores occupancy beats runs
 constexpr unsigned kJBlocksW = GEOHIP_JBLOCKSW;
 constexpr unsigned kJBlocksC = 1280;  // count pass (4 KB LDS, 83 VGPRs: 5 blocks per CU)
 
