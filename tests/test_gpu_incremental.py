@@ -101,11 +101,12 @@ def test_incremental_ppoly_equals_full_window(ctx):
         assert pairs_sorted(got).tolist() == pairs_sorted(want).tolist()
 
 
-@pytest.mark.parametrize("p,k", [(16, 40), (5, 300), (2, 2000)])
+@pytest.mark.parametrize("p,k", [(16, 40), (5, 300), (2, 2000), (3, 1500)])
 def test_pane_merge_many_panes(ctx, p, k):
     """geohip_knn_merge_panes_async over up to 16 panes of a ring (slots rotating, ties across
     panes, panes with fewer candidates than k, the large-k pane pass): every window equals the
-    kNN of the window's concatenated panes."""
+    kNN of the window's concatenated panes.  p k <= 4096 takes the one-workgroup LDS merge, (3,
+    1500) the global one."""
     import torch
     ag, cg = grids(100)
     rng = np.random.default_rng(p * 31 + k)
