@@ -3317,7 +3317,13 @@ struct CandRefine {
 // about one per block (per-wave stages flushed every ~128 pairs cost 83 of the kernel's 148 us
 // for C4: same-address atomics); kRefinePer candidates per thread per round keep their gather
 // chains (slot -> polygon -> refinement base -> word) in flight together.
-constexpr unsigned kRefineBlocks = 1024, kRefinePer = 4, kRefineStage = 4096;
+#ifndef GEOHIP_RF_BLOCKS
+#define GEOHIP_RF_BLOCKS 1024
+#endif
+#ifndef GEOHIP_RF_STAGE
+#define GEOHIP_RF_STAGE 4096
+#endif
+constexpr unsigned kRefineBlocks = GEOHIP_RF_BLOCKS, kRefinePer = 4, kRefineStage = GEOHIP_RF_STAGE;
 __global__ __launch_bounds__(kTB) void ppoly_cand_refine(CandRefine c, StreamOut o) {
     __shared__ uint2 stage[kRefineStage];
     __shared__ unsigned s_n;
@@ -4063,11 +4069,15 @@ __global__ __launch_bounds__(1024) void rsel_small(const unsigned long long* __r
         }
     };
     bool pre = false;  // keys below the round-0 digit were selected outright (LDS-only rounds)
+    bool andor_ok = false;  // s_and_* / s_or_* hold the current matching set's AND / OR (block-uniform)
     for (int round = 0; round < kRselRounds && !all; round++) {
         int field, shift, width;
         rsel_round(round, field, shift, width);
         const unsigned dm = (1u << width) - 1u;
-        if (round > 0 && s_lds) {
+        if (round > 0 && s_lds && andor_ok) {
+            // the matching set is unchanged since the last AND/OR pass: its digits of this round
+            // are already known (uniform -> taken below without a pass)
+        } else if (round > 0 && s_lds) {
             // a round whose digit every matching key shares decides nothing: take it without a
             // histogram (keys at distance 0 inside the polygon skip all the distance rounds)
             if (t == 0) {
@@ -4099,6 +4109,9 @@ __global__ __launch_bounds__(1024) void rsel_small(const unsigned long long* __r
                 atomicOr(&s_or_i, oi);
             }
             __syncthreads();
+            andor_ok = true;
+        }
+        if (round > 0 && s_lds) {
             const unsigned a = field == 0 ? (unsigned)(s_and_d >> shift) & dm : (s_and_i >> shift) & dm;
             const unsigned b = field == 0 ? (unsigned)(s_or_d >> shift) & dm : (s_or_i >> shift) & dm;
             __syncthreads();
@@ -4116,6 +4129,7 @@ __global__ __launch_bounds__(1024) void rsel_small(const unsigned long long* __r
                 continue;
             }
         }
+        andor_ok = false;  // a histogram round narrows the matching set
         if (round == 0) {  // the producers' histogram (ppknn_dist) of the round-0 digits
             for (int b = t; b < kRselBins; b += 1024) h[b] = st->hist0[b];
         } else {
