@@ -2560,7 +2560,10 @@ __device__ __forceinline__ void stream_push(const StreamArgs& a, StreamSink& k, 
 // iteration that exceeds either takes the per-lane walk.
 constexpr unsigned kBalRecs = 128;
 constexpr unsigned kBalWords = 16;
-constexpr unsigned kBalItems = 4;
+#ifndef GEOHIP_PS_BALITEMS
+#define GEOHIP_PS_BALITEMS 2  // entries per lane per balanced step (same box: 1 450, 2 448, 3 457, 4 463, 6 479 us)
+#endif
+constexpr unsigned kBalItems = GEOHIP_PS_BALITEMS;
 
 // the class decision of one entry (ex, word) for a point with subcell / NaN bits sw:
 // PointPolygonRangeQuery.java:105-121 -- G -> pair; C -> by the subcell class (mixed: candidate)
