@@ -3326,7 +3326,10 @@ struct CandRefine {
 #ifndef GEOHIP_RF_STAGE
 #define GEOHIP_RF_STAGE 4096
 #endif
-constexpr unsigned kRefineBlocks = GEOHIP_RF_BLOCKS, kRefinePer = 4, kRefineStage = GEOHIP_RF_STAGE;
+#ifndef GEOHIP_RF_PER
+#define GEOHIP_RF_PER 4
+#endif
+constexpr unsigned kRefineBlocks = GEOHIP_RF_BLOCKS, kRefinePer = GEOHIP_RF_PER, kRefineStage = GEOHIP_RF_STAGE;
 __global__ __launch_bounds__(kTB) void ppoly_cand_refine(CandRefine c, StreamOut o) {
     __shared__ uint2 stage[kRefineStage];
     __shared__ unsigned s_n;
