@@ -842,7 +842,7 @@ __global__ void jq_global(uint64_t nq, unsigned* __restrict__ glist, unsigned* _
 constexpr unsigned kJbSub = 4096;     // points per local sort round (4 per thread)
 constexpr unsigned kJbBlocks = 256;   // level-1 blocks
 #ifndef GEOHIP_JB_ROUND
-#define GEOHIP_JB_ROUND 2048
+#define GEOHIP_JB_ROUND 1024  // records per level-2 round (same box, round 5: 512 118, 1024 92, 2048 109 us of jb_tiles)
 #endif
 #ifndef GEOHIP_JB_L2BLOCKS
 #define GEOHIP_JB_L2BLOCKS 1024

@@ -3,7 +3,8 @@ tests do not (PointPointJoinQuery.java:113-172, JoinQuery.java:73-90).
 
 Round 4's full-scale C3 test once failed with the right pair count and the wrong digest while
 every smaller join test passed: the window sizes of those tests never reach
-  * tiles with more than one level-2 round of records (kJbRound = 2048 records per round),
+  * tiles with more than one level-2 round of records (kJbRound = 1024 records per round; the
+    asserts below ask for tiles over 2048, several rounds at either setting),
   * bands whose records come from more than one window of segments in jb_tiles (a band has one
     segment per level-1 sub-chunk holding its points; jb_tiles reads kWin = 512 of them at a
     time, and a window has 4096-point sub-chunks, so only windows above ~2.1M points have
