@@ -1031,8 +1031,14 @@ __device__ __forceinline__ unsigned block_scan_passes(unsigned n, unsigned* wsum
 
 // Tile starts and cursors from the tile counts, then the join's item starts from the same counts
 // and the query list starts (one block; was a separate join_plan launch).
-constexpr unsigned kJP = 1024;      // points per join work item (4 waves x 4 chunks of 64)
-constexpr unsigned kJQ = 128;       // queries per join work item
+#ifndef GEOHIP_JP
+#define GEOHIP_JP 1024
+#endif
+#ifndef GEOHIP_JQ
+#define GEOHIP_JQ 128
+#endif
+constexpr unsigned kJP = GEOHIP_JP;  // points per join work item (4 waves x 4 chunks of 64)
+constexpr unsigned kJQ = GEOHIP_JQ;  // queries per join work item
 __global__ __launch_bounds__(kBinThreads) void jb_scan(JBin a) {
     __shared__ unsigned wsum[kScanPasses * (kBinThreads / kWave)];
     __shared__ unsigned sitems[kMaxTiles];  // item counts, formed while the tile counts load
