@@ -844,6 +844,18 @@ constexpr unsigned kJbBlocks = 256;   // level-1 blocks
 #ifndef GEOHIP_JB_ROUND
 #define GEOHIP_JB_ROUND 1024  // records per level-2 round (same box, round 5: 512 118, 1024 92, 2048 109 us of jb_tiles)
 #endif
+#ifndef GEOHIP_JB_L1NT
+#define GEOHIP_JB_L1NT 0  // measurement builds only: level-1 records stored nontemporally
+#endif
+#ifndef GEOHIP_JB_TNT
+#define GEOHIP_JB_TNT 2  // jb_tiles' record loads (1, measurement builds) / stores (2) nontemporal.  Same
+                         // box, 2 reps: stores 2 -> C3 kernels 1034-1040 -> 1013-1016 us (jb_tiles 95 -> 87,
+                         // join_fused 813 -> 800); loads 1 -> 1039-1042 (no gain)
+#endif
+#ifndef GEOHIP_JB_XNT
+#define GEOHIP_JB_XNT 1  // the window read nontemporally by jb_bands (same box, 2 reps: jb_bands 92.7 -> 72.6
+                         // us, C3 kernels 1042-1050 -> 1029-1040 us; records also nontemporal: jb_tiles 91 -> 123)
+#endif
 #ifndef GEOHIP_JB_L2BLOCKS
 #define GEOHIP_JB_L2BLOCKS 1024
 #endif
@@ -929,8 +941,13 @@ __global__ __launch_bounds__(kBinThreads) void jb_bands(JBin a) {
         for (int k = 0; k < PPT; k++) {
             const uint64_t i = sb + threadIdx.x + (uint64_t)k * kBinThreads;
             const uint64_t ic = i < b1 ? i : b1 - 1;
+#if GEOHIP_JB_XNT  // read once here (join_fused reads the records): past the caches
+            nx[k] = __builtin_nontemporal_load(a.x + ic);
+            ny[k] = __builtin_nontemporal_load(a.y + ic);
+#else
             nx[k] = a.x[ic];
             ny[k] = a.y[ic];
+#endif
         }
     };
     if (b0 < b1) fetch(b0);
@@ -969,7 +986,16 @@ __global__ __launch_bounds__(kBinThreads) void jb_bands(JBin a) {
 #pragma unroll
         for (int k = 0; k < PPT; k++) {
             const unsigned j = threadIdx.x + k * kBinThreads;
-            if (j < kept) a.l1[sb + j] = st[j];
+            if (j < kept) {
+#if GEOHIP_JB_L1NT
+                typedef unsigned u4v __attribute__((ext_vector_type(4)));
+                const uint4 r = st[j];
+                u4v v = {r.x, r.y, r.z, r.w};
+                __builtin_nontemporal_store(v, reinterpret_cast<u4v*>(a.l1 + sb + j));
+#else
+                a.l1[sb + j] = st[j];
+#endif
+            }
         }
         lds_barrier();
         for (unsigned t = threadIdx.x; t < nbins; t += kBinThreads) lh[t] = 0;
@@ -1224,7 +1250,15 @@ __global__ __launch_bounds__(kJbL2Threads) void jb_tiles(JBin a) {
             }
             uint4 got[PPT];
 #pragma unroll
-            for (int k = 0; k < PPT; k++) got[k] = a.l1[src[k]];  // unconditional (src 0 when none): no branch per load
+            for (int k = 0; k < PPT; k++) {  // unconditional (src 0 when none): no branch per load
+#if GEOHIP_JB_TNT & 1  // measurement builds: level-1 records read nontemporally
+                typedef unsigned u4v __attribute__((ext_vector_type(4)));
+                const u4v g = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(a.l1 + src[k]));
+                got[k] = make_uint4(g.x, g.y, g.z, g.w);
+#else
+                got[k] = a.l1[src[k]];
+#endif
+            }
 #pragma unroll
             for (int k = 0; k < PPT; k++) {
                 rec[k].x = has[k] ? got[k].x : rec[k].x;  // selects, not stores under a branch (kept in VGPRs)
@@ -1259,7 +1293,13 @@ __global__ __launch_bounds__(kJbL2Threads) void jb_tiles(JBin a) {
                 const uint4 q = st[j];
                 const unsigned bq = (q.w >> 20) & (kBandTiles - 1);
                 const unsigned p = base[bq] + (j - ls[bq]);
+#if GEOHIP_JB_TNT & 2  // measurement builds: tile-sorted records stored nontemporally
+                typedef unsigned u4v __attribute__((ext_vector_type(4)));
+                u4v v = {q.x, q.y, q.z, q.w};
+                if (p < a.n && !(GEOHIP_JB_ABL & 1)) __builtin_nontemporal_store(v, reinterpret_cast<u4v*>(a.recs + p));
+#else
                 if (p < a.n && !(GEOHIP_JB_ABL & 1)) a.recs[p] = q;  // bounded even if the counts were not the binning's own
+#endif
             }
         }
         lds_barrier();
