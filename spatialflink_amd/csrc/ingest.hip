@@ -384,20 +384,31 @@ __device__ __forceinline__ unsigned stage_chunk(const uint8_t* __restrict__ text
     return nrec;
 }
 
+#ifndef GEOHIP_ING_NTST
+#define GEOHIP_ING_NTST 0  // measurement builds: the record columns stored nontemporally
+#endif
+template <typename T>
+__device__ __forceinline__ void col_store(T* p, T v) {
+#if GEOHIP_ING_NTST
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
 __device__ __forceinline__ void store_record(const IngestArgs& a, uint64_t idx, const ingest::Parsed& o,
                                              double* __restrict__ x, double* __restrict__ y,
                                              int64_t* __restrict__ ts, uint32_t* __restrict__ cell) {
-    x[idx] = o.x;
-    y[idx] = o.y;
-    if (ts) ts[idx] = o.ts;
-    if (a.oid) a.oid[idx] = o.oid;
+    col_store(x + idx, o.x);
+    col_store(y + idx, o.y);
+    if (ts) col_store(ts + idx, (int64_t)o.ts);
+    if (a.oid) col_store(a.oid + idx, o.oid);
     if (cell && a.pad == 3) {
-        cell[idx] = 0u;
+        col_store(cell + idx, 0u);
     } else if (cell) {
         const int32_t cx = ingest::java_cell(o.x, a.min_x, a.cell_len);
         const int32_t cy = ingest::java_cell(o.y, a.min_y, a.cell_len);
         const bool ok = cx >= 0 && cx < a.n && cy >= 0 && cy < a.n;
-        cell[idx] = ok ? (uint32_t)cx * (uint32_t)a.n + (uint32_t)cy : 0xffffffffu;
+        col_store(cell + idx, ok ? (uint32_t)cx * (uint32_t)a.n + (uint32_t)cy : 0xffffffffu);
     }
 }
 
