@@ -13,7 +13,7 @@ for w in ${WORKLOADS:-knn range c5 join ppoly ingest ppjoin ppknn knn_incr ppoly
     echo "pmc $w $c ok"
   done
 done
-for w in ${FP64_WORKLOADS:-ppoly ppjoin ppknn ppoly_incr}; do
+for w in ${FP64_WORKLOADS-ppoly ppjoin ppknn ppoly_incr}; do
   timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_FP64 --output-format csv -d gpurun_out/pmc -o ${w}_SQ_INSTS_VALU_FLOPS_FP64 -- \
       python3 bench.py --workload "$w" --steps 5 --warmup 1 --no-cpu-baseline --no-e2e --no-pipelined --no-cells-line \
       > gpurun_out/pmc/${w}_fp64.log 2>&1 || { echo "pmc fp64 $w failed"; tail -20 gpurun_out/pmc/${w}_fp64.log; exit 5; }

@@ -36,16 +36,30 @@ struct WaveStage {  // wave-private LDS
     unsigned ci[kCandCap];
 };
 
+#ifndef GEOHIP_L4_NT
+#define GEOHIP_L4_NT 0
+#endif
+#ifndef GEOHIP_KP_NT
+#define GEOHIP_KP_NT 1  // knn_pass: the window read nontemporally (same box, 3 reps: C5 92-93 -> 84 us, C2 40.2-41.3 -> 38.4-38.7 us)
+#endif
 __device__ __forceinline__ void load4(const double* __restrict__ x, const double* __restrict__ y,
                                       uint64_t base, uint64_t end, int lane, double px[4], double py[4],
                                       bool valid[4]) {
     const uint64_t i0 = base + 2 * (uint64_t)lane;
     const uint64_t i1 = base + 128 + 2 * (uint64_t)lane;
     if (base + kPtsIter <= end) {
+#if GEOHIP_L4_NT  // measurement builds: the window read nontemporally (range passes)
+        typedef double d2v __attribute__((ext_vector_type(2)));
+        const d2v a = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(x + i0));
+        const d2v b = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(x + i1));
+        const d2v c = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(y + i0));
+        const d2v d = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(y + i1));
+#else
         const double2 a = *reinterpret_cast<const double2*>(x + i0);
         const double2 b = *reinterpret_cast<const double2*>(x + i1);
         const double2 c = *reinterpret_cast<const double2*>(y + i0);
         const double2 d = *reinterpret_cast<const double2*>(y + i1);
+#endif
         px[0] = a.x; px[1] = a.y; px[2] = b.x; px[3] = b.y;
         py[0] = c.x; py[1] = c.y; py[2] = d.x; py[3] = d.y;
         valid[0] = valid[1] = valid[2] = valid[3] = true;
@@ -1314,10 +1328,18 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
     auto is_full = [&](unsigned it) { return it_base(it) + kPtsIter <= blk_end; };
     auto load_full = [&](unsigned it, double (&px)[4], double (&py)[4]) {
         const uint64_t i0 = it_base(it) + 2 * (uint64_t)lane;
+#if GEOHIP_KP_NT  // read once (candidates keep their coordinates in LDS): past the caches
+        typedef double d2v __attribute__((ext_vector_type(2)));
+        const d2v u0 = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(x + i0));
+        const d2v u1 = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(x + i0 + 128));
+        const d2v v0 = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(y + i0));
+        const d2v v1 = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(y + i0 + 128));
+#else
         const double2 u0 = *reinterpret_cast<const double2*>(x + i0);
         const double2 u1 = *reinterpret_cast<const double2*>(x + i0 + 128);
         const double2 v0 = *reinterpret_cast<const double2*>(y + i0);
         const double2 v1 = *reinterpret_cast<const double2*>(y + i0 + 128);
+#endif
         px[0] = u0.x; px[1] = u0.y; px[2] = u1.x; px[3] = u1.y;
         py[0] = v0.x; py[1] = v0.y; py[2] = v1.x; py[3] = v1.y;
     };
