@@ -3737,6 +3737,10 @@ __global__ __launch_bounds__(kTB) void ppknn_scan(const double* __restrict__ x, 
 // G u C rects as exact coordinate boxes (planner: rect_to_box), classification by compares
 constexpr int kPpBoxes = kMaxPointBoxes + 1;  // a point plan's G u C boxes fit too
 constexpr unsigned kPpBuf = 1024;  // wave-private candidate buffer (u32 window indices)
+#ifndef GEOHIP_PPK_NT
+#define GEOHIP_PPK_NT 1  // ppknn_scan_boxes: the window read nontemporally (same box, 3 reps: scan 184 -> 170 us,
+                          // kernels 250-251 -> 238 us)
+#endif
 struct PpknnBoxes {
     Box b[kPpBoxes];
     int32_t nb, pad;
@@ -3807,10 +3811,20 @@ __global__ __launch_bounds__(kTB) void ppknn_scan_boxes(const double* __restrict
     };
     auto load_full = [&](uint64_t it, double2 v[4]) {
         const uint64_t i0 = it * 256 + 2 * (uint64_t)lane;
+#if GEOHIP_PPK_NT  // read once here (ppknn_dist gathers only the candidates): past the caches
+        typedef double d2v __attribute__((ext_vector_type(2)));
+        const uint64_t io[4] = {i0, i0 + 128, i0, i0 + 128};
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const d2v w = __builtin_nontemporal_load(reinterpret_cast<const d2v*>((u < 2 ? x : y) + io[u]));
+            v[u] = make_double2(w.x, w.y);
+        }
+#else
         v[0] = *reinterpret_cast<const double2*>(x + i0);
         v[1] = *reinterpret_cast<const double2*>(x + i0 + 128);
         v[2] = *reinterpret_cast<const double2*>(y + i0);
         v[3] = *reinterpret_cast<const double2*>(y + i0 + 128);
+#endif
     };
     uint64_t it = (uint64_t)blockIdx.x * per + wid;
     double2 cur[4], nxt[4];
