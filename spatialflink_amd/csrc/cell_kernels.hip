@@ -1330,6 +1330,9 @@ __global__ __launch_bounds__(kJbL2Threads) void jb_tiles(JBin a) {
 // |dx' - dx| <= e = 2.05 u A, so |d2' - d2| <= 4 e A + 2 e^2 + 3 u d2'.  d2' below lo (above hi)
 // puts the true d2 below r2lo (above r2hi), where the fp64 screens already decide (kSqLo/kSqHi).
 constexpr unsigned kJCh = kJP / kWave / (kTB / kWave);  // chunks per wave and item
+#ifndef GEOHIP_JR_NT
+#define GEOHIP_JR_NT 0
+#endif
 #ifndef GEOHIP_JBLOCKSW
 #define GEOHIP_JBLOCKSW 1280
 #endif
@@ -1662,7 +1665,15 @@ __global__ __launch_bounds__(kTB) void join_fused(JoinRun a) {
             const unsigned c = (unsigned)wid + k * (kTB / kWave);
             const unsigned i = ds + c * 64 + (unsigned)lane;
             rk[k] = make_uint4(0u, 0u, 0u, 0u);
+#if GEOHIP_JR_NT  // measurement builds: the records read nontemporally
+            typedef unsigned u4v __attribute__((ext_vector_type(4)));
+            if (c < nch && i < de) {
+                const u4v g = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(a.recs + i));
+                rk[k] = make_uint4(g.x, g.y, g.z, g.w);
+            }
+#else
             if (c < nch && i < de) rk[k] = a.recs[i];
+#endif
         }
 #pragma unroll
         for (unsigned k = 0; k < kJCh; k++) {
