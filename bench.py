@@ -322,11 +322,30 @@ class KnnWorkload(Workload):
                 "skew_max_over_mean": (max(recv) / mean) if mean else None,
                 "matches_arrival_sharding": all(ok)}
 
+    def verify(self):
+        """After the timed region: the last timed step's own top-k (indices and distance bits) --
+        and for C5 its range hit count -- against the synchronous calls on the same window."""
+        import torch
+        if self.args.partition == "cells" or getattr(self, "last_s", None) is None:
+            return None
+        self.ctx.sync()
+        s = self.last_s
+        j, w = s & 1, s % self.windows
+        m = int(self.cnt[0].item())
+        wi, wd = self.ctx.knn_pp(self.grid, self.xs[w], self.ys[w], self.q[0], self.q[1], self.radius, self.k)
+        ok = (m == len(wi) and torch.equal(self.out_i[j][:m].cpu().to(torch.int64), wi.cpu().to(torch.int64)) and
+              torch.equal(self.out_d[j][:m].cpu().view(torch.int64), wd.cpu().view(torch.int64)))
+        if ok and self.has_range:
+            want = self.ctx.range_pp(self.grid, self.xs[w], self.ys[w], self.q[0], self.q[1], self.radius)
+            ok = int(self.out_rc[j].item()) == len(want)
+        return ok
+
     def step(self, s):
         import torch
         if self.args.partition == "cells":
             self.cells_last = self.cells_window(s % self.windows)  # (merged top-k, range hits, received)
             return
+        self.last_s = s
         j = s & 1
         if self.world > 1 and self.ev_done[j] is not None:
             torch.cuda.current_stream(self.dev).wait_event(self.ev_done[j])  # row j free again
@@ -469,6 +488,7 @@ class RangeWorkload(Workload):
         self.hits = None
         self.cs = torch.cuda.Stream(self.dev) if self.world > 1 else None
         self.done = [None] * self.windows
+        self.stepped = set()
 
     def units_per_step(self):
         return self.n
@@ -479,6 +499,8 @@ class RangeWorkload(Workload):
         cur = torch.cuda.current_stream(self.dev)
         if self.world > 1 and self.done[w] is not None:
             cur.wait_event(self.done[w])  # window w's count slot gathered
+        self.last_w = w
+        self.stepped.add(w)
         self.ctx.range_pp_async(self.grid, self.xs[w], self.ys[w], self.q[0], self.q[1], self.radius, False,
                                 self.out, self.n, self.cnt[w:w + 1])
         if self.world > 1:  # result gather: every rank learns each shard's hit count (offsets), on the
@@ -494,6 +516,20 @@ class RangeWorkload(Workload):
                     self.dist.all_gather_into_tensor(self.counts, self.cnt[w:w + 1])
                 self.done[w] = torch.cuda.Event()
                 self.done[w].record(self.cs)
+
+    def verify(self):
+        """After the timed region: every resident window's device hit count, and the last step's
+        hit set, against the synchronous call on the same window."""
+        import torch
+        self.ctx.sync()
+        got = self.cnt.cpu().tolist()
+        want = {w: self.ctx.range_pp(self.grid, self.xs[w], self.ys[w], self.q[0], self.q[1], self.radius)
+                for w in self.stepped}
+        if any(got[w] != len(h) for w, h in want.items()):
+            return False
+        w = self.last_w
+        m = got[w]
+        return torch.equal(torch.sort(self.out[:m].to(torch.int64)).values.cpu(), want[w].cpu().to(torch.int64))
 
     def algorithmic_bytes(self):
         if self.hits is None:
@@ -911,6 +947,9 @@ class KnnIncrWorkload(KnnWorkload):
     def step(self, s):
         w = s % self.windows
         self.inc.push(self.xs[w], self.ys[w], sync=False)
+
+    def verify(self):  # the pane merges are checked by tests/test_gpu_incremental.py
+        return None
 
     def config(self):
         c = super().config()

@@ -39,7 +39,35 @@ static geohip_grid grid_of(JNIEnv* env, jdoubleArray g) {
     return r;
 }
 
-static const double* dbuf(JNIEnv* env, jobject b) { return (const double*)(*env)->GetDirectBufferAddress(env, b); }
+/* The n doubles of a direct ByteBuffer, or NULL when b is null, not direct (a heap buffer has no
+ * address) or smaller than 8 * n bytes: the library would read past it. */
+static const double* dbuf(JNIEnv* env, jobject b, jlong n) {
+    if (!b || n < 0) return NULL;
+    void* p = (*env)->GetDirectBufferAddress(env, b);
+    if (!p || (*env)->GetDirectBufferCapacity(env, b) < 8 * n) return NULL;
+    return (const double*)p;
+}
+
+/* x / y of an n-point window; throws IllegalArgumentException and returns 0 when either is unusable */
+static int window_bufs(JNIEnv* env, jobject x, jobject y, jint n, const double** px, const double** py) {
+    *px = dbuf(env, x, n);
+    *py = dbuf(env, y, n);
+    if (n < 0 || !*px || !*py) {
+        throw_msg(env, "java/lang/IllegalArgumentException",
+                  "coordinates must be direct ByteBuffers of at least 8 * n bytes (n >= 0)");
+        return 0;
+    }
+    return 1;
+}
+
+/* a caller-supplied output array of at least len elements (kNN results) */
+static int out_len_ok(JNIEnv* env, jarray a, jint len) {
+    if (a && (*env)->GetArrayLength(env, a) >= len) return 1;
+    throw_msg(env, "java/lang/IllegalArgumentException", "kNN output arrays must hold k elements");
+    return 0;
+}
+
+static void throw_oom(JNIEnv* env, const char* what) { throw_msg(env, "java/lang/OutOfMemoryError", what); }
 
 /* a Java int[] as a malloc'd uint32_t copy (NULL for a null array); *len its length */
 static uint32_t* u32_copy(JNIEnv* env, jintArray a, jsize* len) {
@@ -84,10 +112,15 @@ JNIEXPORT jintArray JNICALL Java_GeoFlink_utils_GeoHip_rangePP(JNIEnv* env, jcla
                                                                jobject y, jint n, jdouble qx, jdouble qy, jdouble r,
                                                                jboolean approx) {
     geohip_grid grid = grid_of(env, g);
+    const double *px, *py;
+    if (!window_bufs(env, x, y, n, &px, &py)) return NULL;
     uint32_t* out = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(n > 0 ? n : 1));  /* hits <= n */
+    if (!out) {
+        throw_oom(env, "range hit buffer");
+        return NULL;
+    }
     uint64_t cnt = 0;
-    int rc = geohip_range_pp(CTX(h), &grid, dbuf(env, x), dbuf(env, y), (uint64_t)n, qx, qy, r, approx, out,
-                             (uint64_t)n, &cnt);
+    int rc = geohip_range_pp(CTX(h), &grid, px, py, (uint64_t)n, qx, qy, r, approx, out, (uint64_t)n, &cnt);
     jintArray res = NULL;
     if (rc) {
         throw_for(env, CTX(h), rc);
@@ -103,11 +136,18 @@ JNIEXPORT jint JNICALL Java_GeoFlink_utils_GeoHip_knnPP(JNIEnv* env, jclass c, j
                                                         jobject y, jint n, jdouble qx, jdouble qy, jdouble r, jint k,
                                                         jintArray oi, jdoubleArray od) {
     geohip_grid grid = grid_of(env, g);
+    const double *px, *py;
+    if (!window_bufs(env, x, y, n, &px, &py) || !out_len_ok(env, oi, k) || !out_len_ok(env, od, k)) return -1;
     uint32_t* idx = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(k > 0 ? k : 1));
     double* dist = (double*)malloc(sizeof(double) * (size_t)(k > 0 ? k : 1));
+    if (!idx || !dist) {
+        free(idx);
+        free(dist);
+        throw_oom(env, "kNN result buffer");
+        return -1;
+    }
     uint32_t cnt = 0;
-    int rc = geohip_knn_pp(CTX(h), &grid, dbuf(env, x), dbuf(env, y), (uint64_t)n, qx, qy, r, (uint32_t)k, idx, dist,
-                           &cnt);
+    int rc = geohip_knn_pp(CTX(h), &grid, px, py, (uint64_t)n, qx, qy, r, (uint32_t)k, idx, dist, &cnt);
     if (!rc && cnt) {
         (*env)->SetIntArrayRegion(env, oi, 0, (jsize)cnt, (const jint*)idx);
         (*env)->SetDoubleArrayRegion(env, od, 0, (jsize)cnt, dist);
@@ -126,13 +166,22 @@ JNIEXPORT jobjectArray JNICALL Java_GeoFlink_utils_GeoHip_knnRangePP(JNIEnv* env
                                                                       jdouble qy, jdouble r, jint k, jboolean approx,
                                                                       jintArray ki, jdoubleArray kd) {
     geohip_grid grid = grid_of(env, g);
+    const double *px, *py;
+    if (!window_bufs(env, x, y, n, &px, &py) || !out_len_ok(env, ki, k) || !out_len_ok(env, kd, k)) return NULL;
     uint32_t* idx = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(k > 0 ? k : 1));
     double* dist = (double*)malloc(sizeof(double) * (size_t)(k > 0 ? k : 1));
     uint32_t* hits = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(n > 0 ? n : 1));
+    if (!idx || !dist || !hits) {
+        free(idx);
+        free(dist);
+        free(hits);
+        throw_oom(env, "kNN + range result buffers");
+        return NULL;
+    }
     uint32_t kcnt = 0;
     uint64_t rcnt = 0;
-    int rc = geohip_knn_range_pp(CTX(h), &grid, dbuf(env, x), dbuf(env, y), (uint64_t)n, qx, qy, r, (uint32_t)k,
-                                 approx, idx, dist, &kcnt, hits, (uint64_t)n, &rcnt);
+    int rc = geohip_knn_range_pp(CTX(h), &grid, px, py, (uint64_t)n, qx, qy, r, (uint32_t)k, approx, idx, dist, &kcnt,
+                                 hits, (uint64_t)n, &rcnt);
     jobjectArray res = NULL;
     if (rc) {
         throw_for(env, CTX(h), rc);
@@ -165,7 +214,8 @@ JNIEXPORT jintArray JNICALL Java_GeoFlink_utils_GeoHip_joinPP(JNIEnv* env, jclas
                                                               jobject qx, jobject qy, jint nq, jdouble r,
                                                               jboolean approx) {
     geohip_grid a = grid_of(env, gd), b = grid_of(env, gq);
-    const double *px = dbuf(env, dx), *py = dbuf(env, dy), *ox = dbuf(env, qx), *oy = dbuf(env, qy);
+    const double *px, *py, *ox, *oy;
+    if (!window_bufs(env, dx, dy, nd, &px, &py) || !window_bufs(env, qx, qy, nq, &ox, &oy)) return NULL;
     uint64_t cnt = 0;
     int rc = geohip_join_pp_count_only(CTX(h), &a, &b, px, py, (uint64_t)nd, ox, oy, (uint64_t)nq, r, approx, &cnt);
     if (rc) {
@@ -174,7 +224,7 @@ JNIEXPORT jintArray JNICALL Java_GeoFlink_utils_GeoHip_joinPP(JNIEnv* env, jclas
     }
     uint32_t* pairs = (uint32_t*)malloc(sizeof(uint32_t) * 2 * (size_t)(cnt ? cnt : 1));
     if (!pairs) {
-        throw_msg(env, "java/lang/OutOfMemoryError", "join pair buffer");
+        throw_oom(env, "join pair buffer");
         return NULL;
     }
     uint64_t m = 0;
@@ -203,6 +253,8 @@ static jintArray ppoly_pairs(JNIEnv* env, jlong h, ppoly_fn fn, jdoubleArray g1,
                              jint n, jintArray polyRings, jintArray ringOff, jdoubleArray vx, jdoubleArray vy,
                              jdouble r, jboolean approx) {
     geohip_grid a = grid_of(env, g1), b = grid_of(env, g2 ? g2 : g1);
+    const double *px, *py;
+    if (!window_bufs(env, x, y, n, &px, &py)) return NULL;
     jsize npr = 0, nro = 0, nvx = 0, nvy = 0;
     uint32_t* pr = u32_copy(env, polyRings, &npr);
     uint32_t* ro = u32_copy(env, ringOff, &nro);
@@ -214,17 +266,18 @@ static jintArray ppoly_pairs(JNIEnv* env, jlong h, ppoly_fn fn, jdoubleArray g1,
         throw_msg(env, "java/lang/IllegalArgumentException", "polygon arrays");
     } else {
         uint64_t cnt = 0;
-        int rc = fn(CTX(h), &a, &b, dbuf(env, x), dbuf(env, y), (uint64_t)n, pr, ro, hx, hy, (uint64_t)nvx, npoly, r,
-                    approx, NULL, 0, &cnt);
+        int rc = fn(CTX(h), &a, &b, px, py, (uint64_t)n, pr, ro, hx, hy, (uint64_t)nvx, npoly, r, approx, NULL, 0,
+                    &cnt);
         if (rc && rc != GEOHIP_ERR_CAPACITY) {
             throw_for(env, CTX(h), rc);
         } else {
             uint32_t* pairs = (uint32_t*)malloc(sizeof(uint32_t) * 2 * (size_t)(cnt ? cnt : 1));
             uint64_t m = 0;
-            rc = pairs ? fn(CTX(h), &a, &b, dbuf(env, x), dbuf(env, y), (uint64_t)n, pr, ro, hx, hy, (uint64_t)nvx,
-                            npoly, r, approx, pairs, cnt, &m)
+            rc = pairs ? fn(CTX(h), &a, &b, px, py, (uint64_t)n, pr, ro, hx, hy, (uint64_t)nvx, npoly, r, approx, pairs,
+                            cnt, &m)
                        : GEOHIP_ERR_OOM;
-            if (rc) throw_for(env, CTX(h), rc);
+            if (!pairs) throw_oom(env, "point-polygon pair buffer");
+            else if (rc) throw_for(env, CTX(h), rc);
             else res = pairs_array(env, pairs, m);
             free(pairs);
         }
@@ -256,6 +309,8 @@ JNIEXPORT jint JNICALL Java_GeoFlink_utils_GeoHip_knnPPoly(JNIEnv* env, jclass c
                                                            jdoubleArray vy, jdouble r, jint k, jboolean approx,
                                                            jintArray oi, jdoubleArray od) {
     geohip_grid grid = grid_of(env, g);
+    const double *px, *py;
+    if (!window_bufs(env, x, y, n, &px, &py) || !out_len_ok(env, oi, k) || !out_len_ok(env, od, k)) return -1;
     jsize nro = 0, nvx = 0, nvy = 0;
     uint32_t* ro = u32_copy(env, ringOff, &nro);
     double* hx = f64_copy(env, vx, &nvx);
@@ -263,10 +318,12 @@ JNIEXPORT jint JNICALL Java_GeoFlink_utils_GeoHip_knnPPoly(JNIEnv* env, jclass c
     uint32_t* idx = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(k > 0 ? k : 1));
     double* dist = (double*)malloc(sizeof(double) * (size_t)(k > 0 ? k : 1));
     uint32_t cnt = 0;
+    const int oom = !idx || !dist;
     const int bad = !ro || !hx || !hy || nro < 2 || nvx != nvy;
-    int rc = bad ? GEOHIP_ERR_ARG
-                 : geohip_knn_ppoly(CTX(h), &grid, dbuf(env, x), dbuf(env, y), (uint64_t)n, ro, (uint32_t)(nro - 1),
-                                    hx, hy, (uint64_t)nvx, r, (uint32_t)k, approx, idx, dist, &cnt);
+    int rc = oom ? GEOHIP_ERR_OOM
+                 : bad ? GEOHIP_ERR_ARG
+                       : geohip_knn_ppoly(CTX(h), &grid, px, py, (uint64_t)n, ro, (uint32_t)(nro - 1), hx, hy,
+                                          (uint64_t)nvx, r, (uint32_t)k, approx, idx, dist, &cnt);
     if (!rc && cnt) {
         (*env)->SetIntArrayRegion(env, oi, 0, (jsize)cnt, (const jint*)idx);
         (*env)->SetDoubleArrayRegion(env, od, 0, (jsize)cnt, dist);
@@ -277,7 +334,8 @@ JNIEXPORT jint JNICALL Java_GeoFlink_utils_GeoHip_knnPPoly(JNIEnv* env, jclass c
     free(idx);
     free(dist);
     if (rc) {
-        if (bad) throw_msg(env, "java/lang/IllegalArgumentException", "polygon arrays");
+        if (oom) throw_oom(env, "kNN result buffer");
+        else if (bad) throw_msg(env, "java/lang/IllegalArgumentException", "polygon arrays");
         else throw_for(env, CTX(h), rc);
         return -1;
     }

@@ -46,7 +46,9 @@ struct CopyPool {
     unsigned pending = 0;
     bool stop = false;
     explicit CopyPool(unsigned n) {
-        for (unsigned t = 0; t < n; t++)
+        // fewer workers when thread creation fails (RLIMIT_NPROC, a container): std::system_error
+        // must not cross the C ABI; stage_copy splits over the workers that exist (none: memcpy)
+        for (unsigned t = 0; t < n; t++) try {
             th.emplace_back([this, t] {
                 uint64_t seen = 0;
                 for (;;) {
@@ -65,6 +67,9 @@ struct CopyPool {
                     }
                 }
             });
+        } catch (...) {
+            break;
+        }
     }
     ~CopyPool() {
         {
@@ -231,11 +236,18 @@ int queue_fault_read(geohip_ctx* ctx) {
 
 // After the synchronisation that follows queue_fault_read: the faults since the last check as
 // one status (the block cleared on the ctx's stream, the candidate need kept for the next call).
-int report_faults(geohip_ctx* ctx) {
-    const unsigned bits = (unsigned)(ctx->pinned[kPinFault] & 0xffffffffu);
+// `mask` = the fault bits this caller consumes: the synchronous range / kNN calls take only their
+// own look-back bit and leave an earlier async call's faults for geohip_ctx_sync (geohip.h).
+int report_faults(geohip_ctx* ctx, unsigned mask = ~0u) {
+    const unsigned seen = (unsigned)(ctx->pinned[kPinFault] & 0xffffffffu);
+    const unsigned bits = seen & mask;
     if (!bits) return GEOHIP_OK;
     const uint64_t need = ctx->pinned[kPinFault + 1];
-    HIPCHK(hipMemsetAsync(fault_block(ctx), 0, 16, ctx->stream));
+    const unsigned rest = seen & ~mask;
+    if (rest)  // keep the other calls' bits (and the candidate need) for their own check
+        HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(fault_block(ctx)), (int)rest, 1, ctx->stream));
+    else
+        HIPCHK(hipMemsetAsync(fault_block(ctx), 0, 16, ctx->stream));
     if (bits & kFaultCandOverflow) ppoly_note_cand_need(ctx, need);
     if (bits & kFaultLookback)
         return fail(ctx, GEOHIP_ERR_DEVICE, "range look-back wait gave up (a block count never arrived); results invalid");
@@ -300,7 +312,11 @@ int stage_init(geohip_ctx* ctx) {
     HIPCHK(hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking));
     const unsigned hw = std::thread::hardware_concurrency();
     const unsigned nw = std::max(2u, std::min(kStageThreads, hw ? hw : 2u));
-    ctx->copy_pool = std::make_unique<CopyPool>(nw);
+    try {
+        ctx->copy_pool = std::make_unique<CopyPool>(nw);
+    } catch (...) {
+        return fail(ctx, GEOHIP_ERR_OOM, "host staging: copy worker pool");
+    }
     for (int k = 0; k < 2; k++) {
         HIPCHK(hipHostMalloc((void**)&ctx->stg[k], kStagePts * 16, hipHostMallocDefault));
         HIPCHK(hipEventCreateWithFlags(&ctx->stg_ev[k], hipEventDisableTiming));
@@ -311,7 +327,7 @@ int stage_init(geohip_ctx* ctx) {
 
 // x and y of one chunk into a pinned slot, split over the ctx's copy workers
 void stage_copy(geohip_ctx* ctx, char* dx, const char* sx, char* dy, const char* sy, size_t bytes) {
-    if (bytes < (1u << 18) || !ctx->copy_pool) {
+    if (bytes < (1u << 18) || !ctx->copy_pool || ctx->copy_pool->th.empty()) {
         memcpy(dx, sx, bytes);
         memcpy(dy, sy, bytes);
         return;
@@ -836,7 +852,7 @@ int geohip_range_pp_pane(geohip_ctx* ctx, const geohip_grid* grid, const double*
     rc = queue_fault_read(ctx);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(ctx->stream));
-    rc = report_faults(ctx);
+    rc = report_faults(ctx, kFaultLookback);
     if (rc) return rc;
     const uint64_t total = ctx->pinned[0];
     *out_count = total;
@@ -1023,7 +1039,7 @@ int geohip_knn_range_pp(geohip_ctx* ctx, const geohip_grid* grid, const double* 
     rc = queue_fault_read(ctx);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(ctx->stream));
-    rc = report_faults(ctx);
+    rc = report_faults(ctx, kFaultLookback);
     if (rc) return rc;
     *knn_count = (uint32_t)(ctx->pinned[0] & 0xffffffffu);
     const uint64_t total = ctx->pinned[1];

@@ -5444,7 +5444,11 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             const unsigned nth = std::min<unsigned>(std::max(1u, std::min(std::thread::hardware_concurrency(), 16u)),
                                                     std::max<uint32_t>(1u, npoly / 8));
             std::vector<std::thread> th;
-            for (unsigned t = 1; t < nth; t++) th.emplace_back(work);
+            for (unsigned t = 1; t < nth; t++) try {
+                th.emplace_back(work);
+            } catch (...) {  // no more threads (RLIMIT_NPROC, a container): this one does the rest
+                break;
+            }
             work();
             for (auto& t : th) t.join();
             for (uint32_t p = 0; p < npoly; p++) {

@@ -209,6 +209,9 @@ class CellsStep:
         import torch
         m = int(self.count.item())
         h = int(self.hit_count.item())
+        if h > len(self.hits):
+            from ._abi import GeohipCapacityError
+            raise GeohipCapacityError(f"range hits {h} exceed the hit buffer ({len(self.hits)})")
         lh = self.hits[:h].to(torch.int64)
         hits = lh + self.base if self.rg is None else (self.rg[lh] if h else lh)
         allc = self.counts.cpu().tolist()
@@ -232,6 +235,9 @@ def _knn_range_cells_enqueue(x_local, y_local, base, qx, qy, r, k, approximate, 
         px, py, pg, send_counts = band_pack(x_local, y_local, base, int(grid.n), world)
         rx, ry, rg = _exchange_records(px, py, pg, send_counts, group)
         nrecv = len(rx)
+    if b.with_range and nrecv > b.cap:  # skewed shuffle: more points than the rows were sized for
+        b.hits = torch.empty(nrecv, dtype=torch.int32, device=b.hits.device)
+        b.cap = nrecv  # hits <= points received, so the call cannot overflow
     if b.with_range:
         ctx.knn_range_pp_async(grid, rx, ry, qx, qy, r, k, approximate, b.ki, b.kd, b.kc, b.hits, b.cap, b.hc)
     else:

@@ -40,10 +40,10 @@ class IncrementalRange:
     them (the round-4 form added each pane's window offset with a torch pass per window)."""
 
     def __init__(self, ctx: _abi.Context, grid: _abi.Grid, qx: float, qy: float, r: float,
-                 approximate: bool = False, panes: int = 2):
+                 approximate: bool = False, panes: int = 2, start: int = 0):
         self.ctx, self.grid, self.q, self.r, self.approx = ctx, grid, (qx, qy), r, approximate
         self.panes = deque(maxlen=panes)  # (first stream position, pane size, hits as stream positions)
-        self.pos = 0  # stream position of the next pane's first point
+        self.pos = start & 0xFFFFFFFF  # stream position of the next pane's first point (mod 2^32)
 
     def push(self, x, y):
         """Evaluate the new pane; returns the window's hits (window())."""
@@ -58,8 +58,10 @@ class IncrementalRange:
         return self.panes[0][0] if self.panes else self.pos
 
     def window(self):
-        """The window's hits pane by pane (stream positions, ascending): a list of the panes' hit
-        arrays, nothing recomputed or copied."""
+        """The window's hits pane by pane: a list of the panes' hit arrays, nothing recomputed or
+        copied.  Each holds stream positions mod 2^32 as uint32 bit patterns (ascending within a
+        pane until the stream position wraps); a device pane's array is an int32 tensor, so
+        positions from 2^31 on read negative -- mask with & 0xFFFFFFFF, or use window_local()."""
         return [hits for _, _, hits in self.panes]
 
     def window_local(self):

@@ -89,6 +89,29 @@ def test_join_pp_async_approx_and_query_key_error(ctx):
     assert (int(cnt.item()), pair_digest(out[:int(cnt.item())])[1]) == want
 
 
+def test_sync_range_leaves_async_fault_for_ctx_sync(ctx):
+    """A synchronous range / kNN call consumes only its own look-back fault: an earlier async
+    join's query-key fault neither fails it nor is cleared by it; geohip_ctx_sync reports it."""
+    ag, cg = agrid(200)
+    hx, hy = synth.uniform(100_000, 63)
+    dx, dy = _dev(hx, hy)
+    import torch
+    out = torch.empty((1024, 2), dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    l = (BJ[1] - BJ[0]) / 200
+    bqx, bqy = _dev(np.array([BJ[0] + 123456.5 * l]), np.array([BJ[2] - 2.5 * l]))
+    ctx.join_pp_async(ag, ag, dx, dy, bqx, bqy, 0.04, False, out, cnt)
+    q = synth.README_QUERY
+    got = ctx.range_pp(ag, hx, hy, q[0], q[1], 0.05)
+    assert got.tolist() == sorted(cref.range_pp(cg, hx, hy, q[0], q[1], 0.05).tolist())
+    gi, gd = ctx.knn_pp(ag, hx, hy, q[0], q[1], 0.05, 20)
+    wi, wd = cref.knn_pp(cg, hx, hy, q[0], q[1], 0.05, 20)
+    assert gi.tolist() == wi.tolist()
+    with pytest.raises(_abi.GeohipArgumentError):
+        ctx.sync()
+    ctx.sync()  # cleared
+
+
 @pytest.mark.parametrize("join,approx", [(False, False), (False, True), (True, False)])
 def test_ppoly_async_matches_sync(ctx, join, approx):
     import torch

@@ -34,16 +34,19 @@ def pane_stream(seed):
     return out
 
 
-@pytest.mark.parametrize("p", [2, 3])
-def test_incremental_range_equals_full_window(ctx, p):
+@pytest.mark.parametrize("p,start", [(2, 0), (3, 0), (2, (1 << 32) - 250_000), (3, (1 << 31) - 100_000)])
+def test_incremental_range_equals_full_window(ctx, p, start):
+    """Stream positions start at 0, and just below 2^32 / 2^31 (the device pane's int32 hits wrap
+    sign and value inside the stream): window-local indices are (position - start) mod 2^32."""
     import torch
     ag, cg = grids(100)
     panes = pane_stream(11)
-    inc = IncrementalRange(ctx, ag, Q[0], Q[1], 0.5, False, p)
+    inc = IncrementalRange(ctx, ag, Q[0], Q[1], 0.5, False, p, start=start)
     for j, (x, y) in enumerate(panes):
         parts = inc.push(torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda())
         # the panes' hits are stream positions (geohip_range_pp_pane): no per-window pass
-        got = torch.cat([h.to(torch.int64) for h in parts]).cpu().numpy() - inc.window_start
+        got = (torch.cat([h.to(torch.int64) for h in parts]).cpu().numpy() - inc.window_start) & 0xFFFFFFFF
+        assert got.tolist() == inc.window_local().cpu().numpy().tolist()
         win = panes[max(0, j - p + 1):j + 1]
         wx = np.concatenate([w[0] for w in win])
         wy = np.concatenate([w[1] for w in win])
