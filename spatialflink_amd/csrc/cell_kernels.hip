@@ -841,27 +841,14 @@ __global__ void jq_global(uint64_t nq, unsigned* __restrict__ glist, unsigned* _
 // join's decisions are per point, and its pair order was never fixed.
 constexpr unsigned kJbSub = 4096;     // points per local sort round (4 per thread)
 constexpr unsigned kJbBlocks = 256;   // level-1 blocks
-#ifndef GEOHIP_JB_ROUND
-#define GEOHIP_JB_ROUND 1024  // records per level-2 round (same box, round 5: 512 118, 1024 92, 2048 109 us of jb_tiles)
-#endif
-#ifndef GEOHIP_JB_L1NT
-#define GEOHIP_JB_L1NT 0  // measurement builds only: level-1 records stored nontemporally
-#endif
-#ifndef GEOHIP_JB_TNT
-#define GEOHIP_JB_TNT 2  // jb_tiles' record loads (1, measurement builds) / stores (2) nontemporal.  Same
-                         // box, 2 reps: stores 2 -> C3 kernels 1034-1040 -> 1013-1016 us (jb_tiles 95 -> 87,
-                         // join_fused 813 -> 800); loads 1 -> 1039-1042 (no gain)
-#endif
-#ifndef GEOHIP_JB_XNT
-#define GEOHIP_JB_XNT 1  // the window read nontemporally by jb_bands (same box, 2 reps: jb_bands 92.7 -> 72.6
-                         // us, C3 kernels 1042-1050 -> 1029-1040 us; records also nontemporal: jb_tiles 91 -> 123)
-#endif
-#ifndef GEOHIP_JB_L2BLOCKS
-#define GEOHIP_JB_L2BLOCKS 1024
-#endif
+// Cache hints, each a same-box A/B of round 5 (2 reps): the window read nontemporally by
+// jb_bands (jb_bands 92.7 -> 72.6 us); the tile-sorted records stored nontemporally by jb_tiles
+// (jb_tiles 95 -> 87, join_fused 813 -> 800 us); not kept: level-1 records stored (jb_tiles 91 ->
+// 107-123) or read (no gain) nontemporally.
 constexpr unsigned kJbL2Threads = 512;  // level 2: rounds of kJbRound records, 4 blocks per CU
-constexpr unsigned kJbRound = GEOHIP_JB_ROUND;
-constexpr unsigned kJbL2Blocks = GEOHIP_JB_L2BLOCKS;
+// records per level-2 round (same box, round 5: 512 118, 1024 92, 2048 109 us of jb_tiles)
+constexpr unsigned kJbRound = 1024;
+constexpr unsigned kJbL2Blocks = 1024;
 
 struct JBin {
     const double* x;
@@ -941,13 +928,9 @@ __global__ __launch_bounds__(kBinThreads) void jb_bands(JBin a) {
         for (int k = 0; k < PPT; k++) {
             const uint64_t i = sb + threadIdx.x + (uint64_t)k * kBinThreads;
             const uint64_t ic = i < b1 ? i : b1 - 1;
-#if GEOHIP_JB_XNT  // read once here (join_fused reads the records): past the caches
+            // read once here (join_fused reads the records): past the caches
             nx[k] = __builtin_nontemporal_load(a.x + ic);
             ny[k] = __builtin_nontemporal_load(a.y + ic);
-#else
-            nx[k] = a.x[ic];
-            ny[k] = a.y[ic];
-#endif
         }
     };
     if (b0 < b1) fetch(b0);
@@ -987,14 +970,7 @@ __global__ __launch_bounds__(kBinThreads) void jb_bands(JBin a) {
         for (int k = 0; k < PPT; k++) {
             const unsigned j = threadIdx.x + k * kBinThreads;
             if (j < kept) {
-#if GEOHIP_JB_L1NT
-                typedef unsigned u4v __attribute__((ext_vector_type(4)));
-                const uint4 r = st[j];
-                u4v v = {r.x, r.y, r.z, r.w};
-                __builtin_nontemporal_store(v, reinterpret_cast<u4v*>(a.l1 + sb + j));
-#else
                 a.l1[sb + j] = st[j];
-#endif
             }
         }
         lds_barrier();
@@ -1057,14 +1033,8 @@ __device__ __forceinline__ unsigned block_scan_passes(unsigned n, unsigned* wsum
 
 // Tile starts and cursors from the tile counts, then the join's item starts from the same counts
 // and the query list starts (one block; was a separate join_plan launch).
-#ifndef GEOHIP_JP
-#define GEOHIP_JP 1024
-#endif
-#ifndef GEOHIP_JQ
-#define GEOHIP_JQ 128
-#endif
-constexpr unsigned kJP = GEOHIP_JP;  // points per join work item (4 waves x 4 chunks of 64)
-constexpr unsigned kJQ = GEOHIP_JQ;  // queries per join work item
+constexpr unsigned kJP = 1024;  // points per join work item (4 waves x 4 chunks of 64)
+constexpr unsigned kJQ = 128;   // queries per join work item
 __global__ __launch_bounds__(kBinThreads) void jb_scan(JBin a) {
     __shared__ unsigned wsum[kScanPasses * (kBinThreads / kWave)];
     __shared__ unsigned sitems[kMaxTiles];  // item counts, formed while the tile counts load
@@ -1181,10 +1151,6 @@ __global__ __launch_bounds__(kBinThreads) void jb_segs(JBin a) {
 // A round's segments come into LDS in windows of kJbSegBatch; each record finds its segment by a
 // wave-uniform binary search and a per-lane forward step; the round is sorted by tile in LDS and
 // each tile's run reserved with one atomic on its cursor.
-#ifndef GEOHIP_JB_ABL
-#define GEOHIP_JB_ABL 0  // measurement builds only: 1 no record stores, 2 no tile-cursor atomics (each
-                         // round's records kept in place), 4 the join step ends after the binning
-#endif
 __global__ __launch_bounds__(kJbL2Threads) void jb_tiles(JBin a) {
     constexpr int PPT = kJbRound / kJbL2Threads;
     constexpr unsigned kWin = kJbL2Threads;  // segments per window
@@ -1251,13 +1217,7 @@ __global__ __launch_bounds__(kJbL2Threads) void jb_tiles(JBin a) {
             uint4 got[PPT];
 #pragma unroll
             for (int k = 0; k < PPT; k++) {  // unconditional (src 0 when none): no branch per load
-#if GEOHIP_JB_TNT & 1  // measurement builds: level-1 records read nontemporally
-                typedef unsigned u4v __attribute__((ext_vector_type(4)));
-                const u4v g = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(a.l1 + src[k]));
-                got[k] = make_uint4(g.x, g.y, g.z, g.w);
-#else
                 got[k] = a.l1[src[k]];
-#endif
             }
 #pragma unroll
             for (int k = 0; k < PPT; k++) {
@@ -1275,8 +1235,7 @@ __global__ __launch_bounds__(kJbL2Threads) void jb_tiles(JBin a) {
         __syncthreads();
         lds_bins_scan(lh, ls, kBandTiles);
         if (threadIdx.x < kBandTiles && lh[threadIdx.x]) {
-            if (GEOHIP_JB_ABL & 2) base[threadIdx.x] = v0 + ls[threadIdx.x];
-            else base[threadIdx.x] = atomicAdd(&a.tcur[b * kBandTiles + threadIdx.x], lh[threadIdx.x]);
+            base[threadIdx.x] = atomicAdd(&a.tcur[b * kBandTiles + threadIdx.x], lh[threadIdx.x]);
         }
         __syncthreads();
         const unsigned m = v1 - v0;
@@ -1293,13 +1252,10 @@ __global__ __launch_bounds__(kJbL2Threads) void jb_tiles(JBin a) {
                 const uint4 q = st[j];
                 const unsigned bq = (q.w >> 20) & (kBandTiles - 1);
                 const unsigned p = base[bq] + (j - ls[bq]);
-#if GEOHIP_JB_TNT & 2  // measurement builds: tile-sorted records stored nontemporally
                 typedef unsigned u4v __attribute__((ext_vector_type(4)));
                 u4v v = {q.x, q.y, q.z, q.w};
-                if (p < a.n && !(GEOHIP_JB_ABL & 1)) __builtin_nontemporal_store(v, reinterpret_cast<u4v*>(a.recs + p));
-#else
-                if (p < a.n && !(GEOHIP_JB_ABL & 1)) a.recs[p] = q;  // bounded even if the counts were not the binning's own
-#endif
+                // bounded even if the counts were not the binning's own; nontemporal (see kJbRound)
+                if (p < a.n) __builtin_nontemporal_store(v, reinterpret_cast<u4v*>(a.recs + p));
             }
         }
         lds_barrier();
@@ -1330,21 +1286,12 @@ __global__ __launch_bounds__(kJbL2Threads) void jb_tiles(JBin a) {
 // |dx' - dx| <= e = 2.05 u A, so |d2' - d2| <= 4 e A + 2 e^2 + 3 u d2'.  d2' below lo (above hi)
 // puts the true d2 below r2lo (above r2hi), where the fp64 screens already decide (kSqLo/kSqHi).
 constexpr unsigned kJCh = kJP / kWave / (kTB / kWave);  // chunks per wave and item
-#ifndef GEOHIP_JR_NT
-#define GEOHIP_JR_NT 0
-#endif
-#ifndef GEOHIP_JBLOCKSW
-#define GEOHIP_JBLOCKSW 1280
-#endif
-#ifndef GEOHIP_JSTAGE
-#define GEOHIP_JSTAGE 352
-#endif
 // persistent grid of the write pass: 31.2 KB of LDS with 352-pair stages, 5 blocks per CU (89
 // VGPRs allow 5 waves per SIMD).  C3 kernel sums, one box, round 4 (nontemporal pair stores):
 // stage 512 at 4 blocks per CU 1278 us; 640 / 768 / 896 at 3: 1265 / 1262 / 1262; 1024 at 2: 1360;
 // 320 at 5: 1333.  Round 5, plain stores (same box, 2 reps): 768 at 3: 1176-1184; 512 at 4:
 // 1081-1089; 448 at 4: 1078-1091; 352 at 5: 1066-1067 -- with cached stores occupancy beats runs
-constexpr unsigned kJBlocksW = GEOHIP_JBLOCKSW;
+constexpr unsigned kJBlocksW = 1280;
 constexpr unsigned kJBlocksC = 1280;  // count pass (4 KB LDS, 83 VGPRs: 5 blocks per CU)
 
 // query list starts per tile (one block)
@@ -1399,7 +1346,6 @@ struct JPart {  // a PART query: block as (x0, x1 - x0, y0, y1 - y0), tile-relat
 
 // pair (point, query) at output position p (< cap)
 __device__ __forceinline__ void jpair_store(const JoinRun& a, unsigned long long p, unsigned pid, unsigned q) {
-#ifndef JX_NOSTORE
     if (a.aligned8) {  // one 8-byte store per pair (plain: nontemporal stores measured 1028 against
                        // 933 us for C3's join_fused, same box -- the L2 merges the runs' partial lines)
         reinterpret_cast<unsigned long long*>(a.out)[p] = ((unsigned long long)q << 32) | pid;
@@ -1407,7 +1353,6 @@ __device__ __forceinline__ void jpair_store(const JoinRun& a, unsigned long long
         a.out[2 * p] = pid;
         a.out[2 * p + 1] = q;
     }
-#endif
 }
 
 
@@ -1454,7 +1399,7 @@ __device__ __forceinline__ void jpart_quad(const JoinRun& a, const JPart* __rest
 // A wave's pair stage: pairs leave in contiguous runs of full 512-B wave stores.  (One store per
 // (chunk, query) straight from the ballots -- no stage -- measured slower: 1.13 ms against 1.04 ms
 // for C3's write pass; the partial-wave stores are ~3x as many instructions for the same bytes.)
-constexpr unsigned kJStage = GEOHIP_JSTAGE;   // pairs per wave (6 KB)
+constexpr unsigned kJStage = 352;   // pairs per wave (6 KB)
 __device__ __forceinline__ void jstage_flush(const JoinRun& a, uint2* st, unsigned& cnt, unsigned long long& pos) {
     wave_lds_sync();
     for (unsigned t = (unsigned)lane_id(); t < cnt; t += kWave) {
@@ -1481,9 +1426,6 @@ __device__ __forceinline__ void jemit_chunk(const JoinRun& a, unsigned long long
     const unsigned lane = (unsigned)lane_id();
     const bool in_box = (vm >> lane) & 1ull;
     const unsigned vrank = lanes_below(vm), vcnt = (unsigned)__popcll(vm);
-#ifdef JX_NOALL
-    pos += (unsigned long long)nall * vcnt;
-#else
     if (vcnt == kWave) {
         unsigned j = 0;
         for (; j + 4 <= nall; j += 4) {  // four queries' ids in one LDS read
@@ -1507,8 +1449,6 @@ __device__ __forceinline__ void jemit_chunk(const JoinRun& a, unsigned long long
             if (sc > kJStage - 4 * kWave) jstage_flush(a, st, sc, pos);
         }
     }
-#endif
-#ifndef JX_NOPART
     for (unsigned j = 0; j < npart; j += 4) {  // four queries per step, reads first
         const ulonglong2 ma = masks[j / 2], mb = masks[j / 2 + 1];
         const unsigned long long mq[4] = {ma.x, ma.y, mb.x, mb.y};
@@ -1520,7 +1460,6 @@ __device__ __forceinline__ void jemit_chunk(const JoinRun& a, unsigned long long
         }
         if (sc > kJStage - 4 * kWave) jstage_flush(a, st, sc, pos);
     }
-#endif
 }
 
 template <bool APPROX, bool WRITE>
@@ -1665,15 +1604,7 @@ __global__ __launch_bounds__(kTB) void join_fused(JoinRun a) {
             const unsigned c = (unsigned)wid + k * (kTB / kWave);
             const unsigned i = ds + c * 64 + (unsigned)lane;
             rk[k] = make_uint4(0u, 0u, 0u, 0u);
-#if GEOHIP_JR_NT  // measurement builds: the records read nontemporally
-            typedef unsigned u4v __attribute__((ext_vector_type(4)));
-            if (c < nch && i < de) {
-                const u4v g = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(a.recs + i));
-                rk[k] = make_uint4(g.x, g.y, g.z, g.w);
-            }
-#else
-            if (c < nch && i < de) rk[k] = a.recs[i];
-#endif
+            if (c < nch && i < de) rk[k] = a.recs[i];  // (nontemporal: no gain, round 5)
         }
 #pragma unroll
         for (unsigned k = 0; k < kJCh; k++) {
@@ -2477,23 +2408,18 @@ __global__ __launch_bounds__(kTB) void ppoly_outside(const double* __restrict__ 
 constexpr uint32_t kEntC = 0x80000000u;    // entry.x: C cell (class word in entry.y); else G
 constexpr int kStreamNW = 8;               // waves per block
 constexpr unsigned kStreamPts = 256;       // points per wave iteration (4 per lane)
-#ifndef GEOHIP_PS_CHUNK_BITS
-#define GEOHIP_PS_CHUNK_BITS 12  // 2 iterations per wave: 13 (4) spilled 33 VGPRs in the two-phase chunk
-#endif
-constexpr unsigned kStreamChunk = 1u << GEOHIP_PS_CHUNK_BITS;  // points per chunk
-#ifndef GEOHIP_PS_BPC
-#define GEOHIP_PS_BPC 2
-#endif
-constexpr unsigned kStreamBlocksPerCU = GEOHIP_PS_BPC;  // resident blocks per CU (LDS, registers)
+// 4096-point chunks: 2 iterations per wave (8192 spilled 33 VGPRs in the two-phase chunk; 2048
+// measured 626-629 against 591-594 us of C4 kernels, round 5)
+constexpr unsigned kLocalBits = 12;  // point within its chunk
+constexpr unsigned kStreamChunk = 1u << kLocalBits;  // points per chunk
+constexpr unsigned kStreamBlocksPerCU = 2;  // resident blocks per CU (LDS, registers)
 constexpr unsigned kSPairCap = 2 * kStreamChunk;  // block-staged pairs per chunk (4 B each: poly << 12 | point),
                                                   // kSPairCap / kStreamNW per wave
 constexpr unsigned kSCandCap = kStreamChunk / 4;  // block-staged candidates per chunk (per wave likewise)
-constexpr unsigned kLocalBits = GEOHIP_PS_CHUNK_BITS;  // point within its chunk
 constexpr uint32_t kStreamMaxPolys = 1u << (32 - kLocalBits);
-#ifndef GEOHIP_CAND_ITEM
-#define GEOHIP_CAND_ITEM 1024
-#endif
-constexpr unsigned kCandItem = GEOHIP_CAND_ITEM;  // candidates per evaluation work item
+// candidates per evaluation work item (512 / 256 measured slower: 640 / 652 against 622 us of
+// C4 kernels, round 5)
+constexpr unsigned kCandItem = 1024;
 constexpr unsigned kCandLdsPolys = 16384;  // polygons whose per-polygon counters fit LDS
 constexpr unsigned kEvalBlocks = 1024;     // grid of the evaluation pass (strides over its items)
 static_assert(kStreamChunk == (1u << kLocalBits), "chunk-local point ids");
@@ -2548,7 +2474,6 @@ struct StreamSink {
     bool direct;
     unsigned long long base;        // direct: first global slot of the chunk
     unsigned n;                     // staged: entries pushed by this wave (wave-uniform)
-    unsigned acc;                   // measurement only (GEOHIP_PS_ABL 3)
 };
 
 __device__ __forceinline__ void stream_emit_pair(const StreamOut& o, unsigned long long p, unsigned poly, unsigned idx) {
@@ -2569,28 +2494,12 @@ __device__ __forceinline__ void stream_emit_cand(const StreamArgs& a, unsigned l
     a.o.crec[p] = make_double4(a.x[idx], a.y[idx], __longlong_as_double((long long)idx), 0.0);
 }
 
-#ifndef GEOHIP_PS_BATCH
-#define GEOHIP_PS_BATCH 2  // entries whose loads a wave step of the exact walk issues together (0: one
-                           // dependent gather per step; measurement builds).  C4 kernel sums, one
-                           // box: 0 -> 925 us, 1 -> 809, 2 -> 812, 3 -> 822, 4 -> 828, 8 -> 906
-#endif
-#ifndef GEOHIP_PS_NTLOAD
-#define GEOHIP_PS_NTLOAD 0
-#endif
-#ifndef GEOHIP_PS_ABL
-#define GEOHIP_PS_ABL 0  // measurement builds only: 1 no staging pushes, 2 no cell-table reads,
-                          // 3 pushes folded into a register checksum, 4 no chunk write-out
-#endif
 // wave-uniform: the lanes with `hit` add (poly, chunk-local point) to the sink
 template <bool CAND>
 __device__ __forceinline__ void stream_push(const StreamArgs& a, StreamSink& k, bool hit, unsigned poly, unsigned loc,
                                             uint64_t chunk0) {
-    if (GEOHIP_PS_ABL == 3) {
-        k.acc += hit ? (poly ^ loc) : 0u;
-        return;
-    }
     const unsigned long long m = __ballot(hit);
-    if (!m || GEOHIP_PS_ABL == 1) return;
+    if (!m) return;
     if (!k.direct) {
         const unsigned b = k.n + lanes_below(m);
         if (hit && b < k.cap) k.pk[b] = (poly << kLocalBits) | loc;
@@ -2605,10 +2514,8 @@ __device__ __forceinline__ void stream_push(const StreamArgs& a, StreamSink& k, 
     else stream_emit_pair(a.o, k.base + b, poly, (unsigned)(chunk0 + loc));
 }
 
-#ifndef GEOHIP_PS_BAL
-#define GEOHIP_PS_BAL 1  // 0: each lane walks its own points' entries (measurement builds)
-#endif
-// Entry balance of the exact walk (GEOHIP_PS_BAL): per wave iteration, the multi-entry cells'
+// Entry balance of the exact walk (round 5; it replaced each lane walking its own points' entries
+// as one list, entries addressed from the heads' prefix: 512 -> 460 us): per wave iteration, the multi-entry cells'
 // entries are numbered across the wave and every lane takes kBalItems of them per step, so a step
 // serves the wave's entries evenly (a lane's own list had ~7 entries on average and ~14 at the
 // wave's maximum: half of every step's lanes idle) and an iteration needs one round of entry
@@ -2617,10 +2524,8 @@ __device__ __forceinline__ void stream_push(const StreamArgs& a, StreamSink& k, 
 // iteration that exceeds either takes the per-lane walk.
 constexpr unsigned kBalRecs = 128;
 constexpr unsigned kBalWords = 16;
-#ifndef GEOHIP_PS_BALITEMS
-#define GEOHIP_PS_BALITEMS 2  // entries per lane per balanced step (same box: 1 450, 2 448, 3 457, 4 463, 6 479 us)
-#endif
-constexpr unsigned kBalItems = GEOHIP_PS_BALITEMS;
+// entries per lane per balanced step (same box: 1 450, 2 448, 3 457, 4 463, 6 479 us)
+constexpr unsigned kBalItems = 2;
 
 // the class decision of one entry (ex, word) for a point with subcell / NaN bits sw:
 // PointPolygonRangeQuery.java:105-121 -- G -> pair; C -> by the subcell class (mixed: candidate)
@@ -2667,18 +2572,11 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
         const uint64_t base = c0 + (uint64_t)(t * kStreamNW + wid) * kStreamPts;
         const uint64_t i0 = base + 2 * (uint64_t)lane, i1 = i0 + 128;
         if (base + kStreamPts <= c1) {
-#if GEOHIP_PS_NTLOAD  // measurement builds: the window read past L2 (the cell table stays resident)
-            typedef double d2v __attribute__((ext_vector_type(2)));
-            const d2v ax = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(a.x + i0));
-            const d2v bx = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(a.x + i1));
-            const d2v ay = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(a.y + i0));
-            const d2v by = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(a.y + i1));
-#else
+            // plain loads (nontemporal: 472 against 460 us of ppoly_stream, round 5)
             const double2 ax = *reinterpret_cast<const double2*>(a.x + i0);
             const double2 bx = *reinterpret_cast<const double2*>(a.x + i1);
             const double2 ay = *reinterpret_cast<const double2*>(a.y + i0);
             const double2 by = *reinterpret_cast<const double2*>(a.y + i1);
-#endif
             qx[0] = ax.x; qx[1] = ax.y; qx[2] = bx.x; qx[3] = bx.y;
             qy[0] = ay.x; qy[1] = ay.y; qy[2] = by.x; qy[3] = by.y;
         } else {
@@ -2734,8 +2632,7 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
                 bool has = true;
                 if (KL) has = (kl[key >> 5] >> (key & 31u)) & 1u;
                 else if (a.keep) has = (a.keep[key >> 5] >> (key & 31u)) & 1u;
-                if (has && GEOHIP_PS_ABL != 2) hd[t][s] = a.head[key];
-                if (GEOHIP_PS_ABL == 2 && has && key == 0xfffffffu) hd[t][s].x = 0;
+                if (has) hd[t][s] = a.head[key];
                 if (has && !nan && !APPROX) {
                     // the subcell from the cell computation's quotient, exact outside a margin
                     // around the subcell edges; the edges' own arithmetic inside it (rare)
@@ -2749,7 +2646,7 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
             st[t] = s == 0 ? w : (st[t] | (w << (8 * s)));
         }
     }
-    if (!APPROX && GEOHIP_PS_BAL) {
+    if (!APPROX) {
         // Phase B (exact, balanced): per iteration, single-entry slots decided by their own lanes
         // (the head is the entry: no gather), multi-entry slots recorded for the wave
 #pragma unroll
@@ -2834,138 +2731,6 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
                 }
             }
             wave_lds_sync();  // the records and bitmap are reused by the next iteration
-        }
-    } else if (!APPROX && GEOHIP_PS_BATCH > 0) {
-        // Phase B (exact): each lane's entries of its kIters * 4 points form ONE list, numbered
-        // 0 .. tot-1 slot after slot; entry k's address follows from the heads alone (slot = the
-        // last slot whose list start is <= k; a multi cell's entries are consecutive in cell_ent),
-        // so a wave step issues the loads of kPsBatch entries at once instead of a chain of
-        // dependent gathers (each entry's load waited on before the next one was known).
-        constexpr unsigned kSlots = kIters * 4;
-        constexpr unsigned kB = GEOHIP_PS_BATCH > 0 ? GEOHIP_PS_BATCH : 1;
-        unsigned pre[kSlots];
-        unsigned tot = 0;
-#pragma unroll
-        for (unsigned j = 0; j < kSlots; j++) {
-            const uint2 h = hd[j >> 2][j & 3];
-            pre[j] = tot;
-            tot += h.x == kNoEntry ? 0u : ((h.x & kMulti) ? (h.x & ~kMulti) : 1u);
-        }
-        for (unsigned k0 = 0; __ballot(k0 < tot); k0 += kB) {
-            uint2 en[kB];
-            unsigned sj[kB];
-#pragma unroll
-            for (unsigned u = 0; u < kB; u++) {
-                const unsigned k = k0 + u;
-                unsigned j = 0, pj = 0;
-                uint2 h = hd[0][0];
-#pragma unroll
-                for (unsigned i = 1; i < kSlots; i++) {
-                    if (pre[i] <= k) {
-                        j = i;
-                        pj = pre[i];
-                        h = hd[i >> 2][i & 3];
-                    }
-                }
-                sj[u] = j;
-                en[u] = make_uint2(kNoEntry, 0u);
-                if (k < tot) en[u] = (h.x & kMulti) ? a.ent[h.y + (k - pj)] : h;
-            }
-#pragma unroll
-            for (unsigned u = 0; u < kB; u++) {
-                const unsigned j = sj[u];
-                const uint32_t ex = en[u].x, word = en[u].y;
-                bool hit = false, need = false;
-                const unsigned poly = ex & ~kEntC;
-                const unsigned t = j >> 2, sl = j & 3;
-                const unsigned loc = (t * kStreamNW + (unsigned)wid) * kStreamPts + 2u * (unsigned)lane + (sl & 1u) + 128u * (sl >> 1);
-                if (ex != kNoEntry) {
-                    const unsigned sw = (kIters > 1 && t ? st[kIters > 1 ? 1 : 0] : st[0]) >> (8 * sl);
-                    if (!(ex & kEntC)) {
-                        hit = true;
-                    } else {
-                        // a decided class holds for every point in the cell's coordinate box: not for
-                        // NaN coordinates (cell 0 by Java's (int) NaN)
-                        uint32_t kc = kClsMixed;
-                        if (!(sw & kNanBit)) {
-                            if (word == kWordHit) kc = kClsHit;
-                            else if (word == kWordMiss) kc = kClsMiss;
-                            else kc = (word >> (2 * (sw & 15u))) & 3u;
-                        }
-                        hit = kc == kClsHit;
-                        need = kc == kClsMixed;
-                    }
-                }
-                stream_push<false>(a, ps, hit, poly, loc, c0);
-                stream_push<true>(a, cs, need, poly, loc, c0);
-            }
-        }
-    } else if (!APPROX) {
-        // Phase B (exact): each lane walks the entries of its kIters * 4 points as ONE list, slot
-        // after slot (the heads queue in registers, shifted as slots are taken), so a wave step
-        // costs the lanes' largest TOTAL entry count, not the sum over the slots of each slot's
-        // largest count (every slot had some lane with a multi-entry cell: ~3.5 steps per slot).
-        constexpr unsigned kSlots = kIters * 4;
-        uint2 q[kSlots];
-#pragma unroll
-        for (unsigned j = 0; j < kSlots; j++) q[j] = hd[j >> 2][j & 3];
-        unsigned c = 0, cur = 0;  // slots taken; slot of the current entry
-        uint32_t ex = kNoEntry, word = 0;
-        unsigned e = 0, e1 = 0;
-        auto take = [&]() {  // the next slot holding an entry (a multi cell: its first entry loaded)
-            ex = kNoEntry;
-            while (c < kSlots) {
-                const uint2 h = q[0];
-#pragma unroll
-                for (unsigned j = 0; j + 1 < kSlots; j++) q[j] = q[j + 1];
-                cur = c++;
-                if (h.x == kNoEntry) continue;
-                ex = h.x;
-                word = h.y;
-                e = e1 = 0;
-                if (ex & kMulti) {
-                    e = word;
-                    e1 = e + (ex & ~kMulti);
-                    const uint2 en = a.ent[e++];
-                    ex = en.x;
-                    word = en.y;
-                }
-                return;
-            }
-        };
-        take();
-        while (__ballot(ex != kNoEntry)) {
-            bool hit = false, need = false;
-            unsigned poly = 0, loc = 0;
-            if (ex != kNoEntry) {
-                const unsigned t = cur >> 2, sl = cur & 3;
-                loc = (t * kStreamNW + (unsigned)wid) * kStreamPts + 2u * (unsigned)lane + (sl & 1u) + 128u * (sl >> 1);
-                const unsigned sw = (kIters > 1 && t ? st[kIters > 1 ? 1 : 0] : st[0]) >> (8 * sl);
-                poly = ex & ~kEntC;
-                if (!(ex & kEntC)) {
-                    hit = true;
-                } else {
-                    // a decided class holds for every point in the cell's coordinate box: not for
-                    // NaN coordinates (cell 0 by Java's (int) NaN)
-                    uint32_t k = kClsMixed;
-                    if (!(sw & kNanBit)) {
-                        if (word == kWordHit) k = kClsHit;
-                        else if (word == kWordMiss) k = kClsMiss;
-                        else k = (word >> (2 * (sw & 15u))) & 3u;
-                    }
-                    hit = k == kClsHit;
-                    need = k == kClsMixed;
-                }
-                if (e < e1) {  // the cell's next entry
-                    const uint2 en = a.ent[e++];
-                    ex = en.x;
-                    word = en.y;
-                } else {
-                    take();
-                }
-            }
-            stream_push<false>(a, ps, hit, poly, loc, c0);
-            stream_push<true>(a, cs, need, poly, loc, c0);
         }
     }
 #pragma unroll
@@ -3055,18 +2820,16 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
 // candidate totals (the output is unordered: no look-back, no chunk waits for another) and
 // coalesced stores.  A chunk whose stage overflowed runs again with its reservations made from
 // the counts, storing every pair / candidate straight to its slot.
-#ifndef GEOHIP_PS_WPE
-#define GEOHIP_PS_WPE 4  // waves per SIMD the register budget is held to (LDS allows 4)
-#endif
+// the register budget held to 4 waves per SIMD (LDS allows 4; 5-6 spilled, 670-700 us; 3: 1.07 ms)
 template <bool APPROX, bool KL>
-__global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_eu(GEOHIP_PS_WPE))) void ppoly_stream(StreamArgs a) {
+__global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_eu(4))) void ppoly_stream(StreamArgs a) {
     __shared__ unsigned kl[KL ? kKeepLds : 1];
     __shared__ unsigned ppk[kSPairCap];
     __shared__ unsigned cpk[APPROX ? 1 : kSCandCap];
     __shared__ unsigned s_np, s_nc;
     __shared__ unsigned s_wp[kStreamNW], s_wc[kStreamNW];  // per-wave staged counts
     __shared__ unsigned long long s_pb, s_cb;
-    constexpr bool kBal = !APPROX && GEOHIP_PS_BAL;
+    constexpr bool kBal = !APPROX;
     __shared__ uint2 brec[kBal ? kStreamNW * kBalRecs : 1];             // balanced walk: records
     __shared__ unsigned long long bbm[kBal ? kStreamNW * kBalWords : 1];  // and entry-start bitmaps
     constexpr unsigned kWPair = kSPairCap / kStreamNW, kWCand = kSCandCap / kStreamNW;
@@ -3103,13 +2866,12 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
         __syncthreads();  // the previous chunk's stage is drained (and the bitmap staged)
         const uint64_t c0 = (uint64_t)vb * kStreamChunk;
         const uint64_t c1 = c0 + kStreamChunk < a.n ? c0 + kStreamChunk : a.n;
-        StreamSink ps{ppk + wid * kWPair, &s_np, kWPair, false, 0, 0u, 0u};
-        StreamSink cs{cpk + (APPROX ? 0 : wid * kWCand), &s_nc, APPROX ? 0u : kWCand, false, 0, 0u, 0u};
+        StreamSink ps{ppk + wid * kWPair, &s_np, kWPair, false, 0, 0u};
+        StreamSink cs{cpk + (APPROX ? 0 : wid * kWCand), &s_nc, APPROX ? 0u : kWCand, false, 0, 0u};
         uint2* wrec = kBal ? brec + wid * kBalRecs : brec;
         unsigned long long* wbm = kBal ? bbm + wid * kBalWords : bbm;
         stream_chunk<APPROX, KL>(a, kl, c0, c1, ps, cs, wrec, wbm, &pre);
         if (vb + gridDim.x < nchunks) prefetch(vb + gridDim.x);
-        if (GEOHIP_PS_ABL == 3 && ps.acc + cs.acc == 0x9e3779b9u) a.o.ptotal[0] = 1;
         if (lane == 0) {
             s_wp[wid] = ps.n;
             s_wc[wid] = cs.n;
@@ -3132,7 +2894,6 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
         }
         __syncthreads();
         const unsigned long long pb = s_pb, cb = s_cb;
-        if (GEOHIP_PS_ABL == 4) continue;
         if (!over) {  // each wave stores its own region: coalesced runs of the output
             const unsigned* wpk = ppk + wid * kWPair;
             for (unsigned t = (unsigned)lane; t < ps.n; t += kWave) {
@@ -3154,8 +2915,8 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
                 atomicAdd(a.o.reruns, 1u);
             }
             __syncthreads();
-            StreamSink pd{ppk, &s_np, kSPairCap, true, pb, 0u, 0u};
-            StreamSink cd{cpk, &s_nc, kSCandCap, true, cb, 0u, 0u};
+            StreamSink pd{ppk, &s_np, kSPairCap, true, pb, 0u};
+            StreamSink cd{cpk, &s_nc, kSCandCap, true, cb, 0u};
             stream_chunk<APPROX, KL>(a, kl, c0, c1, pd, cd, kBal ? brec + wid * kBalRecs : brec,
                                      kBal ? bbm + wid * kBalWords : bbm, nullptr);
         }
@@ -3377,16 +3138,8 @@ struct CandRefine {
 // about one per block (per-wave stages flushed every ~128 pairs cost 83 of the kernel's 148 us
 // for C4: same-address atomics); kRefinePer candidates per thread per round keep their gather
 // chains (slot -> polygon -> refinement base -> word) in flight together.
-#ifndef GEOHIP_RF_BLOCKS
-#define GEOHIP_RF_BLOCKS 1024
-#endif
-#ifndef GEOHIP_RF_STAGE
-#define GEOHIP_RF_STAGE 4096
-#endif
-#ifndef GEOHIP_RF_PER
-#define GEOHIP_RF_PER 4
-#endif
-constexpr unsigned kRefineBlocks = GEOHIP_RF_BLOCKS, kRefinePer = GEOHIP_RF_PER, kRefineStage = GEOHIP_RF_STAGE;
+// (2 / 8 candidates per thread: 72.5 / 84.4 against 70.9 us at 4, round 5)
+constexpr unsigned kRefineBlocks = 1024, kRefinePer = 4, kRefineStage = 4096;
 __global__ __launch_bounds__(kTB) void ppoly_cand_refine(CandRefine c, StreamOut o) {
     __shared__ uint2 stage[kRefineStage];
     __shared__ unsigned s_n;
@@ -3500,21 +3253,9 @@ __global__ __launch_bounds__(kTB) void ppoly_cand_refine(CandRefine c, StreamOut
 // round-4 sizes -- 512 vertices, 2048 slab entries, 512 staged pairs per wave, 58.6 KB -- left 2
 // blocks per CU and this latency-bound pass at 2 waves per SIMD).  Larger rings and slab lists
 // are read from global memory (as ppoly_eval does past its limits).
-#ifndef GEOHIP_CE_ABL
-#define GEOHIP_CE_ABL 0
-#endif
-#ifndef GEOHIP_CE_VERTS
-#define GEOHIP_CE_VERTS 256
-#endif
-#ifndef GEOHIP_CE_SLAB
-#define GEOHIP_CE_SLAB 1024
-#endif
-#ifndef GEOHIP_CE_PAIRS
-#define GEOHIP_CE_PAIRS 256
-#endif
-constexpr int kEvalLdsVerts = GEOHIP_CE_VERTS;
-constexpr int kEvalLdsSlab = GEOHIP_CE_SLAB;
-constexpr unsigned kEvalPairs = GEOHIP_CE_PAIRS;
+constexpr int kEvalLdsVerts = 256;
+constexpr int kEvalLdsSlab = 1024;
+constexpr unsigned kEvalPairs = 256;
 __global__ __launch_bounds__(kTB) void ppoly_cand_eval(CandGroup c, const PolyDev* __restrict__ polys,
                                                        const double* __restrict__ vx, const double* __restrict__ vy,
                                                        const ring_id_t* __restrict__ vring,
@@ -3616,12 +3357,8 @@ __global__ __launch_bounds__(kTB) void ppoly_cand_eval(CandGroup c, const PolyDe
             if (i < m) {
                 const double px = lqx[i], py = lqy[i];
                 pid = lqi[i];
-#if GEOHIP_CE_ABL  // measurement builds only: no exact tests (results wrong)
-                in = px == 1234.5;
-#else
                 in = holes ? point_polygon_within_rings(px, py, rvx, rvy, rvr, rre, P, sv, r)
                            : point_polygon_within(px, py, rvx, rvy, P, sv, r, v_lds ? lsb : nullptr);
-#endif
             }
             spairs_push<kEvalPairs>(pb, pc, in, poly, pid, o);
         }
@@ -3748,10 +3485,6 @@ __global__ __launch_bounds__(kTB) void ppknn_scan(const double* __restrict__ x, 
 // G u C rects as exact coordinate boxes (planner: rect_to_box), classification by compares
 constexpr int kPpBoxes = kMaxPointBoxes + 1;  // a point plan's G u C boxes fit too
 constexpr unsigned kPpBuf = 1024;  // wave-private candidate buffer (u32 window indices)
-#ifndef GEOHIP_PPK_NT
-#define GEOHIP_PPK_NT 1  // ppknn_scan_boxes: the window read nontemporally (same box, 3 reps: scan 184 -> 170 us,
-                          // kernels 250-251 -> 238 us)
-#endif
 struct PpknnBoxes {
     Box b[kPpBoxes];
     int32_t nb, pad;
@@ -3822,7 +3555,8 @@ __global__ __launch_bounds__(kTB) void ppknn_scan_boxes(const double* __restrict
     };
     auto load_full = [&](uint64_t it, double2 v[4]) {
         const uint64_t i0 = it * 256 + 2 * (uint64_t)lane;
-#if GEOHIP_PPK_NT  // read once here (ppknn_dist gathers only the candidates): past the caches
+        // read once here (ppknn_dist gathers only the candidates): past the caches (same box, 3
+        // reps: scan 184 -> 170 us against plain loads)
         typedef double d2v __attribute__((ext_vector_type(2)));
         const uint64_t io[4] = {i0, i0 + 128, i0, i0 + 128};
 #pragma unroll
@@ -3830,12 +3564,6 @@ __global__ __launch_bounds__(kTB) void ppknn_scan_boxes(const double* __restrict
             const d2v w = __builtin_nontemporal_load(reinterpret_cast<const d2v*>((u < 2 ? x : y) + io[u]));
             v[u] = make_double2(w.x, w.y);
         }
-#else
-        v[0] = *reinterpret_cast<const double2*>(x + i0);
-        v[1] = *reinterpret_cast<const double2*>(x + i0 + 128);
-        v[2] = *reinterpret_cast<const double2*>(y + i0);
-        v[3] = *reinterpret_cast<const double2*>(y + i0 + 128);
-#endif
     };
     uint64_t it = (uint64_t)blockIdx.x * per + wid;
     double2 cur[4], nxt[4];
@@ -4762,7 +4490,6 @@ int join_pp_impl(geohip_ctx* ctx, const geohip_grid* gd, const geohip_grid* gq, 
     const unsigned* tstart = nullptr;
     rc = join_bin(ctx, S, ddx, ddy, nd, geo, tcnt, qstart, misc + 5, istart, items, &recs, &tstart);
     if (rc) return rc;
-    if (GEOHIP_JB_ABL) nq = 0;  // measurement builds: no join over ablated records
     // output: device pointer directly, or a device staging buffer for host output
     unsigned* out = nullptr;
     if (!count_only && cap) {
@@ -5669,14 +5396,8 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             sa.o = so;
             if (nchunks) {
                 const unsigned nblk = (unsigned)std::min<uint64_t>(nchunks, (uint64_t)ctx_cus(ctx) * kStreamBlocksPerCU);
-#ifdef GEOHIP_PS_NOKEEP  // measurement builds: no cell bitmap (every in-grid point gathers its head)
-                sa.keep = nullptr;
-#endif
-#ifdef GEOHIP_PS_NOKL  // measurement builds: the cell bitmap read from global memory, not staged in LDS
-                const bool kl = false;
-#else
+                // the cell bitmap staged in LDS (from global memory: 516 against 460 us; none: 487)
                 const bool kl = sa.keep && sa.keep_words <= kKeepLds;
-#endif
                 if (approximate) {
                     if (kl) tlaunch(ctx, ppoly_stream<true, true>, nblk, kStreamNW * kWave, 0, st, sa);
                     else tlaunch(ctx, ppoly_stream<true, false>, nblk, kStreamNW * kWave, 0, st, sa);

@@ -14,12 +14,10 @@ namespace geohip {
 // Bytes of text owned by one block (its records are those whose preceding '\n' lies in the
 // chunk), and the LDS bytes staged past the chunk for the record that straddles its end (a
 // longer record reads its remaining bytes from global memory through the general parser).
-#ifndef GEOHIP_ING_BPT
-#define GEOHIP_ING_BPT 48  // text bytes per thread of the 512-thread block (16-byte multiple): 24 KB
-                           // chunks, ~430 CSV records for 512 threads (16 KB: ~290, 44 % of the
-                           // lanes idle in the parse); same box: 32 B 494 us, 48 B 422 us, 64 B 466 us
-#endif
-constexpr uint32_t kIngestChunk = 512u * GEOHIP_ING_BPT;
+// 48 text bytes per thread of the 512-thread block (16-byte multiple): 24 KB chunks, ~430 CSV
+// records for 512 threads (16 KB: ~290, 44 % of the lanes idle in the parse); same box: 32 B
+// 494 us, 48 B 422 us, 64 B 466 us
+constexpr uint32_t kIngestChunk = 512u * 48u;
 constexpr uint32_t kIngestTail = 512;
 
 struct IngestArgs {

@@ -115,7 +115,7 @@ struct LdsReader {
 // blanks or quotes, so the span is the field as staged; empty -> kFallback.  c0: the chunk's text
 // offset (spans are batch offsets).
 __device__ __forceinline__ int fast_csv(const uint8_t* __restrict__ s, uint32_t p, uint32_t lim,
-                                        const ingest::Spec& sp, ingest::Parsed* o, uint64_t c0, int ablate = 0) {
+                                        const ingest::Spec& sp, ingest::Parsed* o, uint64_t c0) {
     const uint8_t d = (uint8_t)sp.delim;
     int need = sp.fx > sp.fy ? sp.fx : sp.fy;
     if (sp.fts > need) need = sp.fts;
@@ -154,8 +154,7 @@ __device__ __forceinline__ int fast_csv(const uint8_t* __restrict__ s, uint32_t 
                 // Long.valueOf of the (<= 18 digit) run: w holds it exactly (leading zeros skipped)
                 o->ts = neg ? -(int64_t)w : (int64_t)w;
             } else {
-                const uint64_t bits = (ablate == 2 ? __builtin_bit_cast(uint64_t, (double)w)
-                                                   : ingest::decimal_to_bits(w, q)) | (neg ? 1ull << 63 : 0ull);
+                const uint64_t bits = ingest::decimal_to_bits(w, q) | (neg ? 1ull << 63 : 0ull);
                 const double v = __builtin_bit_cast(double, bits);
                 if (isx) o->x = v;
                 if (isy) o->y = v;
@@ -300,23 +299,12 @@ __device__ __forceinline__ int swar_csv(const uint8_t* __restrict__ s, uint32_t 
                 if (nf == 0) return kSwarNo;
             }
             if (ni == 0 || ni + nf > 19 || (ist && ni > 18)) return kSwarNo;
-#ifdef GEOHIP_ING_NODIG
-            const uint64_t iv = W.v[0] ^ ni;  // measurement only
-#else
             const uint64_t iv = digits_n(W, st, ni);
-#endif
             if (ist) {
                 o->ts = st ? -(int64_t)iv : (int64_t)iv;
             } else {
-#if defined(GEOHIP_ING_NODIG)
-                const uint64_t bits = iv ^ W.v[1] ^ nf;  // measurement only
-#elif defined(GEOHIP_ING_NOEL)
-                const uint64_t w = nf ? iv * kPow10u[nf] + digits_n(W, e1 + 1, nf) : iv;
-                const uint64_t bits = w ^ nf;  // measurement only
-#else
                 const uint64_t w = nf ? iv * kPow10u[nf] + digits_n(W, e1 + 1, nf) : iv;
                 const uint64_t bits = ingest::decimal_to_bits(w, -(int32_t)nf) | (st ? 1ull << 63 : 0ull);
-#endif
                 const double v = __builtin_bit_cast(double, bits);
                 if (isx) o->x = v;
                 if (isy) o->y = v;
@@ -384,16 +372,10 @@ __device__ __forceinline__ unsigned stage_chunk(const uint8_t* __restrict__ text
     return nrec;
 }
 
-#ifndef GEOHIP_ING_NTST
-#define GEOHIP_ING_NTST 0  // measurement builds: the record columns stored nontemporally
-#endif
+// plain column stores (nontemporal ones measured within noise, round 5: 403-415 against 407-417 us)
 template <typename T>
 __device__ __forceinline__ void col_store(T* p, T v) {
-#if GEOHIP_ING_NTST
-    __builtin_nontemporal_store(v, p);
-#else
     *p = v;
-#endif
 }
 __device__ __forceinline__ void store_record(const IngestArgs& a, uint64_t idx, const ingest::Parsed& o,
                                              double* __restrict__ x, double* __restrict__ y,
@@ -402,9 +384,7 @@ __device__ __forceinline__ void store_record(const IngestArgs& a, uint64_t idx, 
     col_store(y + idx, o.y);
     if (ts) col_store(ts + idx, (int64_t)o.ts);
     if (a.oid) col_store(a.oid + idx, o.oid);
-    if (cell && a.pad == 3) {
-        col_store(cell + idx, 0u);
-    } else if (cell) {
+    if (cell) {
         const int32_t cx = ingest::java_cell(o.x, a.min_x, a.cell_len);
         const int32_t cy = ingest::java_cell(o.y, a.min_y, a.cell_len);
         const bool ok = cx >= 0 && cx < a.n && cy >= 0 && cy < a.n;
@@ -419,10 +399,7 @@ __device__ __forceinline__ void store_record(const IngestArgs& a, uint64_t idx, 
 // batch) is listed for ingest_general, which re-parses all its records with the full grammar.
 // The first round of records is parsed before the look-back, so the wait for the earlier
 // chunks' counts overlaps the parse.
-#ifndef GEOHIP_ING_WPE
-#define GEOHIP_ING_WPE 8
-#endif
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(GEOHIP_ING_WPE))) void ingest_fused(const uint8_t* __restrict__ text, uint64_t nbytes,
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8))) void ingest_fused(const uint8_t* __restrict__ text, uint64_t nbytes,
                                                         IngestArgs a, IngestLookback lb,
                                                         double* __restrict__ x, double* __restrict__ y,
                                                         int64_t* __restrict__ ts, uint32_t* __restrict__ cell,
@@ -431,11 +408,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(GEOHIP
     __shared__ unsigned s_vb, s_flag;
     __shared__ unsigned long long s_base;
     if (threadIdx.x == 0) {
-#ifdef GEOHIP_ING_NOTICKET
-        s_vb = blockIdx.x;  // measurement only: in-order dispatch assumed
-#else
         s_vb = atomicAdd(lb.ticket, 1u);
-#endif
         s_flag = 0;
     }
     __syncthreads();
@@ -462,31 +435,20 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(GEOHIP
         o.oid = ingest::kOidNull;
         int rc = ingest::kFallback;
         if (i < nrec && listed_all) {
-            if (a.pad == 1) {
-                o.x = o.y = (double)L.start[i];
-                rc = ingest::kOk;
-            } else if (fast) {
-                rc = a.pad == 0 ? swar_csv(st8, L.start[i], stage_len, a.spec, &o, c0) : kSwarNo;
-                if (rc == kSwarNo) rc = fast_csv(st8, L.start[i], stage_len, a.spec, &o, c0, a.pad);
+            if (fast) {
+                rc = swar_csv(st8, L.start[i], stage_len, a.spec, &o, c0);
+                if (rc == kSwarNo) rc = fast_csv(st8, L.start[i], stage_len, a.spec, &o, c0);
             }
             undecided |= rc != ingest::kOk;
         }
         if (r == 0) {  // the record base: look-back by wave 0, behind its first round's parse
             if (threadIdx.x < kWave) {
-#ifdef GEOHIP_ING_NOLB
-                const unsigned long long excl = (unsigned long long)vb * 287u;  // measurement only
-#else
                 const unsigned long long excl = vb == 0 ? 0ull : lookback_prefix(lb.status, vb, lb.epoch, lb.nlisted + 1);
-#endif
                 if (threadIdx.x == 0) {
                     if (vb != 0) publish_status(lb.status + vb, tag | kPrefixBit | (excl + nrec));
                     s_base = excl;
                     if (vb == gridDim.x - 1) {
-#ifdef GEOHIP_ING_NOLB
-                        *total = cap;
-#else
                         *total = excl + nrec;
-#endif
                         __hip_atomic_store(lb.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
                     }
                 }
@@ -495,11 +457,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(GEOHIP
             rbase = s_base;
         }
         const uint64_t idx = rbase + i;
-#ifndef GEOHIP_ING_NOSTORE
         if (i < nrec && listed_all && rc == ingest::kOk && idx < cap) store_record(a, idx, o, x, y, ts, cell);
-#else
-        if (i < nrec && listed_all && rc == ingest::kOk && idx < cap && o.x == 12345.0) store_record(a, idx, o, x, y, ts, cell);
-#endif
     }
     if (__ballot(undecided) && lane_id() == 0) s_flag = 1u;
     __syncthreads();

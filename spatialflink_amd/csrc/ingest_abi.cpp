@@ -115,10 +115,7 @@ int ingest_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_ingest_sp
         a.cell_len = grid->cell_len;
         a.n = grid->n;
     }
-    // measurement hook (never set in production): 1 = stage + store only, 2 = no Eisel-Lemire,
-    // 3 = no cell division (results are wrong in modes 1-3)
-    static const int ablate = getenv("GEOHIP_INGEST_ABLATE") ? atoi(getenv("GEOHIP_INGEST_ABLATE")) : 0;
-    a.pad = ablate;
+    a.pad = 0;
     const uint64_t nchunks = ingest_chunks(nbytes);
     if (nchunks >= (1ull << 31)) return ctx_fail(ctx, GEOHIP_ERR_UNSUPPORTED, "batch too large");
     hipStream_t st = ctx_stream(ctx);

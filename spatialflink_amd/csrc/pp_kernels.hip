@@ -36,30 +36,18 @@ struct WaveStage {  // wave-private LDS
     unsigned ci[kCandCap];
 };
 
-#ifndef GEOHIP_L4_NT
-#define GEOHIP_L4_NT 0
-#endif
-#ifndef GEOHIP_KP_NT
-#define GEOHIP_KP_NT 1  // knn_pass: the window read nontemporally (same box, 3 reps: C5 92-93 -> 84 us, C2 40.2-41.3 -> 38.4-38.7 us)
-#endif
 __device__ __forceinline__ void load4(const double* __restrict__ x, const double* __restrict__ y,
                                       uint64_t base, uint64_t end, int lane, double px[4], double py[4],
                                       bool valid[4]) {
     const uint64_t i0 = base + 2 * (uint64_t)lane;
     const uint64_t i1 = base + 128 + 2 * (uint64_t)lane;
     if (base + kPtsIter <= end) {
-#if GEOHIP_L4_NT  // measurement builds: the window read nontemporally (range passes)
-        typedef double d2v __attribute__((ext_vector_type(2)));
-        const d2v a = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(x + i0));
-        const d2v b = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(x + i1));
-        const d2v c = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(y + i0));
-        const d2v d = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(y + i1));
-#else
+        // plain loads: nontemporal ones measured no gain for the range passes (47.7-49.0 against
+        // 47.4-47.7 us, round 5)
         const double2 a = *reinterpret_cast<const double2*>(x + i0);
         const double2 b = *reinterpret_cast<const double2*>(x + i1);
         const double2 c = *reinterpret_cast<const double2*>(y + i0);
         const double2 d = *reinterpret_cast<const double2*>(y + i1);
-#endif
         px[0] = a.x; px[1] = a.y; px[2] = b.x; px[3] = b.y;
         py[0] = c.x; py[1] = c.y; py[2] = d.x; py[3] = d.y;
         valid[0] = valid[1] = valid[2] = valid[3] = true;
@@ -1231,18 +1219,12 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
     // first and the last block, measured by the phase trace).  The fused range keeps a contiguous
     // chunk per block (its hit bitmask covers the chunk).  ABL bit 4: chunks (measurement).
     constexpr bool kInterleave = !RANGE && !(ABL & 16);
-    // Front rotation (GEOHIP_KNN_ROT): block b takes slot (b + it * ROT) mod nblocks of front it, so
-    // the blocks of one XCD (b mod 8) do not always read the same 2 KB position mod 16 KB of the
-    // window (with ROT 0 they do: a fixed slice of the address bits per XCD).
-#ifndef GEOHIP_KNN_ROT
-#define GEOHIP_KNN_ROT 0
-#endif
-    constexpr unsigned kRot = GEOHIP_KNN_ROT;
+    // (Rotating each block's slot within a front, so one XCD's blocks do not always read the same
+    // 2 KB position mod 16 KB, measured slower in round 4: 42.3 against 38.7 us.)
     const uint64_t total_iters = (n + kPtsIter - 1) / kPtsIter;
     const uint64_t full_fronts = total_iters / gridDim.x, rem_front = total_iters % gridDim.x;
     const unsigned niters =
-        kInterleave ? (unsigned)(full_fronts + ((rem_front && (blockIdx.x + full_fronts * kRot) % gridDim.x < rem_front)
-                                                    ? 1u : 0u))
+        kInterleave ? (unsigned)(full_fronts + ((rem_front && blockIdx.x < rem_front) ? 1u : 0u))
                     : (unsigned)((blk_end - blk_begin + kPtsIter - 1) / kPtsIter);
     if (kInterleave) blk_end = n;
     unsigned ccnt = 0;
@@ -1322,24 +1304,19 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
     const bool all_valid[4] = {true, true, true, true};
     double ax[4], ay[4], bx[4], by[4];
     auto it_base = [&](unsigned it) {
-        return kInterleave ? ((uint64_t)it * gridDim.x + (blockIdx.x + (uint64_t)it * kRot) % gridDim.x) * kPtsIter
+        return kInterleave ? ((uint64_t)it * gridDim.x + blockIdx.x) * kPtsIter
                            : blk_begin + (uint64_t)it * kPtsIter;
     };
     auto is_full = [&](unsigned it) { return it_base(it) + kPtsIter <= blk_end; };
     auto load_full = [&](unsigned it, double (&px)[4], double (&py)[4]) {
         const uint64_t i0 = it_base(it) + 2 * (uint64_t)lane;
-#if GEOHIP_KP_NT  // read once (candidates keep their coordinates in LDS): past the caches
+        // read once (candidates keep their coordinates in LDS): past the caches (same box, 3 reps:
+        // C5 92-93 -> 84 us, C2 40.2-41.3 -> 38.4-38.7 us against plain loads)
         typedef double d2v __attribute__((ext_vector_type(2)));
         const d2v u0 = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(x + i0));
         const d2v u1 = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(x + i0 + 128));
         const d2v v0 = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(y + i0));
         const d2v v1 = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(y + i0 + 128));
-#else
-        const double2 u0 = *reinterpret_cast<const double2*>(x + i0);
-        const double2 u1 = *reinterpret_cast<const double2*>(x + i0 + 128);
-        const double2 v0 = *reinterpret_cast<const double2*>(y + i0);
-        const double2 v1 = *reinterpret_cast<const double2*>(y + i0 + 128);
-#endif
         px[0] = u0.x; px[1] = u0.y; px[2] = u1.x; px[3] = u1.y;
         py[0] = v0.x; py[1] = v0.y; py[2] = v1.x; py[3] = v1.y;
     };
@@ -1773,9 +1750,9 @@ struct RangeLookback {
     unsigned spin_limit, inject;
 };
 
-// MODE (measurement only): 0 full; 1 no look-back/emission (counts only); 2 loads only;
-// 3 no emission; 4 no look-back wait
-template <bool APPROX, int MODE = 0>
+// (Round-4 ablations of this kernel, rocprof on one box: full 47.9 us; counts only 38.7; loads
+// only 30.2; no emission 40.2; no look-back wait 46.7.)
+template <bool APPROX>
 __global__ __launch_bounds__(kRangeNW * kWave) void range_fused(const double* __restrict__ x,
                                                                 const double* __restrict__ y, uint64_t n, RangeArgs a,
                                                                 unsigned upb, RangeLookback lb,
@@ -1847,20 +1824,6 @@ __global__ __launch_bounds__(kRangeNW * kWave) void range_fused(const double* __
         double nx4[4], ny4[4];
         bool nv[4] = {false, false, false, false};
         if (nit < niters) load4(x, y, p0 + (uint64_t)nit * kPtsIter, p1, lane, nx4, ny4, nv);
-        if (MODE == 2) {
-            double sink = 0.0;
-#pragma unroll
-            for (int s4 = 0; s4 < 4; s4++) sink += cx4[s4] + cy4[s4];
-            if (sink == 12345.678) bmask[0] = 1;
-#pragma unroll
-            for (int s4 = 0; s4 < 4; s4++) {
-                cx4[s4] = nx4[s4];
-                cy4[s4] = ny4[s4];
-                cv[s4] = nv[s4];
-            }
-            it = nit;
-            continue;
-        }
         unsigned long long hb[4];
 #pragma unroll
         for (int s4 = 0; s4 < 4; s4++) {
@@ -1913,13 +1876,6 @@ __global__ __launch_bounds__(kRangeNW * kWave) void range_fused(const double* __
         if (my) atomicAdd(&bcount, my);
     }
     __syncthreads();
-    if (MODE == 1 || MODE == 2) {
-        if (threadIdx.x == 0 && vb == gridDim.x - 1) {
-            *total = bcount;
-            __hip_atomic_store(lb.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        return;
-    }
     // publish this block's count
     const unsigned long long tag = lb.epoch << 40;
     // published with an atomic exchange: performed at the device coherence point, so the other
@@ -1947,7 +1903,7 @@ __global__ __launch_bounds__(kRangeNW * kWave) void range_fused(const double* __
         }
     // exclusive offset = sum of every earlier block's count: one wave polls (with back-off) so
     // blocks that finish early do not flood the status words while others still stream
-    if (wid == 0 && MODE != 4) {
+    if (wid == 0) {
         // lane l reads predecessors l, l + 64, l + 128, l + 192 with all four loads in flight
         // (a dependent chain of device-scope loads costs a memory round trip each)
         const unsigned long long pre = poll_block_counts<kRangeMaxBlocks / kWave>(lb.status, vb, lb.epoch, lb.spin_limit,
@@ -1960,7 +1916,7 @@ __global__ __launch_bounds__(kRangeNW * kWave) void range_fused(const double* __
     // the output, written word after word (consecutive stores complete each other's lines).  Lane
     // l loads word w0 + l once; the per-word bits and offsets then come by readlane, so no LDS
     // round trip sits between two words' stores.
-    if (MODE != 3) {
+    {
         const unsigned wpw = (nw + kRangeNW - 1) / kRangeNW;
         const unsigned wb = (unsigned)wid * wpw;
         const unsigned we = wb + wpw < nw ? wb + wpw : nw;
@@ -2328,15 +2284,12 @@ hipError_t launch_range(const double* x, const double* y, uint64_t n, const Rang
         const unsigned upb = (unsigned)((units + kRangeMaxBlocks - 1) / kRangeMaxBlocks);
         const unsigned nblocks = (unsigned)((units + upb - 1) / upb);
         const RangeLookback lb{lb_status, lb_ticket, epoch, lb_fault, lb_spins, lb_inject};
-#ifndef GEOHIP_RANGE_MODE
-#define GEOHIP_RANGE_MODE 0  // measurement builds only (range_fused MODE)
-#endif
         // one kernel: ev0 / ev1 stamped by its dispatch
         const dim3 g(nblocks), b(kRangeNW * kWave);
         if (approximate)
             hipExtLaunchKernelGGL(range_fused<true>, g, b, 0, st, ev0, ev1, 0, x, y, n, a, upb, lb, out, cap, total);
         else
-            hipExtLaunchKernelGGL(range_fused<false, GEOHIP_RANGE_MODE>, g, b, 0, st, ev0, ev1, 0, x, y, n, a, upb, lb,
+            hipExtLaunchKernelGGL(range_fused<false>, g, b, 0, st, ev0, ev1, 0, x, y, n, a, upb, lb,
                                   out, cap, total);
         return hipGetLastError();
     }
