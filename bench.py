@@ -60,6 +60,8 @@ def parse():
     p.add_argument("--points", type=int, default=None, help="points per window per GPU (default: the config's)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--range-ascending", action="store_true",
+                   help="range: ascending hit order (GEOHIP_ORDER_ASCENDING, range_fused) instead of the unordered set")
     p.add_argument("--no-e2e", action="store_true", help="skip the host-resident end-to-end line")
     p.add_argument("--no-pipelined", action="store_true", help="skip the multi-stream pipelined line")
     p.add_argument("--pipeline-streams", type=int, default=3, help="contexts / HIP streams of the pipelined line")
@@ -468,8 +470,8 @@ class RangeWorkload(Workload):
     """C1 query shape (BASELINE.json configs[0]: 100x100, README query, r=0.5) at 10M points per
     GPU (C1's 1M-point window is the reference's CPU case; on the GPU it is launch-bound)."""
     tag = "range"
-    kernel = ("geohip::range_fused (one launch per window: classify, exact distances in C cells, per-block hit masks, "
-              "ticket-ordered look-back over block counts, ascending emission)")
+    kernel = ("geohip::range_set (one launch per window: classify, exact distances in C cells, hits staged per wave "
+              "and stored in reserved runs while the window streams; unordered-set output, GEOHIP_ORDER_ANY)")
     grid_n, radius, n_default = 100, 0.5, 10_000_000
 
     def __init__(self, *a):
@@ -482,6 +484,11 @@ class RangeWorkload(Workload):
         self.grid = _abi.make_grid(bj[0], bj[2], (bj[1] - bj[0]) / self.grid_n, self.grid_n)
         self.xs, self.ys = _uniform_windows(self.ctx, self.dev, self.n, self.rank,
                                             [1 + 7919 * w for w in range(self.windows)], bj)
+        # the reference's window result is a set (PointPointRangeQuery.java:117-136)
+        self.ctx.set_range_order(not self.args.range_ascending)
+        if self.args.range_ascending:
+            self.kernel = ("geohip::range_fused (one launch per window: classify, exact distances in C cells, per-block "
+                           "hit masks, ticket-ordered look-back over block counts, ascending emission)")
         self.out = torch.empty(self.n, dtype=torch.int32, device=self.dev)
         self.cnt = torch.zeros(self.windows, dtype=torch.int64, device=self.dev)
         self.counts = torch.zeros(self.world, dtype=torch.int64, device=self.dev)
@@ -529,7 +536,8 @@ class RangeWorkload(Workload):
             return False
         w = self.last_w
         m = got[w]
-        return torch.equal(torch.sort(self.out[:m].to(torch.int64)).values.cpu(), want[w].cpu().to(torch.int64))
+        return torch.equal(torch.sort(self.out[:m].to(torch.int64)).values.cpu(),
+                           torch.sort(want[w].to(torch.int64)).values.cpu())
 
     def algorithmic_bytes(self):
         if self.hits is None:
@@ -539,6 +547,7 @@ class RangeWorkload(Workload):
     def config(self):
         return {"workload": f"C1 query shape (point-point range, 100x100 Beijing UniformGrid, README query, r=0.5, "
                             f"exact) over {self.n} uniform points per window per GPU",
+                "output": "ascending hit indices" if self.args.range_ascending else "unordered hit set (GEOHIP_ORDER_ANY)",
                 "points_per_window_per_gpu": self.n, "grid": self.grid_n, "radius": self.radius,
                 "hits_per_window_per_gpu": self.hits, "windows_resident": self.windows,
                 "parallelism": f"shard{self.world}"}

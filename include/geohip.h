@@ -107,6 +107,15 @@ int geohip_ctx_set_stream(geohip_ctx* ctx, void* hip_stream);
 /* Back to the ctx's own (non-blocking) stream, the state after geohip_ctx_create. */
 int geohip_ctx_reset_stream(geohip_ctx* ctx);
 void* geohip_ctx_stream(geohip_ctx* ctx);
+/* Output order of the point-point range calls (geohip_range_pp, _pane, _async):
+   GEOHIP_ORDER_ASCENDING (the default after geohip_ctx_create) -- hit indices ascending;
+   GEOHIP_ORDER_ANY -- the same set in an unspecified order, as the reference's window function
+   emits it (PointPointRangeQuery.java:117-136 collects the filter's hits as they arrive), from
+   one pass with no ordered emission (faster).  The fused geohip_knn_range_pp range stays
+   ascending. */
+#define GEOHIP_ORDER_ASCENDING 0
+#define GEOHIP_ORDER_ANY 1
+int geohip_ctx_set_range_order(geohip_ctx* ctx, int order);
 /* Device timing of each call's step (measurement): while enabled, every query call's device work
    is timed with HIP events on the ctx stream. */
 int geohip_ctx_set_timing(geohip_ctx* ctx, int enable);

@@ -108,6 +108,11 @@ JNIEXPORT jlong JNICALL Java_GeoFlink_utils_GeoHip_create(JNIEnv* env, jclass c,
 
 JNIEXPORT void JNICALL Java_GeoFlink_utils_GeoHip_destroy(JNIEnv* env, jclass c, jlong h) { geohip_ctx_destroy(CTX(h)); }
 
+JNIEXPORT void JNICALL Java_GeoFlink_utils_GeoHip_rangeOrder(JNIEnv* env, jclass c, jlong h, jint order) {
+    int rc = geohip_ctx_set_range_order(CTX(h), (int)order);
+    if (rc) throw_for(env, CTX(h), rc);
+}
+
 JNIEXPORT jintArray JNICALL Java_GeoFlink_utils_GeoHip_rangePP(JNIEnv* env, jclass c, jlong h, jdoubleArray g, jobject x,
                                                                jobject y, jint n, jdouble qx, jdouble qy, jdouble r,
                                                                jboolean approx) {

@@ -33,6 +33,9 @@ public final class GeoHip implements AutoCloseable {
         if (v != ABI_VERSION)
             throw new IllegalStateException("libgeohip ABI " + v + ", facade written for " + ABI_VERSION);
         ctx = create(1 << device);
+        // the window operators emit the hits as a set (PointPointRangeQuery.java:117-136): no
+        // ordered emission (GEOHIP_ORDER_ANY = 1)
+        rangeOrder(ctx, 1);
     }
 
     @Override
@@ -97,7 +100,7 @@ public final class GeoHip implements AutoCloseable {
 
     // ---- one call per window (include/geohip.h; the reference lines each replaces are cited there)
 
-    /** geohip_range_pp: window positions of the hits, ascending. */
+    /** geohip_range_pp: window positions of the hits, in no particular order (a set). */
     public int[] rangePP(double[] grid, ByteBuffer x, ByteBuffer y, int n, double qx, double qy, double r,
                          boolean approximate) {
         return rangePP(ctx, grid, x, y, n, qx, qy, r, approximate);
@@ -143,6 +146,7 @@ public final class GeoHip implements AutoCloseable {
     private static native int abiVersion();
     private static native long create(int deviceMask);
     private static native void destroy(long ctx);
+    private static native void rangeOrder(long ctx, int order);
     private static native int[] rangePP(long ctx, double[] g, ByteBuffer x, ByteBuffer y, int n, double qx, double qy,
                                         double r, boolean approx);
     private static native int knnPP(long ctx, double[] g, ByteBuffer x, ByteBuffer y, int n, double qx, double qy,

@@ -18,6 +18,7 @@ LIB_PATH = Path(os.environ.get("GEOHIP_LIB", Path(__file__).resolve().parent / "
 
 OK, ERR_ARG, ERR_CAPACITY, ERR_DEVICE, ERR_OOM, ERR_UNSUPPORTED = 0, 1, 2, 3, 4, 5
 MEM_HOST, MEM_DEVICE = 0, 1
+ORDER_ASCENDING, ORDER_ANY = 0, 1  # geohip_ctx_set_range_order
 KNN_MAX_K = 1024
 KNN_PPOLY_MAX_K = 256
 SENTINEL_IDX = 0xFFFFFFFF
@@ -175,6 +176,7 @@ _SIGS = {
     "geohip_ctx_reset_stream": (c_int, [_P]),
     "geohip_ctx_stream": (c_void_p, [_P]),
     "geohip_ctx_set_timing": (c_int, [_P, c_int]),
+    "geohip_ctx_set_range_order": (c_int, [_P, c_int]),
     "geohip_ctx_sync": (c_int, [_P]),
     "geohip_debug_lookback_inject": (c_int, [_P, c_int]),
     "geohip_ctx_timing": (c_int, [_P, POINTER(c_double), POINTER(c_uint64), c_int]),
@@ -465,6 +467,13 @@ class Context:
     def debug_lookback_inject(self, on: bool):
         """Test knob: range look-back waits give up (the fault path)."""
         self._check(lib.geohip_debug_lookback_inject(self.h, int(on)), "debug_lookback_inject")
+
+    def set_range_order(self, unordered: bool):
+        """geohip_ctx_set_range_order: False = ascending hit indices (the default), True = the
+        same set in any order (one pass, no ordered emission; the reference's window result is
+        a set)."""
+        self._check(lib.geohip_ctx_set_range_order(self.h, ORDER_ANY if unordered else ORDER_ASCENDING),
+                    "set_range_order")
 
     def set_timing(self, on: bool):
         self._check(lib.geohip_ctx_set_timing(self.h, int(on)), "set_timing")

@@ -122,6 +122,7 @@ struct geohip_ctx {
     PointPlan plan{};
     unsigned long long range_epoch = 0;  // fused range pass: status words of this launch carry it
     bool lb_inject = false;              // test knob: range look-back waits give up (geohip_debug_lookback_inject)
+    int range_order = GEOHIP_ORDER_ASCENDING;  // geohip_ctx_set_range_order
     unsigned long long lb_epoch = 0;     // chunk look-backs (ingest, point-polygon stream): status words of a launch carry it
     // host windows (GEOHIP_MEM_HOST): two pinned staging slots; the DMA of one slot runs on the
     // copy stream while the host fills the other (host_stage)
@@ -190,8 +191,10 @@ int ensure_zeroed(geohip_ctx* ctx, Slot s, size_t bytes) {
 }
 
 // The range look-back words (S_RLB): 256 block-count status words, then the arrival ticket, then
-// the fault word a wait that gives up sets.  Zeroed on allocation; the status words again when the
-// 24-bit epoch wraps (a word last written 2^24 - 1 launches ago must not read as ready).
+// the fault block (16 B), then the unordered range's reservation cursor (u64) and arrival count
+// (u32).  Zeroed on allocation; the status words again when the 24-bit epoch wraps (a word last
+// written 2^24 - 1 launches ago must not read as ready); the cursor and count are re-armed by the
+// last block of each launch.
 constexpr size_t kRlbBytes = 256 * 8 + 64;
 struct RangeLb {
     unsigned long long* status;
@@ -199,6 +202,7 @@ struct RangeLb {
     unsigned* fault;
     unsigned long long epoch;
     unsigned spins, inject;
+    RangeSetIo set;
 };
 int range_lookback(geohip_ctx* ctx, RangeLb* lb) {
     int rc = ensure_zeroed(ctx, S_RLB, kRlbBytes);
@@ -210,6 +214,8 @@ int range_lookback(geohip_ctx* ctx, RangeLb* lb) {
     lb->status = reinterpret_cast<unsigned long long*>(base);
     lb->ticket = reinterpret_cast<unsigned*>(base + 256 * 8);
     lb->fault = reinterpret_cast<unsigned*>(base + 256 * 8 + 16);
+    lb->set.cursor = reinterpret_cast<unsigned long long*>(base + 256 * 8 + 32);
+    lb->set.done = reinterpret_cast<unsigned*>(base + 256 * 8 + 40);
     lb->epoch = ctx->range_epoch;
     lb->spins = ctx->lb_inject ? 4096u : (1u << 22);  // kLookbackSpins (device_common.h): seconds
     lb->inject = ctx->lb_inject ? 1u : 0u;
@@ -584,6 +590,13 @@ int range_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x, con
     rc = range_lookback(ctx, &lb);
     if (rc) return rc;
     hipEvent_t e0, e1;
+    if (ctx->range_order == GEOHIP_ORDER_ANY) {  // one kernel, no look-back, no ordered emission
+        kernel_step_events(ctx, &e0, &e1);
+        hipError_t e = launch_range_set(dx, dy, n, a, approximate, lb.set, total, out, cap, (unsigned)ctx->cus,
+                                        ctx->stream, e0, e1);
+        if (e != hipSuccess) return hip_fail(ctx, e, "range launch");
+        return GEOHIP_OK;
+    }
     if (range_is_one_kernel(n)) kernel_step_events(ctx, &e0, &e1);
     else timing_events(ctx, &e0, &e1);
     hipError_t e = launch_range(dx, dy, n, a, approximate, B<unsigned long long>(ctx, S_MASK), B<unsigned>(ctx, S_UCNT),
@@ -753,6 +766,14 @@ int geohip_ctx_reset_stream(geohip_ctx* ctx) {
 }
 
 void* geohip_ctx_stream(geohip_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int geohip_ctx_set_range_order(geohip_ctx* ctx, int order) {
+    if (!ctx) return GEOHIP_ERR_ARG;
+    if (order != GEOHIP_ORDER_ASCENDING && order != GEOHIP_ORDER_ANY)
+        return fail(ctx, GEOHIP_ERR_ARG, "range order must be GEOHIP_ORDER_ASCENDING or GEOHIP_ORDER_ANY");
+    ctx->range_order = order;
+    return GEOHIP_OK;
+}
 
 int geohip_ctx_set_timing(geohip_ctx* ctx, int enable) {
     if (!ctx) return GEOHIP_ERR_ARG;

@@ -81,6 +81,15 @@ hipError_t launch_range(const double* x, const double* y, uint64_t n, const Rang
                         unsigned* out, uint64_t cap, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1,
                         unsigned long long* lb_status, unsigned* lb_ticket, unsigned long long epoch,
                         unsigned* lb_fault, unsigned lb_spins, unsigned lb_inject);
+// range with unordered-set output: io.cursor (u64) and io.done (u32) zero before the first
+// launch (each launch re-arms them); grid <= cus blocks
+struct RangeSetIo {
+    unsigned long long* cursor;
+    unsigned* done;
+};
+hipError_t launch_range_set(const double* x, const double* y, uint64_t n, const RangeArgs& a, int approximate,
+                            const RangeSetIo& io, uint64_t* total, unsigned* out, uint64_t cap, unsigned cus,
+                            hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_synth_uniform(double* x, double* y, uint64_t n, uint64_t base, uint64_t seed, double min_x,
                                 double max_x, double min_y, double max_y, hipStream_t st);
 hipError_t launch_selftest_fp64(const double* a, const double* b, uint64_t n, double* o_sqrt, double* o_div,

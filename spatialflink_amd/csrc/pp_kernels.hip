@@ -1936,6 +1936,160 @@ __global__ __launch_bounds__(kRangeNW * kWave) void range_fused(const double* __
     }
 }
 
+// ---- range with unordered-set output (geohip_ctx_set_range_order GEOHIP_ORDER_ANY) ---------
+// The reference's window result is a set: the window function collects the filter's hits as they
+// arrive from the parallel filter instances (PointPointRangeQuery.java:117-136), no order promised.
+// Without an order no hit waits for another block's count: every wave sweeps the window in one
+// grid-wide front (wave iteration gw, gw + W, ...: the blocks' stream ends bunch up, as in
+// knn_pass), its hits go to an LDS ring and leave in runs of kSetRun, each reserved with one
+// atomic on the launch's cursor while the stream goes on (~2.2M hits of a C1-shape window: ~4k
+// reservations spread over the stream).  At the end each block reserves its waves' remainders
+// with one atomic, and the last block to finish writes the total and re-arms the cursor.  The
+// decisions are range_fused's (G box -> hit; C box -> squared screens, then the exact distance).
+constexpr int kSetNW = 16;
+constexpr unsigned kSetRing = 1024;  // u32 hits per wave (4 KB); <= 511 + 319 pending at a check
+constexpr unsigned kSetRun = 512;    // hits per reservation
+constexpr unsigned kSetCand = 128;   // candidates per wave, flushed per slot at 64 (<= 63 + 64)
+
+template <bool APPROX>
+__global__ __launch_bounds__(kSetNW * kWave) void range_set(const double* __restrict__ x, const double* __restrict__ y,
+                                                            uint64_t n, RangeArgs a, RangeSetIo io,
+                                                            unsigned* __restrict__ out, uint64_t cap,
+                                                            uint64_t* __restrict__ total) {
+    __shared__ unsigned ring[kSetNW][kSetRing];
+    __shared__ double ccx[APPROX ? 1 : kSetNW][kSetCand], ccy[APPROX ? 1 : kSetNW][kSetCand];
+    __shared__ unsigned cci[APPROX ? 1 : kSetNW][kSetCand];
+    __shared__ unsigned s_left[kSetNW];
+    __shared__ unsigned long long s_base;
+    const int lane = lane_id(), wid = threadIdx.x / kWave;
+    unsigned* rg = ring[wid];
+    double* cx = ccx[APPROX ? 0 : wid];
+    double* cy = ccy[APPROX ? 0 : wid];
+    unsigned* ci = cci[APPROX ? 0 : wid];
+    const uint64_t W = (uint64_t)gridDim.x * kSetNW;
+    const uint64_t iters = (n + kPtsIter - 1) / kPtsIter;
+    unsigned hc = 0, hf = 0;  // hits pushed / stored (ring positions mod kSetRing)
+    unsigned ccnt = 0;
+    auto push = [&](bool hit, unsigned idx) {
+        const unsigned long long m = __ballot(hit);
+        if (hit) rg[(hc + lanes_below(m)) & (kSetRing - 1)] = idx + a.point_base;
+        hc += (unsigned)__popcll(m);
+    };
+    auto store_run = [&](unsigned long long b, unsigned m) {  // ring[hf, hf + m) -> out[b, b + m)
+        for (unsigned t = (unsigned)lane; t < m; t += kWave)
+            if (b + t < cap) out[b + t] = rg[(hf + t) & (kSetRing - 1)];
+        hf += m;
+    };
+    auto reserve = [&](unsigned m) {
+        unsigned lo = 0, hi = 0;
+        if (lane == 0) {
+            const unsigned long long b = atomicAdd(io.cursor, (unsigned long long)m);
+            lo = (unsigned)b;
+            hi = (unsigned)(b >> 32);
+        }
+        return ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)hi) << 32) |
+               (unsigned)__builtin_amdgcn_readfirstlane((int)lo);
+    };
+    auto cand_flush = [&]() {  // the newest <= 64 candidates: exact distance, hits pushed
+        const unsigned take = ccnt >= 64 ? 64u : ccnt;
+        const unsigned from = ccnt - take;
+        bool ok = (unsigned)lane < take;
+        double px = 0.0, py = 0.0;
+        unsigned pi = 0;
+        if (ok) {
+            px = cx[from + lane];
+            py = cy[from + lane];
+            pi = ci[from + lane];
+        }
+        wave_lds_sync();
+        ccnt = from;
+        ok = ok && (jts_pp_distance(a.qx, a.qy, px, py) <= a.r);
+        push(ok, pi);
+    };
+    const Box g0 = a.g[0], c0 = a.c;
+    uint64_t it = (uint64_t)blockIdx.x * kSetNW + (uint64_t)wid;
+    double px4[4], py4[4];
+    bool v4[4] = {false, false, false, false};
+    if (it < iters) load4(x, y, it * kPtsIter, n, lane, px4, py4, v4);
+    while (it < iters) {
+        const uint64_t base = it * kPtsIter;
+        const uint64_t nit = it + W;
+        double nx4[4], ny4[4];
+        bool nv[4] = {false, false, false, false};
+        if (nit < iters) load4(x, y, nit * kPtsIter, n, lane, nx4, ny4, nv);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; s4++) {
+            bool g = a.ng > 0 && in_box(g0, px4[s4], py4[s4]);
+            for (int b = 1; b < a.ng; b++) g = g || in_box(a.g[b], px4[s4], py4[s4]);
+            const bool cbox = !g && a.nc && in_box(c0, px4[s4], py4[s4]);
+            bool hit = v4[s4] && (g || (APPROX && cbox));
+            bool cand = false;
+            if (!APPROX && v4[s4] && cbox) {
+                const double dx = a.qx - px4[s4], dy = a.qy - py4[s4];
+                const double d2 = dx * dx + dy * dy;
+                if (d2 < a.r2lo) hit = true;
+                else if (!(d2 > a.r2hi)) cand = true;
+            }
+            const unsigned idx = (unsigned)slot_index(base, lane, s4);
+            push(hit, idx);
+            if (!APPROX) {
+                const unsigned long long m = __ballot(cand);
+                if (cand) {
+                    const unsigned pos = ccnt + lanes_below(m);
+                    cx[pos] = px4[s4];
+                    cy[pos] = py4[s4];
+                    ci[pos] = idx;
+                }
+                ccnt += (unsigned)__popcll(m);
+                if (ccnt >= 64) {
+                    wave_lds_sync();
+                    cand_flush();
+                }
+            }
+        }
+        if (hc - hf >= kSetRun) {  // a full run: reserved and stored while the next loads fly
+            wave_lds_sync();
+            store_run(reserve(kSetRun), kSetRun);
+        }
+#pragma unroll
+        for (int s4 = 0; s4 < 4; s4++) {
+            px4[s4] = nx4[s4];
+            py4[s4] = ny4[s4];
+            v4[s4] = nv[s4];
+        }
+        it = nit;
+    }
+    if (!APPROX) {
+        wave_lds_sync();
+        while (ccnt) cand_flush();
+    }
+    wave_lds_sync();
+    while (hc - hf >= kSetRun) store_run(reserve(kSetRun), kSetRun);
+    // the block's remainders: one reservation
+    const unsigned left = hc - hf;
+    if (lane == 0) s_left[wid] = left;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned sum = 0;
+        for (int w = 0; w < kSetNW; w++) sum += s_left[w];
+        s_base = sum ? atomicAdd(io.cursor, (unsigned long long)sum) : 0ull;
+    }
+    __syncthreads();
+    unsigned off = 0;
+    for (int w = 0; w < wid; w++) off += s_left[w];
+    if (left) store_run(s_base + off, left);
+    if (threadIdx.x == 0) {
+        __threadfence();  // this block's reservations before its arrival
+        const unsigned d = atomicAdd(io.done, 1u);
+        if (d == gridDim.x - 1) {  // every reservation is made: the total, then the re-arm
+            __threadfence();
+            *total = atomicAdd(io.cursor, 0ull);
+            __hip_atomic_store(io.cursor, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(io.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 // exclusive scan of unit counts by one workgroup; total -> *total
 __global__ __launch_bounds__(1024) void scan_units(const unsigned* __restrict__ cnt, uint64_t units,
                                                    uint64_t* __restrict__ offs, uint64_t* __restrict__ total) {
@@ -2304,6 +2458,22 @@ hipError_t launch_range(const double* x, const double* y, uint64_t n, const Rang
     if (e != hipSuccess) return e;
     range_emit<<<(unsigned)blocks, kBlock, 0, st>>>(bitmask, offs, units, out, cap, a.point_base);
     if (ev1) (void)hipEventRecord(ev1, st);  // timed region: all three kernels
+    return hipGetLastError();
+}
+
+hipError_t launch_range_set(const double* x, const double* y, uint64_t n, const RangeArgs& a, int approximate,
+                            const RangeSetIo& io, uint64_t* total, unsigned* out, uint64_t cap, unsigned cus,
+                            hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+    const uint64_t iters = (n + kPtsIter - 1) / kPtsIter;
+    if (iters == 0) return hipMemsetAsync(total, 0, sizeof(uint64_t), st);
+    // one block of 16 waves per CU (104 KB of LDS), fewer for small windows
+    const uint64_t want = (iters + kSetNW - 1) / kSetNW;
+    const unsigned nblocks = (unsigned)(want < cus ? want : cus);
+    const dim3 g(nblocks), b(kSetNW * kWave);
+    if (approximate)
+        hipExtLaunchKernelGGL(range_set<true>, g, b, 0, st, ev0, ev1, 0, x, y, n, a, io, out, cap, total);
+    else
+        hipExtLaunchKernelGGL(range_set<false>, g, b, 0, st, ev0, ev1, 0, x, y, n, a, io, out, cap, total);
     return hipGetLastError();
 }
 

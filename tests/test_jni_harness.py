@@ -66,6 +66,7 @@ class Jni:
             "abiVersion": (c_int32, E),
             "create": (c_int64, E + [c_int32]),
             "destroy": (None, E + [c_int64]),
+            "rangeOrder": (None, E + [c_int64, c_int32]),
             "rangePP": (J, E + [c_int64, J, J, J, c_int32, c_double, c_double, c_double, c_uint8]),
             "knnPP": (c_int32, E + [c_int64, J, J, J, c_int32, c_double, c_double, c_double, c_int32, J, J]),
             "knnRangePP": (J, E + [c_int64, J, J, J, c_int32, c_double, c_double, c_double, c_int32, c_uint8, J, J]),
@@ -193,9 +194,16 @@ def test_point_point_natives(jni_ctx):
     x, y = j.direct(hx), j.direct(hy)
     qx, qy = synth.README_QUERY
     n = len(hx)
+    want = sorted(cref.range_pp(cg, hx, hy, qx, qy, 0.3).tolist())
     r, exc = j.call("rangePP", h, g, x, y, n, qx, qy, 0.3, 0)
     assert exc is None
-    assert j.int_array(r).tolist() == sorted(cref.range_pp(cg, hx, hy, qx, qy, 0.3).tolist())
+    assert j.int_array(r).tolist() == want  # the default: ascending
+    _, exc = j.call("rangeOrder", h, 1)  # what the GeoHip constructor sets: the unordered set
+    assert exc is None
+    r, exc = j.call("rangePP", h, g, x, y, n, qx, qy, 0.3, 0)
+    assert exc is None and sorted(j.int_array(r).tolist()) == want
+    _, exc = j.call("rangeOrder", h, 5)
+    assert exc[0] == IAE
     k = 50
     oi, od = j.new_ints(k), j.new_doubles(k)
     cnt, exc = j.call("knnPP", h, g, x, y, n, qx, qy, 0.3, k, oi, od)
