@@ -607,24 +607,33 @@ class JoinWorkload(Workload):
     def cells_window(self, w):
         """One window in the north-star layout (PointPointJoinQuery.java:137-150): data points
         packed by owner key band (geohip_band_pack_async), one all-to-all, each owner joins its
-        band against the queries whose Nbr block meets it (halo replication)."""
+        band against the query window (geohip_join_pp_async into preallocated rows), the ranks'
+        pair counts in one device all-gather -- enqueue-only but for the shuffle's split sizes
+        (distributed.join_cells_enqueue)."""
+        import torch
         from spatialflink_amd import distributed as D
-        return D.join_sharded(self.dx[w], self.dy[w], self.rank * self.n, self.qx, self.qy, self.radius,
-                              grid_data=self.grid, grid_query=self.grid, ctx=self.ctx,
-                              partition="cells" if self.world > 1 else "arrival")
+        if getattr(self, "cout", None) is None:  # any rank's pairs <= the whole window's
+            cap = sum(self._gather_ints(max(self.pairs)))
+            self.cout = torch.empty((cap + 1, 2), dtype=torch.int32, device=self.dev)
+            self.ccount = torch.zeros(1, dtype=torch.int64, device=self.dev)
+            self.ccounts = torch.zeros(self.world, dtype=torch.int64, device=self.dev)
+        return D.join_cells_enqueue(self.dx[w], self.dy[w], self.rank * self.n, self.qx, self.qy, self.radius,
+                                    grid_data=self.grid, grid_query=self.grid, ctx=self.ctx, out=self.cout,
+                                    count=self.ccount, counts=self.ccounts)
 
     def cells_partition(self, steps):
         if self.world == 1:
             return None  # one band: the arrival line itself
         t, out = self._timed_side(lambda s: self.cells_window(s % self.windows), steps)
-        pairs, _, total = out
+        pairs, _, total = out.result()
         w = (steps - 1) % self.windows
         want = sum(self._gather_ints(self.pairs[w]))
         pr = self._gather_ints(len(pairs))
         mean = sum(pr) / len(pr)
         return {"value": self.n * self.world * steps / t, "unit": "points/sec", "ms_per_step": t / steps * 1e3,
                 "steps": steps, "layout": "grid-cell key bands: data points packed by owner band "
-                "(geohip_band_pack_async), all_to_all, halo query selection, owner's join",
+                "(geohip_band_pack_async), all_to_all, owner's join of its band against the query window "
+                "(geohip_join_pp_async), device all-gather of the pair counts",
                 "pairs_per_rank": pr, "skew_max_over_mean": (max(pr) / mean) if mean else None,
                 "matches_arrival_sharding": total == want}
 
@@ -652,7 +661,7 @@ class JoinWorkload(Workload):
         if self.args.partition != "cells":
             return None
         want = sum(self._gather_ints(self.pairs[last_step % self.windows]))
-        return (int(self.cells_last[2]) == want) if self.rank == 0 else None
+        return (int(self.cells_last.result()[2]) == want) if self.rank == 0 else None
 
     def algorithmic_bytes(self):
         return BYTES_PER_POINT * self.n + BYTES_PER_POINT * self.nq + 8 * float(np.mean(self.pairs))

@@ -135,9 +135,8 @@ int geohip_ctx_timing_kernels(geohip_ctx* ctx, double* step_ms, uint64_t* steps,
      GEOHIP_ERR_ARG       geohip_join_pp_async: a query key the reference cannot parse back
                           (NumberFormatException) or whose neighbour loop never ends
                           (UniformGrid.java:261-293) -- its results are incomplete,
-     GEOHIP_ERR_CAPACITY  geohip_range_ppoly_async / geohip_join_ppoly_async: the candidate buffer
-                          (sized from the previous call) overflowed; that call's pairs are
-                          incomplete and repeating it succeeds (the buffer is now sized for it).
+   (The point-polygon forms report no error for a short candidate buffer: the candidates past it
+   are decided in the stream, and the count they needed sizes the next call's buffer.)
    The synchronous calls check the look-back themselves. */
 int geohip_ctx_sync(geohip_ctx* ctx);
 int geohip_device_count(int* out_count);
@@ -317,10 +316,14 @@ int geohip_band_pack_async(geohip_ctx* ctx, const geohip_grid* grid_data, int32_
                            const double* x, const double* y, uint64_t n, int64_t base, double* out_x,
                            double* out_y, int64_t* out_idx, uint64_t* out_counts_dev);
 
-/* The same partition for a single point query (kNN / range of (qx, qy) with radius r on
-   grid_data): only the points of the query's guaranteed and candidate cells are kept -- the
-   reference filters them before its keyBy(gridID) (PointPointKNNQuery.java:137-151,
-   PointPointRangeQuery.java:102-116) -- then grouped by the owner of their key band as above. */
+/* The partition for a single point query (kNN / range of (qx, qy) with radius r on grid_data):
+   only the points of the query's guaranteed and candidate cells are kept -- the reference filters
+   them before its keyBy(gridID) (PointPointKNNQuery.java:137-151, PointPointRangeQuery.java:
+   102-116) -- then grouped by owner rank, where column cx belongs to rank (cx / bw) mod world,
+   bw = max(1, (2 Lc + 1) / (8 world)) with Lc = getCandidateNeighboringLayers(r)
+   (UniformGrid.java:440-444): the query's 2 Lc + 1 candidate columns are dealt round-robin in
+   blocks, as keyBy's key hashing spreads them (contiguous bands put one query's whole box on one
+   rank).  Otherwise as geohip_band_pack_async. */
 int geohip_band_pack_query_async(geohip_ctx* ctx, const geohip_grid* grid_data, int32_t nb, uint32_t world,
                                  double qx, double qy, double r, const double* x, const double* y, uint64_t n,
                                  int64_t base, double* out_x, double* out_y, int64_t* out_idx,

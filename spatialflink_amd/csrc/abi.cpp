@@ -191,9 +191,9 @@ int ensure_zeroed(geohip_ctx* ctx, Slot s, size_t bytes) {
 }
 
 // The range look-back words (S_RLB): 256 block-count status words, then the arrival ticket, then
-// the fault block (16 B), then the unordered range's reservation cursor (u64) and arrival count
-// (u32).  Zeroed on allocation; the status words again when the 24-bit epoch wraps (a word last
-// written 2^24 - 1 launches ago must not read as ready); the cursor and count are re-armed by the
+// the fault block (16 B), then the unordered range's reservation word (u64: hits << 20 | blocks
+// arrived).  Zeroed on allocation; the status words again when the 24-bit epoch wraps (a word last
+// written 2^24 - 1 launches ago must not read as ready); the reservation word is re-armed by the
 // last block of each launch.
 constexpr size_t kRlbBytes = 256 * 8 + 64;
 struct RangeLb {
@@ -214,8 +214,7 @@ int range_lookback(geohip_ctx* ctx, RangeLb* lb) {
     lb->status = reinterpret_cast<unsigned long long*>(base);
     lb->ticket = reinterpret_cast<unsigned*>(base + 256 * 8);
     lb->fault = reinterpret_cast<unsigned*>(base + 256 * 8 + 16);
-    lb->set.cursor = reinterpret_cast<unsigned long long*>(base + 256 * 8 + 32);
-    lb->set.done = reinterpret_cast<unsigned*>(base + 256 * 8 + 40);
+    lb->set.word = reinterpret_cast<unsigned long long*>(base + 256 * 8 + 32);
     lb->epoch = ctx->range_epoch;
     lb->spins = ctx->lb_inject ? 4096u : (1u << 22);  // kLookbackSpins (device_common.h): seconds
     lb->inject = ctx->lb_inject ? 1u : 0u;
@@ -254,16 +253,14 @@ int report_faults(geohip_ctx* ctx, unsigned mask = ~0u) {
         HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(fault_block(ctx)), (int)rest, 1, ctx->stream));
     else
         HIPCHK(hipMemsetAsync(fault_block(ctx), 0, 16, ctx->stream));
-    if (bits & kFaultCandOverflow) ppoly_note_cand_need(ctx, need);
+    if (bits & kFaultCandNeed) ppoly_note_cand_need(ctx, need);  // a sizing hint, not an error
     if (bits & kFaultLookback)
         return fail(ctx, GEOHIP_ERR_DEVICE, "range look-back wait gave up (a block count never arrived); results invalid");
     if (bits & kFaultQueryKey)
         return fail(ctx, GEOHIP_ERR_ARG, "async join: NumberFormatException in getIntCellIndices (query point key)");
     if (bits & kFaultQueryLoop)
         return fail(ctx, GEOHIP_ERR_ARG, "async join: reference neighbour loop does not terminate");
-    return fail(ctx, GEOHIP_ERR_CAPACITY, "async point-polygon call: candidate buffer overflow (" + std::to_string(need) +
-                                              " candidates), its pairs are incomplete; repeat the call (it now sizes "
-                                              "the buffer for them)");
+    return GEOHIP_OK;
 }
 
 int begin(geohip_ctx* ctx) {

@@ -46,12 +46,16 @@ struct BandArgs {
     double mnx, mny, l;
     int32_t nb, world;
     Box u[kMaxPointBoxes + 1];  // nu > 0: only points of the query's G u C cells (planner boxes)
-    int32_t nu, pad;
+    int32_t nu;
+    int32_t bw;                 // > 0: block-cyclic owners (column block cx / bw -> rank mod world)
 };
 
 // HelperClass.assignGridCellID (HelperClass.java:104-116) per axis, then the owner of the key's
-// column; -1 when the key is not a cell of the key space (or, with a query filter, when the
-// point lies in none of its guaranteed and candidate cells)
+// column -- its contiguous band (the join: a query's halo stays within few bands) or, for a single
+// point query, its column block dealt round-robin (the reference's keyBy(gridID) hashes keys; one
+// query's G u C box spans 2 Lc + 1 columns, which contiguous bands put on one rank); -1 when the
+// key is not a cell of the key space (or, with a query filter, when the point lies in none of its
+// guaranteed and candidate cells)
 __device__ __forceinline__ int band_owner(const BandArgs& a, uint64_t i) {
     if (a.nu) {
         bool in = false;
@@ -61,6 +65,7 @@ __device__ __forceinline__ int band_owner(const BandArgs& a, uint64_t i) {
     const int32_t cx = band_d2i(__builtin_floor((a.x[i] - a.mnx) / a.l));
     const int32_t cy = band_d2i(__builtin_floor((a.y[i] - a.mny) / a.l));
     if (cx < 0 || cy < 0 || cx >= a.nb || cy >= a.nb) return -1;
+    if (a.bw > 0) return (int)((cx / a.bw) % a.world);
     return (int)(((int64_t)cx * a.world) / a.nb);
 }
 
@@ -154,6 +159,15 @@ __global__ __launch_bounds__(kBandTB) void band_scatter(BandArgs a, const unsign
 
 }  // namespace
 
+// Column block width of the single-query layout: at least 8 blocks per rank across the query's
+// 2 Lc + 1 candidate columns (C5, Lc = 24: width 1 at 2..8 ranks), so each rank's share of the box
+// is within one block of the mean.
+int32_t query_block_width(int32_t layers_c, uint32_t world) {
+    const int64_t cols = 2 * (int64_t)(layers_c > 0 ? layers_c : 0) + 1;
+    const int64_t w = cols / (8 * (int64_t)world);
+    return (int32_t)(w > 1 ? (w < (1 << 20) ? w : (1 << 20)) : 1);
+}
+
 int band_pack_impl(geohip_ctx* ctx, const geohip_grid* grid, int32_t nb, uint32_t world, const double* x,
                    const double* y, uint64_t n, int64_t base, double* out_x, double* out_y, int64_t* out_idx,
                    uint64_t* out_counts, const PointPlan* filter) {
@@ -186,6 +200,7 @@ int band_pack_impl(geohip_ctx* ctx, const geohip_grid* grid, int32_t nb, uint32_
     if (filter) {
         for (int b = 0; b < filter->nu; b++) a.u[b] = filter->u[b];
         a.nu = filter->nu;
+        a.bw = query_block_width(filter->layers_c, world);
         if (a.nu == 0) {  // no candidate cell at all (r <= 0): nothing to send
             if (hipMemsetAsync(out_counts, 0, 8 * (size_t)world, st) != hipSuccess)
                 return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "memset failed");

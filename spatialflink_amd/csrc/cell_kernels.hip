@@ -2438,8 +2438,8 @@ struct StreamOut {
     unsigned point_base;            // added to every point index of a pair (pane stream positions)
     unsigned long long* ptotal;     // pairs: reservation cursor (zero before; an async call's count)
     unsigned long long* ctotal;     // candidates: reservation cursor (zero before)
-    unsigned* reruns;               // chunks whose LDS stage overflowed (run again, direct stores)
-    uint64_t ccap;                  // candidates past it are counted only (the host regrows, re-runs)
+    unsigned* flushes;              // wave stages flushed before their chunk's end (profiling count)
+    uint64_t ccap;                  // candidates past it are decided in the stream (exact test inline)
     unsigned* cpoly;                // candidates in chunk order: polygon (the grouping reads these),
     double4* crec;                  // and (x, y, point bits, -) -- one 32-byte sector per gather
 };
@@ -2460,20 +2460,26 @@ struct StreamArgs {
     int jmode;                      // 0 range, 1 join exact, 2 join approximate
     double r;
     StreamOut o;
+    // the rings, for candidates past the candidate buffer (decided in the stream, as
+    // ppoly_cand_eval decides the others)
+    const double* vx;
+    const double* vy;
+    const ring_id_t* vring;
+    const double* renv;
+    const uint16_t* slabs;
 };
 
-// one pair or candidate of the current chunk: staged in LDS (packed), or -- a chunk whose stage
-// overflowed, re-run once its bases are known -- stored straight to its global slot
-// Staged (the common case): each wave owns a region of the block's LDS stage and counts its
-// entries in a wave-uniform register -- no LDS atomic per push; the block sums the waves' counts at
-// the end of the chunk.  Direct (the overflow re-run): one LDS cursor for the block, global slots.
+// Pairs and candidates of the current chunk are staged in LDS (4 B each: poly << kLocalBits |
+// chunk-local point): each wave owns a region of the block's stage and counts its entries in a
+// wave-uniform register -- no LDS atomic per push.  The block reserves the waves' entries with one
+// atomic per kind at the chunk's end; a wave whose region fills before that (cells of many
+// polygons) flushes it with its own reservation and goes on -- no chunk is ever run twice (the
+// round-5 form re-ran an overflowing chunk with direct stores: every chunk of a window of 3000
+// overlapping polygons re-ran).
 struct StreamSink {
-    unsigned* pk;                   // staged: this wave's LDS region
-    unsigned* cursor;               // direct: the block's LDS counter
-    unsigned cap;                   // staged: region capacity (entries past it: overflow, counted)
-    bool direct;
-    unsigned long long base;        // direct: first global slot of the chunk
-    unsigned n;                     // staged: entries pushed by this wave (wave-uniform)
+    unsigned* pk;                   // this wave's LDS region
+    unsigned cap;                   // its capacity (a push adds <= 64)
+    unsigned n;                     // entries staged (wave-uniform)
 };
 
 __device__ __forceinline__ void stream_emit_pair(const StreamOut& o, unsigned long long p, unsigned poly, unsigned idx) {
@@ -2488,30 +2494,101 @@ __device__ __forceinline__ void stream_emit_pair(const StreamOut& o, unsigned lo
         o.out[2 * p + 1] = v.y;
     }
 }
-__device__ __forceinline__ void stream_emit_cand(const StreamArgs& a, unsigned long long p, unsigned poly, unsigned idx) {
-    if (p >= a.o.ccap) return;
-    a.o.cpoly[p] = poly;
-    a.o.crec[p] = make_double4(a.x[idx], a.y[idx], __longlong_as_double((long long)idx), 0.0);
+
+// one global reservation of m slots on *total by lane 0, broadcast (wave-uniform)
+__device__ __forceinline__ unsigned long long wave_reserve(unsigned long long* total, unsigned m) {
+    unsigned lo = 0, hi = 0;
+    if (lane_id() == 0) {
+        const unsigned long long b = atomicAdd(total, (unsigned long long)m);
+        lo = (unsigned)b;
+        hi = (unsigned)(b >> 32);
+    }
+    return ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)hi) << 32) |
+           (unsigned)__builtin_amdgcn_readfirstlane((int)lo);
 }
 
-// wave-uniform: the lanes with `hit` add (poly, chunk-local point) to the sink
-template <bool CAND>
-__device__ __forceinline__ void stream_push(const StreamArgs& a, StreamSink& k, bool hit, unsigned poly, unsigned loc,
-                                            uint64_t chunk0) {
-    const unsigned long long m = __ballot(hit);
-    if (!m) return;
-    if (!k.direct) {
-        const unsigned b = k.n + lanes_below(m);
-        if (hit && b < k.cap) k.pk[b] = (poly << kLocalBits) | loc;
-        k.n += (unsigned)__popcll(m);
-        return;
+// A candidate (poly, window index idx) stored at slot p of the candidate buffer, or -- past its
+// capacity (the buffer is sized from the previous call's count) -- decided here by the exact test
+// ppoly_cand_eval would run (PointPolygonRangeQuery.java:116, DistanceFunctions.java:33-36); the
+// result says whether it is a pair.  Rare by construction, so this path stays out of the way.
+__device__ __noinline__ bool stream_cand_exact(const StreamArgs& a, unsigned poly, unsigned idx) {
+    const PolyDev P = a.polys[poly];
+    const double px = a.x[idx], py = a.y[idx];
+    const SlabView sv{a.slabs + P.loff, P.ns};
+    return P.nring > 1 ? point_polygon_within_rings(px, py, a.vx + P.voff, a.vy + P.voff, a.vring + P.voff,
+                                                    a.renv + 4 * (size_t)P.eoff, P, sv, a.r)
+                       : point_polygon_within(px, py, a.vx + P.voff, a.vy + P.voff, P, sv, a.r);
+}
+
+// entries [0, m) of a staged region (chunk c0) to their slots from base on (wave-cooperative)
+__device__ __forceinline__ void stream_store_pairs(const StreamArgs& a, const unsigned* pk, unsigned m,
+                                                   unsigned long long base, uint64_t c0) {
+    for (unsigned t = (unsigned)lane_id(); t < m; t += kWave) {
+        const unsigned v = pk[t];
+        stream_emit_pair(a.o, base + t, v >> kLocalBits, (unsigned)(c0 + (v & (kStreamChunk - 1))));
     }
-    unsigned b = 0;
-    if (lane_id() == 0) b = atomicAdd(k.cursor, (unsigned)__popcll(m));  // every lane is active here
-    b = (unsigned)__builtin_amdgcn_readfirstlane((int)b) + lanes_below(m);
-    if (!hit) return;
-    if (CAND) stream_emit_cand(a, k.base + b, poly, (unsigned)(chunk0 + loc));
-    else stream_emit_pair(a.o, k.base + b, poly, (unsigned)(chunk0 + loc));
+}
+__device__ __forceinline__ void stream_store_cands(const StreamArgs& a, const unsigned* pk, unsigned m,
+                                                   unsigned long long base, uint64_t c0) {
+    const bool past = base + m > a.o.ccap;  // wave-uniform
+    for (unsigned t0 = 0; t0 < m; t0 += kWave) {
+        const unsigned t = t0 + (unsigned)lane_id();
+        unsigned poly = 0, idx = 0;
+        bool exact = false;
+        if (t < m) {
+            const unsigned v = pk[t];
+            poly = v >> kLocalBits;
+            idx = (unsigned)(c0 + (v & (kStreamChunk - 1)));
+            const unsigned long long p = base + t;
+            if (p < a.o.ccap) {
+                a.o.cpoly[p] = poly;
+                a.o.crec[p] = make_double4(a.x[idx], a.y[idx], __longlong_as_double((long long)idx), 0.0);
+            } else {
+                exact = true;
+            }
+        }
+        if (past) {  // the buffer is full: these candidates are decided now, their pairs reserved here
+            const bool hit = exact && stream_cand_exact(a, poly, idx);
+            const unsigned long long mh = __ballot(hit);
+            if (mh) {
+                const unsigned long long pb = wave_reserve(a.o.ptotal, (unsigned)__popcll(mh));
+                if (hit) stream_emit_pair(a.o, pb + lanes_below(mh), poly, idx);
+            }
+        }
+    }
+}
+
+// a wave's region flushed before the chunk's end: its own reservation, then the stores
+template <bool CAND>
+__device__ __forceinline__ void stream_flush(const StreamArgs& a, StreamSink& k, uint64_t c0) {
+    wave_lds_sync();
+    const unsigned long long b = wave_reserve(CAND ? a.o.ctotal : a.o.ptotal, k.n);
+    if (CAND) stream_store_cands(a, k.pk, k.n, b, c0);
+    else stream_store_pairs(a, k.pk, k.n, b, c0);
+    if (lane_id() == 0) atomicAdd(a.o.flushes, 1u);
+    wave_lds_sync();
+    k.n = 0;
+}
+
+// wave-uniform: lanes with `hit` stage a pair, lanes with `need` a candidate (never both):
+// two ballots, one LDS store per lane
+template <bool CANDS>
+__device__ __forceinline__ void stream_push(const StreamArgs& a, StreamSink& ps, StreamSink& cs, bool hit, bool need,
+                                            unsigned poly, unsigned loc, uint64_t c0) {
+    const unsigned long long mp = __ballot(hit);
+    const unsigned long long mc = CANDS ? __ballot(need) : 0ull;
+    if (!(mp | mc)) return;
+    const unsigned w = (poly << kLocalBits) | loc;
+    if (CANDS) {
+        unsigned* dst = hit ? ps.pk + ps.n + lanes_below(mp) : cs.pk + cs.n + lanes_below(mc);
+        if (hit || need) *dst = w;
+    } else if (hit) {
+        ps.pk[ps.n + lanes_below(mp)] = w;
+    }
+    ps.n += (unsigned)__popcll(mp);
+    if (CANDS) cs.n += (unsigned)__popcll(mc);
+    if (ps.n > ps.cap - kWave) stream_flush<false>(a, ps, c0);
+    if (CANDS && cs.n > cs.cap - kWave) stream_flush<true>(a, cs, c0);
 }
 
 // Entry balance of the exact walk (round 5; it replaced each lane walking its own points' entries
@@ -2662,8 +2739,7 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
                 bool hit = false, need = false;
                 if (!multi) stream_decide(h.x, h.y, st[t] >> (8 * sl), hit, need);
                 const unsigned loc = loc_of(t, sl);
-                stream_push<false>(a, ps, hit, h.x & ~kEntC, loc, c0);
-                stream_push<true>(a, cs, need, h.x & ~kEntC, loc, c0);
+                stream_push<true>(a, ps, cs, hit, need, h.x & ~kEntC, loc, c0);
             }
             const unsigned ic = wave_incl_scan(lc), in = wave_incl_scan(ln);
             const unsigned T = (unsigned)__builtin_amdgcn_readlane((int)ic, kWave - 1);
@@ -2681,8 +2757,7 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
                         if (e < e1) en = a.ent[e++];
                         bool hit, need;
                         stream_decide(en.x, en.y, sw, hit, need);
-                        stream_push<false>(a, ps, hit, en.x & ~kEntC, loc, c0);
-                        stream_push<true>(a, cs, need, en.x & ~kEntC, loc, c0);
+                        stream_push<true>(a, ps, cs, hit, need, en.x & ~kEntC, loc, c0);
                     }
                 }
                 continue;
@@ -2726,8 +2801,7 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
                     bool hit, need;
                     stream_decide(en[u].x, en[u].y, ry[u] >> 12, hit, need);
                     const unsigned loc = ry[u] & (kStreamChunk - 1);
-                    stream_push<false>(a, ps, hit, en[u].x & ~kEntC, loc, c0);
-                    stream_push<true>(a, cs, need, en[u].x & ~kEntC, loc, c0);
+                    stream_push<true>(a, ps, cs, hit, need, en[u].x & ~kEntC, loc, c0);
                 }
             }
             wave_lds_sync();  // the records and bitmap are reused by the next iteration
@@ -2784,8 +2858,7 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
                         ex = kNoEntry;
                     }
                 }
-                stream_push<false>(a, ps, hit, poly, loc, c0);
-                if (!APPROX) stream_push<true>(a, cs, need, poly, loc, c0);
+                stream_push<!APPROX>(a, ps, cs, hit, need, poly, loc, c0);
             }
         }
         // points outside the grid against the polygons whose rectangles reach outside it (rare)
@@ -2807,8 +2880,7 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
                         in = a.jmode == 1 ? in_rects(a.rects + 4 * P.coff, P.nc, cx, cy)
                                           : in_rects(a.rects + 4 * P.goff, P.ng, cx, cy);
                     const bool dist = !APPROX && a.jmode == 1;
-                    stream_push<false>(a, ps, in && !dist, p, loc_of(t, s), c0);
-                    if (!APPROX) stream_push<true>(a, cs, in && dist, p, loc_of(t, s), c0);
+                    stream_push<!APPROX>(a, ps, cs, in && !dist, in && dist, p, loc_of(t, s), c0);
                 }
             }
         }
@@ -2826,7 +2898,6 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
     __shared__ unsigned kl[KL ? kKeepLds : 1];
     __shared__ unsigned ppk[kSPairCap];
     __shared__ unsigned cpk[APPROX ? 1 : kSCandCap];
-    __shared__ unsigned s_np, s_nc;
     __shared__ unsigned s_wp[kStreamNW], s_wc[kStreamNW];  // per-wave staged counts
     __shared__ unsigned long long s_pb, s_cb;
     constexpr bool kBal = !APPROX;
@@ -2866,8 +2937,8 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
         __syncthreads();  // the previous chunk's stage is drained (and the bitmap staged)
         const uint64_t c0 = (uint64_t)vb * kStreamChunk;
         const uint64_t c1 = c0 + kStreamChunk < a.n ? c0 + kStreamChunk : a.n;
-        StreamSink ps{ppk + wid * kWPair, &s_np, kWPair, false, 0, 0u};
-        StreamSink cs{cpk + (APPROX ? 0 : wid * kWCand), &s_nc, APPROX ? 0u : kWCand, false, 0, 0u};
+        StreamSink ps{ppk + wid * kWPair, kWPair, 0u};
+        StreamSink cs{cpk + (APPROX ? 0 : wid * kWCand), APPROX ? kWave : kWCand, 0u};
         uint2* wrec = kBal ? brec + wid * kBalRecs : brec;
         unsigned long long* wbm = kBal ? bbm + wid * kBalWords : bbm;
         stream_chunk<APPROX, KL>(a, kl, c0, c1, ps, cs, wrec, wbm, &pre);
@@ -2878,11 +2949,9 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
         }
         __syncthreads();
         unsigned np = 0, nc = 0, pex = 0, cex = 0;  // totals; this wave's offsets in the chunk
-        bool over = false;
 #pragma unroll
         for (int w = 0; w < kStreamNW; w++) {
             const unsigned wp = s_wp[w], wc = s_wc[w];
-            over |= wp > kWPair || wc > (APPROX ? 0u : kWCand);
             pex += w < wid ? wp : 0u;
             cex += w < wid ? wc : 0u;
             np += wp;
@@ -2893,33 +2962,9 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
             s_cb = nc ? atomicAdd(a.o.ctotal, (unsigned long long)nc) : 0ull;
         }
         __syncthreads();
-        const unsigned long long pb = s_pb, cb = s_cb;
-        if (!over) {  // each wave stores its own region: coalesced runs of the output
-            const unsigned* wpk = ppk + wid * kWPair;
-            for (unsigned t = (unsigned)lane; t < ps.n; t += kWave) {
-                const unsigned v = wpk[t];
-                stream_emit_pair(a.o, pb + pex + t, v >> kLocalBits, (unsigned)(c0 + (v & (kStreamChunk - 1))));
-            }
-            if (!APPROX) {
-                const unsigned* wck = cpk + wid * kWCand;
-                for (unsigned t = (unsigned)lane; t < cs.n; t += kWave) {
-                    const unsigned v = wck[t];
-                    stream_emit_cand(a, cb + cex + t, v >> kLocalBits, (unsigned)(c0 + (v & (kStreamChunk - 1))));
-                }
-            }
-        } else {  // overflow (many polygons per cell): the chunk again, straight to its slots
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                s_np = 0;
-                s_nc = 0;
-                atomicAdd(a.o.reruns, 1u);
-            }
-            __syncthreads();
-            StreamSink pd{ppk, &s_np, kSPairCap, true, pb, 0u};
-            StreamSink cd{cpk, &s_nc, kSCandCap, true, cb, 0u};
-            stream_chunk<APPROX, KL>(a, kl, c0, c1, pd, cd, kBal ? brec + wid * kBalRecs : brec,
-                                     kBal ? bbm + wid * kBalWords : bbm, nullptr);
-        }
+        // each wave stores its own region: coalesced runs of the output
+        stream_store_pairs(a, ppk + wid * kWPair, ps.n, s_pb + pex, c0);
+        if (!APPROX) stream_store_cands(a, cpk + wid * kWCand, cs.n, s_cb + cex, c0);
     }
 }
 
@@ -2965,7 +3010,7 @@ struct CandGroup {
     const unsigned long long* ccount;  // candidate total (StreamOut::ctotal, or the refined count)
     const unsigned long long* cstream; // the stream's candidate total (the capacity check)
     uint64_t ccap;
-    unsigned* fault;                   // async calls: the ctx's fault word (kFaultCandOverflow), else null
+    unsigned* fault;                   // async calls: the ctx's fault word (kFaultCandNeed), else null
     unsigned long long* need;          // async calls: the candidate count an overflowing call needed
     const unsigned* cpoly;
     const double4* crec;
@@ -3076,11 +3121,11 @@ __global__ __launch_bounds__(kCandThreads) void ppoly_cand_plan(CandGroup c) {
     const unsigned carry_i = F + carry_p;
     if (threadIdx.x == 0) {
         *c.nitems = carry_i;
-        // an async call cannot rerun with a larger buffer: the overflow (the candidates past ccap
-        // are untested, the pairs incomplete) and the size it needed go to the ctx's fault block
+        // a short candidate buffer (the candidates past it were decided in the stream): the size
+        // it needed goes to the ctx's fault block as a hint, so the next async call sizes it
         const unsigned long long nc = *c.cstream;
         if (c.fault && nc > c.ccap) {
-            atomicOr(c.fault, kFaultCandOverflow);
+            atomicOr(c.fault, kFaultCandNeed);
             atomicMax(c.need, nc);
         }
     }
@@ -5348,8 +5393,11 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             rc = ctx_fault_block(ctx, &fault);
             if (rc) return rc;
         }
-        for (int attempt = 0; attempt < 3; attempt++) {
-            // J_MISC: [0..1] pair total, [2..3] candidate total, [4] work items, [5] re-runs, [6] eval ticket
+        {
+            // one pass: candidates past ccap are decided in the stream (stream_store_cands), the
+            // count they needed sizes the next call's buffer
+            // J_MISC: [0..1] pair total, [2..3] candidate total, [4] work items, [5] early wave
+            // flushes, [6] eval ticket
             unsigned* misc = S.get<unsigned>(J_MISC, kMiscWords * 4);
             unsigned* mat = cands ? S.get<unsigned>(J_HIST, ((size_t)kCandGroups + 2) * npoly * 4 + 16) : nullptr;
             void* cbuf = cands ? S.get<void>(J_SY, ccap * 36 + 64) : nullptr;
@@ -5371,7 +5419,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             so.aligned8 = ((uintptr_t)out & 7u) == 0;
             so.swap = join ? 1 : 0;
             so.point_base = point_base;
-            so.reruns = misc + 5;  // zeroed with the totals
+            so.flushes = misc + 5;  // zeroed with the totals
             so.ptotal = async ? reinterpret_cast<unsigned long long*>(count_dev) : reinterpret_cast<unsigned long long*>(misc);
             so.ctotal = reinterpret_cast<unsigned long long*>(misc) + 1;
             so.ccap = cands ? ccap : 0;
@@ -5394,6 +5442,11 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             sa.jmode = jmode;
             sa.r = r;
             sa.o = so;
+            sa.vx = dvx;
+            sa.vy = dvy;
+            sa.vring = dvr;
+            sa.renv = denv;
+            sa.slabs = dslab;
             if (nchunks) {
                 const unsigned nblk = (unsigned)std::min<uint64_t>(nchunks, (uint64_t)ctx_cus(ctx) * kStreamBlocksPerCU);
                 // the cell bitmap staged in LDS (from global memory: 516 against 460 us; none: 487)
@@ -5454,20 +5507,19 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             tot = pin[0];
             const uint64_t ncand = pin[1];
             pc->last_cand = ncand;
-            if (prof && attempt == 0)
+            if (prof)
                 fprintf(stderr, "ppoly host: plan %.1f us (cached %d), %zu refined cells, class table %zu cells\n",
                         std::chrono::duration<double, std::micro>(t_planned - t_start).count(), (int)cached,
                         (size_t)std::count_if(pc->hrf.begin(), pc->hrf.end(), [](uint32_t v) { return v != kNoRefine; }) / 2,
                         pc->hcls.size());
-            if (prof && attempt == 0)
+            if (prof)
                 fprintf(stderr, "ppoly host: refinement words %zu (parts) + %zu (sub-parts)\n", pc->hrfw.size() / 2,
                         pc->hrfw2.size());
-            if (prof) fprintf(stderr, "ppoly stream: %llu pairs, %llu candidates (capacity %llu), %u of %llu chunks re-run\n",
-                              (unsigned long long)tot, (unsigned long long)ncand, (unsigned long long)ccap, (unsigned)(pin[2] >> 32),
+            if (prof) fprintf(stderr, "ppoly stream: %llu pairs, %llu candidates (capacity %llu: %llu decided in the stream), "
+                              "%u early wave flushes over %llu chunks, one pass\n",
+                              (unsigned long long)tot, (unsigned long long)ncand, (unsigned long long)ccap,
+                              (unsigned long long)(ncand > ccap ? ncand - ccap : 0), (unsigned)(pin[2] >> 32),
                               (unsigned long long)nchunks);
-            if (ncand <= ccap) break;
-            if (attempt == 2) return ctx_fail(ctx, GEOHIP_ERR_DEVICE, "candidate buffer did not converge");
-            ccap = ncand + ncand / 4 + 1024;  // grown to the counted need: the step runs again
         }
         *out_count = tot;
         if (!dev && cap) {

@@ -15,7 +15,8 @@ namespace geohip {
 constexpr unsigned kFaultLookback = 1u;       // a look-back wait gave up (GEOHIP_ERR_DEVICE)
 constexpr unsigned kFaultQueryKey = 2u;       // join query key: NumberFormatException (GEOHIP_ERR_ARG)
 constexpr unsigned kFaultQueryLoop = 4u;      // join query block: a loop that never ends (GEOHIP_ERR_ARG)
-constexpr unsigned kFaultCandOverflow = 8u;   // point-polygon candidate buffer overflow (GEOHIP_ERR_CAPACITY)
+constexpr unsigned kFaultCandNeed = 8u;       // point-polygon: the candidate buffer was short (a hint, not an
+                                              // error: the stream decided the rest; the size it needed)
 
 // context services implemented in abi.cpp
 int ctx_fail(geohip_ctx* ctx, int code, const std::string& msg);

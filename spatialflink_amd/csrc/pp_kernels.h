@@ -81,11 +81,10 @@ hipError_t launch_range(const double* x, const double* y, uint64_t n, const Rang
                         unsigned* out, uint64_t cap, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1,
                         unsigned long long* lb_status, unsigned* lb_ticket, unsigned long long epoch,
                         unsigned* lb_fault, unsigned lb_spins, unsigned lb_inject);
-// range with unordered-set output: io.cursor (u64) and io.done (u32) zero before the first
-// launch (each launch re-arms them); grid <= cus blocks
+// range with unordered-set output: io.word = (hits reserved << 20) | blocks arrived, zero before
+// the first launch (each launch's last block re-arms it); grid <= min(cus, 2^20 - 1) blocks
 struct RangeSetIo {
-    unsigned long long* cursor;
-    unsigned* done;
+    unsigned long long* word;
 };
 hipError_t launch_range_set(const double* x, const double* y, uint64_t n, const RangeArgs& a, int approximate,
                             const RangeSetIo& io, uint64_t* total, unsigned* out, uint64_t cap, unsigned cus,

@@ -1939,56 +1939,50 @@ __global__ __launch_bounds__(kRangeNW * kWave) void range_fused(const double* __
 // ---- range with unordered-set output (geohip_ctx_set_range_order GEOHIP_ORDER_ANY) ---------
 // The reference's window result is a set: the window function collects the filter's hits as they
 // arrive from the parallel filter instances (PointPointRangeQuery.java:117-136), no order promised.
-// Without an order no hit waits for another block's count: every wave sweeps the window in one
+// Without an order no block waits for another block's count: every wave sweeps the window in one
 // grid-wide front (wave iteration gw, gw + W, ...: the blocks' stream ends bunch up, as in
-// knn_pass), its hits go to an LDS ring and leave in runs of kSetRun, each reserved with one
-// atomic on the launch's cursor while the stream goes on (~2.2M hits of a C1-shape window: ~4k
-// reservations spread over the stream).  At the end each block reserves its waves' remainders
-// with one atomic, and the last block to finish writes the total and re-arms the cursor.  The
-// decisions are range_fused's (G box -> hit; C box -> squared screens, then the exact distance).
+// knn_pass), its hits go to an LDS buffer, and at the end each block reserves its waves' hits with
+// ONE atomic and the waves store them (full 64-lane stores).  A wave whose buffer fills first
+// reserves and stores a run of kSetRun on its own.  One device-scope word serves a few tens of
+// returning atomics per microsecond (MI355X_MICROARCH.md "dequeue": ~88/us), so runs are long
+// (a first form with 512-hit runs, ~4.3k reservations per C1-shape window, ran 67 us against 48 for
+// the ordered pass) and the block's final reservation doubles as its arrival count: the word holds
+// (hits << 20) | blocks arrived, and the block whose add completes the count writes the total and
+// re-arms the word for the next launch.  The decisions are range_fused's (G box -> hit; C box ->
+// squared screens, then the exact distance).
 constexpr int kSetNW = 16;
-constexpr unsigned kSetRing = 1024;  // u32 hits per wave (4 KB); <= 511 + 319 pending at a check
-constexpr unsigned kSetRun = 512;    // hits per reservation
+constexpr unsigned kSetRun = 1024;   // hits per early reservation
+constexpr unsigned kSetBuf = 1408;   // u32 hits per wave: <= 1023 + 319 pending at a check (5.5 KB)
 constexpr unsigned kSetCand = 128;   // candidates per wave, flushed per slot at 64 (<= 63 + 64)
+constexpr unsigned kSetArrivalBits = 20;
 
 template <bool APPROX>
 __global__ __launch_bounds__(kSetNW * kWave) void range_set(const double* __restrict__ x, const double* __restrict__ y,
                                                             uint64_t n, RangeArgs a, RangeSetIo io,
                                                             unsigned* __restrict__ out, uint64_t cap,
                                                             uint64_t* __restrict__ total) {
-    __shared__ unsigned ring[kSetNW][kSetRing];
+    __shared__ unsigned hbuf[kSetNW][kSetBuf];
     __shared__ double ccx[APPROX ? 1 : kSetNW][kSetCand], ccy[APPROX ? 1 : kSetNW][kSetCand];
     __shared__ unsigned cci[APPROX ? 1 : kSetNW][kSetCand];
     __shared__ unsigned s_left[kSetNW];
     __shared__ unsigned long long s_base;
     const int lane = lane_id(), wid = threadIdx.x / kWave;
-    unsigned* rg = ring[wid];
+    unsigned* hb = hbuf[wid];
     double* cx = ccx[APPROX ? 0 : wid];
     double* cy = ccy[APPROX ? 0 : wid];
     unsigned* ci = cci[APPROX ? 0 : wid];
     const uint64_t W = (uint64_t)gridDim.x * kSetNW;
     const uint64_t iters = (n + kPtsIter - 1) / kPtsIter;
-    unsigned hc = 0, hf = 0;  // hits pushed / stored (ring positions mod kSetRing)
+    unsigned hc = 0;  // hits staged (wave-uniform)
     unsigned ccnt = 0;
     auto push = [&](bool hit, unsigned idx) {
         const unsigned long long m = __ballot(hit);
-        if (hit) rg[(hc + lanes_below(m)) & (kSetRing - 1)] = idx + a.point_base;
+        if (hit) hb[hc + lanes_below(m)] = idx + a.point_base;
         hc += (unsigned)__popcll(m);
     };
-    auto store_run = [&](unsigned long long b, unsigned m) {  // ring[hf, hf + m) -> out[b, b + m)
+    auto store = [&](unsigned long long b, unsigned from, unsigned m) {  // hb[from, from + m) -> out[b, b + m)
         for (unsigned t = (unsigned)lane; t < m; t += kWave)
-            if (b + t < cap) out[b + t] = rg[(hf + t) & (kSetRing - 1)];
-        hf += m;
-    };
-    auto reserve = [&](unsigned m) {
-        unsigned lo = 0, hi = 0;
-        if (lane == 0) {
-            const unsigned long long b = atomicAdd(io.cursor, (unsigned long long)m);
-            lo = (unsigned)b;
-            hi = (unsigned)(b >> 32);
-        }
-        return ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)hi) << 32) |
-               (unsigned)__builtin_amdgcn_readfirstlane((int)lo);
+            if (b + t < cap) out[b + t] = hb[from + t];
     };
     auto cand_flush = [&]() {  // the newest <= 64 candidates: exact distance, hits pushed
         const unsigned take = ccnt >= 64 ? 64u : ccnt;
@@ -2047,9 +2041,27 @@ __global__ __launch_bounds__(kSetNW * kWave) void range_set(const double* __rest
                 }
             }
         }
-        if (hc - hf >= kSetRun) {  // a full run: reserved and stored while the next loads fly
+        if (hc >= kSetRun) {  // rare (dense hits): a run of its own, the rest moved to the front
             wave_lds_sync();
-            store_run(reserve(kSetRun), kSetRun);
+            unsigned lo = 0, hi = 0;
+            if (lane == 0) {
+                const unsigned long long b = atomicAdd(io.word, (unsigned long long)kSetRun << kSetArrivalBits);
+                lo = (unsigned)b;
+                hi = (unsigned)(b >> 32);
+            }
+            const unsigned long long w = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)hi) << 32) |
+                                         (unsigned)__builtin_amdgcn_readfirstlane((int)lo);
+            store(w >> kSetArrivalBits, 0, kSetRun);
+            wave_lds_sync();
+            const unsigned rest = hc - kSetRun;
+            for (unsigned t0 = 0; t0 < rest; t0 += kWave) {
+                const unsigned t = t0 + (unsigned)lane;
+                const unsigned v = t < rest ? hb[kSetRun + t] : 0u;
+                wave_lds_sync();
+                if (t < rest) hb[t] = v;
+                wave_lds_sync();
+            }
+            hc = rest;
         }
 #pragma unroll
         for (int s4 = 0; s4 < 4; s4++) {
@@ -2063,31 +2075,24 @@ __global__ __launch_bounds__(kSetNW * kWave) void range_set(const double* __rest
         wave_lds_sync();
         while (ccnt) cand_flush();
     }
-    wave_lds_sync();
-    while (hc - hf >= kSetRun) store_run(reserve(kSetRun), kSetRun);
-    // the block's remainders: one reservation
-    const unsigned left = hc - hf;
-    if (lane == 0) s_left[wid] = left;
+    // the block's hits: one reservation, which is also its arrival
+    if (lane == 0) s_left[wid] = hc;
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned sum = 0;
         for (int w = 0; w < kSetNW; w++) sum += s_left[w];
-        s_base = sum ? atomicAdd(io.cursor, (unsigned long long)sum) : 0ull;
+        const unsigned long long old =
+            atomicAdd(io.word, ((unsigned long long)sum << kSetArrivalBits) | 1ull);
+        s_base = old >> kSetArrivalBits;
+        if ((unsigned)(old & ((1u << kSetArrivalBits) - 1)) == gridDim.x - 1) {  // every block has reserved
+            *total = (old >> kSetArrivalBits) + sum;
+            __hip_atomic_store(io.word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+        }
     }
     __syncthreads();
     unsigned off = 0;
     for (int w = 0; w < wid; w++) off += s_left[w];
-    if (left) store_run(s_base + off, left);
-    if (threadIdx.x == 0) {
-        __threadfence();  // this block's reservations before its arrival
-        const unsigned d = atomicAdd(io.done, 1u);
-        if (d == gridDim.x - 1) {  // every reservation is made: the total, then the re-arm
-            __threadfence();
-            *total = atomicAdd(io.cursor, 0ull);
-            __hip_atomic_store(io.cursor, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(io.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
+    store(s_base + off, 0, hc);
 }
 
 // exclusive scan of unit counts by one workgroup; total -> *total
@@ -2466,7 +2471,7 @@ hipError_t launch_range_set(const double* x, const double* y, uint64_t n, const 
                             hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
     const uint64_t iters = (n + kPtsIter - 1) / kPtsIter;
     if (iters == 0) return hipMemsetAsync(total, 0, sizeof(uint64_t), st);
-    // one block of 16 waves per CU (104 KB of LDS), fewer for small windows
+    // one block of 16 waves per CU (128 KB of LDS), fewer for small windows
     const uint64_t want = (iters + kSetNW - 1) / kSetNW;
     const unsigned nblocks = (unsigned)(want < cus ? want : cus);
     const dim3 g(nblocks), b(kSetNW * kWave);

@@ -109,10 +109,23 @@ def _java_cell(v, mn: float, l: float):
     return t.clamp(-2147483648.0, 2147483647.0).to(torch.int64)
 
 
-def torch_band_pack(grid_data, keep=None):
+def query_block_width(grid_data, qx: float, qy: float, r: float, world: int) -> int:
+    """Column block width of the single-query key layout (geohip_band_pack_query_async): at least
+    8 blocks per rank across the query's 2 Lc + 1 candidate columns (Lc =
+    UniformGrid.getCandidateNeighboringLayers, UniformGrid.java:440-444)."""
+    from . import _abi
+    try:
+        lc = max(_abi.plan_point(grid_data, qx, qy, r)[3], 0)
+    except _abi.GeohipError:
+        lc = 0
+    return max(1, min((2 * lc + 1) // (8 * world), 1 << 20))
+
+
+def torch_band_pack(grid_data, keep=None, bw: int = 0):
     """band_pack written with torch ops (CPU orchestration tests; the product engine is
     geohip_band_pack_async): same owners, same arrival order inside each owner group.
-    keep(x, y) -> bool mask: an extra filter (the query's G u C cells for band_pack_query)."""
+    keep(x, y) -> bool mask: an extra filter (the query's G u C cells for band_pack_query).
+    bw > 0: block-cyclic owners (cx // bw) % world (the single-query layout)."""
     import torch
 
     def f(x, y, base, nb, world):
@@ -122,7 +135,7 @@ def torch_band_pack(grid_data, keep=None):
         if keep is not None:
             valid = valid & keep(x, y)
         gidx = torch.arange(len(x), dtype=torch.int64, device=x.device) + base
-        owner = (cx * world) // nb
+        owner = (cx // bw) % world if bw > 0 else (cx * world) // nb
         sel = torch.nonzero(valid).flatten()
         order = sel[torch.argsort(owner[sel], stable=True)]
         counts = torch.bincount(owner[order], minlength=world).to(torch.int64)
@@ -142,7 +155,10 @@ def torch_band_pack_query(grid_data, qx: float, qy: float, r: float):
         c = _abi.debug_classify(grid_data, qx, qy, r, x.cpu().numpy(), y.cpu().numpy())
         return torch.from_numpy((c & 4) != 0).to(x.device)
 
-    return torch_band_pack(grid_data, keep)
+    def f(x, y, base, nb, world):
+        return torch_band_pack(grid_data, keep, query_block_width(grid_data, qx, qy, r, world))(x, y, base, nb, world)
+
+    return f
 
 
 def _exchange_records(px, py, pg, send_counts, group):
@@ -378,6 +394,54 @@ def join_sharded(dx_local, dy_local, dbase: int, qx, qy, r: float, approximate: 
         raise ValueError(f"unknown partition {partition!r}")
     offset, total = gather_counts(len(pairs), pairs.device, group)
     return pairs, offset, total
+
+
+@dataclass
+class JoinCellsStep:
+    """join_cells_enqueue's result, nothing read back: out[:count] holds this rank's pairs as
+    (index into its received records, query index); rg maps a record to its window index;
+    counts holds every rank's pair count (device).  result() reads it back as join_sharded
+    returns it: (pairs int64 [m, 2] = (data window idx, query idx), output offset, total)."""
+    out: object
+    count: object
+    rg: object
+    counts: object
+    rank: int
+
+    def result(self):
+        import torch
+        m = int(self.count.item())
+        if m > self.out.shape[0]:
+            from ._abi import GeohipCapacityError
+            raise GeohipCapacityError(f"join pairs {m} exceed the pair buffer ({self.out.shape[0]})")
+        p = self.out[:m].to(torch.int64)
+        if m:
+            p = torch.stack([self.rg[p[:, 0]], p[:, 1]], dim=1)
+        allc = self.counts.cpu().tolist()
+        return p, sum(allc[:self.rank]), sum(allc)
+
+
+def join_cells_enqueue(dx_local, dy_local, dbase: int, qx, qy, r: float, approximate: bool = False, *, grid_data,
+                       grid_query, ctx, out, count, counts, group=None):
+    """The key-band join of one window (PointPointJoinQuery.java:137-150) with no host round
+    trip but the shuffle's split sizes: data points packed by owner band (geohip_band_pack_async)
+    and moved in one all-to-all; the owner joins its band against the whole query window with
+    geohip_join_pp_async into the preallocated out ([cap, 2] int32) / count (int64[1]), and the
+    ranks' counts meet in one device all-gather into counts (int64[world]).  Every rank takes
+    every query: a query whose Nbr block misses a rank's band finds no record there, so the pair
+    sets stay disjoint and their union is the window's join; the query window is small (10k
+    points in C3), and selecting each band's halo queries on the host cost a synchronisation per
+    window."""
+    world, rank = _world_rank(group)
+    nb = int(grid_query.n)
+    px, py, pg, send_counts = ctx.band_pack_async(grid_data, nb, world, dx_local, dy_local, dbase)
+    rx, ry, rg = _exchange_records(px, py, pg, send_counts, group)
+    ctx.join_pp_async(grid_data, grid_query, rx, ry, qx, qy, r, approximate, out, count)
+    if world > 1:
+        all_gather_into(counts, count, group)
+    else:
+        counts.copy_(count)
+    return JoinCellsStep(out, count, rg, counts, rank)
 
 
 def _poly_kw(poly_rings):

@@ -47,6 +47,14 @@ def main(out_dir):
         pairs, off, total = D.join_sharded(dxl, dyl, lo, tqx, tqy, 0.02, grid_data=g, grid_query=g, ctx=ctx,
                                            partition=part)
         res[f"join_{part}"], res[f"join_{part}_off"], res[f"join_{part}_total"] = pairs.cpu().numpy(), off, total
+    # the enqueue-only key-band join (bench's cells line): preallocated rows, device counts
+    cout = torch.empty((16_000_000, 2), dtype=torch.int32, device="cuda")
+    ccount = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ccounts = torch.zeros(world, dtype=torch.int64, device="cuda")
+    step = D.join_cells_enqueue(dxl, dyl, lo, tqx, tqy, 0.02, grid_data=g, grid_query=g, ctx=ctx, out=cout,
+                                count=ccount, counts=ccounts)
+    pairs, off, total = step.result()
+    res["join_enq"], res["join_enq_off"], res["join_enq_total"] = pairs.cpu().numpy(), off, total
     # the band pack kernel against its torch restatement on this shard
     bx, by, bi, bc = ctx.band_pack_async(g, 500, world, dxl, dyl, lo)
     tx, ty, ti, tc = D.torch_band_pack(g)(dxl, dyl, lo, 500, world)

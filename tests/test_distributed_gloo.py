@@ -382,4 +382,9 @@ def test_knn_range_key_band_partition_gloo(tmp_path, world):
         assert r[f"hits_{n_grid}"].tolist() == want.tolist()
         assert (r[f"totals_{n_grid}"] == len(want)).all()
         # only G u C points moved; their total is the candidate count
-        assert r[f"recv_{n_grid}"].sum() < len(x) * 0.3
+        recv = r[f"recv_{n_grid}"]
+        assert recv.sum() < len(x) * 0.3
+        # block-cyclic columns spread the one query's G u C box over the ranks (contiguous bands
+        # gave one rank all of it: skew = world); the 50-point clump sits in one column
+        if world > 1:
+            assert recv.max() / recv.mean() <= 1.5, recv.tolist()

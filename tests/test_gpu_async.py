@@ -4,8 +4,9 @@ geohip_join_ppoly_async) against the synchronous forms and the C oracle.
 They write the pair total to a device word and return without a host round trip; what a
 synchronous call would return as a status surfaces at geohip_ctx_sync: a query key the reference
 cannot parse back (PointPointJoinQuery.java:125 -> UniformGrid.getNeighboringCells ->
-HelperClass.getIntCellIndices, NumberFormatException) and a point-polygon candidate buffer that
-the previous call sized too small (the next call sizes it from the reported need).
+HelperClass.getIntCellIndices, NumberFormatException).  A point-polygon candidate buffer that
+the previous call sized too small is no error: the stream decides the candidates past it, and the
+need it reports sizes the next call's buffer.
 """
 import numpy as np
 import pytest
@@ -137,8 +138,9 @@ def test_ppoly_async_matches_sync(ctx, join, approx):
 
 def test_ppoly_async_candidate_overflow():
     """A fresh ctx sizes the candidate buffer at max(65536, n / 16); a window packed around
-    polygon edges needs more: sync() raises the capacity error, and the repeated call (sized
-    from the reported need) returns the oracle's pairs."""
+    polygon edges needs more.  The candidates past the buffer are decided in the stream itself, so
+    the first call already returns the oracle's pairs in one pass and sync() reports no error; the
+    need it reported sizes the next call's buffer (same pairs again)."""
     import torch
     c = Context(0)
     ag, cg = agrid(500)
@@ -157,12 +159,17 @@ def test_ppoly_async_candidate_overflow():
     x, y = _dev(hx, hy)
     out = torch.empty((want[0] + 8, 2), dtype=torch.int32, device="cuda")
     cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
-    c.range_ppoly_async(ag, x, y, off, vx, vy, 0.002, False, out, cnt)
-    with pytest.raises(_abi.GeohipCapacityError):
+    for _ in range(2):
+        cnt.zero_()
+        c.range_ppoly_async(ag, x, y, off, vx, vy, 0.002, False, out, cnt)
         c.sync()
-    c.range_ppoly_async(ag, x, y, off, vx, vy, 0.002, False, out, cnt)
-    c.sync()
-    assert (int(cnt.item()), pair_digest(out[:int(cnt.item())])[1]) == want
+        assert (int(cnt.item()), pair_digest(out[:int(cnt.item())])[1]) == want
+    # the synchronous forms on a fresh ctx: first call over the buffer, one pass, same pairs
+    c2 = Context(0)
+    got = c2.range_ppoly(ag, hx, hy, off, vx, vy, 0.002)
+    assert pairs_sorted(got).tolist() == pairs_sorted(cref.range_ppoly(cg, hx, hy, off, vx, vy, 0.002)).tolist()
+    got = c2.join_ppoly(ag, ag, hx, hy, off, vx, vy, 0.002)
+    assert pairs_sorted(got).tolist() == pairs_sorted(cref.join_ppoly(cg, cg, hx, hy, off, vx, vy, 0.002)).tolist()
 
 
 def test_ppoly_pane_async(ctx):

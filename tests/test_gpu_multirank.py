@@ -67,7 +67,7 @@ def test_world2_default_engines(tmp_path):
     dx, dy = synth.gaussian_clusters(400_001, 3, sigma=0.1)
     qx, qy = synth.gaussian_clusters(2000, 4, sigma=0.1)
     want = _pairs(cref.join_pp(cg, cg, dx, dy, qx, qy, 0.02))
-    for part in ("arrival", "cells"):
+    for part in ("arrival", "cells", "enq"):
         got = [p for r in range(world) for p in _pairs(R[r][f"join_{part}"])]
         assert len(got) == len(set(got)) and sorted(got) == want, part
         assert all(int(R[r][f"join_{part}_total"]) == len(want) for r in range(world))

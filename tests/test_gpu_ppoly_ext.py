@@ -366,11 +366,11 @@ def test_ppoly_refinement_part_edges(ctx, holes):
 
 def test_ppoly_stream_overflow_and_regrow(ctx):
     """The streaming point-polygon path's rare branches: 96 concentric star polygons put ~96
-    entries in each central cell, so a 4096-point chunk stages more pairs (and mixed-subcell
-    candidates) than its LDS holds and reruns with its reservations known; the candidates of the
-    first call exceed the initial candidate buffer (n / 16) and the step runs again with the
-    buffer regrown.  Range, exact and approximate, and join vs the oracle; a second call reuses
-    the cached plan and the grown buffer."""
+    entries in each central cell, so a wave stages more pairs (and mixed-subcell candidates) than
+    its LDS region holds and flushes it before the chunk's end; the candidates of the first call
+    exceed the initial candidate buffer (n / 16), so those past it are decided in the stream.
+    Range, exact and approximate, and join vs the oracle; a second call reuses the cached plan and
+    the grown buffer."""
     ag, cg = agrid(100)
     rng = np.random.default_rng(123)
     off, vx, vy = [0], [], []
