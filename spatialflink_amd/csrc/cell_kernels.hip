@@ -100,6 +100,31 @@ __device__ __forceinline__ int32_t d_axis_cell_sub(double v, double mn, double l
     return d_cvt_java(f);
 }
 
+// Cell and subcell from ONE floor: q4 = fl(t * il4) with il4 = 4 il (exact) is 4 q exactly (a
+// power-of-two scale commutes with rounding), so f4 = floor(q4) = 4 floor(q) + floor(4 (q - floor q))
+// -- the cell in its high bits, the subcell in its low two.  When q4 lies farther than
+// E = (|q4| + mnl + 4) 2^-44 from every integer, both d_axis_cell_sub's margins hold (its cell
+// margin |q| 2^-49 is a multiple-of-4 distance of q4 / 4, its subcell margin is at most E), so
+// both answers are d_axis_cell_sub's; otherwise (and for NaN / inf / huge values) that function
+// decides.  The (int) of f4 saturates outside +-2^31: those cells lie outside every grid (nb <=
+// 65535) as Java's saturated ones do.  (q4 - f4 is exact: f4 <= q4 < f4 + 1.)
+__device__ __forceinline__ int32_t d_axis_cell_sub4(double v, double mn, double l, double il, double il4, double mnl,
+                                                    unsigned& sub, bool& sub_ok) {
+    const double q4 = (v - mn) * il4;
+    const double f4 = __builtin_floor(q4);
+    const double fr = q4 - f4;
+    const double E = (__builtin_fabs(q4) + mnl + 4.0) * 0x1.0p-44;
+    const bool ok = (fr > E) & ((1.0 - fr) > E);
+    const int32_t fi = d_cvt_java(f4);
+    int32_t c = fi >> 2;  // arithmetic: floor(f4 / 4)
+    sub = (unsigned)fi & 3u;
+    sub_ok = true;
+    if (__ballot(!ok)) {  // wave-uniform, rare: the two-step form with its own fallbacks
+        if (!ok) c = d_axis_cell_sub(v, mn, l, il, mnl, sub, sub_ok);
+    }
+    return c;
+}
+
 // small zero-fills inside timed steps (a kernel, so its time is stamped like the others)
 __global__ void fill_words(unsigned* __restrict__ p, unsigned n, unsigned v) {
     for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = v;
@@ -2406,6 +2431,8 @@ __global__ __launch_bounds__(kTB) void ppoly_outside(const double* __restrict__ 
 // The same decisions as ppoly_eval (PointPolygonRangeQuery.java:105-121; the join's
 // PointPolygonJoinQuery.java:183-195 through jmode's rectangle lists).
 constexpr uint32_t kEntC = 0x80000000u;    // entry.x: C cell (class word in entry.y); else G
+constexpr unsigned kCandGone = 0xffffffffu;  // a candidate slot decided by the refinement, left to the
+                                             // redo pass, or past a range's end: the grouping skips it
 constexpr int kStreamNW = 8;               // waves per block
 constexpr unsigned kStreamPts = 256;       // points per wave iteration (4 per lane)
 // 4096-point chunks: 2 iterations per wave (8192 spilled 33 VGPRs in the two-phase chunk; 2048
@@ -2442,6 +2469,10 @@ struct StreamOut {
     uint64_t ccap;                  // candidates past it are decided in the stream (exact test inline)
     unsigned* cpoly;                // candidates in chunk order: polygon (the grouping reads these),
     double4* crec;                  // and (x, y, point bits, -) -- one 32-byte sector per gather
+    unsigned* covf;                 // per wave: the chunk's candidates staged before its end (packed
+    unsigned covf_wave;             // words), covf_wave each -- a chunk's worth at most
+    unsigned* redo;                 // chunks whose candidates did not fit the buffer (ppoly_stream_redo)
+    unsigned* nredo;                // their count (zero before)
 };
 
 struct StreamArgs {
@@ -2480,6 +2511,7 @@ struct StreamSink {
     unsigned* pk;                   // this wave's LDS region
     unsigned cap;                   // its capacity (a push adds <= 64)
     unsigned n;                     // entries staged (wave-uniform)
+    unsigned ovn;                   // candidates: this chunk's entries in the wave's overflow list
 };
 
 __device__ __forceinline__ void stream_emit_pair(const StreamOut& o, unsigned long long p, unsigned poly, unsigned idx) {
@@ -2507,17 +2539,10 @@ __device__ __forceinline__ unsigned long long wave_reserve(unsigned long long* t
            (unsigned)__builtin_amdgcn_readfirstlane((int)lo);
 }
 
-// A candidate (poly, window index idx) stored at slot p of the candidate buffer, or -- past its
-// capacity (the buffer is sized from the previous call's count) -- decided here by the exact test
-// ppoly_cand_eval would run (PointPolygonRangeQuery.java:116, DistanceFunctions.java:33-36); the
-// result says whether it is a pair.  Rare by construction, so this path stays out of the way.
-__device__ __noinline__ bool stream_cand_exact(const StreamArgs& a, unsigned poly, unsigned idx) {
-    const PolyDev P = a.polys[poly];
-    const double px = a.x[idx], py = a.y[idx];
-    const SlabView sv{a.slabs + P.loff, P.ns};
-    return P.nring > 1 ? point_polygon_within_rings(px, py, a.vx + P.voff, a.vy + P.voff, a.vring + P.voff,
-                                                    a.renv + 4 * (size_t)P.eoff, P, sv, a.r)
-                       : point_polygon_within(px, py, a.vx + P.voff, a.vy + P.voff, P, sv, a.r);
+// the wave's spill list (StreamOut::covf): the chunk's candidates whose LDS region filled before
+// the chunk's end, kept as packed words until the chunk's one reservation
+__device__ __forceinline__ unsigned* stream_ovf(const StreamOut& o) {
+    return o.covf + ((size_t)blockIdx.x * kStreamNW + threadIdx.x / kWave) * o.covf_wave;
 }
 
 // entries [0, m) of a staged region (chunk c0) to their slots from base on (wave-cooperative)
@@ -2528,53 +2553,71 @@ __device__ __forceinline__ void stream_store_pairs(const StreamArgs& a, const un
         stream_emit_pair(a.o, base + t, v >> kLocalBits, (unsigned)(c0 + (v & (kStreamChunk - 1))));
     }
 }
+// packed candidate words [0, m) (LDS or the spill list) to slots base + t of the candidate buffer
 __device__ __forceinline__ void stream_store_cands(const StreamArgs& a, const unsigned* pk, unsigned m,
                                                    unsigned long long base, uint64_t c0) {
-    const bool past = base + m > a.o.ccap;  // wave-uniform
+    for (unsigned t = (unsigned)lane_id(); t < m; t += kWave) {
+        const unsigned v = pk[t];
+        const unsigned idx = (unsigned)(c0 + (v & (kStreamChunk - 1)));
+        a.o.cpoly[base + t] = v >> kLocalBits;
+        a.o.crec[base + t] = make_double4(a.x[idx], a.y[idx], __longlong_as_double((long long)idx), 0.0);
+    }
+}
+
+// ppoly_stream_redo: the staged candidates decided at once by the exact test ppoly_cand_eval runs
+// (PointPolygonRangeQuery.java:116, DistanceFunctions.java:33-36), hits reserved and stored
+__device__ __forceinline__ void stream_decide_cands(const StreamArgs& a, const unsigned* pk, unsigned m, uint64_t c0) {
     for (unsigned t0 = 0; t0 < m; t0 += kWave) {
         const unsigned t = t0 + (unsigned)lane_id();
+        bool hit = false;
         unsigned poly = 0, idx = 0;
-        bool exact = false;
         if (t < m) {
             const unsigned v = pk[t];
             poly = v >> kLocalBits;
             idx = (unsigned)(c0 + (v & (kStreamChunk - 1)));
-            const unsigned long long p = base + t;
-            if (p < a.o.ccap) {
-                a.o.cpoly[p] = poly;
-                a.o.crec[p] = make_double4(a.x[idx], a.y[idx], __longlong_as_double((long long)idx), 0.0);
-            } else {
-                exact = true;
-            }
+            const PolyDev P = a.polys[poly];
+            const double px = a.x[idx], py = a.y[idx];
+            const SlabView sv{a.slabs + P.loff, P.ns};
+            hit = P.nring > 1 ? point_polygon_within_rings(px, py, a.vx + P.voff, a.vy + P.voff, a.vring + P.voff,
+                                                           a.renv + 4 * (size_t)P.eoff, P, sv, a.r)
+                              : point_polygon_within(px, py, a.vx + P.voff, a.vy + P.voff, P, sv, a.r);
         }
-        if (past) {  // the buffer is full: these candidates are decided now, their pairs reserved here
-            const bool hit = exact && stream_cand_exact(a, poly, idx);
-            const unsigned long long mh = __ballot(hit);
-            if (mh) {
-                const unsigned long long pb = wave_reserve(a.o.ptotal, (unsigned)__popcll(mh));
-                if (hit) stream_emit_pair(a.o, pb + lanes_below(mh), poly, idx);
-            }
+        const unsigned long long mh = __ballot(hit);
+        if (mh) {
+            const unsigned long long pb = wave_reserve(a.o.ptotal, (unsigned)__popcll(mh));
+            if (hit) stream_emit_pair(a.o, pb + lanes_below(mh), poly, idx);
         }
     }
 }
 
-// a wave's region flushed before the chunk's end: its own reservation, then the stores
-template <bool CAND>
+// A wave's region full before the chunk's end: pairs get their own reservation and are stored;
+// candidates go to the wave's spill list (the chunk reserves them all at its end, so a chunk's
+// candidates either all fit the buffer or are all left to ppoly_stream_redo); in the redo kernel
+// the candidates are decided at once.
+template <bool CAND, bool REDO>
 __device__ __forceinline__ void stream_flush(const StreamArgs& a, StreamSink& k, uint64_t c0) {
     wave_lds_sync();
-    const unsigned long long b = wave_reserve(CAND ? a.o.ctotal : a.o.ptotal, k.n);
-    if (CAND) stream_store_cands(a, k.pk, k.n, b, c0);
-    else stream_store_pairs(a, k.pk, k.n, b, c0);
-    if (lane_id() == 0) atomicAdd(a.o.flushes, 1u);
+    if (CAND && REDO) {
+        stream_decide_cands(a, k.pk, k.n, c0);
+    } else if (CAND) {
+        unsigned* ovf = stream_ovf(a.o) + k.ovn;
+        for (unsigned t = (unsigned)lane_id(); t < k.n; t += kWave) ovf[t] = k.pk[t];
+        k.ovn += k.n;
+    } else {
+        const unsigned long long b = wave_reserve(a.o.ptotal, k.n);
+        stream_store_pairs(a, k.pk, k.n, b, c0);
+        if (lane_id() == 0) atomicAdd(a.o.flushes, 1u);
+    }
     wave_lds_sync();
     k.n = 0;
 }
 
 // wave-uniform: lanes with `hit` stage a pair, lanes with `need` a candidate (never both):
 // two ballots, one LDS store per lane
-template <bool CANDS>
+template <bool CANDS, bool REDO>
 __device__ __forceinline__ void stream_push(const StreamArgs& a, StreamSink& ps, StreamSink& cs, bool hit, bool need,
                                             unsigned poly, unsigned loc, uint64_t c0) {
+    if (REDO) hit = false;  // the redo kernel's chunks stored their pairs in the stream already
     const unsigned long long mp = __ballot(hit);
     const unsigned long long mc = CANDS ? __ballot(need) : 0ull;
     if (!(mp | mc)) return;
@@ -2587,8 +2630,8 @@ __device__ __forceinline__ void stream_push(const StreamArgs& a, StreamSink& ps,
     }
     ps.n += (unsigned)__popcll(mp);
     if (CANDS) cs.n += (unsigned)__popcll(mc);
-    if (ps.n > ps.cap - kWave) stream_flush<false>(a, ps, c0);
-    if (CANDS && cs.n > cs.cap - kWave) stream_flush<true>(a, cs, c0);
+    if (!REDO && ps.n > ps.cap - kWave) stream_flush<false, REDO>(a, ps, c0);
+    if (CANDS && cs.n > cs.cap - kWave) stream_flush<true, REDO>(a, cs, c0);
 }
 
 // Entry balance of the exact walk (round 5; it replaced each lane walking its own points' entries
@@ -2637,7 +2680,7 @@ __device__ __forceinline__ void stream_decide(uint32_t ex, uint32_t word, unsign
 struct StreamPre {
     double x[4], y[4];
 };
-template <bool APPROX, bool KL>
+template <bool APPROX, bool KL, bool REDO = false>
 __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned* kl, uint64_t c0, uint64_t c1,
                                              StreamSink& ps, StreamSink& cs, uint2* brec, unsigned long long* bbm,
                                              const StreamPre* pre) {
@@ -2670,6 +2713,7 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
                128u * (unsigned)(s >> 1);
     };
     const double mnlx = __builtin_fabs(g.mnx) * g.il, mnly = __builtin_fabs(g.mny) * g.il;
+    const double il4 = g.il * 4.0;
     // point state for phase B: bits 0-3 subcell (4 sx + sy), 4 NaN coordinate, 5 outside the grid
     constexpr unsigned kNanBit = 16u, kOutBit = 32u;
     uint2 hd[kIters][4];
@@ -2698,8 +2742,8 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
             const bool v = c0 + loc_of(t, s) < c1;
             unsigned sx = 0, sy = 0;
             bool okx = false, oky = false;
-            const int32_t cx = d_axis_cell_sub(qx[s], g.mnx, g.l, g.il, mnlx, sx, okx);
-            const int32_t cy = d_axis_cell_sub(qy[s], g.mny, g.l, g.il, mnly, sy, oky);
+            const int32_t cx = d_axis_cell_sub4(qx[s], g.mnx, g.l, g.il, il4, mnlx, sx, okx);
+            const int32_t cy = d_axis_cell_sub4(qy[s], g.mny, g.l, g.il, il4, mnly, sy, oky);
             const bool in = v && cx >= 0 && cy >= 0 && cx < g.nb && cy < g.nb;
             const bool nan = !(qx[s] == qx[s] && qy[s] == qy[s]);
             unsigned w = (nan ? kNanBit : 0u) | ((v && !in) ? kOutBit : 0u);
@@ -2739,7 +2783,7 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
                 bool hit = false, need = false;
                 if (!multi) stream_decide(h.x, h.y, st[t] >> (8 * sl), hit, need);
                 const unsigned loc = loc_of(t, sl);
-                stream_push<true>(a, ps, cs, hit, need, h.x & ~kEntC, loc, c0);
+                stream_push<true, REDO>(a, ps, cs, hit, need, h.x & ~kEntC, loc, c0);
             }
             const unsigned ic = wave_incl_scan(lc), in = wave_incl_scan(ln);
             const unsigned T = (unsigned)__builtin_amdgcn_readlane((int)ic, kWave - 1);
@@ -2757,7 +2801,7 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
                         if (e < e1) en = a.ent[e++];
                         bool hit, need;
                         stream_decide(en.x, en.y, sw, hit, need);
-                        stream_push<true>(a, ps, cs, hit, need, en.x & ~kEntC, loc, c0);
+                        stream_push<true, REDO>(a, ps, cs, hit, need, en.x & ~kEntC, loc, c0);
                     }
                 }
                 continue;
@@ -2801,7 +2845,7 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
                     bool hit, need;
                     stream_decide(en[u].x, en[u].y, ry[u] >> 12, hit, need);
                     const unsigned loc = ry[u] & (kStreamChunk - 1);
-                    stream_push<true>(a, ps, cs, hit, need, en[u].x & ~kEntC, loc, c0);
+                    stream_push<true, REDO>(a, ps, cs, hit, need, en[u].x & ~kEntC, loc, c0);
                 }
             }
             wave_lds_sync();  // the records and bitmap are reused by the next iteration
@@ -2858,7 +2902,7 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
                         ex = kNoEntry;
                     }
                 }
-                stream_push<!APPROX>(a, ps, cs, hit, need, poly, loc, c0);
+                stream_push<!APPROX, REDO>(a, ps, cs, hit, need, poly, loc, c0);
             }
         }
         // points outside the grid against the polygons whose rectangles reach outside it (rare)
@@ -2880,7 +2924,7 @@ __device__ __forceinline__ void stream_chunk(const StreamArgs& a, const unsigned
                         in = a.jmode == 1 ? in_rects(a.rects + 4 * P.coff, P.nc, cx, cy)
                                           : in_rects(a.rects + 4 * P.goff, P.ng, cx, cy);
                     const bool dist = !APPROX && a.jmode == 1;
-                    stream_push<!APPROX>(a, ps, cs, in && !dist, in && dist, p, loc_of(t, s), c0);
+                    stream_push<!APPROX, REDO>(a, ps, cs, in && !dist, in && dist, p, loc_of(t, s), c0);
                 }
             }
         }
@@ -2937,15 +2981,15 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
         __syncthreads();  // the previous chunk's stage is drained (and the bitmap staged)
         const uint64_t c0 = (uint64_t)vb * kStreamChunk;
         const uint64_t c1 = c0 + kStreamChunk < a.n ? c0 + kStreamChunk : a.n;
-        StreamSink ps{ppk + wid * kWPair, kWPair, 0u};
-        StreamSink cs{cpk + (APPROX ? 0 : wid * kWCand), APPROX ? kWave : kWCand, 0u};
+        StreamSink ps{ppk + wid * kWPair, kWPair, 0u, 0u};
+        StreamSink cs{cpk + (APPROX ? 0 : wid * kWCand), APPROX ? kWave : kWCand, 0u, 0u};
         uint2* wrec = kBal ? brec + wid * kBalRecs : brec;
         unsigned long long* wbm = kBal ? bbm + wid * kBalWords : bbm;
         stream_chunk<APPROX, KL>(a, kl, c0, c1, ps, cs, wrec, wbm, &pre);
         if (vb + gridDim.x < nchunks) prefetch(vb + gridDim.x);
         if (lane == 0) {
             s_wp[wid] = ps.n;
-            s_wc[wid] = cs.n;
+            s_wc[wid] = cs.n + cs.ovn;  // staged in LDS + spilled before the chunk's end
         }
         __syncthreads();
         unsigned np = 0, nc = 0, pex = 0, cex = 0;  // totals; this wave's offsets in the chunk
@@ -2960,11 +3004,53 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
         if (threadIdx.x == 0) {
             s_pb = np ? atomicAdd(a.o.ptotal, (unsigned long long)np) : 0ull;
             s_cb = nc ? atomicAdd(a.o.ctotal, (unsigned long long)nc) : 0ull;
+            // a chunk whose candidates do not all fit the buffer leaves them all to the redo pass
+            if (!APPROX && nc && s_cb + nc > a.o.ccap) a.o.redo[atomicAdd(a.o.nredo, 1u)] = vb;
         }
         __syncthreads();
         // each wave stores its own region: coalesced runs of the output
         stream_store_pairs(a, ppk + wid * kWPair, ps.n, s_pb + pex, c0);
-        if (!APPROX) stream_store_cands(a, cpk + wid * kWCand, cs.n, s_cb + cex, c0);
+        if (!APPROX) {
+            const unsigned long long cb = s_cb + cex;
+            const unsigned wc = cs.n + cs.ovn;
+            if (s_cb + nc <= a.o.ccap) {
+                stream_store_cands(a, cpk + wid * kWCand, cs.n, cb, c0);
+                if (cs.ovn) stream_store_cands(a, stream_ovf(a.o), cs.ovn, cb + cs.n, c0);
+            } else {  // its slots below the capacity are marked gone (the grouping skips them)
+                for (unsigned t = (unsigned)lane; t < wc && cb + t < a.o.ccap; t += kWave) a.o.cpoly[cb + t] = kCandGone;
+            }
+        }
+    }
+}
+
+// The chunks ppoly_stream left to redo (their candidates did not fit the candidate buffer, which
+// is sized from the previous call's count): each is walked again with pairs off (the stream stored
+// them) and its candidates decided at once by the exact test.  Rare by construction (a first call,
+// or a window with many more candidates than the last); with an empty list every block exits at
+// once.  No call runs the step twice.
+template <bool KL>
+__global__ __launch_bounds__(kStreamNW * kWave) void ppoly_stream_redo(StreamArgs a) {
+    __shared__ unsigned kl[KL ? kKeepLds : 1];
+    __shared__ unsigned cpk[kSCandCap];
+    __shared__ uint2 brec[kStreamNW * kBalRecs];
+    __shared__ unsigned long long bbm[kStreamNW * kBalWords];
+    constexpr unsigned kWCand = kSCandCap / kStreamNW;
+    const unsigned nredo = *a.o.nredo;
+    if (blockIdx.x >= nredo) return;
+    const int wid = threadIdx.x / kWave;
+    if (KL)
+        for (unsigned t = threadIdx.x; t < a.keep_words; t += kStreamNW * kWave) kl[t] = a.keep[t];
+    unsigned dummy = 0;
+    for (unsigned i = blockIdx.x; i < nredo; i += gridDim.x) {
+        __syncthreads();
+        const unsigned vb = a.o.redo[i];
+        const uint64_t c0 = (uint64_t)vb * kStreamChunk;
+        const uint64_t c1 = c0 + kStreamChunk < a.n ? c0 + kStreamChunk : a.n;
+        StreamSink ps{&dummy, 0x7fffffffu, 0u, 0u};  // pairs off
+        StreamSink cs{cpk + wid * kWCand, kWCand, 0u, 0u};
+        stream_chunk<false, KL, true>(a, kl, c0, c1, ps, cs, brec + wid * kBalRecs, bbm + wid * kBalWords, nullptr);
+        wave_lds_sync();
+        stream_decide_cands(a, cs.pk, cs.n, c0);
     }
 }
 
@@ -3005,7 +3091,6 @@ __device__ __forceinline__ void spairs_push(uint2* buf, unsigned& cnt, bool hit,
 constexpr unsigned kCandGroups = 128;
 constexpr unsigned kCandThreads = 1024;
 constexpr unsigned kCandPer = 4;  // candidates per thread per round (loads in flight together)
-constexpr unsigned kCandGone = 0xffffffffu;  // a candidate slot decided by the refinement (and the range end)
 struct CandGroup {
     const unsigned long long* ccount;  // candidate total (StreamOut::ctotal, or the refined count)
     const unsigned long long* cstream; // the stream's candidate total (the capacity check)
@@ -4210,9 +4295,10 @@ namespace {
 enum JSlot {
     J_HIST, J_TTOT, J_TSTART, J_SEG, J_SX, J_SY, J_SIDX, J_SKEY, J_MISC, J_AUX, J_POLY, J_OUT, J_RECT, J_QSTART,
     J_QLIST, J_GLIST, J_QCNT, J_BCNT, J_BOFF, J_PMASK, J_MWORDS, J_MOFF, J_TCUR,
-    J_KCAND, J_KTEMP, J_KBLOB  // point kNN (large k) and point-polygon kNN scratch
+    J_KCAND, J_KTEMP, J_KBLOB,  // point kNN (large k) and point-polygon kNN scratch
+    J_COVF                      // point-polygon stream: per-wave overflow candidate lists
 };
-static_assert(J_KBLOB <= 27, "scratch slots (abi.cpp S_J0 .. S_J27)");
+static_assert(J_COVF <= 27, "scratch slots (abi.cpp S_J0 .. S_J27)");
 
 // J_MISC words: [0] outside count, [1] outside cursor, [2] scan grand total, [3] global
 // query count, [8..9] pair total (u64)
@@ -4954,6 +5040,7 @@ struct PolyCache {
     std::vector<uint32_t> cell_off;   // nb * nb + 1 (host only)
     std::vector<uint32_t> cell_ent;   // 2 per entry: poly | kEntC, class word
     std::vector<uint32_t> cell_head;  // 2 per cell (see kMulti)
+    uint32_t max_cell_ent = 0;        // the most entries of one cell (sizes the overflow lists)
     std::vector<uint32_t> skeep;
     std::vector<uint32_t> opoly;
     uint64_t last_cand = 0;           // candidates of the previous step (sizes the buffer)
@@ -5082,10 +5169,12 @@ void build_stream_table(PolyCache& c, uint32_t npoly, int32_t nb, bool r_is_max)
     if (npoly >= kStreamMaxPolys || npoly > kCandLdsPolys || c.cell_off[ncell] >= kMulti) return;
     c.skeep.assign((ncell + 31) / 32, 0u);
     c.cell_head.assign(2 * ncell, 0u);
+    c.max_cell_ent = 0;
     for (size_t k = 0; k < ncell; k++) {
         const uint32_t b = c.cell_off[k], e = c.cell_off[k + 1];
         c.cell_head[2 * k] = kNoEntry;
         if (e == b) continue;
+        c.max_cell_ent = std::max(c.max_cell_ent, e - b);
         c.skeep[k >> 5] |= 1u << (k & 31);
         if (e - b == 1) {
             c.cell_head[2 * k] = c.cell_ent[2 * (size_t)b];
@@ -5426,6 +5515,19 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             char* cb = reinterpret_cast<char*>(cbuf);
             so.cpoly = cands ? reinterpret_cast<unsigned*>(cb) : nullptr;
             so.crec = cands ? reinterpret_cast<double4*>(cb + ((ccap * 4 + 31) & ~(uint64_t)31)) : nullptr;
+            // per wave, a chunk's candidates can all lie past the buffer: its points x the most
+            // entries a point meets (a cell's, or the polygons reaching outside the grid)
+            const unsigned stream_blocks =
+                (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(nchunks, (uint64_t)ctx_cus(ctx) * kStreamBlocksPerCU));
+            so.covf_wave = cands ? (kStreamChunk / kStreamNW) *
+                                       std::max<uint32_t>(1u, std::max<uint32_t>(pc->max_cell_ent, (uint32_t)pc->opoly.size()))
+                                 : 0u;
+            const size_t covf_words = (size_t)stream_blocks * kStreamNW * so.covf_wave;
+            unsigned* cov = cands ? S.get<unsigned>(J_COVF, (covf_words + nchunks + 64) * 4) : nullptr;
+            if (S.rc) return S.rc;
+            so.covf = cov;
+            so.redo = cands ? cov + covf_words : nullptr;
+            so.nredo = misc + 7;  // zeroed with the totals
             StreamArgs sa;
             sa.x = dx;
             sa.y = dy;
@@ -5448,7 +5550,7 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             sa.renv = denv;
             sa.slabs = dslab;
             if (nchunks) {
-                const unsigned nblk = (unsigned)std::min<uint64_t>(nchunks, (uint64_t)ctx_cus(ctx) * kStreamBlocksPerCU);
+                const unsigned nblk = stream_blocks;
                 // the cell bitmap staged in LDS (from global memory: 516 against 460 us; none: 487)
                 const bool kl = sa.keep && sa.keep_words <= kKeepLds;
                 if (approximate) {
@@ -5457,6 +5559,10 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
                 } else {
                     if (kl) tlaunch(ctx, ppoly_stream<false, true>, nblk, kStreamNW * kWave, 0, st, sa);
                     else tlaunch(ctx, ppoly_stream<false, false>, nblk, kStreamNW * kWave, 0, st, sa);
+                }
+                if (cands) {  // the chunks whose candidates did not fit (an empty list: blocks exit at once)
+                    if (kl) tlaunch(ctx, ppoly_stream_redo<true>, nblk, kStreamNW * kWave, 0, st, sa);
+                    else tlaunch(ctx, ppoly_stream_redo<false>, nblk, kStreamNW * kWave, 0, st, sa);
                 }
             }
             if (cands) {
