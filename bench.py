@@ -992,6 +992,12 @@ class C5Workload(KnnWorkload):
     def __init__(self, *a):
         super().__init__(*a)
         import torch
+        # the range part's output is a set (PointPointRangeQuery.java:117-136): the fused pass then
+        # sweeps the window in interleaved fronts and reserves its hits without a look-back
+        self.ctx.set_range_order(not self.args.range_ascending)
+        if not self.args.range_ascending:
+            self.kernel = ("geohip::knn_pass<16, range, unordered> (kNN k=100 + range r=0.05 in one pass, interleaved "
+                           "fronts, range hits reserved per block: one launch per step)")
         self.rout = torch.empty(self.n, dtype=torch.int32, device=self.dev)
         self.hits = None
 
@@ -1013,6 +1019,7 @@ class C5Workload(KnnWorkload):
         c = super().config()
         c["workload"] = f"{self.label}, {self.n} uniform points per window per GPU (BASELINE.json configs[4])"
         c["range_hits_per_window_per_gpu"] = self.hits
+        c["range_output"] = "ascending hit indices" if self.args.range_ascending else "unordered hit set (GEOHIP_ORDER_ANY)"
         return c
 
     def cpu_baseline(self, seconds):

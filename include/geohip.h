@@ -111,8 +111,8 @@ void* geohip_ctx_stream(geohip_ctx* ctx);
    GEOHIP_ORDER_ASCENDING (the default after geohip_ctx_create) -- hit indices ascending;
    GEOHIP_ORDER_ANY -- the same set in an unspecified order, as the reference's window function
    emits it (PointPointRangeQuery.java:117-136 collects the filter's hits as they arrive), from
-   one pass with no ordered emission (faster).  The fused geohip_knn_range_pp range stays
-   ascending. */
+   one pass with no ordered emission (faster); geohip_knn_range_pp's range part likewise (its
+   pass then sweeps the window in interleaved fronts as the kNN alone does). */
 #define GEOHIP_ORDER_ASCENDING 0
 #define GEOHIP_ORDER_ANY 1
 int geohip_ctx_set_range_order(geohip_ctx* ctx, int order);

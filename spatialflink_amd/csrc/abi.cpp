@@ -645,6 +645,8 @@ int knn_range_enqueue(geohip_ctx* ctx, const geohip_grid* grid, const double* x,
     rio.out = rout;
     rio.cap = rcap;
     rio.total = rtotal;
+    rio.unordered = ctx->range_order == GEOHIP_ORDER_ANY ? 1 : 0;  // the set, no look-back
+    rio.cursor = lb.set.word;
     hipEvent_t e0, e1;
     kernel_step_events(ctx, &e0, &e1);
     hipError_t e = launch_knn_pass(dx, dy, n, a, B<unsigned long long>(ctx, S_PART_D), B<unsigned>(ctx, S_PART_I),

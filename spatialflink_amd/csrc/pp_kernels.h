@@ -51,6 +51,11 @@ struct PassRangeIo {
     unsigned long long* trace;  // measurement only: look-back done / hits written at [8 b + 5, 6]
     unsigned* fault;            // set when the look-back wait gives up (poll_block_counts)
     unsigned spin_limit, inject;
+    // unordered (geohip_ctx_set_range_order GEOHIP_ORDER_ANY): no look-back -- each block reserves
+    // its hits on *cursor (zero before a launch; the kNN's last block writes the total and
+    // re-arms it) and the pass sweeps the window in interleaved fronts as the kNN alone does
+    int unordered;
+    unsigned long long* cursor;
 };
 // whether a window of n points fits the fused kNN + range pass (block chunk <= 131072 points)
 bool knn_pass_fuses_range(uint64_t n);

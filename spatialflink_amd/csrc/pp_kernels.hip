@@ -768,12 +768,18 @@ struct RangeSide {
     unsigned long long* mask;  // LDS hit bitmask of the block's chunk
     uint64_t base;             // first point of the chunk
     double r;
+    unsigned grid;             // interleaved sweep (unordered range, grid > 0): the block's bit of
+                               // point i is ((i / 256 - blockIdx.x) / grid) * 256 + i % 256
 };
+__device__ __forceinline__ unsigned range_bit(const RangeSide& rs, uint64_t i) {
+    if (rs.grid) return (unsigned)(((i >> 8) - blockIdx.x) / rs.grid) * 256u + (unsigned)(i & 255u);
+    return (unsigned)(i - rs.base);
+}
 
 template <class PB, bool RANGE = false>
 __device__ __forceinline__ void pass_dist_batch(WaveStage& st, unsigned& ccnt, PB& kb, const KnnArgs& a,
                                                 const PassIo& io, unsigned& appended, bool partial,
-                                                const RangeSide& rs = RangeSide{nullptr, 0, 0.0}) {
+                                                const RangeSide& rs = RangeSide{nullptr, 0, 0.0, 0u}) {
     const int lane = lane_id();
     while (ccnt >= 64 || (partial && ccnt > 0)) {
         const unsigned take = ccnt >= 64 ? 64u : ccnt;
@@ -793,7 +799,7 @@ __device__ __forceinline__ void pass_dist_batch(WaveStage& st, unsigned& ccnt, P
         const unsigned long long db = (unsigned long long)__double_as_longlong(d);
         if (RANGE) {
             if (ok && (pi & kFlagBand) && d <= rs.r) {
-                const unsigned off = (unsigned)((pi & kIdxMask) - rs.base);
+                const unsigned off = range_bit(rs, pi & kIdxMask);
                 atomicOr(&rs.mask[off >> 6], 1ull << (off & 63));
             }
             ok = ok && (pi & kFlagKnn);
@@ -1108,33 +1114,60 @@ __device__ __forceinline__ void emit_words(unsigned long long mine, unsigned fir
     }
 }
 
+// The same, each of the 64 words with its own first point (lane l holds word l's in `firsts`):
+// the interleaved sweep's words are 64-point runs of different fronts.
+__device__ __forceinline__ void emit_words_at(unsigned long long mine, unsigned firsts, unsigned* stg, unsigned& sc,
+                                              unsigned long long& obase, unsigned* __restrict__ out,
+                                              unsigned long long cap) {
+    const int lane = lane_id();
+    unsigned long long nz = __ballot(mine != 0ull);
+    while (nz) {
+        const int j = __builtin_ctzll(nz);
+        nz &= nz - 1;
+        const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)mine, j);
+        const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(mine >> 32), j);
+        const unsigned fp = (unsigned)__builtin_amdgcn_readlane((int)firsts, j);
+        const unsigned long long bits = ((unsigned long long)hi << 32) | lo;
+        if ((bits >> lane) & 1ull) stg[sc + lanes_below(bits)] = fp + (unsigned)lane;
+        sc += (unsigned)__popcll(bits);
+        if (sc > kEmitStage - kWave) emit_flush(stg, sc, obase, out, cap);
+    }
+}
+
 // Range hits of a block chunk (LDS bitmask) written in ascending index order: the block
 // publishes its count (status word tagged with the launch epoch, atomic exchange: visible at the
 // device coherence point), sums the counts of every earlier chunk (wave 0, all loads in flight,
 // s_sleep back-off), and each wave stores the hits of a contiguous run of mask words.  The block
 // of the last chunk writes the total.  Earlier chunks were taken by blocks that started earlier,
 // so the wait always ends.
-template <int NW>
+// Unordered (UNORD): the block reserves its hits on the launch's cursor instead -- the slot of
+// its run is known at once, no block waits for another (the kNN's last block writes the total).
+template <int NW, bool UNORD = false>
 __device__ __forceinline__ void pass_range_publish(const PassRangeIo& rio, const unsigned long long* bmask,
-                                                   unsigned& bcount, unsigned vb, uint64_t p0, uint64_t p1) {
+                                                   unsigned& bcount, unsigned long long& excl_sh, unsigned vb,
+                                                   unsigned nw) {
     constexpr int NT = NW * 64;
-    const unsigned nw = p1 > p0 ? (unsigned)((p1 - p0 + 63) / 64) : 0u;
     unsigned my = 0;
     for (unsigned t = threadIdx.x; t < nw; t += NT) my += (unsigned)__popcll(bmask[t]);
     if (my) atomicAdd(&bcount, my);
     __syncthreads();
-    if (threadIdx.x == 0)
-        (void)__hip_atomic_exchange(rio.status + vb, (rio.epoch << 40) | (unsigned long long)bcount, __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) {
+        if (UNORD)
+            excl_sh = bcount ? atomicAdd(rio.cursor, (unsigned long long)bcount) : 0ull;
+        else
+            (void)__hip_atomic_exchange(rio.status + vb, (rio.epoch << 40) | (unsigned long long)bcount,
+                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
-template <int NW>
+// UNORD: the run was reserved at publish time (no look-back); word w covers the 64 points from
+// ((w / 4) * nblocks + block) * 256 + (w % 4) * 64 (the interleaved fronts).
+template <int NW, bool UNORD = false>
 __device__ __forceinline__ void pass_range_emit(const PassRangeIo& rio, const unsigned long long* bmask,
                                                 unsigned* wsum, unsigned& bcount, unsigned long long& excl_sh,
-                                                unsigned vb, uint64_t p0, uint64_t p1, unsigned* stg) {
+                                                unsigned vb, uint64_t p0, unsigned nw, unsigned* stg) {
     const int lane = lane_id(), wid = threadIdx.x / kWave;
-    const unsigned nw = p1 > p0 ? (unsigned)((p1 - p0 + 63) / 64) : 0u;
-    if (wid == 0) {
+    if (!UNORD && wid == 0) {
         const unsigned long long pre = poll_block_counts<kPassMaxBlocks / kWave>(rio.status, vb, rio.epoch, rio.spin_limit,
                                                                                   rio.inject, rio.fault);
         if (lane == 0) excl_sh = pre;
@@ -1155,11 +1188,18 @@ __device__ __forceinline__ void pass_range_emit(const PassRangeIo& rio, const un
     const unsigned ibase = (unsigned)p0 + rio.a.point_base;
     unsigned sc = 0;
     for (unsigned w0 = wb; w0 < we; w0 += kWave) {
-        const unsigned long long mine = w0 + lane < we ? bmask[w0 + lane] : 0ull;
-        emit_words(mine, ibase + w0 * 64u, stg, sc, obase, rio.out, rio.cap);
+        const unsigned w = w0 + (unsigned)lane;
+        const unsigned long long mine = w < we ? bmask[w] : 0ull;
+        if (UNORD) {
+            const unsigned first = (unsigned)((((uint64_t)(w >> 2) * gridDim.x + blockIdx.x) << 8) + (w & 3u) * 64u) +
+                                   rio.a.point_base;
+            emit_words_at(mine, first, stg, sc, obase, rio.out, rio.cap);
+        } else {
+            emit_words(mine, ibase + w0 * 64u, stg, sc, obase, rio.out, rio.cap);
+        }
     }
     if (sc) emit_flush(stg, sc, obase, rio.out, rio.cap);
-    if (threadIdx.x == 0 && vb == gridDim.x - 1) *rio.total = excl_sh + bcount;
+    if (!UNORD && threadIdx.x == 0 && vb == gridDim.x - 1) *rio.total = excl_sh + bcount;
     if (rio.trace && threadIdx.x == 0) rio.trace[16 * (size_t)blockIdx.x + 6] = __builtin_amdgcn_s_memrealtime();
 }
 
@@ -1169,7 +1209,7 @@ __device__ __forceinline__ void pass_range_emit(const PassRangeIo& rio, const un
 // index order behind a look-back over the earlier chunks' hit counts (as range_fused).
 constexpr unsigned kFusedMaskWords = 2048;  // 131072 points per block chunk at most
 
-template <int NW, int ABL = 0, bool RANGE = false>
+template <int NW, int ABL = 0, bool RANGE = false, bool UNORD = false>
 __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x, const double* __restrict__ y,
                                                     uint64_t n, uint64_t chunk, KnnArgs args, PassIo io,
                                                     PassRangeIo rio) {
@@ -1186,7 +1226,7 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
     WaveStage& st = stage[wid];
     if (RANGE) {
         if (threadIdx.x == 0) {
-            rvb = atomicAdd(io.ctr + kVbWord, 1u);
+            rvb = UNORD ? blockIdx.x : atomicAdd(io.ctr + kVbWord, 1u);  // ordered: chunks in start order
             rcount = 0;
         }
         __syncthreads();
@@ -1195,7 +1235,7 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
     const uint64_t blk_begin = (uint64_t)vb * chunk;
     uint64_t blk_end = blk_begin + chunk;
     if (blk_end > n) blk_end = n;
-    const RangeSide rs{rmask, blk_begin, rio.a.r};
+    const RangeSide rs{rmask, blk_begin, rio.a.r, UNORD ? gridDim.x : 0u};
     for (int t = threadIdx.x; t < kHistBins; t += NT) kb.hist[t] = 0;
     if (RANGE)
         for (unsigned t = threadIdx.x; t < kFusedMaskWords; t += NT) rmask[t] = 0ull;
@@ -1218,7 +1258,8 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
     // the blocks' stream ends bunch up (a chunk per block leaves a 4-7 us spread between the
     // first and the last block, measured by the phase trace).  The fused range keeps a contiguous
     // chunk per block (its hit bitmask covers the chunk).  ABL bit 4: chunks (measurement).
-    constexpr bool kInterleave = !RANGE && !(ABL & 16);
+    // The unordered fused range interleaves too: its bitmask words follow the block's fronts.
+    constexpr bool kInterleave = (!RANGE || UNORD) && !(ABL & 16);
     // (Rotating each block's slot within a front, so one XCD's blocks do not always read the same
     // 2 KB position mod 16 KB, measured slower in round 4: 42.3 against 38.7 us.)
     const uint64_t total_iters = (n + kPtsIter - 1) / kPtsIter;
@@ -1237,7 +1278,8 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
             for (int b = 1; b < nu; b++) c = c || in_box(args.u[b], px, py);
         return c;
     };
-    auto iter = [&](auto full, const double (&px)[4], const double (&py)[4], const bool (&valid)[4], uint64_t ib) {
+    auto iter = [&](auto full, const double (&px)[4], const double (&py)[4], const bool (&valid)[4], uint64_t ib,
+                    unsigned mw) {  // mw: the block's first mask word of this iteration (4 per iteration)
         constexpr bool FULL = decltype(full)::value;
         double T2 = __builtin_huge_val();
         const unsigned long long B = lds_fresh(kb.bound);
@@ -1288,7 +1330,7 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
             const unsigned e = (unsigned)(hb[2 * h] >> (32 * half));
             const unsigned o = (unsigned)(hb[2 * h + 1] >> (32 * half));
             const unsigned long long word = spread32(e) | (spread32(o) << 1);
-            if (word) atomicOr(&rmask[(unsigned)((ib - blk_begin) >> 6) + lane], word);
+            if (word) atomicOr(&rmask[mw + lane], word);
         }
         wave_lds_sync();
         if (ccnt >= 64) {
@@ -1327,12 +1369,12 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
     };
     auto run = [&](unsigned it, double (&px)[4], double (&py)[4]) {
         if (is_full(it)) {
-            iter(kFull, px, py, all_valid, it_base(it));
+            iter(kFull, px, py, all_valid, it_base(it), it * 4u);
         } else {
             double qx4[4], qy4[4];
             bool valid[4];
             load4(x, y, it_base(it), blk_end, lane, qx4, qy4, valid);
-            iter(kPart, qx4, qy4, valid, it_base(it));
+            iter(kPart, qx4, qy4, valid, it_base(it), it * 4u);
         }
     };
     unsigned ia = (unsigned)wid, ibb = (unsigned)(NW + wid);
@@ -1380,7 +1422,10 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
     PASS_TRACE(io, 2);
     // the range hit count goes out first (later chunks wait for it); the hits themselves after
     // the kNN part, so the look-back wait never delays the kNN final
-    if (RANGE) pass_range_publish<NW>(rio, rmask, rcount, vb, blk_begin, blk_end);
+    // mask words of the block: its iterations x 4 (the ordered form's chunk [blk_begin, blk_end))
+    const unsigned rnw = kInterleave ? niters * 4u
+                                     : (blk_end > blk_begin ? (unsigned)((blk_end - blk_begin + 63) / 64) : 0u);
+    if (RANGE) pass_range_publish<NW, UNORD>(rio, rmask, rcount, rexcl, vb, rnw);
     // ---- end of block: B (k-th bin edge) and H (kPassHeads-th bin edge) from one scan of the
     // survivor histogram; survivors <= B written unsorted to this block's list; those <= H (the
     // block's smallest, usually 8-12) placed by rank: the kPassHeads smallest are the block's
@@ -1594,7 +1639,8 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
     PASS_TRACE(io, 4);
     if (kb.last == 0) {
         if (RANGE)
-            pass_range_emit<NW>(rio, rmask, rwsum, rcount, rexcl, vb, blk_begin, blk_end, reinterpret_cast<unsigned*>(st.cx));
+            pass_range_emit<NW, UNORD>(rio, rmask, rwsum, rcount, rexcl, vb, blk_begin, rnw,
+                                       reinterpret_cast<unsigned*>(st.cx));
         return;
     }
     if (threadIdx.x == 0) {
@@ -1619,8 +1665,13 @@ __global__ __launch_bounds__(NW * 64) void knn_pass(const double* __restrict__ x
     pass_final<NT>(io, args, gd, gi, kGcap - (kGcap & 1u), kb.hist, kb.fin, kb.bd, kb.bi, kb.bi + kPassMaxBlocks);
     PASS_TRACE(io, 7);
     if (RANGE) {
+        if (UNORD && threadIdx.x == 0) {  // every block reserved before it arrived: the total, re-armed
+            *rio.total = atomicAdd(rio.cursor, 0ull);
+            __hip_atomic_store(rio.cursor, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         __syncthreads();
-        pass_range_emit<NW>(rio, rmask, rwsum, rcount, rexcl, vb, blk_begin, blk_end, reinterpret_cast<unsigned*>(st.cx));
+        pass_range_emit<NW, UNORD>(rio, rmask, rwsum, rcount, rexcl, vb, blk_begin, rnw,
+                                   reinterpret_cast<unsigned*>(st.cx));
     }
 }
 
@@ -2228,7 +2279,10 @@ hipError_t launch_knn_pass(const double* x, const double* y, uint64_t n, const K
     if (range) {
         if (!knn_pass_fuses_range(n)) return hipErrorInvalidValue;
         rio = *range;
-        hipExtLaunchKernelGGL(knn_pass<kPassNW, 0, true>, g, b, 0, st, ev0, ev1, 0, x, y, n, chunk, args, io, rio);
+        if (rio.unordered)
+            hipExtLaunchKernelGGL(knn_pass<kPassNW, 0, true, true>, g, b, 0, st, ev0, ev1, 0, x, y, n, chunk, args, io, rio);
+        else
+            hipExtLaunchKernelGGL(knn_pass<kPassNW, 0, true>, g, b, 0, st, ev0, ev1, 0, x, y, n, chunk, args, io, rio);
     } else {
         switch (abl) {
             case 1: hipExtLaunchKernelGGL(knn_pass<kPassNW, 1>, g, b, 0, st, ev0, ev1, 0, x, y, n, chunk, args, io, rio); break;

@@ -142,3 +142,52 @@ def test_range_set_order_argument():
     c = Context(0)
     with pytest.raises(_abi.GeohipArgumentError):
         _abi.Context._check(c, _abi.lib.geohip_ctx_set_range_order(c.h, 7), "set_range_order")
+
+
+# ---- the fused kNN + range pass (geohip_knn_range_pp, the C5 step) with the unordered range ----
+KR_CASES = [(1000, 0.05, Q, 100, False), (100, 0.5, Q, 50, False), (500, 0.05, (116.3, 40.2), 64, False),
+            (100, 0.5, Q, 50, True), (37, 0.3, (115.45, 39.55), 10, False), (100, 0.0, Q, 5, False),
+            (100, math.nan, Q, 7, False), (100, 0.03, (117.7, 41.3), 3, False), (100, 0.2, (116.0, 40.5), 1000, False)]
+
+
+@pytest.mark.parametrize("case", range(len(KR_CASES)))
+@pytest.mark.parametrize("n", [300000, 1025, 0])
+def test_knn_range_fused_set(sctx, case, n):
+    """The unordered fused pass sweeps the window in interleaved fronts (its hit bitmask follows
+    each block's fronts): the kNN bits and the range set equal the oracle's."""
+    gn, r, q, k, approx = KR_CASES[case]
+    rng = np.random.default_rng(500 + case)
+    x, y = _window(rng, n, nan_every=1009)
+    ag, cg = agrid(gn)
+    (oi, od), got = sctx.knn_range_pp(ag, x, y, q[0], q[1], r, k, approx)
+    wi, wd = cref.knn_pp(cg, x, y, q[0], q[1], r, k)
+    assert oi.tolist() == wi.tolist()
+    assert np.array_equal(od.view(np.uint64), wd.view(np.uint64))
+    _same_set(got, cref.range_pp(cg, x, y, q[0], q[1], r, approx))
+
+
+def test_knn_range_fused_set_c5_shard(sctx, ctx):
+    """The C5 shard (25M points, 1000 x 1000, k = 100, r = 0.05) through the async form twice on
+    one ctx (the reservation cursor re-armed by each launch's last block): the
+    kNN equals the ordered pass's bit for bit, the range hits are the same set."""
+    import torch
+    ag, _ = agrid(1000)
+    n = 25_000_000
+    x = torch.empty(n, dtype=torch.float64, device="cuda")
+    y = torch.empty(n, dtype=torch.float64, device="cuda")
+    sctx.synth_uniform_async(x, y, 0, 7, BJ)
+    (wi, wd), want = ctx.knn_range_pp(ag, x, y, Q[0], Q[1], 0.05, 100)
+    want = torch.as_tensor(want).to(torch.int64).cuda()
+    ki = torch.empty(100, dtype=torch.int32, device="cuda")
+    kd = torch.empty(100, dtype=torch.float64, device="cuda")
+    kc = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ro = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    rc = torch.zeros(1, dtype=torch.int64, device="cuda")
+    for _ in range(2):
+        sctx.knn_range_pp_async(ag, x, y, Q[0], Q[1], 0.05, 100, False, ki, kd, kc, ro, n, rc)
+        sctx.sync()
+        m = int(rc.item())
+        assert int(kc.item()) == 100 and m == len(want) > 10_000
+        assert torch.equal(ki.cpu().to(torch.int64), torch.as_tensor(wi).cpu().to(torch.int64))
+        assert torch.equal(kd.cpu().view(torch.int64), torch.as_tensor(wd).cpu().view(torch.int64))
+        assert torch.equal(torch.sort(ro[:m].to(torch.int64)).values, want)
