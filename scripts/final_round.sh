@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU box, end of round: the GPU suite, every bench workload's line, rocprofv3 kernel stats of each
-# bench command (copied to profiles/r05_*).  Every GPU step has its own limit.
+# bench command (copied to profiles/r06_*).  Every GPU step has its own limit.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/final/prof

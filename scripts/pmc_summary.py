@@ -35,15 +35,17 @@ FP64_LANES = 64
 _JOIN = {"zero_step": 1, "jq_rect": 1, "jq_build<false>": 1, "jq_build<true>": 1, "jq_starts": 1, "jb_bands": 1,
          "jb_scan": 1, "jb_segs": 1, "jb_tiles": 1, "join_fused<false, true>": 1}
 _PS = {**_PS, "zero_step": 1}
-TAGS = {"knn": ("knn_scan", {"knn_pass": 1}),
-        "range": ("range", {"range_fused": 1, "range_scan": 1, "scan_units": 1, "range_emit": 1}),
+# (r06: the bench's set-up launches of the other kNN / range instantiations are told apart by their
+# template arguments)
+TAGS = {"knn": ("knn_scan", {"knn_pass<16, 0, false, false>": 1}),
+        "range": ("range", {"range_set": 1}),
         "join": ("join_probe", _JOIN),
         "ppoly": ("ppoly_probe", _PS),
-        "c5": ("knn_scan_c5", {"knn_pass": 1}),
+        "c5": ("knn_scan_c5", {"knn_pass<16, 0, true, true>": 1}),
         "ingest": ("ingest", {"ingest_fused": 1, "ingest_general": 1}),
         "ppjoin": ("ppjoin", _PS),
         "ppknn": ("ppknn", {"rsel_init": 1, "rsel_small": 1, "ppknn_scan_boxes": 1, "ppknn_dist": 1}),
-        "knn_incr": ("knn_incr", {"knn_pass": 1, "knn_merge_panes": 1}),
+        "knn_incr": ("knn_incr", {"knn_pass<16, 0, false, false>": 1, "knn_merge_panes": 1}),
         "ppoly_incr": ("ppoly_incr", _PS)}
 
 
