@@ -1,6 +1,7 @@
 """Phase timeline of one kNN pass launch (100 MHz timestamps): per-block start, stream end,
 flush (block barrier), stores drained, arrived; the last block's acquire, gather and write.
-Percentiles in microseconds relative to the earliest block start (GPU box measurement)."""
+Percentiles (0, 10, 50, 90, 100) in microseconds relative to the earliest block start (GPU box
+measurement)."""
 import json
 import sys
 from pathlib import Path
@@ -39,7 +40,11 @@ for rep in range(4):
     t0 = tr[:, 0].min()
     rel = (tr - t0) / 100.0
     row = {nm: [round(float(np.percentile(rel[:, j], p)), 2) for p in (0, 10, 50, 90, 100)] for j, nm in enumerate(names)}
-    row["block_median"] = {nm: round(float(np.median(rel[:, j])), 2) for nm, j in blk.items()}
+    # blocks that reached the stamp (0 = not reached: the slot-complete end stamps 8 and 10 but
+    # not 9, the list path all three) -- their median and their number
+    row["block_median"] = {nm: (round(float(np.median(rel[tr[:, j] != 0, j])), 2) if (tr[:, j] != 0).any() else None)
+                           for nm, j in blk.items()}
+    row["blocks_reached"] = {nm: int((tr[:, j] != 0).sum()) for nm, j in blk.items()}
     last = int(np.argmax(tr[:, 7]))
     row["final"] = {nm: round(float(rel[last, j]), 2) for nm, j in fin.items()}
     row["last_block"] = last

@@ -1502,6 +1502,12 @@ __global__ __launch_bounds__(kTB) void join_fused(JoinRun a) {
     const unsigned gq = *a.gcnt;
     const TileGeom& g = a.geo;
     const double slack = 0x1.0p-30 * (__builtin_fabs(g.mnx) + __builtin_fabs(g.mny) + ((double)g.nb + 2.0) * g.l);
+#ifdef GEOHIP_JOIN_TRACE  // measurement build (scripts/join_tail.py): per block start, end, items, last item start
+    unsigned long long* tr = reinterpret_cast<unsigned long long*>(a.out) + (a.cap - 4 * 2048);
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    unsigned long long t_last = t_start;
+    unsigned n_items = 0;
+#endif
     for (bool first = true;; first = false) {
         if (threadIdx.x == 0) {  // the block's first item by its index, the rest from the ticket
             sh_item = first ? blockIdx.x : gridDim.x + atomicAdd(a.ticket, 1u);
@@ -1512,6 +1518,10 @@ __global__ __launch_bounds__(kTB) void join_fused(JoinRun a) {
         // divergent gets structured with lane 0 outside the barrier loop (hangs)
         const unsigned it = (unsigned)__builtin_amdgcn_readfirstlane((int)sh_item);
         if (it >= nitems) break;
+#ifdef GEOHIP_JOIN_TRACE
+        t_last = __builtin_amdgcn_s_memrealtime();
+        n_items++;
+#endif
         const uint2 d = a.items[it];
         const unsigned tile = d.x;
         const unsigned qs = a.qstart[tile], nql = a.qstart[tile + 1] - qs, nqt = nql + gq;
@@ -1687,6 +1697,14 @@ __global__ __launch_bounds__(kTB) void join_fused(JoinRun a) {
         }
         __syncthreads();  // every wave leaves the item together (LDS reuse, uniform loop)
     }
+#ifdef GEOHIP_JOIN_TRACE
+    if (WRITE && threadIdx.x == 0 && blockIdx.x < 2048) {
+        tr[blockIdx.x] = t_start;
+        tr[2048 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+        tr[4096 + blockIdx.x] = n_items;
+        tr[6144 + blockIdx.x] = t_last;
+    }
+#endif
 }
 
 // ------------------------------------------------------------------ point-polygon --------
