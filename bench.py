@@ -625,10 +625,10 @@ class JoinWorkload(Workload):
         if self.world == 1:
             return None  # one band: the arrival line itself
         t, out = self._timed_side(lambda s: self.cells_window(s % self.windows), steps)
-        pairs, _, total = out.result()
+        m, _, total = out.totals()  # counts only (the pairs stay on the device)
         w = (steps - 1) % self.windows
         want = sum(self._gather_ints(self.pairs[w]))
-        pr = self._gather_ints(len(pairs))
+        pr = self._gather_ints(m)
         mean = sum(pr) / len(pr)
         return {"value": self.n * self.world * steps / t, "unit": "points/sec", "ms_per_step": t / steps * 1e3,
                 "steps": steps, "layout": "grid-cell key bands: data points packed by owner band "
@@ -661,7 +661,7 @@ class JoinWorkload(Workload):
         if self.args.partition != "cells":
             return None
         want = sum(self._gather_ints(self.pairs[last_step % self.windows]))
-        return (int(self.cells_last.result()[2]) == want) if self.rank == 0 else None
+        return (int(self.cells_last.totals()[2]) == want) if self.rank == 0 else None
 
     def algorithmic_bytes(self):
         return BYTES_PER_POINT * self.n + BYTES_PER_POINT * self.nq + 8 * float(np.mean(self.pairs))

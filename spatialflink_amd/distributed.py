@@ -221,6 +221,12 @@ class CellsStep:
     rank: int
     nrecv: int
 
+    def totals(self):
+        """(this rank's pair count, its output offset, the total) -- the counts alone, no pairs read."""
+        m = int(self.count.item())
+        allc = self.counts.cpu().tolist()
+        return m, sum(allc[:self.rank]), sum(allc)
+
     def result(self):
         import torch
         m = int(self.count.item())
@@ -407,6 +413,12 @@ class JoinCellsStep:
     rg: object
     counts: object
     rank: int
+
+    def totals(self):
+        """(this rank's pair count, its output offset, the total) -- the counts alone, no pairs read."""
+        m = int(self.count.item())
+        allc = self.counts.cpu().tolist()
+        return m, sum(allc[:self.rank]), sum(allc)
 
     def result(self):
         import torch
