@@ -664,6 +664,12 @@ class JoinWorkload(Workload):
         return (int(self.cells_last.totals()[2]) == want) if self.rank == 0 else None
 
     def algorithmic_bytes(self):
+        if self.args.partition == "cells" and getattr(self, "cells_last", None) is not None:
+            # key bands: this rank's own step (ranks' bands differ: skew) -- its shard read by the
+            # pack, its received band and the queries read by its join, its own pairs written
+            m, _, _ = self.cells_last.totals()
+            nrecv = int(self.cells_last.rg.numel())
+            return BYTES_PER_POINT * (self.n + nrecv + self.nq) + 8 * float(m)
         return BYTES_PER_POINT * self.n + BYTES_PER_POINT * self.nq + 8 * float(np.mean(self.pairs))
 
     def config(self):

@@ -60,7 +60,8 @@ class IncrementalRange:
     def window(self):
         """The window's hits pane by pane: a list of the panes' hit arrays, nothing recomputed or
         copied.  Each holds stream positions mod 2^32 as uint32 bit patterns (ascending within a
-        pane until the stream position wraps); a device pane's array is an int32 tensor, so
+        pane until the stream position wraps, in the ctx's default order; a set in no promised
+        order under GEOHIP_ORDER_ANY); a device pane's array is an int32 tensor, so
         positions from 2^31 on read negative -- mask with & 0xFFFFFFFF, or use window_local()."""
         return [hits for _, _, hits in self.panes]
 

@@ -4,7 +4,7 @@ the range_set kernel) against the C oracle.
 The reference's window result is a set (PointPointRangeQuery.java:117-136), so these tests compare
 SORTED index lists: the same hits, each exactly once, no order promised.  Every case the ascending
 mode's parity tests cover (golden vectors, NaN / out-of-grid points, r = 0 / r < 0 / NaN, window
-sizes around the 256-point iteration and the 512-hit reservation run, approximate mode, two-phase
+sizes around the 256-point iteration and past one 1024-hit run, approximate mode, two-phase
 capacity, panes' point_base) plus what is particular to the set kernel: back-to-back launches on
 one ctx (the reservation cursor re-armed by each launch's last block) interleaved with the
 ascending mode (shared look-back scratch) and with async calls, and the C1 shape at 10M points
