@@ -1,7 +1,8 @@
 """The point-polygon stream on windows that overflow its per-wave LDS stages or its candidate
 buffer: the C4 window, windows packed around polygon edges, and 3000 overlapping polygons over the
 C4 window (range and join).  Run with GEOHIP_HOST_PROFILE=1 (GPU box); the library prints one line
-per call (pairs, candidates, those decided in the stream past the buffer, early wave flushes);
+per call (pairs, candidates, those past the buffer, early wave flushes, chunks decided by the
+redo pass);
 the dense window's device step time is printed for a first call (fresh ctx) and warm calls, and
 its pair count / digest checked against the oracle (threaded C, slow: run once)."""
 import sys

@@ -2484,7 +2484,7 @@ struct StreamOut {
     unsigned long long* ptotal;     // pairs: reservation cursor (zero before; an async call's count)
     unsigned long long* ctotal;     // candidates: reservation cursor (zero before)
     unsigned* flushes;              // wave stages flushed before their chunk's end (profiling count)
-    uint64_t ccap;                  // candidates past it are decided in the stream (exact test inline)
+    uint64_t ccap;                  // candidate buffer: a chunk whose candidates pass it goes to the redo pass
     unsigned* cpoly;                // candidates in chunk order: polygon (the grouping reads these),
     double4* crec;                  // and (x, y, point bits, -) -- one 32-byte sector per gather
     unsigned* covf;                 // per wave: the chunk's candidates staged before its end (packed
@@ -2509,8 +2509,8 @@ struct StreamArgs {
     int jmode;                      // 0 range, 1 join exact, 2 join approximate
     double r;
     StreamOut o;
-    // the rings, for candidates past the candidate buffer (decided in the stream, as
-    // ppoly_cand_eval decides the others)
+    // the rings, for the redo pass's candidates (decided there as ppoly_cand_eval decides the
+    // others)
     const double* vx;
     const double* vy;
     const ring_id_t* vring;
@@ -2530,7 +2530,11 @@ struct StreamSink {
     unsigned cap;                   // its capacity (a push adds <= 64)
     unsigned n;                     // entries staged (wave-uniform)
     unsigned ovn;                   // candidates: this chunk's entries in the wave's overflow list
+                                    // (kOvnLost: the list filled, the chunk goes to the redo pass)
 };
+constexpr unsigned kOvnLost = 0xffffffffu;
+constexpr uint32_t kSpillEnt = 16;  // spill-list entries per chunk point (a window of cells with more
+                                    // polygons than that may send chunks to the redo pass)
 
 __device__ __forceinline__ void stream_emit_pair(const StreamOut& o, unsigned long long p, unsigned poly, unsigned idx) {
     if (p >= o.cap) return;
@@ -2618,9 +2622,15 @@ __device__ __forceinline__ void stream_flush(const StreamArgs& a, StreamSink& k,
     if (CAND && REDO) {
         stream_decide_cands(a, k.pk, k.n, c0);
     } else if (CAND) {
-        unsigned* ovf = stream_ovf(a.o) + k.ovn;
-        for (unsigned t = (unsigned)lane_id(); t < k.n; t += kWave) ovf[t] = k.pk[t];
-        k.ovn += k.n;
+        if (k.ovn != kOvnLost) {  // wave-uniform
+            if (k.ovn + k.n <= a.o.covf_wave) {
+                unsigned* ovf = stream_ovf(a.o) + k.ovn;
+                for (unsigned t = (unsigned)lane_id(); t < k.n; t += kWave) ovf[t] = k.pk[t];
+                k.ovn += k.n;
+            } else {
+                k.ovn = kOvnLost;  // the spill list is full: the chunk's candidates go to the redo pass
+            }
+        }
     } else {
         const unsigned long long b = wave_reserve(a.o.ptotal, k.n);
         stream_store_pairs(a, k.pk, k.n, b, c0);
@@ -3007,28 +3017,34 @@ __global__ __launch_bounds__(kStreamNW * kWave) __attribute__((amdgpu_waves_per_
         if (vb + gridDim.x < nchunks) prefetch(vb + gridDim.x);
         if (lane == 0) {
             s_wp[wid] = ps.n;
-            s_wc[wid] = cs.n + cs.ovn;  // staged in LDS + spilled before the chunk's end
+            // staged in LDS + spilled before the chunk's end (or kOvnLost)
+            s_wc[wid] = cs.ovn == kOvnLost ? kOvnLost : cs.n + cs.ovn;
         }
         __syncthreads();
         unsigned np = 0, nc = 0, pex = 0, cex = 0;  // totals; this wave's offsets in the chunk
+        bool lost = false;                          // block-uniform: a wave's spill list filled
 #pragma unroll
         for (int w = 0; w < kStreamNW; w++) {
-            const unsigned wp = s_wp[w], wc = s_wc[w];
+            const unsigned wp = s_wp[w], wc0 = s_wc[w];
+            lost = lost || wc0 == kOvnLost;
+            const unsigned wc = wc0 == kOvnLost ? 0u : wc0;
             pex += w < wid ? wp : 0u;
             cex += w < wid ? wc : 0u;
             np += wp;
             nc += wc;
         }
+        if (lost) nc = 0;  // nothing reserved: the redo pass decides every candidate of the chunk
         if (threadIdx.x == 0) {
             s_pb = np ? atomicAdd(a.o.ptotal, (unsigned long long)np) : 0ull;
             s_cb = nc ? atomicAdd(a.o.ctotal, (unsigned long long)nc) : 0ull;
-            // a chunk whose candidates do not all fit the buffer leaves them all to the redo pass
-            if (!APPROX && nc && s_cb + nc > a.o.ccap) a.o.redo[atomicAdd(a.o.nredo, 1u)] = vb;
+            // a chunk whose candidates do not all fit the buffer (or its spill lists) leaves them
+            // all to the redo pass
+            if (!APPROX && (lost || (nc && s_cb + nc > a.o.ccap))) a.o.redo[atomicAdd(a.o.nredo, 1u)] = vb;
         }
         __syncthreads();
         // each wave stores its own region: coalesced runs of the output
         stream_store_pairs(a, ppk + wid * kWPair, ps.n, s_pb + pex, c0);
-        if (!APPROX) {
+        if (!APPROX && !lost) {
             const unsigned long long cb = s_cb + cex;
             const unsigned wc = cs.n + cs.ovn;
             if (s_cb + nc <= a.o.ccap) {
@@ -3224,8 +3240,8 @@ __global__ __launch_bounds__(kCandThreads) void ppoly_cand_plan(CandGroup c) {
     const unsigned carry_i = F + carry_p;
     if (threadIdx.x == 0) {
         *c.nitems = carry_i;
-        // a short candidate buffer (the candidates past it were decided in the stream): the size
-        // it needed goes to the ctx's fault block as a hint, so the next async call sizes it
+        // a short candidate buffer (the chunks past it went to the redo pass): the size it needed
+        // goes to the ctx's fault block as a hint, so the next async call sizes it
         const unsigned long long nc = *c.cstream;
         if (c.fault && nc > c.ccap) {
             atomicOr(c.fault, kFaultCandNeed);
@@ -5501,10 +5517,10 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             if (rc) return rc;
         }
         {
-            // one pass: candidates past ccap are decided in the stream (stream_store_cands), the
-            // count they needed sizes the next call's buffer
+            // one pass: the chunks whose candidates pass ccap (or fill a wave's spill list) are
+            // decided by ppoly_stream_redo; the count they needed sizes the next call's buffer
             // J_MISC: [0..1] pair total, [2..3] candidate total, [4] work items, [5] early wave
-            // flushes, [6] eval ticket
+            // flushes, [6] eval ticket, [7] chunks queued for the redo pass
             unsigned* misc = S.get<unsigned>(J_MISC, kMiscWords * 4);
             unsigned* mat = cands ? S.get<unsigned>(J_HIST, ((size_t)kCandGroups + 2) * npoly * 4 + 16) : nullptr;
             void* cbuf = cands ? S.get<void>(J_SY, ccap * 36 + 64) : nullptr;
@@ -5533,13 +5549,13 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             char* cb = reinterpret_cast<char*>(cbuf);
             so.cpoly = cands ? reinterpret_cast<unsigned*>(cb) : nullptr;
             so.crec = cands ? reinterpret_cast<double4*>(cb + ((ccap * 4 + 31) & ~(uint64_t)31)) : nullptr;
-            // per wave, a chunk's candidates can all lie past the buffer: its points x the most
-            // entries a point meets (a cell's, or the polygons reaching outside the grid)
+            // per wave, the spill list holds its chunk points x the most entries a point meets (a
+            // cell's, or the polygons reaching outside the grid), up to kSpillEnt entries per point
+            // (<= 128 MB in all); a wave whose candidates exceed it sends its chunk to the redo pass
             const unsigned stream_blocks =
                 (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(nchunks, (uint64_t)ctx_cus(ctx) * kStreamBlocksPerCU));
-            so.covf_wave = cands ? (kStreamChunk / kStreamNW) *
-                                       std::max<uint32_t>(1u, std::max<uint32_t>(pc->max_cell_ent, (uint32_t)pc->opoly.size()))
-                                 : 0u;
+            const uint32_t ment = std::max<uint32_t>(1u, std::max<uint32_t>(pc->max_cell_ent, (uint32_t)pc->opoly.size()));
+            so.covf_wave = cands ? (kStreamChunk / kStreamNW) * std::min<uint32_t>(ment, kSpillEnt) : 0u;
             const size_t covf_words = (size_t)stream_blocks * kStreamNW * so.covf_wave;
             unsigned* cov = cands ? S.get<unsigned>(J_COVF, (covf_words + nchunks + 64) * 4) : nullptr;
             if (S.rc) return S.rc;
@@ -5639,11 +5655,11 @@ int ppoly_impl(geohip_ctx* ctx, const geohip_grid* grid, const geohip_grid* gq, 
             if (prof)
                 fprintf(stderr, "ppoly host: refinement words %zu (parts) + %zu (sub-parts)\n", pc->hrfw.size() / 2,
                         pc->hrfw2.size());
-            if (prof) fprintf(stderr, "ppoly stream: %llu pairs, %llu candidates (capacity %llu: %llu decided in the stream), "
-                              "%u early wave flushes over %llu chunks, one pass\n",
+            if (prof) fprintf(stderr, "ppoly stream: %llu pairs, %llu candidates (capacity %llu: %llu past it), "
+                              "%u early wave flushes, %u of %llu chunks decided by the redo pass, one pass\n",
                               (unsigned long long)tot, (unsigned long long)ncand, (unsigned long long)ccap,
                               (unsigned long long)(ncand > ccap ? ncand - ccap : 0), (unsigned)(pin[2] >> 32),
-                              (unsigned long long)nchunks);
+                              (unsigned)(pin[3] >> 32), (unsigned long long)nchunks);
         }
         *out_count = tot;
         if (!dev && cap) {

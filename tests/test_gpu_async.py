@@ -138,8 +138,8 @@ def test_ppoly_async_matches_sync(ctx, join, approx):
 
 def test_ppoly_async_candidate_overflow():
     """A fresh ctx sizes the candidate buffer at max(65536, n / 16); a window packed around
-    polygon edges needs more.  The candidates past the buffer are decided in the stream itself, so
-    the first call already returns the oracle's pairs in one pass and sync() reports no error; the
+    polygon edges needs more.  The chunks whose candidates pass the buffer are decided by the redo
+    pass of the same call, so the first call already returns the oracle's pairs in one pass and sync() reports no error; the
     need it reported sizes the next call's buffer (same pairs again)."""
     import torch
     c = Context(0)

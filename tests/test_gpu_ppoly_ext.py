@@ -368,7 +368,8 @@ def test_ppoly_stream_overflow_and_regrow(ctx):
     """The streaming point-polygon path's rare branches: 96 concentric star polygons put ~96
     entries in each central cell, so a wave stages more pairs (and mixed-subcell candidates) than
     its LDS region holds and flushes it before the chunk's end; the candidates of the first call
-    exceed the initial candidate buffer (n / 16), so those past it are decided in the stream.
+    exceed the initial candidate buffer (n / 16), so their chunks go to the redo pass (and a wave's
+    candidates can pass its spill list: ~96 per point against 16, the redo pass again).
     Range, exact and approximate, and join vs the oracle; a second call reuses the cached plan and
     the grown buffer."""
     ag, cg = agrid(100)
