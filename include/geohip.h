@@ -135,8 +135,9 @@ int geohip_ctx_timing_kernels(geohip_ctx* ctx, double* step_ms, uint64_t* steps,
      GEOHIP_ERR_ARG       geohip_join_pp_async: a query key the reference cannot parse back
                           (NumberFormatException) or whose neighbour loop never ends
                           (UniformGrid.java:261-293) -- its results are incomplete,
-   (The point-polygon forms report no error for a short candidate buffer: the candidates past it
-   are decided in the stream, and the count they needed sizes the next call's buffer.)
+   (The point-polygon forms report no error for a short candidate buffer: the chunks whose
+   candidates pass it are decided by a redo pass in the same call, and the count they needed
+   sizes the next call's buffer.)
    The synchronous calls check the look-back themselves. */
 int geohip_ctx_sync(geohip_ctx* ctx);
 int geohip_device_count(int* out_count);
