@@ -2677,24 +2677,20 @@ constexpr unsigned kBalItems = 2;
 
 // the class decision of one entry (ex, word) for a point with subcell / NaN bits sw:
 // PointPolygonRangeQuery.java:105-121 -- G -> pair; C -> by the subcell class (mixed: candidate)
+// (branch-free: selects instead of the early returns, whose exec-mask bookkeeping cost more
+// scalar instructions than the decision itself; kWordHit / kWordMiss are the all-hit / all-miss
+// fields, so the subcell's field covers them)
 __device__ __forceinline__ void stream_decide(uint32_t ex, uint32_t word, unsigned sw, bool& hit, bool& need) {
     constexpr unsigned kNanBit = 16u;
-    hit = need = false;
-    if (ex == kNoEntry) return;
-    if (!(ex & kEntC)) {
-        hit = true;
-        return;
-    }
+    static_assert(kWordHit == 0x55555555u && kClsHit == 1 && kWordMiss == 0xAAAAAAAAu && kClsMiss == 2,
+                  "uniform class words are their fields repeated");
     // a decided class holds for every point in the cell's coordinate box: not for NaN
     // coordinates (cell 0 by Java's (int) NaN)
-    uint32_t kc = kClsMixed;
-    if (!(sw & kNanBit)) {
-        if (word == kWordHit) kc = kClsHit;
-        else if (word == kWordMiss) kc = kClsMiss;
-        else kc = (word >> (2 * (sw & 15u))) & 3u;
-    }
-    hit = kc == kClsHit;
-    need = kc == kClsMixed;
+    const unsigned field = (word >> (2u * (sw & 15u))) & 3u;
+    const unsigned kc = (sw & kNanBit) ? (unsigned)kClsMixed : field;
+    const bool some = ex != kNoEntry, g = (ex & kEntC) == 0u;
+    hit = some & (g | (kc == kClsHit));
+    need = some & !g & (kc == kClsMixed);
 }
 
 // One chunk's points (all waves of the block).  Phase A: every point of the wave's iterations --
